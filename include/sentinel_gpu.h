@@ -1,0 +1,170 @@
+/*
+ * sentinel_gpu.h — C ABI of the MI355X batched flow-decision engine.
+ *
+ * This is the drop-in boundary for Sentinel's cluster token service hot path.
+ * Every entry point below replaces a piece of the Java reference
+ * (paths relative to /root/reference; see INTEGRATION.md for the JNI / Panama
+ * bindings a Sentinel maintainer would add):
+ *
+ *   sg_flow_decide_batch      ← TokenService.requestToken(Long,int,boolean)
+ *                               sentinel-core/.../cluster/TokenService.java:36, implemented by
+ *                               DefaultTokenService.requestToken
+ *                               sentinel-cluster/sentinel-cluster-server-default/.../flow/DefaultTokenService.java:39-50
+ *                               → ClusterFlowChecker.acquireClusterToken (…/flow/ClusterFlowChecker.java:55-112),
+ *                               evaluated for a whole batch of requests in (timestamp, arrival) order.
+ *   sg_load_flow_rules        ← ClusterFlowRuleManager.loadRules / applyClusterFlowRule
+ *                               (…/flow/rule/ClusterFlowRuleManager.java:254-260, 325-375); metrics of a
+ *                               flowId that survives a reload are kept (putMetricIfAbsent :361).
+ *   sg_set_namespaces         ← ClusterServerConfigManager (exceedCount / maxOccupyRatio / maxAllowedQps,
+ *                               …/server/config/ClusterServerConfigManager.java:303-346) +
+ *                               GlobalRequestLimiter.initIfAbsent (…/statistic/limit/GlobalRequestLimiter.java:32-37)
+ *                               + ConnectionManager.getConnectedCount (…/server/connection/ConnectionManager.java:47-51)
+ *   sg_flow_read_state        ← ClusterMetric window contents (…/statistic/metric/ClusterMetric.java) — read back
+ *                               for parity checks and the metric snapshot.
+ *   sg_snapshot_metrics       ← ClusterMetricNodeGenerator.generateCurrentNodeMap passQps/blockQps per flowId
+ *                               (…/flow/statistic/ClusterMetricNodeGenerator.java:39-105).
+ *
+ * Conventions: plain C types only, no exceptions across the ABI, 0 = success, negative SG_E* on error
+ * (the Java shim then answers TokenResult(FAIL) so FlowRuleChecker.fallbackToLocalOrPass applies,
+ * sentinel-core/.../slots/block/flow/FlowRuleChecker.java:166-209). One handle = one submitter.
+ */
+#ifndef SENTINEL_GPU_H
+#define SENTINEL_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---- */
+#define SG_OK              0
+#define SG_E_INVAL        -1   /* bad argument / invalid rule / bad request record layout          */
+#define SG_E_DEVICE       -2   /* HIP runtime error                                               */
+#define SG_E_NOMEM        -3   /* device allocation failed                                        */
+#define SG_E_UNSUPPORTED  -4   /* configuration outside the device path (e.g. sampleCount > 64)   */
+#define SG_E_TIME         -5   /* timestamps negative or not non-decreasing (batch or vs. state)  */
+#define SG_E_CAPACITY     -6   /* batch larger than sg_config.max_batch                           */
+
+/* ---- TokenResultStatus (sentinel-core/.../cluster/TokenResultStatus.java:27-53) ---- */
+#define SG_STATUS_BAD_REQUEST      (-4)
+#define SG_STATUS_TOO_MANY_REQUEST (-2)
+#define SG_STATUS_FAIL             (-1)
+#define SG_STATUS_OK                 0
+#define SG_STATUS_BLOCKED            1
+#define SG_STATUS_SHOULD_WAIT        2
+#define SG_STATUS_NO_RULE_EXISTS     3
+
+/* ---- ClusterRuleConstant (sentinel-core/.../slots/block/ClusterRuleConstant.java:27-28) ---- */
+#define SG_THRESHOLD_AVG_LOCAL 0
+#define SG_THRESHOLD_GLOBAL    1
+
+/* ---- ClusterFlowEvent ordinals (…/flow/statistic/data/ClusterFlowEvent.java:22-52) ---- */
+#define SG_EV_PASS           0
+#define SG_EV_BLOCK          1
+#define SG_EV_PASS_REQUEST   2
+#define SG_EV_BLOCK_REQUEST  3
+#define SG_EV_OCCUPIED_PASS  4
+#define SG_EV_OCCUPIED_BLOCK 5
+#define SG_EV_WAITING        6
+#define SG_NUM_EVENTS        7
+
+/* ---- request key encoding ----
+ * key = dense rule index assigned by sg_load_flow_rules (position in the rule array),
+ * OR-ed with SG_KEY_PRIO for prioritized requests. Two reserved values let the host shim
+ * submit requests it has already classified without splitting the batch:
+ *   SG_KEY_BAD     → BAD_REQUEST   (DefaultTokenService.notValidRequest, id null/<=0, :87-89)
+ *   SG_KEY_NO_RULE → NO_RULE_EXISTS (rule lookup miss, DefaultTokenService.java:44-47)
+ * Any other index >= number of loaded rules also answers NO_RULE_EXISTS. */
+#define SG_KEY_PRIO    0x80000000u
+#define SG_KEY_INDEX   0x7FFFFFFFu
+#define SG_KEY_NO_RULE 0x7FFFFFFFu
+#define SG_KEY_BAD     0x7FFFFFFEu
+
+/* Largest sampleCount the device walker keeps in a wave (one bucket per lane). */
+#define SG_MAX_SAMPLE_COUNT 64
+
+typedef struct sg_handle sg_handle;
+
+typedef struct sg_config {
+    int32_t  device;            /* HIP device ordinal                                   */
+    int32_t  reserved0;
+    double   exceed_count;      /* ServerFlowConfig.exceedCount, default 1.0 (:26)      */
+    double   max_occupy_ratio;  /* ServerFlowConfig.maxOccupyRatio, default 1.0 (:27)  */
+    uint64_t max_batch;         /* largest n accepted by sg_flow_decide_batch           */
+} sg_config;
+
+/* One cluster-mode QPS FlowRule with its ClusterFlowConfig
+ * (FlowRule.java:52-95, ClusterFlowConfig.java:29-74). */
+typedef struct sg_flow_rule {
+    int64_t flow_id;            /* ClusterFlowConfig.flowId (must be > 0)                      */
+    double  count;              /* FlowRule.count (threshold, >= 0)                            */
+    int32_t threshold_type;     /* SG_THRESHOLD_AVG_LOCAL / SG_THRESHOLD_GLOBAL                */
+    int32_t sample_count;       /* ClusterFlowConfig.sampleCount, default 10                   */
+    int32_t window_interval_ms; /* ClusterFlowConfig.windowIntervalMs, default 1000            */
+    int32_t namespace_id;       /* index into the sg_set_namespaces array                      */
+} sg_flow_rule;
+
+/* Per-namespace server settings. */
+typedef struct sg_namespace {
+    int32_t limiter_enabled;    /* GlobalRequestLimiter has a RequestLimiter for this namespace */
+    int32_t connected_count;    /* ConnectionManager.getConnectedCount(namespace)               */
+    double  max_allowed_qps;    /* ServerFlowConfig.maxAllowedQps, default 30000 (:31)          */
+} sg_namespace;
+
+/* One token request: requestToken(flowId→key, acquireCount, prioritized) at time ts_ms. */
+typedef struct sg_req {
+    int64_t  ts_ms;             /* explicit TimeUtil.currentTimeMillis() of the call          */
+    uint32_t key;               /* rule index | SG_KEY_PRIO, or SG_KEY_BAD / SG_KEY_NO_RULE     */
+    int32_t  acquire;           /* acquireCount; <= 0 → BAD_REQUEST                            */
+} sg_req;
+
+/* TokenResult (sentinel-core/.../cluster/TokenResult.java:26-35) minus tokenId/attachments. */
+typedef struct sg_result {
+    int32_t status;
+    int32_t remaining;
+    int32_t wait_ms;
+} sg_result;
+
+/* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
+typedef struct sg_batch_stats {
+    float    total_ms;          /* whole pipeline                                         */
+    float    walk_ms;           /* per-flowId walk kernels                                */
+    float    sort_ms;           /* key partition (radix sort)                             */
+    uint64_t touched_keys;      /* distinct flowIds that received >= 1 request            */
+    uint64_t long_segments;     /* flowIds walked by a whole wave                         */
+} sg_batch_stats;
+
+int         sg_create(const sg_config* cfg, sg_handle** out);
+void        sg_destroy(sg_handle* h);
+const char* sg_last_error(const sg_handle* h);
+
+int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n);
+int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n);
+
+/* Decide a batch. req/out are DEVICE pointers (HBM-resident); stream is a hipStream_t (NULL = default).
+ * Requests must be ordered by (ts_ms, arrival); ts_ms must be >= 0 and >= every ts of earlier batches. */
+int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream);
+
+/* Same with HOST buffers (H2D + D2H included; synchronous). */
+int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out);
+
+/* Opt-in per-call timing (adds HIP events; off by default). */
+int sg_enable_stats(sg_handle* h, int on);
+int sg_get_stats(const sg_handle* h, sg_batch_stats* out);
+
+/* Read one flowId's window: starts[sample_count] (INT64_MIN = never-created bucket),
+ * counters[sample_count * SG_NUM_EVENTS], occupy[2] = {occupied PASS, occupied PASS_REQUEST}. */
+int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
+
+/* Per-flowId {passQps, blockQps} at time now_ms (ClusterMetric.getAvg(PASS/BLOCK) without the
+ * currentWindow side effect); out has 2*n_rules doubles, HOST memory. */
+int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap);
+
+/* Library build identification (architecture the kernels were compiled for). */
+const char* sg_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SENTINEL_GPU_H */

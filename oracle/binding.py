@@ -1,0 +1,226 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+The product path (sentinel_amd) never does.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from sentinel_amd import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+# leap array kinds (sentinel_oracle.h)
+LEAP_BUCKET, LEAP_OCCUPIABLE, LEAP_FUTURE, LEAP_UNARY, LEAP_CLUSTER = range(5)
+# MetricEvent ordinals
+M_PASS, M_BLOCK, M_EXCEPTION, M_SUCCESS, M_RT, M_OCCUPIED_PASS = range(6)
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"oracle not built: {LIB_PATH} (run `make -C oracle`)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, u32, u64, d = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
+    sig = {
+        "or_d2i": (i32, [d]), "or_d2l": (i64, [d]), "or_math_round": (i64, [d]),
+        "or_leap_new": (vp, [C.c_int, C.c_int, C.c_int]), "or_leap_free": (None, [vp]),
+        "or_leap_current_window": (C.c_int, [vp, i64]),
+        "or_leap_slot_start": (i64, [vp, C.c_int]), "or_leap_slot_get": (i64, [vp, C.c_int, C.c_int]),
+        "or_leap_slot_add": (None, [vp, C.c_int, C.c_int, i64]),
+        "or_leap_slot_min_rt": (i64, [vp, C.c_int]), "or_leap_slot_add_rt": (None, [vp, C.c_int, i64]),
+        "or_leap_add": (None, [vp, i64, C.c_int, i64]),
+        "or_leap_values": (C.c_int, [vp, i64, vp]), "or_leap_get_sum": (i64, [vp, i64, C.c_int]),
+        "or_leap_valid_head": (C.c_int, [vp, i64]), "or_leap_previous_window": (C.c_int, [vp, i64]),
+        "or_leap_window_value": (C.c_int, [vp, i64]), "or_leap_interval_sec": (d, [vp]),
+        "or_leap_current_waiting": (i64, [vp, i64]), "or_leap_add_waiting": (None, [vp, i64, C.c_int]),
+        "or_leap_borrow": (vp, [vp]),
+        "or_cluster_metric_new": (vp, [C.c_int, C.c_int]),
+        "or_cluster_metric_add": (None, [vp, i64, C.c_int, i64]),
+        "or_cluster_metric_get_sum": (i64, [vp, i64, C.c_int]),
+        "or_cluster_metric_get_avg": (d, [vp, i64, C.c_int]),
+        "or_cluster_metric_try_occupy_next": (C.c_int, [vp, i64, C.c_int, C.c_int, d]),
+        "or_cluster_metric_occupied": (i64, [vp, C.c_int]),
+        "or_limiter_new": (vp, [d]), "or_limiter_free": (None, [vp]),
+        "or_limiter_add": (None, [vp, i64, C.c_int]), "or_limiter_get_sum": (i64, [vp, i64]),
+        "or_limiter_get_qps": (d, [vp, i64]), "or_limiter_can_pass": (C.c_int, [vp, i64]),
+        "or_limiter_try_pass": (C.c_int, [vp, i64]), "or_limiter_set_qps_allowed": (None, [vp, d]),
+        "or_limiter_get_qps_allowed": (d, [vp]),
+        "or_cts_new": (vp, [d, d]), "or_cts_free": (None, [vp]),
+        "or_cts_set_namespaces": (C.c_int, [vp, vp, u32]),
+        "or_cts_load_rules": (C.c_int, [vp, vp, u32]),
+        "or_cts_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_cts_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
+        "or_cts_sample_count": (C.c_int, [vp, u32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class Leap:
+    """A LeapArray of the given kind (explicit time on every call)."""
+
+    def __init__(self, kind, sample_count, interval_ms, handle=None, owner=None):
+        self._owner = owner
+        if handle is None:
+            handle = lib().or_leap_new(kind, sample_count, interval_ms)
+            if not handle:
+                raise ValueError("invalid window config")
+            self._own = True
+        else:
+            self._own = False
+        self.h = handle
+
+    def __del__(self):
+        if getattr(self, "_own", False) and self.h:
+            lib().or_leap_free(self.h)
+            self.h = None
+
+    def current_window(self, t):
+        return lib().or_leap_current_window(self.h, t)
+
+    def start(self, slot):
+        return lib().or_leap_slot_start(self.h, slot)
+
+    def get(self, slot, ev):
+        return lib().or_leap_slot_get(self.h, slot, ev)
+
+    def slot_add(self, slot, ev, n):
+        lib().or_leap_slot_add(self.h, slot, ev, n)
+
+    def add(self, t, ev, n):
+        lib().or_leap_add(self.h, t, ev, n)
+
+    def values(self, t):
+        out = (C.c_int * 64)()
+        k = lib().or_leap_values(self.h, t, out)
+        return list(out[:k])
+
+    def get_sum(self, t, ev):
+        return lib().or_leap_get_sum(self.h, t, ev)
+
+    def valid_head(self, t):
+        return lib().or_leap_valid_head(self.h, t)
+
+    def previous_window(self, t):
+        return lib().or_leap_previous_window(self.h, t)
+
+    def window_value(self, t):
+        return lib().or_leap_window_value(self.h, t)
+
+    def current_waiting(self, t):
+        return lib().or_leap_current_waiting(self.h, t)
+
+    def add_waiting(self, t, n):
+        lib().or_leap_add_waiting(self.h, t, n)
+
+    def borrow(self):
+        return Leap(None, None, None, handle=lib().or_leap_borrow(self.h), owner=self)
+
+
+class ClusterMetric(Leap):
+    """srv/flow/statistic/metric/ClusterMetric.java with explicit time."""
+
+    def __init__(self, sample_count, interval_ms):
+        h = lib().or_cluster_metric_new(sample_count, interval_ms)
+        if not h:
+            raise ValueError("invalid window config")
+        super().__init__(None, None, None, handle=h)
+        self._own = True
+
+    def add_event(self, t, ev, n):
+        lib().or_cluster_metric_add(self.h, t, ev, n)
+
+    def get_sum_event(self, t, ev):
+        return lib().or_cluster_metric_get_sum(self.h, t, ev)
+
+    def get_avg(self, t, ev):
+        return lib().or_cluster_metric_get_avg(self.h, t, ev)
+
+    def try_occupy_next(self, t, ev, acquire, threshold):
+        return lib().or_cluster_metric_try_occupy_next(self.h, t, ev, acquire, threshold)
+
+    def occupied(self, ev):
+        return lib().or_cluster_metric_occupied(self.h, ev)
+
+
+class RequestLimiter:
+    """srv/flow/statistic/limit/RequestLimiter.java with explicit time."""
+
+    def __init__(self, qps_allowed):
+        self.h = lib().or_limiter_new(qps_allowed)
+
+    def __del__(self):
+        if self.h:
+            lib().or_limiter_free(self.h)
+            self.h = None
+
+    def add(self, t, x):
+        lib().or_limiter_add(self.h, t, x)
+
+    def get_sum(self, t):
+        return lib().or_limiter_get_sum(self.h, t)
+
+    def get_qps(self, t):
+        return lib().or_limiter_get_qps(self.h, t)
+
+    def can_pass(self, t):
+        return bool(lib().or_limiter_can_pass(self.h, t))
+
+    def try_pass(self, t):
+        return bool(lib().or_limiter_try_pass(self.h, t))
+
+    def set_qps_allowed(self, q):
+        lib().or_limiter_set_qps_allowed(self.h, q)
+
+    def qps_allowed(self):
+        return lib().or_limiter_get_qps_allowed(self.h)
+
+
+class ClusterTokenService:
+    """Sequential replay of DefaultTokenService.requestToken → ClusterFlowChecker for a rule set."""
+
+    def __init__(self, exceed_count=1.0, max_occupy_ratio=1.0):
+        self.h = lib().or_cts_new(exceed_count, max_occupy_ratio)
+
+    def __del__(self):
+        if self.h:
+            lib().or_cts_free(self.h)
+            self.h = None
+
+    def set_namespaces(self, ns: np.ndarray):
+        ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
+        rc = lib().or_cts_set_namespaces(self.h, abi.ptr(ns), len(ns))
+        assert rc == 0
+
+    def load_rules(self, rules: np.ndarray):
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        rc = lib().or_cts_load_rules(self.h, abi.ptr(rules), len(rules))
+        if rc != 0:
+            raise ValueError(f"invalid rules ({rc})")
+
+    def decide(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.REQ_DTYPE)
+        out = np.zeros(len(req), dtype=abi.RES_DTYPE)
+        lib().or_cts_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
+        return out
+
+    def read_state(self, key):
+        S = lib().or_cts_sample_count(self.h, key)
+        starts = np.zeros(S, np.int64)
+        counters = np.zeros(S * abi.NUM_EVENTS, np.int64)
+        occ = np.zeros(2, np.int64)
+        rc = lib().or_cts_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ))
+        assert rc == 0
+        return starts, counters.reshape(S, abi.NUM_EVENTS), occ

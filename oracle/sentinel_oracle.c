@@ -1,0 +1,552 @@
+/*
+ * sentinel_oracle.c — TEST INFRASTRUCTURE ONLY (see sentinel_oracle.h).
+ *
+ * Sequential, explicit-time C restatement of Sentinel 1.8.5's sliding-window statistics and
+ * cluster flow checks. Every function cites the Java it follows; paths abbreviated as in SURVEY.md:
+ *   core/ = sentinel-core/src/main/java/com/alibaba/csp/sentinel/
+ *   srv/  = sentinel-cluster/sentinel-cluster-server-default/src/main/java/com/alibaba/csp/sentinel/cluster/
+ * Built with -fwrapv so signed overflow wraps exactly like Java long/int arithmetic.
+ */
+#include "sentinel_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ===================================================================================== */
+/* Java numeric semantics                                                                */
+/* ===================================================================================== */
+
+/* JLS §5.1.3 narrowing double → int: NaN → 0, saturate at the int range, else truncate. */
+int32_t or_d2i(double x) {
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
+/* JLS §5.1.3 narrowing double → long. */
+int64_t or_d2l(double x) {
+    if (x != x) return 0;
+    if (x >= 9223372036854775807.0) return INT64_MAX;
+    if (x <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)x;
+}
+
+/* java.lang.Math.round(double) as implemented since JDK 7u (exact floor(x + 1/2)). */
+int64_t or_math_round(double a) {
+    int64_t bits;
+    memcpy(&bits, &a, 8);
+    int64_t biased_exp = (bits & 0x7FF0000000000000LL) >> 52;
+    int64_t shift = (52 - 1 + 1023) - biased_exp;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    return or_d2l(a);
+}
+
+/* ===================================================================================== */
+/* LeapArray family                                                                      */
+/* ===================================================================================== */
+
+#define OR_MAX_EV 7
+#define OR_STAT_MAX_RT 5000 /* SentinelConfig.DEFAULT_STATISTIC_MAX_RT, core/config/SentinelConfig.java:69 */
+
+typedef struct or_bucket {
+    int64_t start;
+    int64_t c[OR_MAX_EV];
+    int64_t min_rt;
+} or_bucket;
+
+struct or_leap {
+    int kind;
+    int S, wl, interval;   /* sampleCount, windowLengthInMs, intervalInMs (LeapArray.java:43-46) */
+    double isec;           /* intervalInSecond = intervalInMs / 1000.0 (LeapArray.java:68)        */
+    uint8_t* present;      /* AtomicReferenceArray slot != null                                   */
+    or_bucket* b;
+    or_bucket detached;    /* LeapArray.java:197-199: "should not go through here"                */
+    struct or_leap* borrow;            /* OccupiableBucketLeapArray.borrowArray                   */
+    int64_t occ[OR_MAX_EV];            /* ClusterMetricLeapArray.occupyCounter                    */
+    int has_occupied;                  /* ClusterMetricLeapArray.hasOccupied                      */
+};
+
+static or_bucket* slot_ptr(or_leap* l, int slot) {
+    return slot == -2 ? &l->detached : &l->b[slot];
+}
+static const or_bucket* slot_cptr(const or_leap* l, int slot) {
+    return slot == -2 ? &l->detached : &l->b[slot];
+}
+
+or_leap* or_leap_new(int kind, int sample_count, int interval_ms) {
+    /* LeapArray(int sampleCount, int intervalInMs), base/LeapArray.java:61-72 */
+    if (sample_count <= 0 || interval_ms <= 0 || interval_ms % sample_count != 0) return NULL;
+    or_leap* l = (or_leap*)calloc(1, sizeof(or_leap));
+    l->kind = kind;
+    l->S = sample_count;
+    l->wl = interval_ms / sample_count;
+    l->interval = interval_ms;
+    l->isec = interval_ms / 1000.0;
+    l->present = (uint8_t*)calloc((size_t)sample_count, 1);
+    l->b = (or_bucket*)calloc((size_t)sample_count, sizeof(or_bucket));
+    for (int i = 0; i < sample_count; i++) l->b[i].start = INT64_MIN;
+    l->detached.start = INT64_MIN;
+    if (kind == OR_LEAP_OCCUPIABLE) {
+        /* OccupiableBucketLeapArray.java:33-37 */
+        l->borrow = or_leap_new(OR_LEAP_FUTURE, sample_count, interval_ms);
+    }
+    return l;
+}
+
+void or_leap_free(or_leap* l) {
+    if (!l) return;
+    if (l->borrow) or_leap_free(l->borrow);
+    free(l->present);
+    free(l->b);
+    free(l);
+}
+
+or_leap* or_leap_borrow(or_leap* l) { return l->borrow; }
+double or_leap_interval_sec(const or_leap* l) { return l->isec; }
+
+/* LeapArray.isWindowDeprecated(long, WindowWrap), base/LeapArray.java:270-272;
+ * FutureBucketLeapArray overrides it, metric/occupy/FutureBucketLeapArray.java:49-52. */
+static int is_deprecated(const or_leap* l, int64_t t, const or_bucket* w) {
+    if (l->kind == OR_LEAP_FUTURE) return t >= w->start;
+    return t - w->start > l->interval;
+}
+
+/* LeapArray.getWindowValue(long), base/LeapArray.java:244-257 + WindowWrap.isTimeInWindow :87-89 */
+int or_leap_window_value(const or_leap* l, int64_t t) {
+    if (t < 0) return -1;
+    int idx = (int)((t / l->wl) % l->S);
+    if (!l->present[idx]) return -1;
+    const or_bucket* w = &l->b[idx];
+    if (!(w->start <= t && t < w->start + l->wl)) return -1;
+    return idx;
+}
+
+static void zero_counters(or_bucket* w) {
+    for (int e = 0; e < OR_MAX_EV; e++) w->c[e] = 0;
+    w->min_rt = OR_STAT_MAX_RT; /* MetricBucket.initMinRt, data/MetricBucket.java:52-54 */
+}
+
+/* newEmptyBucket(timeMillis) per subclass. */
+static void new_empty_bucket(or_leap* l, or_bucket* w, int64_t t) {
+    zero_counters(w);
+    if (l->kind == OR_LEAP_OCCUPIABLE) {
+        /* OccupiableBucketLeapArray.newEmptyBucket, :40-48: MetricBucket.reset(borrowBucket) copies
+         * all 6 counters (data/MetricBucket.java:43-50); minRt re-initialised. */
+        int bs = or_leap_window_value(l->borrow, t);
+        if (bs >= 0) {
+            for (int e = 0; e < OR_M_NUM; e++) w->c[e] = l->borrow->b[bs].c[e];
+        }
+    }
+}
+
+/* ClusterMetricLeapArray.transferOccupyToBucket, srv/flow/statistic/metric/ClusterMetricLeapArray.java:56-71 */
+static void cluster_transfer_occupy(or_leap* l, or_bucket* w) {
+    if (l->has_occupied) {
+        w->c[SG_EV_OCCUPIED_PASS] += l->occ[SG_EV_PASS]; /* transferOccupiedCount (sum, no reset) */
+        w->c[SG_EV_PASS] += l->occ[SG_EV_PASS];          /* transferOccupiedThenReset            */
+        l->occ[SG_EV_PASS] = 0;
+        w->c[SG_EV_PASS_REQUEST] += l->occ[SG_EV_PASS_REQUEST];
+        l->occ[SG_EV_PASS_REQUEST] = 0;
+        l->has_occupied = 0;
+    }
+}
+
+/* resetWindowTo(w, startTime) per subclass. */
+static void reset_window_to(or_leap* l, or_bucket* w, int64_t start) {
+    w->start = start;
+    switch (l->kind) {
+    case OR_LEAP_OCCUPIABLE: {
+        /* OccupiableBucketLeapArray.resetWindowTo, :50-63 */
+        int bs = or_leap_window_value(l->borrow, start);
+        zero_counters(w);
+        if (bs >= 0) {
+            /* w.value().addPass((int)borrowBucket.pass()): long → int narrowing keeps the low 32 bits */
+            w->c[OR_M_PASS] += (int64_t)(int32_t)l->borrow->b[bs].c[OR_M_PASS];
+        }
+        break;
+    }
+    case OR_LEAP_CLUSTER:
+        /* ClusterMetricLeapArray.resetWindowTo, :49-54 */
+        zero_counters(w);
+        cluster_transfer_occupy(l, w);
+        break;
+    default:
+        /* BucketLeapArray / FutureBucketLeapArray / UnaryLeapArray: reset value */
+        zero_counters(w);
+        break;
+    }
+}
+
+/* LeapArray.currentWindow(long timeMillis), base/LeapArray.java:116-202 (single-threaded: the CAS /
+ * tryLock / yield branches collapse to their successful arm). */
+int or_leap_current_window(or_leap* l, int64_t t) {
+    if (t < 0) return -1;
+    int idx = (int)((t / l->wl) % l->S);                 /* calculateTimeIdx :100-104   */
+    int64_t ws = t - t % l->wl;                          /* calculateWindowStart :106-108 */
+    if (!l->present[idx]) {                              /* (1) bucket absent → create */
+        or_bucket* w = &l->b[idx];
+        new_empty_bucket(l, w, t);
+        w->start = ws;
+        l->present[idx] = 1;
+        return idx;
+    }
+    or_bucket* old = &l->b[idx];
+    if (ws == old->start) return idx;                    /* (2) up to date             */
+    if (ws > old->start) {                               /* (3) deprecated → reset     */
+        reset_window_to(l, old, ws);
+        return idx;
+    }
+    /* ws < old.start: a fresh bucket outside the array; writes to it are lost. */
+    new_empty_bucket(l, &l->detached, t);
+    l->detached.start = ws;
+    return -2;
+}
+
+int64_t or_leap_slot_start(const or_leap* l, int slot) {
+    if (slot >= 0 && !l->present[slot]) return INT64_MIN;
+    return slot_cptr(l, slot)->start;
+}
+int64_t or_leap_slot_get(const or_leap* l, int slot, int ev) { return slot_cptr(l, slot)->c[ev]; }
+void or_leap_slot_add(or_leap* l, int slot, int ev, int64_t n) { slot_ptr(l, slot)->c[ev] += n; }
+int64_t or_leap_slot_min_rt(const or_leap* l, int slot) { return slot_cptr(l, slot)->min_rt; }
+
+/* MetricBucket.addRT, data/MetricBucket.java:126-132 */
+void or_leap_slot_add_rt(or_leap* l, int slot, int64_t rt) {
+    or_bucket* w = slot_ptr(l, slot);
+    w->c[OR_M_RT] += rt;
+    if (rt < w->min_rt) w->min_rt = rt;
+}
+
+void or_leap_add(or_leap* l, int64_t t, int ev, int64_t n) {
+    int s = or_leap_current_window(l, t);
+    if (s == -1) return; /* Java would NPE; callers never pass t < 0 */
+    or_leap_slot_add(l, s, ev, n);
+}
+
+/* LeapArray.values(long), base/LeapArray.java:329-344 */
+int or_leap_values(const or_leap* l, int64_t t, int* out_slots) {
+    if (t < 0) return 0;
+    int k = 0;
+    for (int i = 0; i < l->S; i++) {
+        if (!l->present[i] || is_deprecated(l, t, &l->b[i])) continue;
+        if (out_slots) out_slots[k] = i;
+        k++;
+    }
+    return k;
+}
+
+/* ArrayMetric/ClusterMetric.getSum: currentWindow(); Σ values() (metric/ArrayMetric.java:301-310,
+ * srv/flow/statistic/metric/ClusterMetric.java:53-62). */
+int64_t or_leap_get_sum(or_leap* l, int64_t t, int ev) {
+    or_leap_current_window(l, t);
+    int64_t sum = 0;
+    if (t < 0) return 0;
+    for (int i = 0; i < l->S; i++) {
+        if (!l->present[i] || is_deprecated(l, t, &l->b[i])) continue;
+        sum += l->b[i].c[ev];
+    }
+    return sum;
+}
+
+/* LeapArray.getValidHead(long), base/LeapArray.java:353-363; its isWindowDeprecated(wrap) reads
+ * TimeUtil.currentTimeMillis(), which in replay is the same t. */
+int or_leap_valid_head(const or_leap* l, int64_t t) {
+    int idx = (int)(((t + l->wl) / l->wl) % l->S);
+    if (!l->present[idx] || is_deprecated(l, t, &l->b[idx])) return -1;
+    return idx;
+}
+
+/* LeapArray.getPreviousWindow(long), base/LeapArray.java:210-227 (deprecation at the *current*
+ * time = the original t in replay, since isWindowDeprecated(wrap) reads TimeUtil). */
+int or_leap_previous_window(const or_leap* l, int64_t t) {
+    if (t < 0) return -1;
+    /* For t < windowLength the Java index (t - wl) / wl % S is <= 0: -1 throws
+     * IndexOutOfBoundsException, 0 aliases slot 0. Epoch-time callers never get here. */
+    if (t < l->wl) return -1;
+    int64_t now = t;
+    int idx = (int)(((t - l->wl) / l->wl) % l->S);
+    int64_t tp = t - l->wl;
+    if (!l->present[idx] || is_deprecated(l, now, &l->b[idx])) return -1;
+    if (l->b[idx].start + l->wl < tp) return -1;
+    return idx;
+}
+
+/* OccupiableBucketLeapArray.currentWaiting, :66-75 */
+int64_t or_leap_current_waiting(or_leap* l, int64_t t) {
+    or_leap_current_window(l->borrow, t);
+    int64_t w = 0;
+    for (int i = 0; i < l->borrow->S; i++) {
+        if (!l->borrow->present[i] || is_deprecated(l->borrow, t, &l->borrow->b[i])) continue;
+        w += l->borrow->b[i].c[OR_M_PASS];
+    }
+    return w;
+}
+
+/* OccupiableBucketLeapArray.addWaiting, :77-81 */
+void or_leap_add_waiting(or_leap* l, int64_t t, int acquire) {
+    int s = or_leap_current_window(l->borrow, t);
+    if (s == -1) return;
+    or_leap_slot_add(l->borrow, s, OR_M_PASS, acquire);
+}
+
+/* ===================================================================================== */
+/* ClusterMetric (srv/flow/statistic/metric/ClusterMetric.java:28-99)                    */
+/* ===================================================================================== */
+
+or_leap* or_cluster_metric_new(int sample_count, int interval_ms) {
+    return or_leap_new(OR_LEAP_CLUSTER, sample_count, interval_ms);
+}
+
+/* ClusterMetric.add, :39-41 */
+void or_cluster_metric_add(or_leap* m, int64_t t, int ev, int64_t n) { or_leap_add(m, t, ev, n); }
+
+/* ClusterMetric.getSum, :53-62 */
+int64_t or_cluster_metric_get_sum(or_leap* m, int64_t t, int ev) { return or_leap_get_sum(m, t, ev); }
+
+/* ClusterMetric.getAvg, :70-72 (long / double) */
+double or_cluster_metric_get_avg(or_leap* m, int64_t t, int ev) {
+    return (double)or_leap_get_sum(m, t, ev) / m->isec;
+}
+
+/* ClusterMetricLeapArray.getFirstCountOfWindow, ClusterMetricLeapArray.java:83-92 */
+static int64_t cluster_first_count_of_window(const or_leap* m, int64_t t, int ev) {
+    int h = or_leap_valid_head(m, t);
+    if (h < 0) return 0;
+    return m->b[h].c[ev];
+}
+
+int64_t or_cluster_metric_occupied(const or_leap* m, int ev) { return m->occ[ev]; }
+
+/* ClusterMetric.tryOccupyNext, :79-87, and canOccupy, :89-98 */
+int or_cluster_metric_try_occupy_next(or_leap* m, int64_t t, int ev, int acquire, double threshold) {
+    double latest_qps = or_cluster_metric_get_avg(m, t, SG_EV_PASS);
+    int64_t head_pass = cluster_first_count_of_window(m, t, ev);
+    int64_t occupied = m->occ[ev];
+    /* latestQps + (acquireCount + occupiedCount) - headPass <= threshold:
+     * int + long → long, double + long → double, double - long → double */
+    int can = latest_qps + (double)((int64_t)acquire + occupied) - (double)head_pass <= threshold;
+    if (!can) return 0;
+    /* ClusterMetricLeapArray.addOccupyPass, :73-77 */
+    m->occ[SG_EV_PASS] += acquire;
+    m->occ[SG_EV_PASS_REQUEST] += 1;
+    m->has_occupied = 1;
+    or_cluster_metric_add(m, t, SG_EV_WAITING, acquire);
+    return 1000 / m->S; /* hard-coded 1000, ClusterMetric.java:86 */
+}
+
+/* ===================================================================================== */
+/* RequestLimiter (srv/flow/statistic/limit/RequestLimiter.java:29-88)                   */
+/* ===================================================================================== */
+
+struct or_limiter {
+    double qps_allowed;
+    or_leap* data; /* new UnaryLeapArray(10, 1000), :35-37 */
+};
+
+or_limiter* or_limiter_new(double qps_allowed) {
+    or_limiter* r = (or_limiter*)calloc(1, sizeof(or_limiter));
+    r->qps_allowed = qps_allowed;
+    r->data = or_leap_new(OR_LEAP_UNARY, 10, 1000);
+    return r;
+}
+void or_limiter_free(or_limiter* r) {
+    if (!r) return;
+    or_leap_free(r->data);
+    free(r);
+}
+void or_limiter_add(or_limiter* r, int64_t t, int x) { or_leap_add(r->data, t, 0, x); } /* :49-51 */
+int64_t or_limiter_get_sum(or_limiter* r, int64_t t) { return or_leap_get_sum(r->data, t, 0); } /* :53-62 */
+double or_limiter_get_qps(or_limiter* r, int64_t t) {                                          /* :64-66 */
+    return (double)or_limiter_get_sum(r, t) / r->data->isec;
+}
+int or_limiter_can_pass(or_limiter* r, int64_t t) { return or_limiter_get_qps(r, t) + 1 <= r->qps_allowed; } /* :72-74 */
+int or_limiter_try_pass(or_limiter* r, int64_t t) {                                           /* :81-87 */
+    if (or_limiter_can_pass(r, t)) {
+        or_limiter_add(r, t, 1);
+        return 1;
+    }
+    return 0;
+}
+void or_limiter_set_qps_allowed(or_limiter* r, double q) { r->qps_allowed = q; }
+double or_limiter_get_qps_allowed(const or_limiter* r) { return r->qps_allowed; }
+
+/* ===================================================================================== */
+/* Cluster token service: DefaultTokenService.requestToken → ClusterFlowChecker          */
+/* ===================================================================================== */
+
+typedef struct or_cts_rule {
+    int64_t flow_id;
+    double count;
+    int32_t threshold_type;
+    int32_t ns;
+    or_leap* metric; /* ClusterMetricStatistics.METRIC_MAP[flowId] */
+} or_cts_rule;
+
+struct or_cts {
+    double exceed_count;
+    double max_occupy_ratio;
+    or_cts_rule* rules;
+    uint32_t n_rules;
+    sg_namespace* ns;
+    or_limiter** limiters; /* GlobalRequestLimiter.GLOBAL_QPS_LIMITER_MAP (null = no limiter) */
+    uint32_t n_ns;
+};
+
+or_cts* or_cts_new(double exceed_count, double max_occupy_ratio) {
+    or_cts* s = (or_cts*)calloc(1, sizeof(or_cts));
+    s->exceed_count = exceed_count;
+    s->max_occupy_ratio = max_occupy_ratio;
+    return s;
+}
+
+void or_cts_free(or_cts* s) {
+    if (!s) return;
+    for (uint32_t i = 0; i < s->n_rules; i++) or_leap_free(s->rules[i].metric);
+    free(s->rules);
+    for (uint32_t i = 0; i < s->n_ns; i++) or_limiter_free(s->limiters[i]);
+    free(s->limiters);
+    free(s->ns);
+    free(s);
+}
+
+int or_cts_set_namespaces(or_cts* s, const sg_namespace* ns, uint32_t n) {
+    /* Limiters persist across config updates (GlobalRequestLimiter.initIfAbsent :32-37,
+     * applyMaxQpsChange :73-80); a namespace whose limiter is switched off loses it. */
+    or_limiter** lim = (or_limiter**)calloc(n ? n : 1, sizeof(or_limiter*));
+    for (uint32_t i = 0; i < n; i++) {
+        or_limiter* old = i < s->n_ns ? s->limiters[i] : NULL;
+        if (ns[i].limiter_enabled) {
+            lim[i] = old ? old : or_limiter_new(ns[i].max_allowed_qps);
+            or_limiter_set_qps_allowed(lim[i], ns[i].max_allowed_qps);
+            if (old) s->limiters[i] = NULL;
+        }
+    }
+    for (uint32_t i = 0; i < s->n_ns; i++) or_limiter_free(s->limiters[i]);
+    free(s->limiters);
+    free(s->ns);
+    s->ns = (sg_namespace*)calloc(n ? n : 1, sizeof(sg_namespace));
+    memcpy(s->ns, ns, n * sizeof(sg_namespace));
+    s->limiters = lim;
+    s->n_ns = n;
+    return 0;
+}
+
+/* ClusterFlowRuleManager.applyClusterFlowRule, srv/flow/rule/ClusterFlowRuleManager.java:325-375:
+ * a flowId that survives keeps its ClusterMetric (putMetricIfAbsent :361, even if the window
+ * config changed); removed flowIds lose theirs (clearAndResetRulesConditional :287-302). */
+int or_cts_load_rules(or_cts* s, const sg_flow_rule* rules, uint32_t n) {
+    or_cts_rule* nr = (or_cts_rule*)calloc(n ? n : 1, sizeof(or_cts_rule));
+    for (uint32_t i = 0; i < n; i++) {
+        const sg_flow_rule* r = &rules[i];
+        nr[i].flow_id = r->flow_id;
+        nr[i].count = r->count;
+        nr[i].threshold_type = r->threshold_type;
+        nr[i].ns = r->namespace_id;
+        for (uint32_t j = 0; j < s->n_rules; j++) {
+            if (s->rules[j].metric && s->rules[j].flow_id == r->flow_id) {
+                nr[i].metric = s->rules[j].metric;
+                s->rules[j].metric = NULL;
+                break;
+            }
+        }
+        if (!nr[i].metric) nr[i].metric = or_cluster_metric_new(r->sample_count, r->window_interval_ms);
+        if (!nr[i].metric) {
+            for (uint32_t k = 0; k <= i; k++) or_leap_free(nr[k].metric);
+            free(nr);
+            return SG_E_INVAL;
+        }
+    }
+    for (uint32_t j = 0; j < s->n_rules; j++) or_leap_free(s->rules[j].metric);
+    free(s->rules);
+    s->rules = nr;
+    s->n_rules = n;
+    return 0;
+}
+
+/* ClusterFlowChecker.calcGlobalThreshold, srv/flow/ClusterFlowChecker.java:38-48 */
+static double calc_global_threshold(const or_cts* s, const or_cts_rule* r) {
+    if (r->threshold_type == SG_THRESHOLD_GLOBAL) return r->count;
+    int connected = 0;
+    if (r->ns >= 0 && (uint32_t)r->ns < s->n_ns) connected = s->ns[r->ns].connected_count;
+    return r->count * connected;
+}
+
+static sg_result mk(int32_t status, int32_t remaining, int32_t wait) {
+    sg_result x;
+    x.status = status;
+    x.remaining = remaining;
+    x.wait_ms = wait;
+    return x;
+}
+
+/* ClusterFlowChecker.acquireClusterToken, srv/flow/ClusterFlowChecker.java:55-112 */
+static sg_result acquire_cluster_token(or_cts* s, or_cts_rule* r, int64_t t, int acquire, int prio) {
+    /* allowProceed → GlobalRequestLimiter.tryPass(namespace), :50-53, GlobalRequestLimiter.java:46-55 */
+    if (r->ns < 0 || (uint32_t)r->ns >= s->n_ns) return mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0); /* null ns */
+    or_limiter* lim = s->limiters[r->ns];
+    if (lim && !or_limiter_try_pass(lim, t)) return mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0);
+
+    or_leap* m = r->metric;
+    double latest_qps = or_cluster_metric_get_avg(m, t, SG_EV_PASS);
+    double global_threshold = calc_global_threshold(s, r) * s->exceed_count;
+    double next_remaining = global_threshold - latest_qps - acquire;
+
+    if (next_remaining >= 0) {
+        or_cluster_metric_add(m, t, SG_EV_PASS, acquire);
+        or_cluster_metric_add(m, t, SG_EV_PASS_REQUEST, 1);
+        if (prio) or_cluster_metric_add(m, t, SG_EV_OCCUPIED_PASS, acquire);
+        return mk(SG_STATUS_OK, or_d2i(next_remaining), 0);
+    }
+    if (prio) {
+        double occupy_avg = or_cluster_metric_get_avg(m, t, SG_EV_WAITING);
+        if (occupy_avg <= s->max_occupy_ratio * global_threshold) {
+            int wait = or_cluster_metric_try_occupy_next(m, t, SG_EV_PASS, acquire, global_threshold);
+            if (wait > 0) return mk(SG_STATUS_SHOULD_WAIT, 0, wait);
+        }
+    }
+    or_cluster_metric_add(m, t, SG_EV_BLOCK, acquire);
+    or_cluster_metric_add(m, t, SG_EV_BLOCK_REQUEST, 1);
+    if (prio) or_cluster_metric_add(m, t, SG_EV_OCCUPIED_BLOCK, acquire);
+    return mk(SG_STATUS_BLOCKED, 0, 0);
+}
+
+/* DefaultTokenService.requestToken, srv/flow/DefaultTokenService.java:39-50 */
+int or_cts_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t key = req[i].key & SG_KEY_INDEX;
+        int prio = (req[i].key & SG_KEY_PRIO) != 0;
+        if (key == SG_KEY_BAD || req[i].acquire <= 0) {           /* notValidRequest :87-89 */
+            out[i] = mk(SG_STATUS_BAD_REQUEST, 0, 0);
+            continue;
+        }
+        if (key >= s->n_rules) {                                    /* rule == null :44-47 */
+            out[i] = mk(SG_STATUS_NO_RULE_EXISTS, 0, 0);
+            continue;
+        }
+        out[i] = acquire_cluster_token(s, &s->rules[key], req[i].ts_ms, req[i].acquire, prio);
+    }
+    return 0;
+}
+
+int or_cts_sample_count(const or_cts* s, uint32_t key) {
+    if (key >= s->n_rules) return -1;
+    return s->rules[key].metric->S;
+}
+
+int or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
+    if (key >= s->n_rules) return SG_E_INVAL;
+    const or_leap* m = s->rules[key].metric;
+    for (int j = 0; j < m->S; j++) {
+        starts[j] = m->present[j] ? m->b[j].start : INT64_MIN;
+        for (int e = 0; e < SG_NUM_EVENTS; e++) counters[j * SG_NUM_EVENTS + e] = m->present[j] ? m->b[j].c[e] : 0;
+    }
+    occupy[0] = m->occ[SG_EV_PASS];
+    occupy[1] = m->occ[SG_EV_PASS_REQUEST];
+    return 0;
+}

@@ -1,0 +1,105 @@
+/*
+ * sentinel_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * A sequential, explicit-time CPU restatement of the Sentinel 1.8.5 hot path (Java, at
+ * /root/reference). It is the parity checker for the HIP engine in sentinel_amd/csrc and the
+ * CPU-baseline leg of bench.py. Nothing in the product path may link or call it: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load liboracle.so.
+ *
+ * Replay model: every call takes the TimeUtil.currentTimeMillis() value
+ * explicitly (the reference tests virtualise it the same way, AbstractTimeBasedTest.java:36-58),
+ * and a batch is replayed strictly in (timestamp, arrival) order on one thread.
+ *
+ * Pinning: tests/test_oracle_kat.py restates every known-answer test the reference holds for these
+ * classes (LeapArrayTest, BucketLeapArrayTest, OccupiableBucketLeapArrayTest,
+ * FutureBucketLeapArrayTest, ClusterMetricTest, RequestLimiterTest, GlobalRequestLimiterTest, …)
+ * at several start offsets. The reference itself (Java) cannot be built in this image (no JDK).
+ */
+#ifndef SENTINEL_ORACLE_H
+#define SENTINEL_ORACLE_H
+
+#include <stdint.h>
+#include "../include/sentinel_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------- Java numeric semantics (JLS §5.1.3, §15.17) ---------- */
+int32_t or_d2i(double x);            /* (int) double : saturating, NaN → 0            */
+int64_t or_d2l(double x);            /* (long) double                                  */
+int64_t or_math_round(double x);     /* Math.round(double): floor(x + 1/2), exact      */
+
+/* ---------- LeapArray family ---------- */
+enum {
+    OR_LEAP_BUCKET     = 0,  /* BucketLeapArray (MetricBucket)              metric/BucketLeapArray.java        */
+    OR_LEAP_OCCUPIABLE = 1,  /* OccupiableBucketLeapArray (+ borrow array)  metric/occupy/OccupiableBucketLeapArray.java */
+    OR_LEAP_FUTURE     = 2,  /* FutureBucketLeapArray                       metric/occupy/FutureBucketLeapArray.java */
+    OR_LEAP_UNARY      = 3,  /* UnaryLeapArray (LongAdder)                  base/UnaryLeapArray.java            */
+    OR_LEAP_CLUSTER    = 4,  /* ClusterMetricLeapArray (7 events + occupy)  srv .../metric/ClusterMetricLeapArray.java */
+};
+
+/* MetricEvent ordinals (core/slots/statistic/MetricEvent.java:21-39). */
+enum { OR_M_PASS = 0, OR_M_BLOCK, OR_M_EXCEPTION, OR_M_SUCCESS, OR_M_RT, OR_M_OCCUPIED_PASS, OR_M_NUM };
+
+typedef struct or_leap or_leap;
+
+or_leap* or_leap_new(int kind, int sample_count, int interval_ms);
+void     or_leap_free(or_leap* l);
+/* currentWindow(t): returns slot index 0..S-1, -1 for t < 0 (null), -2 for a detached bucket. */
+int      or_leap_current_window(or_leap* l, int64_t t);
+int64_t  or_leap_slot_start(const or_leap* l, int slot);        /* INT64_MIN when never created */
+int64_t  or_leap_slot_get(const or_leap* l, int slot, int ev);  /* slot -2 = detached bucket   */
+void     or_leap_slot_add(or_leap* l, int slot, int ev, int64_t n);
+int64_t  or_leap_slot_min_rt(const or_leap* l, int slot);
+void     or_leap_slot_add_rt(or_leap* l, int slot, int64_t rt);  /* MetricBucket.addRT          */
+/* currentWindow(t).value().add(ev, n) */
+void     or_leap_add(or_leap* l, int64_t t, int ev, int64_t n);
+/* values(t): number of valid buckets and their slots (out may be NULL). */
+int      or_leap_values(const or_leap* l, int64_t t, int* out_slots);
+/* getSum(ev) at t: currentWindow(t) then Σ values(t). */
+int64_t  or_leap_get_sum(or_leap* l, int64_t t, int ev);
+int      or_leap_valid_head(const or_leap* l, int64_t t);        /* getValidHead, -1 = null     */
+int      or_leap_previous_window(const or_leap* l, int64_t t);   /* getPreviousWindow, -1 = null */
+int      or_leap_window_value(const or_leap* l, int64_t t);      /* getWindowValue, -1 = null    */
+double   or_leap_interval_sec(const or_leap* l);
+/* OccupiableBucketLeapArray.currentWaiting / addWaiting (t explicit). */
+int64_t  or_leap_current_waiting(or_leap* l, int64_t t);
+void     or_leap_add_waiting(or_leap* l, int64_t t, int acquire);
+or_leap* or_leap_borrow(or_leap* l);
+
+/* ---------- ClusterMetric (srv/flow/statistic/metric/ClusterMetric.java) ---------- */
+or_leap* or_cluster_metric_new(int sample_count, int interval_ms);
+void     or_cluster_metric_add(or_leap* m, int64_t t, int ev, int64_t n);
+int64_t  or_cluster_metric_get_sum(or_leap* m, int64_t t, int ev);
+double   or_cluster_metric_get_avg(or_leap* m, int64_t t, int ev);
+int      or_cluster_metric_try_occupy_next(or_leap* m, int64_t t, int ev, int acquire, double threshold);
+int64_t  or_cluster_metric_occupied(const or_leap* m, int ev);
+
+/* ---------- RequestLimiter (srv/flow/statistic/limit/RequestLimiter.java) ---------- */
+typedef struct or_limiter or_limiter;
+or_limiter* or_limiter_new(double qps_allowed);
+void        or_limiter_free(or_limiter* r);
+void        or_limiter_add(or_limiter* r, int64_t t, int x);
+int64_t     or_limiter_get_sum(or_limiter* r, int64_t t);
+double      or_limiter_get_qps(or_limiter* r, int64_t t);
+int         or_limiter_can_pass(or_limiter* r, int64_t t);
+int         or_limiter_try_pass(or_limiter* r, int64_t t);
+void        or_limiter_set_qps_allowed(or_limiter* r, double q);
+double      or_limiter_get_qps_allowed(const or_limiter* r);
+
+/* ---------- cluster token service replay (DefaultTokenService + ClusterFlowChecker) ---------- */
+typedef struct or_cts or_cts;
+or_cts* or_cts_new(double exceed_count, double max_occupy_ratio);
+void    or_cts_free(or_cts* s);
+int     or_cts_set_namespaces(or_cts* s, const sg_namespace* ns, uint32_t n);
+int     or_cts_load_rules(or_cts* s, const sg_flow_rule* rules, uint32_t n);
+/* Replays requests sequentially in array order. Returns 0. */
+int     or_cts_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
+int     or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
+int     or_cts_sample_count(const or_cts* s, uint32_t key);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

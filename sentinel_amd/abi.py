@@ -1,0 +1,85 @@
+"""ctypes mirror of include/sentinel_gpu.h (the C ABI of libsentinel_gpu.so).
+
+Struct layouts here must match the header byte for byte; tests/test_abi.py checks the sizes.
+Status codes follow TokenResultStatus (sentinel-core/.../cluster/TokenResultStatus.java:27-53).
+"""
+import ctypes as C
+
+import numpy as np
+
+SG_OK = 0
+SG_E_INVAL = -1
+SG_E_DEVICE = -2
+SG_E_NOMEM = -3
+SG_E_UNSUPPORTED = -4
+SG_E_TIME = -5
+SG_E_CAPACITY = -6
+
+BAD_REQUEST = -4
+TOO_MANY_REQUEST = -2
+FAIL = -1
+OK = 0
+BLOCKED = 1
+SHOULD_WAIT = 2
+NO_RULE_EXISTS = 3
+
+THRESHOLD_AVG_LOCAL = 0
+THRESHOLD_GLOBAL = 1
+
+# ClusterFlowEvent ordinals (srv/flow/statistic/data/ClusterFlowEvent.java:22-52)
+EV_PASS, EV_BLOCK, EV_PASS_REQUEST, EV_BLOCK_REQUEST, EV_OCCUPIED_PASS, EV_OCCUPIED_BLOCK, EV_WAITING = range(7)
+NUM_EVENTS = 7
+
+KEY_PRIO = 0x80000000
+KEY_INDEX = 0x7FFFFFFF
+KEY_NO_RULE = 0x7FFFFFFF
+KEY_BAD = 0x7FFFFFFE
+
+MAX_SAMPLE_COUNT = 64
+INT64_MIN = -(1 << 63)
+
+
+class sg_config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32), ("exceed_count", C.c_double),
+                ("max_occupy_ratio", C.c_double), ("max_batch", C.c_uint64)]
+
+
+class sg_flow_rule(C.Structure):
+    _fields_ = [("flow_id", C.c_int64), ("count", C.c_double), ("threshold_type", C.c_int32),
+                ("sample_count", C.c_int32), ("window_interval_ms", C.c_int32), ("namespace_id", C.c_int32)]
+
+
+class sg_namespace(C.Structure):
+    _fields_ = [("limiter_enabled", C.c_int32), ("connected_count", C.c_int32), ("max_allowed_qps", C.c_double)]
+
+
+class sg_req(C.Structure):
+    _fields_ = [("ts_ms", C.c_int64), ("key", C.c_uint32), ("acquire", C.c_int32)]
+
+
+class sg_result(C.Structure):
+    _fields_ = [("status", C.c_int32), ("remaining", C.c_int32), ("wait_ms", C.c_int32)]
+
+
+class sg_batch_stats(C.Structure):
+    _fields_ = [("total_ms", C.c_float), ("walk_ms", C.c_float), ("sort_ms", C.c_float),
+                ("touched_keys", C.c_uint64), ("long_segments", C.c_uint64)]
+
+
+# numpy views of the request / result records (same layout as the C structs)
+REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4")], align=True)
+RES_DTYPE = np.dtype([("status", "<i4"), ("remaining", "<i4"), ("wait_ms", "<i4")], align=True)
+RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
+                       ("window_interval_ms", "<i4"), ("namespace_id", "<i4")], align=True)
+NS_DTYPE = np.dtype([("limiter_enabled", "<i4"), ("connected_count", "<i4"), ("max_allowed_qps", "<f8")],
+                    align=True)
+
+assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
+assert RES_DTYPE.itemsize == C.sizeof(sg_result) == 12
+assert RULE_DTYPE.itemsize == C.sizeof(sg_flow_rule) == 32
+assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
+
+
+def ptr(a: np.ndarray) -> C.c_void_p:
+    assert a.flags["C_CONTIGUOUS"]
+    return C.c_void_p(a.ctypes.data)

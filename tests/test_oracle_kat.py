@@ -1,0 +1,366 @@
+"""Known-answer tests: the reference's own unit tests for the hot path, restated against the oracle.
+
+Each test cites the Java test it restates (paths under /root/reference). The Java tests run on a
+PowerMock-virtualised clock seeded with System.currentTimeMillis(); here every one runs at the
+start offsets in conftest.OFFSETS (aligned and unaligned to the bucket length).
+"""
+import math
+
+import pytest
+
+from oracle.binding import (LEAP_BUCKET, LEAP_FUTURE, LEAP_OCCUPIABLE, LEAP_UNARY, M_BLOCK, M_EXCEPTION,
+                            M_PASS, M_RT, M_SUCCESS, ClusterMetric, ClusterTokenService, Leap,
+                            RequestLimiter, lib)
+from sentinel_amd import abi
+import numpy as np
+
+# ---------------------------------------------------------------- Java numerics (JLS §5.1.3)
+
+
+def test_java_d2i_saturation():
+    L = lib()
+    assert L.or_d2i(float("nan")) == 0
+    assert L.or_d2i(1e300) == 2**31 - 1
+    assert L.or_d2i(-1e300) == -(2**31)
+    assert L.or_d2i(2147483647.9) == 2**31 - 1
+    assert L.or_d2i(-3.99) == -3
+    assert L.or_d2i(3.99) == 3
+    assert L.or_d2i(float("inf")) == 2**31 - 1
+
+
+def test_java_math_round():
+    L = lib()
+    cases = {0.49999999999999994: 0, 0.5: 1, -0.5: 0, 2.5: 3, -2.5: -2, -2.51: -3, 1e20: 2**63 - 1,
+             float("nan"): 0, -1e20: -(2**63), 4503599627370497.0: 4503599627370497, 123.456: 123}
+    for x, want in cases.items():
+        assert L.or_math_round(x) == want, x
+
+
+# ---------------------------------------------------------------- LeapArray family
+
+def test_leap_array_get_valid_head(t0):
+    """coreT/slots/statistic/base/LeapArrayTest.java:31-63 (wl=100, interval=1000)."""
+    la = Leap(LEAP_UNARY, 10, 1000)
+    t = t0
+    e1 = la.current_window(t)
+    la.slot_add(e1, 0, 1)
+    t += 100
+    e2 = la.current_window(t)
+    la.slot_add(e2, 0, 2)
+    for i in range(8):
+        t += 100
+        la.slot_add(la.current_window(t), 0, i + 3)
+    assert la.valid_head(t) == e1
+    assert la.get(e1, 0) == 1
+    t += 100
+    assert la.valid_head(t) == e2
+    assert la.get(e2, 0) == 2
+
+
+def test_bucket_leap_array_new_window(t0):
+    """coreT/slots/statistic/metric/BucketLeapArrayTest.java:44-53, :56-66 (wl=1000, interval=2000)."""
+    la = Leap(LEAP_BUCKET, 2, 2000)
+    s = la.current_window(t0)
+    assert la.start(s) == t0 - t0 % 1000
+    assert la.get(s, M_PASS) == 0
+
+
+def test_bucket_leap_array_window_after_one_interval(t0):
+    """BucketLeapArrayTest.java:68-104."""
+    la = Leap(LEAP_BUCKET, 2, 2000)
+    prev_start = t0 - t0 % 1000
+    s = la.current_window(prev_start)
+    assert la.start(s) == prev_start
+    la.slot_add(s, M_PASS, 1)
+    la.slot_add(s, M_BLOCK, 1)
+    middle = prev_start + 500
+    s2 = la.current_window(middle)
+    assert s2 == s and la.start(s2) == prev_start
+    la.slot_add(s2, M_PASS, 1)
+    assert la.get(s2, M_PASS) == 2 and la.get(s2, M_BLOCK) == 1
+    nxt = middle + 500
+    s3 = la.current_window(nxt)
+    assert la.start(s3) - prev_start == 1000
+    assert la.get(s3, M_PASS) == 0 and la.get(s3, M_BLOCK) == 0
+
+
+def test_bucket_leap_array_deprecated_refresh(t0):
+    """BucketLeapArrayTest.java:106-121: the second lap resets every bucket."""
+    la = Leap(LEAP_BUCKET, 2, 2000)
+    for i in range(2):
+        la.slot_add(la.current_window(t0 + 1000 * i), M_PASS, 1)
+    for i in range(2, 4):
+        s = la.current_window(t0 + 1000 * i)
+        assert la.start(s) == (t0 + 1000 * i) - (t0 + 1000 * i) % 1000
+        assert la.get(s, M_PASS) == 0
+
+
+def test_bucket_leap_array_multi_thread_update_empty_window(t0):
+    """BucketLeapArrayTest.java:123-147 (16 adds; sequential replay)."""
+    la = Leap(LEAP_BUCKET, 2, 2000)
+    for _ in range(16):
+        la.slot_add(la.current_window(t0), M_PASS, 1)
+    assert la.get(la.current_window(t0), M_PASS) == 16
+
+
+def test_bucket_leap_array_previous_window(t0):
+    """BucketLeapArrayTest.java:149-162 (written for epoch-scale times: t >= one window length)."""
+    t0 += 5_000
+    la = Leap(LEAP_BUCKET, 2, 2000)
+    s = la.current_window(t0)
+    assert la.previous_window(t0) == -1
+    assert la.previous_window(t0 + 1000) == s
+    assert la.previous_window(t0 + 11 * 1000) == -1
+
+
+def test_bucket_leap_array_list_windows_reset_old(t0):
+    """BucketLeapArrayTest.java:164-188 (the real sleep restated as virtual time)."""
+    la = Leap(LEAP_BUCKET, 10, 1000)
+    a = la.current_window(t0)
+    b = la.current_window(t0 + 100)
+    assert sorted(la.values(t0 + 100)) == sorted({a, b})
+    now = t0 + 100 + 1000
+    la.add(now, M_PASS, 1)
+    assert len(la.values(now)) == 1
+
+
+def test_bucket_leap_array_list_windows_new_bucket(t0):
+    """BucketLeapArrayTest.java:190-216."""
+    la = Leap(LEAP_BUCKET, 10, 1000)
+    a = la.current_window(t0)
+    b = la.current_window(t0 + 100)
+    now = t0 + 1000 + 3 * 100
+    assert set(la.values(now)) <= {a, b}
+    la.add(now, M_PASS, 1)
+    assert len(la.values(now)) == 1
+
+
+def test_future_bucket_leap_array(t0):
+    """coreT/slots/statistic/metric/FutureBucketLeapArrayTest.java:23-31 (wl=200, interval=2000)."""
+    fa = Leap(LEAP_FUTURE, 10, 2000)
+    for i in range(0, 2000, 200):
+        fa.add(i + t0, M_PASS, 1)
+        assert len(fa.values(i + t0)) == 0
+
+
+def test_occupiable_new_window(t0):
+    """coreT/slots/statistic/metric/OccupiableBucketLeapArrayTest.java:29-42."""
+    la = Leap(LEAP_OCCUPIABLE, 10, 2000)
+    s = la.current_window(t0)
+    la.slot_add(s, M_PASS, 1)
+    assert la.get(s, M_PASS) == 1
+    la.add_waiting(t0 + 200, 1)
+    assert la.current_waiting(t0) == 1
+    assert la.get(s, M_PASS) == 1
+
+
+def test_occupiable_window_in_one_interval(t0):
+    """OccupiableBucketLeapArrayTest.java:44-66: borrowed pass is pulled into the new bucket."""
+    la = Leap(LEAP_OCCUPIABLE, 10, 2000)
+    s = la.current_window(t0)
+    la.slot_add(s, M_PASS, 1)
+    la.add_waiting(t0 + 200, 2)
+    assert la.current_waiting(t0) == 2
+    assert la.get(s, M_PASS) == 1
+    la.current_window(t0 + 200)
+    vals = la.values(t0 + 200)
+    assert len(vals) == 2
+    assert sum(la.get(v, M_PASS) for v in vals) == 3
+
+
+def test_occupiable_multi_thread_update_empty_window(t0):
+    """OccupiableBucketLeapArrayTest.java:68-102 (16 threads, sequential replay)."""
+    la = Leap(LEAP_OCCUPIABLE, 10, 2000)
+    for _ in range(16):
+        la.slot_add(la.current_window(t0), M_PASS, 1)
+        la.add_waiting(t0 + 200, 1)
+    assert la.get(la.current_window(t0), M_PASS) == 16
+    assert la.current_waiting(t0) == 16
+    la.current_window(t0 + 200)
+    vals = la.values(t0 + 200)
+    assert len(vals) == 2
+    assert sum(la.get(v, M_PASS) for v in vals) == 32
+
+
+def test_occupiable_window_after_one_interval(t0):
+    """OccupiableBucketLeapArrayTest.java:104-138: 10-bucket sum = 19, waiting = 10
+    (a bucket exactly `interval` old is still summed: the deprecation test is strictly '>')."""
+    la = Leap(LEAP_OCCUPIABLE, 10, 2000)
+    for i in range(10):
+        la.slot_add(la.current_window(t0 + i * 200), M_PASS, 1)
+        la.add_waiting(t0 + (i + 1) * 200, 1)
+    vals = la.values(t0 - t0 % 200 + 2000)
+    assert len(vals) == 10
+    assert sum(la.get(v, M_PASS) for v in vals) == 19
+    assert la.current_waiting(t0) == 10
+
+
+def test_array_metric_operate(t0):
+    """coreT/slots/statistic/metric/ArrayMetricTest.java:44-78 (one bucket; the mock returns it)."""
+    la = Leap(LEAP_BUCKET, 2, 1000)
+    s = la.current_window(t0)
+    lib().or_leap_slot_add_rt(la.h, s, 21)
+    for _ in range(9):
+        la.add(t0, M_PASS, 1)
+    for _ in range(2):
+        la.add(t0, M_BLOCK, 1)
+    for _ in range(9):
+        la.add(t0, M_SUCCESS, 1)
+    for _ in range(6):
+        la.add(t0, M_EXCEPTION, 1)
+    assert la.get_sum(t0, M_PASS) == 9
+    assert la.get_sum(t0, M_BLOCK) == 2
+    assert la.get_sum(t0, M_SUCCESS) == 9
+    assert la.get_sum(t0, M_EXCEPTION) == 6
+    assert la.get_sum(t0, M_RT) == 21
+    assert lib().or_leap_slot_min_rt(la.h, s) == 21
+
+
+# ---------------------------------------------------------------- cluster server metrics
+
+def test_cluster_metric_try_occupy_next(t0):
+    """srvT/flow/statistic/metric/ClusterMetricTest.java:26-45 (S=5, interval=25 ms)."""
+    m = ClusterMetric(5, 25)
+    for n in (1, 2, 1):
+        m.add_event(t0, abi.EV_PASS, n)
+    m.add_event(t0, abi.EV_BLOCK, 1)
+    assert m.get_sum_event(t0, abi.EV_PASS) == 4
+    assert m.get_sum_event(t0, abi.EV_BLOCK) == 1
+    assert math.isclose(m.get_avg(t0, abi.EV_PASS), 160, abs_tol=0.01)
+    assert m.try_occupy_next(t0, abi.EV_PASS, 111, 900) == 200
+    for n in (1, 2, 1):
+        m.add_event(t0, abi.EV_PASS, n)
+    assert m.try_occupy_next(t0, abi.EV_PASS, 222, 900) == 200
+    for n in (1, 2, 1):
+        m.add_event(t0, abi.EV_PASS, n)
+    assert m.try_occupy_next(t0, abi.EV_PASS, 333, 900) == 0
+
+
+def test_request_limiter(t0):
+    """srvT/flow/statistic/limit/RequestLimiterTest.java:26-43."""
+    r = RequestLimiter(10)
+    for _ in range(3):
+        r.add(t0, 3)
+    assert r.can_pass(t0)
+    assert r.get_sum(t0) == 9
+    r.add(t0, 3)
+    assert not r.can_pass(t0)
+    t = t0 + 1000
+    r.add(t, 3)
+    assert r.try_pass(t)
+    assert r.can_pass(t)
+    assert r.get_sum(t) == 4
+
+
+def test_global_request_limiter_pass(t0):
+    """srvT/flow/statistic/limit/GlobalRequestLimiterTest.java:31-47 (maxAllowedQps = 3)."""
+    r = RequestLimiter(3)
+    assert math.isclose(r.qps_allowed(), 3)
+    assert [r.try_pass(t0) for _ in range(4)] == [True, True, True, False]
+    assert math.isclose(r.get_qps(t0), 3, abs_tol=0.01)
+    t = t0 + 1000
+    assert r.try_pass(t) and r.try_pass(t)
+    assert math.isclose(r.get_qps(t), 2, abs_tol=0.01)
+
+
+def test_global_request_limiter_change_max_qps():
+    """GlobalRequestLimiterTest.java:49-55 (applyMaxQpsChange)."""
+    r = RequestLimiter(3)
+    r.set_qps_allowed(10)
+    assert math.isclose(r.qps_allowed(), 10)
+
+
+def _cluster_service(count, sample_count, interval_ms, thr_type=abi.THRESHOLD_GLOBAL, limiter=None, connected=1):
+    s = ClusterTokenService(1.0, 1.0)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["limiter_enabled"] = 1 if limiter is not None else 0
+    ns["max_allowed_qps"] = limiter if limiter is not None else 30000
+    ns["connected_count"] = connected
+    s.set_namespaces(ns)
+    rules = np.zeros(1, abi.RULE_DTYPE)
+    rules["flow_id"] = 98765
+    rules["count"] = count
+    rules["threshold_type"] = thr_type
+    rules["sample_count"] = sample_count
+    rules["window_interval_ms"] = interval_ms
+    s.load_rules(rules)
+    return s
+
+
+def _req(ts, prio=False, acquire=1, key=0):
+    r = np.zeros(1, abi.REQ_DTYPE)
+    r["ts_ms"] = ts
+    r["key"] = key | (abi.KEY_PRIO if prio else 0)
+    r["acquire"] = acquire
+    return r
+
+
+def test_cluster_flow_checker_occupy_pass(t0):
+    """srvT/flow/ClusterFlowCheckerTest.java:37-73 — disabled in the reference (`//@Test`, real sleeps).
+    Restated on virtual time; every expected (status, remaining, wait) was traced by hand through
+    ClusterFlowChecker.acquireClusterToken (:55-112) and ClusterMetric.tryOccupyNext (:79-98):
+    the prioritized request at bucket 4 occupies because the head bucket (2 passes) expires next."""
+    s = _cluster_service(5, 5, 1000)
+    bl = 200
+    t = t0
+    seq = []
+
+    def go(prio):
+        seq.append(tuple(s.decide(_req(t, prio))[0]))
+
+    go(False); go(False)
+    t += bl
+    go(False)
+    t += bl
+    go(True); go(False); go(True)
+    t += bl
+    go(False); go(False)
+    t += bl
+    go(False); go(True); go(False)
+    t += bl
+    go(False)
+    OKs, BL, W = abi.OK, abi.BLOCKED, abi.SHOULD_WAIT
+    assert seq == [(OKs, 4, 0), (OKs, 3, 0), (OKs, 2, 0), (OKs, 1, 0), (OKs, 0, 0), (BL, 0, 0),
+                   (BL, 0, 0), (BL, 0, 0), (BL, 0, 0), (W, 0, bl), (BL, 0, 0), (OKs, 0, 0)]
+    # the occupied pass was transferred into the bucket reset at the last step
+    starts, c, occ = s.read_state(0)
+    last = int(np.argmax(starts))
+    assert c[last, abi.EV_PASS] == 2 and c[last, abi.EV_OCCUPIED_PASS] == 1
+    assert c[last, abi.EV_PASS_REQUEST] == 2
+    assert list(occ) == [0, 0]
+
+
+def test_token_service_validation():
+    """DefaultTokenService.requestToken, srv/flow/DefaultTokenService.java:39-50, 87-89."""
+    s = _cluster_service(5, 10, 1000)
+    out = s.decide(np.concatenate([_req(0, acquire=0), _req(0, acquire=-3), _req(0, key=abi.KEY_BAD),
+                                   _req(0, key=7), _req(0, key=abi.KEY_NO_RULE), _req(0)]))
+    assert list(out["status"]) == [abi.BAD_REQUEST, abi.BAD_REQUEST, abi.BAD_REQUEST, abi.NO_RULE_EXISTS,
+                                   abi.NO_RULE_EXISTS, abi.OK]
+
+
+def test_token_service_namespace_limiter(t0):
+    """ClusterFlowChecker.allowProceed (:50-53) → GlobalRequestLimiter.tryPass: TOO_MANY_REQUEST leaves
+    the flow metric untouched; restates GlobalRequestLimiterTest's T,T,T,F at the service level."""
+    s = _cluster_service(100, 10, 1000, limiter=3)
+    out = s.decide(np.concatenate([_req(t0) for _ in range(4)]))
+    assert list(out["status"]) == [abi.OK, abi.OK, abi.OK, abi.TOO_MANY_REQUEST]
+    assert list(out["remaining"][:3]) == [99, 98, 97]
+    out = s.decide(np.concatenate([_req(t0 + 1000) for _ in range(3)]))
+    assert list(out["status"]) == [abi.OK, abi.OK, abi.OK]
+
+
+def test_token_service_avg_local_threshold(t0):
+    """calcGlobalThreshold, ClusterFlowChecker.java:38-48: AVG_LOCAL multiplies by connectedCount."""
+    s = _cluster_service(2, 10, 1000, thr_type=abi.THRESHOLD_AVG_LOCAL, connected=3)
+    out = s.decide(np.concatenate([_req(t0) for _ in range(7)]))
+    assert list(out["status"]) == [abi.OK] * 6 + [abi.BLOCKED]
+    s0 = _cluster_service(2, 10, 1000, thr_type=abi.THRESHOLD_AVG_LOCAL, connected=0)
+    assert s0.decide(_req(t0))[0]["status"] == abi.BLOCKED
+
+
+def test_token_service_remaining_saturates(t0):
+    """remaining = (int) nextRemaining (ClusterFlowChecker.java:81): saturating double → int cast."""
+    s = _cluster_service(1e12, 10, 1000)
+    out = s.decide(_req(t0))
+    assert out[0]["status"] == abi.OK and out[0]["remaining"] == 2**31 - 1
