@@ -1,0 +1,231 @@
+"""Benchmark: flow decisions/sec of the cluster token-server hot path (BASELINE.json north star, C3).
+
+One step = one 1000 ms simulated batch of token requests decided exactly as
+DefaultTokenService.requestToken → ClusterFlowChecker would, over the flowIds this rank owns
+(flowIds hash-sharded over ranks; weak scaling: every rank decides n_requests per step). Requests
+are synthetic (Zipf(1.0) flowIds, U{1..32} thresholds, 1 % prioritized), generated on the GPU before
+the timed region and resident in HBM. With N > 1 ranks each step also runs the node-wide metric
+rollup over RCCL (all-reduce of pass/block totals, all-gather of per-flowId QPS snapshots).
+
+Prints one JSON line (rank 0). See DESIGN.md §Measurement for the roofline bytes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sentinel_amd import abi  # noqa: E402
+from sentinel_amd.engine import FlowEngine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+REQ_B, RES_B = 16, 12          # sg_req / sg_result bytes
+STATE_B = 2 * 640 + 2 * 64      # bucket ring 10×64 B read+write, occupy read+write
+RULE_B = 16
+
+
+def splitmix64_t(x):
+    x = x + 0x9E3779B97F4A7C15
+    z = x
+    z = (z ^ (z >> 30)) * -4658895280553007687  # 0xBF58476D1CE4E5B9
+    z = (z ^ (z >> 27)) * -7723592293110705685  # 0x94D049BB133111EB
+    return z ^ (z >> 31)
+
+
+class ShardWorkload:
+    """This rank's share of the C3 node workload, generated on the GPU."""
+
+    def __init__(self, n_flows, n_requests, rank, world, device, seed=3, zipf_s=1.0, span_ms=1000,
+                 prio_frac=0.01, multi_frac=0.10, sample_count=10, interval_ms=1000, t0=1_700_000_000_000):
+        self.dev = device
+        self.n_requests = n_requests
+        self.span_ms = span_ms
+        self.t0 = t0
+        self.prio_frac, self.multi_frac = prio_frac, multi_frac
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        perm = torch.randperm(n_flows, generator=g)                  # global rank → flow index
+        flows = torch.arange(n_flows, dtype=torch.int64)
+        owner = (splitmix64_t(flows) & 0x7FFFFFFFFFFFFFFF) % world
+        owned_mask_by_rank = owner[perm] == rank                     # by global rank
+        ranks = torch.nonzero(owned_mask_by_rank).flatten()          # global ranks this rank owns
+        self.flow_idx = perm[ranks]                                  # their global flow indices
+        self.K = int(ranks.numel())
+        w = 1.0 / torch.pow(ranks.to(torch.float64) + 1.0, zipf_s)
+        cdf = torch.cumsum(w, 0)
+        self.cdf = (cdf / cdf[-1]).to(device)
+        # local key i ↔ global flow self.flow_idx[i]; rules follow the global flow index
+        rng = np.random.default_rng(seed)
+        counts = rng.integers(1, 33, n_flows).astype(np.float64)
+        self.rules = np.zeros(self.K, abi.RULE_DTYPE)
+        fi = self.flow_idx.numpy()
+        self.rules["flow_id"] = fi.astype(np.int64) + 10_000_001
+        self.rules["count"] = counts[fi]
+        self.rules["threshold_type"] = abi.THRESHOLD_GLOBAL
+        self.rules["sample_count"] = sample_count
+        self.rules["window_interval_ms"] = interval_ms
+        self.gen = torch.Generator(device=device).manual_seed(seed * 1000 + rank)
+
+    def batch(self, b):
+        """Requests of simulated second b as a uint8 tensor of n × 16 B (sg_req layout) on the GPU."""
+        n, dev, g = self.n_requests, self.dev, self.gen
+        ts = torch.randint(0, self.span_ms, (n,), generator=g, device=dev, dtype=torch.int64)
+        ts = torch.sort(ts).values + (self.t0 + b * self.span_ms)
+        u = torch.rand(n, generator=g, device=dev, dtype=torch.float64)
+        key = torch.searchsorted(self.cdf, u, right=True).clamp_(max=self.K - 1)
+        acq = torch.ones(n, dtype=torch.int64, device=dev)
+        multi = torch.rand(n, generator=g, device=dev) < self.multi_frac
+        acq = torch.where(multi, torch.randint(2, 5, (n,), generator=g, device=dev), acq)
+        prio = (torch.rand(n, generator=g, device=dev) < self.prio_frac).to(torch.int64) << 31
+        words = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        words[:, 0] = ts
+        words[:, 1] = (acq << 32) | key | prio
+        return words.view(torch.uint8).reshape(-1)
+
+
+def cpu_baseline(n_flows, n_requests, seconds_budget=25.0):
+    """The oracle (sequential C restatement, 1 thread) on the same C3 workload: whole 1000 ms batches
+    until ~10 s of decide time or the budget is spent."""
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.workload import ClusterWorkload
+    wl = ClusterWorkload(n_flows=n_flows, n_requests=n_requests)
+    s = ClusterTokenService()
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = 30000
+    s.set_namespaces(ns)
+    s.load_rules(wl.rules())
+    t_start = time.time()
+    done, decide_s, batches = 0, 0.0, 0
+    while decide_s < 10.0 and time.time() - t_start < seconds_budget:
+        req = wl.requests(batches)
+        t = time.perf_counter()
+        s.decide(req)
+        decide_s += time.perf_counter() - t
+        done += len(req)
+        batches += 1
+    return {"value": done / decide_s, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"{batches} consecutive 1000 ms C3 batches ({done} requests, {n_flows} flowIds) through "
+                      f"oracle/liboracle.so (sequential C restatement of DefaultTokenService/ClusterFlowChecker), "
+                      f"single thread, {decide_s:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--flows", type=int, default=1_000_000)
+    ap.add_argument("--requests", type=int, default=16_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    wl = ShardWorkload(args.flows, args.requests, rank, world, dev)
+    eng = FlowEngine(device=local_rank, max_batch=args.requests)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = 30000
+    eng.set_namespaces(ns)
+    eng.load_rules(wl.rules)
+
+    total_steps = args.warmup + args.steps
+    batches = [wl.batch(b) for b in range(total_steps)]
+    out = torch.empty(args.requests * RES_B, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    snap = torch.empty((wl.K, 2), dtype=torch.float64, device=dev) if world > 1 else None
+    gathered = [torch.empty_like(snap) for _ in range(world)] if world > 1 else None
+    totals = torch.zeros(2, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+
+    def step(b):
+        eng.decide_device(batches[b].data_ptr(), args.requests, out.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            now = wl.t0 + (b + 1) * wl.span_ms
+            eng.snapshot_device(now, snap.data_ptr(), wl.K, stream.cuda_stream)
+            torch.sum(snap, 0, out=totals)
+            dist.all_reduce(totals)
+            dist.all_gather(gathered, snap)
+
+    for b in range(args.warmup):
+        step(b)
+    # phase timing (HIP events inside the library, on the call's stream) over the timed steps
+    eng.enable_stats(True)
+    phase = {"sort_ms": 0.0, "walk_ms": 0.0, "total_ms": 0.0}
+    long_segments = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, total_steps):
+        step(b)
+        st = eng.stats()
+        for k in phase:
+            phase[k] += st[k]
+        long_segments = st["long_segments"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+
+    # touched flowIds of the last batch (for the algorithmic byte count)
+    last = batches[-1].view(torch.int64).reshape(-1, 2)[:, 1] & 0x7FFFFFFF
+    touched = int(torch.unique(last).numel())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = args.requests * world / (elapsed / args.steps)
+    b_alg = args.requests * (REQ_B + RES_B) + touched * (STATE_B + RULE_B)
+    walk_ms = phase["walk_ms"] / args.steps
+    total_ms = phase["total_ms"] / args.steps
+    step_gbs = b_alg / (total_ms / 1000.0) / 1e9
+    result = {
+        "metric": "flow decisions/sec (node) at 1M flowIds, 1/2/4/8 GPU; HBM GB/s vs peak",
+        "value": value,
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (GPU-generated, seeded): Zipf(1.0) flowIds, counts U{1..32}, 10% acquire U{2..4}, 1% prioritized",
+        "config": {"workload": "C3 cluster token server: ClusterFlowChecker, FLOW_THRESHOLD_GLOBAL, S=10/1000 ms",
+                   "flow_ids": args.flows, "flow_ids_per_gpu": wl.K, "requests_per_step_per_gpu": args.requests,
+                   "simulated_ms_per_step": wl.span_ms, "parallelism": f"hash-sharded flowIds x{world}",
+                   "rollup": "RCCL all_reduce + all_gather per step" if world > 1 else "none (1 GPU)"},
+        "roofline": {"bound": "hbm", "kernel": "whole batch pipeline (prep + sort + walk), device time",
+                     "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_gbs / HBM_PEAK_GBS,
+                     "traffic": None, "algorithmic_bytes_per_step": b_alg, "touched_flow_ids": touched},
+        "phases_ms": {"device_total": total_ms, "sort": phase["sort_ms"] / args.steps, "walk": walk_ms,
+                      "long_segments": long_segments},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.flows, args.requests)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

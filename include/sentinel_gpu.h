@@ -161,6 +161,10 @@ int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* cou
  * currentWindow side effect); out has 2*n_rules doubles, HOST memory. */
 int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap);
 
+/* Same into DEVICE memory (2*n_rules doubles, {passQps, blockQps} per flowId), asynchronous on `stream`:
+ * the per-GPU input of the node-wide RCCL metric rollup. */
+int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, void* stream);
+
 /* Library build identification (architecture the kernels were compiled for). */
 const char* sg_build_info(void);
 

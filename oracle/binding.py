@@ -59,6 +59,7 @@ def lib():
         "or_cts_decide": (C.c_int, [vp, vp, u64, vp]),
         "or_cts_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
         "or_cts_sample_count": (C.c_int, [vp, u32]),
+        "or_cts_avg": (d, [vp, u32, i64, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -215,6 +216,9 @@ class ClusterTokenService:
         out = np.zeros(len(req), dtype=abi.RES_DTYPE)
         lib().or_cts_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
         return out
+
+    def avg(self, key, now, ev):
+        return lib().or_cts_avg(self.h, key, now, ev)
 
     def read_state(self, key):
         S = lib().or_cts_sample_count(self.h, key)

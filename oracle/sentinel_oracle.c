@@ -534,6 +534,12 @@ int or_cts_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out) {
     return 0;
 }
 
+/* ClusterMetric.getAvg(ev) of one flowId at `now` (with its currentWindow side effect, as in Java). */
+double or_cts_avg(or_cts* s, uint32_t key, int64_t now, int ev) {
+    if (key >= s->n_rules) return 0;
+    return or_cluster_metric_get_avg(s->rules[key].metric, now, ev);
+}
+
 int or_cts_sample_count(const or_cts* s, uint32_t key) {
     if (key >= s->n_rules) return -1;
     return s->rules[key].metric->S;

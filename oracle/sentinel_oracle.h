@@ -98,6 +98,7 @@ int     or_cts_load_rules(or_cts* s, const sg_flow_rule* rules, uint32_t n);
 int     or_cts_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
 int     or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
 int     or_cts_sample_count(const or_cts* s, uint32_t key);
+double  or_cts_avg(or_cts* s, uint32_t key, int64_t now, int ev);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,440 @@
+// api.cpp — the C ABI of libsentinel_gpu.so (include/sentinel_gpu.h): handle, rule tables, batch
+// driver. Device work is in engine.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "engine.h"
+
+using namespace sg;
+
+struct sg_handle {
+    int device = 0;
+    sg_config cfg{};
+    std::string err;
+
+    std::vector<sg_namespace> ns;
+    std::vector<sg_flow_rule> rules;  // as loaded (current rule per key)
+    std::vector<Rule> rule_tab;       // device image
+    uint32_t K = 0;
+    int stride = 0;                   // buckets per flowId
+    int n_wl = 0;
+    int32_t wl[kMaxWl]{};
+
+    Rule* d_rules = nullptr;
+    Bucket* d_ring = nullptr;
+    Occ* d_occ = nullptr;
+
+    // batch workspace (sized for cfg.max_batch)
+    uint64_t* d_rec = nullptr;
+    uint64_t* d_rec_sorted = nullptr;
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    uint32_t* d_bnd = nullptr;
+    int64_t* d_p0 = nullptr;
+    uint32_t* d_np = nullptr;
+    int* d_err = nullptr;
+    int64_t* d_last_ts = nullptr;
+    uint32_t* d_long_list = nullptr;
+    uint32_t* d_long_count = nullptr;
+    int* h_err = nullptr;       // pinned
+    uint32_t* h_long = nullptr; // pinned
+
+    // host-buffer convenience path
+    sg_req* d_req_h = nullptr;
+    sg_result* d_out_h = nullptr;
+
+    int kbits = 0, ibits = 0, abits = 0;
+    bool stats_on = false;
+    hipEvent_t ev[5]{};
+    sg_batch_stats stats{};
+};
+
+namespace {
+
+int fail(sg_handle* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+#define HIP_TRY(h, expr)                                                                        \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return fail((h), SG_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e));     \
+    } while (0)
+
+int bits_for(uint64_t v) {  // bits needed to represent v (v >= 1)
+    int b = 0;
+    while (b < 64 && (v >> b) != 0) ++b;
+    return b;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+// calcGlobalThreshold(rule) * exceedCount (ClusterFlowChecker.java:38-48, :68)
+double global_threshold(const sg_handle* h, const sg_flow_rule& r) {
+    double base;
+    if (r.threshold_type == SG_THRESHOLD_GLOBAL) {
+        base = r.count;
+    } else {
+        int connected = 0;
+        if (r.namespace_id >= 0 && (size_t)r.namespace_id < h->ns.size()) connected = h->ns[r.namespace_id].connected_count;
+        base = r.count * connected;
+    }
+    return base * h->cfg.exceed_count;
+}
+
+int layout_records(sg_handle* h) {
+    h->kbits = bits_for((uint64_t)h->K);  // must hold K itself (sentinel key of rejected requests)
+    if (h->kbits < 1) h->kbits = 1;
+    h->ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
+    h->abits = 64 - h->kbits - h->ibits;
+    if (h->abits < 3) return fail(h, SG_E_UNSUPPORTED, "rule count x max_batch too large for 64-bit records");
+    return SG_OK;
+}
+
+int upload_rule_table(sg_handle* h) {
+    for (uint32_t k = 0; k < h->K; ++k) h->rule_tab[k].thr = global_threshold(h, h->rules[k]);
+    if (h->K) HIP_TRY(h, hipMemcpy(h->d_rules, h->rule_tab.data(), sizeof(Rule) * h->K, hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sg_build_info(void) {
+    return "sentinel_gpu: cluster flow-decision engine, HIP for gfx950 (MI355X)";
+}
+
+int sg_create(const sg_config* cfg, sg_handle** out) {
+    if (!cfg || !out) return SG_E_INVAL;
+    *out = nullptr;
+    if (cfg->max_batch == 0 || cfg->max_batch > (1ull << 32)) return SG_E_INVAL;
+    if (!(cfg->exceed_count >= 0) || !(cfg->max_occupy_ratio >= 0)) return SG_E_INVAL;
+    sg_handle* h = new sg_handle();
+    h->cfg = *cfg;
+    h->device = cfg->device;
+    auto bail = [&](int rc) {
+        sg_destroy(h);
+        return rc;
+    };
+    if (hipSetDevice(h->device) != hipSuccess) return bail(SG_E_DEVICE);
+    const uint64_t n = cfg->max_batch;
+    if (hipMalloc(&h->d_rec, n * 8) != hipSuccess || hipMalloc(&h->d_rec_sorted, n * 8) != hipSuccess)
+        return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_p0, sizeof(int64_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_np, sizeof(uint32_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n / (kShortMax + 1) + 1)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_long_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipHostMalloc(&h->h_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipHostMalloc(&h->h_long, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    int64_t neg = -1;
+    if (hipMemcpy(h->d_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
+    for (auto& e : h->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(SG_E_DEVICE);
+    // default namespace 0, no limiter, 1 connection
+    sg_namespace d0{0, 1, 30000.0};
+    h->ns.push_back(d0);
+    *out = h;
+    return SG_OK;
+}
+
+void sg_destroy(sg_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    dfree(h->d_rules);
+    dfree(h->d_ring);
+    dfree(h->d_occ);
+    dfree(h->d_rec);
+    dfree(h->d_rec_sorted);
+    dfree(h->d_sort_tmp);
+    dfree(h->d_bnd);
+    dfree(h->d_p0);
+    dfree(h->d_np);
+    dfree(h->d_err);
+    dfree(h->d_last_ts);
+    dfree(h->d_long_list);
+    dfree(h->d_long_count);
+    dfree(h->d_req_h);
+    dfree(h->d_out_h);
+    if (h->h_err) (void)hipHostFree(h->h_err);
+    if (h->h_long) (void)hipHostFree(h->h_long);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete h;
+}
+
+const char* sg_last_error(const sg_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
+    if (!h || (!ns && n)) return SG_E_INVAL;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (ns[i].limiter_enabled) {
+            // GlobalRequestLimiter pre-pass is not on the device path yet.
+            return fail(h, SG_E_UNSUPPORTED, "namespace QPS limiter is not supported by the device path yet");
+        }
+    }
+    for (const auto& r : h->rules)
+        if (r.namespace_id < 0 || (uint32_t)r.namespace_id >= n)
+            return fail(h, SG_E_INVAL, "a loaded rule refers to a namespace that would disappear");
+    h->ns.assign(ns, ns + n);
+    (void)hipSetDevice(h->device);
+    return upload_rule_table(h);
+}
+
+int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
+    if (!h || (!rules && n)) return SG_E_INVAL;
+    if (n >= SG_KEY_BAD) return fail(h, SG_E_INVAL, "too many rules");
+    (void)hipSetDevice(h->device);
+    // validate (FlowRuleUtil.isValidRule / checkClusterField, FlowRuleUtil.java:167-229)
+    std::unordered_map<int64_t, uint32_t> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_flow_rule& r = rules[i];
+        if (r.flow_id <= 0) return fail(h, SG_E_INVAL, "flowId must be > 0");
+        if (!(r.count >= 0)) return fail(h, SG_E_INVAL, "count must be >= 0");
+        if (r.sample_count <= 0 || r.window_interval_ms <= 0 || r.window_interval_ms % r.sample_count != 0)
+            return fail(h, SG_E_INVAL, "invalid window config");
+        if (r.namespace_id < 0 || (size_t)r.namespace_id >= h->ns.size())
+            return fail(h, SG_E_INVAL, "unknown namespace");
+        if (!seen.emplace(r.flow_id, i).second) return fail(h, SG_E_INVAL, "duplicate flowId");
+    }
+    // old flowId → old index, to keep the metric of surviving flows (ClusterFlowRuleManager.java:361)
+    std::unordered_map<int64_t, uint32_t> old_index;
+    for (uint32_t k = 0; k < h->K; ++k) old_index.emplace(h->rules[k].flow_id, k);
+
+    std::vector<Rule> tab(n);
+    std::vector<int32_t> src(n, -1);
+    int stride = 1;
+    int n_wl = 0;
+    int32_t wl[kMaxWl]{};
+    for (uint32_t i = 0; i < n; ++i) {
+        int S = rules[i].sample_count, interval = rules[i].window_interval_ms;
+        auto it = old_index.find(rules[i].flow_id);
+        if (it != old_index.end()) {  // the existing ClusterMetric keeps its window shape
+            src[i] = (int32_t)it->second;
+            S = h->rule_tab[it->second].S;
+            interval = h->rule_tab[it->second].S * h->rule_tab[it->second].wl;
+        }
+        if (S > SG_MAX_SAMPLE_COUNT)
+            return fail(h, SG_E_UNSUPPORTED, "sampleCount > 64 is not supported by the device path");
+        Rule R{};
+        R.S = S;
+        R.wl = interval / S;
+        R.isec = interval / 1000.0;
+        R.wait_ms = 1000 / S;
+        int w = 0;
+        while (w < n_wl && wl[w] != R.wl) ++w;
+        if (w == n_wl) {
+            if (n_wl == kMaxWl) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct window lengths");
+            wl[n_wl++] = R.wl;
+        }
+        R.wl_idx = w;
+        stride = std::max(stride, S);
+        tab[i] = R;
+    }
+
+    Rule* d_rules = nullptr;
+    Bucket* d_ring = nullptr;
+    Occ* d_occ = nullptr;
+    int32_t* d_src = nullptr;
+    if (n) {
+        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess ||
+            hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
+            hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
+            dfree(d_rules);
+            dfree(d_ring);
+            dfree(d_occ);
+            dfree(d_src);
+            return fail(h, SG_E_NOMEM, "rule state allocation failed");
+        }
+        HIP_TRY(h, hipMemcpy(d_src, src.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, launch_init_state(d_ring, d_occ, n, stride, d_src, h->d_ring, h->d_occ, h->stride, 0));
+        HIP_TRY(h, hipDeviceSynchronize());
+        dfree(d_src);
+    }
+    dfree(h->d_rules);
+    dfree(h->d_ring);
+    dfree(h->d_occ);
+    h->d_rules = d_rules;
+    h->d_ring = d_ring;
+    h->d_occ = d_occ;
+    h->rules.assign(rules, rules + n);
+    h->rule_tab = tab;
+    h->K = n;
+    h->stride = stride;
+    h->n_wl = n_wl;
+    std::memcpy(h->wl, wl, sizeof(wl));
+    int rc = layout_records(h);
+    if (rc) return rc;
+    // radix sort workspace for this key width
+    size_t need = sort_temp_bytes(h->cfg.max_batch, h->kbits);
+    if (need > h->sort_tmp_bytes) {
+        dfree(h->d_sort_tmp);
+        h->sort_tmp_bytes = 0;
+        if (hipMalloc(&h->d_sort_tmp, need) != hipSuccess) return fail(h, SG_E_NOMEM, "sort workspace");
+        h->sort_tmp_bytes = need;
+    }
+    return upload_rule_table(h);
+}
+
+int sg_enable_stats(sg_handle* h, int on) {
+    if (!h) return SG_E_INVAL;
+    h->stats_on = on != 0;
+    return SG_OK;
+}
+
+int sg_get_stats(const sg_handle* h, sg_batch_stats* out) {
+    if (!h || !out) return SG_E_INVAL;
+    *out = h->stats;
+    return SG_OK;
+}
+
+int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    if (h->K == 0 && h->kbits == 0) {
+        int rc = layout_records(h);
+        if (rc) return rc;
+        size_t need = sort_temp_bytes(h->cfg.max_batch, h->kbits);
+        if (need > h->sort_tmp_bytes) {
+            dfree(h->d_sort_tmp);
+            if (hipMalloc(&h->d_sort_tmp, need) != hipSuccess) return fail(h, SG_E_NOMEM, "sort workspace");
+            h->sort_tmp_bytes = need;
+        }
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+
+    BatchArgs a{};
+    a.req = req;
+    a.out = out;
+    a.n = n;
+    a.rec = h->d_rec;
+    a.rec_sorted = h->d_rec_sorted;
+    a.kshift = 64 - h->kbits;
+    a.abits = h->abits;
+    a.imask = (h->ibits >= 64) ? ~0ull : ((1ull << h->ibits) - 1);
+    a.amask = (1ull << h->abits) - 1;
+    a.aesc = (1ull << (h->abits - 1)) - 1;
+    a.K = h->K;
+    a.rules = h->d_rules;
+    a.ring = h->d_ring;
+    a.occ = h->d_occ;
+    a.stride = h->stride;
+    a.max_occ_ratio = h->cfg.max_occupy_ratio;
+    a.n_wl = h->n_wl;
+    std::memcpy(a.wl, h->wl, sizeof(a.wl));
+    a.bnd = h->d_bnd;
+    a.p0 = h->d_p0;
+    a.np = h->d_np;
+    a.err = h->d_err;
+    a.last_ts = h->d_last_ts;
+    a.long_list = h->d_long_list;
+    a.long_count = h->d_long_count;
+
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_prep(a, stream));
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
+    HIP_TRY(h, launch_sort(a, h->d_sort_tmp, h->sort_tmp_bytes, stream));
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
+    HIP_TRY(h, launch_walk_short(a, stream));
+    HIP_TRY(h, launch_walk_long(a, stream));
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
+    HIP_TRY(h, launch_finish(a, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (h->stats_on) {
+        HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipEventRecord(h->ev[4], stream));
+    }
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (h->stats_on) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[4]);
+        h->stats.total_ms = ms;
+        (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+        h->stats.sort_ms = ms;
+        (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+        h->stats.walk_ms = ms;
+        h->stats.long_segments = *h->h_long;
+    }
+    if (*h->h_err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    return SG_OK;
+}
+
+int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_req_h) {
+        if (hipMalloc(&h->d_req_h, sizeof(sg_req) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_out_h, sizeof(sg_result) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    HIP_TRY(h, hipMemcpy(h->d_req_h, req, sizeof(sg_req) * n, hipMemcpyHostToDevice));
+    int rc = sg_flow_decide_batch(h, h->d_req_h, n, h->d_out_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(out, h->d_out_h, sizeof(sg_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
+    if (!h || key >= h->K || !starts || !counters || !occupy) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const int S = h->rule_tab[key].S;
+    std::vector<Bucket> b(S);
+    HIP_TRY(h, hipMemcpy(b.data(), h->d_ring + (size_t)key * h->stride, sizeof(Bucket) * S, hipMemcpyDeviceToHost));
+    Occ o;
+    HIP_TRY(h, hipMemcpy(&o, h->d_occ + key, sizeof(Occ), hipMemcpyDeviceToHost));
+    for (int j = 0; j < S; ++j) {
+        starts[j] = b[j].start;
+        for (int e = 0; e < SG_NUM_EVENTS; ++e) counters[j * SG_NUM_EVENTS + e] = b[j].start == INT64_MIN ? 0 : b[j].c[e];
+    }
+    occupy[0] = o.pass;
+    occupy[1] = o.pass_req;
+    return SG_OK;
+}
+
+int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap) {
+    if (!h || !out || cap < 2ull * h->K) return SG_E_INVAL;
+    if (h->K == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    double* d_out = nullptr;
+    HIP_TRY(h, hipMalloc(&d_out, sizeof(double) * 2 * h->K));
+    hipError_t e1 = launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, d_out, 0);
+    hipError_t e2 = e1 == hipSuccess ? hipMemcpy(out, d_out, sizeof(double) * 2 * h->K, hipMemcpyDeviceToHost) : e1;
+    (void)hipFree(d_out);
+    if (e2 != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e2));
+    return SG_OK;
+}
+
+int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, void* stream) {
+    if (!h || !out_dev || cap < 2ull * h->K) return SG_E_INVAL;
+    if (h->K == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
+    return SG_OK;
+}
+
+}  // extern "C"

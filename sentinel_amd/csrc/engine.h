@@ -1,0 +1,88 @@
+// engine.h — internal device-side types and launch entry points of libsentinel_gpu.so.
+// Not part of the public ABI (that is include/sentinel_gpu.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sentinel_gpu.h"
+
+namespace sg {
+
+// Per-flowId rule record, 32 B. thr/isec/S/wl describe the flow's ClusterMetric; the window shape is
+// that of the metric created when the flowId first appeared (ClusterFlowRuleManager.java:361 keeps
+// an existing metric across rule reloads), the threshold that of the current rule.
+struct alignas(16) Rule {
+    double thr;       // calcGlobalThreshold(rule) * exceedCount   (ClusterFlowChecker.java:38-48, :68)
+    double isec;      // LeapArray.intervalInSecond = intervalInMs / 1000.0 (LeapArray.java:68)
+    int32_t S;        // sampleCount
+    int32_t wl;       // windowLengthInMs = intervalInMs / sampleCount
+    int32_t wl_idx;   // index into the batch's distinct-window-length table
+    int32_t wait_ms;  // 1000 / sampleCount (ClusterMetric.java:86)
+};
+static_assert(sizeof(Rule) == 32, "Rule layout");
+
+// One ClusterMetricBucket + its WindowWrap start, 64 B (one bucket per cache half-line pair).
+// start == INT64_MIN encodes a never-created slot (AtomicReferenceArray element == null).
+struct alignas(64) Bucket {
+    int64_t start;
+    int64_t c[SG_NUM_EVENTS];
+};
+static_assert(sizeof(Bucket) == 64, "Bucket layout");
+
+// ClusterMetricLeapArray.occupyCounter[PASS], [PASS_REQUEST]; hasOccupied == (pass_req > 0).
+struct alignas(16) Occ {
+    int64_t pass;
+    int64_t pass_req;
+};
+
+constexpr int kMaxWl = 8;                 // distinct window lengths per handle
+constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
+constexpr int kShortMax = 16;             // segments longer than this are walked by a whole wave
+
+// error bits reported through BatchArgs::err
+constexpr int kErrTime = 1;      // negative or decreasing timestamps
+constexpr int kErrPeriods = 2;   // batch spans more than kMaxPeriods windows
+
+struct BatchArgs {
+    const sg_req* req;
+    sg_result* out;
+    uint64_t n;
+    uint64_t* rec;       // packed records, request order
+    uint64_t* rec_sorted;
+    // record layout: [key : kbits][idx : ibits][acode : abits], acode = acquire << 1 | prio
+    int kshift;          // = 64 - kbits
+    int abits;
+    uint64_t imask;      // (1 << ibits) - 1
+    uint64_t amask;      // (1 << abits) - 1
+    uint64_t aesc;       // acquire field value meaning "read req[idx].acquire"
+    uint32_t K;          // number of rules
+    const Rule* rules;
+    Bucket* ring;        // [K][stride]
+    Occ* occ;            // [K]
+    int stride;          // buckets per flowId (max sampleCount)
+    double max_occ_ratio;
+    int n_wl;
+    int32_t wl[kMaxWl];
+    uint32_t* bnd;       // [kMaxWl][kMaxPeriods]: first request index of each window period
+    int64_t* p0;         // [kMaxWl]: first window period of the batch
+    uint32_t* np;        // [kMaxWl]: number of window periods the batch spans
+    int* err;
+    int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
+    uint32_t* long_list; // segment starts handed to the wave walker
+    uint32_t* long_count;
+};
+
+// Launchers (engine.hip). All are asynchronous on `stream`.
+hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_sort(const BatchArgs& a, void* tmp, size_t tmp_bytes, hipStream_t stream);
+size_t sort_temp_bytes(uint64_t n, int kbits);
+hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,
+                             const Bucket* old_ring, const Occ* old_occ, int old_stride, hipStream_t stream);
+hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,
+                           int64_t now, double* out, hipStream_t stream);
+
+}  // namespace sg

@@ -1,0 +1,134 @@
+"""Thin ctypes handle over libsentinel_gpu.so (the C ABI in include/sentinel_gpu.h).
+
+There is no CPU fallback: if the HIP library is missing, constructing a FlowEngine raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
+
+EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
+           "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
+           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_build_info"]
+
+_lib = None
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sentinel_gpu error {code}: {msg}")
+        self.code = code
+
+
+def load_library():
+    """Load the HIP library (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C sentinel_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
+    sig = {
+        "sg_create": (C.c_int, [C.POINTER(abi.sg_config), C.POINTER(vp)]),
+        "sg_destroy": (None, [vp]),
+        "sg_last_error": (C.c_char_p, [vp]),
+        "sg_set_namespaces": (C.c_int, [vp, vp, u32]),
+        "sg_load_flow_rules": (C.c_int, [vp, vp, u32]),
+        "sg_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_enable_stats": (C.c_int, [vp, C.c_int]),
+        "sg_get_stats": (C.c_int, [vp, C.POINTER(abi.sg_batch_stats)]),
+        "sg_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
+        "sg_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
+        "sg_snapshot_metrics_device": (C.c_int, [vp, i64, vp, u64, vp]),
+        "sg_build_info": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class FlowEngine:
+    """One sg_handle: the cluster flow rules of a token server on one GPU."""
+
+    def __init__(self, device=0, max_batch=1 << 20, exceed_count=1.0, max_occupy_ratio=1.0):
+        L = load_library()
+        cfg = abi.sg_config(device=device, reserved0=0, exceed_count=exceed_count,
+                            max_occupy_ratio=max_occupy_ratio, max_batch=max_batch)
+        h = C.c_void_p()
+        rc = L.sg_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise EngineError(rc, "sg_create failed")
+        self._L = L
+        self.h = h
+        self.max_batch = max_batch
+        self.sample_counts = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.sg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise EngineError(rc, self._L.sg_last_error(self.h).decode())
+
+    def set_namespaces(self, ns: np.ndarray):
+        ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
+        self._check(self._L.sg_set_namespaces(self.h, abi.ptr(ns), len(ns)))
+
+    def load_rules(self, rules: np.ndarray):
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        self._check(self._L.sg_load_flow_rules(self.h, abi.ptr(rules), len(rules)))
+
+    def decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        """req_ptr/out_ptr: device addresses of n sg_req / sg_result records (e.g. torch data_ptr())."""
+        self._check(self._L.sg_flow_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr),
+                                                 C.c_void_p(stream_ptr)))
+
+    def decide_host(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.REQ_DTYPE)
+        out = np.zeros(len(req), abi.RES_DTYPE)
+        self._check(self._L.sg_flow_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def enable_stats(self, on=True):
+        self._check(self._L.sg_enable_stats(self.h, 1 if on else 0))
+
+    def stats(self):
+        s = abi.sg_batch_stats()
+        self._check(self._L.sg_get_stats(self.h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in abi.sg_batch_stats._fields_}
+
+    def read_state(self, key, sample_count):
+        starts = np.zeros(sample_count, np.int64)
+        counters = np.zeros(sample_count * abi.NUM_EVENTS, np.int64)
+        occ = np.zeros(2, np.int64)
+        self._check(self._L.sg_flow_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ)))
+        return starts, counters.reshape(sample_count, abi.NUM_EVENTS), occ
+
+    def snapshot_device(self, now_ms, out_ptr, n_rules, stream_ptr=0):
+        """{passQps, blockQps} per flowId into device memory at out_ptr (2*n_rules doubles)."""
+        self._check(self._L.sg_snapshot_metrics_device(self.h, now_ms, C.c_void_p(out_ptr), 2 * n_rules,
+                                                       C.c_void_p(stream_ptr)))
+
+    def snapshot(self, now_ms, n_rules):
+        out = np.zeros(2 * n_rules, np.float64)
+        self._check(self._L.sg_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
+        return out.reshape(n_rules, 2)
