@@ -81,6 +81,10 @@ extern "C" {
 #define SG_KEY_NO_RULE 0x7FFFFFFFu
 #define SG_KEY_BAD     0x7FFFFFFEu
 
+/* sg_config.flags: force one walker for every flowId segment (testing both walkers on any trace). */
+#define SG_FLAG_SERIAL_ONLY 1   /* one lane per flowId, however long its segment */
+#define SG_FLAG_WAVE_ONLY   2   /* one wave per flowId, however short its segment */
+
 /* Largest sampleCount the device walker keeps in a wave (one bucket per lane). */
 #define SG_MAX_SAMPLE_COUNT 64
 
@@ -88,7 +92,7 @@ typedef struct sg_handle sg_handle;
 
 typedef struct sg_config {
     int32_t  device;            /* HIP device ordinal                                   */
-    int32_t  reserved0;
+    int32_t  flags;             /* SG_FLAG_* (0 = default walker selection)             */
     double   exceed_count;      /* ServerFlowConfig.exceedCount, default 1.0 (:26)      */
     double   max_occupy_ratio;  /* ServerFlowConfig.maxOccupyRatio, default 1.0 (:27)  */
     uint64_t max_batch;         /* largest n accepted by sg_flow_decide_batch           */
@@ -164,6 +168,11 @@ int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap)
 /* Same into DEVICE memory (2*n_rules doubles, {passQps, blockQps} per flowId), asynchronous on `stream`:
  * the per-GPU input of the node-wide RCCL metric rollup. */
 int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, void* stream);
+
+/* Testing aid: copy an internal buffer of the last batch to host memory.
+ * what: 0 = records (request order, u64), 1 = records sorted by flowId, 2 = window-period table
+ * (u32 [8][65536]), 3 = first period per window length (i64[8]), 4 = periods per window length (u32[8]). */
+int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes);
 
 /* Library build identification (architecture the kernels were compiled for). */
 const char* sg_build_info(void);

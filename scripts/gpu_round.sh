@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, kernel-trace profile. Stops at the first fault/timeout.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>; continue only on exit 0/1 (test failures), stop on faults
+  local name=$1 tmo=$2; shift 2
+  echo "== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$tmo" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a gpurun_out/steps.log
+  tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = test ]; then
+  step pytest_gpu 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+  step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  step bench 400 python -u bench.py --steps 10 --warmup 3
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  step rocprof 400 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline
+fi
+echo done

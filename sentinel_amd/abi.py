@@ -36,11 +36,13 @@ KEY_NO_RULE = 0x7FFFFFFF
 KEY_BAD = 0x7FFFFFFE
 
 MAX_SAMPLE_COUNT = 64
+FLAG_SERIAL_ONLY = 1
+FLAG_WAVE_ONLY = 2
 INT64_MIN = -(1 << 63)
 
 
 class sg_config(C.Structure):
-    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32), ("exceed_count", C.c_double),
+    _fields_ = [("device", C.c_int32), ("flags", C.c_int32), ("exceed_count", C.c_double),
                 ("max_occupy_ratio", C.c_double), ("max_batch", C.c_uint64)]
 
 

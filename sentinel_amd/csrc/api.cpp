@@ -34,8 +34,8 @@ struct sg_handle {
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
     uint64_t* d_rec_sorted = nullptr;
-    void* d_sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
+    uint64_t* last_sorted = nullptr;  // whichever of d_rec / d_rec_sorted holds the last sort result
+    uint32_t* d_hist = nullptr;       // radix sort histogram workspace
     uint32_t* d_bnd = nullptr;
     int64_t* d_p0 = nullptr;
     uint32_t* d_np = nullptr;
@@ -135,11 +135,12 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_rec, n * 8) != hipSuccess || hipMalloc(&h->d_rec_sorted, n * 8) != hipSuccess)
         return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_hist, sizeof(uint32_t) * radix_hist_words(n)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_p0, sizeof(int64_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_np, sizeof(uint32_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n / (kShortMax + 1) + 1)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipHostMalloc(&h->h_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipHostMalloc(&h->h_long, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -162,7 +163,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_occ);
     dfree(h->d_rec);
     dfree(h->d_rec_sorted);
-    dfree(h->d_sort_tmp);
+    dfree(h->d_hist);
     dfree(h->d_bnd);
     dfree(h->d_p0);
     dfree(h->d_np);
@@ -281,14 +282,6 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     std::memcpy(h->wl, wl, sizeof(wl));
     int rc = layout_records(h);
     if (rc) return rc;
-    // radix sort workspace for this key width
-    size_t need = sort_temp_bytes(h->cfg.max_batch, h->kbits);
-    if (need > h->sort_tmp_bytes) {
-        dfree(h->d_sort_tmp);
-        h->sort_tmp_bytes = 0;
-        if (hipMalloc(&h->d_sort_tmp, need) != hipSuccess) return fail(h, SG_E_NOMEM, "sort workspace");
-        h->sort_tmp_bytes = need;
-    }
     return upload_rule_table(h);
 }
 
@@ -312,12 +305,6 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     if (h->K == 0 && h->kbits == 0) {
         int rc = layout_records(h);
         if (rc) return rc;
-        size_t need = sort_temp_bytes(h->cfg.max_batch, h->kbits);
-        if (need > h->sort_tmp_bytes) {
-            dfree(h->d_sort_tmp);
-            if (hipMalloc(&h->d_sort_tmp, need) != hipSuccess) return fail(h, SG_E_NOMEM, "sort workspace");
-            h->sort_tmp_bytes = need;
-        }
     }
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
@@ -348,13 +335,20 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.last_ts = h->d_last_ts;
     a.long_list = h->d_long_list;
     a.long_count = h->d_long_count;
+    a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
+                  : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : (uint32_t)kShortMax;
 
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_prep(a, stream));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
-    HIP_TRY(h, launch_sort(a, h->d_sort_tmp, h->sort_tmp_bytes, stream));
+    {
+        uint64_t* sorted = nullptr;
+        HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, a.kshift, h->d_hist, &sorted, stream));
+        a.rec_sorted = sorted;
+        h->last_sorted = sorted;
+    }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_walk_short(a, stream));
     HIP_TRY(h, launch_walk_long(a, stream));
@@ -434,6 +428,24 @@ int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, ui
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
+    return SG_OK;
+}
+
+int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {
+    if (!h || !dst) return SG_E_INVAL;
+    const void* src = nullptr;
+    uint64_t cap = 0;
+    switch (what) {
+    case 0: src = (h->last_sorted == h->d_rec) ? h->d_rec_sorted : h->d_rec; cap = h->cfg.max_batch * 8; break;
+    case 1: src = h->last_sorted ? h->last_sorted : h->d_rec_sorted; cap = h->cfg.max_batch * 8; break;
+    case 2: src = h->d_bnd; cap = sizeof(uint32_t) * kMaxWl * kMaxPeriods; break;
+    case 3: src = h->d_p0; cap = sizeof(int64_t) * kMaxWl; break;
+    case 4: src = h->d_np; cap = sizeof(uint32_t) * kMaxWl; break;
+    default: return SG_E_INVAL;
+    }
+    if (bytes > cap) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return SG_OK;
 }
 

@@ -38,7 +38,7 @@ struct alignas(16) Occ {
 
 constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
-constexpr int kShortMax = 16;             // segments longer than this are walked by a whole wave
+constexpr int kShortMax = 16;             // default: segments longer than this are walked by a whole wave
 
 // error bits reported through BatchArgs::err
 constexpr int kErrTime = 1;      // negative or decreasing timestamps
@@ -71,12 +71,15 @@ struct BatchArgs {
     int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
+    uint32_t short_max;  // segments longer than this go to the wave walker
 };
 
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
-hipError_t launch_sort(const BatchArgs& a, void* tmp, size_t tmp_bytes, hipStream_t stream);
-size_t sort_temp_bytes(uint64_t n, int kbits);
+// sort.hip: stable LSD radix sort of records on bits [lo_bit, 64); result buffer is a or b.
+size_t radix_hist_words(uint64_t n);
+hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
+                              uint64_t** result, hipStream_t stream);
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);

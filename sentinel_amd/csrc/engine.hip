@@ -9,7 +9,7 @@
 //   k_prep        request order → packed 64-bit records {flowId index | request index | acquire,prio},
 //                 validation (BAD_REQUEST / NO_RULE_EXISTS written directly), timestamp checks, and the
 //                 window-period boundary table (timestamps are only ever needed as window periods).
-//   radix sort    stable partition of the records by flowId (time order kept within a flowId).
+//   radix sort    stable partition of the records by flowId (sort.hip; time order kept within a flowId).
 //   k_walk_short  one lane per flowId segment of <= kShortMax requests: sequential replay.
 //   k_walk_long   one wave per longer segment: bucket ring in registers (lane j = slot j), requests
 //                 64 at a time with a wave prefix-scan "admit until the first failure" step and a
@@ -20,8 +20,6 @@
 // Only PASS and WAITING are ever read back by decisions; every other counter is an accumulator.
 // Exactness: all window arithmetic is int64 (wrapping, -fwrapv), the QPS comparisons are IEEE double
 // with the reference's operation order and -ffp-contract=off (no FMA contraction).
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include "engine.h"
 
 namespace sg {
@@ -293,8 +291,9 @@ __global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
         if (k >= a.K) continue;
         if (j > 0 && (uint32_t)(a.rec_sorted[j - 1] >> a.kshift) == k) continue;  // not a segment head
         uint64_t e = j + 1;
-        while (e < n && e - j <= (uint64_t)kShortMax && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
-        if (e - j > (uint64_t)kShortMax) {
+        const uint64_t smax = a.short_max;
+        while (e < n && e - j <= smax && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
+        if (e - j > smax) {
             const uint32_t pos = atomicAdd(a.long_count, 1u);
             a.long_list[pos] = (uint32_t)j;
             continue;
@@ -466,7 +465,7 @@ __global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
         const uint64_t s = a.long_list[w];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
         // segment end: gallop then binary search for the first record with a larger flowId
-        uint64_t lo = s + kShortMax, step = 64, hi;
+        uint64_t lo = s + a.short_max, step = 64, hi;
         for (;;) {
             hi = lo + step;
             if (hi >= a.n) {
@@ -565,26 +564,14 @@ hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-size_t sort_temp_bytes(uint64_t n, int kbits) {
-    size_t bytes = 0;
-    (void)rocprim::radix_sort_keys((void*)nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n,
-                             64u - (unsigned)kbits, 64u, (hipStream_t)0);
-    return bytes;
-}
-
-hipError_t launch_sort(const BatchArgs& a, void* tmp, size_t tmp_bytes, hipStream_t stream) {
-    const unsigned kbits = 64u - (unsigned)a.kshift;
-    return rocprim::radix_sort_keys(tmp, tmp_bytes, a.rec, a.rec_sorted, (size_t)a.n, 64u - kbits, 64u, stream);
-}
-
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_walk_short, dim3(grid_for(a.n, 256, 16384)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
-    // upper bound of long segments = n / (kShortMax + 1); waves loop over the list
-    const uint64_t max_long = a.n / (kShortMax + 1) + 1;
+    // upper bound of long segments = n / (short_max + 1); waves loop over the list
+    const uint64_t max_long = a.n / ((uint64_t)a.short_max + 1) + 1;
     const unsigned blocks = grid_for(max_long * 64, 256, 2048);
     hipLaunchKernelGGL(k_walk_long, dim3(blocks), dim3(256), 0, stream, a);
     return hipGetLastError();

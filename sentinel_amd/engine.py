@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
-           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_build_info"]
+           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info"]
 
 _lib = None
 
@@ -48,6 +48,7 @@ def load_library():
         "sg_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
         "sg_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
         "sg_snapshot_metrics_device": (C.c_int, [vp, i64, vp, u64, vp]),
+        "sg_debug_copy": (C.c_int, [vp, C.c_int, vp, u64]),
         "sg_build_info": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -61,9 +62,9 @@ def load_library():
 class FlowEngine:
     """One sg_handle: the cluster flow rules of a token server on one GPU."""
 
-    def __init__(self, device=0, max_batch=1 << 20, exceed_count=1.0, max_occupy_ratio=1.0):
+    def __init__(self, device=0, max_batch=1 << 20, exceed_count=1.0, max_occupy_ratio=1.0, flags=0):
         L = load_library()
-        cfg = abi.sg_config(device=device, reserved0=0, exceed_count=exceed_count,
+        cfg = abi.sg_config(device=device, flags=flags, exceed_count=exceed_count,
                             max_occupy_ratio=max_occupy_ratio, max_batch=max_batch)
         h = C.c_void_p()
         rc = L.sg_create(C.byref(cfg), C.byref(h))
@@ -127,6 +128,12 @@ class FlowEngine:
         """{passQps, blockQps} per flowId into device memory at out_ptr (2*n_rules doubles)."""
         self._check(self._L.sg_snapshot_metrics_device(self.h, now_ms, C.c_void_p(out_ptr), 2 * n_rules,
                                                        C.c_void_p(stream_ptr)))
+
+    def debug_copy(self, what, dtype, count):
+        """Testing aid: an internal buffer of the last batch (see sg_debug_copy)."""
+        out = np.zeros(count, dtype)
+        self._check(self._L.sg_debug_copy(self.h, what, abi.ptr(out), out.nbytes))
+        return out
 
     def snapshot(self, now_ms, n_rules):
         out = np.zeros(2 * n_rules, np.float64)

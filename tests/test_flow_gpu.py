@@ -258,3 +258,33 @@ def test_snapshot_matches_oracle_avg():
     for k in range(len(rules)):
         assert snap[k, 0] == ora.avg(k, now, abi.EV_PASS)
         assert snap[k, 1] == ora.avg(k, now, abi.EV_BLOCK)
+
+
+def _host_records(req, n_rules, max_batch):
+    kbits = max(1, int(n_rules).bit_length())
+    ibits = int(max_batch - 1).bit_length()
+    abits = 64 - kbits - ibits
+    key = (req["key"] & abi.KEY_INDEX).astype(np.uint64)
+    bad = (key == abi.KEY_BAD) | (req["acquire"] <= 0)
+    norule = (~bad) & (key >= n_rules)
+    acq = np.minimum(req["acquire"].astype(np.int64), (1 << (abits - 1)) - 1).astype(np.uint64)
+    ac = (acq << np.uint64(1)) | (req["key"] >> np.uint64(31)).astype(np.uint64)
+    rec = (key << np.uint64(64 - kbits)) | (np.arange(len(req), dtype=np.uint64) << np.uint64(abits)) | ac
+    rec[bad | norule] = np.uint64(n_rules) << np.uint64(64 - kbits)
+    return rec, 64 - kbits
+
+
+@pytest.mark.parametrize("n_keys,n", [(1, 100), (7, 20_000), (3000, 4096 * 3 + 17), (1 << 20, 300_000)])
+def test_radix_sort_is_stable_partition_by_flow(n_keys, n):
+    """The hand-written LSD radix sort (sort.hip) against numpy's stable argsort of the same records."""
+    rng = np.random.default_rng(n_keys + n)
+    rules = _rules(n_keys, rng)
+    max_batch = 1 << 20
+    eng, _ = _pair(rules, max_batch=max_batch)
+    req = _trace(rng, n, n_keys, 1_700_000_000_000, 1000, zipf=1.1)
+    req["key"][rng.random(n) < 0.01] = abi.KEY_NO_RULE
+    eng.decide_host(req)
+    rec, kshift = _host_records(req, n_keys, max_batch)
+    want = rec[np.argsort(rec >> np.uint64(kshift), kind="stable")]
+    got = eng.debug_copy(1, np.uint64, n)
+    assert np.array_equal(got, want)
