@@ -14,9 +14,12 @@ from sentinel_amd.workload import ClusterWorkload, zipf_keys
 pytestmark = pytest.mark.gpu
 
 
-def _engine(max_batch=1 << 20, exceed=1.0, occ_ratio=1.0):
+WALKERS = [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY]  # default split, every flow serial, every flow by a wave
+
+
+def _engine(max_batch=1 << 20, exceed=1.0, occ_ratio=1.0, flags=0):
     from sentinel_amd.engine import FlowEngine
-    return FlowEngine(device=0, max_batch=max_batch, exceed_count=exceed, max_occupy_ratio=occ_ratio)
+    return FlowEngine(device=0, max_batch=max_batch, exceed_count=exceed, max_occupy_ratio=occ_ratio, flags=flags)
 
 
 def _ns(connected=1):
@@ -26,9 +29,9 @@ def _ns(connected=1):
     return ns
 
 
-def _pair(rules, ns=None, exceed=1.0, occ_ratio=1.0, max_batch=1 << 20):
+def _pair(rules, ns=None, exceed=1.0, occ_ratio=1.0, max_batch=1 << 20, flags=0):
     ns = _ns() if ns is None else ns
-    eng = _engine(max_batch, exceed, occ_ratio)
+    eng = _engine(max_batch, exceed, occ_ratio, flags)
     eng.set_namespaces(ns)
     eng.load_rules(rules)
     ora = ClusterTokenService(exceed, occ_ratio)
@@ -78,7 +81,8 @@ def _trace(rng, n, n_keys, t_start, span, zipf=1.0, prio=0.01, multi=0.1, big=0.
     return req
 
 
-def test_cluster_flow_checker_occupy_pass_gpu(t0):
+@pytest.mark.parametrize("flags", WALKERS)
+def test_cluster_flow_checker_occupy_pass_gpu(t0, flags):
     """The hand-traced ClusterFlowCheckerTest sequence (tests/test_oracle_kat.py), one request per batch
     (state carried across batches) and again as a single batch."""
     rules = _rules(1, np.random.default_rng(0), counts=np.array([5.0]), S=5, interval=1000)
@@ -89,10 +93,10 @@ def test_cluster_flow_checker_occupy_pass_gpu(t0):
         req[i] = (t0 + dt, abi.KEY_PRIO if p else 0, 1)
     want = [(0, 4, 0), (0, 3, 0), (0, 2, 0), (0, 1, 0), (0, 0, 0), (1, 0, 0), (1, 0, 0), (1, 0, 0), (1, 0, 0),
             (2, 0, 200), (1, 0, 0), (0, 0, 0)]
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     got = [tuple(eng.decide_host(req[i:i + 1])[0]) for i in range(len(req))]
     assert got == want
-    eng2, _ = _pair(rules)
+    eng2, _ = _pair(rules, flags=flags)
     assert [tuple(x) for x in eng2.decide_host(req)] == want
     ora.decide(req)
     _compare_state(eng, ora, rules)
@@ -113,10 +117,11 @@ def test_cluster_flow_checker_occupy_pass_gpu(t0):
     (40, 30_000, 1.1, 0.2, 5, 25),
     (40, 30_000, 1.1, 0.2, 60, 60000),
 ])
-def test_random_traces_match_oracle(n_keys, n, zipf, prio, S, interval):
+@pytest.mark.parametrize("flags", WALKERS)
+def test_random_traces_match_oracle(n_keys, n, zipf, prio, S, interval, flags):
     rng = np.random.default_rng(n_keys * 1000 + n + S)
     rules = _rules(n_keys, rng, S=S, interval=interval)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     t = 1_700_000_000_017
     for batch in range(3):
         span = int(rng.integers(1, 3 * interval))
@@ -126,11 +131,12 @@ def test_random_traces_match_oracle(n_keys, n, zipf, prio, S, interval):
     _compare_state(eng, ora, rules)
 
 
-def test_fractional_thresholds_and_exceed():
+@pytest.mark.parametrize("flags", WALKERS)
+def test_fractional_thresholds_and_exceed(flags):
     """Non-integer count and exceedCount: the double comparisons of ClusterFlowChecker.java:67-71."""
     rng = np.random.default_rng(5)
     rules = _rules(64, rng, counts=rng.random(64) * 40 + 0.3, S=4, interval=1000)
-    eng, ora = _pair(rules, exceed=1.37, occ_ratio=0.55)
+    eng, ora = _pair(rules, exceed=1.37, occ_ratio=0.55, flags=flags)
     t = 1_700_000_000_500
     for _ in range(3):
         req = _trace(rng, 40_000, 64, t, 1700, prio=0.3, multi=0.4)
@@ -153,12 +159,13 @@ def test_avg_local_threshold_and_connected_count():
     _compare_state(eng, ora, rules)
 
 
-def test_large_acquire_counts_and_huge_thresholds():
+@pytest.mark.parametrize("flags", WALKERS)
+def test_large_acquire_counts_and_huge_thresholds(flags):
     """acquireCount beyond the packed field (escape path) and thresholds beyond int (remaining saturates)."""
     rng = np.random.default_rng(7)
     counts = np.where(rng.random(16) < 0.5, 1e12, rng.integers(1, 1000, 16).astype(float))
     rules = _rules(16, rng, counts=counts)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     req = _trace(rng, 20_000, 16, 1_700_000_000_000, 1500, prio=0.2, big=0.05)
     out_o = ora.decide(req)
     _compare_results(out_o, eng.decide_host(req), req)
@@ -222,11 +229,12 @@ def test_rule_reload_keeps_surviving_metrics():
     _compare_state(eng, ora, new)
 
 
-def test_hot_flow_long_segment_prio_heavy():
+@pytest.mark.parametrize("flags", WALKERS)
+def test_hot_flow_long_segment_prio_heavy(flags):
     """One flow taking most of the traffic: the wave walker's admit / skip / occupy modes."""
     rng = np.random.default_rng(11)
     rules = _rules(3, rng, counts=np.array([25.0, 3.0, 1000.0]), S=10, interval=1000)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     t = 1_700_000_000_000
     for _ in range(4):
         req = _trace(rng, 120_000, 3, t, 2500, zipf=2.0, prio=0.35, multi=0.5)
@@ -235,11 +243,12 @@ def test_hot_flow_long_segment_prio_heavy():
     _compare_state(eng, ora, rules)
 
 
-def test_north_star_shape_small():
+@pytest.mark.parametrize("flags", WALKERS)
+def test_north_star_shape_small(flags):
     """The C3 workload shape (Zipf(1.0), counts U{1..32}, S=10/1000 ms, 1 % prioritized) at 20k flows."""
     wl = ClusterWorkload(n_flows=20_000, n_requests=400_000, seed=12)
     rules = wl.rules()
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     for b in range(2):
         req = wl.requests(b)
         _compare_results(ora.decide(req), eng.decide_host(req), req)
