@@ -143,6 +143,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             if (q > a.aesc) q = a.aesc;
             const uint64_t ac = (q << 1) | (uint64_t)(r.key >> 31);
             rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
+            store_result(a.out, (uint32_t)i, SG_STATUS_BLOCKED, 0, 0);  // walkers write only non-BLOCKED
         }
         a.rec[i] = rec;
     }
@@ -207,55 +208,86 @@ __device__ __forceinline__ void open_bucket(PeriodState& ps, int64_t start, cons
     }
 }
 
+// Period tracking shared by both walkers: requests of one flowId arrive in index order, so the
+// window period only moves forward; the cached boundary of the next period answers most lookups.
+struct PeriodCursor {
+    const uint32_t* bnd;
+    uint32_t np;
+    uint32_t q;       // current period (0-based within the batch), 0xFFFFFFFF before the first
+    uint32_t next_b;  // first request index of period q + 1 (UINT32_MAX past the last)
+
+    __device__ __forceinline__ void seek(uint32_t qq) {
+        q = qq;
+        next_b = (qq + 1 < np) ? bnd[qq + 1] : 0xFFFFFFFFu;
+    }
+    // period of a request index >= every index seen so far
+    __device__ __forceinline__ uint32_t of(uint32_t idx) const {
+        if (q != 0xFFFFFFFFu && idx < next_b) return q;
+        return period_of(bnd, np, idx);
+    }
+};
+
+// Open the bucket of period P (slot I = P % S) from the ring in memory and sum the other valid buckets
+// (values(t): a slot j != I is valid iff its start >= ws - (S-1)*wl, LeapArray.java:270-272 with starts on
+// window boundaries; only slot I can sit exactly `interval` behind and currentWindow resets it first).
+// All loads are issued before any is used.
+__device__ __forceinline__ void open_period_serial(PeriodState& ps, const Bucket* ring, const Rule& R, int64_t P,
+                                                   int* I_out, int64_t* ws_out) {
+    const int S = R.S;
+    const int I = (int)(P % S);
+    const int64_t ws = P * R.wl;
+    const int64_t lo = ws - (int64_t)(S - 1) * R.wl;
+    const int h = (int)((P + 1) % S);
+    ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+    int64_t cI[SG_NUM_EVENTS];
+    int64_t stI = INT64_MIN;
+#pragma unroll 4
+    for (int q = 0; q < S; ++q) {
+        const int64_t st = ring[q].start;
+        const int64_t pp = ring[q].c[SG_EV_PASS];
+        const int64_t ww = ring[q].c[SG_EV_WAITING];
+        const bool v = (q != I) && st != INT64_MIN && st >= lo;
+        ps.wo_pass += v ? pp : 0;
+        ps.wo_wait += v ? ww : 0;
+        if (q == h && v) ps.head_other = pp;
+        if (q == I) stI = st;
+    }
+    if (stI == ws) {
+#pragma unroll
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
+    }
+    open_bucket(ps, stI, cI, ws);
+    *I_out = I;
+    *ws_out = ws;
+}
+
 // ------------------------------------------------------------------------ serial walker (short)
 
+// Outputs start as BLOCKED (k_prep), so only OK / SHOULD_WAIT results are written here.
 __device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
     const Rule R = a.rules[k];
     Bucket* ring = a.ring + (size_t)k * a.stride;
-    const uint32_t* bnd = a.bnd + (size_t)R.wl_idx * kMaxPeriods;
+    PeriodCursor pc{a.bnd + (size_t)R.wl_idx * kMaxPeriods, a.np[R.wl_idx], 0xFFFFFFFFu, 0};
     const int64_t P0 = a.p0[R.wl_idx];
-    const uint32_t np = a.np[R.wl_idx];
     PeriodState ps;
     {
         const Occ o = a.occ[k];
         ps.occ_pass = o.pass;
         ps.occ_req = o.pass_req;
     }
-    int64_t curP = INT64_MIN, ws = 0;
+    int64_t ws = 0;
     int I = -1;
     for (uint64_t j = s; j < e; ++j) {
         const Decoded d = decode(a, a.rec_sorted[j]);
-        const int64_t P = P0 + (int64_t)period_of(bnd, np, d.idx);
-        if (P != curP) {
+        const uint32_t q = pc.of(d.idx);
+        if (q != pc.q) {
             if (I >= 0) {
                 ring[I].start = ws;
 #pragma unroll
                 for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[I].c[ev] = ps.cur[ev];
             }
-            curP = P;
-            I = (int)(P % R.S);
-            ws = P * R.wl;
-            {
-                int64_t c[SG_NUM_EVENTS];
-#pragma unroll
-                for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ring[I].c[ev];
-                open_bucket(ps, ring[I].start, c, ws);
-            }
-            // values(t): a slot j != I is valid iff its start >= ws - (S-1)*wl (LeapArray.java:270-272
-            // with starts on window boundaries; only slot I can sit exactly `interval` behind).
-            const int64_t lo = ws - (int64_t)(R.S - 1) * R.wl;
-            const int h = (int)((P + 1) % R.S);
-            ps.wo_pass = ps.wo_wait = ps.head_other = 0;
-            for (int q = 0; q < R.S; ++q) {
-                if (q == I) continue;
-                const int64_t st = ring[q].start;
-                if (st != INT64_MIN && st >= lo) {
-                    const int64_t pp = ring[q].c[SG_EV_PASS];
-                    ps.wo_pass += pp;
-                    ps.wo_wait += ring[q].c[SG_EV_WAITING];
-                    if (q == h) ps.head_other = pp;
-                }
-            }
+            pc.seek(q);
+            open_period_serial(ps, ring, R, P0 + (int64_t)q, &I, &ws);
         }
         // ClusterFlowChecker.acquireClusterToken, :67-81
         const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
@@ -268,7 +300,7 @@ __device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
         } else {
             int32_t wait;
             const int32_t st = decide_fail(R, a.max_occ_ratio, ps, d.acq, d.prio, &wait);
-            store_result(a.out, d.idx, st, 0, wait);
+            if (st != SG_STATUS_BLOCKED) store_result(a.out, d.idx, st, 0, wait);
         }
     }
     if (I >= 0) {
@@ -304,155 +336,230 @@ __global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
 
 // --------------------------------------------------------------------------- wave walker (long)
 
-__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
-    const int lane = lane_id();
-    const Rule R = a.rules[k];
-    const int S = R.S;
-    Bucket* ring = a.ring + (size_t)k * a.stride;
-    const uint32_t* bnd = a.bnd + (size_t)R.wl_idx * kMaxPeriods;
-    const int64_t P0 = a.p0[R.wl_idx];
-    const uint32_t np = a.np[R.wl_idx];
-    const double max_occ = a.max_occ_ratio;
+constexpr int kWaveUnroll = 8;  // 64-record chunks kept in flight per wave (register double buffer)
 
+struct WaveWalker {
+    const BatchArgs& a;
+    const Rule R;
+    const int lane;
+    Bucket* ring;
+    PeriodCursor pc;
+    int64_t P0;
     // lane q < S holds slot q of the ring
-    int64_t st = INT64_MIN;
+    int64_t st;
     int64_t c[SG_NUM_EVENTS];
+    PeriodState ps;  // wave-uniform
+    int64_t ws;
+    int I;
+    // deferred per-lane BLOCK / BLOCK_REQUEST / OCCUPIED_BLOCK of the current period
+    int64_t d_blk, d_blkn, d_oblk;
+
+    __device__ WaveWalker(const BatchArgs& a_, uint32_t k) : a(a_), R(a_.rules[k]), lane(lane_id()) {
+        ring = a.ring + (size_t)k * a.stride;
+        pc = PeriodCursor{a.bnd + (size_t)R.wl_idx * kMaxPeriods, a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+        P0 = a.p0[R.wl_idx];
+        st = INT64_MIN;
 #pragma unroll
-    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = 0;
-    if (lane < S) {
-        st = ring[lane].start;
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = 0;
+        if (lane < R.S) {
+            st = ring[lane].start;
 #pragma unroll
-        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ring[lane].c[ev];
-    }
-    PeriodState ps;
-    {
+            for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ring[lane].c[ev];
+        }
         const Occ o = a.occ[k];
         ps.occ_pass = o.pass;
         ps.occ_req = o.pass_req;
-    }
 #pragma unroll
-    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
-    ps.wo_pass = ps.wo_wait = ps.head_other = 0;
-    int64_t curP = INT64_MIN, ws = 0;
-    int I = -1;
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
+        ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+        ws = 0;
+        I = -1;
+        d_blk = d_blkn = d_oblk = 0;
+    }
 
-    for (uint64_t base = s; base < e; base += 64) {
-        const uint64_t j = base + (uint64_t)lane;
-        const bool act = j < e;
+    // close the current bucket (flush deferred counts) into its owner lane
+    __device__ void close_period() {
+        if (I < 0) return;
+        ps.cur[SG_EV_BLOCK] += wave_sum(d_blk);
+        ps.cur[SG_EV_BLOCK_REQUEST] += wave_sum(d_blkn);
+        ps.cur[SG_EV_OCCUPIED_BLOCK] += wave_sum(d_oblk);
+        d_blk = d_blkn = d_oblk = 0;
+        if (lane == I) {
+            st = ws;
+#pragma unroll
+            for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ps.cur[ev];
+        }
+    }
+
+    __device__ void open_period(uint32_t q) {
+        close_period();
+        pc.seek(q);
+        const int64_t P = P0 + (int64_t)q;
+        const int S = R.S;
+        I = (int)(P % S);
+        ws = P * R.wl;
+        int64_t cI[SG_NUM_EVENTS];
+#pragma unroll
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = bcast64(c[ev], I);
+        open_bucket(ps, bcast64(st, I), cI, ws);
+        const int64_t lo = ws - (int64_t)(S - 1) * R.wl;
+        const bool valid = lane < S && lane != I && st != INT64_MIN && st >= lo;
+        ps.wo_pass = wave_sum(valid ? c[SG_EV_PASS] : 0);
+        ps.wo_wait = wave_sum(valid ? c[SG_EV_WAITING] : 0);
+        const int h = (int)((P + 1) % S);
+        ps.head_other = (h != I) ? bcast64(valid ? c[SG_EV_PASS] : 0, h) : 0;
+    }
+
+    // Can any prioritized request still occupy in this period? (wave-uniform; the window is fixed.)
+    __device__ __forceinline__ bool occupy_possible(double latest) const {
+        const double occupy_avg = (double)(ps.wo_wait + ps.cur[SG_EV_WAITING]) / R.isec;
+        if (!(occupy_avg <= a.max_occ_ratio * R.thr)) return false;
+        const int64_t head = (R.S == 1) ? ps.cur[SG_EV_PASS] : ps.head_other;
+        return latest + (double)(1 + ps.occ_pass) - (double)head <= R.thr;
+    }
+
+    // Decide the lanes in `run` (contiguous, same period, in order).
+    __device__ void run(uint64_t run_mask, const Decoded& d) {
+        const double latest0 = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+        if (!(R.thr - latest0 - 1.0 >= 0)) {
+            // Saturated: not even acquireCount = 1 fits, and nothing below can add PASS in this period,
+            // so every non-prioritized request blocks; prioritized ones try to occupy one by one until
+            // occupying is impossible too.
+            const bool in = (run_mask >> lane) & 1ull;
+            uint64_t pm = __ballot(in && d.prio);
+            bool occ_ok = pm != 0 && occupy_possible(latest0);
+            while (pm && occ_ok) {
+                const int x = __builtin_ctzll(pm);
+                pm &= pm - 1;
+                const int64_t ax = bcast64(d.acq, x);
+                int32_t wait;
+                const int32_t stx = decide_fail(R, a.max_occ_ratio, ps, ax, true, &wait);
+                if (lane == x && stx != SG_STATUS_BLOCKED) store_result(a.out, d.idx, stx, 0, wait);
+                occ_ok = occupy_possible(latest0);
+            }
+            const bool rest = in && (!d.prio || ((pm >> lane) & 1ull));
+            d_blk += rest ? d.acq : 0;
+            d_blkn += rest ? 1 : 0;
+            d_oblk += (rest && d.prio) ? d.acq : 0;
+            return;
+        }
+        uint64_t pending = run_mask;
+        while (pending) {
+            // -- admit mode: every pending request passes until the first one that does not fit
+            const bool pl = (pending >> lane) & 1ull;
+            const int64_t av = pl ? d.acq : 0;
+            const int64_t ex = wave_excl_scan(av, lane);
+            const int64_t W = ps.wo_pass + ps.cur[SG_EV_PASS];
+            const double latest_l = (double)(W + ex) / R.isec;
+            const double nr_l = R.thr - latest_l - (double)d.acq;
+            const uint64_t fails = __ballot(pl && !(nr_l >= 0));
+            const uint64_t pass_mask = fails ? (pending & below(__builtin_ctzll(fails))) : pending;
+            if (pass_mask) {
+                const bool pm = (pass_mask >> lane) & 1ull;
+                if (pm) store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(nr_l), 0);
+                ps.cur[SG_EV_PASS] += wave_sum(pm ? d.acq : 0);
+                ps.cur[SG_EV_PASS_REQUEST] += (int64_t)__popcll(pass_mask);
+                ps.cur[SG_EV_OCCUPIED_PASS] += wave_sum((pm && d.prio) ? d.acq : 0);
+            }
+            if (!fails) break;
+            int x = __builtin_ctzll(fails);
+            pending &= ~below(x + 1);
+            for (;;) {
+                {  // the request x failed the normal check: occupy branch or block
+                    const int64_t ax = bcast64(d.acq, x);
+                    const bool px = bcast32((int)d.prio, x) != 0;
+                    int32_t wait;
+                    const int32_t stx = decide_fail(R, a.max_occ_ratio, ps, ax, px, &wait);
+                    if (lane == x && stx != SG_STATUS_BLOCKED) store_result(a.out, d.idx, stx, 0, wait);
+                }
+                // -- skip mode: the window is unchanged, so a request passes iff it fits on its own;
+                // prioritized requests that do not fit stop the skip (they may occupy).
+                if (!pending) break;
+                const bool pl2 = (pending >> lane) & 1ull;
+                const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+                const bool fit = pl2 && (R.thr - latest - (double)d.acq >= 0);
+                const uint64_t fitm = __ballot(fit);
+                const uint64_t stop = fitm | __ballot(pl2 && d.prio);
+                const uint64_t blk = stop ? (pending & below(__builtin_ctzll(stop))) : pending;
+                const bool b = (blk >> lane) & 1ull;
+                d_blk += b ? d.acq : 0;  // non-prioritized, not fitting: BLOCKED (output already BLOCKED)
+                d_blkn += b ? 1 : 0;
+                if (!stop) {
+                    pending = 0;
+                    break;
+                }
+                const int g = __builtin_ctzll(stop);
+                pending &= ~below(g);
+                if ((fitm >> g) & 1ull) break;  // back to admit mode starting at g
+                x = g;                          // a prioritized request that does not fit
+                pending &= ~(1ull << g);
+            }
+        }
+    }
+
+    __device__ void chunk(uint64_t rec, bool act) {
         Decoded d;
         d.idx = 0;
         d.acq = 0;
         d.prio = false;
-        int64_t P = INT64_MAX;
+        uint32_t q = 0xFFFFFFFFu;
         if (act) {
-            d = decode(a, a.rec_sorted[j]);
-            P = P0 + (int64_t)period_of(bnd, np, d.idx);
+            d = decode(a, rec);
+            q = pc.of(d.idx);
         }
         uint64_t todo = __ballot(act);
         while (todo) {
-            const int f0 = __builtin_ctzll(todo);
-            const int64_t Prun = bcast64(P, f0);
-            if (Prun != curP) {
-                // close the current bucket into its owner lane, open the bucket of period Prun
-                if (I >= 0 && lane == I) {
-                    st = ws;
-#pragma unroll
-                    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ps.cur[ev];
-                }
-                curP = Prun;
-                I = (int)(Prun % S);
-                ws = Prun * R.wl;
-                {
-                    int64_t cI[SG_NUM_EVENTS];
-#pragma unroll
-                    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = bcast64(c[ev], I);
-                    open_bucket(ps, bcast64(st, I), cI, ws);
-                }
-                const int64_t lo = ws - (int64_t)(S - 1) * R.wl;
-                const bool valid = lane < S && lane != I && st != INT64_MIN && st >= lo;
-                ps.wo_pass = wave_sum(valid ? c[SG_EV_PASS] : 0);
-                ps.wo_wait = wave_sum(valid ? c[SG_EV_WAITING] : 0);
-                const int h = (int)((Prun + 1) % S);
-                ps.head_other = (h != I) ? bcast64(valid ? c[SG_EV_PASS] : 0, h) : 0;
-            }
-            const uint64_t run = __ballot(act && P == Prun) & todo;  // contiguous lanes of this period
-            todo &= ~run;
-
-            uint64_t pending = run;
-            while (pending) {
-                // -- admit mode: every pending request passes until the first one that does not fit
-                const bool pl = (pending >> lane) & 1ull;
-                const int64_t av = pl ? d.acq : 0;
-                const int64_t ex = wave_excl_scan(av, lane);
-                const int64_t W = ps.wo_pass + ps.cur[SG_EV_PASS];
-                const double latest_l = (double)(W + ex) / R.isec;
-                const double nr_l = R.thr - latest_l - (double)d.acq;
-                const uint64_t fails = __ballot(pl && !(nr_l >= 0));
-                const uint64_t pass_mask = fails ? (pending & below(__builtin_ctzll(fails))) : pending;
-                if (pass_mask) {
-                    const bool pm = (pass_mask >> lane) & 1ull;
-                    if (pm) store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(nr_l), 0);
-                    ps.cur[SG_EV_PASS] += wave_sum(pm ? d.acq : 0);
-                    ps.cur[SG_EV_PASS_REQUEST] += (int64_t)__popcll(pass_mask);
-                    ps.cur[SG_EV_OCCUPIED_PASS] += wave_sum((pm && d.prio) ? d.acq : 0);
-                }
-                if (!fails) break;
-                int x = __builtin_ctzll(fails);
-                pending &= ~below(x + 1);
-                // -- resolve the failing request x (normal check failed), then skip mode
-                for (;;) {
-                    {
-                        const int64_t ax = bcast64(d.acq, x);
-                        const bool px = bcast32((int)d.prio, x) != 0;
-                        int32_t wait;
-                        const int32_t stx = decide_fail(R, max_occ, ps, ax, px, &wait);
-                        if (lane == x) store_result(a.out, d.idx, stx, 0, wait);
-                    }
-                    // -- skip mode: the window is unchanged, so a request passes iff it fits on its own;
-                    // prioritized requests that do not fit stop the skip (they may occupy).
-                    if (!pending) break;
-                    const bool pl2 = (pending >> lane) & 1ull;
-                    const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
-                    const bool fit = pl2 && (R.thr - latest - (double)d.acq >= 0);
-                    const uint64_t fitm = __ballot(fit);
-                    const uint64_t stop = fitm | __ballot(pl2 && d.prio);
-                    const uint64_t blk = stop ? (pending & below(__builtin_ctzll(stop))) : pending;
-                    if (blk) {
-                        const bool b = (blk >> lane) & 1ull;
-                        if (b) store_result(a.out, d.idx, SG_STATUS_BLOCKED, 0, 0);
-                        ps.cur[SG_EV_BLOCK] += wave_sum(b ? d.acq : 0);
-                        ps.cur[SG_EV_BLOCK_REQUEST] += (int64_t)__popcll(blk);
-                    }
-                    if (!stop) {
-                        pending = 0;
-                        break;
-                    }
-                    const int g = __builtin_ctzll(stop);
-                    pending &= ~below(g);
-                    if ((fitm >> g) & 1ull) break;  // back to admit mode starting at g
-                    x = g;                          // a prioritized request that does not fit
-                    pending &= ~(1ull << g);
-                }
-            }
+            const uint32_t qrun = (uint32_t)bcast32((int)q, __builtin_ctzll(todo));
+            if (qrun != pc.q) open_period(qrun);
+            const uint64_t rm = __ballot(act && q == qrun) & todo;  // contiguous lanes of this period
+            todo &= ~rm;
+            run(rm, d);
         }
     }
-    // close the last bucket and write the ring back
-    if (I >= 0 && lane == I) {
-        st = ws;
+
+    __device__ void finish(uint32_t k) {
+        close_period();
+        if (lane < R.S) {
+            ring[lane].start = st;
 #pragma unroll
-        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ps.cur[ev];
+            for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[lane].c[ev] = c[ev];
+        }
+        if (lane == 0) {
+            Occ o;
+            o.pass = ps.occ_pass;
+            o.pass_req = ps.occ_req;
+            a.occ[k] = o;
+        }
     }
-    if (lane < S) {
-        ring[lane].start = st;
+};
+
+__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
+    WaveWalker w(a, k);
+    const int lane = w.lane;
+    const uint64_t* rec = a.rec_sorted;
+    constexpr uint64_t kBlock = 64ull * kWaveUnroll;
+    uint64_t cur[kWaveUnroll];
 #pragma unroll
-        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[lane].c[ev] = c[ev];
+    for (int u = 0; u < kWaveUnroll; ++u) {
+        const uint64_t j = s + (uint64_t)u * 64 + lane;
+        cur[u] = j < e ? rec[j] : 0ull;
     }
-    if (lane == 0) {
-        Occ o;
-        o.pass = ps.occ_pass;
-        o.pass_req = ps.occ_req;
-        a.occ[k] = o;
+    for (uint64_t base = s; base < e; base += kBlock) {
+        uint64_t nxt[kWaveUnroll];
+#pragma unroll
+        for (int u = 0; u < kWaveUnroll; ++u) {  // prefetch the next block before deciding this one
+            const uint64_t j = base + kBlock + (uint64_t)u * 64 + lane;
+            nxt[u] = j < e ? rec[j] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kWaveUnroll; ++u) {
+            const uint64_t cb = base + (uint64_t)u * 64;
+            if (cb < e) w.chunk(cur[u], cb + lane < e);
+        }
+#pragma unroll
+        for (int u = 0; u < kWaveUnroll; ++u) cur[u] = nxt[u];
     }
+    w.finish(k);
 }
 
 __global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
