@@ -50,6 +50,17 @@ struct sg_handle {
     sg_req* d_req_h = nullptr;
     sg_result* d_out_h = nullptr;
 
+    // namespace QPS limiters (GlobalRequestLimiter): slot per namespace, device rings and scratch
+    std::vector<int> ns_slot;
+    int n_lim = 0;
+    double lim_qps[kMaxLim]{};
+    int lim_wl_idx = -1;
+    LimRing* d_lim_ring = nullptr;
+    uint8_t* d_rule_lim = nullptr;
+    uint8_t* d_lim_slot = nullptr;
+    uint32_t* d_lim_tile = nullptr;   // tile totals then tile offsets
+    uint32_t* d_lim_period = nullptr; // arrivals, prefix, quota
+
     int kbits = 0, ibits = 0, abits = 0;
     bool stats_on = false;
     hipEvent_t ev[5]{};
@@ -104,9 +115,48 @@ int layout_records(sg_handle* h) {
     return SG_OK;
 }
 
+// Distinct window lengths of the loaded flows (+ the limiter's 100 ms when a limiter is on).
+int rebuild_wl_table(sg_handle* h) {
+    int n_wl = 0;
+    int32_t wl[kMaxWl]{};
+    auto index_of = [&](int32_t v) -> int {
+        for (int w = 0; w < n_wl; ++w)
+            if (wl[w] == v) return w;
+        if (n_wl == kMaxWl) return -1;
+        wl[n_wl] = v;
+        return n_wl++;
+    };
+    for (uint32_t k = 0; k < h->K; ++k) {
+        const int w = index_of(h->rule_tab[k].wl);
+        if (w < 0) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct window lengths");
+        h->rule_tab[k].wl_idx = w;
+    }
+    h->lim_wl_idx = -1;
+    if (h->n_lim > 0) {
+        h->lim_wl_idx = index_of(kLimWindowMs);
+        if (h->lim_wl_idx < 0) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct window lengths");
+    }
+    h->n_wl = n_wl;
+    std::memcpy(h->wl, wl, sizeof(wl));
+    return SG_OK;
+}
+
 int upload_rule_table(sg_handle* h) {
+    int rc = rebuild_wl_table(h);
+    if (rc) return rc;
     for (uint32_t k = 0; k < h->K; ++k) h->rule_tab[k].thr = global_threshold(h, h->rules[k]);
     if (h->K) HIP_TRY(h, hipMemcpy(h->d_rules, h->rule_tab.data(), sizeof(Rule) * h->K, hipMemcpyHostToDevice));
+    // limiter slot of each rule's namespace
+    dfree(h->d_rule_lim);
+    if (h->K) {
+        std::vector<uint8_t> rl(h->K, 0xFF);
+        for (uint32_t k = 0; k < h->K; ++k) {
+            const int ns = h->rules[k].namespace_id;
+            if (ns >= 0 && (size_t)ns < h->ns_slot.size() && h->ns_slot[ns] >= 0) rl[k] = (uint8_t)h->ns_slot[ns];
+        }
+        if (hipMalloc(&h->d_rule_lim, h->K) != hipSuccess) return fail(h, SG_E_NOMEM, "rule limiter table");
+        HIP_TRY(h, hipMemcpy(h->d_rule_lim, rl.data(), h->K, hipMemcpyHostToDevice));
+    }
     return SG_OK;
 }
 
@@ -136,6 +186,14 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_hist, sizeof(uint32_t) * radix_hist_words(n)) != hipSuccess) return bail(SG_E_NOMEM);
+    {
+        const uint64_t tiles = n / 4096 + 1;
+        if (hipMalloc(&h->d_lim_ring, sizeof(LimRing) * kMaxLim) != hipSuccess ||
+            hipMalloc(&h->d_lim_slot, n) != hipSuccess ||
+            hipMalloc(&h->d_lim_tile, sizeof(uint32_t) * tiles * kMaxLim * 2) != hipSuccess ||
+            hipMalloc(&h->d_lim_period, sizeof(uint32_t) * kMaxLim * kMaxPeriods * 3) != hipSuccess)
+            return bail(SG_E_NOMEM);
+    }
     if (hipMalloc(&h->d_p0, sizeof(int64_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_np, sizeof(uint32_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -164,6 +222,11 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_rec);
     dfree(h->d_rec_sorted);
     dfree(h->d_hist);
+    dfree(h->d_lim_ring);
+    dfree(h->d_rule_lim);
+    dfree(h->d_lim_slot);
+    dfree(h->d_lim_tile);
+    dfree(h->d_lim_period);
     dfree(h->d_bnd);
     dfree(h->d_p0);
     dfree(h->d_np);
@@ -184,17 +247,43 @@ const char* sg_last_error(const sg_handle* h) { return h ? h->err.c_str() : "nul
 
 int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
     if (!h || (!ns && n)) return SG_E_INVAL;
+    int want = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (ns[i].limiter_enabled) {
-            // GlobalRequestLimiter pre-pass is not on the device path yet.
-            return fail(h, SG_E_UNSUPPORTED, "namespace QPS limiter is not supported by the device path yet");
+            if (!(ns[i].max_allowed_qps >= 0)) return fail(h, SG_E_INVAL, "max allowed QPS should >= 0");
+            ++want;
         }
     }
+    if (want > kMaxLim) return fail(h, SG_E_UNSUPPORTED, "more than 8 namespaces with a QPS limiter");
     for (const auto& r : h->rules)
         if (r.namespace_id < 0 || (uint32_t)r.namespace_id >= n)
             return fail(h, SG_E_INVAL, "a loaded rule refers to a namespace that would disappear");
+    HIP_TRY(h, hipSetDevice(h->device));
+    // A namespace that keeps its limiter keeps its window (GlobalRequestLimiter.initIfAbsent :32-37,
+    // applyMaxQpsChange :73-80); a newly enabled one starts empty.
+    LimRing old[kMaxLim], nw[kMaxLim];
+    if (h->n_lim) HIP_TRY(h, hipMemcpy(old, h->d_lim_ring, sizeof(LimRing) * kMaxLim, hipMemcpyDeviceToHost));
+    std::vector<int> slot(n, -1);
+    int n_lim = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!ns[i].limiter_enabled) continue;
+        const int s_new = n_lim++;
+        slot[i] = s_new;
+        h->lim_qps[s_new] = ns[i].max_allowed_qps;
+        const int s_old = (i < h->ns_slot.size()) ? h->ns_slot[i] : -1;
+        if (s_old >= 0) {
+            nw[s_new] = old[s_old];
+        } else {
+            for (int j = 0; j < kLimSamples; ++j) {
+                nw[s_new].start[j] = INT64_MIN;
+                nw[s_new].count[j] = 0;
+            }
+        }
+    }
+    if (n_lim) HIP_TRY(h, hipMemcpy(h->d_lim_ring, nw, sizeof(LimRing) * n_lim, hipMemcpyHostToDevice));
     h->ns.assign(ns, ns + n);
-    (void)hipSetDevice(h->device);
+    h->ns_slot = slot;
+    h->n_lim = n_lim;
     return upload_rule_table(h);
 }
 
@@ -244,7 +333,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
             if (n_wl == kMaxWl) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct window lengths");
             wl[n_wl++] = R.wl;
         }
-        R.wl_idx = w;
+        R.wl_idx = w;  // final indices come from rebuild_wl_table (adds the limiter's 100 ms)
         stride = std::max(stride, S);
         tab[i] = R;
     }
@@ -342,6 +431,22 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_prep(a, stream));
+    if (h->n_lim > 0) {
+        LimArgs L{};
+        L.n_lim = h->n_lim;
+        L.wl_idx = h->lim_wl_idx;
+        std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
+        L.rule_lim = h->d_rule_lim;
+        L.slot = h->d_lim_slot;
+        const uint64_t tiles = n / 4096 + 1;
+        L.tile_tot = h->d_lim_tile;
+        L.tile_off = h->d_lim_tile + tiles * kMaxLim;
+        L.arrivals = h->d_lim_period;
+        L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
+        L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
+        L.ring = h->d_lim_ring;
+        HIP_TRY(h, launch_limiter(a, L, stream));
+    }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;

@@ -74,6 +74,32 @@ struct BatchArgs {
     uint32_t short_max;  // segments longer than this go to the wave walker
 };
 
+// ---- namespace QPS limiter (limiter.hip) ----
+constexpr int kMaxLim = 8;          // namespaces with a RequestLimiter on the device path
+constexpr int kLimSamples = 10;     // RequestLimiter: new UnaryLeapArray(10, 1000) (RequestLimiter.java:35-37)
+constexpr int kLimWindowMs = 100;
+
+struct LimRing {                    // one UnaryLeapArray(10, 1000); start INT64_MIN = never created
+    int64_t start[kLimSamples];
+    int64_t count[kLimSamples];
+};
+
+struct LimArgs {
+    int n_lim;
+    int wl_idx;                     // index of the 100 ms window length in the period table
+    double qps[kMaxLim];            // RequestLimiter.qpsAllowed per slot
+    const uint8_t* rule_lim;        // [K]: limiter slot of the rule's namespace, 0xFF = none
+    uint8_t* slot;                  // [n]: limiter slot per request (0xFF = not subject to a limiter)
+    uint32_t* tile_tot;             // [tiles][kMaxLim]
+    uint32_t* tile_off;             // [tiles][kMaxLim]
+    uint32_t* arrivals;             // [kMaxLim][kMaxPeriods]
+    uint32_t* prefix;               // [kMaxLim][kMaxPeriods]
+    uint32_t* quota;                // [kMaxLim][kMaxPeriods]
+    LimRing* ring;                  // [kMaxLim]
+};
+
+hipError_t launch_limiter(const BatchArgs& a, const LimArgs& L, hipStream_t stream);
+
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, 64); result buffer is a or b.

@@ -297,3 +297,51 @@ def test_radix_sort_is_stable_partition_by_flow(n_keys, n):
     want = rec[np.argsort(rec >> np.uint64(kshift), kind="stable")]
     got = eng.debug_copy(1, np.uint64, n)
     assert np.array_equal(got, want)
+
+
+def _ns_multi(specs):
+    """specs: list of (limiter_enabled, max_allowed_qps, connected_count)."""
+    ns = np.zeros(len(specs), abi.NS_DTYPE)
+    for i, (en, q, c) in enumerate(specs):
+        ns[i] = (1 if en else 0, c, q)
+    return ns
+
+
+@pytest.mark.parametrize("flags", WALKERS)
+@pytest.mark.parametrize("qps", [0.0, 1.0, 7.5, 300.0, 5000.0, 1e12])
+def test_namespace_limiter_matches_oracle(qps, flags):
+    """GlobalRequestLimiter.tryPass (GlobalRequestLimiter.java:46-55) before every flow check:
+    TOO_MANY_REQUEST leaves the flow metric untouched; the limiter window persists across batches."""
+    rng = np.random.default_rng(int(qps * 10) % 1000 + 31)
+    rules = _rules(200, rng, counts=rng.integers(1, 200, 200).astype(float))
+    rules["namespace_id"] = rng.integers(0, 3, len(rules))
+    ns = _ns_multi([(True, qps, 1), (False, 0, 2), (True, qps * 2 + 3, 1)])
+    eng, ora = _pair(rules, ns=ns, flags=flags)
+    t = 1_700_000_000_050
+    for _ in range(3):
+        req = _trace(rng, 30_000, 200, t, int(rng.integers(50, 2500)), prio=0.05)
+        req["key"][rng.random(len(req)) < 0.02] = abi.KEY_NO_RULE
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, 700))
+        out_o = ora.decide(req)
+        _compare_results(out_o, eng.decide_host(req), req)
+    _compare_state(eng, ora, rules)
+    if 0 < qps < 1e6:
+        assert (out_o["status"] == abi.TOO_MANY_REQUEST).any()
+
+
+def test_namespace_limiter_config_changes():
+    """applyMaxQpsChange keeps the window; switching a limiter off and on again starts it empty."""
+    rng = np.random.default_rng(41)
+    rules = _rules(50, rng)
+    rules["namespace_id"] = rng.integers(0, 2, len(rules))
+    eng, ora = _pair(rules, ns=_ns_multi([(True, 40, 1), (True, 900, 1)]))
+    t = 1_700_000_000_000
+    for cfg in ([(True, 40, 1), (True, 900, 1)], [(True, 55.5, 1), (True, 10, 1)],
+                [(False, 0, 1), (True, 10, 1)], [(True, 20, 1), (True, 10, 1)]):
+        ns = _ns_multi(cfg)
+        eng.set_namespaces(ns)
+        ora.set_namespaces(ns)
+        req = _trace(rng, 8000, 50, t, 900, prio=0.1)
+        t = int(req["ts_ms"][-1]) + 30
+        _compare_results(ora.decide(req), eng.decide_host(req), req)
+    _compare_state(eng, ora, rules)
