@@ -23,20 +23,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from sentinel_amd import abi  # noqa: E402
+from sentinel_amd.cluster import MetricRollup, shard_flows  # noqa: E402
 from sentinel_amd.engine import FlowEngine  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 REQ_B, RES_B = 16, 12          # sg_req / sg_result bytes
 STATE_B = 2 * 640 + 2 * 64      # bucket ring 10×64 B read+write, occupy read+write
 RULE_B = 16
-
-
-def splitmix64_t(x):
-    x = x + 0x9E3779B97F4A7C15
-    z = x
-    z = (z ^ (z >> 30)) * -4658895280553007687  # 0xBF58476D1CE4E5B9
-    z = (z ^ (z >> 27)) * -7723592293110705685  # 0x94D049BB133111EB
-    return z ^ (z >> 31)
 
 
 class ShardWorkload:
@@ -49,24 +42,19 @@ class ShardWorkload:
         self.span_ms = span_ms
         self.t0 = t0
         self.prio_frac, self.multi_frac = prio_frac, multi_frac
-        g = torch.Generator(device="cpu").manual_seed(seed)
-        perm = torch.randperm(n_flows, generator=g)                  # global rank → flow index
-        flows = torch.arange(n_flows, dtype=torch.int64)
-        owner = (splitmix64_t(flows) & 0x7FFFFFFFFFFFFFFF) % world
-        owned_mask_by_rank = owner[perm] == rank                     # by global rank
-        ranks = torch.nonzero(owned_mask_by_rank).flatten()          # global ranks this rank owns
-        self.flow_idx = perm[ranks]                                  # their global flow indices
-        self.K = int(ranks.numel())
-        w = 1.0 / torch.pow(ranks.to(torch.float64) + 1.0, zipf_s)
-        cdf = torch.cumsum(w, 0)
-        self.cdf = (cdf / cdf[-1]).to(device)
-        # local key i ↔ global flow self.flow_idx[i]; rules follow the global flow index
         rng = np.random.default_rng(seed)
+        perm = rng.permutation(n_flows)                       # global popularity rank → flow index
+        rank_of = np.empty(n_flows, np.int64)
+        rank_of[perm] = np.arange(n_flows)
+        self.flows = shard_flows(n_flows, rank, world)        # local key i ↔ global flow self.flows[i]
+        self.K = len(self.flows)
+        w = 1.0 / np.power(rank_of[self.flows].astype(np.float64) + 1.0, zipf_s)
+        cdf = np.cumsum(w)
+        self.cdf = torch.from_numpy(cdf / cdf[-1]).to(device)
         counts = rng.integers(1, 33, n_flows).astype(np.float64)
         self.rules = np.zeros(self.K, abi.RULE_DTYPE)
-        fi = self.flow_idx.numpy()
-        self.rules["flow_id"] = fi.astype(np.int64) + 10_000_001
-        self.rules["count"] = counts[fi]
+        self.rules["flow_id"] = self.flows.astype(np.int64) + 10_000_001
+        self.rules["count"] = counts[self.flows]
         self.rules["threshold_type"] = abi.THRESHOLD_GLOBAL
         self.rules["sample_count"] = sample_count
         self.rules["window_interval_ms"] = interval_ms
@@ -148,19 +136,16 @@ def main():
     batches = [wl.batch(b) for b in range(total_steps)]
     out = torch.empty(args.requests * RES_B, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    snap = torch.empty((wl.K, 2), dtype=torch.float64, device=dev) if world > 1 else None
-    gathered = [torch.empty_like(snap) for _ in range(world)] if world > 1 else None
-    totals = torch.zeros(2, dtype=torch.float64, device=dev)
+    snap = torch.empty((wl.K, 2), dtype=torch.float64, device=dev)
+    rollup = MetricRollup(wl.K, dev) if world > 1 else None
     torch.cuda.synchronize()
 
     def step(b):
         eng.decide_device(batches[b].data_ptr(), args.requests, out.data_ptr(), stream.cuda_stream)
-        if world > 1:
+        if rollup is not None:  # node-wide metric rollup over RCCL, once per simulated second
             now = wl.t0 + (b + 1) * wl.span_ms
             eng.snapshot_device(now, snap.data_ptr(), wl.K, stream.cuda_stream)
-            torch.sum(snap, 0, out=totals)
-            dist.all_reduce(totals)
-            dist.all_gather(gathered, snap)
+            rollup.run(snap)
 
     for b in range(args.warmup):
         step(b)

@@ -1,0 +1,89 @@
+"""Node-level sharding and the metric rollup.
+
+flowIds are owned by GPU `splitmix64(flowIndex) mod G`; each rank decides only its own flows' requests,
+so the decision path needs no collective. The one exchange is the metric rollup that feeds
+`ClusterMetricNodeGenerator`-style snapshots (srv/flow/statistic/ClusterMetricNodeGenerator.java:39-105):
+per-flow {passQps, blockQps} gathered to every rank and the node totals all-reduced. With backend
+"nccl" this runs over RCCL/xGMI; the same code runs over gloo on CPU in the tests.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser of (x + golden gamma), elementwise on uint64."""
+    with np.errstate(over="ignore"):
+        z = np.asarray(x, dtype=np.uint64) + _G
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def owner_of(flow_index: np.ndarray, world: int) -> np.ndarray:
+    """GPU that owns each flow (by dense flow index)."""
+    return (splitmix64(flow_index) % np.uint64(world)).astype(np.int64)
+
+
+def shard_flows(n_flows: int, rank: int, world: int) -> np.ndarray:
+    """Global flow indices owned by `rank`, ascending (local key i ↔ global flow shard[i])."""
+    idx = np.arange(n_flows, dtype=np.uint64)
+    return np.nonzero(owner_of(idx, world) == rank)[0].astype(np.int64)
+
+
+def route_requests(req_keys: np.ndarray, world: int):
+    """Host-side partition of a node-level request array by owning GPU (stable, keeps arrival order).
+    Returns (order, counts): req_keys[order] grouped by rank, counts per rank."""
+    own = owner_of(req_keys.astype(np.uint64), world)
+    order = np.argsort(own, kind="stable")
+    counts = np.bincount(own, minlength=world)
+    return order, counts
+
+
+class MetricRollup:
+    """Per-step node-wide rollup of per-flow {passQps, blockQps} snapshots.
+
+    `snap` is this rank's [K_local, 2] float64 tensor (on the rank's device for nccl, CPU for gloo).
+    After `run()`, `totals` holds the node-wide Σ passQps / Σ blockQps and `gathered[r]` rank r's
+    snapshot (ranks may own different numbers of flows: snapshots are padded to the largest shard).
+    """
+
+    def __init__(self, k_local: int, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.device = device
+        sizes = torch.tensor([k_local], dtype=torch.int64, device=device)
+        if self.world > 1:
+            all_sizes = [torch.zeros_like(sizes) for _ in range(self.world)]
+            dist.all_gather(all_sizes, sizes, group=group)
+            self.sizes = [int(s.item()) for s in all_sizes]
+        else:
+            self.sizes = [k_local]
+        self.k_max = max(self.sizes)
+        self.padded = torch.zeros((self.k_max, 2), dtype=torch.float64, device=device)
+        self.gathered = [torch.zeros_like(self.padded) for _ in range(self.world)]
+        self.totals = torch.zeros(2, dtype=torch.float64, device=device)
+
+    def run(self, snap: torch.Tensor):
+        k = snap.shape[0]
+        self.padded[:k].copy_(snap)
+        torch.sum(snap, 0, out=self.totals)
+        if self.world > 1:
+            dist.all_reduce(self.totals, group=self.group)
+            dist.all_gather(self.gathered, self.padded, group=self.group)
+        else:
+            self.gathered[0].copy_(self.padded)
+        return self.totals
+
+    def node_snapshot(self, shards):
+        """Reassemble the node-wide [n_flows, 2] snapshot from gathered shards (shards[r] = global
+        flow indices of rank r, as from shard_flows)."""
+        n = sum(len(s) for s in shards)
+        out = torch.zeros((n, 2), dtype=torch.float64, device=self.device)
+        for r, s in enumerate(shards):
+            out[torch.as_tensor(s, device=self.device)] = self.gathered[r][: len(s)]
+        return out
