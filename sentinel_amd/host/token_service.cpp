@@ -1,0 +1,315 @@
+// token_service.cpp — see token_service.hpp.
+#include "token_service.hpp"
+
+#include <algorithm>
+#include <cctype>
+#include <stdexcept>
+
+namespace sentinel {
+namespace cluster {
+
+namespace {
+
+bool isBlank(const std::string& s) {
+    return std::all_of(s.begin(), s.end(), [](unsigned char c) { return std::isspace(c); });
+}
+
+bool validClusterRuleId(const std::optional<int64_t>& id) { return id.has_value() && *id > 0; }
+
+// FlowRuleUtil.isWindowConfigValid, FlowRuleUtil.java:227-229
+bool isWindowConfigValid(int sampleCount, int windowIntervalMs) {
+    return sampleCount > 0 && windowIntervalMs > 0 && windowIntervalMs % sampleCount == 0;
+}
+
+// FlowRuleUtil.checkClusterField, :206-225
+bool checkClusterField(const FlowRule& r) {
+    if (!r.clusterMode) return true;
+    if (!r.clusterConfig) return false;
+    const ClusterFlowConfig& c = *r.clusterConfig;
+    if (!validClusterRuleId(c.flowId)) return false;
+    if (!isWindowConfigValid(c.sampleCount, c.windowIntervalMs)) return false;
+    return c.strategy == ClusterRuleConstant::FLOW_CLUSTER_STRATEGY_NORMAL;
+}
+
+// FlowRuleUtil.checkClusterConcurrentField, :184-204
+bool checkClusterConcurrentField(const FlowRule& r) {
+    if (!r.clusterMode) return true;
+    if (!r.clusterConfig) return false;
+    const ClusterFlowConfig& c = *r.clusterConfig;
+    if (c.clientOfflineTime <= 0 || c.resourceTimeout <= 0) return false;
+    if (c.acquireRefuseStrategy < 0 || c.resourceTimeoutStrategy < 0) return false;
+    if (!validClusterRuleId(c.flowId)) return false;
+    return isWindowConfigValid(c.sampleCount, c.windowIntervalMs);
+}
+
+// FlowRuleUtil.checkStrategyField, :231-236
+bool checkStrategyField(const FlowRule& r) {
+    if (r.strategy == RuleConstant::STRATEGY_RELATE || r.strategy == RuleConstant::STRATEGY_CHAIN)
+        return !isBlank(r.refResource);
+    return true;
+}
+
+// FlowRuleUtil.checkControlBehaviorField, :238-249
+bool checkControlBehaviorField(const FlowRule& r) {
+    switch (r.controlBehavior) {
+    case RuleConstant::CONTROL_BEHAVIOR_WARM_UP: return r.warmUpPeriodSec > 0;
+    case RuleConstant::CONTROL_BEHAVIOR_RATE_LIMITER: return r.maxQueueingTimeMs > 0;
+    case RuleConstant::CONTROL_BEHAVIOR_WARM_UP_RATE_LIMITER: return r.warmUpPeriodSec > 0 && r.maxQueueingTimeMs > 0;
+    default: return true;
+    }
+}
+
+int64_t systemMillis() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+}  // namespace
+
+bool isValidRule(const FlowRule& r) {
+    const bool baseValid = !isBlank(r.resource) && r.count >= 0 && r.grade >= 0 && r.strategy >= 0 &&
+                           r.controlBehavior >= 0;
+    if (!baseValid) return false;
+    if (r.grade == RuleConstant::FLOW_GRADE_QPS)
+        return checkClusterField(r) && checkStrategyField(r) && checkControlBehaviorField(r);
+    if (r.grade == RuleConstant::FLOW_GRADE_THREAD) return checkClusterConcurrentField(r);
+    return false;
+}
+
+GpuTokenService::GpuTokenService(Options opt) : opt_(std::move(opt)) {
+    if (!opt_.clock) opt_.clock = systemMillis;
+    sg_config cfg{};
+    cfg.device = opt_.device;
+    cfg.flags = 0;
+    cfg.exceed_count = opt_.exceedCount;
+    cfg.max_occupy_ratio = opt_.maxOccupyRatio;
+    cfg.max_batch = opt_.maxBatch;
+    int rc = sg_create(&cfg, &h_);
+    if (rc != SG_OK) throw std::runtime_error("sg_create failed: " + std::to_string(rc));
+    nsIndex("default");  // ServerConstants.DEFAULT_NAMESPACE
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        pushNamespacesLocked();
+    }
+    flusher_ = std::thread([this] { flusherLoop(); });
+}
+
+GpuTokenService::~GpuTokenService() {
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        stop_ = true;
+        if (!pending_.empty()) flushLocked(lk);
+    }
+    cv_.notify_all();
+    if (flusher_.joinable()) flusher_.join();
+    sg_destroy(h_);
+}
+
+int GpuTokenService::nsIndex(const std::string& ns) {
+    for (size_t i = 0; i < nsNames_.size(); ++i)
+        if (nsNames_[i] == ns) return (int)i;
+    nsNames_.push_back(ns);
+    sg_namespace c{};
+    c.limiter_enabled = 0;
+    c.connected_count = 0;     // ConnectionManager: no connections until clients connect
+    c.max_allowed_qps = 30000; // ServerFlowConfig.DEFAULT_MAX_ALLOWED_QPS
+    nsCfg_.push_back(c);
+    return (int)nsNames_.size() - 1;
+}
+
+void GpuTokenService::pushNamespacesLocked() {
+    int rc = sg_set_namespaces(h_, nsCfg_.data(), (uint32_t)nsCfg_.size());
+    if (rc != SG_OK) err_ = sg_last_error(h_);
+}
+
+// All namespaces' rules → one dense rule table, ascending flowId (the engine keeps the windows of
+// flowIds that survive, like putMetricIfAbsent).
+void GpuTokenService::pushRulesLocked() {
+    std::vector<int64_t> ids;
+    ids.reserve(rules_.size());
+    for (const auto& kv : rules_) ids.push_back(kv.first);
+    std::sort(ids.begin(), ids.end());
+    std::vector<sg_flow_rule> tab(ids.size());
+    keyOfFlow_.clear();
+    for (size_t i = 0; i < ids.size(); ++i) {
+        const RuleEntry& e = rules_.at(ids[i]);
+        const ClusterFlowConfig& c = *e.rule.clusterConfig;
+        tab[i].flow_id = ids[i];
+        tab[i].count = e.rule.count;
+        tab[i].threshold_type = c.thresholdType;
+        tab[i].sample_count = c.sampleCount;
+        tab[i].window_interval_ms = c.windowIntervalMs;
+        tab[i].namespace_id = nsIndex(e.ns);
+        keyOfFlow_[ids[i]] = (uint32_t)i;
+    }
+    pushNamespacesLocked();
+    int rc = sg_load_flow_rules(h_, tab.data(), (uint32_t)tab.size());
+    if (rc != SG_OK) {
+        err_ = sg_last_error(h_);
+        keyOfFlow_.clear();
+    }
+}
+
+// ClusterFlowRuleManager.applyClusterFlowRule, ClusterFlowRuleManager.java:325-375
+void GpuTokenService::loadRules(const std::string& ns, const std::vector<FlowRule>& list) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);  // a reload is a barrier between batches
+    std::map<int64_t, FlowRule> ruleMap;
+    for (const FlowRule& r0 : list) {
+        if (!r0.clusterMode) continue;
+        if (!isValidRule(r0)) continue;   // "Ignoring invalid flow rule"
+        FlowRule r = r0;
+        if (isBlank(r.limitApp)) r.limitApp = "default";
+        const auto& flowId = r.clusterConfig->flowId;
+        if (!flowId) continue;
+        ruleMap[*flowId] = r;             // the last duplicate wins (ruleMap.put)
+    }
+    // clearAndResetRulesConditional: drop this namespace's flowIds that are not in the new set
+    for (int64_t id : nsFlowIds_[ns])
+        if (!ruleMap.count(id)) rules_.erase(id);
+    std::vector<int64_t> ids;
+    for (auto& kv : ruleMap) {
+        rules_[kv.first] = RuleEntry{kv.second, ns};
+        ids.push_back(kv.first);
+    }
+    nsFlowIds_[ns] = ids;
+    nsIndex(ns);
+    pushRulesLocked();
+}
+
+void GpuTokenService::loadServerFlowConfig(const std::string& ns, bool limiterEnabled, double maxAllowedQps) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    const int i = nsIndex(ns);
+    nsCfg_[i].limiter_enabled = limiterEnabled ? 1 : 0;
+    nsCfg_[i].max_allowed_qps = maxAllowedQps;
+    pushNamespacesLocked();
+}
+
+void GpuTokenService::setConnectedCount(const std::string& ns, int connected) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    nsCfg_[nsIndex(ns)].connected_count = connected;
+    pushNamespacesLocked();
+}
+
+std::optional<FlowRule> GpuTokenService::getFlowRuleById(int64_t id) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (id <= 0) return std::nullopt;  // ClusterRuleUtil.validId
+    auto it = rules_.find(id);
+    if (it == rules_.end()) return std::nullopt;
+    return it->second.rule;
+}
+
+std::optional<std::string> GpuTokenService::getNamespace(int64_t flowId) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    auto it = rules_.find(flowId);
+    if (it == rules_.end()) return std::nullopt;
+    return it->second.ns;
+}
+
+// DefaultTokenService.notValidRequest (id) and the rule lookup (:39-47); acquireCount <= 0 is
+// answered BAD_REQUEST by the engine itself.
+uint32_t GpuTokenService::keyOf(std::optional<int64_t> ruleId, bool prioritized) const {
+    if (!ruleId || *ruleId <= 0) return SG_KEY_BAD;
+    auto it = keyOfFlow_.find(*ruleId);
+    if (it == keyOfFlow_.end()) return SG_KEY_NO_RULE;
+    return it->second | (prioritized ? SG_KEY_PRIO : 0u);
+}
+
+std::vector<TokenResult> GpuTokenService::decideLocked(std::vector<sg_req>& reqs) {
+    std::vector<TokenResult> res(reqs.size(), TokenResult(TokenResultStatus::FAIL));
+    if (reqs.empty()) return res;
+    std::vector<sg_result> out(reqs.size());
+    for (size_t off = 0; off < reqs.size(); off += opt_.maxBatch) {
+        const size_t n = std::min<size_t>(opt_.maxBatch, reqs.size() - off);
+        int rc = sg_flow_decide_batch_host(h_, reqs.data() + off, n, out.data() + off);
+        if (rc != SG_OK) {  // TokenResult(FAIL) → the client falls back to local checking
+            err_ = sg_last_error(h_);
+            continue;
+        }
+        for (size_t i = off; i < off + n; ++i)
+            res[i] = TokenResult(out[i].status).setRemaining(out[i].remaining).setWaitInMs(out[i].wait_ms);
+    }
+    return res;
+}
+
+std::vector<TokenResult> GpuTokenService::requestTokens(const std::vector<TokenRequest>& reqs) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    std::vector<sg_req> r(reqs.size());
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        r[i].ts_ms = reqs[i].timeMillis;
+        r[i].key = keyOf(reqs[i].ruleId, reqs[i].prioritized);
+        r[i].acquire = reqs[i].acquireCount;
+        if (reqs[i].timeMillis > lastTs_) lastTs_ = reqs[i].timeMillis;
+    }
+    return decideLocked(r);
+}
+
+TokenResult GpuTokenService::requestToken(std::optional<int64_t> ruleId, int acquireCount, bool prioritized) {
+    std::promise<TokenResult> p;
+    std::future<TokenResult> f = p.get_future();
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        sg_req r;
+        // TimeUtil.currentTimeMillis at the call; kept non-decreasing in arrival order
+        const int64_t now = opt_.clock();
+        lastTs_ = std::max(lastTs_, now);
+        r.ts_ms = lastTs_;
+        r.key = keyOf(ruleId, prioritized);
+        r.acquire = acquireCount;
+        if (pending_.empty()) oldest_ = std::chrono::steady_clock::now();
+        pending_.push_back(Pending{r, &p});
+        if (pending_.size() >= opt_.flushSize) flushLocked(lk);
+        else if (pending_.size() == 1) cv_.notify_all();
+    }
+    return f.get();
+}
+
+void GpuTokenService::flushLocked(std::unique_lock<std::mutex>& lk) {
+    std::vector<Pending> batch;
+    batch.swap(pending_);
+    std::vector<sg_req> reqs(batch.size());
+    for (size_t i = 0; i < batch.size(); ++i) reqs[i] = batch[i].req;
+    std::vector<TokenResult> res = decideLocked(reqs);
+    for (size_t i = 0; i < batch.size(); ++i) batch[i].result->set_value(res[i]);
+    (void)lk;
+}
+
+void GpuTokenService::flusherLoop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (!stop_) {
+        if (pending_.empty()) {
+            cv_.wait(lk, [this] { return stop_ || !pending_.empty(); });
+            continue;
+        }
+        const auto deadline = oldest_ + opt_.flushDelay;
+        if (std::chrono::steady_clock::now() >= deadline) {
+            flushLocked(lk);
+        } else {
+            cv_.wait_until(lk, deadline);
+        }
+    }
+}
+
+// The device path covers flow tokens only; parameter and concurrent tokens answer FAIL, so the
+// client's fallback (FlowRuleChecker / ParamFlowChecker local checks) applies, as for an absent server.
+TokenResult GpuTokenService::requestParamToken(std::optional<int64_t> ruleId, int acquireCount,
+                                               const std::vector<std::string>& params) {
+    if (!ruleId || *ruleId <= 0 || acquireCount <= 0 || params.empty())
+        return TokenResult(TokenResultStatus::BAD_REQUEST);  // DefaultTokenService.java:53-56
+    return TokenResult(TokenResultStatus::FAIL);
+}
+
+TokenResult GpuTokenService::requestConcurrentToken(const std::string& clientAddress, std::optional<int64_t> ruleId,
+                                                    int acquireCount) {
+    if (clientAddress.empty() || !ruleId || *ruleId <= 0 || acquireCount <= 0)
+        return TokenResult(TokenResultStatus::BAD_REQUEST);  // DefaultTokenService.java:67-70, 91-93
+    return TokenResult(TokenResultStatus::FAIL);
+}
+
+void GpuTokenService::releaseConcurrentToken(std::optional<int64_t>) {}
+
+}  // namespace cluster
+}  // namespace sentinel

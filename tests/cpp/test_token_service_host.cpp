@@ -1,0 +1,154 @@
+// CPU test of the C++ host mirror (sentinel_amd/host/token_service.cpp) against the recording fake.
+// Prints "OK <n checks>" or exits non-zero with the failing check.
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+
+#include "../../sentinel_amd/host/token_service.hpp"
+
+namespace fake {
+extern std::vector<sg_flow_rule> rules;
+extern std::vector<sg_namespace> ns;
+extern std::vector<std::vector<sg_req>> batches;
+extern int fail_next;
+}  // namespace fake
+
+using namespace sentinel::cluster;
+static int checks = 0;
+#define CHECK(c)                                                          \
+    do {                                                                  \
+        ++checks;                                                         \
+        if (!(c)) {                                                       \
+            std::fprintf(stderr, "FAILED %s at line %d\n", #c, __LINE__); \
+            std::exit(1);                                                 \
+        }                                                                 \
+    } while (0)
+
+static FlowRule clusterRule(int64_t flowId, double count, int thr = ClusterRuleConstant::FLOW_THRESHOLD_GLOBAL) {
+    FlowRule r;
+    r.resource = "res" + std::to_string(flowId);
+    r.count = count;
+    r.clusterMode = true;
+    ClusterFlowConfig c;
+    c.flowId = flowId;
+    c.thresholdType = thr;
+    r.clusterConfig = c;
+    return r;
+}
+
+int main() {
+    int64_t now = 1'700'000'000'000;
+    GpuTokenService::Options opt;
+    opt.flushSize = 64;
+    opt.flushDelay = std::chrono::microseconds(300);
+    opt.clock = [&] { return now; };
+    GpuTokenService svc(opt);
+
+    // --- FlowRuleUtil.isValidRule / applyClusterFlowRule filtering
+    std::vector<FlowRule> rs;
+    rs.push_back(clusterRule(30, 5));
+    rs.push_back(clusterRule(10, 7));
+    FlowRule local = clusterRule(11, 3);
+    local.clusterMode = false;                       // not cluster mode: skipped
+    rs.push_back(local);
+    FlowRule bad = clusterRule(12, -1);              // count < 0: invalid
+    rs.push_back(bad);
+    FlowRule badWin = clusterRule(13, 1);
+    badWin.clusterConfig->sampleCount = 3;           // 1000 % 3 != 0: invalid window
+    rs.push_back(badWin);
+    FlowRule noId = clusterRule(14, 1);
+    noId.clusterConfig->flowId.reset();              // flowId null: invalid cluster id
+    rs.push_back(noId);
+    FlowRule relate = clusterRule(15, 1);
+    relate.strategy = RuleConstant::STRATEGY_RELATE; // RELATE without refResource: invalid
+    rs.push_back(relate);
+    FlowRule dup = clusterRule(10, 9);               // duplicate flowId: the last one wins
+    rs.push_back(dup);
+    FlowRule thread = clusterRule(20, 4);
+    thread.grade = RuleConstant::FLOW_GRADE_THREAD;  // concurrent cluster rule: valid, loaded
+    rs.push_back(thread);
+    svc.loadRules("ns-a", rs);
+    CHECK(fake::rules.size() == 3);
+    CHECK(fake::rules[0].flow_id == 10 && fake::rules[0].count == 9);
+    CHECK(fake::rules[1].flow_id == 20 && fake::rules[2].flow_id == 30);
+    CHECK(svc.getFlowRuleById(10).has_value() && !svc.getFlowRuleById(11).has_value());
+    CHECK(!svc.getFlowRuleById(0).has_value() && !svc.getFlowRuleById(-10).has_value());
+    CHECK(svc.getNamespace(30).value() == "ns-a");
+    const int nsA = fake::rules[0].namespace_id;
+    CHECK(fake::ns.size() == 2 && nsA == 1);   // "default" + "ns-a"
+
+    // second namespace; reload of ns-a drops 20 and keeps ns-b's rules
+    svc.loadRules("ns-b", {clusterRule(40, 2, ClusterRuleConstant::FLOW_THRESHOLD_AVG_LOCAL)});
+    svc.loadRules("ns-a", {clusterRule(10, 9), clusterRule(30, 5)});
+    CHECK(fake::rules.size() == 3);
+    CHECK(fake::rules[0].flow_id == 10 && fake::rules[1].flow_id == 30 && fake::rules[2].flow_id == 40);
+    CHECK(fake::rules[2].namespace_id == 2 && fake::rules[2].threshold_type == 0);
+    svc.setConnectedCount("ns-b", 3);
+    svc.loadServerFlowConfig("ns-b", true, 1234.5);
+    CHECK(fake::ns[2].connected_count == 3 && fake::ns[2].limiter_enabled == 1 && fake::ns[2].max_allowed_qps == 1234.5);
+
+    // --- deterministic batch: validation and key mapping (DefaultTokenService.java:39-50, 87-89)
+    fake::batches.clear();
+    std::vector<TokenRequest> reqs = {{now, 30, 2, false}, {now, 10, 1, true}, {now, std::nullopt, 1, false},
+                                      {now, 0, 1, false},  {now, -5, 1, false}, {now + 1, 99, 1, false},
+                                      {now + 2, 40, 3, false}};
+    auto res = svc.requestTokens(reqs);
+    CHECK(fake::batches.size() == 1 && fake::batches[0].size() == reqs.size());
+    const auto& b = fake::batches[0];
+    CHECK(b[0].key == 1u && b[0].acquire == 2 && b[0].ts_ms == now);
+    CHECK(b[1].key == (0u | SG_KEY_PRIO));
+    CHECK(b[2].key == SG_KEY_BAD && b[3].key == SG_KEY_BAD && b[4].key == SG_KEY_BAD);
+    CHECK(b[5].key == SG_KEY_NO_RULE);
+    CHECK(b[6].key == 2u && b[6].ts_ms == now + 2);
+    CHECK(res[0].getStatus().value() == TokenResultStatus::OK && res[0].getRemaining() == 1);
+    CHECK(res[2].getStatus().value() == TokenResultStatus::BAD_REQUEST);
+    CHECK(res[5].getStatus().value() == TokenResultStatus::NO_RULE_EXISTS);
+
+    // --- engine failure → FAIL for the whole batch (client falls back to local)
+    fake::fail_next = 1;
+    auto failed = svc.requestTokens({{now + 3, 30, 1, false}, {now + 3, 10, 1, false}});
+    CHECK(failed[0].getStatus().value() == TokenResultStatus::FAIL && failed[1].getStatus().value() == TokenResultStatus::FAIL);
+
+    // --- param / concurrent tokens are not on the device path: validation, then FAIL
+    CHECK(svc.requestParamToken(30, 1, {}).getStatus().value() == TokenResultStatus::BAD_REQUEST);
+    CHECK(svc.requestParamToken(30, 1, {"x"}).getStatus().value() == TokenResultStatus::FAIL);
+    CHECK(svc.requestConcurrentToken("", 30, 1).getStatus().value() == TokenResultStatus::BAD_REQUEST);
+
+    // --- concurrent requestToken: micro-batched, every caller answered, timestamps non-decreasing
+    fake::batches.clear();
+    std::atomic<int> okCount{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t) {
+        th.emplace_back([&, t] {
+            for (int i = 0; i < 500; ++i) {
+                TokenResult r = svc.requestToken(t % 2 ? 10 : 30, 1 + (i % 3), i % 7 == 0);
+                if (r.getStatus().value() == TokenResultStatus::OK && r.getWaitInMs() == 1 + (i % 3)) ++okCount;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    CHECK(okCount.load() == 4000);
+    size_t total = 0;
+    int64_t last = -1;
+    bool monotone = true;
+    for (const auto& bb : fake::batches) {
+        CHECK(bb.size() <= 64);
+        total += bb.size();
+        for (const auto& r : bb) {
+            monotone = monotone && r.ts_ms >= last;
+            last = r.ts_ms;
+        }
+    }
+    CHECK(total == 4000 && monotone);
+    CHECK(fake::batches.size() >= 4000 / 64);
+
+    // single caller: flushed by the deadline, not by size
+    fake::batches.clear();
+    TokenResult single = svc.requestToken(40, 2, false);
+    CHECK(single.getStatus().value() == TokenResultStatus::OK && single.getRemaining() == 2);
+    CHECK(fake::batches.size() == 1 && fake::batches[0].size() == 1);
+
+    std::printf("OK %d\n", checks);
+    return 0;
+}
