@@ -130,6 +130,36 @@ typedef struct sg_result {
     int32_t wait_ms;
 } sg_result;
 
+/* ---- hot-parameter flow control (ParamFlowChecker, sentinel-extension/sentinel-parameter-flow-control) ---- */
+
+/* One QPS ParamFlowRule (ParamFlowRule.java:45-83). The parameter value itself is a u64 chosen by the
+ * caller (a Long argument as is, other types through the shim's value dictionary). */
+typedef struct sg_param_rule {
+    double   count;             /* ParamFlowRule.count (token count per duration)                 */
+    int64_t  duration_sec;      /* durationInSec, default 1                                       */
+    int32_t  burst;             /* burstCount, default 0                                          */
+    int32_t  behavior;          /* CONTROL_BEHAVIOR_DEFAULT 0 (token bucket) / RATE_LIMITER 2      */
+    int32_t  max_queueing_ms;   /* maxQueueingTimeMs (throttle), default 0                        */
+    uint32_t hot_begin;         /* this rule's hot items: hot[hot_begin .. hot_begin + hot_count) */
+    uint32_t hot_count;
+    int32_t  reserved;
+} sg_param_rule;
+
+/* ParamFlowItem → parsed hot item: value-specific threshold (ParamFlowRuleUtil.parseHotItems :188-209). */
+typedef struct sg_param_hot_item {
+    uint64_t value;
+    int32_t  threshold;
+    int32_t  reserved;
+} sg_param_hot_item;
+
+/* One single-value check: passSingleValueCheck(rule, acquireCount, value) at ts_ms. */
+typedef struct sg_param_req {
+    int64_t  ts_ms;
+    uint64_t value;
+    uint32_t rule;              /* index into the loaded param rules                               */
+    int32_t  acquire;           /* acquireCount                                                    */
+} sg_param_req;
+
 /* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
 typedef struct sg_batch_stats {
     float    total_ms;          /* whole pipeline                                         */

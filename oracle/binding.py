@@ -60,6 +60,11 @@ def lib():
         "or_cts_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
         "or_cts_sample_count": (C.c_int, [vp, u32]),
         "or_cts_avg": (d, [vp, u32, i64, C.c_int]),
+        "or_pf_new": (vp, []), "or_pf_free": (None, [vp]),
+        "or_pf_load_rules": (C.c_int, [vp, vp, u32, vp, u32]),
+        "or_pf_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_pf_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
+        "or_pf_size": (u64, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -228,3 +233,39 @@ class ClusterTokenService:
         rc = lib().or_cts_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ))
         assert rc == 0
         return starts, counters.reshape(S, abi.NUM_EVENTS), occ
+
+
+class ParamFlowChecker:
+    """Sequential replay of ParamFlowChecker.passSingleValueCheck (QPS default / throttle), exact maps."""
+
+    def __init__(self):
+        self.h = lib().or_pf_new()
+
+    def __del__(self):
+        if self.h:
+            lib().or_pf_free(self.h)
+            self.h = None
+
+    def load_rules(self, rules, hot=None):
+        rules = np.ascontiguousarray(rules, dtype=abi.PARAM_RULE_DTYPE)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        assert lib().or_pf_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot)) == 0
+
+    def decide(self, req):
+        req = np.ascontiguousarray(req, dtype=abi.PARAM_REQ_DTYPE)
+        out = np.zeros(len(req), np.int32)
+        lib().or_pf_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
+        return out
+
+    def check(self, t, rule, value, acquire=1):
+        r = np.zeros(1, abi.PARAM_REQ_DTYPE)
+        r[0] = (t, value, rule, acquire)
+        return bool(self.decide(r)[0])
+
+    def state(self, rule, value):
+        lt, tk = C.c_int64(), C.c_int64()
+        flags = lib().or_pf_read_state(self.h, rule, value, C.byref(lt), C.byref(tk))
+        return flags, lt.value, tk.value
+
+    def size(self):
+        return lib().or_pf_size(self.h)

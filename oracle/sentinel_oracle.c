@@ -556,3 +556,194 @@ int or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* c
     occupy[1] = m->occ[SG_EV_PASS_REQUEST];
     return 0;
 }
+
+/* ===================================================================================== */
+/* Hot-parameter flow control: ParamFlowChecker.passDefaultLocalCheck / passThrottleLocalCheck */
+/* (sentinel-extension/sentinel-parameter-flow-control/.../slots/block/flow/param/ParamFlowChecker.java) */
+/* ===================================================================================== */
+/* The reference keeps per-rule CacheMaps (ConcurrentLinkedHashMap LRU, capacity
+ * min(4000 * durationInSec, 200000), ParameterMetric.java:95-122). This restatement keeps exact,
+ * unbounded maps: it equals the reference whenever the distinct values per rule stay within that
+ * capacity (eviction order is CLHM's and is not pinned by any reference test). */
+
+typedef struct or_pf_slot {
+    uint64_t value;
+    uint32_t rule;
+    uint8_t used, has_time, has_tokens;
+    int64_t time;   /* timeCounters[value]  (lastAddTokenTime / last pass time for the throttle) */
+    int64_t tokens; /* tokenCounters[value] */
+} or_pf_slot;
+
+struct or_pf {
+    sg_param_rule* rules;
+    uint32_t n_rules;
+    sg_param_hot_item* hot;
+    uint32_t n_hot;
+    or_pf_slot* tab;
+    uint64_t cap, size;
+};
+
+static uint64_t pf_hash(uint32_t rule, uint64_t v) {
+    uint64_t z = v + 0x9E3779B97F4A7C15ULL * (rule + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+or_pf* or_pf_new(void) {
+    or_pf* p = (or_pf*)calloc(1, sizeof(or_pf));
+    p->cap = 1024;
+    p->tab = (or_pf_slot*)calloc(p->cap, sizeof(or_pf_slot));
+    return p;
+}
+
+void or_pf_free(or_pf* p) {
+    if (!p) return;
+    free(p->rules);
+    free(p->hot);
+    free(p->tab);
+    free(p);
+}
+
+static or_pf_slot* pf_find(const or_pf* p, uint32_t rule, uint64_t v) {
+    uint64_t i = pf_hash(rule, v) & (p->cap - 1);
+    for (;;) {
+        or_pf_slot* s = &p->tab[i];
+        if (!s->used) return s;
+        if (s->rule == rule && s->value == v) return s;
+        i = (i + 1) & (p->cap - 1);
+    }
+}
+
+static void pf_grow(or_pf* p) {
+    or_pf_slot* old = p->tab;
+    uint64_t oc = p->cap;
+    p->cap *= 2;
+    p->tab = (or_pf_slot*)calloc(p->cap, sizeof(or_pf_slot));
+    for (uint64_t i = 0; i < oc; i++)
+        if (old[i].used) *pf_find(p, old[i].rule, old[i].value) = old[i];
+    free(old);
+}
+
+static or_pf_slot* pf_get_or_add(or_pf* p, uint32_t rule, uint64_t v) {
+    if ((p->size + 1) * 2 > p->cap) pf_grow(p);
+    or_pf_slot* s = pf_find(p, rule, v);
+    if (!s->used) {
+        s->used = 1;
+        s->rule = rule;
+        s->value = v;
+        s->has_time = s->has_tokens = 0;
+        p->size++;
+    }
+    return s;
+}
+
+/* A rule reload rebuilds the per-rule maps (ParameterMetricStorage.initParamMetricsFor creates maps for
+ * rules not seen before; rules are keyed by equality, so here by position): state is cleared. */
+int or_pf_load_rules(or_pf* p, const sg_param_rule* rules, uint32_t n, const sg_param_hot_item* hot, uint32_t n_hot) {
+    free(p->rules);
+    free(p->hot);
+    p->rules = (sg_param_rule*)calloc(n ? n : 1, sizeof(sg_param_rule));
+    memcpy(p->rules, rules, n * sizeof(sg_param_rule));
+    p->n_rules = n;
+    p->hot = (sg_param_hot_item*)calloc(n_hot ? n_hot : 1, sizeof(sg_param_hot_item));
+    memcpy(p->hot, hot, n_hot * sizeof(sg_param_hot_item));
+    p->n_hot = n_hot;
+    memset(p->tab, 0, p->cap * sizeof(or_pf_slot));
+    p->size = 0;
+    return 0;
+}
+
+/* tokenCount: the hot item's threshold when the value is one, else (long) rule.count (:137-141). */
+static int64_t pf_token_count(const or_pf* p, const sg_param_rule* r, uint64_t v) {
+    for (uint32_t i = 0; i < r->hot_count; i++)
+        if (p->hot[r->hot_begin + i].value == v) return p->hot[r->hot_begin + i].threshold;
+    return or_d2l(r->count);
+}
+
+/* passDefaultLocalCheck, ParamFlowChecker.java:127-202 (single-threaded: CAS retries collapse). */
+static int pf_default(or_pf* p, uint32_t ri, uint64_t v, int64_t t, int acquire) {
+    const sg_param_rule* r = &p->rules[ri];
+    int64_t token_count = pf_token_count(p, r, v);
+    if (token_count == 0) return 0;
+    int64_t max_count = token_count + r->burst;
+    if (acquire > max_count) return 0;
+    or_pf_slot* s = pf_get_or_add(p, ri, v);
+    if (!s->has_time) {                  /* timeCounters.putIfAbsent → absent */
+        s->has_time = 1;
+        s->time = t;
+        if (!s->has_tokens) {            /* tokenCounters.putIfAbsent keeps existing tokens */
+            s->has_tokens = 1;
+            s->tokens = max_count - acquire;
+        }
+        return 1;
+    }
+    int64_t pass_time = t - s->time;
+    if (pass_time > r->duration_sec * 1000) {
+        if (!s->has_tokens) {
+            s->has_tokens = 1;
+            s->tokens = max_count - acquire;
+            s->time = t;
+            return 1;
+        }
+        int64_t rest = s->tokens;
+        int64_t to_add = (pass_time * token_count) / (r->duration_sec * 1000);
+        int64_t new_qps = to_add + rest > max_count ? (max_count - acquire) : (rest + to_add - acquire);
+        if (new_qps < 0) return 0;       /* lastAddTokenTime unchanged */
+        s->tokens = new_qps;
+        s->time = t;
+        return 1;
+    }
+    if (s->has_tokens) {
+        if (s->tokens - acquire >= 0) {
+            s->tokens -= acquire;
+            return 1;
+        }
+        return 0;
+    }
+    return 0; /* Java spins (Thread.yield) until tokens appear; unreachable without LRU eviction */
+}
+
+/* passThrottleLocalCheck, ParamFlowChecker.java:204-254 (the wait is a sleep; replay skips it). */
+static int pf_throttle(or_pf* p, uint32_t ri, uint64_t v, int64_t t, int acquire) {
+    const sg_param_rule* r = &p->rules[ri];
+    int64_t token_count = pf_token_count(p, r, v);
+    if (token_count == 0) return 0;
+    int64_t cost = or_math_round(1.0 * 1000 * acquire * (double)r->duration_sec / (double)token_count);
+    or_pf_slot* s = pf_get_or_add(p, ri, v);
+    if (!s->has_time) {
+        s->has_time = 1;
+        s->time = t;
+        return 1;
+    }
+    int64_t last = s->time;
+    int64_t expected = last + cost;
+    if (expected <= t || expected - t < r->max_queueing_ms) {
+        s->time = t;
+        if (expected - t > 0) s->time = expected;
+        return 1;
+    }
+    return 0;
+}
+
+int or_pf_decide(or_pf* p, const sg_param_req* req, uint64_t n, int32_t* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t ri = req[i].rule;
+        if (ri >= p->n_rules) { out[i] = 1; continue; } /* no rule for the resource: pass */
+        if (p->rules[ri].behavior == 2)                 /* RuleConstant.CONTROL_BEHAVIOR_RATE_LIMITER */
+            out[i] = pf_throttle(p, ri, req[i].value, req[i].ts_ms, req[i].acquire);
+        else
+            out[i] = pf_default(p, ri, req[i].value, req[i].ts_ms, req[i].acquire);
+    }
+    return 0;
+}
+
+int or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens) {
+    or_pf_slot* s = pf_find(p, rule, value);
+    if (!s->used) return 0;
+    *last_time = s->time;
+    *tokens = s->tokens;
+    return (s->has_time ? 1 : 0) | (s->has_tokens ? 2 : 0);
+}
+
+uint64_t or_pf_size(const or_pf* p) { return p->size; }

@@ -100,6 +100,17 @@ int     or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_
 int     or_cts_sample_count(const or_cts* s, uint32_t key);
 double  or_cts_avg(or_cts* s, uint32_t key, int64_t now, int ev);
 
+/* ---------- hot-parameter flow control (ParamFlowChecker QPS paths, exact unbounded maps) ---------- */
+typedef struct or_pf or_pf;
+or_pf*  or_pf_new(void);
+void    or_pf_free(or_pf* p);
+int     or_pf_load_rules(or_pf* p, const sg_param_rule* rules, uint32_t n, const sg_param_hot_item* hot, uint32_t n_hot);
+/* out[i] = 1 pass / 0 block, replaying in array order. */
+int     or_pf_decide(or_pf* p, const sg_param_req* req, uint64_t n, int32_t* out);
+/* State of (rule, value): returns bit0 = time counter present, bit1 = token counter present. */
+int     or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+uint64_t or_pf_size(const or_pf* p);
+
 #ifdef __cplusplus
 }
 #endif

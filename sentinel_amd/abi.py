@@ -76,6 +76,14 @@ RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", 
 NS_DTYPE = np.dtype([("limiter_enabled", "<i4"), ("connected_count", "<i4"), ("max_allowed_qps", "<f8")],
                     align=True)
 
+PARAM_RULE_DTYPE = np.dtype([("count", "<f8"), ("duration_sec", "<i8"), ("burst", "<i4"), ("behavior", "<i4"),
+                             ("max_queueing_ms", "<i4"), ("hot_begin", "<u4"), ("hot_count", "<u4"),
+                             ("reserved", "<i4")], align=True)
+PARAM_HOT_DTYPE = np.dtype([("value", "<u8"), ("threshold", "<i4"), ("reserved", "<i4")], align=True)
+PARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("value", "<u8"), ("rule", "<u4"), ("acquire", "<i4")], align=True)
+BEHAVIOR_DEFAULT = 0
+BEHAVIOR_RATE_LIMITER = 2
+
 assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
 assert RES_DTYPE.itemsize == C.sizeof(sg_result) == 12
 assert RULE_DTYPE.itemsize == C.sizeof(sg_flow_rule) == 32
