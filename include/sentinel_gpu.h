@@ -167,6 +167,7 @@ typedef struct sg_batch_stats {
     float    sort_ms;           /* key partition (radix sort)                             */
     uint64_t touched_keys;      /* distinct flowIds that received >= 1 request            */
     uint64_t long_segments;     /* flowIds walked by a whole wave                         */
+    uint64_t skipped_ranges;    /* all-BLOCKED period tails the wave walker jumped over   */
 } sg_batch_stats;
 
 int         sg_create(const sg_config* cfg, sg_handle** out);

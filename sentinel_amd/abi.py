@@ -65,7 +65,7 @@ class sg_result(C.Structure):
 
 class sg_batch_stats(C.Structure):
     _fields_ = [("total_ms", C.c_float), ("walk_ms", C.c_float), ("sort_ms", C.c_float),
-                ("touched_keys", C.c_uint64), ("long_segments", C.c_uint64)]
+                ("touched_keys", C.c_uint64), ("long_segments", C.c_uint64), ("skipped_ranges", C.c_uint64)]
 
 
 # numpy views of the request / result records (same layout as the C structs)

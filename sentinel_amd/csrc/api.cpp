@@ -43,8 +43,10 @@ struct sg_handle {
     int64_t* d_last_ts = nullptr;
     uint32_t* d_long_list = nullptr;
     uint32_t* d_long_count = nullptr;
+    uint4* d_skips = nullptr;
+    uint32_t* d_skip_count = nullptr;
     int* h_err = nullptr;       // pinned
-    uint32_t* h_long = nullptr; // pinned
+    uint32_t* h_long = nullptr; // pinned: long segment count, skipped range count
 
     // host-buffer convenience path
     sg_req* d_req_h = nullptr;
@@ -200,8 +202,10 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_skips, sizeof(uint4) * (n / kSkipMin + 1)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_skip_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipHostMalloc(&h->h_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipHostMalloc(&h->h_long, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipHostMalloc(&h->h_long, 2 * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     int64_t neg = -1;
     if (hipMemcpy(h->d_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     for (auto& e : h->ev)
@@ -234,6 +238,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_last_ts);
     dfree(h->d_long_list);
     dfree(h->d_long_count);
+    dfree(h->d_skips);
+    dfree(h->d_skip_count);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
     if (h->h_err) (void)hipHostFree(h->h_err);
@@ -424,12 +430,16 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.last_ts = h->d_last_ts;
     a.long_list = h->d_long_list;
     a.long_count = h->d_long_count;
+    a.skips = h->d_skips;
+    a.skip_count = h->d_skip_count;
+    a.skip_cap = (uint32_t)(h->cfg.max_batch / kSkipMin + 1);
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
                   : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : (uint32_t)kShortMax;
 
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_skip_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_prep(a, stream));
     if (h->n_lim > 0) {
         LimArgs L{};
@@ -457,11 +467,13 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_walk_short(a, stream));
     HIP_TRY(h, launch_walk_long(a, stream));
+    HIP_TRY(h, launch_skip_apply(a, stream));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, launch_finish(a, stream));
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
         HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, h->d_skip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipEventRecord(h->ev[4], stream));
     }
     HIP_TRY(h, hipStreamSynchronize(stream));
@@ -473,7 +485,8 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         h->stats.sort_ms = ms;
         (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
         h->stats.walk_ms = ms;
-        h->stats.long_segments = *h->h_long;
+        h->stats.long_segments = h->h_long[0];
+        h->stats.skipped_ranges = h->h_long[1];
     }
     if (*h->h_err & kErrTime)
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");

@@ -72,7 +72,13 @@ struct BatchArgs {
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
     uint32_t short_max;  // segments longer than this go to the wave walker
+    // ranges of records the wave walker skipped as certainly BLOCKED: {flow key, period q, begin, end}
+    uint4* skips;
+    uint32_t* skip_count;
+    uint32_t skip_cap;
 };
+
+constexpr uint32_t kSkipMin = 256;  // shortest all-BLOCKED tail worth skipping (records)
 
 // ---- namespace QPS limiter (limiter.hip) ----
 constexpr int kMaxLim = 8;          // namespaces with a RequestLimiter on the device path
@@ -109,6 +115,7 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,
                              const Bucket* old_ring, const Occ* old_occ, int old_stride, hipStream_t stream);
 hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,

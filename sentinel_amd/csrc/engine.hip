@@ -353,6 +353,9 @@ struct WaveWalker {
     int I;
     // deferred per-lane BLOCK / BLOCK_REQUEST / OCCUPIED_BLOCK of the current period
     int64_t d_blk, d_blkn, d_oblk;
+    // the current period can admit nothing more: not even acquireCount = 1 fits and no prioritized
+    // request can occupy (both only get harder within a period), so its remaining requests are BLOCKED
+    bool dead;
 
     __device__ WaveWalker(const BatchArgs& a_, uint32_t k) : a(a_), R(a_.rules[k]), lane(lane_id()) {
         ring = a.ring + (size_t)k * a.stride;
@@ -375,6 +378,7 @@ struct WaveWalker {
         ws = 0;
         I = -1;
         d_blk = d_blkn = d_oblk = 0;
+        dead = false;
     }
 
     // close the current bucket (flush deferred counts) into its owner lane
@@ -393,6 +397,7 @@ struct WaveWalker {
 
     __device__ void open_period(uint32_t q) {
         close_period();
+        dead = false;
         pc.seek(q);
         const int64_t P = P0 + (int64_t)q;
         const int S = R.S;
@@ -441,6 +446,7 @@ struct WaveWalker {
             d_blk += rest ? d.acq : 0;
             d_blkn += rest ? 1 : 0;
             d_oblk += (rest && d.prio) ? d.acq : 0;
+            dead = !occupy_possible(latest0);
             return;
         }
         uint64_t pending = run_mask;
@@ -533,6 +539,29 @@ struct WaveWalker {
     }
 };
 
+// First position p in [lo, hi) with pred(p) (pred monotone false→true), hi if none. 64-way wave search:
+// every step probes 64 evenly spaced positions, so a million-record range takes 4 dependent loads.
+template <class Pred>
+__device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t p = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(p >= hi || pred(p));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t p = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(p < hi && pred(p));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
+}
+
 __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
     WaveWalker w(a, k);
     const int lane = w.lane;
@@ -544,20 +573,53 @@ __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e
         const uint64_t j = s + (uint64_t)u * 64 + lane;
         cur[u] = j < e ? rec[j] : 0ull;
     }
-    for (uint64_t base = s; base < e; base += kBlock) {
+    uint32_t skip_tried_q = 0xFFFFFFFFu;
+    uint64_t pos = s;
+    while (pos < e) {
+        uint64_t npos = pos + kBlock;
         uint64_t nxt[kWaveUnroll];
 #pragma unroll
         for (int u = 0; u < kWaveUnroll; ++u) {  // prefetch the next block before deciding this one
-            const uint64_t j = base + kBlock + (uint64_t)u * 64 + lane;
+            const uint64_t j = npos + (uint64_t)u * 64 + lane;
             nxt[u] = j < e ? rec[j] : 0ull;
         }
+        bool skipped = false;
 #pragma unroll
         for (int u = 0; u < kWaveUnroll; ++u) {
-            const uint64_t cb = base + (uint64_t)u * 64;
-            if (cb < e) w.chunk(cur[u], cb + lane < e);
+            const uint64_t cb = pos + (uint64_t)u * 64;
+            if (skipped || cb >= e) continue;
+            w.chunk(cur[u], cb + lane < e);
+            const uint64_t after = cb + 64;
+            if (w.dead && after < e && w.pc.q != skip_tried_q) {
+                // The rest of this window period is BLOCKED: find where the period ends in the segment
+                // and hand the skipped range to k_skip_apply (its BLOCK counts only).
+                skip_tried_q = w.pc.q;
+                const uint32_t nb = w.pc.next_b;
+                const uint64_t pe = wave_search(after, e, [&](uint64_t p) {
+                    return (uint32_t)((rec[p] >> a.abits) & a.imask) >= nb;
+                }, lane);
+                if (pe - after >= kSkipMin) {
+                    uint32_t slot = 0;
+                    if (lane == 0) slot = atomicAdd(a.skip_count, 1u);
+                    slot = (uint32_t)bcast32((int)slot, 0);
+                    if (slot < a.skip_cap) {
+                        if (lane == 0) a.skips[slot] = make_uint4(k, w.pc.q, (uint32_t)after, (uint32_t)pe);
+                        npos = pe;
+                        skipped = true;
+                    }
+                }
+            }
+        }
+        if (skipped) {
+#pragma unroll
+            for (int u = 0; u < kWaveUnroll; ++u) {
+                const uint64_t j = npos + (uint64_t)u * 64 + lane;
+                nxt[u] = j < e ? rec[j] : 0ull;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kWaveUnroll; ++u) cur[u] = nxt[u];
+        pos = npos;
     }
     w.finish(k);
 }
@@ -568,27 +630,54 @@ __global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
     const uint32_t waves_per_block = blockDim.x / 64;
     const uint32_t wave = blockIdx.x * waves_per_block + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * waves_per_block;
+    const int lane = lane_id();
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint64_t s = a.long_list[w];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-        // segment end: gallop then binary search for the first record with a larger flowId
-        uint64_t lo = s + a.short_max, step = 64, hi;
-        for (;;) {
-            hi = lo + step;
-            if (hi >= a.n) {
-                hi = a.n;
-                break;
+        // segment end: the first record with another flowId
+        const uint64_t e = wave_search(s + a.short_max, a.n, [&](uint64_t p) {
+            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
+        }, lane);
+        walk_wave(a, k, s, e);
+    }
+}
+
+// BLOCK / BLOCK_REQUEST / OCCUPIED_BLOCK of the ranges the wave walker skipped, added to their period's
+// bucket unless a later period of the same batch has reset that slot (which discards them anyway).
+__global__ void __launch_bounds__(256) k_skip_apply(BatchArgs a) {
+    __shared__ int64_t part[2][256];
+    if (*a.err) return;
+    const uint32_t cnt = min(*a.skip_count, a.skip_cap);
+    const int tid = threadIdx.x;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const uint4 sk = a.skips[i];
+        int64_t sa = 0, spa = 0;
+        for (uint64_t j = (uint64_t)sk.z + tid; j < sk.w; j += blockDim.x) {
+            const Decoded d = decode(a, a.rec_sorted[j]);
+            sa += d.acq;
+            spa += d.prio ? d.acq : 0;
+        }
+        part[0][tid] = sa;
+        part[1][tid] = spa;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (tid < o) {
+                part[0][tid] += part[0][tid + o];
+                part[1][tid] += part[1][tid + o];
             }
-            if ((uint32_t)(a.rec_sorted[hi] >> a.kshift) != k) break;
-            lo = hi;
-            step <<= 1;
+            __syncthreads();
         }
-        while (hi - lo > 1) {  // invariant: rec[lo] has key k, rec[hi] (or n) does not
-            const uint64_t mid = (lo + hi) >> 1;
-            if ((uint32_t)(a.rec_sorted[mid] >> a.kshift) == k) lo = mid;
-            else hi = mid;
+        if (tid == 0) {
+            const Rule R = a.rules[sk.x];
+            const int64_t P = a.p0[R.wl_idx] + (int64_t)sk.y;
+            Bucket& b = a.ring[(size_t)sk.x * a.stride + (int)(P % R.S)];
+            if (b.start == P * R.wl) {
+                b.c[SG_EV_BLOCK] += part[0][0];
+                b.c[SG_EV_BLOCK_REQUEST] += (int64_t)(sk.w - sk.z);
+                b.c[SG_EV_OCCUPIED_BLOCK] += part[1][0];
+            }
         }
-        walk_wave(a, k, s, hi);
+        __syncthreads();
     }
 }
 
@@ -681,6 +770,11 @@ hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
     const uint64_t max_long = a.n / ((uint64_t)a.short_max + 1) + 1;
     const unsigned blocks = grid_for(max_long * 64, 256, 2048);
     hipLaunchKernelGGL(k_walk_long, dim3(blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_skip_apply, dim3(1024), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

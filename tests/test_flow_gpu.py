@@ -345,3 +345,23 @@ def test_namespace_limiter_config_changes():
         t = int(req["ts_ms"][-1]) + 30
         _compare_results(ora.decide(req), eng.decide_host(req), req)
     _compare_state(eng, ora, rules)
+
+
+@pytest.mark.parametrize("prio", [0.0, 0.01, 0.2])
+def test_hot_flow_saturated_periods_are_skipped_exactly(prio):
+    """A flow far above its threshold: once a window period can admit nothing (not even acquire 1, and no
+    prioritized request can occupy), the wave walker jumps to the period's end and k_skip_apply adds the
+    skipped requests' BLOCK counts. Results and windows must still match the sequential replay."""
+    rng = np.random.default_rng(int(prio * 100) + 77)
+    rules = _rules(3, rng, counts=np.array([10.0, 2.0, 7.5]), S=10, interval=1000)
+    eng, ora = _pair(rules, flags=abi.FLAG_WAVE_ONLY)
+    eng.enable_stats(True)
+    t = 1_700_000_000_010
+    skipped = 0
+    for _ in range(3):
+        req = _trace(rng, 300_000, 3, t, 2300, zipf=1.5, prio=prio, multi=0.2)
+        t = int(req["ts_ms"][-1]) + 1
+        _compare_results(ora.decide(req), eng.decide_host(req), req)
+        skipped += eng.stats()["skipped_ranges"]
+        _compare_state(eng, ora, rules)
+    assert skipped > 0
