@@ -142,7 +142,7 @@ typedef struct sg_param_rule {
     int32_t  max_queueing_ms;   /* maxQueueingTimeMs (throttle), default 0                        */
     uint32_t hot_begin;         /* this rule's hot items: hot[hot_begin .. hot_begin + hot_count) */
     uint32_t hot_count;
-    int32_t  reserved;
+    int32_t  capacity_log2;     /* device table: 2^capacity_log2 distinct values (0 = 2^20)        */
 } sg_param_rule;
 
 /* ParamFlowItem → parsed hot item: value-specific threshold (ParamFlowRuleUtil.parseHotItems :188-209). */
@@ -199,6 +199,17 @@ int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap)
 /* Same into DEVICE memory (2*n_rules doubles, {passQps, blockQps} per flowId), asynchronous on `stream`:
  * the per-GPU input of the node-wide RCCL metric rollup. */
 int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, void* stream);
+
+/* Hot-parameter rules (replaces ParamFlowRuleManager.loadRules → ParameterMetric maps). A reload starts
+ * every rule's value table empty. Hot items of a rule may be given in any order. */
+int sg_param_load_rules(sg_handle* h, const sg_param_rule* rules, uint32_t n,
+                        const sg_param_hot_item* hot, uint32_t n_hot);
+/* passSingleValueCheck for a time-ordered batch: pass[i] = 1 admitted / 0 blocked. req/pass are DEVICE
+ * pointers. Requests naming a rule index >= n pass (no rule). */
+int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass, void* stream);
+int sg_param_decide_batch_host(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass);
+/* State of (rule, value): returns flags (bit0 time counter, bit1 token counter; 0 = absent) or < 0. */
+int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
 
 /* Testing aid: copy an internal buffer of the last batch to host memory.
  * what: 0 = records (request order, u64), 1 = records sorted by flowId, 2 = window-period table

@@ -78,7 +78,7 @@ NS_DTYPE = np.dtype([("limiter_enabled", "<i4"), ("connected_count", "<i4"), ("m
 
 PARAM_RULE_DTYPE = np.dtype([("count", "<f8"), ("duration_sec", "<i8"), ("burst", "<i4"), ("behavior", "<i4"),
                              ("max_queueing_ms", "<i4"), ("hot_begin", "<u4"), ("hot_count", "<u4"),
-                             ("reserved", "<i4")], align=True)
+                             ("capacity_log2", "<i4")], align=True)
 PARAM_HOT_DTYPE = np.dtype([("value", "<u8"), ("threshold", "<i4"), ("reserved", "<i4")], align=True)
 PARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("value", "<u8"), ("rule", "<u4"), ("acquire", "<i4")], align=True)
 BEHAVIOR_DEFAULT = 0

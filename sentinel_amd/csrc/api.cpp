@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -62,6 +63,17 @@ struct sg_handle {
     uint8_t* d_lim_slot = nullptr;
     uint32_t* d_lim_tile = nullptr;   // tile totals then tile offsets
     uint32_t* d_lim_period = nullptr; // arrivals, prefix, quota
+
+    // hot-parameter flow control
+    std::vector<sg_param_rule> prules;
+    std::vector<PRule> ptab;
+    PRule* d_prules = nullptr;
+    sg_param_hot_item* d_phot = nullptr;
+    PSlot* d_ptable = nullptr;
+    uint64_t ptotal = 0;             // slots over all rule sub-tables
+    int64_t* d_plast_ts = nullptr;
+    sg_param_req* d_preq_h = nullptr;
+    int32_t* d_pout_h = nullptr;
 
     int kbits = 0, ibits = 0, abits = 0;
     bool stats_on = false;
@@ -208,6 +220,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipHostMalloc(&h->h_long, 2 * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     int64_t neg = -1;
     if (hipMemcpy(h->d_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
+    if (hipMalloc(&h->d_plast_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMemcpy(h->d_plast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     for (auto& e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(SG_E_DEVICE);
     // default namespace 0, no limiter, 1 connection
@@ -239,6 +253,12 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_long_list);
     dfree(h->d_long_count);
     dfree(h->d_skips);
+    dfree(h->d_prules);
+    dfree(h->d_phot);
+    dfree(h->d_ptable);
+    dfree(h->d_plast_ts);
+    dfree(h->d_preq_h);
+    dfree(h->d_pout_h);
     dfree(h->d_skip_count);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
@@ -547,6 +567,138 @@ int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, ui
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
     return SG_OK;
+}
+
+// ParamFlowRuleManager.loadRules (…/param/ParamFlowRuleManager.java) → fresh ParameterMetric maps.
+int sg_param_load_rules(sg_handle* h, const sg_param_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                        uint32_t n_hot) {
+    if (!h || (!rules && n) || (!hot && n_hot)) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<PRule> tab(n);
+    std::vector<sg_param_hot_item> hot_sorted(hot, hot + n_hot);
+    uint64_t base = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_param_rule& r = rules[i];
+        if (!(r.count >= 0) || r.duration_sec <= 0) return fail(h, SG_E_INVAL, "invalid param rule");
+        if ((uint64_t)r.hot_begin + r.hot_count > n_hot) return fail(h, SG_E_INVAL, "hot item range out of bounds");
+        const int lg = r.capacity_log2 ? r.capacity_log2 : 20;
+        if (lg < 1 || lg > 30) return fail(h, SG_E_INVAL, "capacity_log2 must be in [1, 30]");
+        PRule& R = tab[i];
+        R.token_count = (int64_t)r.count;  // (long) rule.getCount(); count is finite and >= 0 here
+        if (r.count >= 9.2e18) R.token_count = INT64_MAX;
+        R.duration_sec = r.duration_sec;
+        R.burst = r.burst;
+        R.behavior = r.behavior;
+        R.max_queueing_ms = r.max_queueing_ms;
+        R.hot_begin = r.hot_begin;
+        R.hot_count = r.hot_count;
+        R.table_base = base;
+        R.table_mask = (1ull << lg) - 1;
+        base += (1ull << lg) + 1;  // + the side slot for the value ~0
+        std::sort(hot_sorted.begin() + r.hot_begin, hot_sorted.begin() + r.hot_begin + r.hot_count,
+                  [](const sg_param_hot_item& x, const sg_param_hot_item& y) { return x.value < y.value; });
+    }
+    if (base >= (1ull << 32)) return fail(h, SG_E_UNSUPPORTED, "param tables larger than 2^32 slots");
+    dfree(h->d_prules);
+    dfree(h->d_phot);
+    dfree(h->d_ptable);
+    h->ptotal = 0;
+    if (n) {
+        if (hipMalloc(&h->d_prules, sizeof(PRule) * n) != hipSuccess ||
+            hipMalloc(&h->d_ptable, sizeof(PSlot) * base) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "param table allocation");
+        if (n_hot && hipMalloc(&h->d_phot, sizeof(sg_param_hot_item) * n_hot) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "param hot items");
+        HIP_TRY(h, hipMemcpy(h->d_prules, tab.data(), sizeof(PRule) * n, hipMemcpyHostToDevice));
+        if (n_hot)
+            HIP_TRY(h, hipMemcpy(h->d_phot, hot_sorted.data(), sizeof(sg_param_hot_item) * n_hot, hipMemcpyHostToDevice));
+        HIP_TRY(h, launch_param_clear(h->d_ptable, base, 0));
+        HIP_TRY(h, hipDeviceSynchronize());
+    }
+    h->prules.assign(rules, rules + n);
+    h->ptab = tab;
+    h->ptotal = base;
+    return SG_OK;
+}
+
+int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !pass) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    PArgs p{};
+    p.req = req;
+    p.out = pass;
+    p.n = n;
+    p.rec = h->d_rec;
+    p.rec_sorted = h->d_rec_sorted;
+    p.ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
+    p.imask = (1ull << p.ibits) - 1;
+    p.rules = h->d_prules;
+    p.n_rules = (uint32_t)h->ptab.size();
+    p.hot = h->d_phot;
+    p.table = h->d_ptable;
+    p.total_slots = h->ptotal;
+    p.err = h->d_err;
+    p.last_ts = h->d_plast_ts;
+    p.long_list = h->d_long_list;
+    p.long_count = h->d_long_count;
+    p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 16u;
+    const int gbits = bits_for(h->ptotal + 1);
+    if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    uint64_t* sorted = nullptr;
+    HIP_TRY(h, launch_param_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream));
+    h->last_sorted = sorted;
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    const int err = *h->h_err & ~kErrNonPositive;
+    if (err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param rule's value table is full");
+    return SG_OK;
+}
+
+int sg_param_decide_batch_host(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_preq_h) {
+        if (hipMalloc(&h->d_preq_h, sizeof(sg_param_req) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_pout_h, sizeof(int32_t) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    HIP_TRY(h, hipMemcpy(h->d_preq_h, req, sizeof(sg_param_req) * n, hipMemcpyHostToDevice));
+    int rc = sg_param_decide_batch(h, h->d_preq_h, n, h->d_pout_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(pass, h->d_pout_h, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens) {
+    if (!h || rule >= h->ptab.size() || !last_time || !tokens) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const PRule& R = h->ptab[rule];
+    std::vector<PSlot> t(R.table_mask + 2);
+    HIP_TRY(h, hipMemcpy(t.data(), h->d_ptable + R.table_base, sizeof(PSlot) * t.size(), hipMemcpyDeviceToHost));
+    const PSlot* s = nullptr;
+    if (value == ~0ull) {
+        s = &t[R.table_mask + 1];
+    } else {
+        for (const PSlot& x : t)
+            if (x.value == value) {
+                s = &x;
+                break;
+            }
+    }
+    if (!s || !s->flags) return 0;
+    *last_time = s->time;
+    *tokens = s->tokens;
+    return (int)s->flags;
 }
 
 int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {

@@ -106,12 +106,60 @@ struct LimArgs {
 
 hipError_t launch_limiter(const BatchArgs& a, const LimArgs& L, hipStream_t stream);
 
+// ---- hot-parameter flow control (param.hip) ----
+constexpr int kErrNonPositive = 4;  // some acquireCount <= 0 in the batch (disables the skip shortcut)
+constexpr int kErrTableFull = 8;    // a rule's value table is full
+
+struct PRule {
+    int64_t token_count;    // (long) ParamFlowRule.count
+    int64_t duration_sec;
+    int32_t burst;
+    int32_t behavior;       // 2 = CONTROL_BEHAVIOR_RATE_LIMITER (throttle), else token bucket
+    int32_t max_queueing_ms;
+    uint32_t hot_begin, hot_count;
+    uint32_t pad;
+    uint64_t table_base;    // first slot of this rule's sub-table
+    uint64_t table_mask;    // 2^capacity_log2 - 1; slot table_base + mask + 1 holds the value ~0
+};
+
+struct alignas(32) PSlot {  // one (rule, value): timeCounters / tokenCounters entries
+    uint64_t value;         // ~0 = empty (except in the side slot)
+    uint32_t flags;         // bit0 time counter present, bit1 token counter present
+    uint32_t pad;
+    int64_t time;
+    int64_t tokens;
+};
+
+struct PArgs {
+    const sg_param_req* req;
+    int32_t* out;
+    uint64_t n;
+    uint64_t* rec;          // {global slot : high bits | request index : ibits}
+    uint64_t* rec_sorted;
+    int ibits;
+    uint64_t imask;
+    const PRule* rules;
+    uint32_t n_rules;
+    const sg_param_hot_item* hot;  // per rule, sorted by value
+    PSlot* table;
+    uint64_t total_slots;   // all sub-tables; records of requests rejected early carry this as slot
+    int* err;
+    int64_t* last_ts;
+    uint32_t* long_list;
+    uint32_t* long_count;
+    uint32_t short_max;
+};
+
+hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
+hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
+                              uint64_t** sorted_out, hipStream_t stream);
+
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
-// sort.hip: stable LSD radix sort of records on bits [lo_bit, 64); result buffer is a or b.
+// sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream);
+                              uint64_t** result, hipStream_t stream, int hi_bit = 64);
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);

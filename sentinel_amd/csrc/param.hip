@@ -1,0 +1,427 @@
+// param.hip — hot-parameter flow control on the device: ParamFlowChecker.passSingleValueCheck for QPS
+// rules (sentinel-extension/sentinel-parameter-flow-control/.../slots/block/flow/param/ParamFlowChecker.java:
+// passDefaultLocalCheck :127-202, passThrottleLocalCheck :204-254).
+//
+// The reference keeps per-rule LRU CacheMaps (value → lastAddTokenTime, value → tokens); here each rule
+// owns an exact open-addressing sub-table in HBM (2^capacity_log2 slots + one side slot for the value
+// 0xFFFF…FFFF, which doubles as the empty marker). A batch:
+//   k_pprep    early rejections that never touch the maps (no rule, tokenCount 0, acquire > maxCount),
+//              lock-free find-or-insert of (rule, value) by CAS on the slot's value word, packed record
+//              {global slot | request index}; outputs start as "blocked".
+//   radix sort by slot (sort.hip): every (rule, value)'s requests contiguous, in arrival order.
+//   k_pwalk_short / k_pwalk_long  sequential replay per slot; the wave walker decides 64 requests per
+//              step (prefix-scan admit, ballot skip) and, once the bucket cannot pay even 1 token before
+//              the next refill, jumps to the first request after the refill time by a 64-way search.
+#include "engine.h"
+
+namespace sg {
+
+constexpr uint64_t kEmptyValue = ~0ull;
+
+__device__ __forceinline__ int64_t java_math_round(double a) {
+    // java.lang.Math.round(double), exact floor(a + 1/2) (JDK 7u+)
+    const int64_t bits = __double_as_longlong(a);
+    const int64_t biased_exp = (bits & 0x7FF0000000000000LL) >> 52;
+    const int64_t shift = (52 - 1 + 1023) - biased_exp;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    if (a != a) return 0;
+    if (a >= 9223372036854775807.0) return INT64_MAX;
+    if (a <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)a;
+}
+
+// tokenCount of (rule, value): the hot item's threshold, else (long) rule.count (ParamFlowChecker.java:137-141)
+__device__ __forceinline__ int64_t param_token_count(const PArgs& p, const PRule& r, uint64_t v) {
+    uint32_t lo = r.hot_begin, hi = r.hot_begin + r.hot_count;  // hot items sorted by value
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t hv = p.hot[mid].value;
+        if (hv == v) return p.hot[mid].threshold;
+        if (hv < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return r.token_count;
+}
+
+// find-or-insert (rule, value) → global slot index
+__device__ __forceinline__ uint64_t param_slot(const PArgs& p, const PRule& r, uint64_t v) {
+    if (v == kEmptyValue) return r.table_base + r.table_mask + 1;  // side slot
+    uint64_t h = v + 0x9E3779B97F4A7C15ull;
+    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+    h ^= h >> 31;
+    uint64_t i = h & r.table_mask;
+    for (uint64_t probes = 0; probes <= r.table_mask; ++probes) {
+        unsigned long long* vw = (unsigned long long*)&p.table[r.table_base + i].value;
+        const unsigned long long cur = __hip_atomic_load(vw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == v) return r.table_base + i;
+        if (cur == kEmptyValue) {
+            const unsigned long long old = atomicCAS(vw, (unsigned long long)kEmptyValue, (unsigned long long)v);
+            if (old == kEmptyValue || old == v) return r.table_base + i;
+        }
+        i = (i + 1) & r.table_mask;
+    }
+    return ~0ull;  // table full
+}
+
+__global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_param_req q = p.req[i];
+        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *p.last_ts : q.ts_ms < p.req[i - 1].ts_ms)) atomicOr(p.err, kErrTime);
+        if (q.acquire <= 0) atomicOr(p.err, kErrNonPositive);
+        uint64_t rec = sentinel;
+        int32_t pass = 0;
+        if (q.rule >= p.n_rules) {
+            pass = 1;  // no rule for this index: nothing to check
+        } else {
+            const PRule r = p.rules[q.rule];
+            const int64_t tc = param_token_count(p, r, q.value);
+            const bool early_block = tc == 0 || (r.behavior != 2 && (int64_t)q.acquire > tc + r.burst);
+            if (!early_block) {
+                const uint64_t g = param_slot(p, r, q.value);
+                if (g == ~0ull) atomicOr(p.err, kErrTableFull);
+                else rec = (g << p.ibits) | i;
+            }
+        }
+        p.out[i] = pass;
+        p.rec[i] = rec;
+    }
+}
+
+struct PState {
+    int64_t time, tokens;
+    uint32_t flags;  // bit0 time counter present, bit1 token counter present
+};
+
+struct PReqView {
+    int64_t t;
+    int64_t acq;
+};
+
+// One request of passDefaultLocalCheck at time t (ParamFlowChecker.java:147-201); returns pass.
+__device__ __forceinline__ bool param_default_step(PState& s, int64_t tc, int64_t maxc, int64_t dur_ms, int64_t t,
+                                                   int64_t acq) {
+    if (!(s.flags & 1u)) {
+        s.flags |= 1u;
+        s.time = t;
+        if (!(s.flags & 2u)) {
+            s.flags |= 2u;
+            s.tokens = maxc - acq;
+        }
+        return true;
+    }
+    const int64_t pass_time = t - s.time;
+    if (pass_time > dur_ms) {
+        if (!(s.flags & 2u)) {
+            s.flags |= 2u;
+            s.tokens = maxc - acq;
+            s.time = t;
+            return true;
+        }
+        const int64_t rest = s.tokens;
+        const int64_t to_add = (pass_time * tc) / dur_ms;
+        const int64_t nq = to_add + rest > maxc ? (maxc - acq) : (rest + to_add - acq);
+        if (nq < 0) return false;
+        s.tokens = nq;
+        s.time = t;
+        return true;
+    }
+    if ((s.flags & 2u) && s.tokens - acq >= 0) {
+        s.tokens -= acq;
+        return true;
+    }
+    return false;
+}
+
+// One request of passThrottleLocalCheck (:214-253); the wait is a sleep in Java, skipped in replay.
+__device__ __forceinline__ bool param_throttle_step(PState& s, int64_t cost, int32_t max_queue, int64_t t) {
+    if (!(s.flags & 1u)) {
+        s.flags |= 1u;
+        s.time = t;
+        return true;
+    }
+    const int64_t expected = s.time + cost;
+    if (expected <= t || expected - t < max_queue) {
+        s.time = t;
+        if (expected - t > 0) s.time = expected;
+        return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ int64_t throttle_cost(const PRule& r, int64_t tc, int64_t acq) {
+    return java_math_round(1.0 * 1000 * (double)acq * (double)r.duration_sec / (double)tc);
+}
+
+__device__ __forceinline__ uint32_t rule_of_slot(const PArgs& p, uint64_t g) {
+    uint32_t lo = 0, hi = p.n_rules;  // rules sorted by table_base; slot g belongs to the last base <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (p.rules[mid].table_base <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ void pwalk_serial(const PArgs& p, uint64_t g, uint64_t s, uint64_t e) {
+    const uint32_t ri = rule_of_slot(p, g);
+    const PRule r = p.rules[ri];
+    PSlot& slot = p.table[g];
+    const uint64_t value = slot.value;  // the side slot's word stays ~0, which is its value
+    const int64_t tc = param_token_count(p, r, value);
+    PState st{slot.time, slot.tokens, slot.flags};
+    for (uint64_t j = s; j < e; ++j) {
+        const uint32_t idx = (uint32_t)(p.rec_sorted[j] & p.imask);
+        const int64_t t = p.req[idx].ts_ms;
+        const int64_t acq = p.req[idx].acquire;
+        bool ok;
+        if (r.behavior == 2) ok = param_throttle_step(st, throttle_cost(r, tc, acq), r.max_queueing_ms, t);
+        else ok = param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, acq);
+        if (ok) p.out[idx] = 1;
+    }
+    slot.time = st.time;
+    slot.tokens = st.tokens;
+    slot.flags = st.flags;
+}
+
+__global__ void __launch_bounds__(256) k_pwalk_short(PArgs p) {
+    if (*p.err & ~kErrNonPositive) return;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t rec = p.rec_sorted[j];
+        const uint64_t g = rec >> p.ibits;
+        if (g >= p.total_slots) continue;  // rejected before the maps
+        if (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g) continue;
+        uint64_t e = j + 1;
+        while (e < p.n && e - j <= (uint64_t)p.short_max && (p.rec_sorted[e] >> p.ibits) == g) ++e;
+        if (e - j > (uint64_t)p.short_max) {
+            const uint32_t pos = atomicAdd(p.long_count, 1u);
+            p.long_list[pos] = (uint32_t)j;
+            continue;
+        }
+        pwalk_serial(p, g, j, e);
+    }
+}
+
+template <class Pred>
+__device__ __forceinline__ uint64_t pwave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t q = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(q >= hi || pred(q));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t q = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(q < hi && pred(q));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
+}
+
+__device__ __forceinline__ int64_t pwave_scan(int64_t v, int lane) {
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up((long long)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ int64_t pwave_sum(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((long long)v, o, 64);
+    return v;
+}
+
+// Token bucket for one hot (rule, value): sequential semantics, 64 requests per step.
+//   - first sight and refill attempts (t − time > duration) are resolved one request at a time;
+//   - between refills the bucket only pays out: the admit step passes the longest prefix whose running
+//     token count stays >= 0, the skip step passes the next request that fits on its own;
+//   - when fewer tokens remain than any request asks (all acquireCounts >= 1 in the batch), every request
+//     up to the refill time is blocked: jump to the first one after it.
+__device__ void pwalk_wave_default(const PArgs& p, const PRule& r, int64_t tc, PState& st, uint64_t s, uint64_t e) {
+    const int lane = (int)__lane_id();
+    const int64_t maxc = tc + r.burst;
+    const int64_t dur_ms = r.duration_sec * 1000;
+    const bool all_positive = !(*p.err & kErrNonPositive);
+    uint64_t pos = s;
+    while (pos < e) {
+        // sequential head: first sight / refill zone
+        {
+            const uint32_t idx = (uint32_t)(p.rec_sorted[pos] & p.imask);
+            const int64_t t = p.req[idx].ts_ms;
+            if (!(st.flags & 1u) || t - st.time > dur_ms) {
+                const int64_t acq = p.req[idx].acquire;
+                if (param_default_step(st, tc, maxc, dur_ms, t, acq) && lane == 0) p.out[idx] = 1;
+                ++pos;
+                continue;
+            }
+        }
+        // no-refill zone: requests with t <= time + duration
+        const int64_t zone_end_t = st.time + dur_ms;
+        const uint64_t z = pwave_search(pos, e, [&](uint64_t q) {
+            return p.req[(uint32_t)(p.rec_sorted[q] & p.imask)].ts_ms > zone_end_t;
+        }, lane);
+        while (pos < z) {
+            if (all_positive && st.tokens < 1) {  // nothing fits until the refill: all blocked
+                pos = z;
+                break;
+            }
+            const uint64_t j = pos + (uint64_t)lane;
+            const bool act = j < z;
+            uint32_t idx = 0;
+            int64_t acq = 0;
+            if (act) {
+                idx = (uint32_t)(p.rec_sorted[j] & p.imask);
+                acq = p.req[idx].acquire;
+            }
+            uint64_t pending = __ballot(act);
+            while (pending) {
+                const bool pl = (pending >> lane) & 1ull;
+                const int64_t ex = pwave_scan(pl ? acq : 0, lane);
+                const bool fail = pl && !(st.tokens - ex - acq >= 0);
+                const uint64_t fails = __ballot(fail);
+                const uint64_t pass = fails ? (pending & ((1ull << __builtin_ctzll(fails)) - 1ull)) : pending;
+                if (pass) {
+                    if ((pass >> lane) & 1ull) p.out[idx] = 1;
+                    st.tokens -= pwave_sum(((pass >> lane) & 1ull) ? acq : 0);
+                }
+                if (!fails) break;
+                const int f = __builtin_ctzll(fails);
+                pending &= ~((2ull << f) - 1ull);  // f is blocked
+                // skip: the next request that fits on its own
+                const uint64_t fit = __ballot(((pending >> lane) & 1ull) && st.tokens - acq >= 0);
+                if (!fit) break;
+                pending &= ~((1ull << __builtin_ctzll(fit)) - 1ull);
+            }
+            pos += 64;
+            if (pos > z) pos = z;
+        }
+    }
+}
+
+// Throttle (leaky bucket) for one hot (rule, value): 64 requests per step, the first request in the
+// step that would be admitted advances the recorder, repeated until none in the step is.
+__device__ void pwalk_wave_throttle(const PArgs& p, const PRule& r, int64_t tc, PState& st, uint64_t s, uint64_t e) {
+    const int lane = (int)__lane_id();
+    for (uint64_t base = s; base < e; base += 64) {
+        const uint64_t j = base + (uint64_t)lane;
+        const bool act = j < e;
+        uint32_t idx = 0;
+        int64_t t = 0, cost = 0;
+        if (act) {
+            idx = (uint32_t)(p.rec_sorted[j] & p.imask);
+            t = p.req[idx].ts_ms;
+            cost = throttle_cost(r, tc, p.req[idx].acquire);
+        }
+        uint64_t pending = __ballot(act);
+        while (pending) {
+            if (!(st.flags & 1u)) {  // first sight: the first pending request passes
+                const int f = __builtin_ctzll(pending);
+                const int64_t tf = __shfl((long long)t, f, 64);
+                st.flags |= 1u;
+                st.time = tf;
+                if (lane == f) p.out[idx] = 1;
+                pending &= ~(1ull << f);
+                continue;
+            }
+            const int64_t expected = st.time + cost;
+            const bool ok = ((pending >> lane) & 1ull) && (expected <= t || expected - t < r.max_queueing_ms);
+            const uint64_t m = __ballot(ok);
+            if (!m) break;
+            const int f = __builtin_ctzll(m);
+            const int64_t tf = __shfl((long long)t, f, 64);
+            const int64_t ef = __shfl((long long)expected, f, 64);
+            st.time = tf;
+            if (ef - tf > 0) st.time = ef;
+            if (lane == f) p.out[idx] = 1;
+            pending &= ~((2ull << f) - 1ull);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pwalk_long(PArgs p) {
+    if (*p.err & ~kErrNonPositive) return;
+    const uint32_t cnt = *p.long_count;
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const int lane = (int)__lane_id();
+    for (uint32_t w = wave; w < cnt; w += nwaves) {
+        const uint64_t s = p.long_list[w];
+        const uint64_t g = p.rec_sorted[s] >> p.ibits;
+        const uint64_t e = pwave_search(s + p.short_max, p.n, [&](uint64_t q) {
+            return (p.rec_sorted[q] >> p.ibits) != g;
+        }, lane);
+        const uint32_t ri = rule_of_slot(p, g);
+        const PRule r = p.rules[ri];
+        PSlot& slot = p.table[g];
+        const uint64_t value = slot.value;
+        const int64_t tc = param_token_count(p, r, value);
+        PState st{slot.time, slot.tokens, slot.flags};
+        if (r.behavior == 2) pwalk_wave_throttle(p, r, tc, st, s, e);
+        else pwalk_wave_default(p, r, tc, st, s, e);
+        if (lane == 0) {
+            slot.time = st.time;
+            slot.tokens = st.tokens;
+            slot.flags = st.flags;
+        }
+    }
+}
+
+__global__ void k_pfinish(PArgs p) {
+    if ((*p.err & ~kErrNonPositive) == 0 && p.n > 0) *p.last_ts = p.req[p.n - 1].ts_ms;
+}
+
+__global__ void __launch_bounds__(256) k_ptable_clear(PSlot* table, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        PSlot s;
+        s.value = kEmptyValue;
+        s.flags = 0;
+        s.pad = 0;
+        s.time = 0;
+        s.tokens = 0;
+        table[i] = s;
+    }
+}
+
+static unsigned pgrid(uint64_t n, unsigned cap) {
+    uint64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ptable_clear, dim3(pgrid(n, 8192)), dim3(256), 0, stream, table, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
+                              uint64_t** sorted_out, hipStream_t stream) {
+    const uint64_t sentinel = p.total_slots << p.ibits;
+    hipLaunchKernelGGL(k_pprep, dim3(pgrid(p.n, 8192)), dim3(256), 0, stream, p, sentinel);
+    uint64_t* sorted = nullptr;
+    hipError_t e = radix_sort_records(a_buf, b_buf, p.n, lo_bit, hist, &sorted, stream, hi_bit);
+    if (e != hipSuccess) return e;
+    PArgs q = p;
+    q.rec_sorted = sorted;
+    *sorted_out = sorted;
+    hipLaunchKernelGGL(k_pwalk_short, dim3(pgrid(p.n, 16384)), dim3(256), 0, stream, q);
+    const uint64_t max_long = p.n / ((uint64_t)p.short_max + 1) + 1;
+    hipLaunchKernelGGL(k_pwalk_long, dim3(pgrid(max_long * 64, 2048)), dim3(256), 0, stream, q);
+    hipLaunchKernelGGL(k_pfinish, dim3(1), dim3(1), 0, stream, q);
+    return hipGetLastError();
+}
+
+}  // namespace sg

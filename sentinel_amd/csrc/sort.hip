@@ -157,10 +157,11 @@ size_t radix_hist_words(uint64_t n) {
     return (size_t)(words + nb + 64);
 }
 
-// Sorts n records on bits [lo_bit, 64) in passes of 8 bits, ping-ponging between a and b.
+// Sorts n records on bits [lo_bit, hi_bit) in passes of 8 bits (bits above hi_bit must be zero or
+// already grouped), ping-ponging between a and b.
 // Returns the buffer that holds the result through *result.
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream) {
+                              uint64_t** result, hipStream_t stream, int hi_bit) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint64_t words = (uint64_t)ntiles * kBins;
     const uint32_t nb = (uint32_t)((words + kScanChunk - 1) / kScanChunk);
@@ -168,7 +169,7 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
     uint32_t* sums = hist_ws + words;
     uint64_t* src = a;
     uint64_t* dst = b;
-    for (int shift = lo_bit; shift < 64; shift += kRadixBits) {
+    for (int shift = lo_bit; shift < hi_bit; shift += kRadixBits) {
         hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
         hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(kSortThreads), 0, stream, hist, words, sums);
         hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kSortThreads), 0, stream, sums, nb);

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
-           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info"]
+           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
+           "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state"]
 
 _lib = None
 
@@ -49,6 +50,10 @@ def load_library():
         "sg_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
         "sg_snapshot_metrics_device": (C.c_int, [vp, i64, vp, u64, vp]),
         "sg_debug_copy": (C.c_int, [vp, C.c_int, vp, u64]),
+        "sg_param_load_rules": (C.c_int, [vp, vp, u32, vp, u32]),
+        "sg_param_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_param_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_param_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "sg_build_info": (C.c_char_p, []),
     }
     for name, (res, args) in sig.items():
@@ -134,6 +139,29 @@ class FlowEngine:
         out = np.zeros(count, dtype)
         self._check(self._L.sg_debug_copy(self.h, what, abi.ptr(out), out.nbytes))
         return out
+
+    # ---- hot-parameter flow control (ParamFlowChecker.passSingleValueCheck, QPS rules)
+    def param_load_rules(self, rules: np.ndarray, hot: np.ndarray = None):
+        rules = np.ascontiguousarray(rules, dtype=abi.PARAM_RULE_DTYPE)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        self._check(self._L.sg_param_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot)))
+
+    def param_decide_host(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.PARAM_REQ_DTYPE)
+        out = np.zeros(len(req), np.int32)
+        self._check(self._L.sg_param_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def param_decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        self._check(self._L.sg_param_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr),
+                                                  C.c_void_p(stream_ptr)))
+
+    def param_state(self, rule, value):
+        lt, tk = C.c_int64(), C.c_int64()
+        flags = self._L.sg_param_read_state(self.h, rule, value, C.byref(lt), C.byref(tk))
+        if flags < 0:
+            self._check(flags)
+        return flags, lt.value, tk.value
 
     def snapshot(self, now_ms, n_rules):
         out = np.zeros(2 * n_rules, np.float64)
