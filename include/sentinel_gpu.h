@@ -160,6 +160,51 @@ typedef struct sg_param_req {
     int32_t  acquire;           /* acquireCount                                                    */
 } sg_param_req;
 
+/* ---- local slot chain: StatisticSlot → FlowSlot (DefaultController) → DegradeSlot (circuit breakers) ---- */
+
+/* DegradeRule (sentinel-core/.../slots/block/degrade/DegradeRule.java). */
+#define SG_DEGRADE_RT              0
+#define SG_DEGRADE_EXCEPTION_RATIO 1
+#define SG_DEGRADE_EXCEPTION_COUNT 2
+typedef struct sg_degrade_rule {
+    int32_t grade;                /* SG_DEGRADE_*                                            */
+    int32_t time_window_sec;      /* timeWindow: recovery timeout in seconds                  */
+    double  count;                /* RT: max allowed RT (rounded); else ratio / count         */
+    double  slow_ratio_threshold; /* RT only (default 1.0)                                    */
+    int32_t min_request_amount;   /* default 5                                               */
+    int32_t stat_interval_ms;     /* default 1000                                            */
+} sg_degrade_rule;
+
+/* One resource: its FlowRule with the default controller (limitApp "default", DIRECT strategy, read
+ * from the resource's ClusterNode) and up to two DegradeRules, checked in order. */
+typedef struct sg_local_rule {
+    double  flow_count;           /* FlowRule.count                                           */
+    int32_t flow_grade;           /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS, -1 no flow rule    */
+    int32_t n_breakers;           /* 0..2                                                     */
+    sg_degrade_rule breakers[2];
+} sg_local_rule;
+
+#define SG_LOCAL_ENTRY      0     /* SphU.entry(resource, count, prioritized)                 */
+#define SG_LOCAL_EXIT       1     /* Entry.exit() of a passed entry                           */
+#define SG_LOCAL_EXIT_ERROR 2     /* Entry.exit() after Tracer.traceEntry(business exception) */
+typedef struct sg_local_event {
+    int64_t  ts_ms;               /* TimeUtil time of the entry or exit                        */
+    int64_t  create_ts;           /* exit: the entry's createTimestamp                         */
+    uint32_t resource;            /* resource index | SG_KEY_PRIO (prioritized entry)          */
+    int32_t  count;               /* acquireCount of the entry (also the exit's batchCount)    */
+    int32_t  kind;                /* SG_LOCAL_*                                               */
+    int32_t  reserved;
+} sg_local_event;
+
+#define SG_LOCAL_PASS          0
+#define SG_LOCAL_BLOCK_FLOW    1  /* FlowException                                            */
+#define SG_LOCAL_BLOCK_DEGRADE 2  /* DegradeException                                         */
+#define SG_LOCAL_PASS_WAIT     3  /* PriorityWaitException: passes after wait_ms              */
+typedef struct sg_local_result {
+    int32_t status;               /* entries: SG_LOCAL_*; exits: 0                            */
+    int32_t wait_ms;
+} sg_local_result;
+
 /* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
 typedef struct sg_batch_stats {
     float    total_ms;          /* whole pipeline                                         */

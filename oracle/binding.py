@@ -65,6 +65,14 @@ def lib():
         "or_pf_decide": (C.c_int, [vp, vp, u64, vp]),
         "or_pf_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "or_pf_size": (u64, [vp]),
+        "or_local_new": (vp, [C.c_int, C.c_int, C.c_int]), "or_local_free": (None, [vp]),
+        "or_local_load_rules": (C.c_int, [vp, vp, u32]),
+        "or_local_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_local_second_sum": (i64, [vp, u32, i64, C.c_int]),
+        "or_local_minute_sum": (i64, [vp, u32, i64, C.c_int]),
+        "or_local_thread_num": (i64, [vp, u32]), "or_local_waiting": (i64, [vp, u32, i64]),
+        "or_local_breaker_state": (C.c_int, [vp, u32, C.c_int, vp]),
+        "or_local_dump": (C.c_int, [vp, u32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -269,3 +277,79 @@ class ParamFlowChecker:
 
     def size(self):
         return lib().or_pf_size(self.h)
+
+
+def degrade_rule(grade, count, time_window_sec, min_request_amount=5, stat_interval_ms=1000,
+                 slow_ratio_threshold=1.0):
+    r = np.zeros((), abi.DEGRADE_RULE_DTYPE)
+    r["grade"], r["count"], r["time_window_sec"] = grade, count, time_window_sec
+    r["min_request_amount"], r["stat_interval_ms"] = min_request_amount, stat_interval_ms
+    r["slow_ratio_threshold"] = slow_ratio_threshold
+    return r
+
+
+def local_rule(flow_count=0.0, flow_grade=abi.FLOW_GRADE_NONE, breakers=()):
+    r = np.zeros((), abi.LOCAL_RULE_DTYPE)
+    r["flow_count"], r["flow_grade"], r["n_breakers"] = flow_count, flow_grade, len(breakers)
+    for i, b in enumerate(breakers):
+        r["breakers"][i] = b
+    return r
+
+
+class LocalChain:
+    """Sequential replay of the local slot chain (StatisticSlot → FlowSlot/DefaultController → DegradeSlot)
+    for one resource per rule. Events: entries and exits with explicit times."""
+
+    def __init__(self, sample_count=2, interval_ms=1000, occupy_timeout_ms=500):
+        self.h = lib().or_local_new(sample_count, interval_ms, occupy_timeout_ms)
+        self.S = sample_count
+
+    def __del__(self):
+        if self.h:
+            lib().or_local_free(self.h)
+            self.h = None
+
+    def load_rules(self, rules):
+        rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
+        assert lib().or_local_load_rules(self.h, abi.ptr(rules), len(rules)) == 0
+
+    def decide(self, events):
+        ev = np.ascontiguousarray(events, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        out = np.zeros(len(ev), abi.LOCAL_RES_DTYPE)
+        lib().or_local_decide(self.h, abi.ptr(ev), len(ev), abi.ptr(out))
+        return out
+
+    def entry(self, t, res=0, count=1, prio=False):
+        e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
+        e[0] = (t, 0, res | (0x80000000 if prio else 0), count, abi.LOCAL_ENTRY, 0)
+        r = self.decide(e)[0]
+        return int(r["status"]), int(r["wait_ms"])
+
+    def exit(self, t, create_ts, res=0, count=1, error=False):
+        e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
+        e[0] = (t, create_ts, res, count, abi.LOCAL_EXIT_ERROR if error else abi.LOCAL_EXIT, 0)
+        self.decide(e)
+
+    def second_sum(self, res, t, ev):
+        return lib().or_local_second_sum(self.h, res, t, ev)
+
+    def minute_sum(self, res, t, ev):
+        return lib().or_local_minute_sum(self.h, res, t, ev)
+
+    def threads(self, res):
+        return lib().or_local_thread_num(self.h, res)
+
+    def waiting(self, res, t):
+        return lib().or_local_waiting(self.h, res, t)
+
+    def breaker(self, res, i):
+        nr = C.c_int64()
+        st = lib().or_local_breaker_state(self.h, res, i, C.byref(nr))
+        return st, nr.value
+
+    def dump(self, res):
+        sec = np.zeros((self.S, 8), np.int64)
+        bor = np.zeros((self.S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        assert lib().or_local_dump(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt)) == 0
+        return sec, bor, mnt

@@ -747,3 +747,287 @@ int or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* las
 }
 
 uint64_t or_pf_size(const or_pf* p) { return p->size; }
+
+/* ===================================================================================== */
+/* Local slot chain for one resource per rule: StatisticSlot.entry/exit                   */
+/* (core/slots/statistic/StatisticSlot.java:55-165), FlowSlot with DefaultController      */
+/* (core/slots/block/flow/controller/DefaultController.java:49-76), DegradeSlot           */
+/* (core/slots/block/degrade/DegradeSlot.java:43-81) and the circuit breakers             */
+/* (…/degrade/circuitbreaker/{AbstractCircuitBreaker,ResponseTimeCircuitBreaker,ExceptionCircuitBreaker}.java). */
+/* One StatisticNode per resource stands for its DefaultNode and ClusterNode (identical for */
+/* a single context; FlowRuleChecker reads the ClusterNode for limitApp "default").        */
+/* ===================================================================================== */
+
+enum { OR_CB_CLOSED = 0, OR_CB_OPEN = 1, OR_CB_HALF_OPEN = 2 };
+
+typedef struct or_breaker {
+    sg_degrade_rule rule;
+    int state;
+    int64_t next_retry;
+    or_leap* stat; /* LeapArray(1, statIntervalMs): c[0] slow / error count, c[1] total count */
+} or_breaker;
+
+typedef struct or_node {
+    or_leap* second;  /* ArrayMetric(SAMPLE_COUNT, INTERVAL): OccupiableBucketLeapArray (StatisticNode.java:96-97) */
+    or_leap* minute;  /* ArrayMetric(60, 60000, false) (:103)                                                   */
+    int64_t threads;  /* curThreadNum                                                                            */
+    sg_local_rule rule;
+    or_breaker cb[2];
+} or_node;
+
+struct or_local {
+    int S, interval, occupy_timeout;
+    or_node* nodes;
+    uint32_t n;
+};
+
+or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms) {
+    or_local* l = (or_local*)calloc(1, sizeof(or_local));
+    l->S = second_sample_count;            /* SampleCountProperty.SAMPLE_COUNT, default 2   */
+    l->interval = second_interval_ms;      /* IntervalProperty.INTERVAL, default 1000        */
+    l->occupy_timeout = occupy_timeout_ms; /* OccupyTimeoutProperty.occupyTimeout, 500      */
+    return l;
+}
+
+static void free_nodes(or_local* l) {
+    for (uint32_t i = 0; i < l->n; i++) {
+        or_leap_free(l->nodes[i].second);
+        or_leap_free(l->nodes[i].minute);
+        for (int j = 0; j < 2; j++) or_leap_free(l->nodes[i].cb[j].stat);
+    }
+    free(l->nodes);
+    l->nodes = NULL;
+    l->n = 0;
+}
+
+void or_local_free(or_local* l) {
+    if (!l) return;
+    free_nodes(l);
+    free(l);
+}
+
+int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
+    free_nodes(l);
+    l->nodes = (or_node*)calloc(n ? n : 1, sizeof(or_node));
+    l->n = n;
+    for (uint32_t i = 0; i < n; i++) {
+        or_node* nd = &l->nodes[i];
+        nd->rule = rules[i];
+        nd->second = or_leap_new(OR_LEAP_OCCUPIABLE, l->S, l->interval);
+        nd->minute = or_leap_new(OR_LEAP_BUCKET, 60, 60 * 1000);
+        for (int j = 0; j < rules[i].n_breakers && j < 2; j++) {
+            nd->cb[j].rule = rules[i].breakers[j];
+            nd->cb[j].state = OR_CB_CLOSED;
+            nd->cb[j].stat = or_leap_new(OR_LEAP_BUCKET, 1, rules[i].breakers[j].stat_interval_ms);
+            if (!nd->cb[j].stat) return SG_E_INVAL;
+        }
+    }
+    return 0;
+}
+
+/* StatisticNode.passQps = rollingCounterInSecond.pass() / getWindowIntervalInSec (StatisticNode.java:200-202) */
+static double node_pass_qps(or_node* nd, int64_t t) {
+    return (double)or_leap_get_sum(nd->second, t, OR_M_PASS) / nd->second->isec;
+}
+
+/* StatisticNode.tryOccupyNext, StatisticNode.java:288-320 */
+static int64_t node_try_occupy_next(or_local* l, or_node* nd, int64_t now, int acquire, double threshold) {
+    double max_count = threshold * l->interval / 1000;
+    int64_t current_borrow = or_leap_current_waiting(nd->second, now);
+    if (current_borrow >= max_count) return l->occupy_timeout;
+    int window_length = l->interval / l->S;
+    int64_t earliest = now - now % window_length + window_length - l->interval;
+    int idx = 0;
+    int64_t current_pass = or_leap_get_sum(nd->second, now, OR_M_PASS);
+    while (earliest < now) {
+        int64_t wait = (int64_t)idx * window_length + window_length - now % window_length;
+        if (wait >= l->occupy_timeout) break;
+        int wv = or_leap_window_value(nd->second, earliest); /* ArrayMetric.getWindowPass */
+        int64_t window_pass = wv >= 0 ? nd->second->b[wv].c[OR_M_PASS] : 0;
+        if (current_pass + current_borrow + acquire - window_pass <= max_count) return wait;
+        earliest += window_length;
+        current_pass -= window_pass;
+        idx++;
+    }
+    return l->occupy_timeout;
+}
+
+static void node_add(or_leap* w, int64_t t, int ev, int64_t n) { or_leap_add(w, t, ev, n); }
+
+/* AbstractCircuitBreaker.tryPass (:73-84); sets *half when this call moved OPEN → HALF_OPEN. */
+static int cb_try_pass(or_breaker* cb, int64_t t, int* half) {
+    *half = 0;
+    if (cb->state == OR_CB_CLOSED) return 1;
+    if (cb->state == OR_CB_OPEN) {
+        if (t >= cb->next_retry) {
+            cb->state = OR_CB_HALF_OPEN;
+            *half = 1;
+            return 1;
+        }
+        return 0;
+    }
+    return 0;
+}
+
+static void cb_to_open(or_breaker* cb, int64_t t) { /* transformToOpen / fromHalfOpenToOpen */
+    cb->state = OR_CB_OPEN;
+    cb->next_retry = t + (int64_t)cb->rule.time_window_sec * 1000;
+}
+
+/* onRequestComplete at exit time t (ResponseTimeCircuitBreaker.java:63-118, ExceptionCircuitBreaker.java:62-113) */
+static void cb_on_complete(or_breaker* cb, int64_t t, int64_t rt, int error) {
+    int s = or_leap_current_window(cb->stat, t);
+    int is_rt = cb->rule.grade == SG_DEGRADE_RT;
+    int64_t max_rt = or_math_round(cb->rule.count);
+    if (s != -1) {
+        if (is_rt ? (rt > max_rt) : error) or_leap_slot_add(cb->stat, s, 0, 1);
+        or_leap_slot_add(cb->stat, s, 1, 1);
+    }
+    if (cb->state == OR_CB_OPEN) return;
+    if (cb->state == OR_CB_HALF_OPEN) {
+        int bad = is_rt ? (rt > max_rt) : error;
+        if (bad) {
+            cb_to_open(cb, t);
+        } else {
+            cb->state = OR_CB_CLOSED; /* fromHalfOpenToClose → resetStat: currentWindow().value().reset() */
+            int r = or_leap_current_window(cb->stat, t);
+            if (r >= 0 || r == -2) {
+                or_bucket* w = slot_ptr(cb->stat, r);
+                for (int e = 0; e < OR_MAX_EV; e++) w->c[e] = 0;
+            }
+        }
+        return;
+    }
+    int64_t bad = 0, total = 0;
+    for (int i = 0; i < cb->stat->S; i++) { /* values() at the exit time */
+        if (!cb->stat->present[i] || is_deprecated(cb->stat, t, &cb->stat->b[i])) continue;
+        bad += cb->stat->b[i].c[0];
+        total += cb->stat->b[i].c[1];
+    }
+    if (total < cb->rule.min_request_amount) return;
+    if (is_rt) {
+        double ratio = bad * 1.0 / total;
+        if (ratio > cb->rule.slow_ratio_threshold) cb_to_open(cb, t);
+        if (ratio == cb->rule.slow_ratio_threshold && cb->rule.slow_ratio_threshold == 1.0 && cb->state == OR_CB_CLOSED)
+            cb_to_open(cb, t);
+    } else {
+        double cur = (double)bad;
+        if (cb->rule.grade == SG_DEGRADE_EXCEPTION_RATIO) cur = bad * 1.0 / total;
+        if (cur > cb->rule.count) cb_to_open(cb, t);
+    }
+}
+
+int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        const sg_local_event* e = &ev[i];
+        uint32_t res = e->resource & SG_KEY_INDEX;
+        int prio = (e->resource & SG_KEY_PRIO) != 0;
+        out[i].status = SG_LOCAL_PASS;
+        out[i].wait_ms = 0;
+        if (res >= l->n) continue;
+        or_node* nd = &l->nodes[res];
+        int64_t t = e->ts_ms;
+        int count = e->count;
+        if (e->kind == SG_LOCAL_ENTRY) {
+            /* FlowSlot → DefaultController.canPass */
+            int status = SG_LOCAL_PASS;
+            int64_t wait = 0;
+            if (nd->rule.flow_grade >= 0) {
+                int32_t cur = nd->rule.flow_grade == 0 ? (int32_t)nd->threads : or_d2i(node_pass_qps(nd, t));
+                int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)count); /* int + int wraps */
+                if ((double)sum > nd->rule.flow_count) {
+                    status = SG_LOCAL_BLOCK_FLOW;
+                    if (prio && nd->rule.flow_grade == 1) {
+                        wait = node_try_occupy_next(l, nd, t, count, nd->rule.flow_count);
+                        if (wait < l->occupy_timeout) {
+                            or_leap_add_waiting(nd->second, t + wait, count); /* addWaitingRequest */
+                            node_add(nd->minute, t, OR_M_OCCUPIED_PASS, count); /* addOccupiedPass */
+                            node_add(nd->minute, t, OR_M_PASS, count);
+                            status = SG_LOCAL_PASS_WAIT;
+                        }
+                    }
+                }
+            }
+            int half[2] = {0, 0};
+            if (status == SG_LOCAL_PASS) { /* DegradeSlot.performChecking */
+                for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) {
+                    if (!cb_try_pass(&nd->cb[j], t, &half[j])) {
+                        status = SG_LOCAL_BLOCK_DEGRADE;
+                        break;
+                    }
+                }
+                if (status == SG_LOCAL_BLOCK_DEGRADE) /* whenTerminate hook: blocked probe → OPEN again */
+                    for (int j = 0; j < 2; j++)
+                        if (half[j] && nd->cb[j].state == OR_CB_HALF_OPEN) nd->cb[j].state = OR_CB_OPEN;
+            }
+            /* StatisticSlot.entry */
+            if (status == SG_LOCAL_PASS) {
+                nd->threads++;
+                node_add(nd->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
+                node_add(nd->minute, t, OR_M_PASS, count);
+            } else if (status == SG_LOCAL_PASS_WAIT) {
+                nd->threads++;
+                out[i].wait_ms = (int32_t)wait;
+            } else {
+                node_add(nd->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
+                node_add(nd->minute, t, OR_M_BLOCK, count);
+            }
+            out[i].status = status;
+        } else {
+            /* StatisticSlot.exit: addRtAndSuccess, decreaseThreadNum, increaseExceptionQps */
+            int error = e->kind == SG_LOCAL_EXIT_ERROR;
+            int64_t rt = t - e->create_ts;
+            node_add(nd->second, t, OR_M_SUCCESS, count);
+            { int s = or_leap_current_window(nd->second, t); if (s != -1) or_leap_slot_add_rt(nd->second, s, rt); }
+            node_add(nd->minute, t, OR_M_SUCCESS, count);
+            { int s = or_leap_current_window(nd->minute, t); if (s != -1) or_leap_slot_add_rt(nd->minute, s, rt); }
+            nd->threads--;
+            if (error) {
+                node_add(nd->second, t, OR_M_EXCEPTION, count);
+                node_add(nd->minute, t, OR_M_EXCEPTION, count);
+            }
+            /* DegradeSlot.exit → onRequestComplete */
+            for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) cb_on_complete(&nd->cb[j], t, rt, error);
+        }
+    }
+    return 0;
+}
+
+int64_t or_local_second_sum(or_local* l, uint32_t res, int64_t t, int ev) {
+    return res < l->n ? or_leap_get_sum(l->nodes[res].second, t, ev) : 0;
+}
+int64_t or_local_minute_sum(or_local* l, uint32_t res, int64_t t, int ev) {
+    return res < l->n ? or_leap_get_sum(l->nodes[res].minute, t, ev) : 0;
+}
+int64_t or_local_thread_num(const or_local* l, uint32_t res) { return res < l->n ? l->nodes[res].threads : 0; }
+int64_t or_local_waiting(or_local* l, uint32_t res, int64_t t) {
+    return res < l->n ? or_leap_current_waiting(l->nodes[res].second, t) : 0;
+}
+int or_local_breaker_state(const or_local* l, uint32_t res, int i, int64_t* next_retry) {
+    if (res >= l->n || i < 0 || i >= l->nodes[res].rule.n_breakers) return -1;
+    *next_retry = l->nodes[res].cb[i].next_retry;
+    return l->nodes[res].cb[i].state;
+}
+
+static void dump_leap(const or_leap* w, int64_t* out, int with_minrt) {
+    for (int i = 0; i < w->S; i++) {
+        int64_t* o = out + (size_t)i * (with_minrt ? 8 : 2);
+        if (!with_minrt) {
+            o[0] = w->present[i] ? w->b[i].start : INT64_MIN;
+            o[1] = w->present[i] ? w->b[i].c[OR_M_PASS] : 0;
+            continue;
+        }
+        o[0] = w->present[i] ? w->b[i].start : INT64_MIN;
+        for (int e = 0; e < OR_M_NUM; e++) o[1 + e] = w->present[i] ? w->b[i].c[e] : 0;
+        o[7] = w->present[i] ? w->b[i].min_rt : 0;
+    }
+}
+
+int or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute) {
+    if (res >= l->n) return SG_E_INVAL;
+    const or_node* nd = &l->nodes[res];
+    dump_leap(nd->second, second, 1);
+    dump_leap(nd->second->borrow, borrow, 0);
+    dump_leap(nd->minute, minute, 1);
+    return 0;
+}

@@ -111,6 +111,21 @@ int     or_pf_decide(or_pf* p, const sg_param_req* req, uint64_t n, int32_t* out
 int     or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
 uint64_t or_pf_size(const or_pf* p);
 
+/* ---------- local slot chain: StatisticSlot / FlowSlot(DefaultController) / DegradeSlot ---------- */
+typedef struct or_local or_local;
+or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms);
+void      or_local_free(or_local* l);
+int       or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n);
+int       or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_result* out);
+/* Node statistics of a resource at t (ArrayMetric sums with the currentWindow side effect). */
+int64_t   or_local_second_sum(or_local* l, uint32_t res, int64_t t, int ev);
+int64_t   or_local_minute_sum(or_local* l, uint32_t res, int64_t t, int ev);
+int64_t   or_local_thread_num(const or_local* l, uint32_t res);
+int64_t   or_local_waiting(or_local* l, uint32_t res, int64_t t);
+int       or_local_breaker_state(const or_local* l, uint32_t res, int i, int64_t* next_retry);
+/* Raw window dumps for parity: second main ring [S][8] (start, 6 counters, minRt), borrow [S][2], minute [60][8]. */
+int       or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute);
+
 #ifdef __cplusplus
 }
 #endif

@@ -84,10 +84,26 @@ PARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("value", "<u8"), ("rule", "<u4"),
 BEHAVIOR_DEFAULT = 0
 BEHAVIOR_RATE_LIMITER = 2
 
+# local slot chain (sg_local_*)
+DEGRADE_RULE_DTYPE = np.dtype([("grade", "<i4"), ("time_window_sec", "<i4"), ("count", "<f8"),
+                               ("slow_ratio_threshold", "<f8"), ("min_request_amount", "<i4"),
+                               ("stat_interval_ms", "<i4")], align=True)
+LOCAL_RULE_DTYPE = np.dtype([("flow_count", "<f8"), ("flow_grade", "<i4"), ("n_breakers", "<i4"),
+                             ("breakers", DEGRADE_RULE_DTYPE, (2,))], align=True)
+LOCAL_EVENT_DTYPE = np.dtype([("ts_ms", "<i8"), ("create_ts", "<i8"), ("resource", "<u4"), ("count", "<i4"),
+                              ("kind", "<i4"), ("reserved", "<i4")], align=True)
+LOCAL_RES_DTYPE = np.dtype([("status", "<i4"), ("wait_ms", "<i4")], align=True)
+DEGRADE_RT, DEGRADE_EXCEPTION_RATIO, DEGRADE_EXCEPTION_COUNT = 0, 1, 2
+FLOW_GRADE_THREAD, FLOW_GRADE_QPS, FLOW_GRADE_NONE = 0, 1, -1
+LOCAL_ENTRY, LOCAL_EXIT, LOCAL_EXIT_ERROR = 0, 1, 2
+LOCAL_PASS, LOCAL_BLOCK_FLOW, LOCAL_BLOCK_DEGRADE, LOCAL_PASS_WAIT = 0, 1, 2, 3
+
 assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
 assert RES_DTYPE.itemsize == C.sizeof(sg_result) == 12
 assert RULE_DTYPE.itemsize == C.sizeof(sg_flow_rule) == 32
 assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
+assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
+assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:
