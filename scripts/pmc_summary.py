@@ -1,0 +1,54 @@
+"""Per-kernel HBM traffic from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; counter_collection.csv).
+
+FETCH_SIZE is doubled (MI355X_MICROARCH.md §HBM: on gfx950 it reports half the bytes of wide coalesced
+reads); both are KiB in rocprofv3's derived-counter units. Output: {kernel: {launches, fetch_bytes,
+write_bytes}} averaged per launch, and the per-step sum over the decision pipeline's kernels.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+PIPELINE = ("k_prep", "k_lim_", "k_radix_", "k_scan_", "k_walk_", "k_skip_apply", "k_finish",
+            "k_lprep", "k_lwalk_", "k_lskip_apply", "k_lfinish")
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"].split("(")[0].split("<")[0].strip()
+            per[name].append(float(r["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main(fetch_dir, write_dir, out):
+    f = load(fetch_dir, "FETCH_SIZE")
+    w = load(write_dir, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        fb = 2.0 * sum(f.get(k, [])) / max(1, len(f.get(k, [])))
+        wb = sum(w.get(k, [])) / max(1, len(w.get(k, [])))
+        res[k] = {"launches": max(len(f.get(k, [])), len(w.get(k, []))), "fetch_bytes": fb, "write_bytes": wb}
+    # per step: every pipeline kernel's per-launch traffic × launches per step (launch counts / steps)
+    steps = None
+    for k in ("k_finish", "k_lfinish"):
+        if k in res:
+            steps = res[k]["launches"]
+    step_bytes = 0.0
+    if steps:
+        for k, v in res.items():
+            if k.startswith(PIPELINE):
+                step_bytes += (v["fetch_bytes"] + v["write_bytes"]) * v["launches"] / steps
+    json.dump({"kernels": res, "pipeline_bytes_per_step": step_bytes, "steps_seen": steps,
+               "note": "FETCH_SIZE x2 (gfx950 correction), KiB→bytes"}, open(out, "w"), indent=1)
+    print(json.dumps({"pipeline_bytes_per_step": step_bytes, "steps_seen": steps}))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
