@@ -84,6 +84,7 @@ extern "C" {
 /* sg_config.flags: force one walker for every flowId segment (testing both walkers on any trace). */
 #define SG_FLAG_SERIAL_ONLY 1   /* one lane per flowId, however long its segment */
 #define SG_FLAG_WAVE_ONLY   2   /* one wave per flowId, however short its segment */
+#define SG_FLAG_RING_REREAD 4   /* short walker without the register ring snapshot (re-reads the ring)   */
 
 /* Largest sampleCount the device walker keeps in a wave (one bucket per lane). */
 #define SG_MAX_SAMPLE_COUNT 64

@@ -11,7 +11,7 @@ import os
 import sys
 from collections import defaultdict
 
-PIPELINE = ("k_prep", "k_lim_", "k_radix_", "k_scan_", "k_walk_", "k_skip_apply", "k_finish",
+PIPELINE = ("k_prep", "k_seg", "k_lim_", "k_radix_", "k_scan_", "k_walk_", "k_skip_apply", "k_finish",
             "k_lprep", "k_lwalk_", "k_lskip_apply", "k_lfinish")
 
 
@@ -22,7 +22,7 @@ def load(d, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            name = r["Kernel_Name"].split("(")[0].split("<")[0].strip()
+            name = r["Kernel_Name"].split("(")[0].split("<")[0].strip().split("::")[-1]
             per[name].append(float(r["Counter_Value"]) * 1024.0)
     return per
 

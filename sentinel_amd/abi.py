@@ -38,6 +38,7 @@ KEY_BAD = 0x7FFFFFFE
 MAX_SAMPLE_COUNT = 64
 FLAG_SERIAL_ONLY = 1
 FLAG_WAVE_ONLY = 2
+FLAG_RING_REREAD = 4
 INT64_MIN = -(1 << 63)
 
 

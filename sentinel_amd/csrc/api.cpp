@@ -6,6 +6,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -43,7 +44,10 @@ struct sg_handle {
     int* d_err = nullptr;
     int64_t* d_last_ts = nullptr;
     uint32_t* d_long_list = nullptr;
-    uint32_t* d_long_count = nullptr;
+    uint32_t* d_long_count = nullptr;  // [4]: long count, short count, work cursors (long, short)
+    uint32_t* d_short_list = nullptr;
+    uint64_t class_off[kClasses]{};
+    unsigned long long* d_dbg = nullptr;   // [16] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
     uint32_t* d_skip_count = nullptr;
     int* h_err = nullptr;       // pinned
@@ -77,8 +81,12 @@ struct sg_handle {
 
     int kbits = 0, ibits = 0, abits = 0;
     bool stats_on = false;
+    uint32_t short_max = kShortMax;   // default walker split (env SG_SHORT_MAX overrides, for tuning)
+    int dbg = 0;                      // env SG_DEBUG: see BatchArgs::dbg
     hipEvent_t ev[5]{};
     sg_batch_stats stats{};
+    hipStream_t aux = nullptr;        // second stream: the long-segment walker runs beside the short one
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -213,8 +221,17 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipMalloc(&h->d_long_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipMalloc(&h->d_skips, sizeof(uint4) * (n / kSkipMin + 1)) != hipSuccess) return bail(SG_E_NOMEM);
+    {  // short-segment class slices: class c holds segments longer than kClassMax[c-1], so at most n/(that+1)
+        uint64_t off = 0;
+        for (int c = 0; c < kClasses; ++c) {
+            h->class_off[c] = off;
+            off += (c == 0 ? n : n / (kClassMax[c - 1] + 1)) + 1;
+        }
+        if (hipMalloc(&h->d_short_list, sizeof(uint32_t) * off) != hipSuccess) return bail(SG_E_NOMEM);
+    }
+    if (hipMalloc(&h->d_dbg, 16 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 16 * 8) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_long_count, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_skips, sizeof(uint4) * (2 * n / kSkipMin + 1)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_skip_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipHostMalloc(&h->h_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipHostMalloc(&h->h_long, 2 * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -224,6 +241,12 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMemcpy(h->d_plast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     for (auto& e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(SG_E_DEVICE);
+    if (hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->join, hipEventDisableTiming) != hipSuccess)
+        return bail(SG_E_DEVICE);
+    if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
+    if (const char* sm = std::getenv("SG_SHORT_MAX")) h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
     // default namespace 0, no limiter, 1 connection
     sg_namespace d0{0, 1, 30000.0};
     h->ns.push_back(d0);
@@ -252,6 +275,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_last_ts);
     dfree(h->d_long_list);
     dfree(h->d_long_count);
+    dfree(h->d_short_list);
+    dfree(h->d_dbg);
     dfree(h->d_skips);
     dfree(h->d_prules);
     dfree(h->d_phot);
@@ -266,6 +291,9 @@ void sg_destroy(sg_handle* h) {
     if (h->h_long) (void)hipHostFree(h->h_long);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
+    if (h->fork) (void)hipEventDestroy(h->fork);
+    if (h->join) (void)hipEventDestroy(h->join);
+    if (h->aux) (void)hipStreamDestroy(h->aux);
     delete h;
 }
 
@@ -450,15 +478,21 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.last_ts = h->d_last_ts;
     a.long_list = h->d_long_list;
     a.long_count = h->d_long_count;
+    a.short_list = h->d_short_list;
+    a.short_count = h->d_long_count + 1;
+    for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
     a.skips = h->d_skips;
     a.skip_count = h->d_skip_count;
-    a.skip_cap = (uint32_t)(h->cfg.max_batch / kSkipMin + 1);
+    a.dbg = h->dbg;
+    a.generic_walker = (h->cfg.flags & SG_FLAG_RING_REREAD) != 0;
+    a.dbg_ctr = h->d_dbg;
+    a.skip_cap = (uint32_t)(2 * h->cfg.max_batch / kSkipMin + 1);
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
-                  : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : (uint32_t)kShortMax;
+                  : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : h->short_max;
 
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_skip_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_prep(a, stream));
     if (h->n_lim > 0) {
@@ -485,8 +519,19 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         h->last_sorted = sorted;
     }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
-    HIP_TRY(h, launch_walk_short(a, stream));
-    HIP_TRY(h, launch_walk_long(a, stream));
+    HIP_TRY(h, launch_seg(a, stream));
+    // fork: long segments on the aux stream, short ones on the caller's stream, then join
+    if (h->dbg & 2) {
+        HIP_TRY(h, launch_walk_long(a, stream));
+        HIP_TRY(h, launch_walk_short(a, stream));
+    } else {
+        HIP_TRY(h, hipEventRecord(h->fork, stream));
+        HIP_TRY(h, hipStreamWaitEvent(h->aux, h->fork, 0));
+        HIP_TRY(h, launch_walk_long(a, h->aux));
+        HIP_TRY(h, launch_walk_short(a, stream));
+        HIP_TRY(h, hipEventRecord(h->join, h->aux));
+        HIP_TRY(h, hipStreamWaitEvent(stream, h->join, 0));
+    }
     HIP_TRY(h, launch_skip_apply(a, stream));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, launch_finish(a, stream));
@@ -511,6 +556,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     if (*h->h_err & kErrTime)
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
     if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
     return SG_OK;
 }
 
@@ -711,6 +757,7 @@ int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {
     case 2: src = h->d_bnd; cap = sizeof(uint32_t) * kMaxWl * kMaxPeriods; break;
     case 3: src = h->d_p0; cap = sizeof(int64_t) * kMaxWl; break;
     case 4: src = h->d_np; cap = sizeof(uint32_t) * kMaxWl; break;
+    case 5: src = h->d_dbg; cap = 16 * 8; break;
     default: return SG_E_INVAL;
     }
     if (bytes > cap) return SG_E_INVAL;

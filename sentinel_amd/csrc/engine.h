@@ -38,11 +38,17 @@ struct alignas(16) Occ {
 
 constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
-constexpr int kShortMax = 16;             // default: segments longer than this are walked by a whole wave
+constexpr int kShortMax = 256;            // default: segments longer than this are walked by a whole wave
+constexpr int kLdsBnd = 4096;             // period-table entries the walk kernel stages in LDS
+// Short segments are grouped by length class (length <= 4, 16, 64, 256, 1024, more) so that the 64 lanes
+// of a short-walker wave walk segments of similar length.
+constexpr int kClasses = 6;
+constexpr uint32_t kClassMax[kClasses - 1] = {4, 16, 64, 256, 1024};
 
 // error bits reported through BatchArgs::err
 constexpr int kErrTime = 1;      // negative or decreasing timestamps
 constexpr int kErrPeriods = 2;   // batch spans more than kMaxPeriods windows
+constexpr int kErrInternal = 16; // a walker loop exceeded its bound (never expected)
 
 struct BatchArgs {
     const sg_req* req;
@@ -71,14 +77,22 @@ struct BatchArgs {
     int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
+    uint32_t* short_list; // segment starts walked one lane each, per length class (slices, see class_off)
+    uint32_t* short_count; // [kClasses] per length class
+    uint64_t class_off[kClasses]; // first entry of each class slice in short_list
     uint32_t short_max;  // segments longer than this go to the wave walker
+    int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
+                         // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr
+    int generic_walker;  // SG_FLAG_RING_REREAD: short walker re-reads the ring (no register snapshot)
+    unsigned long long* dbg_ctr;  // [16]
     // ranges of records the wave walker skipped as certainly BLOCKED: {flow key, period q, begin, end}
     uint4* skips;
     uint32_t* skip_count;
     uint32_t skip_cap;
 };
 
-constexpr uint32_t kSkipMin = 256;  // shortest all-BLOCKED tail worth skipping (records)
+constexpr uint32_t kSkipMin = 256;    // shortest all-BLOCKED tail worth skipping (records)
+constexpr uint32_t kSkipPiece = 4096; // skipped ranges are handed to k_skip_apply in pieces of this size
 
 // ---- namespace QPS limiter (limiter.hip) ----
 constexpr int kMaxLim = 8;          // namespaces with a RequestLimiter on the device path
@@ -160,8 +174,9 @@ hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 size_t radix_hist_words(uint64_t n);
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit = 64);
-hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);
-hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
+hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,

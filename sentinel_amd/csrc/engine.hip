@@ -36,6 +36,12 @@ __device__ __forceinline__ int32_t java_d2i(double x) {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// LeapArray sum / intervalInSecond (ClusterMetric.getAvg, ClusterMetric.java:70-72). x / 1.0 == x exactly,
+// so the common 1000 ms interval skips the fp64 division.
+__device__ __forceinline__ double qps_of(int64_t sum, double isec) {
+    return isec == 1.0 ? (double)sum : (double)sum / isec;
+}
+
 __device__ __forceinline__ int64_t wave_sum(int64_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((long long)v, o, 64);
@@ -168,9 +174,9 @@ __device__ __forceinline__ int32_t decide_fail(const Rule& R, double max_occ_rat
                                                int64_t acq, bool prio, int32_t* wait) {
     *wait = 0;
     if (prio) {
-        const double occupy_avg = (double)(ps.wo_wait + ps.cur[SG_EV_WAITING]) / R.isec;
+        const double occupy_avg = qps_of(ps.wo_wait + ps.cur[SG_EV_WAITING], R.isec);
         if (occupy_avg <= max_occ_ratio * R.thr) {
-            const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+            const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
             const int64_t head = (R.S == 1) ? ps.cur[SG_EV_PASS] : ps.head_other;
             if (latest + (double)(acq + ps.occ_pass) - (double)head <= R.thr) {
                 ps.occ_pass += acq;  // addOccupyPass, ClusterMetricLeapArray.java:73-77
@@ -264,10 +270,11 @@ __device__ __forceinline__ void open_period_serial(PeriodState& ps, const Bucket
 // ------------------------------------------------------------------------ serial walker (short)
 
 // Outputs start as BLOCKED (k_prep), so only OK / SHOULD_WAIT results are written here.
-__device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
+__device__ uint32_t walk_serial(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e) {
+    uint32_t opened = 0;
     const Rule R = a.rules[k];
     Bucket* ring = a.ring + (size_t)k * a.stride;
-    PeriodCursor pc{a.bnd + (size_t)R.wl_idx * kMaxPeriods, a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+    PeriodCursor pc{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
     const int64_t P0 = a.p0[R.wl_idx];
     PeriodState ps;
     {
@@ -277,8 +284,11 @@ __device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
     }
     int64_t ws = 0;
     int I = -1;
+    uint64_t nxt = a.rec_sorted[s];
     for (uint64_t j = s; j < e; ++j) {
-        const Decoded d = decode(a, a.rec_sorted[j]);
+        const uint64_t cur = nxt;
+        if (j + 1 < e) nxt = a.rec_sorted[j + 1];  // issue the next record's load before deciding this one
+        const Decoded d = decode(a, cur);
         const uint32_t q = pc.of(d.idx);
         if (q != pc.q) {
             if (I >= 0) {
@@ -288,9 +298,10 @@ __device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
             }
             pc.seek(q);
             open_period_serial(ps, ring, R, P0 + (int64_t)q, &I, &ws);
+            ++opened;
         }
         // ClusterFlowChecker.acquireClusterToken, :67-81
-        const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+        const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
         const double next_remaining = R.thr - latest - (double)d.acq;
         if (next_remaining >= 0) {
             ps.cur[SG_EV_PASS] += d.acq;
@@ -312,26 +323,7 @@ __device__ void walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
     o.pass = ps.occ_pass;
     o.pass_req = ps.occ_req;
     a.occ[k] = o;
-}
-
-__global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
-    if (*a.err) return;
-    const uint64_t n = a.n;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t rec = a.rec_sorted[j];
-        const uint32_t k = (uint32_t)(rec >> a.kshift);
-        if (k >= a.K) continue;
-        if (j > 0 && (uint32_t)(a.rec_sorted[j - 1] >> a.kshift) == k) continue;  // not a segment head
-        uint64_t e = j + 1;
-        const uint64_t smax = a.short_max;
-        while (e < n && e - j <= smax && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
-        if (e - j > smax) {
-            const uint32_t pos = atomicAdd(a.long_count, 1u);
-            a.long_list[pos] = (uint32_t)j;
-            continue;
-        }
-        walk_serial(a, k, j, e);
-    }
+    return opened;
 }
 
 // --------------------------------------------------------------------------- wave walker (long)
@@ -357,9 +349,10 @@ struct WaveWalker {
     // request can occupy (both only get harder within a period), so its remaining requests are BLOCKED
     bool dead;
 
-    __device__ WaveWalker(const BatchArgs& a_, uint32_t k) : a(a_), R(a_.rules[k]), lane(lane_id()) {
+    __device__ WaveWalker(const BatchArgs& a_, const uint32_t* const* bndp, uint32_t k)
+        : a(a_), R(a_.rules[k]), lane(lane_id()) {
         ring = a.ring + (size_t)k * a.stride;
-        pc = PeriodCursor{a.bnd + (size_t)R.wl_idx * kMaxPeriods, a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+        pc = PeriodCursor{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
         P0 = a.p0[R.wl_idx];
         st = INT64_MIN;
 #pragma unroll
@@ -417,7 +410,7 @@ struct WaveWalker {
 
     // Can any prioritized request still occupy in this period? (wave-uniform; the window is fixed.)
     __device__ __forceinline__ bool occupy_possible(double latest) const {
-        const double occupy_avg = (double)(ps.wo_wait + ps.cur[SG_EV_WAITING]) / R.isec;
+        const double occupy_avg = qps_of(ps.wo_wait + ps.cur[SG_EV_WAITING], R.isec);
         if (!(occupy_avg <= a.max_occ_ratio * R.thr)) return false;
         const int64_t head = (R.S == 1) ? ps.cur[SG_EV_PASS] : ps.head_other;
         return latest + (double)(1 + ps.occ_pass) - (double)head <= R.thr;
@@ -425,7 +418,7 @@ struct WaveWalker {
 
     // Decide the lanes in `run` (contiguous, same period, in order).
     __device__ void run(uint64_t run_mask, const Decoded& d) {
-        const double latest0 = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+        const double latest0 = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
         if (!(R.thr - latest0 - 1.0 >= 0)) {
             // Saturated: not even acquireCount = 1 fits, and nothing below can add PASS in this period,
             // so every non-prioritized request blocks; prioritized ones try to occupy one by one until
@@ -450,13 +443,18 @@ struct WaveWalker {
             return;
         }
         uint64_t pending = run_mask;
+        int guard = 0;
         while (pending) {
+            if (++guard > 64) {  // every pass removes >= 1 pending lane
+                atomicOr(a.err, kErrInternal);
+                break;
+            }
             // -- admit mode: every pending request passes until the first one that does not fit
             const bool pl = (pending >> lane) & 1ull;
             const int64_t av = pl ? d.acq : 0;
             const int64_t ex = wave_excl_scan(av, lane);
             const int64_t W = ps.wo_pass + ps.cur[SG_EV_PASS];
-            const double latest_l = (double)(W + ex) / R.isec;
+            const double latest_l = qps_of(W + ex, R.isec);
             const double nr_l = R.thr - latest_l - (double)d.acq;
             const uint64_t fails = __ballot(pl && !(nr_l >= 0));
             const uint64_t pass_mask = fails ? (pending & below(__builtin_ctzll(fails))) : pending;
@@ -482,7 +480,7 @@ struct WaveWalker {
                 // prioritized requests that do not fit stop the skip (they may occupy).
                 if (!pending) break;
                 const bool pl2 = (pending >> lane) & 1ull;
-                const double latest = (double)(ps.wo_pass + ps.cur[SG_EV_PASS]) / R.isec;
+                const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
                 const bool fit = pl2 && (R.thr - latest - (double)d.acq >= 0);
                 const uint64_t fitm = __ballot(fit);
                 const uint64_t stop = fitm | __ballot(pl2 && d.prio);
@@ -514,7 +512,12 @@ struct WaveWalker {
             q = pc.of(d.idx);
         }
         uint64_t todo = __ballot(act);
+        int guard = 0;
         while (todo) {
+            if (++guard > 64) {  // at most one run per lane; anything else is an internal error
+                atomicOr(a.err, kErrInternal);
+                break;
+            }
             const uint32_t qrun = (uint32_t)bcast32((int)q, __builtin_ctzll(todo));
             if (qrun != pc.q) open_period(qrun);
             const uint64_t rm = __ballot(act && q == qrun) & todo;  // contiguous lanes of this period
@@ -562,8 +565,8 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
     return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
-__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
-    WaveWalker w(a, k);
+__device__ void walk_wave(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e) {
+    WaveWalker w(a, bndp, k);
     const int lane = w.lane;
     const uint64_t* rec = a.rec_sorted;
     constexpr uint64_t kBlock = 64ull * kWaveUnroll;
@@ -599,11 +602,17 @@ __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e
                     return (uint32_t)((rec[p] >> a.abits) & a.imask) >= nb;
                 }, lane);
                 if (pe - after >= kSkipMin) {
+                    // hand the range over in pieces of <= kSkipPiece records (one k_skip_apply wave each)
+                    const uint32_t np = (uint32_t)((pe - after + kSkipPiece - 1) / kSkipPiece);
                     uint32_t slot = 0;
-                    if (lane == 0) slot = atomicAdd(a.skip_count, 1u);
+                    if (lane == 0) slot = atomicAdd(a.skip_count, np);
                     slot = (uint32_t)bcast32((int)slot, 0);
-                    if (slot < a.skip_cap) {
-                        if (lane == 0) a.skips[slot] = make_uint4(k, w.pc.q, (uint32_t)after, (uint32_t)pe);
+                    if (slot + np <= a.skip_cap) {
+                        for (uint32_t pi = lane; pi < np; pi += 64) {
+                            const uint64_t b0 = after + (uint64_t)pi * kSkipPiece;
+                            const uint64_t b1 = min(pe, b0 + kSkipPiece);
+                            a.skips[slot + pi] = make_uint4(k, w.pc.q, (uint32_t)b0, (uint32_t)b1);
+                        }
                         npos = pe;
                         skipped = true;
                     }
@@ -624,60 +633,323 @@ __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e
     w.finish(k);
 }
 
-__global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
+// ------------------------------------------------------------------- segments and the walk kernel
+
+// Segment heads of the sorted records (first record of each flowId), compacted into two work lists:
+// segments of more than short_max records (one wave each) and the rest (one lane each). One block per
+// tile of kSegTile records; appends are block-aggregated (one atomic per block and list), since
+// same-address atomics from every wave serialise at the L2.
+constexpr int kSegThreads = 256;
+constexpr int kSegItems = 16;
+constexpr uint32_t kSegTile = kSegThreads * kSegItems;
+
+__global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
+    constexpr int kL = kClasses + 1;  // list 0..kClasses-1: short length classes, kClasses: long
+    __shared__ uint32_t cnt[kL];
+    __shared__ uint32_t base[kL];
     if (*a.err) return;
-    const uint32_t cnt = *a.long_count;
-    const uint32_t waves_per_block = blockDim.x / 64;
-    const uint32_t wave = blockIdx.x * waves_per_block + threadIdx.x / 64;
-    const uint32_t nwaves = gridDim.x * waves_per_block;
-    const int lane = lane_id();
-    for (uint32_t w = wave; w < cnt; w += nwaves) {
-        const uint64_t s = a.long_list[w];
-        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-        // segment end: the first record with another flowId
-        const uint64_t e = wave_search(s + a.short_max, a.n, [&](uint64_t p) {
-            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
-        }, lane);
-        walk_wave(a, k, s, e);
+    const uint64_t n = a.n;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kSegTile; t0 < n; t0 += (uint64_t)gridDim.x * kSegTile) {
+        if (tid < kL) cnt[tid] = 0;
+        __syncthreads();
+        // item u of wave w covers records t0 + (w*kSegItems + u)*64 + lane (wave-contiguous rows)
+        uint32_t key[kSegItems];
+#pragma unroll
+        for (int u = 0; u < kSegItems; ++u) {
+            const uint64_t j = t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane;
+            key[u] = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
+        }
+        uint32_t slot[kSegItems];  // (list << 24) | position within the block's share of that list
+#pragma unroll
+        for (int u = 0; u < kSegItems; ++u) {
+            const uint64_t j = t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane;
+            uint32_t kp = (uint32_t)__shfl_up((int)key[u], 1u, 64);
+            if (lane == 0) kp = (j < n && j > 0) ? (uint32_t)(a.rec_sorted[j - 1] >> a.kshift) : 0xFFFFFFFFu;
+            slot[u] = 0xFFFFFFFFu;
+            if (j < n && key[u] < a.K && key[u] != kp) {
+                // length probes: the segment is longer than m iff record j + m has the same flowId
+                auto longer = [&](uint64_t m) {
+                    return j + m < n && (uint32_t)(a.rec_sorted[j + m] >> a.kshift) == key[u];
+                };
+                uint32_t l = kClasses;
+                if (!longer(a.short_max)) {
+                    l = kClasses - 1;
+                    for (int c = kClasses - 2; c >= 0; --c)
+                        if (!longer(kClassMax[c])) l = (uint32_t)c;
+                }
+                slot[u] = (l << 24) | atomicAdd(&cnt[l], 1u);  // order within a list is irrelevant
+            }
+        }
+        __syncthreads();
+        if (tid < kL) {
+            const uint32_t t = cnt[tid];
+            uint32_t* ctr = tid == kClasses ? a.long_count : a.short_count + tid;
+            base[tid] = t ? atomicAdd(ctr, t) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kSegItems; ++u) {
+            if (slot[u] == 0xFFFFFFFFu) continue;
+            const uint32_t j = (uint32_t)(t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane);
+            const uint32_t l = slot[u] >> 24, pos = base[l] + (slot[u] & 0xFFFFFFu);
+            if (l == (uint32_t)kClasses) a.long_list[pos] = j;
+            else a.short_list[a.class_off[l] + pos] = j;
+        }
+        __syncthreads();  // cnt / base are reused by the next tile
     }
 }
 
-// BLOCK / BLOCK_REQUEST / OCCUPIED_BLOCK of the ranges the wave walker skipped, added to their period's
-// bucket unless a later period of the same batch has reset that slot (which discards them anyway).
+// The period table of the batch, staged in LDS when it fits (else read from HBM/L2): bndp[w] points at
+// window length w's boundaries.
+__device__ __forceinline__ void stage_periods(const BatchArgs& a, uint32_t* sbnd, const uint32_t** bndp) {
+    uint32_t tot = 0;
+    for (int w = 0; w < a.n_wl; ++w) tot += a.np[w];
+    const bool lds = tot <= (uint32_t)kLdsBnd && !(a.dbg & 1);
+    uint32_t off = 0;
+    for (int w = 0; w < a.n_wl; ++w) {
+        const uint32_t npw = a.np[w];
+        const uint32_t* g = a.bnd + (size_t)w * kMaxPeriods;
+        if (lds) {
+            for (uint32_t i = threadIdx.x; i < npw; i += blockDim.x) sbnd[off + i] = g[i];
+            if (threadIdx.x == 0) bndp[w] = sbnd + off;
+        } else if (threadIdx.x == 0) {
+            bndp[w] = g;
+        }
+        off += npw;
+    }
+    __syncthreads();
+}
+
+// Long-segment walker: one wave per segment of more than short_max records (grid-stride over the list,
+// grid sized to what is resident at once). Runs concurrently with k_walk_short (separate stream).
+__global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_periods(a, sbnd, bndp);
+    const int lane = lane_id();
+    const uint32_t n_long = *a.long_count;
+    // static wave → item assignment (wave-uniform loop control; a dynamic atomic work queue here
+    // miscompiled: lanes of a wave lost convergence after the first walk)
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t item = wave; item < n_long; item += nwaves) {
+        const uint64_t s = a.long_list[item];
+        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+        // segment end: the first record with another flowId
+        const uint64_t e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
+            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
+        }, lane);
+        walk_wave(a, bndp, k, s, e);
+    }
+}
+
+// Serial walk of one flowId segment with the ring's {period, PASS, WAITING} of all SM >= S slots held in
+// registers: the ring is read from HBM once (and slot I's full bucket only when the batch continues the
+// stored period), each closed bucket is written back, nothing is re-read. Same decisions as walk_serial,
+// which re-reads the ring at every new period (the working set of all lanes does not fit L2).
+constexpr int32_t kRelAbsent = INT32_MIN;      // slot never created
+constexpr int32_t kRelOld = INT32_MIN + 1;     // created, but too old to be valid anywhere in this batch
+
+template <int SM>
+__device__ void walk_reg(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s) {
+    const Rule R = a.rules[k];
+    Bucket* ring = a.ring + (size_t)k * a.stride;
+    const int S = R.S;
+    const int64_t wl = R.wl;
+    PeriodCursor pc{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+    const int64_t P0 = a.p0[R.wl_idx];
+    const int64_t base_ws = P0 * wl;  // window start of the batch's first period: rel period 0
+    int32_t rel[SM];
+    int64_t pa[SM], wa[SM];
+#pragma unroll
+    for (int j = 0; j < SM; ++j) {
+        rel[j] = kRelAbsent;
+        pa[j] = wa[j] = 0;
+        if (j < S) {
+            const int64_t st = ring[j].start;
+            pa[j] = ring[j].c[SG_EV_PASS];
+            wa[j] = ring[j].c[SG_EV_WAITING];
+            if (st != INT64_MIN) {
+                const int64_t d = st - base_ws;  // <= 0: stored buckets are older than this batch
+                rel[j] = (d < -(int64_t)S * wl) ? kRelOld : (int32_t)(d / wl);
+            }
+        }
+    }
+    PeriodState ps;
+    {
+        const Occ o = a.occ[k];
+        ps.occ_pass = o.pass;
+        ps.occ_req = o.pass_req;
+    }
+    int I = -1;      // slot of the open period
+    int32_t r = 0;   // open period, relative to P0
+    bool first = true;
+    uint64_t j = s;
+    uint64_t nxt = a.rec_sorted[j];
+    for (;;) {
+        const uint64_t cur = nxt;
+        if ((uint32_t)(cur >> a.kshift) != k) break;
+        ++j;
+        nxt = j < a.n ? a.rec_sorted[j] : ~0ull;  // the next record's load is in flight while this one is decided
+        const Decoded d = decode(a, cur);
+        const uint32_t q = pc.of(d.idx);
+        if (q != pc.q) {
+            if (I >= 0) {  // close the open bucket: memory and the register snapshot
+                Bucket& b = ring[I];
+                b.start = base_ws + (int64_t)r * wl;
+#pragma unroll
+                for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) b.c[ev] = ps.cur[ev];
+#pragma unroll
+                for (int x = 0; x < SM; ++x)
+                    if (x == I) {
+                        rel[x] = r;
+                        pa[x] = ps.cur[SG_EV_PASS];
+                        wa[x] = ps.cur[SG_EV_WAITING];
+                    }
+            }
+            pc.seek(q);
+            const int32_t rn = (int32_t)q;
+            I = first ? (int)((P0 + (int64_t)q) % S) : (I + (rn - r)) % S;
+            r = rn;
+            const int h = (I + 1) % S;
+            ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+            int32_t relI = kRelAbsent;
+#pragma unroll
+            for (int x = 0; x < SM; ++x) {
+                if (x < S) {
+                    const bool v = x != I && rel[x] > r - S;  // LeapArray.isWindowDeprecated, strictly greater
+                    ps.wo_pass += v ? pa[x] : 0;
+                    ps.wo_wait += v ? wa[x] : 0;
+                    if (x == h && v) ps.head_other = pa[x];
+                    if (x == I) relI = rel[x];
+                }
+            }
+            // currentWindow on slot I: continue (only possible at the batch's first period), create or reset
+            const int64_t ws = base_ws + (int64_t)r * wl;
+            int64_t cI[SG_NUM_EVENTS];
+            int64_t stI = relI == kRelAbsent ? INT64_MIN : (relI == kRelOld ? INT64_MIN + 1 : base_ws + (int64_t)relI * wl);
+            if (stI == ws) {
+#pragma unroll
+                for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
+            }
+            open_bucket(ps, stI, cI, ws);
+            first = false;
+        }
+        // ClusterFlowChecker.acquireClusterToken, :67-81
+        const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
+        const double next_remaining = R.thr - latest - (double)d.acq;
+        if (next_remaining >= 0) {
+            ps.cur[SG_EV_PASS] += d.acq;
+            ps.cur[SG_EV_PASS_REQUEST] += 1;
+            if (d.prio) ps.cur[SG_EV_OCCUPIED_PASS] += d.acq;
+            store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+        } else {
+            int32_t wait;
+            const int32_t st = decide_fail(R, a.max_occ_ratio, ps, d.acq, d.prio, &wait);
+            if (st != SG_STATUS_BLOCKED) store_result(a.out, d.idx, st, 0, wait);
+        }
+    }
+    if (I >= 0) {
+        Bucket& b = ring[I];
+        b.start = base_ws + (int64_t)r * wl;
+#pragma unroll
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) b.c[ev] = ps.cur[ev];
+    }
+    Occ o;
+    o.pass = ps.occ_pass;
+    o.pass_req = ps.occ_req;
+    a.occ[k] = o;
+}
+
+// Short-segment walker: each wave takes 64 segments of <= short_max records of one length class and
+// walks one per lane; the classes of longer segments go first. SM > 0: ring snapshot in registers
+// (every flow has sampleCount <= SM); SM == 0: generic walker re-reading the ring.
+template <int SM>
+__global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_periods(a, sbnd, bndp);
+    const int lane = lane_id();
+    uint32_t cnt[kClasses], grp_end[kClasses];
+    uint32_t total = 0;
+#pragma unroll
+    for (int c = kClasses - 1; c >= 0; --c) {  // group order: longest class first
+        cnt[c] = a.short_count[c];
+        total += (cnt[c] + 63) / 64;
+        grp_end[c] = total;
+    }
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t g = wave; g < total; g += nwaves) {
+        int c = kClasses - 1;
+        uint32_t g0 = 0;
+        while (g >= grp_end[c]) {
+            g0 = grp_end[c];
+            --c;
+        }
+        const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
+        if (i >= cnt[c]) continue;
+        const uint64_t t0 = (a.dbg & 64) ? clock64() : 0;
+        const uint64_t s = a.short_list[a.class_off[c] + i];
+        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+        uint32_t opened = 0;
+        uint64_t e = s + 1;
+        if constexpr (SM > 0) {
+            walk_reg<SM>(a, bndp, k, s);
+        } else {
+            const uint64_t lim = s + (uint64_t)min(a.short_max, c < kClasses - 1 ? kClassMax[c] : 0xFFFFFFFFu) + 1;
+            while (e < a.n && e < lim && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
+            opened = walk_serial(a, bndp, k, s, e);
+        }
+        if (a.dbg & 64) {
+            const uint64_t t2 = clock64();
+            const int64_t len = (int64_t)(e - s);
+            const int64_t op = wave_sum((int64_t)opened), rs = wave_sum(len);
+            int64_t mx = len;
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
+            if (lane == __builtin_ctzll(__ballot(1))) {
+                atomicAdd(&a.dbg_ctr[0], 1ull);
+                atomicAdd(&a.dbg_ctr[2], (unsigned long long)(t2 - t0));
+                atomicAdd(&a.dbg_ctr[3], (unsigned long long)op);
+                atomicAdd(&a.dbg_ctr[4], (unsigned long long)rs);
+                atomicAdd(&a.dbg_ctr[5], (unsigned long long)mx);
+                atomicAdd(&a.dbg_ctr[6 + c], (unsigned long long)(t2 - t0));
+            }
+        }
+    }
+}
+
+// One wave per skipped piece: Σ acquire and Σ prioritized acquire over its records, added with 64-bit
+// atomics (pieces of one range share a bucket).
 __global__ void __launch_bounds__(256) k_skip_apply(BatchArgs a) {
-    __shared__ int64_t part[2][256];
     if (*a.err) return;
     const uint32_t cnt = min(*a.skip_count, a.skip_cap);
-    const int tid = threadIdx.x;
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const int lane = lane_id();
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t i = wave; i < cnt; i += nwaves) {
         const uint4 sk = a.skips[i];
         int64_t sa = 0, spa = 0;
-        for (uint64_t j = (uint64_t)sk.z + tid; j < sk.w; j += blockDim.x) {
+        for (uint64_t j = (uint64_t)sk.z + lane; j < sk.w; j += 64) {
             const Decoded d = decode(a, a.rec_sorted[j]);
             sa += d.acq;
             spa += d.prio ? d.acq : 0;
         }
-        part[0][tid] = sa;
-        part[1][tid] = spa;
-        __syncthreads();
-        for (int o = 128; o > 0; o >>= 1) {
-            if (tid < o) {
-                part[0][tid] += part[0][tid + o];
-                part[1][tid] += part[1][tid + o];
-            }
-            __syncthreads();
-        }
-        if (tid == 0) {
+        sa = wave_sum(sa);
+        spa = wave_sum(spa);
+        if (lane == 0) {
             const Rule R = a.rules[sk.x];
             const int64_t P = a.p0[R.wl_idx] + (int64_t)sk.y;
-            Bucket& b = a.ring[(size_t)sk.x * a.stride + (int)(P % R.S)];
-            if (b.start == P * R.wl) {
-                b.c[SG_EV_BLOCK] += part[0][0];
-                b.c[SG_EV_BLOCK_REQUEST] += (int64_t)(sk.w - sk.z);
-                b.c[SG_EV_OCCUPIED_BLOCK] += part[1][0];
+            Bucket& bk = a.ring[(size_t)sk.x * a.stride + (int)(P % R.S)];
+            if (bk.start == P * R.wl) {
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK], (unsigned long long)sa);
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK_REQUEST], (unsigned long long)(sk.w - sk.z));
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_OCCUPIED_BLOCK], (unsigned long long)spa);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -760,21 +1032,48 @@ hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_walk_short, dim3(grid_for(a.n, 256, 16384)), dim3(256), 0, stream, a);
+hipError_t launch_seg(const BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_seg, dim3(grid_for(a.n, kSegTile, 8192)), dim3(kSegThreads), 0, stream, a);
     return hipGetLastError();
 }
 
+static unsigned resident_blocks(const void* kernel, int block) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0);
+    return (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+}
+
+// Persistent walkers: at most as many blocks as fit on the chip at once (each wave loops over its queue).
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
-    // upper bound of long segments = n / (short_max + 1); waves loop over the list
-    const uint64_t max_long = a.n / ((uint64_t)a.short_max + 1) + 1;
-    const unsigned blocks = grid_for(max_long * 64, 256, 2048);
+    static unsigned blocks = 0;
+    if (blocks == 0) blocks = resident_blocks((const void*)k_walk_long, 256);
     hipLaunchKernelGGL(k_walk_long, dim3(blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
+template <int SM>
+static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
+    static unsigned blocks = 0;
+    if (blocks == 0) blocks = resident_blocks((const void*)k_walk_short<SM>, 256);
+    hipLaunchKernelGGL(k_walk_short<SM>, dim3(blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {
+    // the register-snapshot walker for the handle's largest sampleCount (a.stride)
+    if (a.generic_walker) return launch_short_sm<0>(a, stream);
+    if (a.stride <= 2) return launch_short_sm<2>(a, stream);
+    if (a.stride <= 4) return launch_short_sm<4>(a, stream);
+    if (a.stride <= 8) return launch_short_sm<8>(a, stream);
+    if (a.stride <= 10) return launch_short_sm<10>(a, stream);  // ClusterFlowConfig default sampleCount
+    if (a.stride <= 16) return launch_short_sm<16>(a, stream);
+    return launch_short_sm<0>(a, stream);
+}
+
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_skip_apply, dim3(1024), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_skip_apply, dim3(2048), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

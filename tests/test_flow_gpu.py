@@ -14,7 +14,8 @@ from sentinel_amd.workload import ClusterWorkload, zipf_keys
 pytestmark = pytest.mark.gpu
 
 
-WALKERS = [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY]  # default split, every flow serial, every flow by a wave
+# default split, every flow serial, every flow by a wave, short walker re-reading the ring (no register snapshot)
+WALKERS = [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY, abi.FLAG_RING_REREAD]
 
 
 def _engine(max_batch=1 << 20, exceed=1.0, occ_ratio=1.0, flags=0):
