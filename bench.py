@@ -77,6 +77,20 @@ class ShardWorkload:
         return words.view(torch.uint8).reshape(-1)
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_c3_pmc_summary.json")
+
+
+def pmc_traffic():
+    """HBM bytes per step of the decision pipeline's kernels from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this same command (scripts/gpu_round.sh pmc, summarised by scripts/pmc_summary.py;
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None when no summary is committed."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            return float(json.load(f)["pipeline_bytes_per_step"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(n_flows, n_requests, seconds_budget=25.0):
     """The oracle (sequential C restatement, 1 thread) on the same C3 workload: whole 1000 ms batches
     until ~10 s of decide time or the budget is spent."""
@@ -200,7 +214,8 @@ def main():
                    "rollup": "RCCL all_reduce + all_gather per step" if world > 1 else "none (1 GPU)"},
         "roofline": {"bound": "hbm", "kernel": "whole batch pipeline (prep + sort + walk), device time",
                      "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_gbs / HBM_PEAK_GBS,
-                     "traffic": None, "algorithmic_bytes_per_step": b_alg, "touched_flow_ids": touched},
+                     "traffic": pmc_traffic(), "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT),
+                     "algorithmic_bytes_per_step": b_alg, "touched_flow_ids": touched},
         "phases_ms": {"device_total": total_ms, "sort": phase["sort_ms"] / args.steps, "walk": walk_ms,
                       "long_segments": long_segments},
     }
