@@ -206,6 +206,14 @@ typedef struct sg_local_result {
     int32_t wait_ms;
 } sg_local_result;
 
+/* Node-wide statistic settings of the local chain (static properties in the reference). */
+typedef struct sg_local_config {
+    int32_t sample_count;         /* SampleCountProperty.SAMPLE_COUNT, default 2 (1..60)          */
+    int32_t interval_ms;          /* IntervalProperty.INTERVAL, default 1000                      */
+    int32_t occupy_timeout_ms;    /* OccupyTimeoutProperty.occupyTimeout, default 500              */
+    int32_t reserved;
+} sg_local_config;
+
 /* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
 typedef struct sg_batch_stats {
     float    total_ms;          /* whole pipeline                                         */
@@ -256,6 +264,26 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
 int sg_param_decide_batch_host(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass);
 /* State of (rule, value): returns flags (bit0 time counter, bit1 token counter; 0 = absent) or < 0. */
 int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+
+/* ---- local slot chain (the ProcessorSlot chain's statistic / flow / degrade slots, batched) ----
+ *   sg_local_load_rules    ← FlowRuleManager.loadRules + DegradeRuleManager.loadRules for one resource each
+ *                            (one DefaultController QPS/thread rule per resource, limitApp "default",
+ *                            DIRECT strategy; up to two circuit breakers), with fresh StatisticNodes.
+ *   sg_local_decide_batch  ← SphU.entry(resource, count, prioritized) → StatisticSlot.entry around
+ *                            FlowSlot.checkFlow (DefaultController.canPass, DefaultController.java:49-76) and
+ *                            DegradeSlot.performChecking (DegradeSlot.java:43-81); Entry.exit() →
+ *                            StatisticSlot.exit (StatisticSlot.java:124-165) + DegradeSlot.exit →
+ *                            onRequestComplete. Events in (timestamp, arrival) order; exits only for entries
+ *                            that passed (the caller holds no Entry for a blocked one).
+ * Event/result types: sg_local_event / sg_local_result above. */
+int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local_rule* rules, uint32_t n);
+int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, void* stream);
+int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out);
+/* Resource state: second window [S][8] {start, PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS, minRt},
+ * borrow array [S][2] {start, PASS}, minute window [60][8] (start INT64_MIN = never created; counters of
+ * such slots read 0), head[14] = {curThreadNum, then per breaker: state, nextRetry, stat start, slow/error
+ * count, total count, 0}. */
+int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head);
 
 /* Testing aid: copy an internal buffer of the last batch to host memory.
  * what: 0 = records (request order, u64), 1 = records sorted by flowId, 2 = window-period table

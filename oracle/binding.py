@@ -73,6 +73,9 @@ def lib():
         "or_local_thread_num": (i64, [vp, u32]), "or_local_waiting": (i64, [vp, u32, i64]),
         "or_local_breaker_state": (C.c_int, [vp, u32, C.c_int, vp]),
         "or_local_dump": (C.c_int, [vp, u32, vp, vp, vp]),
+        "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
+        "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
+        "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -353,3 +356,40 @@ class LocalChain:
         mnt = np.zeros((60, 8), np.int64)
         assert lib().or_local_dump(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt)) == 0
         return sec, bor, mnt
+
+
+    def breaker_stat(self, res, i):
+        a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+        assert lib().or_local_breaker_stat(self.h, res, i, C.byref(a), C.byref(b), C.byref(c)) == 0
+        return a.value, b.value, c.value
+
+
+class LocalTraceGen:
+    """Client model over a LocalChain (test infrastructure): time-ordered entries with planned response
+    times and business errors; each entry that passes exits at ts + waitInMs + rt (SphU.entry callers
+    only exit entries they obtained). run() returns the merged event stream up to t_end and the oracle's
+    decision for every event; exits due later stay pending for the next call."""
+
+    def __init__(self, chain):
+        self.chain = chain
+        self.h = lib().or_lgen_new(chain.h)
+
+    def __del__(self):
+        if self.h:
+            lib().or_lgen_free(self.h)
+            self.h = None
+
+    def pending(self):
+        return int(lib().or_lgen_pending(self.h))
+
+    def run(self, entries, rt, err, t_end):
+        entries = np.ascontiguousarray(entries, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        rt = np.ascontiguousarray(rt, dtype=np.int32)
+        err = np.ascontiguousarray(err, dtype=np.uint8)
+        cap = 2 * len(entries) + self.pending() + 16
+        out = np.zeros(cap, abi.LOCAL_EVENT_DTYPE)
+        res = np.zeros(cap, abi.LOCAL_RES_DTYPE)
+        k = lib().or_lgen_run(self.h, abi.ptr(entries), abi.ptr(rt), abi.ptr(err), len(entries), int(t_end),
+                              abi.ptr(out), abi.ptr(res), cap)
+        assert k != 2**64 - 1
+        return out[:k].copy(), res[:k].copy()

@@ -871,7 +871,8 @@ static int cb_try_pass(or_breaker* cb, int64_t t, int* half) {
 
 static void cb_to_open(or_breaker* cb, int64_t t) { /* transformToOpen / fromHalfOpenToOpen */
     cb->state = OR_CB_OPEN;
-    cb->next_retry = t + (int64_t)cb->rule.time_window_sec * 1000;
+    /* recoveryTimeoutMs = rule.getTimeWindow() * 1000 is an int (AbstractCircuitBreaker.java:36,54): wraps */
+    cb->next_retry = t + (int64_t)(int32_t)((uint32_t)cb->rule.time_window_sec * 1000u);
 }
 
 /* onRequestComplete at exit time t (ResponseTimeCircuitBreaker.java:63-118, ExceptionCircuitBreaker.java:62-113) */
@@ -1029,5 +1030,137 @@ int or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* bor
     dump_leap(nd->second, second, 1);
     dump_leap(nd->second->borrow, borrow, 0);
     dump_leap(nd->minute, minute, 1);
+    return 0;
+}
+
+/* ===================================================================================== */
+/* Local-chain trace generator (test infrastructure): a client that exits only the entries */
+/* that passed, as SphU.entry callers do (a BlockException means there is no Entry to exit) */
+/* ===================================================================================== */
+
+typedef struct or_pending {
+    int64_t ts, create_ts, seq;
+    uint32_t resource;
+    int32_t count, error;
+} or_pending;
+
+struct or_lgen {
+    or_local* l;
+    or_pending* heap;
+    uint64_t n, cap;
+    int64_t seq;
+};
+
+static int pend_less(const or_pending* a, const or_pending* b) {
+    return a->ts < b->ts || (a->ts == b->ts && a->seq < b->seq);
+}
+
+static void pend_push(or_lgen* g, or_pending p) {
+    if (g->n == g->cap) {
+        g->cap = g->cap ? 2 * g->cap : 1024;
+        g->heap = (or_pending*)realloc(g->heap, g->cap * sizeof(or_pending));
+    }
+    uint64_t i = g->n++;
+    g->heap[i] = p;
+    while (i > 0) {
+        uint64_t par = (i - 1) / 2;
+        if (!pend_less(&g->heap[i], &g->heap[par])) break;
+        or_pending t = g->heap[i];
+        g->heap[i] = g->heap[par];
+        g->heap[par] = t;
+        i = par;
+    }
+}
+
+static or_pending pend_pop(or_lgen* g) {
+    or_pending top = g->heap[0];
+    g->heap[0] = g->heap[--g->n];
+    uint64_t i = 0;
+    for (;;) {
+        uint64_t l = 2 * i + 1, r = l + 1, m = i;
+        if (l < g->n && pend_less(&g->heap[l], &g->heap[m])) m = l;
+        if (r < g->n && pend_less(&g->heap[r], &g->heap[m])) m = r;
+        if (m == i) break;
+        or_pending t = g->heap[i];
+        g->heap[i] = g->heap[m];
+        g->heap[m] = t;
+        i = m;
+    }
+    return top;
+}
+
+or_lgen* or_lgen_new(or_local* l) {
+    or_lgen* g = (or_lgen*)calloc(1, sizeof(or_lgen));
+    g->l = l;
+    return g;
+}
+
+void or_lgen_free(or_lgen* g) {
+    if (!g) return;
+    free(g->heap);
+    free(g);
+}
+
+uint64_t or_lgen_pending(const or_lgen* g) { return g->n; }
+
+/* Merge time-ordered entries with the exits of the passed ones (exit at ts + waitInMs + rt; exits due at
+ * the same ms as an entry go first), replaying every emitted event through the oracle. Events with
+ * ts >= t_end are not emitted (exits stay pending for the next call). Returns the number emitted, or
+ * UINT64_MAX when `cap` is too small. */
+uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
+                     int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap) {
+    uint64_t k = 0, i = 0;
+    for (;;) {
+        int take_exit;
+        if (i < n && g->n) take_exit = g->heap[0].ts <= entries[i].ts_ms;
+        else if (g->n) take_exit = 1;
+        else if (i < n) take_exit = 0;
+        else break;
+        if (take_exit && g->heap[0].ts >= t_end) {
+            if (i >= n) break;
+            take_exit = 0;
+        }
+        if (k == cap) return UINT64_MAX;
+        sg_local_event* e = &out[k];
+        if (take_exit) {
+            or_pending p = pend_pop(g);
+            e->ts_ms = p.ts;
+            e->create_ts = p.create_ts;
+            e->resource = p.resource;
+            e->count = p.count;
+            e->kind = p.error ? SG_LOCAL_EXIT_ERROR : SG_LOCAL_EXIT;
+            e->reserved = 0;
+            or_local_decide(g->l, e, 1, &res[k]);
+            k++;
+            continue;
+        }
+        *e = entries[i];
+        e->kind = SG_LOCAL_ENTRY;
+        e->create_ts = 0;
+        or_local_decide(g->l, e, 1, &res[k]);
+        if (res[k].status == SG_LOCAL_PASS || res[k].status == SG_LOCAL_PASS_WAIT) {
+            or_pending p;
+            p.create_ts = e->ts_ms;
+            p.ts = e->ts_ms + res[k].wait_ms + (rt ? rt[i] : 0);
+            p.seq = g->seq++;
+            p.resource = e->resource & SG_KEY_INDEX;
+            p.count = e->count;
+            p.error = err ? err[i] : 0;
+            pend_push(g, p);
+        }
+        k++;
+        i++;
+    }
+    return k;
+}
+
+/* Breaker i's statistic bucket (LeapArray(1, statIntervalMs)): start (INT64_MIN if never created), slow or
+ * error count, total count. */
+int or_local_breaker_stat(const or_local* l, uint32_t res, int i, int64_t* start, int64_t* bad, int64_t* total) {
+    if (res >= l->n || i < 0 || i >= l->nodes[res].rule.n_breakers) return -1;
+    const or_leap* s = l->nodes[res].cb[i].stat;
+    *start = s->present[0] ? s->b[0].start : INT64_MIN;
+    *bad = s->present[0] ? s->b[0].c[0] : 0;
+    *total = s->present[0] ? s->b[0].c[1] : 0;
     return 0;
 }

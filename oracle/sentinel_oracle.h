@@ -126,6 +126,16 @@ int       or_local_breaker_state(const or_local* l, uint32_t res, int i, int64_t
 /* Raw window dumps for parity: second main ring [S][8] (start, 6 counters, minRt), borrow [S][2], minute [60][8]. */
 int       or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute);
 
+int       or_local_breaker_stat(const or_local* l, uint32_t res, int i, int64_t* start, int64_t* bad, int64_t* total);
+
+/* Trace generator for the local chain (test infrastructure): entries + the exits of the passed ones. */
+typedef struct or_lgen or_lgen;
+or_lgen*  or_lgen_new(or_local* l);
+void      or_lgen_free(or_lgen* g);
+uint64_t  or_lgen_pending(const or_lgen* g);
+uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
+                      int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,11 @@ FLOW_GRADE_THREAD, FLOW_GRADE_QPS, FLOW_GRADE_NONE = 0, 1, -1
 LOCAL_ENTRY, LOCAL_EXIT, LOCAL_EXIT_ERROR = 0, 1, 2
 LOCAL_PASS, LOCAL_BLOCK_FLOW, LOCAL_BLOCK_DEGRADE, LOCAL_PASS_WAIT = 0, 1, 2, 3
 
+class sg_local_config(C.Structure):
+    _fields_ = [("sample_count", C.c_int32), ("interval_ms", C.c_int32), ("occupy_timeout_ms", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
 assert RES_DTYPE.itemsize == C.sizeof(sg_result) == 12
 assert RULE_DTYPE.itemsize == C.sizeof(sg_flow_rule) == 32

@@ -79,6 +79,20 @@ struct sg_handle {
     sg_param_req* d_preq_h = nullptr;
     int32_t* d_pout_h = nullptr;
 
+    // local slot chain
+    sg_local_config lcfg{2, 1000, 500, 0};
+    std::vector<LRule> ltab;
+    LRule* d_lrules = nullptr;
+    LHead* d_lhead = nullptr;
+    LBucket* d_lsec = nullptr;
+    LFuture* d_lbor = nullptr;
+    LBucket* d_lmin = nullptr;
+    int64_t* d_llast_ts = nullptr;
+    int l_n_wl = 0, l_wsec = 0, l_wmin = 0;
+    int32_t l_wl[kMaxWl]{};
+    sg_local_event* d_lev_h = nullptr;
+    sg_local_result* d_lout_h = nullptr;
+
     int kbits = 0, ibits = 0, abits = 0;
     bool stats_on = false;
     uint32_t short_max = kShortMax;   // default walker split (env SG_SHORT_MAX overrides, for tuning)
@@ -126,6 +140,23 @@ double global_threshold(const sg_handle* h, const sg_flow_rule& r) {
         base = r.count * connected;
     }
     return base * h->cfg.exceed_count;
+}
+
+// java.lang.Math.round(double) (JDK 7u+): floor(x + 1/2) computed exactly on the bits; saturating.
+int64_t java_math_round(double a) {
+    int64_t bits;
+    std::memcpy(&bits, &a, 8);
+    const int64_t biased_exp = (bits & 0x7FF0000000000000LL) >> 52;
+    const int64_t shift = (52 - 1 + 1023) - biased_exp;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    if (a != a) return 0;
+    if (a >= 9223372036854775807.0) return INT64_MAX;
+    if (a <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)a;
 }
 
 int layout_records(sg_handle* h) {
@@ -285,6 +316,14 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_preq_h);
     dfree(h->d_pout_h);
     dfree(h->d_skip_count);
+    dfree(h->d_lrules);
+    dfree(h->d_lhead);
+    dfree(h->d_lsec);
+    dfree(h->d_lbor);
+    dfree(h->d_lmin);
+    dfree(h->d_llast_ts);
+    dfree(h->d_lev_h);
+    dfree(h->d_lout_h);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
     if (h->h_err) (void)hipHostFree(h->h_err);
@@ -745,6 +784,233 @@ int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* la
     *last_time = s->time;
     *tokens = s->tokens;
     return (int)s->flags;
+}
+
+// ------------------------------------------------------------------------------ local slot chain
+
+int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local_rule* rules, uint32_t n) {
+    if (!h || !cfg || (!rules && n)) return SG_E_INVAL;
+    if (n >= SG_KEY_BAD) return fail(h, SG_E_INVAL, "too many resources");
+    if (cfg->sample_count <= 0 || cfg->interval_ms <= 0 || cfg->interval_ms % cfg->sample_count != 0)
+        return fail(h, SG_E_INVAL, "invalid statistic window (SAMPLE_COUNT / INTERVAL)");
+    if (cfg->sample_count > kMinuteS) return fail(h, SG_E_UNSUPPORTED, "SAMPLE_COUNT > 60");
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<LRule> tab(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_local_rule& r = rules[i];
+        if (r.flow_grade < -1 || r.flow_grade > 1) return fail(h, SG_E_INVAL, "flow grade");
+        if (r.flow_grade >= 0 && !(r.flow_count >= 0)) return fail(h, SG_E_INVAL, "flow count must be >= 0");
+        if (r.n_breakers < 0 || r.n_breakers > 2) return fail(h, SG_E_INVAL, "at most two degrade rules");
+        LRule& L = tab[i];
+        L.flow_count = r.flow_count;
+        L.flow_grade = r.flow_grade;
+        L.nb = r.n_breakers;
+        for (int j = 0; j < 2; ++j) {
+            LBreakerRule& b = L.b[j];
+            b = LBreakerRule{};
+            b.stat_ms = 1;
+            if (j >= r.n_breakers) continue;
+            const sg_degrade_rule& d = r.breakers[j];
+            if (d.grade < SG_DEGRADE_RT || d.grade > SG_DEGRADE_EXCEPTION_COUNT || d.stat_interval_ms <= 0 ||
+                !(d.count >= 0))
+                return fail(h, SG_E_INVAL, "invalid degrade rule");
+            b.grade = d.grade;
+            b.count = d.count;
+            b.slow_ratio = d.slow_ratio_threshold;
+            b.max_rt = java_math_round(d.count);  // ResponseTimeCircuitBreaker.java:52
+            b.min_request = d.min_request_amount;
+            b.recovery_ms = (int32_t)((uint32_t)d.time_window_sec * 1000u);  // int arithmetic, wraps
+            b.stat_ms = d.stat_interval_ms;
+        }
+    }
+    // window lengths of the period tables: the second window's bucket and the minute window's 1000 ms
+    h->l_n_wl = 0;
+    const int32_t wl2 = cfg->interval_ms / cfg->sample_count;
+    h->l_wl[h->l_n_wl++] = wl2;
+    h->l_wsec = 0;
+    h->l_wmin = (wl2 == kMinuteWl) ? 0 : h->l_n_wl;
+    if (wl2 != kMinuteWl) h->l_wl[h->l_n_wl++] = kMinuteWl;
+
+    dfree(h->d_lrules);
+    dfree(h->d_lhead);
+    dfree(h->d_lsec);
+    dfree(h->d_lbor);
+    dfree(h->d_lmin);
+    if (!h->d_llast_ts && hipMalloc(&h->d_llast_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "ts");
+    const int64_t neg = -1;
+    HIP_TRY(h, hipMemcpy(h->d_llast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
+    h->lcfg = *cfg;
+    h->ltab = tab;
+    if (n) {
+        if (hipMalloc(&h->d_lrules, sizeof(LRule) * n) != hipSuccess || hipMalloc(&h->d_lhead, sizeof(LHead) * n) != hipSuccess ||
+            hipMalloc(&h->d_lsec, sizeof(LBucket) * (size_t)n * cfg->sample_count) != hipSuccess ||
+            hipMalloc(&h->d_lbor, sizeof(LFuture) * (size_t)n * cfg->sample_count) != hipSuccess ||
+            hipMalloc(&h->d_lmin, sizeof(LBucket) * (size_t)n * kMinuteS) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "local state allocation");
+        HIP_TRY(h, hipMemcpy(h->d_lrules, tab.data(), sizeof(LRule) * n, hipMemcpyHostToDevice));
+        LArgs L{};
+        L.K = n;
+        L.S = cfg->sample_count;
+        L.head = h->d_lhead;
+        L.sec = h->d_lsec;
+        L.bor = h->d_lbor;
+        L.minute = h->d_lmin;
+        HIP_TRY(h, launch_local_init(L, 0));
+        HIP_TRY(h, hipDeviceSynchronize());
+    }
+    return SG_OK;
+}
+
+int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const uint32_t K = (uint32_t)h->ltab.size();
+    int kbits = bits_for((uint64_t)K);
+    if (kbits < 1) kbits = 1;
+    const int ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
+    const int abits = 64 - kbits - ibits;
+    if (abits < 4) return fail(h, SG_E_UNSUPPORTED, "resources x max_batch too large for 64-bit records");
+
+    LArgs L{};
+    L.ev = ev;
+    L.out = out;
+    L.n = n;
+    L.rec = h->d_rec;
+    L.rec_sorted = h->d_rec_sorted;
+    L.kshift = 64 - kbits;
+    L.abits = abits;
+    L.imask = (ibits >= 64) ? ~0ull : ((1ull << ibits) - 1);
+    L.amask = (1ull << abits) - 1;
+    L.aesc = (1ull << (abits - 3)) - 1;
+    L.K = K;
+    L.rules = h->d_lrules;
+    L.head = h->d_lhead;
+    L.sec = h->d_lsec;
+    L.bor = h->d_lbor;
+    L.minute = h->d_lmin;
+    L.S = h->lcfg.sample_count;
+    L.wl2 = h->lcfg.interval_ms / h->lcfg.sample_count;
+    L.interval = h->lcfg.interval_ms;
+    L.isec = h->lcfg.interval_ms / 1000.0;
+    L.occupy_timeout = h->lcfg.occupy_timeout_ms;
+    L.wsec = h->l_wsec;
+    L.wmin = h->l_wmin;
+    L.n_wl = h->l_n_wl;
+    std::memcpy(L.wl, h->l_wl, sizeof(L.wl));
+    L.bnd = h->d_bnd;
+    L.p0 = h->d_p0;
+    L.np = h->d_np;
+    L.err = h->d_err;
+    L.last_ts = h->d_llast_ts;
+
+    BatchArgs sgm{};  // segment lists (k_seg)
+    sgm.n = n;
+    sgm.rec_sorted = h->d_rec_sorted;
+    sgm.kshift = L.kshift;
+    sgm.K = K;
+    sgm.err = h->d_err;
+    sgm.long_list = h->d_long_list;
+    sgm.long_count = h->d_long_count;
+    sgm.short_list = h->d_short_list;
+    sgm.short_count = h->d_long_count + 1;
+    for (int c = 0; c < kClasses; ++c) sgm.class_off[c] = h->class_off[c];
+    sgm.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : h->short_max;
+
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_local_prep(L, stream));
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
+    uint64_t* sorted = nullptr;
+    HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, L.kshift, h->d_hist, &sorted, stream));
+    h->last_sorted = sorted;
+    L.rec_sorted = sorted;
+    sgm.rec_sorted = sorted;
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
+    HIP_TRY(h, launch_seg(sgm, stream));
+    HIP_TRY(h, launch_local_walk(L, sgm, h->aux, stream, h->fork, h->join));
+    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (h->stats_on) {
+        HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipEventRecord(h->ev[4], stream));
+    }
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (h->stats_on) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, h->ev[0], h->ev[4]);
+        h->stats.total_ms = ms;
+        (void)hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+        h->stats.sort_ms = ms;
+        (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+        h->stats.walk_ms = ms;
+        h->stats.long_segments = h->h_long[0];
+        h->stats.skipped_ranges = 0;
+    }
+    if (*h->h_err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    return SG_OK;
+}
+
+int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_lev_h) {
+        if (hipMalloc(&h->d_lev_h, sizeof(sg_local_event) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_lout_h, sizeof(sg_local_result) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    HIP_TRY(h, hipMemcpy(h->d_lev_h, ev, sizeof(sg_local_event) * n, hipMemcpyHostToDevice));
+    int rc = sg_local_decide_batch(h, h->d_lev_h, n, h->d_lout_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(out, h->d_lout_h, sizeof(sg_local_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
+    if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    const int S = h->lcfg.sample_count;
+    std::vector<LBucket> sb(S), mb(kMinuteS);
+    std::vector<LFuture> fb(S);
+    LHead hd;
+    HIP_TRY(h, hipMemcpy(sb.data(), h->d_lsec + (size_t)res * S, sizeof(LBucket) * S, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(fb.data(), h->d_lbor + (size_t)res * S, sizeof(LFuture) * S, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(mb.data(), h->d_lmin + (size_t)res * kMinuteS, sizeof(LBucket) * kMinuteS, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(&hd, h->d_lhead + res, sizeof(LHead), hipMemcpyDeviceToHost));
+    auto dump = [](const LBucket& b, int64_t* o) {
+        const bool p = b.start != INT64_MIN;
+        o[0] = b.start;
+        for (int e = 0; e < kLEv; ++e) o[1 + e] = p ? b.c[e] : 0;
+        o[7] = p ? b.min_rt : 0;
+    };
+    for (int j = 0; j < S; ++j) {
+        dump(sb[j], second + 8 * j);
+        borrow[2 * j] = fb[j].start;
+        borrow[2 * j + 1] = fb[j].start != INT64_MIN ? fb[j].pass : 0;
+    }
+    for (int j = 0; j < kMinuteS; ++j) dump(mb[j], minute + 8 * j);
+    head[0] = hd.threads;
+    for (int j = 0; j < 2; ++j) {
+        int64_t* o = head + 1 + 6 * j;
+        o[0] = hd.cb[j].state;
+        o[1] = hd.cb[j].next_retry;
+        o[2] = hd.cb[j].stat_start;
+        o[3] = hd.cb[j].stat_start != INT64_MIN ? hd.cb[j].bad : 0;
+        o[4] = hd.cb[j].stat_start != INT64_MIN ? hd.cb[j].total : 0;
+        o[5] = 0;
+    }
+    head[13] = 0;
+    return SG_OK;
 }
 
 int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {

@@ -168,6 +168,94 @@ hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
 hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
                               uint64_t** sorted_out, hipStream_t stream);
 
+// ---- local slot chain: StatisticSlot → FlowSlot(DefaultController) → DegradeSlot (local.hip) ----
+constexpr int kLEv = 6;             // MetricEvent PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS
+constexpr int kLPass = 0, kLBlock = 1, kLExc = 2, kLSucc = 3, kLRt = 4, kLOccPass = 5;
+constexpr int64_t kStatMaxRt = 5000; // SentinelConfig.statisticMaxRt default (MetricBucket.initMinRt)
+constexpr int kMinuteS = 60;         // StatisticNode.rollingCounterInMinute = ArrayMetric(60, 60000, false)
+constexpr int kMinuteWl = 1000;
+constexpr int kCbClosed = 0, kCbOpen = 1, kCbHalfOpen = 2;
+
+struct alignas(64) LBucket {  // WindowWrap<MetricBucket>: start (INT64_MIN = null slot), 6 counters, minRt
+    int64_t start;
+    int64_t c[kLEv];
+    int64_t min_rt;
+};
+static_assert(sizeof(LBucket) == 64, "LBucket layout");
+
+struct alignas(16) LFuture {  // borrow ring (FutureBucketLeapArray) slot: only PASS is ever added
+    int64_t start;
+    int64_t pass;
+};
+
+struct LBreaker {             // AbstractCircuitBreaker state + its LeapArray(1, statIntervalMs) bucket
+    int64_t next_retry;
+    int64_t stat_start;       // INT64_MIN = bucket never created
+    int64_t bad;              // slowCount / errorCount
+    int64_t total;
+    int32_t state;            // kCb*
+    int32_t pad;
+};
+
+struct alignas(64) LHead {    // per resource: curThreadNum + up to two breakers (128 B)
+    int64_t threads;
+    int64_t pad;
+    LBreaker cb[2];
+    int64_t pad2[2];
+};
+static_assert(sizeof(LHead) == 128, "LHead layout");
+
+struct LBreakerRule {
+    double count;             // RT: maxAllowedRt source; ratio / count threshold
+    double slow_ratio;        // maxSlowRequestRatio (RT)
+    int64_t max_rt;           // Math.round(count) (ResponseTimeCircuitBreaker.java:52)
+    int32_t grade;            // SG_DEGRADE_*
+    int32_t min_request;
+    int32_t recovery_ms;      // timeWindow * 1000, int (AbstractCircuitBreaker.java:54)
+    int32_t stat_ms;          // statIntervalMs
+};
+
+struct alignas(16) LRule {
+    double flow_count;
+    int32_t flow_grade;       // 0 thread, 1 QPS, -1 no flow rule
+    int32_t nb;               // breakers 0..2
+    LBreakerRule b[2];
+};
+
+struct LArgs {
+    const sg_local_event* ev;
+    sg_local_result* out;
+    uint64_t n;
+    uint64_t* rec;            // [res : kbits][idx : ibits][count << 3 | kind << 1 | prio : abits]
+    uint64_t* rec_sorted;
+    int kshift, abits;
+    uint64_t imask, amask, aesc;
+    uint32_t K;
+    const LRule* rules;
+    LHead* head;              // [K]
+    LBucket* sec;             // [K][S]   second window (OccupiableBucketLeapArray)
+    LFuture* bor;             // [K][S]   its borrow array
+    LBucket* minute;          // [K][60]  minute window (BucketLeapArray)
+    int S;                    // SampleCountProperty.SAMPLE_COUNT
+    int32_t wl2;              // INTERVAL / SAMPLE_COUNT
+    int32_t interval;         // IntervalProperty.INTERVAL
+    double isec;              // INTERVAL / 1000.0
+    int32_t occupy_timeout;   // OccupyTimeoutProperty
+    int wsec, wmin;           // period-table indices of the second / minute window lengths
+    int n_wl;
+    int32_t wl[kMaxWl];
+    uint32_t* bnd;
+    int64_t* p0;
+    uint32_t* np;
+    int* err;
+    int64_t* last_ts;
+};
+
+hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
+hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, hipStream_t aux, hipStream_t stream,
+                             hipEvent_t fork, hipEvent_t join);
+hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
+
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.

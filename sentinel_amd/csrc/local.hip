@@ -1,0 +1,864 @@
+// local.hip — gfx950 kernels of the local slot chain for a time-ordered batch of entry/exit events:
+// StatisticSlot (core/slots/statistic/StatisticSlot.java:55-165) around FlowSlot's DefaultController
+// (core/slots/block/flow/controller/DefaultController.java:49-76) and DegradeSlot's circuit breakers
+// (core/slots/block/degrade/DegradeSlot.java:43-81, circuitbreaker/*), over each resource's
+// StatisticNode (core/node/StatisticNode.java): the occupiable second window with its borrow array
+// (OccupiableBucketLeapArray / FutureBucketLeapArray), the 60-bucket minute window and curThreadNum.
+//
+// Pipeline: k_local_prep (records + period tables) → radix sort by resource (sort.hip) → k_seg (segment
+// heads by length class, engine.hip) → k_lwalk_long (one wave per hot resource) beside k_lwalk_short (one
+// lane per resource).
+//
+// Every event of a resource opens the second- and minute-window buckets of its time (passQps / addPass /
+// increaseBlockQps / addRtAndSuccess all call currentWindow first), so both walkers keep the two current
+// buckets in registers and touch the rings in memory only when a window period changes. The rarely used
+// paths (prioritized occupy through the borrow array, thread-grade rules, breaker state changes) run one
+// event at a time ("serial step"); the wave walker decides everything else 64 events at a time.
+#include "engine.h"
+
+namespace sg {
+
+namespace {
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ int32_t java_d2i(double x) {  // JLS §5.1.3
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
+__device__ __forceinline__ double qps_of(int64_t sum, double isec) {
+    return isec == 1.0 ? (double)sum : (double)sum / isec;
+}
+
+__device__ __forceinline__ int64_t wave_sum(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((long long)v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ int64_t wave_min(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up((long long)v, (unsigned)o, 64);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int64_t bcast64(int64_t v, int src) { return __shfl((long long)v, src, 64); }
+__device__ __forceinline__ int bcast32(int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ uint64_t below(int f) { return f >= 64 ? ~0ull : ((1ull << f) - 1ull); }
+
+__device__ __forceinline__ uint32_t period_of(const uint32_t* bnd, uint32_t np, uint32_t idx) {
+    uint32_t lo = 0, hi = np;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bnd[mid] <= idx) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct Cursor {  // window period of monotonically increasing request indices (see PeriodCursor)
+    const uint32_t* bnd;
+    uint32_t np, q, next_b;
+    __device__ __forceinline__ void seek(uint32_t qq) {
+        q = qq;
+        next_b = (qq + 1 < np) ? bnd[qq + 1] : 0xFFFFFFFFu;
+    }
+    __device__ __forceinline__ uint32_t of(uint32_t idx) const {
+        if (q != 0xFFFFFFFFu && idx < next_b) return q;
+        return period_of(bnd, np, idx);
+    }
+};
+
+struct LEvent {  // one decoded event
+    uint32_t idx;
+    int32_t count;
+    int kind;    // SG_LOCAL_ENTRY / EXIT / EXIT_ERROR
+    bool prio;
+};
+
+__device__ __forceinline__ LEvent ldecode(const LArgs& a, uint64_t rec) {
+    LEvent e;
+    e.idx = (uint32_t)((rec >> a.abits) & a.imask);
+    const uint64_t ac = rec & a.amask;
+    e.prio = (ac & 1ull) != 0;
+    e.kind = (int)((ac >> 1) & 3ull);
+    const uint64_t c = ac >> 3;
+    e.count = (c == a.aesc) ? a.ev[e.idx].count : (int32_t)c;
+    return e;
+}
+
+__device__ __forceinline__ void lstore(const LArgs& a, uint32_t idx, int32_t st, int32_t wait) {
+    sg_local_result r;
+    r.status = st;
+    r.wait_ms = wait;
+    a.out[idx] = r;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------ prep
+
+__global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
+    const uint64_t n = a.n;
+    const int64_t t0 = a.ev[0].ts_ms;
+    const uint64_t sentinel = (uint64_t)a.K << a.kshift;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_local_event e = a.ev[i];
+        const int64_t t = e.ts_ms;
+        if (i == 0) {
+            if (t < 0 || t < *a.last_ts) atomicOr(a.err, kErrTime);
+            for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
+        } else {
+            const int64_t tp = a.ev[i - 1].ts_ms;
+            if (t < tp || t < 0) {
+                atomicOr(a.err, kErrTime);
+            } else {
+                for (int w = 0; w < a.n_wl; ++w) {
+                    const int64_t wl = a.wl[w];
+                    const int64_t P0 = t0 / wl, Pp = tp / wl, Pi = t / wl;
+                    for (int64_t p = Pp + 1; p <= Pi; ++p) {
+                        const int64_t q = p - P0;
+                        if (q >= (int64_t)kMaxPeriods) {
+                            atomicOr(a.err, kErrPeriods);
+                            break;
+                        }
+                        a.bnd[(size_t)w * kMaxPeriods + q] = (uint32_t)i;
+                    }
+                }
+            }
+        }
+        if (i == n - 1) {
+            for (int w = 0; w < a.n_wl; ++w) {
+                const int64_t q = t / a.wl[w] - t0 / a.wl[w] + 1;
+                a.np[w] = q > (int64_t)kMaxPeriods ? kMaxPeriods : (uint32_t)q;
+            }
+        }
+        const uint32_t res = e.resource & SG_KEY_INDEX;
+        uint64_t rec = sentinel;
+        if (res < a.K) {
+            uint64_t c = (e.count < 0) ? a.aesc : (uint64_t)(uint32_t)e.count;
+            if (c > a.aesc) c = a.aesc;
+            // kind: 0 entry, 2 exit after a business error, anything else a plain exit
+            const uint64_t kind = e.kind == SG_LOCAL_ENTRY ? 0 : (e.kind == SG_LOCAL_EXIT_ERROR ? 2 : 1);
+            const uint64_t ac = (c << 3) | (kind << 1) | (uint64_t)(e.resource >> 31);
+            rec = ((uint64_t)res << a.kshift) | ((uint64_t)i << a.abits) | ac;
+        }
+        lstore(a, (uint32_t)i, SG_LOCAL_PASS, 0);  // walkers write only other results
+        a.rec[i] = rec;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_local_init(LArgs a) {
+    const uint64_t total = (uint64_t)a.K * kMinuteS;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        LBucket b;
+        b.start = INT64_MIN;
+        for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+        b.min_rt = kStatMaxRt;
+        a.minute[i] = b;
+        const uint64_t k = i / kMinuteS;
+        const int q = (int)(i % kMinuteS);
+        if (q < a.S) {
+            a.sec[k * a.S + q] = b;
+            LFuture f;
+            f.start = INT64_MIN;
+            f.pass = 0;
+            a.bor[k * a.S + q] = f;
+        }
+        if (q == 0) {
+            LHead h;
+            h.threads = 0;
+            h.pad = 0;
+            for (int j = 0; j < 2; ++j) {
+                h.cb[j].next_retry = 0;
+                h.cb[j].stat_start = INT64_MIN;
+                h.cb[j].bad = h.cb[j].total = 0;
+                h.cb[j].state = kCbClosed;
+                h.cb[j].pad = 0;
+            }
+            h.pad2[0] = h.pad2[1] = 0;
+            a.head[k] = h;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------- per-resource state
+
+// The state of one resource during a walk. In the wave walker every field is wave-uniform and every lane
+// executes the serial step identically (stores from all lanes carry the same value).
+struct LNode {
+    const LArgs& a;
+    LRule R;
+    uint32_t k;
+    LBucket* sec;
+    LFuture* bor;
+    LBucket* mnt;
+    Cursor cs, cm;     // second / minute window periods
+    int64_t P0s, P0m;
+    // open second-window bucket
+    int64_t sc[kLEv], s_min, s_ws, s_wo;  // s_wo: Σ PASS of the other valid buckets
+    int sI;
+    // open minute-window bucket
+    int64_t mc[kLEv], m_min, m_ws;
+    int mI;
+    int64_t threads;
+    LBreaker cb[2];
+
+    __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), R(a_.rules[k_]), k(k_) {
+        sec = a.sec + (size_t)k * a.S;
+        bor = a.bor + (size_t)k * a.S;
+        mnt = a.minute + (size_t)k * kMinuteS;
+        cs = Cursor{bndp[a.wsec], a.np[a.wsec], 0xFFFFFFFFu, 0};
+        cm = Cursor{bndp[a.wmin], a.np[a.wmin], 0xFFFFFFFFu, 0};
+        P0s = a.p0[a.wsec];
+        P0m = a.p0[a.wmin];
+        sI = mI = -1;
+        s_ws = m_ws = 0;
+        s_wo = 0;
+        s_min = m_min = kStatMaxRt;
+        for (int e = 0; e < kLEv; ++e) sc[e] = mc[e] = 0;
+        const LHead h = a.head[k];
+        threads = h.threads;
+        cb[0] = h.cb[0];
+        cb[1] = h.cb[1];
+    }
+
+    // -------- second window (OccupiableBucketLeapArray) --------
+    __device__ void sec_close() {
+        if (sI < 0) return;
+        LBucket b;
+        b.start = s_ws;
+        for (int e = 0; e < kLEv; ++e) b.c[e] = sc[e];
+        b.min_rt = s_min;
+        sec[sI] = b;
+    }
+
+    // currentWindow(t) for the period q (LeapArray.java:116-202; newEmptyBucket / resetWindowTo of
+    // OccupiableBucketLeapArray.java:40-63 read the borrow bucket of the same window), then the PASS sum
+    // of the other valid buckets (values(t): valid iff start >= windowStart - (S-1)*windowLength).
+    __device__ void sec_open(uint32_t q) {
+        sec_close();
+        cs.seek(q);
+        const int S = a.S;
+        const int64_t P = P0s + (int64_t)q;
+        const int I = (int)(P % S);
+        const int64_t ws = P * a.wl2;
+        const LBucket old = sec[I];
+        const LFuture fb = bor[I];
+        const bool borrow = fb.start == ws;  // borrowArray.getWindowValue(t): same window
+        if (old.start == ws) {
+            for (int e = 0; e < kLEv; ++e) sc[e] = old.c[e];
+            s_min = old.min_rt;
+        } else {
+            for (int e = 0; e < kLEv; ++e) sc[e] = 0;
+            s_min = kStatMaxRt;
+            if (borrow) {
+                if (old.start == INT64_MIN) sc[kLPass] = fb.pass;  // new bucket: reset(borrowBucket) copies it
+                else sc[kLPass] += (int64_t)(int32_t)fb.pass;      // reset: addPass((int) borrowBucket.pass())
+            }
+        }
+        sI = I;
+        s_ws = ws;
+        const int64_t lo = ws - (int64_t)(S - 1) * a.wl2;
+        int64_t wo = 0;
+        for (int j = 0; j < S; ++j) {
+            if (j == I) continue;
+            const int64_t st = sec[j].start;
+            if (st != INT64_MIN && st >= lo) wo += sec[j].c[kLPass];
+        }
+        s_wo = wo;
+    }
+
+    // -------- minute window (BucketLeapArray, 60 x 1000 ms) --------
+    __device__ void min_close() {
+        if (mI < 0) return;
+        LBucket b;
+        b.start = m_ws;
+        for (int e = 0; e < kLEv; ++e) b.c[e] = mc[e];
+        b.min_rt = m_min;
+        mnt[mI] = b;
+    }
+
+    __device__ void min_open(uint32_t q) {
+        min_close();
+        cm.seek(q);
+        const int64_t P = P0m + (int64_t)q;
+        const int I = (int)(P % kMinuteS);
+        const int64_t ws = P * kMinuteWl;
+        const LBucket old = mnt[I];
+        if (old.start == ws) {
+            for (int e = 0; e < kLEv; ++e) mc[e] = old.c[e];
+            m_min = old.min_rt;
+        } else {
+            for (int e = 0; e < kLEv; ++e) mc[e] = 0;
+            m_min = kStatMaxRt;
+        }
+        mI = I;
+        m_ws = ws;
+    }
+
+    __device__ __forceinline__ void at(uint32_t qs, uint32_t qm) {
+        if (qs != cs.q) sec_open(qs);
+        if (qm != cm.q) min_open(qm);
+    }
+
+    __device__ __forceinline__ double pass_qps() const { return qps_of(s_wo + sc[kLPass], a.isec); }
+
+    // -------- borrow array (FutureBucketLeapArray; memory only, prioritized path) --------
+    __device__ int bor_window(int64_t t) {  // currentWindow(t): slot, or -2 for a detached bucket
+        const int S = a.S;
+        const int idx = (int)((t / a.wl2) % S);
+        const int64_t ws = t - t % a.wl2;
+        const int64_t st = bor[idx].start;
+        if (st == INT64_MIN || ws > st) {
+            LFuture f;
+            f.start = ws;
+            f.pass = 0;
+            bor[idx] = f;
+            return idx;
+        }
+        return ws == st ? idx : -2;
+    }
+    // OccupiableBucketLeapArray.currentWaiting (:66-75): future buckets only (deprecated iff t >= start)
+    __device__ int64_t waiting(int64_t t) {
+        bor_window(t);
+        int64_t w = 0;
+        for (int j = 0; j < a.S; ++j) {
+            const LFuture f = bor[j];
+            if (f.start != INT64_MIN && t < f.start) w += f.pass;
+        }
+        return w;
+    }
+    // ArrayMetric.getWindowPass(t) = data.getWindowValue(t).pass(): the second-window bucket holding t
+    __device__ int64_t window_pass(int64_t t) {
+        if (t < 0) return 0;
+        const int idx = (int)((t / a.wl2) % a.S);
+        if (idx == sI) return (s_ws <= t && t < s_ws + a.wl2) ? sc[kLPass] : 0;  // the open bucket
+        const LBucket b = sec[idx];
+        if (b.start == INT64_MIN || !(b.start <= t && t < b.start + a.wl2)) return 0;
+        return b.c[kLPass];
+    }
+    // StatisticNode.tryOccupyNext, StatisticNode.java:288-320
+    __device__ int64_t try_occupy_next(int64_t now, int32_t acquire, double threshold) {
+        const double max_count = threshold * a.interval / 1000;
+        const int64_t borrow = waiting(now);
+        if ((double)borrow >= max_count) return a.occupy_timeout;
+        const int32_t wlen = a.interval / a.S;
+        int64_t earliest = now - now % wlen + wlen - a.interval;
+        int32_t idx = 0;
+        int64_t current_pass = s_wo + sc[kLPass];  // pass(): the open period's window sum
+        while (earliest < now) {
+            const int64_t wait = (int64_t)(int32_t)((uint32_t)idx * (uint32_t)wlen) + wlen - now % wlen;
+            if (wait >= a.occupy_timeout) break;
+            const int64_t wp = window_pass(earliest);
+            if ((double)(current_pass + borrow + (int64_t)acquire - wp) <= max_count) return wait;
+            earliest += wlen;
+            current_pass -= wp;
+            ++idx;
+        }
+        return a.occupy_timeout;
+    }
+
+    // -------- circuit breakers --------
+    __device__ void cb_to_open(int j, int64_t t) {
+        cb[j].state = kCbOpen;
+        cb[j].next_retry = t + (int64_t)R.b[j].recovery_ms;
+    }
+    __device__ __forceinline__ void cb_stat_window(int j, int64_t t) {  // LeapArray(1, statIntervalMs).currentWindow
+        const int64_t ws = t - t % R.b[j].stat_ms;
+        if (cb[j].stat_start == INT64_MIN || ws > cb[j].stat_start) {
+            cb[j].stat_start = ws;
+            cb[j].bad = cb[j].total = 0;
+        }
+    }
+    __device__ __forceinline__ bool cb_bad(int j, int64_t rt, bool error) const {
+        return R.b[j].grade == SG_DEGRADE_RT ? rt > R.b[j].max_rt : error;
+    }
+    // CLOSED: would the counts (bad, total) open the breaker? (ResponseTimeCircuitBreaker.java:101-118,
+    // ExceptionCircuitBreaker.java:88-108)
+    __device__ __forceinline__ bool cb_trips(int j, int64_t bad, int64_t total) const {
+        if (total < R.b[j].min_request) return false;
+        if (R.b[j].grade == SG_DEGRADE_RT) {
+            const double ratio = bad * 1.0 / total;
+            return ratio > R.b[j].slow_ratio || (ratio == R.b[j].slow_ratio && R.b[j].slow_ratio == 1.0);
+        }
+        const double cur = R.b[j].grade == SG_DEGRADE_EXCEPTION_RATIO ? bad * 1.0 / total : (double)bad;
+        return cur > R.b[j].count;
+    }
+    // onRequestComplete at exit time t
+    __device__ void cb_complete(int j, int64_t t, int64_t rt, bool error) {
+        cb_stat_window(j, t);
+        const bool bad = cb_bad(j, rt, error);
+        cb[j].bad += bad ? 1 : 0;
+        cb[j].total += 1;
+        if (cb[j].state == kCbOpen) return;
+        if (cb[j].state == kCbHalfOpen) {
+            if (bad) {
+                cb_to_open(j, t);
+            } else {  // fromHalfOpenToClose → resetStat(): currentWindow().value().reset()
+                cb[j].state = kCbClosed;
+                cb[j].bad = cb[j].total = 0;
+            }
+            return;
+        }
+        if (cb_trips(j, cb[j].bad, cb[j].total)) cb_to_open(j, t);
+    }
+
+    // -------- one event, sequentially (the oracle's or_local_decide step) --------
+    // Entry: FlowSlot (DefaultController.canPass) → DegradeSlot.performChecking → StatisticSlot.
+    __device__ void entry(const LEvent& e, int64_t t) {
+        int32_t status = SG_LOCAL_PASS;
+        int64_t wait = 0;
+        if (R.flow_grade >= 0) {
+            const int32_t cur = R.flow_grade == 0 ? (int32_t)threads : java_d2i(pass_qps());
+            const int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)e.count);  // int + int wraps
+            if ((double)sum > R.flow_count) {
+                status = SG_LOCAL_BLOCK_FLOW;
+                if (e.prio && R.flow_grade == 1) {
+                    wait = try_occupy_next(t, e.count, R.flow_count);
+                    if (wait < a.occupy_timeout) {
+                        const int s = bor_window(t + wait);  // addWaitingRequest
+                        if (s >= 0) bor[s].pass += e.count;
+                        mc[kLOccPass] += e.count;  // addOccupiedPass: minute window (StatisticNode.java:333-336)
+                        mc[kLPass] += e.count;
+                        status = SG_LOCAL_PASS_WAIT;
+                    }
+                }
+            }
+        }
+        if (status == SG_LOCAL_PASS) {
+            bool half[2] = {false, false};
+            for (int j = 0; j < R.nb; ++j) {  // AbstractCircuitBreaker.tryPass (:73-84)
+                bool ok;
+                if (cb[j].state == kCbClosed) {
+                    ok = true;
+                } else if (cb[j].state == kCbOpen && t >= cb[j].next_retry) {
+                    cb[j].state = kCbHalfOpen;
+                    half[j] = true;
+                    ok = true;
+                } else {
+                    ok = false;
+                }
+                if (!ok) {
+                    status = SG_LOCAL_BLOCK_DEGRADE;
+                    break;
+                }
+            }
+            if (status == SG_LOCAL_BLOCK_DEGRADE)  // whenTerminate of a blocked probe: back to OPEN
+                for (int j = 0; j < 2; ++j)
+                    if (half[j] && cb[j].state == kCbHalfOpen) cb[j].state = kCbOpen;
+        }
+        if (status == SG_LOCAL_PASS) {
+            threads += 1;
+            sc[kLPass] += e.count;
+            mc[kLPass] += e.count;
+        } else if (status == SG_LOCAL_PASS_WAIT) {
+            threads += 1;
+        } else {
+            sc[kLBlock] += e.count;
+            mc[kLBlock] += e.count;
+        }
+        if (status != SG_LOCAL_PASS) lstore(a, e.idx, status, status == SG_LOCAL_PASS_WAIT ? (int32_t)wait : 0);
+    }
+
+    // Exit: StatisticSlot.exit (addRtAndSuccess, decreaseThreadNum, increaseExceptionQps) → DegradeSlot.exit.
+    __device__ void exit(const LEvent& e, int64_t t, int64_t create) {
+        const int64_t rt = t - create;
+        const bool error = e.kind == SG_LOCAL_EXIT_ERROR;
+        sc[kLSucc] += e.count;
+        sc[kLRt] += rt;
+        if (rt < s_min) s_min = rt;
+        mc[kLSucc] += e.count;
+        mc[kLRt] += rt;
+        if (rt < m_min) m_min = rt;
+        threads -= 1;
+        if (error) {
+            sc[kLExc] += e.count;
+            mc[kLExc] += e.count;
+        }
+        for (int j = 0; j < R.nb; ++j) cb_complete(j, t, rt, error);
+    }
+
+    __device__ void step(const LEvent& e, int64_t t, int64_t create) {
+        at(cs.of(e.idx), cm.of(e.idx));
+        if (e.kind == SG_LOCAL_ENTRY) entry(e, t);
+        else exit(e, t, create);
+    }
+
+    __device__ void finish() {
+        sec_close();
+        min_close();
+        LHead h;
+        h.threads = threads;
+        h.pad = 0;
+        h.cb[0] = cb[0];
+        h.cb[1] = cb[1];
+        h.pad2[0] = h.pad2[1] = 0;
+        a.head[k] = h;
+    }
+};
+
+// ------------------------------------------------------------------------------ short walker
+
+__device__ __forceinline__ void stage_lperiods(const LArgs& a, uint32_t* sbnd, const uint32_t** bndp) {
+    uint32_t tot = 0;
+    for (int w = 0; w < a.n_wl; ++w) tot += a.np[w];
+    const bool lds = tot <= (uint32_t)kLdsBnd;
+    uint32_t off = 0;
+    for (int w = 0; w < a.n_wl; ++w) {
+        const uint32_t npw = a.np[w];
+        const uint32_t* g = a.bnd + (size_t)w * kMaxPeriods;
+        if (lds) {
+            for (uint32_t i = threadIdx.x; i < npw; i += blockDim.x) sbnd[off + i] = g[i];
+            if (threadIdx.x == 0) bndp[w] = sbnd + off;
+        } else if (threadIdx.x == 0) {
+            bndp[w] = g;
+        }
+        off += npw;
+    }
+    __syncthreads();
+}
+
+// One lane per resource segment: the serial step for every event.
+__global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_lperiods(a, sbnd, bndp);
+    const int lane = lane_id();
+    uint32_t cnt[kClasses], grp_end[kClasses];
+    uint32_t total = 0;
+    for (int c = kClasses - 1; c >= 0; --c) {
+        cnt[c] = sg.short_count[c];
+        total += (cnt[c] + 63) / 64;
+        grp_end[c] = total;
+    }
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t g = wave; g < total; g += nwaves) {
+        int c = kClasses - 1;
+        uint32_t g0 = 0;
+        while (g >= grp_end[c]) {
+            g0 = grp_end[c];
+            --c;
+        }
+        const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
+        if (i >= cnt[c]) continue;
+        uint64_t j = sg.short_list[sg.class_off[c] + i];
+        const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+        LNode nd(a, bndp, k);
+        uint64_t nxt = a.rec_sorted[j];
+        for (;;) {
+            const uint64_t cur = nxt;
+            if ((uint32_t)(cur >> a.kshift) != k) break;
+            ++j;
+            nxt = j < a.n ? a.rec_sorted[j] : ~0ull;
+            const LEvent e = ldecode(a, cur);
+            const sg_local_event ev = a.ev[e.idx];
+            nd.step(e, ev.ts_ms, ev.create_ts);
+        }
+        nd.finish();
+    }
+}
+
+// ------------------------------------------------------------------------------- wave walker
+
+// One wave per hot resource. Events come 64 at a time (lane = event); a chunk is cut into runs of equal
+// second/minute window periods and breaker statistic windows, and each run into epochs that end at the
+// next event needing the serial step:
+//   - an entry whose flow check fails and that is prioritized (occupy path), or any entry of a
+//     thread-grade rule;
+//   - an entry that passes the flow check while a breaker is OPEN with its retry time reached (→ HALF_OPEN);
+//   - an exit that would open a CLOSED breaker, or the first exit while a breaker is HALF_OPEN.
+// Inside an epoch the breakers are fixed, so entries are decided by the flow rule alone (greedy admit by a
+// wave prefix scan, then "fits on its own" for the rest, exactly like ClusterFlowChecker's walker) or are
+// all blocked (a breaker rejects whatever passes the flow check), and exits only accumulate.
+__device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e_end) {
+    const int lane = lane_id();
+    LNode nd(a, bndp, k);
+    const int nb = nd.R.nb;
+    const bool thread_grade = nd.R.flow_grade == 0;
+    for (uint64_t base = s; base < e_end; base += 64) {
+        const uint64_t j = base + lane;
+        const bool act = j < e_end;
+        LEvent ev;
+        ev.idx = 0;
+        ev.count = 0;
+        ev.kind = -1;
+        ev.prio = false;
+        int64_t t = 0, create = 0;
+        uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
+        int64_t sw0 = 0, sw1 = 0;  // breaker statistic windows of this event (exits)
+        if (act) {
+            ev = ldecode(a, a.rec_sorted[j]);
+            const sg_local_event le = a.ev[ev.idx];
+            t = le.ts_ms;
+            create = le.create_ts;
+            qs = nd.cs.of(ev.idx);
+            qm = nd.cm.of(ev.idx);
+            if (nb > 0) sw0 = t - t % nd.R.b[0].stat_ms;
+            if (nb > 1) sw1 = t - t % nd.R.b[1].stat_ms;
+        }
+        const int nact = (int)__popcll(__ballot(act));
+        const bool is_entry = act && ev.kind == SG_LOCAL_ENTRY;
+        const bool is_exit = act && ev.kind != SG_LOCAL_ENTRY;
+        const int64_t rt = t - create;
+        int pos = 0;
+        while (pos < nact) {
+            // run: lanes [pos, rend) with the same windows as lane pos
+            const uint32_t qs0 = (uint32_t)bcast32((int)qs, pos), qm0 = (uint32_t)bcast32((int)qm, pos);
+            const int64_t a0 = bcast64(sw0, pos), a1 = bcast64(sw1, pos);
+            const uint64_t diff = __ballot(act && lane > pos && (qs != qs0 || qm != qm0 || sw0 != a0 || sw1 != a1));
+            const int rend = diff ? __builtin_ctzll(diff) : nact;
+            nd.at(qs0, qm0);
+            int p = pos;
+            while (p < rend) {
+                const bool in = lane >= p && lane < rend;
+                // ---- the breakers' fixed verdict for entries passing the flow check in this epoch
+                // the first breaker (in order) that is not CLOSED decides: HALF_OPEN rejects, OPEN rejects
+                // before its retry time and lets a probe through after it
+                bool all_closed = true;
+                int64_t retry = INT64_MAX;
+                for (int x = 0; x < nb; ++x) {
+                    if (nd.cb[x].state == kCbClosed) continue;
+                    all_closed = false;
+                    if (nd.cb[x].state == kCbOpen) retry = nd.cb[x].next_retry;
+                    break;
+                }
+                // ---- first lane needing the serial step (epoch end), from everything that does not
+                // depend on this epoch's entry decisions
+                uint64_t special = 0;
+                if (thread_grade) special |= __ballot(in && is_entry);
+                // exits: would a CLOSED breaker open here? first exit while HALF_OPEN.
+                for (int x = 0; x < nb; ++x) {
+                    if (nd.cb[x].state == kCbOpen) continue;
+                    const bool ex = in && is_exit;
+                    if (nd.cb[x].state == kCbHalfOpen) {
+                        special |= __ballot(ex);
+                        continue;
+                    }
+                    const int64_t swx = x == 0 ? a0 : a1;  // the run's statistic window for breaker x
+                    const bool fresh = nd.cb[x].stat_start == INT64_MIN || swx > nd.cb[x].stat_start;
+                    const int64_t b0 = fresh ? 0 : nd.cb[x].bad, t0 = fresh ? 0 : nd.cb[x].total;
+                    const bool bad = ex && nd.cb_bad(x, rt, ev.kind == SG_LOCAL_EXIT_ERROR);
+                    const int64_t pb = wave_incl_scan(bad ? 1 : 0, lane), pt = wave_incl_scan(ex ? 1 : 0, lane);
+                    special |= __ballot(ex && nd.cb_trips(x, b0 + pb, t0 + pt));
+                }
+                // entries: flow decisions. The window sum moves only through passes of this epoch.
+                const double thr = nd.R.flow_count;
+                const bool flow_rule = nd.R.flow_grade == 1;
+                uint64_t pass_m = 0, blk_flow = 0, blk_deg = 0;
+                const uint64_t entries = __ballot(in && is_entry);
+                uint64_t todo = entries & ~below(p);
+                int E = special ? __builtin_ctzll(special) : rend;
+                todo &= below(E);
+                if (!all_closed) {
+                    // fixed window: an entry passes the flow check iff it fits on its own
+                    const int32_t cur = java_d2i(nd.pass_qps());
+                    const bool fits = !flow_rule || !((double)(int32_t)((uint32_t)cur + (uint32_t)ev.count) > thr);
+                    const uint64_t fm = __ballot(fits) & todo;
+                    // a flow-passing entry at or after the retry time is a probe (serial); a prioritized
+                    // flow failure may occupy (serial)
+                    const uint64_t sp = (__ballot(fits && t >= retry) | (__ballot(!fits && ev.prio && flow_rule))) & todo;
+                    if (sp) {
+                        E = __builtin_ctzll(sp);
+                        todo &= below(E);
+                    }
+                    blk_deg = fm & todo;
+                    blk_flow = todo & ~fm;
+                } else if (!flow_rule) {
+                    pass_m = todo;  // no flow rule (or none that counts QPS): every entry passes
+                } else {
+                    // greedy admit (DefaultController.canPass with a window that grows by the passes)
+                    uint64_t pending = todo;
+                    int64_t W = nd.s_wo + nd.sc[kLPass];
+                    int guard = 0;
+                    while (pending) {
+                        if (++guard > 130) {
+                            atomicOr(a.err, kErrInternal);
+                            break;
+                        }
+                        const bool pl = (pending >> lane) & 1ull;
+                        const int64_t av = pl ? (int64_t)ev.count : 0;
+                        const int64_t ex = wave_incl_scan(av, lane) - av;
+                        const int32_t cur = java_d2i(qps_of(W + ex, a.isec));
+                        const bool ok = !((double)(int32_t)((uint32_t)cur + (uint32_t)ev.count) > thr);
+                        const uint64_t fails = __ballot(pl && !ok);
+                        const uint64_t adm = fails ? (pending & below(__builtin_ctzll(fails))) : pending;
+                        pass_m |= adm;
+                        W += wave_sum(((adm >> lane) & 1ull) ? (int64_t)ev.count : 0);
+                        if (!fails) break;
+                        const int f = __builtin_ctzll(fails);
+                        const bool fprio = bcast32((int)ev.prio, f) != 0;
+                        if (fprio) {  // a prioritized failure may occupy: serial step
+                            E = f;
+                            break;
+                        }
+                        blk_flow |= 1ull << f;
+                        pending &= ~below(f + 1);
+                        // skip mode: the window is fixed until the next entry that fits on its own
+                        const int32_t curw = java_d2i(qps_of(W, a.isec));
+                        const bool fit = pl && !((double)(int32_t)((uint32_t)curw + (uint32_t)ev.count) > thr);
+                        const uint64_t stop = (__ballot(fit) | __ballot(pl && ev.prio)) & pending;
+                        const uint64_t blk = stop ? (pending & below(__builtin_ctzll(stop))) : pending;
+                        blk_flow |= blk;
+                        pending &= ~blk;
+                    }
+                    todo &= below(E);
+                    pass_m &= todo;
+                    blk_flow &= todo;
+                }
+                // ---- apply lanes [p, E): entries by their verdict, exits accumulate
+                const uint64_t ex_m = __ballot(in && is_exit) & below(E) & ~below(p);
+                const bool mp = (pass_m >> lane) & 1ull, mf = (blk_flow >> lane) & 1ull, md = (blk_deg >> lane) & 1ull;
+                const bool mx = (ex_m >> lane) & 1ull;
+                if (mf) lstore(a, ev.idx, SG_LOCAL_BLOCK_FLOW, 0);
+                if (md) lstore(a, ev.idx, SG_LOCAL_BLOCK_DEGRADE, 0);
+                const int64_t c = ev.count;
+                const int64_t passed = wave_sum(mp ? c : 0), blocked = wave_sum((mf || md) ? c : 0);
+                const int64_t succ = wave_sum(mx ? c : 0), rts = wave_sum(mx ? rt : 0);
+                const int64_t excs = wave_sum((mx && ev.kind == SG_LOCAL_EXIT_ERROR) ? c : 0);
+                const int64_t rmin = wave_min(mx ? rt : INT64_MAX);
+                nd.sc[kLPass] += passed;
+                nd.mc[kLPass] += passed;
+                nd.sc[kLBlock] += blocked;
+                nd.mc[kLBlock] += blocked;
+                nd.sc[kLSucc] += succ;
+                nd.mc[kLSucc] += succ;
+                nd.sc[kLRt] += rts;
+                nd.mc[kLRt] += rts;
+                nd.sc[kLExc] += excs;
+                nd.mc[kLExc] += excs;
+                if (rmin < nd.s_min) nd.s_min = rmin;
+                if (rmin < nd.m_min) nd.m_min = rmin;
+                nd.threads += (int64_t)__popcll(pass_m) - (int64_t)__popcll(ex_m);
+                for (int x = 0; x < nb; ++x) {  // breaker statistics of the exits (no state change by construction)
+                    if (!ex_m) break;
+                    const int64_t swx = x == 0 ? a0 : a1;
+                    nd.cb_stat_window(x, swx);
+                    nd.cb[x].bad += wave_sum((mx && nd.cb_bad(x, rt, ev.kind == SG_LOCAL_EXIT_ERROR)) ? 1 : 0);
+                    nd.cb[x].total += (int64_t)__popcll(ex_m);
+                }
+                if (E >= rend) break;
+                // ---- lane E: the serial step
+                {
+                    LEvent es;
+                    es.idx = (uint32_t)bcast32((int)ev.idx, E);
+                    es.count = bcast32(ev.count, E);
+                    es.kind = bcast32(ev.kind, E);
+                    es.prio = bcast32((int)ev.prio, E) != 0;
+                    const int64_t te = bcast64(t, E), ce = bcast64(create, E);
+                    if (es.kind == SG_LOCAL_ENTRY) nd.entry(es, te);
+                    else nd.exit(es, te, ce);
+                }
+                p = E + 1;
+            }
+            pos = rend;
+        }
+    }
+    nd.finish();
+}
+
+// First position p in [lo, hi) with pred(p) (monotone), hi if none: 64-way wave search.
+template <class Pred>
+__device__ __forceinline__ uint64_t lwave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t p = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(p >= hi || pred(p));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t p = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(p < hi && pred(p));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
+}
+
+__global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_lperiods(a, sbnd, bndp);
+    const int lane = lane_id();
+    const uint32_t n_long = *sg.long_count;
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t item = wave; item < n_long; item += nwaves) {
+        const uint64_t s = sg.long_list[item];
+        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+        const uint64_t e = lwave_search(s + 1, a.n, [&](uint64_t p) {
+            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
+        }, lane);
+        lwalk_wave(a, bndp, k, s, e);
+    }
+}
+
+__global__ void k_local_finish(LArgs a) {
+    if (*a.err == 0 && a.n > 0) *a.last_ts = a.ev[a.n - 1].ts_ms;
+}
+
+// ---------------------------------------------------------------------------------- launchers
+
+static unsigned lgrid(uint64_t n, unsigned block, unsigned cap) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+static unsigned lresident(const void* kernel) {
+    int dev = 0, cus = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+    return (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+}
+
+hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_local_prep, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_init(const LArgs& a, hipStream_t stream) {
+    if (a.K == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_local_init, dim3(lgrid((uint64_t)a.K * kMinuteS, 256, 8192)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, hipStream_t aux, hipStream_t stream, hipEvent_t fork,
+                             hipEvent_t join) {
+    static unsigned bl = 0, bs = 0;
+    if (bl == 0) bl = lresident((const void*)k_lwalk_long);
+    if (bs == 0) bs = lresident((const void*)k_lwalk_short);
+    hipError_t e = hipEventRecord(fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
+    hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
+    e = hipEventRecord(join, aux);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_local_finish, dim3(1), dim3(1), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace sg

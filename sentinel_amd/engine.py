@@ -15,7 +15,8 @@ LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
            "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
-           "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state"]
+           "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
+           "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state"]
 
 _lib = None
 
@@ -55,6 +56,10 @@ def load_library():
         "sg_param_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_param_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "sg_build_info": (C.c_char_p, []),
+        "sg_local_load_rules": (C.c_int, [vp, vp, vp, u32]),
+        "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -167,3 +172,31 @@ class FlowEngine:
         out = np.zeros(2 * n_rules, np.float64)
         self._check(self._L.sg_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
         return out.reshape(n_rules, 2)
+
+    # ---- local slot chain (StatisticSlot → FlowSlot/DefaultController → DegradeSlot)
+    def local_load_rules(self, rules: np.ndarray, sample_count=2, interval_ms=1000, occupy_timeout_ms=500):
+        rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
+        cfg = abi.sg_local_config(sample_count=sample_count, interval_ms=interval_ms,
+                                  occupy_timeout_ms=occupy_timeout_ms, reserved=0)
+        self._check(self._L.sg_local_load_rules(self.h, C.byref(cfg), abi.ptr(rules), len(rules)))
+        self.local_S = sample_count
+
+    def local_decide_host(self, ev: np.ndarray) -> np.ndarray:
+        ev = np.ascontiguousarray(ev, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        out = np.zeros(len(ev), abi.LOCAL_RES_DTYPE)
+        self._check(self._L.sg_local_decide_batch_host(self.h, abi.ptr(ev), len(ev), abi.ptr(out)))
+        return out
+
+    def local_decide_device(self, ev_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        self._check(self._L.sg_local_decide_batch(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr),
+                                                  C.c_void_p(stream_ptr)))
+
+    def local_state(self, res):
+        """(second [S][8], borrow [S][2], minute [60][8], head[14]) — see sg_local_read_state."""
+        S = self.local_S
+        sec = np.zeros((S, 8), np.int64)
+        bor = np.zeros((S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        head = np.zeros(14, np.int64)
+        self._check(self._L.sg_local_read_state(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), abi.ptr(head)))
+        return sec, bor, mnt, head
