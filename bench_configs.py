@@ -1,0 +1,231 @@
+"""Secondary benchmarks: the other BASELINE.json configurations, on one GPU, with the same JSON contract as
+bench.py (which measures the headline C3 workload).
+
+  --workload c2  10k resources, QPS FlowRule each (count U{1..64}), DefaultController over each resource's
+                 StatisticNode (second window S=2/1000 ms + minute window), 16M entries per 1000 ms batch,
+                 Zipf(1.0) resources, acquire 1 (10 % U{2..4}), no prioritized requests, no exits.
+  --workload c4  one ParamFlowRule (count 5, durationInSec 1, DEFAULT token bucket) over 10M distinct u64
+                 values, Zipf(1.1), 16M requests per 1000 ms batch, exact HBM table (2^25 slots).
+  --workload c5  1M resources, each a QPS FlowRule + RT breaker (100 ms, slow ratio 0.5) + exception-ratio
+                 breaker (0.5); statIntervalMs 1000, minRequestAmount 5, timeWindow 10 s; 16M entries per
+                 1000 ms batch plus the exits of the passed ones (rt ~ lognormal, median 12 ms; 5 % errors).
+                 The event stream depends on the decisions (only passed entries exit), so it is produced by
+                 the CPU oracle's client model (oracle.binding.LocalTraceGen) before the timed region.
+
+Inputs are resident in HBM before the timed region; one step = one batch. cpu_baseline = the oracle
+(sequential C restatement, 1 thread) on the first batch of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sentinel_amd import abi  # noqa: E402
+from sentinel_amd.engine import FlowEngine  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+T0 = 1_700_000_000_000
+
+
+def zipf_cdf(n, s, seed):
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(n)
+    w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+    cdf = np.cumsum(w)
+    return cdf / cdf[-1], perm
+
+
+def gpu_keys(cdf_t, perm_t, n, gen):
+    u = torch.rand(n, generator=gen, device=cdf_t.device, dtype=torch.float64)
+    r = torch.searchsorted(cdf_t, u, right=True).clamp_(max=len(cdf_t) - 1)
+    return perm_t[r]
+
+
+def timed(step, warmup, steps):
+    for b in range(warmup):
+        step(b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(warmup, warmup + steps):
+        step(b)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def c2(args, dev):
+    K, n = 10_000, args.events
+    rng = np.random.default_rng(2)
+    rules = np.zeros(K, abi.LOCAL_RULE_DTYPE)
+    rules["flow_count"] = rng.integers(1, 65, K).astype(np.float64)
+    rules["flow_grade"] = abi.FLOW_GRADE_QPS
+    cdf, perm = zipf_cdf(K, 1.0, 2)
+    cdf_t, perm_t = torch.from_numpy(cdf).to(dev), torch.from_numpy(perm.astype(np.int64)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(2)
+
+    def batch(b):
+        w = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+        w[:, 0] = torch.sort(torch.randint(0, 1000, (n,), generator=gen, device=dev)).values + T0 + 1000 * b
+        cnt = torch.where(torch.rand(n, generator=gen, device=dev) < 0.1,
+                          torch.randint(2, 5, (n,), generator=gen, device=dev), torch.ones(n, dtype=torch.int64, device=dev))
+        w[:, 2] = gpu_keys(cdf_t, perm_t, n, gen) | (cnt << 32)   # resource | count << 32; kind = 0 (entry)
+        return w.view(torch.uint8).reshape(-1)
+
+    eng = FlowEngine(device=0, max_batch=n)
+    eng.local_load_rules(rules, 2, 1000, 500)
+    batches = [batch(b) for b in range(args.warmup + args.steps)]
+    out = torch.empty(n * 8, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    el = timed(lambda b: eng.local_decide_device(batches[b].data_ptr(), n, out.data_ptr(), stream), args.warmup, args.steps)
+    touched = int(torch.unique(batches[-1].view(torch.int64).reshape(-1, 4)[:, 2] & 0xFFFFFFFF).numel())
+    # per event: 32 B sg_local_event in + 8 B result out; per touched resource: second window 2x64 B read +
+    # write, one minute bucket read + write, curThreadNum/breaker head 2x16 B, rule 16 B
+    b_alg = n * (32 + 8) + touched * (2 * 128 + 2 * 64 + 2 * 16 + 16)
+    base = None
+    if not args.no_cpu_baseline:
+        from oracle.binding import LocalChain
+        ev = batches[0].view(torch.int64).reshape(-1, 4)[: args.cpu_events].cpu().numpy().copy().view(abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        ora = LocalChain(2, 1000, 500)
+        ora.load_rules(rules)
+        t = time.perf_counter()
+        ora.decide(ev)
+        dt = time.perf_counter() - t
+        base = {"value": len(ev) / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"first {len(ev)} events of batch 0 through oracle LocalChain (1 thread), {dt:.1f} s"}
+    return {"metric": "local flow decisions/sec (DefaultController over StatisticNode), 10k resources",
+            "workload": "C2: 10k resources x QPS FlowRule, S=2/1000 ms second window + minute window, 16M entries/batch",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
+            "data": "synthetic (GPU-generated, seeded): Zipf(1.0) resources, counts U{1..64}, 10% acquire U{2..4}"}
+
+
+def c4(args, dev):
+    n, V = args.events, 10_000_000
+    rules = np.zeros(1, abi.PARAM_RULE_DTYPE)
+    rules["count"], rules["duration_sec"], rules["behavior"], rules["capacity_log2"] = 5, 1, abi.BEHAVIOR_DEFAULT, 25
+    cdf, perm = zipf_cdf(V, 1.1, 4)
+    cdf_t, perm_t = torch.from_numpy(cdf).to(dev), torch.from_numpy(perm.astype(np.int64)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(4)
+
+    def batch(b):
+        w = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+        w[:, 0] = torch.sort(torch.randint(0, 1000, (n,), generator=gen, device=dev)).values + T0 + 1000 * b
+        w[:, 1] = gpu_keys(cdf_t, perm_t, n, gen) * 0x9E3779B1 + 17     # distinct u64 values
+        w[:, 2] = 1 << 32                                                # rule 0, acquireCount 1
+        return w.view(torch.uint8).reshape(-1)
+
+    eng = FlowEngine(device=0, max_batch=n)
+    eng.param_load_rules(rules)
+    batches = [batch(b) for b in range(args.warmup + args.steps)]
+    out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    el = timed(lambda b: eng.param_decide_device(batches[b].data_ptr(), n, out.data_ptr(), stream), args.warmup, args.steps)
+    touched = int(torch.unique(batches[-1].view(torch.int64).reshape(-1, 3)[:, 1]).numel())
+    b_alg = n * (24 + 4) + touched * (2 * 32)   # request in, pass bit out; per value slot 32 B read + write
+    base = None
+    if not args.no_cpu_baseline:
+        from oracle.binding import ParamFlowChecker
+        req = batches[0].view(torch.int64).reshape(-1, 3)[: args.cpu_events].cpu().numpy().copy().view(abi.PARAM_REQ_DTYPE).reshape(-1)
+        ora = ParamFlowChecker()
+        ora.load_rules(rules)
+        t = time.perf_counter()
+        ora.decide(req)
+        dt = time.perf_counter() - t
+        base = {"value": len(req) / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"first {len(req)} requests of batch 0 through oracle ParamFlowChecker (1 thread), {dt:.1f} s"}
+    return {"metric": "hot-parameter decisions/sec (ParamFlowChecker token bucket), 10M values",
+            "workload": "C4: 1 ParamFlowRule count=5/1 s, 10M distinct values Zipf(1.1), 16M requests/batch",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
+            "data": "synthetic (GPU-generated, seeded)"}
+
+
+def c5(args, dev):
+    from oracle.binding import LocalChain, LocalTraceGen, degrade_rule, local_rule
+    K, n = args.resources, args.events
+    rng = np.random.default_rng(5)
+    rules = np.zeros(K, abi.LOCAL_RULE_DTYPE)
+    rules["flow_count"] = rng.integers(1, 65, K).astype(np.float64)
+    rules["flow_grade"] = abi.FLOW_GRADE_QPS
+    rules["n_breakers"] = 2
+    b = np.zeros(2, abi.DEGRADE_RULE_DTYPE)
+    b[0] = degrade_rule(abi.DEGRADE_RT, 100, 10, 5, 1000, 0.5)
+    b[1] = degrade_rule(abi.DEGRADE_EXCEPTION_RATIO, 0.5, 10, 5, 1000)
+    rules["breakers"] = b
+    cdf, perm = zipf_cdf(K, 1.0, 5)
+    ora = LocalChain(2, 1000, 500)
+    ora.load_rules(rules)
+    gen = LocalTraceGen(ora)
+    t_gen = time.time()
+    host = []
+    gen_s = 0.0
+    for bt in range(args.warmup + args.steps):
+        ent = np.zeros(n, abi.LOCAL_EVENT_DTYPE)
+        ent["ts_ms"] = T0 + 1000 * bt + np.sort(rng.integers(0, 1000, n))
+        ent["resource"] = perm[np.minimum(np.searchsorted(cdf, rng.random(n), side="right"), K - 1)]
+        ent["count"] = 1
+        rt = np.minimum(np.round(np.exp(rng.normal(2.5, 0.8, n))), 10_000).astype(np.int32)
+        err = (rng.random(n) < 0.05).astype(np.uint8)
+        t = time.perf_counter()
+        ev, _ = gen.run(ent, rt, err, T0 + 1000 * (bt + 1))
+        gen_s += time.perf_counter() - t
+        host.append(ev)
+    print(f"# c5 trace: {sum(len(e) for e in host)} events generated by the oracle client model in "
+          f"{time.time() - t_gen:.1f} s", file=sys.stderr)
+    eng = FlowEngine(device=0, max_batch=max(len(e) for e in host))
+    eng.local_load_rules(rules, 2, 1000, 500)
+    batches = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e in host]
+    out = torch.empty(max(len(e) for e in host) * 8, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    sizes = [len(e) for e in host]
+    el = timed(lambda b: eng.local_decide_device(batches[b].data_ptr(), sizes[b], out.data_ptr(), stream),
+               args.warmup, args.steps)
+    decided = sum(sizes[args.warmup:])
+    touched = int(np.unique(host[-1]["resource"] & 0x7FFFFFFF).size)
+    # per event 32 B in + 8 B out; per touched resource: second window 2x128 B, two minute buckets 2x2x64 B,
+    # head (threads + two breakers) 2x128 B, rule 80 B
+    b_alg = sizes[-1] * (32 + 8) + touched * (2 * 128 + 2 * 2 * 64 + 2 * 128 + 80)
+    base = {"value": sum(sizes) / gen_s, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"the oracle replaying all {sum(sizes)} events while generating them (client model, 1 thread), "
+                      f"{gen_s:.1f} s"}
+    return {"metric": "local flow + circuit-breaker decisions/sec (entries + exits), 1M resources",
+            "workload": "C5: 1M resources x (QPS FlowRule + RT breaker + exception-ratio breaker), minute window, "
+                        "16M entries/batch + exits of passed entries",
+            "value": decided / el, "el": el, "n": decided // args.steps, "b_alg": b_alg, "touched": touched,
+            "cpu": base, "data": "synthetic (seeded): Zipf(1.0) resources, rt lognormal(2.5, 0.8) ms, 5% errors; "
+                                 "exits generated by the oracle client model"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--events", type=int, default=16_000_000)
+    ap.add_argument("--resources", type=int, default=1_000_000)
+    ap.add_argument("--cpu-events", type=int, default=4_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    r = {"c2": c2, "c4": c4, "c5": c5}[args.workload](args, dev)
+    ms = r["el"] * 1000.0 / args.steps
+    gbs = r["b_alg"] / (ms / 1000.0) / 1e9
+    res = {"metric": r["metric"], "value": r["value"], "unit": "decisions/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "int64", "data": r["data"],
+           "config": {"workload": r["workload"], "decisions_per_step": r["n"], "touched_keys": r["touched"]},
+           "roofline": {"bound": "hbm", "kernel": "whole batch pipeline, wall time per step", "achieved": gbs,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                        "algorithmic_bytes_per_step": r["b_alg"]}}
+    if r["cpu"] is not None:
+        res["cpu_baseline"] = r["cpu"]
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -91,6 +91,12 @@ struct sg_handle {
     int l_n_wl = 0, l_wsec = 0, l_wmin = 0;
     int32_t l_wl[kMaxWl]{};
     sg_local_event* d_lev_h = nullptr;
+    int* d_lflags = nullptr;
+    uint32_t* d_lexit_pos = nullptr;
+    uint32_t* d_lexit_cnt = nullptr;
+    LSkip* d_lskips = nullptr;
+    uint32_t* d_lskip_count = nullptr;
+    uint32_t lskip_cap = 0;
     sg_local_result* d_lout_h = nullptr;
 
     int kbits = 0, ibits = 0, abits = 0;
@@ -323,6 +329,11 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lmin);
     dfree(h->d_llast_ts);
     dfree(h->d_lev_h);
+    dfree(h->d_lflags);
+    dfree(h->d_lexit_pos);
+    dfree(h->d_lexit_cnt);
+    dfree(h->d_lskips);
+    dfree(h->d_lskip_count);
     dfree(h->d_lout_h);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
@@ -907,6 +918,22 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     L.np = h->d_np;
     L.err = h->d_err;
     L.last_ts = h->d_llast_ts;
+    if (!h->d_lflags) {  // batch workspace of the local path (sized for max_batch)
+        const uint64_t mb = h->cfg.max_batch;
+        h->lskip_cap = (uint32_t)(2 * mb / kSkipMin + 1);
+        if (hipMalloc(&h->d_lflags, sizeof(int)) != hipSuccess ||
+            hipMalloc(&h->d_lexit_pos, sizeof(uint32_t) * (mb + 1)) != hipSuccess ||
+            hipMalloc(&h->d_lexit_cnt, sizeof(uint32_t) * (mb / kLTile + 2)) != hipSuccess ||
+            hipMalloc(&h->d_lskips, sizeof(LSkip) * h->lskip_cap) != hipSuccess ||
+            hipMalloc(&h->d_lskip_count, sizeof(uint32_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "local batch workspace");
+    }
+    L.flags = h->d_lflags;
+    L.exit_pos = h->d_lexit_pos;
+    L.exit_cnt = h->d_lexit_cnt;
+    L.skips = h->d_lskips;
+    L.skip_count = h->d_lskip_count;
+    L.skip_cap = h->lskip_cap;
 
     BatchArgs sgm{};  // segment lists (k_seg)
     sgm.n = n;
@@ -924,6 +951,8 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_lflags, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_lskip_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_local_prep(L, stream));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     uint64_t* sorted = nullptr;
@@ -938,6 +967,7 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
         HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, h->d_lskip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipEventRecord(h->ev[4], stream));
     }
     HIP_TRY(h, hipStreamSynchronize(stream));
@@ -950,7 +980,7 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
         (void)hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
         h->stats.walk_ms = ms;
         h->stats.long_segments = h->h_long[0];
-        h->stats.skipped_ranges = 0;
+        h->stats.skipped_ranges = h->h_long[1];
     }
     if (*h->h_err & kErrTime)
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");

@@ -249,6 +249,20 @@ struct LArgs {
     uint32_t* np;
     int* err;
     int64_t* last_ts;
+    int* flags;               // kLFlag*: batch properties that rule out the dead-period skip
+    uint32_t* exit_pos;       // sorted positions of exit records (ascending), exit_cnt[0] of them
+    uint32_t* exit_cnt;       // [0] total, then per-tile counts / offsets
+    struct LSkip* skips;      // dead-period ranges handed to k_lskip_apply
+    uint32_t* skip_count;
+    uint32_t skip_cap;
+};
+
+constexpr int kLFlagPrio = 1;    // some entry is prioritized (may occupy in a saturated window)
+constexpr int kLFlagNonPos = 2;  // some entry has acquireCount <= 0 (may fit in a saturated window)
+constexpr uint32_t kLTile = 4096;  // records per tile of the exit-position compaction
+
+struct LSkip {                   // entries [b0, b1) of resource k, all FLOW-blocked in periods (qs, qm)
+    uint32_t k, qs, qm, b0, b1, pad[3];
 };
 
 hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);

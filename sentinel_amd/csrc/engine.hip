@@ -786,13 +786,19 @@ __device__ void walk_reg(const BatchArgs& a, const uint32_t* const* bndp, uint32
     int I = -1;      // slot of the open period
     int32_t r = 0;   // open period, relative to P0
     bool first = true;
-    uint64_t j = s;
-    uint64_t nxt = a.rec_sorted[j];
+    // records kAhead ahead in a register shift pipeline (a lane may walk up to short_max records)
+    constexpr int kAhead = 8;
+    uint64_t rq[kAhead];
+    uint64_t nextp = s;
+#pragma unroll
+    for (int u = 0; u < kAhead; ++u, ++nextp) rq[u] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
     for (;;) {
-        const uint64_t cur = nxt;
+        const uint64_t cur = rq[0];
         if ((uint32_t)(cur >> a.kshift) != k) break;
-        ++j;
-        nxt = j < a.n ? a.rec_sorted[j] : ~0ull;  // the next record's load is in flight while this one is decided
+#pragma unroll
+        for (int u = 0; u < kAhead - 1; ++u) rq[u] = rq[u + 1];
+        rq[kAhead - 1] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
+        ++nextp;
         const Decoded d = decode(a, cur);
         const uint32_t q = pc.of(d.idx);
         if (q != pc.q) {

@@ -154,8 +154,12 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
             const uint64_t kind = e.kind == SG_LOCAL_ENTRY ? 0 : (e.kind == SG_LOCAL_EXIT_ERROR ? 2 : 1);
             const uint64_t ac = (c << 3) | (kind << 1) | (uint64_t)(e.resource >> 31);
             rec = ((uint64_t)res << a.kshift) | ((uint64_t)i << a.abits) | ac;
+            if (kind == 0 && (e.resource >> 31)) atomicOr(a.flags, kLFlagPrio);
+            if (kind == 0 && e.count <= 0) atomicOr(a.flags, kLFlagNonPos);
         }
-        lstore(a, (uint32_t)i, SG_LOCAL_PASS, 0);  // walkers write only other results
+        // default result: FlowException for entries (the common outcome of a saturated resource; the walkers
+        // write every other outcome), plain 0 for exits and events of unknown resources
+        lstore(a, (uint32_t)i, (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS, 0);
         a.rec[i] = rec;
     }
 }
@@ -372,16 +376,15 @@ struct LNode {
     }
 
     // -------- circuit breakers --------
-    __device__ void cb_to_open(int j, int64_t t) {
+    __device__ __forceinline__ void cb_to_open(int j, int64_t t) {
         cb[j].state = kCbOpen;
         cb[j].next_retry = t + (int64_t)R.b[j].recovery_ms;
     }
     __device__ __forceinline__ void cb_stat_window(int j, int64_t t) {  // LeapArray(1, statIntervalMs).currentWindow
-        const int64_t ws = t - t % R.b[j].stat_ms;
-        if (cb[j].stat_start == INT64_MIN || ws > cb[j].stat_start) {
-            cb[j].stat_start = ws;
-            cb[j].bad = cb[j].total = 0;
-        }
+        // events are time-ordered: t >= the bucket's start, so the bucket is current iff t < start + length
+        if (cb[j].stat_start != INT64_MIN && t - cb[j].stat_start < R.b[j].stat_ms) return;
+        cb[j].stat_start = t - t % R.b[j].stat_ms;
+        cb[j].bad = cb[j].total = 0;
     }
     __device__ __forceinline__ bool cb_bad(int j, int64_t rt, bool error) const {
         return R.b[j].grade == SG_DEGRADE_RT ? rt > R.b[j].max_rt : error;
@@ -398,7 +401,7 @@ struct LNode {
         return cur > R.b[j].count;
     }
     // onRequestComplete at exit time t
-    __device__ void cb_complete(int j, int64_t t, int64_t rt, bool error) {
+    __device__ __forceinline__ void cb_complete(int j, int64_t t, int64_t rt, bool error) {
         cb_stat_window(j, t);
         const bool bad = cb_bad(j, rt, error);
         cb[j].bad += bad ? 1 : 0;
@@ -418,7 +421,13 @@ struct LNode {
 
     // -------- one event, sequentially (the oracle's or_local_decide step) --------
     // Entry: FlowSlot (DefaultController.canPass) → DegradeSlot.performChecking → StatisticSlot.
+    // t: the entry's timestamp, or INT64_MIN when not loaded yet (read only on the paths that need it:
+    // the prioritized occupy and an OPEN breaker's retry check)
     __device__ void entry(const LEvent& e, int64_t t) {
+        auto ts = [&]() {
+            if (t == INT64_MIN) t = a.ev[e.idx].ts_ms;
+            return t;
+        };
         int32_t status = SG_LOCAL_PASS;
         int64_t wait = 0;
         if (R.flow_grade >= 0) {
@@ -427,7 +436,7 @@ struct LNode {
             if ((double)sum > R.flow_count) {
                 status = SG_LOCAL_BLOCK_FLOW;
                 if (e.prio && R.flow_grade == 1) {
-                    wait = try_occupy_next(t, e.count, R.flow_count);
+                    wait = try_occupy_next(ts(), e.count, R.flow_count);
                     if (wait < a.occupy_timeout) {
                         const int s = bor_window(t + wait);  // addWaitingRequest
                         if (s >= 0) bor[s].pass += e.count;
@@ -439,26 +448,26 @@ struct LNode {
             }
         }
         if (status == SG_LOCAL_PASS) {
-            bool half[2] = {false, false};
-            for (int j = 0; j < R.nb; ++j) {  // AbstractCircuitBreaker.tryPass (:73-84)
-                bool ok;
-                if (cb[j].state == kCbClosed) {
-                    ok = true;
-                } else if (cb[j].state == kCbOpen && t >= cb[j].next_retry) {
+            // AbstractCircuitBreaker.tryPass (:73-84) in rule order; the loops are fully unrolled so the
+            // breaker state stays in registers
+            bool blocked = false, half0 = false, half1 = false;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                if (j >= R.nb || blocked) continue;
+                if (cb[j].state == kCbClosed) continue;
+                if (cb[j].state == kCbOpen && ts() >= cb[j].next_retry) {
                     cb[j].state = kCbHalfOpen;
-                    half[j] = true;
-                    ok = true;
+                    if (j == 0) half0 = true;
+                    else half1 = true;
                 } else {
-                    ok = false;
-                }
-                if (!ok) {
-                    status = SG_LOCAL_BLOCK_DEGRADE;
-                    break;
+                    blocked = true;
                 }
             }
-            if (status == SG_LOCAL_BLOCK_DEGRADE)  // whenTerminate of a blocked probe: back to OPEN
-                for (int j = 0; j < 2; ++j)
-                    if (half[j] && cb[j].state == kCbHalfOpen) cb[j].state = kCbOpen;
+            if (blocked) {  // DegradeException; whenTerminate of a blocked probe: back to OPEN
+                status = SG_LOCAL_BLOCK_DEGRADE;
+                if (half0 && cb[0].state == kCbHalfOpen) cb[0].state = kCbOpen;
+                if (half1 && cb[1].state == kCbHalfOpen) cb[1].state = kCbOpen;
+            }
         }
         if (status == SG_LOCAL_PASS) {
             threads += 1;
@@ -470,7 +479,7 @@ struct LNode {
             sc[kLBlock] += e.count;
             mc[kLBlock] += e.count;
         }
-        if (status != SG_LOCAL_PASS) lstore(a, e.idx, status, status == SG_LOCAL_PASS_WAIT ? (int32_t)wait : 0);
+        if (status != SG_LOCAL_BLOCK_FLOW) lstore(a, e.idx, status, status == SG_LOCAL_PASS_WAIT ? (int32_t)wait : 0);
     }
 
     // Exit: StatisticSlot.exit (addRtAndSuccess, decreaseThreadNum, increaseExceptionQps) → DegradeSlot.exit.
@@ -488,7 +497,9 @@ struct LNode {
             sc[kLExc] += e.count;
             mc[kLExc] += e.count;
         }
-        for (int j = 0; j < R.nb; ++j) cb_complete(j, t, rt, error);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (j < R.nb) cb_complete(j, t, rt, error);
     }
 
     __device__ void step(const LEvent& e, int64_t t, int64_t create) {
@@ -556,21 +567,70 @@ __global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
         }
         const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
         if (i >= cnt[c]) continue;
-        uint64_t j = sg.short_list[sg.class_off[c] + i];
+        const uint64_t j = sg.short_list[sg.class_off[c] + i];
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
         LNode nd(a, bndp, k);
-        uint64_t nxt = a.rec_sorted[j];
+        // software pipeline: records kRecAhead ahead, exit timestamps kEvAhead ahead (a lane walks up to
+        // short_max contiguous records; one load in flight per record would leave it latency-bound)
+        constexpr int kRecAhead = 8, kEvAhead = 4;
+        uint64_t r[kRecAhead];
+        int64_t ets[kEvAhead], ecr[kEvAhead];
+        uint64_t nextp = j;
+#pragma unroll
+        for (int u = 0; u < kRecAhead; ++u, ++nextp) r[u] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
+        auto ev_load = [&](uint64_t rec, int64_t& ts, int64_t& cr) {
+            ts = cr = 0;
+            if ((uint32_t)(rec >> a.kshift) == k && ((rec & a.amask) >> 1 & 3ull) != 0) {
+                const sg_local_event* p = a.ev + ((rec >> a.abits) & a.imask);
+                ts = p->ts_ms;
+                cr = p->create_ts;
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kEvAhead; ++u) ev_load(r[u], ets[u], ecr[u]);
         for (;;) {
-            const uint64_t cur = nxt;
+            const uint64_t cur = r[0];
             if ((uint32_t)(cur >> a.kshift) != k) break;
-            ++j;
-            nxt = j < a.n ? a.rec_sorted[j] : ~0ull;
+            const int64_t t = ets[0], cr = ecr[0];
+#pragma unroll
+            for (int u = 0; u < kRecAhead - 1; ++u) r[u] = r[u + 1];
+            r[kRecAhead - 1] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
+            ++nextp;
+#pragma unroll
+            for (int u = 0; u < kEvAhead - 1; ++u) {
+                ets[u] = ets[u + 1];
+                ecr[u] = ecr[u + 1];
+            }
+            ev_load(r[kEvAhead - 1], ets[kEvAhead - 1], ecr[kEvAhead - 1]);
             const LEvent e = ldecode(a, cur);
-            const sg_local_event ev = a.ev[e.idx];
-            nd.step(e, ev.ts_ms, ev.create_ts);
+            nd.at(nd.cs.of(e.idx), nd.cm.of(e.idx));
+            if (e.kind == SG_LOCAL_ENTRY) nd.entry(e, INT64_MIN);
+            else nd.exit(e, t, cr);
         }
         nd.finish();
     }
+}
+
+// First position p in [lo, hi) with pred(p) (monotone), hi if none: 64-way wave search.
+template <class Pred>
+__device__ __forceinline__ uint64_t lwave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t p = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(p >= hi || pred(p));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t p = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(p < hi && pred(p));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
 // ------------------------------------------------------------------------------- wave walker
@@ -590,7 +650,17 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
     LNode nd(a, bndp, k);
     const int nb = nd.R.nb;
     const bool thread_grade = nd.R.flow_grade == 0;
-    for (uint64_t base = s; base < e_end; base += 64) {
+    // a saturated second window (not even acquireCount 1 fits) FLOW-blocks every entry until the period
+    // ends, whatever the breakers are, unless an entry may occupy (prioritized) or has a count <= 0
+    const bool may_skip = nd.R.flow_grade == 1 && !(*a.flags & (kLFlagPrio | kLFlagNonPos));
+    uint64_t skip_retry = 0;  // after a failed attempt: retry once the walk is past the obstacle
+    // the resource's exits in the sorted exit list, consumed in order; the end of the current pair of
+    // window periods, found once per pair
+    const uint32_t ne = a.exit_cnt[0];
+    uint64_t xi = may_skip ? lwave_search(0, ne, [&](uint64_t i) { return (uint64_t)a.exit_pos[i] >= s; }, lane) : ne;
+    uint32_t pe_qs = 0xFFFFFFFFu, pe_qm = 0xFFFFFFFFu;
+    uint64_t pe = 0;
+    for (uint64_t base = s; base < e_end;) {
         const uint64_t j = base + lane;
         const bool act = j < e_end;
         LEvent ev;
@@ -603,14 +673,20 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
         int64_t sw0 = 0, sw1 = 0;  // breaker statistic windows of this event (exits)
         if (act) {
             ev = ldecode(a, a.rec_sorted[j]);
-            const sg_local_event le = a.ev[ev.idx];
-            t = le.ts_ms;
-            create = le.create_ts;
             qs = nd.cs.of(ev.idx);
             qm = nd.cm.of(ev.idx);
-            if (nb > 0) sw0 = t - t % nd.R.b[0].stat_ms;
-            if (nb > 1) sw1 = t - t % nd.R.b[1].stat_ms;
+            // timestamps: exits always (rt, statistic window); entries only when breakers may need them
+            if (ev.kind != SG_LOCAL_ENTRY || nb > 0) {
+                const sg_local_event le = a.ev[ev.idx];
+                t = le.ts_ms;
+                create = le.create_ts;
+            }
+            if (ev.kind != SG_LOCAL_ENTRY) {
+                if (nb > 0) sw0 = t - t % nd.R.b[0].stat_ms;
+                if (nb > 1) sw1 = t - t % nd.R.b[1].stat_ms;
+            }
         }
+        base += 64;
         const int nact = (int)__popcll(__ballot(act));
         const bool is_entry = act && ev.kind == SG_LOCAL_ENTRY;
         const bool is_exit = act && ev.kind != SG_LOCAL_ENTRY;
@@ -619,8 +695,11 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
         while (pos < nact) {
             // run: lanes [pos, rend) with the same windows as lane pos
             const uint32_t qs0 = (uint32_t)bcast32((int)qs, pos), qm0 = (uint32_t)bcast32((int)qm, pos);
-            const int64_t a0 = bcast64(sw0, pos), a1 = bcast64(sw1, pos);
-            const uint64_t diff = __ballot(act && lane > pos && (qs != qs0 || qm != qm0 || sw0 != a0 || sw1 != a1));
+            const uint64_t exr = __ballot(is_exit) & ~below(pos);
+            const int fx = exr ? __builtin_ctzll(exr) : pos;  // the run's first exit fixes its statistic windows
+            const int64_t a0 = bcast64(sw0, fx), a1 = bcast64(sw1, fx);
+            const uint64_t diff = __ballot(act && lane > pos &&
+                                           (qs != qs0 || qm != qm0 || (is_exit && (sw0 != a0 || sw1 != a1))));
             const int rend = diff ? __builtin_ctzll(diff) : nact;
             nd.at(qs0, qm0);
             int p = pos;
@@ -631,19 +710,20 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                 // before its retry time and lets a probe through after it
                 bool all_closed = true;
                 int64_t retry = INT64_MAX;
-                for (int x = 0; x < nb; ++x) {
-                    if (nd.cb[x].state == kCbClosed) continue;
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    if (x >= nb || !all_closed || nd.cb[x].state == kCbClosed) continue;
                     all_closed = false;
                     if (nd.cb[x].state == kCbOpen) retry = nd.cb[x].next_retry;
-                    break;
                 }
                 // ---- first lane needing the serial step (epoch end), from everything that does not
                 // depend on this epoch's entry decisions
                 uint64_t special = 0;
                 if (thread_grade) special |= __ballot(in && is_entry);
                 // exits: would a CLOSED breaker open here? first exit while HALF_OPEN.
-                for (int x = 0; x < nb; ++x) {
-                    if (nd.cb[x].state == kCbOpen) continue;
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {
+                    if (x >= nb || nd.cb[x].state == kCbOpen) continue;
                     const bool ex = in && is_exit;
                     if (nd.cb[x].state == kCbHalfOpen) {
                         special |= __ballot(ex);
@@ -724,7 +804,7 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                 const uint64_t ex_m = __ballot(in && is_exit) & below(E) & ~below(p);
                 const bool mp = (pass_m >> lane) & 1ull, mf = (blk_flow >> lane) & 1ull, md = (blk_deg >> lane) & 1ull;
                 const bool mx = (ex_m >> lane) & 1ull;
-                if (mf) lstore(a, ev.idx, SG_LOCAL_BLOCK_FLOW, 0);
+                if (mp) lstore(a, ev.idx, SG_LOCAL_PASS, 0);
                 if (md) lstore(a, ev.idx, SG_LOCAL_BLOCK_DEGRADE, 0);
                 const int64_t c = ev.count;
                 const int64_t passed = wave_sum(mp ? c : 0), blocked = wave_sum((mf || md) ? c : 0);
@@ -744,8 +824,9 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                 if (rmin < nd.s_min) nd.s_min = rmin;
                 if (rmin < nd.m_min) nd.m_min = rmin;
                 nd.threads += (int64_t)__popcll(pass_m) - (int64_t)__popcll(ex_m);
-                for (int x = 0; x < nb; ++x) {  // breaker statistics of the exits (no state change by construction)
-                    if (!ex_m) break;
+#pragma unroll
+                for (int x = 0; x < 2; ++x) {  // breaker statistics of the exits (no state change by construction)
+                    if (x >= nb || !ex_m) continue;
                     const int64_t swx = x == 0 ? a0 : a1;
                     nd.cb_stat_window(x, swx);
                     nd.cb[x].bad += wave_sum((mx && nd.cb_bad(x, rt, ev.kind == SG_LOCAL_EXIT_ERROR)) ? 1 : 0);
@@ -760,37 +841,61 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                     es.kind = bcast32(ev.kind, E);
                     es.prio = bcast32((int)ev.prio, E) != 0;
                     const int64_t te = bcast64(t, E), ce = bcast64(create, E);
-                    if (es.kind == SG_LOCAL_ENTRY) nd.entry(es, te);
+                    if (es.kind == SG_LOCAL_ENTRY) nd.entry(es, nb > 0 ? te : INT64_MIN);
                     else nd.exit(es, te, ce);
                 }
                 p = E + 1;
             }
             pos = rend;
         }
+        // dead-period skip: the open second window admits nothing any more → jump to the first of (end of
+        // this second-window period, end of this minute period, next exit of the resource); k_lskip_apply
+        // adds the skipped entries' BLOCK counts to both windows
+        if (may_skip && base < e_end && base >= skip_retry &&
+            (double)(int32_t)((uint32_t)java_d2i(nd.pass_qps()) + 1u) > nd.R.flow_count) {
+            if (nd.cs.q != pe_qs || nd.cm.q != pe_qm) {
+                pe_qs = nd.cs.q;
+                pe_qm = nd.cm.q;
+                const uint32_t nbs = nd.cs.next_b, nbm = nd.cm.next_b;
+                pe = lwave_search(base, e_end, [&](uint64_t p) {
+                    const uint32_t idx = (uint32_t)((a.rec_sorted[p] >> a.abits) & a.imask);
+                    return idx >= nbs || idx >= nbm;
+                }, lane);
+            }
+            for (;;) {  // advance to the first exit at or after base, 64 entries per step
+                const uint64_t i = xi + (uint64_t)lane;
+                const uint64_t m = __ballot(i >= ne || (uint64_t)a.exit_pos[i] >= base);
+                if (m) {
+                    xi += (uint64_t)__builtin_ctzll(m);
+                    break;
+                }
+                xi += 64;
+            }
+            const uint64_t nx = xi < ne ? min((uint64_t)a.exit_pos[xi], e_end) : e_end;
+            const uint64_t end = min(pe, nx);
+            skip_retry = end + 1;
+            if (end > base && end - base >= kSkipMin) {
+                const uint32_t np = (uint32_t)((end - base + kSkipPiece - 1) / kSkipPiece);
+                uint32_t slot = 0;
+                if (lane == 0) slot = atomicAdd(a.skip_count, np);
+                slot = (uint32_t)bcast32((int)slot, 0);
+                if (slot + np <= a.skip_cap) {
+                    for (uint32_t pi = lane; pi < np; pi += 64) {
+                        LSkip sk;
+                        sk.k = k;
+                        sk.qs = nd.cs.q;
+                        sk.qm = nd.cm.q;
+                        sk.b0 = (uint32_t)(base + (uint64_t)pi * kSkipPiece);
+                        sk.b1 = (uint32_t)min(end, base + (uint64_t)(pi + 1) * kSkipPiece);
+                        sk.pad[0] = sk.pad[1] = sk.pad[2] = 0;
+                        a.skips[slot + pi] = sk;
+                    }
+                    base = end;
+                }
+            }
+        }
     }
     nd.finish();
-}
-
-// First position p in [lo, hi) with pred(p) (monotone), hi if none: 64-way wave search.
-template <class Pred>
-__device__ __forceinline__ uint64_t lwave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
-    while (hi - lo > 64) {
-        const uint64_t step = (hi - lo + 63) / 64;
-        const uint64_t p = lo + (uint64_t)lane * step;
-        const uint64_t m = __ballot(p >= hi || pred(p));
-        if (m == 0) {
-            lo = lo + 63 * step + 1;
-            continue;
-        }
-        const int f = __builtin_ctzll(m);
-        if (f == 0) return lo;
-        const uint64_t nhi = lo + (uint64_t)f * step;
-        lo = lo + (uint64_t)(f - 1) * step + 1;
-        hi = nhi < hi ? nhi : hi;
-    }
-    const uint64_t p = lo + (uint64_t)lane;
-    const uint64_t m = __ballot(p < hi && pred(p));
-    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
 __global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
@@ -809,6 +914,94 @@ __global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
         lwalk_wave(a, bndp, k, s, e);
+    }
+}
+
+// Sorted positions of the exit records, in ascending order: per-tile counts, a one-block exclusive scan,
+// then each tile writes its positions in order (the dead-period skip stops at the next exit).
+__global__ void __launch_bounds__(256) k_lexit_count(LArgs a) {
+    __shared__ uint32_t wc[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kLTile;
+    uint32_t c = 0;
+    for (uint64_t j = t0 + threadIdx.x; j < min(a.n, t0 + kLTile); j += blockDim.x) {
+        const uint64_t r = a.rec_sorted[j];
+        c += ((uint32_t)(r >> a.kshift) < a.K && ((r & a.amask) >> 1 & 3ull) != 0) ? 1u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+    if (lane_id() == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) a.exit_cnt[1 + blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ void __launch_bounds__(1024) k_lexit_scan(LArgs a, uint32_t tiles) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < tiles; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < tiles ? a.exit_cnt[1 + i] : 0u;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t x = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] += x;
+            __syncthreads();
+        }
+        const uint32_t c = carry;
+        if (i < tiles) a.exit_cnt[1 + i] = c + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = c + part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.exit_cnt[0] = carry;
+}
+
+__global__ void __launch_bounds__(256) k_lexit_write(LArgs a) {
+    __shared__ uint32_t wc[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kLTile;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    uint32_t off = a.exit_cnt[1 + blockIdx.x];
+    for (uint64_t r0 = t0; r0 < min(a.n, t0 + kLTile); r0 += blockDim.x) {
+        const uint64_t j = r0 + threadIdx.x;
+        bool x = false;
+        if (j < a.n) {
+            const uint64_t r = a.rec_sorted[j];
+            x = (uint32_t)(r >> a.kshift) < a.K && ((r & a.amask) >> 1 & 3ull) != 0;
+        }
+        const uint64_t m = __ballot(x);
+        if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t pre = off;
+        for (int w = 0; w < wave; ++w) pre += wc[w];
+        if (x) a.exit_pos[pre + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)j;
+        off += wc[0] + wc[1] + wc[2] + wc[3];
+        __syncthreads();
+    }
+}
+
+// BLOCK counts of the skipped entries (one wave per piece; their FlowException results are k_local_prep's
+// default), added to the second- and minute-window buckets of their periods unless a later period of the
+// batch reset that slot.
+__global__ void __launch_bounds__(256) k_lskip_apply(LArgs a) {
+    if (*a.err) return;
+    const uint32_t cnt = min(*a.skip_count, a.skip_cap);
+    const int lane = lane_id();
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t i = wave; i < cnt; i += nwaves) {
+        const LSkip sk = a.skips[i];
+        int64_t sum = 0;
+        for (uint64_t j = (uint64_t)sk.b0 + lane; j < sk.b1; j += 64) sum += ldecode(a, a.rec_sorted[j]).count;
+        sum = wave_sum(sum);
+        if (lane == 0) {
+            const int64_t Ps = a.p0[a.wsec] + (int64_t)sk.qs, Pm = a.p0[a.wmin] + (int64_t)sk.qm;
+            LBucket& bs = a.sec[(size_t)sk.k * a.S + (int)(Ps % a.S)];
+            if (bs.start == Ps * a.wl2) atomicAdd((unsigned long long*)&bs.c[kLBlock], (unsigned long long)sum);
+            LBucket& bm = a.minute[(size_t)sk.k * kMinuteS + (int)(Pm % kMinuteS)];
+            if (bm.start == Pm * kMinuteWl) atomicAdd((unsigned long long*)&bm.c[kLBlock], (unsigned long long)sum);
+        }
     }
 }
 
@@ -849,6 +1042,10 @@ hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, hipStream_t au
     static unsigned bl = 0, bs = 0;
     if (bl == 0) bl = lresident((const void*)k_lwalk_long);
     if (bs == 0) bs = lresident((const void*)k_lwalk_short);
+    const uint32_t tiles = (uint32_t)((a.n + kLTile - 1) / kLTile);
+    hipLaunchKernelGGL(k_lexit_count, dim3(tiles), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_lexit_scan, dim3(1), dim3(1024), 0, stream, a, tiles);
+    hipLaunchKernelGGL(k_lexit_write, dim3(tiles), dim3(256), 0, stream, a);
     hipError_t e = hipEventRecord(fork, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e != hipSuccess) return e;
@@ -857,6 +1054,7 @@ hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, hipStream_t au
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lskip_apply, dim3(1024), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(k_local_finish, dim3(1), dim3(1), 0, stream, a);
     return hipGetLastError();
 }

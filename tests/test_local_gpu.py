@@ -62,8 +62,10 @@ def _run(rules, batches, flags=0, S=2, interval=1000, occupy=500, seed=0, rt_hi=
     gen = LocalTraceGen(ora)
     eng = _engine(flags=flags)
     eng.local_load_rules(rules, S, interval, occupy)
+    eng.enable_stats(True)
     t = 1_700_000_000_000 + int(rng.integers(0, 1000))
     total = 0
+    skipped = 0
     for n, span in batches:
         ent = _entries(rng, n, n_res, t, span, **kw)
         rt = rng.integers(0, rt_hi + 1, n).astype(np.int32)
@@ -75,9 +77,10 @@ def _run(rules, batches, flags=0, S=2, interval=1000, occupy=500, seed=0, rt_hi=
             i = bad[0]
             raise AssertionError(f"{len(bad)} results differ; first at {i}: ev={ev[i]} oracle={want[i]} gpu={got[i]}")
         total += len(ev)
+        skipped += eng.stats()["skipped_ranges"]
         t += span
     _compare(eng, ora, n_res, S)
-    return total
+    return total, skipped
 
 
 def _rules(n, rng, grade=abi.FLOW_GRADE_QPS, lo=1, hi=30, breakers=()):
@@ -181,3 +184,15 @@ def test_breakers_near_their_thresholds(flags):
                                                     degrade_rule(abi.DEGRADE_RT, 35, 2, 30, 1000, 0.2)])
     rules[3] = local_rule(1e6, abi.FLOW_GRADE_NONE, [degrade_rule(abi.DEGRADE_EXCEPTION_RATIO, 0.1, 1, 10, 250)])
     _run(rules, [(60_000, 3000), (60_000, 3000)], flags=flags, seed=9, zipf=0.5, err=0.1, rt_hi=40)
+
+
+@pytest.mark.parametrize("breakers", [False, True])
+def test_saturated_periods_are_skipped(breakers):
+    """Hot resources far above their QPS threshold: once the second window cannot admit even one more
+    request, the wave walker jumps to the end of the period (or the resource's next exit) and
+    k_lskip_apply adds the skipped entries' BLOCK counts. Results and windows must still match."""
+    rng = np.random.default_rng(10)
+    brk = [degrade_rule(abi.DEGRADE_EXCEPTION_RATIO, 0.3, 1, 5, 1000)] if breakers else []
+    rules = _rules(5, rng, lo=5, hi=40, breakers=brk)
+    _, skipped = _run(rules, [(200_000, 1000), (200_000, 1700)], seed=10, zipf=1.5, rt_hi=20, err=0.2)
+    assert skipped > 0
