@@ -647,39 +647,54 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
     constexpr int kL = kClasses + 1;  // list 0..kClasses-1: short length classes, kClasses: long
     __shared__ uint32_t cnt[kL];
     __shared__ uint32_t base[kL];
+    __shared__ uint32_t nheads;
+    __shared__ uint32_t hpos[kSegTile];  // heads of this tile (tile offsets), in any order
     if (*a.err) return;
     const uint64_t n = a.n;
     const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     for (uint64_t t0 = (uint64_t)blockIdx.x * kSegTile; t0 < n; t0 += (uint64_t)gridDim.x * kSegTile) {
         if (tid < kL) cnt[tid] = 0;
+        if (tid == 0) nheads = 0;
         __syncthreads();
-        // item u of wave w covers records t0 + (w*kSegItems + u)*64 + lane (wave-contiguous rows)
+        // 1. heads: item u of wave w covers records t0 + (w*kSegItems + u)*64 + lane (wave-contiguous rows)
         uint32_t key[kSegItems];
 #pragma unroll
         for (int u = 0; u < kSegItems; ++u) {
             const uint64_t j = t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane;
             key[u] = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
         }
-        uint32_t slot[kSegItems];  // (list << 24) | position within the block's share of that list
+        const uint64_t jw = t0 + ((uint64_t)(wave * kSegItems) << 6);  // the wave's first record
+        const uint32_t before = (jw > 0 && jw < n) ? (uint32_t)(a.rec_sorted[jw - 1] >> a.kshift) : 0xFFFFFFFFu;
 #pragma unroll
         for (int u = 0; u < kSegItems; ++u) {
-            const uint64_t j = t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane;
+            const uint32_t j_off = (uint32_t)((wave * kSegItems + u) << 6) + (uint32_t)lane;
             uint32_t kp = (uint32_t)__shfl_up((int)key[u], 1u, 64);
-            if (lane == 0) kp = (j < n && j > 0) ? (uint32_t)(a.rec_sorted[j - 1] >> a.kshift) : 0xFFFFFFFFu;
-            slot[u] = 0xFFFFFFFFu;
-            if (j < n && key[u] < a.K && key[u] != kp) {
-                // length probes: the segment is longer than m iff record j + m has the same flowId
-                auto longer = [&](uint64_t m) {
-                    return j + m < n && (uint32_t)(a.rec_sorted[j + m] >> a.kshift) == key[u];
-                };
-                uint32_t l = kClasses;
-                if (!longer(a.short_max)) {
-                    l = kClasses - 1;
-                    for (int c = kClasses - 2; c >= 0; --c)
-                        if (!longer(kClassMax[c])) l = (uint32_t)c;
-                }
-                slot[u] = (l << 24) | atomicAdd(&cnt[l], 1u);  // order within a list is irrelevant
+            if (lane == 0) kp = u == 0 ? before : (uint32_t)__shfl((int)key[u - 1], 63, 64);
+            if (t0 + j_off < n && key[u] < a.K && key[u] != kp) hpos[atomicAdd(&nheads, 1u)] = j_off;
+        }
+        __syncthreads();
+        // 2. classify the heads, one per thread: all length probes issued at once (the segment is longer
+        // than m iff record j + m has the same key; the class is the number of bounds it exceeds)
+        const uint32_t nh = nheads;
+        uint32_t slot[kSegTile / kSegThreads];
+#pragma unroll
+        for (int r = 0; r < (int)(kSegTile / kSegThreads); ++r) {
+            const uint32_t h = (uint32_t)r * kSegThreads + (uint32_t)tid;
+            slot[r] = 0xFFFFFFFFu;
+            if (h >= nh) continue;
+            const uint64_t j = t0 + hpos[h];
+            const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+            uint32_t pk[kClasses];
+#pragma unroll
+            for (int c = 0; c < kClasses; ++c) {
+                const uint64_t m = c < kClasses - 1 ? (uint64_t)kClassMax[c] : (uint64_t)a.short_max;
+                pk[c] = (j + m < n) ? (uint32_t)(a.rec_sorted[j + m] >> a.kshift) : 0xFFFFFFFFu;
             }
+            uint32_t l = 0;
+#pragma unroll
+            for (int c = 0; c < kClasses - 1; ++c) l += pk[c] == k ? 1u : 0u;
+            if (pk[kClasses - 1] == k) l = kClasses;  // longer than short_max: the wave walker
+            slot[r] = (l << 24) | atomicAdd(&cnt[l], 1u);  // order within a list is irrelevant
         }
         __syncthreads();
         if (tid < kL) {
@@ -689,14 +704,14 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kSegItems; ++u) {
-            if (slot[u] == 0xFFFFFFFFu) continue;
-            const uint32_t j = (uint32_t)(t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane);
-            const uint32_t l = slot[u] >> 24, pos = base[l] + (slot[u] & 0xFFFFFFu);
+        for (int r = 0; r < (int)(kSegTile / kSegThreads); ++r) {
+            if (slot[r] == 0xFFFFFFFFu) continue;
+            const uint32_t j = (uint32_t)(t0 + hpos[(uint32_t)r * kSegThreads + (uint32_t)tid]);
+            const uint32_t l = slot[r] >> 24, pos = base[l] + (slot[r] & 0xFFFFFFu);
             if (l == (uint32_t)kClasses) a.long_list[pos] = j;
             else a.short_list[a.class_off[l] + pos] = j;
         }
-        __syncthreads();  // cnt / base are reused by the next tile
+        __syncthreads();  // cnt / base / hpos are reused by the next tile
     }
 }
 
