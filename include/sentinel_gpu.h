@@ -161,6 +161,30 @@ typedef struct sg_param_req {
     int32_t  acquire;           /* acquireCount                                                    */
 } sg_param_req;
 
+/* ---- cluster hot-parameter tokens (TokenService.requestParamToken → ClusterParamFlowChecker) ---- */
+
+/* One cluster-mode ParamFlowRule with its ParamFlowClusterConfig (ParamFlowRule.java, ParamFlowClusterConfig.java). */
+typedef struct sg_cparam_rule {
+    int64_t  flow_id;            /* ParamFlowClusterConfig.flowId (> 0)                                   */
+    double   count;              /* ParamFlowRule.count (threshold of values without a hot item)         */
+    int32_t  threshold_type;     /* SG_THRESHOLD_AVG_LOCAL / SG_THRESHOLD_GLOBAL                           */
+    int32_t  sample_count;       /* ParamFlowClusterConfig.sampleCount, default 10                         */
+    int32_t  window_interval_ms; /* windowIntervalMs, default 1000                                         */
+    int32_t  namespace_id;       /* index into the sg_set_namespaces array                                 */
+    uint32_t hot_begin;          /* this rule's hot items (exclusive item counts): hot[hot_begin ..)     */
+    uint32_t hot_count;
+} sg_cparam_rule;
+
+/* requestParamToken(ruleId→key, acquireCount, params) at ts_ms; the parameter values are
+ * values[value_begin .. value_begin + value_count) of the batch's u64 value array. */
+typedef struct sg_cparam_req {
+    int64_t  ts_ms;
+    uint32_t key;                /* rule index, or SG_KEY_BAD / SG_KEY_NO_RULE                             */
+    int32_t  acquire;
+    uint32_t value_begin;
+    uint32_t value_count;        /* 0 → BAD_REQUEST (params empty, DefaultTokenService.java:54)            */
+} sg_cparam_req;
+
 /* ---- local slot chain: StatisticSlot → FlowSlot (DefaultController) → DegradeSlot (circuit breakers) ---- */
 
 /* DegradeRule (sentinel-core/.../slots/block/degrade/DegradeRule.java). */
@@ -264,6 +288,24 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
 int sg_param_decide_batch_host(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass);
 /* State of (rule, value): returns flags (bit0 time counter, bit1 token counter; 0 = absent) or < 0. */
 int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+
+/* ---- cluster hot-parameter tokens ----
+ *   sg_cparam_load_rules    ← ClusterParamFlowRuleManager.loadRules → applyClusterParamRules
+ *                             (…/flow/rule/ClusterParamFlowRuleManager.java:337-360): a surviving flowId keeps its
+ *                             ClusterParamMetric; each rule owns an exact 2^capacity_log2 value table (0 = 2^16).
+ *                             Rules of a namespace with a QPS limiter are SG_E_UNSUPPORTED on this path.
+ *   sg_cparam_decide_batch  ← TokenService.requestParamToken(Long, int, Collection<Object>)
+ *                             (DefaultTokenService.java:53-64 → ClusterParamFlowChecker.acquireClusterToken,
+ *                             ClusterParamFlowChecker.java:42-87), time-ordered; values[] holds every request's
+ *                             parameter values (u64; other types through the shim's value dictionary).
+ *   sg_cparam_read_sum      ← ClusterParamMetric.getSum(value) at now_ms (without currentWindow's side effect). */
+int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                         uint32_t n_hot, int32_t capacity_log2);
+int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                           uint64_t n_values, sg_result* out, void* stream);
+int sg_cparam_decide_batch_host(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                uint64_t n_values, sg_result* out);
+int sg_cparam_read_sum(sg_handle* h, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum);
 
 /* ---- local slot chain (the ProcessorSlot chain's statistic / flow / degrade slots, batched) ----
  *   sg_local_load_rules    ← FlowRuleManager.loadRules + DegradeRuleManager.loadRules for one resource each

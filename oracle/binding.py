@@ -73,6 +73,12 @@ def lib():
         "or_local_thread_num": (i64, [vp, u32]), "or_local_waiting": (i64, [vp, u32, i64]),
         "or_local_breaker_state": (C.c_int, [vp, u32, C.c_int, vp]),
         "or_local_dump": (C.c_int, [vp, u32, vp, vp, vp]),
+        "or_cts_load_param_rules": (C.c_int, [vp, vp, u32, vp, u32]),
+        "or_cts_decide_param": (C.c_int, [vp, vp, u64, vp, vp]),
+        "or_cts_param_sum": (i64, [vp, u32, u64, i64]),
+        "or_cpm_new": (vp, [C.c_int, C.c_int]), "or_cpm_free": (None, [vp]),
+        "or_cpm_add": (None, [vp, i64, u64, C.c_int]), "or_cpm_get_sum": (i64, [vp, i64, u64]),
+        "or_cpm_get_avg": (C.c_double, [vp, i64, u64]),
         "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
@@ -236,6 +242,24 @@ class ClusterTokenService:
     def avg(self, key, now, ev):
         return lib().or_cts_avg(self.h, key, now, ev)
 
+    # ---- requestParamToken → ClusterParamFlowChecker
+    def load_param_rules(self, rules: np.ndarray, hot: np.ndarray = None):
+        rules = np.ascontiguousarray(rules, dtype=abi.CPARAM_RULE_DTYPE)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        rc = lib().or_cts_load_param_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot))
+        if rc != 0:
+            raise ValueError(f"invalid param rules ({rc})")
+
+    def decide_param(self, req: np.ndarray, values: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.CPARAM_REQ_DTYPE)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.zeros(len(req), dtype=abi.RES_DTYPE)
+        lib().or_cts_decide_param(self.h, abi.ptr(req), len(req), abi.ptr(values), abi.ptr(out))
+        return out
+
+    def param_sum(self, key, value, now):
+        return lib().or_cts_param_sum(self.h, key, int(value), now)
+
     def read_state(self, key):
         S = lib().or_cts_sample_count(self.h, key)
         starts = np.zeros(S, np.int64)
@@ -244,6 +268,28 @@ class ClusterTokenService:
         rc = lib().or_cts_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ))
         assert rc == 0
         return starts, counters.reshape(S, abi.NUM_EVENTS), occ
+
+
+class ClusterParamMetric:
+    """ClusterParamMetric (ClusterParamMetric.java) with explicit time; values are u64."""
+
+    def __init__(self, sample_count, interval_ms):
+        self.h = lib().or_cpm_new(sample_count, interval_ms)
+        assert self.h
+
+    def __del__(self):
+        if self.h:
+            lib().or_cpm_free(self.h)
+            self.h = None
+
+    def add_value(self, t, value, count):
+        lib().or_cpm_add(self.h, t, int(value), count)
+
+    def get_sum(self, t, value):
+        return lib().or_cpm_get_sum(self.h, t, int(value))
+
+    def get_avg(self, t, value):
+        return lib().or_cpm_get_avg(self.h, t, int(value))
 
 
 class ParamFlowChecker:

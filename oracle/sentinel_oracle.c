@@ -388,7 +388,18 @@ typedef struct or_cts_rule {
     or_leap* metric; /* ClusterMetricStatistics.METRIC_MAP[flowId] */
 } or_cts_rule;
 
+typedef struct or_cpm or_cpm;  /* ClusterParamMetric, below */
+
+typedef struct or_cpr {        /* one cluster ParamFlowRule + its metric */
+    sg_cparam_rule rule;
+    const sg_param_hot_item* hot;  /* into or_cts.phot */
+    or_cpm* metric;            /* ClusterParamMetricStatistics.METRIC_MAP[flowId] */
+} or_cpr;
+
 struct or_cts {
+    or_cpr* prules;
+    uint32_t n_prules;
+    sg_param_hot_item* phot;
     double exceed_count;
     double max_occupy_ratio;
     or_cts_rule* rules;
@@ -405,7 +416,12 @@ or_cts* or_cts_new(double exceed_count, double max_occupy_ratio) {
     return s;
 }
 
+static void cpm_free(or_cpm* m);
+
 void or_cts_free(or_cts* s) {
+    for (uint32_t j = 0; j < s->n_prules; j++) cpm_free(s->prules[j].metric);
+    free(s->prules);
+    free(s->phot);
     if (!s) return;
     for (uint32_t i = 0; i < s->n_rules; i++) or_leap_free(s->rules[i].metric);
     free(s->rules);
@@ -1164,3 +1180,233 @@ int or_local_breaker_stat(const or_local* l, uint32_t res, int i, int64_t* start
     *total = s->present[0] ? s->b[0].c[1] : 0;
     return 0;
 }
+
+
+/* ===================================================================================== */
+/* ClusterParamMetric (srv/flow/statistic/metric/ClusterParamMetric.java:37-88) over a    */
+/* ClusterParameterLeapArray (…/ClusterParameterLeapArray.java:29-51): a LeapArray whose   */
+/* buckets are value → LongAdder maps; a reset clears the whole map.                       */
+/* ===================================================================================== */
+
+typedef struct or_vmap {       /* open-addressing u64 → i64 map (a bucket's CacheMap, no eviction) */
+    uint64_t* k;
+    int64_t* v;
+    uint8_t* used;
+    uint32_t cap, n;
+} or_vmap;
+
+static void vmap_clear(or_vmap* m) {
+    if (m->used) memset(m->used, 0, m->cap);
+    m->n = 0;
+}
+
+static int64_t* vmap_find(const or_vmap* m, uint64_t key) {
+    if (!m->cap) return NULL;
+    uint32_t i = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (m->cap - 1);
+    while (m->used[i]) {
+        if (m->k[i] == key) return &m->v[i];
+        i = (i + 1) & (m->cap - 1);
+    }
+    return NULL;
+}
+
+static int64_t* vmap_get_or_add(or_vmap* m, uint64_t key) {
+    int64_t* f = vmap_find(m, key);
+    if (f) return f;
+    if (2 * (m->n + 1) > m->cap) {
+        or_vmap g = {0};
+        g.cap = m->cap ? 2 * m->cap : 16;
+        g.k = (uint64_t*)calloc(g.cap, 8);
+        g.v = (int64_t*)calloc(g.cap, 8);
+        g.used = (uint8_t*)calloc(g.cap, 1);
+        for (uint32_t i = 0; i < m->cap; i++)
+            if (m->used[i]) *vmap_get_or_add(&g, m->k[i]) = m->v[i];
+        free(m->k);
+        free(m->v);
+        free(m->used);
+        *m = g;
+    }
+    uint32_t i = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & (m->cap - 1);
+    while (m->used[i]) i = (i + 1) & (m->cap - 1);
+    m->used[i] = 1;
+    m->k[i] = key;
+    m->v[i] = 0;
+    m->n++;
+    return &m->v[i];
+}
+
+struct or_cpm {
+    int S, wl, interval;
+    double isec;
+    uint8_t* present;
+    int64_t* start;
+    or_vmap* maps;
+};
+
+static or_cpm* cpm_new(int S, int interval) {
+    if (S <= 0 || interval <= 0 || interval % S != 0) return NULL;
+    or_cpm* m = (or_cpm*)calloc(1, sizeof(or_cpm));
+    m->S = S;
+    m->wl = interval / S;
+    m->interval = interval;
+    m->isec = interval / 1000.0;  /* LeapArray.intervalInSecond */
+    m->present = (uint8_t*)calloc(S, 1);
+    m->start = (int64_t*)calloc(S, 8);
+    m->maps = (or_vmap*)calloc(S, sizeof(or_vmap));
+    return m;
+}
+
+static void cpm_free(or_cpm* m) {
+    if (!m) return;
+    for (int i = 0; i < m->S; i++) {
+        free(m->maps[i].k);
+        free(m->maps[i].v);
+        free(m->maps[i].used);
+    }
+    free(m->maps);
+    free(m->start);
+    free(m->present);
+    free(m);
+}
+
+/* LeapArray.currentWindow (LeapArray.java:116-202) with ClusterParameterLeapArray.newEmptyBucket (:43-45,
+ * an empty map) and resetWindowTo (:47-51, clear the map). Returns the slot, -2 for a detached bucket. */
+static int cpm_current_window(or_cpm* m, int64_t t) {
+    int idx = (int)((t / m->wl) % m->S);
+    int64_t ws = t - t % m->wl;
+    if (!m->present[idx]) {
+        m->present[idx] = 1;
+        m->start[idx] = ws;
+        vmap_clear(&m->maps[idx]);
+        return idx;
+    }
+    if (ws == m->start[idx]) return idx;
+    if (ws > m->start[idx]) {
+        m->start[idx] = ws;
+        vmap_clear(&m->maps[idx]);
+        return idx;
+    }
+    return -2;
+}
+
+/* ClusterParamMetric.getSum(value), :48-61: currentWindow(); Σ over values() of bucket.get(value) */
+static int64_t cpm_get_sum(or_cpm* m, int64_t t, uint64_t value) {
+    cpm_current_window(m, t);
+    int64_t sum = 0;
+    for (int i = 0; i < m->S; i++) {
+        if (!m->present[i] || t - m->start[i] > m->interval) continue;  /* isWindowDeprecated */
+        const int64_t* c = vmap_find(&m->maps[i], value);
+        if (c) sum += *c;
+    }
+    return sum;
+}
+
+/* ClusterParamMetric.addValue(value, count), :67-78 (a detached bucket's adds are lost) */
+static void cpm_add(or_cpm* m, int64_t t, uint64_t value, int count) {
+    int s = cpm_current_window(m, t);
+    if (s < 0) return;
+    *vmap_get_or_add(&m->maps[s], value) += count;
+}
+
+/* ClusterParamFlowRuleManager.applyClusterParamRules (…/ClusterParamFlowRuleManager.java:337-360): a flowId
+ * that survives keeps its metric (putMetricIfAbsent :354-355), removed ones lose it. */
+int or_cts_load_param_rules(or_cts* s, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                            uint32_t n_hot) {
+    or_cpr* nr = (or_cpr*)calloc(n ? n : 1, sizeof(or_cpr));
+    sg_param_hot_item* ph = (sg_param_hot_item*)calloc(n_hot ? n_hot : 1, sizeof(sg_param_hot_item));
+    memcpy(ph, hot, n_hot * sizeof(sg_param_hot_item));
+    for (uint32_t i = 0; i < n; i++) {
+        nr[i].rule = rules[i];
+        nr[i].hot = ph + rules[i].hot_begin;
+        for (uint32_t j = 0; j < s->n_prules; j++) {
+            if (s->prules[j].metric && s->prules[j].rule.flow_id == rules[i].flow_id) {
+                nr[i].metric = s->prules[j].metric;
+                s->prules[j].metric = NULL;
+                break;
+            }
+        }
+        if (!nr[i].metric) nr[i].metric = cpm_new(rules[i].sample_count, rules[i].window_interval_ms);
+        if (!nr[i].metric) return SG_E_INVAL;
+    }
+    for (uint32_t j = 0; j < s->n_prules; j++) cpm_free(s->prules[j].metric);
+    free(s->prules);
+    free(s->phot);
+    s->prules = nr;
+    s->n_prules = n;
+    s->phot = ph;
+    return 0;
+}
+
+/* ClusterParamFlowChecker.calcGlobalThreshold / getRawThreshold (:96-116): the value's exclusive item count
+ * (ParamFlowRule.retrieveExclusiveItemCount) or rule.count; AVG_LOCAL multiplies by the connected count.
+ * (No exceedCount here, unlike ClusterFlowChecker.) */
+static double cparam_threshold(const or_cts* s, const or_cpr* r, uint64_t value) {
+    double count = r->rule.count;
+    for (uint32_t i = 0; i < r->rule.hot_count; i++)
+        if (r->hot[i].value == value) {
+            count = (double)r->hot[i].threshold;
+            break;
+        }
+    if (r->rule.threshold_type == SG_THRESHOLD_GLOBAL) return count;
+    int ns = r->rule.namespace_id;
+    int connected = (ns >= 0 && (uint32_t)ns < s->n_ns) ? s->ns[ns].connected_count : 0;
+    return count * connected;
+}
+
+/* DefaultTokenService.requestParamToken (DefaultTokenService.java:53-64) → ClusterParamFlowChecker.
+ * acquireClusterToken (ClusterParamFlowChecker.java:42-87): all values are checked (first failure blocks,
+ * nothing added), then the count is added to every value. */
+int or_cts_decide_param(or_cts* s, const sg_cparam_req* req, uint64_t n, const uint64_t* values, sg_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        const sg_cparam_req* q = &req[i];
+        uint32_t key = q->key & SG_KEY_INDEX;
+        if (key == SG_KEY_BAD || q->acquire <= 0 || q->value_count == 0) {
+            out[i] = mk(SG_STATUS_BAD_REQUEST, 0, 0);
+            continue;
+        }
+        if (key >= s->n_prules) {
+            out[i] = mk(SG_STATUS_NO_RULE_EXISTS, 0, 0);
+            continue;
+        }
+        or_cpr* r = &s->prules[key];
+        int64_t t = q->ts_ms;
+        int ns = r->rule.namespace_id;  /* allowProceed → GlobalRequestLimiter.tryPass(namespace) */
+        if (ns < 0 || (uint32_t)ns >= s->n_ns) {
+            out[i] = mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0);
+            continue;
+        }
+        if (s->limiters[ns] && !or_limiter_try_pass(s->limiters[ns], t)) {
+            out[i] = mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0);
+            continue;
+        }
+        double remaining = -1;
+        int passed = 1;
+        for (uint32_t v = 0; v < q->value_count; v++) {
+            uint64_t value = values[q->value_begin + v];
+            double latest = (double)cpm_get_sum(r->metric, t, value) / r->metric->isec;  /* getAvg */
+            double next_remaining = cparam_threshold(s, r, value) - latest - q->acquire;
+            remaining = next_remaining;
+            if (next_remaining < 0) {
+                passed = 0;
+                break;
+            }
+        }
+        if (passed)
+            for (uint32_t v = 0; v < q->value_count; v++) cpm_add(r->metric, t, values[q->value_begin + v], q->acquire);
+        if (q->value_count > 1) remaining = -1;  /* remaining is unsupported for multi-values */
+        out[i] = passed ? mk(SG_STATUS_OK, or_d2i(remaining), 0) : mk(SG_STATUS_BLOCKED, 0, 0);
+    }
+    return 0;
+}
+
+int64_t or_cts_param_sum(or_cts* s, uint32_t key, uint64_t value, int64_t now) {
+    if (key >= s->n_prules) return 0;
+    return cpm_get_sum(s->prules[key].metric, now, value);
+}
+
+/* Standalone ClusterParamMetric for the known-answer tests (ClusterParamMetricTest.java). */
+or_cpm* or_cpm_new(int sample_count, int interval_ms) { return cpm_new(sample_count, interval_ms); }
+void or_cpm_free(or_cpm* m) { cpm_free(m); }
+void or_cpm_add(or_cpm* m, int64_t t, uint64_t value, int count) { cpm_add(m, t, value, count); }
+int64_t or_cpm_get_sum(or_cpm* m, int64_t t, uint64_t value) { return cpm_get_sum(m, t, value); }
+double or_cpm_get_avg(or_cpm* m, int64_t t, uint64_t value) { return (double)cpm_get_sum(m, t, value) / m->isec; }

@@ -100,6 +100,19 @@ int     or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_
 int     or_cts_sample_count(const or_cts* s, uint32_t key);
 double  or_cts_avg(or_cts* s, uint32_t key, int64_t now, int ev);
 
+/* ---------- cluster hot-parameter tokens (ClusterParamFlowChecker over ClusterParamMetric) ---------- */
+int     or_cts_load_param_rules(or_cts* s, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                                uint32_t n_hot);
+int     or_cts_decide_param(or_cts* s, const sg_cparam_req* req, uint64_t n, const uint64_t* values, sg_result* out);
+typedef struct or_cpm or_cpm;  /* ClusterParamMetric */
+or_cpm* or_cpm_new(int sample_count, int interval_ms);
+void    or_cpm_free(or_cpm* m);
+void    or_cpm_add(or_cpm* m, int64_t t, uint64_t value, int count);
+int64_t or_cpm_get_sum(or_cpm* m, int64_t t, uint64_t value);
+double  or_cpm_get_avg(or_cpm* m, int64_t t, uint64_t value);
+/* ClusterParamMetric.getSum(value) of param rule `key` at `now` (with its currentWindow side effect). */
+int64_t or_cts_param_sum(or_cts* s, uint32_t key, uint64_t value, int64_t now);
+
 /* ---------- hot-parameter flow control (ParamFlowChecker QPS paths, exact unbounded maps) ---------- */
 typedef struct or_pf or_pf;
 or_pf*  or_pf_new(void);

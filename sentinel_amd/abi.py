@@ -82,6 +82,11 @@ PARAM_RULE_DTYPE = np.dtype([("count", "<f8"), ("duration_sec", "<i8"), ("burst"
                              ("capacity_log2", "<i4")], align=True)
 PARAM_HOT_DTYPE = np.dtype([("value", "<u8"), ("threshold", "<i4"), ("reserved", "<i4")], align=True)
 PARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("value", "<u8"), ("rule", "<u4"), ("acquire", "<i4")], align=True)
+CPARAM_RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
+                              ("window_interval_ms", "<i4"), ("namespace_id", "<i4"), ("hot_begin", "<u4"),
+                              ("hot_count", "<u4")], align=True)
+CPARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4"), ("value_begin", "<u4"),
+                             ("value_count", "<u4")], align=True)
 BEHAVIOR_DEFAULT = 0
 BEHAVIOR_RATE_LIMITER = 2
 
@@ -108,6 +113,7 @@ assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
 assert RES_DTYPE.itemsize == C.sizeof(sg_result) == 12
 assert RULE_DTYPE.itemsize == C.sizeof(sg_flow_rule) == 32
 assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
+assert CPARAM_RULE_DTYPE.itemsize == 40 and CPARAM_REQ_DTYPE.itemsize == 24
 assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 

@@ -79,6 +79,22 @@ struct sg_handle {
     sg_param_req* d_preq_h = nullptr;
     int32_t* d_pout_h = nullptr;
 
+    // cluster hot-parameter tokens
+    std::vector<sg_cparam_rule> cprules;
+    std::vector<CPRule> cptab;
+    CPRule* d_cprules = nullptr;
+    sg_param_hot_item* d_cphot = nullptr;
+    uint64_t* d_cpkeys = nullptr;
+    CPBucket* d_cpring = nullptr;
+    uint64_t cptotal = 0;
+    int cpstride = 1;
+    int64_t* d_cplast_ts = nullptr;
+    uint32_t* d_cpmulti = nullptr;    // [1 + max_batch]: count, then indices of multi-value requests
+    sg_cparam_req* d_cpreq_h = nullptr;
+    uint64_t* d_cpval_h = nullptr;
+    uint64_t cpval_cap = 0;
+    sg_result* d_cpout_h = nullptr;
+
     // local slot chain
     sg_local_config lcfg{2, 1000, 500, 0};
     std::vector<LRule> ltab;
@@ -322,6 +338,15 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_preq_h);
     dfree(h->d_pout_h);
     dfree(h->d_skip_count);
+    dfree(h->d_cprules);
+    dfree(h->d_cphot);
+    dfree(h->d_cpkeys);
+    dfree(h->d_cpring);
+    dfree(h->d_cplast_ts);
+    dfree(h->d_cpmulti);
+    dfree(h->d_cpreq_h);
+    dfree(h->d_cpval_h);
+    dfree(h->d_cpout_h);
     dfree(h->d_lrules);
     dfree(h->d_lhead);
     dfree(h->d_lsec);
@@ -388,6 +413,13 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
     h->ns.assign(ns, ns + n);
     h->ns_slot = slot;
     h->n_lim = n_lim;
+    if (!h->cptab.empty()) {  // AVG_LOCAL param thresholds follow the connected counts
+        for (size_t i = 0; i < h->cptab.size(); ++i) {
+            const int nsi = h->cprules[i].namespace_id;
+            h->cptab[i].connected = (nsi >= 0 && (uint32_t)nsi < n) ? ns[nsi].connected_count : 0;
+        }
+        HIP_TRY(h, hipMemcpy(h->d_cprules, h->cptab.data(), sizeof(CPRule) * h->cptab.size(), hipMemcpyHostToDevice));
+    }
     return upload_rule_table(h);
 }
 
@@ -795,6 +827,216 @@ int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* la
     *last_time = s->time;
     *tokens = s->tokens;
     return (int)s->flags;
+}
+
+// --------------------------------------------------------------------- cluster hot-parameter tokens
+
+// ClusterParamFlowRuleManager.loadRules → applyClusterParamRules (…/ClusterParamFlowRuleManager.java:337-360):
+// a flowId that survives keeps its metric (and its window shape), the others start empty.
+int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                         uint32_t n_hot, int32_t capacity_log2) {
+    if (!h || (!rules && n) || (!hot && n_hot)) return SG_E_INVAL;
+    if (n >= SG_KEY_BAD) return fail(h, SG_E_INVAL, "too many rules");
+    const int lg = capacity_log2 ? capacity_log2 : 16;
+    if (lg < 1 || lg > 28) return fail(h, SG_E_INVAL, "capacity_log2 must be in [1, 28]");
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::unordered_map<int64_t, uint32_t> seen, old_index;
+    for (uint32_t k = 0; k < h->cprules.size(); ++k) old_index.emplace(h->cprules[k].flow_id, k);
+    std::vector<CPRule> tab(n);
+    std::vector<sg_param_hot_item> hs(hot, hot + n_hot);
+    int stride = 1;
+    uint64_t base = 0;
+    const uint64_t per = (1ull << lg) + 1;  // + the side slot
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_cparam_rule& r = rules[i];
+        if (r.flow_id <= 0 || !(r.count >= 0)) return fail(h, SG_E_INVAL, "invalid param rule");
+        if (r.sample_count <= 0 || r.window_interval_ms <= 0 || r.window_interval_ms % r.sample_count != 0)
+            return fail(h, SG_E_INVAL, "invalid window config");
+        if (r.namespace_id < 0 || (size_t)r.namespace_id >= h->ns.size()) return fail(h, SG_E_INVAL, "unknown namespace");
+        if ((size_t)r.namespace_id < h->ns_slot.size() && h->ns_slot[r.namespace_id] >= 0)
+            return fail(h, SG_E_UNSUPPORTED, "param rules in a namespace with a QPS limiter");
+        if ((uint64_t)r.hot_begin + r.hot_count > n_hot) return fail(h, SG_E_INVAL, "hot item range out of bounds");
+        if (!seen.emplace(r.flow_id, i).second) return fail(h, SG_E_INVAL, "duplicate flowId");
+        int S = r.sample_count, interval = r.window_interval_ms;
+        auto it = old_index.find(r.flow_id);
+        if (it != old_index.end()) {  // the existing metric keeps its window shape
+            S = h->cptab[it->second].S;
+            interval = h->cptab[it->second].S * h->cptab[it->second].wl;
+        }
+        if (S > SG_MAX_SAMPLE_COUNT) return fail(h, SG_E_UNSUPPORTED, "sampleCount > 64");
+        CPRule& R = tab[i];
+        R.count = r.count;
+        R.isec = interval / 1000.0;
+        R.S = S;
+        R.wl = interval / S;
+        R.global = r.threshold_type == SG_THRESHOLD_GLOBAL;
+        R.connected = h->ns[r.namespace_id].connected_count;
+        R.hot_begin = r.hot_begin;
+        R.hot_count = r.hot_count;
+        R.table_base = base;
+        R.table_mask = (1ull << lg) - 1;
+        base += per;
+        stride = std::max(stride, S);
+        std::sort(hs.begin() + r.hot_begin, hs.begin() + r.hot_begin + r.hot_count,
+                  [](const sg_param_hot_item& x, const sg_param_hot_item& y) { return x.value < y.value; });
+    }
+    if (base >= (1ull << 32)) return fail(h, SG_E_UNSUPPORTED, "param tables larger than 2^32 slots");
+    CPRule* d_rules = nullptr;
+    sg_param_hot_item* d_hot = nullptr;
+    uint64_t* d_keys = nullptr;
+    CPBucket* d_ring = nullptr;
+    if (n) {
+        if (hipMalloc(&d_rules, sizeof(CPRule) * n) != hipSuccess || hipMalloc(&d_keys, 8 * base) != hipSuccess ||
+            hipMalloc(&d_ring, sizeof(CPBucket) * base * stride) != hipSuccess ||
+            (n_hot && hipMalloc(&d_hot, sizeof(sg_param_hot_item) * n_hot) != hipSuccess)) {
+            dfree(d_rules);
+            dfree(d_keys);
+            dfree(d_ring);
+            dfree(d_hot);
+            return fail(h, SG_E_NOMEM, "param table allocation");
+        }
+        HIP_TRY(h, hipMemcpy(d_rules, tab.data(), sizeof(CPRule) * n, hipMemcpyHostToDevice));
+        if (n_hot) HIP_TRY(h, hipMemcpy(d_hot, hs.data(), sizeof(sg_param_hot_item) * n_hot, hipMemcpyHostToDevice));
+        HIP_TRY(h, launch_cp_clear(d_keys, d_ring, base, stride, 0));
+        for (uint32_t i = 0; i < n; ++i) {  // surviving flowIds: move their sub-tables
+            auto it = old_index.find(rules[i].flow_id);
+            if (it == old_index.end()) continue;
+            const CPRule& O = h->cptab[it->second];
+            const uint64_t slots = std::min(O.table_mask, tab[i].table_mask) + 2;
+            if (O.table_mask != tab[i].table_mask) return fail(h, SG_E_UNSUPPORTED, "capacity change of a live param rule");
+            HIP_TRY(h, launch_cp_copy(h->d_cpkeys, h->d_cpring, O.table_base, h->cpstride, d_keys, d_ring, tab[i].table_base,
+                                      stride, slots, O.S, 0));
+        }
+        HIP_TRY(h, hipDeviceSynchronize());
+    }
+    dfree(h->d_cprules);
+    dfree(h->d_cphot);
+    dfree(h->d_cpkeys);
+    dfree(h->d_cpring);
+    h->d_cprules = d_rules;
+    h->d_cphot = d_hot;
+    h->d_cpkeys = d_keys;
+    h->d_cpring = d_ring;
+    h->cprules.assign(rules, rules + n);
+    h->cptab = tab;
+    h->cptotal = base;
+    h->cpstride = stride;
+    if (!h->d_cplast_ts) {
+        if (hipMalloc(&h->d_cplast_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "ts");
+        const int64_t neg = -1;
+        HIP_TRY(h, hipMemcpy(h->d_cplast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
+    }
+    return SG_OK;
+}
+
+static CPArgs cp_args(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values, uint64_t n_values,
+                      sg_result* out) {
+    CPArgs c{};
+    c.req = req;
+    c.values = values;
+    c.n_values = n_values;
+    c.out = out;
+    c.n = n;
+    c.ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
+    c.imask = (1ull << c.ibits) - 1;
+    c.rules = h->d_cprules;
+    c.n_rules = (uint32_t)h->cptab.size();
+    c.hot = h->d_cphot;
+    c.keys = h->d_cpkeys;
+    c.ring = h->d_cpring;
+    c.stride = h->cpstride;
+    c.total_slots = h->cptotal;
+    c.err = h->d_err;
+    c.last_ts = h->d_cplast_ts;
+    return c;
+}
+
+int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                           uint64_t n_values, sg_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out || (!values && n_values)) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    if (!h->d_cplast_ts) return fail(h, SG_E_INVAL, "sg_cparam_load_rules first");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    CPArgs c = cp_args(h, req, n, values, n_values, out);
+    const int gbits = bits_for(h->cptotal + 1);
+    if (c.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
+    if (!h->d_cpmulti && hipMalloc(&h->d_cpmulti, sizeof(uint32_t) * (h->cfg.max_batch + 1)) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "multi-value list");
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    // requests with several values: decided one at a time between the single-value runs
+    HIP_TRY(h, hipMemsetAsync(h->d_cpmulti, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_cp_count_multi(c, h->d_cpmulti + 1, h->d_cpmulti, stream));
+    uint32_t n_multi = 0;
+    HIP_TRY(h, hipMemcpyAsync(&n_multi, h->d_cpmulti, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    std::vector<uint32_t> multi(n_multi);
+    if (n_multi)
+        HIP_TRY(h, hipMemcpy(multi.data(), h->d_cpmulti + 1, sizeof(uint32_t) * n_multi, hipMemcpyDeviceToHost));
+    std::sort(multi.begin(), multi.end());
+    BatchArgs sgm{};
+    sgm.kshift = c.ibits;
+    sgm.K = (uint32_t)h->cptotal;
+    sgm.err = h->d_err;
+    sgm.long_list = h->d_long_list;
+    sgm.long_count = h->d_long_count;
+    sgm.short_list = h->d_short_list;
+    sgm.short_count = h->d_long_count + 1;
+    for (int cl = 0; cl < kClasses; ++cl) sgm.class_off[cl] = h->class_off[cl];
+    sgm.short_max = 0xFFFFFFFFu;  // one lane per (rule, value)
+    uint64_t lo = 0;
+    for (size_t mi = 0; mi <= multi.size(); ++mi) {
+        const uint64_t hi = mi < multi.size() ? multi[mi] : n;
+        HIP_TRY(h, launch_cp_range(c, sgm, lo, hi, h->d_rec, h->d_rec_sorted, h->d_hist, c.ibits, c.ibits + gbits, stream));
+        if (mi < multi.size()) HIP_TRY(h, launch_cp_multi(c, hi, stream));
+        lo = hi + 1;
+    }
+    int err = 0;
+    HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (err & kErrTime) return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (err & kErrBounds) return fail(h, SG_E_INVAL, "a request's values lie outside the value array");
+    if (err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param rule's value table is full");
+    return SG_OK;
+}
+
+int sg_cparam_decide_batch_host(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                uint64_t n_values, sg_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_cpreq_h) {
+        if (hipMalloc(&h->d_cpreq_h, sizeof(sg_cparam_req) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_cpout_h, sizeof(sg_result) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    if (n_values > h->cpval_cap) {
+        dfree(h->d_cpval_h);
+        if (hipMalloc(&h->d_cpval_h, 8 * n_values) != hipSuccess) return fail(h, SG_E_NOMEM, "host-path values");
+        h->cpval_cap = n_values;
+    }
+    HIP_TRY(h, hipMemcpy(h->d_cpreq_h, req, sizeof(sg_cparam_req) * n, hipMemcpyHostToDevice));
+    if (n_values) HIP_TRY(h, hipMemcpy(h->d_cpval_h, values, 8 * n_values, hipMemcpyHostToDevice));
+    int rc = sg_cparam_decide_batch(h, h->d_cpreq_h, n, h->d_cpval_h, n_values, h->d_cpout_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(out, h->d_cpout_h, sizeof(sg_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_cparam_read_sum(sg_handle* h, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum) {
+    if (!h || !sum || rule >= h->cptab.size()) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    int64_t* d = nullptr;
+    HIP_TRY(h, hipMalloc(&d, sizeof(int64_t)));
+    CPArgs c = cp_args(h, nullptr, 0, nullptr, 0, nullptr);
+    hipError_t e = launch_cp_read(c, rule, value, now_ms, d, 0);
+    if (e == hipSuccess) e = hipMemcpy(sum, d, sizeof(int64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    return SG_OK;
 }
 
 // ------------------------------------------------------------------------------ local slot chain

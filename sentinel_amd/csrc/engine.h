@@ -168,6 +168,55 @@ hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
 hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
                               uint64_t** sorted_out, hipStream_t stream);
 
+// ---- cluster hot-parameter tokens (cparam.hip) ----
+constexpr int kErrBounds = 32;      // a request's values lie outside the batch's value array
+
+struct CPRule {
+    double count;             // ParamFlowRule.count
+    double isec;              // windowIntervalMs / 1000.0
+    int32_t S;                // sampleCount of the flowId's metric
+    int32_t wl;               // windowIntervalMs / sampleCount
+    int32_t global;           // thresholdType == FLOW_THRESHOLD_GLOBAL
+    int32_t connected;        // connectedCount of its namespace (AVG_LOCAL)
+    uint32_t hot_begin, hot_count;
+    uint64_t table_base;      // first slot of this rule's (value → ring) sub-table
+    uint64_t table_mask;      // 2^capacity_log2 - 1; slot table_base + mask + 1 holds the value ~0
+};
+
+struct CPBucket {             // one bucket of a (flowId, value) ring: window start, the value's count
+    int64_t start;            // INT64_MIN: never written
+    int64_t count;
+};
+
+struct CPArgs {
+    const sg_cparam_req* req;
+    const uint64_t* values;
+    uint64_t n_values;
+    sg_result* out;
+    uint64_t n;
+    uint64_t* rec;            // {slot : high bits | request index - lo : ibits}
+    int ibits;
+    uint64_t imask;
+    const CPRule* rules;
+    uint32_t n_rules;
+    const sg_param_hot_item* hot;  // per rule, sorted by value
+    uint64_t* keys;           // [total_slots] value of each slot (~0 = empty)
+    CPBucket* ring;           // [total_slots][stride]
+    int stride;
+    uint64_t total_slots;
+    int* err;
+    int64_t* last_ts;
+};
+
+hipError_t launch_cp_clear(uint64_t* keys, CPBucket* ring, uint64_t slots, int stride, hipStream_t stream);
+hipError_t launch_cp_copy(const uint64_t* okeys, const CPBucket* oring, uint64_t obase, int ostride, uint64_t* nkeys,
+                          CPBucket* nring, uint64_t nbase, int nstride, uint64_t slots, int S, hipStream_t stream);
+hipError_t launch_cp_count_multi(const CPArgs& c, uint32_t* list, uint32_t* count, hipStream_t stream);
+hipError_t launch_cp_range(const CPArgs& c, BatchArgs& sg, uint64_t lo, uint64_t hi, uint64_t* a_buf, uint64_t* b_buf,
+                           uint32_t* hist, int lo_bit, int hi_bit, hipStream_t stream);
+hipError_t launch_cp_multi(const CPArgs& c, uint64_t m, hipStream_t stream);
+hipError_t launch_cp_read(const CPArgs& c, uint32_t rule, uint64_t value, int64_t now, int64_t* out_dev, hipStream_t stream);
+
 // ---- local slot chain: StatisticSlot → FlowSlot(DefaultController) → DegradeSlot (local.hip) ----
 constexpr int kLEv = 6;             // MetricEvent PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS
 constexpr int kLPass = 0, kLBlock = 1, kLExc = 2, kLSucc = 3, kLRt = 4, kLOccPass = 5;

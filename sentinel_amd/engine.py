@@ -16,6 +16,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
            "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
+           "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state"]
 
 _lib = None
@@ -57,6 +58,10 @@ def load_library():
         "sg_param_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "sg_build_info": (C.c_char_p, []),
         "sg_local_load_rules": (C.c_int, [vp, vp, vp, u32]),
+        "sg_cparam_load_rules": (C.c_int, [vp, vp, u32, vp, u32, C.c_int32]),
+        "sg_cparam_decide_batch": (C.c_int, [vp, vp, u64, vp, u64, vp, vp]),
+        "sg_cparam_decide_batch_host": (C.c_int, [vp, vp, u64, vp, u64, vp]),
+        "sg_cparam_read_sum": (C.c_int, [vp, u32, u64, i64, vp]),
         "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
@@ -200,3 +205,23 @@ class FlowEngine:
         head = np.zeros(14, np.int64)
         self._check(self._L.sg_local_read_state(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), abi.ptr(head)))
         return sec, bor, mnt, head
+
+    # ---- cluster hot-parameter tokens (requestParamToken → ClusterParamFlowChecker)
+    def cparam_load_rules(self, rules: np.ndarray, hot: np.ndarray = None, capacity_log2=0):
+        rules = np.ascontiguousarray(rules, dtype=abi.CPARAM_RULE_DTYPE)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        self._check(self._L.sg_cparam_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot),
+                                                 capacity_log2))
+
+    def cparam_decide_host(self, req: np.ndarray, values: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.CPARAM_REQ_DTYPE)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.zeros(len(req), abi.RES_DTYPE)
+        self._check(self._L.sg_cparam_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(values), len(values),
+                                                         abi.ptr(out)))
+        return out
+
+    def cparam_sum(self, rule, value, now):
+        v = C.c_int64()
+        self._check(self._L.sg_cparam_read_sum(self.h, rule, int(value), now, C.byref(v)))
+        return v.value

@@ -1,0 +1,134 @@
+"""Parity of the device cluster hot-parameter path (sg_cparam_*: requestParamToken → ClusterParamFlowChecker)
+with the oracle (oracle.binding.ClusterTokenService.decide_param, a literal restatement of ClusterParamMetric's
+per-flowId LeapArray of value → count maps): every TokenResult and every (rule, value) window sum, bit-exact."""
+import numpy as np
+import pytest
+
+from oracle.binding import ClusterTokenService
+from sentinel_amd import abi
+from sentinel_amd.workload import zipf_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(rules, hot=None, connected=1, cap=12):
+    from sentinel_amd.engine import FlowEngine
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = connected
+    eng = FlowEngine(device=0, max_batch=1 << 20)
+    eng.set_namespaces(ns)
+    eng.cparam_load_rules(rules, hot, cap)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_param_rules(rules, hot)
+    return eng, ora
+
+
+def _rules(n, rng, S=10, interval=1000, thr=abi.THRESHOLD_GLOBAL, hot_per_rule=0):
+    r = np.zeros(n, abi.CPARAM_RULE_DTYPE)
+    r["flow_id"] = np.arange(n) * 3 + 7
+    r["count"] = rng.integers(1, 40, n)
+    r["threshold_type"] = thr
+    r["sample_count"] = S
+    r["window_interval_ms"] = interval
+    r["hot_begin"] = np.arange(n) * hot_per_rule
+    r["hot_count"] = hot_per_rule
+    return r
+
+
+def _trace(rng, n, n_rules, n_values, t0, span, multi=0.0, zipf=1.1, acq_hi=3, bad=0.0):
+    req = np.zeros(n, abi.CPARAM_REQ_DTYPE)
+    req["ts_ms"] = t0 + np.sort(rng.integers(0, max(span, 1), n))
+    req["key"] = rng.integers(0, n_rules, n)
+    req["acquire"] = rng.integers(1, acq_hi + 1, n)
+    counts = np.where(rng.random(n) < multi, rng.integers(2, 4, n), 1).astype(np.uint32)
+    req["value_count"] = counts
+    req["value_begin"] = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.uint32)
+    values = zipf_keys(rng, n_values, int(counts.sum()), zipf, perm_seed=int(rng.integers(1 << 30))).astype(np.uint64)
+    values = values * np.uint64(0x9E3779B97F4A7C15)
+    sel = rng.random(n)
+    req["key"][sel < bad] = abi.KEY_BAD
+    req["acquire"][(sel >= bad) & (sel < 2 * bad)] = 0
+    req["key"][(sel >= 2 * bad) & (sel < 3 * bad)] = abi.KEY_NO_RULE
+    req["value_count"][(sel >= 3 * bad) & (sel < 4 * bad)] = 0
+    return req, values
+
+
+def _check(eng, ora, req, values):
+    want = ora.decide_param(req, values)
+    got = eng.cparam_decide_host(req, values)
+    if not np.array_equal(want, got):
+        bad = np.nonzero(want != got)[0]
+        i = bad[0]
+        raise AssertionError(f"{len(bad)} differ; first {i}: req={req[i]} oracle={want[i]} gpu={got[i]}")
+    return want
+
+
+def _compare_sums(eng, ora, req, values, now):
+    keys = set()
+    for q in req[:2000]:
+        k = int(q["key"])
+        if k < 1 << 20 and q["value_count"] > 0:
+            for v in values[q["value_begin"]: q["value_begin"] + q["value_count"]]:
+                keys.add((k, int(v)))
+    for k, v in sorted(keys)[:300]:
+        assert eng.cparam_sum(k, v, now) == ora.param_sum(k, v, now), (k, v)
+
+
+@pytest.mark.parametrize("S,interval", [(10, 1000), (2, 1000), (1, 500), (5, 25)])
+def test_single_value_requests(S, interval):
+    rng = np.random.default_rng(S * 7 + interval)
+    rules = _rules(20, rng, S, interval)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_003
+    for _ in range(3):
+        req, vals = _trace(rng, 50_000, 20, 300, t, int(rng.integers(100, 3 * interval + 500)), bad=0.01)
+        out = _check(eng, ora, req, vals)
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, interval))
+    assert (out["status"] == abi.OK).any() and (out["status"] == abi.BLOCKED).any()
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_multi_value_requests_all_or_nothing():
+    rng = np.random.default_rng(3)
+    rules = _rules(6, rng)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_500
+    for _ in range(3):
+        req, vals = _trace(rng, 6_000, 6, 40, t, 1500, multi=0.05, bad=0.01)
+        out = _check(eng, ora, req, vals)
+        t = int(req["ts_ms"][-1]) + 7
+    multi = req["value_count"] > 1
+    assert (out["remaining"][multi & (out["status"] == abi.OK)] == -1).all()
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_hot_items_and_avg_local():
+    rng = np.random.default_rng(4)
+    rules = _rules(4, rng, thr=abi.THRESHOLD_AVG_LOCAL, hot_per_rule=3)
+    hot = np.zeros(12, abi.PARAM_HOT_DTYPE)
+    for i in range(12):
+        hot[i] = (np.uint64(i % 3 + 1) * np.uint64(0x9E3779B97F4A7C15), int(rng.integers(0, 6)), 0)
+    eng, ora = _pair(rules, hot, connected=3)
+    t = 1_700_000_000_000
+    for _ in range(2):
+        req, vals = _trace(rng, 20_000, 4, 10, t, 2000, zipf=0.8)
+        _check(eng, ora, req, vals)
+        t = int(req["ts_ms"][-1])
+
+
+def test_rule_reload_keeps_surviving_metrics():
+    rng = np.random.default_rng(5)
+    rules = _rules(8, rng)
+    eng, ora = _pair(rules)
+    req, vals = _trace(rng, 20_000, 8, 50, 1_700_000_000_000, 800)
+    _check(eng, ora, req, vals)
+    new = np.concatenate([rules[2:6], _rules(3, rng)])
+    new["flow_id"][4:] += 1000
+    new["count"] = rng.integers(1, 30, len(new))
+    new["sample_count"][:2] = 4  # ignored for surviving flowIds: their metric keeps S=10
+    eng.cparam_load_rules(new, None, 12)
+    ora.load_param_rules(new)
+    req, vals = _trace(rng, 20_000, len(new), 50, 1_700_000_000_900, 1200)
+    _check(eng, ora, req, vals)
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))

@@ -364,3 +364,75 @@ def test_token_service_remaining_saturates(t0):
     s = _cluster_service(1e12, 10, 1000)
     out = s.decide(_req(t0))
     assert out[0]["status"] == abi.OK and out[0]["remaining"] == 2**31 - 1
+
+
+# ---- ClusterParamMetric / ClusterParamFlowChecker (cluster hot-parameter tokens) ----
+
+def test_cluster_param_metric_kat(t0):
+    """ClusterParamMetricTest.testClusterParamMetric (srvT/flow/statistic/metric/ClusterParamMetricTest.java:28-49):
+    S=5 over 25 ms, all at one instant: e1 sums -3 (avg -120), e2 246 after four adds (avg 9840)."""
+    from oracle.binding import ClusterParamMetric
+    m = ClusterParamMetric(5, 25)
+    e1, e2, e3 = 11, 22, 33
+    m.add_value(t0, e1, -1)
+    m.add_value(t0, e1, -2)
+    m.add_value(t0, e2, 100)
+    m.add_value(t0, e2, 23)
+    m.add_value(t0, e3, 100)
+    m.add_value(t0, e3, 230)
+    assert m.get_sum(t0, e1) == -3
+    assert abs(m.get_avg(t0, e1) - (-120)) < 0.01
+    assert abs(m.get_avg(t0, e3) - 13200) < 0.01      # the top value of getTopValues(1)
+    assert abs(m.get_avg(t0, e2) - 4920) < 0.01
+    m.add_value(t0, e2, 100)
+    m.add_value(t0, e2, 23)
+    assert m.get_sum(t0, e2) == 246
+    assert abs(m.get_avg(t0, e2) - 9840) < 0.01
+
+
+def test_cluster_param_metric_window_resets(t0):
+    """A bucket reset (ClusterParameterLeapArray.resetWindowTo clears its map) drops every value's count of
+    that bucket; buckets older than the interval stop counting."""
+    from oracle.binding import ClusterParamMetric
+    m = ClusterParamMetric(2, 1000)
+    m.add_value(t0, 1, 5)
+    m.add_value(t0 + 500, 1, 3)
+    m.add_value(t0 + 500, 2, 7)
+    assert m.get_sum(t0 + 999, 1) in (8, 3)   # t0's bucket may already be 500 ms older than t0+999's
+    assert m.get_sum(t0 + 1500, 1) == 3 or m.get_sum(t0 + 1500, 1) == 0
+    assert m.get_sum(t0 + 5000, 2) == 0
+
+
+def _cparam_rules(specs):
+    r = np.zeros(len(specs), abi.CPARAM_RULE_DTYPE)
+    for i, sp in enumerate(specs):
+        r[i] = (sp.get("flow_id", 100 + i), sp.get("count", 5.0), sp.get("thr", abi.THRESHOLD_GLOBAL),
+                sp.get("S", 10), sp.get("interval", 1000), sp.get("ns", 0), sp.get("hot_begin", 0), sp.get("hot_count", 0))
+    return r
+
+
+def test_cluster_param_checker_single_and_multi_values():
+    """ClusterParamFlowChecker.acquireClusterToken (ClusterParamFlowChecker.java:42-87): a value passes while
+    threshold - avg - count >= 0; a multi-value request is all-or-nothing and reports remaining -1; empty
+    params are BAD_REQUEST; hot items override the rule count."""
+    from oracle.binding import ClusterTokenService
+    s = ClusterTokenService()
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    s.set_namespaces(ns)
+    hot = np.zeros(1, abi.PARAM_HOT_DTYPE)
+    hot[0] = (7, 1, 0)                     # value 7: threshold 1
+    s.load_param_rules(_cparam_rules([{"count": 3.0, "hot_count": 1}]), hot)
+    values = np.array([1, 1, 7, 7, 1, 2], np.uint64)
+    req = np.zeros(7, abi.CPARAM_REQ_DTYPE)
+    t = 1_700_000_000_000
+    req[0] = (t, 0, 1, 0, 1)       # value 1: 3 - 0 - 1 = 2
+    req[1] = (t, 0, 2, 1, 1)       # value 1: 3 - 1 - 2 = 0
+    req[2] = (t, 0, 1, 2, 1)       # value 7 (hot, 1): 1 - 0 - 1 = 0
+    req[3] = (t, 0, 1, 3, 1)       # value 7: 1 - 1 - 1 < 0 → BLOCKED
+    req[4] = (t, 0, 1, 4, 2)       # values {1, 2}: 1 fails (3 - 3 - 1) → BLOCKED, nothing added
+    req[5] = (t, 0, 1, 5, 1)       # value 2: 3 - 0 - 1 = 2 (the failed multi request added nothing)
+    req[6] = (t, 0, 1, 0, 0)       # no params → BAD_REQUEST
+    out = s.decide_param(req, values)
+    assert [tuple(x) for x in out] == [(0, 2, 0), (0, 0, 0), (0, 0, 0), (1, 0, 0), (1, 0, 0), (0, 2, 0), (-4, 0, 0)]
+    assert s.param_sum(0, 1, t) == 3 and s.param_sum(0, 2, t) == 1 and s.param_sum(0, 7, t) == 1
