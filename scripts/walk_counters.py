@@ -1,4 +1,5 @@
-"""Short-walker cycle counters (SG_DEBUG & 64) on the C3 bench workload: one batch, then the counters."""
+"""Short-walker timers (SG_DEBUG & 64) on the C3 bench workload: one batch, then per length class the
+number of wave groups and the average gather / walk time per group (s_memrealtime, 100 MHz)."""
 import os, sys
 os.environ["SG_DEBUG"] = str(int(os.environ.get("SG_DEBUG", "0")) | 64 | 2)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,8 +18,11 @@ for b in range(2):
     x = wl.batch(b)
     torch.cuda.synchronize()
     eng.decide_device(x.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-c = eng.debug_copy(5, np.uint64, 16).astype(np.int64)
-g = max(1, c[0])
-print(f"groups {c[0]}  scan cyc/group {c[1]/g:.0f}  walk cyc/group {c[2]/g:.0f}  periods opened/lane {c[3]/g/64:.2f}  "
-      f"records/lane {c[4]/g/64:.2f}  max len/group {c[5]/g:.1f}")
-print("cycles per class (sum over groups):", list(c[6:12]))
+c = eng.debug_copy(5, np.uint64, 16).astype(np.uint64)
+print(f"total group time {int(c[0]) / 100:.0f} us (summed over waves)")
+for cl in range(6):
+    g = int(c[1 + cl])
+    if not g:
+        continue
+    gat, wk = int(c[7 + cl]) & 0xFFFFFFFF, int(c[7 + cl]) >> 32
+    print(f"class {cl}: groups {g:7d}  gather {gat / g / 100:7.2f} us/group  walk {wk / g / 100:8.2f} us/group")

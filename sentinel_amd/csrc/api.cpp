@@ -46,6 +46,7 @@ struct sg_handle {
     uint32_t* d_long_list = nullptr;
     uint32_t* d_long_count = nullptr;  // [4]: long count, short count, work cursors (long, short)
     uint32_t* d_short_list = nullptr;
+    uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
     uint64_t class_off[kClasses]{};
     unsigned long long* d_dbg = nullptr;   // [16] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
@@ -280,7 +281,9 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
             h->class_off[c] = off;
             off += (c == 0 ? n : n / (kClassMax[c - 1] + 1)) + 1;
         }
-        if (hipMalloc(&h->d_short_list, sizeof(uint32_t) * off) != hipSuccess) return bail(SG_E_NOMEM);
+        if (hipMalloc(&h->d_short_list, sizeof(uint32_t) * off) != hipSuccess ||
+            hipMalloc(&h->d_short_key, sizeof(uint32_t) * off) != hipSuccess)
+            return bail(SG_E_NOMEM);
     }
     if (hipMalloc(&h->d_dbg, 16 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 16 * 8) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_count, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -329,6 +332,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_long_list);
     dfree(h->d_long_count);
     dfree(h->d_short_list);
+    dfree(h->d_short_key);
     dfree(h->d_dbg);
     dfree(h->d_skips);
     dfree(h->d_prules);
@@ -561,6 +565,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.long_list = h->d_long_list;
     a.long_count = h->d_long_count;
     a.short_list = h->d_short_list;
+    a.short_key = h->d_short_key;
     a.short_count = h->d_long_count + 1;
     for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
     a.skips = h->d_skips;

@@ -71,17 +71,6 @@ __device__ __forceinline__ void store_result(sg_result* out, uint32_t idx, int32
     out[idx] = r;
 }
 
-// Window period q (0-based within the batch) of request `idx`: the largest q with bnd[q] <= idx.
-__device__ __forceinline__ uint32_t period_of(const uint32_t* bnd, uint32_t np, uint32_t idx) {
-    uint32_t lo = 0, hi = np;
-    while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (bnd[mid] <= idx) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
 struct Decoded {
     uint32_t idx;
     int64_t acq;
@@ -214,22 +203,51 @@ __device__ __forceinline__ void open_bucket(PeriodState& ps, int64_t start, cons
     }
 }
 
-// Period tracking shared by both walkers: requests of one flowId arrive in index order, so the
+// The batch's period tables (first request index of every window period, per distinct window length),
+// staged in LDS by stage_periods when they fit, else read from a.bnd. File-scope LDS keeps every access a
+// ds_read: a table pointer that may point at LDS or HBM compiles to flat loads, and each of those waits
+// for every outstanding global load and store of the wave (s_waitcnt vmcnt(0) lgkmcnt(0)).
+__shared__ uint32_t g_sbnd[kLdsBnd];
+__shared__ uint32_t g_boff[kMaxWl];  // offset of window length w's table in g_sbnd
+__shared__ int g_blds;               // 1: tables in g_sbnd, 0: read from a.bnd
+
+// Period tracking shared by the walkers: requests of one flowId arrive in index order, so the
 // window period only moves forward; the cached boundary of the next period answers most lookups.
+// L: the tables are staged in g_sbnd (a compile-time choice: a run-time one is if-converted into a
+// select of two pointers and one flat load). Kernels branch once on g_blds into the two instantiations.
+template <bool L>
 struct PeriodCursor {
-    const uint32_t* bnd;
+    const uint32_t* gbnd;  // this window length's table in HBM (!L)
+    uint32_t base;         // its offset in g_sbnd (L)
     uint32_t np;
     uint32_t q;       // current period (0-based within the batch), 0xFFFFFFFF before the first
     uint32_t next_b;  // first request index of period q + 1 (UINT32_MAX past the last)
 
+    __device__ __forceinline__ void init(const BatchArgs& a, int w) {
+        gbnd = a.bnd + (size_t)w * kMaxPeriods;
+        base = g_boff[w];
+        np = a.np[w];
+        q = 0xFFFFFFFFu;
+        next_b = 0;
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t i) const {
+        if constexpr (L) return g_sbnd[base + i];
+        else return gbnd[i];
+    }
     __device__ __forceinline__ void seek(uint32_t qq) {
         q = qq;
-        next_b = (qq + 1 < np) ? bnd[qq + 1] : 0xFFFFFFFFu;
+        next_b = (qq + 1 < np) ? at(qq + 1) : 0xFFFFFFFFu;
     }
-    // period of a request index >= every index seen so far
+    // period of a request index >= every index seen so far: the largest p with table[p] <= idx
     __device__ __forceinline__ uint32_t of(uint32_t idx) const {
         if (q != 0xFFFFFFFFu && idx < next_b) return q;
-        return period_of(bnd, np, idx);
+        uint32_t lo = 0, hi = np;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (at(mid) <= idx) lo = mid;
+            else hi = mid;
+        }
+        return lo;
     }
 };
 
@@ -270,11 +288,13 @@ __device__ __forceinline__ void open_period_serial(PeriodState& ps, const Bucket
 // ------------------------------------------------------------------------ serial walker (short)
 
 // Outputs start as BLOCKED (k_prep), so only OK / SHOULD_WAIT results are written here.
-__device__ uint32_t walk_serial(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e) {
+template <bool L>
+__device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
     uint32_t opened = 0;
     const Rule R = a.rules[k];
     Bucket* ring = a.ring + (size_t)k * a.stride;
-    PeriodCursor pc{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+    PeriodCursor<L> pc;
+    pc.init(a, R.wl_idx);
     const int64_t P0 = a.p0[R.wl_idx];
     PeriodState ps;
     {
@@ -330,12 +350,13 @@ __device__ uint32_t walk_serial(const BatchArgs& a, const uint32_t* const* bndp,
 
 constexpr int kWaveUnroll = 8;  // 64-record chunks kept in flight per wave (register double buffer)
 
+template <bool L>
 struct WaveWalker {
     const BatchArgs& a;
     const Rule R;
     const int lane;
     Bucket* ring;
-    PeriodCursor pc;
+    PeriodCursor<L> pc;
     int64_t P0;
     // lane q < S holds slot q of the ring
     int64_t st;
@@ -349,10 +370,10 @@ struct WaveWalker {
     // request can occupy (both only get harder within a period), so its remaining requests are BLOCKED
     bool dead;
 
-    __device__ WaveWalker(const BatchArgs& a_, const uint32_t* const* bndp, uint32_t k)
+    __device__ WaveWalker(const BatchArgs& a_, uint32_t k)
         : a(a_), R(a_.rules[k]), lane(lane_id()) {
         ring = a.ring + (size_t)k * a.stride;
-        pc = PeriodCursor{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
+        pc.init(a, R.wl_idx);
         P0 = a.p0[R.wl_idx];
         st = INT64_MIN;
 #pragma unroll
@@ -565,8 +586,9 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
     return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
-__device__ void walk_wave(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e) {
-    WaveWalker w(a, bndp, k);
+template <bool L>
+__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
+    WaveWalker<L> w(a, k);
     const int lane = w.lane;
     const uint64_t* rec = a.rec_sorted;
     constexpr uint64_t kBlock = 64ull * kWaveUnroll;
@@ -676,7 +698,7 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
         // 2. classify the heads, one per thread: all length probes issued at once (the segment is longer
         // than m iff record j + m has the same key; the class is the number of bounds it exceeds)
         const uint32_t nh = nheads;
-        uint32_t slot[kSegTile / kSegThreads];
+        uint32_t slot[kSegTile / kSegThreads], hkey[kSegTile / kSegThreads];
 #pragma unroll
         for (int r = 0; r < (int)(kSegTile / kSegThreads); ++r) {
             const uint32_t h = (uint32_t)r * kSegThreads + (uint32_t)tid;
@@ -684,6 +706,7 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
             if (h >= nh) continue;
             const uint64_t j = t0 + hpos[h];
             const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+            hkey[r] = k;
             uint32_t pk[kClasses];
 #pragma unroll
             for (int c = 0; c < kClasses; ++c) {
@@ -709,40 +732,38 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
             const uint32_t j = (uint32_t)(t0 + hpos[(uint32_t)r * kSegThreads + (uint32_t)tid]);
             const uint32_t l = slot[r] >> 24, pos = base[l] + (slot[r] & 0xFFFFFFu);
             if (l == (uint32_t)kClasses) a.long_list[pos] = j;
-            else a.short_list[a.class_off[l] + pos] = j;
+            else {
+                a.short_list[a.class_off[l] + pos] = j;
+                if (a.short_key) a.short_key[a.class_off[l] + pos] = hkey[r];
+            }
         }
         __syncthreads();  // cnt / base / hpos are reused by the next tile
     }
 }
 
-// The period table of the batch, staged in LDS when it fits (else read from HBM/L2): bndp[w] points at
-// window length w's boundaries.
-__device__ __forceinline__ void stage_periods(const BatchArgs& a, uint32_t* sbnd, const uint32_t** bndp) {
+// Stage the batch's period tables in g_sbnd when they fit (else the cursors read a.bnd).
+__device__ __forceinline__ void stage_periods(const BatchArgs& a) {
     uint32_t tot = 0;
     for (int w = 0; w < a.n_wl; ++w) tot += a.np[w];
     const bool lds = tot <= (uint32_t)kLdsBnd && !(a.dbg & 1);
     uint32_t off = 0;
     for (int w = 0; w < a.n_wl; ++w) {
         const uint32_t npw = a.np[w];
-        const uint32_t* g = a.bnd + (size_t)w * kMaxPeriods;
         if (lds) {
-            for (uint32_t i = threadIdx.x; i < npw; i += blockDim.x) sbnd[off + i] = g[i];
-            if (threadIdx.x == 0) bndp[w] = sbnd + off;
-        } else if (threadIdx.x == 0) {
-            bndp[w] = g;
+            const uint32_t* g = a.bnd + (size_t)w * kMaxPeriods;
+            for (uint32_t i = threadIdx.x; i < npw; i += blockDim.x) g_sbnd[off + i] = g[i];
         }
+        if (threadIdx.x == 0) g_boff[w] = off;
         off += npw;
     }
+    if (threadIdx.x == 0) g_blds = lds ? 1 : 0;
     __syncthreads();
 }
 
 // Long-segment walker: one wave per segment of more than short_max records (grid-stride over the list,
 // grid sized to what is resident at once). Runs concurrently with k_walk_short (separate stream).
-__global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
-    __shared__ uint32_t sbnd[kLdsBnd];
-    __shared__ const uint32_t* bndp[kMaxWl];
-    if (*a.err) return;
-    stage_periods(a, sbnd, bndp);
+template <bool L>
+__device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
     const int lane = lane_id();
     const uint32_t n_long = *a.long_count;
     // static wave → item assignment (wave-uniform loop control; a dynamic atomic work queue here
@@ -756,144 +777,187 @@ __global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
         const uint64_t e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
-        walk_wave(a, bndp, k, s, e);
+        walk_wave<L>(a, k, s, e);
     }
+}
+
+__global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
+    if (*a.err) return;
+    stage_periods(a);
+    if (g_blds) walk_long_body<true>(a);
+    else walk_long_body<false>(a);
 }
 
 // Serial walk of one flowId segment with the ring's {period, PASS, WAITING} of all SM >= S slots held in
 // registers: the ring is read from HBM once (and slot I's full bucket only when the batch continues the
 // stored period), each closed bucket is written back, nothing is re-read. Same decisions as walk_serial,
 // which re-reads the ring at every new period (the working set of all lanes does not fit L2).
-constexpr int32_t kRelAbsent = INT32_MIN;      // slot never created
-constexpr int32_t kRelOld = INT32_MIN + 1;     // created, but too old to be valid anywhere in this batch
 
-template <int SM>
-__device__ void walk_reg(const BatchArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s) {
-    const Rule R = a.rules[k];
+// {start, PASS, WAITING} of one ring slot, staged in LDS by a wave's cooperative ring gather.
+struct SlotSnap {
+    int64_t start, pass, wait;
+};
+
+__device__ __forceinline__ void store_bucket(Bucket* b, int64_t start, const int64_t* c) {
+    ulonglong2* p = reinterpret_cast<ulonglong2*>(b);
+    p[0] = make_ulonglong2((unsigned long long)start, (unsigned long long)c[0]);
+    p[1] = make_ulonglong2((unsigned long long)c[1], (unsigned long long)c[2]);
+    p[2] = make_ulonglong2((unsigned long long)c[3], (unsigned long long)c[4]);
+    p[3] = make_ulonglong2((unsigned long long)c[5], (unsigned long long)c[6]);
+}
+
+constexpr int kBlk = 8;  // records per block of the short walker's double-buffered record stream
+
+// Walk of one flowId segment per lane, all 64 lanes of the wave together (inactive lanes pass act =
+// false). `snap` holds the lane's ring snapshot {start, PASS, WAITING} of its S <= SM slots (gathered
+// by the wave into LDS, kept up to date as buckets close) and `buf` its first kBlk records (loaded by the
+// caller, so that every load of the wave's group is in flight at once). Same decisions as walk_serial.
+//
+// Phased for SIMT: a lane whose next record starts a new window period parks; the wave runs the cheap
+// per-record step (one decision) while any lane can take it, then opens the parked lanes' periods in one
+// pass. The period-open code (ring sums over S slots, bucket close) thus runs ~once per period of the
+// wave instead of in almost every record step (64 lanes each change period every few records).
+template <int SM, bool L>
+__device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, const Rule& R,
+                                         const Occ& occ, SlotSnap* snap, uint64_t* buf) {
     Bucket* ring = a.ring + (size_t)k * a.stride;
     const int S = R.S;
     const int64_t wl = R.wl;
-    PeriodCursor pc{bndp[R.wl_idx], a.np[R.wl_idx], 0xFFFFFFFFu, 0};
-    const int64_t P0 = a.p0[R.wl_idx];
-    const int64_t base_ws = P0 * wl;  // window start of the batch's first period: rel period 0
-    int32_t rel[SM];
-    int64_t pa[SM], wa[SM];
+    PeriodCursor<L> pc;
+    pc.init(a, act ? R.wl_idx : 0);
+    const int64_t P0 = a.p0[act ? R.wl_idx : 0];
+    PeriodState ps;
+    ps.occ_pass = occ.pass;
+    ps.occ_req = occ.pass_req;
 #pragma unroll
-    for (int j = 0; j < SM; ++j) {
-        rel[j] = kRelAbsent;
-        pa[j] = wa[j] = 0;
-        if (j < S) {
-            const int64_t st = ring[j].start;
-            pa[j] = ring[j].c[SG_EV_PASS];
-            wa[j] = ring[j].c[SG_EV_WAITING];
-            if (st != INT64_MIN) {
-                const int64_t d = st - base_ws;  // <= 0: stored buckets are older than this batch
-                rel[j] = (d < -(int64_t)S * wl) ? kRelOld : (int32_t)(d / wl);
+    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
+    ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+    int I = -1;      // slot of the open period
+    int64_t ws = 0;  // its window start
+    uint64_t nb[kBlk];
+    uint64_t p = s;  // position of buf[0]'s block
+    int left = kBlk; // records of the current block not yet consumed (buf[0] is the next one)
+    bool more = act && (uint32_t)(buf[kBlk - 1] >> a.kshift) == k;  // the segment continues past this block
+    if (more) {
+#pragma unroll
+        for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
+    }
+    bool live = act;  // records left
+    uint32_t qn = 0;  // period of the next record (valid when live)
+    Decoded dn;       // the next record, decoded
+    auto peek = [&]() {  // look at buf[0]: end of segment, or decode it and find its period
+        const uint64_t cur = buf[0];
+        if ((uint32_t)(cur >> a.kshift) != k) {
+            live = false;
+            return;
+        }
+        dn = decode(a, cur);
+        qn = pc.of(dn.idx);
+    };
+    auto advance = [&]() {  // consume buf[0]
+#pragma unroll
+        for (int v = 0; v < kBlk - 1; ++v) buf[v] = buf[v + 1];  // resident values: plain moves
+        buf[kBlk - 1] = ~0ull;
+        if (--left == 0) {
+            if (!more) {
+                live = false;
+                return;
+            }
+#pragma unroll
+            for (int u = 0; u < kBlk; ++u) buf[u] = nb[u];
+            p += kBlk;
+            left = kBlk;
+            more = (uint32_t)(buf[kBlk - 1] >> a.kshift) == k;
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
             }
         }
-    }
-    PeriodState ps;
-    {
-        const Occ o = a.occ[k];
-        ps.occ_pass = o.pass;
-        ps.occ_req = o.pass_req;
-    }
-    int I = -1;      // slot of the open period
-    int32_t r = 0;   // open period, relative to P0
-    bool first = true;
-    // records kAhead ahead in a register shift pipeline (a lane may walk up to short_max records)
-    constexpr int kAhead = 8;
-    uint64_t rq[kAhead];
-    uint64_t nextp = s;
-#pragma unroll
-    for (int u = 0; u < kAhead; ++u, ++nextp) rq[u] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
-    for (;;) {
-        const uint64_t cur = rq[0];
-        if ((uint32_t)(cur >> a.kshift) != k) break;
-#pragma unroll
-        for (int u = 0; u < kAhead - 1; ++u) rq[u] = rq[u + 1];
-        rq[kAhead - 1] = nextp < a.n ? a.rec_sorted[nextp] : ~0ull;
-        ++nextp;
-        const Decoded d = decode(a, cur);
-        const uint32_t q = pc.of(d.idx);
-        if (q != pc.q) {
-            if (I >= 0) {  // close the open bucket: memory and the register snapshot
-                Bucket& b = ring[I];
-                b.start = base_ws + (int64_t)r * wl;
-#pragma unroll
-                for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) b.c[ev] = ps.cur[ev];
-#pragma unroll
-                for (int x = 0; x < SM; ++x)
-                    if (x == I) {
-                        rel[x] = r;
-                        pa[x] = ps.cur[SG_EV_PASS];
-                        wa[x] = ps.cur[SG_EV_WAITING];
-                    }
+    };
+    if (live) peek();
+    while (__ballot(live)) {
+        // 1. open the period of every lane whose next record starts one (the first record included)
+        if (live && qn != pc.q) {
+            if (I >= 0) {  // close the open bucket: memory and the snapshot
+                if (!(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
+                snap[I].start = ws;
+                snap[I].pass = ps.cur[SG_EV_PASS];
+                snap[I].wait = ps.cur[SG_EV_WAITING];
             }
-            pc.seek(q);
-            const int32_t rn = (int32_t)q;
-            I = first ? (int)((P0 + (int64_t)q) % S) : (I + (rn - r)) % S;
-            r = rn;
-            const int h = (I + 1) % S;
+            const uint32_t qprev = pc.q;
+            pc.seek(qn);
+            const int64_t P = P0 + (int64_t)qn;
+            I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
+            ws = P * wl;
+            const int64_t lo = ws - (int64_t)S * wl;  // LeapArray.isWindowDeprecated: valid iff start > lo
+            const int h = I + 1 == S ? 0 : I + 1;
             ps.wo_pass = ps.wo_wait = ps.head_other = 0;
-            int32_t relI = kRelAbsent;
 #pragma unroll
             for (int x = 0; x < SM; ++x) {
-                if (x < S) {
-                    const bool v = x != I && rel[x] > r - S;  // LeapArray.isWindowDeprecated, strictly greater
-                    ps.wo_pass += v ? pa[x] : 0;
-                    ps.wo_wait += v ? wa[x] : 0;
-                    if (x == h && v) ps.head_other = pa[x];
-                    if (x == I) relI = rel[x];
+                if (x < S && x != I) {
+                    const SlotSnap& e = snap[x];
+                    const bool v = e.start > lo;
+                    ps.wo_pass += v ? e.pass : 0;
+                    ps.wo_wait += v ? e.wait : 0;
+                    if (x == h && v) ps.head_other = e.pass;
                 }
             }
             // currentWindow on slot I: continue (only possible at the batch's first period), create or reset
-            const int64_t ws = base_ws + (int64_t)r * wl;
+            const int64_t stI = snap[I].start;
             int64_t cI[SG_NUM_EVENTS];
-            int64_t stI = relI == kRelAbsent ? INT64_MIN : (relI == kRelOld ? INT64_MIN + 1 : base_ws + (int64_t)relI * wl);
             if (stI == ws) {
 #pragma unroll
                 for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
             }
             open_bucket(ps, stI, cI, ws);
-            first = false;
         }
-        // ClusterFlowChecker.acquireClusterToken, :67-81
-        const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
-        const double next_remaining = R.thr - latest - (double)d.acq;
-        if (next_remaining >= 0) {
-            ps.cur[SG_EV_PASS] += d.acq;
-            ps.cur[SG_EV_PASS_REQUEST] += 1;
-            if (d.prio) ps.cur[SG_EV_OCCUPIED_PASS] += d.acq;
-            store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
-        } else {
-            int32_t wait;
-            const int32_t st = decide_fail(R, a.max_occ_ratio, ps, d.acq, d.prio, &wait);
-            if (st != SG_STATUS_BLOCKED) store_result(a.out, d.idx, st, 0, wait);
+        // 2. decide records while they stay in the open period (ClusterFlowChecker.acquireClusterToken :67-111)
+        while (live && qn == pc.q) {
+            const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
+            const double next_remaining = R.thr - latest - (double)dn.acq;
+            if (next_remaining >= 0) {
+                ps.cur[SG_EV_PASS] += dn.acq;
+                ps.cur[SG_EV_PASS_REQUEST] += 1;
+                if (dn.prio) ps.cur[SG_EV_OCCUPIED_PASS] += dn.acq;
+                if (!(a.dbg & 256)) store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+            } else {
+                int32_t wait;
+                const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, dn.acq, dn.prio, &wait);
+                if (stt != SG_STATUS_BLOCKED) store_result(a.out, dn.idx, stt, 0, wait);
+            }
+            advance();
+            if (live) peek();
         }
     }
-    if (I >= 0) {
-        Bucket& b = ring[I];
-        b.start = base_ws + (int64_t)r * wl;
-#pragma unroll
-        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) b.c[ev] = ps.cur[ev];
+    if (act) {
+        if (I >= 0 && !(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
+        Occ o;
+        o.pass = ps.occ_pass;
+        o.pass_req = ps.occ_req;
+        a.occ[k] = o;
     }
-    Occ o;
-    o.pass = ps.occ_pass;
-    o.pass_req = ps.occ_req;
-    a.occ[k] = o;
 }
 
 // Short-segment walker: each wave takes 64 segments of <= short_max records of one length class and
-// walks one per lane; the classes of longer segments go first. SM > 0: ring snapshot in registers
-// (every flow has sampleCount <= SM); SM == 0: generic walker re-reading the ring.
-template <int SM>
-__global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
-    __shared__ uint32_t sbnd[kLdsBnd];
-    __shared__ const uint32_t* bndp[kMaxWl];
-    if (*a.err) return;
-    stage_periods(a, sbnd, bndp);
+// walks one per lane; the classes of longer segments go first. SM > 0: ring snapshot in LDS (every flow
+// has sampleCount <= SM <= kGatherMaxS); SM == 0: generic walker re-reading the ring.
+//
+// SM > 0, one group of 64 segments: every load the group needs is issued before any is waited for
+// (k_seg hands over each segment's flowId with its start): the rules, occupy counters, first record
+// blocks, and the rings. Rings of up to kGatherMaxS slots are gathered cooperatively into LDS — a
+// wave-instruction loads 16-B pieces of ~3 consecutive rings ({start, PASS} at byte 0 and
+// {OCCUPIED_BLOCK, WAITING} at byte 48 of each bucket), row-shaped instead of 64 lanes in 64 rows.
+constexpr int kGatherMaxS = 10;
+#ifndef SG_SHORT_BLOCKS
+#define SG_SHORT_BLOCKS 2
+#endif
+constexpr int kShortBlocksPerCu = SG_SHORT_BLOCKS;  // occupancy target (VGPR budget) of the short walker
+
+template <int SM, bool L>
+__device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* snap_all) {
+    constexpr int kSnapPerWave = SM > 0 ? 64 * SM : 1;
     const int lane = lane_id();
+    SlotSnap* snap = snap_all + (threadIdx.x / 64) * kSnapPerWave;
     uint32_t cnt[kClasses], grp_end[kClasses];
     uint32_t total = 0;
 #pragma unroll
@@ -911,36 +975,85 @@ __global__ void __launch_bounds__(256) k_walk_short(BatchArgs a) {
             g0 = grp_end[c];
             --c;
         }
+        c = __builtin_amdgcn_readfirstlane(c);
         const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
-        if (i >= cnt[c]) continue;
-        const uint64_t t0 = (a.dbg & 64) ? clock64() : 0;
+        const bool act = i < cnt[c];
+        if constexpr (SM > 0) {
+            const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
+            // 1. segment descriptors (inactive lanes of the last group repeat entry 0: valid addresses)
+            const uint64_t li = a.class_off[c] + (act ? i : 0u);
+            const uint64_t s = a.short_list[li];
+            const uint32_t k = a.short_key[li];
+            // 2. everything that depends on (s, k) only
+            const Rule R = a.rules[k];
+            const Occ occ = a.occ[k];
+            uint64_t buf[kBlk];
+#pragma unroll
+            for (int u = 0; u < kBlk; ++u) buf[u] = s + u < a.n ? a.rec_sorted[s + u] : ~0ull;
+            {
+                // piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS}, 1: WAITING);
+                // slots past the handle's stride read slot 0 again (ignored: q >= S)
+                constexpr int kT = 2 * SM;  // pieces per lane, loaded in two batches of SM
+#pragma unroll
+                for (int t0 = 0; t0 < kT; t0 += SM) {
+                    ulonglong2 v[SM];
+#pragma unroll
+                    for (int t = 0; t < SM; ++t) {
+                        const int pc = (t0 + t) * 64 + lane;
+                        const int j = pc / kT;
+                        const int q = (pc % kT) >> 1;
+                        const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
+                        const int qq = q < a.stride ? q : 0;
+                        v[t] = *(reinterpret_cast<const ulonglong2*>(a.ring + (size_t)kj * a.stride + qq) +
+                                 ((pc & 1) ? 3 : 0));
+                    }
+#pragma unroll
+                    for (int t = 0; t < SM; ++t) {
+                        const int pc = (t0 + t) * 64 + lane;
+                        SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
+                        if (pc & 1) {
+                            d.wait = (int64_t)v[t].y;
+                        } else {
+                            d.start = (int64_t)v[t].x;
+                            d.pass = (int64_t)v[t].y;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            const uint64_t tw1 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
+            walk_reg<SM, L>(a, act, k, s, R, occ, snap + lane * SM, buf);
+            if (a.dbg & 64) {  // per class: groups, gather time, walk time (100 MHz ticks)
+                const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
+                if (lane == 0) {
+                    atomicAdd(&a.dbg_ctr[0], (unsigned long long)(tw2 - tw0));
+                    atomicAdd(&a.dbg_ctr[1 + c], 1ull);
+                    atomicAdd(&a.dbg_ctr[7 + c], (unsigned long long)(tw1 - tw0));
+                    atomicAdd(&a.dbg_ctr[7 + c], (unsigned long long)(tw2 - tw1) << 32);
+                }
+            }
+            continue;
+        }
+        if (!act) continue;
         const uint64_t s = a.short_list[a.class_off[c] + i];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-        uint32_t opened = 0;
+        const uint64_t lim = s + (uint64_t)min(a.short_max, c < kClasses - 1 ? kClassMax[c] : 0xFFFFFFFFu) + 1;
         uint64_t e = s + 1;
-        if constexpr (SM > 0) {
-            walk_reg<SM>(a, bndp, k, s);
-        } else {
-            const uint64_t lim = s + (uint64_t)min(a.short_max, c < kClasses - 1 ? kClassMax[c] : 0xFFFFFFFFu) + 1;
-            while (e < a.n && e < lim && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
-            opened = walk_serial(a, bndp, k, s, e);
-        }
-        if (a.dbg & 64) {
-            const uint64_t t2 = clock64();
-            const int64_t len = (int64_t)(e - s);
-            const int64_t op = wave_sum((int64_t)opened), rs = wave_sum(len);
-            int64_t mx = len;
-            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (int64_t)__shfl_xor((long long)mx, o, 64));
-            if (lane == __builtin_ctzll(__ballot(1))) {
-                atomicAdd(&a.dbg_ctr[0], 1ull);
-                atomicAdd(&a.dbg_ctr[2], (unsigned long long)(t2 - t0));
-                atomicAdd(&a.dbg_ctr[3], (unsigned long long)op);
-                atomicAdd(&a.dbg_ctr[4], (unsigned long long)rs);
-                atomicAdd(&a.dbg_ctr[5], (unsigned long long)mx);
-                atomicAdd(&a.dbg_ctr[6 + c], (unsigned long long)(t2 - t0));
-            }
-        }
+        while (e < a.n && e < lim && (uint32_t)(a.rec_sorted[e] >> a.kshift) == k) ++e;
+        walk_serial<L>(a, k, s, e);
     }
+}
+
+template <int SM>
+__global__ void __launch_bounds__(256, kShortBlocksPerCu) k_walk_short(BatchArgs a) {
+    static_assert(SM <= kGatherMaxS, "LDS budget of the ring snapshot");
+    __shared__ SlotSnap snap_all[4 * (SM > 0 ? 64 * SM : 1)];
+    if (*a.err) return;
+    stage_periods(a);
+    if (g_blds) walk_short_body<SM, true>(a, snap_all);
+    else walk_short_body<SM, false>(a, snap_all);
 }
 
 // One wave per skipped piece: Σ acquire and Σ prioritized acquire over its records, added with 64-bit
@@ -1089,7 +1202,6 @@ hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {
     if (a.stride <= 4) return launch_short_sm<4>(a, stream);
     if (a.stride <= 8) return launch_short_sm<8>(a, stream);
     if (a.stride <= 10) return launch_short_sm<10>(a, stream);  // ClusterFlowConfig default sampleCount
-    if (a.stride <= 16) return launch_short_sm<16>(a, stream);
     return launch_short_sm<0>(a, stream);
 }
 
