@@ -1,5 +1,6 @@
-"""Short-walker timers (SG_DEBUG & 64) on the C3 bench workload: one batch, then per length class the
-number of wave groups and the average gather / walk time per group (s_memrealtime, 100 MHz)."""
+"""Long-walker timers (SG_DEBUG & 64 with SG_SHORT_MAX set, e.g. 16): per segment length bucket, segments and
+average wave time per segment (s_memrealtime, 100 MHz). The short walker's timers are zeroed first by running
+it with no short segments... (both walkers share dbg_ctr: run with SG_SHORT_MAX small and read [1..8])."""
 import os, sys
 os.environ["SG_DEBUG"] = str(int(os.environ.get("SG_DEBUG", "0")) | 64 | 2)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -10,7 +11,7 @@ from sentinel_amd.engine import FlowEngine
 dev = torch.device("cuda", 0)
 n = 16_000_000
 wl = bench.ShardWorkload(1_000_000, n, 0, 1, dev)
-eng = FlowEngine(device=0, max_batch=n)
+eng = FlowEngine(device=0, max_batch=n, flags=int(os.environ.get("SG_FLAGS", "0")))
 ns = np.zeros(1, abi.NS_DTYPE); ns["connected_count"] = 1; ns["max_allowed_qps"] = 30000
 eng.set_namespaces(ns); eng.load_rules(wl.rules)
 out = torch.empty(n * 12, dtype=torch.uint8, device=dev)
@@ -19,11 +20,7 @@ for b in range(2):
     torch.cuda.synchronize()
     eng.decide_device(x.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
 c = eng.debug_copy(5, np.uint64, 16).astype(np.uint64)
-print(f"total group time {int(c[0]) / 100:.0f} us (summed over waves)")
-for cl in range(6):
-    g = int(c[1 + cl])
-    if not g:
-        continue
-    gat, wk = int(c[7 + cl]) & 0xFFFFFFFF, int(c[7 + cl]) >> 32
-    print(f"class {cl}: groups {g:7d}  gather {gat / g / 100:7.2f} us/group  walk {wk / g / 100:8.2f} us/group")
-print(f"all groups: outer trips {int(c[13])}, max-lane records (sum over groups) {int(c[14])}, records {int(c[15])}")
+for i, name in enumerate(["<=64", "<=256", "<=1024", ">1024"]):
+    cnt, t = int(c[1 + 2 * i]), int(c[2 + 2 * i])
+    if cnt:
+        print(f"long segments {name:7s}: {cnt:7d}  {t / cnt / 100:8.2f} us/segment")

@@ -32,6 +32,7 @@ struct sg_handle {
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
     Occ* d_occ = nullptr;
+    uint32_t* d_seg_end = nullptr;   // [K] end of each flowId's segment in the sorted records (k_seg)
 
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
@@ -47,6 +48,7 @@ struct sg_handle {
     uint32_t* d_long_count = nullptr;  // [4]: long count, short count, work cursors (long, short)
     uint32_t* d_short_list = nullptr;
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
+    uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
     uint64_t class_off[kClasses]{};
     unsigned long long* d_dbg = nullptr;   // [16] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
@@ -274,7 +276,9 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_np, sizeof(uint32_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&h->d_long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess)
+        return bail(SG_E_NOMEM);
     {  // short-segment class slices: class c holds segments longer than kClassMax[c-1], so at most n/(that+1)
         uint64_t off = 0;
         for (int c = 0; c < kClasses; ++c) {
@@ -316,6 +320,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
+    dfree(h->d_seg_end);
     dfree(h->d_rec);
     dfree(h->d_rec_sorted);
     dfree(h->d_hist);
@@ -333,6 +338,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_long_count);
     dfree(h->d_short_list);
     dfree(h->d_short_key);
+    dfree(h->d_long_key);
     dfree(h->d_dbg);
     dfree(h->d_skips);
     dfree(h->d_prules);
@@ -481,14 +487,16 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
     Occ* d_occ = nullptr;
+    uint32_t* d_seg_end = nullptr;
     int32_t* d_src = nullptr;
     if (n) {
-        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess ||
+        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * n) != hipSuccess ||
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
             dfree(d_rules);
             dfree(d_ring);
             dfree(d_occ);
+            dfree(d_seg_end);
             dfree(d_src);
             return fail(h, SG_E_NOMEM, "rule state allocation failed");
         }
@@ -500,9 +508,11 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
+    dfree(h->d_seg_end);
     h->d_rules = d_rules;
     h->d_ring = d_ring;
     h->d_occ = d_occ;
+    h->d_seg_end = d_seg_end;
     h->rules.assign(rules, rules + n);
     h->rule_tab = tab;
     h->K = n;
@@ -553,6 +563,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.rules = h->d_rules;
     a.ring = h->d_ring;
     a.occ = h->d_occ;
+    a.seg_end = h->d_seg_end;
     a.stride = h->stride;
     a.max_occ_ratio = h->cfg.max_occupy_ratio;
     a.n_wl = h->n_wl;
@@ -566,6 +577,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.long_count = h->d_long_count;
     a.short_list = h->d_short_list;
     a.short_key = h->d_short_key;
+    a.long_key = h->d_long_key;
     a.short_count = h->d_long_count + 1;
     for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
     a.skips = h->d_skips;

@@ -80,6 +80,8 @@ struct BatchArgs {
     uint32_t* short_list; // segment starts walked one lane each, per length class (slices, see class_off)
     uint32_t* short_count; // [kClasses] per length class
     uint32_t* short_key;   // flowId of each short_list entry (nullptr: not written)
+    uint32_t* long_key;    // flowId of each long_list entry (nullptr: not written)
+    uint32_t* seg_end;     // [K] end of each present key's segment in rec_sorted (nullptr: not written)
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
     uint32_t short_max;  // segments longer than this go to the wave walker
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream

@@ -692,7 +692,11 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
             const uint32_t j_off = (uint32_t)((wave * kSegItems + u) << 6) + (uint32_t)lane;
             uint32_t kp = (uint32_t)__shfl_up((int)key[u], 1u, 64);
             if (lane == 0) kp = u == 0 ? before : (uint32_t)__shfl((int)key[u - 1], 63, 64);
-            if (t0 + j_off < n && key[u] < a.K && key[u] != kp) hpos[atomicAdd(&nheads, 1u)] = j_off;
+            if (t0 + j_off < n && key[u] != kp) {
+                if (key[u] < a.K) hpos[atomicAdd(&nheads, 1u)] = j_off;
+                if (a.seg_end && kp < a.K) a.seg_end[kp] = (uint32_t)(t0 + j_off);  // the previous key ends here
+            }
+            if (a.seg_end && t0 + j_off == n - 1 && key[u] < a.K) a.seg_end[key[u]] = (uint32_t)n;
         }
         __syncthreads();
         // 2. classify the heads, one per thread: all length probes issued at once (the segment is longer
@@ -731,8 +735,10 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
             if (slot[r] == 0xFFFFFFFFu) continue;
             const uint32_t j = (uint32_t)(t0 + hpos[(uint32_t)r * kSegThreads + (uint32_t)tid]);
             const uint32_t l = slot[r] >> 24, pos = base[l] + (slot[r] & 0xFFFFFFu);
-            if (l == (uint32_t)kClasses) a.long_list[pos] = j;
-            else {
+            if (l == (uint32_t)kClasses) {
+                a.long_list[pos] = j;
+                if (a.long_key) a.long_key[pos] = hkey[r];
+            } else {
                 a.short_list[a.class_off[l] + pos] = j;
                 if (a.short_key) a.short_key[a.class_off[l] + pos] = hkey[r];
             }
@@ -772,16 +778,32 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     for (uint32_t item = wave; item < n_long; item += nwaves) {
         const uint64_t s = a.long_list[item];
-        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-        // segment end: the first record with another flowId
-        const uint64_t e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
-            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
-        }, lane);
+        uint32_t k;
+        uint64_t e;
+        if (a.long_key && a.seg_end) {  // segment key and end from k_seg
+            k = a.long_key[item];
+            e = a.seg_end[k];
+        } else {  // segment end: the first record with another flowId
+            k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+            e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
+                return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
+            }, lane);
+        }
+        const uint64_t t0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
         walk_wave<L>(a, k, s, e);
+        if (a.dbg & 64) {
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t len = e - s;
+            const int b = len <= 64 ? 0 : len <= 256 ? 1 : len <= 1024 ? 2 : 3;
+            if (lane == 0) {
+                atomicAdd(&a.dbg_ctr[1 + 2 * b], 1ull);
+                atomicAdd(&a.dbg_ctr[2 + 2 * b], (unsigned long long)(t1 - t0));
+            }
+        }
     }
 }
 
-__global__ void __launch_bounds__(256) k_walk_long(BatchArgs a) {
+__global__ void __launch_bounds__(256, 2) k_walk_long(BatchArgs a) {
     if (*a.err) return;
     stage_periods(a);
     if (g_blds) walk_long_body<true>(a);
@@ -818,8 +840,8 @@ constexpr int kBlk = 8;  // records per block of the short walker's double-buffe
 // pass. The period-open code (ring sums over S slots, bucket close) thus runs ~once per period of the
 // wave instead of in almost every record step (64 lanes each change period every few records).
 template <int SM, bool L>
-__device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, const Rule& R,
-                                         const Occ& occ, SlotSnap* snap, uint64_t* buf) {
+__device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, uint64_t e,
+                                         const Rule& R, const Occ& occ, SlotSnap* snap, uint64_t* buf) {
     Bucket* ring = a.ring + (size_t)k * a.stride;
     const int S = R.S;
     const int64_t wl = R.wl;
@@ -837,7 +859,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     uint64_t nb[kBlk];
     uint64_t p = s;  // position of buf[0]'s block
     int left = kBlk; // records of the current block not yet consumed (buf[0] is the next one)
-    bool more = act && (uint32_t)(buf[kBlk - 1] >> a.kshift) == k;  // the segment continues past this block
+    bool more = act && p + kBlk < e;  // the segment continues past this block
     if (more) {
 #pragma unroll
         for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
@@ -867,7 +889,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
             for (int u = 0; u < kBlk; ++u) buf[u] = nb[u];
             p += kBlk;
             left = kBlk;
-            more = (uint32_t)(buf[kBlk - 1] >> a.kshift) == k;
+            more = p + kBlk < e;
             if (more) {
 #pragma unroll
                 for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
@@ -879,7 +901,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                if (!(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
+                store_bucket(ring + I, ws, ps.cur);
                 snap[I].start = ws;
                 snap[I].pass = ps.cur[SG_EV_PASS];
                 snap[I].wait = ps.cur[SG_EV_WAITING];
@@ -919,7 +941,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
                 ps.cur[SG_EV_PASS] += dn.acq;
                 ps.cur[SG_EV_PASS_REQUEST] += 1;
                 if (dn.prio) ps.cur[SG_EV_OCCUPIED_PASS] += dn.acq;
-                if (!(a.dbg & 256)) store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+                store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
             } else {
                 int32_t wait;
                 const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, dn.acq, dn.prio, &wait);
@@ -929,8 +951,9 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
             if (live) peek();
         }
     }
+
     if (act) {
-        if (I >= 0 && !(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
+        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
         Occ o;
         o.pass = ps.occ_pass;
         o.pass_req = ps.occ_req;
@@ -985,6 +1008,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
             const uint64_t s = a.short_list[li];
             const uint32_t k = a.short_key[li];
             // 2. everything that depends on (s, k) only
+            const uint64_t e = a.seg_end[k];
             const Rule R = a.rules[k];
             const Occ occ = a.occ[k];
             uint64_t buf[kBlk];
@@ -1024,7 +1048,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const uint64_t tw1 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-            walk_reg<SM, L>(a, act, k, s, R, occ, snap + lane * SM, buf);
+            walk_reg<SM, L>(a, act, k, s, e, R, occ, snap + lane * SM, buf);
             if (a.dbg & 64) {  // per class: groups, gather time, walk time (100 MHz ticks)
                 const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
                 if (lane == 0) {
