@@ -554,6 +554,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.n = n;
     a.rec = h->d_rec;
     a.rec_sorted = h->d_rec_sorted;
+    a.hist0 = h->n_lim > 0 ? nullptr : h->d_hist;  // the limiter pre-pass rewrites records after k_prep
     a.kshift = 64 - h->kbits;
     a.abits = h->abits;
     a.imask = (h->ibits >= 64) ? ~0ull : ((1ull << h->ibits) - 1);
@@ -613,7 +614,8 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
-        HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, a.kshift, h->d_hist, &sorted, stream));
+        HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, a.kshift, h->d_hist, &sorted, stream, 64,
+                                      a.hist0 != nullptr));
         a.rec_sorted = sorted;
         h->last_sorted = sorted;
     }

@@ -55,6 +55,7 @@ struct BatchArgs {
     sg_result* out;
     uint64_t n;
     uint64_t* rec;       // packed records, request order
+    uint32_t* hist0;     // k_prep: per-tile histogram of the first sort digit (radix_hist layout), or nullptr
     uint64_t* rec_sorted;
     // record layout: [key : kbits][idx : ibits][acode : abits], acode = acquire << 1 | prio
     int kshift;          // = 64 - kbits
@@ -327,7 +328,7 @@ hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream, int hi_bit = 64);
+                              uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker

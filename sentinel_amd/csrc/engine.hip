@@ -89,11 +89,23 @@ __device__ __forceinline__ Decoded decode(const BatchArgs& a, uint64_t rec) {
 
 // ------------------------------------------------------------------------------------------- prep
 
+// One block per 4096-request tile (the radix sort's tile). With a.hist0 set the block also counts the
+// first sort pass's digits of its records (the sort then skips that histogram read).
+constexpr int kPrepItems = 16;
+constexpr uint32_t kPrepTile = 256 * kPrepItems;
+
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
+    __shared__ uint32_t dcnt[256];
     const uint64_t n = a.n;
     const int64_t t0 = a.req[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (a.hist0) dcnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kPrepTile;
+#pragma unroll 4
+    for (int it = 0; it < kPrepItems; ++it) {
+        const uint64_t i = base + (uint64_t)it * 256 + threadIdx.x;
+        if (i >= n) break;
         const sg_req r = a.req[i];
         const int64_t t = r.ts_ms;
         if (i == 0) {
@@ -141,6 +153,11 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             store_result(a.out, (uint32_t)i, SG_STATUS_BLOCKED, 0, 0);  // walkers write only non-BLOCKED
         }
         a.rec[i] = rec;
+        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & 255u], 1u);
+    }
+    if (a.hist0) {
+        __syncthreads();
+        a.hist0[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = dcnt[threadIdx.x];
     }
 }
 
@@ -1186,7 +1203,7 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 }
 
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_prep, dim3(grid_for(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -196,13 +196,15 @@ size_t radix_hist_words(uint64_t n) {
     return (size_t)(words + nb + 64);
 }
 
-static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream) {
+static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
+                       bool hist_ready) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint64_t words = (uint64_t)ntiles * kBins;
     const uint32_t nb = (uint32_t)((words + kScanChunk - 1) / kScanChunk);
     uint32_t* hist = hist_ws;
     uint32_t* sums = hist_ws + words;
-    hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
+    if (!hist_ready)
+        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
     hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(kSortThreads), 0, stream, hist, words, sums);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kSortThreads), 0, stream, sums, nb);
     hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, sums,
@@ -211,12 +213,13 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),
 // ping-ponging between a and b. Returns the buffer that holds the result through *result.
+// first_hist_ready: the first pass's per-tile histogram is already in hist_ws (k_prep counted it).
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream, int hi_bit) {
+                              uint64_t** result, hipStream_t stream, int hi_bit, bool first_hist_ready) {
     uint64_t* src = a;
     uint64_t* dst = b;
     for (int shift = lo_bit; shift < hi_bit && n > 0; shift += 8) {
-        radix_pass(src, dst, n, shift, hist_ws, stream);
+        radix_pass(src, dst, n, shift, hist_ws, stream, shift == lo_bit && first_hist_ready);
         uint64_t* t = src;
         src = dst;
         dst = t;
