@@ -18,7 +18,7 @@ for b in range(2):
     x = wl.batch(b)
     torch.cuda.synchronize()
     eng.decide_device(x.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-c = eng.debug_copy(5, np.uint64, 16).astype(np.uint64)
+c = eng.debug_copy(5, np.uint64, 32).astype(np.uint64)
 print(f"total group time {int(c[0]) / 100:.0f} us (summed over waves)")
 for cl in range(6):
     g = int(c[1 + cl])

@@ -1,4 +1,4 @@
-"""Long-walker timers (SG_DEBUG & 64 with SG_SHORT_MAX set, e.g. 16): per segment length bucket, segments and
+"""Long-walker timers (SG_DEBUG & 64): per segment length bucket, segments and
 average wave time per segment (s_memrealtime, 100 MHz). The short walker's timers are zeroed first by running
 it with no short segments... (both walkers share dbg_ctr: run with SG_SHORT_MAX small and read [1..8])."""
 import os, sys
@@ -19,8 +19,8 @@ for b in range(2):
     x = wl.batch(b)
     torch.cuda.synchronize()
     eng.decide_device(x.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-c = eng.debug_copy(5, np.uint64, 16).astype(np.uint64)
+c = eng.debug_copy(5, np.uint64, 32).astype(np.uint64)
 for i, name in enumerate(["<=64", "<=256", "<=1024", ">1024"]):
-    cnt, t = int(c[1 + 2 * i]), int(c[2 + 2 * i])
+    cnt, t, mx = int(c[16 + 2 * i]), int(c[17 + 2 * i]), int(c[24 + i])
     if cnt:
-        print(f"long segments {name:7s}: {cnt:7d}  {t / cnt / 100:8.2f} us/segment")
+        print(f"long segments {name:7s}: {cnt:7d}  {t / cnt / 100:8.2f} us/segment  max {mx / 100:8.2f} us")

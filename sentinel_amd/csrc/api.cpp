@@ -50,7 +50,7 @@ struct sg_handle {
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
     uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
     uint64_t class_off[kClasses]{};
-    unsigned long long* d_dbg = nullptr;   // [16] debug counters (SG_DEBUG & 64)
+    unsigned long long* d_dbg = nullptr;   // [32] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
     uint32_t* d_skip_count = nullptr;
     int* h_err = nullptr;       // pinned
@@ -122,6 +122,7 @@ struct sg_handle {
     bool stats_on = false;
     uint32_t short_max = kShortMax;   // default walker split (env SG_SHORT_MAX overrides, for tuning)
     int dbg = 0;                      // env SG_DEBUG: see BatchArgs::dbg
+    bool wide_seen = false;           // some loaded rule allowed bucket counts >= 2^30 (sticky: the ring keeps them)
     hipEvent_t ev[5]{};
     sg_batch_stats stats{};
     hipStream_t aux = nullptr;        // second stream: the long-segment walker runs beside the short one
@@ -222,7 +223,16 @@ int rebuild_wl_table(sg_handle* h) {
 int upload_rule_table(sg_handle* h) {
     int rc = rebuild_wl_table(h);
     if (rc) return rc;
-    for (uint32_t k = 0; k < h->K; ++k) h->rule_tab[k].thr = global_threshold(h, h->rules[k]);
+    // Bucket counts stay below thr * (2 + isec) * (2 + maxOccupyRatio): a pass needs PASS sum <= thr * isec,
+    // an occupy acquire + occupied <= thr + head and WAITING sum <= ratio * thr * isec before it adds acquire.
+    // Below 2^30 the short walker may hold PASS / WAITING in int32 (BatchArgs::narrow).
+    const double ratio = h->cfg.max_occupy_ratio > 0 ? h->cfg.max_occupy_ratio : 0.0;
+    for (uint32_t k = 0; k < h->K; ++k) {
+        Rule& R = h->rule_tab[k];
+        R.thr = global_threshold(h, h->rules[k]);
+        const double bound = (R.thr > 0 ? R.thr : 0.0) * (2.0 + R.isec) * (2.0 + ratio);
+        if (!(bound < 1073741824.0)) h->wide_seen = true;
+    }
     if (h->K) HIP_TRY(h, hipMemcpy(h->d_rules, h->rule_tab.data(), sizeof(Rule) * h->K, hipMemcpyHostToDevice));
     // limiter slot of each rule's namespace
     dfree(h->d_rule_lim);
@@ -289,7 +299,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
             hipMalloc(&h->d_short_key, sizeof(uint32_t) * off) != hipSuccess)
             return bail(SG_E_NOMEM);
     }
-    if (hipMalloc(&h->d_dbg, 16 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 16 * 8) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_dbg, 32 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 32 * 8) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_count, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_skips, sizeof(uint4) * (2 * n / kSkipMin + 1)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_skip_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -585,6 +595,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.skip_count = h->d_skip_count;
     a.dbg = h->dbg;
     a.generic_walker = (h->cfg.flags & SG_FLAG_RING_REREAD) != 0;
+    a.narrow = h->wide_seen ? 0 : 1;
     a.dbg_ctr = h->d_dbg;
     a.skip_cap = (uint32_t)(2 * h->cfg.max_batch / kSkipMin + 1);
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
@@ -1314,7 +1325,7 @@ int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {
     case 2: src = h->d_bnd; cap = sizeof(uint32_t) * kMaxWl * kMaxPeriods; break;
     case 3: src = h->d_p0; cap = sizeof(int64_t) * kMaxWl; break;
     case 4: src = h->d_np; cap = sizeof(uint32_t) * kMaxWl; break;
-    case 5: src = h->d_dbg; cap = 16 * 8; break;
+    case 5: src = h->d_dbg; cap = 32 * 8; break;
     default: return SG_E_INVAL;
     }
     if (bytes > cap) return SG_E_INVAL;

@@ -40,6 +40,7 @@ constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
 constexpr int kShortMax = 256;            // default: segments longer than this are walked by a whole wave
 constexpr int kLdsBnd = 4096;             // period-table entries the walk kernel stages in LDS
+constexpr int kLdsBndFlow = 2048;         // the same for the cluster flow walkers (LDS budget of the short walker)
 // Short segments are grouped by length class (length <= 4, 16, 64, 256, 1024, more) so that the 64 lanes
 // of a short-walker wave walk segments of similar length.
 constexpr int kClasses = 6;
@@ -87,8 +88,9 @@ struct BatchArgs {
     uint32_t short_max;  // segments longer than this go to the wave walker
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
                          // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr
+    int narrow;          // PASS / WAITING of every bucket provably < 2^30 (short walker's 12 B LDS snapshot)
     int generic_walker;  // SG_FLAG_RING_REREAD: short walker re-reads the ring (no register snapshot)
-    unsigned long long* dbg_ctr;  // [16]
+    unsigned long long* dbg_ctr;  // [32]
     // ranges of records the wave walker skipped as certainly BLOCKED: {flow key, period q, begin, end}
     uint4* skips;
     uint32_t* skip_count;

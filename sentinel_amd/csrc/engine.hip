@@ -224,7 +224,7 @@ __device__ __forceinline__ void open_bucket(PeriodState& ps, int64_t start, cons
 // staged in LDS by stage_periods when they fit, else read from a.bnd. File-scope LDS keeps every access a
 // ds_read: a table pointer that may point at LDS or HBM compiles to flat loads, and each of those waits
 // for every outstanding global load and store of the wave (s_waitcnt vmcnt(0) lgkmcnt(0)).
-__shared__ uint32_t g_sbnd[kLdsBnd];
+__shared__ uint32_t g_sbnd[kLdsBndFlow];
 __shared__ uint32_t g_boff[kMaxWl];  // offset of window length w's table in g_sbnd
 __shared__ int g_blds;               // 1: tables in g_sbnd, 0: read from a.bnd
 
@@ -768,7 +768,7 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
 __device__ __forceinline__ void stage_periods(const BatchArgs& a) {
     uint32_t tot = 0;
     for (int w = 0; w < a.n_wl; ++w) tot += a.np[w];
-    const bool lds = tot <= (uint32_t)kLdsBnd && !(a.dbg & 1);
+    const bool lds = tot <= (uint32_t)kLdsBndFlow && !(a.dbg & 1);
     uint32_t off = 0;
     for (int w = 0; w < a.n_wl; ++w) {
         const uint32_t npw = a.np[w];
@@ -813,8 +813,9 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
             const uint64_t len = e - s;
             const int b = len <= 64 ? 0 : len <= 256 ? 1 : len <= 1024 ? 2 : 3;
             if (lane == 0) {
-                atomicAdd(&a.dbg_ctr[1 + 2 * b], 1ull);
-                atomicAdd(&a.dbg_ctr[2 + 2 * b], (unsigned long long)(t1 - t0));
+                atomicAdd(&a.dbg_ctr[16 + 2 * b], 1ull);
+                atomicAdd(&a.dbg_ctr[17 + 2 * b], (unsigned long long)(t1 - t0));
+                atomicMax(&a.dbg_ctr[24 + b], (unsigned long long)(t1 - t0));
             }
         }
     }
@@ -832,10 +833,34 @@ __global__ void __launch_bounds__(256, 2) k_walk_long(BatchArgs a) {
 // stored period), each closed bucket is written back, nothing is re-read. Same decisions as walk_serial,
 // which re-reads the ring at every new period (the working set of all lanes does not fit L2).
 
-// {start, PASS, WAITING} of one ring slot, staged in LDS by a wave's cooperative ring gather.
+// {start, PASS, WAITING} of one ring slot, staged in LDS by a wave's cooperative ring gather: 12 B, so that
+// four 256-thread blocks of the short walker fit a CU's LDS. `st` is the window start relative to the batch's
+// base time T0 (INT32_MIN: never created; starts older than T0 - 2^30 clamp to -2^30, which every validity
+// test treats as deprecated). PASS and WAITING are exact in int32 when BatchArgs::narrow holds (the host's
+// bound on every rule's threshold, see upload_rule_table); the walker runs only then, and when the batch's
+// periods lie within 2^29 ms of T0 (narrow_span).
 struct SlotSnap {
-    int64_t start, pass, wait;
+    int32_t st, pass, wait;
 };
+constexpr int32_t kSnapOld = -(1 << 30);
+
+__device__ __forceinline__ int32_t snap_rel(int64_t start, int64_t T0) {
+    if (start == INT64_MIN) return INT32_MIN;
+    const int64_t d = start - T0;
+    return d < (int64_t)kSnapOld ? kSnapOld : d > (int64_t)(1 << 30) ? (1 << 30) : (int32_t)d;
+}
+
+// All of the batch's window periods, and S + 1 periods before them, lie within 2^29 ms of T0 (wave-uniform).
+__device__ __forceinline__ bool narrow_span(const BatchArgs& a, int64_t T0) {
+    bool ok = true;
+    for (int w = 0; w < a.n_wl; ++w) {
+        const int64_t wl = a.wl[w];
+        const int64_t b = a.p0[w] * wl;
+        ok = ok && (b + ((int64_t)a.np[w] + 1) * wl - T0 < (1ll << 29)) &&
+             (b - ((int64_t)a.stride + 1) * wl - T0 > -(1ll << 29));
+    }
+    return ok;
+}
 
 __device__ __forceinline__ void store_bucket(Bucket* b, int64_t start, const int64_t* c) {
     ulonglong2* p = reinterpret_cast<ulonglong2*>(b);
@@ -845,7 +870,7 @@ __device__ __forceinline__ void store_bucket(Bucket* b, int64_t start, const int
     p[3] = make_ulonglong2((unsigned long long)c[5], (unsigned long long)c[6]);
 }
 
-constexpr int kBlk = 8;  // records per block of the short walker's double-buffered record stream
+constexpr int kBlk = 4;  // records per block of the short walker's double-buffered record stream
 
 // Walk of one flowId segment per lane, all 64 lanes of the wave together (inactive lanes pass act =
 // false). `snap` holds the lane's ring snapshot {start, PASS, WAITING} of its S <= SM slots (gathered
@@ -858,7 +883,7 @@ constexpr int kBlk = 8;  // records per block of the short walker's double-buffe
 // wave instead of in almost every record step (64 lanes each change period every few records).
 template <int SM, bool L>
 __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, uint64_t e,
-                                         const Rule& R, const Occ& occ, SlotSnap* snap, uint64_t* buf) {
+                                         const Rule& R, const Occ& occ, SlotSnap* snap, uint64_t* buf, int64_t T0) {
     Bucket* ring = a.ring + (size_t)k * a.stride;
     const int S = R.S;
     const int64_t wl = R.wl;
@@ -873,24 +898,25 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     ps.wo_pass = ps.wo_wait = ps.head_other = 0;
     int I = -1;      // slot of the open period
     int64_t ws = 0;  // its window start
+    // Record loads are unconditional (indices clamped to n - 1; the segment end is tested by position): a
+    // conditional load's value meets a constant in a phi, and that copy waits for the load at once, which
+    // turned the prefetch into a full memory round trip every kBlk records.
+    const uint64_t n1 = a.n - 1;
     uint64_t nb[kBlk];
     uint64_t p = s;  // position of buf[0]'s block
     int left = kBlk; // records of the current block not yet consumed (buf[0] is the next one)
     bool more = act && p + kBlk < e;  // the segment continues past this block
-    if (more) {
 #pragma unroll
-        for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
-    }
+    for (int u = 0; u < kBlk; ++u) nb[u] = a.rec_sorted[min(p + kBlk + u, n1)];
     bool live = act;  // records left
     uint32_t qn = 0;  // period of the next record (valid when live)
     Decoded dn;       // the next record, decoded
     auto peek = [&]() {  // look at buf[0]: end of segment, or decode it and find its period
-        const uint64_t cur = buf[0];
-        if ((uint32_t)(cur >> a.kshift) != k) {
+        if (p + (uint64_t)(kBlk - left) >= e) {
             live = false;
             return;
         }
-        dn = decode(a, cur);
+        dn = decode(a, buf[0]);
         qn = pc.of(dn.idx);
     };
     auto advance = [&]() {  // consume buf[0]
@@ -907,10 +933,8 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
             p += kBlk;
             left = kBlk;
             more = p + kBlk < e;
-            if (more) {
 #pragma unroll
-                for (int u = 0; u < kBlk; ++u) nb[u] = p + kBlk + u < a.n ? a.rec_sorted[p + kBlk + u] : ~0ull;
-            }
+            for (int u = 0; u < kBlk; ++u) nb[u] = a.rec_sorted[min(p + kBlk + u, n1)];
         }
     };
     if (live) peek();
@@ -919,30 +943,42 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
         if (live && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
                 store_bucket(ring + I, ws, ps.cur);
-                snap[I].start = ws;
-                snap[I].pass = ps.cur[SG_EV_PASS];
-                snap[I].wait = ps.cur[SG_EV_WAITING];
+                snap[I].st = (int32_t)(ws - T0);
+                snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
+                snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
             }
             const uint32_t qprev = pc.q;
             pc.seek(qn);
             const int64_t P = P0 + (int64_t)qn;
             I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
             ws = P * wl;
-            const int64_t lo = ws - (int64_t)S * wl;  // LeapArray.isWindowDeprecated: valid iff start > lo
+            // LeapArray.isWindowDeprecated: valid iff start > ws - S*wl (compared relative to T0)
+            const int64_t lo_rel = ws - (int64_t)S * wl - T0;
             const int h = I + 1 == S ? 0 : I + 1;
-            ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+            // all slots read at once, then summed branch-free; sums of valid buckets are window sums, < 2^30
+            // under BatchArgs::narrow, so 32-bit accumulation is exact
+            int32_t sx[SM], px[SM], wx[SM];
 #pragma unroll
             for (int x = 0; x < SM; ++x) {
-                if (x < S && x != I) {
-                    const SlotSnap& e = snap[x];
-                    const bool v = e.start > lo;
-                    ps.wo_pass += v ? e.pass : 0;
-                    ps.wo_wait += v ? e.wait : 0;
-                    if (x == h && v) ps.head_other = e.pass;
-                }
+                sx[x] = snap[x].st;
+                px[x] = snap[x].pass;
+                wx[x] = snap[x].wait;
             }
+            uint32_t wp = 0, ww = 0, ho = 0;
+#pragma unroll
+            for (int x = 0; x < SM; ++x) {
+                const bool v = (x < S) & (x != I) & ((int64_t)sx[x] > lo_rel);
+                const uint32_t m = v ? 0xFFFFFFFFu : 0u;
+                wp += (uint32_t)px[x] & m;
+                ww += (uint32_t)wx[x] & m;
+                ho = (x == h) ? ((uint32_t)px[x] & m) : ho;
+            }
+            ps.wo_pass = (int64_t)wp;
+            ps.wo_wait = (int64_t)ww;
+            ps.head_other = (int64_t)ho;
             // currentWindow on slot I: continue (only possible at the batch's first period), create or reset
-            const int64_t stI = snap[I].start;
+            const int32_t stI_rel = snap[I].st;
+            const int64_t stI = stI_rel == INT32_MIN ? INT64_MIN : T0 + (int64_t)stI_rel;
             int64_t cI[SG_NUM_EVENTS];
             if (stI == ws) {
 #pragma unroll
@@ -989,7 +1025,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
 // {OCCUPIED_BLOCK, WAITING} at byte 48 of each bucket), row-shaped instead of 64 lanes in 64 rows.
 constexpr int kGatherMaxS = 10;
 #ifndef SG_SHORT_BLOCKS
-#define SG_SHORT_BLOCKS 2
+#define SG_SHORT_BLOCKS 3
 #endif
 constexpr int kShortBlocksPerCu = SG_SHORT_BLOCKS;  // occupancy target (VGPR budget) of the short walker
 
@@ -1008,6 +1044,9 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
     }
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    // the LDS-snapshot walker needs the narrow encoding (else every lane re-reads its ring: walk_serial)
+    const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
+    const bool snap_ok = SM > 0 && a.narrow && narrow_span(a, T0);
     for (uint32_t g = wave; g < total; g += nwaves) {
         int c = kClasses - 1;
         uint32_t g0 = 0;
@@ -1018,7 +1057,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
         c = __builtin_amdgcn_readfirstlane(c);
         const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
         const bool act = i < cnt[c];
-        if constexpr (SM > 0) {
+        if constexpr (SM > 0) if (snap_ok) {
             const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
             // 1. segment descriptors (inactive lanes of the last group repeat entry 0: valid addresses)
             const uint64_t li = a.class_off[c] + (act ? i : 0u);
@@ -1030,17 +1069,21 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
             const Occ occ = a.occ[k];
             uint64_t buf[kBlk];
 #pragma unroll
-            for (int u = 0; u < kBlk; ++u) buf[u] = s + u < a.n ? a.rec_sorted[s + u] : ~0ull;
+            for (int u = 0; u < kBlk; ++u) buf[u] = a.rec_sorted[min(s + u, a.n - 1)];
             {
                 // piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS}, 1: WAITING);
                 // slots past the handle's stride read slot 0 again (ignored: q >= S)
                 constexpr int kT = 2 * SM;  // pieces per lane, loaded in two batches of SM
+                // the piece addresses depend on the lane only: an opaque copy of it keeps the compiler from
+                // hoisting ~3 * kT of them out of the group loop (they held 60+ VGPRs for the whole walk)
+                int gl = lane;
+                asm volatile("" : "+v"(gl));
 #pragma unroll
                 for (int t0 = 0; t0 < kT; t0 += SM) {
                     ulonglong2 v[SM];
 #pragma unroll
                     for (int t = 0; t < SM; ++t) {
-                        const int pc = (t0 + t) * 64 + lane;
+                        const int pc = (t0 + t) * 64 + gl;
                         const int j = pc / kT;
                         const int q = (pc % kT) >> 1;
                         const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
@@ -1050,13 +1093,13 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
                     }
 #pragma unroll
                     for (int t = 0; t < SM; ++t) {
-                        const int pc = (t0 + t) * 64 + lane;
+                        const int pc = (t0 + t) * 64 + gl;
                         SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
                         if (pc & 1) {
-                            d.wait = (int64_t)v[t].y;
+                            d.wait = (int32_t)v[t].y;
                         } else {
-                            d.start = (int64_t)v[t].x;
-                            d.pass = (int64_t)v[t].y;
+                            d.st = snap_rel((int64_t)v[t].x, T0);
+                            d.pass = (int32_t)v[t].y;
                         }
                     }
                 }
@@ -1065,7 +1108,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const uint64_t tw1 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-            walk_reg<SM, L>(a, act, k, s, e, R, occ, snap + lane * SM, buf);
+            walk_reg<SM, L>(a, act, k, s, e, R, occ, snap + lane * SM, buf, T0);
             if (a.dbg & 64) {  // per class: groups, gather time, walk time (100 MHz ticks)
                 const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
                 if (lane == 0) {
