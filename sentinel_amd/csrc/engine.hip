@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             const int64_t tp = a.req[i - 1].ts_ms;
             if (t < tp || t < 0) {
                 atomicOr(a.err, kErrTime);
-            } else {
+            } else if (t != tp) {  // a new period can only start at a new timestamp (skips the int64 divisions)
                 for (int w = 0; w < a.n_wl; ++w) {
                     const int64_t wl = a.wl[w];
                     const int64_t P0 = t0 / wl, Pp = tp / wl, Pi = t / wl;
@@ -942,7 +942,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                store_bucket(ring + I, ws, ps.cur);
+                if (!(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
                 snap[I].st = (int32_t)(ws - T0);
                 snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
                 snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
@@ -994,11 +994,11 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
                 ps.cur[SG_EV_PASS] += dn.acq;
                 ps.cur[SG_EV_PASS_REQUEST] += 1;
                 if (dn.prio) ps.cur[SG_EV_OCCUPIED_PASS] += dn.acq;
-                store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+                if (!(a.dbg & 256)) store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
             } else {
                 int32_t wait;
                 const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, dn.acq, dn.prio, &wait);
-                if (stt != SG_STATUS_BLOCKED) store_result(a.out, dn.idx, stt, 0, wait);
+                if (stt != SG_STATUS_BLOCKED && !(a.dbg & 256)) store_result(a.out, dn.idx, stt, 0, wait);
             }
             advance();
             if (live) peek();

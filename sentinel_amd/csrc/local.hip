@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
             const int64_t tp = a.ev[i - 1].ts_ms;
             if (t < tp || t < 0) {
                 atomicOr(a.err, kErrTime);
-            } else {
+            } else if (t != tp) {  // a new period can only start at a new timestamp (skips the int64 divisions)
                 for (int w = 0; w < a.n_wl; ++w) {
                     const int64_t wl = a.wl[w];
                     const int64_t P0 = t0 / wl, Pp = tp / wl, Pi = t / wl;
