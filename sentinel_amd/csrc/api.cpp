@@ -49,6 +49,7 @@ struct sg_handle {
     uint32_t* d_short_list = nullptr;
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
     uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
+    uint32_t* d_long_pend = nullptr;  // [kLongTab][kLongPeriods] period ends of the long segments
     uint64_t class_off[kClasses]{};
     unsigned long long* d_dbg = nullptr;   // [32] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
@@ -287,7 +288,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
-        hipMalloc(&h->d_long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess)
+        hipMalloc(&h->d_long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&h->d_long_pend, sizeof(uint32_t) * (size_t)kLongTab * kLongPeriods) != hipSuccess)
         return bail(SG_E_NOMEM);
     {  // short-segment class slices: class c holds segments longer than kClassMax[c-1], so at most n/(that+1)
         uint64_t off = 0;
@@ -349,6 +351,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_short_list);
     dfree(h->d_short_key);
     dfree(h->d_long_key);
+    dfree(h->d_long_pend);
     dfree(h->d_dbg);
     dfree(h->d_skips);
     dfree(h->d_prules);
@@ -589,6 +592,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.short_list = h->d_short_list;
     a.short_key = h->d_short_key;
     a.long_key = h->d_long_key;
+    a.long_pend = h->d_long_pend;
     a.short_count = h->d_long_count + 1;
     for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
     a.skips = h->d_skips;

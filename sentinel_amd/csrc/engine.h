@@ -84,6 +84,8 @@ struct BatchArgs {
     uint32_t* short_key;   // flowId of each short_list entry (nullptr: not written)
     uint32_t* long_key;    // flowId of each long_list entry (nullptr: not written)
     uint32_t* seg_end;     // [K] end of each present key's segment in rec_sorted (nullptr: not written)
+    uint32_t* long_pend;   // [kLongTab][kLongPeriods]: position in rec_sorted where period q + 1 of long segment
+                           // i begins (k_long_bounds; nullptr: the wave walker searches for it)
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
     uint32_t short_max;  // segments longer than this go to the wave walker
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
@@ -97,6 +99,8 @@ struct BatchArgs {
     uint32_t skip_cap;
 };
 
+constexpr int kLongPeriods = 16;       // period-end table of the wave walker: batches of <= 16 window periods
+constexpr uint32_t kLongTab = 65536;  // long segments with a table (later ones search)
 constexpr uint32_t kSkipMin = 256;    // shortest all-BLOCKED tail worth skipping (records)
 constexpr uint32_t kSkipPiece = 4096; // skipped ranges are handed to k_skip_apply in pieces of this size
 

@@ -604,9 +604,13 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
 }
 
 template <bool L>
-__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e) {
+__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e, uint32_t item) {
     WaveWalker<L> w(a, k);
     const int lane = w.lane;
+    // period ends of this segment from k_long_bounds: lane q holds the first position of period q + 1
+    const bool tab = a.long_pend != nullptr && item < kLongTab && w.pc.np <= (uint32_t)kLongPeriods;
+    uint32_t pend_l = 0;
+    if (tab && lane < kLongPeriods) pend_l = a.long_pend[(size_t)item * kLongPeriods + lane];
     const uint64_t* rec = a.rec_sorted;
     constexpr uint64_t kBlock = 64ull * kWaveUnroll;
     uint64_t cur[kWaveUnroll];
@@ -637,9 +641,15 @@ __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e
                 // and hand the skipped range to k_skip_apply (its BLOCK counts only).
                 skip_tried_q = w.pc.q;
                 const uint32_t nb = w.pc.next_b;
-                const uint64_t pe = wave_search(after, e, [&](uint64_t p) {
-                    return (uint32_t)((rec[p] >> a.abits) & a.imask) >= nb;
-                }, lane);
+                uint64_t pe;
+                if (tab) {
+                    pe = w.pc.q + 1 >= w.pc.np ? e : (uint64_t)(uint32_t)bcast32((int)pend_l, (int)w.pc.q);
+                    pe = pe < after ? after : pe;
+                } else {
+                    pe = wave_search(after, e, [&](uint64_t p) {
+                        return (uint32_t)((rec[p] >> a.abits) & a.imask) >= nb;
+                    }, lane);
+                }
                 if (pe - after >= kSkipMin) {
                     // hand the range over in pieces of <= kSkipPiece records (one k_skip_apply wave each)
                     const uint32_t np = (uint32_t)((pe - after + kSkipPiece - 1) / kSkipPiece);
@@ -807,7 +817,7 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
             }, lane);
         }
         const uint64_t t0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-        walk_wave<L>(a, k, s, e);
+        walk_wave<L>(a, k, s, e, item);
         if (a.dbg & 64) {
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
             const uint64_t len = e - s;
@@ -818,6 +828,30 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
                 atomicMax(&a.dbg_ctr[24 + b], (unsigned long long)(t1 - t0));
             }
         }
+    }
+}
+
+// Period ends of the long segments (one thread per segment and period): the wave walker jumps over a
+// window period that can admit nothing more without searching for where it ends (that search was a
+// chain of dependent loads per period). Runs on the wave walker's stream just before it.
+__global__ void __launch_bounds__(256) k_long_bounds(BatchArgs a) {
+    if (*a.err) return;
+    const uint32_t n_long = min(*a.long_count, kLongTab);
+    const uint32_t total = n_long * (uint32_t)kLongPeriods;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const uint32_t item = t / kLongPeriods, q = t % kLongPeriods;
+        const uint32_t k = a.long_key[item];
+        const int w = a.rules[k].wl_idx;
+        const uint32_t npw = a.np[w];
+        if (npw > (uint32_t)kLongPeriods || q + 1 >= npw) continue;
+        const uint32_t nb = a.bnd[(size_t)w * kMaxPeriods + q + 1];
+        uint64_t lo = a.long_list[item], hi = a.seg_end[k];
+        while (lo < hi) {  // first record of the segment in period q + 1 or later
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((uint32_t)((a.rec_sorted[mid] >> a.abits) & a.imask) >= nb) hi = mid;
+            else lo = mid + 1;
+        }
+        a.long_pend[t] = (uint32_t)lo;
     }
 }
 
@@ -1265,6 +1299,7 @@ static unsigned resident_blocks(const void* kernel, int block) {
 
 // Persistent walkers: at most as many blocks as fit on the chip at once (each wave loops over its queue).
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
+    if (a.long_pend && a.long_key && a.seg_end) hipLaunchKernelGGL(k_long_bounds, dim3(1024), dim3(256), 0, stream, a);
     static unsigned blocks = 0;
     if (blocks == 0) blocks = resident_blocks((const void*)k_walk_long, 256);
     hipLaunchKernelGGL(k_walk_long, dim3(blocks), dim3(256), 0, stream, a);
