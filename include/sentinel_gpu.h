@@ -327,6 +327,37 @@ int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t 
  * count, total count, 0}. */
 int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head);
 
+/* ---------- token-server wire codec ----------
+ * The default token server frames every message with a 2-byte big-endian length
+ * (LengthFieldBasedFrameDecoder(1024, 0, 2, 0, 2) / LengthFieldPrepender(2),
+ * srv/server/NettyTransportServer.java:89-92). A request payload is [i32 xid][u8 type][data]
+ * (DefaultRequestEntityDecoder.java:36-58); MSG_TYPE_FLOW data is [i64 flowId][i32 count][bool priority?]
+ * (FlowRequestDataDecoder.java:31-43). A response frame is [u16 len = 14][i32 xid][u8 type][u8 status]
+ * [i32 remaining][i32 waitInMs] (DefaultResponseEntityWriter.java:32-51, FlowResponseDataWriter.java:28-32),
+ * all big-endian (Netty ByteBuf). The batching front-end that a Netty handler feeds appends each frame's
+ * payload (length prefix stripped) to one buffer and records where it starts.
+ *
+ * sg_codec_decode_flow: payload bytes + offsets[n + 1] (frame i = [offsets[i], offsets[i+1])) + arrival
+ * timestamps → sg_req records for sg_flow_decide_batch (flowId → rule index through the handle's device
+ * table: unknown → SG_KEY_NO_RULE, flowId <= 0 → SG_KEY_BAD, as DefaultTokenService.requestToken would
+ * answer), the xid of every frame and its kind (SG_FRAME_*). Frames that are not decodable flow requests
+ * get key SG_KEY_BAD and acquire 0 (a harmless BAD_REQUEST slot in the batch). All pointers are device
+ * memory; the call is asynchronous on `stream`.
+ * sg_codec_encode_flow: one 16-byte response frame per request at frames_out + 16 * i (zero-filled for
+ * frames whose kind is not SG_FRAME_FLOW: the Java server sends nothing for those). */
+#define SG_MSG_TYPE_PING       0
+#define SG_MSG_TYPE_FLOW       1
+#define SG_MSG_TYPE_PARAM_FLOW 2
+#define SG_FRAME_FLOW     0   /* a flow token request, decoded                                          */
+#define SG_FRAME_SHORT    1   /* fewer than 5 bytes: DefaultRequestEntityDecoder returns null            */
+#define SG_FRAME_NO_DATA  2   /* MSG_TYPE_FLOW without a decodable body (fewer than 12 data bytes)       */
+#define SG_FRAME_OTHER    3   /* another message type (ping, param, concurrent): the host's own path     */
+#define SG_RESPONSE_FRAME_BYTES 16
+int sg_codec_decode_flow(sg_handle* h, const uint8_t* payload, const uint32_t* offsets, const int64_t* ts_ms,
+                         uint64_t n, sg_req* req_out, int32_t* xid_out, uint8_t* kind_out, void* stream);
+int sg_codec_encode_flow(sg_handle* h, const int32_t* xid, const uint8_t* kind, const sg_result* res, uint64_t n,
+                         uint8_t* frames_out, void* stream);
+
 /* Testing aid: copy an internal buffer of the last batch to host memory.
  * what: 0 = records (request order, u64), 1 = records sorted by flowId, 2 = window-period table
  * (u32 [8][65536]), 3 = first period per window length (i64[8]), 4 = periods per window length (u32[8]). */

@@ -82,6 +82,8 @@ def lib():
         "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
+        "or_codec_decode_flow": (None, [vp, vp, vp, u64, vp, u32, vp, vp, vp]),
+        "or_codec_encode_flow": (None, [vp, vp, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -439,3 +441,31 @@ class LocalTraceGen:
                               abi.ptr(out), abi.ptr(res), cap)
         assert k != 2**64 - 1
         return out[:k].copy(), res[:k].copy()
+
+
+# ---- token-server wire codec (DefaultRequestEntityDecoder / FlowRequestDataDecoder / DefaultResponseEntityWriter)
+def codec_decode_flow(payload: np.ndarray, offsets: np.ndarray, ts_ms: np.ndarray, flow_ids: np.ndarray):
+    """Frame payloads → (sg_req records, xids, kinds), as the default token server decodes them."""
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    if len(payload) == 0:
+        payload = np.zeros(1, np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    ts_ms = np.ascontiguousarray(ts_ms, dtype=np.int64)
+    flow_ids = np.ascontiguousarray(flow_ids, dtype=np.int64)
+    n = len(offsets) - 1
+    req = np.zeros(max(n, 1), abi.REQ_DTYPE)
+    xid = np.zeros(max(n, 1), np.int32)
+    kind = np.zeros(max(n, 1), np.uint8)
+    lib().or_codec_decode_flow(abi.ptr(payload), abi.ptr(offsets), abi.ptr(ts_ms), n, abi.ptr(flow_ids),
+                               len(flow_ids), abi.ptr(req), abi.ptr(xid), abi.ptr(kind))
+    return req[:n], xid[:n], kind[:n]
+
+
+def codec_encode_flow(xid: np.ndarray, kind: np.ndarray, res: np.ndarray) -> np.ndarray:
+    """16-byte response frames (length-prefixed), zeros where the kind is not a flow request."""
+    xid = np.ascontiguousarray(xid, dtype=np.int32)
+    kind = np.ascontiguousarray(kind, dtype=np.uint8)
+    res = np.ascontiguousarray(res, dtype=abi.RES_DTYPE)
+    out = np.zeros(max(len(xid), 1) * 16, np.uint8)
+    lib().or_codec_encode_flow(abi.ptr(xid), abi.ptr(kind), abi.ptr(res), len(xid), abi.ptr(out))
+    return out[:len(xid) * 16]

@@ -1410,3 +1410,104 @@ void or_cpm_free(or_cpm* m) { cpm_free(m); }
 void or_cpm_add(or_cpm* m, int64_t t, uint64_t value, int count) { cpm_add(m, t, value, count); }
 int64_t or_cpm_get_sum(or_cpm* m, int64_t t, uint64_t value) { return cpm_get_sum(m, t, value); }
 double or_cpm_get_avg(or_cpm* m, int64_t t, uint64_t value) { return (double)cpm_get_sum(m, t, value) / m->isec; }
+
+/* ==================================================================================== wire codec ==== */
+/* Restates the default token server's request decoding and response encoding byte for byte. Paths:
+ * srv/ = sentinel-cluster-server-default/.../cluster/server/. Netty's ByteBuf is big-endian:
+ * readInt/readLong/writeInt are network order. */
+
+static int64_t or_be64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+    return (int64_t)v;
+}
+
+static int32_t or_be32(const uint8_t* p) {
+    return (int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3]);
+}
+
+static void or_put32(uint8_t* p, int32_t v) {
+    p[0] = (uint8_t)((uint32_t)v >> 24);
+    p[1] = (uint8_t)((uint32_t)v >> 16);
+    p[2] = (uint8_t)((uint32_t)v >> 8);
+    p[3] = (uint8_t)v;
+}
+
+typedef struct {
+    int64_t fid;
+    uint32_t idx;
+} or_fid;
+
+static int or_fid_cmp(const void* a, const void* b) {
+    const or_fid* x = (const or_fid*)a;
+    const or_fid* y = (const or_fid*)b;
+    return x->fid < y->fid ? -1 : x->fid > y->fid ? 1 : 0;
+}
+
+void or_codec_decode_flow(const uint8_t* payload, const uint32_t* offsets, const int64_t* ts_ms, uint64_t n,
+                          const int64_t* flow_ids, uint32_t n_rules, sg_req* req_out, int32_t* xid_out,
+                          uint8_t* kind_out) {
+    /* ClusterFlowRuleManager.getFlowRuleById: flowId → rule (here its index; flowIds are unique) */
+    or_fid* map = (or_fid*)malloc(sizeof(or_fid) * (n_rules ? n_rules : 1));
+    for (uint32_t i = 0; i < n_rules; ++i) {
+        map[i].fid = flow_ids[i];
+        map[i].idx = i;
+    }
+    qsort(map, n_rules, sizeof(or_fid), or_fid_cmp);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t* p = payload + offsets[i];
+        const uint32_t len = offsets[i + 1] - offsets[i];
+        sg_req r;
+        r.ts_ms = ts_ms[i];
+        r.key = SG_KEY_BAD;
+        r.acquire = 0;
+        int32_t xid = 0;
+        uint8_t kind;
+        if (len < 5) {  /* DefaultRequestEntityDecoder.decode (:37): readableBytes() >= 5, else null */
+            kind = SG_FRAME_SHORT;
+        } else {
+            xid = or_be32(p);                 /* :38 source.readInt() */
+            const int type = (int8_t)p[4];    /* :39 source.readByte() */
+            const uint32_t rem = len - 5;
+            if (type != SG_MSG_TYPE_FLOW) {
+                kind = SG_FRAME_OTHER;
+            } else if (rem < 12) {  /* FlowRequestDataDecoder.decode (:33): readableBytes() >= 12, else null */
+                kind = SG_FRAME_NO_DATA;
+            } else {
+                kind = SG_FRAME_FLOW;
+                const int64_t flow_id = or_be64(p + 5);       /* :35 readLong() */
+                const int32_t count = or_be32(p + 13);        /* :36 readInt() */
+                const int prio = rem >= 13 ? p[17] != 0 : 0;  /* :37-39 readBoolean() when a byte is left */
+                r.acquire = count;
+                if (flow_id <= 0) {  /* DefaultTokenService.notValidRequest (:87-89) → badRequest() */
+                    r.key = SG_KEY_BAD;
+                } else {
+                    or_fid want = {flow_id, 0};
+                    const or_fid* hit = (const or_fid*)bsearch(&want, map, n_rules, sizeof(or_fid), or_fid_cmp);
+                    r.key = hit ? hit->idx : SG_KEY_NO_RULE;  /* rule == null → NO_RULE_EXISTS (:44-47) */
+                }
+                if (prio) r.key |= SG_KEY_PRIO;
+            }
+        }
+        req_out[i] = r;
+        xid_out[i] = xid;
+        kind_out[i] = kind;
+    }
+    free(map);
+}
+
+void or_codec_encode_flow(const int32_t* xid, const uint8_t* kind, const sg_result* res, uint64_t n,
+                          uint8_t* frames_out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        uint8_t* f = frames_out + (size_t)SG_RESPONSE_FRAME_BYTES * i;
+        memset(f, 0, SG_RESPONSE_FRAME_BYTES);
+        if (kind[i] != SG_FRAME_FLOW) continue;
+        f[0] = 0;  /* LengthFieldPrepender(2) (NettyTransportServer.java:91): payload length 14, big-endian */
+        f[1] = 14;
+        or_put32(f + 2, xid[i]);                /* DefaultResponseEntityWriter.writeHead: writeInt(id) */
+        f[6] = (uint8_t)SG_MSG_TYPE_FLOW;       /* writeByte(type) */
+        f[7] = (uint8_t)(int8_t)res[i].status;  /* writeByte(status): the low 8 bits */
+        or_put32(f + 8, res[i].remaining);      /* FlowResponseDataWriter.writeTo: writeInt(remainingCount) */
+        or_put32(f + 12, res[i].wait_ms);       /* writeInt(waitInMs) */
+    }
+}

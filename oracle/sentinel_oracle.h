@@ -149,6 +149,17 @@ uint64_t  or_lgen_pending(const or_lgen* g);
 uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
                       int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
 
+/* ---------- token-server wire codec (srv/server/codec and the cluster-common codec package) ---------- */
+/* Decodes n frame payloads (frame i = payload[offsets[i] .. offsets[i+1])) as the default token server
+ * would, mapping flowIds through flow_ids[0..n_rules) (rule index = position). Same outputs as
+ * sg_codec_decode_flow. */
+void or_codec_decode_flow(const uint8_t* payload, const uint32_t* offsets, const int64_t* ts_ms, uint64_t n,
+                          const int64_t* flow_ids, uint32_t n_rules, sg_req* req_out, int32_t* xid_out,
+                          uint8_t* kind_out);
+/* One 16-byte response frame per request (zeros for kinds other than SG_FRAME_FLOW). */
+void or_codec_encode_flow(const int32_t* xid, const uint8_t* kind, const sg_result* res, uint64_t n,
+                          uint8_t* frames_out);
+
 #ifdef __cplusplus
 }
 #endif

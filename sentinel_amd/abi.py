@@ -31,6 +31,11 @@ EV_PASS, EV_BLOCK, EV_PASS_REQUEST, EV_BLOCK_REQUEST, EV_OCCUPIED_PASS, EV_OCCUP
 NUM_EVENTS = 7
 
 KEY_PRIO = 0x80000000
+
+# token-server wire codec (include/sentinel_gpu.h SG_FRAME_*, SG_MSG_TYPE_*)
+MSG_TYPE_PING, MSG_TYPE_FLOW, MSG_TYPE_PARAM_FLOW = 0, 1, 2
+FRAME_FLOW, FRAME_SHORT, FRAME_NO_DATA, FRAME_OTHER = 0, 1, 2, 3
+RESPONSE_FRAME_BYTES = 16
 KEY_INDEX = 0x7FFFFFFF
 KEY_NO_RULE = 0x7FFFFFFF
 KEY_BAD = 0x7FFFFFFE

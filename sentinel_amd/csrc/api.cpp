@@ -49,7 +49,9 @@ struct sg_handle {
     uint32_t* d_short_list = nullptr;
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
     uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
-    uint32_t* d_long_pend = nullptr;  // [kLongTab][kLongPeriods] period ends of the long segments
+    uint32_t* d_long_pend = nullptr;
+    FidSlot* d_fid = nullptr;         // flowId → rule index (wire codec), 2^k slots
+    uint64_t fid_mask = 0;  // [kLongTab][kLongPeriods] period ends of the long segments
     uint64_t class_off[kClasses]{};
     unsigned long long* d_dbg = nullptr;   // [32] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
@@ -130,6 +132,10 @@ struct sg_handle {
     hipEvent_t fork = nullptr, join = nullptr;
 };
 
+extern "C" {
+static int upload_fid_table(sg_handle* h);  // flowId → rule index for the wire codec (defined below)
+}
+
 namespace {
 
 int fail(sg_handle* h, int code, const std::string& msg) {
@@ -185,6 +191,7 @@ int64_t java_math_round(double a) {
     if (a <= -9223372036854775808.0) return INT64_MIN;
     return (int64_t)a;
 }
+
 
 int layout_records(sg_handle* h) {
     h->kbits = bits_for((uint64_t)h->K);  // must hold K itself (sentinel key of rejected requests)
@@ -352,6 +359,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_short_key);
     dfree(h->d_long_key);
     dfree(h->d_long_pend);
+    dfree(h->d_fid);
     dfree(h->d_dbg);
     dfree(h->d_skips);
     dfree(h->d_prules);
@@ -534,7 +542,81 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     std::memcpy(h->wl, wl, sizeof(wl));
     int rc = layout_records(h);
     if (rc) return rc;
+    rc = upload_fid_table(h);
+    if (rc) return rc;
     return upload_rule_table(h);
+}
+
+// flowId → rule index for the wire codec: open addressing, linear probing, load factor <= 1/2 (the same
+// splitmix64 finaliser as codec.hip's fid_hash). flowIds are > 0 and unique (validated above).
+static uint64_t host_fid_hash(int64_t fid) {
+    uint64_t z = (uint64_t)fid + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int upload_fid_table(sg_handle* h) {
+    uint64_t cap = 2;
+    while (cap < 2ull * h->K) cap <<= 1;
+    std::vector<FidSlot> tab(cap, FidSlot{0, 0, 0});
+    for (uint32_t k = 0; k < h->K; ++k) {
+        const int64_t fid = h->rules[k].flow_id;
+        uint64_t p = host_fid_hash(fid) & (cap - 1);
+        while (tab[p].fid != 0) p = (p + 1) & (cap - 1);
+        tab[p] = FidSlot{fid, k, 0};
+    }
+    FidSlot* d = nullptr;
+    if (hipMalloc(&d, sizeof(FidSlot) * cap) != hipSuccess) return fail(h, SG_E_NOMEM, "flowId table");
+    if (hipMemcpy(d, tab.data(), sizeof(FidSlot) * cap, hipMemcpyHostToDevice) != hipSuccess) {
+        dfree(d);
+        return fail(h, SG_E_DEVICE, "flowId table upload");
+    }
+    dfree(h->d_fid);
+    h->d_fid = d;
+    h->fid_mask = cap - 1;
+    return SG_OK;
+}
+
+int sg_codec_decode_flow(sg_handle* h, const uint8_t* payload, const uint32_t* offsets, const int64_t* ts_ms,
+                         uint64_t n, sg_req* req_out, int32_t* xid_out, uint8_t* kind_out, void* stream) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!payload || !offsets || !ts_ms || !req_out || !xid_out || !kind_out) return fail(h, SG_E_INVAL, "null buffer");
+    if (!h->d_fid) {
+        int rc = upload_fid_table(h);  // no rules loaded yet: every flowId is unknown
+        if (rc) return rc;
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    CodecArgs c{};
+    c.n = n;
+    c.payload = payload;
+    c.offsets = offsets;
+    c.ts = ts_ms;
+    c.req = req_out;
+    c.xid = xid_out;
+    c.kind = kind_out;
+    c.fid_tab = h->d_fid;
+    c.fid_mask = h->fid_mask;
+    HIP_TRY(h, launch_codec_decode(c, (hipStream_t)stream));
+    return SG_OK;
+}
+
+int sg_codec_encode_flow(sg_handle* h, const int32_t* xid, const uint8_t* kind, const sg_result* res, uint64_t n,
+                         uint8_t* frames_out, void* stream) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!xid || !kind || !res || !frames_out) return fail(h, SG_E_INVAL, "null buffer");
+    if (((uintptr_t)frames_out & 15u) != 0) return fail(h, SG_E_INVAL, "frames_out must be 16-byte aligned");
+    HIP_TRY(h, hipSetDevice(h->device));
+    CodecArgs c{};
+    c.n = n;
+    c.xid_in = xid;
+    c.kind_in = kind;
+    c.res = res;
+    c.frames = frames_out;
+    HIP_TRY(h, launch_codec_encode(c, (hipStream_t)stream));
+    return SG_OK;
 }
 
 int sg_enable_stats(sg_handle* h, int on) {

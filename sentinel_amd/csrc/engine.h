@@ -345,4 +345,32 @@ hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, con
 hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,
                            int64_t now, double* out, hipStream_t stream);
 
+// ---- token-server wire codec (codec.hip) ----
+struct FidSlot {      // flowId → rule index, open addressing with linear probing (fid 0 = empty)
+    int64_t fid;
+    uint32_t idx;
+    uint32_t pad;
+};
+
+struct CodecArgs {
+    uint64_t n;
+    // decode
+    const uint8_t* payload;
+    const uint32_t* offsets;  // [n + 1]
+    const int64_t* ts;
+    sg_req* req;
+    int32_t* xid;
+    uint8_t* kind;
+    const FidSlot* fid_tab;
+    uint64_t fid_mask;
+    // encode
+    const int32_t* xid_in;
+    const uint8_t* kind_in;
+    const sg_result* res;
+    uint8_t* frames;
+};
+
+hipError_t launch_codec_decode(const CodecArgs& c, hipStream_t stream);
+hipError_t launch_codec_encode(const CodecArgs& c, hipStream_t stream);
+
 }  // namespace sg

@@ -17,7 +17,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
-           "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state"]
+           "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
+           "sg_codec_decode_flow", "sg_codec_encode_flow"]
 
 _lib = None
 
@@ -65,6 +66,8 @@ def load_library():
         "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
+        "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
+        "sg_codec_encode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -116,6 +119,19 @@ class FlowEngine:
     def decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
         """req_ptr/out_ptr: device addresses of n sg_req / sg_result records (e.g. torch data_ptr())."""
         self._check(self._L.sg_flow_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr),
+                                                 C.c_void_p(stream_ptr)))
+
+    def codec_decode(self, payload_ptr: int, offsets_ptr: int, ts_ptr: int, n: int, req_ptr: int, xid_ptr: int,
+                     kind_ptr: int, stream_ptr: int = 0):
+        """Device addresses: frame payloads, offsets[n + 1] (u32), arrival ms (i64) → sg_req, xid (i32), kind (u8)."""
+        self._check(self._L.sg_codec_decode_flow(self.h, C.c_void_p(payload_ptr), C.c_void_p(offsets_ptr),
+                                                 C.c_void_p(ts_ptr), n, C.c_void_p(req_ptr), C.c_void_p(xid_ptr),
+                                                 C.c_void_p(kind_ptr), C.c_void_p(stream_ptr)))
+
+    def codec_encode(self, xid_ptr: int, kind_ptr: int, res_ptr: int, n: int, frames_ptr: int, stream_ptr: int = 0):
+        """Device addresses: xid (i32), kind (u8), sg_result → n 16-byte response frames."""
+        self._check(self._L.sg_codec_encode_flow(self.h, C.c_void_p(xid_ptr), C.c_void_p(kind_ptr),
+                                                 C.c_void_p(res_ptr), n, C.c_void_p(frames_ptr),
                                                  C.c_void_p(stream_ptr)))
 
     def decide_host(self, req: np.ndarray) -> np.ndarray:
