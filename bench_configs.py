@@ -200,9 +200,101 @@ def c5(args, dev):
                                  "exits generated by the oracle client model"}
 
 
+def codec(args, dev):
+    """Token-server step from the wire: 16M MSG_TYPE_FLOW frames (the C3 traffic, 1M flowIds, Zipf 1.0)
+    → sg_codec_decode_flow → sg_flow_decide_batch → sg_codec_encode_flow, all resident in HBM."""
+    import bench
+    from sentinel_amd.engine import FlowEngine
+    n = args.events
+    wl = bench.ShardWorkload(args.resources, n, 0, 1, dev)
+    fid_t = torch.from_numpy(wl.rules["flow_id"].astype(np.int64)).to(dev)
+    FB = 18  # [i32 xid][u8 type][i64 flowId][i32 count][bool prio]
+
+    def be(x, nbytes):  # int64 tensor → big-endian bytes [n, nbytes]
+        return torch.stack([(x >> (8 * (nbytes - 1 - j))) & 0xFF for j in range(nbytes)], dim=1).to(torch.uint8)
+
+    def frames(b):
+        req = wl.batch(b).view(torch.int64).reshape(-1, 2)
+        ts, kw = req[:, 0].contiguous(), req[:, 1]
+        key, acq = kw & 0x7FFFFFFF, (kw >> 32) & 0xFFFFFFFF
+        prio = (kw >> 31) & 1
+        xid = torch.arange(n, device=dev, dtype=torch.int64) + b * n
+        pay = torch.cat([be(xid, 4), torch.ones((n, 1), dtype=torch.uint8, device=dev), be(fid_t[key], 8),
+                         be(acq, 4), prio.to(torch.uint8).reshape(-1, 1)], dim=1).reshape(-1).contiguous()
+        return pay, ts
+
+    eng = FlowEngine(device=0, max_batch=n)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = 30000
+    eng.set_namespaces(ns)
+    eng.load_rules(wl.rules)
+    batches = [frames(b) for b in range(args.warmup + args.steps)]
+    offsets = (torch.arange(n + 1, device=dev, dtype=torch.int64) * FB).to(torch.int32)
+    req = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    xid = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    kind = torch.empty(n, dtype=torch.uint8, device=dev)
+    res = torch.empty(n * 12, dtype=torch.uint8, device=dev)
+    out = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    s = stream.cuda_stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    t_codec = [0.0, 0.0]
+
+    def step(b, timed_codec=False):
+        pay, ts = batches[b]
+        ev[0].record(stream)
+        eng.codec_decode(pay.data_ptr(), offsets.data_ptr(), ts.data_ptr(), n, req.data_ptr(), xid.data_ptr(),
+                         kind.data_ptr(), s)
+        ev[1].record(stream)
+        eng.decide_device(req.data_ptr(), n, res.data_ptr(), s)
+        ev[2].record(stream)
+        eng.codec_encode(xid.data_ptr(), kind.data_ptr(), res.data_ptr(), n, out.data_ptr(), s)
+        ev[3].record(stream)
+        if timed_codec:
+            ev[3].synchronize()
+            t_codec[0] += ev[0].elapsed_time(ev[1])
+            t_codec[1] += ev[2].elapsed_time(ev[3])
+
+    el = timed(lambda b: step(b, b >= args.warmup), args.warmup, args.steps)
+    dec_ms, enc_ms = t_codec[0] / args.steps, t_codec[1] / args.steps
+    dec_b, enc_b = n * (FB + 4 + 8 + 16 + 4 + 1), n * (4 + 1 + 12 + 16)
+    touched = int(torch.unique(batches[-1][0].reshape(-1, FB)[:, 5:13].contiguous().view(torch.int64)).numel())
+    b_alg = n * (FB + 4 + 16) + touched * (bench.STATE_B + bench.RULE_B)  # frames in/out + the C3 state
+    base = None
+    if not args.no_cpu_baseline:
+        from oracle import binding
+        from oracle.binding import ClusterTokenService
+        m = min(args.cpu_events, n)
+        pay, ts = batches[0]
+        pay_h = pay[: m * FB].cpu().numpy()
+        off_h = np.arange(m + 1, dtype=np.uint32) * FB
+        ts_h = ts[:m].cpu().numpy()
+        ora = ClusterTokenService()
+        ora.set_namespaces(ns)
+        ora.load_rules(wl.rules)
+        t = time.perf_counter()
+        r_h, x_h, k_h = binding.codec_decode_flow(pay_h, off_h, ts_h, wl.rules["flow_id"])
+        binding.codec_encode_flow(x_h, k_h, ora.decide(r_h))
+        dt = time.perf_counter() - t
+        base = {"value": m / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                "sample": f"first {m} frames of batch 0 through the oracle codec + ClusterTokenService (1 thread), {dt:.1f} s"}
+    return {"metric": "token-server frames/sec (decode + decide + encode), 1M flowIds",
+            "workload": "C3 traffic as MSG_TYPE_FLOW frames: sg_codec_decode_flow -> sg_flow_decide_batch -> "
+                        "sg_codec_encode_flow, 16M frames per 1000 ms batch",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
+            "unit": "frames/s", "dtype": "u8",
+            "extra": {"codec_kernels": {"decode_ms": dec_ms, "encode_ms": enc_ms,
+                                        "decode_gbs": dec_b / dec_ms / 1e6, "encode_gbs": enc_b / enc_ms / 1e6,
+                                        "decode_frac": dec_b / dec_ms / 1e6 / HBM_PEAK_GBS,
+                                        "encode_frac": enc_b / enc_ms / 1e6 / HBM_PEAK_GBS,
+                                        "bytes_per_frame": {"decode": dec_b // n, "encode": enc_b // n}}},
+            "data": "synthetic (GPU-generated, seeded): the bench.py C3 trace encoded as big-endian flow frames"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4", "c5"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec"], default="c2")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=16_000_000)
@@ -212,16 +304,17 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = {"c2": c2, "c4": c4, "c5": c5}[args.workload](args, dev)
+    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec}[args.workload](args, dev)
     ms = r["el"] * 1000.0 / args.steps
     gbs = r["b_alg"] / (ms / 1000.0) / 1e9
-    res = {"metric": r["metric"], "value": r["value"], "unit": "decisions/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "int64", "data": r["data"],
+    res = {"metric": r["metric"], "value": r["value"], "unit": r.get("unit", "decisions/s"), "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": r.get("dtype", "int64"), "data": r["data"],
            "config": {"workload": r["workload"], "decisions_per_step": r["n"], "touched_keys": r["touched"]},
            "roofline": {"bound": "hbm", "kernel": "whole batch pipeline, wall time per step", "achieved": gbs,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
                         "algorithmic_bytes_per_step": r["b_alg"]}}
+    res.update(r.get("extra", {}))
     if r["cpu"] is not None:
         res["cpu_baseline"] = r["cpu"]
     print(json.dumps(res), flush=True)

@@ -342,7 +342,7 @@ int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* bo
  * table: unknown → SG_KEY_NO_RULE, flowId <= 0 → SG_KEY_BAD, as DefaultTokenService.requestToken would
  * answer), the xid of every frame and its kind (SG_FRAME_*). Frames that are not decodable flow requests
  * get key SG_KEY_BAD and acquire 0 (a harmless BAD_REQUEST slot in the batch). All pointers are device
- * memory; the call is asynchronous on `stream`.
+ * memory (payload 4-byte aligned); the call is asynchronous on `stream`.
  * sg_codec_encode_flow: one 16-byte response frame per request at frames_out + 16 * i (zero-filled for
  * frames whose kind is not SG_FRAME_FLOW: the Java server sends nothing for those). */
 #define SG_MSG_TYPE_PING       0

@@ -583,6 +583,7 @@ int sg_codec_decode_flow(sg_handle* h, const uint8_t* payload, const uint32_t* o
     if (!h) return SG_E_INVAL;
     if (n == 0) return SG_OK;
     if (!payload || !offsets || !ts_ms || !req_out || !xid_out || !kind_out) return fail(h, SG_E_INVAL, "null buffer");
+    if (((uintptr_t)payload & 3u) != 0) return fail(h, SG_E_INVAL, "payload must be 4-byte aligned");
     if (!h->d_fid) {
         int rc = upload_fid_table(h);  // no rules loaded yet: every flowId is unknown
         if (rc) return rc;

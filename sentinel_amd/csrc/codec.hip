@@ -25,53 +25,78 @@ __device__ __forceinline__ int64_t rd_be64(const uint8_t* p) {
     return (int64_t)(((uint64_t)(uint32_t)rd_be32(p) << 32) | (uint64_t)(uint32_t)rd_be32(p + 4));
 }
 
-__global__ void __launch_bounds__(256) k_codec_decode(CodecArgs c) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t off = c.offsets[i];
-        const uint32_t len = c.offsets[i + 1] - off;
-        const uint8_t* p = c.payload + off;
-        sg_req r;
-        r.ts_ms = c.ts[i];
-        r.key = SG_KEY_BAD;
-        r.acquire = 0;
-        int32_t xid = 0;
-        uint8_t kind;
-        if (len < 5) {  // DefaultRequestEntityDecoder.decode: readableBytes() >= 5, else null (:37)
-            kind = SG_FRAME_SHORT;
+constexpr int kDecFrames = 256;        // frames per block step (one per thread)
+constexpr uint32_t kDecStage = 16384;  // LDS bytes staged per step
+
+// Decode one frame from `p` (LDS or HBM) of `len` bytes.
+__device__ __forceinline__ void decode_frame(const CodecArgs& c, uint64_t i, const uint8_t* p, uint32_t len) {
+    sg_req r;
+    r.ts_ms = c.ts[i];
+    r.key = SG_KEY_BAD;
+    r.acquire = 0;
+    int32_t xid = 0;
+    uint8_t kind;
+    if (len < 5) {  // DefaultRequestEntityDecoder.decode: readableBytes() >= 5, else null (:37)
+        kind = SG_FRAME_SHORT;
+    } else {
+        xid = rd_be32(p);                        // readInt() (:38)
+        const int type = (int)(int8_t)p[4];      // readByte() (:39)
+        const uint32_t rem = len - 5;
+        if (type != SG_MSG_TYPE_FLOW) {
+            kind = SG_FRAME_OTHER;
+        } else if (rem < 12) {  // FlowRequestDataDecoder.decode: readableBytes() >= 12, else null (:33)
+            kind = SG_FRAME_NO_DATA;
         } else {
-            xid = rd_be32(p);                        // readInt() (:38)
-            const int type = (int)(int8_t)p[4];      // readByte() (:39)
-            const uint32_t rem = len - 5;
-            if (type != SG_MSG_TYPE_FLOW) {
-                kind = SG_FRAME_OTHER;
-            } else if (rem < 12) {  // FlowRequestDataDecoder.decode: readableBytes() >= 12, else null (:33)
-                kind = SG_FRAME_NO_DATA;
+            kind = SG_FRAME_FLOW;
+            const int64_t fid = rd_be64(p + 5);             // readLong() (:35)
+            r.acquire = rd_be32(p + 13);                    // readInt() (:36)
+            const bool prio = rem >= 13 && p[17] != 0;      // readBoolean() if a byte is left (:37-39)
+            if (fid <= 0) {
+                r.key = SG_KEY_BAD;  // DefaultTokenService.notValidRequest → badRequest() (:87-89)
             } else {
-                kind = SG_FRAME_FLOW;
-                const int64_t fid = rd_be64(p + 5);             // readLong() (:35)
-                r.acquire = rd_be32(p + 13);                    // readInt() (:36)
-                const bool prio = rem >= 13 && p[17] != 0;      // readBoolean() if a byte is left (:37-39)
-                if (fid <= 0) {
-                    r.key = SG_KEY_BAD;  // DefaultTokenService.notValidRequest → badRequest() (:87-89)
-                } else {
-                    uint32_t key = SG_KEY_NO_RULE;  // rule == null → NO_RULE_EXISTS (:44-47)
-                    for (uint64_t h = fid_hash(fid) & c.fid_mask;; h = (h + 1) & c.fid_mask) {
-                        const FidSlot s = c.fid_tab[h];
-                        if (s.fid == fid) {
-                            key = s.idx;
-                            break;
-                        }
-                        if (s.fid == 0) break;  // empty slot: not present (the table is never full)
+                uint32_t key = SG_KEY_NO_RULE;  // rule == null → NO_RULE_EXISTS (:44-47)
+                for (uint64_t h = fid_hash(fid) & c.fid_mask;; h = (h + 1) & c.fid_mask) {
+                    const FidSlot s = c.fid_tab[h];
+                    if (s.fid == fid) {
+                        key = s.idx;
+                        break;
                     }
-                    r.key = key;
+                    if (s.fid == 0) break;  // empty slot: not present (the table is never full)
                 }
-                if (prio) r.key |= SG_KEY_PRIO;
+                r.key = key;
             }
+            if (prio) r.key |= SG_KEY_PRIO;
         }
-        c.req[i] = r;
-        c.xid[i] = xid;
-        c.kind[i] = kind;
+    }
+    c.req[i] = r;
+    c.xid[i] = xid;
+    c.kind[i] = kind;
+}
+
+// One block step = kDecFrames consecutive frames. Their payload bytes are contiguous, so when they fit the
+// block stages them in LDS with coalesced aligned 4-byte loads (the word holding a frame's last byte never
+// crosses the allocation's end) and parses from there; larger steps read their bytes from HBM directly.
+__global__ void __launch_bounds__(kDecFrames) k_codec_decode(CodecArgs c) {
+    __shared__ uint32_t stage[kDecStage / 4];
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage);
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kDecFrames; i0 < c.n; i0 += (uint64_t)gridDim.x * kDecFrames) {
+        const uint64_t i1 = min(i0 + (uint64_t)kDecFrames, c.n);
+        const uint32_t lo = c.offsets[i0], hi = c.offsets[i1];
+        const uint32_t a0 = lo & ~3u;
+        const bool staged = hi - a0 <= kDecStage;
+        if (staged && hi > lo) {
+            const uint32_t words = (hi - a0 + 3) / 4;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(c.payload) + a0 / 4;
+            for (uint32_t w = threadIdx.x; w < words; w += kDecFrames) stage[w] = src[w];
+        }
+        __syncthreads();
+        const uint64_t i = i0 + threadIdx.x;
+        if (i < i1) {
+            const uint32_t off = c.offsets[i];
+            const uint32_t len = c.offsets[i + 1] - off;
+            decode_frame(c, i, staged ? sb + (off - a0) : c.payload + off, len);
+        }
+        __syncthreads();  // the stage is refilled by the next step
     }
 }
 
@@ -102,7 +127,8 @@ static unsigned codec_grid(uint64_t n) {
 }
 
 hipError_t launch_codec_decode(const CodecArgs& c, hipStream_t stream) {
-    hipLaunchKernelGGL(k_codec_decode, dim3(codec_grid(c.n)), dim3(256), 0, stream, c);
+    if (((uintptr_t)c.payload & 3u) != 0) return hipErrorInvalidValue;  // staged loads are 4-byte words
+    hipLaunchKernelGGL(k_codec_decode, dim3(codec_grid(c.n)), dim3(kDecFrames), 0, stream, c);
     return hipGetLastError();
 }
 
