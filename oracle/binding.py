@@ -82,6 +82,7 @@ def lib():
         "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
+        "or_rls_decide": (C.c_int, [vp, vp, u64, vp]),
         "or_codec_decode_flow": (None, [vp, vp, vp, u64, vp, u32, vp, vp, vp]),
         "or_codec_encode_flow": (None, [vp, vp, vp, u64, vp]),
     }
@@ -243,6 +244,13 @@ class ClusterTokenService:
 
     def avg(self, key, now, ev):
         return lib().or_cts_avg(self.h, key, now, ev)
+
+    def decide_rls(self, req: np.ndarray) -> np.ndarray:
+        """Envoy RLS path: SimpleClusterFlowChecker.acquireClusterToken per request (no limiter, no occupy)."""
+        req = np.ascontiguousarray(req, dtype=abi.REQ_DTYPE)
+        out = np.zeros(max(len(req), 1), dtype=abi.RES_DTYPE)
+        lib().or_rls_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
+        return out[:len(req)]
 
     # ---- requestParamToken → ClusterParamFlowChecker
     def load_param_rules(self, rules: np.ndarray, hot: np.ndarray = None):

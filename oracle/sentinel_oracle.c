@@ -1511,3 +1511,35 @@ void or_codec_encode_flow(const int32_t* xid, const uint8_t* kind, const sg_resu
         or_put32(f + 12, res[i].wait_ms);       /* writeInt(waitInMs) */
     }
 }
+
+/* ============================================================================== Envoy RLS path ==== */
+/* SimpleClusterFlowChecker.acquireClusterToken (sentinel-cluster-server-envoy-rls/.../flow/
+ * SimpleClusterFlowChecker.java:33-65) for each request in array order: the same ClusterMetric as the token
+ * server, threshold rule.count * exceedCount whatever the threshold type, no namespace limiter, no
+ * prioritized occupy. acquire is the service's acquireCount (hitsAddend, 0 → 1,
+ * SentinelEnvoyRlsServiceImpl.java:35-44); key >= rules → NO_RULE_EXISTS (checkToken :99-109). */
+int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t key = req[i].key & SG_KEY_INDEX;
+        const int64_t t = req[i].ts_ms;
+        const int acq = req[i].acquire;
+        if (key >= s->n_rules) {
+            out[i] = mk(SG_STATUS_NO_RULE_EXISTS, 0, 0);
+            continue;
+        }
+        or_cts_rule* r = &s->rules[key];
+        const double latest = or_cluster_metric_get_avg(r->metric, t, SG_EV_PASS);  /* :41 */
+        const double thr = r->count * s->exceed_count;                              /* :42 */
+        const double next_remaining = thr - latest - (double)acq;                   /* :43 */
+        if (next_remaining >= 0) {
+            or_cluster_metric_add(r->metric, t, SG_EV_PASS, acq);                   /* :46-47 */
+            or_cluster_metric_add(r->metric, t, SG_EV_PASS_REQUEST, 1);
+            out[i] = mk(SG_STATUS_OK, or_d2i(next_remaining), 0);                   /* :53-55 */
+        } else {
+            or_cluster_metric_add(r->metric, t, SG_EV_BLOCK, acq);                  /* :58-59 */
+            or_cluster_metric_add(r->metric, t, SG_EV_BLOCK_REQUEST, 1);
+            out[i] = mk(SG_STATUS_BLOCKED, 0, 0);                                   /* blockedResult :67-71 */
+        }
+    }
+    return 0;
+}

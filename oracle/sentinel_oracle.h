@@ -149,6 +149,9 @@ uint64_t  or_lgen_pending(const or_lgen* g);
 uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
                       int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
 
+/* ---------- Envoy RLS (SimpleClusterFlowChecker over the same ClusterMetric) ---------- */
+int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
+
 /* ---------- token-server wire codec (srv/server/codec and the cluster-common codec package) ---------- */
 /* Decodes n frame payloads (frame i = payload[offsets[i] .. offsets[i+1])) as the default token server
  * would, mapping flowIds through flow_ids[0..n_rules) (rule index = position). Same outputs as
