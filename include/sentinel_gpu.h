@@ -161,6 +161,26 @@ typedef struct sg_param_req {
     int32_t  acquire;           /* acquireCount                                                    */
 } sg_param_req;
 
+/* ---- pace controller: FlowRule with CONTROL_BEHAVIOR_RATE_LIMITER (RateLimiterController) ---- */
+
+/* One FlowRule whose controller is RateLimiterController(maxQueueingTimeMs, count)
+ * (sentinel-core/.../slots/block/flow/controller/RateLimiterController.java:35-38). Each rule owns one
+ * latestPassedTime, initially -1. */
+typedef struct sg_pace_rule {
+    double   count;             /* FlowRule.count (requests per second), >= 0                      */
+    int32_t  max_queueing_ms;   /* FlowRule.maxQueueingTimeMs, default 500                         */
+    int32_t  reserved;
+} sg_pace_rule;
+
+/* canPass(node, acquireCount) at ts_ms (RateLimiterController.java:46-91). */
+typedef struct sg_pace_req {
+    int64_t  ts_ms;
+    uint32_t rule;              /* index into the loaded pace rules; >= n passes (no rule)         */
+    int32_t  acquire;           /* acquireCount                                                    */
+} sg_pace_req;
+
+#define SG_PACE_BLOCKED (-1)    /* result: canPass false; >= 0: passes after sleeping that many ms */
+
 /* ---- cluster hot-parameter tokens (TokenService.requestParamToken → ClusterParamFlowChecker) ---- */
 
 /* One cluster-mode ParamFlowRule with its ParamFlowClusterConfig (ParamFlowRule.java, ParamFlowClusterConfig.java). */
@@ -288,6 +308,18 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
 int sg_param_decide_batch_host(sg_handle* h, const sg_param_req* req, uint64_t n, int32_t* pass);
 /* State of (rule, value): returns flags (bit0 time counter, bit1 token counter; 0 = absent) or < 0. */
 int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+
+/* ---- pace controller ----
+ *   sg_pace_load_rules    ← FlowRuleUtil.generateRater for CONTROL_BEHAVIOR_RATE_LIMITER rules
+ *                           (core/.../flow/FlowRuleUtil.java:132-145): fresh controllers, latestPassedTime -1.
+ *   sg_pace_decide_batch  ← RateLimiterController.canPass (RateLimiterController.java:46-91) for a
+ *                           time-ordered batch; wait[i] = SG_PACE_BLOCKED or the sleep in ms (the caller
+ *                           sleeps; the reference sleeps inside canPass). req/wait are DEVICE pointers.
+ *   sg_pace_read_state    ← latestPassedTime.get() of a rule's controller. */
+int sg_pace_load_rules(sg_handle* h, const sg_pace_rule* rules, uint32_t n);
+int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32_t* wait, void* stream);
+int sg_pace_decide_batch_host(sg_handle* h, const sg_pace_req* req, uint64_t n, int32_t* wait);
+int sg_pace_read_state(sg_handle* h, uint32_t rule, int64_t* latest_passed_time);
 
 /* ---- cluster hot-parameter tokens ----
  *   sg_cparam_load_rules    ← ClusterParamFlowRuleManager.loadRules → applyClusterParamRules

@@ -65,6 +65,10 @@ def lib():
         "or_pf_decide": (C.c_int, [vp, vp, u64, vp]),
         "or_pf_read_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "or_pf_size": (u64, [vp]),
+        "or_pace_new": (vp, []), "or_pace_free": (None, [vp]),
+        "or_pace_load_rules": (C.c_int, [vp, vp, u32]),
+        "or_pace_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_pace_latest": (i64, [vp, u32]),
         "or_local_new": (vp, [C.c_int, C.c_int, C.c_int]), "or_local_free": (None, [vp]),
         "or_local_load_rules": (C.c_int, [vp, vp, u32]),
         "or_local_decide": (C.c_int, [vp, vp, u64, vp]),
@@ -336,6 +340,47 @@ class ParamFlowChecker:
 
     def size(self):
         return lib().or_pf_size(self.h)
+
+
+class RateLimiterController:
+    """Sequential replay of RateLimiterController.canPass, one controller per rule (latestPassedTime -1).
+    decide() returns the sleep in ms per request, or abi.PACE_BLOCKED."""
+
+    def __init__(self, rules=None):
+        self.h = lib().or_pace_new()
+        if rules is not None:
+            self.load_rules(rules)
+
+    def __del__(self):
+        if self.h:
+            lib().or_pace_free(self.h)
+            self.h = None
+
+    def load_rules(self, rules):
+        rules = np.ascontiguousarray(rules, dtype=abi.PACE_RULE_DTYPE)
+        if lib().or_pace_load_rules(self.h, abi.ptr(rules), len(rules)) != 0:
+            raise ValueError("invalid pace rule (count must be >= 0)")
+
+    def decide(self, req):
+        req = np.ascontiguousarray(req, dtype=abi.PACE_REQ_DTYPE)
+        out = np.zeros(len(req), np.int32)
+        lib().or_pace_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
+        return out
+
+    def can_pass(self, t, rule=0, acquire=1):
+        r = np.zeros(1, abi.PACE_REQ_DTYPE)
+        r[0] = (t, rule, acquire)
+        return int(self.decide(r)[0])
+
+    def latest(self, rule):
+        return lib().or_pace_latest(self.h, rule)
+
+
+def pace_rule(count, max_queueing_ms=500):
+    r = np.zeros((), abi.PACE_RULE_DTYPE)
+    r["count"] = count
+    r["max_queueing_ms"] = max_queueing_ms
+    return r
 
 
 def degrade_rule(grade, count, time_window_sec, min_request_amount=5, stat_interval_ms=1000,

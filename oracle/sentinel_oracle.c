@@ -765,6 +765,74 @@ int or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* las
 uint64_t or_pf_size(const or_pf* p) { return p->size; }
 
 /* ===================================================================================== */
+/* Pace controller: RateLimiterController.canPass                                          */
+/* (sentinel-core/.../slots/block/flow/controller/RateLimiterController.java:46-91)        */
+/* ===================================================================================== */
+/* One controller per CONTROL_BEHAVIOR_RATE_LIMITER FlowRule (FlowRuleUtil.generateRater,
+ * FlowRuleUtil.java:132-145). Single-threaded replay: TimeUtil.currentTimeMillis() is the request's
+ * ts for every read inside one call, and Thread.sleep(waitTime) is returned to the caller instead. */
+
+struct or_pace {
+    sg_pace_rule* rules;
+    int64_t* latest;            /* latestPassedTime, AtomicLong(-1) (:33) */
+    uint32_t n;
+};
+
+or_pace* or_pace_new(void) { return (or_pace*)calloc(1, sizeof(or_pace)); }
+
+void or_pace_free(or_pace* p) {
+    if (!p) return;
+    free(p->rules);
+    free(p->latest);
+    free(p);
+}
+
+int or_pace_load_rules(or_pace* p, const sg_pace_rule* rules, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+        if (!(rules[i].count >= 0)) return -1;   /* FlowRuleUtil.isValidRule: count >= 0 (:167-175) */
+    free(p->rules);
+    free(p->latest);
+    p->rules = (sg_pace_rule*)calloc(n ? n : 1, sizeof(sg_pace_rule));
+    memcpy(p->rules, rules, n * sizeof(sg_pace_rule));
+    p->latest = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+    for (uint32_t i = 0; i < n; i++) p->latest[i] = -1;
+    p->n = n;
+    return 0;
+}
+
+static int32_t pace_can_pass(or_pace* p, uint32_t ri, int64_t now, int acquire) {
+    const sg_pace_rule* r = &p->rules[ri];
+    if (acquire <= 0) return 0;                                  /* :48-50 */
+    if (r->count <= 0) return SG_PACE_BLOCKED;                   /* :53-55 */
+    int64_t cost = or_math_round(1.0 * (acquire) / r->count * 1000);   /* :59 */
+    int64_t expected = cost + p->latest[ri];                     /* :62 (long wraps: -fwrapv) */
+    if (expected <= now) {                                       /* :64-67 */
+        p->latest[ri] = now;
+        return 0;
+    }
+    int64_t wait = cost + p->latest[ri] - now;                   /* :70 */
+    if (wait > r->max_queueing_ms) return SG_PACE_BLOCKED;       /* :71-72 */
+    p->latest[ri] += cost;                                       /* :74 addAndGet */
+    int64_t old = p->latest[ri];
+    wait = old - now;                                            /* :76 */
+    if (wait > r->max_queueing_ms) {                             /* :77-80, unreachable single-threaded */
+        p->latest[ri] -= cost;
+        return SG_PACE_BLOCKED;
+    }
+    return wait > 0 ? (int32_t)wait : 0;                         /* :82-85 sleeps waitTime if > 0 */
+}
+
+int or_pace_decide(or_pace* p, const sg_pace_req* req, uint64_t n, int32_t* wait) {
+    for (uint64_t i = 0; i < n; i++) {
+        if (req[i].rule >= p->n) { wait[i] = 0; continue; }      /* no rule for the resource: pass */
+        wait[i] = pace_can_pass(p, req[i].rule, req[i].ts_ms, req[i].acquire);
+    }
+    return 0;
+}
+
+int64_t or_pace_latest(const or_pace* p, uint32_t rule) { return rule < p->n ? p->latest[rule] : INT64_MIN; }
+
+/* ===================================================================================== */
 /* Local slot chain for one resource per rule: StatisticSlot.entry/exit                   */
 /* (core/slots/statistic/StatisticSlot.java:55-165), FlowSlot with DefaultController      */
 /* (core/slots/block/flow/controller/DefaultController.java:49-76), DegradeSlot           */

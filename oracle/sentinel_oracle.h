@@ -124,6 +124,15 @@ int     or_pf_decide(or_pf* p, const sg_param_req* req, uint64_t n, int32_t* out
 int     or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
 uint64_t or_pf_size(const or_pf* p);
 
+/* ---------- pace controller: RateLimiterController (core/.../flow/controller/RateLimiterController.java) ---------- */
+typedef struct or_pace or_pace;
+or_pace* or_pace_new(void);
+void     or_pace_free(or_pace* p);
+int      or_pace_load_rules(or_pace* p, const sg_pace_rule* rules, uint32_t n);
+/* wait[i] = SG_PACE_BLOCKED or the sleep of a passing request (ms) */
+int      or_pace_decide(or_pace* p, const sg_pace_req* req, uint64_t n, int32_t* wait);
+int64_t  or_pace_latest(const or_pace* p, uint32_t rule);
+
 /* ---------- local slot chain: StatisticSlot / FlowSlot(DefaultController) / DegradeSlot ---------- */
 typedef struct or_local or_local;
 or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms);

@@ -87,6 +87,9 @@ PARAM_RULE_DTYPE = np.dtype([("count", "<f8"), ("duration_sec", "<i8"), ("burst"
                              ("capacity_log2", "<i4")], align=True)
 PARAM_HOT_DTYPE = np.dtype([("value", "<u8"), ("threshold", "<i4"), ("reserved", "<i4")], align=True)
 PARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("value", "<u8"), ("rule", "<u4"), ("acquire", "<i4")], align=True)
+PACE_RULE_DTYPE = np.dtype([("count", "<f8"), ("max_queueing_ms", "<i4"), ("reserved", "<i4")], align=True)
+PACE_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("rule", "<u4"), ("acquire", "<i4")], align=True)
+PACE_BLOCKED = -1
 CPARAM_RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
                               ("window_interval_ms", "<i4"), ("namespace_id", "<i4"), ("hot_begin", "<u4"),
                               ("hot_count", "<u4")], align=True)

@@ -85,6 +85,14 @@ struct sg_handle {
     sg_param_req* d_preq_h = nullptr;
     int32_t* d_pout_h = nullptr;
 
+    // pace controller (RateLimiterController per FlowRule)
+    std::vector<PaceRule> pace_tab;
+    PaceRule* d_pace_rules = nullptr;
+    int64_t* d_pace_latest = nullptr;
+    int64_t* d_pace_last_ts = nullptr;
+    sg_pace_req* d_pace_req_h = nullptr;
+    int32_t* d_pace_out_h = nullptr;
+
     // cluster hot-parameter tokens
     std::vector<sg_cparam_rule> cprules;
     std::vector<CPRule> cptab;
@@ -368,6 +376,11 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_plast_ts);
     dfree(h->d_preq_h);
     dfree(h->d_pout_h);
+    dfree(h->d_pace_rules);
+    dfree(h->d_pace_latest);
+    dfree(h->d_pace_last_ts);
+    dfree(h->d_pace_req_h);
+    dfree(h->d_pace_out_h);
     dfree(h->d_skip_count);
     dfree(h->d_cprules);
     dfree(h->d_cphot);
@@ -944,6 +957,103 @@ int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* la
     *last_time = s->time;
     *tokens = s->tokens;
     return (int)s->flags;
+}
+
+// --------------------------------------------------------------------- pace controller
+// FlowRuleUtil.generateRater (core/.../flow/FlowRuleUtil.java:132-145) builds one RateLimiterController per
+// CONTROL_BEHAVIOR_RATE_LIMITER rule; a rebuild starts every latestPassedTime at -1
+// (RateLimiterController.java:33). FlowRuleUtil.isValidRule (:167-175) requires count >= 0.
+int sg_pace_load_rules(sg_handle* h, const sg_pace_rule* rules, uint32_t n) {
+    if (!h || (!rules && n)) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<PaceRule> tab(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!(rules[i].count >= 0)) return fail(h, SG_E_INVAL, "invalid pace rule: count must be >= 0");
+        tab[i].count = rules[i].count;
+        tab[i].max_queueing_ms = rules[i].max_queueing_ms;
+        tab[i].pad = 0;
+    }
+    dfree(h->d_pace_rules);
+    dfree(h->d_pace_latest);
+    h->pace_tab.clear();
+    if (!h->d_pace_last_ts) {
+        const int64_t neg = INT64_MIN;
+        if (hipMalloc(&h->d_pace_last_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "pace state");
+        HIP_TRY(h, hipMemcpy(h->d_pace_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
+    }
+    if (n) {
+        if (hipMalloc(&h->d_pace_rules, sizeof(PaceRule) * n) != hipSuccess ||
+            hipMalloc(&h->d_pace_latest, sizeof(int64_t) * n) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "pace rule allocation");
+        std::vector<int64_t> init(n, -1);
+        HIP_TRY(h, hipMemcpy(h->d_pace_rules, tab.data(), sizeof(PaceRule) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_pace_latest, init.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
+    }
+    h->pace_tab = tab;
+    return SG_OK;
+}
+
+int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32_t* wait, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !wait) return fail(h, SG_E_INVAL, "null buffer");
+    if (!h->d_pace_last_ts) return fail(h, SG_E_INVAL, "sg_pace_load_rules first");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    PaceArgs p{};
+    p.req = req;
+    p.out = wait;
+    p.n = n;
+    p.rec = h->d_rec;
+    p.rec_sorted = h->d_rec_sorted;
+    p.ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
+    p.imask = (1ull << p.ibits) - 1;
+    p.rules = h->d_pace_rules;
+    p.n_rules = (uint32_t)h->pace_tab.size();
+    p.latest = h->d_pace_latest;
+    p.err = h->d_err;
+    p.last_ts = h->d_pace_last_ts;
+    p.long_list = h->d_long_list;
+    p.long_count = h->d_long_count;
+    p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 32u;
+    const int gbits = bits_for((uint64_t)p.n_rules + 1);
+    if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "pace rules x max_batch too large for 64-bit records");
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    uint64_t* sorted = nullptr;
+    HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream));
+    h->last_sorted = sorted;
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (*h->h_err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    return SG_OK;
+}
+
+int sg_pace_decide_batch_host(sg_handle* h, const sg_pace_req* req, uint64_t n, int32_t* wait) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !wait) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_pace_req_h) {
+        if (hipMalloc(&h->d_pace_req_h, sizeof(sg_pace_req) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_pace_out_h, sizeof(int32_t) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    HIP_TRY(h, hipMemcpy(h->d_pace_req_h, req, sizeof(sg_pace_req) * n, hipMemcpyHostToDevice));
+    int rc = sg_pace_decide_batch(h, h->d_pace_req_h, n, h->d_pace_out_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(wait, h->d_pace_out_h, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_pace_read_state(sg_handle* h, uint32_t rule, int64_t* latest_passed_time) {
+    if (!h || rule >= h->pace_tab.size() || !latest_passed_time) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipMemcpy(latest_passed_time, h->d_pace_latest + rule, sizeof(int64_t), hipMemcpyDeviceToHost));
+    return SG_OK;
 }
 
 // --------------------------------------------------------------------- cluster hot-parameter tokens

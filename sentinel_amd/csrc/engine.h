@@ -178,6 +178,34 @@ hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
 hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
                               uint64_t** sorted_out, hipStream_t stream);
 
+// ---- pace controller: RateLimiterController per FlowRule (pace.hip) ----
+struct PaceRule {
+    double count;           // FlowRule.count
+    int32_t max_queueing_ms;
+    int32_t pad;
+};
+
+struct PaceArgs {
+    const sg_pace_req* req;
+    int32_t* out;           // wait ms or SG_PACE_BLOCKED
+    uint64_t n;
+    uint64_t* rec;          // {rule : high bits | request index : ibits}
+    uint64_t* rec_sorted;
+    int ibits;
+    uint64_t imask;
+    const PaceRule* rules;
+    uint32_t n_rules;       // records of requests decided before the walk carry n_rules as rule
+    int64_t* latest;        // [n_rules] latestPassedTime
+    int* err;
+    int64_t* last_ts;
+    uint32_t* long_list;
+    uint32_t* long_count;
+    uint32_t short_max;
+};
+
+hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
+                             uint64_t** sorted_out, hipStream_t stream);
+
 // ---- cluster hot-parameter tokens (cparam.hip) ----
 constexpr int kErrBounds = 32;      // a request's values lie outside the batch's value array
 

@@ -1,0 +1,188 @@
+// pace.hip — RateLimiterController on the device: FlowRules with CONTROL_BEHAVIOR_RATE_LIMITER
+// (sentinel-core/src/main/java/com/alibaba/csp/sentinel/slots/block/flow/controller/
+//  RateLimiterController.java:46-91), a leaky bucket with one latestPassedTime per rule.
+//
+// Replay semantics: requests are applied in (ts, arrival) order per rule, currentTimeMillis() = the
+// request's ts for the whole call (the reference reads the clock up to three times inside one call; a
+// single-threaded caller sees them equal to the millisecond it started in). Under that order the
+// second queue check after addAndGet (:76-80) can never fail, so one request is:
+//   expected = latest + cost                  (Java long arithmetic: wraps)
+//   expected <= now      → latest = now, pass with no sleep
+//   expected - now > maxQ → block, latest unchanged
+//   else                 → latest = expected, pass after sleeping expected - now ms
+// A batch:
+//   k_pace_prep     decides what never touches latestPassedTime (no rule, acquireCount <= 0 → pass;
+//                   count <= 0 → block), packs {rule | request index} for the rest, outputs "blocked"
+//   radix sort by rule (sort.hip): each rule's requests contiguous, in arrival order
+//   k_pace_short    one lane per rule with <= short_max requests, serial recurrence in registers
+//   k_pace_long     one wave per longer rule: 64 requests per step; the first request of the step the
+//                   bucket admits advances latestPassedTime, every pending request before it is blocked
+#include "engine.h"
+
+namespace sg {
+
+namespace {
+
+__device__ __forceinline__ int64_t pace_java_round(double a) {
+    // java.lang.Math.round(double) (JDK 7u+): floor(a + 1/2) on the bits, saturating
+    const int64_t bits = __double_as_longlong(a);
+    const int64_t biased_exp = (bits & 0x7FF0000000000000LL) >> 52;
+    const int64_t shift = (52 - 1 + 1023) - biased_exp;
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    if (a != a) return 0;
+    if (a >= 9223372036854775807.0) return INT64_MAX;
+    if (a <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)a;
+}
+
+// costTime = Math.round(1.0 * acquireCount / count * 1000) (:59)
+__device__ __forceinline__ int64_t pace_cost(double count, int32_t acq) {
+    return pace_java_round(1.0 * (double)acq / count * 1000.0);
+}
+
+__device__ __forceinline__ int64_t wrap_add(int64_t a, int64_t b) {
+    return (int64_t)((uint64_t)a + (uint64_t)b);
+}
+
+// One canPass under the replay order; returns the sleep in ms or SG_PACE_BLOCKED.
+__device__ __forceinline__ int32_t pace_step(int64_t& latest, int64_t cost, int32_t maxq, int64_t t) {
+    const int64_t expected = wrap_add(latest, cost);
+    if (expected <= t) {
+        latest = t;
+        return 0;
+    }
+    const int64_t wait = expected - t;  // > 0, no overflow: expected > t >= 0
+    if (wait > (int64_t)maxq) return SG_PACE_BLOCKED;
+    latest = expected;
+    return (int32_t)wait;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_pace_prep(PaceArgs p) {
+    const uint64_t none = (uint64_t)p.n_rules << p.ibits;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_pace_req q = p.req[i];
+        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *p.last_ts : q.ts_ms < p.req[i - 1].ts_ms)) atomicOr(p.err, kErrTime);
+        uint64_t rec = none;
+        int32_t out = SG_PACE_BLOCKED;
+        if (q.rule >= p.n_rules || q.acquire <= 0) {
+            out = 0;  // no rule for the resource / acquireCount <= 0 (:48-50)
+        } else if (!(p.rules[q.rule].count > 0.0)) {
+            out = SG_PACE_BLOCKED;  // count <= 0 (:53-55)
+        } else {
+            rec = ((uint64_t)q.rule << p.ibits) | i;
+        }
+        p.out[i] = out;
+        p.rec[i] = rec;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
+    if (*p.err) return;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t g = p.rec_sorted[j] >> p.ibits;
+        if (g >= p.n_rules) continue;  // decided in k_pace_prep (these sort last)
+        if (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g) continue;
+        uint64_t e = j + 1;
+        while (e < p.n && e - j <= (uint64_t)p.short_max && (p.rec_sorted[e] >> p.ibits) == g) ++e;
+        if (e - j > (uint64_t)p.short_max) {
+            const uint32_t pos = atomicAdd(p.long_count, 1u);
+            p.long_list[pos] = (uint32_t)j;
+            continue;
+        }
+        const PaceRule r = p.rules[g];
+        int64_t latest = p.latest[g];
+        for (uint64_t k = j; k < e; ++k) {
+            const uint32_t idx = (uint32_t)(p.rec_sorted[k] & p.imask);
+            const sg_pace_req q = p.req[idx];
+            const int32_t w = pace_step(latest, pace_cost(r.count, q.acquire), r.max_queueing_ms, q.ts_ms);
+            if (w != SG_PACE_BLOCKED) p.out[idx] = w;
+        }
+        p.latest[g] = latest;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
+    if (*p.err) return;
+    const uint32_t cnt = *p.long_count;
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const int lane = (int)__lane_id();
+    for (uint32_t w = wave; w < cnt; w += nwaves) {
+        const uint64_t s = p.long_list[w];
+        const uint64_t g = p.rec_sorted[s] >> p.ibits;
+        // segment end: first record of another rule, 64 probes per step
+        uint64_t e = s + p.short_max;
+        for (;;) {
+            const uint64_t q = e + (uint64_t)lane;
+            const uint64_t m = __ballot(q >= p.n || (p.rec_sorted[q] >> p.ibits) != g);
+            if (m) {
+                e += (uint64_t)__builtin_ctzll(m);
+                break;
+            }
+            e += 64;
+        }
+        const PaceRule r = p.rules[g];
+        int64_t latest = p.latest[g];
+        for (uint64_t base = s; base < e; base += 64) {
+            const uint64_t j = base + (uint64_t)lane;
+            const bool act = j < e;
+            uint32_t idx = 0;
+            int64_t t = 0, cost = 0;
+            if (act) {
+                idx = (uint32_t)(p.rec_sorted[j] & p.imask);
+                const sg_pace_req q = p.req[idx];
+                t = q.ts_ms;
+                cost = pace_cost(r.count, q.acquire);
+            }
+            uint64_t pending = __ballot(act);
+            while (pending) {
+                const int64_t expected = wrap_add(latest, cost);
+                const bool ok = ((pending >> lane) & 1ull) && (expected <= t || expected - t <= (int64_t)r.max_queueing_ms);
+                const uint64_t m = __ballot(ok);
+                if (!m) break;  // every pending request of this step is blocked
+                const int f = __builtin_ctzll(m);
+                const int64_t tf = __shfl((long long)t, f, 64);
+                const int64_t ef = __shfl((long long)expected, f, 64);
+                if (lane == f) p.out[idx] = ef <= tf ? 0 : (int32_t)(ef - tf);
+                latest = ef <= tf ? tf : ef;
+                pending &= ~((2ull << f) - 1ull);
+            }
+        }
+        if (lane == 0) p.latest[g] = latest;
+    }
+}
+
+__global__ void k_pace_finish(PaceArgs p) {
+    if (*p.err == 0 && p.n > 0) *p.last_ts = p.req[p.n - 1].ts_ms;
+}
+
+static unsigned pace_grid(uint64_t n, unsigned cap) {
+    uint64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
+                             uint64_t** sorted_out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_pace_prep, dim3(pace_grid(p.n, 8192)), dim3(256), 0, stream, p);
+    uint64_t* sorted = nullptr;
+    hipError_t e = radix_sort_records(a_buf, b_buf, p.n, lo_bit, hist, &sorted, stream, hi_bit);
+    if (e != hipSuccess) return e;
+    PaceArgs q = p;
+    q.rec_sorted = sorted;
+    *sorted_out = sorted;
+    hipLaunchKernelGGL(k_pace_short, dim3(pace_grid(p.n, 16384)), dim3(256), 0, stream, q);
+    const uint64_t max_long = p.n / ((uint64_t)p.short_max + 1) + 1;
+    hipLaunchKernelGGL(k_pace_long, dim3(pace_grid(max_long * 64, 2048)), dim3(256), 0, stream, q);
+    hipLaunchKernelGGL(k_pace_finish, dim3(1), dim3(1), 0, stream, q);
+    return hipGetLastError();
+}
+
+}  // namespace sg

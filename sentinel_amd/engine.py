@@ -18,7 +18,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
-           "sg_codec_decode_flow", "sg_codec_encode_flow"]
+           "sg_codec_decode_flow", "sg_codec_encode_flow",
+           "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
 
 _lib = None
 
@@ -68,6 +69,10 @@ def load_library():
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "sg_codec_encode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
+        "sg_pace_load_rules": (C.c_int, [vp, vp, u32]),
+        "sg_pace_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_pace_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_pace_read_state": (C.c_int, [vp, u32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -188,6 +193,27 @@ class FlowEngine:
         if flags < 0:
             self._check(flags)
         return flags, lt.value, tk.value
+
+    # ---- pace controller (RateLimiterController.canPass per CONTROL_BEHAVIOR_RATE_LIMITER FlowRule)
+    def pace_load_rules(self, rules: np.ndarray):
+        rules = np.ascontiguousarray(rules, dtype=abi.PACE_RULE_DTYPE)
+        self._check(self._L.sg_pace_load_rules(self.h, abi.ptr(rules), len(rules)))
+
+    def pace_decide_host(self, req: np.ndarray) -> np.ndarray:
+        """wait ms per request, abi.PACE_BLOCKED (-1) when canPass is false."""
+        req = np.ascontiguousarray(req, dtype=abi.PACE_REQ_DTYPE)
+        out = np.zeros(len(req), np.int32)
+        self._check(self._L.sg_pace_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def pace_decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        self._check(self._L.sg_pace_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr),
+                                                 C.c_void_p(stream_ptr)))
+
+    def pace_latest(self, rule):
+        v = C.c_int64()
+        self._check(self._L.sg_pace_read_state(self.h, rule, C.byref(v)))
+        return v.value
 
     def snapshot(self, now_ms, n_rules):
         out = np.zeros(2 * n_rules, np.float64)
