@@ -11,6 +11,9 @@ bench.py (which measures the headline C3 workload).
                  1000 ms batch plus the exits of the passed ones (rt ~ lognormal, median 12 ms; 5 % errors).
                  The event stream depends on the decisions (only passed entries exit), so it is produced by
                  the CPU oracle's client model (oracle.binding.LocalTraceGen) before the timed region.
+  --workload pace  1M resources, each a FlowRule with CONTROL_BEHAVIOR_RATE_LIMITER (RateLimiterController,
+                 count U{1..64}, maxQueueingTimeMs 500), 16M canPass calls per 1000 ms batch, Zipf(1.0),
+                 acquire 1 (10 % U{2..4}).
 
 Inputs are resident in HBM before the timed region; one step = one batch. cpu_baseline = the oracle
 (sequential C restatement, 1 thread) on the first batch of the same workload.
@@ -292,9 +295,51 @@ def codec(args, dev):
             "data": "synthetic (GPU-generated, seeded): the bench.py C3 trace encoded as big-endian flow frames"}
 
 
+def pace(args, dev):
+    K, n = args.resources, args.events
+    rng = np.random.default_rng(6)
+    rules = np.zeros(K, abi.PACE_RULE_DTYPE)
+    rules["count"] = rng.integers(1, 65, K).astype(np.float64)
+    rules["max_queueing_ms"] = 500
+    cdf, perm = zipf_cdf(K, 1.0, 6)
+    cdf_t, perm_t = torch.from_numpy(cdf).to(dev), torch.from_numpy(perm.astype(np.int64)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(6)
+
+    def batch(b):
+        w = torch.zeros((n, 2), dtype=torch.int64, device=dev)
+        w[:, 0] = torch.sort(torch.randint(0, 1000, (n,), generator=gen, device=dev)).values + T0 + 1000 * b
+        acq = torch.where(torch.rand(n, generator=gen, device=dev) < 0.1,
+                          torch.randint(2, 5, (n,), generator=gen, device=dev), torch.ones(n, dtype=torch.int64, device=dev))
+        w[:, 1] = gpu_keys(cdf_t, perm_t, n, gen) | (acq << 32)       # rule | acquireCount << 32
+        return w.view(torch.uint8).reshape(-1)
+
+    eng = FlowEngine(device=0, max_batch=n)
+    eng.pace_load_rules(rules)
+    batches = [batch(b) for b in range(args.warmup + args.steps)]
+    out = torch.empty(n * 4, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    el = timed(lambda b: eng.pace_decide_device(batches[b].data_ptr(), n, out.data_ptr(), stream), args.warmup, args.steps)
+    touched = int(torch.unique(batches[-1].view(torch.int64).reshape(-1, 2)[:, 1] & 0xFFFFFFFF).numel())
+    b_alg = n * (16 + 4) + touched * (16 + 2 * 8)   # request in, wait out; per rule: rule 16 B, latest read + write
+    base = None
+    if not args.no_cpu_baseline:
+        from oracle.binding import RateLimiterController
+        req = batches[0].view(torch.int64).reshape(-1, 2)[: args.cpu_events].cpu().numpy().copy().view(abi.PACE_REQ_DTYPE).reshape(-1)
+        ora = RateLimiterController(rules)
+        t = time.perf_counter()
+        ora.decide(req)
+        dt = time.perf_counter() - t
+        base = {"value": len(req) / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"first {len(req)} requests of batch 0 through oracle RateLimiterController (1 thread), {dt:.1f} s"}
+    return {"metric": "pace decisions/sec (RateLimiterController.canPass), 1M rate-limited resources",
+            "workload": "pace: 1M RATE_LIMITER FlowRules count U{1..64} maxQueueing 500 ms, 16M canPass/batch",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
+            "data": "synthetic (GPU-generated, seeded): Zipf(1.0) resources, 10% acquire U{2..4}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace"], default="c2")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=16_000_000)
@@ -304,7 +349,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec}[args.workload](args, dev)
+    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace}[args.workload](args, dev)
     ms = r["el"] * 1000.0 / args.steps
     gbs = r["b_alg"] / (ms / 1000.0) / 1e9
     res = {"metric": r["metric"], "value": r["value"], "unit": r.get("unit", "decisions/s"), "n_gpus": 1,

@@ -16,7 +16,9 @@
 //   radix sort by rule (sort.hip): each rule's requests contiguous, in arrival order
 //   k_pace_short    one lane per rule with <= short_max requests, serial recurrence in registers
 //   k_pace_long     one wave per longer rule: 64 requests per step; the first request of the step the
-//                   bucket admits advances latestPassedTime, every pending request before it is blocked
+//                   bucket admits advances latestPassedTime, every pending request before it is blocked;
+//                   requests before the earliest instant any of them could pass are jumped over by a
+//                   64-way search (a saturated rule costs a few searches per admitted request)
 #include "engine.h"
 
 namespace sg {
@@ -59,6 +61,28 @@ __device__ __forceinline__ int32_t pace_step(int64_t& latest, int64_t cost, int3
     if (wait > (int64_t)maxq) return SG_PACE_BLOCKED;
     latest = expected;
     return (int32_t)wait;
+}
+
+// First q in [lo, hi) with pred(q) (pred monotone: false…false true…true), else hi; 64 probes per round.
+template <class Pred>
+__device__ __forceinline__ uint64_t pace_wave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t q = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(q >= hi || pred(q));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t q = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(q < hi && pred(q));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
 }  // namespace
@@ -116,20 +140,28 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint64_t s = p.long_list[w];
         const uint64_t g = p.rec_sorted[s] >> p.ibits;
-        // segment end: first record of another rule, 64 probes per step
-        uint64_t e = s + p.short_max;
-        for (;;) {
-            const uint64_t q = e + (uint64_t)lane;
-            const uint64_t m = __ballot(q >= p.n || (p.rec_sorted[q] >> p.ibits) != g);
-            if (m) {
-                e += (uint64_t)__builtin_ctzll(m);
-                break;
-            }
-            e += 64;
-        }
+        // segment end: first record of another rule (records are sorted by rule)
+        const uint64_t e = pace_wave_search(s + p.short_max, p.n, [&](uint64_t q) {
+            return (p.rec_sorted[q] >> p.ibits) != g;
+        }, lane);
         const PaceRule r = p.rules[g];
         int64_t latest = p.latest[g];
-        for (uint64_t base = s; base < e; base += 64) {
+        // Every walked request has acquireCount >= 1 (k_pace_prep decides the rest), so its cost is at
+        // least cost(1) and it can only pass at t >= latest + cost(1) - max(maxQ, 0): requests before that
+        // instant are blocked without changing latestPassedTime, and the walker jumps over them.
+        const int64_t cost1 = pace_cost(r.count, 1);
+        const int64_t slack = r.max_queueing_ms > 0 ? (int64_t)r.max_queueing_ms : 0;
+        auto ts_at = [&](uint64_t q) { return p.req[(uint32_t)(p.rec_sorted[q] & p.imask)].ts_ms; };
+        uint64_t base = s;
+        while (base < e) {
+            int64_t horizon;
+            if (!__builtin_add_overflow(latest, cost1, &horizon)) {  // no wrap: the bound is exact
+                horizon -= slack;
+                if (ts_at(base) < horizon) {
+                    base = pace_wave_search(base, e, [&](uint64_t q) { return ts_at(q) >= horizon; }, lane);
+                    continue;
+                }
+            }
             const uint64_t j = base + (uint64_t)lane;
             const bool act = j < e;
             uint32_t idx = 0;
@@ -153,6 +185,7 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
                 latest = ef <= tf ? tf : ef;
                 pending &= ~((2ull << f) - 1ull);
             }
+            base += 64;
         }
         if (lane == 0) p.latest[g] = latest;
     }
