@@ -1016,13 +1016,15 @@ int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32
     p.last_ts = h->d_pace_last_ts;
     p.long_list = h->d_long_list;
     p.long_count = h->d_long_count;
+    p.short_list = h->d_short_list;
     p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 32u;
     const int gbits = bits_for((uint64_t)p.n_rules + 1);
     if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "pace rules x max_batch too large for 64-bit records");
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, 2 * sizeof(uint32_t), stream));
     uint64_t* sorted = nullptr;
-    HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream));
+    HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream,
+                                 h->aux, h->fork, h->join));
     h->last_sorted = sorted;
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipStreamSynchronize(stream));

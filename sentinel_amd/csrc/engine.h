@@ -199,12 +199,15 @@ struct PaceArgs {
     int* err;
     int64_t* last_ts;
     uint32_t* long_list;
-    uint32_t* long_count;
+    uint32_t* long_count;   // [0] long segments, [1] short segments
+    uint32_t* short_list;
     uint32_t short_max;
 };
 
+// The long-rule walker runs on `aux` beside the short one (fork / join events).
 hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
-                             uint64_t** sorted_out, hipStream_t stream);
+                             uint64_t** sorted_out, hipStream_t stream, hipStream_t aux, hipEvent_t fork,
+                             hipEvent_t join);
 
 // ---- cluster hot-parameter tokens (cparam.hip) ----
 constexpr int kErrBounds = 32;      // a request's values lie outside the batch's value array

@@ -14,8 +14,9 @@
 //   k_pace_prep     decides what never touches latestPassedTime (no rule, acquireCount <= 0 → pass;
 //                   count <= 0 → block), packs {rule | request index} for the rest, outputs "blocked"
 //   radix sort by rule (sort.hip): each rule's requests contiguous, in arrival order
+//   k_pace_seg      segment heads split by length into the lane walker's and the wave walker's lists
 //   k_pace_short    one lane per rule with <= short_max requests, serial recurrence in registers
-//   k_pace_long     one wave per longer rule: 64 requests per step; the first request of the step the
+//   k_pace_long     (second stream, beside k_pace_short) one wave per longer rule: 64 requests per step; the first request of the step the
 //                   bucket admits advances latestPassedTime, every pending request before it is blocked;
 //                   requests before the earliest instant any of them could pass are jumped over by a
 //                   64-way search (a saturated rule costs a few searches per admitted request)
@@ -106,26 +107,82 @@ __global__ void __launch_bounds__(256) k_pace_prep(PaceArgs p) {
     }
 }
 
+// 0 = not a segment head, 1 = head of a rule walked by one lane, 2 = head of a rule walked by a wave
+__device__ __forceinline__ int pace_head_class(const PaceArgs& p, uint64_t j) {
+    const uint64_t g = p.rec_sorted[j] >> p.ibits;
+    if (g >= p.n_rules || (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g)) return 0;
+    const uint64_t e = j + (uint64_t)p.short_max;  // segments are contiguous: one probe decides the length class
+    return e < p.n && (p.rec_sorted[e] >> p.ibits) == g ? 2 : 1;
+}
+
+// Segment heads by length class: rules with more than short_max requests go to the wave walker's list,
+// the rest to the lane walker's. Each block owns a contiguous chunk: it counts its heads, reserves its
+// slice of each list with one global atomic per list, then writes the heads in order.
+__global__ void __launch_bounds__(256) k_pace_seg(PaceArgs p, uint64_t chunk) {
+    if (*p.err) return;
+    __shared__ uint32_t tot[2], wcnt[4][2], base[2];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t lo = (uint64_t)blockIdx.x * chunk;
+    const uint64_t hi = lo + chunk < p.n ? lo + chunk : p.n;
+    if (tid < 2) tot[tid] = 0;
+    __syncthreads();
+    uint32_t cs = 0, cl = 0;
+    for (uint64_t j = lo + tid; j < hi; j += 256) {
+        const int c = pace_head_class(p, j);
+        cs += c == 1;
+        cl += c == 2;
+    }
+    if (cs) atomicAdd(&tot[0], cs);
+    if (cl) atomicAdd(&tot[1], cl);
+    __syncthreads();
+    if (tid == 0) {
+        base[0] = tot[0] ? atomicAdd(&p.long_count[1], tot[0]) : 0;
+        base[1] = tot[1] ? atomicAdd(&p.long_count[0], tot[1]) : 0;
+    }
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint64_t r = lo; r < hi; r += 256) {
+        const uint64_t j = r + tid;
+        const int c = j < hi ? pace_head_class(p, j) : 0;
+        const uint64_t sm = __ballot(c == 1), lm = __ballot(c == 2);
+        if (lane == 0) {
+            wcnt[wv][0] = (uint32_t)__popcll(sm);
+            wcnt[wv][1] = (uint32_t)__popcll(lm);
+        }
+        __syncthreads();
+        uint32_t os = base[0], ol = base[1];
+        for (int w = 0; w < wv; ++w) {
+            os += wcnt[w][0];
+            ol += wcnt[w][1];
+        }
+        if (c == 1) p.short_list[os + __popcll(sm & below)] = (uint32_t)j;
+        if (c == 2) p.long_list[ol + __popcll(lm & below)] = (uint32_t)j;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 0; w < 4; ++w) {
+                base[0] += wcnt[w][0];
+                base[1] += wcnt[w][1];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 __global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
     if (*p.err) return;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t cnt = p.long_count[1];
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < cnt; w += gridDim.x * blockDim.x) {
+        const uint64_t j = p.short_list[w];
         const uint64_t g = p.rec_sorted[j] >> p.ibits;
-        if (g >= p.n_rules) continue;  // decided in k_pace_prep (these sort last)
-        if (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g) continue;
-        uint64_t e = j + 1;
-        while (e < p.n && e - j <= (uint64_t)p.short_max && (p.rec_sorted[e] >> p.ibits) == g) ++e;
-        if (e - j > (uint64_t)p.short_max) {
-            const uint32_t pos = atomicAdd(p.long_count, 1u);
-            p.long_list[pos] = (uint32_t)j;
-            continue;
-        }
         const PaceRule r = p.rules[g];
         int64_t latest = p.latest[g];
-        for (uint64_t k = j; k < e; ++k) {
-            const uint32_t idx = (uint32_t)(p.rec_sorted[k] & p.imask);
+        for (uint64_t k = j; k < p.n; ++k) {
+            const uint64_t rec = p.rec_sorted[k];
+            if ((rec >> p.ibits) != g) break;
+            const uint32_t idx = (uint32_t)(rec & p.imask);
             const sg_pace_req q = p.req[idx];
-            const int32_t w = pace_step(latest, pace_cost(r.count, q.acquire), r.max_queueing_ms, q.ts_ms);
-            if (w != SG_PACE_BLOCKED) p.out[idx] = w;
+            const int32_t w8 = pace_step(latest, pace_cost(r.count, q.acquire), r.max_queueing_ms, q.ts_ms);
+            if (w8 != SG_PACE_BLOCKED) p.out[idx] = w8;
         }
         p.latest[g] = latest;
     }
@@ -203,7 +260,8 @@ static unsigned pace_grid(uint64_t n, unsigned cap) {
 }
 
 hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
-                             uint64_t** sorted_out, hipStream_t stream) {
+                             uint64_t** sorted_out, hipStream_t stream, hipStream_t aux, hipEvent_t fork,
+                             hipEvent_t join) {
     hipLaunchKernelGGL(k_pace_prep, dim3(pace_grid(p.n, 8192)), dim3(256), 0, stream, p);
     uint64_t* sorted = nullptr;
     hipError_t e = radix_sort_records(a_buf, b_buf, p.n, lo_bit, hist, &sorted, stream, hi_bit);
@@ -211,9 +269,13 @@ hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf
     PaceArgs q = p;
     q.rec_sorted = sorted;
     *sorted_out = sorted;
-    hipLaunchKernelGGL(k_pace_short, dim3(pace_grid(p.n, 16384)), dim3(256), 0, stream, q);
+    const uint64_t chunk = ((p.n + 2047) / 2048 + 255) / 256 * 256;  // <= 2048 blocks, whole rounds of 256
+    hipLaunchKernelGGL(k_pace_seg, dim3((unsigned)((p.n + chunk - 1) / chunk)), dim3(256), 0, stream, q, chunk);
+    if ((e = hipEventRecord(fork, stream)) != hipSuccess || (e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
     const uint64_t max_long = p.n / ((uint64_t)p.short_max + 1) + 1;
-    hipLaunchKernelGGL(k_pace_long, dim3(pace_grid(max_long * 64, 2048)), dim3(256), 0, stream, q);
+    hipLaunchKernelGGL(k_pace_long, dim3(pace_grid(max_long * 64, 2048)), dim3(256), 0, aux, q);
+    hipLaunchKernelGGL(k_pace_short, dim3(pace_grid(p.n, 4096)), dim3(256), 0, stream, q);
+    if ((e = hipEventRecord(join, aux)) != hipSuccess || (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_pace_finish, dim3(1), dim3(1), 0, stream, q);
     return hipGetLastError();
 }
