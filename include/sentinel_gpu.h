@@ -290,6 +290,19 @@ int sg_get_stats(const sg_handle* h, sg_batch_stats* out);
  * counters[sample_count * SG_NUM_EVENTS], occupy[2] = {occupied PASS, occupied PASS_REQUEST}. */
 int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
 
+/* Bulk copy of every flowId's window to / from HOST memory — the checkpoint of the cluster flow state (the
+ * reference keeps it only in memory; SURVEY §5 "checkpoint / resume") and the parity harness's state dump.
+ * ring: n_rules * stride * 8 int64 = per flowId `stride` buckets {start, PASS, BLOCK, PASS_REQUEST,
+ * BLOCK_REQUEST, OCCUPIED_PASS, OCCUPIED_BLOCK, WAITING} (start INT64_MIN = never-created slot; slots >= the
+ * flow's sampleCount are unused and stay INT64_MIN), occ: n_rules * 2 int64 = {occupied PASS, occupied
+ * PASS_REQUEST} (ClusterMetricLeapArray.occupyCounter). stride = the largest sampleCount of the loaded rules
+ * (written to *stride; with ring == NULL only *stride is written). Import expects the same layout and the same
+ * loaded rules; it is synchronous. */
+int sg_flow_export_state(sg_handle* h, int64_t* ring, uint64_t ring_words, int64_t* occ, uint64_t occ_words,
+                         int32_t* stride);
+int sg_flow_import_state(sg_handle* h, const int64_t* ring, uint64_t ring_words, const int64_t* occ,
+                         uint64_t occ_words);
+
 /* Per-flowId {passQps, blockQps} at time now_ms (ClusterMetric.getAvg(PASS/BLOCK) without the
  * currentWindow side effect); out has 2*n_rules doubles, HOST memory. */
 int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap);

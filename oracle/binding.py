@@ -60,6 +60,7 @@ def lib():
         "or_cts_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
         "or_cts_sample_count": (C.c_int, [vp, u32]),
         "or_cts_avg": (d, [vp, u32, i64, C.c_int]),
+        "or_cts_export_state": (C.c_int, [vp, C.c_int, vp, vp]),
         "or_pf_new": (vp, []), "or_pf_free": (None, [vp]),
         "or_pf_load_rules": (C.c_int, [vp, vp, u32, vp, u32]),
         "or_pf_decide": (C.c_int, [vp, vp, u64, vp]),
@@ -274,6 +275,13 @@ class ClusterTokenService:
     def param_sum(self, key, value, now):
         return lib().or_cts_param_sum(self.h, key, int(value), now)
 
+    def export_state(self, n_rules, stride):
+        """(ring [K][stride][8] {start, 7 counters}, occ [K][2]) — same layout as FlowEngine.export_state."""
+        ring = np.zeros((n_rules, stride, 8), np.int64)
+        occ = np.zeros((n_rules, 2), np.int64)
+        assert lib().or_cts_export_state(self.h, stride, abi.ptr(ring), abi.ptr(occ)) == 0
+        return ring, occ
+
     def read_state(self, key):
         S = lib().or_cts_sample_count(self.h, key)
         starts = np.zeros(S, np.int64)
@@ -282,6 +290,59 @@ class ClusterTokenService:
         rc = lib().or_cts_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ))
         assert rc == 0
         return starts, counters.reshape(S, abi.NUM_EVENTS), occ
+
+
+class ShardedClusterTokenService:
+    """The oracle's ClusterTokenService over T independent shards (flowId key % T), replayed on T host threads
+    (ctypes releases the GIL inside or_cts_decide). Exact for rule sets without a namespace limiter: flowIds
+    share no state then, so per-shard sequential replay equals one global sequential replay."""
+
+    def __init__(self, rules, ns, threads, exceed_count=1.0, max_occupy_ratio=1.0):
+        from concurrent.futures import ThreadPoolExecutor
+        ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
+        assert not ns["limiter_enabled"].any(), "a namespace limiter couples flowIds: replay sequentially"
+        self.T, self.K = threads, len(rules)
+        self.pool = ThreadPoolExecutor(max_workers=threads)
+        self.shards = []
+        for t in range(threads):
+            s = ClusterTokenService(exceed_count, max_occupy_ratio)
+            s.set_namespaces(ns)
+            s.load_rules(np.ascontiguousarray(rules[t::threads]))
+            self.shards.append(s)
+
+    def decide(self, req):
+        req = np.ascontiguousarray(req, dtype=abi.REQ_DTYPE)
+        key = req["key"] & abi.KEY_INDEX
+        valid = (key < self.K)
+        shard = np.where(valid, key % self.T, np.arange(len(req)) % self.T)
+        out = np.zeros(len(req), abi.RES_DTYPE)
+        idx = [np.nonzero(shard == t)[0] for t in range(self.T)]
+
+        def run(t):
+            part = req[idx[t]].copy()
+            k = part["key"] & abi.KEY_INDEX
+            inb = k < self.K
+            # local rule index; out-of-range keys (BAD / NO_RULE) keep their reserved values
+            part["key"] = np.where(inb, (part["key"] & np.uint32(abi.KEY_PRIO)) | (k // self.T).astype(np.uint32),
+                                   part["key"])
+            # a local index can collide with a reserved key only for K >= 2^31 * T: not reachable here
+            out[idx[t]] = self.shards[t].decide(part)
+
+        list(self.pool.map(run, range(self.T)))
+        return out
+
+    def export_state(self, stride):
+        ring = np.zeros((self.K, stride, 8), np.int64)
+        occ = np.zeros((self.K, 2), np.int64)
+        for t, s in enumerate(self.shards):
+            n = len(range(t, self.K, self.T))
+            r, o = s.export_state(n, stride)
+            ring[t::self.T] = r
+            occ[t::self.T] = o
+        return ring, occ
+
+    def close(self):
+        self.pool.shutdown()
 
 
 class ClusterParamMetric:

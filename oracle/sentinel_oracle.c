@@ -419,10 +419,10 @@ or_cts* or_cts_new(double exceed_count, double max_occupy_ratio) {
 static void cpm_free(or_cpm* m);
 
 void or_cts_free(or_cts* s) {
+    if (!s) return;
     for (uint32_t j = 0; j < s->n_prules; j++) cpm_free(s->prules[j].metric);
     free(s->prules);
     free(s->phot);
-    if (!s) return;
     for (uint32_t i = 0; i < s->n_rules; i++) or_leap_free(s->rules[i].metric);
     free(s->rules);
     for (uint32_t i = 0; i < s->n_ns; i++) or_limiter_free(s->limiters[i]);
@@ -570,6 +570,24 @@ int or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* c
     }
     occupy[0] = m->occ[SG_EV_PASS];
     occupy[1] = m->occ[SG_EV_PASS_REQUEST];
+    return 0;
+}
+
+/* Every flowId's window in the layout of sg_flow_export_state: ring[k][stride][8] = {start, 7 counters}
+ * (start INT64_MIN and zero counters for never-created slots and slots >= S), occ[k][2]. */
+int or_cts_export_state(const or_cts* s, int stride, int64_t* ring, int64_t* occ) {
+    for (uint32_t k = 0; k < s->n_rules; k++) {
+        const or_leap* m = s->rules[k].metric;
+        if (m->S > stride) return SG_E_INVAL;
+        int64_t* o = ring + (size_t)k * stride * 8;
+        for (int j = 0; j < stride; j++) {
+            const int p = j < m->S && m->present[j];
+            o[8 * j] = p ? m->b[j].start : INT64_MIN;
+            for (int e = 0; e < SG_NUM_EVENTS; e++) o[8 * j + 1 + e] = p ? m->b[j].c[e] : 0;
+        }
+        occ[2 * (size_t)k] = m->occ[SG_EV_PASS];
+        occ[2 * (size_t)k + 1] = m->occ[SG_EV_PASS_REQUEST];
+    }
     return 0;
 }
 

@@ -99,6 +99,8 @@ int     or_cts_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
 int     or_cts_read_state(const or_cts* s, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
 int     or_cts_sample_count(const or_cts* s, uint32_t key);
 double  or_cts_avg(or_cts* s, uint32_t key, int64_t now, int ev);
+/* Every flowId's window, layout of sg_flow_export_state: ring[K][stride][8] {start, 7 counters}, occ[K][2]. */
+int     or_cts_export_state(const or_cts* s, int stride, int64_t* ring, int64_t* occ);
 
 /* ---------- cluster hot-parameter tokens (ClusterParamFlowChecker over ClusterParamMetric) ---------- */
 int     or_cts_load_param_rules(or_cts* s, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,

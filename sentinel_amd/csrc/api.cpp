@@ -806,6 +806,33 @@ int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* cou
     return SG_OK;
 }
 
+int sg_flow_export_state(sg_handle* h, int64_t* ring, uint64_t ring_words, int64_t* occ, uint64_t occ_words,
+                         int32_t* stride) {
+    if (!h || !stride) return SG_E_INVAL;
+    *stride = h->stride;
+    if (!ring) return SG_OK;
+    const uint64_t rw = (uint64_t)h->K * h->stride * 8, ow = 2ull * h->K;
+    if (ring_words < rw || !occ || occ_words < ow) return fail(h, SG_E_INVAL, "export buffers too small");
+    if (h->K == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    static_assert(sizeof(Bucket) == 64 && sizeof(Occ) == 16, "export layout");
+    HIP_TRY(h, hipMemcpy(ring, h->d_ring, rw * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(occ, h->d_occ, ow * 8, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_flow_import_state(sg_handle* h, const int64_t* ring, uint64_t ring_words, const int64_t* occ,
+                         uint64_t occ_words) {
+    if (!h || !ring || !occ) return SG_E_INVAL;
+    const uint64_t rw = (uint64_t)h->K * h->stride * 8, ow = 2ull * h->K;
+    if (ring_words != rw || occ_words != ow) return fail(h, SG_E_INVAL, "import size does not match the loaded rules");
+    if (h->K == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipMemcpy(h->d_ring, ring, rw * 8, hipMemcpyHostToDevice));
+    HIP_TRY(h, hipMemcpy(h->d_occ, occ, ow * 8, hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
 int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap) {
     if (!h || !out || cap < 2ull * h->K) return SG_E_INVAL;
     if (h->K == 0) return SG_OK;
@@ -941,22 +968,40 @@ int sg_param_read_state(sg_handle* h, uint32_t rule, uint64_t value, int64_t* la
     if (!h || rule >= h->ptab.size() || !last_time || !tokens) return SG_E_INVAL;
     HIP_TRY(h, hipSetDevice(h->device));
     const PRule& R = h->ptab[rule];
-    std::vector<PSlot> t(R.table_mask + 2);
-    HIP_TRY(h, hipMemcpy(t.data(), h->d_ptable + R.table_base, sizeof(PSlot) * t.size(), hipMemcpyDeviceToHost));
-    const PSlot* s = nullptr;
-    if (value == ~0ull) {
-        s = &t[R.table_mask + 1];
+    PSlot found{};
+    bool hit = false;
+    if (value == ~0ull) {  // the side slot
+        HIP_TRY(h, hipMemcpy(&found, h->d_ptable + R.table_base + R.table_mask + 1, sizeof(PSlot), hipMemcpyDeviceToHost));
+        hit = true;
     } else {
-        for (const PSlot& x : t)
-            if (x.value == value) {
-                s = &x;
-                break;
+        // the probe sequence of param.hip's param_slot, read in chunks of 64 slots
+        uint64_t x = value + 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        x ^= x >> 31;
+        uint64_t i = x & R.table_mask, seen = 0;
+        PSlot chunk[64];
+        while (!hit && seen <= R.table_mask) {
+            const uint64_t m = std::min<uint64_t>(64, R.table_mask + 1 - i);  // up to the table's end
+            HIP_TRY(h, hipMemcpy(chunk, h->d_ptable + R.table_base + i, sizeof(PSlot) * m, hipMemcpyDeviceToHost));
+            bool empty = false;
+            for (uint64_t j = 0; j < m && !hit && !empty; ++j) {
+                if (chunk[j].value == value) {
+                    found = chunk[j];
+                    hit = true;
+                } else if (chunk[j].value == ~0ull) {
+                    empty = true;
+                }
             }
+            if (empty) break;
+            seen += m;
+            i = (i + m) & R.table_mask;
+        }
     }
-    if (!s || !s->flags) return 0;
-    *last_time = s->time;
-    *tokens = s->tokens;
-    return (int)s->flags;
+    if (!hit || !found.flags) return 0;
+    *last_time = found.time;
+    *tokens = found.tokens;
+    return (int)found.flags;
 }
 
 // --------------------------------------------------------------------- pace controller

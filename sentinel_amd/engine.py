@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
-           "sg_flow_read_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
+           "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
@@ -51,6 +51,8 @@ def load_library():
         "sg_enable_stats": (C.c_int, [vp, C.c_int]),
         "sg_get_stats": (C.c_int, [vp, C.POINTER(abi.sg_batch_stats)]),
         "sg_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
+        "sg_flow_export_state": (C.c_int, [vp, vp, u64, vp, u64, vp]),
+        "sg_flow_import_state": (C.c_int, [vp, vp, u64, vp, u64]),
         "sg_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
         "sg_snapshot_metrics_device": (C.c_int, [vp, i64, vp, u64, vp]),
         "sg_debug_copy": (C.c_int, [vp, C.c_int, vp, u64]),
@@ -159,6 +161,26 @@ class FlowEngine:
         occ = np.zeros(2, np.int64)
         self._check(self._L.sg_flow_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ)))
         return starts, counters.reshape(sample_count, abi.NUM_EVENTS), occ
+
+    def state_stride(self):
+        st = C.c_int32()
+        self._check(self._L.sg_flow_export_state(self.h, None, 0, None, 0, C.byref(st)))
+        return st.value
+
+    def export_state(self, n_rules):
+        """(ring [K][stride][8] {start, 7 ClusterFlowEvent counters}, occ [K][2]) of every flowId."""
+        stride = self.state_stride()
+        ring = np.zeros((n_rules, stride, 8), np.int64)
+        occ = np.zeros((n_rules, 2), np.int64)
+        st = C.c_int32()
+        self._check(self._L.sg_flow_export_state(self.h, abi.ptr(ring), ring.size, abi.ptr(occ), occ.size,
+                                                 C.byref(st)))
+        return ring, occ
+
+    def import_state(self, ring, occ):
+        ring = np.ascontiguousarray(ring, dtype=np.int64)
+        occ = np.ascontiguousarray(occ, dtype=np.int64)
+        self._check(self._L.sg_flow_import_state(self.h, abi.ptr(ring), ring.size, abi.ptr(occ), occ.size))
 
     def snapshot_device(self, now_ms, out_ptr, n_rules, stream_ptr=0):
         """{passQps, blockQps} per flowId into device memory at out_ptr (2*n_rules doubles)."""
