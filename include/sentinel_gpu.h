@@ -221,7 +221,8 @@ typedef struct sg_degrade_rule {
 } sg_degrade_rule;
 
 /* One resource: its FlowRule with the default controller (limitApp "default", DIRECT strategy, read
- * from the resource's ClusterNode) and up to two DegradeRules, checked in order. */
+ * from the resource's ClusterNode) and up to two DegradeRules, checked in order. sg_local_load_flow_rules
+ * below replaces the flow rules with any number per resource. */
 typedef struct sg_local_rule {
     double  flow_count;           /* FlowRule.count                                           */
     int32_t flow_grade;           /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS, -1 no flow rule    */
@@ -238,10 +239,10 @@ typedef struct sg_local_event {
     uint32_t resource;            /* resource index | SG_KEY_PRIO (prioritized entry)          */
     int32_t  count;               /* acquireCount of the entry (also the exit's batchCount)    */
     int32_t  kind;                /* SG_LOCAL_*                                               */
-    int32_t  reserved;
+    int32_t  origin;              /* Context origin: 0 = none (""), 1..n_origins = an origin id   */
 } sg_local_event;
 
-#define SG_LOCAL_PASS          0
+#define SG_LOCAL_PASS          0  /* passes; wait_ms > 0: after the rate limiter's sleep        */
 #define SG_LOCAL_BLOCK_FLOW    1  /* FlowException                                            */
 #define SG_LOCAL_BLOCK_DEGRADE 2  /* DegradeException                                         */
 #define SG_LOCAL_PASS_WAIT     3  /* PriorityWaitException: passes after wait_ms              */
@@ -255,8 +256,32 @@ typedef struct sg_local_config {
     int32_t sample_count;         /* SampleCountProperty.SAMPLE_COUNT, default 2 (1..60)          */
     int32_t interval_ms;          /* IntervalProperty.INTERVAL, default 1000                      */
     int32_t occupy_timeout_ms;    /* OccupyTimeoutProperty.occupyTimeout, default 500              */
-    int32_t reserved;
+    int32_t cold_factor;          /* ColdFactorProperty.coldFactor (SentinelConfig, default 3; <= 1 → 3) */
 } sg_local_config;
+
+/* ---- the flow rules of the local chain: FlowRuleManager.loadRules → FlowRuleChecker.checkFlow ----
+ * FlowRule (core/.../slots/block/flow/FlowRule.java) of one resource, with its traffic-shaping controller
+ * (FlowRuleUtil.generateRater, FlowRuleUtil.java:132-149) and limitApp node selection
+ * (FlowRuleChecker.selectNodeByRequesterAndStrategy, FlowRuleChecker.java:115-145). Origins are the caller's
+ * dense ids for the Context origin strings (never "default" / "other"). */
+#define SG_CONTROL_DEFAULT               0  /* DefaultController (THREAD rules always use it)        */
+#define SG_CONTROL_WARM_UP               1  /* WarmUpController                                       */
+#define SG_CONTROL_RATE_LIMITER          2  /* RateLimiterController                                  */
+#define SG_CONTROL_WARM_UP_RATE_LIMITER  3  /* WarmUpRateLimiterController                            */
+#define SG_LIMIT_APP_DEFAULT   0            /* limitApp "default": the resource's ClusterNode         */
+#define SG_LIMIT_APP_OTHER   (-1)           /* limitApp "other": origins no rule of the resource names */
+#define SG_STRATEGY_DIRECT     0            /* RELATE / CHAIN read other nodes: SG_E_UNSUPPORTED      */
+typedef struct sg_local_flow_rule {
+    uint32_t resource;            /* resource index (sg_local_load_rules order)                    */
+    int32_t  grade;               /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS                        */
+    double   count;
+    int32_t  control_behavior;    /* SG_CONTROL_*                                                 */
+    int32_t  limit_app;           /* SG_LIMIT_APP_DEFAULT, SG_LIMIT_APP_OTHER or an origin id > 0   */
+    int32_t  strategy;            /* SG_STRATEGY_DIRECT                                           */
+    int32_t  warm_up_period_sec;  /* warmUpPeriodSec, default 10                                  */
+    int32_t  max_queueing_ms;     /* maxQueueingTimeMs, default 500                               */
+    int32_t  reserved;
+} sg_local_flow_rule;
 
 /* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
 typedef struct sg_batch_stats {
@@ -371,6 +396,23 @@ int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t 
  * such slots read 0), head[14] = {curThreadNum, then per breaker: state, nextRetry, stat start, slow/error
  * count, total count, 0}. */
 int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head);
+/*   sg_local_load_flow_rules ← FlowRuleManager.loadRules (FlowRuleManager.java, FlowRuleUtil.buildFlowRuleMap
+ *                              :83-130): replaces every resource's flow rules. Invalid rules are ignored as the
+ *                              reference ignores them (FlowRuleUtil.isValidRule :167-251), duplicates are dropped
+ *                              (its HashSet), and each resource's rules are stably sorted by FlowRuleComparator
+ *                              (FlowRuleComparator.java:30-55: specific/other limitApps before "default"). Fresh
+ *                              controllers (warm-up tokens 0, latestPassedTime -1); resource statistics are kept.
+ *                              n_origins: the largest origin id events may carry. Resources with a limitApp other
+ *                              than "default" keep one origin StatisticNode per origin id (ClusterNode
+ *                              .getOrCreateOriginNode), which starts empty at every load. Returns the number of
+ *                              rules kept (>= 0) or an error.
+ *   sg_local_read_origin_state ← that origin node: same layout as sg_local_read_state (head[0] = curThreadNum).
+ *   sg_local_read_controller   ← the controller of input rule i: {storedTokens, lastFilledTime, latestPassedTime};
+ *                              SG_E_INVAL for an ignored rule. */
+int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins);
+int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64_t* second, int64_t* borrow,
+                               int64_t* minute, int64_t* head);
+int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);
 
 /* ---------- token-server wire codec ----------
  * The default token server frames every message with a 2-byte big-endian length

@@ -85,6 +85,16 @@ def lib():
         "or_cpm_add": (None, [vp, i64, u64, C.c_int]), "or_cpm_get_sum": (i64, [vp, i64, u64]),
         "or_cpm_get_avg": (C.c_double, [vp, i64, u64]),
         "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
+        "or_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32]),
+        "or_local_set_cold_factor": (None, [vp, C.c_int]),
+        "or_local_origin_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
+        "or_local_controller": (C.c_int, [vp, u32, vp]),
+        "or_local_rule_order": (C.c_int, [vp, u32, vp, u32]),
+        "or_ctl_new": (vp, [vp, C.c_int]), "or_ctl_free": (None, [vp]), "or_ctl_state": (None, [vp, vp]),
+        "or_ctl_warning_token": (C.c_int32, [vp]), "or_ctl_max_token": (C.c_int32, [vp]),
+        "or_warm_can_pass": (C.c_int, [vp, i64, d, d, C.c_int]),
+        "or_warm_rl_can_pass": (C.c_int, [vp, i64, d, C.c_int, vp]),
+        "or_select_node": (C.c_int, [vp, u32, u32, C.c_int]),
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
         "or_rls_decide": (C.c_int, [vp, vp, u64, vp]),
@@ -453,6 +463,59 @@ def degrade_rule(grade, count, time_window_sec, min_request_amount=5, stat_inter
     return r
 
 
+def local_flow_rule(resource=0, count=0.0, grade=abi.FLOW_GRADE_QPS, behavior=abi.CONTROL_DEFAULT,
+                    limit_app=abi.LIMIT_APP_DEFAULT, warm_up_sec=10, max_queueing_ms=500, strategy=abi.STRATEGY_DIRECT):
+    """sg_local_flow_rule: FlowRule defaults (FlowRule.java: warmUpPeriodSec 10, maxQueueingTimeMs 500)."""
+    r = np.zeros((), abi.LOCAL_FLOW_RULE_DTYPE)
+    r["resource"], r["grade"], r["count"], r["control_behavior"] = resource, grade, count, behavior
+    r["limit_app"], r["strategy"], r["warm_up_period_sec"], r["max_queueing_ms"] = (limit_app, strategy, warm_up_sec,
+                                                                                   max_queueing_ms)
+    return r
+
+
+class Controller:
+    """One WarmUpController / WarmUpRateLimiterController on its own (the reference's controller tests mock the
+    node's passQps and previousPassQps)."""
+
+    def __init__(self, count, warm_up_sec, cold_factor=3, behavior=abi.CONTROL_WARM_UP, max_queueing_ms=500):
+        r = local_flow_rule(count=count, behavior=behavior, warm_up_sec=warm_up_sec, max_queueing_ms=max_queueing_ms)
+        r = np.ascontiguousarray(r.reshape(1))
+        self.h = lib().or_ctl_new(abi.ptr(r), cold_factor)
+
+    def __del__(self):
+        if self.h:
+            lib().or_ctl_free(self.h)
+            self.h = None
+
+    def warm_can_pass(self, now, pass_qps, prev_qps, acquire=1):
+        return bool(lib().or_warm_can_pass(self.h, now, float(pass_qps), float(prev_qps), acquire))
+
+    def warm_rl_can_pass(self, now, prev_qps, acquire=1):
+        w = C.c_int64()
+        ok = lib().or_warm_rl_can_pass(self.h, now, float(prev_qps), acquire, C.byref(w))
+        return bool(ok), w.value
+
+    def state(self):
+        out = np.zeros(3, np.int64)
+        lib().or_ctl_state(self.h, abi.ptr(out))
+        return out
+
+    @property
+    def warning_token(self):
+        return lib().or_ctl_warning_token(self.h)
+
+    @property
+    def max_token(self):
+        return lib().or_ctl_max_token(self.h)
+
+
+def select_node(rules, i, origin):
+    """FlowRuleChecker.selectNodeByRequesterAndStrategy: 0 ClusterNode, 1 origin node, None."""
+    rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
+    r = lib().or_select_node(abi.ptr(rules), len(rules), i, origin)
+    return None if r < 0 else r
+
+
 def local_rule(flow_count=0.0, flow_grade=abi.FLOW_GRADE_NONE, breakers=()):
     r = np.zeros((), abi.LOCAL_RULE_DTYPE)
     r["flow_count"], r["flow_grade"], r["n_breakers"] = flow_count, flow_grade, len(breakers)
@@ -465,8 +528,9 @@ class LocalChain:
     """Sequential replay of the local slot chain (StatisticSlot → FlowSlot/DefaultController → DegradeSlot)
     for one resource per rule. Events: entries and exits with explicit times."""
 
-    def __init__(self, sample_count=2, interval_ms=1000, occupy_timeout_ms=500):
+    def __init__(self, sample_count=2, interval_ms=1000, occupy_timeout_ms=500, cold_factor=3):
         self.h = lib().or_local_new(sample_count, interval_ms, occupy_timeout_ms)
+        lib().or_local_set_cold_factor(self.h, cold_factor)
         self.S = sample_count
 
     def __del__(self):
@@ -478,22 +542,54 @@ class LocalChain:
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
         assert lib().or_local_load_rules(self.h, abi.ptr(rules), len(rules)) == 0
 
+    def load_flow_rules(self, rules, n_origins=0):
+        """FlowRuleManager.loadRules: returns the number of rules kept."""
+        rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
+        rc = lib().or_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins)
+        if rc < 0:
+            raise ValueError(f"or_local_load_flow_rules: {rc}")
+        return rc
+
     def decide(self, events):
         ev = np.ascontiguousarray(events, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
         out = np.zeros(len(ev), abi.LOCAL_RES_DTYPE)
-        lib().or_local_decide(self.h, abi.ptr(ev), len(ev), abi.ptr(out))
+        rc = lib().or_local_decide(self.h, abi.ptr(ev), len(ev), abi.ptr(out))
+        if rc != 0:
+            raise ValueError(f"or_local_decide: {rc}")
         return out
 
-    def entry(self, t, res=0, count=1, prio=False):
+    def entry(self, t, res=0, count=1, prio=False, origin=0):
         e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
-        e[0] = (t, 0, res | (0x80000000 if prio else 0), count, abi.LOCAL_ENTRY, 0)
+        e[0] = (t, 0, res | (0x80000000 if prio else 0), count, abi.LOCAL_ENTRY, origin)
         r = self.decide(e)[0]
         return int(r["status"]), int(r["wait_ms"])
 
-    def exit(self, t, create_ts, res=0, count=1, error=False):
+    def exit(self, t, create_ts, res=0, count=1, error=False, origin=0):
         e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
-        e[0] = (t, create_ts, res, count, abi.LOCAL_EXIT_ERROR if error else abi.LOCAL_EXIT, 0)
+        e[0] = (t, create_ts, res, count, abi.LOCAL_EXIT_ERROR if error else abi.LOCAL_EXIT, origin)
         self.decide(e)
+
+    def origin_dump(self, res, origin):
+        """(second, borrow, minute, threads, exists) of the origin node of (res, origin)."""
+        sec = np.zeros((self.S, 8), np.int64)
+        bor = np.zeros((self.S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        th = C.c_int64()
+        rc = lib().or_local_origin_dump(self.h, res, origin, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), C.byref(th))
+        assert rc >= 0
+        return sec, bor, mnt, th.value, rc == 1
+
+    def rule_order(self, res):
+        out = np.zeros(256, np.int32)
+        k = lib().or_local_rule_order(self.h, res, abi.ptr(out), len(out))
+        assert k >= 0
+        return [int(x) for x in out[:k]]
+
+    def controller(self, i):
+        out = np.zeros(3, np.int64)
+        if lib().or_local_controller(self.h, i, abi.ptr(out)) != 0:
+            return None
+        return out
 
     def second_sum(self, res, t, ev):
         return lib().or_local_second_sum(self.h, res, t, ev)

@@ -869,18 +869,36 @@ typedef struct or_breaker {
     or_leap* stat; /* LeapArray(1, statIntervalMs): c[0] slow / error count, c[1] total count */
 } or_breaker;
 
+/* One FlowRule of a resource with its TrafficShapingController (FlowRuleUtil.generateRater, :132-149). */
+typedef struct or_ctl {
+    sg_local_flow_rule rule;
+    int behavior;              /* the controller: THREAD rules and unknown behaviours use DefaultController */
+    /* WarmUpController fields (WarmUpController.java:66-73), fixed by construct (:83-106) */
+    int32_t warning_token, max_token, cold;
+    double slope;
+    int64_t stored_tokens, last_filled;   /* AtomicLong(0) each */
+    int64_t latest;                       /* RateLimiter / WarmUpRateLimiter latestPassedTime, AtomicLong(-1) */
+    int32_t input;                        /* index in the loaded rule array */
+} or_ctl;
+
 typedef struct or_node {
     or_leap* second;  /* ArrayMetric(SAMPLE_COUNT, INTERVAL): OccupiableBucketLeapArray (StatisticNode.java:96-97) */
     or_leap* minute;  /* ArrayMetric(60, 60000, false) (:103)                                                   */
     int64_t threads;  /* curThreadNum                                                                            */
     sg_local_rule rule;
     or_breaker cb[2];
+    or_ctl* ctl;      /* the resource's flow rules in FlowRuleComparator order */
+    uint32_t n_ctl;
+    struct or_node** origin;  /* ClusterNode.originCountMap: [n_origins + 1], created on first use */
 } or_node;
 
 struct or_local {
-    int S, interval, occupy_timeout;
+    int S, interval, occupy_timeout, cold_factor;
     or_node* nodes;
     uint32_t n;
+    int32_t n_origins;
+    int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
+    uint32_t n_rules;
 };
 
 or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms) {
@@ -888,7 +906,29 @@ or_local* or_local_new(int second_sample_count, int second_interval_ms, int occu
     l->S = second_sample_count;            /* SampleCountProperty.SAMPLE_COUNT, default 2   */
     l->interval = second_interval_ms;      /* IntervalProperty.INTERVAL, default 1000        */
     l->occupy_timeout = occupy_timeout_ms; /* OccupyTimeoutProperty.occupyTimeout, 500      */
+    l->cold_factor = 3;                    /* ColdFactorProperty.coldFactor (SentinelConfig default 3) */
     return l;
+}
+
+void or_local_set_cold_factor(or_local* l, int cold_factor) { l->cold_factor = cold_factor > 1 ? cold_factor : 3; }
+
+static or_node* node_new_plain(or_local* l) {
+    or_node* o = (or_node*)calloc(1, sizeof(or_node));
+    o->second = or_leap_new(OR_LEAP_OCCUPIABLE, l->S, l->interval);
+    o->minute = or_leap_new(OR_LEAP_BUCKET, 60, 60 * 1000);
+    return o;
+}
+
+static void free_origins(or_local* l, or_node* nd) {
+    if (!nd->origin) return;
+    for (int32_t o = 0; o <= l->n_origins; o++) {
+        if (!nd->origin[o]) continue;
+        or_leap_free(nd->origin[o]->second);
+        or_leap_free(nd->origin[o]->minute);
+        free(nd->origin[o]);
+    }
+    free(nd->origin);
+    nd->origin = NULL;
 }
 
 static void free_nodes(or_local* l) {
@@ -896,8 +936,13 @@ static void free_nodes(or_local* l) {
         or_leap_free(l->nodes[i].second);
         or_leap_free(l->nodes[i].minute);
         for (int j = 0; j < 2; j++) or_leap_free(l->nodes[i].cb[j].stat);
+        free(l->nodes[i].ctl);
+        free_origins(l, &l->nodes[i]);
     }
     free(l->nodes);
+    free(l->rule_pos);
+    l->rule_pos = NULL;
+    l->n_rules = 0;
     l->nodes = NULL;
     l->n = 0;
 }
@@ -908,10 +953,96 @@ void or_local_free(or_local* l) {
     free(l);
 }
 
+/* WarmUpController.construct (WarmUpController.java:83-106), int arithmetic as Java's */
+static void ctl_init(or_ctl* c, const sg_local_flow_rule* r, int cold, int32_t input) {
+    memset(c, 0, sizeof(*c));
+    c->rule = *r;
+    c->input = input;
+    c->behavior = (r->grade == 1 && r->control_behavior >= SG_CONTROL_WARM_UP &&
+                   r->control_behavior <= SG_CONTROL_WARM_UP_RATE_LIMITER) ? r->control_behavior : SG_CONTROL_DEFAULT;
+    c->latest = -1;
+    c->cold = cold;
+    if (c->behavior == SG_CONTROL_WARM_UP || c->behavior == SG_CONTROL_WARM_UP_RATE_LIMITER) {
+        c->warning_token = or_d2i(r->warm_up_period_sec * r->count) / (cold - 1);
+        const int32_t two_w = (int32_t)(2u * (uint32_t)r->warm_up_period_sec);      /* 2 * warmUpPeriodInSec: int */
+        c->max_token = (int32_t)((uint32_t)c->warning_token + (uint32_t)or_d2i(two_w * r->count / (1.0 + cold)));
+        c->slope = (cold - 1.0) / r->count / (double)(int32_t)((uint32_t)c->max_token - (uint32_t)c->warning_token);
+    }
+}
+
+/* FlowRuleUtil.isValidRule (:167-182) for DIRECT rules outside cluster mode: count >= 0, grade THREAD/QPS,
+ * behaviour >= 0; QPS rules: checkControlBehaviorField (:240-251). */
+static int flow_rule_valid(const sg_local_flow_rule* r) {
+    if (!(r->count >= 0) || r->grade < 0 || r->strategy < 0 || r->control_behavior < 0) return 0;
+    if (r->grade == 1) {
+        switch (r->control_behavior) {
+        case SG_CONTROL_WARM_UP: return r->warm_up_period_sec > 0;
+        case SG_CONTROL_RATE_LIMITER: return r->max_queueing_ms > 0;
+        case SG_CONTROL_WARM_UP_RATE_LIMITER: return r->warm_up_period_sec > 0 && r->max_queueing_ms > 0;
+        default: return 1;
+        }
+    }
+    return r->grade == 0;
+}
+
+/* FlowRule.equals over the fields the ABI carries (the reference's HashSet drops duplicates, :109-117) */
+static int flow_rule_same(const sg_local_flow_rule* a, const sg_local_flow_rule* b) {
+    return a->resource == b->resource && a->grade == b->grade && a->count == b->count &&
+           a->control_behavior == b->control_behavior && a->limit_app == b->limit_app && a->strategy == b->strategy &&
+           a->warm_up_period_sec == b->warm_up_period_sec && a->max_queueing_ms == b->max_queueing_ms;
+}
+
+int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins) {
+    for (uint32_t i = 0; i < n; i++)
+        if (rules[i].strategy != SG_STRATEGY_DIRECT && flow_rule_valid(&rules[i])) return SG_E_UNSUPPORTED;
+    if (n_origins < 0) return SG_E_INVAL;
+    for (uint32_t k = 0; k < l->n; k++) {
+        free(l->nodes[k].ctl);
+        l->nodes[k].ctl = NULL;
+        l->nodes[k].n_ctl = 0;
+        free_origins(l, &l->nodes[k]);
+    }
+    l->n_origins = n_origins;
+    free(l->rule_pos);
+    l->rule_pos = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    l->n_rules = n;
+    uint32_t* cnt = (uint32_t*)calloc(l->n ? l->n : 1, sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; i++) {
+        l->rule_pos[i] = -1;
+        const sg_local_flow_rule* r = &rules[i];
+        if (r->resource >= l->n || !flow_rule_valid(r)) continue;   /* ignored, as RecordLog.warn + continue */
+        if (r->limit_app > n_origins) { free(cnt); return SG_E_INVAL; }
+        int dup = 0;
+        for (uint32_t j = 0; j < i && !dup; j++) dup = l->rule_pos[j] >= 0 && flow_rule_same(&rules[j], r);
+        if (dup) continue;
+        l->rule_pos[i] = 0;
+        cnt[r->resource]++;
+    }
+    for (uint32_t k = 0; k < l->n; k++)
+        if (cnt[k]) l->nodes[k].ctl = (or_ctl*)calloc(cnt[k], sizeof(or_ctl));
+    /* Collections.sort(rules, FlowRuleComparator): stable; non-"default" limitApps first (:30-55) */
+    for (int pass = 0; pass < 2; pass++) {
+        for (uint32_t i = 0; i < n; i++) {
+            if (l->rule_pos[i] < 0) continue;
+            const int is_default = rules[i].limit_app == SG_LIMIT_APP_DEFAULT;
+            if (is_default != pass) continue;
+            or_node* nd = &l->nodes[rules[i].resource];
+            ctl_init(&nd->ctl[nd->n_ctl], &rules[i], l->cold_factor, (int32_t)i);
+            l->rule_pos[i] = (int32_t)((rules[i].resource << 16) | nd->n_ctl);
+            nd->n_ctl++;
+        }
+    }
+    free(cnt);
+    uint32_t kept = 0;
+    for (uint32_t i = 0; i < n; i++) kept += l->rule_pos[i] >= 0;
+    return (int)kept;
+}
+
 int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
     free_nodes(l);
     l->nodes = (or_node*)calloc(n ? n : 1, sizeof(or_node));
     l->n = n;
+    l->n_origins = 0;
     for (uint32_t i = 0; i < n; i++) {
         or_node* nd = &l->nodes[i];
         nd->rule = rules[i];
@@ -923,6 +1054,16 @@ int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
             nd->cb[j].stat = or_leap_new(OR_LEAP_BUCKET, 1, rules[i].breakers[j].stat_interval_ms);
             if (!nd->cb[j].stat) return SG_E_INVAL;
         }
+        if (rules[i].flow_grade >= 0) {  /* the one DefaultController rule, limitApp "default" */
+            sg_local_flow_rule fr;
+            memset(&fr, 0, sizeof(fr));
+            fr.resource = i;
+            fr.grade = rules[i].flow_grade;
+            fr.count = rules[i].flow_count;
+            nd->ctl = (or_ctl*)calloc(1, sizeof(or_ctl));
+            ctl_init(&nd->ctl[0], &fr, l->cold_factor, -1);
+            nd->n_ctl = 1;
+        }
     }
     return 0;
 }
@@ -930,6 +1071,14 @@ int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
 /* StatisticNode.passQps = rollingCounterInSecond.pass() / getWindowIntervalInSec (StatisticNode.java:200-202) */
 static double node_pass_qps(or_node* nd, int64_t t) {
     return (double)or_leap_get_sum(nd->second, t, OR_M_PASS) / nd->second->isec;
+}
+
+/* StatisticNode.previousPassQps = rollingCounterInMinute.previousWindowPass() (StatisticNode.java:175-177,
+ * ArrayMetric.java:270-277): currentWindow, then getPreviousWindow's PASS */
+static double node_previous_pass_qps(or_node* nd, int64_t t) {
+    or_leap_current_window(nd->minute, t);
+    int s = or_leap_previous_window(nd->minute, t);
+    return s < 0 ? 0.0 : (double)nd->minute->b[s].c[OR_M_PASS];
 }
 
 /* StatisticNode.tryOccupyNext, StatisticNode.java:288-320 */
@@ -955,6 +1104,199 @@ static int64_t node_try_occupy_next(or_local* l, or_node* nd, int64_t now, int a
 }
 
 static void node_add(or_leap* w, int64_t t, int ev, int64_t n) { or_leap_add(w, t, ev, n); }
+
+/* ---- traffic-shaping controllers (core/.../slots/block/flow/controller) ---- */
+
+/* WarmUpController.coolDownTokens (:161-175) */
+static int64_t warm_cool_down(const or_ctl* c, int64_t current_time, int64_t pass_qps) {
+    int64_t old = c->stored_tokens, nv = old;
+    if (old < c->warning_token) {
+        nv = or_d2l((double)old + (double)(current_time - c->last_filled) * c->rule.count / 1000);
+    } else if (old > c->warning_token) {
+        if (pass_qps < or_d2i(c->rule.count) / c->cold)
+            nv = or_d2l((double)old + (double)(current_time - c->last_filled) * c->rule.count / 1000);
+    }
+    return nv < c->max_token ? nv : (int64_t)c->max_token;
+}
+
+/* WarmUpController.syncToken (:140-159), single-threaded: the compareAndSet succeeds */
+static void warm_sync_token(or_ctl* c, int64_t now, int64_t pass_qps) {
+    int64_t current_time = now - now % 1000;
+    if (current_time <= c->last_filled) return;
+    c->stored_tokens = warm_cool_down(c, current_time, pass_qps);
+    int64_t cur = (int64_t)((uint64_t)c->stored_tokens - (uint64_t)pass_qps);   /* addAndGet(0 - passQps) */
+    c->stored_tokens = cur < 0 ? 0 : cur;
+    c->last_filled = current_time;
+}
+
+/* Math.nextUp(1.0 / (aboveToken * slope + 1.0 / count)) */
+static double warm_qps(const or_ctl* c, int64_t above) {
+    return nextafter(1.0 / ((double)above * c->slope + 1.0 / c->rule.count), INFINITY);
+}
+
+/* WarmUpController.canPass (:113-138) with the node's passQps / previousPassQps */
+int or_warm_can_pass(or_ctl* c, int64_t now, double pass_qps_d, double prev_qps_d, int acquire) {
+    int64_t pass_qps = or_d2l(pass_qps_d);
+    int64_t prev = or_d2l(prev_qps_d);
+    warm_sync_token(c, now, prev);
+    int64_t rest = c->stored_tokens;
+    int64_t sum = (int64_t)((uint64_t)pass_qps + (uint64_t)(int64_t)acquire);   /* long + int */
+    if (rest >= c->warning_token) return (double)sum <= warm_qps(c, rest - c->warning_token);
+    return (double)sum <= c->rule.count;
+}
+
+/* WarmUpRateLimiterController.canPass (:43-87): 1 pass (*wait = the sleep), 0 block */
+int or_warm_rl_can_pass(or_ctl* c, int64_t now, double prev_qps_d, int acquire, int64_t* wait) {
+    *wait = 0;
+    warm_sync_token(c, now, or_d2l(prev_qps_d));
+    int64_t rest = c->stored_tokens;
+    int64_t cost;
+    if (rest >= c->warning_token) cost = or_math_round(1.0 * (acquire) / warm_qps(c, rest - c->warning_token) * 1000);
+    else cost = or_math_round(1.0 * (acquire) / c->rule.count * 1000);
+    int64_t expected = cost + c->latest;
+    if (expected <= now) {
+        c->latest = now;
+        return 1;
+    }
+    int64_t w = cost + c->latest - now;
+    if (w > c->rule.max_queueing_ms) return 0;
+    c->latest += cost;
+    w = c->latest - now;
+    if (w > c->rule.max_queueing_ms) {  /* unreachable single-threaded */
+        c->latest -= cost;
+        return 0;
+    }
+    *wait = w > 0 ? w : 0;
+    return 1;
+}
+
+/* RateLimiterController.canPass (:46-91) on the rule's own latestPassedTime */
+static int rl_can_pass(or_ctl* c, int64_t now, int acquire, int64_t* wait) {
+    *wait = 0;
+    if (acquire <= 0) return 1;
+    if (c->rule.count <= 0) return 0;
+    int64_t cost = or_math_round(1.0 * (acquire) / c->rule.count * 1000);
+    int64_t expected = cost + c->latest;
+    if (expected <= now) {
+        c->latest = now;
+        return 1;
+    }
+    int64_t w = cost + c->latest - now;
+    if (w > c->rule.max_queueing_ms) return 0;
+    c->latest += cost;
+    w = c->latest - now;
+    if (w > c->rule.max_queueing_ms) {
+        c->latest -= cost;
+        return 0;
+    }
+    *wait = w > 0 ? w : 0;
+    return 1;
+}
+
+/* Stand-alone controllers for the reference's own controller tests (mocked nodes). */
+or_ctl* or_ctl_new(const sg_local_flow_rule* r, int cold_factor) {
+    or_ctl* c = (or_ctl*)malloc(sizeof(or_ctl));
+    ctl_init(c, r, cold_factor > 1 ? cold_factor : 3, -1);
+    return c;
+}
+void or_ctl_free(or_ctl* c) { free(c); }
+void or_ctl_state(const or_ctl* c, int64_t* out3) {
+    out3[0] = c->stored_tokens;
+    out3[1] = c->last_filled;
+    out3[2] = c->latest;
+}
+int32_t or_ctl_warning_token(const or_ctl* c) { return c->warning_token; }
+int32_t or_ctl_max_token(const or_ctl* c) { return c->max_token; }
+
+/* FlowRuleManager.isOtherOrigin (FlowRuleManager.java:132-148): no rule of the resource names the origin */
+static int is_other_origin(const or_node* nd, int origin) {
+    if (origin <= 0) return 0;
+    for (uint32_t i = 0; i < nd->n_ctl; i++)
+        if (nd->ctl[i].rule.limit_app == origin) return 0;
+    return 1;
+}
+
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy (FlowRuleChecker.java:115-145), DIRECT strategy:
+ * 0 the ClusterNode, 1 the origin node, -1 none (the rule passes) */
+static int select_node(const or_node* nd, const sg_local_flow_rule* r, int origin) {
+    if (origin > 0 && r->limit_app == origin) return 1;   /* limitApp.equals(origin) && filterOrigin(origin) */
+    if (r->limit_app == SG_LIMIT_APP_DEFAULT) return 0;
+    if (r->limit_app == SG_LIMIT_APP_OTHER && is_other_origin(nd, origin)) return 1;
+    return -1;
+}
+
+/* For the FlowRuleCheckerTest restatement: the rules of one resource and a request origin. */
+int or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin) {
+    or_node nd;
+    memset(&nd, 0, sizeof(nd));
+    or_ctl* c = (or_ctl*)calloc(n ? n : 1, sizeof(or_ctl));
+    for (uint32_t j = 0; j < n; j++) c[j].rule = rules[j];
+    nd.ctl = c;
+    nd.n_ctl = n;
+    int r = select_node(&nd, &rules[i], origin);
+    free(c);
+    return r;
+}
+
+static or_node* origin_node(or_local* l, or_node* nd, int origin) {   /* ClusterNode.getOrCreateOriginNode */
+    if (origin <= 0 || origin > l->n_origins) return NULL;
+    if (!nd->origin) nd->origin = (or_node**)calloc((size_t)l->n_origins + 1, sizeof(or_node*));
+    if (!nd->origin[origin]) nd->origin[origin] = node_new_plain(l);
+    return nd->origin[origin];
+}
+
+/* DefaultController.canPass (DefaultController.java:49-76) on the selected node: 1 pass, 0 block, 2 priority wait */
+static int default_can_pass(or_local* l, or_node* sn, const or_ctl* c, int64_t t, int count, int prio, int64_t* wait) {
+    int32_t cur = c->rule.grade == 0 ? (int32_t)sn->threads : or_d2i(node_pass_qps(sn, t));
+    int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)count); /* int + int wraps */
+    if (!((double)sum > c->rule.count)) return 1;
+    if (prio && c->rule.grade == 1) {
+        int64_t w = node_try_occupy_next(l, sn, t, count, c->rule.count);
+        if (w < l->occupy_timeout) {
+            or_leap_add_waiting(sn->second, t + w, count);        /* addWaitingRequest */
+            node_add(sn->minute, t, OR_M_OCCUPIED_PASS, count);   /* addOccupiedPass (StatisticNode.java:333-336) */
+            node_add(sn->minute, t, OR_M_PASS, count);
+            *wait = w;
+            return 2;                                             /* PriorityWaitException */
+        }
+    }
+    return 0;
+}
+
+/* FlowSlot.checkFlow → FlowRuleChecker.checkFlow (:44-57): the rules in order, the first failure throws */
+static int check_flow(or_local* l, or_node* nd, int64_t t, int count, int prio, int origin, int64_t* wait) {
+    *wait = 0;
+    for (uint32_t i = 0; i < nd->n_ctl; i++) {
+        or_ctl* c = &nd->ctl[i];
+        int s = select_node(nd, &c->rule, origin);
+        if (s < 0) continue;
+        or_node* sn = s == 0 ? nd : origin_node(l, nd, origin);
+        int64_t w = 0;
+        switch (c->behavior) {
+        case SG_CONTROL_WARM_UP:
+            if (!or_warm_can_pass(c, t, node_pass_qps(sn, t), node_previous_pass_qps(sn, t), count))
+                return SG_LOCAL_BLOCK_FLOW;
+            break;
+        case SG_CONTROL_RATE_LIMITER:
+            if (!rl_can_pass(c, t, count, &w)) return SG_LOCAL_BLOCK_FLOW;
+            *wait += w;   /* each controller sleeps in turn */
+            break;
+        case SG_CONTROL_WARM_UP_RATE_LIMITER:
+            if (!or_warm_rl_can_pass(c, t, node_previous_pass_qps(sn, t), count, &w)) return SG_LOCAL_BLOCK_FLOW;
+            *wait += w;
+            break;
+        default: {
+            int r = default_can_pass(l, sn, c, t, count, prio, &w);
+            if (r == 0) return SG_LOCAL_BLOCK_FLOW;
+            if (r == 2) {
+                *wait = w;
+                return SG_LOCAL_PASS_WAIT;
+            }
+        }
+        }
+    }
+    return SG_LOCAL_PASS;
+}
 
 /* AbstractCircuitBreaker.tryPass (:73-84); sets *half when this call moved OPEN → HALF_OPEN. */
 static int cb_try_pass(or_breaker* cb, int64_t t, int* half) {
@@ -1020,7 +1362,23 @@ static void cb_on_complete(or_breaker* cb, int64_t t, int64_t rt, int error) {
     }
 }
 
+/* StatisticSlot.exit → recordCompleteFor (StatisticSlot.java:124-165): addRtAndSuccess, decreaseThreadNum,
+ * increaseExceptionQps */
+static void record_complete(or_node* nd, int64_t t, int count, int64_t rt, int error) {
+    node_add(nd->second, t, OR_M_SUCCESS, count);
+    { int s = or_leap_current_window(nd->second, t); if (s != -1) or_leap_slot_add_rt(nd->second, s, rt); }
+    node_add(nd->minute, t, OR_M_SUCCESS, count);
+    { int s = or_leap_current_window(nd->minute, t); if (s != -1) or_leap_slot_add_rt(nd->minute, s, rt); }
+    nd->threads--;
+    if (error) {
+        node_add(nd->second, t, OR_M_EXCEPTION, count);
+        node_add(nd->minute, t, OR_M_EXCEPTION, count);
+    }
+}
+
 int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
+    for (uint64_t i = 0; i < n; i++)
+        if (ev[i].origin < 0 || ev[i].origin > l->n_origins) return SG_E_INVAL;
     for (uint64_t i = 0; i < n; i++) {
         const sg_local_event* e = &ev[i];
         uint32_t res = e->resource & SG_KEY_INDEX;
@@ -1029,28 +1387,12 @@ int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_
         out[i].wait_ms = 0;
         if (res >= l->n) continue;
         or_node* nd = &l->nodes[res];
+        or_node* on = origin_node(l, nd, e->origin);   /* context.getCurEntry().getOriginNode() */
         int64_t t = e->ts_ms;
         int count = e->count;
         if (e->kind == SG_LOCAL_ENTRY) {
-            /* FlowSlot → DefaultController.canPass */
-            int status = SG_LOCAL_PASS;
             int64_t wait = 0;
-            if (nd->rule.flow_grade >= 0) {
-                int32_t cur = nd->rule.flow_grade == 0 ? (int32_t)nd->threads : or_d2i(node_pass_qps(nd, t));
-                int32_t sum = (int32_t)((uint32_t)cur + (uint32_t)count); /* int + int wraps */
-                if ((double)sum > nd->rule.flow_count) {
-                    status = SG_LOCAL_BLOCK_FLOW;
-                    if (prio && nd->rule.flow_grade == 1) {
-                        wait = node_try_occupy_next(l, nd, t, count, nd->rule.flow_count);
-                        if (wait < l->occupy_timeout) {
-                            or_leap_add_waiting(nd->second, t + wait, count); /* addWaitingRequest */
-                            node_add(nd->minute, t, OR_M_OCCUPIED_PASS, count); /* addOccupiedPass */
-                            node_add(nd->minute, t, OR_M_PASS, count);
-                            status = SG_LOCAL_PASS_WAIT;
-                        }
-                    }
-                }
-            }
+            int status = check_flow(l, nd, t, count, prio, e->origin, &wait);   /* FlowSlot */
             int half[2] = {0, 0};
             if (status == SG_LOCAL_PASS) { /* DegradeSlot.performChecking */
                 for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) {
@@ -1063,32 +1405,30 @@ int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_
                     for (int j = 0; j < 2; j++)
                         if (half[j] && nd->cb[j].state == OR_CB_HALF_OPEN) nd->cb[j].state = OR_CB_OPEN;
             }
-            /* StatisticSlot.entry */
+            /* StatisticSlot.entry (:55-122): the DefaultNode/ClusterNode and the origin node */
             if (status == SG_LOCAL_PASS) {
-                nd->threads++;
-                node_add(nd->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
-                node_add(nd->minute, t, OR_M_PASS, count);
+                for (or_node* x = nd; x; x = (x == nd ? on : NULL)) {
+                    x->threads++;
+                    node_add(x->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
+                    node_add(x->minute, t, OR_M_PASS, count);
+                }
+                out[i].wait_ms = wait > INT32_MAX ? INT32_MAX : (int32_t)wait;   /* the rate limiters' sleep */
             } else if (status == SG_LOCAL_PASS_WAIT) {
                 nd->threads++;
+                if (on) on->threads++;
                 out[i].wait_ms = (int32_t)wait;
             } else {
-                node_add(nd->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
-                node_add(nd->minute, t, OR_M_BLOCK, count);
+                for (or_node* x = nd; x; x = (x == nd ? on : NULL)) {
+                    node_add(x->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
+                    node_add(x->minute, t, OR_M_BLOCK, count);
+                }
             }
             out[i].status = status;
         } else {
-            /* StatisticSlot.exit: addRtAndSuccess, decreaseThreadNum, increaseExceptionQps */
             int error = e->kind == SG_LOCAL_EXIT_ERROR;
             int64_t rt = t - e->create_ts;
-            node_add(nd->second, t, OR_M_SUCCESS, count);
-            { int s = or_leap_current_window(nd->second, t); if (s != -1) or_leap_slot_add_rt(nd->second, s, rt); }
-            node_add(nd->minute, t, OR_M_SUCCESS, count);
-            { int s = or_leap_current_window(nd->minute, t); if (s != -1) or_leap_slot_add_rt(nd->minute, s, rt); }
-            nd->threads--;
-            if (error) {
-                node_add(nd->second, t, OR_M_EXCEPTION, count);
-                node_add(nd->minute, t, OR_M_EXCEPTION, count);
-            }
+            record_complete(nd, t, count, rt, error);
+            if (on) record_complete(on, t, count, rt, error);
             /* DegradeSlot.exit → onRequestComplete */
             for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) cb_on_complete(&nd->cb[j], t, rt, error);
         }
@@ -1135,6 +1475,47 @@ int or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* bor
     return 0;
 }
 
+/* The origin node of (res, origin): windows as or_local_dump, *threads = curThreadNum. Returns 1 when the node
+ * exists (some event carried the origin), 0 when it was never created (all-empty dumps), < 0 on bad input. */
+int or_local_origin_dump(const or_local* l, uint32_t res, int origin, int64_t* second, int64_t* borrow,
+                         int64_t* minute, int64_t* threads) {
+    if (res >= l->n || origin <= 0 || origin > l->n_origins) return SG_E_INVAL;
+    const or_node* nd = &l->nodes[res];
+    const or_node* on = nd->origin ? nd->origin[origin] : NULL;
+    if (!on) {
+        for (int i = 0; i < l->S; i++) {
+            for (int e = 0; e < 8; e++) second[8 * i + e] = e == 0 ? INT64_MIN : 0;
+            borrow[2 * i] = INT64_MIN;
+            borrow[2 * i + 1] = 0;
+        }
+        for (int i = 0; i < 60; i++)
+            for (int e = 0; e < 8; e++) minute[8 * i + e] = e == 0 ? INT64_MIN : 0;
+        *threads = 0;
+        return 0;
+    }
+    dump_leap(on->second, second, 1);
+    dump_leap(on->second->borrow, borrow, 0);
+    dump_leap(on->minute, minute, 1);
+    *threads = on->threads;
+    return 1;
+}
+
+/* The input indices of resource res's flow rules in check order; returns their number. */
+int or_local_rule_order(const or_local* l, uint32_t res, int32_t* out, uint32_t cap) {
+    if (res >= l->n) return SG_E_INVAL;
+    const or_node* nd = &l->nodes[res];
+    for (uint32_t i = 0; i < nd->n_ctl && i < cap; i++) out[i] = nd->ctl[i].input;
+    return (int)nd->n_ctl;
+}
+
+/* {storedTokens, lastFilledTime, latestPassedTime} of loaded flow rule i; SG_E_INVAL when it was ignored. */
+int or_local_controller(const or_local* l, uint32_t i, int64_t* out3) {
+    if (i >= l->n_rules || l->rule_pos[i] < 0) return SG_E_INVAL;
+    const or_node* nd = &l->nodes[(uint32_t)l->rule_pos[i] >> 16];
+    or_ctl_state(&nd->ctl[l->rule_pos[i] & 0xFFFF], out3);
+    return 0;
+}
+
 /* ===================================================================================== */
 /* Local-chain trace generator (test infrastructure): a client that exits only the entries */
 /* that passed, as SphU.entry callers do (a BlockException means there is no Entry to exit) */
@@ -1143,7 +1524,7 @@ int or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* bor
 typedef struct or_pending {
     int64_t ts, create_ts, seq;
     uint32_t resource;
-    int32_t count, error;
+    int32_t count, error, origin;
 } or_pending;
 
 struct or_lgen {
@@ -1231,7 +1612,7 @@ uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* r
             e->resource = p.resource;
             e->count = p.count;
             e->kind = p.error ? SG_LOCAL_EXIT_ERROR : SG_LOCAL_EXIT;
-            e->reserved = 0;
+            e->origin = p.origin;
             or_local_decide(g->l, e, 1, &res[k]);
             k++;
             continue;
@@ -1248,6 +1629,7 @@ uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* r
             p.resource = e->resource & SG_KEY_INDEX;
             p.count = e->count;
             p.error = err ? err[i] : 0;
+            p.origin = e->origin;
             pend_push(g, p);
         }
         k++;

@@ -151,6 +151,28 @@ int       or_local_breaker_state(const or_local* l, uint32_t res, int i, int64_t
 int       or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute);
 
 int       or_local_breaker_stat(const or_local* l, uint32_t res, int i, int64_t* start, int64_t* bad, int64_t* total);
+/* FlowRuleManager.loadRules for the local chain (any number of rules per resource, limitApp, controllers);
+ * returns the number of rules kept. */
+int       or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins);
+void      or_local_set_cold_factor(or_local* l, int cold_factor);
+int       or_local_origin_dump(const or_local* l, uint32_t res, int origin, int64_t* second, int64_t* borrow,
+                               int64_t* minute, int64_t* threads);
+int       or_local_controller(const or_local* l, uint32_t i, int64_t* out3);
+int       or_local_rule_order(const or_local* l, uint32_t res, int32_t* out, uint32_t cap);
+
+/* Traffic-shaping controllers on their own (the reference's controller tests mock the node's passQps and
+ * previousPassQps): WarmUpController / WarmUpRateLimiterController. */
+typedef struct or_ctl or_ctl;
+or_ctl*   or_ctl_new(const sg_local_flow_rule* r, int cold_factor);
+void      or_ctl_free(or_ctl* c);
+void      or_ctl_state(const or_ctl* c, int64_t* out3);   /* storedTokens, lastFilledTime, latestPassedTime */
+int32_t   or_ctl_warning_token(const or_ctl* c);
+int32_t   or_ctl_max_token(const or_ctl* c);
+int       or_warm_can_pass(or_ctl* c, int64_t now, double pass_qps, double prev_qps, int acquire);
+int       or_warm_rl_can_pass(or_ctl* c, int64_t now, double prev_qps, int acquire, int64_t* wait);
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy for rule i of a resource's rules: 0 ClusterNode, 1 origin
+ * node, -1 none. */
+int       or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin);
 
 /* Trace generator for the local chain (test infrastructure): entries + the exits of the passed ones. */
 typedef struct or_lgen or_lgen;

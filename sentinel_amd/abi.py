@@ -105,16 +105,24 @@ DEGRADE_RULE_DTYPE = np.dtype([("grade", "<i4"), ("time_window_sec", "<i4"), ("c
 LOCAL_RULE_DTYPE = np.dtype([("flow_count", "<f8"), ("flow_grade", "<i4"), ("n_breakers", "<i4"),
                              ("breakers", DEGRADE_RULE_DTYPE, (2,))], align=True)
 LOCAL_EVENT_DTYPE = np.dtype([("ts_ms", "<i8"), ("create_ts", "<i8"), ("resource", "<u4"), ("count", "<i4"),
-                              ("kind", "<i4"), ("reserved", "<i4")], align=True)
+                              ("kind", "<i4"), ("origin", "<i4")], align=True)
 LOCAL_RES_DTYPE = np.dtype([("status", "<i4"), ("wait_ms", "<i4")], align=True)
 DEGRADE_RT, DEGRADE_EXCEPTION_RATIO, DEGRADE_EXCEPTION_COUNT = 0, 1, 2
 FLOW_GRADE_THREAD, FLOW_GRADE_QPS, FLOW_GRADE_NONE = 0, 1, -1
 LOCAL_ENTRY, LOCAL_EXIT, LOCAL_EXIT_ERROR = 0, 1, 2
 LOCAL_PASS, LOCAL_BLOCK_FLOW, LOCAL_BLOCK_DEGRADE, LOCAL_PASS_WAIT = 0, 1, 2, 3
+# sg_local_flow_rule (FlowRule of the local chain)
+LOCAL_FLOW_RULE_DTYPE = np.dtype([("resource", "<u4"), ("grade", "<i4"), ("count", "<f8"),
+                                  ("control_behavior", "<i4"), ("limit_app", "<i4"), ("strategy", "<i4"),
+                                  ("warm_up_period_sec", "<i4"), ("max_queueing_ms", "<i4"), ("reserved", "<i4")],
+                                 align=True)
+CONTROL_DEFAULT, CONTROL_WARM_UP, CONTROL_RATE_LIMITER, CONTROL_WARM_UP_RATE_LIMITER = 0, 1, 2, 3
+LIMIT_APP_DEFAULT, LIMIT_APP_OTHER = 0, -1
+STRATEGY_DIRECT, STRATEGY_RELATE, STRATEGY_CHAIN = 0, 1, 2
 
 class sg_local_config(C.Structure):
     _fields_ = [("sample_count", C.c_int32), ("interval_ms", C.c_int32), ("occupy_timeout_ms", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("cold_factor", C.c_int32)]
 
 
 assert REQ_DTYPE.itemsize == C.sizeof(sg_req) == 16
@@ -124,6 +132,7 @@ assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
 assert CPARAM_RULE_DTYPE.itemsize == 40 and CPARAM_REQ_DTYPE.itemsize == 24
 assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
+assert LOCAL_FLOW_RULE_DTYPE.itemsize == 40
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:

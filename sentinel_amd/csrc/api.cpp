@@ -111,7 +111,13 @@ struct sg_handle {
 
     // local slot chain
     sg_local_config lcfg{2, 1000, 500, 0};
-    std::vector<LRule> ltab;
+    std::vector<LRule> ltab;          // [K] the resources (sg_local_load_rules), origin nodes not included
+    uint32_t l_nodes = 0;             // resources + origin nodes
+    int32_t l_n_origins = 0;
+    bool l_has_cx = false;
+    std::vector<int64_t> l_rule_slot; // loaded flow rule i → its LCtl index, -2 stateless fast-path rule, -1 ignored
+    LFlowRule* d_lfrules = nullptr;
+    LCtl* d_lctl = nullptr;
     LRule* d_lrules = nullptr;
     LHead* d_lhead = nullptr;
     LBucket* d_lsec = nullptr;
@@ -392,6 +398,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cpval_h);
     dfree(h->d_cpout_h);
     dfree(h->d_lrules);
+    dfree(h->d_lfrules);
+    dfree(h->d_lctl);
     dfree(h->d_lhead);
     dfree(h->d_lsec);
     dfree(h->d_lbor);
@@ -1329,9 +1337,11 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
         if (r.flow_grade >= 0 && !(r.flow_count >= 0)) return fail(h, SG_E_INVAL, "flow count must be >= 0");
         if (r.n_breakers < 0 || r.n_breakers > 2) return fail(h, SG_E_INVAL, "at most two degrade rules");
         LRule& L = tab[i];
+        L = LRule{};
         L.flow_count = r.flow_count;
         L.flow_grade = r.flow_grade;
         L.nb = r.n_breakers;
+        L.onode = kNoNode;
         for (int j = 0; j < 2; ++j) {
             LBreakerRule& b = L.b[j];
             b = LBreakerRule{};
@@ -1359,10 +1369,16 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     if (wl2 != kMinuteWl) h->l_wl[h->l_n_wl++] = kMinuteWl;
 
     dfree(h->d_lrules);
+    dfree(h->d_lfrules);
+    dfree(h->d_lctl);
     dfree(h->d_lhead);
     dfree(h->d_lsec);
     dfree(h->d_lbor);
     dfree(h->d_lmin);
+    h->l_nodes = n;
+    h->l_n_origins = 0;
+    h->l_has_cx = false;
+    h->l_rule_slot.clear();
     if (!h->d_llast_ts && hipMalloc(&h->d_llast_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "ts");
     const int64_t neg = -1;
     HIP_TRY(h, hipMemcpy(h->d_llast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
@@ -1377,6 +1393,7 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
         HIP_TRY(h, hipMemcpy(h->d_lrules, tab.data(), sizeof(LRule) * n, hipMemcpyHostToDevice));
         LArgs L{};
         L.K = n;
+        L.N = n;
         L.S = cfg->sample_count;
         L.head = h->d_lhead;
         L.sec = h->d_lsec;
@@ -1415,7 +1432,11 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     L.amask = (1ull << abits) - 1;
     L.aesc = (1ull << (abits - 3)) - 1;
     L.K = K;
+    L.N = h->l_nodes;
     L.rules = h->d_lrules;
+    L.frules = h->d_lfrules;
+    L.ctl = h->d_lctl;
+    L.n_origins = h->l_n_origins;
     L.head = h->d_lhead;
     L.sec = h->d_lsec;
     L.bor = h->d_lbor;
@@ -1478,7 +1499,7 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     sgm.rec_sorted = sorted;
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg(sgm, stream));
-    HIP_TRY(h, launch_local_walk(L, sgm, h->aux, stream, h->fork, h->join));
+    HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx, h->aux, stream, h->fork, h->join));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
@@ -1501,6 +1522,7 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     if (*h->h_err & kErrTime)
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
     if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    if (*h->h_err & kErrBounds) return fail(h, SG_E_INVAL, "an event's origin id is outside 0..n_origins");
     if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
     return SG_OK;
 }
@@ -1522,17 +1544,19 @@ int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t 
     return SG_OK;
 }
 
-int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
-    if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
+namespace {
+
+// One node's windows (resource or origin node) in the sg_local_read_state layout.
+int local_read_node(sg_handle* h, uint32_t node, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
     HIP_TRY(h, hipSetDevice(h->device));
     const int S = h->lcfg.sample_count;
     std::vector<LBucket> sb(S), mb(kMinuteS);
     std::vector<LFuture> fb(S);
     LHead hd;
-    HIP_TRY(h, hipMemcpy(sb.data(), h->d_lsec + (size_t)res * S, sizeof(LBucket) * S, hipMemcpyDeviceToHost));
-    HIP_TRY(h, hipMemcpy(fb.data(), h->d_lbor + (size_t)res * S, sizeof(LFuture) * S, hipMemcpyDeviceToHost));
-    HIP_TRY(h, hipMemcpy(mb.data(), h->d_lmin + (size_t)res * kMinuteS, sizeof(LBucket) * kMinuteS, hipMemcpyDeviceToHost));
-    HIP_TRY(h, hipMemcpy(&hd, h->d_lhead + res, sizeof(LHead), hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(sb.data(), h->d_lsec + (size_t)node * S, sizeof(LBucket) * S, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(fb.data(), h->d_lbor + (size_t)node * S, sizeof(LFuture) * S, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(mb.data(), h->d_lmin + (size_t)node * kMinuteS, sizeof(LBucket) * kMinuteS, hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(&hd, h->d_lhead + node, sizeof(LHead), hipMemcpyDeviceToHost));
     auto dump = [](const LBucket& b, int64_t* o) {
         const bool p = b.start != INT64_MIN;
         o[0] = b.start;
@@ -1557,6 +1581,242 @@ int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* bo
     }
     head[13] = 0;
     return SG_OK;
+}
+
+// FlowRuleUtil.isValidRule (:167-251) for local rules: count >= 0, grade THREAD / QPS, behaviour >= 0 with its
+// parameters (warm-up period > 0, queueing time > 0)
+bool local_flow_rule_valid(const sg_local_flow_rule& r) {
+    if (!(r.count >= 0) || r.grade < 0 || r.strategy < 0 || r.control_behavior < 0) return false;
+    if (r.grade == 0) return true;
+    if (r.grade != 1) return false;
+    switch (r.control_behavior) {
+    case SG_CONTROL_WARM_UP: return r.warm_up_period_sec > 0;
+    case SG_CONTROL_RATE_LIMITER: return r.max_queueing_ms > 0;
+    case SG_CONTROL_WARM_UP_RATE_LIMITER: return r.warm_up_period_sec > 0 && r.max_queueing_ms > 0;
+    default: return true;
+    }
+}
+
+bool local_flow_rule_same(const sg_local_flow_rule& a, const sg_local_flow_rule& b) {  // FlowRule.equals
+    return a.resource == b.resource && a.grade == b.grade && a.count == b.count &&
+           a.control_behavior == b.control_behavior && a.limit_app == b.limit_app && a.strategy == b.strategy &&
+           a.warm_up_period_sec == b.warm_up_period_sec && a.max_queueing_ms == b.max_queueing_ms;
+}
+
+int32_t d2i_host(double x) {  // (int) double
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
+// The controller constants of one flow rule (FlowRuleUtil.generateRater; WarmUpController.construct :83-106 in
+// Java int arithmetic).
+LFlowRule make_flow_rule(const sg_local_flow_rule& r, int cold) {
+    LFlowRule f{};
+    f.count = r.count;
+    f.grade = r.grade;
+    f.behavior = (r.grade == 1 && r.control_behavior >= SG_CONTROL_WARM_UP &&
+                  r.control_behavior <= SG_CONTROL_WARM_UP_RATE_LIMITER) ? r.control_behavior : SG_CONTROL_DEFAULT;
+    f.limit_app = r.limit_app;
+    f.max_queue_ms = r.max_queueing_ms;
+    f.cold = cold;
+    if (f.behavior == SG_CONTROL_WARM_UP || f.behavior == SG_CONTROL_WARM_UP_RATE_LIMITER) {
+        f.warning_token = d2i_host(r.warm_up_period_sec * r.count) / (cold - 1);
+        const int32_t two_w = (int32_t)(2u * (uint32_t)r.warm_up_period_sec);  // 2 * warmUpPeriodInSec: int
+        f.max_token = (int32_t)((uint32_t)f.warning_token + (uint32_t)d2i_host(two_w * r.count / (1.0 + cold)));
+        f.slope = (cold - 1.0) / r.count / (double)(int32_t)((uint32_t)f.max_token - (uint32_t)f.warning_token);
+    }
+    return f;
+}
+
+}  // namespace
+
+int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
+    if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
+    return local_read_node(h, res, second, borrow, minute, head);
+}
+
+int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64_t* second, int64_t* borrow,
+                               int64_t* minute, int64_t* head) {
+    if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
+    if (origin <= 0 || origin > h->l_n_origins) return fail(h, SG_E_INVAL, "origin id outside 1..n_origins");
+    const uint32_t on = h->ltab[res].onode;
+    if (on == kNoNode) return fail(h, SG_E_INVAL, "the resource has no limitApp rule, so no origin nodes");
+    return local_read_node(h, on + (uint32_t)origin - 1, second, borrow, minute, head);
+}
+
+int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3) {
+    if (!h || !state3 || rule >= h->l_rule_slot.size() || h->l_rule_slot[rule] == -1) return SG_E_INVAL;
+    const int64_t slot = h->l_rule_slot[rule];
+    if (slot == -2) {  // a DefaultController keeps no state
+        state3[0] = 0;
+        state3[1] = 0;
+        state3[2] = -1;
+        return SG_OK;
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    LCtl c;
+    HIP_TRY(h, hipMemcpy(&c, h->d_lctl + slot, sizeof(LCtl), hipMemcpyDeviceToHost));
+    state3[0] = c.stored;
+    state3[1] = c.last_filled;
+    state3[2] = c.latest;
+    return SG_OK;
+}
+
+int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins) {
+    if (!h || (!rules && n)) return SG_E_INVAL;
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    if (n_origins < 0) return fail(h, SG_E_INVAL, "n_origins < 0");
+    const uint32_t K = (uint32_t)h->ltab.size();
+    const int cold = h->lcfg.cold_factor > 1 ? h->lcfg.cold_factor : 3;
+    // FlowRuleUtil.buildFlowRuleMap (:83-130): drop invalid rules and duplicates (its HashSet), group by resource
+    std::vector<int64_t> slot(n, -1);
+    std::vector<std::vector<uint32_t>> by_res(K);
+    for (uint32_t i = 0; i < n; ++i) {
+        const sg_local_flow_rule& r = rules[i];
+        if (r.resource >= K || !local_flow_rule_valid(r)) continue;
+        if (r.strategy != SG_STRATEGY_DIRECT)
+            return fail(h, SG_E_UNSUPPORTED, "RELATE / CHAIN strategies read other resources' nodes");
+        if (r.limit_app > n_origins || r.limit_app < SG_LIMIT_APP_OTHER)
+            return fail(h, SG_E_INVAL, "limit_app names an origin id outside 1..n_origins");
+        bool dup = false;
+        for (uint32_t j : by_res[r.resource]) dup = dup || local_flow_rule_same(rules[j], r);
+        if (!dup) by_res[r.resource].push_back(i);
+    }
+    std::vector<LRule> tab = h->ltab;
+    std::vector<LFlowRule> fr;
+    uint32_t onodes = 0;
+    bool has_cx = false;
+    for (uint32_t k = 0; k < K; ++k) {
+        std::vector<uint32_t>& v = by_res[k];
+        // Collections.sort(FlowRuleComparator) (:30-55): stable, limitApp "default" last
+        std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) {
+            return (rules[x].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0) <
+                   (rules[y].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
+        });
+        LRule& L = tab[k];
+        L.fr_begin = L.fr_n = 0;
+        L.onode = kNoNode;
+        L.cx = 0;
+        L.flow_grade = -1;
+        L.flow_count = 0;
+        if (v.empty()) continue;
+        const sg_local_flow_rule& r0 = rules[v[0]];
+        if (v.size() == 1 && r0.limit_app == SG_LIMIT_APP_DEFAULT &&
+            make_flow_rule(r0, cold).behavior == SG_CONTROL_DEFAULT) {  // the fast walkers' one DefaultController rule
+            L.flow_grade = r0.grade;
+            L.flow_count = r0.count;
+            slot[v[0]] = -2;
+            continue;
+        }
+        L.cx = 1;
+        has_cx = true;
+        L.fr_begin = (uint32_t)fr.size();
+        L.fr_n = (uint32_t)v.size();
+        bool origin_rules = false;
+        for (uint32_t i : v) {
+            origin_rules = origin_rules || rules[i].limit_app != SG_LIMIT_APP_DEFAULT;
+            slot[i] = (int64_t)fr.size();
+            fr.push_back(make_flow_rule(rules[i], cold));
+        }
+        if (origin_rules && n_origins > 0) {  // ClusterNode.originCountMap: one node per origin id
+            L.onode = K + onodes;
+            onodes += (uint32_t)n_origins;
+        }
+    }
+    const uint64_t N = (uint64_t)K + onodes;
+    if (N >= SG_KEY_BAD) return fail(h, SG_E_UNSUPPORTED, "too many origin nodes");
+    tab.resize(N);
+    for (uint64_t i = K; i < N; ++i) {  // origin nodes: no rules, no breakers
+        tab[i] = LRule{};
+        tab[i].flow_grade = -1;
+        tab[i].onode = kNoNode;
+        for (int j = 0; j < 2; ++j) tab[i].b[j].stat_ms = 1;
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipDeviceSynchronize());
+    // the resources' statistics survive the load; origin nodes start empty
+    const int S = h->lcfg.sample_count;
+    LRule* d_rules = nullptr;
+    LHead* d_head = nullptr;
+    LBucket *d_sec = nullptr, *d_min = nullptr;
+    LFuture* d_bor = nullptr;
+    LFlowRule* d_fr = nullptr;
+    LCtl* d_ctl = nullptr;
+    auto release = [&]() {
+        dfree(d_rules);
+        dfree(d_head);
+        dfree(d_sec);
+        dfree(d_bor);
+        dfree(d_min);
+        dfree(d_fr);
+        dfree(d_ctl);
+    };
+    if (N && (hipMalloc(&d_rules, sizeof(LRule) * N) != hipSuccess || hipMalloc(&d_head, sizeof(LHead) * N) != hipSuccess ||
+              hipMalloc(&d_sec, sizeof(LBucket) * N * S) != hipSuccess ||
+              hipMalloc(&d_bor, sizeof(LFuture) * N * S) != hipSuccess ||
+              hipMalloc(&d_min, sizeof(LBucket) * N * kMinuteS) != hipSuccess)) {
+        release();
+        return fail(h, SG_E_NOMEM, "local node allocation");
+    }
+    if (!fr.empty() && (hipMalloc(&d_fr, sizeof(LFlowRule) * fr.size()) != hipSuccess ||
+                        hipMalloc(&d_ctl, sizeof(LCtl) * fr.size()) != hipSuccess)) {
+        release();
+        return fail(h, SG_E_NOMEM, "local flow rule allocation");
+    }
+    hipError_t e = hipSuccess;
+    if (N) {
+        LArgs L{};
+        L.K = K;
+        L.N = (uint32_t)N;
+        L.S = S;
+        L.head = d_head;
+        L.sec = d_sec;
+        L.bor = d_bor;
+        L.minute = d_min;
+        e = launch_local_init(L, 0);
+        if (e == hipSuccess) e = hipMemcpy(d_rules, tab.data(), sizeof(LRule) * N, hipMemcpyHostToDevice);
+        if (e == hipSuccess && K) {
+            e = hipMemcpy(d_head, h->d_lhead, sizeof(LHead) * K, hipMemcpyDeviceToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_sec, h->d_lsec, sizeof(LBucket) * K * S, hipMemcpyDeviceToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_bor, h->d_lbor, sizeof(LFuture) * K * S, hipMemcpyDeviceToDevice);
+            if (e == hipSuccess) e = hipMemcpy(d_min, h->d_lmin, sizeof(LBucket) * K * kMinuteS, hipMemcpyDeviceToDevice);
+        }
+    }
+    if (e == hipSuccess && !fr.empty()) {
+        e = hipMemcpy(d_fr, fr.data(), sizeof(LFlowRule) * fr.size(), hipMemcpyHostToDevice);
+        std::vector<LCtl> c(fr.size(), LCtl{0, 0, -1, 0});  // storedTokens 0, lastFilledTime 0, latestPassedTime -1
+        if (e == hipSuccess) e = hipMemcpy(d_ctl, c.data(), sizeof(LCtl) * c.size(), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        release();
+        return fail(h, SG_E_DEVICE, std::string("local flow rule upload: ") + hipGetErrorString(e));
+    }
+    dfree(h->d_lrules);
+    dfree(h->d_lhead);
+    dfree(h->d_lsec);
+    dfree(h->d_lbor);
+    dfree(h->d_lmin);
+    dfree(h->d_lfrules);
+    dfree(h->d_lctl);
+    h->d_lrules = d_rules;
+    h->d_lhead = d_head;
+    h->d_lsec = d_sec;
+    h->d_lbor = d_bor;
+    h->d_lmin = d_min;
+    h->d_lfrules = d_fr;
+    h->d_lctl = d_ctl;
+    tab.resize(K);
+    h->ltab = tab;
+    h->l_nodes = (uint32_t)N;
+    h->l_n_origins = n_origins;
+    h->l_has_cx = has_cx;
+    h->l_rule_slot = slot;
+    int kept = 0;
+    for (int64_t x : slot) kept += x != -1;
+    return kept;
 }
 
 int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {

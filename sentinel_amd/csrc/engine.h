@@ -307,9 +307,30 @@ struct LBreakerRule {
 
 struct alignas(16) LRule {
     double flow_count;
-    int32_t flow_grade;       // 0 thread, 1 QPS, -1 no flow rule
+    int32_t flow_grade;       // 0 thread, 1 QPS, -1 no flow rule (the fast walkers' one DefaultController rule)
     int32_t nb;               // breakers 0..2
     LBreakerRule b[2];
+    uint32_t fr_begin, fr_n;  // cx: the resource's flow rules frules[fr_begin .. + fr_n) in check order
+    uint32_t onode;           // node index of origin 1 (origin o: onode + o - 1); kNoNode without origin nodes
+    int32_t cx;               // 1: walked by k_lwalk_cx (several rules, limitApps or shaping controllers)
+};
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// A flow rule of the local chain with its controller's constants (FlowRuleUtil.generateRater, WarmUpController
+// .construct :83-106).
+struct alignas(16) LFlowRule {
+    double count;
+    double slope;
+    int32_t grade;            // 0 thread, 1 QPS
+    int32_t behavior;         // SG_CONTROL_* actually used (THREAD rules: DEFAULT)
+    int32_t limit_app;        // SG_LIMIT_APP_DEFAULT / _OTHER / origin id
+    int32_t max_queue_ms;
+    int32_t warning_token, max_token, cold;
+    int32_t pad;
+};
+
+struct alignas(32) LCtl {     // the controller's state: storedTokens, lastFilledTime, latestPassedTime
+    int64_t stored, last_filled, latest, pad;
 };
 
 struct LArgs {
@@ -320,8 +341,12 @@ struct LArgs {
     uint64_t* rec_sorted;
     int kshift, abits;
     uint64_t imask, amask, aesc;
-    uint32_t K;
-    const LRule* rules;
+    uint32_t K;               // resources (record keys)
+    uint32_t N;               // nodes: the K resources, then the origin nodes
+    const LRule* rules;       // [N] (origin nodes: no rules, no breakers)
+    const LFlowRule* frules;  // flow rules of the cx resources
+    LCtl* ctl;                // [frules] controller state
+    int32_t n_origins;
     LHead* head;              // [K]
     LBucket* sec;             // [K][S]   second window (OccupiableBucketLeapArray)
     LFuture* bor;             // [K][S]   its borrow array
@@ -356,7 +381,7 @@ struct LSkip {                   // entries [b0, b1) of resource k, all FLOW-blo
 };
 
 hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
-hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, hipStream_t aux, hipStream_t stream,
+hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
 

@@ -146,6 +146,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
             }
         }
         const uint32_t res = e.resource & SG_KEY_INDEX;
+        if (e.origin < 0 || e.origin > a.n_origins) atomicOr(a.err, kErrBounds);
         uint64_t rec = sentinel;
         if (res < a.K) {
             uint64_t c = (e.count < 0) ? a.aesc : (uint64_t)(uint32_t)e.count;
@@ -165,7 +166,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_local_init(LArgs a) {
-    const uint64_t total = (uint64_t)a.K * kMinuteS;
+    const uint64_t total = (uint64_t)a.N * kMinuteS;  // resources and origin nodes
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         LBucket b;
         b.start = INT64_MIN;
@@ -419,6 +420,48 @@ struct LNode {
         if (cb_trips(j, cb[j].bad, cb[j].total)) cb_to_open(j, t);
     }
 
+    // DegradeSlot.performChecking: AbstractCircuitBreaker.tryPass (:73-84) in rule order; the loops are fully
+    // unrolled so the breaker state stays in registers. ts() yields the entry's time (read only when needed).
+    template <class TS>
+    __device__ __forceinline__ bool degrade_blocks(TS&& ts) {
+        bool blocked = false, half0 = false, half1 = false;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (j >= R.nb || blocked) continue;
+            if (cb[j].state == kCbClosed) continue;
+            if (cb[j].state == kCbOpen && ts() >= cb[j].next_retry) {
+                cb[j].state = kCbHalfOpen;
+                if (j == 0) half0 = true;
+                else half1 = true;
+            } else {
+                blocked = true;
+            }
+        }
+        if (blocked) {  // DegradeException; whenTerminate of a blocked probe: back to OPEN
+            if (half0 && cb[0].state == kCbHalfOpen) cb[0].state = kCbOpen;
+            if (half1 && cb[1].state == kCbHalfOpen) cb[1].state = kCbOpen;
+        }
+        return blocked;
+    }
+
+    // StatisticNode.previousPassQps at t: the minute window's previous bucket (ArrayMetric.previousWindowPass,
+    // LeapArray.getPreviousWindow :210-227; t < 1000 reads as null, see the oracle)
+    __device__ int64_t prev_pass(int64_t t) const {
+        if (t < kMinuteWl) return 0;
+        const int idx = (int)(((t - kMinuteWl) / kMinuteWl) % kMinuteS);
+        int64_t st, pass;
+        if (idx == mI) {
+            st = m_ws;
+            pass = mc[kLPass];
+        } else {
+            st = mnt[idx].start;
+            pass = mnt[idx].c[kLPass];
+        }
+        if (st == INT64_MIN || t - st > (int64_t)kMinuteS * kMinuteWl) return 0;
+        if (st + kMinuteWl < t - kMinuteWl) return 0;
+        return pass;
+    }
+
     // -------- one event, sequentially (the oracle's or_local_decide step) --------
     // Entry: FlowSlot (DefaultController.canPass) → DegradeSlot.performChecking → StatisticSlot.
     // t: the entry's timestamp, or INT64_MIN when not loaded yet (read only on the paths that need it:
@@ -447,28 +490,7 @@ struct LNode {
                 }
             }
         }
-        if (status == SG_LOCAL_PASS) {
-            // AbstractCircuitBreaker.tryPass (:73-84) in rule order; the loops are fully unrolled so the
-            // breaker state stays in registers
-            bool blocked = false, half0 = false, half1 = false;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                if (j >= R.nb || blocked) continue;
-                if (cb[j].state == kCbClosed) continue;
-                if (cb[j].state == kCbOpen && ts() >= cb[j].next_retry) {
-                    cb[j].state = kCbHalfOpen;
-                    if (j == 0) half0 = true;
-                    else half1 = true;
-                } else {
-                    blocked = true;
-                }
-            }
-            if (blocked) {  // DegradeException; whenTerminate of a blocked probe: back to OPEN
-                status = SG_LOCAL_BLOCK_DEGRADE;
-                if (half0 && cb[0].state == kCbHalfOpen) cb[0].state = kCbOpen;
-                if (half1 && cb[1].state == kCbHalfOpen) cb[1].state = kCbOpen;
-            }
-        }
+        if (status == SG_LOCAL_PASS && degrade_blocks(ts)) status = SG_LOCAL_BLOCK_DEGRADE;
         if (status == SG_LOCAL_PASS) {
             threads += 1;
             sc[kLPass] += e.count;
@@ -569,6 +591,7 @@ __global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
         if (i >= cnt[c]) continue;
         const uint64_t j = sg.short_list[sg.class_off[c] + i];
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+        if (a.rules[k].cx) continue;  // k_lwalk_cx
         LNode nd(a, bndp, k);
         // software pipeline: records kRecAhead ahead, exit timestamps kEvAhead ahead (a lane walks up to
         // short_max contiguous records; one load in flight per record would leave it latency-bound)
@@ -910,10 +933,236 @@ __global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
     for (uint32_t item = wave; item < n_long; item += nwaves) {
         const uint64_t s = sg.long_list[item];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+        if (a.rules[k].cx) continue;  // k_lwalk_cx
         const uint64_t e = lwave_search(s + 1, a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
         lwalk_wave(a, bndp, k, s, e);
+    }
+}
+
+// ------------------------------------------------------------------------ the flow-rule layer (cx)
+//
+// Resources whose flow rules are more than the fast walkers' one DefaultController rule with limitApp
+// "default" — several rules (FlowRuleChecker.checkFlow, FlowRuleChecker.java:44-57: in FlowRuleComparator
+// order, the first failing rule throws), limitApp origin / "other" rules reading the origin's StatisticNode
+// (selectNodeByRequesterAndStrategy :115-145), WarmUp / RateLimiter / WarmUpRateLimiter controllers — are
+// walked one event at a time, one lane per resource segment, by k_lwalk_cx. The resource's ClusterNode stays
+// in registers (LNode); an origin node is opened from memory for the event that needs it.
+
+namespace {
+
+__device__ __forceinline__ int64_t java_d2l(double x) {  // JLS §5.1.3
+    if (x != x) return 0;
+    if (x >= 9223372036854775807.0) return INT64_MAX;
+    if (x <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)x;
+}
+
+__device__ __forceinline__ int64_t java_round(double a) {  // Math.round(double), floor(a + 1/2) on the bits
+    const int64_t bits = __double_as_longlong(a);
+    const int64_t shift = (52 - 1 + 1023) - ((bits & 0x7FF0000000000000LL) >> 52);
+    if ((shift & -64) == 0) {
+        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
+        if (bits < 0) r = -r;
+        return ((r >> shift) + 1) >> 1;
+    }
+    return java_d2l(a);
+}
+
+// WarmUpController.coolDownTokens (WarmUpController.java:161-175)
+__device__ int64_t warm_cool_down(const LFlowRule& r, const LCtl& c, int64_t ct, int64_t pass_qps) {
+    const int64_t old = c.stored;
+    int64_t nv = old;
+    if (old < r.warning_token || (old > r.warning_token && pass_qps < java_d2i(r.count) / r.cold))
+        nv = java_d2l((double)old + (double)(ct - c.last_filled) * r.count / 1000);
+    return nv < r.max_token ? nv : (int64_t)r.max_token;
+}
+
+// WarmUpController.syncToken (:140-159)
+__device__ void warm_sync(const LFlowRule& r, LCtl& c, int64_t now, int64_t pass_qps) {
+    const int64_t ct = now - now % 1000;
+    if (ct <= c.last_filled) return;
+    const int64_t cur = (int64_t)((uint64_t)warm_cool_down(r, c, ct, pass_qps) - (uint64_t)pass_qps);
+    c.stored = cur < 0 ? 0 : cur;
+    c.last_filled = ct;
+}
+
+__device__ __forceinline__ double warm_qps(const LFlowRule& r, int64_t above) {  // Math.nextUp(1 / (…))
+    return nextafter(1.0 / ((double)above * r.slope + 1.0 / r.count), (double)INFINITY);
+}
+
+// RateLimiterController.canPass (:46-91) / the tail of WarmUpRateLimiterController.canPass (:61-86) with the
+// cost already known; *wait = the sleep. The acquire/count checks only exist in RateLimiterController.
+__device__ bool pace_step(const LFlowRule& r, LCtl& c, int64_t now, int64_t cost, int64_t* wait) {
+    *wait = 0;
+    if (cost + c.latest <= now) {
+        c.latest = now;
+        return true;
+    }
+    if (cost + c.latest - now > r.max_queue_ms) return false;
+    c.latest += cost;
+    const int64_t w = c.latest - now;
+    if (w > r.max_queue_ms) {  // unreachable without concurrent callers
+        c.latest -= cost;
+        return false;
+    }
+    *wait = w > 0 ? w : 0;
+    return true;
+}
+
+// FlowRuleChecker.selectNodeByRequesterAndStrategy (DIRECT): 0 the ClusterNode, 1 the origin node, -1 none
+__device__ int cx_select(const LArgs& a, const LRule& R, int32_t limit_app, int origin) {
+    if (origin > 0 && limit_app == origin) return 1;
+    if (limit_app == SG_LIMIT_APP_DEFAULT) return 0;
+    if (limit_app == SG_LIMIT_APP_OTHER && origin > 0) {  // FlowRuleManager.isOtherOrigin (:132-148)
+        for (uint32_t i = 0; i < R.fr_n; ++i)
+            if (a.frules[R.fr_begin + i].limit_app == origin) return -1;
+        return 1;
+    }
+    return -1;
+}
+
+// One rule's canPass on the selected node: 0 block, 1 pass (*wait: the controller's sleep), 2 PriorityWaitException
+__device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, const LEvent& e, int64_t t,
+                       int64_t* wait) {
+    *wait = 0;
+    switch (r.behavior) {
+    case SG_CONTROL_WARM_UP: {  // WarmUpController.canPass (:113-138)
+        const int64_t pass_qps = java_d2l(n.pass_qps());
+        warm_sync(r, c, t, java_d2l((double)n.prev_pass(t)));
+        const int64_t sum = (int64_t)((uint64_t)pass_qps + (uint64_t)(int64_t)e.count);
+        const double lim = c.stored >= r.warning_token ? warm_qps(r, c.stored - r.warning_token) : r.count;
+        return (double)sum <= lim ? 1 : 0;
+    }
+    case SG_CONTROL_RATE_LIMITER:
+        if (e.count <= 0) return 1;
+        if (r.count <= 0) return 0;
+        return pace_step(r, c, t, java_round(1.0 * (double)e.count / r.count * 1000), wait) ? 1 : 0;
+    case SG_CONTROL_WARM_UP_RATE_LIMITER: {  // WarmUpRateLimiterController.canPass (:43-87)
+        warm_sync(r, c, t, java_d2l((double)n.prev_pass(t)));
+        const double q = c.stored >= r.warning_token ? warm_qps(r, c.stored - r.warning_token) : r.count;
+        return pace_step(r, c, t, java_round(1.0 * (double)e.count / q * 1000), wait) ? 1 : 0;
+    }
+    default: {  // DefaultController.canPass (:49-76)
+        const int32_t cur = r.grade == 0 ? (int32_t)n.threads : java_d2i(n.pass_qps());
+        if (!((double)(int32_t)((uint32_t)cur + (uint32_t)e.count) > r.count)) return 1;
+        if (e.prio && r.grade == 1) {
+            const int64_t w = n.try_occupy_next(t, e.count, r.count);
+            if (w < a.occupy_timeout) {
+                const int s = n.bor_window(t + w);  // addWaitingRequest
+                if (s >= 0) n.bor[s].pass += e.count;
+                n.mc[kLOccPass] += e.count;         // addOccupiedPass: the minute window
+                n.mc[kLPass] += e.count;
+                *wait = w;
+                return 2;
+            }
+        }
+        return 0;
+    }
+    }
+}
+
+// One entry of a cx resource: FlowSlot (every rule) → DegradeSlot → StatisticSlot on the ClusterNode and the
+// origin node (StatisticSlot.java:55-122).
+__device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, uint32_t on_idx, const LEvent& e,
+                         int64_t t, int origin, uint32_t qs, uint32_t qm) {
+    const bool have_on = on_idx != kNoNode;
+    LNode on(a, bndp, have_on ? on_idx : nd.k);
+    if (have_on) on.at(qs, qm);
+    int32_t status = SG_LOCAL_PASS;
+    int64_t wait = 0;
+    const LRule& R = nd.R;
+    for (uint32_t i = 0; i < R.fr_n; ++i) {
+        const LFlowRule r = a.frules[R.fr_begin + i];
+        const int sel = cx_select(a, R, r.limit_app, origin);
+        if (sel < 0 || (sel == 1 && !have_on)) continue;
+        LCtl& c = a.ctl[R.fr_begin + i];
+        int64_t w = 0;
+        const int v = sel == 0 ? cx_rule(a, nd, r, c, e, t, &w) : cx_rule(a, on, r, c, e, t, &w);
+        if (v == 0) {
+            status = SG_LOCAL_BLOCK_FLOW;
+            break;
+        }
+        if (v == 2) {
+            status = SG_LOCAL_PASS_WAIT;
+            wait = w;
+            break;
+        }
+        wait += w;  // each rate limiter sleeps in turn
+    }
+    if (status == SG_LOCAL_PASS && nd.degrade_blocks([&]() { return t; })) status = SG_LOCAL_BLOCK_DEGRADE;
+    if (status == SG_LOCAL_PASS) {
+        nd.threads += 1;
+        nd.sc[kLPass] += e.count;
+        nd.mc[kLPass] += e.count;
+        if (have_on) {
+            on.threads += 1;
+            on.sc[kLPass] += e.count;
+            on.mc[kLPass] += e.count;
+        }
+    } else if (status == SG_LOCAL_PASS_WAIT) {
+        nd.threads += 1;
+        if (have_on) on.threads += 1;
+    } else {
+        nd.sc[kLBlock] += e.count;
+        nd.mc[kLBlock] += e.count;
+        if (have_on) {
+            on.sc[kLBlock] += e.count;
+            on.mc[kLBlock] += e.count;
+        }
+        wait = 0;
+    }
+    lstore(a, e.idx, status, wait > INT32_MAX ? INT32_MAX : (int32_t)wait);
+    if (have_on) on.finish();
+}
+
+}  // namespace
+
+// One lane per segment of a cx resource, from every length class of k_seg's lists.
+__global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_lperiods(a, sbnd, bndp);
+    uint32_t total = *sg.long_count;
+    for (int c = 0; c < kClasses; ++c) total += sg.short_count[c];
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+        uint32_t r = i;
+        uint64_t j;
+        if (r < *sg.long_count) {
+            j = sg.long_list[r];
+        } else {
+            r -= *sg.long_count;
+            int c = 0;
+            while (r >= sg.short_count[c]) r -= sg.short_count[c++];
+            j = sg.short_list[sg.class_off[c] + r];
+        }
+        const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+        if (!a.rules[k].cx) continue;
+        LNode nd(a, bndp, k);
+        for (uint64_t p = j; p < a.n; ++p) {
+            const uint64_t rec = a.rec_sorted[p];
+            if ((uint32_t)(rec >> a.kshift) != k) break;
+            const LEvent e = ldecode(a, rec);
+            const sg_local_event le = a.ev[e.idx];
+            const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
+            nd.at(qs, qm);
+            const uint32_t on_idx = (nd.R.onode != kNoNode && le.origin > 0) ? nd.R.onode + (uint32_t)le.origin - 1
+                                                                              : kNoNode;
+            if (e.kind == SG_LOCAL_ENTRY) {
+                cx_entry(a, bndp, nd, on_idx, e, le.ts_ms, le.origin, qs, qm);
+            } else {
+                nd.exit(e, le.ts_ms, le.create_ts);
+                if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
+                    LNode on(a, bndp, on_idx);
+                    on.at(qs, qm);
+                    on.exit(e, le.ts_ms, le.create_ts);
+                    on.finish();
+                }
+            }
+        }
+        nd.finish();
     }
 }
 
@@ -1037,8 +1286,8 @@ hipError_t launch_local_init(const LArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, hipStream_t aux, hipStream_t stream, hipEvent_t fork,
-                             hipEvent_t join) {
+hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, bool has_cx, hipStream_t aux, hipStream_t stream,
+                             hipEvent_t fork, hipEvent_t join) {
     static unsigned bl = 0, bs = 0;
     if (bl == 0) bl = lresident((const void*)k_lwalk_long);
     if (bs == 0) bs = lresident((const void*)k_lwalk_short);
@@ -1051,6 +1300,7 @@ hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, hipStream_t au
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
     hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
+    if (has_cx) hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, stream, a, sg);
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
     if (e != hipSuccess) return e;

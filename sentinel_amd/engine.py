@@ -18,6 +18,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
+           "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
 
@@ -69,6 +70,9 @@ def load_library():
         "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
+        "sg_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32]),
+        "sg_local_read_origin_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
+        "sg_local_read_controller": (C.c_int, [vp, u32, vp]),
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "sg_codec_encode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
         "sg_pace_load_rules": (C.c_int, [vp, vp, u32]),
@@ -243,10 +247,11 @@ class FlowEngine:
         return out.reshape(n_rules, 2)
 
     # ---- local slot chain (StatisticSlot → FlowSlot/DefaultController → DegradeSlot)
-    def local_load_rules(self, rules: np.ndarray, sample_count=2, interval_ms=1000, occupy_timeout_ms=500):
+    def local_load_rules(self, rules: np.ndarray, sample_count=2, interval_ms=1000, occupy_timeout_ms=500,
+                         cold_factor=3):
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
         cfg = abi.sg_local_config(sample_count=sample_count, interval_ms=interval_ms,
-                                  occupy_timeout_ms=occupy_timeout_ms, reserved=0)
+                                  occupy_timeout_ms=occupy_timeout_ms, cold_factor=cold_factor)
         self._check(self._L.sg_local_load_rules(self.h, C.byref(cfg), abi.ptr(rules), len(rules)))
         self.local_S = sample_count
 
@@ -269,6 +274,29 @@ class FlowEngine:
         head = np.zeros(14, np.int64)
         self._check(self._L.sg_local_read_state(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), abi.ptr(head)))
         return sec, bor, mnt, head
+
+    def local_load_flow_rules(self, rules: np.ndarray, n_origins=0) -> int:
+        """FlowRuleManager.loadRules for the local chain: returns the number of rules kept."""
+        rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
+        rc = self._L.sg_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins)
+        self._check(min(rc, 0))
+        return rc
+
+    def local_origin_state(self, res, origin):
+        S = self.local_S
+        sec = np.zeros((S, 8), np.int64)
+        bor = np.zeros((S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        head = np.zeros(14, np.int64)
+        self._check(self._L.sg_local_read_origin_state(self.h, res, origin, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt),
+                                                       abi.ptr(head)))
+        return sec, bor, mnt, head
+
+    def local_controller(self, rule):
+        """{storedTokens, lastFilledTime, latestPassedTime} of input flow rule `rule`."""
+        out = np.zeros(3, np.int64)
+        self._check(self._L.sg_local_read_controller(self.h, rule, abi.ptr(out)))
+        return out
 
     # ---- cluster hot-parameter tokens (requestParamToken → ClusterParamFlowChecker)
     def cparam_load_rules(self, rules: np.ndarray, hot: np.ndarray = None, capacity_log2=0):

@@ -1,0 +1,214 @@
+"""Known-answer tests of the local chain's flow-rule layer in the oracle: several rules per resource,
+limitApp node selection, rule order and the warm-up / rate-limiter controllers. Each restates a test the
+reference holds:
+
+  WarmUpControllerTest.testWarmUp            sentinel-core/src/test/.../flow/controller/WarmUpControllerTest.java:33-63
+  WarmUpRateLimiterControllerTest.{testPace, testPaceCanNotPass}   …/controller/WarmUpRateLimiterControllerTest.java:33-66
+  FlowRuleCheckerTest (limitApp selection)   sentinel-core/src/test/.../flow/FlowRuleCheckerTest.java:40-175
+  FlowRuleComparatorTest.testFlowRuleComparator                    …/flow/FlowRuleComparatorTest.java:33-52
+  FlowPartialIntegrationTest.{testQPSGrade, testThreadGrade, testOriginFlowRule, testFlowRule_other, testStrategy}
+                                             sentinel-core/src/test/.../flow/FlowPartialIntegrationTest.java:48-215
+
+The controller tests mock the node (passQps / previousPassQps) and the clock (AbstractTimeBasedTest, or real
+sleeps for testPace): here the controller is driven with explicit values and an explicit clock that advances by
+the sleep canPass asks for. Origins are dense ids (appA = 1, appB = 2, …).
+"""
+import numpy as np
+import pytest
+
+from oracle.binding import Controller, LocalChain, local_flow_rule, local_rule, select_node
+from sentinel_amd import abi
+
+T0S = [1_700_000_000_000, 1_700_000_000_437, 1_650_000_123_999, 86_400_000 * 365 + 17]
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_warm_up_controller(t0):
+    c = Controller(10, 10, 3)
+    assert (c.warning_token, c.max_token) == (50, 100)
+    t = t0
+    assert not c.warm_can_pass(t, 8, 1)          # passQps 8, previousPassQps 1
+    assert c.warm_can_pass(t, 1, 1)
+    for _ in range(100):                          # previousPassQps 10, 100 x sleep(100)
+        t += 100
+        c.warm_can_pass(t, 1, 10)
+    assert c.warm_can_pass(t, 8, 10)
+    assert not c.warm_can_pass(t, 10, 10)
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_warm_up_rate_limiter_pace(t0):
+    c = Controller(10, 10, 3, behavior=abi.CONTROL_WARM_UP_RATE_LIMITER, max_queueing_ms=1000)
+    t = t0
+    ok, w = c.warm_rl_can_pass(t, 100)
+    assert ok
+    t += w
+    start = t
+    for _ in range(10):
+        ok, w = c.warm_rl_can_pass(t, 100)
+        assert ok
+        t += w                                   # Thread.sleep(waitTime) inside canPass
+    cost = (t - start) / 10
+    assert abs(cost - 100) < 10
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_warm_up_rate_limiter_cannot_pass(t0):
+    c = Controller(10, 10, 3, behavior=abi.CONTROL_WARM_UP_RATE_LIMITER, max_queueing_ms=10)
+    assert c.warm_rl_can_pass(t0, 100)[0]
+    assert not c.warm_rl_can_pass(t0, 100)[0]
+
+
+def test_warm_up_token_arithmetic():
+    """The constructor's int arithmetic and the cold-factor branch of coolDownTokens (:161-175)."""
+    c = Controller(7.5, 3, 4)
+    assert c.warning_token == int(3 * 7.5) // 3
+    assert c.max_token == c.warning_token + int(2 * 3 * 7.5 / 5.0)
+    t = 1_700_000_000_000
+    c.warm_can_pass(t, 0, 0)                     # first sync fills to maxToken
+    assert c.state()[0] == c.max_token and c.state()[1] == t
+    c.warm_can_pass(t + 1000, 0, 1)              # stored > warning and not (1 < (int)7.5 / 4): no refill, - 1
+    assert c.state()[0] == c.max_token - 1
+
+
+def test_select_node_default():
+    rules = np.array([local_flow_rule(count=1)])
+    assert select_node(rules, 0, 0) == 0
+    assert select_node(rules, 0, 3) == 0
+
+
+def test_select_node_custom_origin():
+    appA, appB = 1, 2
+    rules = np.array([local_flow_rule(count=1, limit_app=appA)])
+    assert select_node(rules, 0, appA) == 1      # origin matches: the origin node
+    rules = np.array([local_flow_rule(count=1, limit_app=appB)])
+    assert select_node(rules, 0, appA) is None   # mismatch: no node
+
+
+def test_select_node_other_origin():
+    appA, appB = 1, 2
+    rules = np.array([local_flow_rule(count=1, limit_app=appA), local_flow_rule(count=2, limit_app=abi.LIMIT_APP_OTHER)])
+    assert select_node(rules, 1, appB) == 1      # appB is "other"
+    assert select_node(rules, 1, appA) is None   # appA has its own rule
+    assert select_node(rules, 1, 0) is None      # no origin: isOtherOrigin("") is false
+
+
+def test_pass_check_select_empty_node_success():
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule()]))
+    abc, defo = 1, 2
+    assert ch.load_flow_rules(np.array([local_flow_rule(count=1, limit_app=abc)]), n_origins=2) == 1
+    t = 1_700_000_000_000
+    for i in range(5):
+        assert ch.entry(t + i, origin=defo)[0] == abi.LOCAL_PASS
+
+
+def test_reference_strategies_are_refused():
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule()]))
+    with pytest.raises(ValueError):
+        ch.load_flow_rules(np.array([local_flow_rule(count=1, strategy=abi.STRATEGY_RELATE)]))
+
+
+def test_flow_rule_comparator_order():
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule()]))
+    A = local_flow_rule(count=10)
+    B = local_flow_rule(limit_app=1)
+    C_ = local_flow_rule(limit_app=2)
+    D = local_flow_rule(limit_app=abi.LIMIT_APP_OTHER)
+    E = local_flow_rule(count=20)
+    assert ch.load_flow_rules(np.array([A, B, C_, D, E]), n_origins=2) == 5
+    assert ch.rule_order(0) == [1, 2, 3, 0, 4]   # B, C, D, A, E
+
+
+def test_invalid_and_duplicate_rules_are_ignored():
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule(), local_rule()]))
+    rules = np.array([local_flow_rule(count=-1),                                       # count < 0
+                      local_flow_rule(count=5, behavior=abi.CONTROL_WARM_UP, warm_up_sec=0),
+                      local_flow_rule(count=5, behavior=abi.CONTROL_RATE_LIMITER, max_queueing_ms=0),
+                      local_flow_rule(count=5),
+                      local_flow_rule(count=5),                                        # duplicate (HashSet)
+                      local_flow_rule(resource=1, count=3, grade=abi.FLOW_GRADE_THREAD, behavior=7)])
+    assert ch.load_flow_rules(rules) == 2
+    assert ch.rule_order(0) == [3] and ch.rule_order(1) == [5]
+    assert ch.controller(0) is None and ch.controller(4) is None
+
+
+def _chain(rules, n_res=1, n_origins=0):
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule() for _ in range(n_res)]))
+    ch.load_flow_rules(np.array(rules), n_origins=n_origins)
+    return ch
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_qps_grade(t0):
+    ch = _chain([local_flow_rule(count=1)])
+    assert ch.entry(t0)[0] == abi.LOCAL_PASS
+    ch.exit(t0, t0)
+    assert ch.entry(t0)[0] == abi.LOCAL_BLOCK_FLOW
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_thread_grade(t0):
+    ch = _chain([local_flow_rule(count=1, grade=abi.FLOW_GRADE_THREAD)])
+    assert ch.entry(t0)[0] == abi.LOCAL_PASS         # the other thread holds its entry for 100 ms
+    assert ch.entry(t0 + 1)[0] == abi.LOCAL_BLOCK_FLOW
+    ch.exit(t0 + 100, t0)
+    assert ch.entry(t0 + 101)[0] == abi.LOCAL_PASS
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_origin_flow_rule(t0):
+    app1, app2 = 1, 2
+    ch = _chain([local_flow_rule(count=0, limit_app=abi.LIMIT_APP_OTHER), local_flow_rule(count=1, limit_app=app2)],
+                n_origins=2)
+    assert ch.entry(t0, origin=app1)[0] == abi.LOCAL_BLOCK_FLOW
+    assert ch.entry(t0, origin=app2)[0] == abi.LOCAL_PASS
+    ch.exit(t0, t0, origin=app2)
+    # the origin nodes saw their own traffic: app1 one block, app2 one pass and its exit
+    s1 = ch.origin_dump(0, app1)
+    s2 = ch.origin_dump(0, app2)
+    assert s1[4] and s2[4]
+    assert s1[0][:, 2].sum() == 1 and s1[0][:, 1].sum() == 0
+    assert s2[0][:, 1].sum() == 1 and s2[0][:, 4].sum() == 1 and s2[3] == 0
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_other_without_origin(t0):
+    ch = _chain([local_flow_rule(count=0, limit_app=abi.LIMIT_APP_OTHER)])
+    assert ch.entry(t0)[0] == abi.LOCAL_PASS          # no origin: the "other" rule selects no node
+    ch.exit(t0, t0)
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_strategy_direct(t0):
+    ch = _chain([local_flow_rule(count=0)])
+    assert ch.entry(t0)[0] == abi.LOCAL_BLOCK_FLOW
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_chain_rate_limiter_records_statistics(t0):
+    """A RATE_LIMITER rule inside the chain: its passes (after the returned sleep) reach the StatisticNode."""
+    ch = _chain([local_flow_rule(count=10, behavior=abi.CONTROL_RATE_LIMITER, max_queueing_ms=250)])
+    waits = [ch.entry(t0)[1] for _ in range(4)]
+    assert waits == [0, 100, 200, 0] or waits[:3] == [0, 100, 200]
+    st = [ch.entry(t0)[0] for _ in range(2)]
+    assert st == [abi.LOCAL_BLOCK_FLOW] * 2
+    assert ch.second_sum(0, t0, 0) == 3 and ch.second_sum(0, t0, 1) == 3 and ch.threads(0) == 3
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_chain_two_rules_first_failure_wins(t0):
+    """A rate limiter before a default rule: the limiter's latestPassedTime moves even when the next rule
+    blocks (each rule's canPass runs in order until one fails)."""
+    ch = _chain([local_flow_rule(count=1, limit_app=1),
+                 local_flow_rule(count=1000, behavior=abi.CONTROL_RATE_LIMITER, max_queueing_ms=500)], n_origins=1)
+    assert ch.rule_order(0) == [0, 1]
+    assert ch.entry(t0, origin=1) == (abi.LOCAL_PASS, 0)
+    assert ch.entry(t0 + 5, origin=1)[0] == abi.LOCAL_BLOCK_FLOW   # the origin rule (count 1) blocks first
+    assert ch.controller(1)[2] == t0                                  # the limiter did not run
+    assert ch.entry(t0 + 5)[0] == abi.LOCAL_PASS                      # no origin: only the limiter
+    assert ch.controller(1)[2] == t0 + 5
