@@ -298,6 +298,13 @@ void        sg_destroy(sg_handle* h);
 const char* sg_last_error(const sg_handle* h);
 
 int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n);
+
+/* Marks the handle as one of `world` shards of a node's flowIds (flowIds hashed over the GPUs,
+ * no collective on the decision path). GlobalRequestLimiter's per-namespace QPS limiter counts every request of
+ * the namespace in node order (GlobalRequestLimiter.java:46-55, ClusterFlowChecker.allowProceed :45-51), which a
+ * shard does not see: with world > 1, limiter-enabled namespaces are SG_E_UNSUPPORTED (in either call order) and
+ * the Java shim keeps such namespaces on one GPU. */
+int sg_set_shard(sg_handle* h, int32_t rank, int32_t world);
 int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n);
 
 /* Decide a batch. req/out are DEVICE pointers (HBM-resident); stream is a hipStream_t (NULL = default).
@@ -306,6 +313,20 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
 
 /* Same with HOST buffers (H2D + D2H included; synchronous). */
 int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out);
+
+/* Asynchronous host pipeline — what a token server's request loop calls: sg_flow_submit
+ * enqueues H2D of req, the decision pipeline and D2H into out, and returns at once with a ticket; up to 3
+ * batches are in flight (H2D of batch i+1 and D2H of batch i-1 overlap the compute of batch i; compute runs in
+ * submission order, so batches must still be time-ordered). A 4th submit first completes the oldest batch.
+ * req/out are HOST memory and must stay untouched until the ticket completes; allocate them with sg_host_alloc
+ * (pinned) for the copies to run asynchronously. sg_flow_poll: 1 done and OK, 0 still running, < 0 that batch's
+ * error (the batch was rejected, as sg_flow_decide_batch would); sg_flow_wait blocks and returns SG_OK or that
+ * error. Every other call on the handle first completes the batches in flight. Ticket 0 (empty batch) is done. */
+int   sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket);
+int   sg_flow_poll(sg_handle* h, uint64_t ticket);
+int   sg_flow_wait(sg_handle* h, uint64_t ticket);
+void* sg_host_alloc(sg_handle* h, uint64_t bytes);   /* pinned (page-locked) host memory, NULL on failure */
+void  sg_host_free(sg_handle* h, void* p);
 
 /* Opt-in per-call timing (adds HIP events; off by default). */
 int sg_enable_stats(sg_handle* h, int on);

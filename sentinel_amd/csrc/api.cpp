@@ -16,6 +16,8 @@
 
 using namespace sg;
 
+constexpr int kAsyncSlots = 3;  // batches of one handle in flight on the host pipeline
+
 struct sg_handle {
     int device = 0;
     sg_config cfg{};
@@ -136,6 +138,19 @@ struct sg_handle {
     sg_local_result* d_lout_h = nullptr;
 
     int kbits = 0, ibits = 0, abits = 0;
+    int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
+    // asynchronous host pipeline (sg_flow_submit): H2D / compute / D2H streams, kAsyncSlots batches in flight
+    struct Slot {
+        uint64_t ticket = 0;            // 0 = free
+        sg_req* d_req = nullptr;
+        sg_result* d_out = nullptr;
+        int* h_err = nullptr;           // pinned: the batch's error flags
+        hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    };
+    Slot slots[kAsyncSlots];
+    hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
+    uint64_t next_ticket = 1;
+    std::unordered_map<uint64_t, int> finished;  // tickets completed while making room, not yet collected
     bool stats_on = false;
     uint32_t short_max = kShortMax;   // default walker split (env SG_SHORT_MAX overrides, for tuning)
     int dbg = 0;                      // env SG_DEBUG: see BatchArgs::dbg
@@ -145,6 +160,10 @@ struct sg_handle {
     hipStream_t aux = nullptr;        // second stream: the long-segment walker runs beside the short one
     hipEvent_t fork = nullptr, join = nullptr;
 };
+
+namespace {
+int drain_async(sg_handle* h);  // below: completes the handle's in-flight host-pipeline batches
+}
 
 extern "C" {
 static int upload_fid_table(sg_handle* h);  // flowId → rule index for the wire codec (defined below)
@@ -414,6 +433,16 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lout_h);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
+    drain_async(h);
+    for (auto& sl : h->slots) {
+        dfree(sl.d_req);
+        dfree(sl.d_out);
+        if (sl.h_err) (void)hipHostFree(sl.h_err);
+        for (hipEvent_t e : {sl.h2d, sl.comp, sl.d2h})
+            if (e) (void)hipEventDestroy(e);
+    }
+    for (hipStream_t st : {h->s_in, h->s_comp, h->s_out})
+        if (st) (void)hipStreamDestroy(st);
     if (h->h_err) (void)hipHostFree(h->h_err);
     if (h->h_long) (void)hipHostFree(h->h_long);
     for (auto& e : h->ev)
@@ -426,6 +455,16 @@ void sg_destroy(sg_handle* h) {
 
 const char* sg_last_error(const sg_handle* h) { return h ? h->err.c_str() : "null handle"; }
 
+int sg_set_shard(sg_handle* h, int32_t rank, int32_t world) {
+    if (h) drain_async(h);
+    if (!h || world < 1 || rank < 0 || rank >= world) return SG_E_INVAL;
+    if (world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "a namespace QPS limiter is node-wide (GlobalRequestLimiter): not on a shard");
+    h->shard_rank = rank;
+    h->shard_world = world;
+    return SG_OK;
+}
+
 int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
     if (!h || (!ns && n)) return SG_E_INVAL;
     int want = 0;
@@ -436,10 +475,13 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
         }
     }
     if (want > kMaxLim) return fail(h, SG_E_UNSUPPORTED, "more than 8 namespaces with a QPS limiter");
+    if (want && h->shard_world > 1)
+        return fail(h, SG_E_UNSUPPORTED, "a namespace QPS limiter is node-wide (GlobalRequestLimiter): not on a shard");
     for (const auto& r : h->rules)
         if (r.namespace_id < 0 || (uint32_t)r.namespace_id >= n)
             return fail(h, SG_E_INVAL, "a loaded rule refers to a namespace that would disappear");
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     // A namespace that keeps its limiter keeps its window (GlobalRequestLimiter.initIfAbsent :32-37,
     // applyMaxQpsChange :73-80); a newly enabled one starts empty.
     LimRing old[kMaxLim], nw[kMaxLim];
@@ -476,6 +518,7 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
 }
 
 int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
+    if (h) drain_async(h);
     if (!h || (!rules && n)) return SG_E_INVAL;
     if (n >= SG_KEY_BAD) return fail(h, SG_E_INVAL, "too many rules");
     (void)hipSetDevice(h->device);
@@ -653,17 +696,25 @@ int sg_get_stats(const sg_handle* h, sg_batch_stats* out) {
     return SG_OK;
 }
 
-int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
-    if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
-    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+namespace {
+
+// The batch's error flags → return code (the batch is rejected as a whole; no state changed).
+int flow_status(sg_handle* h, int err) {
+    if (err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    if (err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    return SG_OK;
+}
+
+// Enqueue one batch's whole pipeline on `stream` (req/out device-resident); its error flags land in the pinned
+// word err_dst when the stream reaches the end. Stats events only for the synchronous call.
+int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipStream_t stream, int* err_dst,
+                 bool stats) {
     if (h->K == 0 && h->kbits == 0) {
         int rc = layout_records(h);
         if (rc) return rc;
     }
-    hipStream_t stream = (hipStream_t)stream_;
-    HIP_TRY(h, hipSetDevice(h->device));
 
     BatchArgs a{};
     a.req = req;
@@ -709,7 +760,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
                   : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : h->short_max;
 
-    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
+    if (stats) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_skip_count, 0, sizeof(uint32_t), stream));
@@ -730,7 +781,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         L.ring = h->d_lim_ring;
         HIP_TRY(h, launch_limiter(a, L, stream));
     }
-    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
+    if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
         HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, a.kshift, h->d_hist, &sorted, stream, 64,
@@ -738,7 +789,7 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         a.rec_sorted = sorted;
         h->last_sorted = sorted;
     }
-    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
+    if (stats) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg(a, stream));
     // fork: long segments on the aux stream, short ones on the caller's stream, then join
     if (h->dbg & 2) {
@@ -753,14 +804,41 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         HIP_TRY(h, hipStreamWaitEvent(stream, h->join, 0));
     }
     HIP_TRY(h, launch_skip_apply(a, stream));
-    if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
+    if (stats) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, launch_finish(a, stream));
-    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
-    if (h->stats_on) {
+    HIP_TRY(h, hipMemcpyAsync(err_dst, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (stats) {
         HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, h->d_skip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipEventRecord(h->ev[4], stream));
     }
+    return SG_OK;
+}
+
+// Completes every batch of the host pipeline (their statuses are kept for sg_flow_poll / sg_flow_wait): the
+// synchronous entry points and every state-changing call start from a drained handle.
+int drain_async(sg_handle* h) {
+    for (auto& sl : h->slots) {
+        if (!sl.ticket) continue;
+        hipError_t e = hipEventSynchronize(sl.d2h);
+        h->finished[sl.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *sl.h_err);
+        sl.ticket = 0;
+    }
+    return SG_OK;
+}
+
+}  // namespace
+
+int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = enqueue_flow(h, req, n, out, stream, h->h_err, h->stats_on);
+    if (rc) return rc;
     HIP_TRY(h, hipStreamSynchronize(stream));
     if (h->stats_on) {
         float ms = 0;
@@ -773,11 +851,97 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
         h->stats.long_segments = h->h_long[0];
         h->stats.skipped_ranges = h->h_long[1];
     }
-    if (*h->h_err & kErrTime)
-        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
-    if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
-    if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    return flow_status(h, *h->h_err);
+}
+
+void* sg_host_alloc(sg_handle* h, uint64_t bytes) {
+    if (!h || bytes == 0) return nullptr;
+    if (hipSetDevice(h->device) != hipSuccess) return nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        fail(h, SG_E_NOMEM, "pinned host allocation");
+        return nullptr;
+    }
+    return p;
+}
+
+void sg_host_free(sg_handle* h, void* p) {
+    if (!h || !p) return;
+    (void)hipSetDevice(h->device);
+    (void)hipHostFree(p);
+}
+
+int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
+    if (!h || !ticket) return SG_E_INVAL;
+    *ticket = 0;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->s_comp) {  // first use: streams, per-slot device buffers, events, pinned error words
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking));
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_comp, hipStreamNonBlocking));
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_out, hipStreamNonBlocking));
+        for (auto& sl : h->slots) {
+            if (hipMalloc(&sl.d_req, sizeof(sg_req) * h->cfg.max_batch) != hipSuccess ||
+                hipMalloc(&sl.d_out, sizeof(sg_result) * h->cfg.max_batch) != hipSuccess ||
+                hipHostMalloc(&sl.h_err, sizeof(int)) != hipSuccess)
+                return fail(h, SG_E_NOMEM, "host pipeline buffers");
+            HIP_TRY(h, hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming));
+            HIP_TRY(h, hipEventCreateWithFlags(&sl.comp, hipEventDisableTiming));
+            HIP_TRY(h, hipEventCreateWithFlags(&sl.d2h, hipEventDisableTiming));
+        }
+    }
+    sg_handle::Slot& sl = h->slots[h->next_ticket % kAsyncSlots];
+    if (sl.ticket) {  // all slots in flight: complete the oldest (its status waits in `finished`)
+        hipError_t e = hipEventSynchronize(sl.d2h);
+        h->finished[sl.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *sl.h_err);
+        sl.ticket = 0;
+    }
+    // H2D of this batch overlaps the previous batch's compute; compute stays in submission order (the
+    // batches are time-ordered and share the window state); D2H overlaps the next batch's compute
+    HIP_TRY(h, hipMemcpyAsync(sl.d_req, req, sizeof(sg_req) * n, hipMemcpyHostToDevice, h->s_in));
+    HIP_TRY(h, hipEventRecord(sl.h2d, h->s_in));
+    HIP_TRY(h, hipStreamWaitEvent(h->s_comp, sl.h2d, 0));
+    int rc = enqueue_flow(h, sl.d_req, n, sl.d_out, h->s_comp, sl.h_err, false);
+    if (rc) return rc;
+    HIP_TRY(h, hipEventRecord(sl.comp, h->s_comp));
+    HIP_TRY(h, hipStreamWaitEvent(h->s_out, sl.comp, 0));
+    HIP_TRY(h, hipMemcpyAsync(out, sl.d_out, sizeof(sg_result) * n, hipMemcpyDeviceToHost, h->s_out));
+    HIP_TRY(h, hipEventRecord(sl.d2h, h->s_out));
+    // the next batch's H2D into this slot's buffers must wait for this D2H
+    HIP_TRY(h, hipStreamWaitEvent(h->s_in, sl.d2h, 0));
+    sl.ticket = h->next_ticket++;
+    *ticket = sl.ticket;
     return SG_OK;
+}
+
+static int collect(sg_handle* h, uint64_t ticket, bool block) {
+    if (!h) return SG_E_INVAL;
+    if (ticket == 0) return 1;
+    auto it = h->finished.find(ticket);
+    if (it != h->finished.end()) {
+        const int st = it->second;
+        h->finished.erase(it);
+        return st == SG_OK ? 1 : st;
+    }
+    for (auto& sl : h->slots) {
+        if (sl.ticket != ticket) continue;
+        hipError_t e = block ? hipEventSynchronize(sl.d2h) : hipEventQuery(sl.d2h);
+        if (e == hipErrorNotReady) return 0;
+        sl.ticket = 0;
+        if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+        const int st = flow_status(h, *sl.h_err);
+        return st == SG_OK ? 1 : st;
+    }
+    return fail(h, SG_E_INVAL, "unknown or already collected ticket");
+}
+
+int sg_flow_poll(sg_handle* h, uint64_t ticket) { return collect(h, ticket, false); }
+
+int sg_flow_wait(sg_handle* h, uint64_t ticket) {
+    const int r = collect(h, ticket, true);
+    return r == 1 ? SG_OK : r;
 }
 
 int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out) {
@@ -800,6 +964,7 @@ int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_re
 int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
     if (!h || key >= h->K || !starts || !counters || !occupy) return SG_E_INVAL;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     const int S = h->rule_tab[key].S;
     std::vector<Bucket> b(S);
     HIP_TRY(h, hipMemcpy(b.data(), h->d_ring + (size_t)key * h->stride, sizeof(Bucket) * S, hipMemcpyDeviceToHost));
@@ -823,6 +988,7 @@ int sg_flow_export_state(sg_handle* h, int64_t* ring, uint64_t ring_words, int64
     if (ring_words < rw || !occ || occ_words < ow) return fail(h, SG_E_INVAL, "export buffers too small");
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     static_assert(sizeof(Bucket) == 64 && sizeof(Occ) == 16, "export layout");
     HIP_TRY(h, hipMemcpy(ring, h->d_ring, rw * 8, hipMemcpyDeviceToHost));
     HIP_TRY(h, hipMemcpy(occ, h->d_occ, ow * 8, hipMemcpyDeviceToHost));
@@ -836,6 +1002,7 @@ int sg_flow_import_state(sg_handle* h, const int64_t* ring, uint64_t ring_words,
     if (ring_words != rw || occ_words != ow) return fail(h, SG_E_INVAL, "import size does not match the loaded rules");
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     HIP_TRY(h, hipMemcpy(h->d_ring, ring, rw * 8, hipMemcpyHostToDevice));
     HIP_TRY(h, hipMemcpy(h->d_occ, occ, ow * 8, hipMemcpyHostToDevice));
     return SG_OK;
@@ -845,6 +1012,7 @@ int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap)
     if (!h || !out || cap < 2ull * h->K) return SG_E_INVAL;
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     double* d_out = nullptr;
     HIP_TRY(h, hipMalloc(&d_out, sizeof(double) * 2 * h->K));
     hipError_t e1 = launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, d_out, 0);
@@ -858,6 +1026,7 @@ int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, ui
     if (!h || !out_dev || cap < 2ull * h->K) return SG_E_INVAL;
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
     return SG_OK;
 }

@@ -12,8 +12,9 @@ from . import abi
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 
-EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_load_flow_rules",
-           "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_enable_stats", "sg_get_stats",
+EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_load_flow_rules",
+           "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_poll", "sg_flow_wait",
+           "sg_host_alloc", "sg_host_free", "sg_enable_stats", "sg_get_stats",
            "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
@@ -46,9 +47,15 @@ def load_library():
         "sg_destroy": (None, [vp]),
         "sg_last_error": (C.c_char_p, [vp]),
         "sg_set_namespaces": (C.c_int, [vp, vp, u32]),
+        "sg_set_shard": (C.c_int, [vp, C.c_int32, C.c_int32]),
         "sg_load_flow_rules": (C.c_int, [vp, vp, u32]),
         "sg_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_flow_submit": (C.c_int, [vp, vp, u64, vp, C.POINTER(u64)]),
+        "sg_flow_poll": (C.c_int, [vp, u64]),
+        "sg_flow_wait": (C.c_int, [vp, u64]),
+        "sg_host_alloc": (vp, [vp, u64]),
+        "sg_host_free": (None, [vp, vp]),
         "sg_enable_stats": (C.c_int, [vp, C.c_int]),
         "sg_get_stats": (C.c_int, [vp, C.POINTER(abi.sg_batch_stats)]),
         "sg_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
@@ -106,6 +113,9 @@ class FlowEngine:
 
     def close(self):
         if getattr(self, "h", None):
+            for p in getattr(self, "_pinned", {}).values():
+                self._L.sg_host_free(self.h, C.c_void_p(p))
+            self._pinned = {}
             self._L.sg_destroy(self.h)
             self.h = None
 
@@ -122,6 +132,10 @@ class FlowEngine:
     def set_namespaces(self, ns: np.ndarray):
         ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
         self._check(self._L.sg_set_namespaces(self.h, abi.ptr(ns), len(ns)))
+
+    def set_shard(self, rank: int, world: int):
+        """This handle decides shard `rank` of `world` (refuses namespace QPS limiters when world > 1)."""
+        self._check(self._L.sg_set_shard(self.h, rank, world))
 
     def load_rules(self, rules: np.ndarray):
         rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
@@ -150,6 +164,40 @@ class FlowEngine:
         out = np.zeros(len(req), abi.RES_DTYPE)
         self._check(self._L.sg_flow_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
         return out
+
+    # ---- asynchronous host pipeline (pinned buffers, tickets)
+    def host_array(self, n, dtype):
+        """A numpy array of n `dtype` records in pinned host memory (freed with the engine or free_host)."""
+        dtype = np.dtype(dtype)
+        p = self._L.sg_host_alloc(self.h, max(1, n * dtype.itemsize))
+        if not p:
+            raise EngineError(abi.SG_E_NOMEM, "sg_host_alloc")
+        buf = (C.c_uint8 * (n * dtype.itemsize)).from_address(p)
+        arr = np.frombuffer(buf, dtype=dtype, count=n)
+        self._pinned = getattr(self, "_pinned", {})
+        self._pinned[arr.__array_interface__["data"][0]] = p
+        return arr
+
+    def free_host(self, arr):
+        p = self._pinned.pop(arr.__array_interface__["data"][0], None)
+        if p:
+            self._L.sg_host_free(self.h, C.c_void_p(p))
+
+    def submit(self, req: np.ndarray, out: np.ndarray) -> int:
+        """sg_flow_submit over host arrays (pinned ones from host_array overlap); returns the ticket."""
+        t = C.c_uint64()
+        self._check(self._L.sg_flow_submit(self.h, C.c_void_p(req.ctypes.data), len(req), C.c_void_p(out.ctypes.data),
+                                           C.byref(t)))
+        return t.value
+
+    def poll(self, ticket) -> bool:
+        r = self._L.sg_flow_poll(self.h, ticket)
+        if r < 0:
+            self._check(r)
+        return r == 1
+
+    def wait(self, ticket):
+        self._check(self._L.sg_flow_wait(self.h, ticket))
 
     def enable_stats(self, on=True):
         self._check(self._L.sg_enable_stats(self.h, 1 if on else 0))

@@ -86,11 +86,29 @@ GpuTokenService::GpuTokenService(Options opt) : opt_(std::move(opt)) {
     cfg.max_batch = opt_.maxBatch;
     int rc = sg_create(&cfg, &h_);
     if (rc != SG_OK) throw std::runtime_error("sg_create failed: " + std::to_string(rc));
+    const int depth = std::max(1, std::min(3, opt_.pipelineDepth));
+    for (int i = 0; i < depth; ++i) {
+        sg_req* rq = static_cast<sg_req*>(sg_host_alloc(h_, sizeof(sg_req) * opt_.maxBatch));
+        sg_result* rs = static_cast<sg_result*>(sg_host_alloc(h_, sizeof(sg_result) * opt_.maxBatch));
+        if (!rq || !rs) {
+            sg_host_free(h_, rq);
+            sg_host_free(h_, rs);
+            for (auto& b : bufs_) {
+                sg_host_free(h_, b.first);
+                sg_host_free(h_, b.second);
+            }
+            sg_destroy(h_);
+            throw std::runtime_error("sg_host_alloc failed");
+        }
+        bufs_.emplace_back(rq, rs);
+        freeBufs_.push_back(i);
+    }
     nsIndex("default");  // ServerConstants.DEFAULT_NAMESPACE
     {
         std::lock_guard<std::mutex> lk(mu_);
         pushNamespacesLocked();
     }
+    completer_ = std::thread([this] { completerLoop(); });
     flusher_ = std::thread([this] { flusherLoop(); });
 }
 
@@ -102,7 +120,70 @@ GpuTokenService::~GpuTokenService() {
     }
     cv_.notify_all();
     if (flusher_.joinable()) flusher_.join();
+    waitIdle();
+    {
+        std::lock_guard<std::mutex> lk(qmu_);
+        stopCompleter_ = true;
+    }
+    qcv_.notify_all();
+    if (completer_.joinable()) completer_.join();
+    for (auto& b : bufs_) {
+        sg_host_free(h_, b.first);
+        sg_host_free(h_, b.second);
+    }
     sg_destroy(h_);
+}
+
+void GpuTokenService::waitIdle() {
+    std::unique_lock<std::mutex> lk(qmu_);
+    qcv_.wait(lk, [this] { return inflight_.empty(); });
+}
+
+// Answers the micro-batches in submission order: polls the front ticket (without holding the engine lock
+// while the GPU works), then fulfils its callers' promises from the pinned result buffer.
+void GpuTokenService::completerLoop() {
+    for (;;) {
+        InFlight f;
+        {
+            std::unique_lock<std::mutex> lk(qmu_);
+            qcv_.wait(lk, [this] { return stopCompleter_ || !inflight_.empty(); });
+            if (inflight_.empty()) return;
+            f = inflight_.front();
+        }
+        int rc = f.rc;
+        if (rc == SG_OK) {
+            for (;;) {
+                int r;
+                {
+                    std::lock_guard<std::mutex> e(engMu_);
+                    r = sg_flow_poll(h_, f.ticket);
+                    if (r < 0) err_ = sg_last_error(h_);
+                }
+                if (r != 0) {
+                    rc = r < 0 ? r : SG_OK;
+                    break;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+        }
+        const size_t n = f.waiters.size();
+        const sg_result* out = bufs_[f.buf].second;
+        if (opt_.onBatch) {
+            std::vector<sg_req> rq(bufs_[f.buf].first, bufs_[f.buf].first + n);
+            std::vector<sg_result> rs(out, out + n);
+            opt_.onBatch(rq, rs, rc);
+        }
+        for (size_t i = 0; i < n; ++i) {
+            if (rc != SG_OK) f.waiters[i]->set_value(TokenResult(TokenResultStatus::FAIL));
+            else f.waiters[i]->set_value(TokenResult(out[i].status).setRemaining(out[i].remaining).setWaitInMs(out[i].wait_ms));
+        }
+        {
+            std::lock_guard<std::mutex> lk(qmu_);
+            inflight_.pop_front();
+            freeBufs_.push_back(f.buf);
+        }
+        qcv_.notify_all();
+    }
 }
 
 int GpuTokenService::nsIndex(const std::string& ns) {
@@ -118,6 +199,8 @@ int GpuTokenService::nsIndex(const std::string& ns) {
 }
 
 void GpuTokenService::pushNamespacesLocked() {
+    waitIdle();
+    std::lock_guard<std::mutex> e(engMu_);
     int rc = sg_set_namespaces(h_, nsCfg_.data(), (uint32_t)nsCfg_.size());
     if (rc != SG_OK) err_ = sg_last_error(h_);
 }
@@ -143,6 +226,7 @@ void GpuTokenService::pushRulesLocked() {
         keyOfFlow_[ids[i]] = (uint32_t)i;
     }
     pushNamespacesLocked();
+    std::lock_guard<std::mutex> e(engMu_);
     int rc = sg_load_flow_rules(h_, tab.data(), (uint32_t)tab.size());
     if (rc != SG_OK) {
         err_ = sg_last_error(h_);
@@ -220,6 +304,8 @@ uint32_t GpuTokenService::keyOf(std::optional<int64_t> ruleId, bool prioritized)
 std::vector<TokenResult> GpuTokenService::decideLocked(std::vector<sg_req>& reqs) {
     std::vector<TokenResult> res(reqs.size(), TokenResult(TokenResultStatus::FAIL));
     if (reqs.empty()) return res;
+    waitIdle();
+    std::lock_guard<std::mutex> e(engMu_);
     std::vector<sg_result> out(reqs.size());
     for (size_t off = 0; off < reqs.size(); off += opt_.maxBatch) {
         const size_t n = std::min<size_t>(opt_.maxBatch, reqs.size() - off);
@@ -267,13 +353,37 @@ TokenResult GpuTokenService::requestToken(std::optional<int64_t> ruleId, int acq
     return f.get();
 }
 
+// Submit the pending requests (time-ordered by construction) as micro-batches through the host pipeline;
+// called with mu_ held, so submission order = arrival order. Blocks only while every pipeline slot is busy.
 void GpuTokenService::flushLocked(std::unique_lock<std::mutex>& lk) {
     std::vector<Pending> batch;
     batch.swap(pending_);
-    std::vector<sg_req> reqs(batch.size());
-    for (size_t i = 0; i < batch.size(); ++i) reqs[i] = batch[i].req;
-    std::vector<TokenResult> res = decideLocked(reqs);
-    for (size_t i = 0; i < batch.size(); ++i) batch[i].result->set_value(res[i]);
+    for (size_t off = 0; off < batch.size(); off += opt_.maxBatch) {
+        const size_t n = std::min<size_t>(opt_.maxBatch, batch.size() - off);
+        int b;
+        {
+            std::unique_lock<std::mutex> q(qmu_);
+            qcv_.wait(q, [this] { return !freeBufs_.empty(); });
+            b = freeBufs_.back();
+            freeBufs_.pop_back();
+        }
+        InFlight f{0, b, SG_OK, {}};
+        f.waiters.reserve(n);
+        for (size_t i = 0; i < n; ++i) {
+            bufs_[b].first[i] = batch[off + i].req;
+            f.waiters.push_back(batch[off + i].result);
+        }
+        {
+            std::lock_guard<std::mutex> e(engMu_);
+            f.rc = sg_flow_submit(h_, bufs_[b].first, n, bufs_[b].second, &f.ticket);
+            if (f.rc != SG_OK) err_ = sg_last_error(h_);
+        }
+        {
+            std::lock_guard<std::mutex> q(qmu_);
+            inflight_.push_back(std::move(f));
+        }
+        qcv_.notify_all();
+    }
     (void)lk;
 }
 

@@ -13,14 +13,17 @@
 //                                                   ConnectionManager.getConnectedCount (:47-51)
 //
 // requestToken may be called from many threads (the Netty workers of the token server): calls are
-// stamped with TimeUtil-equivalent time and an arrival sequence under one lock, micro-batched, and
-// decided together on the GPU; each caller blocks on its own result. A failed batch answers FAIL for
-// every request in it, so the client's fallbackToLocalOrPass applies (FlowRuleChecker.java:166-209).
+// stamped with TimeUtil-equivalent time and an arrival sequence under one lock and micro-batched; a full
+// batch goes to the GPU through the asynchronous host pipeline (sg_flow_submit: pinned buffers, up to
+// `pipelineDepth` batches in flight, H2D / compute / D2H overlapped) while the next batch keeps filling, and a
+// completion thread hands each caller its own result. A failed batch answers FAIL for every request in it,
+// so the client's fallbackToLocalOrPass applies (FlowRuleChecker.java:166-209).
 #pragma once
 
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <future>
 #include <map>
@@ -152,6 +155,9 @@ public:
         size_t flushSize = 4096;       // micro-batch: flush at this many pending requests ...
         std::chrono::microseconds flushDelay{200};  // ... or when the oldest has waited this long
         std::function<int64_t()> clock;             // TimeUtil.currentTimeMillis (default: system clock)
+        int pipelineDepth = 3;                      // micro-batches in flight on the GPU (1..3)
+        // observer of every decided micro-batch (requests as submitted, results, status) — tests and tracing
+        std::function<void(const std::vector<sg_req>&, const std::vector<sg_result>&, int)> onBatch;
     };
 
     explicit GpuTokenService(Options opt);
@@ -190,6 +196,12 @@ private:
         FlowRule rule;
         std::string ns;
     };
+    struct InFlight {  // one submitted micro-batch
+        uint64_t ticket;
+        int buf;
+        int rc;        // submit status (non-zero: answered FAIL without a ticket)
+        std::vector<std::promise<TokenResult>*> waiters;
+    };
 
     uint32_t keyOf(std::optional<int64_t> ruleId, bool prioritized) const;
     int nsIndex(const std::string& ns);  // creates the namespace entry if needed
@@ -197,6 +209,8 @@ private:
     void pushRulesLocked();
     void flushLocked(std::unique_lock<std::mutex>& lk);
     void flusherLoop();
+    void completerLoop();
+    void waitIdle();  // every submitted micro-batch answered
     std::vector<TokenResult> decideLocked(std::vector<sg_req>& reqs);
 
     Options opt_;
@@ -210,6 +224,15 @@ private:
     int64_t lastTs_ = -1;
     bool stop_ = false;
     std::thread flusher_;
+
+    std::mutex engMu_;                     // every sg_* call on h_ (one handle = one submitter)
+    std::mutex qmu_;                       // inflight_, freeBufs_, stopCompleter_
+    std::condition_variable qcv_;
+    std::deque<InFlight> inflight_;
+    std::vector<int> freeBufs_;
+    std::vector<std::pair<sg_req*, sg_result*>> bufs_;  // pinned staging buffers, one pair per pipeline slot
+    bool stopCompleter_ = false;
+    std::thread completer_;
 
     std::vector<std::string> nsNames_;
     std::vector<sg_namespace> nsCfg_;

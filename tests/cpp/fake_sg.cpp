@@ -1,7 +1,9 @@
 // Recording stand-in for the C ABI, used only by the CPU test of the host mirror: it stores what the
 // mirror submits and answers each request with status OK, remaining = key index, wait = acquire, so the
 // test can check validation, flowId → key mapping, timestamps and batching without a GPU.
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -15,6 +17,8 @@ std::vector<sg_flow_rule> rules;
 std::vector<sg_namespace> ns;
 std::vector<std::vector<sg_req>> batches;
 int fail_next = 0;
+std::map<uint64_t, int> tickets;  // submitted batch → its status
+uint64_t next_ticket = 1;
 }  // namespace fake
 
 extern "C" {
@@ -42,5 +46,27 @@ int sg_flow_decide_batch_host(sg_handle*, const sg_req* req, uint64_t n, sg_resu
         out[i].wait_ms = req[i].acquire;
     }
     return SG_OK;
+}
+void* sg_host_alloc(sg_handle*, uint64_t bytes) { return std::malloc(bytes ? bytes : 1); }
+void sg_host_free(sg_handle*, void* p) { std::free(p); }
+// the pipeline decides at submit time; the status is handed out by poll / wait
+int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
+    const int rc = sg_flow_decide_batch_host(h, req, n, out);
+    std::lock_guard<std::mutex> lk(fake::mu);
+    *ticket = fake::next_ticket++;
+    fake::tickets[*ticket] = rc;
+    return SG_OK;
+}
+int sg_flow_poll(sg_handle*, uint64_t ticket) {
+    std::lock_guard<std::mutex> lk(fake::mu);
+    auto it = fake::tickets.find(ticket);
+    if (it == fake::tickets.end()) return SG_E_INVAL;
+    const int rc = it->second;
+    fake::tickets.erase(it);
+    return rc == SG_OK ? 1 : rc;
+}
+int sg_flow_wait(sg_handle* h, uint64_t ticket) {
+    const int r = sg_flow_poll(h, ticket);
+    return r == 1 ? SG_OK : r;
 }
 }
