@@ -77,7 +77,7 @@ class ShardWorkload:
         return words.view(torch.uint8).reshape(-1)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_c3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_c3_pmc_summary.json")
 
 
 def pmc_traffic():
@@ -150,6 +150,29 @@ def cpu_baseline(n_flows, n_requests, seconds_budget=25.0, threads=None):
                       f"(shard split not timed); single thread on batch 0: {single / 1e6:.2f} M decisions/s"}
 
 
+def end_to_end(eng, wl, first_b, n_batches, n_req):
+    """Decisions/s with the requests in HOST memory (what a JVM token server hands over through JNI): pinned
+    buffers → sg_flow_submit (H2D, decide, D2H on three streams, 3 batches in flight) → sg_flow_wait. The
+    batches continue the timed run's simulated time; filling the pinned buffers is not timed."""
+    ins = [eng.host_array(n_req, abi.REQ_DTYPE) for _ in range(n_batches)]
+    outs = [eng.host_array(n_req, abi.RES_DTYPE) for _ in range(n_batches)]
+    for i in range(n_batches):
+        ins[i][:] = wl.batch(first_b + i).cpu().numpy().view(abi.REQ_DTYPE)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tickets = [eng.submit(ins[i], outs[i]) for i in range(n_batches)]
+    for t in tickets:
+        eng.wait(t)
+    el = time.perf_counter() - t0
+    ok = int((outs[-1]["status"] == abi.OK).sum())
+    for a in ins + outs:
+        eng.free_host(a)
+    return {"value": n_batches * n_req / el, "unit": "decisions/s", "batches": n_batches,
+            "ms_per_batch": el * 1000.0 / n_batches, "h2d_bytes_per_batch": n_req * REQ_B,
+            "d2h_bytes_per_batch": n_req * RES_B, "ok_last_batch": ok,
+            "path": "pinned host buffers -> sg_flow_submit (H2D / decide / D2H overlapped, 3 in flight) -> sg_flow_wait"}
+
+
 def launch_ranks(n):
     """Run this script as n ranks of one node (the driver's own launch line), as a child process."""
     import socket
@@ -172,6 +195,7 @@ def main():
     ap.add_argument("--flows", type=int, default=1_000_000)
     ap.add_argument("--requests", type=int, default=16_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-batches", type=int, default=4, help="host-buffer batches for the end-to-end figure (0: skip)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -271,6 +295,9 @@ def main():
         "phases_ms": {"device_total": total_ms, "sort": phase["sort_ms"] / args.steps, "walk": walk_ms,
                       "long_segments": long_segments},
     }
+    if world == 1 and args.e2e_batches > 0:
+        eng.enable_stats(False)
+        result["end_to_end"] = end_to_end(eng, wl, total_steps, args.e2e_batches, args.requests)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.flows, args.requests)
     if rank == 0:

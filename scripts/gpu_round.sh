@@ -15,19 +15,19 @@ step() {  # step <name> <timeout> <cmd...>; continue only on exit 0/1 (test fail
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  step pytest_gpu 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+  step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 400 python -u bench.py --steps 10 --warmup 3
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step rocprof 400 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline
+  step rocprof 400 rocprofv3 --kernel-trace --stats -T -d gpurun_out/prof -o run --output-format csv -- python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-batches 0
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
   # HBM traffic: one counter per pass (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2)
-  step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
-  step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
+  step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
+  step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
   step pmc_summary 60 python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_summary.json
 fi
 echo done

@@ -909,8 +909,7 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
     HIP_TRY(h, hipStreamWaitEvent(h->s_out, sl.comp, 0));
     HIP_TRY(h, hipMemcpyAsync(out, sl.d_out, sizeof(sg_result) * n, hipMemcpyDeviceToHost, h->s_out));
     HIP_TRY(h, hipEventRecord(sl.d2h, h->s_out));
-    // the next batch's H2D into this slot's buffers must wait for this D2H
-    HIP_TRY(h, hipStreamWaitEvent(h->s_in, sl.d2h, 0));
+    // (a slot is reused only after its batch completed: above, or when its ticket was collected)
     sl.ticket = h->next_ticket++;
     *ticket = sl.ticket;
     return SG_OK;
