@@ -205,6 +205,45 @@ typedef struct sg_cparam_req {
     uint32_t value_count;        /* 0 → BAD_REQUEST (params empty, DefaultTokenService.java:54)            */
 } sg_cparam_req;
 
+/* ---- concurrent (thread-grade) cluster tokens: TokenService.requestConcurrentToken / releaseConcurrentToken ----
+ * DefaultTokenService.java:66-85 → ConcurrentClusterFlowChecker.acquireConcurrentToken / releaseConcurrentToken
+ * (srv/flow/ConcurrentClusterFlowChecker.java:48-101) over the loaded cluster flow rules: one nowCalls counter per
+ * flowId (CurrentConcurrencyManager; kept for flowIds that survive a rule reload, ClusterFlowRuleManager.java:
+ * 356-358) and a token table (TokenCacheNodeManager). Token ids are deterministic instead of UUID bits: an acquire
+ * that passes gets id 1 + (number of concurrent requests this handle decided before it). */
+#define SG_CONC_ACQUIRE 0
+#define SG_CONC_RELEASE 1
+#define SG_STATUS_RELEASE_OK      6   /* TokenResultStatus.RELEASE_OK      */
+#define SG_STATUS_ALREADY_RELEASE 7   /* TokenResultStatus.ALREADY_RELEASE */
+typedef struct sg_conc_req {
+    int64_t  ts_ms;
+    uint64_t token_id;           /* release: the token (0 = null → BAD_REQUEST); acquire: ignored          */
+    uint32_t key;                /* acquire: rule index (or SG_KEY_BAD / SG_KEY_NO_RULE); release: ignored   */
+    int32_t  acquire;            /* acquire: acquireCount (<= 0 → BAD_REQUEST)                              */
+    uint32_t client;             /* acquire: client address id, 0 = null / "" (→ BAD_REQUEST)               */
+    int32_t  kind;               /* SG_CONC_*                                                              */
+} sg_conc_req;
+typedef struct sg_conc_result {
+    int32_t  status;             /* OK / BLOCKED / BAD_REQUEST / NO_RULE_EXISTS / RELEASE_OK / ALREADY_RELEASE */
+    int32_t  reserved;
+    uint64_t token_id;           /* acquire OK: the new token                                               */
+} sg_conc_result;
+
+/* Per-rule ClusterFlowConfig.clientOfflineTime / resourceTimeout (ms) for the token expiry, rule index order;
+ * defaults 2000 / 2000 (ClusterFlowConfig.java); reset to the defaults by sg_load_flow_rules. */
+int sg_conc_set_rule_timeouts(sg_handle* h, const int64_t* client_offline_ms, const int64_t* resource_timeout_ms,
+                              uint32_t n);
+/* A time-ordered batch of acquires and releases (DEVICE pointers; asynchronous on stream). */
+int sg_conc_decide_batch(sg_handle* h, const sg_conc_req* req, uint64_t n, sg_conc_result* out, void* stream);
+int sg_conc_decide_batch_host(sg_handle* h, const sg_conc_req* req, uint64_t n, sg_conc_result* out);
+/* RegularExpireStrategy.clearToken (…/statistic/concurrent/expire/RegularExpireStrategy.java:94-123) at now_ms:
+ * removes tokens whose client is offline past clientOfflineTime, or held more than 2 x resourceTimeout, and gives
+ * their counts back. client_online[c] = ConnectionManager.isClientOnline(client c) (ids >= n_clients: offline).
+ * Every token is examined (the reference stops after 1000 keys in ConcurrentHashMap order). *removed = count. */
+int sg_conc_expire(sg_handle* h, int64_t now_ms, const uint8_t* client_online, uint32_t n_clients, uint64_t* removed);
+/* nowCalls of rule `key` and the number of live tokens. */
+int sg_conc_read_state(sg_handle* h, uint32_t key, int32_t* now_calls, uint64_t* live_tokens);
+
 /* ---- local slot chain: StatisticSlot → FlowSlot (DefaultController) → DegradeSlot (circuit breakers) ---- */
 
 /* DegradeRule (sentinel-core/.../slots/block/degrade/DegradeRule.java). */

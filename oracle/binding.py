@@ -90,6 +90,12 @@ def lib():
         "or_local_origin_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
         "or_local_controller": (C.c_int, [vp, u32, vp]),
         "or_local_rule_order": (C.c_int, [vp, u32, vp, u32]),
+        "or_conc_new": (vp, []), "or_conc_free": (None, [vp]),
+        "or_conc_set_namespaces": (C.c_int, [vp, vp, u32]), "or_conc_load_rules": (C.c_int, [vp, vp, u32]),
+        "or_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
+        "or_conc_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_conc_expire": (u64, [vp, i64, vp, u32]),
+        "or_conc_now_calls": (C.c_int32, [vp, u32]), "or_conc_live": (u64, [vp]),
         "or_ctl_new": (vp, [vp, C.c_int]), "or_ctl_free": (None, [vp]), "or_ctl_state": (None, [vp, vp]),
         "or_ctl_warning_token": (C.c_int32, [vp]), "or_ctl_max_token": (C.c_int32, [vp]),
         "or_warm_can_pass": (C.c_int, [vp, i64, d, d, C.c_int]),
@@ -353,6 +359,48 @@ class ShardedClusterTokenService:
 
     def close(self):
         self.pool.shutdown()
+
+
+class ConcurrentTokenService:
+    """Sequential replay of DefaultTokenService.requestConcurrentToken / releaseConcurrentToken
+    (ConcurrentClusterFlowChecker + CurrentConcurrencyManager + TokenCacheNodeManager)."""
+
+    def __init__(self):
+        self.h = lib().or_conc_new()
+
+    def __del__(self):
+        if self.h:
+            lib().or_conc_free(self.h)
+            self.h = None
+
+    def set_namespaces(self, ns):
+        ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
+        lib().or_conc_set_namespaces(self.h, abi.ptr(ns), len(ns))
+
+    def load_rules(self, rules):
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        lib().or_conc_load_rules(self.h, abi.ptr(rules), len(rules))
+
+    def set_rule_timeouts(self, client_offline_ms, resource_timeout_ms):
+        a = np.ascontiguousarray(client_offline_ms, dtype=np.int64)
+        b = np.ascontiguousarray(resource_timeout_ms, dtype=np.int64)
+        assert lib().or_conc_set_rule_timeouts(self.h, abi.ptr(a), abi.ptr(b), len(a)) == 0
+
+    def decide(self, req):
+        req = np.ascontiguousarray(req, dtype=abi.CONC_REQ_DTYPE)
+        out = np.zeros(len(req), abi.CONC_RES_DTYPE)
+        lib().or_conc_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
+        return out
+
+    def expire(self, now, online):
+        online = np.ascontiguousarray(online, dtype=np.uint8)
+        return int(lib().or_conc_expire(self.h, now, abi.ptr(online) if len(online) else None, len(online)))
+
+    def now_calls(self, k):
+        return int(lib().or_conc_now_calls(self.h, k))
+
+    def live(self):
+        return int(lib().or_conc_live(self.h))
 
 
 class ClusterParamMetric:

@@ -2011,3 +2011,176 @@ int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out) {
     }
     return 0;
 }
+
+/* ===================================================================================== */
+/* Concurrent cluster tokens: ConcurrentClusterFlowChecker (srv/flow/ConcurrentClusterFlowChecker.java:34-101), */
+/* CurrentConcurrencyManager (nowCalls per flowId), TokenCacheNodeManager (the token map) and              */
+/* RegularExpireStrategy.clearToken (…/statistic/concurrent/expire/RegularExpireStrategy.java:94-137).    */
+/* Token ids are 1 + the number of requests decided before the acquire (sg_conc_req contract).             */
+/* ===================================================================================== */
+
+typedef struct or_ctok {         /* TokenCacheNode (TokenCacheNode.java) */
+    uint64_t id;
+    int64_t flow_id, client_timeout, resource_timeout;
+    int32_t acquire;
+    uint32_t client;
+    int alive;
+} or_ctok;
+
+struct or_conc {
+    sg_flow_rule* rules;
+    int64_t* client_off;          /* ClusterFlowConfig.clientOfflineTime per rule */
+    int64_t* res_to;              /* ClusterFlowConfig.resourceTimeout per rule   */
+    int32_t* now_calls;           /* CurrentConcurrencyManager.NOW_CALLS_MAP       */
+    uint32_t n;
+    sg_namespace* ns;
+    uint32_t n_ns;
+    or_ctok* tok;                 /* in id order (ids increase) */
+    uint64_t n_tok, cap_tok, live;
+    uint64_t seq;                 /* requests decided so far */
+};
+
+or_conc* or_conc_new(void) { return (or_conc*)calloc(1, sizeof(or_conc)); }
+
+void or_conc_free(or_conc* c) {
+    if (!c) return;
+    free(c->rules);
+    free(c->client_off);
+    free(c->res_to);
+    free(c->now_calls);
+    free(c->ns);
+    free(c->tok);
+    free(c);
+}
+
+int or_conc_set_namespaces(or_conc* c, const sg_namespace* ns, uint32_t n) {
+    free(c->ns);
+    c->ns = (sg_namespace*)malloc((n ? n : 1) * sizeof(sg_namespace));
+    memcpy(c->ns, ns, n * sizeof(sg_namespace));
+    c->n_ns = n;
+    return 0;
+}
+
+/* ClusterFlowRuleManager.applyClusterFlowRule: nowCalls put(flowId, 0) when absent (:356-358), removed with the
+ * flowId (clearAndResetRulesConditional :287-300) */
+int or_conc_load_rules(or_conc* c, const sg_flow_rule* rules, uint32_t n) {
+    int32_t* now = (int32_t*)calloc(n ? n : 1, sizeof(int32_t));
+    for (uint32_t i = 0; i < n; i++)
+        for (uint32_t j = 0; j < c->n; j++)
+            if (c->rules[j].flow_id == rules[i].flow_id) now[i] = c->now_calls[j];
+    free(c->rules);
+    free(c->now_calls);
+    free(c->client_off);
+    free(c->res_to);
+    c->rules = (sg_flow_rule*)malloc((n ? n : 1) * sizeof(sg_flow_rule));
+    memcpy(c->rules, rules, n * sizeof(sg_flow_rule));
+    c->now_calls = now;
+    c->client_off = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+    c->res_to = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+    for (uint32_t i = 0; i < n; i++) c->client_off[i] = c->res_to[i] = 2000;   /* ClusterFlowConfig defaults */
+    c->n = n;
+    return 0;
+}
+
+int or_conc_set_rule_timeouts(or_conc* c, const int64_t* client_off, const int64_t* res_to, uint32_t n) {
+    if (n != c->n) return SG_E_INVAL;
+    memcpy(c->client_off, client_off, n * sizeof(int64_t));
+    memcpy(c->res_to, res_to, n * sizeof(int64_t));
+    return 0;
+}
+
+static int conc_rule_of(const or_conc* c, int64_t flow_id) {   /* ClusterFlowRuleManager.getFlowRuleById */
+    for (uint32_t i = 0; i < c->n; i++)
+        if (c->rules[i].flow_id == flow_id) return (int)i;
+    return -1;
+}
+
+/* ConcurrentClusterFlowChecker.calcGlobalThreshold (:36-46): no exceedCount on this path */
+static double conc_threshold(const or_conc* c, uint32_t k) {
+    const sg_flow_rule* r = &c->rules[k];
+    if (r->threshold_type == SG_THRESHOLD_GLOBAL) return r->count;
+    int connected = (r->namespace_id >= 0 && (uint32_t)r->namespace_id < c->n_ns) ? c->ns[r->namespace_id].connected_count : 0;
+    return r->count * connected;
+}
+
+static or_ctok* conc_find(or_conc* c, uint64_t id) {          /* TokenCacheNodeManager.getTokenCacheNode */
+    uint64_t lo = 0, hi = c->n_tok;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) / 2;
+        if (c->tok[mid].id < id) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < c->n_tok && c->tok[lo].id == id && c->tok[lo].alive) ? &c->tok[lo] : NULL;
+}
+
+int or_conc_decide(or_conc* c, const sg_conc_req* req, uint64_t n, sg_conc_result* out) {
+    for (uint64_t i = 0; i < n; i++, c->seq++) {
+        const sg_conc_req* q = &req[i];
+        sg_conc_result* o = &out[i];
+        o->reserved = 0;
+        o->token_id = 0;
+        if (q->kind == SG_CONC_ACQUIRE) {
+            /* DefaultTokenService.requestConcurrentToken (:66-77) */
+            const uint32_t k = q->key & SG_KEY_INDEX;
+            if (q->client == 0 || k == SG_KEY_BAD || q->acquire <= 0) { o->status = SG_STATUS_BAD_REQUEST; continue; }
+            if (k >= c->n) { o->status = SG_STATUS_NO_RULE_EXISTS; continue; }
+            /* acquireConcurrentToken (:48-79): nowCalls + acquireCount > threshold (int + int, then double) */
+            const int32_t sum = (int32_t)((uint32_t)c->now_calls[k] + (uint32_t)q->acquire);
+            if ((double)sum > conc_threshold(c, k)) { o->status = SG_STATUS_BLOCKED; continue; }
+            c->now_calls[k] = sum;
+            if (c->n_tok == c->cap_tok) {
+                c->cap_tok = c->cap_tok ? 2 * c->cap_tok : 1024;
+                c->tok = (or_ctok*)realloc(c->tok, c->cap_tok * sizeof(or_ctok));
+            }
+            or_ctok* t = &c->tok[c->n_tok++];
+            t->id = c->seq + 1;
+            t->flow_id = c->rules[k].flow_id;
+            t->client_timeout = c->client_off[k] + q->ts_ms;   /* setClientTimeout: + currentTimeMillis */
+            t->resource_timeout = c->res_to[k] + q->ts_ms;
+            t->acquire = q->acquire;
+            t->client = q->client;
+            t->alive = 1;
+            c->live++;
+            o->status = SG_STATUS_OK;
+            o->token_id = t->id;
+        } else if (q->kind == SG_CONC_RELEASE) {
+            /* releaseConcurrentToken (:81-101) */
+            if (q->token_id == 0) { o->status = SG_STATUS_BAD_REQUEST; continue; }
+            or_ctok* t = conc_find(c, q->token_id);
+            if (!t) { o->status = SG_STATUS_ALREADY_RELEASE; continue; }
+            const int r = conc_rule_of(c, t->flow_id);
+            if (r < 0) { o->status = SG_STATUS_NO_RULE_EXISTS; continue; }
+            t->alive = 0;
+            c->live--;
+            c->now_calls[r] = (int32_t)((uint32_t)c->now_calls[r] - (uint32_t)t->acquire);
+            o->status = SG_STATUS_RELEASE_OK;
+        } else {
+            o->status = SG_STATUS_BAD_REQUEST;
+        }
+    }
+    return 0;
+}
+
+/* RegularExpireStrategy.clearToken over every token: client offline past clientTimeout, or held for more than
+ * resourceTimeout past its resource deadline (rule looked up by flowId; tokens of a removed rule only expire by
+ * the client condition). Returns the number removed. */
+uint64_t or_conc_expire(or_conc* c, int64_t now, const uint8_t* online, uint32_t n_clients) {
+    uint64_t removed = 0;
+    for (uint64_t i = 0; i < c->n_tok; i++) {
+        or_ctok* t = &c->tok[i];
+        if (!t->alive) continue;
+        const int on = t->client < n_clients && online[t->client];
+        const int r = conc_rule_of(c, t->flow_id);
+        int drop = !on && t->client_timeout - now < 0;
+        if (!drop && r >= 0 && now - t->resource_timeout > c->res_to[r]) drop = 1;
+        if (!drop) continue;
+        t->alive = 0;
+        c->live--;
+        removed++;
+        if (r >= 0) c->now_calls[r] = (int32_t)((uint32_t)c->now_calls[r] - (uint32_t)t->acquire);
+    }
+    return removed;
+}
+
+int32_t or_conc_now_calls(const or_conc* c, uint32_t k) { return k < c->n ? c->now_calls[k] : 0; }
+uint64_t or_conc_live(const or_conc* c) { return c->live; }

@@ -182,6 +182,18 @@ uint64_t  or_lgen_pending(const or_lgen* g);
 uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
                       int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
 
+/* ---------- concurrent cluster tokens (ConcurrentClusterFlowChecker + TokenCacheNodeManager) ---------- */
+typedef struct or_conc or_conc;
+or_conc* or_conc_new(void);
+void     or_conc_free(or_conc* c);
+int      or_conc_set_namespaces(or_conc* c, const sg_namespace* ns, uint32_t n);
+int      or_conc_load_rules(or_conc* c, const sg_flow_rule* rules, uint32_t n);
+int      or_conc_set_rule_timeouts(or_conc* c, const int64_t* client_off, const int64_t* res_to, uint32_t n);
+int      or_conc_decide(or_conc* c, const sg_conc_req* req, uint64_t n, sg_conc_result* out);
+uint64_t or_conc_expire(or_conc* c, int64_t now, const uint8_t* online, uint32_t n_clients);
+int32_t  or_conc_now_calls(const or_conc* c, uint32_t k);
+uint64_t or_conc_live(const or_conc* c);
+
 /* ---------- Envoy RLS (SimpleClusterFlowChecker over the same ClusterMetric) ---------- */
 int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
 

@@ -98,6 +98,13 @@ CPARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4"
 BEHAVIOR_DEFAULT = 0
 BEHAVIOR_RATE_LIMITER = 2
 
+# concurrent cluster tokens (sg_conc_*)
+CONC_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("token_id", "<u8"), ("key", "<u4"), ("acquire", "<i4"),
+                           ("client", "<u4"), ("kind", "<i4")], align=True)
+CONC_RES_DTYPE = np.dtype([("status", "<i4"), ("reserved", "<i4"), ("token_id", "<u8")], align=True)
+CONC_ACQUIRE, CONC_RELEASE = 0, 1
+RELEASE_OK, ALREADY_RELEASE = 6, 7
+
 # local slot chain (sg_local_*)
 DEGRADE_RULE_DTYPE = np.dtype([("grade", "<i4"), ("time_window_sec", "<i4"), ("count", "<f8"),
                                ("slow_ratio_threshold", "<f8"), ("min_request_amount", "<i4"),
@@ -133,6 +140,7 @@ assert CPARAM_RULE_DTYPE.itemsize == 40 and CPARAM_REQ_DTYPE.itemsize == 24
 assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 assert LOCAL_FLOW_RULE_DTYPE.itemsize == 40
+assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:

@@ -139,6 +139,23 @@ struct sg_handle {
 
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
+    // concurrent cluster tokens (sg_conc_*)
+    int32_t* d_cnow = nullptr;        // nowCalls per rule
+    double* d_cthr = nullptr;
+    int64_t* d_coff = nullptr;
+    int64_t* d_cres = nullptr;
+    int64_t* d_cfid = nullptr;
+    CTok* d_ctok = nullptr;
+    uint64_t ctok_slots = 0, ctok_used = 0;  // table size; slots taken since the last rehash (upper bound)
+    uint8_t* d_calive = nullptr;
+    int64_t* d_clast_ts = nullptr;
+    sg_conc_req* d_creq_h = nullptr;
+    sg_conc_result* d_cout_h = nullptr;
+    uint64_t conc_seq = 0;            // requests decided so far (token ids)
+    bool conc_dirty = true;           // rules / namespaces / timeouts changed since the last upload
+    bool cnow_pending = false;        // cnow_host holds the remapped counters of a rule reload
+    std::vector<int32_t> cnow_host;
+    std::vector<int64_t> c_off, c_res;
     // asynchronous host pipeline (sg_flow_submit): H2D / compute / D2H streams, kAsyncSlots batches in flight
     struct Slot {
         uint64_t ticket = 0;            // 0 = free
@@ -419,6 +436,16 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lrules);
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
+    dfree(h->d_cnow);
+    dfree(h->d_cthr);
+    dfree(h->d_coff);
+    dfree(h->d_cres);
+    dfree(h->d_cfid);
+    dfree(h->d_ctok);
+    dfree(h->d_calive);
+    dfree(h->d_clast_ts);
+    dfree(h->d_creq_h);
+    dfree(h->d_cout_h);
     dfree(h->d_lhead);
     dfree(h->d_lsec);
     dfree(h->d_lbor);
@@ -477,6 +504,7 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
     if (want > kMaxLim) return fail(h, SG_E_UNSUPPORTED, "more than 8 namespaces with a QPS limiter");
     if (want && h->shard_world > 1)
         return fail(h, SG_E_UNSUPPORTED, "a namespace QPS limiter is node-wide (GlobalRequestLimiter): not on a shard");
+    h->conc_dirty = true;  // AVG_LOCAL concurrency thresholds read connectedCount
     for (const auto& r : h->rules)
         if (r.namespace_id < 0 || (uint32_t)r.namespace_id >= n)
             return fail(h, SG_E_INVAL, "a loaded rule refers to a namespace that would disappear");
@@ -590,6 +618,17 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         HIP_TRY(h, hipDeviceSynchronize());
         dfree(d_src);
     }
+    if (h->d_cnow) {  // CurrentConcurrencyManager: surviving flowIds keep nowCalls, new ones start at 0
+        std::vector<int32_t> old(h->K);
+        if (h->K) HIP_TRY(h, hipMemcpy(old.data(), h->d_cnow, sizeof(int32_t) * h->K, hipMemcpyDeviceToHost));
+        h->cnow_host.assign(n, 0);
+        for (uint32_t i = 0; i < n; ++i)
+            if (src[i] >= 0) h->cnow_host[i] = old[src[i]];
+        h->cnow_pending = true;
+    }
+    h->c_off.assign(n, 2000);  // ClusterFlowConfig.clientOfflineTime / resourceTimeout defaults
+    h->c_res.assign(n, 2000);
+    h->conc_dirty = true;
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
@@ -1985,6 +2024,221 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     int kept = 0;
     for (int64_t x : slot) kept += x != -1;
     return kept;
+}
+
+// ------------------------------------------------------------------------ concurrent cluster tokens
+
+namespace {
+
+// Upload what the concurrency kernels read (thresholds, timeouts, flowIds, counters) after rules / namespaces /
+// timeouts changed; first use allocates the token table and the per-batch buffers.
+int conc_prepare(sg_handle* h) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_ctok) {
+        h->ctok_slots = 1ull << 20;
+        if (hipMalloc(&h->d_ctok, sizeof(CTok) * h->ctok_slots) != hipSuccess ||
+            hipMalloc(&h->d_calive, h->cfg.max_batch) != hipSuccess || hipMalloc(&h->d_clast_ts, sizeof(int64_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "concurrent token table");
+        HIP_TRY(h, hipMemset(h->d_ctok, 0, sizeof(CTok) * h->ctok_slots));
+        const int64_t neg = -1;
+        HIP_TRY(h, hipMemcpy(h->d_clast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
+        h->ctok_used = 0;
+    }
+    if (!h->conc_dirty) return SG_OK;
+    const uint32_t K = h->K;
+    if (h->c_off.size() != K) {
+        h->c_off.assign(K, 2000);
+        h->c_res.assign(K, 2000);
+    }
+    std::vector<double> thr(K);
+    std::vector<int64_t> fid(K);
+    for (uint32_t k = 0; k < K; ++k) {  // ConcurrentClusterFlowChecker.calcGlobalThreshold (:36-46)
+        const sg_flow_rule& r = h->rules[k];
+        const int connected = (r.namespace_id >= 0 && (size_t)r.namespace_id < h->ns.size())
+                                  ? h->ns[r.namespace_id].connected_count : 0;
+        thr[k] = r.threshold_type == SG_THRESHOLD_GLOBAL ? r.count : r.count * connected;
+        fid[k] = r.flow_id;
+    }
+    std::vector<int32_t> now = h->cnow_pending ? h->cnow_host : std::vector<int32_t>(K, 0);
+    if (!h->cnow_pending && h->d_cnow && now.size() == K) {  // unchanged rules: keep the device counters
+        HIP_TRY(h, hipMemcpy(now.data(), h->d_cnow, sizeof(int32_t) * K, hipMemcpyDeviceToHost));
+    }
+    dfree(h->d_cnow);
+    dfree(h->d_cthr);
+    dfree(h->d_coff);
+    dfree(h->d_cres);
+    dfree(h->d_cfid);
+    const size_t k1 = K ? K : 1;
+    if (hipMalloc(&h->d_cnow, sizeof(int32_t) * k1) != hipSuccess || hipMalloc(&h->d_cthr, sizeof(double) * k1) != hipSuccess ||
+        hipMalloc(&h->d_coff, sizeof(int64_t) * k1) != hipSuccess || hipMalloc(&h->d_cres, sizeof(int64_t) * k1) != hipSuccess ||
+        hipMalloc(&h->d_cfid, sizeof(int64_t) * k1) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "concurrency rule state");
+    if (K) {
+        HIP_TRY(h, hipMemcpy(h->d_cnow, now.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_cthr, thr.data(), sizeof(double) * K, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_coff, h->c_off.data(), sizeof(int64_t) * K, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_cres, h->c_res.data(), sizeof(int64_t) * K, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_cfid, fid.data(), sizeof(int64_t) * K, hipMemcpyHostToDevice));
+    }
+    if (!h->d_fid) {
+        int rc = upload_fid_table(h);
+        if (rc) return rc;
+    }
+    h->cnow_pending = false;
+    h->conc_dirty = false;
+    return SG_OK;
+}
+
+ConcArgs conc_args(sg_handle* h) {
+    ConcArgs c{};
+    c.base = h->conc_seq;
+    c.K = h->K;
+    c.thr = h->d_cthr;
+    c.now = h->d_cnow;
+    c.client_off = h->d_coff;
+    c.res_to = h->d_cres;
+    c.flow_id = h->d_cfid;
+    c.tab = h->d_ctok;
+    c.tmask = h->ctok_slots - 1;
+    c.fid = h->d_fid;
+    c.fid_mask = h->fid_mask;
+    c.alive = h->d_calive;
+    c.err = h->d_err;
+    c.last_ts = h->d_clast_ts;
+    return c;
+}
+
+// Keeps the token table at most half full: a rehash into a larger table when the batch could overflow it.
+int conc_reserve(sg_handle* h, uint64_t n) {
+    if (h->ctok_used + n <= h->ctok_slots / 2) return SG_OK;
+    ConcArgs c = conc_args(h);
+    unsigned long long* d_live = nullptr;
+    HIP_TRY(h, hipMalloc(&d_live, sizeof(unsigned long long)));
+    HIP_TRY(h, hipMemset(d_live, 0, sizeof(unsigned long long)));
+    HIP_TRY(h, launch_conc_count(c, d_live, 0));
+    unsigned long long live = 0;
+    HIP_TRY(h, hipMemcpy(&live, d_live, sizeof(live), hipMemcpyDeviceToHost));
+    (void)hipFree(d_live);
+    uint64_t slots = 1ull << 20;
+    while (slots < 4 * (live + n)) slots <<= 1;
+    CTok* t = nullptr;
+    if (hipMalloc(&t, sizeof(CTok) * slots) != hipSuccess) return fail(h, SG_E_NOMEM, "concurrent token table");
+    HIP_TRY(h, hipMemset(t, 0, sizeof(CTok) * slots));
+    HIP_TRY(h, hipMemset(h->d_err, 0, sizeof(int)));
+    HIP_TRY(h, launch_conc_rehash(h->d_ctok, h->ctok_slots, t, slots - 1, h->d_err, 0));
+    HIP_TRY(h, hipDeviceSynchronize());
+    dfree(h->d_ctok);
+    h->d_ctok = t;
+    h->ctok_slots = slots;
+    h->ctok_used = live;
+    return SG_OK;
+}
+
+}  // namespace
+
+int sg_conc_set_rule_timeouts(sg_handle* h, const int64_t* client_offline_ms, const int64_t* resource_timeout_ms,
+                              uint32_t n) {
+    if (!h || (n && (!client_offline_ms || !resource_timeout_ms))) return SG_E_INVAL;
+    if (n != h->K) return fail(h, SG_E_INVAL, "one timeout pair per loaded rule");
+    drain_async(h);
+    h->c_off.assign(client_offline_ms, client_offline_ms + n);
+    h->c_res.assign(resource_timeout_ms, resource_timeout_ms + n);
+    h->conc_dirty = true;
+    return SG_OK;
+}
+
+int sg_conc_decide_batch(sg_handle* h, const sg_conc_req* req, uint64_t n, sg_conc_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = conc_prepare(h);
+    if (rc) return rc;
+    rc = conc_reserve(h, n);
+    if (rc) return rc;
+    hipStream_t stream = (hipStream_t)stream_;
+    int kbits = bits_for((uint64_t)h->K);
+    if (kbits < 1) kbits = 1;
+    if (kbits + bits_for(h->cfg.max_batch) > 64) return fail(h, SG_E_UNSUPPORTED, "rules x max_batch too large");
+    ConcArgs c = conc_args(h);
+    c.req = req;
+    c.out = out;
+    c.n = n;
+    c.rec = h->d_rec;
+    c.kshift = 64 - kbits;
+    c.imask = (1ull << c.kshift) - 1;
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, launch_conc_batch(c, h->d_rec_sorted, h->d_hist, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (*h->h_err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (*h->h_err & kErrTableFull) return fail(h, SG_E_CAPACITY, "concurrent token table full");
+    h->conc_seq += n;
+    h->ctok_used += n;
+    return SG_OK;
+}
+
+int sg_conc_decide_batch_host(sg_handle* h, const sg_conc_req* req, uint64_t n, sg_conc_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_creq_h) {
+        if (hipMalloc(&h->d_creq_h, sizeof(sg_conc_req) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_cout_h, sizeof(sg_conc_result) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    HIP_TRY(h, hipMemcpy(h->d_creq_h, req, sizeof(sg_conc_req) * n, hipMemcpyHostToDevice));
+    int rc = sg_conc_decide_batch(h, h->d_creq_h, n, h->d_cout_h, nullptr);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemcpy(out, h->d_cout_h, sizeof(sg_conc_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_conc_expire(sg_handle* h, int64_t now_ms, const uint8_t* client_online, uint32_t n_clients, uint64_t* removed) {
+    if (!h || (n_clients && !client_online)) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = conc_prepare(h);
+    if (rc) return rc;
+    uint8_t* d_on = nullptr;
+    unsigned long long* d_rm = nullptr;
+    HIP_TRY(h, hipMalloc(&d_on, n_clients ? n_clients : 1));
+    HIP_TRY(h, hipMalloc(&d_rm, sizeof(unsigned long long)));
+    hipError_t e = n_clients ? hipMemcpy(d_on, client_online, n_clients, hipMemcpyHostToDevice) : hipSuccess;
+    if (e == hipSuccess) e = hipMemset(d_rm, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = launch_conc_expire(conc_args(h), now_ms, d_on, n_clients, d_rm, 0);
+    unsigned long long rm = 0;
+    if (e == hipSuccess) e = hipMemcpy(&rm, d_rm, sizeof(rm), hipMemcpyDeviceToHost);
+    (void)hipFree(d_on);
+    (void)hipFree(d_rm);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    if (removed) *removed = rm;
+    return SG_OK;
+}
+
+int sg_conc_read_state(sg_handle* h, uint32_t key, int32_t* now_calls, uint64_t* live_tokens) {
+    if (!h || key >= h->K) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = conc_prepare(h);
+    if (rc) return rc;
+    if (now_calls) HIP_TRY(h, hipMemcpy(now_calls, h->d_cnow + key, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (live_tokens) {
+        unsigned long long* d = nullptr;
+        HIP_TRY(h, hipMalloc(&d, sizeof(unsigned long long)));
+        hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+        if (e == hipSuccess) e = launch_conc_count(conc_args(h), d, 0);
+        unsigned long long v = 0;
+        if (e == hipSuccess) e = hipMemcpy(&v, d, sizeof(v), hipMemcpyDeviceToHost);
+        (void)hipFree(d);
+        if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+        *live_tokens = v;
+    }
+    return SG_OK;
 }
 
 int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {

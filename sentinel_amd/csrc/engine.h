@@ -258,6 +258,56 @@ hipError_t launch_cp_range(const CPArgs& c, BatchArgs& sg, uint64_t lo, uint64_t
 hipError_t launch_cp_multi(const CPArgs& c, uint64_t m, hipStream_t stream);
 hipError_t launch_cp_read(const CPArgs& c, uint32_t rule, uint64_t value, int64_t now, int64_t* out_dev, hipStream_t stream);
 
+struct FidSlot {      // flowId → rule index, open addressing with linear probing (fid 0 = empty)
+    int64_t fid;
+    uint32_t idx;
+    uint32_t pad;
+};
+
+// ---- concurrent cluster tokens (conc.hip): ConcurrentClusterFlowChecker + TokenCacheNodeManager ----
+struct alignas(16) CTok {     // TokenCacheNode in an open-addressing table keyed by token id
+    uint64_t id;              // 0 = empty slot
+    int64_t flow_id;
+    int64_t client_to;        // clientOfflineTime + creation time
+    int64_t res_to;           // resourceTimeout + creation time
+    int32_t acquire;
+    uint32_t client;
+    int32_t state;            // 1 live, 2 removed (slots are never reused until the table is rebuilt)
+    int32_t pad;
+};
+static_assert(sizeof(CTok) == 48, "CTok layout");
+
+struct ConcArgs {
+    const sg_conc_req* req;
+    sg_conc_result* out;
+    uint64_t n;
+    uint64_t base;            // requests decided before this batch: token id of acquire i = base + i + 1
+    uint32_t K;
+    const double* thr;        // calcGlobalThreshold per rule
+    int32_t* now;             // nowCalls per rule
+    const int64_t* client_off;
+    const int64_t* res_to;
+    const int64_t* flow_id;
+    CTok* tab;
+    uint64_t tmask;
+    const FidSlot* fid;
+    uint64_t fid_mask;
+    uint64_t* rec;            // [rule : K bits][request index]
+    uint64_t* rec_sorted;
+    int kshift;
+    uint64_t imask;
+    uint8_t* alive;           // per request: an acquire of this batch whose token is live
+    int* err;
+    int64_t* last_ts;
+};
+
+hipError_t launch_conc_batch(ConcArgs& c, uint64_t* b_buf, uint32_t* hist, hipStream_t stream);
+hipError_t launch_conc_expire(const ConcArgs& c, int64_t now, const uint8_t* online, uint32_t n_clients,
+                              unsigned long long* removed, hipStream_t stream);
+hipError_t launch_conc_count(const ConcArgs& c, unsigned long long* live, hipStream_t stream);
+hipError_t launch_conc_rehash(const CTok* old_tab, uint64_t old_slots, CTok* tab, uint64_t tmask, int* err,
+                              hipStream_t stream);
+
 // ---- local slot chain: StatisticSlot → FlowSlot(DefaultController) → DegradeSlot (local.hip) ----
 constexpr int kLEv = 6;             // MetricEvent PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS
 constexpr int kLPass = 0, kLBlock = 1, kLExc = 2, kLSucc = 3, kLRt = 4, kLOccPass = 5;
@@ -402,11 +452,6 @@ hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ
                            int64_t now, double* out, hipStream_t stream);
 
 // ---- token-server wire codec (codec.hip) ----
-struct FidSlot {      // flowId → rule index, open addressing with linear probing (fid 0 = empty)
-    int64_t fid;
-    uint32_t idx;
-    uint32_t pad;
-};
 
 struct CodecArgs {
     uint64_t n;

@@ -21,6 +21,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
            "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
+           "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
+           "sg_conc_read_state",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
 
 _lib = None
@@ -81,6 +83,11 @@ def load_library():
         "sg_local_read_origin_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
         "sg_local_read_controller": (C.c_int, [vp, u32, vp]),
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
+        "sg_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
+        "sg_conc_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_conc_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_conc_expire": (C.c_int, [vp, i64, vp, u32, C.POINTER(u64)]),
+        "sg_conc_read_state": (C.c_int, [vp, u32, C.POINTER(C.c_int32), C.POINTER(u64)]),
         "sg_codec_encode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
         "sg_pace_load_rules": (C.c_int, [vp, vp, u32]),
         "sg_pace_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
@@ -293,6 +300,31 @@ class FlowEngine:
         out = np.zeros(2 * n_rules, np.float64)
         self._check(self._L.sg_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
         return out.reshape(n_rules, 2)
+
+    # ---- concurrent cluster tokens (requestConcurrentToken / releaseConcurrentToken)
+    def conc_set_rule_timeouts(self, client_offline_ms, resource_timeout_ms):
+        a = np.ascontiguousarray(client_offline_ms, dtype=np.int64)
+        b = np.ascontiguousarray(resource_timeout_ms, dtype=np.int64)
+        self._check(self._L.sg_conc_set_rule_timeouts(self.h, abi.ptr(a), abi.ptr(b), len(a)))
+
+    def conc_decide_host(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.CONC_REQ_DTYPE)
+        out = np.zeros(len(req), abi.CONC_RES_DTYPE)
+        self._check(self._L.sg_conc_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def conc_expire(self, now_ms, online) -> int:
+        online = np.ascontiguousarray(online, dtype=np.uint8)
+        rm = C.c_uint64()
+        self._check(self._L.sg_conc_expire(self.h, now_ms, abi.ptr(online) if len(online) else None, len(online),
+                                           C.byref(rm)))
+        return rm.value
+
+    def conc_state(self, key):
+        """(nowCalls of rule key, live tokens)."""
+        now, live = C.c_int32(), C.c_uint64()
+        self._check(self._L.sg_conc_read_state(self.h, key, C.byref(now), C.byref(live)))
+        return now.value, live.value
 
     # ---- local slot chain (StatisticSlot → FlowSlot/DefaultController → DegradeSlot)
     def local_load_rules(self, rules: np.ndarray, sample_count=2, interval_ms=1000, occupy_timeout_ms=500,

@@ -412,14 +412,51 @@ TokenResult GpuTokenService::requestParamToken(std::optional<int64_t> ruleId, in
     return TokenResult(TokenResultStatus::FAIL);
 }
 
+// DefaultTokenService.requestConcurrentToken (:66-77) → ConcurrentClusterFlowChecker.acquireConcurrentToken on
+// the device (sg_conc_*): one request per call, in arrival order with the other concurrency calls.
 TokenResult GpuTokenService::requestConcurrentToken(const std::string& clientAddress, std::optional<int64_t> ruleId,
                                                     int acquireCount) {
     if (clientAddress.empty() || !ruleId || *ruleId <= 0 || acquireCount <= 0)
         return TokenResult(TokenResultStatus::BAD_REQUEST);  // DefaultTokenService.java:67-70, 91-93
-    return TokenResult(TokenResultStatus::FAIL);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    waitIdle();
+    auto it = clientIds_.find(clientAddress);
+    const uint32_t client = it != clientIds_.end() ? it->second : (clientIds_[clientAddress] = (uint32_t)clientIds_.size() + 1);
+    sg_conc_req r{};
+    r.ts_ms = std::max(lastTs_, opt_.clock());
+    lastTs_ = r.ts_ms;
+    r.kind = SG_CONC_ACQUIRE;
+    r.key = keyOf(ruleId, false);
+    r.acquire = acquireCount;
+    r.client = client;
+    sg_conc_result o{};
+    std::lock_guard<std::mutex> e(engMu_);
+    if (sg_conc_decide_batch_host(h_, &r, 1, &o) != SG_OK) {
+        err_ = sg_last_error(h_);
+        return TokenResult(TokenResultStatus::FAIL);
+    }
+    TokenResult res(o.status);
+    res.setTokenId((int64_t)o.token_id);
+    return res;
 }
 
-void GpuTokenService::releaseConcurrentToken(std::optional<int64_t>) {}
+// DefaultTokenService.releaseConcurrentToken (:79-85): null ids are ignored; the checker's status is dropped
+// as in the reference (the method is void).
+void GpuTokenService::releaseConcurrentToken(std::optional<int64_t> tokenId) {
+    if (!tokenId) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    waitIdle();
+    sg_conc_req r{};
+    r.ts_ms = std::max(lastTs_, opt_.clock());
+    lastTs_ = r.ts_ms;
+    r.kind = SG_CONC_RELEASE;
+    r.token_id = (uint64_t)*tokenId;
+    sg_conc_result o{};
+    std::lock_guard<std::mutex> e(engMu_);
+    if (sg_conc_decide_batch_host(h_, &r, 1, &o) != SG_OK) err_ = sg_last_error(h_);
+}
 
 }  // namespace cluster
 }  // namespace sentinel

@@ -239,6 +239,7 @@ private:
     std::map<std::string, std::vector<int64_t>> nsFlowIds_;   // NAMESPACE_FLOW_ID_MAP
     std::unordered_map<int64_t, RuleEntry> rules_;            // FLOW_RULES + FLOW_NAMESPACE_MAP
     std::unordered_map<int64_t, uint32_t> keyOfFlow_;         // flowId → dense engine key
+    std::unordered_map<std::string, uint32_t> clientIds_;     // client address → sg_conc_req.client (1, 2, …)
 };
 
 }  // namespace cluster

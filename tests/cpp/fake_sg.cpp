@@ -69,4 +69,13 @@ int sg_flow_wait(sg_handle* h, uint64_t ticket) {
     const int r = sg_flow_poll(h, ticket);
     return r == 1 ? SG_OK : r;
 }
+int sg_conc_decide_batch_host(sg_handle*, const sg_conc_req* req, uint64_t n, sg_conc_result* out) {
+    std::lock_guard<std::mutex> lk(fake::mu);
+    for (uint64_t i = 0; i < n; ++i) {  // acquire: OK with token id 100 + client; release: RELEASE_OK
+        out[i].status = req[i].kind == SG_CONC_ACQUIRE ? SG_STATUS_OK : SG_STATUS_RELEASE_OK;
+        out[i].reserved = 0;
+        out[i].token_id = req[i].kind == SG_CONC_ACQUIRE ? 100 + req[i].client : 0;
+    }
+    return SG_OK;
+}
 }

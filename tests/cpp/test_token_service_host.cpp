@@ -110,10 +110,19 @@ int main() {
     auto failed = svc.requestTokens({{now + 3, 30, 1, false}, {now + 3, 10, 1, false}});
     CHECK(failed[0].getStatus().value() == TokenResultStatus::FAIL && failed[1].getStatus().value() == TokenResultStatus::FAIL);
 
-    // --- param / concurrent tokens are not on the device path: validation, then FAIL
+    // --- param tokens are not on this device path: validation, then FAIL
     CHECK(svc.requestParamToken(30, 1, {}).getStatus().value() == TokenResultStatus::BAD_REQUEST);
     CHECK(svc.requestParamToken(30, 1, {"x"}).getStatus().value() == TokenResultStatus::FAIL);
+    // --- concurrent tokens: validation, then sg_conc_* with a dense client id per address
     CHECK(svc.requestConcurrentToken("", 30, 1).getStatus().value() == TokenResultStatus::BAD_REQUEST);
+    CHECK(svc.requestConcurrentToken("10.0.0.1", 30, 0).getStatus().value() == TokenResultStatus::BAD_REQUEST);
+    TokenResult c1 = svc.requestConcurrentToken("10.0.0.1", 30, 1);
+    TokenResult c2 = svc.requestConcurrentToken("10.0.0.2", 30, 1);
+    TokenResult c3 = svc.requestConcurrentToken("10.0.0.1", 30, 1);
+    CHECK(c1.getStatus().value() == TokenResultStatus::OK && c1.getTokenId() == 101);
+    CHECK(c2.getTokenId() == 102 && c3.getTokenId() == 101);
+    svc.releaseConcurrentToken(c1.getTokenId());
+    svc.releaseConcurrentToken(std::nullopt);
 
     // --- concurrent requestToken: micro-batched, every caller answered, timestamps non-decreasing
     fake::batches.clear();
