@@ -436,6 +436,15 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
 int sg_cparam_decide_batch_host(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
                                 uint64_t n_values, sg_result* out);
 int sg_cparam_read_sum(sg_handle* h, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum);
+/*   sg_cparam_top_values ← ClusterParamMetric.getTopValues(number) (…/metric/ClusterParamMetric.java:90-133), the
+ *                          topParams of ClusterMetricNodeGenerator.paramToMetricNode (:88-104): per rule up to
+ *                          `number` values with the largest window sums at now_ms (count / intervalSec), zero sums
+ *                          excluded; ties by ascending value (the reference's order among equal counts is HashMap
+ *                          order). values / qps: n_rules * number entries, HOST memory; counts[r] = entries of rule
+ *                          r. Without currentWindow's side effect. Like sg_cparam_read_sum, exact for now_ms at or
+ *                          after the latest decided request (the metricList task's current time): the device keeps a
+ *                          ring per (rule, value), which equals the reference's bucket maps from that time on. */
+int sg_cparam_top_values(sg_handle* h, int64_t now_ms, uint32_t number, uint64_t* values, double* qps, uint32_t* counts);
 
 /* ---- local slot chain (the ProcessorSlot chain's statistic / flow / degrade slots, batched) ----
  *   sg_local_load_rules    ← FlowRuleManager.loadRules + DegradeRuleManager.loadRules for one resource each
@@ -470,6 +479,25 @@ int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* bo
  *   sg_local_read_controller   ← the controller of input rule i: {storedTokens, lastFilledTime, latestPassedTime};
  *                              SG_E_INVAL for an ignored rule. */
 int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins);
+
+/* ---- metric snapshots ----
+ *   sg_local_metrics ← MetricTimerListener.run (core/.../node/metric/MetricTimerListener.java:40-69) over every
+ *                      resource's ClusterNode: StatisticNode.metrics() (StatisticNode.java:116-133) at now_ms — the
+ *                      minute window's buckets (ArrayMetric.details, :156-204, with currentWindow's side effect) newer
+ *                      than the node's lastFetchTime and older than now's second, non-empty; lastFetchTime advances.
+ *                      Rows sorted by (timestamp, resource) into HOST memory; *n_rows = the number of rows (with
+ *                      SG_E_CAPACITY and no side effect when cap is too small). The host formats them as metrics.log
+ *                      lines (MetricNode.toFatString, MetricNode.java:213-229; sentinel_amd/metrics.py). The
+ *                      ENTRY_NODE aggregate (__total_inbound_traffic__) is not kept on the device. */
+typedef struct sg_metric_node {
+    int64_t  timestamp;
+    int64_t  pass_qps, block_qps, success_qps, exception_qps;
+    int64_t  rt;                  /* rt / success when success != 0, else the raw rt sum (ArrayMetric.fromBucket) */
+    int64_t  occupied_pass_qps;
+    uint32_t resource;
+    int32_t  concurrency;         /* 0, as fromBucket leaves it */
+} sg_metric_node;
+int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows);
 int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64_t* second, int64_t* borrow,
                                int64_t* minute, int64_t* head);
 int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);

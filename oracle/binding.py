@@ -90,6 +90,9 @@ def lib():
         "or_local_origin_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
         "or_local_controller": (C.c_int, [vp, u32, vp]),
         "or_local_rule_order": (C.c_int, [vp, u32, vp, u32]),
+        "or_local_metrics": (i64, [vp, i64, vp, u64]),
+        "or_cts_param_top": (C.c_int, [vp, u32, i64, C.c_int, vp, vp]),
+        "or_cpm_top": (C.c_int, [vp, i64, C.c_int, vp, vp]),
         "or_conc_new": (vp, []), "or_conc_free": (None, [vp]),
         "or_conc_set_namespaces": (C.c_int, [vp, vp, u32]), "or_conc_load_rules": (C.c_int, [vp, vp, u32]),
         "or_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
@@ -291,6 +294,14 @@ class ClusterTokenService:
     def param_sum(self, key, value, now):
         return lib().or_cts_param_sum(self.h, key, int(value), now)
 
+    def param_top(self, key, now, number=5):
+        """ClusterParamMetric.getTopValues(number): [(value, qps), ...] by count, ties by value."""
+        vals = np.zeros(number, np.uint64)
+        qps = np.zeros(number, np.float64)
+        k = lib().or_cts_param_top(self.h, key, now, number, abi.ptr(vals), abi.ptr(qps))
+        assert k >= 0
+        return [(int(vals[i]), float(qps[i])) for i in range(k)]
+
     def export_state(self, n_rules, stride):
         """(ring [K][stride][8] {start, 7 counters}, occ [K][2]) — same layout as FlowEngine.export_state."""
         ring = np.zeros((n_rules, stride, 8), np.int64)
@@ -423,6 +434,15 @@ class ClusterParamMetric:
 
     def get_avg(self, t, value):
         return lib().or_cpm_get_avg(self.h, t, int(value))
+
+    def top_values(self, t, number):
+        """getTopValues(number) → {value: qps}; raises for number <= 0 (AssertUtil)."""
+        vals = np.zeros(max(1, number), np.uint64)
+        qps = np.zeros(max(1, number), np.float64)
+        k = lib().or_cpm_top(self.h, t, number, abi.ptr(vals), abi.ptr(qps))
+        if k < 0:
+            raise ValueError("number must be positive")
+        return {int(vals[i]): float(qps[i]) for i in range(k)}
 
 
 class ParamFlowChecker:
@@ -626,6 +646,14 @@ class LocalChain:
         rc = lib().or_local_origin_dump(self.h, res, origin, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), C.byref(th))
         assert rc >= 0
         return sec, bor, mnt, th.value, rc == 1
+
+    def metrics(self, now):
+        """StatisticNode.metrics() rows of every resource at now (MetricTimerListener.run), time-sorted."""
+        n = int(lib().or_local_metrics(self.h, now, None, 0))
+        out = np.zeros(max(1, n), abi.METRIC_NODE_DTYPE)
+        m = int(lib().or_local_metrics(self.h, now, abi.ptr(out), len(out)))
+        assert m == n
+        return out[:n]
 
     def rule_order(self, res):
         out = np.zeros(256, np.int32)

@@ -896,6 +896,7 @@ struct or_local {
     int S, interval, occupy_timeout, cold_factor;
     or_node* nodes;
     uint32_t n;
+    int64_t* last_fetch;     /* StatisticNode.lastFetchTime per resource (metrics()) */
     int32_t n_origins;
     int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
     uint32_t n_rules;
@@ -941,6 +942,8 @@ static void free_nodes(or_local* l) {
     }
     free(l->nodes);
     free(l->rule_pos);
+    free(l->last_fetch);
+    l->last_fetch = NULL;
     l->rule_pos = NULL;
     l->n_rules = 0;
     l->nodes = NULL;
@@ -2184,3 +2187,117 @@ uint64_t or_conc_expire(or_conc* c, int64_t now, const uint8_t* online, uint32_t
 
 int32_t or_conc_now_calls(const or_conc* c, uint32_t k) { return k < c->n ? c->now_calls[k] : 0; }
 uint64_t or_conc_live(const or_conc* c) { return c->live; }
+
+/* ===================================================================================== */
+/* Metric snapshots: StatisticNode.metrics() rows (core/.../node/StatisticNode.java:116-147 over             */
+/* ArrayMetric.details, ArrayMetric.java:156-204) and ClusterParamMetric.getTopValues (…/ClusterParamMetric.java: */
+/* 90-133).                                                                                                      */
+/* ===================================================================================== */
+
+static int metric_row_less(const sg_metric_node* a, const sg_metric_node* b) {
+    return a->timestamp != b->timestamp ? a->timestamp < b->timestamp : a->resource < b->resource;
+}
+
+/* MetricTimerListener.run over every resource: rows sorted by (timestamp, resource); returns the number of rows
+ * (all of them are written when cap allows; lastFetchTime advances only then). */
+int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap) {
+    if (!l->last_fetch) {
+        l->last_fetch = (int64_t*)malloc((l->n ? l->n : 1) * sizeof(int64_t));
+        for (uint32_t k = 0; k < l->n; k++) l->last_fetch[k] = -1;
+    }
+    const int64_t cur = now - now % 1000;
+    uint64_t rows = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        rows = 0;
+        for (uint32_t k = 0; k < l->n; k++) {
+            or_leap* m = l->nodes[k].minute;
+            if (pass == 1) or_leap_current_window(m, now);           /* data.currentWindow() */
+            int64_t newest = l->last_fetch[k];
+            for (int j = 0; j < m->S; j++) {                        /* data.list(): not deprecated at now */
+                if (!m->present[j] || is_deprecated(m, now, &m->b[j])) continue;
+                const or_bucket* b = &m->b[j];
+                if (!(b->start > l->last_fetch[k] && b->start < cur)) continue;   /* isNodeInTime */
+                const int64_t succ = b->c[OR_M_SUCCESS];
+                const int64_t rt = succ != 0 ? b->c[OR_M_RT] / succ : b->c[OR_M_RT];
+                if (!(b->c[OR_M_PASS] > 0 || b->c[OR_M_BLOCK] > 0 || succ > 0 || b->c[OR_M_EXCEPTION] > 0 || rt > 0 ||
+                      b->c[OR_M_OCCUPIED_PASS] > 0))
+                    continue;                                       /* isValidMetricNode */
+                if (pass == 1) {
+                    sg_metric_node* r = &out[rows];
+                    r->timestamp = b->start;
+                    r->pass_qps = b->c[OR_M_PASS];
+                    r->block_qps = b->c[OR_M_BLOCK];
+                    r->success_qps = succ;
+                    r->exception_qps = b->c[OR_M_EXCEPTION];
+                    r->rt = rt;
+                    r->occupied_pass_qps = b->c[OR_M_OCCUPIED_PASS];
+                    r->resource = k;
+                    r->concurrency = 0;
+                    if (b->start > newest) newest = b->start;
+                }
+                rows++;
+            }
+            if (pass == 1) l->last_fetch[k] = newest;
+        }
+        if (pass == 0 && rows > cap) return (int64_t)rows;
+    }
+    for (uint64_t i = 1; i < rows; i++) {                           /* insertion sort by (timestamp, resource) */
+        sg_metric_node x = out[i];
+        uint64_t j = i;
+        while (j > 0 && metric_row_less(&x, &out[j - 1])) {
+            out[j] = out[j - 1];
+            j--;
+        }
+        out[j] = x;
+    }
+    return (int64_t)rows;
+}
+
+typedef struct { uint64_t v; int64_t c; } or_topent;
+
+static int topent_cmp(const void* x, const void* y) {
+    const or_topent* a = (const or_topent*)x;
+    const or_topent* b = (const or_topent*)y;
+    const int32_t ca = (int32_t)a->c, cb = (int32_t)b->c;   /* the comparator compares (int) casts */
+    if (ca != cb) return ca > cb ? -1 : 1;
+    return a->v < b->v ? -1 : (a->v > b->v ? 1 : 0);          /* ties: value order (HashMap order in Java) */
+}
+
+/* ClusterParamMetric.getTopValues(number) at now: values[] / qps[] get up to `number` entries. */
+int or_cpm_top(or_cpm* m, int64_t now, int number, uint64_t* values, double* qps) {
+    if (number <= 0) return SG_E_INVAL;   /* AssertUtil.isTrue(number > 0) */
+    cpm_current_window(m, now);
+    uint64_t cap = 0, n = 0;
+    for (int i = 0; i < m->S; i++) cap += m->maps[i].n;
+    or_topent* e = (or_topent*)malloc((cap ? cap : 1) * sizeof(or_topent));
+    for (int i = 0; i < m->S; i++) {                                /* merge the valid buckets' maps */
+        if (!m->present[i] || now - m->start[i] > m->interval) continue;
+        const or_vmap* mp = &m->maps[i];
+        for (uint32_t j = 0; j < mp->cap; j++) {
+            if (!mp->used[j]) continue;
+            uint64_t x = 0;
+            while (x < n && e[x].v != mp->k[j]) x++;
+            if (x == n) {
+                e[n].v = mp->k[j];
+                e[n].c = 0;
+                n++;
+            }
+            e[x].c += mp->v[j];
+        }
+    }
+    qsort(e, n, sizeof(or_topent), topent_cmp);
+    int k = 0;
+    for (uint64_t i = 0; i < n && k < number; i++) {
+        if (e[i].c == 0) break;
+        values[k] = e[i].v;
+        qps[k] = (double)e[i].c / m->isec;
+        k++;
+    }
+    free(e);
+    return k;
+}
+
+int or_cts_param_top(or_cts* s, uint32_t key, int64_t now, int number, uint64_t* values, double* qps) {
+    if (key >= s->n_prules) return SG_E_INVAL;
+    return or_cpm_top(s->prules[key].metric, now, number, values, qps);
+}

@@ -182,6 +182,14 @@ uint64_t  or_lgen_pending(const or_lgen* g);
 uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
                       int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
 
+/* ---------- metric snapshots ---------- */
+/* StatisticNode.metrics() of every resource at now (MetricTimerListener.run), sorted by (timestamp, resource);
+ * returns the number of rows (written only when <= cap). */
+int64_t  or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap);
+/* ClusterParamMetric.getTopValues(number) of cluster param rule key at now; returns the entries written. */
+int      or_cts_param_top(or_cts* s, uint32_t key, int64_t now, int number, uint64_t* values, double* qps);
+int      or_cpm_top(or_cpm* m, int64_t now, int number, uint64_t* values, double* qps);
+
 /* ---------- concurrent cluster tokens (ConcurrentClusterFlowChecker + TokenCacheNodeManager) ---------- */
 typedef struct or_conc or_conc;
 or_conc* or_conc_new(void);

@@ -98,6 +98,11 @@ CPARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4"
 BEHAVIOR_DEFAULT = 0
 BEHAVIOR_RATE_LIMITER = 2
 
+# metric snapshots (sg_local_metrics)
+METRIC_NODE_DTYPE = np.dtype([("timestamp", "<i8"), ("pass_qps", "<i8"), ("block_qps", "<i8"), ("success_qps", "<i8"),
+                              ("exception_qps", "<i8"), ("rt", "<i8"), ("occupied_pass_qps", "<i8"),
+                              ("resource", "<u4"), ("concurrency", "<i4")], align=True)
+
 # concurrent cluster tokens (sg_conc_*)
 CONC_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("token_id", "<u8"), ("key", "<u4"), ("acquire", "<i4"),
                            ("client", "<u4"), ("kind", "<i4")], align=True)
@@ -141,6 +146,7 @@ assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 assert LOCAL_FLOW_RULE_DTYPE.itemsize == 40
 assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
+assert METRIC_NODE_DTYPE.itemsize == 64
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:

@@ -120,6 +120,7 @@ struct sg_handle {
     std::vector<int64_t> l_rule_slot; // loaded flow rule i → its LCtl index, -2 stateless fast-path rule, -1 ignored
     LFlowRule* d_lfrules = nullptr;
     LCtl* d_lctl = nullptr;
+    int64_t* d_llast_fetch = nullptr; // [K] StatisticNode.lastFetchTime
     LRule* d_lrules = nullptr;
     LHead* d_lhead = nullptr;
     LBucket* d_lsec = nullptr;
@@ -436,6 +437,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lrules);
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
+    dfree(h->d_llast_fetch);
     dfree(h->d_cnow);
     dfree(h->d_cthr);
     dfree(h->d_coff);
@@ -1528,6 +1530,47 @@ int sg_cparam_read_sum(sg_handle* h, uint32_t rule, uint64_t value, int64_t now_
     return SG_OK;
 }
 
+int sg_cparam_top_values(sg_handle* h, int64_t now_ms, uint32_t number, uint64_t* values, double* qps, uint32_t* counts) {
+    if (!h || number == 0 || (!h->cptab.empty() && (!values || !qps || !counts))) return SG_E_INVAL;
+    const uint32_t R = (uint32_t)h->cptab.size();
+    if (R == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    CPArgs c = cp_args(h, nullptr, 0, nullptr, 0, nullptr);
+    const uint64_t per = h->cptotal / R;
+    CPTop* d_top = nullptr;
+    unsigned long long* d_cnt = nullptr;
+    if (hipMalloc(&d_top, sizeof(CPTop) * h->cptotal) != hipSuccess || hipMalloc(&d_cnt, sizeof(unsigned long long)) != hipSuccess) {
+        dfree(d_top);
+        return fail(h, SG_E_NOMEM, "top values buffer");
+    }
+    unsigned long long cnt = 0;
+    hipError_t e = hipMemset(d_cnt, 0, sizeof(cnt));
+    if (e == hipSuccess) e = launch_cp_top(c, now_ms, per, d_top, d_cnt, 0);
+    if (e == hipSuccess) e = hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost);
+    std::vector<CPTop> top(cnt);
+    if (e == hipSuccess && cnt) e = hipMemcpy(top.data(), d_top, sizeof(CPTop) * cnt, hipMemcpyDeviceToHost);
+    (void)hipFree(d_top);
+    (void)hipFree(d_cnt);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    // per rule: count descending (the reference compares (int) casts of the counts), ties by value
+    std::sort(top.begin(), top.end(), [](const CPTop& a, const CPTop& b) {
+        if (a.rule != b.rule) return a.rule < b.rule;
+        const int32_t ca = (int32_t)a.sum, cb = (int32_t)b.sum;
+        if (ca != cb) return ca > cb;
+        return a.value < b.value;
+    });
+    std::fill(counts, counts + R, 0u);
+    for (const CPTop& t : top) {
+        uint32_t& k = counts[t.rule];
+        if (k >= number) continue;
+        values[(size_t)t.rule * number + k] = t.value;
+        qps[(size_t)t.rule * number + k] = (double)t.sum / h->cptab[t.rule].isec;  // count / getIntervalInSecond
+        ++k;
+    }
+    return SG_OK;
+}
+
 // ------------------------------------------------------------------------------ local slot chain
 
 int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local_rule* rules, uint32_t n) {
@@ -1607,8 +1650,55 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
         L.bor = h->d_lbor;
         L.minute = h->d_lmin;
         HIP_TRY(h, launch_local_init(L, 0));
+        dfree(h->d_llast_fetch);
+        if (hipMalloc(&h->d_llast_fetch, sizeof(int64_t) * n) != hipSuccess) return fail(h, SG_E_NOMEM, "lastFetchTime");
+        std::vector<int64_t> neg1(n, -1);  // StatisticNode.lastFetchTime = -1
+        HIP_TRY(h, hipMemcpy(h->d_llast_fetch, neg1.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, hipDeviceSynchronize());
     }
+    return SG_OK;
+}
+
+int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows) {
+    if (!h || !n_rows || (!out && cap)) return SG_E_INVAL;
+    *n_rows = 0;
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    if (h->ltab.empty()) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    LArgs L{};
+    L.K = (uint32_t)h->ltab.size();
+    L.minute = h->d_lmin;
+    L.last_fetch = h->d_llast_fetch;
+    unsigned long long* d_cnt = nullptr;
+    HIP_TRY(h, hipMalloc(&d_cnt, sizeof(unsigned long long)));
+    unsigned long long cnt = 0;
+    hipError_t e = hipMemset(d_cnt, 0, sizeof(cnt));
+    if (e == hipSuccess) e = launch_local_metrics(L, now_ms, nullptr, d_cnt, 0, 0);
+    if (e == hipSuccess) e = hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        (void)hipFree(d_cnt);
+        return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    }
+    *n_rows = cnt;
+    if (cnt > cap) {
+        (void)hipFree(d_cnt);
+        return fail(h, SG_E_CAPACITY, "metric row buffer too small (*n_rows rows)");
+    }
+    sg_metric_node* d_out = nullptr;
+    if (cnt && hipMalloc(&d_out, sizeof(sg_metric_node) * cnt) != hipSuccess) {
+        (void)hipFree(d_cnt);
+        return fail(h, SG_E_NOMEM, "metric rows");
+    }
+    e = hipMemset(d_cnt, 0, sizeof(cnt));
+    if (e == hipSuccess) e = launch_local_metrics(L, now_ms, d_out, d_cnt, 1, 0);
+    if (e == hipSuccess && cnt) e = hipMemcpy(out, d_out, sizeof(sg_metric_node) * cnt, hipMemcpyDeviceToHost);
+    (void)hipFree(d_cnt);
+    if (d_out) (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    std::sort(out, out + cnt, [](const sg_metric_node& a, const sg_metric_node& b) {  // the listener's TreeMap by time
+        return a.timestamp != b.timestamp ? a.timestamp < b.timestamp : a.resource < b.resource;
+    });
     return SG_OK;
 }
 

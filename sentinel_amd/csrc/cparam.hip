@@ -293,6 +293,29 @@ __global__ void k_cp_read(CPArgs c, uint32_t rule, uint64_t value, int64_t now, 
     *out = other + cur;
 }
 
+// ClusterParamMetric.getTopValues: every (rule, value) with a positive window sum at now, appended in any order
+// (the host picks each rule's top entries). per = slots per rule (all rules share one table size).
+__global__ void __launch_bounds__(256) k_cp_top(CPArgs c, int64_t now, uint64_t per, CPTop* out,
+                                                unsigned long long* count) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < c.total_slots;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t rule = (uint32_t)(g / per);
+        const CPRule r = c.rules[rule];
+        const bool side = g == r.table_base + r.table_mask + 1;  // the slot of the value ~0
+        const uint64_t v = side ? kCpEmpty : c.keys[g];
+        if (!side && v == kCpEmpty) continue;
+        int64_t cur = 0;
+        const int64_t sum = cp_window(c.ring + g * (uint64_t)c.stride, r.S, r.wl, now / r.wl, &cur) + cur;
+        if (sum <= 0) continue;
+        CPTop t;
+        t.value = v;
+        t.sum = sum;
+        t.rule = rule;
+        t.pad = 0;
+        out[atomicAdd(count, 1ull)] = t;
+    }
+}
+
 static unsigned cgrid(uint64_t n, unsigned cap) {
     uint64_t g = (n + 255) / 256;
     if (g < 1) g = 1;
@@ -315,6 +338,13 @@ hipError_t launch_cp_copy(const uint64_t* okeys, const CPBucket* oring, uint64_t
 
 hipError_t launch_cp_read(const CPArgs& c, uint32_t rule, uint64_t value, int64_t now, int64_t* out_dev, hipStream_t stream) {
     hipLaunchKernelGGL(k_cp_read, dim3(1), dim3(1), 0, stream, c, rule, value, now, out_dev);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out, unsigned long long* count,
+                         hipStream_t stream) {
+    if (c.total_slots == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cp_top, dim3(cgrid(c.total_slots, 8192)), dim3(256), 0, stream, c, now, per, out, count);
     return hipGetLastError();
 }
 

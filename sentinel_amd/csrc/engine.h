@@ -257,6 +257,14 @@ hipError_t launch_cp_range(const CPArgs& c, BatchArgs& sg, uint64_t lo, uint64_t
                            uint32_t* hist, int lo_bit, int hi_bit, hipStream_t stream);
 hipError_t launch_cp_multi(const CPArgs& c, uint64_t m, hipStream_t stream);
 hipError_t launch_cp_read(const CPArgs& c, uint32_t rule, uint64_t value, int64_t now, int64_t* out_dev, hipStream_t stream);
+struct CPTop {                // a (rule, value) window sum for ClusterParamMetric.getTopValues
+    uint64_t value;
+    int64_t sum;
+    uint32_t rule;
+    uint32_t pad;
+};
+hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out, unsigned long long* count,
+                         hipStream_t stream);
 
 struct FidSlot {      // flowId → rule index, open addressing with linear probing (fid 0 = empty)
     int64_t fid;
@@ -420,6 +428,7 @@ struct LArgs {
     struct LSkip* skips;      // dead-period ranges handed to k_lskip_apply
     uint32_t* skip_count;
     uint32_t skip_cap;
+    int64_t* last_fetch;      // [K] StatisticNode.lastFetchTime (metric rows already reported)
 };
 
 constexpr int kLFlagPrio = 1;    // some entry is prioritized (may occupy in a saturated window)
@@ -434,6 +443,10 @@ hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
 hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
+// StatisticNode.metrics() of every resource at now: emit == 0 counts the rows (no side effect), emit == 1 writes
+// them (any order) and applies currentWindow / lastFetchTime.
+hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
+                                hipStream_t stream);
 
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);

@@ -1258,6 +1258,54 @@ __global__ void k_local_finish(LArgs a) {
     if (*a.err == 0 && a.n > 0) *a.last_ts = a.ev[a.n - 1].ts_ms;
 }
 
+// ------------------------------------------------------------------------------- metric rows
+
+// StatisticNode.metrics() at now (StatisticNode.java:116-147, ArrayMetric.details / fromBucket :156-204), one
+// thread per resource over its 60 minute buckets.
+__global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_metric_node* out,
+                                                       unsigned long long* count, int emit) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.K; k += (uint64_t)gridDim.x * blockDim.x) {
+        LBucket* m = a.minute + k * kMinuteS;
+        const int64_t cur = now - now % 1000;
+        // data.currentWindow(now): an absent or stale bucket in now's slot becomes an empty one
+        const int I = (int)((now / kMinuteWl) % kMinuteS);
+        if (emit && (m[I].start == INT64_MIN || m[I].start < cur)) {
+            LBucket b;
+            b.start = cur;
+            for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+            b.min_rt = kStatMaxRt;
+            m[I] = b;
+        }
+        const int64_t last = a.last_fetch[k];
+        int64_t newest = last;
+        uint32_t rows = 0;
+        for (int j = 0; j < kMinuteS; ++j) {  // data.list(now): present and not deprecated
+            const LBucket b = m[j];
+            if (b.start == INT64_MIN || now - b.start > (int64_t)kMinuteS * kMinuteWl) continue;
+            if (!(b.start > last && b.start < cur)) continue;  // isNodeInTime
+            const int64_t pass = b.c[kLPass], block = b.c[kLBlock], succ = b.c[kLSucc], exc = b.c[kLExc];
+            const int64_t rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
+            if (!(pass > 0 || block > 0 || succ > 0 || exc > 0 || rt > 0 || b.c[kLOccPass] > 0)) continue;
+            newest = b.start > newest ? b.start : newest;
+            ++rows;
+            if (!emit) continue;
+            sg_metric_node r;
+            r.timestamp = b.start;
+            r.pass_qps = pass;
+            r.block_qps = block;
+            r.success_qps = succ;
+            r.exception_qps = exc;
+            r.rt = rt;
+            r.occupied_pass_qps = b.c[kLOccPass];
+            r.resource = (uint32_t)k;
+            r.concurrency = 0;
+            out[atomicAdd(count, 1ull)] = r;
+        }
+        if (!emit && rows) atomicAdd(count, (unsigned long long)rows);
+        if (emit) a.last_fetch[k] = newest;
+    }
+}
+
 // ---------------------------------------------------------------------------------- launchers
 
 static unsigned lgrid(uint64_t n, unsigned block, unsigned cap) {
@@ -1277,6 +1325,13 @@ static unsigned lresident(const void* kernel) {
 
 hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_local_prep, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
+                                hipStream_t stream) {
+    if (a.K == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit);
     return hipGetLastError();
 }
 

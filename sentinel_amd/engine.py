@@ -22,7 +22,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
-           "sg_conc_read_state",
+           "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
 
 _lib = None
@@ -84,6 +84,8 @@ def load_library():
         "sg_local_read_controller": (C.c_int, [vp, u32, vp]),
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "sg_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
+        "sg_local_metrics": (C.c_int, [vp, i64, vp, u64, C.POINTER(u64)]),
+        "sg_cparam_top_values": (C.c_int, [vp, i64, u32, vp, vp, vp]),
         "sg_conc_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_conc_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_conc_expire": (C.c_int, [vp, i64, vp, u32, C.POINTER(u64)]),
@@ -355,6 +357,16 @@ class FlowEngine:
         self._check(self._L.sg_local_read_state(self.h, res, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), abi.ptr(head)))
         return sec, bor, mnt, head
 
+    def local_metrics(self, now_ms) -> np.ndarray:
+        """MetricTimerListener.run: every resource's new minute-bucket rows (sg_metric_node), time-sorted."""
+        n = C.c_uint64()
+        rc = self._L.sg_local_metrics(self.h, now_ms, None, 0, C.byref(n))
+        if rc not in (0, abi.SG_E_CAPACITY):
+            self._check(rc)
+        out = np.zeros(max(1, n.value), abi.METRIC_NODE_DTYPE)
+        self._check(self._L.sg_local_metrics(self.h, now_ms, abi.ptr(out), len(out), C.byref(n)))
+        return out[:n.value]
+
     def local_load_flow_rules(self, rules: np.ndarray, n_origins=0) -> int:
         """FlowRuleManager.loadRules for the local chain: returns the number of rules kept."""
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
@@ -392,6 +404,15 @@ class FlowEngine:
         self._check(self._L.sg_cparam_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(values), len(values),
                                                          abi.ptr(out)))
         return out
+
+    def cparam_top_values(self, now_ms, n_rules, number=5):
+        """ClusterParamMetric.getTopValues(number) of every cluster param rule: list of [(value, qps), ...]."""
+        vals = np.zeros(n_rules * number, np.uint64)
+        qps = np.zeros(n_rules * number, np.float64)
+        cnt = np.zeros(max(1, n_rules), np.uint32)
+        self._check(self._L.sg_cparam_top_values(self.h, now_ms, number, abi.ptr(vals), abi.ptr(qps), abi.ptr(cnt)))
+        return [[(int(vals[r * number + i]), float(qps[r * number + i])) for i in range(int(cnt[r]))]
+                for r in range(n_rules)]
 
     def cparam_sum(self, rule, value, now):
         v = C.c_int64()
