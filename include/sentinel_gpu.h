@@ -161,6 +161,57 @@ typedef struct sg_param_req {
     int32_t  acquire;           /* acquireCount                                                    */
 } sg_param_req;
 
+/* ---- ParamFlowSlot: every param rule of a resource, collection/array arguments, THREAD grade ----
+ * SphU.entry(resource, count, args...) through ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93): the resource's
+ * rules in load order (the first failing one throws ParamFlowException), each on args[paramIdx]
+ * (ParamFlowChecker.passCheck :48-73): no argument or a null one passes, a collection / array is checked element by
+ * element in order with the state changes of the elements before a failing one kept (passLocalCheck :75-104),
+ * QPS rules through the token bucket / throttle of sg_param_*, THREAD rules against the per-(resource, paramIdx,
+ * value) thread counts (passSingleValueCheck :114-122) that ParamFlowStatisticEntryCallback / ExitCallback keep
+ * (ParameterMetric.addThreadCount / decreaseThreadCount :125-239). Rules are sg_param_rule plus the fields below;
+ * a negative paramIdx is resolved against the first call's argument count and then kept (applyRealParamIdx
+ * :57-64). Resources with several rules and collection arguments are walked one event at a time per resource. */
+#define SG_ARG_NULL        0
+#define SG_ARG_VALUE       1
+#define SG_ARG_COLLECTION  2
+typedef struct sg_pslot_rule {
+    sg_param_rule rule;          /* token bucket / throttle parameters, hot items                          */
+    uint32_t      resource;      /* resource index                                                         */
+    int32_t       param_idx;     /* ParamFlowRule.paramIdx                                                 */
+    int32_t       grade;         /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS                                 */
+    int32_t       reserved;
+} sg_pslot_rule;
+typedef struct sg_pslot_arg {    /* one argument: null, a value, or a collection / array of values        */
+    uint32_t value_begin;
+    uint32_t value_count;
+    int32_t  kind;               /* SG_ARG_*                                                              */
+    int32_t  reserved;
+} sg_pslot_arg;
+typedef struct sg_pslot_event {  /* an entry (SphU.entry) or the exit of a passed entry (its own arguments) */
+    int64_t  ts_ms;
+    uint32_t resource;
+    int32_t  count;              /* acquireCount                                                          */
+    int32_t  kind;               /* SG_LOCAL_ENTRY / SG_LOCAL_EXIT                                         */
+    uint32_t arg_begin;          /* args[arg_begin .. + arg_count)                                         */
+    uint32_t arg_count;
+    int32_t  args_null;          /* 1: the Object[] args itself is null (checkFlow returns at once)         */
+} sg_pslot_event;
+typedef struct sg_pslot_result {
+    int32_t pass;                /* entries: 1 pass / 0 ParamFlowException; exits: 1                       */
+    int32_t rule;                /* the rule that threw (index into the loaded rules), else -1              */
+} sg_pslot_result;
+/* Loads the rules (state of sg_param_* starts empty, as for sg_param_load_rules). */
+int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                        uint32_t n_hot, uint32_t n_resources);
+/* A time-ordered batch; events, args, values and results are DEVICE pointers (asynchronous on stream). */
+int sg_pslot_decide_batch(sg_handle* h, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
+                          uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_pslot_result* out, void* stream);
+int sg_pslot_decide_batch_host(sg_handle* h, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
+                               uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_pslot_result* out);
+/* ParameterMetric.getThreadCount(paramIdx, value) of a resource, and a rule's current paramIdx. */
+int sg_pslot_thread_count(sg_handle* h, uint32_t resource, int32_t param_idx, uint64_t value, int64_t* count);
+int sg_pslot_param_idx(sg_handle* h, uint32_t rule, int32_t* param_idx);
+
 /* ---- pace controller: FlowRule with CONTROL_BEHAVIOR_RATE_LIMITER (RateLimiterController) ---- */
 
 /* One FlowRule whose controller is RateLimiterController(maxQueueingTimeMs, count)

@@ -93,6 +93,12 @@ def lib():
         "or_local_metrics": (i64, [vp, i64, vp, u64]),
         "or_cts_param_top": (C.c_int, [vp, u32, i64, C.c_int, vp, vp]),
         "or_cpm_top": (C.c_int, [vp, i64, C.c_int, vp, vp]),
+        "or_pslot_new": (vp, []), "or_pslot_free": (None, [vp]),
+        "or_pslot_load_rules": (C.c_int, [vp, vp, u32, vp, u32, u32]),
+        "or_pslot_decide": (C.c_int, [vp, vp, u64, vp, vp, vp]),
+        "or_pslot_thread_count": (i64, [vp, u32, C.c_int32, u64]),
+        "or_pslot_param_idx": (C.c_int32, [vp, u32]),
+        "or_pslot_token_state": (C.c_int, [vp, u32, u64, vp, vp]),
         "or_conc_new": (vp, []), "or_conc_free": (None, [vp]),
         "or_conc_set_namespaces": (C.c_int, [vp, vp, u32]), "or_conc_load_rules": (C.c_int, [vp, vp, u32]),
         "or_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
@@ -370,6 +376,43 @@ class ShardedClusterTokenService:
 
     def close(self):
         self.pool.shutdown()
+
+
+class ParamFlowSlot:
+    """Sequential replay of ParamFlowSlot.checkFlow over every param rule of a resource (collection / array
+    arguments, THREAD grade, negative paramIdx resolution)."""
+
+    def __init__(self, rules, hot=None, n_resources=None):
+        self.h = lib().or_pslot_new()
+        rules = np.ascontiguousarray(rules, dtype=abi.PSLOT_RULE_DTYPE).reshape(-1)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        n_res = int(rules["resource"].max()) + 1 if n_resources is None else n_resources
+        lib().or_pslot_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot) if len(hot) else None, len(hot), n_res)
+
+    def __del__(self):
+        if self.h:
+            lib().or_pslot_free(self.h)
+            self.h = None
+
+    def decide(self, ev, args, values):
+        ev = np.ascontiguousarray(ev, dtype=abi.PSLOT_EVENT_DTYPE).reshape(-1)
+        args = np.ascontiguousarray(args, dtype=abi.PSLOT_ARG_DTYPE).reshape(-1)
+        values = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1)
+        out = np.zeros(len(ev), abi.PSLOT_RES_DTYPE)
+        lib().or_pslot_decide(self.h, abi.ptr(ev), len(ev), abi.ptr(args) if len(args) else None,
+                              abi.ptr(values) if len(values) else None, abi.ptr(out))
+        return out
+
+    def thread_count(self, res, idx, value):
+        return int(lib().or_pslot_thread_count(self.h, res, idx, int(value)))
+
+    def param_idx(self, rule):
+        return int(lib().or_pslot_param_idx(self.h, rule))
+
+    def token_state(self, rule, value):
+        lt, tk = C.c_int64(), C.c_int64()
+        f = lib().or_pslot_token_state(self.h, rule, int(value), C.byref(lt), C.byref(tk))
+        return f, lt.value, tk.value
 
 
 class ConcurrentTokenService:

@@ -2301,3 +2301,198 @@ int or_cts_param_top(or_cts* s, uint32_t key, int64_t now, int number, uint64_t*
     if (key >= s->n_prules) return SG_E_INVAL;
     return or_cpm_top(s->prules[key].metric, now, number, values, qps);
 }
+
+/* ===================================================================================== */
+/* ParamFlowSlot.checkFlow (sentinel-extension/sentinel-parameter-flow-control/.../ParamFlowSlot.java:55-93)  */
+/* over ParamFlowChecker.passCheck / passLocalCheck / passSingleValueCheck (ParamFlowChecker.java:48-122)      */
+/* and ParameterMetric's thread counts (ParameterMetric.java:125-249), on top of or_pf's token maps.          */
+/* ===================================================================================== */
+
+typedef struct or_tc {            /* threadCountMap entry: (resource, paramIdx, value) → count */
+    uint64_t value;
+    uint32_t res;
+    int32_t idx;
+    int64_t count;
+    uint8_t used;
+} or_tc;
+
+struct or_pslot {
+    or_pf* pf;                    /* token / time counters per (rule, value) */
+    sg_pslot_rule* rules;
+    int32_t* cur_idx;             /* the rule's paramIdx (applyRealParamIdx rewrites a negative one once) */
+    uint8_t* inited;              /* initParamMetricsFor ran: threadCountMap.get(paramIdx) exists */
+    uint32_t n, n_res;
+    or_tc* tc;
+    uint64_t tc_cap, tc_size;
+    int64_t now;                  /* the event's TimeUtil time */
+};
+
+or_pslot* or_pslot_new(void) {
+    or_pslot* s = (or_pslot*)calloc(1, sizeof(or_pslot));
+    s->pf = or_pf_new();
+    s->tc_cap = 1024;
+    s->tc = (or_tc*)calloc(s->tc_cap, sizeof(or_tc));
+    return s;
+}
+
+void or_pslot_free(or_pslot* s) {
+    if (!s) return;
+    or_pf_free(s->pf);
+    free(s->rules);
+    free(s->cur_idx);
+    free(s->inited);
+    free(s->tc);
+    free(s);
+}
+
+int or_pslot_load_rules(or_pslot* s, const sg_pslot_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                        uint32_t n_hot, uint32_t n_res) {
+    sg_param_rule* pr = (sg_param_rule*)calloc(n ? n : 1, sizeof(sg_param_rule));
+    for (uint32_t i = 0; i < n; i++) pr[i] = rules[i].rule;
+    or_pf_load_rules(s->pf, pr, n, hot, n_hot);
+    free(pr);
+    free(s->rules);
+    free(s->cur_idx);
+    free(s->inited);
+    s->rules = (sg_pslot_rule*)malloc((n ? n : 1) * sizeof(sg_pslot_rule));
+    memcpy(s->rules, rules, n * sizeof(sg_pslot_rule));
+    s->cur_idx = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    s->inited = (uint8_t*)calloc(n ? n : 1, 1);
+    for (uint32_t i = 0; i < n; i++) s->cur_idx[i] = rules[i].param_idx;
+    s->n = n;
+    s->n_res = n_res;
+    memset(s->tc, 0, s->tc_cap * sizeof(or_tc));
+    s->tc_size = 0;
+    return 0;
+}
+
+static uint64_t tc_hash(uint32_t res, int32_t idx, uint64_t v) {
+    uint64_t z = v + 0x9E3779B97F4A7C15ULL * ((uint64_t)res * 64 + (uint32_t)idx + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static or_tc* tc_find(const or_pslot* s, uint32_t res, int32_t idx, uint64_t v) {
+    uint64_t i = tc_hash(res, idx, v) & (s->tc_cap - 1);
+    for (;;) {
+        or_tc* e = &s->tc[i];
+        if (!e->used || (e->res == res && e->idx == idx && e->value == v)) return e;
+        i = (i + 1) & (s->tc_cap - 1);
+    }
+}
+
+static or_tc* tc_get_or_add(or_pslot* s, uint32_t res, int32_t idx, uint64_t v) {
+    if ((s->tc_size + 1) * 2 > s->tc_cap) {
+        or_tc* old = s->tc;
+        uint64_t oc = s->tc_cap;
+        s->tc_cap *= 2;
+        s->tc = (or_tc*)calloc(s->tc_cap, sizeof(or_tc));
+        for (uint64_t i = 0; i < oc; i++)
+            if (old[i].used) *tc_find(s, old[i].res, old[i].idx, old[i].value) = old[i];
+        free(old);
+    }
+    or_tc* e = tc_find(s, res, idx, v);
+    if (!e->used) {
+        e->used = 1;
+        e->res = res;
+        e->idx = idx;
+        e->value = v;
+        e->count = 0;
+        s->tc_size++;
+    }
+    return e;
+}
+
+int64_t or_pslot_thread_count(const or_pslot* s, uint32_t res, int32_t idx, uint64_t v) {
+    or_tc* e = tc_find(s, res, idx, v);
+    return e->used ? e->count : 0;
+}
+
+int32_t or_pslot_param_idx(const or_pslot* s, uint32_t rule) { return rule < s->n ? s->cur_idx[rule] : INT32_MIN; }
+
+/* passSingleValueCheck (:106-125) */
+static int pslot_single(or_pslot* s, uint32_t ri, uint32_t res, int count, uint64_t v) {
+    const sg_pslot_rule* r = &s->rules[ri];
+    if (r->grade == 1) {
+        if (r->rule.behavior == 2) return pf_throttle(s->pf, ri, v, s->now, count);
+        return pf_default(s->pf, ri, v, s->now, count);
+    }
+    if (r->grade == 0) {
+        or_tc* e = tc_find(s, res, s->cur_idx[ri], v);
+        int64_t threads = e->used ? e->count : 0;
+        for (uint32_t i = 0; i < r->rule.hot_count; i++)   /* exclusionItems: the hot item's threshold */
+            if (s->pf->hot[r->rule.hot_begin + i].value == v) return ++threads <= s->pf->hot[r->rule.hot_begin + i].threshold;
+        return ++threads <= or_d2l(r->rule.count);
+    }
+    return 1;
+}
+
+/* ParameterMetric.addThreadCount / decreaseThreadCount (:184-239) over the indices whose map exists */
+static void pslot_threads(or_pslot* s, uint32_t res, const sg_pslot_arg* args, uint32_t na, const uint64_t* values, int d) {
+    for (uint32_t idx = 0; idx < na; idx++) {
+        int has_map = 0;
+        for (uint32_t r = 0; r < s->n && !has_map; r++)
+            has_map = s->rules[r].resource == res && s->inited[r] && s->cur_idx[r] == (int32_t)idx;
+        if (!has_map) continue;
+        const sg_pslot_arg* a = &args[idx];
+        if (a->kind == SG_ARG_NULL) continue;
+        const uint32_t m = a->kind == SG_ARG_COLLECTION ? a->value_count : 1;
+        for (uint32_t j = 0; j < m; j++) {
+            const uint64_t v = values[a->value_begin + j];
+            if (d > 0) {
+                tc_get_or_add(s, res, (int32_t)idx, v)->count += 1;
+            } else {
+                /* putIfAbsent(value, new AtomicInteger()): an absent value is inserted at 0 and not decremented;
+                 * a present one is decremented and removed at <= 0 (a removed entry reads 0) */
+                or_tc* e = tc_find(s, res, (int32_t)idx, v);
+                if (e->used && e->count > 0) e->count -= 1;
+                else if (e->used) e->count = 0;
+                else tc_get_or_add(s, res, (int32_t)idx, v);
+            }
+        }
+    }
+}
+
+int or_pslot_decide(or_pslot* s, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
+                    const uint64_t* values, sg_pslot_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        const sg_pslot_event* e = &ev[i];
+        out[i].pass = 1;
+        out[i].rule = -1;
+        const sg_pslot_arg* a = args + e->arg_begin;
+        const uint32_t na = e->arg_count;
+        s->now = e->ts_ms;
+        if (e->resource >= s->n_res || e->args_null) continue;   /* ParamFlowSlot.checkFlow: args == null */
+        if (e->kind != SG_LOCAL_ENTRY) {           /* ParamFlowStatisticExitCallback: passed entries only */
+            pslot_threads(s, e->resource, a, na, values, -1);
+            continue;
+        }
+        int pass = 1;
+        for (uint32_t r = 0; r < s->n && pass; r++) {
+            if (s->rules[r].resource != e->resource) continue;
+            /* applyRealParamIdx(rule, args.length) */
+            if (s->cur_idx[r] < 0) s->cur_idx[r] = (-s->cur_idx[r] <= (int32_t)na) ? (int32_t)na + s->cur_idx[r] : -s->cur_idx[r];
+            s->inited[r] = 1;                      /* ParameterMetricStorage.initParamMetricsFor */
+            const int32_t idx = s->cur_idx[r];
+            if ((int32_t)na <= idx) continue;      /* args.length <= paramIdx */
+            const sg_pslot_arg* x = &a[idx];
+            if (x->kind == SG_ARG_NULL) continue;
+            const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
+            for (uint32_t j = 0; j < m; j++) {
+                if (!pslot_single(s, r, e->resource, e->count, values[x->value_begin + j])) {
+                    pass = 0;
+                    out[i].rule = (int32_t)r;
+                    break;
+                }
+            }
+        }
+        out[i].pass = pass;
+        if (pass) pslot_threads(s, e->resource, a, na, values, +1);   /* ParamFlowStatisticEntryCallback.onPass */
+    }
+    return 0;
+}
+
+int or_pslot_token_state(const or_pslot* s, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens) {
+    return or_pf_read_state(s->pf, rule, value, last_time, tokens);
+}

@@ -126,6 +126,18 @@ int     or_pf_decide(or_pf* p, const sg_param_req* req, uint64_t n, int32_t* out
 int     or_pf_read_state(const or_pf* p, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
 uint64_t or_pf_size(const or_pf* p);
 
+/* ---------- ParamFlowSlot chain (all rules of a resource, collection args, THREAD grade) ---------- */
+typedef struct or_pslot or_pslot;
+or_pslot* or_pslot_new(void);
+void      or_pslot_free(or_pslot* s);
+int       or_pslot_load_rules(or_pslot* s, const sg_pslot_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                              uint32_t n_hot, uint32_t n_res);
+int       or_pslot_decide(or_pslot* s, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
+                          const uint64_t* values, sg_pslot_result* out);
+int64_t   or_pslot_thread_count(const or_pslot* s, uint32_t res, int32_t idx, uint64_t v);
+int32_t   or_pslot_param_idx(const or_pslot* s, uint32_t rule);
+int       or_pslot_token_state(const or_pslot* s, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+
 /* ---------- pace controller: RateLimiterController (core/.../flow/controller/RateLimiterController.java) ---------- */
 typedef struct or_pace or_pace;
 or_pace* or_pace_new(void);

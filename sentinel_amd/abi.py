@@ -98,6 +98,16 @@ CPARAM_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4"
 BEHAVIOR_DEFAULT = 0
 BEHAVIOR_RATE_LIMITER = 2
 
+# ParamFlowSlot chain (sg_pslot_*)
+PSLOT_RULE_DTYPE = np.dtype([("rule", PARAM_RULE_DTYPE), ("resource", "<u4"), ("param_idx", "<i4"), ("grade", "<i4"),
+                             ("reserved", "<i4")], align=True)
+PSLOT_ARG_DTYPE = np.dtype([("value_begin", "<u4"), ("value_count", "<u4"), ("kind", "<i4"), ("reserved", "<i4")],
+                           align=True)
+PSLOT_EVENT_DTYPE = np.dtype([("ts_ms", "<i8"), ("resource", "<u4"), ("count", "<i4"), ("kind", "<i4"),
+                              ("arg_begin", "<u4"), ("arg_count", "<u4"), ("args_null", "<i4")], align=True)
+PSLOT_RES_DTYPE = np.dtype([("pass", "<i4"), ("rule", "<i4")], align=True)
+ARG_NULL, ARG_VALUE, ARG_COLLECTION = 0, 1, 2
+
 # metric snapshots (sg_local_metrics)
 METRIC_NODE_DTYPE = np.dtype([("timestamp", "<i8"), ("pass_qps", "<i8"), ("block_qps", "<i8"), ("success_qps", "<i8"),
                               ("exception_qps", "<i8"), ("rt", "<i8"), ("occupied_pass_qps", "<i8"),
@@ -147,6 +157,7 @@ assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 assert LOCAL_FLOW_RULE_DTYPE.itemsize == 40
 assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
 assert METRIC_NODE_DTYPE.itemsize == 64
+assert PSLOT_RULE_DTYPE.itemsize == PARAM_RULE_DTYPE.itemsize + 16 and PSLOT_EVENT_DTYPE.itemsize == 32
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:

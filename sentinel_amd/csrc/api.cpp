@@ -140,6 +140,17 @@ struct sg_handle {
 
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
+    // ParamFlowSlot chain (sg_pslot_*)
+    uint32_t ps_nres = 0;
+    bool ps_loaded = false;
+    uint32_t* d_ps_begin = nullptr;
+    uint32_t* d_ps_rules = nullptr;
+    int32_t* d_ps_grade = nullptr;
+    int32_t* d_ps_idx = nullptr;
+    int32_t* d_ps_init = nullptr;
+    PSThread* d_ps_tc = nullptr;
+    uint64_t ps_tc_slots = 0;
+    int64_t* d_ps_last_ts = nullptr;
     // concurrent cluster tokens (sg_conc_*)
     int32_t* d_cnow = nullptr;        // nowCalls per rule
     double* d_cthr = nullptr;
@@ -438,6 +449,13 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
     dfree(h->d_llast_fetch);
+    dfree(h->d_ps_begin);
+    dfree(h->d_ps_rules);
+    dfree(h->d_ps_grade);
+    dfree(h->d_ps_idx);
+    dfree(h->d_ps_init);
+    dfree(h->d_ps_tc);
+    dfree(h->d_ps_last_ts);
     dfree(h->d_cnow);
     dfree(h->d_cthr);
     dfree(h->d_coff);
@@ -2328,6 +2346,175 @@ int sg_conc_read_state(sg_handle* h, uint32_t key, int32_t* now_calls, uint64_t*
         if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
         *live_tokens = v;
     }
+    return SG_OK;
+}
+
+// ------------------------------------------------------------------------------ ParamFlowSlot chain
+
+namespace {
+
+PSArgs pslot_args(sg_handle* h) {
+    PSArgs s{};
+    s.p.rules = h->d_prules;
+    s.p.n_rules = (uint32_t)h->ptab.size();
+    s.p.hot = h->d_phot;
+    s.p.table = h->d_ptable;
+    s.p.total_slots = h->ptotal;
+    s.p.err = h->d_err;
+    s.n_res = h->ps_nres;
+    s.res_begin = h->d_ps_begin;
+    s.res_rules = h->d_ps_rules;
+    s.grade = h->d_ps_grade;
+    s.cur_idx = h->d_ps_idx;
+    s.inited = h->d_ps_init;
+    s.tc = h->d_ps_tc;
+    s.tc_mask = h->ps_tc_slots - 1;
+    s.err = h->d_err;
+    s.last_ts = h->d_ps_last_ts;
+    return s;
+}
+
+}  // namespace
+
+int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                        uint32_t n_hot, uint32_t n_resources) {
+    if (!h || (!rules && n)) return SG_E_INVAL;
+    drain_async(h);
+    std::vector<sg_param_rule> pr(n);
+    std::vector<std::vector<uint32_t>> per(n_resources);
+    std::vector<int32_t> grade(n), idx(n), zero(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (rules[i].resource >= n_resources) return fail(h, SG_E_INVAL, "rule resource >= n_resources");
+        if (rules[i].grade != 0 && rules[i].grade != 1) return fail(h, SG_E_INVAL, "grade must be THREAD or QPS");
+        pr[i] = rules[i].rule;
+        per[rules[i].resource].push_back(i);  // ParamFlowRuleManager.getRulesOfResource: load order
+        grade[i] = rules[i].grade;
+        idx[i] = rules[i].param_idx;
+    }
+    int rc = sg_param_load_rules(h, pr.data(), n, hot, n_hot);
+    if (rc) return rc;
+    std::vector<uint32_t> begin(n_resources + 1, 0), list;
+    for (uint32_t r = 0; r < n_resources; ++r) {
+        begin[r] = (uint32_t)list.size();
+        list.insert(list.end(), per[r].begin(), per[r].end());
+    }
+    begin[n_resources] = (uint32_t)list.size();
+    HIP_TRY(h, hipSetDevice(h->device));
+    dfree(h->d_ps_begin);
+    dfree(h->d_ps_rules);
+    dfree(h->d_ps_grade);
+    dfree(h->d_ps_idx);
+    dfree(h->d_ps_init);
+    const size_t n1 = n ? n : 1;
+    if (hipMalloc(&h->d_ps_begin, sizeof(uint32_t) * (n_resources + 1)) != hipSuccess ||
+        hipMalloc(&h->d_ps_rules, sizeof(uint32_t) * n1) != hipSuccess ||
+        hipMalloc(&h->d_ps_grade, sizeof(int32_t) * n1) != hipSuccess ||
+        hipMalloc(&h->d_ps_idx, sizeof(int32_t) * n1) != hipSuccess || hipMalloc(&h->d_ps_init, sizeof(int32_t) * n1) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "param slot rules");
+    HIP_TRY(h, hipMemcpy(h->d_ps_begin, begin.data(), sizeof(uint32_t) * (n_resources + 1), hipMemcpyHostToDevice));
+    if (n) {
+        HIP_TRY(h, hipMemcpy(h->d_ps_rules, list.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_ps_grade, grade.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_ps_idx, idx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_ps_init, zero.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+    }
+    if (!h->d_ps_tc) {
+        h->ps_tc_slots = 1ull << 20;
+        if (hipMalloc(&h->d_ps_tc, sizeof(PSThread) * h->ps_tc_slots) != hipSuccess ||
+            hipMalloc(&h->d_ps_last_ts, sizeof(int64_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "thread count table");
+    }
+    HIP_TRY(h, launch_pslot_clear(h->d_ps_tc, h->ps_tc_slots, 0));
+    const int64_t neg = -1;
+    HIP_TRY(h, hipMemcpy(h->d_ps_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
+    HIP_TRY(h, hipDeviceSynchronize());
+    h->ps_nres = n_resources;
+    h->ps_loaded = true;
+    return SG_OK;
+}
+
+int sg_pslot_decide_batch(sg_handle* h, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args, uint64_t n_args,
+                          const uint64_t* values, uint64_t n_values, sg_pslot_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (!h->ps_loaded) return fail(h, SG_E_INVAL, "sg_pslot_load_rules first");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int kbits = bits_for((uint64_t)h->ps_nres);
+    if (kbits < 1) kbits = 1;
+    if (kbits + bits_for(h->cfg.max_batch) > 64) return fail(h, SG_E_UNSUPPORTED, "resources x max_batch too large");
+    hipStream_t stream = (hipStream_t)stream_;
+    PSArgs s = pslot_args(h);
+    s.ev = ev;
+    s.args = args;
+    s.n_args = n_args;
+    s.values = values;
+    s.n_values = n_values;
+    s.out = out;
+    s.n = n;
+    s.rec = h->d_rec;
+    s.kshift = 64 - kbits;
+    s.imask = (1ull << s.kshift) - 1;
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, launch_pslot_batch(s, h->d_rec_sorted, h->d_hist, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    if (*h->h_err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (*h->h_err & kErrBounds) return fail(h, SG_E_INVAL, "an event's arguments lie outside the arg / value arrays");
+    if (*h->h_err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param or thread-count table is full");
+    return SG_OK;
+}
+
+int sg_pslot_decide_batch_host(sg_handle* h, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
+                               uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_pslot_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    sg_pslot_event* d_ev = nullptr;
+    sg_pslot_arg* d_args = nullptr;
+    uint64_t* d_vals = nullptr;
+    sg_pslot_result* d_out = nullptr;
+    hipError_t e = hipMalloc(&d_ev, sizeof(sg_pslot_event) * n);
+    if (e == hipSuccess) e = hipMalloc(&d_args, sizeof(sg_pslot_arg) * (n_args ? n_args : 1));
+    if (e == hipSuccess) e = hipMalloc(&d_vals, sizeof(uint64_t) * (n_values ? n_values : 1));
+    if (e == hipSuccess) e = hipMalloc(&d_out, sizeof(sg_pslot_result) * n);
+    if (e == hipSuccess) e = hipMemcpy(d_ev, ev, sizeof(sg_pslot_event) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_args) e = hipMemcpy(d_args, args, sizeof(sg_pslot_arg) * n_args, hipMemcpyHostToDevice);
+    if (e == hipSuccess && n_values) e = hipMemcpy(d_vals, values, sizeof(uint64_t) * n_values, hipMemcpyHostToDevice);
+    int rc = SG_E_DEVICE;
+    if (e == hipSuccess) {
+        rc = sg_pslot_decide_batch(h, d_ev, n, d_args, n_args, d_vals, n_values, d_out, nullptr);
+        if (rc == SG_OK) e = hipMemcpy(out, d_out, sizeof(sg_pslot_result) * n, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(d_ev);
+    (void)hipFree(d_args);
+    (void)hipFree(d_vals);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    return rc;
+}
+
+int sg_pslot_thread_count(sg_handle* h, uint32_t resource, int32_t param_idx, uint64_t value, int64_t* count) {
+    if (!h || !count || !h->ps_loaded || resource >= h->ps_nres || param_idx < 0) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int64_t* d = nullptr;
+    HIP_TRY(h, hipMalloc(&d, sizeof(int64_t)));
+    hipError_t e = launch_pslot_thread_read(pslot_args(h), resource, param_idx, value, d, 0);
+    if (e == hipSuccess) e = hipMemcpy(count, d, sizeof(int64_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    return SG_OK;
+}
+
+int sg_pslot_param_idx(sg_handle* h, uint32_t rule, int32_t* param_idx) {
+    if (!h || !param_idx || !h->ps_loaded || rule >= h->ptab.size()) return SG_E_INVAL;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    HIP_TRY(h, hipMemcpy(param_idx, h->d_ps_idx + rule, sizeof(int32_t), hipMemcpyDeviceToHost));
     return SG_OK;
 }
 

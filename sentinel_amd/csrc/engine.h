@@ -174,6 +174,43 @@ struct PArgs {
     uint32_t short_max;
 };
 
+// ParamFlowSlot chain (param.hip): every param rule of a resource on one lane per resource
+struct alignas(32) PSThread {  // ParameterMetric.threadCountMap entry: (resource, paramIdx) owner word + value
+    unsigned long long owner;  // 0 = empty, else (resource + 1) << 32 | (paramIdx + 1)
+    uint64_t value;
+    int64_t count;
+    int64_t pad;
+};
+
+struct PSArgs {
+    PArgs p;                  // rules (token / throttle parameters), hot items, token table
+    const sg_pslot_event* ev;
+    const sg_pslot_arg* args;
+    uint64_t n_args;
+    const uint64_t* values;
+    uint64_t n_values;
+    sg_pslot_result* out;
+    uint64_t n;
+    uint32_t n_res;
+    const uint32_t* res_begin;  // [n_res + 1] the resource's rules: res_rules[res_begin[r] .. res_begin[r + 1])
+    const uint32_t* res_rules;  // rule indices in load order
+    const int32_t* grade;       // per rule
+    int32_t* cur_idx;           // per rule: paramIdx (applyRealParamIdx rewrites a negative one once)
+    int32_t* inited;            // per rule: initParamMetricsFor ran (its paramIdx has a thread map)
+    PSThread* tc;
+    uint64_t tc_mask;
+    uint64_t* rec;              // [resource : high bits][event index]
+    int kshift;
+    uint64_t imask;
+    int* err;
+    int64_t* last_ts;
+};
+
+hipError_t launch_pslot_batch(PSArgs& s, uint64_t* b_buf, uint32_t* hist, hipStream_t stream);
+hipError_t launch_pslot_clear(PSThread* tc, uint64_t n, hipStream_t stream);
+hipError_t launch_pslot_thread_read(const PSArgs& s, uint32_t res, int32_t idx, uint64_t value, int64_t* out,
+                                    hipStream_t stream);
+
 hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
 hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
                               uint64_t** sorted_out, hipStream_t stream);

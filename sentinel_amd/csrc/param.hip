@@ -425,3 +425,229 @@ hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, 
 }
 
 }  // namespace sg
+
+// ------------------------------------------------------------------------------ ParamFlowSlot chain
+//
+// SphU.entry(resource, count, args...) through ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93): every param rule
+// of the resource in load order on args[paramIdx] — a collection / array element by element with early exit
+// (ParamFlowChecker.passLocalCheck :75-104), QPS rules through the token bucket / throttle steps above, THREAD rules
+// against ParameterMetric's thread counts (:114-122), which passed entries raise and their exits lower
+// (ParameterMetric.addThreadCount / decreaseThreadCount :125-239). A resource's rules share its ParameterMetric, so
+// its events are walked in order on one lane (k_pswalk); different resources are independent.
+
+namespace sg {
+
+namespace {
+
+__device__ __forceinline__ uint64_t ps_hash(unsigned long long owner, uint64_t v) {
+    uint64_t z = v + 0x9E3779B97F4A7C15ull * (owner + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ unsigned long long ps_owner(uint32_t res, int32_t idx) {
+    return ((unsigned long long)(res + 1) << 32) | (unsigned long long)(uint32_t)(idx + 1);
+}
+
+// threadCountMap lookup; create: insert at 0 when absent (putIfAbsent). Returns the slot or -1.
+__device__ int64_t ps_tc(const PSArgs& s, uint32_t res, int32_t idx, uint64_t v, bool create) {
+    const unsigned long long own = ps_owner(res, idx);
+    uint64_t h = ps_hash(own, v) & s.tc_mask;
+    for (uint64_t probes = 0; probes <= s.tc_mask; ++probes, h = (h + 1) & s.tc_mask) {
+        PSThread& e = s.tc[h];
+        const unsigned long long o = __hip_atomic_load(&e.owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == own && e.value == v) return (int64_t)h;
+        if (o == 0) {
+            if (!create) return -1;
+            // claim the slot; only this resource's lane ever reads entries with this owner word
+            if (atomicCAS(&e.owner, 0ull, own) == 0ull) {
+                e.value = v;
+                e.count = 0;
+                return (int64_t)h;
+            }
+        }
+    }
+    if (create) atomicOr(s.err, kErrTableFull);
+    return -1;
+}
+
+// passSingleValueCheck (:106-125) for rule ri at time t
+__device__ bool ps_single(const PSArgs& s, uint32_t ri, uint32_t res, int64_t t, int64_t acq, uint64_t v) {
+    const PRule r = s.p.rules[ri];
+    const int64_t tc = param_token_count(s.p, r, v);  // the hot item's threshold, else (long) count
+    if (s.grade[ri] == 1) {
+        if (tc == 0) return false;
+        if (r.behavior != 2 && acq > tc + r.burst) return false;
+        const uint64_t g = param_slot(s.p, r, v);
+        if (g == ~0ull) {
+            atomicOr(s.err, kErrTableFull);
+            return false;
+        }
+        PSlot& slot = s.p.table[g];
+        PState st{slot.time, slot.tokens, slot.flags};
+        const bool ok = r.behavior == 2 ? param_throttle_step(st, throttle_cost(r, tc, acq), r.max_queueing_ms, t)
+                                        : param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, acq);
+        slot.time = st.time;
+        slot.tokens = st.tokens;
+        slot.flags = st.flags;
+        return ok;
+    }
+    if (s.grade[ri] == 0) {
+        const int64_t e = ps_tc(s, res, s.cur_idx[ri], v, false);
+        const int64_t threads = e >= 0 ? s.tc[e].count : 0;
+        return threads + 1 <= tc;
+    }
+    return true;
+}
+
+// addThreadCount / decreaseThreadCount over the argument indices that have a thread map
+__device__ void ps_threads(const PSArgs& s, uint32_t res, const sg_pslot_event& e, int d) {
+    const uint32_t rb = s.res_begin[res], re = s.res_begin[res + 1];
+    for (uint32_t idx = 0; idx < e.arg_count; ++idx) {
+        bool has_map = false;
+        for (uint32_t k = rb; k < re && !has_map; ++k) {
+            const uint32_t ri = s.res_rules[k];
+            has_map = s.inited[ri] && s.cur_idx[ri] == (int32_t)idx;
+        }
+        if (!has_map) continue;
+        const sg_pslot_arg a = s.args[e.arg_begin + idx];
+        if (a.kind == SG_ARG_NULL) continue;
+        const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint64_t v = s.values[a.value_begin + j];
+            if (d > 0) {
+                const int64_t x = ps_tc(s, res, (int32_t)idx, v, true);
+                if (x >= 0) s.tc[x].count += 1;
+            } else {
+                const int64_t x = ps_tc(s, res, (int32_t)idx, v, false);
+                if (x >= 0) s.tc[x].count = s.tc[x].count > 0 ? s.tc[x].count - 1 : 0;  // <= 0: removed (reads 0)
+                else ps_tc(s, res, (int32_t)idx, v, true);                             // putIfAbsent(0)
+            }
+        }
+    }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_psprep(PSArgs s) {
+    const uint64_t sentinel = (uint64_t)s.n_res << s.kshift;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < s.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_pslot_event e = s.ev[i];
+        if (e.ts_ms < 0 || (i == 0 ? e.ts_ms < *s.last_ts : e.ts_ms < s.ev[i - 1].ts_ms)) atomicOr(s.err, kErrTime);
+        sg_pslot_result r;
+        r.pass = 1;
+        r.rule = -1;
+        s.out[i] = r;
+        uint64_t rec = sentinel | i;
+        if (e.resource < s.n_res && !e.args_null) {
+            bool ok = (uint64_t)e.arg_begin + e.arg_count <= s.n_args;
+            for (uint32_t k = 0; ok && k < e.arg_count; ++k) {
+                const sg_pslot_arg a = s.args[e.arg_begin + k];
+                const uint64_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : (a.kind == SG_ARG_VALUE ? 1 : 0);
+                ok = (uint64_t)a.value_begin + m <= s.n_values;
+            }
+            if (!ok) atomicOr(s.err, kErrBounds);
+            else rec = ((uint64_t)e.resource << s.kshift) | i;
+        }
+        s.rec[i] = rec;
+    }
+}
+
+// One lane per resource segment of the sorted records.
+__global__ void __launch_bounds__(256) k_pswalk(PSArgs s, const uint64_t* sorted) {
+    if (*s.err) return;
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < s.n; p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t res = (uint32_t)(sorted[p] >> s.kshift);
+        if (res >= s.n_res || (p > 0 && (uint32_t)(sorted[p - 1] >> s.kshift) == res)) continue;
+        const uint32_t rb = s.res_begin[res], re = s.res_begin[res + 1];
+        for (uint64_t q = p; q < s.n; ++q) {
+            const uint64_t rec = sorted[q];
+            if ((uint32_t)(rec >> s.kshift) != res) break;
+            const uint64_t i = rec & s.imask;
+            const sg_pslot_event e = s.ev[i];
+            if (e.kind != SG_LOCAL_ENTRY) {  // ParamFlowStatisticExitCallback (passed entries only)
+                ps_threads(s, res, e, -1);
+                continue;
+            }
+            bool pass = true;
+            int32_t failed = -1;
+            for (uint32_t k = rb; k < re && pass; ++k) {
+                const uint32_t ri = s.res_rules[k];
+                int32_t idx = s.cur_idx[ri];
+                if (idx < 0) {  // applyRealParamIdx(rule, args.length)
+                    idx = (-idx <= (int32_t)e.arg_count) ? (int32_t)e.arg_count + idx : -idx;
+                    s.cur_idx[ri] = idx;
+                }
+                s.inited[ri] = 1;
+                if ((int32_t)e.arg_count <= idx) continue;
+                const sg_pslot_arg a = s.args[e.arg_begin + (uint32_t)idx];
+                if (a.kind == SG_ARG_NULL) continue;
+                const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
+                for (uint32_t j = 0; j < m; ++j) {
+                    if (!ps_single(s, ri, res, e.ts_ms, (int64_t)e.count, s.values[a.value_begin + j])) {
+                        pass = false;
+                        failed = (int32_t)ri;
+                        break;
+                    }
+                }
+            }
+            if (pass) {
+                ps_threads(s, res, e, +1);
+            } else {
+                sg_pslot_result r;
+                r.pass = 0;
+                r.rule = failed;
+                s.out[i] = r;
+            }
+        }
+    }
+}
+
+__global__ void k_psfinish(PSArgs s) {
+    if (*s.err == 0 && s.n > 0) *s.last_ts = s.ev[s.n - 1].ts_ms;
+}
+
+__global__ void __launch_bounds__(256) k_psclear(PSThread* tc, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        PSThread e;
+        e.owner = 0;
+        e.value = 0;
+        e.count = 0;
+        e.pad = 0;
+        tc[i] = e;
+    }
+}
+
+__global__ void k_psread(PSArgs s, uint32_t res, int32_t idx, uint64_t value, int64_t* out) {
+    const int64_t x = ps_tc(s, res, idx, value, false);
+    *out = x >= 0 ? s.tc[x].count : 0;
+}
+
+static unsigned psgrid(uint64_t n, unsigned cap) {
+    uint64_t g = (n + 255) / 256;
+    return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
+}
+
+hipError_t launch_pslot_batch(PSArgs& s, uint64_t* b_buf, uint32_t* hist, hipStream_t stream) {
+    hipLaunchKernelGGL(k_psprep, dim3(psgrid(s.n, 8192)), dim3(256), 0, stream, s);
+    uint64_t* sorted = nullptr;
+    hipError_t e = radix_sort_records(s.rec, b_buf, s.n, s.kshift, hist, &sorted, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pswalk, dim3(psgrid(s.n, 8192)), dim3(256), 0, stream, s, (const uint64_t*)sorted);
+    hipLaunchKernelGGL(k_psfinish, dim3(1), dim3(1), 0, stream, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_pslot_clear(PSThread* tc, uint64_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(k_psclear, dim3(psgrid(n, 8192)), dim3(256), 0, stream, tc, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_pslot_thread_read(const PSArgs& s, uint32_t res, int32_t idx, uint64_t value, int64_t* out,
+                                    hipStream_t stream) {
+    hipLaunchKernelGGL(k_psread, dim3(1), dim3(1), 0, stream, s, res, idx, value, out);
+    return hipGetLastError();
+}
+
+}  // namespace sg

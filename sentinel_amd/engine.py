@@ -23,6 +23,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
            "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values",
+           "sg_pslot_load_rules", "sg_pslot_decide_batch", "sg_pslot_decide_batch_host", "sg_pslot_thread_count",
+           "sg_pslot_param_idx",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
 
 _lib = None
@@ -85,6 +87,11 @@ def load_library():
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "sg_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
         "sg_local_metrics": (C.c_int, [vp, i64, vp, u64, C.POINTER(u64)]),
+        "sg_pslot_load_rules": (C.c_int, [vp, vp, u32, vp, u32, u32]),
+        "sg_pslot_decide_batch": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp, vp]),
+        "sg_pslot_decide_batch_host": (C.c_int, [vp, vp, u64, vp, u64, vp, u64, vp]),
+        "sg_pslot_thread_count": (C.c_int, [vp, u32, C.c_int32, u64, C.POINTER(i64)]),
+        "sg_pslot_param_idx": (C.c_int, [vp, u32, C.POINTER(C.c_int32)]),
         "sg_cparam_top_values": (C.c_int, [vp, i64, u32, vp, vp, vp]),
         "sg_conc_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_conc_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
@@ -302,6 +309,34 @@ class FlowEngine:
         out = np.zeros(2 * n_rules, np.float64)
         self._check(self._L.sg_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
         return out.reshape(n_rules, 2)
+
+    # ---- ParamFlowSlot chain (every param rule of a resource, collection args, THREAD grade)
+    def pslot_load_rules(self, rules, hot=None, n_resources=None):
+        rules = np.ascontiguousarray(rules, dtype=abi.PSLOT_RULE_DTYPE).reshape(-1)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        n_res = int(rules["resource"].max()) + 1 if n_resources is None else n_resources
+        self._check(self._L.sg_pslot_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot) if len(hot) else None,
+                                                len(hot), n_res))
+
+    def pslot_decide_host(self, ev, args, values):
+        ev = np.ascontiguousarray(ev, dtype=abi.PSLOT_EVENT_DTYPE).reshape(-1)
+        args = np.ascontiguousarray(args, dtype=abi.PSLOT_ARG_DTYPE).reshape(-1)
+        values = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1)
+        out = np.zeros(len(ev), abi.PSLOT_RES_DTYPE)
+        self._check(self._L.sg_pslot_decide_batch_host(self.h, abi.ptr(ev), len(ev), abi.ptr(args) if len(args) else None,
+                                                       len(args), abi.ptr(values) if len(values) else None,
+                                                       len(values), abi.ptr(out)))
+        return out
+
+    def pslot_thread_count(self, res, idx, value):
+        v = C.c_int64()
+        self._check(self._L.sg_pslot_thread_count(self.h, res, idx, int(value), C.byref(v)))
+        return v.value
+
+    def pslot_param_idx(self, rule):
+        v = C.c_int32()
+        self._check(self._L.sg_pslot_param_idx(self.h, rule, C.byref(v)))
+        return v.value
 
     # ---- concurrent cluster tokens (requestConcurrentToken / releaseConcurrentToken)
     def conc_set_rule_timeouts(self, client_offline_ms, resource_timeout_ms):
