@@ -474,11 +474,18 @@ int sg_pace_read_state(sg_handle* h, uint32_t rule, int64_t* latest_passed_time)
  *   sg_cparam_load_rules    ← ClusterParamFlowRuleManager.loadRules → applyClusterParamRules
  *                             (…/flow/rule/ClusterParamFlowRuleManager.java:337-360): a surviving flowId keeps its
  *                             ClusterParamMetric; each rule owns an exact 2^capacity_log2 value table (0 = 2^16).
- *                             Rules of a namespace with a QPS limiter are SG_E_UNSUPPORTED on this path.
  *   sg_cparam_decide_batch  ← TokenService.requestParamToken(Long, int, Collection<Object>)
  *                             (DefaultTokenService.java:53-64 → ClusterParamFlowChecker.acquireClusterToken,
  *                             ClusterParamFlowChecker.java:42-87), time-ordered; values[] holds every request's
- *                             parameter values (u64; other types through the shim's value dictionary).
+ *                             parameter values (u64; other types through the shim's value dictionary). Request i's
+ *                             values are values[value_begin, value_begin + value_count): the ranges of the valid
+ *                             requests must not overlap and must follow request order (value_begin increasing with
+ *                             i, as a packer appending each request's values produces) — else SG_E_INVAL.
+ *                             allowProceed goes through the namespace's QPS limiter, the same state the flow-token
+ *                             path uses (GlobalRequestLimiter is per namespace): keep flow and param batches that
+ *                             share a limiter in time order. A rejected batch changes no state.
+ *   sg_cparam_last_rounds   fixed-point rounds the last batch needed (1 = single pass; requests with several values
+ *                           may need more; max_rounds + 1 = it was decided serially). Tuning / tests.
  *   sg_cparam_read_sum      ← ClusterParamMetric.getSum(value) at now_ms (without currentWindow's side effect). */
 int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
                          uint32_t n_hot, int32_t capacity_log2);
@@ -487,6 +494,7 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
 int sg_cparam_decide_batch_host(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
                                 uint64_t n_values, sg_result* out);
 int sg_cparam_read_sum(sg_handle* h, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum);
+int sg_cparam_last_rounds(const sg_handle* h, uint32_t* rounds);
 /*   sg_cparam_top_values ← ClusterParamMetric.getTopValues(number) (…/metric/ClusterParamMetric.java:90-133), the
  *                          topParams of ClusterMetricNodeGenerator.paramToMetricNode (:88-104): per rule up to
  *                          `number` values with the largest window sums at now_ms (count / intervalSec), zero sums
@@ -568,7 +576,10 @@ int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);
  * table: unknown → SG_KEY_NO_RULE, flowId <= 0 → SG_KEY_BAD, as DefaultTokenService.requestToken would
  * answer), the xid of every frame and its kind (SG_FRAME_*). Frames that are not decodable flow requests
  * get key SG_KEY_BAD and acquire 0 (a harmless BAD_REQUEST slot in the batch). All pointers are device
- * memory (payload 4-byte aligned); the call is asynchronous on `stream`.
+ * memory (payload 4-byte aligned); the call is asynchronous on `stream`. offsets must be non-decreasing and
+ * offsets[n] <= the payload's size, and the payload allocation must reach the next 4-byte multiple past offsets[n]
+ * (staged loads read whole aligned words; hipMalloc'd buffers always do): the kernel does not know the payload's
+ * size, so an offset past it is read as given. A frame whose end lies before its start decodes as SG_FRAME_SHORT.
  * sg_codec_encode_flow: one 16-byte response frame per request at frames_out + 16 * i (zero-filled for
  * frames whose kind is not SG_FRAME_FLOW: the Java server sends nothing for those). */
 #define SG_MSG_TYPE_PING       0

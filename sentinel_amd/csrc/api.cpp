@@ -105,7 +105,21 @@ struct sg_handle {
     uint64_t cptotal = 0;
     int cpstride = 1;
     int64_t* d_cplast_ts = nullptr;
-    uint32_t* d_cpmulti = nullptr;    // [1 + max_batch]: count, then indices of multi-value requests
+    // one-pipeline batch scratch (value-position records, fixed point over multi-value requests)
+    uint32_t* d_cp_owner = nullptr;
+    uint8_t* d_cp_chk = nullptr;
+    uint8_t* d_cp_assume = nullptr;
+    uint64_t* d_cp_rec = nullptr;
+    uint64_t* d_cp_rec2 = nullptr;
+    uint32_t* d_cp_hist = nullptr;
+    uint64_t cp_val_cap = 0;
+    CPBucket* d_cp_save = nullptr;
+    uint64_t cp_save_cap = 0;
+    int* d_cp_changed = nullptr;
+    uint8_t* d_cp_rule_lim = nullptr; // [cparam rules] limiter slot of the rule's namespace (0xFF none)
+    std::vector<uint8_t> cp_rule_lim_host;
+    uint32_t cp_rounds = 0;           // fixed-point rounds of the last batch (stats / tests)
+    uint32_t cp_max_rounds = 64;      // env SG_CP_MAX_ROUNDS overrides (tests force the serial fallback)
     sg_cparam_req* d_cpreq_h = nullptr;
     uint64_t* d_cpval_h = nullptr;
     uint64_t cpval_cap = 0;
@@ -388,6 +402,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         return bail(SG_E_DEVICE);
     if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
     if (const char* sm = std::getenv("SG_SHORT_MAX")) h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
+    if (const char* mr = std::getenv("SG_CP_MAX_ROUNDS")) h->cp_max_rounds = (uint32_t)std::strtoul(mr, nullptr, 10);
     // default namespace 0, no limiter, 1 connection
     sg_namespace d0{0, 1, 30000.0};
     h->ns.push_back(d0);
@@ -441,7 +456,6 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cpkeys);
     dfree(h->d_cpring);
     dfree(h->d_cplast_ts);
-    dfree(h->d_cpmulti);
     dfree(h->d_cpreq_h);
     dfree(h->d_cpval_h);
     dfree(h->d_cpout_h);
@@ -456,6 +470,15 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_ps_init);
     dfree(h->d_ps_tc);
     dfree(h->d_ps_last_ts);
+    dfree(h->d_cp_owner);
+    dfree(h->d_cp_chk);
+    dfree(h->d_cp_assume);
+    dfree(h->d_cp_rec);
+    dfree(h->d_cp_rec2);
+    dfree(h->d_cp_hist);
+    dfree(h->d_cp_save);
+    dfree(h->d_cp_changed);
+    dfree(h->d_cp_rule_lim);
     dfree(h->d_cnow);
     dfree(h->d_cthr);
     dfree(h->d_coff);
@@ -1362,8 +1385,6 @@ int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, 
         if (r.sample_count <= 0 || r.window_interval_ms <= 0 || r.window_interval_ms % r.sample_count != 0)
             return fail(h, SG_E_INVAL, "invalid window config");
         if (r.namespace_id < 0 || (size_t)r.namespace_id >= h->ns.size()) return fail(h, SG_E_INVAL, "unknown namespace");
-        if ((size_t)r.namespace_id < h->ns_slot.size() && h->ns_slot[r.namespace_id] >= 0)
-            return fail(h, SG_E_UNSUPPORTED, "param rules in a namespace with a QPS limiter");
         if ((uint64_t)r.hot_begin + r.hot_count > n_hot) return fail(h, SG_E_INVAL, "hot item range out of bounds");
         if (!seen.emplace(r.flow_id, i).second) return fail(h, SG_E_INVAL, "duplicate flowId");
         int S = r.sample_count, interval = r.window_interval_ms;
@@ -1469,24 +1490,107 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     if (!h->d_cplast_ts) return fail(h, SG_E_INVAL, "sg_cparam_load_rules first");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     CPArgs c = cp_args(h, req, n, values, n_values, out);
+    const uint64_t nv = n_values ? n_values : 1;
     const int gbits = bits_for(h->cptotal + 1);
-    if (c.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
-    if (!h->d_cpmulti && hipMalloc(&h->d_cpmulti, sizeof(uint32_t) * (h->cfg.max_batch + 1)) != hipSuccess)
-        return fail(h, SG_E_NOMEM, "multi-value list");
+    const int pbits = bits_for(nv);
+    if (pbits + gbits > 64 || gbits > 32) return fail(h, SG_E_UNSUPPORTED, "param tables x values too large for 64-bit records");
+    if (nv > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "more values than max_batch");
+    // scratch sized for the batch's value positions
+    if (nv > h->cp_val_cap) {
+        dfree(h->d_cp_owner);
+        dfree(h->d_cp_chk);
+        dfree(h->d_cp_rec);
+        dfree(h->d_cp_rec2);
+        dfree(h->d_cp_hist);
+        if (hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
+            hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
+            hipMalloc(&h->d_cp_hist, sizeof(uint32_t) * radix_hist_words(nv)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "cparam batch scratch");
+        h->cp_val_cap = nv;
+    }
+    if (!h->d_cp_assume && (hipMalloc(&h->d_cp_assume, h->cfg.max_batch) != hipSuccess ||
+                            hipMalloc(&h->d_cp_changed, sizeof(int)) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "cparam batch scratch");
+    // allowProceed → GlobalRequestLimiter.tryPass for the namespaces with a limiter (state shared with flow tokens)
+    const uint32_t R = (uint32_t)h->cprules.size();
+    std::vector<uint8_t> rl(R ? R : 1, 0xFF);
+    bool any_lim = false;
+    for (uint32_t k = 0; k < R; ++k) {
+        const int ns = h->cprules[k].namespace_id;
+        if (ns >= 0 && (size_t)ns < h->ns_slot.size() && h->ns_slot[ns] >= 0) {
+            rl[k] = (uint8_t)h->ns_slot[ns];
+            any_lim = true;
+        }
+    }
+    if (any_lim && (rl != h->cp_rule_lim_host || !h->d_cp_rule_lim)) {
+        dfree(h->d_cp_rule_lim);
+        if (hipMalloc(&h->d_cp_rule_lim, rl.size()) != hipSuccess) return fail(h, SG_E_NOMEM, "cparam limiter table");
+        HIP_TRY(h, hipMemcpyAsync(h->d_cp_rule_lim, rl.data(), rl.size(), hipMemcpyHostToDevice, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        h->cp_rule_lim_host = rl;
+    }
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    // requests with several values: decided one at a time between the single-value runs
-    HIP_TRY(h, hipMemsetAsync(h->d_cpmulti, 0, sizeof(uint32_t), stream));
-    HIP_TRY(h, launch_cp_count_multi(c, h->d_cpmulti + 1, h->d_cpmulti, stream));
-    uint32_t n_multi = 0;
-    HIP_TRY(h, hipMemcpyAsync(&n_multi, h->d_cpmulti, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(h, hipStreamSynchronize(stream));
-    std::vector<uint32_t> multi(n_multi);
-    if (n_multi)
-        HIP_TRY(h, hipMemcpy(multi.data(), h->d_cpmulti + 1, sizeof(uint32_t) * n_multi, hipMemcpyDeviceToHost));
-    std::sort(multi.begin(), multi.end());
+    CPBatch b{};
+    b.owner = h->d_cp_owner;
+    b.chk = h->d_cp_chk;
+    b.assume = h->d_cp_assume;
+    b.rec = h->d_cp_rec;
+    b.pbits = pbits;
+    b.pmask = (1ull << pbits) - 1;
+    b.changed = h->d_cp_changed;
+    b.lim = any_lim ? 1 : 0;
+    HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
+    HIP_TRY(h, launch_cp_prep2(c, b, stream));  // sets *changed iff a request has several values
+    if (n_values == 0) {  // every request is BAD_REQUEST, NO_RULE_EXISTS or out of bounds (none reaches the limiter)
+        HIP_TRY(h, launch_cp_finish_batch(c, stream));
+        int err = 0;
+        HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        h->cp_rounds = 0;
+        if (err & kErrTime) return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+        if (err & kErrBounds) return fail(h, SG_E_INVAL, "a request's values lie outside the value array");
+        if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 limiter periods");
+        return SG_OK;
+    }
+    uint64_t* sorted = nullptr;
+    HIP_TRY(h, radix_sort_records(h->d_cp_rec, h->d_cp_rec2, nv, pbits, h->d_cp_hist, &sorted, stream, pbits + gbits));
+    HIP_TRY(h, launch_cp_order(c, b, sorted, nv, stream));
+    if (any_lim) {  // after validation: a rejected batch leaves the limiter untouched
+        BatchArgs a{};
+        int kb = bits_for((uint64_t)R);
+        if (kb < 1) kb = 1;
+        a.n = n;
+        a.rec = h->d_rec;
+        a.kshift = 64 - kb;
+        a.K = R;
+        a.bnd = h->d_bnd;
+        a.np = h->d_np;
+        a.p0 = h->d_p0;
+        a.out = out;
+        a.err = h->d_err;
+        HIP_TRY(h, launch_cp_limprep(c, a, stream));
+        LimArgs L{};
+        L.n_lim = h->n_lim;
+        L.wl_idx = 0;  // the cparam batch's 100 ms periods are row 0
+        std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
+        L.rule_lim = h->d_cp_rule_lim;
+        L.slot = h->d_lim_slot;
+        const uint64_t tiles = n / 4096 + 1;
+        L.tile_tot = h->d_lim_tile;
+        L.tile_off = h->d_lim_tile + tiles * kMaxLim;
+        L.arrivals = h->d_lim_period;
+        L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
+        L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
+        L.ring = h->d_lim_ring;
+        HIP_TRY(h, launch_limiter(a, L, stream));
+    }
+    // one lane per (rule, value) slot: k_seg's lists over the sorted value records
     BatchArgs sgm{};
-    sgm.kshift = c.ibits;
+    sgm.n = nv;
+    sgm.rec_sorted = sorted;
+    sgm.kshift = pbits;
     sgm.K = (uint32_t)h->cptotal;
     sgm.err = h->d_err;
     sgm.long_list = h->d_long_list;
@@ -1494,20 +1598,70 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     sgm.short_list = h->d_short_list;
     sgm.short_count = h->d_long_count + 1;
     for (int cl = 0; cl < kClasses; ++cl) sgm.class_off[cl] = h->class_off[cl];
-    sgm.short_max = 0xFFFFFFFFu;  // one lane per (rule, value)
-    uint64_t lo = 0;
-    for (size_t mi = 0; mi <= multi.size(); ++mi) {
-        const uint64_t hi = mi < multi.size() ? multi[mi] : n;
-        HIP_TRY(h, launch_cp_range(c, sgm, lo, hi, h->d_rec, h->d_rec_sorted, h->d_hist, c.ibits, c.ibits + gbits, stream));
-        if (mi < multi.size()) HIP_TRY(h, launch_cp_multi(c, hi, stream));
-        lo = hi + 1;
+    sgm.short_max = 0xFFFFFFFFu;
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_seg(sgm, stream));
+    // are there multi-value requests? (then the rings of the touched slots are saved for the re-walks)
+    uint32_t counts[1 + kClasses];
+    int err = 0, has_multi = 0;
+    HIP_TRY(h, hipMemcpyAsync(counts, h->d_long_count, sizeof(counts), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipMemcpyAsync(&has_multi, h->d_cp_changed, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    uint64_t touched = 0;
+    for (uint32_t x : counts) touched += x;
+    if (!err && has_multi && touched > 0) {
+        if (touched * h->cpstride > h->cp_save_cap) {
+            dfree(h->d_cp_save);
+            if (hipMalloc(&h->d_cp_save, sizeof(CPBucket) * touched * h->cpstride) != hipSuccess)
+                return fail(h, SG_E_NOMEM, "cparam ring save area");
+            h->cp_save_cap = touched * h->cpstride;
+        }
+        b.save = h->d_cp_save;
+        HIP_TRY(h, launch_cp_saverings(c, b, sgm, 0, stream));
     }
-    int err = 0;
+    // rounds: walk every slot under the assumed multi-value outcomes, then recompute the outcomes
+    const uint32_t kMaxRounds = h->cp_max_rounds;
+    uint32_t round = 0;
+    bool converged = false;
+    if (!err && !has_multi) {  // single-value requests only: the slots are independent, one walk is exact
+        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
+        converged = true;
+    }
+    while (!err && !converged && round < kMaxRounds) {
+        if (round > 0) HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
+        HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
+        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
+        HIP_TRY(h, launch_cp_combine(c, b, stream));
+        int changed = 0;
+        HIP_TRY(h, hipMemcpyAsync(&changed, h->d_cp_changed, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        ++round;
+        if (!changed) {
+            converged = true;
+            break;
+        }
+    }
+    if (!err && !converged) {  // rare: the batch on one thread, from the saved rings
+        HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
+        HIP_TRY(h, launch_cp_serial(c, b, stream));
+    }
+    h->cp_rounds = converged ? (round ? round : 1) : kMaxRounds + 1;
+    HIP_TRY(h, launch_cp_finish_batch(c, stream));
     HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipStreamSynchronize(stream));
     if (err & kErrTime) return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
-    if (err & kErrBounds) return fail(h, SG_E_INVAL, "a request's values lie outside the value array");
+    if (err & kErrBounds)
+        return fail(h, SG_E_INVAL, "a request's values lie outside the value array, overlap another's or go backwards");
     if (err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param rule's value table is full");
+    if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 limiter periods");
+    return SG_OK;
+}
+
+int sg_cparam_last_rounds(const sg_handle* h, uint32_t* rounds) {
+    if (!h || !rounds) return SG_E_INVAL;
+    *rounds = h->cp_rounds;
     return SG_OK;
 }
 

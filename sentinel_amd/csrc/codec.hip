@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(kDecFrames) k_codec_decode(CodecArgs c) {
         const uint64_t i1 = min(i0 + (uint64_t)kDecFrames, c.n);
         const uint32_t lo = c.offsets[i0], hi = c.offsets[i1];
         const uint32_t a0 = lo & ~3u;
-        const bool staged = hi - a0 <= kDecStage;
+        const bool staged = hi >= lo && hi - a0 <= kDecStage;  // (offsets running backwards: read in place)
         if (staged && hi > lo) {
             const uint32_t words = (hi - a0 + 3) / 4;
             const uint32_t* src = reinterpret_cast<const uint32_t*>(c.payload) + a0 / 4;
@@ -92,8 +92,8 @@ __global__ void __launch_bounds__(kDecFrames) k_codec_decode(CodecArgs c) {
         __syncthreads();
         const uint64_t i = i0 + threadIdx.x;
         if (i < i1) {
-            const uint32_t off = c.offsets[i];
-            const uint32_t len = c.offsets[i + 1] - off;
+            const uint32_t off = c.offsets[i], end = c.offsets[i + 1];
+            const uint32_t len = end >= off ? end - off : 0u;  // a backwards frame decodes as SG_FRAME_SHORT
             decode_frame(c, i, staged ? sb + (off - a0) : c.payload + off, len);
         }
         __syncthreads();  // the stage is refilled by the next step

@@ -10,12 +10,13 @@
 // a value's adds in period p imply the flow was touched in p). So each (rule, value) is an independent
 // ring of S {period start, count} — an exact open-addressing sub-table per rule in HBM, as for the local
 // hot-parameter path (param.hip) — and single-value requests are independent per (rule, value):
-//   k_cp_prep   validation (BAD_REQUEST / NO_RULE_EXISTS), find-or-insert of (rule, value), packed record
-//               {slot | request index}; results start as BLOCKED.
-//   radix sort by slot (sort.hip), then k_seg (engine.hip) + k_cp_walk: one lane per (rule, value)
-//               segment, sequential replay (window sum, threshold - avg - count >= 0, add).
-// A request with several values is all-or-nothing across its values: the host driver (api.cpp) cuts the
-// batch at such requests and decides each of them alone (k_cp_multi) between the single-value runs.
+//   k_cp_limprep + launch_limiter (limiter.hip)  allowProceed → GlobalRequestLimiter.tryPass of the rule's
+//               namespace (ClusterParamFlowChecker.java:43-45), state shared with the flow-token path;
+//   k_cp_prep2  validation (BAD_REQUEST / NO_RULE_EXISTS), find-or-insert of every (rule, value), one packed
+//               record {slot | value position} per value;
+//   radix sort by slot (sort.hip), k_seg (engine.hip), then k_cp_walk2: one lane per (rule, value) slot,
+//               sequential replay (window sum, threshold - avg - count >= 0, add);
+//   requests with several values (all-or-nothing over their values) are resolved by the fixed point below.
 #include "engine.h"
 
 namespace sg {
@@ -104,153 +105,6 @@ __device__ __forceinline__ int64_t cp_window(const CPBucket* ring, int S, int64_
 }
 
 }  // namespace
-
-__global__ void __launch_bounds__(256) k_cp_prep(CPArgs c, uint64_t lo, uint64_t hi, uint64_t sentinel) {
-    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * blockDim.x) {
-        const sg_cparam_req q = c.req[i];
-        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *c.last_ts : q.ts_ms < c.req[i - 1].ts_ms)) atomicOr(c.err, kErrTime);
-        const uint32_t key = q.key & SG_KEY_INDEX;
-        uint64_t rec = sentinel;
-        if (key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) {
-            cp_store(c.out, i, SG_STATUS_BAD_REQUEST, 0);
-        } else if (key >= c.n_rules) {
-            cp_store(c.out, i, SG_STATUS_NO_RULE_EXISTS, 0);
-        } else {
-            cp_store(c.out, i, SG_STATUS_BLOCKED, 0);  // the walkers write the passes
-            if ((uint64_t)q.value_begin + q.value_count > c.n_values) {
-                atomicOr(c.err, kErrBounds);
-            } else if (q.value_count == 1) {  // (several values: decided alone by k_cp_multi)
-                const uint64_t g = cp_slot(c, c.rules[key], c.values[q.value_begin]);
-                if (g == ~0ull) atomicOr(c.err, kErrTableFull);
-                else rec = (g << c.ibits) | (i - lo);
-            }
-        }
-        c.rec[i - lo] = rec;
-    }
-}
-
-// One lane per (rule, value) segment of the sorted records of [lo, hi).
-__global__ void __launch_bounds__(256) k_cp_walk(CPArgs c, BatchArgs sg, uint64_t lo) {
-    if (*c.err) return;
-    const int lane = (int)__lane_id();
-    uint32_t cnt[kClasses], grp_end[kClasses];
-    uint32_t total = 0;
-    for (int k = kClasses - 1; k >= 0; --k) {
-        cnt[k] = sg.short_count[k];
-        total += (cnt[k] + 63) / 64;
-        grp_end[k] = total;
-    }
-    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t gi = wave; gi < total; gi += nwaves) {
-        int cl = kClasses - 1;
-        uint32_t g0 = 0;
-        while (gi >= grp_end[cl]) {
-            g0 = grp_end[cl];
-            --cl;
-        }
-        const uint32_t i = (gi - g0) * 64 + (uint32_t)lane;
-        if (i >= cnt[cl]) continue;
-        uint64_t j = sg.short_list[sg.class_off[cl] + i];
-        const uint64_t g = sg.rec_sorted[j] >> c.ibits;
-        const CPRule r = c.rules[cp_rule_of_slot(c, g)];
-        const double thr = cp_threshold(c, r, c.keys[g]);  // the side slot's key stays ~0, its value
-        CPBucket* ring = c.ring + g * (uint64_t)c.stride;
-        const int S = r.S;
-        const int64_t wl = r.wl;
-        int64_t P = INT64_MIN, other = 0, cur = 0;
-        for (; j < sg.n; ++j) {
-            const uint64_t rec = sg.rec_sorted[j];
-            if ((rec >> c.ibits) != g) break;
-            const uint64_t idx = lo + (rec & c.imask);
-            const sg_cparam_req q = c.req[idx];
-            const int64_t Pq = q.ts_ms / wl;
-            if (Pq != P) {  // currentWindow(t): close the open period, open this one
-                if (P != INT64_MIN) {
-                    CPBucket b;
-                    b.start = P * wl;
-                    b.count = cur;
-                    ring[(int)(P % S)] = b;
-                }
-                P = Pq;
-                other = cp_window(ring, S, wl, P, &cur);
-            }
-            // ClusterParamFlowChecker.java:62-70: threshold - getAvg(value) - count
-            const double latest = (double)(other + cur) / r.isec;
-            const double rem = thr - latest - (double)q.acquire;
-            if (rem >= 0) {
-                cur += q.acquire;  // addValue
-                cp_store(c.out, idx, SG_STATUS_OK, cp_d2i(rem));
-            }
-        }
-        if (P != INT64_MIN) {
-            CPBucket b;
-            b.start = P * wl;
-            b.count = cur;
-            ring[(int)(P % S)] = b;
-        }
-    }
-}
-
-// One request with several values (index m), all-or-nothing (ClusterParamFlowChecker.java:58-80).
-__global__ void k_cp_multi(CPArgs c, uint64_t m) {
-    if (*c.err) return;
-    const sg_cparam_req q = c.req[m];
-    if (q.ts_ms < 0 || (m == 0 ? q.ts_ms < *c.last_ts : q.ts_ms < c.req[m - 1].ts_ms)) {
-        atomicOr(c.err, kErrTime);
-        return;
-    }
-    const uint32_t key = q.key & SG_KEY_INDEX;
-    if (key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) {
-        cp_store(c.out, m, SG_STATUS_BAD_REQUEST, 0);
-        return;
-    }
-    if (key >= c.n_rules) {
-        cp_store(c.out, m, SG_STATUS_NO_RULE_EXISTS, 0);
-        return;
-    }
-    if ((uint64_t)q.value_begin + q.value_count > c.n_values) {
-        atomicOr(c.err, kErrBounds);
-        return;
-    }
-    const CPRule r = c.rules[key];
-    const int64_t P = q.ts_ms / r.wl;
-    bool passed = true;
-    for (uint32_t v = 0; v < q.value_count && passed; ++v) {
-        const uint64_t value = c.values[q.value_begin + v];
-        const uint64_t g = cp_slot(c, r, value);
-        if (g == ~0ull) {
-            atomicOr(c.err, kErrTableFull);
-            return;
-        }
-        int64_t cur = 0;
-        const int64_t other = cp_window(c.ring + g * (uint64_t)c.stride, r.S, r.wl, P, &cur);
-        const double rem = cp_threshold(c, r, value) - (double)(other + cur) / r.isec - (double)q.acquire;
-        passed = rem >= 0;
-    }
-    if (passed) {
-        for (uint32_t v = 0; v < q.value_count; ++v) {  // addValue for every value (duplicates add twice)
-            const uint64_t g = cp_slot(c, r, c.values[q.value_begin + v]);
-            CPBucket* ring = c.ring + g * (uint64_t)c.stride;
-            CPBucket& b = ring[(int)(P % r.S)];
-            if (b.start != P * r.wl) {
-                b.start = P * r.wl;
-                b.count = 0;
-            }
-            b.count += q.acquire;
-        }
-    }
-    cp_store(c.out, m, passed ? SG_STATUS_OK : SG_STATUS_BLOCKED, passed ? -1 : 0);
-}
-
-__global__ void k_cp_finish(CPArgs c, uint64_t last) {
-    if (*c.err == 0) *c.last_ts = c.req[last].ts_ms;
-}
-
-__global__ void __launch_bounds__(256) k_cp_count_multi(CPArgs c, uint32_t* list, uint32_t* count) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (c.req[i].value_count > 1 && (c.req[i].key & SG_KEY_INDEX) < c.n_rules) list[atomicAdd(count, 1u)] = (uint32_t)i;
-}
 
 __global__ void __launch_bounds__(256) k_cp_clear(uint64_t* keys, CPBucket* ring, uint64_t slots, int stride) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < slots * stride; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -348,45 +202,316 @@ hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out,
     return hipGetLastError();
 }
 
-hipError_t launch_cp_count_multi(const CPArgs& c, uint32_t* list, uint32_t* count, hipStream_t stream) {
-    hipLaunchKernelGGL(k_cp_count_multi, dim3(cgrid(c.n, 4096)), dim3(256), 0, stream, c, list, count);
-    return hipGetLastError();
+}  // namespace sg
+
+// ------------------------------------------------------------------- one pipeline, multi-value requests
+//
+// Every value of every request becomes a record {slot | value position}; value positions increase with the
+// request index (sg_cparam_req contract), so a slot's records sorted by position are in arrival order and a
+// request's duplicate values are adjacent. A lane walks a slot: single-value requests exactly as k_cp_walk; a
+// multi-value request (ClusterParamFlowChecker.java:58-80: every value checked against the pre-request state,
+// then all added iff all passed) writes its check for this value and adds its count iff its outcome is assumed to
+// be a pass. k_cp_combine then sets each multi-value request's outcome to the AND of its checks. The walk of a
+// slot is exact once the outcomes of the earlier multi-value requests touching it are, so re-walking from the
+// saved pre-batch rings until no outcome changes converges to the sequential answer; with the assumption
+// "passes" most batches need one or two rounds. k_cp_serial (one thread, arrival order) is the fallback when
+// the rounds run out.
+
+namespace sg {
+
+namespace {
+
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool cp_valid(const CPArgs& c, const sg_cparam_req& q) {
+    const uint32_t key = q.key & SG_KEY_INDEX;
+    return !(key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) && key < c.n_rules;
 }
 
-// Single-value requests of [lo, hi): prep, sort by slot, segments, walk.
-hipError_t launch_cp_range(const CPArgs& c, BatchArgs& sg, uint64_t lo, uint64_t hi, uint64_t* a_buf, uint64_t* b_buf,
-                           uint32_t* hist, int lo_bit, int hi_bit, hipStream_t stream) {
-    const uint64_t n = hi - lo;
-    if (n == 0) return hipSuccess;
-    const uint64_t sentinel = c.total_slots << c.ibits;
-    CPArgs q = c;
-    q.rec = a_buf;
-    hipLaunchKernelGGL(k_cp_prep, dim3(cgrid(n, 8192)), dim3(256), 0, stream, q, lo, hi, sentinel);
-    uint64_t* sorted = nullptr;
-    hipError_t e = radix_sort_records(a_buf, b_buf, n, lo_bit, hist, &sorted, stream, hi_bit);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(sg.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
-    sg.n = n;
-    sg.rec_sorted = sorted;
-    e = launch_seg(sg, stream);
-    if (e != hipSuccess) return e;
-    static unsigned blocks = 0;
-    if (blocks == 0) {
-        int dev = 0, cus = 0, per_cu = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cp_walk, 256, 0);
-        blocks = (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+}  // namespace
+
+// The 100 ms limiter periods of the batch (row 0 of the period table) and {cparam rule | request} records of the
+// valid requests; runs after k_cp_prep2, and the limiter then overwrites the refused requests' results with
+// TOO_MANY_REQUEST (the walkers skip them).
+__global__ void __launch_bounds__(256) k_cp_limprep(CPArgs c, BatchArgs a) {
+    const int64_t t0 = c.req[0].ts_ms;
+    const uint64_t sentinel = (uint64_t)a.K << a.kshift;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[i];
+        const int64_t t = q.ts_ms;
+        if (i == 0) {
+            a.p0[0] = t / 100;
+        } else {
+            const int64_t tp = c.req[i - 1].ts_ms;
+            if (t > tp && tp >= 0) {
+                for (int64_t p = tp / 100 + 1; p <= t / 100; ++p) {
+                    const int64_t qq = p - t0 / 100;
+                    if (qq >= (int64_t)kMaxPeriods) {
+                        atomicOr(c.err, kErrPeriods);
+                        break;
+                    }
+                    if (qq > 0) a.bnd[qq] = (uint32_t)i;
+                }
+            }
+        }
+        if (i == c.n - 1) {
+            const int64_t qq = t / 100 - t0 / 100 + 1;
+            a.np[0] = qq > (int64_t)kMaxPeriods ? kMaxPeriods : (uint32_t)qq;
+        }
+        a.rec[i] = cp_valid(c, q) ? (((uint64_t)(q.key & SG_KEY_INDEX) << a.kshift) | i) : sentinel;
     }
-    hipLaunchKernelGGL(k_cp_walk, dim3(blocks), dim3(256), 0, stream, c, sg, lo);
-    hipLaunchKernelGGL(k_cp_finish, dim3(1), dim3(1), 0, stream, c, hi - 1);
+}
+
+__global__ void __launch_bounds__(256) k_cp_recinit(CPBatch b, uint64_t n_values, uint64_t sentinel) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_values; p += (uint64_t)gridDim.x * blockDim.x) {
+        b.rec[p] = sentinel | p;
+        b.owner[p] = kNoOwner;
+        b.chk[p] = 0;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[i];
+        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *c.last_ts : q.ts_ms < c.req[i - 1].ts_ms)) atomicOr(c.err, kErrTime);
+        const uint32_t key = q.key & SG_KEY_INDEX;
+        b.assume[i] = 1;
+        if (key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) {
+            cp_store(c.out, i, SG_STATUS_BAD_REQUEST, 0);
+            continue;
+        }
+        if (key >= c.n_rules) {
+            cp_store(c.out, i, SG_STATUS_NO_RULE_EXISTS, 0);
+            continue;
+        }
+        cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+        if ((uint64_t)q.value_begin + q.value_count > c.n_values) {
+            atomicOr(c.err, kErrBounds);
+            continue;
+        }
+        if (q.value_count > 1) *b.changed = 1;  // vector store; the host reads it as "has multi-value requests"
+        const CPRule r = c.rules[key];
+        for (uint32_t j = 0; j < q.value_count; ++j) {
+            const uint64_t p = (uint64_t)q.value_begin + j;
+            if (atomicCAS(&b.owner[p], kNoOwner, (uint32_t)i) != kNoOwner) {  // value ranges must not overlap
+                atomicOr(c.err, kErrBounds);
+                continue;
+            }
+            const uint64_t g = cp_slot(c, r, c.values[p]);
+            if (g == ~0ull) atomicOr(c.err, kErrTableFull);
+            else b.rec[p] = (g << b.pbits) | p;
+        }
+    }
+}
+
+// Within a slot, value positions (the sort order) must follow the request order: the walk replays them in that
+// order. Checked on the sorted records, before anything is charged.
+__global__ void __launch_bounds__(256) k_cp_order(CPArgs c, CPBatch b, const uint64_t* sorted, uint64_t n) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r0 = sorted[j - 1], r1 = sorted[j];
+        if ((r0 >> b.pbits) != (r1 >> b.pbits)) continue;
+        const uint32_t a0 = b.owner[r0 & b.pmask], a1 = b.owner[r1 & b.pmask];
+        if (a0 != kNoOwner && a1 != kNoOwner && a1 < a0) atomicOr(c.err, kErrBounds);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cp_walk2(CPArgs c, CPBatch b, BatchArgs sg) {
+    if (*c.err) return;
+    uint32_t total = *sg.long_count;
+    for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        uint32_t r0 = t;
+        uint64_t j;
+        if (r0 < *sg.long_count) {
+            j = sg.long_list[r0];
+        } else {
+            r0 -= *sg.long_count;
+            int k = 0;
+            while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
+            j = sg.short_list[sg.class_off[k] + r0];
+        }
+        const uint64_t g = sg.rec_sorted[j] >> b.pbits;
+        const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+        const double thr = cp_threshold(c, r, c.keys[g]);
+        CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+        const int S = r.S;
+        const int64_t wl = r.wl;
+        int64_t P = INT64_MIN, other = 0, cur = 0;
+        while (j < sg.n) {
+            const uint64_t rec = sg.rec_sorted[j];
+            if ((rec >> b.pbits) != g) break;
+            const uint64_t p = rec & b.pmask;
+            const uint32_t i = b.owner[p];
+            if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) {  // allowProceed refused it
+                ++j;
+                continue;
+            }
+            const sg_cparam_req q = c.req[i];
+            const int64_t Pq = q.ts_ms / wl;
+            if (Pq != P) {  // currentWindow(t): close the open period, open this one
+                if (P != INT64_MIN) {
+                    CPBucket bk;
+                    bk.start = P * wl;
+                    bk.count = cur;
+                    ring[(int)(P % S)] = bk;
+                }
+                P = Pq;
+                other = cp_window(ring, S, wl, P, &cur);
+            }
+            const double rem = thr - (double)(other + cur) / r.isec - (double)q.acquire;
+            if (q.value_count == 1) {
+                if (rem >= 0) {
+                    cur += q.acquire;
+                    cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
+                } else {
+                    cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+                }
+                ++j;
+                continue;
+            }
+            // a multi-value request: its records in this slot (duplicate values) all check the pre-request state
+            uint64_t e = j;
+            while (e < sg.n && (sg.rec_sorted[e] >> b.pbits) == g && b.owner[sg.rec_sorted[e] & b.pmask] == i) {
+                b.chk[sg.rec_sorted[e] & b.pmask] = rem >= 0 ? 1 : 0;
+                ++e;
+            }
+            if (b.assume[i]) cur += (int64_t)q.acquire * (int64_t)(e - j);
+            j = e;
+        }
+        if (P != INT64_MIN) {
+            CPBucket bk;
+            bk.start = P * wl;
+            bk.count = cur;
+            ring[(int)(P % S)] = bk;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
+    if (*c.err) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[i];
+        if (q.value_count < 2 || !cp_valid(c, q)) continue;
+        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
+        bool pass = true;
+        for (uint32_t j = 0; j < q.value_count && pass; ++j) pass = b.chk[(uint64_t)q.value_begin + j] != 0;
+        cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? -1 : 0);  // remaining -1: multi-value
+        if ((b.assume[i] != 0) != pass) {
+            b.assume[i] = pass ? 1 : 0;
+            *b.changed = 1;
+        }
+    }
+}
+
+// Save (restore = 0) or restore (1) the first S buckets of every touched slot.
+__global__ void __launch_bounds__(256) k_cp_saverings(CPArgs c, CPBatch b, BatchArgs sg, int restore) {
+    uint32_t total = *sg.long_count;
+    for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
+    const uint64_t work = (uint64_t)total * c.stride;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < work; w += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t r0 = (uint32_t)(w / c.stride);
+        const int x = (int)(w % c.stride);
+        const uint32_t t = r0;
+        uint64_t j;
+        if (r0 < *sg.long_count) {
+            j = sg.long_list[r0];
+        } else {
+            r0 -= *sg.long_count;
+            int k = 0;
+            while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
+            j = sg.short_list[sg.class_off[k] + r0];
+        }
+        const uint64_t g = sg.rec_sorted[j] >> b.pbits;
+        CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+        if (restore) ring[x] = b.save[(uint64_t)t * c.stride + x];
+        else b.save[(uint64_t)t * c.stride + x] = ring[x];
+    }
+}
+
+// Fallback: the whole batch on one thread in arrival order (the rings are the pre-batch ones).
+__global__ void k_cp_serial(CPArgs c, CPBatch b) {
+    if (*c.err) return;
+    for (uint64_t i = 0; i < c.n; ++i) {
+        const sg_cparam_req q = c.req[i];
+        if (!cp_valid(c, q)) continue;
+        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
+        const CPRule r = c.rules[q.key & SG_KEY_INDEX];
+        const int64_t P = q.ts_ms / r.wl;
+        bool pass = true;
+        double rem = -1;
+        for (uint32_t v = 0; v < q.value_count && pass; ++v) {
+            const uint64_t value = c.values[q.value_begin + v];
+            const uint64_t g = cp_slot(c, r, value);
+            int64_t cur = 0;
+            const int64_t other = cp_window(c.ring + g * (uint64_t)c.stride, r.S, r.wl, P, &cur);
+            rem = cp_threshold(c, r, value) - (double)(other + cur) / r.isec - (double)q.acquire;
+            pass = rem >= 0;
+        }
+        if (pass) {
+            for (uint32_t v = 0; v < q.value_count; ++v) {
+                const uint64_t g = cp_slot(c, r, c.values[q.value_begin + v]);
+                CPBucket& bk = c.ring[g * (uint64_t)c.stride + (int)(P % r.S)];
+                if (bk.start != P * r.wl) {
+                    bk.start = P * r.wl;
+                    bk.count = 0;
+                }
+                bk.count += q.acquire;
+            }
+        }
+        if (q.value_count > 1) rem = -1;
+        cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? cp_d2i(rem) : 0);
+    }
+}
+
+static unsigned cgrid2(uint64_t n, unsigned cap) {
+    uint64_t g = (n + 255) / 256;
+    return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
+}
+
+hipError_t launch_cp_limprep(const CPArgs& c, BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_limprep, dim3(cgrid2(c.n, 8192)), dim3(256), 0, stream, c, a);
     return hipGetLastError();
 }
 
-hipError_t launch_cp_multi(const CPArgs& c, uint64_t m, hipStream_t stream) {
-    hipLaunchKernelGGL(k_cp_multi, dim3(1), dim3(1), 0, stream, c, m);
-    hipLaunchKernelGGL(k_cp_finish, dim3(1), dim3(1), 0, stream, c, m);
+hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
+    const uint64_t sentinel = c.total_slots << b.pbits;
+    hipLaunchKernelGGL(k_cp_recinit, dim3(cgrid2(c.n_values, 8192)), dim3(256), 0, stream, b, c.n_values, sentinel);
+    hipLaunchKernelGGL(k_cp_prep2, dim3(cgrid2(c.n, 8192)), dim3(256), 0, stream, c, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_order(const CPArgs& c, const CPBatch& b, const uint64_t* sorted, uint64_t n, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_order, dim3(cgrid2(n, 8192)), dim3(256), 0, stream, c, b, sorted, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_walk2, dim3(cgrid2(sg.n, 4096)), dim3(256), 0, stream, c, b, sg);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_combine, dim3(cgrid2(c.n, 8192)), dim3(256), 0, stream, c, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_saverings(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, int restore, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_saverings, dim3(cgrid2(sg.n * (uint64_t)c.stride, 8192)), dim3(256), 0, stream, c, b, sg,
+                       restore);
+    return hipGetLastError();
+}
+
+__global__ void k_cp_finish_batch(CPArgs c) {
+    if (*c.err == 0) *c.last_ts = c.req[c.n - 1].ts_ms;
+}
+
+hipError_t launch_cp_finish_batch(const CPArgs& c, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_finish_batch, dim3(1), dim3(1), 0, stream, c);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_serial(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_serial, dim3(1), dim3(1), 0, stream, c, b);
     return hipGetLastError();
 }
 

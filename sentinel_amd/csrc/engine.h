@@ -286,13 +286,32 @@ struct CPArgs {
     int64_t* last_ts;
 };
 
+// One pipeline for single- and multi-value requests (cparam.hip): per-value records sorted by (slot, value
+// position), a lane per slot, and a fixed point over the multi-value requests' all-or-nothing outcomes.
+struct CPBatch {
+    uint32_t* owner;          // [n_values] request that owns value position p (~0 = none)
+    uint8_t* chk;             // [n_values] the value's check at its request (multi-value requests)
+    uint8_t* assume;          // [n] multi-value request: assumed outcome of this iteration
+    uint64_t* rec;            // [n_values] {slot : high bits | value position : pbits}
+    int pbits;
+    uint64_t pmask;
+    int* changed;
+    CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots
+    int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
+};
+hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream);
+hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+hipError_t launch_cp_saverings(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, int restore, hipStream_t stream);
+hipError_t launch_cp_serial(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+hipError_t launch_cp_finish_batch(const CPArgs& c, hipStream_t stream);
+hipError_t launch_cp_order(const CPArgs& c, const CPBatch& b, const uint64_t* sorted, uint64_t n, hipStream_t stream);
+// The namespace limiter for a cparam batch: 100 ms period table (row 0 of a.bnd) and per-request records with the
+// cparam rule index as key; then launch_limiter marks TOO_MANY_REQUEST.
+hipError_t launch_cp_limprep(const CPArgs& c, BatchArgs& a, hipStream_t stream);
 hipError_t launch_cp_clear(uint64_t* keys, CPBucket* ring, uint64_t slots, int stride, hipStream_t stream);
 hipError_t launch_cp_copy(const uint64_t* okeys, const CPBucket* oring, uint64_t obase, int ostride, uint64_t* nkeys,
                           CPBucket* nring, uint64_t nbase, int nstride, uint64_t slots, int S, hipStream_t stream);
-hipError_t launch_cp_count_multi(const CPArgs& c, uint32_t* list, uint32_t* count, hipStream_t stream);
-hipError_t launch_cp_range(const CPArgs& c, BatchArgs& sg, uint64_t lo, uint64_t hi, uint64_t* a_buf, uint64_t* b_buf,
-                           uint32_t* hist, int lo_bit, int hi_bit, hipStream_t stream);
-hipError_t launch_cp_multi(const CPArgs& c, uint64_t m, hipStream_t stream);
 hipError_t launch_cp_read(const CPArgs& c, uint32_t rule, uint64_t value, int64_t now, int64_t* out_dev, hipStream_t stream);
 struct CPTop {                // a (rule, value) window sum for ClusterParamMetric.getTopValues
     uint64_t value;

@@ -84,6 +84,7 @@ __device__ int64_t lim_xmax(double qps) {
 }
 
 __global__ void __launch_bounds__(kLimThreads) k_lim_plan(BatchArgs a, LimArgs L, uint32_t ntiles) {
+    if (*a.err) return;  // a rejected batch leaves the limiter untouched
     const int tid = threadIdx.x;
     // (1) exclusive scan of per-tile totals, slot by slot (thread-strided partial sums + carry)
     __shared__ uint32_t part[kLimThreads];
@@ -150,6 +151,7 @@ __global__ void __launch_bounds__(kLimThreads) k_lim_apply(BatchArgs a, LimArgs 
     const uint32_t* bnd = a.bnd + (size_t)L.wl_idx * kMaxPeriods;
     const uint32_t np = a.np[L.wl_idx];
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
+    if (*a.err) return;
     if (tid < kMaxLim) run[tid] = L.tile_off[(size_t)blockIdx.x * kMaxLim + tid];
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;

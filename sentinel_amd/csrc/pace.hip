@@ -206,13 +206,17 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
         // Every walked request has acquireCount >= 1 (k_pace_prep decides the rest), so its cost is at
         // least cost(1) and it can only pass at t >= latest + cost(1) - max(maxQ, 0): requests before that
         // instant are blocked without changing latestPassedTime, and the walker jumps over them.
+        // The bound needs latest + cost(a) not to wrap for any acquireCount a: a wrapped sum is negative and
+        // passes (Java long arithmetic), however early the request. cost is monotone in a, so checking the
+        // largest int acquireCount covers them all; otherwise the walker takes every request in turn.
         const int64_t cost1 = pace_cost(r.count, 1);
+        const int64_t cost_max = pace_cost(r.count, INT32_MAX);
         const int64_t slack = r.max_queueing_ms > 0 ? (int64_t)r.max_queueing_ms : 0;
         auto ts_at = [&](uint64_t q) { return p.req[(uint32_t)(p.rec_sorted[q] & p.imask)].ts_ms; };
         uint64_t base = s;
         while (base < e) {
-            int64_t horizon;
-            if (!__builtin_add_overflow(latest, cost1, &horizon)) {  // no wrap: the bound is exact
+            int64_t horizon, top;
+            if (!__builtin_add_overflow(latest, cost_max, &top) && !__builtin_add_overflow(latest, cost1, &horizon)) {
                 horizon -= slack;
                 if (ts_at(base) < horizon) {
                     base = pace_wave_search(base, e, [&](uint64_t q) { return ts_at(q) >= horizon; }, lane);

@@ -22,7 +22,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
-           "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values",
+           "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values", "sg_cparam_last_rounds",
            "sg_pslot_load_rules", "sg_pslot_decide_batch", "sg_pslot_decide_batch_host", "sg_pslot_thread_count",
            "sg_pslot_param_idx",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
@@ -93,6 +93,7 @@ def load_library():
         "sg_pslot_thread_count": (C.c_int, [vp, u32, C.c_int32, u64, C.POINTER(i64)]),
         "sg_pslot_param_idx": (C.c_int, [vp, u32, C.POINTER(C.c_int32)]),
         "sg_cparam_top_values": (C.c_int, [vp, i64, u32, vp, vp, vp]),
+        "sg_cparam_last_rounds": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
         "sg_conc_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_conc_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_conc_expire": (C.c_int, [vp, i64, vp, u32, C.POINTER(u64)]),
@@ -431,6 +432,12 @@ class FlowEngine:
         hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
         self._check(self._L.sg_cparam_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot),
                                                  capacity_log2))
+
+    def cparam_last_rounds(self) -> int:
+        """Fixed-point rounds the last sg_cparam_decide_batch needed (max_rounds + 1: decided serially)."""
+        r = C.c_uint32()
+        self._check(self._L.sg_cparam_last_rounds(self.h, C.byref(r)))
+        return r.value
 
     def cparam_decide_host(self, req: np.ndarray, values: np.ndarray) -> np.ndarray:
         req = np.ascontiguousarray(req, dtype=abi.CPARAM_REQ_DTYPE)

@@ -31,3 +31,14 @@ _ensure_oracle()
 @pytest.fixture(params=OFFSETS)
 def t0(request):
     return request.param
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _torch_hip_first(request):
+    """GPU runs: torch's HIP runtime initialises before the library's (tests that hand torch device buffers to
+    the library find no device when the library came first). Only when GPU tests were selected."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield

@@ -93,6 +93,20 @@ def test_decode_without_rules_is_no_rule():
     assert list(kind_t.cpu().numpy()) == [abi.FRAME_FLOW, abi.FRAME_FLOW]
 
 
+def test_decode_backwards_offsets_are_short_frames():
+    """A frame whose end offset lies before its start is decoded as SG_FRAME_SHORT (no read), the rest as usual."""
+    rules = _rules(4, np.random.default_rng(2))
+    eng = _engine(rules)
+    frames = [flow_frame(i + 1, int(rules["flow_id"][i % 4]), 1, False) for i in range(6)]
+    payload, offsets = pack(frames)
+    offsets = offsets.copy()
+    offsets[3] = offsets[2] - 3   # frame 2 runs backwards, frame 3 is then longer
+    _, xid_t, kind_t = _decode_gpu(eng, payload, offsets, np.full(6, T0, np.int64))
+    kinds = list(kind_t.cpu().numpy()[:6])
+    assert kinds[2] == abi.FRAME_SHORT
+    assert kinds[:2] == [abi.FRAME_FLOW] * 2 and kinds[4:] == [abi.FRAME_FLOW] * 2
+
+
 def test_encode_matches_oracle():
     import torch
     rng = np.random.default_rng(9)

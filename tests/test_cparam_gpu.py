@@ -108,7 +108,7 @@ def test_hot_items_and_avg_local():
     rules = _rules(4, rng, thr=abi.THRESHOLD_AVG_LOCAL, hot_per_rule=3)
     hot = np.zeros(12, abi.PARAM_HOT_DTYPE)
     for i in range(12):
-        hot[i] = (np.uint64(i % 3 + 1) * np.uint64(0x9E3779B97F4A7C15), int(rng.integers(0, 6)), 0)
+        hot[i] = (int(np.array([i % 3 + 1], np.uint64)[0] * 0x9E3779B97F4A7C15 % (1 << 64)), int(rng.integers(0, 6)), 0)
     eng, ora = _pair(rules, hot, connected=3)
     t = 1_700_000_000_000
     for _ in range(2):
@@ -132,3 +132,106 @@ def test_rule_reload_keeps_surviving_metrics():
     req, vals = _trace(rng, 20_000, len(new), 50, 1_700_000_000_900, 1200)
     _check(eng, ora, req, vals)
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+@pytest.mark.parametrize("seed,multi", [(11, 0.3), (12, 0.8)])
+def test_multi_value_heavy_fixed_point(seed, multi):
+    """Most requests carry several (possibly repeated) values over a few hot values: the all-or-nothing outcomes
+    chain across slots, so the device needs several fixed-point rounds; every result and window sum must still
+    equal the sequential replay."""
+    rng = np.random.default_rng(seed)
+    rules = _rules(5, rng)
+    rules["count"] = rng.integers(3, 12, 5)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_250
+    rounds = []
+    for _ in range(3):
+        req, vals = _trace(rng, 30_000, 5, 12, t, 2500, multi=multi, zipf=1.3, bad=0.005)
+        _check(eng, ora, req, vals)
+        rounds.append(eng.cparam_last_rounds())
+        t = int(req["ts_ms"][-1]) + 3
+    assert max(rounds) > 1
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_serial_fallback(monkeypatch):
+    """With no fixed-point rounds allowed the batch is decided on one thread — same answers."""
+    monkeypatch.setenv("SG_CP_MAX_ROUNDS", "0")
+    rng = np.random.default_rng(13)
+    rules = _rules(4, rng)
+    eng, ora = _pair(rules)
+    req, vals = _trace(rng, 4_000, 4, 10, 1_700_000_000_000, 1500, multi=0.4, zipf=1.2, bad=0.01)
+    _check(eng, ora, req, vals)
+    assert eng.cparam_last_rounds() == 1  # max_rounds (0) + 1: serial
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_limiter_shared_with_flow_tokens():
+    """allowProceed → GlobalRequestLimiter.tryPass (ClusterParamFlowChecker.java:45): the namespace's limiter
+    admits param and flow requests from one 10 x 100 ms window, so time-ordered flow and param batches interleave."""
+    from sentinel_amd.engine import FlowEngine
+    rng = np.random.default_rng(14)
+    ns = np.zeros(2, abi.NS_DTYPE)
+    ns["connected_count"] = [2, 1]
+    ns["limiter_enabled"] = [1, 0]             # namespace 1: no limiter
+    ns["max_allowed_qps"] = [1500, 0]
+    prules = _rules(8, rng)
+    prules["namespace_id"] = np.arange(8) % 2
+    frules = np.zeros(6, abi.RULE_DTYPE)
+    frules["flow_id"] = np.arange(6) + 900
+    frules["count"] = rng.integers(20, 400, 6)
+    frules["threshold_type"] = abi.THRESHOLD_GLOBAL
+    frules["sample_count"], frules["window_interval_ms"] = 10, 1000
+    eng = FlowEngine(device=0, max_batch=1 << 18)
+    eng.set_namespaces(ns)
+    eng.load_rules(frules)
+    eng.cparam_load_rules(prules, None, 12)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(frules)
+    ora.load_param_rules(prules)
+    t = 1_700_000_000_040
+    seen = set()
+    for b in range(4):
+        span = int(rng.integers(300, 1500))
+        req, vals = _trace(rng, 6_000, 8, 60, t, span, multi=0.2, bad=0.01)
+        out = _check(eng, ora, req, vals)
+        seen |= set(out["status"].tolist())
+        t = int(req["ts_ms"][-1])
+        f = np.zeros(3_000, abi.REQ_DTYPE)
+        f["ts_ms"] = t + np.sort(rng.integers(0, 400, len(f)))
+        f["key"] = rng.integers(0, 6, len(f))
+        f["acquire"] = 1
+        want, got = ora.decide(f), eng.decide_host(f)
+        assert np.array_equal(want, got), f"flow batch {b}"
+        seen |= set(want["status"].tolist())
+        t = int(f["ts_ms"][-1])
+    assert abi.TOO_MANY_REQUEST in seen and abi.OK in seen
+
+
+def test_value_range_contract():
+    """Overlapping, backwards or out-of-range value ranges are SG_E_INVAL and change no state."""
+    from sentinel_amd.engine import EngineError
+    rng = np.random.default_rng(15)
+    rules = _rules(3, rng)
+    eng, ora = _pair(rules)
+    req, vals = _trace(rng, 2_000, 3, 20, 1_700_000_000_000, 900, multi=0.3)
+    _check(eng, ora, req, vals)
+    t = int(req["ts_ms"][-1])
+    nxt, nvals = _trace(rng, 1_000, 3, 20, t, 500, multi=0.3)
+    for mutate in ("overlap", "backwards", "outside"):
+        bad = nxt.copy()
+        if mutate == "overlap":
+            bad["value_begin"][10] = bad["value_begin"][9]
+        elif mutate == "backwards":  # two requests on one (rule, value) whose positions run backwards
+            bad["value_begin"][[20, 21]] = bad["value_begin"][[21, 20]]
+            bad["value_count"][[20, 21]] = 1
+            bad["key"][21] = bad["key"][20]
+            bv = nvals.copy()
+            bv[bad["value_begin"][21]] = bv[bad["value_begin"][20]]
+        else:
+            bad["value_begin"][-1] = len(nvals)
+        with pytest.raises(EngineError):
+            eng.cparam_decide_host(bad, bv if mutate == "backwards" else nvals)
+    _check(eng, ora, nxt, nvals)   # the rejected batches left nothing behind
+    _compare_sums(eng, ora, nxt, nvals, int(nxt["ts_ms"][-1]))

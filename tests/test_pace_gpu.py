@@ -106,3 +106,25 @@ def test_pace_reload_resets_and_time_order():
     bad[:] = [(900, 0, 1), (800, 0, 1)]
     with pytest.raises(EngineError):
         eng.pace_decide_host(bad)
+
+
+@pytest.mark.parametrize("flags", WALKERS)
+def test_pace_saturated_cost_wraps(flags):
+    """A tiny count with a huge acquireCount saturates Math.round at Long.MAX_VALUE, and Java's
+    costTime + latestPassedTime wraps negative: the request passes at once (RateLimiterController.java:58-62).
+    The wave walker's horizon jump must not skip such requests."""
+    eng = _engine(flags)
+    rules = np.zeros(2, abi.PACE_RULE_DTYPE)
+    rules[:] = [(1e-7, 0, 0), (2e-7, 500, 0)]
+    eng.pace_load_rules(rules)
+    ora = RateLimiterController(rules)
+    rng = np.random.default_rng(9)
+    t = 1_700_000_000_000
+    for _ in range(2):
+        req = np.zeros(4000, abi.PACE_REQ_DTYPE)
+        req["ts_ms"] = t + np.sort(rng.integers(0, 3000, len(req)))
+        req["rule"] = rng.integers(0, 2, len(req))
+        req["acquire"] = np.where(rng.random(len(req)) < 0.05, rng.integers(1 << 29, (1 << 31) - 1, len(req)), 1)
+        w = _check(eng, ora, req, 2)
+        assert (w[req["acquire"] > 1] == 0).any() and (w[req["acquire"] == 1] == abi.PACE_BLOCKED).any()
+        t = int(req["ts_ms"][-1])
