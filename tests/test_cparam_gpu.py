@@ -108,7 +108,7 @@ def test_hot_items_and_avg_local():
     rules = _rules(4, rng, thr=abi.THRESHOLD_AVG_LOCAL, hot_per_rule=3)
     hot = np.zeros(12, abi.PARAM_HOT_DTYPE)
     for i in range(12):
-        hot[i] = (int(np.array([i % 3 + 1], np.uint64)[0] * 0x9E3779B97F4A7C15 % (1 << 64)), int(rng.integers(0, 6)), 0)
+        hot[i] = ((i % 3 + 1) * 0x9E3779B97F4A7C15 % (1 << 64), int(rng.integers(0, 6)), 0)
     eng, ora = _pair(rules, hot, connected=3)
     t = 1_700_000_000_000
     for _ in range(2):
