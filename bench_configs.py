@@ -11,6 +11,8 @@ bench.py (which measures the headline C3 workload).
                  1000 ms batch plus the exits of the passed ones (rt ~ lognormal, median 12 ms; 5 % errors).
                  The event stream depends on the decisions (only passed entries exit), so it is produced by
                  the CPU oracle's client model (oracle.binding.LocalTraceGen) before the timed region.
+  --workload cparam  cluster hot-parameter tokens: 1000 ClusterParamFlowRules, 50k values each Zipf(1.1), 16M
+                 requests per batch, 10 % with 2-3 values (the fixed-point path).
   --workload pace  1M resources, each a FlowRule with CONTROL_BEHAVIOR_RATE_LIMITER (RateLimiterController,
                  count U{1..64}, maxQueueingTimeMs 500), 16M canPass calls per 1000 ms batch, Zipf(1.0),
                  acquire 1 (10 % U{2..4}).
@@ -337,9 +339,88 @@ def pace(args, dev):
             "data": "synthetic (GPU-generated, seeded): Zipf(1.0) resources, 10% acquire U{2..4}"}
 
 
+def cparam(args, dev):
+    """Cluster hot-parameter tokens: 1000 ClusterParamFlowRules (GLOBAL, count U{1..40}, S=10 / 1000 ms), rules
+    Zipf(1.0), each rule's values Zipf(1.1) over 50k distinct u64, 16M requests per 1000 ms batch, 10 % of them
+    carrying 2-3 values (all-or-nothing)."""
+    R, n, V = 1000, args.events, 50_000
+    rng = np.random.default_rng(7)
+    rules = np.zeros(R, abi.CPARAM_RULE_DTYPE)
+    rules["flow_id"] = np.arange(R) + 1
+    rules["count"] = rng.integers(1, 41, R)
+    rules["threshold_type"] = abi.THRESHOLD_GLOBAL
+    rules["sample_count"], rules["window_interval_ms"] = 10, 1000
+    rcdf, rperm = zipf_cdf(R, 1.0, 7)
+    vcdf, vperm = zipf_cdf(V, 1.1, 8)
+    rcdf_t, rperm_t = torch.from_numpy(rcdf).to(dev), torch.from_numpy(rperm.astype(np.int64)).to(dev)
+    vcdf_t, vperm_t = torch.from_numpy(vcdf).to(dev), torch.from_numpy(vperm.astype(np.int64)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(7)
+
+    def batch(b):
+        w = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+        w[:, 0] = torch.sort(torch.randint(0, 1000, (n,), generator=gen, device=dev)).values + T0 + 1000 * b
+        key = gpu_keys(rcdf_t, rperm_t, n, gen)
+        cnt = torch.where(torch.rand(n, generator=gen, device=dev) < 0.1,
+                          torch.randint(2, 4, (n,), generator=gen, device=dev), torch.ones(n, dtype=torch.int64, device=dev))
+        begin = torch.cumsum(cnt, 0) - cnt
+        w[:, 1] = key | (1 << 32)                     # key, acquireCount 1
+        w[:, 2] = begin | (cnt << 32)                 # value_begin, value_count
+        nv = int(cnt.sum())
+        owner = torch.repeat_interleave(key, cnt)
+        vals = gpu_keys(vcdf_t, vperm_t, nv, gen) * 0x9E3779B1 + owner * 0x85EBCA77 + 11
+        return w.view(torch.uint8).reshape(-1), vals, nv
+
+    batches = [batch(b) for b in range(args.warmup + args.steps)]
+    max_nv = max(x[2] for x in batches)
+    eng = FlowEngine(device=0, max_batch=max(n, max_nv))
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    eng.set_namespaces(ns)
+    eng.cparam_load_rules(rules, None, 17)
+    out = torch.empty(n * 12, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rounds = []
+
+    def step(b):
+        req, vals, nv = batches[b]
+        eng.cparam_decide_device(req.data_ptr(), n, vals.data_ptr(), nv, out.data_ptr(), stream)
+        rounds.append(eng.cparam_last_rounds())
+
+    el = timed(step, args.warmup, args.steps)
+    req_l, vals_l, nv_l = batches[-1]
+    keys_l = torch.repeat_interleave(req_l.view(torch.int64).reshape(-1, 3)[:, 1] & 0xFFFFFFFF,
+                                     (req_l.view(torch.int64).reshape(-1, 3)[:, 2] >> 32))
+    touched = int(torch.unique(keys_l * 1_000_003 + vals_l).numel())
+    # per request 24 B in + 12 B out; per value 8 B; per touched (rule, value) slot: key 8 B + ring S x 16 B read
+    # and written once
+    b_alg = n * (24 + 12) + nv_l * 8 + touched * (8 + 2 * 10 * 16)
+    base = None
+    if not args.no_cpu_baseline:
+        from oracle.binding import ClusterTokenService
+        m = min(args.cpu_events, n)
+        req0, vals0, _ = batches[0]
+        req_h = req0.view(torch.int64).reshape(-1, 3)[:m].cpu().numpy().copy().view(abi.CPARAM_REQ_DTYPE).reshape(-1)
+        end = int(req_h["value_begin"][-1]) + int(req_h["value_count"][-1])
+        vals_h = vals0[:end].cpu().numpy().astype(np.uint64)
+        ora = ClusterTokenService()
+        ora.set_namespaces(ns)
+        ora.load_param_rules(rules)
+        t = time.perf_counter()
+        ora.decide_param(req_h, vals_h)
+        dt = time.perf_counter() - t
+        base = {"value": m / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"first {m} requests of batch 0 through oracle ClusterTokenService.decide_param (1 thread), "
+                          f"{dt:.1f} s"}
+    return {"metric": "cluster hot-parameter token decisions/sec (ClusterParamFlowChecker), 1000 param rules",
+            "workload": "cparam: 1000 ClusterParamFlowRules x 50k values Zipf(1.1), 16M requests/batch, 10% multi-value",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
+            "extra": {"fixed_point_rounds": rounds[args.warmup:], "values_per_step": nv_l},
+            "data": "synthetic (GPU-generated, seeded): rules Zipf(1.0), values Zipf(1.1) per rule, 10% 2-3 values"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam"], default="c2")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=16_000_000)
@@ -349,7 +430,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace}[args.workload](args, dev)
+    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace, "cparam": cparam}[args.workload](args, dev)
     ms = r["el"] * 1000.0 / args.steps
     gbs = r["b_alg"] / (ms / 1000.0) / 1e9
     res = {"metric": r["metric"], "value": r["value"], "unit": r.get("unit", "decisions/s"), "n_gpus": 1,

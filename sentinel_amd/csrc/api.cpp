@@ -107,6 +107,9 @@ struct sg_handle {
     int64_t* d_cplast_ts = nullptr;
     // one-pipeline batch scratch (value-position records, fixed point over multi-value requests)
     uint32_t* d_cp_owner = nullptr;
+    uint32_t* d_cp_pslot = nullptr;
+    uint8_t* d_cp_dirty = nullptr;    // [cptotal] re-walk flags, kept all-zero between batches
+    uint64_t cp_dirty_cap = 0;
     uint8_t* d_cp_chk = nullptr;
     uint8_t* d_cp_assume = nullptr;
     uint64_t* d_cp_rec = nullptr;
@@ -471,6 +474,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_ps_tc);
     dfree(h->d_ps_last_ts);
     dfree(h->d_cp_owner);
+    dfree(h->d_cp_pslot);
+    dfree(h->d_cp_dirty);
     dfree(h->d_cp_chk);
     dfree(h->d_cp_assume);
     dfree(h->d_cp_rec);
@@ -1500,15 +1505,23 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     // scratch sized for the batch's value positions
     if (nv > h->cp_val_cap) {
         dfree(h->d_cp_owner);
+        dfree(h->d_cp_pslot);
         dfree(h->d_cp_chk);
         dfree(h->d_cp_rec);
         dfree(h->d_cp_rec2);
         dfree(h->d_cp_hist);
-        if (hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
+        if (hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
+            hipMalloc(&h->d_cp_pslot, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_hist, sizeof(uint32_t) * radix_hist_words(nv)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "cparam batch scratch");
         h->cp_val_cap = nv;
+    }
+    if (h->cptotal > h->cp_dirty_cap) {
+        dfree(h->d_cp_dirty);
+        if (hipMalloc(&h->d_cp_dirty, h->cptotal) != hipSuccess) return fail(h, SG_E_NOMEM, "cparam re-walk flags");
+        HIP_TRY(h, hipMemsetAsync(h->d_cp_dirty, 0, h->cptotal, stream));
+        h->cp_dirty_cap = h->cptotal;
     }
     if (!h->d_cp_assume && (hipMalloc(&h->d_cp_assume, h->cfg.max_batch) != hipSuccess ||
                             hipMalloc(&h->d_cp_changed, sizeof(int)) != hipSuccess))
@@ -1540,6 +1553,8 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     b.pbits = pbits;
     b.pmask = (1ull << pbits) - 1;
     b.changed = h->d_cp_changed;
+    b.pslot = h->d_cp_pslot;
+    b.dirty = h->d_cp_dirty;
     b.lim = any_lim ? 1 : 0;
     HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
     HIP_TRY(h, launch_cp_prep2(c, b, stream));  // sets *changed iff a request has several values
@@ -1598,10 +1613,10 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     sgm.short_list = h->d_short_list;
     sgm.short_count = h->d_long_count + 1;
     for (int cl = 0; cl < kClasses; ++cl) sgm.class_off[cl] = h->class_off[cl];
-    sgm.short_max = 0xFFFFFFFFu;
+    sgm.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 32u;
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, launch_seg(sgm, stream));
-    // are there multi-value requests? (then the rings of the touched slots are saved for the re-walks)
+    // are there multi-value requests? (then the first walk saves the touched rings for the re-walks)
     uint32_t counts[1 + kClasses];
     int err = 0, has_multi = 0;
     HIP_TRY(h, hipMemcpyAsync(counts, h->d_long_count, sizeof(counts), hipMemcpyDeviceToHost, stream));
@@ -1617,8 +1632,7 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
                 return fail(h, SG_E_NOMEM, "cparam ring save area");
             h->cp_save_cap = touched * h->cpstride;
         }
-        b.save = h->d_cp_save;
-        HIP_TRY(h, launch_cp_saverings(c, b, sgm, 0, stream));
+        b.save = h->d_cp_save;  // the first walk saves the touched rings, re-walks restore the dirty ones
     }
     // rounds: walk every slot under the assumed multi-value outcomes, then recompute the outcomes
     const uint32_t kMaxRounds = h->cp_max_rounds;
@@ -1629,7 +1643,7 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
         converged = true;
     }
     while (!err && !converged && round < kMaxRounds) {
-        if (round > 0) HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
+        b.round = (int)round;
         HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
         HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
         HIP_TRY(h, launch_cp_combine(c, b, stream));
@@ -1644,7 +1658,7 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
         }
     }
     if (!err && !converged) {  // rare: the batch on one thread, from the saved rings
-        HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
+        if (round > 0) HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
         HIP_TRY(h, launch_cp_serial(c, b, stream));
     }
     h->cp_rounds = converged ? (round ? round : 1) : kMaxRounds + 1;

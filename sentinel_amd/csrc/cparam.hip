@@ -298,8 +298,12 @@ __global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
                 continue;
             }
             const uint64_t g = cp_slot(c, r, c.values[p]);
-            if (g == ~0ull) atomicOr(c.err, kErrTableFull);
-            else b.rec[p] = (g << b.pbits) | p;
+            if (g == ~0ull) {
+                atomicOr(c.err, kErrTableFull);
+            } else {
+                b.rec[p] = (g << b.pbits) | p;
+                b.pslot[p] = (uint32_t)g;
+            }
         }
     }
 }
@@ -315,74 +319,265 @@ __global__ void __launch_bounds__(256) k_cp_order(CPArgs c, CPBatch b, const uin
     }
 }
 
+// Slot prologue of a walk: round 0 saves the pre-batch ring (when re-walks may follow); later rounds skip clean
+// slots and restore the dirty ones. `x0`/`dx` spread the bucket copies over the caller's lanes.
+__device__ __forceinline__ bool cp_prologue(const CPArgs& c, const CPBatch& b, uint64_t g, uint64_t t, int x0, int dx) {
+    CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+    CPBucket* sv = b.save + t * (uint64_t)c.stride;
+    if (b.round > 0) {
+        if (!b.dirty[g]) return false;
+        for (int x = x0; x < c.stride; x += dx) ring[x] = sv[x];
+        if (x0 == 0) b.dirty[g] = 0;
+    } else if (b.save) {
+        for (int x = x0; x < c.stride; x += dx) sv[x] = ring[x];
+    }
+    return true;
+}
+
+// Sequential replay of the records [j, ...) of slot g (one lane). Single-value requests: window check and add.
+// A multi-value request's records in this slot (repeated values) check the state before the request, and add
+// its count each iff its outcome is assumed to be a pass.
+__device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j) {
+    const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+    const double thr = cp_threshold(c, r, c.keys[g]);
+    CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+    const int S = r.S;
+    const int64_t wl = r.wl;
+    int64_t P = INT64_MIN, other = 0, cur = 0;
+    while (j < sg.n) {
+        const uint64_t rec = sg.rec_sorted[j];
+        if ((rec >> b.pbits) != g) break;
+        const uint64_t p = rec & b.pmask;
+        const uint32_t i = b.owner[p];
+        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) {  // allowProceed refused it
+            ++j;
+            continue;
+        }
+        const sg_cparam_req q = c.req[i];
+        const int64_t Pq = q.ts_ms / wl;
+        if (Pq != P) {  // currentWindow(t): close the open period, open this one
+            if (P != INT64_MIN) {
+                CPBucket bk;
+                bk.start = P * wl;
+                bk.count = cur;
+                ring[(int)(P % S)] = bk;
+            }
+            P = Pq;
+            other = cp_window(ring, S, wl, P, &cur);
+        }
+        const double rem = thr - (double)(other + cur) / r.isec - (double)q.acquire;
+        if (q.value_count == 1) {
+            if (rem >= 0) {
+                cur += q.acquire;
+                cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
+            } else {
+                cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+            }
+            ++j;
+            continue;
+        }
+        uint64_t e = j;
+        while (e < sg.n && (sg.rec_sorted[e] >> b.pbits) == g && b.owner[sg.rec_sorted[e] & b.pmask] == i) {
+            b.chk[sg.rec_sorted[e] & b.pmask] = rem >= 0 ? 1 : 0;
+            ++e;
+        }
+        if (b.assume[i]) cur += (int64_t)q.acquire * (int64_t)(e - j);
+        j = e;
+    }
+    if (P != INT64_MIN) {
+        CPBucket bk;
+        bk.start = P * wl;
+        bk.count = cur;
+        ring[(int)(P % S)] = bk;
+    }
+}
+
+// One lane per slot of at most short_max records. Work item t: the slot's index in the save area (the long
+// list comes first, then the short lists in class order).
 __global__ void __launch_bounds__(256) k_cp_walk2(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
-    uint32_t total = *sg.long_count;
+    const uint32_t nlong = *sg.long_count;
+    uint32_t total = 0;
     for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        uint32_t r0 = t;
-        uint64_t j;
-        if (r0 < *sg.long_count) {
-            j = sg.long_list[r0];
-        } else {
-            r0 -= *sg.long_count;
-            int k = 0;
-            while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
-            j = sg.short_list[sg.class_off[k] + r0];
-        }
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+        uint32_t r0 = u;
+        int k = 0;
+        while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
+        const uint64_t j = sg.short_list[sg.class_off[k] + r0];
         const uint64_t g = sg.rec_sorted[j] >> b.pbits;
+        if (!cp_prologue(c, b, g, (uint64_t)nlong + u, 0, 1)) continue;
+        cp_walk_serial(c, b, sg, g, j);
+    }
+}
+
+template <class Pred>
+__device__ __forceinline__ uint64_t cp_wave_search(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t q = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(q >= hi || pred(q));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    const uint64_t q = lo + (uint64_t)lane;
+    const uint64_t m = __ballot(q < hi && pred(q));
+    return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
+}
+
+__device__ __forceinline__ int64_t cp_excl_scan(int64_t v, int lane) {
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up((long long)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ int64_t cp_wave_sum(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor((long long)v, o, 64);
+    return v;
+}
+
+enum : int { kCpSkip = 0, kCpSingle = 1, kCpMulti = 2, kCpDup = 3 };
+
+// One wave per slot of more than short_max records (a hot (rule, value)), 64 records per step with the ring in
+// registers (lane x < S holds bucket x). Within one window period the state is the running count `cur`; every
+// record's check is thr - (other + cur_before) / intervalSec - acquire >= 0, monotone in cur_before. A step
+// assumes every unresolved single-value request passes, takes the exclusive scan of the adds, and commits the
+// lanes up to the first single-value request whose check fails (that one is blocked); single-value requests
+// that fail even at the committed state are blocked at once (cur only grows). Multi-value records add their
+// count unconditionally when their outcome is assumed a pass, and record their check; a repeated value of the
+// same request (adjacent record, same owner) only adds. A saturated period resolves in two steps per 64
+// records, an open one in one.
+__global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, BatchArgs sg) {
+    if (*c.err) return;
+    const int lane = (int)__lane_id();
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    const uint32_t cnt = *sg.long_count;
+    for (uint32_t t = wave; t < cnt; t += nwaves) {
+        const uint64_t s = sg.long_list[t];
+        const uint64_t g = sg.rec_sorted[s] >> b.pbits;
+        if (!cp_prologue(c, b, g, t, lane, 64)) continue;
         const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+        if (r.S > 64) {  // the ring does not fit the wave's registers
+            if (lane == 0) cp_walk_serial(c, b, sg, g, s);
+            continue;
+        }
+        const uint64_t e = cp_wave_search(s + sg.short_max, sg.n, [&](uint64_t q) {
+            return (sg.rec_sorted[q] >> b.pbits) != g;
+        }, lane);
         const double thr = cp_threshold(c, r, c.keys[g]);
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
         const int S = r.S;
         const int64_t wl = r.wl;
-        int64_t P = INT64_MIN, other = 0, cur = 0;
-        while (j < sg.n) {
-            const uint64_t rec = sg.rec_sorted[j];
-            if ((rec >> b.pbits) != g) break;
-            const uint64_t p = rec & b.pmask;
-            const uint32_t i = b.owner[p];
-            if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) {  // allowProceed refused it
-                ++j;
-                continue;
-            }
-            const sg_cparam_req q = c.req[i];
-            const int64_t Pq = q.ts_ms / wl;
-            if (Pq != P) {  // currentWindow(t): close the open period, open this one
-                if (P != INT64_MIN) {
-                    CPBucket bk;
-                    bk.start = P * wl;
-                    bk.count = cur;
-                    ring[(int)(P % S)] = bk;
-                }
-                P = Pq;
-                other = cp_window(ring, S, wl, P, &cur);
-            }
-            const double rem = thr - (double)(other + cur) / r.isec - (double)q.acquire;
-            if (q.value_count == 1) {
-                if (rem >= 0) {
-                    cur += q.acquire;
-                    cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
-                } else {
-                    cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
-                }
-                ++j;
-                continue;
-            }
-            // a multi-value request: its records in this slot (duplicate values) all check the pre-request state
-            uint64_t e = j;
-            while (e < sg.n && (sg.rec_sorted[e] >> b.pbits) == g && b.owner[sg.rec_sorted[e] & b.pmask] == i) {
-                b.chk[sg.rec_sorted[e] & b.pmask] = rem >= 0 ? 1 : 0;
-                ++e;
-            }
-            if (b.assume[i]) cur += (int64_t)q.acquire * (int64_t)(e - j);
-            j = e;
+        int64_t bst = INT64_MIN, bcnt = 0;
+        if (lane < S) {
+            const CPBucket bk = ring[lane];
+            bst = bk.start;
+            bcnt = bk.count;
         }
-        if (P != INT64_MIN) {
+        int64_t P = INT64_MIN, other = 0, cur = 0;
+        for (uint64_t base = s; base < e; base += 64) {
+            const uint64_t j = base + (uint64_t)lane;
+            const bool act = j < e;
+            int typ = kCpSkip;
+            uint32_t i = 0;
+            uint64_t p = 0;
+            int64_t acq = 0, Pq = 0, uadd = 0;
+            if (act) {
+                p = sg.rec_sorted[j] & b.pmask;
+                i = b.owner[p];
+                if (!(b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST)) {
+                    const sg_cparam_req q = c.req[i];
+                    acq = q.acquire;
+                    Pq = q.ts_ms / wl;
+                    if (q.value_count == 1) {
+                        typ = kCpSingle;
+                    } else {
+                        const uint32_t prev = j > s ? b.owner[sg.rec_sorted[j - 1] & b.pmask] : kNoOwner;
+                        typ = prev == i ? kCpDup : kCpMulti;
+                        if (b.assume[i]) uadd = acq;
+                        if (typ == kCpDup) b.chk[p] = 1;  // the request's first record here carries the check
+                    }
+                }
+            }
+            uint64_t pending = __ballot(typ != kCpSkip);
+            uint64_t failed = 0;
+            while (pending) {
+                const int f = __builtin_ctzll(pending);
+                const int64_t Pf = __shfl((long long)Pq, f, 64);
+                if (Pf != P) {  // currentWindow: close the open period, open Pf
+                    if (P != INT64_MIN && lane == (int)(P % S)) {
+                        bst = P * wl;
+                        bcnt = cur;
+                    }
+                    P = Pf;
+                    const int I = (int)(P % S);
+                    const int64_t ws = P * wl, lo = ws - (int64_t)(S - 1) * wl;
+                    int64_t o = 0, cc = 0;
+                    if (lane < S) {
+                        if (lane == I) cc = bst == ws ? bcnt : 0;
+                        else if (bst != INT64_MIN && bst >= lo) o = bcnt;
+                    }
+                    other = cp_wave_sum(o);
+                    cur = cp_wave_sum(cc);
+                }
+                uint64_t open = pending & __ballot(typ != kCpSkip && Pq == P);
+                pending &= ~open;
+                while (open) {
+                    const bool mine = (open >> lane) & 1ull;
+                    const bool dead = (failed >> lane) & 1ull;
+                    int64_t a = 0;
+                    if (mine) a = typ == kCpSingle ? (dead ? 0 : acq) : uadd;
+                    const int64_t excl = cp_excl_scan(a, lane);
+                    const double rem = thr - (double)(other + cur + excl) / r.isec - (double)acq;
+                    const bool ok = rem >= 0;
+                    const uint64_t bad = __ballot(mine && typ == kCpSingle && !dead && !ok);
+                    uint64_t done = open;
+                    int64_t adv;
+                    if (bad) {
+                        const int k = __builtin_ctzll(bad);
+                        done = open & ((2ull << k) - 1ull);
+                        adv = __shfl((long long)excl, k, 64);  // the blocked lane k adds nothing
+                    } else {
+                        adv = cp_wave_sum(a);
+                    }
+                    if ((done >> lane) & 1ull) {
+                        if (typ == kCpSingle) {
+                            if (ok && !dead) cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
+                            else cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+                        } else if (typ == kCpMulti) {
+                            b.chk[p] = ok ? 1 : 0;
+                        }
+                    }
+                    cur += adv;
+                    open &= ~done;
+                    if (bad && open) {  // blocked even at the committed state: blocked for good
+                        const double lb = thr - (double)(other + cur) / r.isec - (double)acq;
+                        failed |= __ballot(((open >> lane) & 1ull) && typ == kCpSingle && lb < 0);
+                    }
+                }
+            }
+        }
+        if (P != INT64_MIN && lane == (int)(P % S)) {
+            bst = P * wl;
+            bcnt = cur;
+        }
+        if (lane < S) {
             CPBucket bk;
-            bk.start = P * wl;
-            bk.count = cur;
-            ring[(int)(P % S)] = bk;
+            bk.start = bst;
+            bk.count = bcnt;
+            ring[lane] = bk;
         }
     }
 }
@@ -396,9 +591,10 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
         bool pass = true;
         for (uint32_t j = 0; j < q.value_count && pass; ++j) pass = b.chk[(uint64_t)q.value_begin + j] != 0;
         cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? -1 : 0);  // remaining -1: multi-value
-        if ((b.assume[i] != 0) != pass) {
+        if ((b.assume[i] != 0) != pass) {  // its slots are re-walked in the next round
             b.assume[i] = pass ? 1 : 0;
             *b.changed = 1;
+            for (uint32_t j = 0; j < q.value_count; ++j) b.dirty[b.pslot[(uint64_t)q.value_begin + j]] = 1;
         }
     }
 }
@@ -423,8 +619,12 @@ __global__ void __launch_bounds__(256) k_cp_saverings(CPArgs c, CPBatch b, Batch
         }
         const uint64_t g = sg.rec_sorted[j] >> b.pbits;
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
-        if (restore) ring[x] = b.save[(uint64_t)t * c.stride + x];
-        else b.save[(uint64_t)t * c.stride + x] = ring[x];
+        if (restore) {
+            ring[x] = b.save[(uint64_t)t * c.stride + x];
+            if (x == 0) b.dirty[g] = 0;
+        } else {
+            b.save[(uint64_t)t * c.stride + x] = ring[x];
+        }
     }
 }
 
@@ -486,6 +686,8 @@ hipError_t launch_cp_order(const CPArgs& c, const CPBatch& b, const uint64_t* so
 }
 
 hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream) {
+    const uint64_t waves = sg.n / ((uint64_t)sg.short_max + 1) + 1;  // bound on the long list's length
+    hipLaunchKernelGGL(k_cp_walk2_long, dim3(cgrid2(waves * 64, 2048)), dim3(256), 0, stream, c, b, sg);
     hipLaunchKernelGGL(k_cp_walk2, dim3(cgrid2(sg.n, 4096)), dim3(256), 0, stream, c, b, sg);
     return hipGetLastError();
 }

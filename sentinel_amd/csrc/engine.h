@@ -296,7 +296,10 @@ struct CPBatch {
     int pbits;
     uint64_t pmask;
     int* changed;
-    CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots
+    CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots (null: no re-walks)
+    uint32_t* pslot;          // [n_values] slot of value position p
+    uint8_t* dirty;           // [total slots] slot must be re-walked (an assumed outcome in it changed)
+    int round;                // 0: first walk (saves the rings); > 0: re-walk the dirty slots from the saves
     int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
 };
 hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream);

@@ -433,6 +433,12 @@ class FlowEngine:
         self._check(self._L.sg_cparam_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot),
                                                  capacity_log2))
 
+    def cparam_decide_device(self, req_ptr: int, n: int, values_ptr: int, n_values: int, out_ptr: int,
+                             stream_ptr: int = 0):
+        """DEVICE pointers: n sg_cparam_req, n_values u64 values, n sg_result."""
+        self._check(self._L.sg_cparam_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(values_ptr), n_values,
+                                                   C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
+
     def cparam_last_rounds(self) -> int:
         """Fixed-point rounds the last sg_cparam_decide_batch needed (max_rounds + 1: decided serially)."""
         r = C.c_uint32()

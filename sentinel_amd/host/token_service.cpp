@@ -76,6 +76,34 @@ bool isValidRule(const FlowRule& r) {
     return false;
 }
 
+// ParamFlowRuleUtil.isValidRule / checkCluster, ParamFlowRuleUtil.java:46-66
+bool isValidParamRule(const ParamFlowRule& r) {
+    if (isBlank(r.resource) || !(r.count >= 0) || r.grade < 0 || !r.paramIdx || r.burstCount < 0 ||
+        r.controlBehavior < 0 || r.durationInSec <= 0 || r.maxQueueingTimeMs < 0)
+        return false;
+    if (!r.clusterMode) return true;
+    if (!r.clusterConfig) return false;
+    const ParamFlowClusterConfig& c = *r.clusterConfig;
+    if (!isWindowConfigValid(c.sampleCount, c.windowIntervalMs)) return false;
+    return validClusterRuleId(c.flowId);
+}
+
+namespace {
+
+// ParamFlowRuleUtil.parseItemValue (:211-240): the classTypes that parse to a primitive wrapper (never equal to
+// a String parameter); any other classType, or none, keeps the string.
+bool parsesToString(const std::string& classType) {
+    static const char* prim[] = {"int", "java.lang.Integer", "boolean", "java.lang.Boolean", "long", "java.lang.Long",
+                                 "double", "java.lang.Double", "float", "java.lang.Float", "byte", "java.lang.Byte",
+                                 "short", "java.lang.Short", "char"};
+    if (isBlank(classType)) return true;
+    for (const char* p : prim)
+        if (classType == p) return false;
+    return true;
+}
+
+}  // namespace
+
 GpuTokenService::GpuTokenService(Options opt) : opt_(std::move(opt)) {
     if (!opt_.clock) opt_.clock = systemMillis;
     sg_config cfg{};
@@ -403,13 +431,136 @@ void GpuTokenService::flusherLoop() {
     }
 }
 
-// The device path covers flow tokens only; parameter and concurrent tokens answer FAIL, so the
-// client's fallback (FlowRuleChecker / ParamFlowChecker local checks) applies, as for an absent server.
+uint64_t GpuTokenService::valueId(const std::string& v) {
+    auto it = valueIds_.find(v);
+    if (it != valueIds_.end()) return it->second;
+    const uint64_t id = (uint64_t)valueIds_.size() + 1;
+    valueIds_.emplace(v, id);
+    return id;
+}
+
+// All namespaces' cluster param rules → one table, ascending flowId; hot items through the value dictionary
+// (ParamFlowRuleUtil.parseHotItems :188-209: null object or count < 0 skipped, a later duplicate wins).
+void GpuTokenService::pushParamRulesLocked() {
+    std::vector<sg_cparam_rule> tab;
+    std::vector<sg_param_hot_item> hot;
+    keyOfParam_.clear();
+    for (const auto& kv : paramRules_) {
+        const ParamFlowRule& r = kv.second.rule;
+        const ParamFlowClusterConfig& c = *r.clusterConfig;
+        sg_cparam_rule t{};
+        t.flow_id = kv.first;
+        t.count = r.count;
+        t.threshold_type = c.thresholdType;
+        t.sample_count = c.sampleCount;
+        t.window_interval_ms = c.windowIntervalMs;
+        t.namespace_id = nsIndex(kv.second.ns);
+        std::map<uint64_t, int> items;
+        for (const ParamFlowItem& it : r.paramFlowItemList) {
+            if (!it.object || !it.count || *it.count < 0) continue;
+            if (!parsesToString(it.classType)) continue;  // an Integer / Long … key never equals a String parameter
+            items[valueId(*it.object)] = *it.count;
+        }
+        t.hot_begin = (uint32_t)hot.size();
+        t.hot_count = (uint32_t)items.size();
+        for (const auto& x : items) {
+            sg_param_hot_item h{};
+            h.value = x.first;
+            h.threshold = x.second;
+            hot.push_back(h);
+        }
+        keyOfParam_[kv.first] = (uint32_t)tab.size();
+        tab.push_back(t);
+    }
+    pushNamespacesLocked();
+    std::lock_guard<std::mutex> e(engMu_);
+    int rc = sg_cparam_load_rules(h_, tab.data(), (uint32_t)tab.size(), hot.data(), (uint32_t)hot.size(),
+                                  opt_.paramCapacityLog2);
+    if (rc != SG_OK) {
+        err_ = sg_last_error(h_);
+        keyOfParam_.clear();
+    }
+}
+
+// ClusterParamFlowRuleManager.applyClusterParamRules, ClusterParamFlowRuleManager.java:318-365
+void GpuTokenService::loadParamRules(const std::string& ns, const std::vector<ParamFlowRule>& list) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    waitIdle();
+    std::map<int64_t, ParamFlowRule> ruleMap;
+    for (const ParamFlowRule& r0 : list) {
+        if (!r0.clusterMode) continue;
+        if (!isValidParamRule(r0)) continue;  // "Ignoring invalid param flow rule"
+        ParamFlowRule r = r0;
+        if (isBlank(r.limitApp)) r.limitApp = "default";
+        const auto& flowId = r.clusterConfig->flowId;
+        if (!flowId) continue;
+        ruleMap[*flowId] = r;
+    }
+    for (int64_t id : nsParamIds_[ns])
+        if (!ruleMap.count(id)) paramRules_.erase(id);
+    std::vector<int64_t> ids;
+    for (auto& kv : ruleMap) {
+        paramRules_[kv.first] = ParamRuleEntry{kv.second, ns};
+        ids.push_back(kv.first);
+    }
+    nsParamIds_[ns] = ids;
+    nsIndex(ns);
+    pushParamRulesLocked();
+}
+
+std::vector<TokenResult> GpuTokenService::decideParamLocked(const std::vector<ParamTokenRequest>& reqs) {
+    std::vector<TokenResult> res(reqs.size(), TokenResult(TokenResultStatus::FAIL));
+    if (reqs.empty()) return res;
+    std::vector<sg_cparam_req> rq(reqs.size());
+    std::vector<uint64_t> vals;
+    for (size_t i = 0; i < reqs.size(); ++i) {
+        const ParamTokenRequest& q = reqs[i];
+        sg_cparam_req& r = rq[i];
+        r.ts_ms = q.timeMillis;
+        r.acquire = q.acquireCount;
+        if (!q.ruleId || *q.ruleId <= 0) {
+            r.key = SG_KEY_BAD;
+        } else {
+            auto it = keyOfParam_.find(*q.ruleId);
+            r.key = it == keyOfParam_.end() ? SG_KEY_NO_RULE : it->second;
+        }
+        r.value_begin = (uint32_t)vals.size();
+        r.value_count = (uint32_t)q.params.size();
+        for (const std::string& v : q.params) vals.push_back(valueId(v));
+    }
+    std::vector<sg_result> out(reqs.size());
+    std::lock_guard<std::mutex> e(engMu_);
+    if (sg_cparam_decide_batch_host(h_, rq.data(), rq.size(), vals.data(), vals.size(), out.data()) != SG_OK) {
+        err_ = sg_last_error(h_);  // TokenResult(FAIL) → the client falls back to local checking
+        return res;
+    }
+    for (size_t i = 0; i < reqs.size(); ++i)
+        res[i] = TokenResult(out[i].status).setRemaining(out[i].remaining).setWaitInMs(out[i].wait_ms);
+    return res;
+}
+
+// DefaultTokenService.requestParamToken (:53-64) → ClusterParamFlowChecker.acquireClusterToken on the device
+// (sg_cparam_*): one request per call, in arrival order with the flow-token micro-batches (they share the
+// namespace's GlobalRequestLimiter).
 TokenResult GpuTokenService::requestParamToken(std::optional<int64_t> ruleId, int acquireCount,
                                                const std::vector<std::string>& params) {
     if (!ruleId || *ruleId <= 0 || acquireCount <= 0 || params.empty())
         return TokenResult(TokenResultStatus::BAD_REQUEST);  // DefaultTokenService.java:53-56
-    return TokenResult(TokenResultStatus::FAIL);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    waitIdle();
+    ParamTokenRequest q{std::max(lastTs_, opt_.clock()), ruleId, acquireCount, params};
+    lastTs_ = q.timeMillis;
+    return decideParamLocked({q})[0];
+}
+
+std::vector<TokenResult> GpuTokenService::requestParamTokens(const std::vector<ParamTokenRequest>& reqs) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (!pending_.empty()) flushLocked(lk);
+    waitIdle();
+    for (const auto& q : reqs) lastTs_ = std::max(lastTs_, q.timeMillis);
+    return decideParamLocked(reqs);
 }
 
 // DefaultTokenService.requestConcurrentToken (:66-77) → ConcurrentClusterFlowChecker.acquireConcurrentToken on

@@ -8,6 +8,12 @@
 //   GpuTokenService::requestToken                   DefaultTokenService.requestToken (srv/flow/DefaultTokenService.java:39-50)
 //   GpuTokenService::loadRules                      ClusterFlowRuleManager.loadRules → applyClusterFlowRule
 //                                                   (srv/flow/rule/ClusterFlowRuleManager.java:254-260, 325-375)
+//   GpuTokenService::requestParamToken              DefaultTokenService.requestParamToken (:53-64) →
+//                                                   ClusterParamFlowChecker.acquireClusterToken (:42-87)
+//   GpuTokenService::loadParamRules                 ClusterParamFlowRuleManager.loadRules → applyClusterParamRules
+//                                                   (srv/flow/rule/ClusterParamFlowRuleManager.java:318-365)
+//   GpuTokenService::requestConcurrentToken / releaseConcurrentToken
+//                                                   DefaultTokenService (:66-85) → ConcurrentClusterFlowChecker
 //   GpuTokenService::loadServerFlowConfig / setConnectedCount
 //                                                   ClusterServerConfigManager.loadFlowConfig (:303-346),
 //                                                   ConnectionManager.getConnectedCount (:47-51)
@@ -126,6 +132,38 @@ struct FlowRule {  // FlowRule.java:52-95
 // FlowRuleUtil.isValidRule (sentinel-core/.../slots/block/flow/FlowRuleUtil.java:167-229)
 bool isValidRule(const FlowRule& rule);
 
+struct ParamFlowClusterConfig {  // ParamFlowClusterConfig.java:32-44 (defaults included)
+    std::optional<int64_t> flowId;
+    int thresholdType = ClusterRuleConstant::FLOW_THRESHOLD_AVG_LOCAL;
+    bool fallbackToLocalWhenFail = false;
+    int sampleCount = ClusterRuleConstant::DEFAULT_CLUSTER_SAMPLE_COUNT;
+    int windowIntervalMs = 1000;
+};
+
+struct ParamFlowItem {  // ParamFlowItem.java: object (string form), classType, count
+    std::optional<std::string> object;
+    std::string classType;
+    std::optional<int> count;
+};
+
+struct ParamFlowRule {  // ParamFlowRule.java (defaults included)
+    std::string resource;
+    std::string limitApp = "default";
+    int grade = RuleConstant::FLOW_GRADE_QPS;
+    std::optional<int> paramIdx;
+    double count = 0;
+    int controlBehavior = RuleConstant::CONTROL_BEHAVIOR_DEFAULT;
+    int maxQueueingTimeMs = 0;
+    int burstCount = 0;
+    int64_t durationInSec = 1;
+    std::vector<ParamFlowItem> paramFlowItemList;
+    bool clusterMode = false;
+    std::optional<ParamFlowClusterConfig> clusterConfig;
+};
+
+// ParamFlowRuleUtil.isValidRule (sentinel-extension/.../param/ParamFlowRuleUtil.java:46-66)
+bool isValidParamRule(const ParamFlowRule& rule);
+
 class TokenService {
 public:
     virtual ~TokenService() = default;
@@ -156,6 +194,7 @@ public:
         std::chrono::microseconds flushDelay{200};  // ... or when the oldest has waited this long
         std::function<int64_t()> clock;             // TimeUtil.currentTimeMillis (default: system clock)
         int pipelineDepth = 3;                      // micro-batches in flight on the GPU (1..3)
+        int paramCapacityLog2 = 16;                 // exact (value → window) table per cluster param rule
         // observer of every decided micro-batch (requests as submitted, results, status) — tests and tracing
         std::function<void(const std::vector<sg_req>&, const std::vector<sg_result>&, int)> onBatch;
     };
@@ -169,6 +208,10 @@ public:
     void loadRules(const std::string& ns, const std::vector<FlowRule>& rules);
     // ClusterServerConfigManager: per-namespace QPS limiter (GlobalRequestLimiter) and max QPS.
     void loadServerFlowConfig(const std::string& ns, bool limiterEnabled, double maxAllowedQps);
+    // ClusterParamFlowRuleManager.loadRules(namespace, rules): replaces the namespace's cluster param rules (a
+    // surviving flowId keeps its ClusterParamMetric). Parameters are strings here: a hot item matches when its
+    // parsed value is a String (blank or non-primitive classType), as Java's equals would decide.
+    void loadParamRules(const std::string& ns, const std::vector<ParamFlowRule>& rules);
     // ConnectionManager.getConnectedCount(namespace), used by FLOW_THRESHOLD_AVG_LOCAL rules.
     void setConnectedCount(const std::string& ns, int connected);
 
@@ -184,6 +227,14 @@ public:
 
     // Deterministic replay: decide `reqs` (time-ordered) in one batch.
     std::vector<TokenResult> requestTokens(const std::vector<TokenRequest>& reqs);
+    // Deterministic replay of requestParamToken calls at explicit times, one device batch.
+    struct ParamTokenRequest {
+        int64_t timeMillis;
+        std::optional<int64_t> ruleId;
+        int acquireCount;
+        std::vector<std::string> params;
+    };
+    std::vector<TokenResult> requestParamTokens(const std::vector<ParamTokenRequest>& reqs);
 
     const std::string& lastError() const { return err_; }
 
@@ -203,7 +254,14 @@ private:
         std::vector<std::promise<TokenResult>*> waiters;
     };
 
+    struct ParamRuleEntry {
+        ParamFlowRule rule;
+        std::string ns;
+    };
     uint32_t keyOf(std::optional<int64_t> ruleId, bool prioritized) const;
+    uint64_t valueId(const std::string& v);  // exact dictionary: the same string is the same value forever
+    void pushParamRulesLocked();
+    std::vector<TokenResult> decideParamLocked(const std::vector<ParamTokenRequest>& reqs);
     int nsIndex(const std::string& ns);  // creates the namespace entry if needed
     void pushNamespacesLocked();
     void pushRulesLocked();
@@ -240,6 +298,10 @@ private:
     std::unordered_map<int64_t, RuleEntry> rules_;            // FLOW_RULES + FLOW_NAMESPACE_MAP
     std::unordered_map<int64_t, uint32_t> keyOfFlow_;         // flowId → dense engine key
     std::unordered_map<std::string, uint32_t> clientIds_;     // client address → sg_conc_req.client (1, 2, …)
+    std::map<int64_t, ParamRuleEntry> paramRules_;            // PARAM_RULES (flowId → rule, namespace)
+    std::map<std::string, std::vector<int64_t>> nsParamIds_;  // NAMESPACE_FLOW_ID_MAP of the param rules
+    std::unordered_map<int64_t, uint32_t> keyOfParam_;        // flowId → dense cparam rule index
+    std::unordered_map<std::string, uint64_t> valueIds_;      // parameter string → u64 value
 };
 
 }  // namespace cluster

@@ -18,6 +18,11 @@ std::vector<sg_namespace> ns;
 std::vector<std::vector<sg_req>> batches;
 int fail_next = 0;
 std::map<uint64_t, int> tickets;  // submitted batch → its status
+std::vector<sg_cparam_rule> cprules;
+std::vector<sg_param_hot_item> cphot;
+int cp_capacity = 0;
+std::vector<sg_cparam_req> cpreqs;
+std::vector<uint64_t> cpvalues;
 uint64_t next_ticket = 1;
 }  // namespace fake
 
@@ -68,6 +73,29 @@ int sg_flow_poll(sg_handle*, uint64_t ticket) {
 int sg_flow_wait(sg_handle* h, uint64_t ticket) {
     const int r = sg_flow_poll(h, ticket);
     return r == 1 ? SG_OK : r;
+}
+int sg_cparam_load_rules(sg_handle*, const sg_cparam_rule* r, uint32_t n, const sg_param_hot_item* hot, uint32_t n_hot,
+                         int32_t capacity_log2) {
+    std::lock_guard<std::mutex> lk(fake::mu);
+    fake::cprules.assign(r, r + n);
+    fake::cphot.assign(hot, hot + n_hot);
+    fake::cp_capacity = capacity_log2;
+    return SG_OK;
+}
+// records the batch; answers OK with remaining = number of values, wait = key (BAD / NO_RULE as the engine would)
+int sg_cparam_decide_batch_host(sg_handle*, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                uint64_t n_values, sg_result* out) {
+    std::lock_guard<std::mutex> lk(fake::mu);
+    fake::cpreqs.assign(req, req + n);
+    fake::cpvalues.assign(values, values + n_values);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t k = req[i].key & SG_KEY_INDEX;
+        out[i].status = (k == SG_KEY_BAD) ? SG_STATUS_BAD_REQUEST
+                        : (k >= fake::cprules.size()) ? SG_STATUS_NO_RULE_EXISTS : SG_STATUS_OK;
+        out[i].remaining = (int32_t)req[i].value_count;
+        out[i].wait_ms = (int32_t)k;
+    }
+    return SG_OK;
 }
 int sg_conc_decide_batch_host(sg_handle*, const sg_conc_req* req, uint64_t n, sg_conc_result* out) {
     std::lock_guard<std::mutex> lk(fake::mu);

@@ -134,6 +134,88 @@ int main(int argc, char** argv) {
         for (const auto& x : v) ++a[x];
     for (const auto& r : rec_res) ++b[std::make_tuple(r.status, r.remaining, r.wait_ms)];
     CHECK(a == b);
-    std::printf("OK %zu %d\n", total, batches);
+
+    // cluster param tokens through the mirror (requestParamTokens: one device batch, explicit times) against the
+    // oracle's ClusterParamFlowChecker on the same requests; decisions only depend on value equality, so the
+    // test's own string → u64 dictionary stands in for the mirror's
+    std::vector<ParamFlowRule> prules;
+    std::vector<sg_cparam_rule> ptab;
+    std::vector<sg_param_hot_item> phot;
+    std::map<std::string, uint64_t> dict;
+    auto vid = [&](const std::string& v) {
+        auto it = dict.find(v);
+        return it != dict.end() ? it->second : (dict[v] = dict.size() + 1);
+    };
+    for (int i = 0; i < 40; ++i) {
+        ParamFlowRule r;
+        r.resource = "pres" + std::to_string(i);
+        r.paramIdx = 0;
+        r.count = (double)(2 + g() % 20);
+        r.clusterMode = true;
+        ParamFlowClusterConfig c;
+        c.flowId = 5000 + i;
+        c.thresholdType = ClusterRuleConstant::FLOW_THRESHOLD_GLOBAL;
+        c.sampleCount = (i % 2) ? 10 : 5;
+        r.clusterConfig = c;
+        sg_cparam_rule t{};
+        t.flow_id = 5000 + i;
+        t.count = r.count;
+        t.threshold_type = c.thresholdType;
+        t.sample_count = c.sampleCount;
+        t.window_interval_ms = 1000;
+        t.hot_begin = (uint32_t)phot.size();
+        if (i % 4 == 0) {
+            r.paramFlowItemList = {{std::string("v1"), "", 40}};
+            phot.push_back(sg_param_hot_item{vid("v1"), 40, 0});
+        }
+        t.hot_count = (uint32_t)phot.size() - t.hot_begin;
+        prules.push_back(r);
+        ptab.push_back(t);
+    }
+    svc.loadParamRules("default", prules);
+    CHECK(svc.lastError().empty());
+    std::vector<GpuTokenService::ParamTokenRequest> preq;
+    std::vector<sg_cparam_req> oreq;
+    std::vector<uint64_t> ovals;
+    std::mt19937_64 pg(11);
+    int64_t pt = 1'700'000'100'000;
+    for (int i = 0; i < 30000; ++i) {
+        pt += (int64_t)(pg() % 3 == 0);
+        const int k = (int)(pg() % 42);  // two unknown flowIds
+        const int nv = pg() % 10 == 0 ? 2 + (int)(pg() % 2) : 1;
+        GpuTokenService::ParamTokenRequest q{pt, (int64_t)(5000 + k), 1 + (int)(pg() % 2), {}};
+        sg_cparam_req o{};
+        o.ts_ms = pt;
+        o.key = k < 40 ? (uint32_t)k : SG_KEY_NO_RULE;
+        o.acquire = q.acquireCount;
+        o.value_begin = (uint32_t)ovals.size();
+        o.value_count = (uint32_t)nv;
+        for (int j = 0; j < nv; ++j) {
+            const std::string v = "v" + std::to_string(1 + (int)(pg() % 30));
+            q.params.push_back(v);
+            ovals.push_back(vid(v));
+        }
+        preq.push_back(q);
+        oreq.push_back(o);
+    }
+    std::vector<TokenResult> pres = svc.requestParamTokens(preq);
+    CHECK(svc.lastError().empty());
+    or_cts* pora = or_cts_new(1.0, 1.0);
+    CHECK(or_cts_set_namespaces(pora, &ns, 1) == 0);
+    CHECK(or_cts_load_param_rules(pora, ptab.data(), (uint32_t)ptab.size(), phot.data(), (uint32_t)phot.size()) == 0);
+    std::vector<sg_result> pwant(oreq.size());
+    CHECK(or_cts_decide_param(pora, oreq.data(), oreq.size(), ovals.data(), pwant.data()) == 0);
+    int passes = 0;
+    for (size_t i = 0; i < pwant.size(); ++i) {
+        if (pwant[i].status != *pres[i].getStatus() || pwant[i].remaining != pres[i].getRemaining()) {
+            std::fprintf(stderr, "param mismatch at %zu: oracle (%d,%d) gpu (%d,%d)\n", i, pwant[i].status,
+                         pwant[i].remaining, *pres[i].getStatus(), pres[i].getRemaining());
+            return 1;
+        }
+        passes += pwant[i].status == SG_STATUS_OK;
+    }
+    CHECK(passes > 0 && passes < (int)pwant.size());
+    or_cts_free(pora);
+    std::printf("OK %zu %d %d\n", total, batches, passes);
     return 0;
 }

@@ -12,6 +12,11 @@ extern std::vector<sg_flow_rule> rules;
 extern std::vector<sg_namespace> ns;
 extern std::vector<std::vector<sg_req>> batches;
 extern int fail_next;
+extern std::vector<sg_cparam_rule> cprules;
+extern std::vector<sg_param_hot_item> cphot;
+extern int cp_capacity;
+extern std::vector<sg_cparam_req> cpreqs;
+extern std::vector<uint64_t> cpvalues;
 }  // namespace fake
 
 using namespace sentinel::cluster;
@@ -110,9 +115,50 @@ int main() {
     auto failed = svc.requestTokens({{now + 3, 30, 1, false}, {now + 3, 10, 1, false}});
     CHECK(failed[0].getStatus().value() == TokenResultStatus::FAIL && failed[1].getStatus().value() == TokenResultStatus::FAIL);
 
-    // --- param tokens are not on this device path: validation, then FAIL
+    // --- cluster param rules: applyClusterParamRules filtering, ascending flowId, hot items via the dictionary
+    auto prule = [](int64_t flowId, double count) {
+        ParamFlowRule r;
+        r.resource = "p" + std::to_string(flowId);
+        r.paramIdx = 0;
+        r.count = count;
+        r.clusterMode = true;
+        ParamFlowClusterConfig c;
+        c.flowId = flowId;
+        c.thresholdType = ClusterRuleConstant::FLOW_THRESHOLD_GLOBAL;
+        r.clusterConfig = c;
+        return r;
+    };
+    ParamFlowRule p90 = prule(90, 5), p70 = prule(70, 3), pdup = prule(70, 4), pnoidx = prule(80, 1),
+                  plocal = prule(60, 1), pbadwin = prule(50, 1);
+    pnoidx.paramIdx.reset();                        // paramIdx null: invalid
+    plocal.clusterMode = false;                     // not a cluster rule: skipped
+    pbadwin.clusterConfig->windowIntervalMs = 999;  // 999 % 10 != 0: invalid window
+    p90.paramFlowItemList = {{std::string("hot"), "", 7},             // String key
+                             {std::string("hot"), "java.lang.String", 9},  // same key, later one wins
+                             {std::string("5"), "int", 2},            // Integer key: never equals a String
+                             {std::nullopt, "", 3},                    // null object: skipped
+                             {std::string("neg"), "", -1}};           // count < 0: skipped
+    svc.loadParamRules("default", {p90, p70, pdup, pnoidx, plocal, pbadwin});
+    CHECK(fake::cprules.size() == 2);
+    CHECK(fake::cprules[0].flow_id == 70 && fake::cprules[0].count == 4);  // the last duplicate wins
+    CHECK(fake::cprules[1].flow_id == 90 && fake::cprules[1].hot_count == 1);
+    CHECK(fake::cphot.size() == 1 && fake::cphot[0].threshold == 9);
+    CHECK(fake::cprules[1].sample_count == 10 && fake::cprules[1].window_interval_ms == 1000);
+    CHECK(fake::cp_capacity == 16);
+    // --- param tokens: validation, then sg_cparam_* with values through the same dictionary
     CHECK(svc.requestParamToken(30, 1, {}).getStatus().value() == TokenResultStatus::BAD_REQUEST);
-    CHECK(svc.requestParamToken(30, 1, {"x"}).getStatus().value() == TokenResultStatus::FAIL);
+    CHECK(svc.requestParamToken(std::nullopt, 1, {"x"}).getStatus().value() == TokenResultStatus::BAD_REQUEST);
+    TokenResult pt = svc.requestParamToken(90, 2, {"hot", "x", "hot"});
+    CHECK(pt.getStatus().value() == TokenResultStatus::OK && pt.getRemaining() == 3 && pt.getWaitInMs() == 1);
+    CHECK(fake::cpreqs.size() == 1 && fake::cpreqs[0].acquire == 2 && fake::cpreqs[0].value_count == 3);
+    CHECK(fake::cpvalues.size() == 3 && fake::cpvalues[0] == fake::cphot[0].value && fake::cpvalues[2] == fake::cpvalues[0]);
+    CHECK(fake::cpvalues[1] != fake::cpvalues[0]);
+    CHECK(svc.requestParamToken(12345, 1, {"x"}).getStatus().value() == TokenResultStatus::NO_RULE_EXISTS);
+    auto pts = svc.requestParamTokens({{now + 5, 70, 1, {"a"}}, {now + 6, 90, 1, {"b", "c"}}});
+    CHECK(pts.size() == 2 && pts[0].getWaitInMs() == 0 && pts[1].getRemaining() == 2);
+    CHECK(fake::cpreqs[1].value_begin == 1 && fake::cpreqs[1].ts_ms == now + 6);
+    svc.loadParamRules("default", {p90});  // flowId 70 dropped from the namespace
+    CHECK(fake::cprules.size() == 1 && fake::cprules[0].flow_id == 90);
     // --- concurrent tokens: validation, then sg_conc_* with a dense client id per address
     CHECK(svc.requestConcurrentToken("", 30, 1).getStatus().value() == TokenResultStatus::BAD_REQUEST);
     CHECK(svc.requestConcurrentToken("10.0.0.1", 30, 0).getStatus().value() == TokenResultStatus::BAD_REQUEST);

@@ -11,11 +11,14 @@ from sentinel_amd.workload import zipf_keys
 pytestmark = pytest.mark.gpu
 
 
-def _pair(rules, hot=None, connected=1, cap=12):
+WALKERS = [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY]
+
+
+def _pair(rules, hot=None, connected=1, cap=12, flags=0):
     from sentinel_amd.engine import FlowEngine
     ns = np.zeros(1, abi.NS_DTYPE)
     ns["connected_count"] = connected
-    eng = FlowEngine(device=0, max_batch=1 << 20)
+    eng = FlowEngine(device=0, max_batch=1 << 20, flags=flags)
     eng.set_namespaces(ns)
     eng.cparam_load_rules(rules, hot, cap)
     ora = ClusterTokenService()
@@ -75,11 +78,12 @@ def _compare_sums(eng, ora, req, values, now):
         assert eng.cparam_sum(k, v, now) == ora.param_sum(k, v, now), (k, v)
 
 
+@pytest.mark.parametrize("flags", WALKERS)
 @pytest.mark.parametrize("S,interval", [(10, 1000), (2, 1000), (1, 500), (5, 25)])
-def test_single_value_requests(S, interval):
+def test_single_value_requests(S, interval, flags):
     rng = np.random.default_rng(S * 7 + interval)
     rules = _rules(20, rng, S, interval)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     t = 1_700_000_000_003
     for _ in range(3):
         req, vals = _trace(rng, 50_000, 20, 300, t, int(rng.integers(100, 3 * interval + 500)), bad=0.01)
@@ -89,10 +93,11 @@ def test_single_value_requests(S, interval):
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
 
 
-def test_multi_value_requests_all_or_nothing():
+@pytest.mark.parametrize("flags", WALKERS)
+def test_multi_value_requests_all_or_nothing(flags):
     rng = np.random.default_rng(3)
     rules = _rules(6, rng)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     t = 1_700_000_000_500
     for _ in range(3):
         req, vals = _trace(rng, 6_000, 6, 40, t, 1500, multi=0.05, bad=0.01)
@@ -134,15 +139,16 @@ def test_rule_reload_keeps_surviving_metrics():
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
 
 
+@pytest.mark.parametrize("flags", WALKERS)
 @pytest.mark.parametrize("seed,multi", [(11, 0.3), (12, 0.8)])
-def test_multi_value_heavy_fixed_point(seed, multi):
+def test_multi_value_heavy_fixed_point(seed, multi, flags):
     """Most requests carry several (possibly repeated) values over a few hot values: the all-or-nothing outcomes
     chain across slots, so the device needs several fixed-point rounds; every result and window sum must still
     equal the sequential replay."""
     rng = np.random.default_rng(seed)
     rules = _rules(5, rng)
     rules["count"] = rng.integers(3, 12, 5)
-    eng, ora = _pair(rules)
+    eng, ora = _pair(rules, flags=flags)
     t = 1_700_000_000_250
     rounds = []
     for _ in range(3):
