@@ -108,6 +108,9 @@ struct sg_handle {
     // one-pipeline batch scratch (value-position records, fixed point over multi-value requests)
     uint32_t* d_cp_owner = nullptr;
     uint32_t* d_cp_pslot = nullptr;
+    uint32_t* d_cp_long = nullptr;    // segment lists over the value records (capacity cp_val_cap)
+    uint32_t* d_cp_short = nullptr;
+    uint64_t cp_class_off[kClasses]{};
     uint8_t* d_cp_dirty = nullptr;    // [cptotal] re-walk flags, kept all-zero between batches
     uint64_t cp_dirty_cap = 0;
     uint8_t* d_cp_chk = nullptr;
@@ -475,6 +478,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_ps_last_ts);
     dfree(h->d_cp_owner);
     dfree(h->d_cp_pslot);
+    dfree(h->d_cp_long);
+    dfree(h->d_cp_short);
     dfree(h->d_cp_dirty);
     dfree(h->d_cp_chk);
     dfree(h->d_cp_assume);
@@ -1501,11 +1506,12 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     const int gbits = bits_for(h->cptotal + 1);
     const int pbits = bits_for(nv);
     if (pbits + gbits > 64 || gbits > 32) return fail(h, SG_E_UNSUPPORTED, "param tables x values too large for 64-bit records");
-    if (nv > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "more values than max_batch");
     // scratch sized for the batch's value positions
     if (nv > h->cp_val_cap) {
         dfree(h->d_cp_owner);
         dfree(h->d_cp_pslot);
+        dfree(h->d_cp_long);
+        dfree(h->d_cp_short);
         dfree(h->d_cp_chk);
         dfree(h->d_cp_rec);
         dfree(h->d_cp_rec2);
@@ -1515,6 +1521,14 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_hist, sizeof(uint32_t) * radix_hist_words(nv)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "cparam batch scratch");
+        uint64_t off = 0;  // k_seg's class slices for nv records (as sg_create sizes them for max_batch)
+        for (int c = 0; c < kClasses; ++c) {
+            h->cp_class_off[c] = off;
+            off += (c == 0 ? nv : nv / (kClassMax[c - 1] + 1)) + 1;
+        }
+        if (hipMalloc(&h->d_cp_long, sizeof(uint32_t) * (nv + 1)) != hipSuccess ||
+            hipMalloc(&h->d_cp_short, sizeof(uint32_t) * off) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "cparam segment lists");
         h->cp_val_cap = nv;
     }
     if (h->cptotal > h->cp_dirty_cap) {
@@ -1608,11 +1622,11 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     sgm.kshift = pbits;
     sgm.K = (uint32_t)h->cptotal;
     sgm.err = h->d_err;
-    sgm.long_list = h->d_long_list;
+    sgm.long_list = h->d_cp_long;
     sgm.long_count = h->d_long_count;
-    sgm.short_list = h->d_short_list;
+    sgm.short_list = h->d_cp_short;
     sgm.short_count = h->d_long_count + 1;
-    for (int cl = 0; cl < kClasses; ++cl) sgm.class_off[cl] = h->class_off[cl];
+    for (int cl = 0; cl < kClasses; ++cl) sgm.class_off[cl] = h->cp_class_off[cl];
     sgm.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 32u;
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, launch_seg(sgm, stream));
