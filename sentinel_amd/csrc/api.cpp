@@ -279,7 +279,9 @@ int layout_records(sg_handle* h) {
     h->kbits = bits_for((uint64_t)h->K);  // must hold K itself (sentinel key of rejected requests)
     if (h->kbits < 1) h->kbits = 1;
     h->ibits = bits_for(h->cfg.max_batch > 1 ? h->cfg.max_batch - 1 : 1);
-    h->abits = 64 - h->kbits - h->ibits;
+    // acquire field: 7 bits + prio (larger acquireCounts escape to the request), so that {idx, acode} fit the
+    // low 32 bits whenever ibits <= 24 (the short walker's compact LDS records)
+    h->abits = std::min(8, 64 - h->kbits - h->ibits);
     if (h->abits < 3) return fail(h, SG_E_UNSUPPORTED, "rule count x max_batch too large for 64-bit records");
     return SG_OK;
 }
@@ -360,7 +362,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     };
     if (hipSetDevice(h->device) != hipSuccess) return bail(SG_E_DEVICE);
     const uint64_t n = cfg->max_batch;
-    if (hipMalloc(&h->d_rec, n * 8) != hipSuccess || hipMalloc(&h->d_rec_sorted, n * 8) != hipSuccess)
+    // + kRecW records of slack: the short walker stages record windows past a segment's end unclamped
+    if (hipMalloc(&h->d_rec, (n + kRecW) * 8) != hipSuccess || hipMalloc(&h->d_rec_sorted, (n + kRecW) * 8) != hipSuccess)
         return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_hist, sizeof(uint32_t) * radix_hist_words(n)) != hipSuccess) return bail(SG_E_NOMEM);

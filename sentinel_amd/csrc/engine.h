@@ -40,7 +40,8 @@ constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
 constexpr int kShortMax = 256;            // default: segments longer than this are walked by a whole wave
 constexpr int kLdsBnd = 4096;             // period-table entries the walk kernel stages in LDS
-constexpr int kLdsBndFlow = 2048;         // the same for the cluster flow walkers (LDS budget of the short walker)
+constexpr int kLdsBndFlow = 1024;         // the same for the cluster flow walkers (LDS budget of the short walker)
+constexpr int kRecW = 32;                 // records per lane the short walker stages in LDS at a time
 // Short segments are grouped by length class (length <= 4, 16, 64, 256, 1024, more) so that the 64 lanes
 // of a short-walker wave walk segments of similar length.
 constexpr int kClasses = 6;
@@ -58,7 +59,9 @@ struct BatchArgs {
     uint64_t* rec;       // packed records, request order
     uint32_t* hist0;     // k_prep: per-tile histogram of the first sort digit (radix_hist layout), or nullptr
     uint64_t* rec_sorted;
-    // record layout: [key : kbits][idx : ibits][acode : abits], acode = acquire << 1 | prio
+    // record layout: [key : kbits][0 …][idx : ibits][acode : abits], acode = acquire << 1 | prio, abits <= 8;
+    // with abits == 8 and ibits <= 24 the low 32 bits {idx, acode} are the compact record the short walker stages
+    // in LDS
     int kshift;          // = 64 - kbits
     int abits;
     uint64_t imask;      // (1 << ibits) - 1

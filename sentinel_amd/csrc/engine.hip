@@ -87,6 +87,16 @@ __device__ __forceinline__ Decoded decode(const BatchArgs& a, uint64_t rec) {
     return d;
 }
 
+// The compact record (low 32 bits of a record when abits == 8 and ibits <= 24): {idx : 24, acquire : 7, prio : 1}.
+__device__ __forceinline__ Decoded decode_c(const BatchArgs& a, uint32_t c) {
+    Decoded d;
+    d.idx = c >> 8;
+    d.prio = (c & 1u) != 0;
+    const uint32_t q = (c >> 1) & 127u;
+    d.acq = (q == 127u) ? (int64_t)a.req[d.idx].acquire : (int64_t)q;
+    return d;
+}
+
 // ------------------------------------------------------------------------------------------- prep
 
 // One block per 4096-request tile (the radix sort's tile). With a.hist0 set the block also counts the
@@ -227,6 +237,8 @@ __device__ __forceinline__ void open_bucket(PeriodState& ps, int64_t start, cons
 __shared__ uint32_t g_sbnd[kLdsBndFlow];
 __shared__ uint32_t g_boff[kMaxWl];  // offset of window length w's table in g_sbnd
 __shared__ int g_blds;               // 1: tables in g_sbnd, 0: read from a.bnd
+__shared__ int64_t g_p0[kMaxWl];     // a.p0 / a.np staged by stage_periods: per-lane reads of these tiny tables
+__shared__ uint32_t g_np[kMaxWl];    // (indexed by the rule's window length) were each a memory round trip
 
 // Period tracking shared by the walkers: requests of one flowId arrive in index order, so the
 // window period only moves forward; the cached boundary of the next period answers most lookups.
@@ -243,7 +255,7 @@ struct PeriodCursor {
     __device__ __forceinline__ void init(const BatchArgs& a, int w) {
         gbnd = a.bnd + (size_t)w * kMaxPeriods;
         base = g_boff[w];
-        np = a.np[w];
+        np = g_np[w];
         q = 0xFFFFFFFFu;
         next_b = 0;
     }
@@ -312,7 +324,7 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
     Bucket* ring = a.ring + (size_t)k * a.stride;
     PeriodCursor<L> pc;
     pc.init(a, R.wl_idx);
-    const int64_t P0 = a.p0[R.wl_idx];
+    const int64_t P0 = g_p0[R.wl_idx];
     PeriodState ps;
     {
         const Occ o = a.occ[k];
@@ -391,7 +403,7 @@ struct WaveWalker {
         : a(a_), R(a_.rules[k]), lane(lane_id()) {
         ring = a.ring + (size_t)k * a.stride;
         pc.init(a, R.wl_idx);
-        P0 = a.p0[R.wl_idx];
+        P0 = g_p0[R.wl_idx];
         st = INT64_MIN;
 #pragma unroll
         for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = 0;
@@ -790,6 +802,10 @@ __device__ __forceinline__ void stage_periods(const BatchArgs& a) {
         off += npw;
     }
     if (threadIdx.x == 0) g_blds = lds ? 1 : 0;
+    if (threadIdx.x < (unsigned)a.n_wl) {
+        g_p0[threadIdx.x] = a.p0[threadIdx.x];
+        g_np[threadIdx.x] = a.np[threadIdx.x];
+    }
     __syncthreads();
 }
 
@@ -923,7 +939,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     const int64_t wl = R.wl;
     PeriodCursor<L> pc;
     pc.init(a, act ? R.wl_idx : 0);
-    const int64_t P0 = a.p0[act ? R.wl_idx : 0];
+    const int64_t P0 = g_p0[act ? R.wl_idx : 0];
     PeriodState ps;
     ps.occ_pass = occ.pass;
     ps.occ_req = occ.pass_req;
@@ -1048,6 +1064,161 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     }
 }
 
+// LDS-DMA of the compact records at positions p .. p + R - 1 of every active lane
+// into its column of `wrecs` ([kRecW][64] words: row r, lane j). No VGPR holds a record in flight, so nothing
+// waits for these loads until the walk reads them (one vmcnt wait per window instead of one per few records).
+// p < n: the record buffers have kRecW records of slack past max_batch, so the window needs no clamping.
+// s_waitcnt vmcnt(0) as a builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), not inline asm: the compiler's
+// wait-count pass sees it and knows the LDS-DMA writes have landed. After an inline-asm wait it still counted them
+// as pending and put a vmcnt(0) before every later LDS read of the loop — each one also waiting for the stores
+// issued since (a store round trip per period open).
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+template <int R>
+__device__ __forceinline__ void glds_rows(const uint32_t* src, uint32_t* wrecs) {
+    if constexpr (R > 0) {
+        // row R - 1: the low word of record R - 1. The immediate offset (8 (R - 1) bytes) is added to the LDS
+        // address too, so the LDS base is moved back by as much.
+        glds_rows<R - 1>(src, wrecs);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(wrecs + (R - 1) * 64 - 2 * (R - 1)),
+                                         4, 8 * (R - 1), 0);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void stage_records(const BatchArgs& a, uint32_t* wrecs, uint64_t p) {
+    glds_rows<R>(reinterpret_cast<const uint32_t*>(a.rec_sorted + p), wrecs);
+}
+
+// walk_reg with the records read from LDS: the group staged each lane's first kRecW compact records (with the
+// ring gather, one wait for both); a lane that has used its window parks, and when no lane can go on the wave
+// stages the parked lanes' next windows at once. Same decisions as walk_serial.
+template <int SM, bool L>
+__device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t k, uint64_t s, uint64_t e,
+                                         const Rule& R, const Occ& occ, SlotSnap* snap, uint32_t* wrecs, int lane,
+                                         int64_t T0, int rows) {
+    Bucket* ring = a.ring + (size_t)k * a.stride;
+    const int S = R.S;
+    const int64_t wl = R.wl;
+    PeriodCursor<L> pc;
+    pc.init(a, act ? R.wl_idx : 0);
+    const int64_t P0 = g_p0[act ? R.wl_idx : 0];
+    PeriodState ps;
+    ps.occ_pass = occ.pass;
+    ps.occ_req = occ.pass_req;
+#pragma unroll
+    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
+    ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+    int I = -1;      // slot of the open period
+    int64_t ws = 0;  // its window start
+    uint64_t wb = s;  // position of the lane's LDS window row 0
+    uint64_t p = s;   // position of the next record
+    bool live = act && p < e;
+    bool park = false;  // window used up, records left
+    uint32_t win = (uint32_t)rows;  // records in the lane's window (the first window may be shorter than kRecW)
+    uint32_t qn = 0;    // period of the next record (valid when live && !park)
+    Decoded dn;
+    auto peek = [&]() {
+        if (p >= e) {
+            live = false;
+            return;
+        }
+        if (p - wb >= (uint64_t)win) {
+            park = true;
+            return;
+        }
+        dn = decode_c(a, wrecs[(uint32_t)(p - wb) * 64 + lane]);
+        qn = pc.of(dn.idx);
+    };
+    if (live) peek();
+    for (;;) {
+        if (!__ballot(live && !park)) {
+            if (!__ballot(live)) break;
+            // every live lane waits for its next window: stage them all, one wait
+            if (park) {
+                stage_records<kRecW>(a, wrecs, p);
+                wb = p;
+                win = kRecW;
+            }
+            wait_vm0();
+            __builtin_amdgcn_wave_barrier();
+            if (park) {
+                park = false;
+                peek();
+            }
+            continue;
+        }
+        // 1. open the period of every lane whose next record starts one (the first record included)
+        if (live && !park && qn != pc.q) {
+            if (I >= 0) {  // close the open bucket: memory and the snapshot
+                store_bucket(ring + I, ws, ps.cur);
+                snap[I].st = (int32_t)(ws - T0);
+                snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
+                snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
+            }
+            const uint32_t qprev = pc.q;
+            pc.seek(qn);
+            const int64_t P = P0 + (int64_t)qn;
+            I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
+            ws = P * wl;
+            const int64_t lo_rel = ws - (int64_t)S * wl - T0;
+            const int h = I + 1 == S ? 0 : I + 1;
+            int32_t sx[SM], px[SM], wx[SM];
+#pragma unroll
+            for (int x = 0; x < SM; ++x) {
+                sx[x] = snap[x].st;
+                px[x] = snap[x].pass;
+                wx[x] = snap[x].wait;
+            }
+            uint32_t wp = 0, ww = 0, ho = 0;
+#pragma unroll
+            for (int x = 0; x < SM; ++x) {
+                const bool v = (x < S) & (x != I) & ((int64_t)sx[x] > lo_rel);
+                const uint32_t m = v ? 0xFFFFFFFFu : 0u;
+                wp += (uint32_t)px[x] & m;
+                ww += (uint32_t)wx[x] & m;
+                ho = (x == h) ? ((uint32_t)px[x] & m) : ho;
+            }
+            ps.wo_pass = (int64_t)wp;
+            ps.wo_wait = (int64_t)ww;
+            ps.head_other = (int64_t)ho;
+            const int32_t stI_rel = snap[I].st;
+            const int64_t stI = stI_rel == INT32_MIN ? INT64_MIN : T0 + (int64_t)stI_rel;
+            int64_t cI[SG_NUM_EVENTS];
+            if (stI == ws) {
+#pragma unroll
+                for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
+            }
+            open_bucket(ps, stI, cI, ws);
+        }
+        // 2. decide records while they stay in the open period (ClusterFlowChecker.acquireClusterToken :67-111)
+        while (live && !park && qn == pc.q) {
+            const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
+            const double next_remaining = R.thr - latest - (double)dn.acq;
+            if (next_remaining >= 0) {
+                ps.cur[SG_EV_PASS] += dn.acq;
+                ps.cur[SG_EV_PASS_REQUEST] += 1;
+                if (dn.prio) ps.cur[SG_EV_OCCUPIED_PASS] += dn.acq;
+                store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+            } else {
+                int32_t wait;
+                const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, dn.acq, dn.prio, &wait);
+                if (stt != SG_STATUS_BLOCKED) store_result(a.out, dn.idx, stt, 0, wait);
+            }
+            ++p;
+            peek();
+        }
+    }
+    if (act) {
+        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        Occ o;
+        o.pass = ps.occ_pass;
+        o.pass_req = ps.occ_req;
+        a.occ[k] = o;
+    }
+}
+
 // Short-segment walker: each wave takes 64 segments of <= short_max records of one length class and
 // walks one per lane; the classes of longer segments go first. SM > 0: ring snapshot in LDS (every flow
 // has sampleCount <= SM <= kGatherMaxS); SM == 0: generic walker re-reading the ring.
@@ -1063,8 +1234,126 @@ constexpr int kGatherMaxS = 10;
 #endif
 constexpr int kShortBlocksPerCu = SG_SHORT_BLOCKS;  // occupancy target (VGPR budget) of the short walker
 
+// Short walker over compact LDS records (C): as walk_short_body, with each group's segment descriptors loaded
+// one group ahead (they ride along with the previous group's loads, so a group costs one memory round trip
+// before its walk: ring, rule, occupy counters, segment end and records together) and first record windows
+// sized to the length class.
 template <int SM, bool L>
-__device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* snap_all) {
+__device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* snap_all, uint32_t* recs_all) {
+    static_assert(SM > 0, "LDS ring snapshot");
+    const int lane = lane_id();
+    SlotSnap* snap = snap_all + (threadIdx.x / 64) * (64 * SM);
+    uint32_t* wrecs = recs_all + (threadIdx.x / 64) * (kRecW * 64);
+    uint32_t cnt[kClasses], grp_end[kClasses];
+    uint32_t total = 0;
+#pragma unroll
+    for (int c = kClasses - 1; c >= 0; --c) {  // group order: longest class first
+        cnt[c] = a.short_count[c];
+        total += (cnt[c] + 63) / 64;
+        grp_end[c] = total;
+    }
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    if (wave >= total) return;
+    const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
+    // group g: class (wave-uniform), this lane's list entry; inactive lanes of a class's last group repeat
+    // the class's entry 0 (valid addresses)
+    auto desc = [&](uint32_t g, int& c, bool& act, uint32_t& s, uint32_t& k) {
+        c = kClasses - 1;
+        uint32_t g0 = 0;
+        while (g >= grp_end[c]) {
+            g0 = grp_end[c];
+            --c;
+        }
+        c = __builtin_amdgcn_readfirstlane(c);
+        const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
+        act = i < cnt[c];
+        const uint64_t li = a.class_off[c] + (act ? i : 0u);
+        s = a.short_list[li];
+        k = a.short_key[li];
+    };
+    int c_n;
+    bool act_n;
+    uint32_t s_n, k_n;
+    desc(wave, c_n, act_n, s_n, k_n);
+    for (uint32_t g = wave; g < total; g += nwaves) {
+        const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
+        const int c = c_n;
+        const bool act = act_n;
+        const uint64_t s = s_n;
+        const uint32_t k = k_n;
+        const uint64_t e = a.seg_end[k];
+        const Rule R = a.rules[k];
+        const Occ occ = a.occ[k];
+        // first window: the class's longest segment (<= 4, <= 16 records) or kRecW
+        const int rows = c == 0 ? (int)kClassMax[0] : c == 1 ? (int)kClassMax[1] : kRecW;
+        if (c == 0) stage_records<kClassMax[0]>(a, wrecs, s);
+        else if (c == 1) stage_records<kClassMax[1]>(a, wrecs, s);
+        else stage_records<kRecW>(a, wrecs, s);
+        // the next group's descriptors (unconditional: a conditional load would be copied, and wait, at the merge)
+        desc(min(g + nwaves, total - 1), c_n, act_n, s_n, k_n);
+        {
+            // ring gather: piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS},
+            // 1: WAITING); slots past the handle's stride read slot 0 again (ignored: q >= S)
+            // every piece is loaded before any is used (the scheduling barrier keeps the compiler from
+            // interleaving the loads with their LDS writes, which serialised the gather into round trips)
+            constexpr int kT = 2 * SM;
+            int gl = lane;
+            asm volatile("" : "+v"(gl));
+            ulonglong2 v[kT];
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                const int pc = t * 64 + gl;
+                const int j = pc / kT;
+                const int q = (pc % kT) >> 1;
+                const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
+                const int qq = q < a.stride ? q : 0;
+                v[t] = *(reinterpret_cast<const ulonglong2*>(a.ring + (size_t)kj * a.stride + qq) + ((pc & 1) ? 3 : 0));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // every dword of every piece stays live until here: the allocator would otherwise reuse the unused
+            // halves as temporaries, and overwriting a register a load is still filling waits for that load
+#pragma unroll
+            for (int t = 0; t < kT; ++t) asm volatile("" ::"v"(v[t].x), "v"(v[t].y));
+#pragma unroll
+            for (int t = 0; t < kT; ++t) {
+                const int pc = t * 64 + gl;
+                SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
+                if (pc & 1) {
+                    d.wait = (int32_t)v[t].y;
+                } else {
+                    d.st = snap_rel((int64_t)v[t].x, T0);
+                    d.pass = (int32_t)v[t].y;
+                }
+            }
+        }
+        wait_vm0();  // the staged records have landed
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t tw1 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
+        walk_lds<SM, L>(a, act, k, s, e, R, occ, snap + lane * SM, wrecs, lane, T0, rows);
+        if (a.dbg & 64) {  // per class: groups, gather time, walk time (100 MHz ticks)
+            const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) {
+                atomicAdd(&a.dbg_ctr[0], (unsigned long long)(tw2 - tw0));
+                atomicAdd(&a.dbg_ctr[1 + c], 1ull);
+                atomicAdd(&a.dbg_ctr[7 + c], (unsigned long long)(tw1 - tw0));
+                atomicAdd(&a.dbg_ctr[7 + c], (unsigned long long)(tw2 - tw1) << 32);
+            }
+        }
+    }
+}
+
+template <int SM, bool L, bool C>
+__device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* snap_all, uint32_t* recs_all) {
+    if constexpr (SM > 0 && C) {
+        const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
+        if (a.narrow && narrow_span(a, T0)) {
+            walk_short_lds<SM, L>(a, snap_all, recs_all);
+            return;
+        }
+    }
     constexpr int kSnapPerWave = SM > 0 ? 64 * SM : 1;
     const int lane = lane_id();
     SlotSnap* snap = snap_all + (threadIdx.x / 64) * kSnapPerWave;
@@ -1091,7 +1380,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
         c = __builtin_amdgcn_readfirstlane(c);
         const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
         const bool act = i < cnt[c];
-        if constexpr (SM > 0) if (snap_ok) {
+        if constexpr (SM > 0 && !C) if (snap_ok) {
             const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
             // 1. segment descriptors (inactive lanes of the last group repeat entry 0: valid addresses)
             const uint64_t li = a.class_off[c] + (act ? i : 0u);
@@ -1164,14 +1453,15 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
     }
 }
 
-template <int SM>
-__global__ void __launch_bounds__(256, kShortBlocksPerCu) k_walk_short(BatchArgs a) {
+template <int SM, bool C>
+__global__ void __launch_bounds__(256, C ? 2 : kShortBlocksPerCu) k_walk_short(BatchArgs a) {
     static_assert(SM <= kGatherMaxS, "LDS budget of the ring snapshot");
     __shared__ SlotSnap snap_all[4 * (SM > 0 ? 64 * SM : 1)];
+    __shared__ uint32_t recs_all[SM > 0 && C ? 4 * kRecW * 64 : 1];
     if (*a.err) return;
     stage_periods(a);
-    if (g_blds) walk_short_body<SM, true>(a, snap_all);
-    else walk_short_body<SM, false>(a, snap_all);
+    if (g_blds) walk_short_body<SM, true, C>(a, snap_all, recs_all);
+    else walk_short_body<SM, false, C>(a, snap_all, recs_all);
 }
 
 // One wave per skipped piece: Σ acquire and Σ prioritized acquire over its records, added with 64-bit
@@ -1306,11 +1596,17 @@ hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// Compact LDS records for the short walker: {idx, acode} fill the low 32 bits (abits == 8, ibits <= 24).
+static bool short_compact(const BatchArgs& a) { return a.abits == 8 && a.imask <= 0xFFFFFFull && !(a.dbg & 4); }
+
 template <int SM>
 static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
-    static unsigned blocks = 0;
-    if (blocks == 0) blocks = resident_blocks((const void*)k_walk_short<SM>, 256);
-    hipLaunchKernelGGL(k_walk_short<SM>, dim3(blocks), dim3(256), 0, stream, a);
+    static unsigned blocks[2] = {0, 0};
+    const bool c = SM > 0 && short_compact(a);
+    const void* kern = c ? (const void*)k_walk_short<SM, true> : (const void*)k_walk_short<SM, false>;
+    if (blocks[c] == 0) blocks[c] = resident_blocks(kern, 256);
+    if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c]), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks[c]), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -273,7 +273,7 @@ def test_snapshot_matches_oracle_avg():
 def _host_records(req, n_rules, max_batch):
     kbits = max(1, int(n_rules).bit_length())
     ibits = int(max_batch - 1).bit_length()
-    abits = 64 - kbits - ibits
+    abits = min(8, 64 - kbits - ibits)  # acquire field: 7 bits + prio, larger acquires escape to the request
     key = (req["key"] & abi.KEY_INDEX).astype(np.uint64)
     bad = (key == abi.KEY_BAD) | (req["acquire"] <= 0)
     norule = (~bad) & (key >= n_rules)
