@@ -411,8 +411,16 @@ int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_re
  * req/out are HOST memory and must stay untouched until the ticket completes; allocate them with sg_host_alloc
  * (pinned) for the copies to run asynchronously. sg_flow_poll: 1 done and OK, 0 still running, < 0 that batch's
  * error (the batch was rejected, as sg_flow_decide_batch would); sg_flow_wait blocks and returns SG_OK or that
- * error. Every other call on the handle first completes the batches in flight. Ticket 0 (empty batch) is done. */
+ * error. Every other call on the handle first completes the batches in flight. Ticket 0 (empty batch) is done.
+ * Batches in flight are pipelined on the device: the front half of batch i+1 (validation, sort by flowId,
+ * segment lists) runs beside the walkers of batch i, two batch workspaces alternating; a batch that fails the
+ * cross-batch time check is still rejected as a whole (checked before its walkers). */
 int   sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket);
+/* The same pipeline for DEVICE buffers (ClusterFlowChecker over HBM-resident batches back to back: the
+ * DefaultTokenService request loop at full rate): enqueues the batch and returns a ticket for
+ * sg_flow_poll / sg_flow_wait. req/out must stay allocated and untouched until the ticket completes (each batch
+ * in flight needs its own out buffer); up to 4 batches in flight (a 5th enqueue first completes the oldest). */
+int   sg_flow_enqueue(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket);
 int   sg_flow_poll(sg_handle* h, uint64_t ticket);
 int   sg_flow_wait(sg_handle* h, uint64_t ticket);
 void* sg_host_alloc(sg_handle* h, uint64_t bytes);   /* pinned (page-locked) host memory, NULL on failure */
@@ -446,6 +454,9 @@ int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap)
 /* Same into DEVICE memory (2*n_rules doubles, {passQps, blockQps} per flowId), asynchronous on `stream`:
  * the per-GPU input of the node-wide RCCL metric rollup. */
 int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, void* stream);
+/* sg_snapshot_metrics_device ordered after every batch enqueued so far on the pipeline (sg_flow_enqueue /
+ * sg_flow_submit), without draining it: completes with the returned ticket (sg_flow_poll / sg_flow_wait). */
+int sg_snapshot_metrics_enqueue(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, uint64_t* ticket);
 
 /* Hot-parameter rules (replaces ParamFlowRuleManager.loadRules → ParameterMetric maps). A reload starts
  * every rule's value table empty. Hot items of a rule may be given in any order. */

@@ -17,6 +17,7 @@
 using namespace sg;
 
 constexpr int kAsyncSlots = 3;  // batches of one handle in flight on the host pipeline
+constexpr int kDevSlots = 4;    // device-buffer batches of one handle in flight (sg_flow_enqueue)
 
 struct sg_handle {
     int device = 0;
@@ -208,6 +209,38 @@ struct sg_handle {
     sg_batch_stats stats{};
     hipStream_t aux = nullptr;        // second stream: the long-segment walker runs beside the short one
     hipEvent_t fork = nullptr, join = nullptr;
+    // Pipelined flow batches (sg_flow_enqueue, sg_flow_submit): the front half of a batch (validation, sort,
+    // segments) runs on s_front while the previous batch's walkers run on s_back. Two workspaces alternate:
+    // workspace 0 is the handle's own batch buffers above, workspace 1 (pws) is allocated on first use.
+    struct FlowWs {
+        uint64_t* rec = nullptr;
+        uint64_t* rec_sorted = nullptr;
+        uint32_t* hist = nullptr;
+        uint32_t* bnd = nullptr;
+        int64_t* p0 = nullptr;
+        uint32_t* np = nullptr;
+        int* err = nullptr;
+        uint32_t* long_list = nullptr;
+        uint32_t* long_key = nullptr;
+        uint32_t* long_pend = nullptr;
+        uint32_t* short_list = nullptr;
+        uint32_t* short_key = nullptr;
+        uint32_t* counts = nullptr;   // [1 + kClasses]: long count, short counts per class
+        uint4* skips = nullptr;
+        uint32_t* skip_count = nullptr;
+        uint32_t* seg_end = nullptr;  // [K]
+    };
+    FlowWs pws{};
+    uint32_t pws_segcap = 0;
+    hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
+    hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
+    uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
+    struct DevTicket {                // sg_flow_enqueue batches in flight
+        uint64_t ticket = 0;
+        int* h_err = nullptr;         // pinned
+        hipEvent_t done = nullptr;
+    };
+    DevTicket dev[kDevSlots];
 };
 
 namespace {
@@ -422,6 +455,38 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
 void sg_destroy(sg_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    {
+        auto& w = h->pws;
+        if (h->s_back) (void)hipStreamSynchronize(h->s_back);
+        dfree(w.rec);
+        dfree(w.rec_sorted);
+        dfree(w.hist);
+        dfree(w.bnd);
+        dfree(w.p0);
+        dfree(w.np);
+        dfree(w.err);
+        dfree(w.long_list);
+        dfree(w.long_key);
+        dfree(w.long_pend);
+        dfree(w.short_list);
+        dfree(w.short_key);
+        dfree(w.counts);
+        dfree(w.skips);
+        dfree(w.skip_count);
+        dfree(w.seg_end);
+        for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2})
+            if (*st) (void)hipStreamDestroy(*st);
+        for (int x = 0; x < 2; ++x) {
+            if (h->front_done[x]) (void)hipEventDestroy(h->front_done[x]);
+            if (h->back_done[x]) (void)hipEventDestroy(h->back_done[x]);
+        }
+        if (h->pfork) (void)hipEventDestroy(h->pfork);
+        if (h->pjoin) (void)hipEventDestroy(h->pjoin);
+        for (auto& d : h->dev) {
+            if (d.done) (void)hipEventDestroy(d.done);
+            if (d.h_err) (void)hipHostFree(d.h_err);
+        }
+    }
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
@@ -802,22 +867,73 @@ int flow_status(sg_handle* h, int err) {
     return SG_OK;
 }
 
-// Enqueue one batch's whole pipeline on `stream` (req/out device-resident); its error flags land in the pinned
-// word err_dst when the stream reaches the end. Stats events only for the synchronous call.
-int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipStream_t stream, int* err_dst,
-                 bool stats) {
-    if (h->K == 0 && h->kbits == 0) {
-        int rc = layout_records(h);
-        if (rc) return rc;
-    }
+// Workspace 0: the handle's own batch buffers.
+void main_ws(sg_handle* h, sg_handle::FlowWs& w) {
+    w.rec = h->d_rec;
+    w.rec_sorted = h->d_rec_sorted;
+    w.hist = h->d_hist;
+    w.bnd = h->d_bnd;
+    w.p0 = h->d_p0;
+    w.np = h->d_np;
+    w.err = h->d_err;
+    w.long_list = h->d_long_list;
+    w.long_key = h->d_long_key;
+    w.long_pend = h->d_long_pend;
+    w.short_list = h->d_short_list;
+    w.short_key = h->d_short_key;
+    w.counts = h->d_long_count;
+    w.skips = h->d_skips;
+    w.skip_count = h->d_skip_count;
+    w.seg_end = h->d_seg_end;
+}
 
+// Workspace 1 and the pipeline's streams / events, allocated on first pipelined batch (seg_end grows with K).
+int pipe_setup(sg_handle* h) {
+    auto& w = h->pws;
+    const uint64_t n = h->cfg.max_batch;
+    if (!w.rec) {
+        uint64_t short_words = 0;
+        for (int c = 0; c < kClasses; ++c) short_words += (c == 0 ? n : n / (kClassMax[c - 1] + 1)) + 1;
+        if (hipMalloc(&w.rec, (n + kRecW) * 8) != hipSuccess || hipMalloc(&w.rec_sorted, (n + kRecW) * 8) != hipSuccess ||
+            hipMalloc(&w.hist, sizeof(uint32_t) * radix_hist_words(n)) != hipSuccess ||
+            hipMalloc(&w.bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess ||
+            hipMalloc(&w.p0, sizeof(int64_t) * kMaxWl) != hipSuccess ||
+            hipMalloc(&w.np, sizeof(uint32_t) * kMaxWl) != hipSuccess || hipMalloc(&w.err, sizeof(int)) != hipSuccess ||
+            hipMalloc(&w.long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+            hipMalloc(&w.long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+            hipMalloc(&w.long_pend, sizeof(uint32_t) * (size_t)kLongTab * kLongPeriods) != hipSuccess ||
+            hipMalloc(&w.short_list, sizeof(uint32_t) * short_words) != hipSuccess ||
+            hipMalloc(&w.short_key, sizeof(uint32_t) * short_words) != hipSuccess ||
+            hipMalloc(&w.counts, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&w.skips, sizeof(uint4) * (2 * n / kSkipMin + 1)) != hipSuccess ||
+            hipMalloc(&w.skip_count, sizeof(uint32_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "pipeline workspace");
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_front, hipStreamNonBlocking));
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking));
+        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_aux2, hipStreamNonBlocking));
+        for (int x = 0; x < 2; ++x) {
+            HIP_TRY(h, hipEventCreateWithFlags(&h->front_done[x], hipEventDisableTiming));
+            HIP_TRY(h, hipEventCreateWithFlags(&h->back_done[x], hipEventDisableTiming));
+        }
+        HIP_TRY(h, hipEventCreateWithFlags(&h->pfork, hipEventDisableTiming));
+        HIP_TRY(h, hipEventCreateWithFlags(&h->pjoin, hipEventDisableTiming));
+    }
+    if (h->pws_segcap < h->K) {
+        dfree(w.seg_end);
+        if (hipMalloc(&w.seg_end, sizeof(uint32_t) * (h->K + 1)) != hipSuccess) return fail(h, SG_E_NOMEM, "pipeline workspace");
+        h->pws_segcap = h->K + 1;
+    }
+    return SG_OK;
+}
+
+BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req, uint64_t n, sg_result* out) {
     BatchArgs a{};
     a.req = req;
     a.out = out;
     a.n = n;
-    a.rec = h->d_rec;
-    a.rec_sorted = h->d_rec_sorted;
-    a.hist0 = h->n_lim > 0 ? nullptr : h->d_hist;  // the limiter pre-pass rewrites records after k_prep
+    a.rec = w.rec;
+    a.rec_sorted = w.rec_sorted;
+    a.hist0 = h->n_lim > 0 ? nullptr : w.hist;  // the limiter pre-pass rewrites records after k_prep
     a.kshift = 64 - h->kbits;
     a.abits = h->abits;
     a.imask = (h->ibits >= 64) ? ~0ull : ((1ull << h->ibits) - 1);
@@ -827,26 +943,27 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
     a.rules = h->d_rules;
     a.ring = h->d_ring;
     a.occ = h->d_occ;
-    a.seg_end = h->d_seg_end;
+    a.seg_end = w.seg_end;
     a.stride = h->stride;
     a.max_occ_ratio = h->cfg.max_occupy_ratio;
     a.n_wl = h->n_wl;
     std::memcpy(a.wl, h->wl, sizeof(a.wl));
-    a.bnd = h->d_bnd;
-    a.p0 = h->d_p0;
-    a.np = h->d_np;
-    a.err = h->d_err;
+    a.bnd = w.bnd;
+    a.p0 = w.p0;
+    a.np = w.np;
+    a.err = w.err;
     a.last_ts = h->d_last_ts;
-    a.long_list = h->d_long_list;
-    a.long_count = h->d_long_count;
-    a.short_list = h->d_short_list;
-    a.short_key = h->d_short_key;
-    a.long_key = h->d_long_key;
-    a.long_pend = h->d_long_pend;
-    a.short_count = h->d_long_count + 1;
+    a.check_last = 1;
+    a.long_list = w.long_list;
+    a.long_count = w.counts;
+    a.short_list = w.short_list;
+    a.short_key = w.short_key;
+    a.long_key = w.long_key;
+    a.long_pend = w.long_pend;
+    a.short_count = w.counts + 1;
     for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
-    a.skips = h->d_skips;
-    a.skip_count = h->d_skip_count;
+    a.skips = w.skips;
+    a.skip_count = w.skip_count;
     a.dbg = h->dbg;
     a.generic_walker = (h->cfg.flags & SG_FLAG_RING_REREAD) != 0;
     a.narrow = h->wide_seen ? 0 : 1;
@@ -854,11 +971,17 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
     a.skip_cap = (uint32_t)(2 * h->cfg.max_batch / kSkipMin + 1);
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
                   : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : h->short_max;
+    return a;
+}
 
+// Front half of a batch on `stream`: validation and packed records (k_prep), the namespace limiter pre-pass,
+// the stable sort by flowId and the segment lists. Touches only the workspace, the caller's output (default
+// results) and the limiter state.
+int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, bool stats) {
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_skip_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(a.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(a.skip_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_prep(a, stream));
     if (h->n_lim > 0) {
         LimArgs L{};
@@ -867,7 +990,7 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
         std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
         L.rule_lim = h->d_rule_lim;
         L.slot = h->d_lim_slot;
-        const uint64_t tiles = n / 4096 + 1;
+        const uint64_t tiles = a.n / 4096 + 1;
         L.tile_tot = h->d_lim_tile;
         L.tile_off = h->d_lim_tile + tiles * kMaxLim;
         L.arrivals = h->d_lim_period;
@@ -879,34 +1002,96 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
-        HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, a.kshift, h->d_hist, &sorted, stream, 64,
-                                      a.hist0 != nullptr));
+        HIP_TRY(h, radix_sort_records(a.rec, a.rec_sorted, a.n, a.kshift, hist, &sorted, stream, 64, a.hist0 != nullptr));
         a.rec_sorted = sorted;
-        h->last_sorted = sorted;
+        if (a.rec == h->d_rec) h->last_sorted = sorted;
     }
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg(a, stream));
-    // fork: long segments on the aux stream, short ones on the caller's stream, then join
+    return SG_OK;
+}
+
+// Back half on `stream` (after the front half and after the previous batch's back half): the cross-batch time
+// check (when the front half skipped it), both walkers (long segments on `aux`), skipped BLOCK counts, the
+// handle's last timestamp; the error word lands in the pinned err_dst.
+int flow_back(sg_handle* h, const BatchArgs& a, hipStream_t stream, hipStream_t aux, hipEvent_t fork, hipEvent_t join,
+              int* err_dst, bool stats) {
+    if (!a.check_last) HIP_TRY(h, launch_check_last(a, stream));
     if (h->dbg & 2) {
         HIP_TRY(h, launch_walk_long(a, stream));
         HIP_TRY(h, launch_walk_short(a, stream));
     } else {
-        HIP_TRY(h, hipEventRecord(h->fork, stream));
-        HIP_TRY(h, hipStreamWaitEvent(h->aux, h->fork, 0));
-        HIP_TRY(h, launch_walk_long(a, h->aux));
+        HIP_TRY(h, hipEventRecord(fork, stream));
+        HIP_TRY(h, hipStreamWaitEvent(aux, fork, 0));
+        HIP_TRY(h, launch_walk_long(a, aux));
         HIP_TRY(h, launch_walk_short(a, stream));
-        HIP_TRY(h, hipEventRecord(h->join, h->aux));
-        HIP_TRY(h, hipStreamWaitEvent(stream, h->join, 0));
+        HIP_TRY(h, hipEventRecord(join, aux));
+        HIP_TRY(h, hipStreamWaitEvent(stream, join, 0));
     }
     HIP_TRY(h, launch_skip_apply(a, stream));
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, launch_finish(a, stream));
-    HIP_TRY(h, hipMemcpyAsync(err_dst, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipMemcpyAsync(err_dst, a.err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (stats) {
-        HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, h->d_skip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_long, a.long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, a.skip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipEventRecord(h->ev[4], stream));
     }
+    return SG_OK;
+}
+
+int ensure_layout(sg_handle* h) {
+    if (h->K == 0 && h->kbits == 0) return layout_records(h);
+    return SG_OK;
+}
+
+// Enqueue one batch's whole pipeline on `stream` with workspace 0 (req/out device-resident); its error flags
+// land in the pinned word err_dst when the stream reaches the end. Stats events only for the synchronous call.
+int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipStream_t stream, int* err_dst,
+                 bool stats) {
+    int rc = ensure_layout(h);
+    if (rc) return rc;
+    sg_handle::FlowWs w;
+    main_ws(h, w);
+    BatchArgs a = flow_args(h, w, req, n, out);
+    rc = flow_front(h, a, w.hist, stream, stats);
+    if (rc) return rc;
+    return flow_back(h, a, stream, h->aux, h->fork, h->join, err_dst, stats);
+}
+
+// Enqueue one batch on the pipeline: its front half waits for `after` (its input's arrival, may be null) and for
+// the walkers of the batch two back (same workspace); its back half follows its front half and the previous
+// batch's back half. With namespace limiters the front half also waits for the previous back half (the limiter
+// pre-pass must see only accepted batches, so the cross-batch time check stays in k_prep). Returns the event
+// that marks the batch's completion through *done (the back half's end, recorded on s_back).
+int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipEvent_t after, int* err_dst,
+                           hipEvent_t done) {
+    int rc = ensure_layout(h);
+    if (rc) return rc;
+    rc = pipe_setup(h);
+    if (rc) return rc;
+    const int x = (int)(h->pipe_seq & 1);
+    const int xp = x ^ 1;
+    const bool first = h->pipe_seq == 0;
+    sg_handle::FlowWs w = h->pws;
+    if (x == 0) main_ws(h, w);
+    BatchArgs a = flow_args(h, w, req, n, out);
+    if (after) HIP_TRY(h, hipStreamWaitEvent(h->s_front, after, 0));
+    if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
+    if (h->n_lim > 0) {
+        if (!first) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[xp], 0));
+    } else {
+        a.check_last = 0;  // checked by the back half, after the previous batch has advanced last_ts
+    }
+    rc = flow_front(h, a, w.hist, h->s_front, false);
+    if (rc) return rc;
+    HIP_TRY(h, hipEventRecord(h->front_done[x], h->s_front));
+    HIP_TRY(h, hipStreamWaitEvent(h->s_back, h->front_done[x], 0));
+    rc = flow_back(h, a, h->s_back, h->s_aux2, h->pfork, h->pjoin, err_dst, false);
+    if (rc) return rc;
+    HIP_TRY(h, hipEventRecord(h->back_done[x], h->s_back));
+    if (done) HIP_TRY(h, hipEventRecord(done, h->s_back));
+    h->pipe_seq++;
     return SG_OK;
 }
 
@@ -919,6 +1104,13 @@ int drain_async(sg_handle* h) {
         h->finished[sl.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *sl.h_err);
         sl.ticket = 0;
     }
+    for (auto& d : h->dev) {
+        if (!d.ticket) continue;
+        hipError_t e = hipEventSynchronize(d.done);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        d.ticket = 0;
+    }
+    if (h->s_back) (void)hipStreamSynchronize(h->s_back);  // workspace 0 is the synchronous path's too
     return SG_OK;
 }
 
@@ -993,20 +1185,43 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
         h->finished[sl.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *sl.h_err);
         sl.ticket = 0;
     }
-    // H2D of this batch overlaps the previous batch's compute; compute stays in submission order (the
-    // batches are time-ordered and share the window state); D2H overlaps the next batch's compute
+    // H2D of this batch overlaps the previous batches' compute; the batch's front half (sort) overlaps the
+    // previous batch's walkers, the walkers stay in submission order (the batches are time-ordered and share the
+    // window state); D2H overlaps the next batch's compute
     HIP_TRY(h, hipMemcpyAsync(sl.d_req, req, sizeof(sg_req) * n, hipMemcpyHostToDevice, h->s_in));
     HIP_TRY(h, hipEventRecord(sl.h2d, h->s_in));
-    HIP_TRY(h, hipStreamWaitEvent(h->s_comp, sl.h2d, 0));
-    int rc = enqueue_flow(h, sl.d_req, n, sl.d_out, h->s_comp, sl.h_err, false);
+    int rc = enqueue_flow_pipelined(h, sl.d_req, n, sl.d_out, sl.h2d, sl.h_err, sl.comp);
     if (rc) return rc;
-    HIP_TRY(h, hipEventRecord(sl.comp, h->s_comp));
     HIP_TRY(h, hipStreamWaitEvent(h->s_out, sl.comp, 0));
     HIP_TRY(h, hipMemcpyAsync(out, sl.d_out, sizeof(sg_result) * n, hipMemcpyDeviceToHost, h->s_out));
     HIP_TRY(h, hipEventRecord(sl.d2h, h->s_out));
     // (a slot is reused only after its batch completed: above, or when its ticket was collected)
     sl.ticket = h->next_ticket++;
     *ticket = sl.ticket;
+    return SG_OK;
+}
+
+int sg_flow_enqueue(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
+    if (!h || !ticket) return SG_E_INVAL;
+    *ticket = 0;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    sg_handle::DevTicket& d = h->dev[h->next_ticket % kDevSlots];
+    if (!d.done) {
+        if (hipHostMalloc(&d.h_err, sizeof(int)) != hipSuccess) return fail(h, SG_E_NOMEM, "pinned error word");
+        HIP_TRY(h, hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    }
+    if (d.ticket) {  // every slot in flight: complete the oldest (its status waits in `finished`)
+        hipError_t e = hipEventSynchronize(d.done);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        d.ticket = 0;
+    }
+    int rc = enqueue_flow_pipelined(h, req, n, out, nullptr, d.h_err, d.done);
+    if (rc) return rc;
+    d.ticket = h->next_ticket++;
+    *ticket = d.ticket;
     return SG_OK;
 }
 
@@ -1026,6 +1241,15 @@ static int collect(sg_handle* h, uint64_t ticket, bool block) {
         sl.ticket = 0;
         if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
         const int st = flow_status(h, *sl.h_err);
+        return st == SG_OK ? 1 : st;
+    }
+    for (auto& d : h->dev) {
+        if (d.ticket != ticket) continue;
+        hipError_t e = block ? hipEventSynchronize(d.done) : hipEventQuery(d.done);
+        if (e == hipErrorNotReady) return 0;
+        d.ticket = 0;
+        if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+        const int st = flow_status(h, *d.h_err);
         return st == SG_OK ? 1 : st;
     }
     return fail(h, SG_E_INVAL, "unknown or already collected ticket");
@@ -1122,6 +1346,33 @@ int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, ui
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
     HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
+    return SG_OK;
+}
+
+// The same snapshot ordered on the pipeline after every batch enqueued so far (sg_flow_enqueue / submit): the
+// node-wide rollup of one simulated second can run while the next second's batches are being decided.
+int sg_snapshot_metrics_enqueue(sg_handle* h, int64_t now_ms, double* out_dev, uint64_t cap, uint64_t* ticket) {
+    if (!h || !out_dev || !ticket || cap < 2ull * h->K) return SG_E_INVAL;
+    *ticket = 0;
+    if (h->K == 0) return SG_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    int rc = pipe_setup(h);
+    if (rc) return rc;
+    sg_handle::DevTicket& d = h->dev[h->next_ticket % kDevSlots];
+    if (!d.done) {
+        if (hipHostMalloc(&d.h_err, sizeof(int)) != hipSuccess) return fail(h, SG_E_NOMEM, "pinned error word");
+        HIP_TRY(h, hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    }
+    if (d.ticket) {
+        hipError_t e = hipEventSynchronize(d.done);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        d.ticket = 0;
+    }
+    *d.h_err = 0;
+    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, h->s_back));
+    HIP_TRY(h, hipEventRecord(d.done, h->s_back));
+    d.ticket = h->next_ticket++;
+    *ticket = d.ticket;
     return SG_OK;
 }
 

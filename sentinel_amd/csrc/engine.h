@@ -80,6 +80,7 @@ struct BatchArgs {
     uint32_t* np;        // [kMaxWl]: number of window periods the batch spans
     int* err;
     int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
+    int check_last;      // k_prep checks the first timestamp against last_ts (0: k_check_last does, pipelined)
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
     uint32_t* short_list; // segment starts walked one lane each, per length class (slices, see class_off)
@@ -519,6 +520,7 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
+hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         const sg_req r = a.req[i];
         const int64_t t = r.ts_ms;
         if (i == 0) {
-            if (t < 0 || t < *a.last_ts) atomicOr(a.err, kErrTime);
+            if (t < 0 || (a.check_last && t < *a.last_ts)) atomicOr(a.err, kErrTime);
             for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
         } else {
             const int64_t tp = a.req[i - 1].ts_ms;
@@ -1495,6 +1495,12 @@ __global__ void __launch_bounds__(256) k_skip_apply(BatchArgs a) {
     }
 }
 
+// The cross-batch half of k_prep's time check, for a batch whose front half ran before the previous batch
+// finished (pipelined): the first timestamp may not precede the last one of every earlier accepted batch.
+__global__ void k_check_last(BatchArgs a) {
+    if (a.n > 0 && a.req[0].ts_ms < *a.last_ts) atomicOr(a.err, kErrTime);
+}
+
 __global__ void k_finish(BatchArgs a) {
     if (*a.err == 0 && a.n > 0) *a.last_ts = a.req[a.n - 1].ts_ms;
 }
@@ -1622,6 +1628,11 @@ hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {
 
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_skip_apply, dim3(2048), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_check_last, dim3(1), dim3(1), 0, stream, a);
     return hipGetLastError();
 }
 

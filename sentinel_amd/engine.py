@@ -13,9 +13,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_load_flow_rules",
-           "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_poll", "sg_flow_wait",
+           "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_enqueue", "sg_flow_poll", "sg_flow_wait",
            "sg_host_alloc", "sg_host_free", "sg_enable_stats", "sg_get_stats",
-           "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_debug_copy", "sg_build_info",
+           "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_snapshot_metrics_enqueue", "sg_debug_copy", "sg_build_info",
            "sg_param_load_rules", "sg_param_decide_batch", "sg_param_decide_batch_host", "sg_param_read_state",
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
@@ -56,6 +56,7 @@ def load_library():
         "sg_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_flow_submit": (C.c_int, [vp, vp, u64, vp, C.POINTER(u64)]),
+        "sg_flow_enqueue": (C.c_int, [vp, vp, u64, vp, C.POINTER(u64)]),
         "sg_flow_poll": (C.c_int, [vp, u64]),
         "sg_flow_wait": (C.c_int, [vp, u64]),
         "sg_host_alloc": (vp, [vp, u64]),
@@ -67,6 +68,7 @@ def load_library():
         "sg_flow_import_state": (C.c_int, [vp, vp, u64, vp, u64]),
         "sg_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
         "sg_snapshot_metrics_device": (C.c_int, [vp, i64, vp, u64, vp]),
+        "sg_snapshot_metrics_enqueue": (C.c_int, [vp, i64, vp, u64, C.POINTER(u64)]),
         "sg_debug_copy": (C.c_int, [vp, C.c_int, vp, u64]),
         "sg_param_load_rules": (C.c_int, [vp, vp, u32, vp, u32]),
         "sg_param_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
@@ -207,6 +209,13 @@ class FlowEngine:
                                            C.byref(t)))
         return t.value
 
+    def enqueue_device(self, req_ptr: int, n: int, out_ptr: int) -> int:
+        """sg_flow_enqueue: a device-resident batch on the pipelined path (front half beside the previous batch's
+        walkers); returns the ticket for poll / wait. The buffers must stay untouched until it completes."""
+        t = C.c_uint64()
+        self._check(self._L.sg_flow_enqueue(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr), C.byref(t)))
+        return t.value
+
     def poll(self, ticket) -> bool:
         r = self._L.sg_flow_poll(self.h, ticket)
         if r < 0:
@@ -255,6 +264,13 @@ class FlowEngine:
         """{passQps, blockQps} per flowId into device memory at out_ptr (2*n_rules doubles)."""
         self._check(self._L.sg_snapshot_metrics_device(self.h, now_ms, C.c_void_p(out_ptr), 2 * n_rules,
                                                        C.c_void_p(stream_ptr)))
+
+    def snapshot_enqueue(self, now_ms, out_ptr, n_rules) -> int:
+        """{passQps, blockQps} per flowId into device memory at out_ptr, ordered after every batch enqueued so far
+        (sg_snapshot_metrics_enqueue); returns the ticket for wait."""
+        t = C.c_uint64()
+        self._check(self._L.sg_snapshot_metrics_enqueue(self.h, now_ms, C.c_void_p(out_ptr), 2 * n_rules, C.byref(t)))
+        return t.value
 
     def debug_copy(self, what, dtype, count):
         """Testing aid: an internal buffer of the last batch (see sg_debug_copy)."""

@@ -86,3 +86,92 @@ def test_other_calls_drain_the_pipeline():
     now = int(reqs[-1]["ts_ms"][-1]) + 1
     want = np.array([[ora.avg(k, now, abi.EV_PASS), ora.avg(k, now, abi.EV_BLOCK)] for k in range(len(wl.rules()))])
     assert np.array_equal(snap, want)
+
+
+def _dev(arr):
+    import torch
+    return torch.from_numpy(arr.view(np.uint8).copy()).to("cuda:0")
+
+
+def test_device_enqueue_pipelined_equal_oracle():
+    """sg_flow_enqueue: device batches back to back (more than the 4 slots), each batch's sort beside the previous
+    batch's walkers; decisions and the final window state equal the oracle's sequential replay."""
+    import torch
+    wl, eng, ora = _setup(seed=33)
+    nb = 9
+    reqs = [wl.requests(b) for b in range(nb)]
+    d_in = [_dev(r) for r in reqs]
+    d_out = [torch.empty(len(r) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0") for r in reqs]
+    torch.cuda.synchronize()
+    tickets = [eng.enqueue_device(i.data_ptr(), len(r), o.data_ptr()) for i, o, r in zip(d_in, d_out, reqs)]
+    for t in tickets:
+        eng.wait(t)
+    for b in range(nb):
+        got = d_out[b].cpu().numpy().view(abi.RES_DTYPE)
+        want = ora.decide(reqs[b])
+        assert np.array_equal(got, want), f"batch {b}: {(got != want).sum()} differ"
+    ring, occ = eng.export_state(len(wl.rules()))
+    ring_o, occ_o = ora.export_state(len(wl.rules()), ring.shape[1])
+    assert np.array_equal(ring, ring_o) and np.array_equal(occ, occ_o)
+
+
+def test_device_enqueue_cross_batch_time_check():
+    """A batch starting before the previous batch's last timestamp is rejected on its own ticket although its
+    front half ran before the previous batch finished; the batches around it decide as the oracle."""
+    import torch
+    from sentinel_amd.engine import EngineError
+    wl, eng, ora = _setup(seed=35)
+    r0, r1, r2 = wl.requests(0), wl.requests(1), wl.requests(2)
+    late = r0.copy()  # batch 0's timestamps again: older than batch 0's last
+    bufs = [(_dev(r), torch.empty(len(r) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0"))
+            for r in (r0, late, r1, r2)]
+    torch.cuda.synchronize()
+    t = [eng.enqueue_device(i.data_ptr(), len(i) // abi.REQ_DTYPE.itemsize, o.data_ptr()) for i, o in bufs]
+    eng.wait(t[0])
+    with pytest.raises(EngineError) as ei:
+        eng.wait(t[1])
+    assert ei.value.code == abi.SG_E_TIME
+    eng.wait(t[2])
+    eng.wait(t[3])
+    for (i, o), r in zip([bufs[0], bufs[2], bufs[3]], [r0, r1, r2]):
+        assert np.array_equal(o.cpu().numpy().view(abi.RES_DTYPE), ora.decide(r))
+
+
+def test_device_enqueue_with_limiter_and_sync_calls_between():
+    """Pipelined batches with a namespace limiter (front halves wait for the previous batch: the limiter pre-pass
+    sees accepted batches only) mixed with synchronous calls, which drain the pipeline first."""
+    import torch
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.engine import FlowEngine
+    from sentinel_amd.workload import ClusterWorkload
+    wl = ClusterWorkload(n_flows=2000, n_requests=60_000, seed=37, prio_frac=0.05)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = 20_000
+    ns["limiter_enabled"] = 1
+    eng = FlowEngine(device=0, max_batch=60_000)
+    eng.set_namespaces(ns)
+    eng.load_rules(wl.rules())
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(wl.rules())
+    reqs = [wl.requests(b) for b in range(6)]
+    outs = {}
+    pend = []
+    for b, r in enumerate(reqs):
+        if b == 3:  # synchronous call in between
+            outs[b] = eng.decide_host(r)
+            continue
+        i, o = _dev(r), torch.empty(len(r) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0")
+        pend.append((b, i, o, eng.enqueue_device(i.data_ptr(), len(r), o.data_ptr())))
+        if b == 2:
+            for bb, _, oo, t in pend:
+                eng.wait(t)
+                outs[bb] = oo.cpu().numpy().view(abi.RES_DTYPE)
+            pend = []
+    for bb, _, oo, t in pend:
+        eng.wait(t)
+        outs[bb] = oo.cpu().numpy().view(abi.RES_DTYPE)
+    for b, r in enumerate(reqs):
+        want = ora.decide(r)
+        assert np.array_equal(outs[b], want), f"batch {b}: {(outs[b] != want).sum()} differ"
