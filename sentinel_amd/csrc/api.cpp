@@ -35,7 +35,7 @@ struct sg_handle {
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
     Occ* d_occ = nullptr;
-    uint32_t* d_seg_end = nullptr;   // [K] end of each flowId's segment in the sorted records (k_seg)
+    uint32_t* d_seg_end = nullptr;   // [2K] end, then start (k_seg_mark) of each flowId's segment in the sorted records
 
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
@@ -51,6 +51,7 @@ struct sg_handle {
     uint32_t* d_long_count = nullptr;  // [4]: long count, short count, work cursors (long, short)
     uint32_t* d_short_list = nullptr;
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
+    uint32_t* d_short_end = nullptr;  // segment end of each d_short_list entry (cluster flow path)
     uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
     uint32_t* d_long_pend = nullptr;
     FidSlot* d_fid = nullptr;         // flowId → rule index (wire codec), 2^k slots
@@ -229,12 +230,16 @@ struct sg_handle {
         uint4* skips = nullptr;
         uint32_t* skip_count = nullptr;
         uint32_t* seg_end = nullptr;  // [K]
+        uint32_t* seg_start = nullptr;  // [K], all 0xFFFFFFFF between batches
+        uint32_t* short_end = nullptr;
     };
     FlowWs pws{};
     uint32_t pws_segcap = 0;
     hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
     uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
+    int front_eighths = 0;            // CU partition of the pipeline streams (see pipe_setup)
+    int walk_cus = 0;                 // CUs of the walkers' streams when partitioned (0 = all)
     struct DevTicket {                // sg_flow_enqueue batches in flight
         uint64_t ticket = 0;
         int* h_err = nullptr;         // pinned
@@ -423,7 +428,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
             off += (c == 0 ? n : n / (kClassMax[c - 1] + 1)) + 1;
         }
         if (hipMalloc(&h->d_short_list, sizeof(uint32_t) * off) != hipSuccess ||
-            hipMalloc(&h->d_short_key, sizeof(uint32_t) * off) != hipSuccess)
+            hipMalloc(&h->d_short_key, sizeof(uint32_t) * off) != hipSuccess ||
+            hipMalloc(&h->d_short_end, sizeof(uint32_t) * off) != hipSuccess)
             return bail(SG_E_NOMEM);
     }
     if (hipMalloc(&h->d_dbg, 32 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 32 * 8) != hipSuccess) return bail(SG_E_NOMEM);
@@ -470,6 +476,7 @@ void sg_destroy(sg_handle* h) {
         dfree(w.long_pend);
         dfree(w.short_list);
         dfree(w.short_key);
+        dfree(w.short_end);
         dfree(w.counts);
         dfree(w.skips);
         dfree(w.skip_count);
@@ -508,6 +515,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_long_count);
     dfree(h->d_short_list);
     dfree(h->d_short_key);
+    dfree(h->d_short_end);
     dfree(h->d_long_key);
     dfree(h->d_long_pend);
     dfree(h->d_fid);
@@ -724,7 +732,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     uint32_t* d_seg_end = nullptr;
     int32_t* d_src = nullptr;
     if (n) {
-        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * n) != hipSuccess ||
+        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * 2 * n) != hipSuccess ||
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
             dfree(d_rules);
@@ -734,6 +742,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
             dfree(d_src);
             return fail(h, SG_E_NOMEM, "rule state allocation failed");
         }
+        HIP_TRY(h, hipMemset(d_seg_end + n, 0xFF, sizeof(uint32_t) * n));  // no segment starts marked
         HIP_TRY(h, hipMemcpy(d_src, src.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, launch_init_state(d_ring, d_occ, n, stride, d_src, h->d_ring, h->d_occ, h->stride, 0));
         HIP_TRY(h, hipDeviceSynchronize());
@@ -885,6 +894,8 @@ void main_ws(sg_handle* h, sg_handle::FlowWs& w) {
     w.skips = h->d_skips;
     w.skip_count = h->d_skip_count;
     w.seg_end = h->d_seg_end;
+    w.seg_start = h->d_seg_end ? h->d_seg_end + h->K : nullptr;
+    w.short_end = h->d_short_end;
 }
 
 // Workspace 1 and the pipeline's streams / events, allocated on first pipelined batch (seg_end grows with K).
@@ -904,13 +915,36 @@ int pipe_setup(sg_handle* h) {
             hipMalloc(&w.long_pend, sizeof(uint32_t) * (size_t)kLongTab * kLongPeriods) != hipSuccess ||
             hipMalloc(&w.short_list, sizeof(uint32_t) * short_words) != hipSuccess ||
             hipMalloc(&w.short_key, sizeof(uint32_t) * short_words) != hipSuccess ||
+            hipMalloc(&w.short_end, sizeof(uint32_t) * short_words) != hipSuccess ||
             hipMalloc(&w.counts, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess ||
             hipMalloc(&w.skips, sizeof(uint4) * (2 * n / kSkipMin + 1)) != hipSuccess ||
             hipMalloc(&w.skip_count, sizeof(uint32_t)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "pipeline workspace");
-        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_front, hipStreamNonBlocking));
-        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking));
-        HIP_TRY(h, hipStreamCreateWithFlags(&h->s_aux2, hipStreamNonBlocking));
+        // CU partition between the halves (env SG_FRONT_EIGHTHS = k: the front half gets CUs i with i % 8 < k,
+        // the walkers the rest; 0 = no masks, both halves on every CU)
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
+        int k8 = h->front_eighths;
+        if (const char* e = std::getenv("SG_FRONT_EIGHTHS")) k8 = std::atoi(e);
+        if (k8 > 0 && k8 < 8 && cus >= 8) {
+            std::vector<uint32_t> fm((cus + 31) / 32, 0u), bm((cus + 31) / 32, 0u);
+            int nb = 0;
+            for (int i = 0; i < cus; ++i) {
+                if (i % 8 < k8) fm[i / 32] |= 1u << (i % 32);
+                else {
+                    bm[i / 32] |= 1u << (i % 32);
+                    ++nb;
+                }
+            }
+            HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_front, (uint32_t)fm.size(), fm.data()));
+            HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_back, (uint32_t)bm.size(), bm.data()));
+            HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_aux2, (uint32_t)bm.size(), bm.data()));
+            h->walk_cus = nb;
+        } else {
+            HIP_TRY(h, hipStreamCreateWithFlags(&h->s_front, hipStreamNonBlocking));
+            HIP_TRY(h, hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking));
+            HIP_TRY(h, hipStreamCreateWithFlags(&h->s_aux2, hipStreamNonBlocking));
+        }
         for (int x = 0; x < 2; ++x) {
             HIP_TRY(h, hipEventCreateWithFlags(&h->front_done[x], hipEventDisableTiming));
             HIP_TRY(h, hipEventCreateWithFlags(&h->back_done[x], hipEventDisableTiming));
@@ -920,9 +954,12 @@ int pipe_setup(sg_handle* h) {
     }
     if (h->pws_segcap < h->K) {
         dfree(w.seg_end);
-        if (hipMalloc(&w.seg_end, sizeof(uint32_t) * (h->K + 1)) != hipSuccess) return fail(h, SG_E_NOMEM, "pipeline workspace");
+        if (hipMalloc(&w.seg_end, sizeof(uint32_t) * 2 * (h->K + 1)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "pipeline workspace");
         h->pws_segcap = h->K + 1;
+        HIP_TRY(h, hipMemset(w.seg_end + h->pws_segcap, 0xFF, sizeof(uint32_t) * h->pws_segcap));
     }
+    w.seg_start = w.seg_end + h->pws_segcap;
     return SG_OK;
 }
 
@@ -934,6 +971,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.rec = w.rec;
     a.rec_sorted = w.rec_sorted;
     a.hist0 = h->n_lim > 0 ? nullptr : w.hist;  // the limiter pre-pass rewrites records after k_prep
+    a.hist0_bits = radix_digit_bits(h->kbits);
     a.kshift = 64 - h->kbits;
     a.abits = h->abits;
     a.imask = (h->ibits >= 64) ? ~0ull : ((1ull << h->ibits) - 1);
@@ -944,6 +982,8 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.ring = h->d_ring;
     a.occ = h->d_occ;
     a.seg_end = w.seg_end;
+    a.seg_start = w.seg_start;
+    a.short_end = w.short_end;
     a.stride = h->stride;
     a.max_occ_ratio = h->cfg.max_occupy_ratio;
     a.n_wl = h->n_wl;
@@ -954,6 +994,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.err = w.err;
     a.last_ts = h->d_last_ts;
     a.check_last = 1;
+    a.walk_cus = 0;
     a.long_list = w.long_list;
     a.long_count = w.counts;
     a.short_list = w.short_list;
@@ -1007,7 +1048,7 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
         if (a.rec == h->d_rec) h->last_sorted = sorted;
     }
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
-    HIP_TRY(h, launch_seg(a, stream));
+    HIP_TRY(h, launch_seg_flow(a, stream));
     return SG_OK;
 }
 
@@ -1087,6 +1128,7 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
     if (rc) return rc;
     HIP_TRY(h, hipEventRecord(h->front_done[x], h->s_front));
     HIP_TRY(h, hipStreamWaitEvent(h->s_back, h->front_done[x], 0));
+    a.walk_cus = h->walk_cus;
     rc = flow_back(h, a, h->s_back, h->s_aux2, h->pfork, h->pjoin, err_dst, false);
     if (rc) return rc;
     HIP_TRY(h, hipEventRecord(h->back_done[x], h->s_back));

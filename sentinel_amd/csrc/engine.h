@@ -58,6 +58,7 @@ struct BatchArgs {
     uint64_t n;
     uint64_t* rec;       // packed records, request order
     uint32_t* hist0;     // k_prep: per-tile histogram of the first sort digit (radix_hist layout), or nullptr
+    int hist0_bits;      // width of that digit (radix_digit_bits of the key width)
     uint64_t* rec_sorted;
     // record layout: [key : kbits][0 …][idx : ibits][acode : abits], acode = acquire << 1 | prio, abits <= 8;
     // with abits == 8 and ibits <= 24 the low 32 bits {idx, acode} are the compact record the short walker stages
@@ -81,6 +82,7 @@ struct BatchArgs {
     int* err;
     int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
     int check_last;      // k_prep checks the first timestamp against last_ts (0: k_check_last does, pipelined)
+    int walk_cus;        // CUs the walkers' stream may use (CU-masked pipeline streams), 0 = all
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
     uint32_t* short_list; // segment starts walked one lane each, per length class (slices, see class_off)
@@ -88,6 +90,8 @@ struct BatchArgs {
     uint32_t* short_key;   // flowId of each short_list entry (nullptr: not written)
     uint32_t* long_key;    // flowId of each long_list entry (nullptr: not written)
     uint32_t* seg_end;     // [K] end of each present key's segment in rec_sorted (nullptr: not written)
+    uint32_t* seg_start;   // [K] start of each present key's segment (k_seg_mark), 0xFFFFFFFF between batches
+    uint32_t* short_end;   // end of each short_list entry's segment (k_seg_classify)
     uint32_t* long_pend;   // [kLongTab][kLongPeriods]: position in rec_sorted where period q + 1 of long segment
                            // i begins (k_long_bounds; nullptr: the wave walker searches for it)
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
@@ -515,9 +519,11 @@ hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
+int radix_digit_bits(int bits);  // digit width radix_sort_records uses for `bits` key bits (8 or 10)
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);

@@ -22,6 +22,9 @@
 // with the reference's operation order and -ffp-contract=off (no FMA contraction).
 #include "engine.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace sg {
 
 // ----------------------------------------------------------------------------------------- helpers
@@ -105,11 +108,13 @@ constexpr int kPrepItems = 16;
 constexpr uint32_t kPrepTile = 256 * kPrepItems;
 
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
-    __shared__ uint32_t dcnt[256];
+    __shared__ uint32_t dcnt[1024];
     const uint64_t n = a.n;
     const int64_t t0 = a.req[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
-    if (a.hist0) dcnt[threadIdx.x] = 0;
+    const uint32_t dmask = (1u << a.hist0_bits) - 1u;
+    if (a.hist0)
+        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) dcnt[d] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kPrepTile;
 #pragma unroll 4
@@ -163,11 +168,11 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             store_result(a.out, (uint32_t)i, SG_STATUS_BLOCKED, 0, 0);  // walkers write only non-BLOCKED
         }
         a.rec[i] = rec;
-        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & 255u], 1u);
+        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
     }
     if (a.hist0) {
         __syncthreads();
-        a.hist0[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = dcnt[threadIdx.x];
+        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)blockIdx.x * (dmask + 1) + d] = dcnt[d];
     }
 }
 
@@ -786,6 +791,82 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
     }
 }
 
+// Cluster flow segments in two passes without length probes: k_seg_mark finds every flowId's first and last
+// record in the sorted batch (one coalesced read; a head writes seg_start of its key and seg_end of the key before
+// it), k_seg_classify walks the flowId range in order, turns each marked key into a list entry {start, end, key}
+// of its length class (or the long list) and clears the mark for the next batch. Both run whatever the batch's
+// error flags (the marks must be consumed); the walkers check them.
+__global__ void __launch_bounds__(256) k_seg_mark(BatchArgs a) {
+    const uint64_t n = a.n;
+    const int lane = lane_id();
+    for (uint64_t j0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); j0 < n; j0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t j = j0 + lane;
+        const uint32_t key = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
+        uint32_t kp = (uint32_t)__shfl_up((int)key, 1u, 64);
+        if (lane == 0) kp = j0 > 0 ? (uint32_t)(a.rec_sorted[j0 - 1] >> a.kshift) : 0xFFFFFFFFu;
+        if (j < n && key != kp) {
+            if (key < a.K) a.seg_start[key] = (uint32_t)j;
+            if (kp < a.K) a.seg_end[kp] = (uint32_t)j;
+        }
+        if (j == n - 1 && key < a.K) a.seg_end[key] = (uint32_t)n;
+    }
+}
+
+constexpr int kClsItems = 16;  // flowIds per thread of k_seg_classify
+
+__global__ void __launch_bounds__(256) k_seg_classify(BatchArgs a) {
+    constexpr int kL = kClasses + 1;  // lists 0..kClasses-1: short length classes, kClasses: long
+    __shared__ uint32_t cnt[kL], base[kL];
+    const int tid = threadIdx.x;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * 256 * kClsItems; k0 < a.K; k0 += (uint64_t)gridDim.x * 256 * kClsItems) {
+        if (tid < kL) cnt[tid] = 0;
+        __syncthreads();
+        uint32_t st[kClsItems], en[kClsItems], slot[kClsItems];
+#pragma unroll
+        for (int u = 0; u < kClsItems; ++u) {
+            const uint64_t k = k0 + (uint64_t)u * 256 + tid;
+            st[u] = k < a.K ? a.seg_start[k] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < kClsItems; ++u) {
+            const uint64_t k = k0 + (uint64_t)u * 256 + tid;
+            slot[u] = 0xFFFFFFFFu;
+            if (st[u] == 0xFFFFFFFFu) continue;
+            a.seg_start[k] = 0xFFFFFFFFu;
+            en[u] = a.seg_end[k];
+            const uint32_t len = en[u] - st[u];
+            uint32_t l = 0;
+#pragma unroll
+            for (int c = 0; c < kClasses - 1; ++c) l += len > kClassMax[c] ? 1u : 0u;
+            if (len > a.short_max) l = kClasses;
+            slot[u] = (l << 24) | atomicAdd(&cnt[l], 1u);
+        }
+        __syncthreads();
+        if (tid < kL) {
+            const uint32_t t = cnt[tid];
+            uint32_t* ctr = tid == kClasses ? a.long_count : a.short_count + tid;
+            base[tid] = t ? atomicAdd(ctr, t) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kClsItems; ++u) {
+            if (slot[u] == 0xFFFFFFFFu) continue;
+            const uint32_t k = (uint32_t)(k0 + (uint64_t)u * 256 + tid);
+            const uint32_t l = slot[u] >> 24, pos = base[l] + (slot[u] & 0xFFFFFFu);
+            if (l == (uint32_t)kClasses) {
+                a.long_list[pos] = st[u];
+                a.long_key[pos] = k;
+            } else {
+                const uint64_t q = a.class_off[l] + pos;
+                a.short_list[q] = st[u];
+                a.short_key[q] = k;
+                a.short_end[q] = en[u];
+            }
+        }
+        __syncthreads();  // cnt / base are reused by the next range
+    }
+}
+
 // Stage the batch's period tables in g_sbnd when they fit (else the cursors read a.bnd).
 __device__ __forceinline__ void stage_periods(const BatchArgs& a) {
     uint32_t tot = 0;
@@ -1258,7 +1339,7 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
     const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
     // group g: class (wave-uniform), this lane's list entry; inactive lanes of a class's last group repeat
     // the class's entry 0 (valid addresses)
-    auto desc = [&](uint32_t g, int& c, bool& act, uint32_t& s, uint32_t& k) {
+    auto desc = [&](uint32_t g, int& c, bool& act, uint32_t& s, uint32_t& k, uint32_t& e) {
         c = kClasses - 1;
         uint32_t g0 = 0;
         while (g >= grp_end[c]) {
@@ -1271,18 +1352,19 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         const uint64_t li = a.class_off[c] + (act ? i : 0u);
         s = a.short_list[li];
         k = a.short_key[li];
+        e = a.short_end[li];
     };
     int c_n;
     bool act_n;
-    uint32_t s_n, k_n;
-    desc(wave, c_n, act_n, s_n, k_n);
+    uint32_t s_n, k_n, e_n;
+    desc(wave, c_n, act_n, s_n, k_n, e_n);
     for (uint32_t g = wave; g < total; g += nwaves) {
         const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
         const int c = c_n;
         const bool act = act_n;
         const uint64_t s = s_n;
         const uint32_t k = k_n;
-        const uint64_t e = a.seg_end[k];
+        const uint64_t e = e_n;
         const Rule R = a.rules[k];
         const Occ occ = a.occ[k];
         // first window: the class's longest segment (<= 4, <= 16 records) or kRecW
@@ -1291,7 +1373,7 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         else if (c == 1) stage_records<kClassMax[1]>(a, wrecs, s);
         else stage_records<kRecW>(a, wrecs, s);
         // the next group's descriptors (unconditional: a conditional load would be copied, and wait, at the merge)
-        desc(min(g + nwaves, total - 1), c_n, act_n, s_n, k_n);
+        desc(min(g + nwaves, total - 1), c_n, act_n, s_n, k_n, e_n);
         {
             // ring gather: piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS},
             // 1: WAITING); slots past the handle's stride read slot 0 again (ignored: q >= S)
@@ -1585,20 +1667,35 @@ hipError_t launch_seg(const BatchArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-static unsigned resident_blocks(const void* kernel, int block) {
+hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_seg_mark, dim3(grid_for(a.n, 256 * 16, 8192)), dim3(256), 0, stream, a);
+    if (a.K) hipLaunchKernelGGL(k_seg_classify, dim3(grid_for(a.K, 256 * kClsItems, 4096)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+// Blocks of `kernel` resident at once on `cus` CUs (0: all of the device's).
+static unsigned resident_blocks(const void* kernel, int block, int cus_used) {
     int dev = 0, cus = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0);
-    return (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+    if (cus_used > 0 && cus_used < cus) cus = cus_used;
+    unsigned b = (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+    // env SG_WALK_PCT (tuning): persistent walker grids at this percentage of what is resident at once
+    if (const char* e = std::getenv("SG_WALK_PCT")) {
+        const long pct = std::strtol(e, nullptr, 10);
+        if (pct > 0 && pct < 100) b = std::max(1u, (unsigned)(b * pct / 100));
+    }
+    return b;
 }
 
 // Persistent walkers: at most as many blocks as fit on the chip at once (each wave loops over its queue).
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
     if (a.long_pend && a.long_key && a.seg_end) hipLaunchKernelGGL(k_long_bounds, dim3(1024), dim3(256), 0, stream, a);
-    static unsigned blocks = 0;
-    if (blocks == 0) blocks = resident_blocks((const void*)k_walk_long, 256);
-    hipLaunchKernelGGL(k_walk_long, dim3(blocks), dim3(256), 0, stream, a);
+    static unsigned blocks[2] = {0, 0};  // all CUs / the pipeline's walker CUs
+    const int m = a.walk_cus > 0 ? 1 : 0;
+    if (blocks[m] == 0) blocks[m] = resident_blocks((const void*)k_walk_long, 256, a.walk_cus);
+    hipLaunchKernelGGL(k_walk_long, dim3(blocks[m]), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -1607,12 +1704,13 @@ static bool short_compact(const BatchArgs& a) { return a.abits == 8 && a.imask <
 
 template <int SM>
 static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
-    static unsigned blocks[2] = {0, 0};
+    static unsigned blocks[2][2] = {{0, 0}, {0, 0}};  // [compact][all CUs / the pipeline's walker CUs]
     const bool c = SM > 0 && short_compact(a);
+    const int m = a.walk_cus > 0 ? 1 : 0;
     const void* kern = c ? (const void*)k_walk_short<SM, true> : (const void*)k_walk_short<SM, false>;
-    if (blocks[c] == 0) blocks[c] = resident_blocks(kern, 256);
-    if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c]), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks[c]), dim3(256), 0, stream, a);
+    if (blocks[c][m] == 0) blocks[c][m] = resident_blocks(kern, 256, a.walk_cus);
+    if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -1,18 +1,24 @@
 // sort.hip — stable LSD radix sort of the 64-bit request records by their key field.
 //
 // The walkers need each key's requests contiguous and still in (timestamp, arrival) order, i.e. a stable
-// partition by key. Records are sorted on bits [lo_bit, hi_bit) in 8-bit digits, reduce-then-scan per
+// partition by key. Records are sorted on bits [lo_bit, hi_bit) in 8-bit digits, or two 10-bit digits for
+// 17..20-bit keys (the C3 flowIds: one pass of traffic fewer than three 8-bit passes), reduce-then-scan per
 // pass (no inter-block look-back: the 8 XCDs' L2s are not coherent, so a chained scan pays an uncached
 // round trip per link — measured 149 µs per pass against 77 µs for this scheme):
-//   k_radix_hist     per 4096-record tile: digit histogram (LDS atomics), stored digit-major [bins][tiles]
-//   k_scan_*         exclusive scan of that histogram (the global position of each tile's digit run)
+//   k_radix_hist     per 4096-record tile: digit histogram (LDS atomics), one contiguous row per tile [tiles][bins]
+//                    (k_prep counts the first pass's row itself)
+//   k_colsum, k_chunkscan, k_rescan   exclusive scan of those rows in (digit, tile) order: the global start of
+//                    every tile's run of every digit, written over the rows in place
 //   k_radix_scatter  per tile: each wave ranks its contiguous 1024 records, 64 at a time, against a
 //                    wave-private running count per digit (match-any ballots give the rank among equal
 //                    digits of a round; no block barrier inside the loop), then the records are placed
 //                    digit-sorted in LDS and written in that order (consecutive lanes → consecutive addresses
-//                    of one digit's run: coalesced stores, no partial-line write amplification).
+//                    of one digit's run); tiles are dealt to XCDs in contiguous ranges, so the partial lines
+//                    two adjacent tiles share in a digit's run are completed in one L2.
 // Stability: waves in index order within a tile, rounds then lanes within a wave.
 #include "engine.h"
+
+#include <type_traits>
 
 namespace sg {
 
@@ -21,27 +27,37 @@ constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kRounds = 16;
 constexpr int kTile = kSortThreads * kRounds;  // 4096 records per tile
 constexpr int kWaveRecs = kTile / kSortWaves;  // 1024 contiguous records per wave
-constexpr int kBins = 256;                     // 8-bit digits; one digit per thread
-constexpr int kScanItems = 8;
-constexpr int kScanChunk = kSortThreads * kScanItems;  // 2048 counters per scan block
-static_assert(kBins == kSortThreads, "one digit per thread");
+constexpr int kMaxDigit = 10;                  // widest digit (1024 bins)
 
-// Lanes of this wave whose `digit` equals this lane's (8 ballots).
+// Lanes of this wave whose D-bit `digit` equals this lane's (D ballots).
+template <int D>
 __device__ __forceinline__ uint64_t match_digit(uint32_t digit) {
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < D; ++b) {
         const uint64_t m = __ballot((digit >> b) & 1u);
         peers &= ((digit >> b) & 1u) ? m : ~m;
     }
     return peers;
 }
 
+// XCD-aware tile order for the scatter: blocks are dealt round-robin over the 8 XCDs (observed dispatch, a speed
+// matter only), so block b takes tile (b % 8) * per + b / 8 and every XCD scatters a contiguous range of tiles.
+// Adjacent tiles' runs of one digit are adjacent in the output: their shared partial lines meet in one L2.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
+    const uint32_t per = (ntiles + 7) / 8;
+    return (b % 8) * per + b / 8;
+}
+
+template <int D>
 __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in, uint64_t n, int shift, uint32_t* hist,
                                                              uint32_t ntiles) {
+    constexpr int kBins = 1 << D;
+    constexpr int kPer = kBins / kSortThreads;
     __shared__ uint32_t cnt[kBins];
     const int tid = threadIdx.x;
-    cnt[tid] = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) cnt[tid + i * kSortThreads] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kTile;
     uint64_t rec[kRounds];
@@ -54,80 +70,110 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in,
     for (int r = 0; r < kRounds; ++r)
         if (base + (uint64_t)r * kSortThreads + tid < n) atomicAdd(&cnt[(uint32_t)(rec[r] >> shift) & (kBins - 1)], 1u);
     __syncthreads();
-    hist[(size_t)tid * ntiles + blockIdx.x] = cnt[tid];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) hist[(size_t)blockIdx.x * kBins + tid + i * kSortThreads] = cnt[tid + i * kSortThreads];
 }
 
-// Block-local exclusive scan of kScanChunk counters; writes the chunk total to sums[blockIdx.x].
-__global__ void __launch_bounds__(kSortThreads) k_scan_local(uint32_t* data, uint64_t n, uint32_t* sums) {
-    __shared__ uint32_t part[kSortThreads];
-    const int tid = threadIdx.x;
-    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + (uint64_t)tid * kScanItems;
-    uint32_t v[kScanItems];
-    uint32_t s = 0;
+// The per-tile histograms are stored tile-major (hist[t][d]: each tile writes and reads one contiguous row); the
+// scatter needs each (tile, digit) run's global start, the exclusive scan in (digit, tile) order. Three passes:
+// per-chunk column sums, one block scanning the chunks per digit and the digit totals, then each chunk rewrites
+// its rows in place as offsets.
+constexpr uint32_t kChunkTiles = 32;
+
+template <int D>
+__global__ void __launch_bounds__(kSortThreads) k_colsum(const uint32_t* hist, uint32_t ntiles, uint32_t* csum) {
+    constexpr int kBins = 1 << D;
+    constexpr int kPer = kBins / kSortThreads;
+    const uint32_t t0 = blockIdx.x * kChunkTiles, t1 = min(t0 + kChunkTiles, ntiles);
+    uint32_t acc[kPer];
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        v[i] = (base + i < n) ? data[base + i] : 0u;
-        s += v[i];
-    }
-    part[tid] = s;
-    __syncthreads();
-    for (int o = 1; o < kSortThreads; o <<= 1) {  // Hillis-Steele inclusive scan of per-thread sums
-        uint32_t x = tid >= o ? part[tid - o] : 0u;
-        __syncthreads();
-        part[tid] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[tid] - s;
+    for (int i = 0; i < kPer; ++i) acc[i] = 0;
+    for (uint32_t t = t0; t < t1; ++t)
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i) {
-        if (base + i < n) data[base + i] = run;
-        run += v[i];
-    }
-    if (tid == kSortThreads - 1) sums[blockIdx.x] = part[tid];
+        for (int i = 0; i < kPer; ++i) acc[i] += hist[(size_t)t * kBins + threadIdx.x + i * kSortThreads];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads] = acc[i];
 }
 
-// Single-block exclusive scan of the chunk totals (any count, carried across 256-wide steps).
-__global__ void __launch_bounds__(kSortThreads) k_scan_top(uint32_t* sums, uint32_t nb) {
-    __shared__ uint32_t part[kSortThreads];
-    __shared__ uint32_t carry;
-    const int tid = threadIdx.x;
-    if (tid == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < nb; b0 += kSortThreads) {
-        const uint32_t i = b0 + tid;
-        const uint32_t v = i < nb ? sums[i] : 0u;
-        part[tid] = v;
-        __syncthreads();
-        for (int o = 1; o < kSortThreads; o <<= 1) {
-            uint32_t x = tid >= o ? part[tid - o] : 0u;
-            __syncthreads();
-            part[tid] += x;
-            __syncthreads();
+// One block of kBins threads (thread = digit): exclusive scan of the chunk sums per digit, plus the base of the
+// digit (exclusive scan of the digit totals), written back into csum as each chunk's starting offsets.
+template <int D>
+__global__ void __launch_bounds__(1024) k_chunkscan(uint32_t* csum, uint32_t nchunks) {
+    constexpr int kBins = 1 << D;
+    __shared__ uint32_t wsum[kBins / 64];
+    const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
+    constexpr uint32_t kB = 16;  // chunks loaded before any is stored (the loads do not wait on each other)
+    uint32_t run = 0;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
+        uint32_t v[kB];
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u) v[u] = c0 + u < nchunks ? csum[(size_t)(c0 + u) * kBins + d] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u) {
+            if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = run;
+            run += v[u];
         }
-        const uint32_t c = carry;
-        if (i < nb) sums[i] = c + part[tid] - v;
-        __syncthreads();
-        if (tid == kSortThreads - 1) carry = c + part[tid];
-        __syncthreads();
+    }
+    uint32_t x = run;  // inclusive scan of the digit totals over the block
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t base = x - run;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
+        uint32_t v[kB];
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u) v[u] = c0 + u < nchunks ? csum[(size_t)(c0 + u) * kBins + d] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < kB; ++u)
+            if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = v[u] + base;
     }
 }
 
-__global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* in, uint64_t* out, uint64_t n, int shift,
-                                                                const uint32_t* hist, const uint32_t* sums,
-                                                                uint32_t ntiles) {
-    __shared__ uint64_t stage[kTile];
-    __shared__ uint32_t wcnt[kSortWaves][kBins];  // per-wave running digit count, then per-wave base
-    __shared__ uint32_t dstart[kBins];            // tile-local start of each digit's run
-    __shared__ uint32_t gbase[kBins];             // global start of each digit's run of this tile
-    __shared__ uint32_t wtot[kSortWaves];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    {
-        const uint64_t hi = (uint64_t)tid * ntiles + blockIdx.x;
-        gbase[tid] = hist[hi] + sums[hi / kScanChunk];
-    }
+template <int D>
+__global__ void __launch_bounds__(kSortThreads) k_rescan(uint32_t* hist, const uint32_t* csum, uint32_t ntiles) {
+    constexpr int kBins = 1 << D;
+    constexpr int kPer = kBins / kSortThreads;
+    const uint32_t t0 = blockIdx.x * kChunkTiles, t1 = min(t0 + kChunkTiles, ntiles);
+    uint32_t run[kPer];
 #pragma unroll
-    for (int w = 0; w < kSortWaves; ++w) wcnt[w][tid] = 0;
-    const uint64_t base = (uint64_t)blockIdx.x * kTile;
+    for (int i = 0; i < kPer; ++i) run[i] = csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads];
+    for (uint32_t t = t0; t < t1; ++t)
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            uint32_t* p = hist + (size_t)t * kBins + threadIdx.x + i * kSortThreads;
+            const uint32_t v = *p;
+            *p = run[i];
+            run[i] += v;
+        }
+}
+
+template <int D>
+__global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* in, uint64_t* out, uint64_t n, int shift,
+                                                                const uint32_t* hist, uint32_t ntiles) {
+    constexpr int kBins = 1 << D;
+    constexpr int kPer = kBins / kSortThreads;  // digits per thread
+    using Cnt = typename std::conditional<(D > 8), uint16_t, uint32_t>::type;  // wave counts <= 1024
+    __shared__ uint64_t stage[kTile];
+    __shared__ Cnt wcnt[kSortWaves][kBins];  // per-wave running digit count, then per-wave base
+    __shared__ uint32_t dstart[kBins];       // tile-local start of each digit's run
+    __shared__ uint32_t gbase[kBins];        // global start of each digit's run of this tile
+    __shared__ uint32_t wtot[kSortWaves];
+    const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
+    if (tile >= ntiles) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int d = tid + i * kSortThreads;
+        gbase[d] = hist[(size_t)tile * kBins + d];  // the tile's row of run offsets (k_rescan)
+#pragma unroll
+        for (int w = 0; w < kSortWaves; ++w) wcnt[w][d] = 0;
+    }
+    const uint64_t base = (uint64_t)tile * kTile;
     const uint64_t wbase = base + (uint64_t)wave * kWaveRecs;
     const uint64_t lt = (1ull << lane) - 1ull;
     uint64_t rec[kRounds];
@@ -143,22 +189,29 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     for (int r = 0; r < kRounds; ++r) {
         const bool valid = wbase + (uint64_t)r * 64 + lane < n;
         const uint32_t d = (uint32_t)(rec[r] >> shift) & (kBins - 1);
-        const uint64_t peers = match_digit(d) & __ballot(valid);
+        const uint64_t peers = match_digit<D>(d) & __ballot(valid);
         const uint32_t c = wcnt[wave][d];
         rank[r] = c + (uint32_t)__popcll(peers & lt);
-        if (valid && lane == __builtin_ctzll(peers)) wcnt[wave][d] = c + (uint32_t)__popcll(peers);
+        if (valid && lane == __builtin_ctzll(peers)) wcnt[wave][d] = (Cnt)(c + (uint32_t)__popcll(peers));
     }
     __syncthreads();
-    // 2. digit `tid`: per-wave bases, tile total, tile-local digit start (block scan over the digits)
+    // 2. digits tid*kPer .. +kPer-1: per-wave bases, tile totals, tile-local digit starts (block scan)
     {
-        uint32_t tot = 0;
+        uint32_t tot[kPer], sum = 0;
 #pragma unroll
-        for (int w = 0; w < kSortWaves; ++w) {
-            const uint32_t c = wcnt[w][tid];
-            wcnt[w][tid] = tot;
-            tot += c;
+        for (int i = 0; i < kPer; ++i) {
+            const int d = tid * kPer + i;
+            uint32_t t = 0;
+#pragma unroll
+            for (int w = 0; w < kSortWaves; ++w) {
+                const uint32_t c = wcnt[w][d];
+                wcnt[w][d] = (Cnt)t;
+                t += c;
+            }
+            tot[i] = t;
+            sum += t;
         }
-        uint32_t x = tot;
+        uint32_t x = sum;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
@@ -166,9 +219,13 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
         }
         if (lane == 63) wtot[wave] = x;
         __syncthreads();
-        uint32_t off = x - tot;
+        uint32_t off = x - sum;
         for (int w = 0; w < wave; ++w) off += wtot[w];
-        dstart[tid] = off;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            dstart[tid * kPer + i] = off;
+            off += tot[i];
+        }
     }
     __syncthreads();
     // 3. place the records digit-sorted in LDS
@@ -176,7 +233,7 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     for (int r = 0; r < kRounds; ++r) {
         if (wbase + (uint64_t)r * 64 + lane < n) {
             const uint32_t d = (uint32_t)(rec[r] >> shift) & (kBins - 1);
-            stage[dstart[d] + wcnt[wave][d] + rank[r]] = rec[r];
+            stage[dstart[d] + (uint32_t)wcnt[wave][d] + rank[r]] = rec[r];
         }
     }
     __syncthreads();
@@ -191,35 +248,42 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
 
 size_t radix_hist_words(uint64_t n) {
     const uint64_t ntiles = (n + kTile - 1) / kTile;
-    const uint64_t words = ntiles * kBins;
-    const uint64_t nb = (words + kScanChunk - 1) / kScanChunk;
-    return (size_t)(words + nb + 64);
+    const uint64_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    return (size_t)((ntiles + nchunks) * (1ull << kMaxDigit) + 64);
 }
 
+// Digit width of a sort over `bits` key bits: 8-bit digits, except 2 passes of 10 bits for 17..20 bits (one pass
+// of memory traffic fewer than three 8-bit passes).
+int radix_digit_bits(int bits) { return (bits > 16 && bits <= 20) ? 10 : 8; }
+
+template <int D>
 static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
                        bool hist_ready) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
-    const uint64_t words = (uint64_t)ntiles * kBins;
-    const uint32_t nb = (uint32_t)((words + kScanChunk - 1) / kScanChunk);
-    uint32_t* hist = hist_ws;
-    uint32_t* sums = hist_ws + words;
+    const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    uint32_t* hist = hist_ws;                                   // [ntiles][bins], then run offsets in place
+    uint32_t* csum = hist_ws + (size_t)ntiles * (1u << D);       // [nchunks][bins]
     if (!hist_ready)
-        hipLaunchKernelGGL(k_radix_hist, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
-    hipLaunchKernelGGL(k_scan_local, dim3(nb), dim3(kSortThreads), 0, stream, hist, words, sums);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kSortThreads), 0, stream, sums, nb);
-    hipLaunchKernelGGL(k_radix_scatter, dim3(ntiles), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, sums,
-                       ntiles);
+        hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
+    hipLaunchKernelGGL(k_colsum<D>, dim3(nchunks), dim3(kSortThreads), 0, stream, hist, ntiles, csum);
+    hipLaunchKernelGGL(k_chunkscan<D>, dim3(1), dim3(1u << D), 0, stream, csum, nchunks);
+    hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(kSortThreads), 0, stream, hist, csum, ntiles);
+    const uint32_t grid = 8 * ((ntiles + 7) / 8);  // xcd_tile: blocks past ntiles return at once
+    hipLaunchKernelGGL(k_radix_scatter<D>, dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, ntiles);
 }
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),
 // ping-ponging between a and b. Returns the buffer that holds the result through *result.
-// first_hist_ready: the first pass's per-tile histogram is already in hist_ws (k_prep counted it).
+// first_hist_ready: the first pass's per-tile histogram (radix_digit_bits wide) is already in hist_ws (k_prep).
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit, bool first_hist_ready) {
     uint64_t* src = a;
     uint64_t* dst = b;
-    for (int shift = lo_bit; shift < hi_bit && n > 0; shift += 8) {
-        radix_pass(src, dst, n, shift, hist_ws, stream, shift == lo_bit && first_hist_ready);
+    const int D = radix_digit_bits(hi_bit - lo_bit);
+    for (int shift = lo_bit; shift < hi_bit && n > 0; shift += D) {
+        const bool ready = shift == lo_bit && first_hist_ready;
+        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready);
+        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready);
         uint64_t* t = src;
         src = dst;
         dst = t;
