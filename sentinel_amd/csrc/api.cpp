@@ -34,8 +34,7 @@ struct sg_handle {
 
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
-    Occ* d_occ = nullptr;             // staging for reloads / imports / exports (canonical occupy counters: d_hot)
-    HotSlot* d_hot = nullptr;         // [K][kHotHdr + stride] read-optimised mirror (engine.h HotSlot)
+    Occ* d_occ = nullptr;
     uint32_t* d_seg_end = nullptr;   // [2K] end, then start (k_seg_mark) of each flowId's segment in the sorted records
 
     // batch workspace (sized for cfg.max_batch)
@@ -365,10 +364,6 @@ int upload_rule_table(sg_handle* h) {
         if (!(bound < 1073741824.0)) h->wide_seen = true;
     }
     if (h->K) HIP_TRY(h, hipMemcpy(h->d_rules, h->rule_tab.data(), sizeof(Rule) * h->K, hipMemcpyHostToDevice));
-    if (h->K && h->d_hot) {  // the hot blocks' rule headers follow (a rule load rebuilds the blocks afterwards)
-        HIP_TRY(h, launch_hot_rules(h->d_rules, h->K, h->d_hot, kHotHdr + h->stride, 0));
-        HIP_TRY(h, hipDeviceSynchronize());
-    }
     // limiter slot of each rule's namespace
     dfree(h->d_rule_lim);
     if (h->K) {
@@ -502,7 +497,6 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
-    dfree(h->d_hot);
     dfree(h->d_seg_end);
     dfree(h->d_rec);
     dfree(h->d_rec_sorted);
@@ -735,20 +729,12 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
     Occ* d_occ = nullptr;
-    HotSlot* d_hot = nullptr;
     uint32_t* d_seg_end = nullptr;
     int32_t* d_src = nullptr;
-    // the canonical occupy counters of the surviving flowIds live in the old hot blocks
-    if (h->d_hot && h->K) {
-        HIP_TRY(h, launch_hot_occ_out(h->d_hot, kHotHdr + h->stride, h->K, h->d_occ, 0));
-        HIP_TRY(h, hipDeviceSynchronize());
-    }
     if (n) {
         if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * 2 * n) != hipSuccess ||
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
-            hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess ||
-            hipMalloc(&d_hot, sizeof(HotSlot) * (size_t)n * (kHotHdr + stride)) != hipSuccess) {
-            dfree(d_hot);
+            hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
             dfree(d_rules);
             dfree(d_ring);
             dfree(d_occ);
@@ -776,12 +762,10 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     dfree(h->d_rules);
     dfree(h->d_ring);
     dfree(h->d_occ);
-    dfree(h->d_hot);
     dfree(h->d_seg_end);
     h->d_rules = d_rules;
     h->d_ring = d_ring;
     h->d_occ = d_occ;
-    h->d_hot = d_hot;
     h->d_seg_end = d_seg_end;
     h->rules.assign(rules, rules + n);
     h->rule_tab = tab;
@@ -793,12 +777,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     if (rc) return rc;
     rc = upload_fid_table(h);
     if (rc) return rc;
-    rc = upload_rule_table(h);
-    if (rc) return rc;
-    // hot blocks of the new rule set: rules, the remapped ring and occupy counters
-    HIP_TRY(h, launch_build_hot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, h->d_hot, 0));
-    HIP_TRY(h, hipDeviceSynchronize());
-    return SG_OK;
+    return upload_rule_table(h);
 }
 
 // flowId → rule index for the wire codec: open addressing, linear probing, load factor <= 1/2 (the same
@@ -1002,8 +981,6 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.rules = h->d_rules;
     a.ring = h->d_ring;
     a.occ = h->d_occ;
-    a.hot = h->d_hot;
-    a.hstride = kHotHdr + h->stride;
     a.seg_end = w.seg_end;
     a.seg_start = w.seg_start;
     a.short_end = w.short_end;
@@ -1072,7 +1049,6 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     }
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg_flow(a, stream));
-    HIP_TRY(h, launch_long_bounds(a, stream));
     return SG_OK;
 }
 
@@ -1353,7 +1329,7 @@ int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* cou
     std::vector<Bucket> b(S);
     HIP_TRY(h, hipMemcpy(b.data(), h->d_ring + (size_t)key * h->stride, sizeof(Bucket) * S, hipMemcpyDeviceToHost));
     Occ o;
-    HIP_TRY(h, hipMemcpy(&o, h->d_hot + (size_t)key * (kHotHdr + h->stride) + 1, sizeof(Occ), hipMemcpyDeviceToHost));
+    HIP_TRY(h, hipMemcpy(&o, h->d_occ + key, sizeof(Occ), hipMemcpyDeviceToHost));
     for (int j = 0; j < S; ++j) {
         starts[j] = b[j].start;
         for (int e = 0; e < SG_NUM_EVENTS; ++e) counters[j * SG_NUM_EVENTS + e] = b[j].start == INT64_MIN ? 0 : b[j].c[e];
@@ -1375,7 +1351,6 @@ int sg_flow_export_state(sg_handle* h, int64_t* ring, uint64_t ring_words, int64
     drain_async(h);
     static_assert(sizeof(Bucket) == 64 && sizeof(Occ) == 16, "export layout");
     HIP_TRY(h, hipMemcpy(ring, h->d_ring, rw * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(h, launch_hot_occ_out(h->d_hot, kHotHdr + h->stride, h->K, h->d_occ, 0));
     HIP_TRY(h, hipMemcpy(occ, h->d_occ, ow * 8, hipMemcpyDeviceToHost));
     return SG_OK;
 }
@@ -1390,8 +1365,6 @@ int sg_flow_import_state(sg_handle* h, const int64_t* ring, uint64_t ring_words,
     drain_async(h);
     HIP_TRY(h, hipMemcpy(h->d_ring, ring, rw * 8, hipMemcpyHostToDevice));
     HIP_TRY(h, hipMemcpy(h->d_occ, occ, ow * 8, hipMemcpyHostToDevice));
-    HIP_TRY(h, launch_build_hot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, h->d_hot, 0));
-    HIP_TRY(h, hipDeviceSynchronize());
     return SG_OK;
 }
 
@@ -1402,7 +1375,7 @@ int sg_snapshot_metrics(sg_handle* h, int64_t now_ms, double* out, uint64_t cap)
     drain_async(h);
     double* d_out = nullptr;
     HIP_TRY(h, hipMalloc(&d_out, sizeof(double) * 2 * h->K));
-    hipError_t e1 = launch_snapshot(h->d_rules, h->d_ring, h->d_hot, kHotHdr + h->stride, h->K, h->stride, now_ms, d_out, 0);
+    hipError_t e1 = launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, d_out, 0);
     hipError_t e2 = e1 == hipSuccess ? hipMemcpy(out, d_out, sizeof(double) * 2 * h->K, hipMemcpyDeviceToHost) : e1;
     (void)hipFree(d_out);
     if (e2 != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e2));
@@ -1414,7 +1387,7 @@ int sg_snapshot_metrics_device(sg_handle* h, int64_t now_ms, double* out_dev, ui
     if (h->K == 0) return SG_OK;
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
-    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_hot, kHotHdr + h->stride, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
+    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, (hipStream_t)stream));
     return SG_OK;
 }
 
@@ -1438,7 +1411,7 @@ int sg_snapshot_metrics_enqueue(sg_handle* h, int64_t now_ms, double* out_dev, u
         d.ticket = 0;
     }
     *d.h_err = 0;
-    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_hot, kHotHdr + h->stride, h->K, h->stride, now_ms, out_dev, h->s_back));
+    HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, h->s_back));
     HIP_TRY(h, hipEventRecord(d.done, h->s_back));
     d.ticket = h->next_ticket++;
     *ticket = d.ticket;

@@ -36,19 +36,6 @@ struct alignas(16) Occ {
     int64_t pass_req;
 };
 
-// Read-optimised mirror of a flowId's state, 32 B slots, 2 + stride of them per flowId (one contiguous block):
-// slot 0 = its Rule, slot 1 = its Occ (the canonical occupy counters), slot 2 + q = {start, PASS, WAITING} of
-// ring slot q (a copy of Bucket q's fields, written together with the Bucket). The short walker gathers a
-// flowId's whole window from this block (3 lines at stride 10 instead of the 10 Bucket lines + rule + occupy).
-struct alignas(32) HotSlot {
-    int64_t start;
-    int64_t pass;
-    int64_t wait;
-    int64_t pad;
-};
-static_assert(sizeof(HotSlot) == 32, "HotSlot layout");
-constexpr int kHotHdr = 2;  // header slots (Rule, Occ) before the ring slots
-
 constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
 constexpr int kShortMax = 256;            // default: segments longer than this are walked by a whole wave
@@ -84,9 +71,7 @@ struct BatchArgs {
     uint32_t K;          // number of rules
     const Rule* rules;
     Bucket* ring;        // [K][stride]
-    Occ* occ;            // [K] staging only (rule reloads, state import): the canonical counters are in hot
-    HotSlot* hot;        // [K][hstride]
-    int hstride;         // kHotHdr + stride
+    Occ* occ;            // [K]
     int stride;          // buckets per flowId (max sampleCount)
     double max_occ_ratio;
     int n_wl;
@@ -539,7 +524,6 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
                               uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
-hipError_t launch_long_bounds(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);
@@ -547,12 +531,8 @@ hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,
                              const Bucket* old_ring, const Occ* old_occ, int old_stride, hipStream_t stream);
-hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const HotSlot* hot, int hstride, uint32_t K, int stride,
+hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,
                            int64_t now, double* out, hipStream_t stream);
-hipError_t launch_build_hot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride, HotSlot* hot,
-                            hipStream_t stream);
-hipError_t launch_hot_rules(const Rule* rules, uint32_t K, HotSlot* hot, int hstride, hipStream_t stream);
-hipError_t launch_hot_occ_out(const HotSlot* hot, int hstride, uint32_t K, Occ* occ, hipStream_t stream);
 
 // ---- token-server wire codec (codec.hip) ----
 

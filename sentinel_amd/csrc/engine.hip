@@ -74,28 +74,6 @@ __device__ __forceinline__ void store_result(sg_result* out, uint32_t idx, int32
     out[idx] = r;
 }
 
-// The hot mirror (engine.h HotSlot): occupy counters in header slot 1, ring slot q's {start, PASS, WAITING}
-// in slot kHotHdr + q, written with the Bucket whenever a bucket closes.
-__device__ __forceinline__ HotSlot* hot_of(const BatchArgs& a, uint32_t k) { return a.hot + (size_t)k * a.hstride; }
-
-__device__ __forceinline__ Occ load_occ(const BatchArgs& a, uint32_t k) {
-    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(hot_of(a, k) + 1);
-    Occ o;
-    o.pass = (int64_t)v.x;
-    o.pass_req = (int64_t)v.y;
-    return o;
-}
-
-__device__ __forceinline__ void store_occ(const BatchArgs& a, uint32_t k, int64_t pass, int64_t pass_req) {
-    *reinterpret_cast<ulonglong2*>(hot_of(a, k) + 1) = make_ulonglong2((unsigned long long)pass, (unsigned long long)pass_req);
-}
-
-__device__ __forceinline__ void store_hot(const BatchArgs& a, uint32_t k, int q, int64_t start, const int64_t* c) {
-    ulonglong2* p = reinterpret_cast<ulonglong2*>(hot_of(a, k) + kHotHdr + q);
-    p[0] = make_ulonglong2((unsigned long long)start, (unsigned long long)c[SG_EV_PASS]);
-    p[1] = make_ulonglong2((unsigned long long)c[SG_EV_WAITING], 0ull);
-}
-
 struct Decoded {
     uint32_t idx;
     int64_t acq;
@@ -354,7 +332,7 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
     const int64_t P0 = g_p0[R.wl_idx];
     PeriodState ps;
     {
-        const Occ o = load_occ(a, k);
+        const Occ o = a.occ[k];
         ps.occ_pass = o.pass;
         ps.occ_req = o.pass_req;
     }
@@ -371,7 +349,6 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
                 ring[I].start = ws;
 #pragma unroll
                 for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[I].c[ev] = ps.cur[ev];
-                store_hot(a, k, I, ws, ps.cur);
             }
             pc.seek(q);
             open_period_serial(ps, ring, R, P0 + (int64_t)q, &I, &ws);
@@ -395,9 +372,11 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
         ring[I].start = ws;
 #pragma unroll
         for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[I].c[ev] = ps.cur[ev];
-        store_hot(a, k, I, ws, ps.cur);
     }
-    store_occ(a, k, ps.occ_pass, ps.occ_req);
+    Occ o;
+    o.pass = ps.occ_pass;
+    o.pass_req = ps.occ_req;
+    a.occ[k] = o;
     return opened;
 }
 
@@ -438,7 +417,7 @@ struct WaveWalker {
 #pragma unroll
             for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) c[ev] = ring[lane].c[ev];
         }
-        const Occ o = load_occ(a, k);
+        const Occ o = a.occ[k];
         ps.occ_pass = o.pass;
         ps.occ_req = o.pass_req;
 #pragma unroll
@@ -608,9 +587,13 @@ struct WaveWalker {
             ring[lane].start = st;
 #pragma unroll
             for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[lane].c[ev] = c[ev];
-            store_hot(a, k, lane, st, c);
         }
-        if (lane == 0) store_occ(a, k, ps.occ_pass, ps.occ_req);
+        if (lane == 0) {
+            Occ o;
+            o.pass = ps.occ_pass;
+            o.pass_req = ps.occ_req;
+            a.occ[k] = o;
+        }
     }
 };
 
@@ -1095,10 +1078,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                if (!(a.dbg & 512)) {
-                    store_bucket(ring + I, ws, ps.cur);
-                    store_hot(a, k, I, ws, ps.cur);
-                }
+                if (!(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
                 snap[I].st = (int32_t)(ws - T0);
                 snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
                 snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
@@ -1162,11 +1142,11 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     }
 
     if (act) {
-        if (I >= 0) {
-            store_bucket(ring + I, ws, ps.cur);
-            store_hot(a, k, I, ws, ps.cur);
-        }
-        store_occ(a, k, ps.occ_pass, ps.occ_req);
+        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        Occ o;
+        o.pass = ps.occ_pass;
+        o.pass_req = ps.occ_req;
+        a.occ[k] = o;
     }
 }
 
@@ -1258,10 +1238,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && !park && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                if (!(a.dbg & 512)) {  // (debug: stores off, to time the walk without them)
-                    store_bucket(ring + I, ws, ps.cur);
-                    store_hot(a, k, I, ws, ps.cur);
-                }
+                store_bucket(ring + I, ws, ps.cur);
                 snap[I].st = (int32_t)(ws - T0);
                 snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
                 snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
@@ -1309,7 +1286,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
                 ps.cur[SG_EV_PASS] += dn.acq;
                 ps.cur[SG_EV_PASS_REQUEST] += 1;
                 if (dn.prio) ps.cur[SG_EV_OCCUPIED_PASS] += dn.acq;
-                if (!(a.dbg & 256)) store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+                store_result(a.out, dn.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
             } else {
                 int32_t wait;
                 const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, dn.acq, dn.prio, &wait);
@@ -1320,11 +1297,11 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
         }
     }
     if (act) {
-        if (I >= 0) {
-            store_bucket(ring + I, ws, ps.cur);
-            store_hot(a, k, I, ws, ps.cur);
-        }
-        store_occ(a, k, ps.occ_pass, ps.occ_req);
+        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        Occ o;
+        o.pass = ps.occ_pass;
+        o.pass_req = ps.occ_req;
+        a.occ[k] = o;
     }
 }
 
@@ -1393,9 +1370,8 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         const uint64_t s = s_n;
         const uint32_t k = k_n;
         const uint64_t e = e_n;
-        // rule, occupy counters and ring slots from the flowId's hot block (3 lines at stride 10)
-        const Rule R = *reinterpret_cast<const Rule*>(hot_of(a, k));
-        const Occ occ = load_occ(a, k);
+        const Rule R = a.rules[k];
+        const Occ occ = a.occ[k];
         // first window: the class's longest segment (<= 4, <= 16 records) or kRecW
         const int rows = c == 0 ? (int)kClassMax[0] : c == 1 ? (int)kClassMax[1] : kRecW;
         if (c == 0) stage_records<kClassMax[0]>(a, wrecs, s);
@@ -1404,8 +1380,8 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         // the next group's descriptors (unconditional: a conditional load would be copied, and wait, at the merge)
         desc(min(g + nwaves, total - 1), c_n, act_n, s_n, k_n, e_n);
         {
-            // ring gather: piece t*64 + lane: hot block of lane j = piece / (2*SM), slot q, half (0: {start, PASS},
-            // 1: {WAITING, pad}); slots past the handle's stride read slot 0 again (ignored: q >= S)
+            // ring gather: piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS},
+            // 1: WAITING); slots past the handle's stride read slot 0 again (ignored: q >= S)
             // every piece is loaded before any is used (the scheduling barrier keeps the compiler from
             // interleaving the loads with their LDS writes, which serialised the gather into round trips)
             constexpr int kT = 2 * SM;
@@ -1419,7 +1395,7 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
                 const int q = (pc % kT) >> 1;
                 const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
                 const int qq = q < a.stride ? q : 0;
-                v[t] = *(reinterpret_cast<const ulonglong2*>(hot_of(a, kj) + kHotHdr + qq) + (pc & 1));
+                v[t] = *(reinterpret_cast<const ulonglong2*>(a.ring + (size_t)kj * a.stride + qq) + ((pc & 1) ? 3 : 0));
             }
             __builtin_amdgcn_sched_barrier(0);
             // every dword of every piece stays live until here: the allocator would otherwise reuse the unused
@@ -1431,7 +1407,7 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
                 const int pc = t * 64 + gl;
                 SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
                 if (pc & 1) {
-                    d.wait = (int32_t)v[t].x;
+                    d.wait = (int32_t)v[t].y;
                 } else {
                     d.st = snap_rel((int64_t)v[t].x, T0);
                     d.pass = (int32_t)v[t].y;
@@ -1500,7 +1476,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
             // 2. everything that depends on (s, k) only
             const uint64_t e = a.seg_end[k];
             const Rule R = a.rules[k];
-            const Occ occ = load_occ(a, k);
+            const Occ occ = a.occ[k];
             uint64_t buf[kBlk];
 #pragma unroll
             for (int u = 0; u < kBlk; ++u) buf[u] = a.rec_sorted[min(s + u, a.n - 1)];
@@ -1647,12 +1623,11 @@ __global__ void __launch_bounds__(256) k_init_state(Bucket* ring, Occ* occ, uint
 // ClusterMetric.getAvg(PASS) / getAvg(BLOCK) at `now` for every flowId, evaluated as if currentWindow(now)
 // had run (the stale slot reads as reset, plus the occupied transfer) without mutating the state
 // (ClusterMetricNodeGenerator.java:39-105 reads these per flowId).
-__global__ void __launch_bounds__(256) k_snapshot(const Rule* rules, const Bucket* ring, const HotSlot* hot, int hstride,
-                                                  uint32_t K, int stride, int64_t now, double* out) {
+__global__ void __launch_bounds__(256) k_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K,
+                                                  int stride, int64_t now, double* out) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
         const Rule R = rules[k];
         const Bucket* rg = ring + (size_t)k * stride;
-        const HotSlot oc = hot[(size_t)k * hstride + 1];  // {Occ.pass, Occ.pass_req}
         const int64_t P = now / R.wl;
         const int I = (int)(P % R.S);
         const int64_t ws = P * R.wl;
@@ -1663,8 +1638,8 @@ __global__ void __launch_bounds__(256) k_snapshot(const Rule* rules, const Bucke
                 if (s0 == ws) {
                     pass += rg[q].c[SG_EV_PASS];
                     block += rg[q].c[SG_EV_BLOCK];
-                } else if (s0 != INT64_MIN && s0 < ws && oc.pass > 0) {
-                    pass += oc.start;
+                } else if (s0 != INT64_MIN && s0 < ws && occ[k].pass_req > 0) {
+                    pass += occ[k].pass;
                 }
                 continue;
             }
@@ -1675,50 +1650,6 @@ __global__ void __launch_bounds__(256) k_snapshot(const Rule* rules, const Bucke
         }
         out[2 * (size_t)k] = (double)pass / R.isec;
         out[2 * (size_t)k + 1] = (double)block / R.isec;
-    }
-}
-
-// The hot blocks from the canonical arrays: rule, occupy counters, {start, PASS, WAITING} of every ring slot
-// (after a rule load / state import; the walkers keep them in step afterwards).
-__global__ void __launch_bounds__(256) k_build_hot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K,
-                                                   int stride, HotSlot* hot) {
-    const int hs = kHotHdr + stride;
-    const uint64_t total = (uint64_t)K * hs;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = (uint32_t)(i / hs);
-        const int q = (int)(i % hs);
-        HotSlot h;
-        if (q == 0) {
-            h = *reinterpret_cast<const HotSlot*>(rules + k);
-        } else if (q == 1) {
-            h.start = occ[k].pass;
-            h.pass = occ[k].pass_req;
-            h.wait = h.pad = 0;
-        } else {
-            const Bucket& b = ring[(size_t)k * stride + (q - kHotHdr)];
-            h.start = b.start;
-            h.pass = b.c[SG_EV_PASS];
-            h.wait = b.c[SG_EV_WAITING];
-            h.pad = 0;
-        }
-        hot[i] = h;
-    }
-}
-
-// Rule headers of the hot blocks after a threshold change (namespaces reloaded; the state stays).
-__global__ void __launch_bounds__(256) k_hot_rules(const Rule* rules, uint32_t K, HotSlot* hot, int hstride) {
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x)
-        hot[(size_t)k * hstride] = *reinterpret_cast<const HotSlot*>(rules + k);
-}
-
-// The canonical occupy counters (hot header slot 1) into an Occ array (state export, rule reload remap).
-__global__ void __launch_bounds__(256) k_hot_occ_out(const HotSlot* hot, int hstride, uint32_t K, Occ* occ) {
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
-        const HotSlot h = hot[(size_t)k * hstride + 1];
-        Occ o;
-        o.pass = h.start;
-        o.pass_req = h.pass;
-        occ[k] = o;
     }
 }
 
@@ -1764,14 +1695,8 @@ static unsigned resident_blocks(const void* kernel, int block, int cus_used) {
 }
 
 // Persistent walkers: at most as many blocks as fit on the chip at once (each wave loops over its queue).
-// Period ends of the long segments: part of the front half (it needs only the sorted records and the lists), so
-// the wave walker starts as soon as the back half does.
-hipError_t launch_long_bounds(const BatchArgs& a, hipStream_t stream) {
-    if (a.long_pend && a.long_key && a.seg_end) hipLaunchKernelGGL(k_long_bounds, dim3(1024), dim3(256), 0, stream, a);
-    return hipGetLastError();
-}
-
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
+    if (a.long_pend && a.long_key && a.seg_end) hipLaunchKernelGGL(k_long_bounds, dim3(1024), dim3(256), 0, stream, a);
     static unsigned blocks[2] = {0, 0};  // all CUs / the pipeline's walker CUs
     const int m = a.walk_cus > 0 ? 1 : 0;
     if (blocks[m] == 0) blocks[m] = resident_blocks((const void*)k_walk_long, 256, a.walk_cus);
@@ -1827,31 +1752,11 @@ hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, con
     return hipGetLastError();
 }
 
-hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const HotSlot* hot, int hstride, uint32_t K, int stride,
+hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,
                            int64_t now, double* out, hipStream_t stream) {
     if (K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_snapshot, dim3(grid_for(K, 256, 4096)), dim3(256), 0, stream, rules, ring, hot, hstride, K,
-                       stride, now, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_build_hot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride, HotSlot* hot,
-                            hipStream_t stream) {
-    if (K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_build_hot, dim3(grid_for((uint64_t)K * (kHotHdr + stride), 256, 8192)), dim3(256), 0, stream,
-                       rules, ring, occ, K, stride, hot);
-    return hipGetLastError();
-}
-
-hipError_t launch_hot_rules(const Rule* rules, uint32_t K, HotSlot* hot, int hstride, hipStream_t stream) {
-    if (K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hot_rules, dim3(grid_for(K, 256, 4096)), dim3(256), 0, stream, rules, K, hot, hstride);
-    return hipGetLastError();
-}
-
-hipError_t launch_hot_occ_out(const HotSlot* hot, int hstride, uint32_t K, Occ* occ, hipStream_t stream) {
-    if (K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hot_occ_out, dim3(grid_for(K, 256, 4096)), dim3(256), 0, stream, hot, hstride, K, occ);
+    hipLaunchKernelGGL(k_snapshot, dim3(grid_for(K, 256, 4096)), dim3(256), 0, stream, rules, ring, occ, K, stride,
+                       now, out);
     return hipGetLastError();
 }
 

@@ -10,7 +10,7 @@ import numpy as np
 from . import abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsentinel_gpu.so")
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsentinel_gpu.so")  # override: A/B tuning runs
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_enqueue", "sg_flow_poll", "sg_flow_wait",
