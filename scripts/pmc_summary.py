@@ -11,7 +11,8 @@ import os
 import sys
 from collections import defaultdict
 
-PIPELINE = ("k_prep", "k_seg", "k_lim_", "k_radix_", "k_scan_", "k_walk_", "k_skip_apply", "k_finish",
+PIPELINE = ("k_prep", "k_seg", "k_lim_", "k_radix_", "k_scan_", "k_colsum", "k_chunkscan", "k_rescan",
+            "k_long_bounds", "k_walk_", "k_skip_apply", "k_check_last", "k_finish",
             "k_lprep", "k_lwalk_", "k_lskip_apply", "k_lfinish")
 
 
