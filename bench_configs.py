@@ -427,6 +427,8 @@ def main():
     ap.add_argument("--resources", type=int, default=1_000_000)
     ap.add_argument("--cpu-events", type=int, default=4_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-summary", default=None,
+                    help="scripts/pmc_summary.py output of this workload's FETCH_SIZE / WRITE_SIZE passes (roofline traffic)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -440,6 +442,9 @@ def main():
            "roofline": {"bound": "hbm", "kernel": "whole batch pipeline, wall time per step", "achieved": gbs,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS, "traffic": None,
                         "algorithmic_bytes_per_step": r["b_alg"]}}
+    if args.pmc_summary and os.path.exists(args.pmc_summary):
+        res["roofline"]["traffic"] = json.load(open(args.pmc_summary)).get("pipeline_bytes_per_step")
+        res["roofline"]["traffic_source"] = args.pmc_summary
     res.update(r.get("extra", {}))
     if r["cpu"] is not None:
         res["cpu_baseline"] = r["cpu"]

@@ -392,9 +392,28 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n);
 /* Marks the handle as one of `world` shards of a node's flowIds (flowIds hashed over the GPUs,
  * no collective on the decision path). GlobalRequestLimiter's per-namespace QPS limiter counts every request of
  * the namespace in node order (GlobalRequestLimiter.java:46-55, ClusterFlowChecker.allowProceed :45-51), which a
- * shard does not see: with world > 1, limiter-enabled namespaces are SG_E_UNSUPPORTED (in either call order) and
- * the Java shim keeps such namespaces on one GPU. */
+ * shard does not see on its own: with world > 1 and limiter-enabled namespaces every flow batch of the shard goes
+ * through the exchange below (the pipelined / async flow entry points and cluster param batches refuse such a
+ * handle with SG_E_UNSUPPORTED; sg_flow_decide_batch without an armed exchange does too). */
 int sg_set_shard(sg_handle* h, int32_t rank, int32_t world);
+
+/* Sharded namespace limiter exchange (replaces GlobalRequestLimiter.tryPass's node-wide counting):
+ *   1. sg_lim_arrivals: this shard's valid requests of limited namespaces per (limiter slot, millisecond),
+ *      counts_out[slot * n_ms + (ts_ms - t_base)] (DEVICE, n_lim * n_ms uint32; slots = the limiter-enabled
+ *      namespaces in sg_set_namespaces order). [t_base, t_base + n_ms) is node-wide and must hold every shard's
+ *      limited requests of the node batch (SG_E_INVAL otherwise); n_ms <= 65536. Synchronous on `stream`.
+ *   2. the node all-gathers the counts of its `world` shards (RCCL) into gathered[world][n_lim][n_ms] (DEVICE);
+ *   3. sg_lim_exchange arms the handle's next sg_flow_decide_batch / _host with them (that call consumes it; the
+ *      buffer must stay valid until it returns).
+ * The node's arrival order is (ts_ms, shard rank, position in the shard's batch). Every shard walks the same
+ * per-100 ms node arrivals, so each keeps an identical replica of the namespace windows, and admits its request
+ * iff its node-wide rank in the period is below the period's quota: the results equal one handle deciding the
+ * merged batch. A shard with no requests in a node batch still calls sg_lim_exchange and sg_flow_decide_batch
+ * with n = 0 (its replica advances). A shard batch rejected by an error leaves its replica behind: the node must
+ * then reload the namespaces on every shard. */
+int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base, uint32_t n_ms, uint32_t* counts_out,
+                    void* stream);
+int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, int64_t t_base, uint32_t n_ms);
 int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n);
 
 /* Decide a batch. req/out are DEVICE pointers (HBM-resident); stream is a hipStream_t (NULL = default).

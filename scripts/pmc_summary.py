@@ -11,9 +11,10 @@ import os
 import sys
 from collections import defaultdict
 
-PIPELINE = ("k_prep", "k_seg", "k_lim_", "k_radix_", "k_scan_", "k_colsum", "k_chunkscan", "k_rescan",
-            "k_long_bounds", "k_walk_", "k_skip_apply", "k_check_last", "k_finish",
-            "k_lprep", "k_lwalk_", "k_lskip_apply", "k_lfinish")
+# every decision-pipeline kernel (k_*) except one-off state setup / readout; steps = launches of the batch's finish kernel
+NOT_PIPELINE = ("k_init_state", "k_local_init", "k_ptable_clear", "k_psclear", "k_psread", "k_snapshot",
+                "k_local_metrics")
+FINISH = ("k_finish", "k_local_finish", "k_pfinish", "k_psfinish")
 
 
 def load(d, counter):
@@ -38,13 +39,13 @@ def main(fetch_dir, write_dir, out):
         res[k] = {"launches": max(len(f.get(k, [])), len(w.get(k, []))), "fetch_bytes": fb, "write_bytes": wb}
     # per step: every pipeline kernel's per-launch traffic × launches per step (launch counts / steps)
     steps = None
-    for k in ("k_finish", "k_lfinish"):
+    for k in FINISH:
         if k in res:
             steps = res[k]["launches"]
     step_bytes = 0.0
     if steps:
         for k, v in res.items():
-            if k.startswith(PIPELINE):
+            if k.startswith("k_") and k not in NOT_PIPELINE:
                 step_bytes += (v["fetch_bytes"] + v["write_bytes"]) * v["launches"] / steps
     json.dump({"kernels": res, "pipeline_bytes_per_step": step_bytes, "steps_seen": steps,
                "note": "FETCH_SIZE x2 (gfx950 correction), KiB→bytes"}, open(out, "w"), indent=1)

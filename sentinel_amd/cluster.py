@@ -87,3 +87,64 @@ class MetricRollup:
         for r, s in enumerate(shards):
             out[torch.as_tensor(s, device=self.device)] = self.gathered[r][: len(s)]
         return out
+
+
+def node_order(shard_ts):
+    """The node's arrival order under the sharded limiter exchange: (ts_ms, shard rank, position in the shard's
+    batch). `shard_ts[r]` = rank r's batch timestamps (time-ordered). Returns the permutation that puts the
+    concatenation [rank 0's batch, rank 1's, ...] into node order (stable sort by ts)."""
+    cat = np.concatenate([np.asarray(t, np.int64) for t in shard_ts]) if shard_ts else np.zeros(0, np.int64)
+    return np.argsort(cat, kind="stable")
+
+
+class LimiterExchange:
+    """SURVEY §8(e) exchange step for the namespace QPS limiter (GlobalRequestLimiter.java:46-55): one node-wide
+    window per namespace although every GPU sees only its flows' requests.
+
+    Per node batch: all_reduce(MAX) of (-first ts, last ts) → the node's millisecond range; sg_lim_arrivals counts
+    this shard's limited requests per (namespace slot, millisecond); all_gather of those counts (n_lim × n_ms × 4
+    bytes per rank: 4 KB for one namespace over a 1 s batch); sg_lim_exchange arms the engine's next flow batch.
+    The node's arrival order is then (ts, rank, position) — `node_order`. Collectives run on `coll_device` (the
+    rank's GPU for RCCL, "cpu" for gloo)."""
+
+    def __init__(self, engine, n_lim: int, device, coll_device=None, group=None):
+        self.eng = engine
+        self.n_lim = n_lim
+        self.device = torch.device(device)
+        self.coll = torch.device(coll_device) if coll_device is not None else self.device
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self._gathered = None  # kept alive until the armed batch has been decided
+
+    def time_range(self, t_first, t_last):
+        """Node-wide [t_base, t_base + n_ms) from each rank's first / last timestamp (None: empty batch)."""
+        big = np.iinfo(np.int64).max
+        v = torch.tensor([-(t_first if t_first is not None else big), t_last if t_last is not None else -big],
+                         dtype=torch.int64, device=self.coll)
+        if self.world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
+        lo, hi = -int(v[0]), int(v[1])
+        if hi < lo:
+            return None
+        return lo, hi - lo + 1
+
+    def arm(self, req_ptr: int, n: int, t_first, t_last, stream_ptr: int = 0):
+        """Count, exchange and arm for this rank's batch (device records at req_ptr). Every rank calls this for
+        every node batch, with n = 0 when it has no requests; the caller then decides its batch (n may be 0)."""
+        rng = self.time_range(t_first, t_last)
+        if rng is None:
+            rng = (0, 1)  # no requests anywhere: nothing to count, the windows see no tryPass
+        t_base, n_ms = rng
+        mine = torch.zeros(max(1, self.n_lim) * n_ms, dtype=torch.int32, device=self.device)
+        self.eng.lim_arrivals(req_ptr if n else 0, n, t_base, n_ms, mine.data_ptr(), stream_ptr)
+        if self.world > 1:
+            parts = [torch.zeros_like(mine, device=self.coll) for _ in range(self.world)]
+            dist.all_gather(parts, mine.to(self.coll), group=self.group)
+            gathered = torch.cat(parts).to(self.device)
+        else:
+            gathered = mine
+        self._gathered = gathered
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        self.eng.lim_exchange(gathered.data_ptr(), t_base, n_ms)
+        return t_base, n_ms

@@ -162,6 +162,11 @@ struct sg_handle {
 
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
+    // sg_lim_exchange: the node's gathered per-millisecond limiter arrivals for the next flow batch of a shard
+    const uint32_t* lim_xg = nullptr;
+    int64_t lim_xt = 0;
+    uint32_t lim_xn = 0;
+    bool lim_x_armed = false;
     // ParamFlowSlot chain (sg_pslot_*)
     uint32_t ps_nres = 0;
     bool ps_loaded = false;
@@ -249,6 +254,8 @@ struct sg_handle {
 };
 
 namespace {
+int ensure_layout(sg_handle* h);          // below: record layout of the loaded rules
+int flow_status(sg_handle* h, int err);   // below: batch error flags -> SG_E_*
 int drain_async(sg_handle* h);  // below: completes the handle's in-flight host-pipeline batches
 }
 
@@ -614,10 +621,37 @@ const char* sg_last_error(const sg_handle* h) { return h ? h->err.c_str() : "nul
 int sg_set_shard(sg_handle* h, int32_t rank, int32_t world) {
     if (h) drain_async(h);
     if (!h || world < 1 || rank < 0 || rank >= world) return SG_E_INVAL;
-    if (world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "a namespace QPS limiter is node-wide (GlobalRequestLimiter): not on a shard");
     h->shard_rank = rank;
     h->shard_world = world;
+    return SG_OK;
+}
+
+int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base, uint32_t n_ms, uint32_t* counts_out,
+                    void* stream_) {
+    if (!h || (!req && n) || !counts_out) return SG_E_INVAL;
+    if (t_base < 0 || n_ms == 0 || n_ms > kMaxPeriods) return fail(h, SG_E_INVAL, "exchange range: t_base >= 0, 1 <= n_ms <= 65536");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = ensure_layout(h);
+    if (rc) return rc;
+    HIP_TRY(h, hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * (size_t)h->n_lim * n_ms, stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    if (h->n_lim > 0)
+        HIP_TRY(h, launch_lim_arrivals(req, n, h->K, h->d_rule_lim, t_base, n_ms, counts_out, h->d_err, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    return flow_status(h, *h->h_err);
+}
+
+int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, int64_t t_base, uint32_t n_ms) {
+    if (!h || !gathered) return SG_E_INVAL;
+    if (t_base < 0 || n_ms == 0 || n_ms > kMaxPeriods) return fail(h, SG_E_INVAL, "exchange range: t_base >= 0, 1 <= n_ms <= 65536");
+    h->lim_xg = gathered;
+    h->lim_xt = t_base;
+    h->lim_xn = n_ms;
+    h->lim_x_armed = true;
     return SG_OK;
 }
 
@@ -631,8 +665,6 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
         }
     }
     if (want > kMaxLim) return fail(h, SG_E_UNSUPPORTED, "more than 8 namespaces with a QPS limiter");
-    if (want && h->shard_world > 1)
-        return fail(h, SG_E_UNSUPPORTED, "a namespace QPS limiter is node-wide (GlobalRequestLimiter): not on a shard");
     h->conc_dirty = true;  // AVG_LOCAL concurrency thresholds read connectedCount
     for (const auto& r : h->rules)
         if (r.namespace_id < 0 || (uint32_t)r.namespace_id >= n)
@@ -873,6 +905,8 @@ int flow_status(sg_handle* h, int err) {
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
     if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
     if (err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    if (err & kErrExchange)
+        return fail(h, SG_E_INVAL, "a request of a limited namespace lies outside the limiter exchange's time range");
     return SG_OK;
 }
 
@@ -1038,6 +1072,13 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
         L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
         L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
         L.ring = h->d_lim_ring;
+        if (h->lim_x_armed) {
+            L.xg = h->lim_xg;
+            L.t_base = h->lim_xt;
+            L.n_ms = h->lim_xn;
+            L.world = h->shard_world;
+            L.rank = h->shard_rank;
+        }
         HIP_TRY(h, launch_limiter(a, L, stream));
     }
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
@@ -1107,6 +1148,8 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
 // that marks the batch's completion through *done (the back half's end, recorded on s_back).
 int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipEvent_t after, int* err_dst,
                            hipEvent_t done) {
+    if (h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
     int rc = ensure_layout(h);
     if (rc) return rc;
     rc = pipe_setup(h);
@@ -1160,13 +1203,44 @@ int drain_async(sg_handle* h) {
 
 int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
     if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
+    const bool xshard = h->shard_world > 1 && h->n_lim > 0;
+    if (xshard && !h->lim_x_armed)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: sg_lim_exchange must precede every flow batch");
+    const bool armed = h->lim_x_armed;
+    h->lim_x_armed = false;  // the exchange is consumed by this call, whatever its outcome
+    if (n == 0 && !armed) return SG_OK;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (n == 0) {  // no requests on this shard: its replica of the namespace windows still advances
+        HIP_TRY(h, hipSetDevice(h->device));
+        drain_async(h);
+        int rc = ensure_layout(h);
+        if (rc) return rc;
+        BatchArgs a{};
+        a.err = h->d_err;
+        LimArgs L{};
+        L.n_lim = h->n_lim;
+        std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
+        L.arrivals = h->d_lim_period;
+        L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
+        L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
+        L.ring = h->d_lim_ring;
+        L.xg = h->lim_xg;
+        L.t_base = h->lim_xt;
+        L.n_ms = h->lim_xn;
+        L.world = h->shard_world;
+        L.rank = h->shard_rank;
+        HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
+        HIP_TRY(h, launch_limiter_plan_only(a, L, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        return SG_OK;
+    }
     if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
-    hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
+    h->lim_x_armed = armed;  // read by flow_front
     int rc = enqueue_flow(h, req, n, out, stream, h->h_err, h->stats_on);
+    h->lim_x_armed = false;
     if (rc) return rc;
     HIP_TRY(h, hipStreamSynchronize(stream));
     if (h->stats_on) {
@@ -1203,6 +1277,8 @@ void sg_host_free(sg_handle* h, void* p) {
 int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
     if (!h || !ticket) return SG_E_INVAL;
     *ticket = 0;
+    if (h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
     if (n == 0) return SG_OK;
     if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
@@ -1246,6 +1322,8 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
 int sg_flow_enqueue(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
     if (!h || !ticket) return SG_E_INVAL;
     *ticket = 0;
+    if (h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
     if (n == 0) return SG_OK;
     if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
@@ -1306,7 +1384,7 @@ int sg_flow_wait(sg_handle* h, uint64_t ticket) {
 
 int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out) {
     if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
+    if (n == 0) return sg_flow_decide_batch(h, nullptr, 0, nullptr, nullptr);  // (advances a sharded limiter)
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     HIP_TRY(h, hipSetDevice(h->device));
     if (!h->d_req_h) {
@@ -1794,6 +1872,8 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     if (!req || !out || (!values && n_values)) return fail(h, SG_E_INVAL, "null buffer");
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     if (!h->d_cplast_ts) return fail(h, SG_E_INVAL, "sg_cparam_load_rules first");
+    if (h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "cluster param tokens on a shard with a namespace limiter (the exchange covers flow batches)");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);

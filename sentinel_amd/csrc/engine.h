@@ -51,6 +51,7 @@ constexpr uint32_t kClassMax[kClasses - 1] = {4, 16, 64, 256, 1024};
 constexpr int kErrTime = 1;      // negative or decreasing timestamps
 constexpr int kErrPeriods = 2;   // batch spans more than kMaxPeriods windows
 constexpr int kErrInternal = 16; // a walker loop exceeded its bound (never expected)
+constexpr int kErrExchange = 64; // a limited request lies outside the sharded limiter exchange's time range
 
 struct BatchArgs {
     const sg_req* req;
@@ -134,9 +135,20 @@ struct LimArgs {
     uint32_t* prefix;               // [kMaxLim][kMaxPeriods]
     uint32_t* quota;                // [kMaxLim][kMaxPeriods]
     LimRing* ring;                  // [kMaxLim]
+    // sharded limiter: per-millisecond arrivals of every shard, gathered by the node; null = this
+    // handle sees the namespace's whole arrival sequence
+    const uint32_t* xg;             // [world][n_lim][n_ms]
+    int64_t t_base;                 // the exchange's first millisecond (node-wide)
+    uint32_t n_ms;                  // milliseconds covered, <= kMaxPeriods
+    int world, rank;
 };
 
 hipError_t launch_limiter(const BatchArgs& a, const LimArgs& L, hipStream_t stream);
+// A shard with no requests in a node batch still advances its replica of the namespace windows.
+hipError_t launch_limiter_plan_only(const BatchArgs& a, const LimArgs& L, hipStream_t stream);
+// This shard's arrivals per (limiter slot, millisecond) for the exchange: counts[slot * n_ms + (ts - t_base)].
+hipError_t launch_lim_arrivals(const sg_req* req, uint64_t n, uint32_t K, const uint8_t* rule_lim, int64_t t_base,
+                               uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream);
 
 // ---- hot-parameter flow control (param.hip) ----
 constexpr int kErrNonPositive = 4;  // some acquireCount <= 0 in the batch (disables the skip shortcut)

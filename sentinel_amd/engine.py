@@ -12,7 +12,8 @@ from . import abi
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsentinel_gpu.so")  # override: A/B tuning runs
 
-EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_load_flow_rules",
+EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_lim_arrivals",
+           "sg_lim_exchange", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_enqueue", "sg_flow_poll", "sg_flow_wait",
            "sg_host_alloc", "sg_host_free", "sg_enable_stats", "sg_get_stats",
            "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_snapshot_metrics_enqueue", "sg_debug_copy", "sg_build_info",
@@ -52,6 +53,8 @@ def load_library():
         "sg_last_error": (C.c_char_p, [vp]),
         "sg_set_namespaces": (C.c_int, [vp, vp, u32]),
         "sg_set_shard": (C.c_int, [vp, C.c_int32, C.c_int32]),
+        "sg_lim_arrivals": (C.c_int, [vp, vp, u64, i64, u32, vp, vp]),
+        "sg_lim_exchange": (C.c_int, [vp, vp, i64, u32]),
         "sg_load_flow_rules": (C.c_int, [vp, vp, u32]),
         "sg_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
@@ -155,6 +158,14 @@ class FlowEngine:
     def set_shard(self, rank: int, world: int):
         """This handle decides shard `rank` of `world` (refuses namespace QPS limiters when world > 1)."""
         self._check(self._L.sg_set_shard(self.h, rank, world))
+
+    def lim_arrivals(self, req_ptr: int, n: int, t_base: int, n_ms: int, counts_ptr: int, stream_ptr: int = 0):
+        """This shard's limited arrivals per (limiter slot, millisecond) into device counts[n_lim][n_ms]."""
+        self._check(self._L.sg_lim_arrivals(self.h, req_ptr, n, t_base, n_ms, counts_ptr, stream_ptr))
+
+    def lim_exchange(self, gathered_ptr: int, t_base: int, n_ms: int):
+        """Arm the next flow batch with the node's gathered arrivals (device [world][n_lim][n_ms])."""
+        self._check(self._L.sg_lim_exchange(self.h, gathered_ptr, t_base, n_ms))
 
     def load_rules(self, rules: np.ndarray):
         rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)

@@ -110,3 +110,65 @@ def test_sharded_decisions_and_rollup_equal_node_replay(world):
         assert np.array_equal(node_snap, node)
         assert np.allclose(totals, node.sum(0), rtol=1e-12)
     assert np.array_equal(got, want)
+
+
+class _CountingEngine:
+    """Stands in for the engine's two exchange entry points (no GPU here): records what LimiterExchange asks for."""
+
+    def __init__(self):
+        self.calls = []
+
+    def lim_arrivals(self, req_ptr, n, t_base, n_ms, counts_ptr, stream_ptr=0):
+        self.calls.append(("arrivals", n, t_base, n_ms))
+
+    def lim_exchange(self, gathered_ptr, t_base, n_ms):
+        self.calls.append(("exchange", t_base, n_ms))
+
+
+def _xch_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sentinel_amd.cluster import LimiterExchange
+        eng = _CountingEngine()
+        x = LimiterExchange(eng, 2, "cpu")
+        # rank r's batch spans [100 + 10 r, 150 + 20 r]; the last rank has no requests in the second batch
+        t_first, t_last = 100 + 10 * rank, 150 + 20 * rank
+        r1 = x.arm(0, 5, t_first, t_last)
+        empty = rank == world - 1
+        r2 = x.arm(0, 0 if empty else 3, None if empty else 500 + rank, None if empty else 600 - rank)
+        q.put((rank, r1, r2, eng.calls, tuple(x._gathered.shape)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_limiter_exchange_time_range_and_gather(world):
+    """cluster.LimiterExchange (SURVEY §8(e) limiter exchange) over gloo: every rank derives the same node-wide
+    millisecond range (empty batches are neutral), counts with it, gathers world x n_lim x n_ms counts and arms."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+    lo1, hi1 = 100, 150 + 20 * (world - 1)
+    lo2, hi2 = 500, 600
+    for rank, r1, r2, calls, shape in res:
+        assert r1 == (lo1, hi1 - lo1 + 1)
+        assert r2 == (lo2, hi2 - lo2 + 1)
+        assert calls[0] == ("arrivals", 5, lo1, hi1 - lo1 + 1) and calls[1] == ("exchange", lo1, hi1 - lo1 + 1)
+        assert calls[3] == ("exchange", lo2, hi2 - lo2 + 1)
+        assert shape == (world * 2 * (hi2 - lo2 + 1),)
+
+
+def test_node_order_is_ts_then_rank_then_position():
+    from sentinel_amd.cluster import node_order
+    ts = [np.array([5, 5, 7]), np.array([4, 5, 7, 7])]
+    perm = node_order(ts)
+    # concatenation: r0 = [5, 5, 7] at 0..2, r1 = [4, 5, 7, 7] at 3..6
+    assert perm.tolist() == [3, 0, 1, 4, 2, 5, 6]

@@ -1,0 +1,170 @@
+"""Sharded namespace limiter (SURVEY §8(e) exchange step; GlobalRequestLimiter.java:46-55,
+ClusterFlowChecker.allowProceed :45-51): every GPU holds a share of the flowIds but the namespace window is
+node-wide. Shards count their limited arrivals per millisecond (sg_lim_arrivals), the node gathers them, every
+shard is armed with the gathered counts (sg_lim_exchange) and decides its own requests. The results must equal one
+oracle replay of the merged batch in the node's arrival order (ts, shard rank, position in the shard's batch),
+batch after batch (each shard keeps a replica of the namespace windows), including shards with no requests.
+Here the shards are handles in one process and the gather is a device concat; tests/test_dist_gpu.py runs the
+same exchange over torch.distributed."""
+import numpy as np
+import pytest
+import torch
+
+from sentinel_amd import abi
+from sentinel_amd.cluster import node_order, route_requests, shard_flows
+
+pytestmark = pytest.mark.gpu
+
+N_FLOWS = 3000
+
+
+def _ns(qps):
+    ns = np.zeros(3, abi.NS_DTYPE)
+    ns["connected_count"] = [1, 2, 1]
+    ns["limiter_enabled"] = [1, 0, 1]
+    ns["max_allowed_qps"] = [qps, 0, qps * 3 + 7]
+    return ns
+
+
+def _rules(rng):
+    from sentinel_amd.workload import ClusterWorkload
+    r = ClusterWorkload(n_flows=N_FLOWS, seed=5).rules()
+    r["count"] = rng.integers(1, 400, N_FLOWS).astype(np.float64)
+    r["namespace_id"] = rng.integers(0, 3, N_FLOWS)
+    return r
+
+
+def _batches(rng, t0):
+    """Time-ordered node batches with many requests per millisecond (the interleaving matters), invalid keys,
+    gaps between batches, and one batch whose requests all belong to few flows (some shards get none)."""
+    out, t = [], t0
+    for b in range(4):
+        n = int(rng.integers(20_000, 60_000))
+        span = int(rng.integers(80, 1500))
+        req = np.zeros(n, abi.REQ_DTYPE)
+        req["ts_ms"] = t + np.sort(rng.integers(0, span, n))
+        if b == 2:
+            req["key"] = rng.integers(0, 2, n).astype(np.uint32)  # two flows only
+        else:
+            req["key"] = np.minimum(rng.zipf(1.2, n) - 1, N_FLOWS - 1).astype(np.uint32)
+            req["key"][rng.random(n) < 0.01] = abi.KEY_NO_RULE
+        req["acquire"] = np.where(rng.random(n) < 0.1, rng.integers(2, 5, n), 1)
+        req["acquire"][rng.random(n) < 0.005] = 0  # BAD_REQUEST: not a tryPass
+        req["key"] |= np.where(rng.random(n) < 0.03, np.uint32(abi.KEY_PRIO), np.uint32(0))
+        out.append(req)
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, 900))
+    return out
+
+
+def _split(req, world, local):
+    """Per rank: node indices (arrival order) and the shard batch with shard-local keys (KEY_NO_RULE / BAD keys
+    go to flow 0's owner, which answers them as the node would)."""
+    keys = (req["key"] & abi.KEY_INDEX).astype(np.int64)
+    valid = keys < N_FLOWS
+    route = np.where(valid, keys, 0)
+    order, counts = route_requests(route, world)
+    parts, start = [], 0
+    for r in range(world):
+        mine = np.sort(order[start:start + counts[r]])
+        start += counts[r]
+        sub = req[mine].copy()
+        k = keys[mine]
+        ok = k < N_FLOWS
+        sub["key"] = np.where(ok, local[r][np.where(ok, k, 0)], sub["key"] & abi.KEY_INDEX).astype(np.uint32) | \
+            (sub["key"] & np.uint32(abi.KEY_PRIO))
+        parts.append((mine, sub))
+    return parts
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("qps", [0.0, 40.0, 3000.0, 1e12])
+def test_sharded_limiter_equals_node_replay(world, qps):
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.engine import FlowEngine
+    rng = np.random.default_rng(world * 1000 + int(qps) % 997)
+    rules = _rules(rng)
+    ns = _ns(qps)
+    shards = [shard_flows(N_FLOWS, r, world) for r in range(world)]
+    local = []
+    for s in shards:
+        m = np.full(N_FLOWS, abi.KEY_NO_RULE, np.int64)
+        m[s] = np.arange(len(s))
+        local.append(m)
+    engs = []
+    for r in range(world):
+        e = FlowEngine(device=0, max_batch=1 << 16)
+        e.set_shard(r, world)
+        e.set_namespaces(ns)
+        e.load_rules(rules[shards[r]])
+        engs.append(e)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(rules)
+    dev = torch.device("cuda:0")
+    n_lim = int(ns["limiter_enabled"].sum())
+    saw_tmr = False
+    for req in _batches(rng, 1_700_000_000_033):
+        parts = _split(req, world, local)
+        ts = [p[1]["ts_ms"] for p in parts]
+        t_base = min(int(t[0]) for t in ts if len(t))
+        n_ms = max(int(t[-1]) for t in ts if len(t)) - t_base + 1
+        reqs_d = [torch.from_numpy(p[1].view(np.uint8).copy()).to(dev) for p in parts]
+        counts = []
+        for r in range(world):
+            c = torch.zeros(n_lim * n_ms, dtype=torch.int32, device=dev)
+            engs[r].lim_arrivals(reqs_d[r].data_ptr() if len(parts[r][1]) else 0, len(parts[r][1]), t_base, n_ms,
+                                 c.data_ptr())
+            counts.append(c)
+        gathered = torch.cat(counts)
+        torch.cuda.synchronize()
+        got = []
+        for r in range(world):
+            n = len(parts[r][1])
+            out = torch.zeros(max(1, n) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            engs[r].lim_exchange(gathered.data_ptr(), t_base, n_ms)
+            engs[r].decide_device(reqs_d[r].data_ptr() if n else 0, n, out.data_ptr())
+            got.append(out.cpu().numpy().view(abi.RES_DTYPE)[:n])
+        # the oracle decides the merged batch in node order (ts, rank, position)
+        cat_idx = np.concatenate([p[0] for p in parts])
+        perm = node_order(ts)
+        want_node = ora.decide(req[cat_idx[perm]])
+        want = np.empty_like(want_node)
+        want[perm] = want_node
+        got_cat = np.concatenate(got)
+        bad = np.nonzero(got_cat != want)[0]
+        assert len(bad) == 0, f"{len(bad)} of {len(want)} differ; first {got_cat[bad[:3]]} vs {want[bad[:3]]}"
+        saw_tmr |= bool((want["status"] == abi.TOO_MANY_REQUEST).any())
+    assert saw_tmr == (qps < 1e6)
+
+
+def test_sharded_limiter_contract():
+    """A sharded handle with a limited namespace decides only through the exchange: a flow batch without an
+    armed exchange, the pipelined entry points and requests outside the exchange's range are refused."""
+    from sentinel_amd.engine import EngineError, FlowEngine
+    rng = np.random.default_rng(3)
+    rules = _rules(rng)
+    e = FlowEngine(device=0, max_batch=4096)
+    e.set_shard(0, 2)
+    e.set_namespaces(_ns(100.0))
+    mine = rules[shard_flows(N_FLOWS, 0, 2)]
+    e.load_rules(mine)
+    req = np.zeros(16, abi.REQ_DTYPE)
+    req["ts_ms"] = 1_700_000_000_000 + np.arange(16)
+    req["acquire"] = 1
+    req["key"] = int(np.nonzero(mine["namespace_id"] == 0)[0][0])  # a flow of a limited namespace
+    with pytest.raises(EngineError) as ei:
+        e.decide_host(req)
+    assert ei.value.code == abi.SG_E_UNSUPPORTED
+    out = e.host_array(len(req), abi.RES_DTYPE)
+    with pytest.raises(EngineError) as ei:
+        e.submit(req, out)
+    assert ei.value.code == abi.SG_E_UNSUPPORTED
+    dev = torch.device("cuda:0")
+    rq = torch.from_numpy(req.view(np.uint8).copy()).to(dev)
+    c = torch.zeros(2 * 8, dtype=torch.int32, device=dev)
+    with pytest.raises(EngineError) as ei:  # the range must hold every limited request
+        e.lim_arrivals(rq.data_ptr(), len(req), 1_700_000_000_004, 8, c.data_ptr())
+    assert ei.value.code == abi.SG_E_INVAL
+    # the same handle unsharded decides without the exchange
+    e.set_shard(0, 1)
+    assert len(e.decide_host(req)) == len(req)
