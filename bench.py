@@ -207,11 +207,20 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with --nproc-per-node {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # SG_BENCH_ONE_DEVICE=1: rehearsal of the N-rank path on a one-GPU box (every rank on device 0, gloo on CPU
+    # tensors instead of RCCL); never the measured configuration
+    one_dev = os.environ.get("SG_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local_rank = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
+    coll = torch.device("cpu") if one_dev else dev  # where the collectives' tensors live
     torch.cuda.set_device(dev)
 
     wl = ShardWorkload(args.flows, args.requests, rank, world, dev)
@@ -228,7 +237,7 @@ def main():
     # one output buffer per batch in flight (the pipeline keeps up to 4 batches enqueued)
     outs = [torch.empty(args.requests * RES_B, dtype=torch.uint8, device=dev) for _ in range(4)]
     snaps = [torch.empty((wl.K, 2), dtype=torch.float64, device=dev) for _ in range(2)]
-    rollup = MetricRollup(wl.K, dev) if world > 1 else None
+    rollup = MetricRollup(wl.K, coll) if world > 1 else None
     torch.cuda.synchronize()
 
     def run_steps(b0, b1):
@@ -243,13 +252,13 @@ def main():
                 t_snap = eng.snapshot_enqueue(now, snaps[b % 2].data_ptr(), wl.K)
                 if pend is not None:
                     eng.wait(pend[0])
-                    rollup.run(snaps[pend[1] % 2])
+                    rollup.run(snaps[pend[1] % 2].to(coll))
                 pend = (t_snap, b)
         for t in tickets:
             eng.wait(t)
         if pend is not None:
             eng.wait(pend[0])
-            rollup.run(snaps[pend[1] % 2])
+            rollup.run(snaps[pend[1] % 2].to(coll))
 
     run_steps(0, args.warmup)
     if world > 1:
@@ -261,7 +270,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=coll)
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
@@ -302,7 +311,7 @@ def main():
         "data": "synthetic (GPU-generated, seeded): Zipf(1.0) flowIds, counts U{1..32}, 10% acquire U{2..4}, 1% prioritized",
         "config": {"workload": "C3 cluster token server: ClusterFlowChecker, FLOW_THRESHOLD_GLOBAL, S=10/1000 ms",
                    "flow_ids": args.flows, "flow_ids_per_gpu": wl.K, "requests_per_step_per_gpu": args.requests,
-                   "simulated_ms_per_step": wl.span_ms, "parallelism": f"hash-sharded flowIds x{world}",
+                   "simulated_ms_per_step": wl.span_ms, "parallelism": f"hash-sharded flowIds x{world}" + (" (one-device rehearsal)" if one_dev else ""),
                    "rollup": "RCCL all_reduce + all_gather per step" if world > 1 else "none (1 GPU)"},
         "roofline": {"bound": "hbm", "kernel": "whole batch pipeline (prep + sort + walk), step time with batches "
                                                "pipelined (sort of batch i+1 beside the walkers of batch i)",
