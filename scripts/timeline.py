@@ -6,7 +6,7 @@ k_prep), each kernel's start / end relative to the first k_prep shown, in µs, t
 import csv
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sg::" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sg::" in r["Kernel_Name"] or r["Kernel_Name"].startswith(("k_", "void k_"))]
 n_show = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 preps = [i for i, r in enumerate(rows) if "k_prep" in r["Kernel_Name"]]
