@@ -77,22 +77,30 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in,
 // The per-tile histograms are stored tile-major (hist[t][d]: each tile writes and reads one contiguous row); the
 // scatter needs each (tile, digit) run's global start, the exclusive scan in (digit, tile) order. Three passes:
 // per-chunk column sums, one block scanning the chunks per digit and the digit totals, then each chunk rewrites
-// its rows in place as offsets.
+// its rows in place as offsets. These kernels are latency-bound (a few MB): every load of a thread is issued
+// before any is used (indices clamped, values masked, no branch between the loads), so each pass costs one or
+// two memory round trips instead of one per tile / chunk — in the pipelined flow path they run beside the
+// walkers, whose traffic stretches each round trip to several µs (a per-tile loop took 120 µs there).
 constexpr uint32_t kChunkTiles = 32;
 
 template <int D>
 __global__ void __launch_bounds__(kSortThreads) k_colsum(const uint32_t* hist, uint32_t ntiles, uint32_t* csum) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;
-    const uint32_t t0 = blockIdx.x * kChunkTiles, t1 = min(t0 + kChunkTiles, ntiles);
-    uint32_t acc[kPer];
+    const uint32_t t0 = blockIdx.x * kChunkTiles, nt = min(kChunkTiles, ntiles - t0);
+    uint32_t v[kChunkTiles][kPer];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) acc[i] = 0;
-    for (uint32_t t = t0; t < t1; ++t)
+    for (uint32_t u = 0; u < kChunkTiles; ++u)
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) acc[i] += hist[(size_t)t * kBins + threadIdx.x + i * kSortThreads];
+        for (int i = 0; i < kPer; ++i)
+            v[u][i] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + threadIdx.x + i * kSortThreads];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads] = acc[i];
+    for (int i = 0; i < kPer; ++i) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kChunkTiles; ++u) acc += u < nt ? v[u][i] : 0u;
+        csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads] = acc;
+    }
 }
 
 // One block of kBins threads (thread = digit): exclusive scan of the chunk sums per digit, plus the base of the
@@ -102,16 +110,17 @@ __global__ void __launch_bounds__(1024) k_chunkscan(uint32_t* csum, uint32_t nch
     constexpr int kBins = 1 << D;
     __shared__ uint32_t wsum[kBins / 64];
     const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
-    constexpr uint32_t kB = 16;  // chunks loaded before any is stored (the loads do not wait on each other)
+    constexpr uint32_t kB = 64;  // chunks loaded before any is stored (one round trip per kB chunks)
+    const uint32_t last = nchunks - 1;
     uint32_t run = 0;
     for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
         uint32_t v[kB];
 #pragma unroll
-        for (uint32_t u = 0; u < kB; ++u) v[u] = c0 + u < nchunks ? csum[(size_t)(c0 + u) * kBins + d] : 0u;
+        for (uint32_t u = 0; u < kB; ++u) v[u] = csum[(size_t)min(c0 + u, last) * kBins + d];
 #pragma unroll
         for (uint32_t u = 0; u < kB; ++u) {
             if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = run;
-            run += v[u];
+            run += c0 + u < nchunks ? v[u] : 0u;
         }
     }
     uint32_t x = run;  // inclusive scan of the digit totals over the block
@@ -127,7 +136,7 @@ __global__ void __launch_bounds__(1024) k_chunkscan(uint32_t* csum, uint32_t nch
     for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
         uint32_t v[kB];
 #pragma unroll
-        for (uint32_t u = 0; u < kB; ++u) v[u] = c0 + u < nchunks ? csum[(size_t)(c0 + u) * kBins + d] : 0u;
+        for (uint32_t u = 0; u < kB; ++u) v[u] = csum[(size_t)min(c0 + u, last) * kBins + d];
 #pragma unroll
         for (uint32_t u = 0; u < kB; ++u)
             if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = v[u] + base;
@@ -138,18 +147,24 @@ template <int D>
 __global__ void __launch_bounds__(kSortThreads) k_rescan(uint32_t* hist, const uint32_t* csum, uint32_t ntiles) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;
-    const uint32_t t0 = blockIdx.x * kChunkTiles, t1 = min(t0 + kChunkTiles, ntiles);
+    const uint32_t t0 = blockIdx.x * kChunkTiles, nt = min(kChunkTiles, ntiles - t0);
     uint32_t run[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) run[i] = csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads];
-    for (uint32_t t = t0; t < t1; ++t)
+    uint32_t v[kChunkTiles][kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kChunkTiles; ++u)
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            v[u][i] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + threadIdx.x + i * kSortThreads];
+#pragma unroll
+    for (uint32_t u = 0; u < kChunkTiles; ++u) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
-            uint32_t* p = hist + (size_t)t * kBins + threadIdx.x + i * kSortThreads;
-            const uint32_t v = *p;
-            *p = run[i];
-            run[i] += v;
+            if (u < nt) hist[(size_t)(t0 + u) * kBins + threadIdx.x + i * kSortThreads] = run[i];
+            run[i] += v[u][i];  // (past nt: unused)
         }
+    }
 }
 
 template <int D>
