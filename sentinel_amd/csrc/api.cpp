@@ -1576,7 +1576,9 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
     p.last_ts = h->d_plast_ts;
     p.long_list = h->d_long_list;
     p.long_count = h->d_long_count;
-    p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : 16u;
+    uint32_t psplit = 32u;  // lane / wave walker split of the hot-parameter walkers (SG_PARAM_SHORT_MAX: tuning)
+    if (const char* e = std::getenv("SG_PARAM_SHORT_MAX")) psplit = (uint32_t)std::strtoul(e, nullptr, 10);
+    p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : psplit;
     const int gbits = bits_for(h->ptotal + 1);
     if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
