@@ -57,7 +57,10 @@ __device__ __forceinline__ uint64_t param_slot(const PArgs& p, const PRule& r, u
     uint64_t i = h & r.table_mask;
     for (uint64_t probes = 0; probes <= r.table_mask; ++probes) {
         unsigned long long* vw = (unsigned long long*)&p.table[r.table_base + i].value;
-        const unsigned long long cur = __hip_atomic_load(vw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a plain (L2-cached) load: a slot only ever goes from empty to its value, so a stale read can only say
+        // "empty", and the CAS below then returns the value that is there (an agent-scope atomic load bypassed
+        // the XCD's L2 on every probe, also for the hot values that repeat throughout a batch)
+        const unsigned long long cur = *vw;
         if (cur == v) return r.table_base + i;
         if (cur == kEmptyValue) {
             const unsigned long long old = atomicCAS(vw, (unsigned long long)kEmptyValue, (unsigned long long)v);
