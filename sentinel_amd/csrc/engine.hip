@@ -1373,6 +1373,7 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         const Rule R = a.rules[k];
         const Occ occ = a.occ[k];
         // first window: the class's longest segment (<= 4, <= 16 records) or kRecW
+        static_assert(kRecW >= (int)kClassMax[1], "the first window of class 1 must fit the lane's LDS rows");
         const int rows = c == 0 ? (int)kClassMax[0] : c == 1 ? (int)kClassMax[1] : kRecW;
         if (c == 0) stage_records<kClassMax[0]>(a, wrecs, s);
         else if (c == 1) stage_records<kClassMax[1]>(a, wrecs, s);
