@@ -409,11 +409,15 @@ int sg_set_shard(sg_handle* h, int32_t rank, int32_t world);
  * per-100 ms node arrivals, so each keeps an identical replica of the namespace windows, and admits its request
  * iff its node-wide rank in the period is below the period's quota: the results equal one handle deciding the
  * merged batch. A shard with no requests in a node batch still calls sg_lim_exchange and sg_flow_decide_batch
- * with n = 0 (its replica advances). A shard batch rejected by an error leaves its replica behind: the node must
- * then reload the namespaces on every shard. */
+ * with n = 0 (its replica advances). A shard batch rejected by an error (SG_E_TIME, SG_E_INVAL, SG_E_CAPACITY …)
+ * still walks the armed node arrivals, so its replica stays equal to the other shards' (the node counted that shard's
+ * requests as limiter arrivals; their flow decisions did not happen). */
 int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base, uint32_t n_ms, uint32_t* counts_out,
-                    void* stream);
-int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, int64_t t_base, uint32_t n_ms);
+                    uint64_t counts_words, void* stream);
+int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, uint64_t gathered_words, int64_t t_base, uint32_t n_ms);
+/* The handle's limiter-slot count n_lim (limiter-enabled namespaces of sg_set_namespaces): counts_words of
+ * sg_lim_arrivals must equal n_lim * n_ms and gathered_words of sg_lim_exchange world * n_lim * n_ms (SG_E_INVAL). */
+int sg_lim_slots(const sg_handle* h, uint32_t* n_lim);
 int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n);
 
 /* Decide a batch. req/out are DEVICE pointers (HBM-resident); stream is a hipStream_t (NULL = default).

@@ -107,9 +107,9 @@ class LimiterExchange:
     The node's arrival order is then (ts, rank, position) — `node_order`. Collectives run on `coll_device` (the
     rank's GPU for RCCL, "cpu" for gloo)."""
 
-    def __init__(self, engine, n_lim: int, device, coll_device=None, group=None):
+    def __init__(self, engine, device, coll_device=None, group=None):
         self.eng = engine
-        self.n_lim = n_lim
+        self.n_lim = engine.lim_slots()  # the layout [world][n_lim][n_ms] is the engine's, not the caller's
         self.device = torch.device(device)
         self.coll = torch.device(coll_device) if coll_device is not None else self.device
         self.group = group
@@ -135,8 +135,9 @@ class LimiterExchange:
         if rng is None:
             rng = (0, 1)  # no requests anywhere: nothing to count, the windows see no tryPass
         t_base, n_ms = rng
-        mine = torch.zeros(max(1, self.n_lim) * n_ms, dtype=torch.int32, device=self.device)
-        self.eng.lim_arrivals(req_ptr if n else 0, n, t_base, n_ms, mine.data_ptr(), stream_ptr)
+        mine = torch.zeros(max(1, self.n_lim * n_ms), dtype=torch.int32, device=self.device)
+        self.eng.lim_arrivals(req_ptr if n else 0, n, t_base, n_ms, mine.data_ptr(), stream_ptr,
+                              counts_words=self.n_lim * n_ms)
         if self.world > 1:
             parts = [torch.zeros_like(mine, device=self.coll) for _ in range(self.world)]
             dist.all_gather(parts, mine.to(self.coll), group=self.group)
@@ -146,5 +147,5 @@ class LimiterExchange:
         self._gathered = gathered
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
-        self.eng.lim_exchange(gathered.data_ptr(), t_base, n_ms)
+        self.eng.lim_exchange(gathered.data_ptr(), t_base, n_ms, gathered_words=self.world * self.n_lim * n_ms)
         return t_base, n_ms

@@ -630,10 +630,18 @@ int sg_set_shard(sg_handle* h, int32_t rank, int32_t world) {
     return SG_OK;
 }
 
+int sg_lim_slots(const sg_handle* h, uint32_t* n_lim) {
+    if (!h || !n_lim) return SG_E_INVAL;
+    *n_lim = (uint32_t)h->n_lim;
+    return SG_OK;
+}
+
 int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base, uint32_t n_ms, uint32_t* counts_out,
-                    void* stream_) {
+                    uint64_t counts_words, void* stream_) {
     if (!h || (!req && n) || !counts_out) return SG_E_INVAL;
     if (t_base < 0 || n_ms == 0 || n_ms > kMaxPeriods) return fail(h, SG_E_INVAL, "exchange range: t_base >= 0, 1 <= n_ms <= 65536");
+    if (counts_words != (uint64_t)h->n_lim * n_ms)
+        return fail(h, SG_E_INVAL, "counts buffer must hold n_lim * n_ms words (sg_lim_slots)");
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
@@ -649,9 +657,11 @@ int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base,
     return flow_status(h, *h->h_err);
 }
 
-int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, int64_t t_base, uint32_t n_ms) {
+int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, uint64_t gathered_words, int64_t t_base, uint32_t n_ms) {
     if (!h || !gathered) return SG_E_INVAL;
     if (t_base < 0 || n_ms == 0 || n_ms > kMaxPeriods) return fail(h, SG_E_INVAL, "exchange range: t_base >= 0, 1 <= n_ms <= 65536");
+    if (gathered_words != (uint64_t)h->shard_world * (uint64_t)h->n_lim * n_ms)
+        return fail(h, SG_E_INVAL, "gathered buffer must hold world * n_lim * n_ms words (sg_lim_slots)");
     h->lim_xg = gathered;
     h->lim_xt = t_base;
     h->lim_xn = n_ms;
@@ -785,8 +795,14 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         dfree(d_src);
     }
     if (h->d_cnow) {  // CurrentConcurrencyManager: surviving flowIds keep nowCalls, new ones start at 0
-        std::vector<int32_t> old(h->K);
-        if (h->K) HIP_TRY(h, hipMemcpy(old.data(), h->d_cnow, sizeof(int32_t) * h->K, hipMemcpyDeviceToHost));
+        // the counters in the current rule order: a reload not yet uploaded (cnow_pending) already holds them
+        // remapped to h->K / h->rules; d_cnow is still in the order of the rules before that reload
+        std::vector<int32_t> old(h->K, 0);
+        if (h->cnow_pending) {
+            for (uint32_t k = 0; k < h->K && k < h->cnow_host.size(); ++k) old[k] = h->cnow_host[k];
+        } else if (h->K) {
+            HIP_TRY(h, hipMemcpy(old.data(), h->d_cnow, sizeof(int32_t) * h->K, hipMemcpyDeviceToHost));
+        }
         h->cnow_host.assign(n, 0);
         for (uint32_t i = 0; i < n; ++i)
             if (src[i] >= 0) h->cnow_host[i] = old[src[i]];
@@ -1203,6 +1219,33 @@ int drain_async(sg_handle* h) {
     return SG_OK;
 }
 
+// The sharded limiter's plan over the armed exchange alone (no local batch): every shard's replica of the namespace
+// windows walks the same node arrivals.
+int lim_plan_only(sg_handle* h, hipStream_t stream) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int rc = ensure_layout(h);
+    if (rc) return rc;
+    BatchArgs a{};
+    a.err = h->d_err;
+    LimArgs L{};
+    L.n_lim = h->n_lim;
+    std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
+    L.arrivals = h->d_lim_period;
+    L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
+    L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
+    L.ring = h->d_lim_ring;
+    L.xg = h->lim_xg;
+    L.t_base = h->lim_xt;
+    L.n_ms = h->lim_xn;
+    L.world = h->shard_world;
+    L.rank = h->shard_rank;
+    HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
+    HIP_TRY(h, launch_limiter_plan_only(a, L, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    return SG_OK;
+}
+
 }  // namespace
 
 int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
@@ -1214,32 +1257,17 @@ int sg_flow_decide_batch(sg_handle* h, const sg_req* req, uint64_t n, sg_result*
     h->lim_x_armed = false;  // the exchange is consumed by this call, whatever its outcome
     if (n == 0 && !armed) return SG_OK;
     hipStream_t stream = (hipStream_t)stream_;
-    if (n == 0) {  // no requests on this shard: its replica of the namespace windows still advances
-        HIP_TRY(h, hipSetDevice(h->device));
-        drain_async(h);
-        int rc = ensure_layout(h);
-        if (rc) return rc;
-        BatchArgs a{};
-        a.err = h->d_err;
-        LimArgs L{};
-        L.n_lim = h->n_lim;
-        std::memcpy(L.qps, h->lim_qps, sizeof(L.qps));
-        L.arrivals = h->d_lim_period;
-        L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
-        L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
-        L.ring = h->d_lim_ring;
-        L.xg = h->lim_xg;
-        L.t_base = h->lim_xt;
-        L.n_ms = h->lim_xn;
-        L.world = h->shard_world;
-        L.rank = h->shard_rank;
-        HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
-        HIP_TRY(h, launch_limiter_plan_only(a, L, stream));
-        HIP_TRY(h, hipStreamSynchronize(stream));
-        return SG_OK;
+    // no requests on this shard, or a batch rejected before the device sees it: the shard's replica of the
+    // namespace windows still walks the node's gathered arrivals (the other shards charge them too)
+    const char* early = n == 0 ? "" : (!req || !out) ? "null buffer" : n > h->cfg.max_batch ? "batch larger than max_batch" : nullptr;
+    if (early) {
+        if (armed) {
+            int rc = lim_plan_only(h, stream);
+            if (rc) return rc;
+        }
+        if (n == 0) return SG_OK;
+        return fail(h, (!req || !out) ? SG_E_INVAL : SG_E_CAPACITY, early);
     }
-    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
     h->lim_x_armed = armed;  // read by flow_front

@@ -176,7 +176,12 @@ __device__ void limx_plan(const LimArgs& L) {
 }
 
 __global__ void __launch_bounds__(kLimThreads) k_lim_plan(BatchArgs a, LimArgs L, uint32_t ntiles) {
-    if (*a.err) return;  // a rejected batch leaves the limiter untouched
+    if (*a.err) {
+        // a rejected batch leaves the limiter untouched — except a shard's replica of the node-wide windows,
+        // which walks the gathered node arrivals whatever this shard's batch was (every shard charges them)
+        if (L.xg) limx_plan(L);
+        return;
+    }
     const int tid = threadIdx.x;
     // (1) exclusive scan of per-tile totals, slot by slot (thread-strided partial sums + carry)
     __shared__ uint32_t part[kLimThreads];

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsentinel_gpu.so")  # override: A/B tuning runs
 
 EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_lim_arrivals",
-           "sg_lim_exchange", "sg_load_flow_rules",
+           "sg_lim_exchange", "sg_lim_slots", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_enqueue", "sg_flow_poll", "sg_flow_wait",
            "sg_host_alloc", "sg_host_free", "sg_enable_stats", "sg_get_stats",
            "sg_flow_read_state", "sg_flow_export_state", "sg_flow_import_state", "sg_snapshot_metrics", "sg_snapshot_metrics_device", "sg_snapshot_metrics_enqueue", "sg_debug_copy", "sg_build_info",
@@ -53,8 +53,9 @@ def load_library():
         "sg_last_error": (C.c_char_p, [vp]),
         "sg_set_namespaces": (C.c_int, [vp, vp, u32]),
         "sg_set_shard": (C.c_int, [vp, C.c_int32, C.c_int32]),
-        "sg_lim_arrivals": (C.c_int, [vp, vp, u64, i64, u32, vp, vp]),
-        "sg_lim_exchange": (C.c_int, [vp, vp, i64, u32]),
+        "sg_lim_arrivals": (C.c_int, [vp, vp, u64, i64, u32, vp, u64, vp]),
+        "sg_lim_exchange": (C.c_int, [vp, vp, u64, i64, u32]),
+        "sg_lim_slots": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
         "sg_load_flow_rules": (C.c_int, [vp, vp, u32]),
         "sg_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
@@ -121,6 +122,7 @@ class FlowEngine:
     """One sg_handle: the cluster flow rules of a token server on one GPU."""
 
     def __init__(self, device=0, max_batch=1 << 20, exceed_count=1.0, max_occupy_ratio=1.0, flags=0):
+        self._world = 1
         L = load_library()
         cfg = abi.sg_config(device=device, flags=flags, exceed_count=exceed_count,
                             max_occupy_ratio=max_occupy_ratio, max_batch=max_batch)
@@ -156,16 +158,32 @@ class FlowEngine:
         self._check(self._L.sg_set_namespaces(self.h, abi.ptr(ns), len(ns)))
 
     def set_shard(self, rank: int, world: int):
-        """This handle decides shard `rank` of `world` (refuses namespace QPS limiters when world > 1)."""
+        """This handle decides shard `rank` of `world`. With world > 1 and a namespace QPS limiter every
+        decide_device / decide_host must follow lim_arrivals + lim_exchange (cluster.LimiterExchange); the
+        pipelined submit / enqueue entry points and cluster param batches refuse such a handle."""
         self._check(self._L.sg_set_shard(self.h, rank, world))
+        self._world = world
 
-    def lim_arrivals(self, req_ptr: int, n: int, t_base: int, n_ms: int, counts_ptr: int, stream_ptr: int = 0):
-        """This shard's limited arrivals per (limiter slot, millisecond) into device counts[n_lim][n_ms]."""
-        self._check(self._L.sg_lim_arrivals(self.h, req_ptr, n, t_base, n_ms, counts_ptr, stream_ptr))
+    def lim_slots(self) -> int:
+        """The handle's limiter-slot count n_lim (limiter-enabled namespaces)."""
+        n = C.c_uint32(0)
+        self._check(self._L.sg_lim_slots(self.h, C.byref(n)))
+        return int(n.value)
 
-    def lim_exchange(self, gathered_ptr: int, t_base: int, n_ms: int):
-        """Arm the next flow batch with the node's gathered arrivals (device [world][n_lim][n_ms])."""
-        self._check(self._L.sg_lim_exchange(self.h, gathered_ptr, t_base, n_ms))
+    def lim_arrivals(self, req_ptr: int, n: int, t_base: int, n_ms: int, counts_ptr: int, stream_ptr: int = 0,
+                     counts_words: int = None):
+        """This shard's limited arrivals per (limiter slot, millisecond) into device counts[n_lim][n_ms]
+        (counts_words: the buffer's uint32 count, n_lim * n_ms by default; the library checks it)."""
+        if counts_words is None:
+            counts_words = self.lim_slots() * n_ms
+        self._check(self._L.sg_lim_arrivals(self.h, req_ptr, n, t_base, n_ms, counts_ptr, counts_words, stream_ptr))
+
+    def lim_exchange(self, gathered_ptr: int, t_base: int, n_ms: int, gathered_words: int = None):
+        """Arm the next flow batch with the node's gathered arrivals (device [world][n_lim][n_ms]; gathered_words
+        defaults to world * n_lim * n_ms with the world of set_shard)."""
+        if gathered_words is None:
+            gathered_words = self._world * self.lim_slots() * n_ms
+        self._check(self._L.sg_lim_exchange(self.h, gathered_ptr, gathered_words, t_base, n_ms))
 
     def load_rules(self, rules: np.ndarray):
         rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)

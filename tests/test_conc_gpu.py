@@ -149,6 +149,27 @@ def test_reload_keeps_surviving_counters():
     _check_state(eng, ora, len(new))
 
 
+def test_two_reloads_in_a_row():
+    """Two rule reloads with no concurrent call between them (the counters of the first reload are still
+    host-side when the second remaps them): grow the rule set, then permute it; nowCalls and the releases of the
+    live tokens must follow their flowIds."""
+    rng = np.random.default_rng(6)
+    k = 50
+    rules = _rules(rng, k)
+    eng, ora = _pair(rules)
+    tr = Trace(6, k)
+    _step(eng, ora, tr, tr.batch(6_000, 500))
+    grown = np.concatenate([rules, _rules(rng, 30, fid0=7000)])
+    perm = grown[rng.permutation(len(grown))]
+    for new in (grown, perm):
+        eng.load_rules(new)
+        ora.load_rules(new)
+    tr.k = len(perm)
+    _check_state(eng, ora, len(perm))
+    _step(eng, ora, tr, tr.batch(6_000, 500))
+    _check_state(eng, ora, len(perm))
+
+
 def test_hot_flow_large_batch():
     """One flowId takes most of a 200k-request batch (one lane walks its segment)."""
     rng = np.random.default_rng(5)

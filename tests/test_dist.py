@@ -118,11 +118,15 @@ class _CountingEngine:
     def __init__(self):
         self.calls = []
 
-    def lim_arrivals(self, req_ptr, n, t_base, n_ms, counts_ptr, stream_ptr=0):
+    def lim_slots(self):
+        return 2
+
+    def lim_arrivals(self, req_ptr, n, t_base, n_ms, counts_ptr, stream_ptr=0, counts_words=None):
+        assert counts_words == 2 * n_ms
         self.calls.append(("arrivals", n, t_base, n_ms))
 
-    def lim_exchange(self, gathered_ptr, t_base, n_ms):
-        self.calls.append(("exchange", t_base, n_ms))
+    def lim_exchange(self, gathered_ptr, t_base, n_ms, gathered_words=None):
+        self.calls.append(("exchange", t_base, n_ms, gathered_words))
 
 
 def _xch_worker(rank, world, port, q):
@@ -132,7 +136,7 @@ def _xch_worker(rank, world, port, q):
     try:
         from sentinel_amd.cluster import LimiterExchange
         eng = _CountingEngine()
-        x = LimiterExchange(eng, 2, "cpu")
+        x = LimiterExchange(eng, "cpu")
         # rank r's batch spans [100 + 10 r, 150 + 20 r]; the last rank has no requests in the second batch
         t_first, t_last = 100 + 10 * rank, 150 + 20 * rank
         r1 = x.arm(0, 5, t_first, t_last)
@@ -161,8 +165,9 @@ def test_limiter_exchange_time_range_and_gather(world):
     for rank, r1, r2, calls, shape in res:
         assert r1 == (lo1, hi1 - lo1 + 1)
         assert r2 == (lo2, hi2 - lo2 + 1)
-        assert calls[0] == ("arrivals", 5, lo1, hi1 - lo1 + 1) and calls[1] == ("exchange", lo1, hi1 - lo1 + 1)
-        assert calls[3] == ("exchange", lo2, hi2 - lo2 + 1)
+        assert calls[0] == ("arrivals", 5, lo1, hi1 - lo1 + 1)
+        assert calls[1] == ("exchange", lo1, hi1 - lo1 + 1, world * 2 * (hi1 - lo1 + 1))
+        assert calls[3] == ("exchange", lo2, hi2 - lo2 + 1, world * 2 * (hi2 - lo2 + 1))
         assert shape == (world * 2 * (hi2 - lo2 + 1),)
 
 

@@ -67,7 +67,7 @@ def _worker(rank, world, port, q, limiter=False):
         eng.set_shard(rank, world)
         eng.set_namespaces(_ns(limiter))
         eng.load_rules(rules[shard])
-        xch = LimiterExchange(eng, 1, "cuda:0", coll_device="cpu") if limiter else None
+        xch = LimiterExchange(eng, "cuda:0", coll_device="cpu") if limiter else None
         outs = []
         for req in batches:
             mine, sub = _shard_batch(req, rank, world, local)

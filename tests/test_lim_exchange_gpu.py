@@ -168,3 +168,98 @@ def test_sharded_limiter_contract():
     # the same handle unsharded decides without the exchange
     e.set_shard(0, 1)
     assert len(e.decide_host(req)) == len(req)
+
+
+def test_rejected_shard_batch_keeps_replicas_equal():
+    """A shard whose batch is rejected (a batch out of time order → SG_E_TIME on the device; a null output buffer →
+    SG_E_INVAL before the device) still walks the node's gathered arrivals, so its replica of the namespace windows
+    stays equal to the other shards' and later batches still equal the node replay. The node counted the rejected
+    requests as limiter arrivals, so the oracle replays them against stand-in flows of the same namespaces (huge
+    thresholds, never compared): their flow windows stay untouched, as on the rejecting shard."""
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.engine import EngineError, FlowEngine
+    world = 3
+    rng = np.random.default_rng(77)
+    rules = _rules(rng)
+    ns = _ns(120.0)
+    shards = [shard_flows(N_FLOWS, r, world) for r in range(world)]
+    local = []
+    for s in shards:
+        m = np.full(N_FLOWS, abi.KEY_NO_RULE, np.int64)
+        m[s] = np.arange(len(s))
+        local.append(m)
+    engs = []
+    for r in range(world):
+        e = FlowEngine(device=0, max_batch=1 << 16)
+        e.set_shard(r, world)
+        e.set_namespaces(ns)
+        e.load_rules(rules[shards[r]])
+        engs.append(e)
+    stand_in = np.zeros(3, abi.RULE_DTYPE)  # one per namespace, after the real flows
+    stand_in["flow_id"] = 10_000_000 + np.arange(3)
+    stand_in["count"] = 1e15
+    stand_in["threshold_type"] = abi.THRESHOLD_GLOBAL
+    stand_in["sample_count"], stand_in["window_interval_ms"] = 10, 1000
+    stand_in["namespace_id"] = np.arange(3)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(np.concatenate([rules, stand_in]))
+    dev = torch.device("cuda:0")
+    n_lim = int(ns["limiter_enabled"].sum())
+    reject = {1: (0, "unordered"), 2: (1, "null")}  # node batch → (shard, how)
+    compared = 0
+    for b, req in enumerate(_batches(rng, 1_700_000_000_500)):
+        parts = _split(req, world, local)
+        ts = [p[1]["ts_ms"] for p in parts]
+        t_base = min(int(t[0]) for t in ts if len(t))
+        n_ms = max(int(t[-1]) for t in ts if len(t)) - t_base + 1
+        rr, how = reject.get(b, (-1, None))
+        if rr >= 0 and len(parts[rr][1]) < 3:
+            rr = -1
+        sub_r = parts[rr][1].copy() if rr >= 0 else None
+        if how == "unordered":  # swap the first and last timestamps: same per-millisecond counts
+            sub_r["ts_ms"][[0, -1]] = sub_r["ts_ms"][[-1, 0]]
+        subs = [sub_r if r == rr else parts[r][1] for r in range(world)]
+        reqs_d = [torch.from_numpy(s.view(np.uint8).copy()).to(dev) for s in subs]
+        counts = []
+        for r in range(world):
+            c = torch.zeros(n_lim * n_ms, dtype=torch.int32, device=dev)
+            engs[r].lim_arrivals(reqs_d[r].data_ptr() if len(subs[r]) else 0, len(subs[r]), t_base, n_ms, c.data_ptr())
+            counts.append(c)
+        gathered = torch.cat(counts)
+        torch.cuda.synchronize()
+        got = []
+        for r in range(world):
+            n = len(subs[r])
+            out = torch.zeros(max(1, n) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+            engs[r].lim_exchange(gathered.data_ptr(), t_base, n_ms)
+            if r == rr:
+                with pytest.raises(EngineError) as ei:
+                    engs[r].decide_device(reqs_d[r].data_ptr(), n, 0 if how == "null" else out.data_ptr())
+                assert ei.value.code == (abi.SG_E_INVAL if how == "null" else abi.SG_E_TIME)
+                got.append(None)
+            else:
+                engs[r].decide_device(reqs_d[r].data_ptr() if n else 0, n, out.data_ptr())
+                got.append(out.cpu().numpy().view(abi.RES_DTYPE)[:n])
+        node_req = req.copy()
+        if rr >= 0:  # the rejected shard's valid requests → the stand-in flow of their namespace
+            mine = parts[rr][0]
+            k = (node_req["key"][mine] & abi.KEY_INDEX).astype(np.int64)
+            ok = (k < N_FLOWS) & (node_req["acquire"][mine] > 0)
+            nsid = rules["namespace_id"][np.where(ok, k, 0)]
+            node_req["key"][mine[ok]] = (N_FLOWS + nsid[ok]).astype(np.uint32) | \
+                (node_req["key"][mine[ok]] & np.uint32(abi.KEY_PRIO))
+        cat_idx = np.concatenate([p[0] for p in parts])
+        perm = node_order(ts)
+        want_node = ora.decide(node_req[cat_idx[perm]])
+        want = np.empty_like(want_node)
+        want[perm] = want_node
+        off = 0
+        for r in range(world):
+            n = len(parts[r][1])
+            if got[r] is not None:
+                bad = np.nonzero(got[r] != want[off:off + n])[0]
+                assert len(bad) == 0, f"batch {b} shard {r}: {len(bad)} of {n} differ"
+                compared += n
+            off += n
+    assert compared > 0
