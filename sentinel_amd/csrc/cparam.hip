@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(256) k_cp_limprep(CPArgs c, BatchArgs a) {
         }
         if (i == c.n - 1) {
             const int64_t qq = t / 100 - t0 / 100 + 1;
-            a.np[0] = qq > (int64_t)kMaxPeriods ? kMaxPeriods : (uint32_t)qq;
+            a.np[0] = qq > (int64_t)kMaxPeriods ? kMaxPeriods : qq < 1 ? 1u : (uint32_t)qq;  // < 1: out of order
         }
         a.rec[i] = cp_valid(c, q) ? (((uint64_t)(q.key & SG_KEY_INDEX) << a.kshift) | i) : sentinel;
     }

@@ -130,6 +130,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
                     const int64_t P0 = t0 / wl, Pp = tp / wl, Pi = t / wl;
                     for (int64_t p = Pp + 1; p <= Pi; ++p) {
                         const int64_t q = p - P0;
+                        if (q <= 0) continue;  // an out-of-order batch (kErrTime already set by an earlier index)
                         if (q >= (int64_t)kMaxPeriods) {
                             atomicOr(a.err, kErrPeriods);
                             break;
@@ -142,7 +143,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         if (i == n - 1) {
             for (int w = 0; w < a.n_wl; ++w) {
                 const int64_t q = t / a.wl[w] - t0 / a.wl[w] + 1;
-                a.np[w] = q > (int64_t)kMaxPeriods ? kMaxPeriods : (uint32_t)q;
+                a.np[w] = q > (int64_t)kMaxPeriods ? kMaxPeriods : q < 1 ? 1u : (uint32_t)q;  // < 1: out of order
             }
         }
         const uint32_t res = e.resource & SG_KEY_INDEX;

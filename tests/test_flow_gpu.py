@@ -206,6 +206,13 @@ def test_timestamp_violations_rejected_without_side_effects():
     unsorted["ts_ms"][500] -= 300
     with pytest.raises(EngineError):
         eng.decide_host(unsorted)
+    # the first request later than the rest by many window periods: every later period lies before the batch's
+    # first one (the period tables must not be written below their start)
+    first_late = _trace(rng, 1000, 10, 1_700_000_002_000, 1000)
+    first_late["ts_ms"][0] += 20_000
+    with pytest.raises(EngineError) as ei:
+        eng.decide_host(first_late)
+    assert ei.value.code == abi.SG_E_TIME
     _compare_state(eng, ora, rules)
     nxt = _trace(rng, 1000, 10, 1_700_000_003_000, 1000)
     _compare_results(ora.decide(nxt), eng.decide_host(nxt), nxt)

@@ -171,6 +171,11 @@ def test_timestamps_rejected():
     with pytest.raises(EngineError) as ei:
         eng.local_decide_host(ev)
     assert ei.value.code == abi.SG_E_TIME
+    # the first event later than the rest by many periods (below the period tables' start)
+    ev["ts_ms"] = [90_000, 900, 1100]
+    with pytest.raises(EngineError) as ei:
+        eng.local_decide_host(ev)
+    assert ei.value.code == abi.SG_E_TIME
 
 
 @pytest.mark.parametrize("flags", [0, abi.FLAG_WAVE_ONLY, abi.FLAG_SERIAL_ONLY])
