@@ -336,6 +336,7 @@ typedef struct sg_local_event {
 #define SG_LOCAL_BLOCK_FLOW    1  /* FlowException                                            */
 #define SG_LOCAL_BLOCK_DEGRADE 2  /* DegradeException                                         */
 #define SG_LOCAL_PASS_WAIT     3  /* PriorityWaitException: passes after wait_ms              */
+                                  /* 4: SG_LOCAL_BLOCK_PARAM (sg_slot_decide_batch, below)     */
 typedef struct sg_local_result {
     int32_t status;               /* entries: SG_LOCAL_*; exits: 0                            */
     int32_t wait_ms;
@@ -360,18 +361,41 @@ typedef struct sg_local_config {
 #define SG_CONTROL_WARM_UP_RATE_LIMITER  3  /* WarmUpRateLimiterController                            */
 #define SG_LIMIT_APP_DEFAULT   0            /* limitApp "default": the resource's ClusterNode         */
 #define SG_LIMIT_APP_OTHER   (-1)           /* limitApp "other": origins no rule of the resource names */
-#define SG_STRATEGY_DIRECT     0            /* RELATE / CHAIN read other nodes: SG_E_UNSUPPORTED      */
+#define SG_STRATEGY_DIRECT     0            /* RuleConstant.STRATEGY_DIRECT: the node limitApp selects      */
+#define SG_STRATEGY_RELATE     1            /* STRATEGY_RELATE: the ClusterNode of resource ref_resource     */
+#define SG_STRATEGY_CHAIN      2            /* STRATEGY_CHAIN: the resource's DefaultNode of context ref_resource,
+                                               only for entries in that context                             */
+/* FlowRule.clusterMode with its ClusterFlowConfig (FlowRuleChecker.passClusterCheck :147-164). The device decides
+ * cluster-mode rules as a node whose ClusterStateManager is neither client nor server (the default,
+ * CLUSTER_NOT_STARTED): pickClusterService() is null, so fallbackToLocalOrPass (:166-175) applies. */
+#define SG_CLUSTER_MODE_OFF         0       /* a local rule                                                 */
+#define SG_CLUSTER_MODE_FALLBACK    1       /* clusterMode, fallbackToLocalWhenFail: checked as a local rule  */
+#define SG_CLUSTER_MODE_NO_FALLBACK 2       /* clusterMode without fallback: the rule is not activated (pass) */
+#define SG_CLUSTER_MODE_INVALID   (-1)      /* clusterMode with an invalid ClusterFlowConfig
+                                               (FlowRuleUtil.checkClusterField :197-215): ignored at load   */
 typedef struct sg_local_flow_rule {
     uint32_t resource;            /* resource index (sg_local_load_rules order)                    */
     int32_t  grade;               /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS                        */
     double   count;
     int32_t  control_behavior;    /* SG_CONTROL_*                                                 */
     int32_t  limit_app;           /* SG_LIMIT_APP_DEFAULT, SG_LIMIT_APP_OTHER or an origin id > 0   */
-    int32_t  strategy;            /* SG_STRATEGY_DIRECT                                           */
+    int32_t  strategy;            /* SG_STRATEGY_*                                                */
     int32_t  warm_up_period_sec;  /* warmUpPeriodSec, default 10                                  */
     int32_t  max_queueing_ms;     /* maxQueueingTimeMs, default 500                               */
-    int32_t  reserved;
+    int32_t  ref_resource;        /* RELATE: resource index; CHAIN: context id; < 0: refResource blank */
+    int32_t  cluster_mode;        /* SG_CLUSTER_MODE_*                                            */
+    int32_t  cluster_config;      /* the caller's id of the ClusterFlowConfig value (FlowRule.equals
+                                     compares it; 0 = none)                                       */
 } sg_local_flow_rule;
+
+/* ClusterStateManager state of the node (ClusterStateManager.java: CLUSTER_CLIENT 0, CLUSTER_SERVER 1,
+ * CLUSTER_NOT_STARTED -1). Only NOT_STARTED is decided on the device; with CLIENT / SERVER, cluster-mode rules go
+ * through a token service the batch cannot call in order, so loading them (or setting such a state while they
+ * are loaded) is SG_E_UNSUPPORTED. */
+#define SG_CLUSTER_CLIENT        0
+#define SG_CLUSTER_SERVER        1
+#define SG_CLUSTER_NOT_STARTED (-1)
+int sg_local_set_cluster_state(sg_handle* h, int32_t state);
 
 /* Per-call timing of the last sg_flow_decide_batch (device time, HIP events on the call's stream). */
 typedef struct sg_batch_stats {
@@ -562,16 +586,62 @@ int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* bo
  *                              :83-130): replaces every resource's flow rules. Invalid rules are ignored as the
  *                              reference ignores them (FlowRuleUtil.isValidRule :167-251), duplicates are dropped
  *                              (its HashSet), and each resource's rules are stably sorted by FlowRuleComparator
- *                              (FlowRuleComparator.java:30-55: specific/other limitApps before "default"). Fresh
- *                              controllers (warm-up tokens 0, latestPassedTime -1); resource statistics are kept.
- *                              n_origins: the largest origin id events may carry. Resources with a limitApp other
- *                              than "default" keep one origin StatisticNode per origin id (ClusterNode
- *                              .getOrCreateOriginNode), which starts empty at every load. Returns the number of
- *                              rules kept (>= 0) or an error.
- *   sg_local_read_origin_state ← that origin node: same layout as sg_local_read_state (head[0] = curThreadNum).
+ *                              (FlowRuleComparator.java:30-55: local rules before cluster-mode ones, specific /
+ *                              other limitApps before "default"). Fresh controllers (warm-up tokens 0,
+ *                              latestPassedTime -1); resource statistics are kept. Returns the number of rules kept
+ *                              (>= 0) or an error.
+ *                              n_origins: the largest origin id events may carry; n_contexts: context ids events may
+ *                              carry are 0 .. n_contexts - 1 (sg_slot_ext.context; 0 when no ext). Origin and context
+ *                              ids are the caller's dense ids of the Context origin / name strings and must keep
+ *                              their meaning across loads (neither count may shrink).
+ *                              Nodes besides the ClusterNodes: a resource whose rules name an origin (a limitApp
+ *                              other than "default") keeps an origin StatisticNode per origin id
+ *                              (ClusterNode.getOrCreateOriginNode), and one with a CHAIN rule a DefaultNode per
+ *                              context id (NodeSelectorSlot's per-context node). They are created empty at the
+ *                              first load that needs them and then kept across every later load (ClusterNode
+ *                              .originCountMap and the DefaultNodes outlive rule reloads); the reference creates
+ *                              them at the resource's first entry with that origin / in that context, so traffic
+ *                              before that load is the one difference. A RELATE rule joins its
+ *                              resource and ref_resource into one key group walked in event order (the read of
+ *                              another resource's ClusterNode, FlowRuleChecker.selectReferenceNode :96-112); a
+ *                              resource never entered has no ClusterNode yet (ClusterBuilderSlot), and the rule
+ *                              then passes.
+ *   sg_local_read_origin_state  ← that origin node: same layout as sg_local_read_state (head[0] = curThreadNum).
+ *   sg_local_read_context_state ← the DefaultNode of (resource, context): same layout.
  *   sg_local_read_controller   ← the controller of input rule i: {storedTokens, lastFilledTime, latestPassedTime};
  *                              SG_E_INVAL for an ignored rule. */
-int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins);
+int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
+                             int32_t n_contexts);
+
+/* ---- the whole slot chain in one batch (the ProcessorSlot chain's SPI order, Constants.java:76-83 and
+ * ParamFlowSlot @Spi(order = -3000)): StatisticSlot.entry around ParamFlowSlot → FlowSlot → DegradeSlot.
+ *   sg_slot_decide_batch ← SphU.entry(resource, count, prioritized, args...) / Entry.exit(count, args...) for a
+ *     time-ordered batch. Per entry: ParamFlowSlot.checkFlow (the param rules sg_pslot_load_rules loaded for the
+ *     resource, args of the event; args_null or no rules: nothing) — a ParamFlowException ends the chain
+ *     (SG_LOCAL_BLOCK_PARAM, wait_ms = the index of the param rule that threw); FlowSlot (the flow rules above);
+ *     DegradeSlot; then StatisticSlot (StatisticSlot.java:55-122): a pass raises curThreadNum and PASS on the
+ *     ClusterNode, the origin node and the DefaultNode and runs ParamFlowStatisticEntryCallback.onPass (the param
+ *     thread counts of the args, ParameterMetric.addThreadCount); a PriorityWaitException raises the thread counts
+ *     and runs onPass; any BlockException — ParamFlowException included — adds BLOCK to those nodes. Exit
+ *     (StatisticSlot.exit :124-165, passed entries only): RT / success / exception and curThreadNum on the nodes,
+ *     ParamFlowStatisticExitCallback (decreaseThreadCount of the exit's args), DegradeSlot.exit.
+ *     ext[i] (nullable: every event in context 0 with null args) carries the event's context and arguments; args,
+ *     values and ext are DEVICE pointers like ev and out. sg_local_decide_batch = this call with ext = NULL. */
+typedef struct sg_slot_ext {
+    uint32_t context;             /* Context name id (0 .. n_contexts - 1); CHAIN rules select by it              */
+    uint32_t arg_begin;           /* the event's args: args[arg_begin .. + arg_count)                           */
+    uint32_t arg_count;
+    int32_t  args_null;           /* 1: Object[] args is null (ParamFlowSlot.checkFlow returns at once)          */
+} sg_slot_ext;
+#define SG_LOCAL_BLOCK_PARAM   4  /* ParamFlowException (result wait_ms: the index of the param rule that threw) */
+int sg_slot_decide_batch(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                         const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values,
+                         sg_local_result* out, void* stream);
+int sg_slot_decide_batch_host(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                              const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values,
+                              sg_local_result* out);
+int sg_local_read_context_state(sg_handle* h, uint32_t res, int32_t context, int64_t* second, int64_t* borrow,
+                                int64_t* minute, int64_t* head);
 
 /* ---- metric snapshots ----
  *   sg_local_metrics ← MetricTimerListener.run (core/.../node/metric/MetricTimerListener.java:40-69) over every

@@ -85,7 +85,11 @@ def lib():
         "or_cpm_add": (None, [vp, i64, u64, C.c_int]), "or_cpm_get_sum": (i64, [vp, i64, u64]),
         "or_cpm_get_avg": (C.c_double, [vp, i64, u64]),
         "or_local_breaker_stat": (C.c_int, [vp, u32, C.c_int, vp, vp, vp]),
-        "or_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32]),
+        "or_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
+        "or_local_decide_ext": (C.c_int, [vp, vp, vp, u64, vp, vp, vp]),
+        "or_local_attach_pslot": (None, [vp, vp]),
+        "or_local_context_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
+        "or_lgen_run_ext": (u64, [vp, vp, vp, vp, vp, u64, i64, vp, vp, vp, u64, vp, vp]),
         "or_local_set_cold_factor": (None, [vp, C.c_int]),
         "or_local_origin_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
         "or_local_controller": (C.c_int, [vp, u32, vp]),
@@ -109,7 +113,7 @@ def lib():
         "or_ctl_warning_token": (C.c_int32, [vp]), "or_ctl_max_token": (C.c_int32, [vp]),
         "or_warm_can_pass": (C.c_int, [vp, i64, d, d, C.c_int]),
         "or_warm_rl_can_pass": (C.c_int, [vp, i64, d, C.c_int, vp]),
-        "or_select_node": (C.c_int, [vp, u32, u32, C.c_int]),
+        "or_select_node": (C.c_int, [vp, u32, u32, C.c_int, C.c_int, C.c_int]),
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
         "or_rls_decide": (C.c_int, [vp, vp, u64, vp]),
@@ -575,12 +579,15 @@ def degrade_rule(grade, count, time_window_sec, min_request_amount=5, stat_inter
 
 
 def local_flow_rule(resource=0, count=0.0, grade=abi.FLOW_GRADE_QPS, behavior=abi.CONTROL_DEFAULT,
-                    limit_app=abi.LIMIT_APP_DEFAULT, warm_up_sec=10, max_queueing_ms=500, strategy=abi.STRATEGY_DIRECT):
-    """sg_local_flow_rule: FlowRule defaults (FlowRule.java: warmUpPeriodSec 10, maxQueueingTimeMs 500)."""
+                    limit_app=abi.LIMIT_APP_DEFAULT, warm_up_sec=10, max_queueing_ms=500, strategy=abi.STRATEGY_DIRECT,
+                    ref=-1, cluster_mode=abi.CLUSTER_MODE_OFF, cluster_config=0):
+    """sg_local_flow_rule: FlowRule defaults (FlowRule.java: warmUpPeriodSec 10, maxQueueingTimeMs 500; refResource
+    null = -1; clusterMode false)."""
     r = np.zeros((), abi.LOCAL_FLOW_RULE_DTYPE)
     r["resource"], r["grade"], r["count"], r["control_behavior"] = resource, grade, count, behavior
     r["limit_app"], r["strategy"], r["warm_up_period_sec"], r["max_queueing_ms"] = (limit_app, strategy, warm_up_sec,
                                                                                    max_queueing_ms)
+    r["ref_resource"], r["cluster_mode"], r["cluster_config"] = ref, cluster_mode, cluster_config
     return r
 
 
@@ -620,10 +627,11 @@ class Controller:
         return lib().or_ctl_max_token(self.h)
 
 
-def select_node(rules, i, origin):
-    """FlowRuleChecker.selectNodeByRequesterAndStrategy: 0 ClusterNode, 1 origin node, None."""
+def select_node(rules, i, origin, context=0, ref_exists=True):
+    """FlowRuleChecker.selectNodeByRequesterAndStrategy / selectReferenceNode: 0 ClusterNode, 1 origin node,
+    2 the DefaultNode of the context (CHAIN), 3 the referenced ClusterNode (RELATE), None."""
     rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
-    r = lib().or_select_node(abi.ptr(rules), len(rules), i, origin)
+    r = lib().or_select_node(abi.ptr(rules), len(rules), i, origin, context, 1 if ref_exists else 0)
     return None if r < 0 else r
 
 
@@ -653,10 +661,10 @@ class LocalChain:
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
         assert lib().or_local_load_rules(self.h, abi.ptr(rules), len(rules)) == 0
 
-    def load_flow_rules(self, rules, n_origins=0):
+    def load_flow_rules(self, rules, n_origins=0, n_contexts=0):
         """FlowRuleManager.loadRules: returns the number of rules kept."""
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
-        rc = lib().or_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins)
+        rc = lib().or_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins, n_contexts)
         if rc < 0:
             raise ValueError(f"or_local_load_flow_rules: {rc}")
         return rc
@@ -679,6 +687,38 @@ class LocalChain:
         e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
         e[0] = (t, create_ts, res, count, abi.LOCAL_EXIT_ERROR if error else abi.LOCAL_EXIT, origin)
         self.decide(e)
+
+    def attach_params(self, pslot):
+        """The ParamFlowSlot of the chain: a ParamSlot whose rules name this chain's resources."""
+        self._ps = pslot
+        lib().or_local_attach_pslot(self.h, pslot.h)
+
+    def decide_ext(self, events, ext, args, values):
+        """The whole slot chain (sg_slot_decide_batch): events with their context / argument records."""
+        ev = np.ascontiguousarray(events, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        ext = np.ascontiguousarray(ext, dtype=abi.SLOT_EXT_DTYPE).reshape(-1)
+        args = np.ascontiguousarray(args, dtype=abi.PSLOT_ARG_DTYPE).reshape(-1)
+        values = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1)
+        if len(args) == 0:
+            args = np.zeros(1, abi.PSLOT_ARG_DTYPE)
+        if len(values) == 0:
+            values = np.zeros(1, np.uint64)
+        out = np.zeros(len(ev), abi.LOCAL_RES_DTYPE)
+        rc = lib().or_local_decide_ext(self.h, abi.ptr(ev), abi.ptr(ext), len(ev), abi.ptr(args), abi.ptr(values),
+                                       abi.ptr(out))
+        if rc != 0:
+            raise ValueError(f"or_local_decide_ext: {rc}")
+        return out
+
+    def context_dump(self, res, context):
+        """(second, borrow, minute, threads, exists) of the DefaultNode of (res, context)."""
+        sec = np.zeros((self.S, 8), np.int64)
+        bor = np.zeros((self.S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        th = C.c_int64()
+        rc = lib().or_local_context_dump(self.h, res, context, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), C.byref(th))
+        assert rc >= 0
+        return sec, bor, mnt, th.value, rc == 1
 
     def origin_dump(self, res, origin):
         """(second, borrow, minute, threads, exists) of the origin node of (res, origin)."""
@@ -770,6 +810,25 @@ class LocalTraceGen:
                               abi.ptr(out), abi.ptr(res), cap)
         assert k != 2**64 - 1
         return out[:k].copy(), res[:k].copy()
+
+    def run_ext(self, entries, ext, rt, err, t_end, args, values):
+        """run() for the whole slot chain: each entry's context / argument record (ext) travels to its exit; args /
+        values are the argument pool the records index (the same pool for every call)."""
+        entries = np.ascontiguousarray(entries, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        ext = np.ascontiguousarray(ext, dtype=abi.SLOT_EXT_DTYPE).reshape(-1)
+        rt = np.ascontiguousarray(rt, dtype=np.int32)
+        err = np.ascontiguousarray(err, dtype=np.uint8)
+        args = np.ascontiguousarray(args, dtype=abi.PSLOT_ARG_DTYPE).reshape(-1)
+        values = np.ascontiguousarray(values, dtype=np.uint64).reshape(-1)
+        cap = 2 * len(entries) + self.pending() + 16
+        out = np.zeros(cap, abi.LOCAL_EVENT_DTYPE)
+        xo = np.zeros(cap, abi.SLOT_EXT_DTYPE)
+        res = np.zeros(cap, abi.LOCAL_RES_DTYPE)
+        k = lib().or_lgen_run_ext(self.h, abi.ptr(entries), abi.ptr(ext), abi.ptr(rt), abi.ptr(err), len(entries),
+                                  int(t_end), abi.ptr(out), abi.ptr(xo), abi.ptr(res), cap, abi.ptr(args),
+                                  abi.ptr(values))
+        assert k != 2**64 - 1
+        return out[:k].copy(), xo[:k].copy(), res[:k].copy()
 
 
 # ---- token-server wire codec (DefaultRequestEntityDecoder / FlowRequestDataDecoder / DefaultResponseEntityWriter)

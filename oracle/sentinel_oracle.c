@@ -889,7 +889,13 @@ typedef struct or_node {
     or_breaker cb[2];
     or_ctl* ctl;      /* the resource's flow rules in FlowRuleComparator order */
     uint32_t n_ctl;
-    struct or_node** origin;  /* ClusterNode.originCountMap: [n_origins + 1], created on first use */
+    int created;      /* ClusterBuilderSlot created the ClusterNode (the resource's first entry)                 */
+    struct or_node** origin;  /* ClusterNode.originCountMap: [n_origins + 1], created on first use, kept across
+                                 rule reloads */
+    int32_t origin_cap;       /* entries of origin[] */
+    struct or_node** ctxn;    /* NodeSelectorSlot's DefaultNode per context id: [ctx_cap], created at the first
+                                 event in the context */
+    int32_t ctx_cap;
 } or_node;
 
 struct or_local {
@@ -897,9 +903,10 @@ struct or_local {
     or_node* nodes;
     uint32_t n;
     int64_t* last_fetch;     /* StatisticNode.lastFetchTime per resource (metrics()) */
-    int32_t n_origins;
+    int32_t n_origins, n_contexts;
     int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
     uint32_t n_rules;
+    struct or_pslot* ps;     /* ParamFlowSlot's rules and metrics (or_local_attach_pslot), NULL = none */
 };
 
 or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms) {
@@ -920,16 +927,23 @@ static or_node* node_new_plain(or_local* l) {
     return o;
 }
 
+static void free_plain(or_node* x) {
+    if (!x) return;
+    or_leap_free(x->second);
+    or_leap_free(x->minute);
+    free(x);
+}
+
 static void free_origins(or_local* l, or_node* nd) {
-    if (!nd->origin) return;
-    for (int32_t o = 0; o <= l->n_origins; o++) {
-        if (!nd->origin[o]) continue;
-        or_leap_free(nd->origin[o]->second);
-        or_leap_free(nd->origin[o]->minute);
-        free(nd->origin[o]);
-    }
+    (void)l;
+    for (int32_t o = 0; o < nd->origin_cap; o++) free_plain(nd->origin[o]);
     free(nd->origin);
     nd->origin = NULL;
+    nd->origin_cap = 0;
+    for (int32_t c = 0; c < nd->ctx_cap; c++) free_plain(nd->ctxn[c]);
+    free(nd->ctxn);
+    nd->ctxn = NULL;
+    nd->ctx_cap = 0;
 }
 
 static void free_nodes(or_local* l) {
@@ -973,11 +987,14 @@ static void ctl_init(or_ctl* c, const sg_local_flow_rule* r, int cold, int32_t i
     }
 }
 
-/* FlowRuleUtil.isValidRule (:167-182) for DIRECT rules outside cluster mode: count >= 0, grade THREAD/QPS,
- * behaviour >= 0; QPS rules: checkControlBehaviorField (:240-251). */
+/* FlowRuleUtil.isValidRule (:167-251): count >= 0, grade / strategy / behaviour >= 0; QPS rules: checkClusterField
+ * (an invalid ClusterFlowConfig), checkStrategyField (RELATE / CHAIN need a refResource) and
+ * checkControlBehaviorField; THREAD rules: checkClusterConcurrentField. */
 static int flow_rule_valid(const sg_local_flow_rule* r) {
     if (!(r->count >= 0) || r->grade < 0 || r->strategy < 0 || r->control_behavior < 0) return 0;
     if (r->grade == 1) {
+        if (r->cluster_mode == SG_CLUSTER_MODE_INVALID) return 0;
+        if ((r->strategy == SG_STRATEGY_RELATE || r->strategy == SG_STRATEGY_CHAIN) && r->ref_resource < 0) return 0;
         switch (r->control_behavior) {
         case SG_CONTROL_WARM_UP: return r->warm_up_period_sec > 0;
         case SG_CONTROL_RATE_LIMITER: return r->max_queueing_ms > 0;
@@ -985,27 +1002,30 @@ static int flow_rule_valid(const sg_local_flow_rule* r) {
         default: return 1;
         }
     }
-    return r->grade == 0;
+    return r->grade == 0 && r->cluster_mode != SG_CLUSTER_MODE_INVALID;
 }
 
-/* FlowRule.equals over the fields the ABI carries (the reference's HashSet drops duplicates, :109-117) */
+/* FlowRule.equals (FlowRule.java, AbstractRule.equals) over the fields the ABI carries (the reference's HashSet
+ * drops duplicates, FlowRuleUtil.java:109-117); Double.compare on count */
 static int flow_rule_same(const sg_local_flow_rule* a, const sg_local_flow_rule* b) {
-    return a->resource == b->resource && a->grade == b->grade && a->count == b->count &&
+    return a->resource == b->resource && a->grade == b->grade && memcmp(&a->count, &b->count, sizeof(double)) == 0 &&
            a->control_behavior == b->control_behavior && a->limit_app == b->limit_app && a->strategy == b->strategy &&
-           a->warm_up_period_sec == b->warm_up_period_sec && a->max_queueing_ms == b->max_queueing_ms;
+           a->warm_up_period_sec == b->warm_up_period_sec && a->max_queueing_ms == b->max_queueing_ms &&
+           (a->ref_resource < 0 ? b->ref_resource < 0 : a->ref_resource == b->ref_resource) &&
+           (a->cluster_mode != 0) == (b->cluster_mode != 0) &&
+           (a->cluster_mode == 0 || (a->cluster_mode == b->cluster_mode && a->cluster_config == b->cluster_config));
 }
 
-int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins) {
-    for (uint32_t i = 0; i < n; i++)
-        if (rules[i].strategy != SG_STRATEGY_DIRECT && flow_rule_valid(&rules[i])) return SG_E_UNSUPPORTED;
-    if (n_origins < 0) return SG_E_INVAL;
-    for (uint32_t k = 0; k < l->n; k++) {
+int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
+                             int32_t n_contexts) {
+    if (n_origins < l->n_origins || n_contexts < l->n_contexts) return SG_E_INVAL;   /* ids keep their meaning */
+    for (uint32_t k = 0; k < l->n; k++) {   /* the origin / context nodes stay (they outlive rule reloads) */
         free(l->nodes[k].ctl);
         l->nodes[k].ctl = NULL;
         l->nodes[k].n_ctl = 0;
-        free_origins(l, &l->nodes[k]);
     }
     l->n_origins = n_origins;
+    l->n_contexts = n_contexts;
     free(l->rule_pos);
     l->rule_pos = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
     l->n_rules = n;
@@ -1015,6 +1035,7 @@ int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint3
         const sg_local_flow_rule* r = &rules[i];
         if (r->resource >= l->n || !flow_rule_valid(r)) continue;   /* ignored, as RecordLog.warn + continue */
         if (r->limit_app > n_origins) { free(cnt); return SG_E_INVAL; }
+        if (r->strategy == SG_STRATEGY_CHAIN && r->ref_resource >= n_contexts) { free(cnt); return SG_E_INVAL; }
         int dup = 0;
         for (uint32_t j = 0; j < i && !dup; j++) dup = l->rule_pos[j] >= 0 && flow_rule_same(&rules[j], r);
         if (dup) continue;
@@ -1023,12 +1044,14 @@ int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint3
     }
     for (uint32_t k = 0; k < l->n; k++)
         if (cnt[k]) l->nodes[k].ctl = (or_ctl*)calloc(cnt[k], sizeof(or_ctl));
-    /* Collections.sort(rules, FlowRuleComparator): stable; non-"default" limitApps first (:30-55) */
-    for (int pass = 0; pass < 2; pass++) {
+    /* Collections.sort(rules, FlowRuleComparator): stable; local rules before cluster-mode ones, then non-"default"
+     * limitApps before "default" (:30-55) */
+    for (int pass = 0; pass < 4; pass++) {
         for (uint32_t i = 0; i < n; i++) {
             if (l->rule_pos[i] < 0) continue;
-            const int is_default = rules[i].limit_app == SG_LIMIT_APP_DEFAULT;
-            if (is_default != pass) continue;
+            const int key = (rules[i].cluster_mode != SG_CLUSTER_MODE_OFF ? 2 : 0) +
+                            (rules[i].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
+            if (key != pass) continue;
             or_node* nd = &l->nodes[rules[i].resource];
             ctl_init(&nd->ctl[nd->n_ctl], &rules[i], l->cold_factor, (int32_t)i);
             l->rule_pos[i] = (int32_t)((rules[i].resource << 16) | nd->n_ctl);
@@ -1046,6 +1069,7 @@ int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
     l->nodes = (or_node*)calloc(n ? n : 1, sizeof(or_node));
     l->n = n;
     l->n_origins = 0;
+    l->n_contexts = 0;
     for (uint32_t i = 0; i < n; i++) {
         or_node* nd = &l->nodes[i];
         nd->rule = rules[i];
@@ -1219,33 +1243,58 @@ static int is_other_origin(const or_node* nd, int origin) {
     return 1;
 }
 
-/* FlowRuleChecker.selectNodeByRequesterAndStrategy (FlowRuleChecker.java:115-145), DIRECT strategy:
- * 0 the ClusterNode, 1 the origin node, -1 none (the rule passes) */
-static int select_node(const or_node* nd, const sg_local_flow_rule* r, int origin) {
-    if (origin > 0 && r->limit_app == origin) return 1;   /* limitApp.equals(origin) && filterOrigin(origin) */
-    if (r->limit_app == SG_LIMIT_APP_DEFAULT) return 0;
-    if (r->limit_app == SG_LIMIT_APP_OTHER && is_other_origin(nd, origin)) return 1;
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy (FlowRuleChecker.java:115-145) with selectReferenceNode
+ * (:96-112): 0 the ClusterNode, 1 the origin node, 2 the resource's DefaultNode of the current context (CHAIN),
+ * 3 the ClusterNode of ref_resource (RELATE), -1 none (the rule passes). ref_exists: that ClusterNode exists. */
+static int select_kind(const or_node* nd, const sg_local_flow_rule* r, int origin, int context, int ref_exists) {
+    int matched;   /* 1: limitApp is the origin / "other" (origin node for DIRECT), 0: "default" */
+    if (origin > 0 && r->limit_app == origin) matched = 1;   /* limitApp.equals(origin) && filterOrigin(origin) */
+    else if (r->limit_app == SG_LIMIT_APP_DEFAULT) matched = 0;
+    else if (r->limit_app == SG_LIMIT_APP_OTHER && is_other_origin(nd, origin)) matched = 1;
+    else return -1;
+    if (r->strategy == SG_STRATEGY_DIRECT) return matched ? 1 : 0;
+    if (r->ref_resource < 0) return -1;                         /* StringUtil.isEmpty(refResource) */
+    if (r->strategy == SG_STRATEGY_RELATE) return ref_exists ? 3 : -1;   /* ClusterBuilderSlot.getClusterNode */
+    if (r->strategy == SG_STRATEGY_CHAIN) return r->ref_resource == context ? 2 : -1;
     return -1;
 }
 
-/* For the FlowRuleCheckerTest restatement: the rules of one resource and a request origin. */
-int or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin) {
+/* For the FlowRuleCheckerTest restatement: the rules of one resource, a request origin / context, and whether the
+ * RELATE target's ClusterNode exists. */
+int or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin, int context, int ref_exists) {
     or_node nd;
     memset(&nd, 0, sizeof(nd));
     or_ctl* c = (or_ctl*)calloc(n ? n : 1, sizeof(or_ctl));
     for (uint32_t j = 0; j < n; j++) c[j].rule = rules[j];
     nd.ctl = c;
     nd.n_ctl = n;
-    int r = select_node(&nd, &rules[i], origin);
+    int r = select_kind(&nd, &rules[i], origin, context, ref_exists);
     free(c);
     return r;
 }
 
 static or_node* origin_node(or_local* l, or_node* nd, int origin) {   /* ClusterNode.getOrCreateOriginNode */
     if (origin <= 0 || origin > l->n_origins) return NULL;
-    if (!nd->origin) nd->origin = (or_node**)calloc((size_t)l->n_origins + 1, sizeof(or_node*));
+    if (origin >= nd->origin_cap) {
+        const int32_t cap = l->n_origins + 1;
+        nd->origin = (or_node**)realloc(nd->origin, (size_t)cap * sizeof(or_node*));
+        for (int32_t o = nd->origin_cap; o < cap; o++) nd->origin[o] = NULL;
+        nd->origin_cap = cap;
+    }
     if (!nd->origin[origin]) nd->origin[origin] = node_new_plain(l);
     return nd->origin[origin];
+}
+
+static or_node* context_node(or_local* l, or_node* nd, int context) {   /* NodeSelectorSlot: DefaultNode per context */
+    if (context < 0 || context >= l->n_contexts) return NULL;
+    if (context >= nd->ctx_cap) {
+        const int32_t cap = l->n_contexts;
+        nd->ctxn = (or_node**)realloc(nd->ctxn, (size_t)cap * sizeof(or_node*));
+        for (int32_t c = nd->ctx_cap; c < cap; c++) nd->ctxn[c] = NULL;
+        nd->ctx_cap = cap;
+    }
+    if (!nd->ctxn[context]) nd->ctxn[context] = node_new_plain(l);
+    return nd->ctxn[context];
 }
 
 /* DefaultController.canPass (DefaultController.java:49-76) on the selected node: 1 pass, 0 block, 2 priority wait */
@@ -1266,14 +1315,18 @@ static int default_can_pass(or_local* l, or_node* sn, const or_ctl* c, int64_t t
     return 0;
 }
 
-/* FlowSlot.checkFlow → FlowRuleChecker.checkFlow (:44-57): the rules in order, the first failure throws */
-static int check_flow(or_local* l, or_node* nd, int64_t t, int count, int prio, int origin, int64_t* wait) {
+/* FlowSlot.checkFlow → FlowRuleChecker.checkFlow (:44-57): the rules in order, the first failure throws. A cluster-mode
+ * rule on a node that is neither token client nor server: passClusterCheck → fallbackToLocalOrPass (:147-175). */
+static int check_flow(or_local* l, or_node* nd, int64_t t, int count, int prio, int origin, int context, int64_t* wait) {
     *wait = 0;
     for (uint32_t i = 0; i < nd->n_ctl; i++) {
         or_ctl* c = &nd->ctl[i];
-        int s = select_node(nd, &c->rule, origin);
+        if (c->rule.cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) continue;   /* the rule is not activated */
+        const int32_t ref = c->rule.ref_resource;
+        or_node* rn = (ref >= 0 && (uint32_t)ref < l->n) ? &l->nodes[ref] : NULL;
+        int s = select_kind(nd, &c->rule, origin, context, rn && rn->created);
         if (s < 0) continue;
-        or_node* sn = s == 0 ? nd : origin_node(l, nd, origin);
+        or_node* sn = s == 0 ? nd : s == 1 ? origin_node(l, nd, origin) : s == 2 ? context_node(l, nd, context) : rn;
         int64_t w = 0;
         switch (c->behavior) {
         case SG_CONTROL_WARM_UP:
@@ -1379,65 +1432,106 @@ static void record_complete(or_node* nd, int64_t t, int count, int64_t rt, int e
     }
 }
 
-int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
-    for (uint64_t i = 0; i < n; i++)
-        if (ev[i].origin < 0 || ev[i].origin > l->n_origins) return SG_E_INVAL;
-    for (uint64_t i = 0; i < n; i++) {
-        const sg_local_event* e = &ev[i];
-        uint32_t res = e->resource & SG_KEY_INDEX;
-        int prio = (e->resource & SG_KEY_PRIO) != 0;
-        out[i].status = SG_LOCAL_PASS;
-        out[i].wait_ms = 0;
-        if (res >= l->n) continue;
-        or_node* nd = &l->nodes[res];
-        or_node* on = origin_node(l, nd, e->origin);   /* context.getCurEntry().getOriginNode() */
-        int64_t t = e->ts_ms;
-        int count = e->count;
-        if (e->kind == SG_LOCAL_ENTRY) {
-            int64_t wait = 0;
-            int status = check_flow(l, nd, t, count, prio, e->origin, &wait);   /* FlowSlot */
-            int half[2] = {0, 0};
-            if (status == SG_LOCAL_PASS) { /* DegradeSlot.performChecking */
-                for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) {
-                    if (!cb_try_pass(&nd->cb[j], t, &half[j])) {
-                        status = SG_LOCAL_BLOCK_DEGRADE;
-                        break;
-                    }
-                }
-                if (status == SG_LOCAL_BLOCK_DEGRADE) /* whenTerminate hook: blocked probe → OPEN again */
-                    for (int j = 0; j < 2; j++)
-                        if (half[j] && nd->cb[j].state == OR_CB_HALF_OPEN) nd->cb[j].state = OR_CB_OPEN;
-            }
-            /* StatisticSlot.entry (:55-122): the DefaultNode/ClusterNode and the origin node */
-            if (status == SG_LOCAL_PASS) {
-                for (or_node* x = nd; x; x = (x == nd ? on : NULL)) {
-                    x->threads++;
-                    node_add(x->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
-                    node_add(x->minute, t, OR_M_PASS, count);
-                }
-                out[i].wait_ms = wait > INT32_MAX ? INT32_MAX : (int32_t)wait;   /* the rate limiters' sleep */
-            } else if (status == SG_LOCAL_PASS_WAIT) {
-                nd->threads++;
-                if (on) on->threads++;
-                out[i].wait_ms = (int32_t)wait;
-            } else {
-                for (or_node* x = nd; x; x = (x == nd ? on : NULL)) {
-                    node_add(x->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
-                    node_add(x->minute, t, OR_M_BLOCK, count);
-                }
-            }
-            out[i].status = status;
-        } else {
-            int error = e->kind == SG_LOCAL_EXIT_ERROR;
-            int64_t rt = t - e->create_ts;
-            record_complete(nd, t, count, rt, error);
-            if (on) record_complete(on, t, count, rt, error);
-            /* DegradeSlot.exit → onRequestComplete */
-            for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) cb_on_complete(&nd->cb[j], t, rt, error);
+static int pslot_entry(struct or_pslot* s, uint32_t res, int64_t t, int count, const sg_pslot_arg* a, uint32_t na,
+                       const uint64_t* values);
+static void pslot_exit(struct or_pslot* s, uint32_t res, int64_t t, const sg_pslot_arg* a, uint32_t na,
+                       const uint64_t* values, int d);
+
+/* The slot chain for one event (CtSph.entryWithPriority → the ProcessorSlot chain in @Spi order, Constants.java:76-83):
+ * StatisticSlot.entry (:55-122) around ParamFlowSlot (order -3000, ParamFlowSlot.java:38-93) → FlowSlot → DegradeSlot;
+ * Entry.exit → StatisticSlot.exit (:124-165) with the param exit callback, DegradeSlot.exit. */
+static void local_event(or_local* l, const sg_local_event* e, const sg_slot_ext* x, const sg_pslot_arg* args,
+                        const uint64_t* values, sg_local_result* out) {
+    uint32_t res = e->resource & SG_KEY_INDEX;
+    int prio = (e->resource & SG_KEY_PRIO) != 0;
+    out->status = SG_LOCAL_PASS;
+    out->wait_ms = 0;
+    if (res >= l->n) return;
+    const int context = x ? (int)x->context : 0;
+    const int args_null = !x || x->args_null;
+    const sg_pslot_arg* a = x ? args + x->arg_begin : NULL;
+    const uint32_t na = x ? x->arg_count : 0;
+    or_node* nd = &l->nodes[res];
+    or_node* on = origin_node(l, nd, e->origin);   /* context.getCurEntry().getOriginNode() */
+    or_node* dn = context_node(l, nd, context);    /* the DefaultNode (NodeSelectorSlot); mirrors into nd */
+    int64_t t = e->ts_ms;
+    int count = e->count;
+    if (e->kind == SG_LOCAL_ENTRY) {
+        nd->created = 1;                           /* ClusterBuilderSlot */
+        int64_t wait = 0;
+        int status = SG_LOCAL_PASS;
+        int32_t prule = -1;
+        if (l->ps && !args_null) {                 /* ParamFlowSlot.checkFlow */
+            prule = pslot_entry(l->ps, res, t, count, a, na, values);
+            if (prule >= 0) status = SG_LOCAL_BLOCK_PARAM;
         }
+        if (status == SG_LOCAL_PASS) status = check_flow(l, nd, t, count, prio, e->origin, context, &wait);   /* FlowSlot */
+        int half[2] = {0, 0};
+        if (status == SG_LOCAL_PASS) { /* DegradeSlot.performChecking */
+            for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) {
+                if (!cb_try_pass(&nd->cb[j], t, &half[j])) {
+                    status = SG_LOCAL_BLOCK_DEGRADE;
+                    break;
+                }
+            }
+            if (status == SG_LOCAL_BLOCK_DEGRADE) /* whenTerminate hook: blocked probe → OPEN again */
+                for (int j = 0; j < 2; j++)
+                    if (half[j] && nd->cb[j].state == OR_CB_HALF_OPEN) nd->cb[j].state = OR_CB_OPEN;
+        }
+        /* StatisticSlot.entry (:55-122): the DefaultNode (→ ClusterNode) and the origin node */
+        or_node* upd[3] = {nd, on, dn};
+        if (status == SG_LOCAL_PASS) {
+            for (int u = 0; u < 3; u++) {
+                if (!upd[u]) continue;
+                upd[u]->threads++;
+                node_add(upd[u]->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
+                node_add(upd[u]->minute, t, OR_M_PASS, count);
+            }
+            out->wait_ms = wait > INT32_MAX ? INT32_MAX : (int32_t)wait;   /* the rate limiters' sleep */
+        } else if (status == SG_LOCAL_PASS_WAIT) {
+            for (int u = 0; u < 3; u++)
+                if (upd[u]) upd[u]->threads++;
+            out->wait_ms = (int32_t)wait;
+        } else {
+            for (int u = 0; u < 3; u++) {
+                if (!upd[u]) continue;
+                node_add(upd[u]->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
+                node_add(upd[u]->minute, t, OR_M_BLOCK, count);
+            }
+            if (status == SG_LOCAL_BLOCK_PARAM) out->wait_ms = prule;
+        }
+        /* ParamFlowStatisticEntryCallback.onPass: ParameterMetric.addThreadCount(args) */
+        if ((status == SG_LOCAL_PASS || status == SG_LOCAL_PASS_WAIT) && l->ps && !args_null)
+            pslot_exit(l->ps, res, t, a, na, values, +1);
+        out->status = status;
+    } else {
+        int error = e->kind == SG_LOCAL_EXIT_ERROR;
+        int64_t rt = t - e->create_ts;
+        record_complete(nd, t, count, rt, error);
+        if (on) record_complete(on, t, count, rt, error);
+        if (dn) record_complete(dn, t, count, rt, error);
+        /* ParamFlowStatisticExitCallback.onExit: decreaseThreadCount(args) (the entry passed) */
+        if (l->ps && !args_null) pslot_exit(l->ps, res, t, a, na, values, -1);
+        /* DegradeSlot.exit → onRequestComplete */
+        for (int j = 0; j < nd->rule.n_breakers && j < 2; j++) cb_on_complete(&nd->cb[j], t, rt, error);
     }
+}
+
+int or_local_decide_ext(or_local* l, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                        const sg_pslot_arg* args, const uint64_t* values, sg_local_result* out) {
+    for (uint64_t i = 0; i < n; i++) {
+        if (ev[i].origin < 0 || ev[i].origin > l->n_origins) return SG_E_INVAL;
+        if (ext && (int64_t)ext[i].context >= (int64_t)(l->n_contexts > 0 ? l->n_contexts : 1)) return SG_E_INVAL;
+    }
+    for (uint64_t i = 0; i < n; i++) local_event(l, &ev[i], ext ? &ext[i] : NULL, args, values, &out[i]);
     return 0;
 }
+
+int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
+    return or_local_decide_ext(l, ev, NULL, n, NULL, NULL, out);
+}
+
+void or_local_attach_pslot(or_local* l, struct or_pslot* ps) { l->ps = ps; }
 
 int64_t or_local_second_sum(or_local* l, uint32_t res, int64_t t, int ev) {
     return res < l->n ? or_leap_get_sum(l->nodes[res].second, t, ev) : 0;
@@ -1478,13 +1572,29 @@ int or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_t* bor
     return 0;
 }
 
+static int dump_plain(const or_local* l, const or_node* on, int64_t* second, int64_t* borrow, int64_t* minute,
+                      int64_t* threads);
+
 /* The origin node of (res, origin): windows as or_local_dump, *threads = curThreadNum. Returns 1 when the node
  * exists (some event carried the origin), 0 when it was never created (all-empty dumps), < 0 on bad input. */
 int or_local_origin_dump(const or_local* l, uint32_t res, int origin, int64_t* second, int64_t* borrow,
                          int64_t* minute, int64_t* threads) {
     if (res >= l->n || origin <= 0 || origin > l->n_origins) return SG_E_INVAL;
     const or_node* nd = &l->nodes[res];
-    const or_node* on = nd->origin ? nd->origin[origin] : NULL;
+    const or_node* on = origin < nd->origin_cap ? nd->origin[origin] : NULL;
+    return dump_plain(l, on, second, borrow, minute, threads);
+}
+
+/* The DefaultNode of (res, context) (NodeSelectorSlot): same outputs as or_local_origin_dump. */
+int or_local_context_dump(const or_local* l, uint32_t res, int context, int64_t* second, int64_t* borrow,
+                          int64_t* minute, int64_t* threads) {
+    if (res >= l->n || context < 0 || context >= l->n_contexts) return SG_E_INVAL;
+    const or_node* nd = &l->nodes[res];
+    return dump_plain(l, context < nd->ctx_cap ? nd->ctxn[context] : NULL, second, borrow, minute, threads);
+}
+
+static int dump_plain(const or_local* l, const or_node* on, int64_t* second, int64_t* borrow, int64_t* minute,
+                      int64_t* threads) {
     if (!on) {
         for (int i = 0; i < l->S; i++) {
             for (int e = 0; e < 8; e++) second[8 * i + e] = e == 0 ? INT64_MIN : 0;
@@ -1528,6 +1638,7 @@ typedef struct or_pending {
     int64_t ts, create_ts, seq;
     uint32_t resource;
     int32_t count, error, origin;
+    sg_slot_ext ext;          /* the entry's context and arguments (Entry.exit(count, args) passes them again) */
 } or_pending;
 
 struct or_lgen {
@@ -1592,9 +1703,11 @@ uint64_t or_lgen_pending(const or_lgen* g) { return g->n; }
 /* Merge time-ordered entries with the exits of the passed ones (exit at ts + waitInMs + rt; exits due at
  * the same ms as an entry go first), replaying every emitted event through the oracle. Events with
  * ts >= t_end are not emitted (exits stay pending for the next call). Returns the number emitted, or
- * UINT64_MAX when `cap` is too small. */
-uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
-                     int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap) {
+ * UINT64_MAX when `cap` is too small. ext_in / ext_out (both NULL or both given): each entry's context and
+ * arguments, which its exit carries again; args / values: the argument pool the ext records index. */
+uint64_t or_lgen_run_ext(or_lgen* g, const sg_local_event* entries, const sg_slot_ext* ext_in, const int32_t* rt,
+                         const uint8_t* err, uint64_t n, int64_t t_end, sg_local_event* out, sg_slot_ext* ext_out,
+                         sg_local_result* res, uint64_t cap, const sg_pslot_arg* args, const uint64_t* values) {
     uint64_t k = 0, i = 0;
     for (;;) {
         int take_exit;
@@ -1608,6 +1721,7 @@ uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* r
         }
         if (k == cap) return UINT64_MAX;
         sg_local_event* e = &out[k];
+        sg_slot_ext* x = ext_out ? &ext_out[k] : NULL;
         if (take_exit) {
             or_pending p = pend_pop(g);
             e->ts_ms = p.ts;
@@ -1616,14 +1730,16 @@ uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* r
             e->count = p.count;
             e->kind = p.error ? SG_LOCAL_EXIT_ERROR : SG_LOCAL_EXIT;
             e->origin = p.origin;
-            or_local_decide(g->l, e, 1, &res[k]);
+            if (x) *x = p.ext;
+            or_local_decide_ext(g->l, e, x, 1, args, values, &res[k]);
             k++;
             continue;
         }
         *e = entries[i];
         e->kind = SG_LOCAL_ENTRY;
         e->create_ts = 0;
-        or_local_decide(g->l, e, 1, &res[k]);
+        if (x) *x = ext_in[i];
+        or_local_decide_ext(g->l, e, x, 1, args, values, &res[k]);
         if (res[k].status == SG_LOCAL_PASS || res[k].status == SG_LOCAL_PASS_WAIT) {
             or_pending p;
             p.create_ts = e->ts_ms;
@@ -1633,12 +1749,19 @@ uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* r
             p.count = e->count;
             p.error = err ? err[i] : 0;
             p.origin = e->origin;
+            if (x) p.ext = *x;
+            else memset(&p.ext, 0, sizeof(p.ext));
             pend_push(g, p);
         }
         k++;
         i++;
     }
     return k;
+}
+
+uint64_t or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
+                     int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap) {
+    return or_lgen_run_ext(g, entries, NULL, rt, err, n, t_end, out, NULL, res, cap, NULL, NULL);
 }
 
 /* Breaker i's statistic bucket (LeapArray(1, statIntervalMs)): start (INT64_MIN if never created), slow or
@@ -2454,6 +2577,36 @@ static void pslot_threads(or_pslot* s, uint32_t res, const sg_pslot_arg* args, u
     }
 }
 
+/* ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93) for one entry with non-null args: the index of the rule that
+ * throws ParamFlowException, or -1 */
+static int pslot_entry(or_pslot* s, uint32_t res, int64_t t, int count, const sg_pslot_arg* a, uint32_t na,
+                       const uint64_t* values) {
+    s->now = t;
+    if (res >= s->n_res) return -1;
+    for (uint32_t r = 0; r < s->n; r++) {
+        if (s->rules[r].resource != res) continue;
+        /* applyRealParamIdx(rule, args.length) */
+        if (s->cur_idx[r] < 0) s->cur_idx[r] = (-s->cur_idx[r] <= (int32_t)na) ? (int32_t)na + s->cur_idx[r] : -s->cur_idx[r];
+        s->inited[r] = 1;                      /* ParameterMetricStorage.initParamMetricsFor */
+        const int32_t idx = s->cur_idx[r];
+        if ((int32_t)na <= idx) continue;      /* args.length <= paramIdx */
+        const sg_pslot_arg* x = &a[idx];
+        if (x->kind == SG_ARG_NULL) continue;
+        const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
+        for (uint32_t j = 0; j < m; j++)
+            if (!pslot_single(s, r, res, count, values[x->value_begin + j])) return (int32_t)r;
+    }
+    return -1;
+}
+
+/* ParamFlowStatisticEntryCallback.onPass (d = +1) / ParamFlowStatisticExitCallback.onExit (d = -1) */
+static void pslot_exit(or_pslot* s, uint32_t res, int64_t t, const sg_pslot_arg* a, uint32_t na,
+                       const uint64_t* values, int d) {
+    s->now = t;
+    if (res >= s->n_res) return;
+    pslot_threads(s, res, a, na, values, d);
+}
+
 int or_pslot_decide(or_pslot* s, const sg_pslot_event* ev, uint64_t n, const sg_pslot_arg* args,
                     const uint64_t* values, sg_pslot_result* out) {
     for (uint64_t i = 0; i < n; i++) {
@@ -2465,30 +2618,13 @@ int or_pslot_decide(or_pslot* s, const sg_pslot_event* ev, uint64_t n, const sg_
         s->now = e->ts_ms;
         if (e->resource >= s->n_res || e->args_null) continue;   /* ParamFlowSlot.checkFlow: args == null */
         if (e->kind != SG_LOCAL_ENTRY) {           /* ParamFlowStatisticExitCallback: passed entries only */
-            pslot_threads(s, e->resource, a, na, values, -1);
+            pslot_exit(s, e->resource, e->ts_ms, a, na, values, -1);
             continue;
         }
-        int pass = 1;
-        for (uint32_t r = 0; r < s->n && pass; r++) {
-            if (s->rules[r].resource != e->resource) continue;
-            /* applyRealParamIdx(rule, args.length) */
-            if (s->cur_idx[r] < 0) s->cur_idx[r] = (-s->cur_idx[r] <= (int32_t)na) ? (int32_t)na + s->cur_idx[r] : -s->cur_idx[r];
-            s->inited[r] = 1;                      /* ParameterMetricStorage.initParamMetricsFor */
-            const int32_t idx = s->cur_idx[r];
-            if ((int32_t)na <= idx) continue;      /* args.length <= paramIdx */
-            const sg_pslot_arg* x = &a[idx];
-            if (x->kind == SG_ARG_NULL) continue;
-            const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
-            for (uint32_t j = 0; j < m; j++) {
-                if (!pslot_single(s, r, e->resource, e->count, values[x->value_begin + j])) {
-                    pass = 0;
-                    out[i].rule = (int32_t)r;
-                    break;
-                }
-            }
-        }
-        out[i].pass = pass;
-        if (pass) pslot_threads(s, e->resource, a, na, values, +1);   /* ParamFlowStatisticEntryCallback.onPass */
+        const int r = pslot_entry(s, e->resource, e->ts_ms, e->count, a, na, values);
+        out[i].pass = r < 0;
+        out[i].rule = r;
+        if (r < 0) pslot_exit(s, e->resource, e->ts_ms, a, na, values, +1);   /* onPass */
     }
     return 0;
 }

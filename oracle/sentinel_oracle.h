@@ -165,7 +165,16 @@ int       or_local_dump(const or_local* l, uint32_t res, int64_t* second, int64_
 int       or_local_breaker_stat(const or_local* l, uint32_t res, int i, int64_t* start, int64_t* bad, int64_t* total);
 /* FlowRuleManager.loadRules for the local chain (any number of rules per resource, limitApp, controllers);
  * returns the number of rules kept. */
-int       or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins);
+int       or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
+                                   int32_t n_contexts);
+/* The whole slot chain (StatisticSlot around ParamFlowSlot → FlowSlot → DegradeSlot, sg_slot_decide_batch): ext may be
+ * NULL (context 0, null args); the param rules are those of the attached or_pslot (or none). */
+int       or_local_decide_ext(or_local* l, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                              const sg_pslot_arg* args, const uint64_t* values, sg_local_result* out);
+struct or_pslot;
+void      or_local_attach_pslot(or_local* l, struct or_pslot* ps);
+int       or_local_context_dump(const or_local* l, uint32_t res, int context, int64_t* second, int64_t* borrow,
+                                int64_t* minute, int64_t* threads);
 void      or_local_set_cold_factor(or_local* l, int cold_factor);
 int       or_local_origin_dump(const or_local* l, uint32_t res, int origin, int64_t* second, int64_t* borrow,
                                int64_t* minute, int64_t* threads);
@@ -182,9 +191,9 @@ int32_t   or_ctl_warning_token(const or_ctl* c);
 int32_t   or_ctl_max_token(const or_ctl* c);
 int       or_warm_can_pass(or_ctl* c, int64_t now, double pass_qps, double prev_qps, int acquire);
 int       or_warm_rl_can_pass(or_ctl* c, int64_t now, double prev_qps, int acquire, int64_t* wait);
-/* FlowRuleChecker.selectNodeByRequesterAndStrategy for rule i of a resource's rules: 0 ClusterNode, 1 origin
- * node, -1 none. */
-int       or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin);
+/* FlowRuleChecker.selectNodeByRequesterAndStrategy / selectReferenceNode for rule i of a resource's rules: 0 ClusterNode,
+ * 1 origin node, 2 the DefaultNode of the context (CHAIN), 3 the referenced ClusterNode (RELATE), -1 none. */
+int       or_select_node(const sg_local_flow_rule* rules, uint32_t n, uint32_t i, int origin, int context, int ref_exists);
 
 /* Trace generator for the local chain (test infrastructure): entries + the exits of the passed ones. */
 typedef struct or_lgen or_lgen;
@@ -193,6 +202,9 @@ void      or_lgen_free(or_lgen* g);
 uint64_t  or_lgen_pending(const or_lgen* g);
 uint64_t  or_lgen_run(or_lgen* g, const sg_local_event* entries, const int32_t* rt, const uint8_t* err, uint64_t n,
                       int64_t t_end, sg_local_event* out, sg_local_result* res, uint64_t cap);
+uint64_t  or_lgen_run_ext(or_lgen* g, const sg_local_event* entries, const sg_slot_ext* ext_in, const int32_t* rt,
+                          const uint8_t* err, uint64_t n, int64_t t_end, sg_local_event* out, sg_slot_ext* ext_out,
+                          sg_local_result* res, uint64_t cap, const sg_pslot_arg* args, const uint64_t* values);
 
 /* ---------- metric snapshots ---------- */
 /* StatisticNode.metrics() of every resource at now (MetricTimerListener.run), sorted by (timestamp, resource);

@@ -136,8 +136,15 @@ LOCAL_PASS, LOCAL_BLOCK_FLOW, LOCAL_BLOCK_DEGRADE, LOCAL_PASS_WAIT = 0, 1, 2, 3
 # sg_local_flow_rule (FlowRule of the local chain)
 LOCAL_FLOW_RULE_DTYPE = np.dtype([("resource", "<u4"), ("grade", "<i4"), ("count", "<f8"),
                                   ("control_behavior", "<i4"), ("limit_app", "<i4"), ("strategy", "<i4"),
-                                  ("warm_up_period_sec", "<i4"), ("max_queueing_ms", "<i4"), ("reserved", "<i4")],
+                                  ("warm_up_period_sec", "<i4"), ("max_queueing_ms", "<i4"),
+                                  ("ref_resource", "<i4"), ("cluster_mode", "<i4"), ("cluster_config", "<i4")],
                                  align=True)
+CLUSTER_MODE_OFF, CLUSTER_MODE_FALLBACK, CLUSTER_MODE_NO_FALLBACK, CLUSTER_MODE_INVALID = 0, 1, 2, -1
+CLUSTER_CLIENT, CLUSTER_SERVER, CLUSTER_NOT_STARTED = 0, 1, -1
+# the whole slot chain (sg_slot_decide_batch): per-event context and arguments
+SLOT_EXT_DTYPE = np.dtype([("context", "<u4"), ("arg_begin", "<u4"), ("arg_count", "<u4"), ("args_null", "<i4")],
+                          align=True)
+LOCAL_BLOCK_PARAM = 4
 CONTROL_DEFAULT, CONTROL_WARM_UP, CONTROL_RATE_LIMITER, CONTROL_WARM_UP_RATE_LIMITER = 0, 1, 2, 3
 LIMIT_APP_DEFAULT, LIMIT_APP_OTHER = 0, -1
 STRATEGY_DIRECT, STRATEGY_RELATE, STRATEGY_CHAIN = 0, 1, 2
@@ -154,7 +161,7 @@ assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
 assert CPARAM_RULE_DTYPE.itemsize == 40 and CPARAM_REQ_DTYPE.itemsize == 24
 assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
-assert LOCAL_FLOW_RULE_DTYPE.itemsize == 40
+assert LOCAL_FLOW_RULE_DTYPE.itemsize == 48 and SLOT_EXT_DTYPE.itemsize == 16
 assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
 assert METRIC_NODE_DTYPE.itemsize == 64
 assert PSLOT_RULE_DTYPE.itemsize == PARAM_RULE_DTYPE.itemsize + 16 and PSLOT_EVENT_DTYPE.itemsize == 32

@@ -159,6 +159,16 @@ struct sg_handle {
     uint32_t* d_lskip_count = nullptr;
     uint32_t lskip_cap = 0;
     sg_local_result* d_lout_h = nullptr;
+    // nodes besides the ClusterNodes (kept across flow-rule reloads): per resource, origin nodes (ids 1 .. on_n at
+    // on_base) and context DefaultNodes (ids 0 .. cn_n - 1 at cn_base)
+    std::vector<uint32_t> l_on_n, l_on_base, l_cn_n, l_cn_base;
+    int32_t l_n_contexts = 0;
+    int32_t l_cluster_state = SG_CLUSTER_NOT_STARTED;
+    bool l_cluster_rules = false;     // some loaded flow rule is in cluster mode
+    uint32_t* d_lgkey = nullptr;      // [K] RELATE key groups (record key of each resource), null without groups
+    uint64_t l_ps_applied = 0;        // ps_gen whose param flags d_lrules carries (0: none)
+    bool l_has_cx_ps = false;         // some resource is cx because of param rules
+    sg_slot_ext* d_lext_h = nullptr;  // host-path buffers of sg_slot_decide_batch_host
 
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
@@ -178,6 +188,8 @@ struct sg_handle {
     PSThread* d_ps_tc = nullptr;
     uint64_t ps_tc_slots = 0;
     int64_t* d_ps_last_ts = nullptr;
+    std::vector<uint32_t> ps_res_rules;  // param rules per resource
+    uint64_t ps_gen = 0;              // sg_pslot_load_rules calls so far
     // concurrent cluster tokens (sg_conc_*)
     int32_t* d_cnow = nullptr;        // nowCalls per rule
     double* d_cthr = nullptr;
@@ -255,6 +267,7 @@ struct sg_handle {
 };
 
 namespace {
+PSArgs pslot_args(sg_handle* h);          // below: the ParamFlowSlot state's device arguments
 int ensure_layout(sg_handle* h);          // below: record layout of the loaded rules
 int flow_status(sg_handle* h, int err);   // below: batch error flags -> SG_E_*
 int drain_async(sg_handle* h);  // below: completes the handle's in-flight host-pipeline batches
@@ -598,6 +611,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lskips);
     dfree(h->d_lskip_count);
     dfree(h->d_lout_h);
+    dfree(h->d_lext_h);
+    dfree(h->d_lgkey);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
     drain_async(h);
@@ -2242,8 +2257,16 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     dfree(h->d_lmin);
     h->l_nodes = n;
     h->l_n_origins = 0;
+    h->l_n_contexts = 0;
     h->l_has_cx = false;
+    h->l_cluster_rules = false;
     h->l_rule_slot.clear();
+    h->l_on_n.assign(n, 0);
+    h->l_on_base.assign(n, kNoNode);
+    h->l_cn_n.assign(n, 0);
+    h->l_cn_base.assign(n, kNoNode);
+    dfree(h->d_lgkey);
+    h->l_ps_applied = 0;
     if (!h->d_llast_ts && hipMalloc(&h->d_llast_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "ts");
     const int64_t neg = -1;
     HIP_TRY(h, hipMemcpy(h->d_llast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
@@ -2317,7 +2340,31 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
     return SG_OK;
 }
 
-int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, void* stream_) {
+namespace {
+
+// The ParamFlowSlot flags of the resources (LRule.ps: rules loaded by sg_pslot_load_rules for the resource) on the
+// device rule image: a resource with param rules is walked by the full-chain walker.
+int local_apply_params(sg_handle* h) {
+    const uint64_t want = h->ps_loaded ? h->ps_gen : 0;
+    if (h->l_ps_applied == want) return SG_OK;
+    const uint32_t K = (uint32_t)h->ltab.size();
+    std::vector<LRule> tab = h->ltab;
+    bool any = false;
+    for (uint32_t k = 0; k < K && h->ps_loaded && k < h->ps_res_rules.size(); ++k) {
+        if (!h->ps_res_rules[k]) continue;
+        tab[k].ps = 1;
+        tab[k].cx = 1;
+        any = true;
+    }
+    if (K) HIP_TRY(h, hipMemcpy(h->d_lrules, tab.data(), sizeof(LRule) * K, hipMemcpyHostToDevice));
+    h->l_has_cx_ps = any;
+    h->l_ps_applied = want;
+    return SG_OK;
+}
+
+// StatisticSlot around ParamFlowSlot → FlowSlot → DegradeSlot for a time-ordered batch (ext nullable).
+int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n, const sg_pslot_arg* args,
+                 uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_local_result* out, void* stream_) {
     if (!h) return SG_E_INVAL;
     if (n == 0) return SG_OK;
     if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
@@ -2325,6 +2372,9 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    int prc = local_apply_params(h);
+    if (prc) return prc;
     const uint32_t K = (uint32_t)h->ltab.size();
     int kbits = bits_for((uint64_t)K);
     if (kbits < 1) kbits = 1;
@@ -2367,6 +2417,17 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     L.np = h->d_np;
     L.err = h->d_err;
     L.last_ts = h->d_llast_ts;
+    L.ext = ext;
+    L.n_contexts = h->l_n_contexts;
+    L.gkey = h->d_lgkey;
+    L.has_ps = h->ps_loaded ? 1 : 0;
+    if (h->ps_loaded) {
+        L.ps = pslot_args(h);
+        L.ps.args = args;
+        L.ps.n_args = args ? n_args : 0;
+        L.ps.values = values;
+        L.ps.n_values = values ? n_values : 0;
+    }
     if (!h->d_lflags) {  // batch workspace of the local path (sized for max_batch)
         const uint64_t mb = h->cfg.max_batch;
         h->lskip_cap = (uint32_t)(2 * mb / kSkipMin + 1);
@@ -2415,7 +2476,7 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     sgm.rec_sorted = sorted;
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg(sgm, stream));
-    HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx, h->aux, stream, h->fork, h->join));
+    HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx || h->l_has_cx_ps, h->aux, stream, h->fork, h->join));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
@@ -2438,9 +2499,63 @@ int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg
     if (*h->h_err & kErrTime)
         return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
     if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
-    if (*h->h_err & kErrBounds) return fail(h, SG_E_INVAL, "an event's origin id is outside 0..n_origins");
+    if (*h->h_err & kErrBounds)
+        return fail(h, SG_E_INVAL, "an event's origin id (0..n_origins), context id (0..n_contexts-1) or arguments "
+                                   "(the arg / value arrays) are out of range");
+    if (*h->h_err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param value or thread-count table is full");
     if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
     return SG_OK;
+}
+
+}  // namespace
+
+int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, void* stream) {
+    return local_decide(h, ev, nullptr, n, nullptr, 0, nullptr, 0, out, stream);
+}
+
+int sg_slot_decide_batch(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                         const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values,
+                         sg_local_result* out, void* stream) {
+    return local_decide(h, ev, ext, n, args, n_args, values, n_values, out, stream);
+}
+
+int sg_slot_decide_batch_host(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+                              const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values,
+                              sg_local_result* out) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->d_lev_h) {
+        if (hipMalloc(&h->d_lev_h, sizeof(sg_local_event) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_lout_h, sizeof(sg_local_result) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "host-path buffers");
+    }
+    if (ext && !h->d_lext_h && hipMalloc(&h->d_lext_h, sizeof(sg_slot_ext) * h->cfg.max_batch) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "host-path buffers");
+    sg_pslot_arg* d_args = nullptr;
+    uint64_t* d_vals = nullptr;
+    hipError_t e = hipMemcpy(h->d_lev_h, ev, sizeof(sg_local_event) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && ext) e = hipMemcpy(h->d_lext_h, ext, sizeof(sg_slot_ext) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && args && n_args) {
+        e = hipMalloc(&d_args, sizeof(sg_pslot_arg) * n_args);
+        if (e == hipSuccess) e = hipMemcpy(d_args, args, sizeof(sg_pslot_arg) * n_args, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && values && n_values) {
+        e = hipMalloc(&d_vals, sizeof(uint64_t) * n_values);
+        if (e == hipSuccess) e = hipMemcpy(d_vals, values, sizeof(uint64_t) * n_values, hipMemcpyHostToDevice);
+    }
+    int rc = SG_E_DEVICE;
+    if (e == hipSuccess) {
+        rc = local_decide(h, h->d_lev_h, ext ? h->d_lext_h : nullptr, n, d_args, d_args ? n_args : 0, d_vals,
+                          d_vals ? n_values : 0, h->d_lout_h, nullptr);
+        if (rc == SG_OK) e = hipMemcpy(out, h->d_lout_h, sizeof(sg_local_result) * n, hipMemcpyDeviceToHost);
+    }
+    if (d_args) (void)hipFree(d_args);
+    if (d_vals) (void)hipFree(d_vals);
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    return rc;
 }
 
 int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out) {
@@ -2499,12 +2614,15 @@ int local_read_node(sg_handle* h, uint32_t node, int64_t* second, int64_t* borro
     return SG_OK;
 }
 
-// FlowRuleUtil.isValidRule (:167-251) for local rules: count >= 0, grade THREAD / QPS, behaviour >= 0 with its
-// parameters (warm-up period > 0, queueing time > 0)
+// FlowRuleUtil.isValidRule (:167-251) for local rules: count >= 0, grade / strategy / behaviour >= 0; QPS rules:
+// checkClusterField (an invalid ClusterFlowConfig), checkStrategyField (RELATE / CHAIN need a refResource) and
+// checkControlBehaviorField (warm-up period > 0, queueing time > 0); THREAD rules: checkClusterConcurrentField
 bool local_flow_rule_valid(const sg_local_flow_rule& r) {
     if (!(r.count >= 0) || r.grade < 0 || r.strategy < 0 || r.control_behavior < 0) return false;
+    if (r.cluster_mode == SG_CLUSTER_MODE_INVALID) return false;
     if (r.grade == 0) return true;
     if (r.grade != 1) return false;
+    if ((r.strategy == SG_STRATEGY_RELATE || r.strategy == SG_STRATEGY_CHAIN) && r.ref_resource < 0) return false;
     switch (r.control_behavior) {
     case SG_CONTROL_WARM_UP: return r.warm_up_period_sec > 0;
     case SG_CONTROL_RATE_LIMITER: return r.max_queueing_ms > 0;
@@ -2513,10 +2631,15 @@ bool local_flow_rule_valid(const sg_local_flow_rule& r) {
     }
 }
 
-bool local_flow_rule_same(const sg_local_flow_rule& a, const sg_local_flow_rule& b) {  // FlowRule.equals
-    return a.resource == b.resource && a.grade == b.grade && a.count == b.count &&
+// FlowRule.equals (FlowRule.java, AbstractRule.equals): Double.compare on count, refResource, clusterMode and the
+// ClusterFlowConfig (its caller-given id)
+bool local_flow_rule_same(const sg_local_flow_rule& a, const sg_local_flow_rule& b) {
+    return a.resource == b.resource && a.grade == b.grade && std::memcmp(&a.count, &b.count, sizeof(double)) == 0 &&
            a.control_behavior == b.control_behavior && a.limit_app == b.limit_app && a.strategy == b.strategy &&
-           a.warm_up_period_sec == b.warm_up_period_sec && a.max_queueing_ms == b.max_queueing_ms;
+           a.warm_up_period_sec == b.warm_up_period_sec && a.max_queueing_ms == b.max_queueing_ms &&
+           (a.ref_resource < 0 ? b.ref_resource < 0 : a.ref_resource == b.ref_resource) &&
+           (a.cluster_mode != 0) == (b.cluster_mode != 0) &&
+           (a.cluster_mode == 0 || (a.cluster_mode == b.cluster_mode && a.cluster_config == b.cluster_config));
 }
 
 int32_t d2i_host(double x) {  // (int) double
@@ -2537,6 +2660,9 @@ LFlowRule make_flow_rule(const sg_local_flow_rule& r, int cold) {
     f.limit_app = r.limit_app;
     f.max_queue_ms = r.max_queueing_ms;
     f.cold = cold;
+    f.strategy = r.strategy;
+    f.ref = r.ref_resource < 0 ? -1 : r.ref_resource;
+    f.cluster_mode = r.cluster_mode;
     if (f.behavior == SG_CONTROL_WARM_UP || f.behavior == SG_CONTROL_WARM_UP_RATE_LIMITER) {
         f.warning_token = d2i_host(r.warm_up_period_sec * r.count) / (cold - 1);
         const int32_t two_w = (int32_t)(2u * (uint32_t)r.warm_up_period_sec);  // 2 * warmUpPeriodInSec: int
@@ -2558,8 +2684,19 @@ int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64
     if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
     if (origin <= 0 || origin > h->l_n_origins) return fail(h, SG_E_INVAL, "origin id outside 1..n_origins");
     const uint32_t on = h->ltab[res].onode;
-    if (on == kNoNode) return fail(h, SG_E_INVAL, "the resource has no limitApp rule, so no origin nodes");
+    if (on == kNoNode || (uint32_t)origin > h->ltab[res].on_n)
+        return fail(h, SG_E_INVAL, "the resource keeps no origin nodes (no rule of it named an origin)");
     return local_read_node(h, on + (uint32_t)origin - 1, second, borrow, minute, head);
+}
+
+int sg_local_read_context_state(sg_handle* h, uint32_t res, int32_t context, int64_t* second, int64_t* borrow,
+                                int64_t* minute, int64_t* head) {
+    if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
+    if (context < 0 || context >= h->l_n_contexts) return fail(h, SG_E_INVAL, "context id outside 0..n_contexts-1");
+    const uint32_t cn = h->ltab[res].cnode;
+    if (cn == kNoNode || (uint32_t)context >= h->ltab[res].cn_n)
+        return fail(h, SG_E_INVAL, "the resource keeps no context DefaultNodes (no CHAIN rule)");
+    return local_read_node(h, cn + (uint32_t)context, second, borrow, minute, head);
 }
 
 int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3) {
@@ -2580,79 +2717,150 @@ int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3) {
     return SG_OK;
 }
 
-int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins) {
+int sg_local_set_cluster_state(sg_handle* h, int32_t state) {
+    if (!h) return SG_E_INVAL;
+    if (state != SG_CLUSTER_CLIENT && state != SG_CLUSTER_SERVER && state != SG_CLUSTER_NOT_STARTED)
+        return fail(h, SG_E_INVAL, "cluster state: CLIENT 0, SERVER 1 or NOT_STARTED -1");
+    if (state != SG_CLUSTER_NOT_STARTED && h->l_cluster_rules)
+        return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules need the token client / server: decided in order only "
+                                         "on a node that is neither (INTEGRATION.md §8)");
+    h->l_cluster_state = state;
+    return SG_OK;
+}
+
+int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
+                             int32_t n_contexts) {
     if (!h || (!rules && n)) return SG_E_INVAL;
     if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
-    if (n_origins < 0) return fail(h, SG_E_INVAL, "n_origins < 0");
+    if (n_origins < 0 || n_contexts < 0) return fail(h, SG_E_INVAL, "n_origins / n_contexts < 0");
+    if (n_origins < h->l_n_origins || n_contexts < h->l_n_contexts)
+        return fail(h, SG_E_INVAL, "origin / context ids keep their meaning across loads: the counts cannot shrink");
     const uint32_t K = (uint32_t)h->ltab.size();
     const int cold = h->lcfg.cold_factor > 1 ? h->lcfg.cold_factor : 3;
     // FlowRuleUtil.buildFlowRuleMap (:83-130): drop invalid rules and duplicates (its HashSet), group by resource
     std::vector<int64_t> slot(n, -1);
     std::vector<std::vector<uint32_t>> by_res(K);
+    bool cluster_rules = false;
     for (uint32_t i = 0; i < n; ++i) {
         const sg_local_flow_rule& r = rules[i];
         if (r.resource >= K || !local_flow_rule_valid(r)) continue;
-        if (r.strategy != SG_STRATEGY_DIRECT)
-            return fail(h, SG_E_UNSUPPORTED, "RELATE / CHAIN strategies read other resources' nodes");
         if (r.limit_app > n_origins || r.limit_app < SG_LIMIT_APP_OTHER)
             return fail(h, SG_E_INVAL, "limit_app names an origin id outside 1..n_origins");
+        if (r.strategy == SG_STRATEGY_CHAIN && r.ref_resource >= n_contexts)
+            return fail(h, SG_E_INVAL, "a CHAIN rule names a context id outside 0..n_contexts-1");
+        if (r.cluster_mode != SG_CLUSTER_MODE_OFF && r.cluster_mode != SG_CLUSTER_MODE_FALLBACK &&
+            r.cluster_mode != SG_CLUSTER_MODE_NO_FALLBACK)
+            return fail(h, SG_E_INVAL, "cluster_mode");
+        if (r.cluster_mode != SG_CLUSTER_MODE_OFF && h->l_cluster_state != SG_CLUSTER_NOT_STARTED)
+            return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules on a token client / server (INTEGRATION.md §8)");
         bool dup = false;
         for (uint32_t j : by_res[r.resource]) dup = dup || local_flow_rule_same(rules[j], r);
         if (!dup) by_res[r.resource].push_back(i);
+        cluster_rules = cluster_rules || r.cluster_mode != SG_CLUSTER_MODE_OFF;
     }
+    // RELATE key groups: a rule reading another resource's ClusterNode joins the two (union-find, smallest index first)
+    std::vector<uint32_t> parent(K);
+    for (uint32_t k = 0; k < K; ++k) parent[k] = k;
+    auto find = [&](uint32_t x) {
+        while (parent[x] != x) x = parent[x] = parent[parent[x]];
+        return x;
+    };
+    bool groups = false;
+    for (uint32_t k = 0; k < K; ++k)
+        for (uint32_t i : by_res[k]) {
+            const sg_local_flow_rule& r = rules[i];
+            if (r.strategy != SG_STRATEGY_RELATE || r.ref_resource < 0 || (uint32_t)r.ref_resource >= K ||
+                (uint32_t)r.ref_resource == k)
+                continue;
+            const uint32_t x = find(k), y = find((uint32_t)r.ref_resource);
+            if (x != y) parent[std::max(x, y)] = std::min(x, y);
+            groups = true;
+        }
+    std::vector<uint32_t> gkey(K);
+    std::vector<uint32_t> gsize(K, 0);
+    for (uint32_t k = 0; k < K; ++k) ++gsize[gkey[k] = find(k)];
+
     std::vector<LRule> tab = h->ltab;
     std::vector<LFlowRule> fr;
-    uint32_t onodes = 0;
+    std::vector<uint32_t> on_n(K), cn_n(K);
     bool has_cx = false;
     for (uint32_t k = 0; k < K; ++k) {
         std::vector<uint32_t>& v = by_res[k];
-        // Collections.sort(FlowRuleComparator) (:30-55): stable, limitApp "default" last
-        std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) {
-            return (rules[x].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0) <
-                   (rules[y].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
-        });
+        // Collections.sort(FlowRuleComparator) (:30-55): stable; cluster-mode rules last, then limitApp "default" last
+        auto key = [&](uint32_t x) {
+            return (rules[x].cluster_mode != SG_CLUSTER_MODE_OFF ? 2 : 0) + (rules[x].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
+        };
+        std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) { return key(x) < key(y); });
+        bool origin_rules = false, chain_rules = false;
+        for (uint32_t i : v) {
+            origin_rules = origin_rules || rules[i].limit_app != SG_LIMIT_APP_DEFAULT;
+            chain_rules = chain_rules || rules[i].strategy == SG_STRATEGY_CHAIN;
+        }
+        // nodes, once kept, stay (and follow the grown id ranges)
+        on_n[k] = (h->l_on_n[k] > 0 || origin_rules) ? (uint32_t)n_origins : 0u;
+        cn_n[k] = (h->l_cn_n[k] > 0 || chain_rules) ? (uint32_t)n_contexts : 0u;
         LRule& L = tab[k];
         L.fr_begin = L.fr_n = 0;
-        L.onode = kNoNode;
+        L.onode = L.cnode = kNoNode;
+        L.on_n = L.cn_n = 0;
         L.cx = 0;
+        L.ps = 0;
+        L.grp = gsize[gkey[k]] > 1 ? 1 : 0;
         L.flow_grade = -1;
         L.flow_count = 0;
-        if (v.empty()) continue;
-        const sg_local_flow_rule& r0 = rules[v[0]];
-        if (v.size() == 1 && r0.limit_app == SG_LIMIT_APP_DEFAULT &&
-            make_flow_rule(r0, cold).behavior == SG_CONTROL_DEFAULT) {  // the fast walkers' one DefaultController rule
-            L.flow_grade = r0.grade;
-            L.flow_count = r0.count;
+        const bool fast = v.size() == 1 && !L.grp && on_n[k] == 0 && cn_n[k] == 0 &&
+                          rules[v[0]].limit_app == SG_LIMIT_APP_DEFAULT && rules[v[0]].strategy == SG_STRATEGY_DIRECT &&
+                          rules[v[0]].cluster_mode == SG_CLUSTER_MODE_OFF &&
+                          make_flow_rule(rules[v[0]], cold).behavior == SG_CONTROL_DEFAULT;
+        if (fast) {  // the fast walkers' one DefaultController rule on the ClusterNode
+            L.flow_grade = rules[v[0]].grade;
+            L.flow_count = rules[v[0]].count;
             slot[v[0]] = -2;
             continue;
         }
+        if (v.empty() && !L.grp && on_n[k] == 0 && cn_n[k] == 0) continue;
         L.cx = 1;
         has_cx = true;
         L.fr_begin = (uint32_t)fr.size();
         L.fr_n = (uint32_t)v.size();
-        bool origin_rules = false;
         for (uint32_t i : v) {
-            origin_rules = origin_rules || rules[i].limit_app != SG_LIMIT_APP_DEFAULT;
             slot[i] = (int64_t)fr.size();
             fr.push_back(make_flow_rule(rules[i], cold));
         }
-        if (origin_rules && n_origins > 0) {  // ClusterNode.originCountMap: one node per origin id
-            L.onode = K + onodes;
-            onodes += (uint32_t)n_origins;
-        }
     }
-    const uint64_t N = (uint64_t)K + onodes;
-    if (N >= SG_KEY_BAD) return fail(h, SG_E_UNSUPPORTED, "too many origin nodes");
+    // node layout: the K resources, then the origin blocks, then the context blocks; src = the old node of each
+    std::vector<int64_t> src;
+    src.reserve(K);
+    for (uint32_t k = 0; k < K; ++k) src.push_back(k);
+    std::vector<uint32_t> on_base(K, kNoNode), cn_base(K, kNoNode);
+    for (uint32_t k = 0; k < K; ++k) {
+        if (!on_n[k]) continue;
+        on_base[k] = (uint32_t)src.size();
+        for (uint32_t o = 1; o <= on_n[k]; ++o)
+            src.push_back(o <= h->l_on_n[k] ? (int64_t)h->l_on_base[k] + o - 1 : -1);
+    }
+    for (uint32_t k = 0; k < K; ++k) {
+        if (!cn_n[k]) continue;
+        cn_base[k] = (uint32_t)src.size();
+        for (uint32_t c = 0; c < cn_n[k]; ++c) src.push_back(c < h->l_cn_n[k] ? (int64_t)h->l_cn_base[k] + c : -1);
+    }
+    const uint64_t N = src.size();
+    if (N >= SG_KEY_BAD) return fail(h, SG_E_UNSUPPORTED, "too many origin / context nodes");
+    for (uint32_t k = 0; k < K; ++k) {
+        tab[k].onode = on_base[k];
+        tab[k].on_n = on_n[k];
+        tab[k].cnode = cn_base[k];
+        tab[k].cn_n = cn_n[k];
+    }
     tab.resize(N);
-    for (uint64_t i = K; i < N; ++i) {  // origin nodes: no rules, no breakers
+    for (uint64_t i = K; i < N; ++i) {  // origin / context nodes: no rules, no breakers
         tab[i] = LRule{};
         tab[i].flow_grade = -1;
-        tab[i].onode = kNoNode;
+        tab[i].onode = tab[i].cnode = kNoNode;
         for (int j = 0; j < 2; ++j) tab[i].b[j].stat_ms = 1;
     }
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipDeviceSynchronize());
-    // the resources' statistics survive the load; origin nodes start empty
     const int S = h->lcfg.sample_count;
     LRule* d_rules = nullptr;
     LHead* d_head = nullptr;
@@ -2660,6 +2868,8 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     LFuture* d_bor = nullptr;
     LFlowRule* d_fr = nullptr;
     LCtl* d_ctl = nullptr;
+    int64_t* d_src = nullptr;
+    uint32_t* d_gkey = nullptr;
     auto release = [&]() {
         dfree(d_rules);
         dfree(d_head);
@@ -2668,11 +2878,14 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
         dfree(d_min);
         dfree(d_fr);
         dfree(d_ctl);
+        dfree(d_src);
+        dfree(d_gkey);
     };
     if (N && (hipMalloc(&d_rules, sizeof(LRule) * N) != hipSuccess || hipMalloc(&d_head, sizeof(LHead) * N) != hipSuccess ||
               hipMalloc(&d_sec, sizeof(LBucket) * N * S) != hipSuccess ||
               hipMalloc(&d_bor, sizeof(LFuture) * N * S) != hipSuccess ||
-              hipMalloc(&d_min, sizeof(LBucket) * N * kMinuteS) != hipSuccess)) {
+              hipMalloc(&d_min, sizeof(LBucket) * N * kMinuteS) != hipSuccess ||
+              hipMalloc(&d_src, sizeof(int64_t) * N) != hipSuccess)) {
         release();
         return fail(h, SG_E_NOMEM, "local node allocation");
     }
@@ -2680,6 +2893,10 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
                         hipMalloc(&d_ctl, sizeof(LCtl) * fr.size()) != hipSuccess)) {
         release();
         return fail(h, SG_E_NOMEM, "local flow rule allocation");
+    }
+    if (groups && hipMalloc(&d_gkey, sizeof(uint32_t) * K) != hipSuccess) {
+        release();
+        return fail(h, SG_E_NOMEM, "key groups");
     }
     hipError_t e = hipSuccess;
     if (N) {
@@ -2691,21 +2908,18 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
         L.sec = d_sec;
         L.bor = d_bor;
         L.minute = d_min;
-        e = launch_local_init(L, 0);
+        e = hipMemcpy(d_src, src.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = launch_local_remap(L, d_src, h->d_lhead, h->d_lsec, h->d_lbor, h->d_lmin, 0);
         if (e == hipSuccess) e = hipMemcpy(d_rules, tab.data(), sizeof(LRule) * N, hipMemcpyHostToDevice);
-        if (e == hipSuccess && K) {
-            e = hipMemcpy(d_head, h->d_lhead, sizeof(LHead) * K, hipMemcpyDeviceToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_sec, h->d_lsec, sizeof(LBucket) * K * S, hipMemcpyDeviceToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_bor, h->d_lbor, sizeof(LFuture) * K * S, hipMemcpyDeviceToDevice);
-            if (e == hipSuccess) e = hipMemcpy(d_min, h->d_lmin, sizeof(LBucket) * K * kMinuteS, hipMemcpyDeviceToDevice);
-        }
     }
+    if (e == hipSuccess && groups) e = hipMemcpy(d_gkey, gkey.data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice);
     if (e == hipSuccess && !fr.empty()) {
         e = hipMemcpy(d_fr, fr.data(), sizeof(LFlowRule) * fr.size(), hipMemcpyHostToDevice);
         std::vector<LCtl> c(fr.size(), LCtl{0, 0, -1, 0});  // storedTokens 0, lastFilledTime 0, latestPassedTime -1
         if (e == hipSuccess) e = hipMemcpy(d_ctl, c.data(), sizeof(LCtl) * c.size(), hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
+    dfree(d_src);
     if (e != hipSuccess) {
         release();
         return fail(h, SG_E_DEVICE, std::string("local flow rule upload: ") + hipGetErrorString(e));
@@ -2717,6 +2931,7 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     dfree(h->d_lmin);
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
+    dfree(h->d_lgkey);
     h->d_lrules = d_rules;
     h->d_lhead = d_head;
     h->d_lsec = d_sec;
@@ -2724,12 +2939,20 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     h->d_lmin = d_min;
     h->d_lfrules = d_fr;
     h->d_lctl = d_ctl;
+    h->d_lgkey = d_gkey;
     tab.resize(K);
     h->ltab = tab;
     h->l_nodes = (uint32_t)N;
     h->l_n_origins = n_origins;
+    h->l_n_contexts = n_contexts;
     h->l_has_cx = has_cx;
+    h->l_cluster_rules = cluster_rules;
     h->l_rule_slot = slot;
+    h->l_on_n = on_n;
+    h->l_on_base = on_base;
+    h->l_cn_n = cn_n;
+    h->l_cn_base = cn_base;
+    h->l_ps_applied = 0;  // param flags are re-applied to the new rule image by the next batch
     int kept = 0;
     for (int64_t x : slot) kept += x != -1;
     return kept;
@@ -3031,6 +3254,9 @@ int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, co
     HIP_TRY(h, hipDeviceSynchronize());
     h->ps_nres = n_resources;
     h->ps_loaded = true;
+    h->ps_res_rules.assign(n_resources, 0);
+    for (uint32_t r = 0; r < n_resources; ++r) h->ps_res_rules[r] = (uint32_t)per[r].size();
+    ++h->ps_gen;
     return SG_OK;
 }
 

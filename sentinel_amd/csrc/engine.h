@@ -426,7 +426,7 @@ struct LBreaker {             // AbstractCircuitBreaker state + its LeapArray(1,
 
 struct alignas(64) LHead {    // per resource: curThreadNum + up to two breakers (128 B)
     int64_t threads;
-    int64_t pad;
+    int64_t created;          // 1: the resource's ClusterNode exists (ClusterBuilderSlot ran for an entry)
     LBreaker cb[2];
     int64_t pad2[2];
 };
@@ -448,8 +448,14 @@ struct alignas(16) LRule {
     int32_t nb;               // breakers 0..2
     LBreakerRule b[2];
     uint32_t fr_begin, fr_n;  // cx: the resource's flow rules frules[fr_begin .. + fr_n) in check order
-    uint32_t onode;           // node index of origin 1 (origin o: onode + o - 1); kNoNode without origin nodes
-    int32_t cx;               // 1: walked by k_lwalk_cx (several rules, limitApps or shaping controllers)
+    uint32_t onode;           // node index of origin 1 (origin o: onode + o - 1, o <= on_n); kNoNode without origin nodes
+    int32_t cx;               // 1: walked by k_lwalk_cx (several rules, limitApps, shaping controllers, param rules,
+                              // origin / context nodes, RELATE groups)
+    uint32_t on_n;            // origin nodes of the resource (origin ids 1 .. on_n)
+    uint32_t cnode;           // node index of the DefaultNode of context 0 (context c: cnode + c, c < cn_n)
+    uint32_t cn_n;
+    int32_t ps;               // 1: the resource has ParamFlowSlot rules (sg_pslot_load_rules)
+    int32_t grp;              // 1: in a RELATE key group (walked event by event from memory, k_lwalk_cx)
 };
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
@@ -463,7 +469,9 @@ struct alignas(16) LFlowRule {
     int32_t limit_app;        // SG_LIMIT_APP_DEFAULT / _OTHER / origin id
     int32_t max_queue_ms;
     int32_t warning_token, max_token, cold;
-    int32_t pad;
+    int32_t strategy;         // SG_STRATEGY_*
+    int32_t ref;              // RELATE: resource index; CHAIN: context id; < 0: refResource blank
+    int32_t cluster_mode;     // SG_CLUSTER_MODE_* (cluster-mode rules are checked last, NOT_STARTED semantics)
 };
 
 struct alignas(32) LCtl {     // the controller's state: storedTokens, lastFilledTime, latestPassedTime
@@ -501,6 +509,11 @@ struct LArgs {
     uint32_t* np;
     int* err;
     int64_t* last_ts;
+    const sg_slot_ext* ext;   // per event: context and arguments (nullable: context 0, null args)
+    int32_t n_contexts;       // context ids 0 .. n_contexts - 1
+    const uint32_t* gkey;     // [K] record key of each resource (its RELATE group's first resource), or null
+    PSArgs ps;                // ParamFlowSlot rules, value tables and thread counts; ps.args / ps.values: the batch's
+    int32_t has_ps;           // 1: ps is loaded (resources with LRule.ps run ParamFlowSlot)
     int* flags;               // kLFlag*: batch properties that rule out the dead-period skip
     uint32_t* exit_pos;       // sorted positions of exit records (ascending), exit_cnt[0] of them
     uint32_t* exit_cnt;       // [0] total, then per-tile counts / offsets
@@ -522,6 +535,9 @@ hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
 hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
+// New node arrays of a flow-rule reload: node i copies old node src[i] (>= 0) or starts empty (L: the new arrays, N nodes)
+hipError_t launch_local_remap(const LArgs& L, const int64_t* src, const LHead* ohead, const LBucket* osec,
+                              const LFuture* obor, const LBucket* omin, hipStream_t stream);
 // StatisticNode.metrics() of every resource at now: emit == 0 counts the rows (no side effect), emit == 1 writes
 // them (any order) and applies currentWindow / lastFetchTime.
 hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,

@@ -14,7 +14,7 @@
 // buckets in registers and touch the rings in memory only when a window period changes. The rarely used
 // paths (prioritized occupy through the borrow array, thread-grade rules, breaker state changes) run one
 // event at a time ("serial step"); the wave walker decides everything else 64 events at a time.
-#include "engine.h"
+#include "pslot_dev.h"
 
 namespace sg {
 
@@ -148,14 +148,28 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         }
         const uint32_t res = e.resource & SG_KEY_INDEX;
         if (e.origin < 0 || e.origin > a.n_origins) atomicOr(a.err, kErrBounds);
+        if (a.ext) {  // the event's context and argument records (ParamFlowSlot reads them)
+            const sg_slot_ext x = a.ext[i];
+            if ((int64_t)x.context >= (int64_t)(a.n_contexts > 0 ? a.n_contexts : 1)) atomicOr(a.err, kErrBounds);
+            if (a.has_ps && !x.args_null && res < a.K) {
+                bool ok = (uint64_t)x.arg_begin + x.arg_count <= a.ps.n_args;
+                for (uint32_t k = 0; ok && k < x.arg_count; ++k) {
+                    const sg_pslot_arg g = a.ps.args[x.arg_begin + k];
+                    const uint64_t m = g.kind == SG_ARG_COLLECTION ? g.value_count : (g.kind == SG_ARG_VALUE ? 1 : 0);
+                    ok = (uint64_t)g.value_begin + m <= a.ps.n_values;
+                }
+                if (!ok) atomicOr(a.err, kErrBounds);
+            }
+        }
         uint64_t rec = sentinel;
         if (res < a.K) {
+            const uint32_t key = a.gkey ? a.gkey[res] : res;  // a RELATE group sorts as one key
             uint64_t c = (e.count < 0) ? a.aesc : (uint64_t)(uint32_t)e.count;
             if (c > a.aesc) c = a.aesc;
             // kind: 0 entry, 2 exit after a business error, anything else a plain exit
             const uint64_t kind = e.kind == SG_LOCAL_ENTRY ? 0 : (e.kind == SG_LOCAL_EXIT_ERROR ? 2 : 1);
             const uint64_t ac = (c << 3) | (kind << 1) | (uint64_t)(e.resource >> 31);
-            rec = ((uint64_t)res << a.kshift) | ((uint64_t)i << a.abits) | ac;
+            rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
             if (kind == 0 && (e.resource >> 31)) atomicOr(a.flags, kLFlagPrio);
             if (kind == 0 && e.count <= 0) atomicOr(a.flags, kLFlagNonPos);
         }
@@ -186,7 +200,7 @@ __global__ void __launch_bounds__(256) k_local_init(LArgs a) {
         if (q == 0) {
             LHead h;
             h.threads = 0;
-            h.pad = 0;
+            h.created = 0;
             for (int j = 0; j < 2; ++j) {
                 h.cb[j].next_retry = 0;
                 h.cb[j].stat_start = INT64_MIN;
@@ -196,6 +210,44 @@ __global__ void __launch_bounds__(256) k_local_init(LArgs a) {
             }
             h.pad2[0] = h.pad2[1] = 0;
             a.head[k] = h;
+        }
+    }
+}
+
+// Node i of the new arrays: a copy of old node src[i], or empty (src[i] < 0) — a flow-rule reload keeps every
+// resource's and every kept origin / context node's statistics (ClusterNode.originCountMap outlives the reload).
+__global__ void __launch_bounds__(256) k_local_remap(LArgs a, const int64_t* src, const LHead* ohead,
+                                                     const LBucket* osec, const LFuture* obor, const LBucket* omin) {
+    const uint64_t total = (uint64_t)a.N * kMinuteS;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = i / kMinuteS;
+        const int q = (int)(i % kMinuteS);
+        const int64_t from = src[k];
+        LBucket b;
+        b.start = INT64_MIN;
+        for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+        b.min_rt = kStatMaxRt;
+        a.minute[i] = from >= 0 ? omin[(uint64_t)from * kMinuteS + q] : b;
+        if (q < a.S) {
+            LFuture f;
+            f.start = INT64_MIN;
+            f.pass = 0;
+            a.sec[k * a.S + q] = from >= 0 ? osec[(uint64_t)from * a.S + q] : b;
+            a.bor[k * a.S + q] = from >= 0 ? obor[(uint64_t)from * a.S + q] : f;
+        }
+        if (q == 0) {
+            LHead h;
+            h.threads = 0;
+            h.created = 0;
+            for (int j = 0; j < 2; ++j) {
+                h.cb[j].next_retry = 0;
+                h.cb[j].stat_start = INT64_MIN;
+                h.cb[j].bad = h.cb[j].total = 0;
+                h.cb[j].state = kCbClosed;
+                h.cb[j].pad = 0;
+            }
+            h.pad2[0] = h.pad2[1] = 0;
+            a.head[k] = from >= 0 ? ohead[from] : h;
         }
     }
 }
@@ -220,6 +272,7 @@ struct LNode {
     int64_t mc[kLEv], m_min, m_ws;
     int mI;
     int64_t threads;
+    int64_t created;   // LHead.created (set by the walkers for a resource with events: ClusterBuilderSlot)
     LBreaker cb[2];
 
     __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), R(a_.rules[k_]), k(k_) {
@@ -237,6 +290,7 @@ struct LNode {
         for (int e = 0; e < kLEv; ++e) sc[e] = mc[e] = 0;
         const LHead h = a.head[k];
         threads = h.threads;
+        created = h.created;
         cb[0] = h.cb[0];
         cb[1] = h.cb[1];
     }
@@ -536,7 +590,7 @@ struct LNode {
         min_close();
         LHead h;
         h.threads = threads;
-        h.pad = 0;
+        h.created = created;
         h.cb[0] = cb[0];
         h.cb[1] = cb[1];
         h.pad2[0] = h.pad2[1] = 0;
@@ -594,6 +648,7 @@ __global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
         if (a.rules[k].cx) continue;  // k_lwalk_cx
         LNode nd(a, bndp, k);
+        nd.created = 1;  // the resource has events, so an entry reached ClusterBuilderSlot
         // software pipeline: records kRecAhead ahead, exit timestamps kEvAhead ahead (a lane walks up to
         // short_max contiguous records; one load in flight per record would leave it latency-bound)
         constexpr int kRecAhead = 8, kEvAhead = 4;
@@ -672,6 +727,7 @@ __device__ __forceinline__ uint64_t lwave_search(uint64_t lo, uint64_t hi, Pred 
 __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e_end) {
     const int lane = lane_id();
     LNode nd(a, bndp, k);
+    nd.created = 1;
     const int nb = nd.R.nb;
     const bool thread_grade = nd.R.flow_grade == 0;
     // a saturated second window (not even acquireCount 1 fits) FLOW-blocks every entry until the period
@@ -1012,15 +1068,27 @@ __device__ bool pace_step(const LFlowRule& r, LCtl& c, int64_t now, int64_t cost
     return true;
 }
 
-// FlowRuleChecker.selectNodeByRequesterAndStrategy (DIRECT): 0 the ClusterNode, 1 the origin node, -1 none
-__device__ int cx_select(const LArgs& a, const LRule& R, int32_t limit_app, int origin) {
-    if (origin > 0 && limit_app == origin) return 1;
-    if (limit_app == SG_LIMIT_APP_DEFAULT) return 0;
-    if (limit_app == SG_LIMIT_APP_OTHER && origin > 0) {  // FlowRuleManager.isOtherOrigin (:132-148)
+// FlowRuleChecker.selectNodeByRequesterAndStrategy (:115-145) with selectReferenceNode (:96-112): 0 the ClusterNode,
+// 1 the origin node, 2 the resource's DefaultNode of the current context (CHAIN), 3 the ClusterNode of r.ref
+// (RELATE; ref_exists() says whether ClusterBuilderSlot created it), -1 none (the rule passes)
+template <class RefExists>
+__device__ int cx_select(const LArgs& a, const LRule& R, const LFlowRule& r, int origin, int ctx, RefExists&& ref_exists) {
+    int matched;
+    if (origin > 0 && r.limit_app == origin) {
+        matched = 1;
+    } else if (r.limit_app == SG_LIMIT_APP_DEFAULT) {
+        matched = 0;
+    } else if (r.limit_app == SG_LIMIT_APP_OTHER && origin > 0) {  // FlowRuleManager.isOtherOrigin (:132-148)
         for (uint32_t i = 0; i < R.fr_n; ++i)
             if (a.frules[R.fr_begin + i].limit_app == origin) return -1;
-        return 1;
+        matched = 1;
+    } else {
+        return -1;
     }
+    if (r.strategy == SG_STRATEGY_DIRECT) return matched;
+    if (r.ref < 0) return -1;  // StringUtil.isEmpty(refResource)
+    if (r.strategy == SG_STRATEGY_RELATE) return ref_exists() ? 3 : -1;
+    if (r.strategy == SG_STRATEGY_CHAIN) return r.ref == ctx ? 2 : -1;
     return -1;
 }
 
@@ -1064,23 +1132,62 @@ __device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, co
     }
 }
 
-// One entry of a cx resource: FlowSlot (every rule) → DegradeSlot → StatisticSlot on the ClusterNode and the
-// origin node (StatisticSlot.java:55-122).
-__device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, uint32_t on_idx, const LEvent& e,
-                         int64_t t, int origin, uint32_t qs, uint32_t qm) {
-    const bool have_on = on_idx != kNoNode;
+// The nodes StatisticSlot updates for one event besides the ClusterNode: the origin node (ClusterBuilderSlot, origin
+// o of the event) and the DefaultNode of the event's context (NodeSelectorSlot), when the resource keeps them.
+__device__ __forceinline__ uint32_t origin_node_of(const LRule& R, int origin) {
+    return (R.onode != kNoNode && origin > 0 && (uint32_t)origin <= R.on_n) ? R.onode + (uint32_t)origin - 1 : kNoNode;
+}
+__device__ __forceinline__ uint32_t context_node_of(const LRule& R, int ctx) {
+    return (R.cnode != kNoNode && ctx >= 0 && (uint32_t)ctx < R.cn_n) ? R.cnode + (uint32_t)ctx : kNoNode;
+}
+
+// One entry of a cx resource, the slot chain in SPI order inside StatisticSlot.entry (StatisticSlot.java:55-122):
+// ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93, the event's arguments) → FlowSlot (every rule,
+// FlowRuleChecker.checkFlow :44-57; cluster-mode rules as on a node that is neither token client nor server,
+// passClusterCheck → fallbackToLocalOrPass :147-175) → DegradeSlot, then the StatisticSlot updates of the
+// ClusterNode, the origin node and the context's DefaultNode, and ParamFlowStatisticEntryCallback.onPass.
+__device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t, int origin,
+                         int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
+    const LRule& R = nd.R;
+    const uint32_t on_idx = origin_node_of(R, origin), cn_idx = context_node_of(R, ctx);
+    const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
     LNode on(a, bndp, have_on ? on_idx : nd.k);
     if (have_on) on.at(qs, qm);
+    LNode cn(a, bndp, have_cn ? cn_idx : nd.k);
+    if (have_cn) cn.at(qs, qm);
+    const bool params = R.ps && a.has_ps && x && !x->args_null;
     int32_t status = SG_LOCAL_PASS;
     int64_t wait = 0;
-    const LRule& R = nd.R;
-    for (uint32_t i = 0; i < R.fr_n; ++i) {
+    if (params) {  // ParamFlowSlot (@Spi order -3000): before FlowSlot
+        const int32_t pr = ps_check_entry(a.ps, nd.k, t, e.count, x->arg_begin, x->arg_count);
+        if (pr >= 0) {
+            status = SG_LOCAL_BLOCK_PARAM;
+            wait = pr;  // reported in wait_ms: the rule that threw ParamFlowException
+        }
+    }
+    for (uint32_t i = 0; status == SG_LOCAL_PASS && i < R.fr_n; ++i) {
         const LFlowRule r = a.frules[R.fr_begin + i];
-        const int sel = cx_select(a, R, r.limit_app, origin);
-        if (sel < 0 || (sel == 1 && !have_on)) continue;
+        if (r.cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) continue;  // cluster rule not activated: passes
+        const int sel = cx_select(a, R, r, origin, ctx, [&]() {
+            if (r.ref == (int32_t)nd.k) return true;  // this entry reached ClusterBuilderSlot
+            return (uint32_t)r.ref < a.K && a.head[r.ref].created != 0;
+        });
+        if (sel < 0 || (sel == 1 && !have_on) || (sel == 2 && !have_cn)) continue;
         LCtl& c = a.ctl[R.fr_begin + i];
         int64_t w = 0;
-        const int v = sel == 0 ? cx_rule(a, nd, r, c, e, t, &w) : cx_rule(a, on, r, c, e, t, &w);
+        int v;
+        if (sel == 0 || (sel == 3 && r.ref == (int32_t)nd.k)) {
+            v = cx_rule(a, nd, r, c, e, t, &w);
+        } else if (sel == 1) {
+            v = cx_rule(a, on, r, c, e, t, &w);
+        } else if (sel == 2) {
+            v = cx_rule(a, cn, r, c, e, t, &w);
+        } else {  // RELATE: another resource of this key group, kept in memory between its events
+            LNode rn(a, bndp, (uint32_t)r.ref);
+            rn.at(qs, qm);
+            v = cx_rule(a, rn, r, c, e, t, &w);
+            rn.finish();
+        }
         if (v == 0) {
             status = SG_LOCAL_BLOCK_FLOW;
             break;
@@ -1102,9 +1209,15 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
             on.sc[kLPass] += e.count;
             on.mc[kLPass] += e.count;
         }
+        if (have_cn) {
+            cn.threads += 1;
+            cn.sc[kLPass] += e.count;
+            cn.mc[kLPass] += e.count;
+        }
     } else if (status == SG_LOCAL_PASS_WAIT) {
         nd.threads += 1;
         if (have_on) on.threads += 1;
+        if (have_cn) cn.threads += 1;
     } else {
         nd.sc[kLBlock] += e.count;
         nd.mc[kLBlock] += e.count;
@@ -1112,15 +1225,45 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
             on.sc[kLBlock] += e.count;
             on.mc[kLBlock] += e.count;
         }
-        wait = 0;
+        if (have_cn) {
+            cn.sc[kLBlock] += e.count;
+            cn.mc[kLBlock] += e.count;
+        }
+        if (status != SG_LOCAL_BLOCK_PARAM) wait = 0;
     }
+    if (params && (status == SG_LOCAL_PASS || status == SG_LOCAL_PASS_WAIT))
+        ps_threads(a.ps, nd.k, x->arg_begin, x->arg_count, +1);  // ParamFlowStatisticEntryCallback.onPass
     lstore(a, e.idx, status, wait > INT32_MAX ? INT32_MAX : (int32_t)wait);
     if (have_on) on.finish();
+    if (have_cn) cn.finish();
+}
+
+// One exit of a cx resource: StatisticSlot.exit (:124-165) on the ClusterNode (+ DegradeSlot.exit), the origin node
+// and the context's DefaultNode; ParamFlowStatisticExitCallback.onExit (decreaseThreadCount of the exit's args).
+__device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t,
+                        int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
+    nd.exit(e, t, create);
+    const uint32_t on_idx = origin_node_of(nd.R, origin), cn_idx = context_node_of(nd.R, ctx);
+    if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
+        LNode on(a, bndp, on_idx);
+        on.at(qs, qm);
+        on.exit(e, t, create);
+        on.finish();
+    }
+    if (cn_idx != kNoNode) {
+        LNode cn(a, bndp, cn_idx);
+        cn.at(qs, qm);
+        cn.exit(e, t, create);
+        cn.finish();
+    }
+    if (nd.R.ps && a.has_ps && x && !x->args_null) ps_threads(a.ps, nd.k, x->arg_begin, x->arg_count, -1);
 }
 
 }  // namespace
 
-// One lane per segment of a cx resource, from every length class of k_seg's lists.
+// One lane per segment of a cx resource (or a RELATE key group), from every length class of k_seg's lists. A lone
+// resource keeps its ClusterNode in registers for the whole segment; a group's events belong to several resources
+// (one reads another's ClusterNode), so each event opens its resource's node from memory and writes it back.
 __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
@@ -1141,27 +1284,37 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
         }
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
         if (!a.rules[k].cx) continue;
+        if (a.rules[k].grp) {
+            for (uint64_t p = j; p < a.n; ++p) {
+                const uint64_t rec = a.rec_sorted[p];
+                if ((uint32_t)(rec >> a.kshift) != k) break;
+                const LEvent e = ldecode(a, rec);
+                const sg_local_event le = a.ev[e.idx];
+                const sg_slot_ext* x = a.ext ? a.ext + e.idx : nullptr;
+                const int ctx = x ? (int)x->context : 0;
+                LNode nd(a, bndp, le.resource & SG_KEY_INDEX);
+                nd.created = 1;
+                const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
+                nd.at(qs, qm);
+                if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
+                else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
+                nd.finish();
+            }
+            continue;
+        }
         LNode nd(a, bndp, k);
+        nd.created = 1;
         for (uint64_t p = j; p < a.n; ++p) {
             const uint64_t rec = a.rec_sorted[p];
             if ((uint32_t)(rec >> a.kshift) != k) break;
             const LEvent e = ldecode(a, rec);
             const sg_local_event le = a.ev[e.idx];
+            const sg_slot_ext* x = a.ext ? a.ext + e.idx : nullptr;
+            const int ctx = x ? (int)x->context : 0;
             const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
             nd.at(qs, qm);
-            const uint32_t on_idx = (nd.R.onode != kNoNode && le.origin > 0) ? nd.R.onode + (uint32_t)le.origin - 1
-                                                                              : kNoNode;
-            if (e.kind == SG_LOCAL_ENTRY) {
-                cx_entry(a, bndp, nd, on_idx, e, le.ts_ms, le.origin, qs, qm);
-            } else {
-                nd.exit(e, le.ts_ms, le.create_ts);
-                if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
-                    LNode on(a, bndp, on_idx);
-                    on.at(qs, qm);
-                    on.exit(e, le.ts_ms, le.create_ts);
-                    on.finish();
-                }
-            }
+            if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
+            else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
         }
         nd.finish();
     }
@@ -1339,6 +1492,14 @@ hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out
 hipError_t launch_local_init(const LArgs& a, hipStream_t stream) {
     if (a.K == 0) return hipSuccess;
     hipLaunchKernelGGL(k_local_init, dim3(lgrid((uint64_t)a.K * kMinuteS, 256, 8192)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_remap(const LArgs& a, const int64_t* src, const LHead* ohead, const LBucket* osec,
+                              const LFuture* obor, const LBucket* omin, hipStream_t stream) {
+    if (a.N == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_local_remap, dim3(lgrid((uint64_t)a.N * kMinuteS, 256, 8192)), dim3(256), 0, stream, a, src,
+                       ohead, osec, obor, omin);
     return hipGetLastError();
 }
 

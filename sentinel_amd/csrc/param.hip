@@ -12,64 +12,9 @@
 //   k_pwalk_short / k_pwalk_long  sequential replay per slot; the wave walker decides 64 requests per
 //              step (prefix-scan admit, ballot skip) and, once the bucket cannot pay even 1 token before
 //              the next refill, jumps to the first request after the refill time by a 64-way search.
-#include "engine.h"
+#include "pslot_dev.h"
 
 namespace sg {
-
-constexpr uint64_t kEmptyValue = ~0ull;
-
-__device__ __forceinline__ int64_t java_math_round(double a) {
-    // java.lang.Math.round(double), exact floor(a + 1/2) (JDK 7u+)
-    const int64_t bits = __double_as_longlong(a);
-    const int64_t biased_exp = (bits & 0x7FF0000000000000LL) >> 52;
-    const int64_t shift = (52 - 1 + 1023) - biased_exp;
-    if ((shift & -64) == 0) {
-        int64_t r = (bits & 0x000FFFFFFFFFFFFFLL) | 0x0010000000000000LL;
-        if (bits < 0) r = -r;
-        return ((r >> shift) + 1) >> 1;
-    }
-    if (a != a) return 0;
-    if (a >= 9223372036854775807.0) return INT64_MAX;
-    if (a <= -9223372036854775808.0) return INT64_MIN;
-    return (int64_t)a;
-}
-
-// tokenCount of (rule, value): the hot item's threshold, else (long) rule.count (ParamFlowChecker.java:137-141)
-__device__ __forceinline__ int64_t param_token_count(const PArgs& p, const PRule& r, uint64_t v) {
-    uint32_t lo = r.hot_begin, hi = r.hot_begin + r.hot_count;  // hot items sorted by value
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const uint64_t hv = p.hot[mid].value;
-        if (hv == v) return p.hot[mid].threshold;
-        if (hv < v) lo = mid + 1;
-        else hi = mid;
-    }
-    return r.token_count;
-}
-
-// find-or-insert (rule, value) → global slot index
-__device__ __forceinline__ uint64_t param_slot(const PArgs& p, const PRule& r, uint64_t v) {
-    if (v == kEmptyValue) return r.table_base + r.table_mask + 1;  // side slot
-    uint64_t h = v + 0x9E3779B97F4A7C15ull;
-    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
-    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
-    h ^= h >> 31;
-    uint64_t i = h & r.table_mask;
-    for (uint64_t probes = 0; probes <= r.table_mask; ++probes) {
-        unsigned long long* vw = (unsigned long long*)&p.table[r.table_base + i].value;
-        // a plain (L2-cached) load: a slot only ever goes from empty to its value, so a stale read can only say
-        // "empty", and the CAS below then returns the value that is there (an agent-scope atomic load bypassed
-        // the XCD's L2 on every probe, also for the hot values that repeat throughout a batch)
-        const unsigned long long cur = *vw;
-        if (cur == v) return r.table_base + i;
-        if (cur == kEmptyValue) {
-            const unsigned long long old = atomicCAS(vw, (unsigned long long)kEmptyValue, (unsigned long long)v);
-            if (old == kEmptyValue || old == v) return r.table_base + i;
-        }
-        i = (i + 1) & r.table_mask;
-    }
-    return ~0ull;  // table full
-}
 
 __global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -93,71 +38,6 @@ __global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
         p.out[i] = pass;
         p.rec[i] = rec;
     }
-}
-
-struct PState {
-    int64_t time, tokens;
-    uint32_t flags;  // bit0 time counter present, bit1 token counter present
-};
-
-struct PReqView {
-    int64_t t;
-    int64_t acq;
-};
-
-// One request of passDefaultLocalCheck at time t (ParamFlowChecker.java:147-201); returns pass.
-__device__ __forceinline__ bool param_default_step(PState& s, int64_t tc, int64_t maxc, int64_t dur_ms, int64_t t,
-                                                   int64_t acq) {
-    if (!(s.flags & 1u)) {
-        s.flags |= 1u;
-        s.time = t;
-        if (!(s.flags & 2u)) {
-            s.flags |= 2u;
-            s.tokens = maxc - acq;
-        }
-        return true;
-    }
-    const int64_t pass_time = t - s.time;
-    if (pass_time > dur_ms) {
-        if (!(s.flags & 2u)) {
-            s.flags |= 2u;
-            s.tokens = maxc - acq;
-            s.time = t;
-            return true;
-        }
-        const int64_t rest = s.tokens;
-        const int64_t to_add = (pass_time * tc) / dur_ms;
-        const int64_t nq = to_add + rest > maxc ? (maxc - acq) : (rest + to_add - acq);
-        if (nq < 0) return false;
-        s.tokens = nq;
-        s.time = t;
-        return true;
-    }
-    if ((s.flags & 2u) && s.tokens - acq >= 0) {
-        s.tokens -= acq;
-        return true;
-    }
-    return false;
-}
-
-// One request of passThrottleLocalCheck (:214-253); the wait is a sleep in Java, skipped in replay.
-__device__ __forceinline__ bool param_throttle_step(PState& s, int64_t cost, int32_t max_queue, int64_t t) {
-    if (!(s.flags & 1u)) {
-        s.flags |= 1u;
-        s.time = t;
-        return true;
-    }
-    const int64_t expected = s.time + cost;
-    if (expected <= t || expected - t < max_queue) {
-        s.time = t;
-        if (expected - t > 0) s.time = expected;
-        return true;
-    }
-    return false;
-}
-
-__device__ __forceinline__ int64_t throttle_cost(const PRule& r, int64_t tc, int64_t acq) {
-    return java_math_round(1.0 * 1000 * (double)acq * (double)r.duration_sec / (double)tc);
 }
 
 __device__ __forceinline__ uint32_t rule_of_slot(const PArgs& p, uint64_t g) {
@@ -440,99 +320,6 @@ hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, 
 
 namespace sg {
 
-namespace {
-
-__device__ __forceinline__ uint64_t ps_hash(unsigned long long owner, uint64_t v) {
-    uint64_t z = v + 0x9E3779B97F4A7C15ull * (owner + 1);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-__device__ __forceinline__ unsigned long long ps_owner(uint32_t res, int32_t idx) {
-    return ((unsigned long long)(res + 1) << 32) | (unsigned long long)(uint32_t)(idx + 1);
-}
-
-// threadCountMap lookup; create: insert at 0 when absent (putIfAbsent). Returns the slot or -1.
-__device__ int64_t ps_tc(const PSArgs& s, uint32_t res, int32_t idx, uint64_t v, bool create) {
-    const unsigned long long own = ps_owner(res, idx);
-    uint64_t h = ps_hash(own, v) & s.tc_mask;
-    for (uint64_t probes = 0; probes <= s.tc_mask; ++probes, h = (h + 1) & s.tc_mask) {
-        PSThread& e = s.tc[h];
-        const unsigned long long o = __hip_atomic_load(&e.owner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o == own && e.value == v) return (int64_t)h;
-        if (o == 0) {
-            if (!create) return -1;
-            // claim the slot; only this resource's lane ever reads entries with this owner word
-            if (atomicCAS(&e.owner, 0ull, own) == 0ull) {
-                e.value = v;
-                e.count = 0;
-                return (int64_t)h;
-            }
-        }
-    }
-    if (create) atomicOr(s.err, kErrTableFull);
-    return -1;
-}
-
-// passSingleValueCheck (:106-125) for rule ri at time t
-__device__ bool ps_single(const PSArgs& s, uint32_t ri, uint32_t res, int64_t t, int64_t acq, uint64_t v) {
-    const PRule r = s.p.rules[ri];
-    const int64_t tc = param_token_count(s.p, r, v);  // the hot item's threshold, else (long) count
-    if (s.grade[ri] == 1) {
-        if (tc == 0) return false;
-        if (r.behavior != 2 && acq > tc + r.burst) return false;
-        const uint64_t g = param_slot(s.p, r, v);
-        if (g == ~0ull) {
-            atomicOr(s.err, kErrTableFull);
-            return false;
-        }
-        PSlot& slot = s.p.table[g];
-        PState st{slot.time, slot.tokens, slot.flags};
-        const bool ok = r.behavior == 2 ? param_throttle_step(st, throttle_cost(r, tc, acq), r.max_queueing_ms, t)
-                                        : param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, acq);
-        slot.time = st.time;
-        slot.tokens = st.tokens;
-        slot.flags = st.flags;
-        return ok;
-    }
-    if (s.grade[ri] == 0) {
-        const int64_t e = ps_tc(s, res, s.cur_idx[ri], v, false);
-        const int64_t threads = e >= 0 ? s.tc[e].count : 0;
-        return threads + 1 <= tc;
-    }
-    return true;
-}
-
-// addThreadCount / decreaseThreadCount over the argument indices that have a thread map
-__device__ void ps_threads(const PSArgs& s, uint32_t res, const sg_pslot_event& e, int d) {
-    const uint32_t rb = s.res_begin[res], re = s.res_begin[res + 1];
-    for (uint32_t idx = 0; idx < e.arg_count; ++idx) {
-        bool has_map = false;
-        for (uint32_t k = rb; k < re && !has_map; ++k) {
-            const uint32_t ri = s.res_rules[k];
-            has_map = s.inited[ri] && s.cur_idx[ri] == (int32_t)idx;
-        }
-        if (!has_map) continue;
-        const sg_pslot_arg a = s.args[e.arg_begin + idx];
-        if (a.kind == SG_ARG_NULL) continue;
-        const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
-        for (uint32_t j = 0; j < m; ++j) {
-            const uint64_t v = s.values[a.value_begin + j];
-            if (d > 0) {
-                const int64_t x = ps_tc(s, res, (int32_t)idx, v, true);
-                if (x >= 0) s.tc[x].count += 1;
-            } else {
-                const int64_t x = ps_tc(s, res, (int32_t)idx, v, false);
-                if (x >= 0) s.tc[x].count = s.tc[x].count > 0 ? s.tc[x].count - 1 : 0;  // <= 0: removed (reads 0)
-                else ps_tc(s, res, (int32_t)idx, v, true);                             // putIfAbsent(0)
-            }
-        }
-    }
-}
-
-}  // namespace
-
 __global__ void __launch_bounds__(256) k_psprep(PSArgs s) {
     const uint64_t sentinel = (uint64_t)s.n_res << s.kshift;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < s.n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -563,40 +350,18 @@ __global__ void __launch_bounds__(256) k_pswalk(PSArgs s, const uint64_t* sorted
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < s.n; p += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t res = (uint32_t)(sorted[p] >> s.kshift);
         if (res >= s.n_res || (p > 0 && (uint32_t)(sorted[p - 1] >> s.kshift) == res)) continue;
-        const uint32_t rb = s.res_begin[res], re = s.res_begin[res + 1];
         for (uint64_t q = p; q < s.n; ++q) {
             const uint64_t rec = sorted[q];
             if ((uint32_t)(rec >> s.kshift) != res) break;
             const uint64_t i = rec & s.imask;
             const sg_pslot_event e = s.ev[i];
             if (e.kind != SG_LOCAL_ENTRY) {  // ParamFlowStatisticExitCallback (passed entries only)
-                ps_threads(s, res, e, -1);
+                ps_threads(s, res, e.arg_begin, e.arg_count, -1);
                 continue;
             }
-            bool pass = true;
-            int32_t failed = -1;
-            for (uint32_t k = rb; k < re && pass; ++k) {
-                const uint32_t ri = s.res_rules[k];
-                int32_t idx = s.cur_idx[ri];
-                if (idx < 0) {  // applyRealParamIdx(rule, args.length)
-                    idx = (-idx <= (int32_t)e.arg_count) ? (int32_t)e.arg_count + idx : -idx;
-                    s.cur_idx[ri] = idx;
-                }
-                s.inited[ri] = 1;
-                if ((int32_t)e.arg_count <= idx) continue;
-                const sg_pslot_arg a = s.args[e.arg_begin + (uint32_t)idx];
-                if (a.kind == SG_ARG_NULL) continue;
-                const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
-                for (uint32_t j = 0; j < m; ++j) {
-                    if (!ps_single(s, ri, res, e.ts_ms, (int64_t)e.count, s.values[a.value_begin + j])) {
-                        pass = false;
-                        failed = (int32_t)ri;
-                        break;
-                    }
-                }
-            }
-            if (pass) {
-                ps_threads(s, res, e, +1);
+            const int32_t failed = ps_check_entry(s, res, e.ts_ms, e.count, e.arg_begin, e.arg_count);
+            if (failed < 0) {
+                ps_threads(s, res, e.arg_begin, e.arg_count, +1);
             } else {
                 sg_pslot_result r;
                 r.pass = 0;

@@ -21,6 +21,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
            "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
+           "sg_local_read_context_state", "sg_local_set_cluster_state", "sg_slot_decide_batch",
+           "sg_slot_decide_batch_host",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
            "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values", "sg_cparam_last_rounds",
@@ -87,7 +89,11 @@ def load_library():
         "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
-        "sg_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32]),
+        "sg_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
+        "sg_local_read_context_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
+        "sg_local_set_cluster_state": (C.c_int, [vp, C.c_int32]),
+        "sg_slot_decide_batch": (C.c_int, [vp, vp, vp, u64, vp, u64, vp, u64, vp, vp]),
+        "sg_slot_decide_batch_host": (C.c_int, [vp, vp, vp, u64, vp, u64, vp, u64, vp]),
         "sg_local_read_origin_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
         "sg_local_read_controller": (C.c_int, [vp, u32, vp]),
         "sg_codec_decode_flow": (C.c_int, [vp, vp, vp, vp, u64, vp, vp, vp, vp]),
@@ -448,12 +454,54 @@ class FlowEngine:
         self._check(self._L.sg_local_metrics(self.h, now_ms, abi.ptr(out), len(out), C.byref(n)))
         return out[:n.value]
 
-    def local_load_flow_rules(self, rules: np.ndarray, n_origins=0) -> int:
-        """FlowRuleManager.loadRules for the local chain: returns the number of rules kept."""
+    def local_load_flow_rules(self, rules: np.ndarray, n_origins=0, n_contexts=0) -> int:
+        """FlowRuleManager.loadRules for the local chain; returns the number of rules kept."""
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_FLOW_RULE_DTYPE).reshape(-1)
-        rc = self._L.sg_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins)
+        rc = self._L.sg_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins, n_contexts)
         self._check(min(rc, 0))
         return rc
+
+    def local_set_cluster_state(self, state):
+        """ClusterStateManager state (CLUSTER_NOT_STARTED -1 is the one the device decides cluster rules in)."""
+        self._check(self._L.sg_local_set_cluster_state(self.h, state))
+
+    def slot_decide_host(self, ev, ext, args, values) -> np.ndarray:
+        """The whole slot chain (sg_slot_decide_batch_host): StatisticSlot around ParamFlowSlot → FlowSlot →
+        DegradeSlot for HOST events with their context / argument records (ext may be None)."""
+        ev = np.ascontiguousarray(ev, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
+        out = np.zeros(len(ev), abi.LOCAL_RES_DTYPE)
+        if len(ev) == 0:
+            return out
+        xp = None
+        if ext is not None:
+            ext = np.ascontiguousarray(ext, dtype=abi.SLOT_EXT_DTYPE).reshape(-1)
+            xp = abi.ptr(ext)
+        args = np.ascontiguousarray(np.zeros(0, abi.PSLOT_ARG_DTYPE) if args is None else args,
+                                    dtype=abi.PSLOT_ARG_DTYPE).reshape(-1)
+        values = np.ascontiguousarray(np.zeros(0, np.uint64) if values is None else values, dtype=np.uint64).reshape(-1)
+        self._check(self._L.sg_slot_decide_batch_host(self.h, abi.ptr(ev), xp, len(ev),
+                                                      abi.ptr(args) if len(args) else None, len(args),
+                                                      abi.ptr(values) if len(values) else None, len(values),
+                                                      abi.ptr(out)))
+        return out
+
+    def slot_decide_device(self, ev_ptr: int, ext_ptr: int, n: int, args_ptr: int, n_args: int, values_ptr: int,
+                           n_values: int, out_ptr: int, stream_ptr: int = 0):
+        """DEVICE pointers (ext_ptr 0: no ext)."""
+        self._check(self._L.sg_slot_decide_batch(self.h, C.c_void_p(ev_ptr), C.c_void_p(ext_ptr or None), n,
+                                                 C.c_void_p(args_ptr or None), n_args, C.c_void_p(values_ptr or None),
+                                                 n_values, C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
+
+    def local_context_state(self, res, context):
+        """The DefaultNode of (res, context): (second, borrow, minute, head) as local_state."""
+        S = self.local_S
+        sec = np.zeros((S, 8), np.int64)
+        bor = np.zeros((S, 2), np.int64)
+        mnt = np.zeros((60, 8), np.int64)
+        head = np.zeros(14, np.int64)
+        self._check(self._L.sg_local_read_context_state(self.h, res, context, abi.ptr(sec), abi.ptr(bor),
+                                                        abi.ptr(mnt), abi.ptr(head)))
+        return sec, bor, mnt, head
 
     def local_origin_state(self, res, origin):
         S = self.local_S

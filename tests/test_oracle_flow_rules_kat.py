@@ -103,11 +103,111 @@ def test_pass_check_select_empty_node_success():
         assert ch.entry(t + i, origin=defo)[0] == abi.LOCAL_PASS
 
 
-def test_reference_strategies_are_refused():
+def test_select_node_for_empty_reference():
+    """testSelectNodeForEmptyReference: a CHAIN rule without refResource selects no node."""
+    rules = np.array([local_flow_rule(count=1, strategy=abi.STRATEGY_CHAIN, ref=-1)])
+    assert select_node(rules, 0, 0, context=0) is None
+
+
+def test_select_node_for_relate_reference():
+    """testSelectNodeForRelateReference: RELATE reads refResource's ClusterNode when ClusterBuilderSlot created it
+    (the test puts it into the map); without it, no node."""
+    rules = np.array([local_flow_rule(count=1, strategy=abi.STRATEGY_RELATE, ref=1)])
+    assert select_node(rules, 0, 0, ref_exists=True) == 3
+    assert select_node(rules, 0, 0, ref_exists=False) is None
+
+
+def test_select_reference_node_for_context_entrance():
+    """testSelectReferenceNodeForContextEntrance: CHAIN selects the DefaultNode only in the named context."""
+    good, other = 5, 6
+    rules = np.array([local_flow_rule(count=1, strategy=abi.STRATEGY_CHAIN, ref=good)])
+    assert select_node(rules, 0, 0, context=good) == 2
+    assert select_node(rules, 0, 0, context=other) is None
+
+
+def test_select_reference_node_for_origin_rules():
+    """A limitApp origin / "other" rule with a reference strategy: the origin match decides whether the reference
+    node is looked at at all (selectNodeByRequesterAndStrategy :122-141)."""
+    appA, appB, ctx = 1, 2, 3
+    rules = np.array([local_flow_rule(count=1, limit_app=appA, strategy=abi.STRATEGY_CHAIN, ref=ctx),
+                      local_flow_rule(count=1, limit_app=abi.LIMIT_APP_OTHER, strategy=abi.STRATEGY_RELATE, ref=0)])
+    assert select_node(rules, 0, appA, context=ctx) == 2
+    assert select_node(rules, 0, appB, context=ctx) is None
+    assert select_node(rules, 1, appB) == 3
+    assert select_node(rules, 1, appA) is None    # appA has its own rule: not "other"
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_partial_integration_strategy(t0):
+    """FlowPartialIntegrationTest.testStrategy: a DIRECT count-0 rule blocks inside a named context; then the rule is
+    replaced by a CHAIN rule of another resource without refResource (invalid, ignored): the entry passes."""
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule(), local_rule()]))
+    assert ch.load_flow_rules(np.array([local_flow_rule(0, count=0)]), n_contexts=3) == 1
+    x = np.zeros(1, abi.SLOT_EXT_DTYPE)
+    x["context"], x["args_null"] = 1, 1                           # ContextUtil.enter("testStrategy")
+    ev = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
+    ev["ts_ms"], ev["count"] = t0, 1
+    assert ch.decide_ext(ev, x, [], [])[0]["status"] == abi.LOCAL_BLOCK_FLOW
+    assert ch.load_flow_rules(np.array([local_flow_rule(1, count=0, strategy=abi.STRATEGY_CHAIN)]), n_contexts=3) == 0
+    x["context"] = 2                                              # ContextUtil.enter("entry1")
+    assert ch.decide_ext(ev, x, [], [])[0]["status"] == abi.LOCAL_PASS
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_chain_rule_reads_the_context_default_node(t0):
+    """A CHAIN rule limits the resource's entries through one context only; the DefaultNode of that context counts
+    that context's traffic, while the ClusterNode counts every context's."""
     ch = LocalChain()
     ch.load_rules(np.array([local_rule()]))
-    with pytest.raises(ValueError):
-        ch.load_flow_rules(np.array([local_flow_rule(count=1, strategy=abi.STRATEGY_RELATE)]))
+    assert ch.load_flow_rules(np.array([local_flow_rule(0, count=2, strategy=abi.STRATEGY_CHAIN, ref=1)]),
+                              n_contexts=2) == 1
+    ev = np.zeros(6, abi.LOCAL_EVENT_DTYPE)
+    ev["ts_ms"], ev["count"] = t0, 1
+    x = np.zeros(6, abi.SLOT_EXT_DTYPE)
+    x["args_null"] = 1
+    x["context"] = [1, 0, 1, 0, 1, 0]
+    st = ch.decide_ext(ev, x, [], [])["status"].tolist()
+    assert st == [abi.LOCAL_PASS, abi.LOCAL_PASS, abi.LOCAL_PASS, abi.LOCAL_PASS, abi.LOCAL_BLOCK_FLOW, abi.LOCAL_PASS]
+    assert ch.second_sum(0, t0, 0) == 5 and ch.second_sum(0, t0, 1) == 1
+    d1 = ch.context_dump(0, 1)
+    assert d1[4] and d1[0][:, 1].sum() == 2 and d1[0][:, 2].sum() == 1 and d1[3] == 2
+    d0 = ch.context_dump(0, 0)
+    assert d0[0][:, 1].sum() == 3 and d0[3] == 3
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_relate_rule_reads_the_referenced_cluster_node(t0):
+    """A RELATE rule on resource 0 limits it by resource 1's pass QPS; before resource 1's first entry there is no
+    ClusterNode (ClusterBuilderSlot), so the rule passes even at count 0."""
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule(), local_rule()]))
+    assert ch.load_flow_rules(np.array([local_flow_rule(0, count=0, strategy=abi.STRATEGY_RELATE, ref=1)])) == 1
+    assert ch.entry(t0, res=0)[0] == abi.LOCAL_PASS          # no ClusterNode of resource 1 yet
+    ch.load_flow_rules(np.array([local_flow_rule(0, count=2, strategy=abi.STRATEGY_RELATE, ref=1)]))
+    for _ in range(2):
+        assert ch.entry(t0, res=1)[0] == abi.LOCAL_PASS      # resource 1: no rule
+    assert ch.entry(t0, res=0)[0] == abi.LOCAL_BLOCK_FLOW    # 2 + 1 > 2 on resource 1's node
+    assert ch.second_sum(1, t0, 0) == 2 and ch.second_sum(0, t0, 1) == 1
+    assert ch.entry(t0 + 1000, res=0)[0] == abi.LOCAL_PASS   # resource 1's second is over
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_cluster_mode_rules_without_a_token_service(t0):
+    """FlowRuleChecker.passClusterCheck on a node that is neither token client nor server: fallbackToLocalOrPass —
+    with fallbackToLocalWhenFail the rule is checked locally, without it the rule passes; cluster rules sort after
+    local ones (FlowRuleComparator :31-37)."""
+    ch = LocalChain()
+    ch.load_rules(np.array([local_rule(), local_rule()]))
+    rules = np.array([local_flow_rule(0, count=0, cluster_mode=abi.CLUSTER_MODE_NO_FALLBACK, cluster_config=7),
+                      local_flow_rule(1, count=1, cluster_mode=abi.CLUSTER_MODE_FALLBACK, cluster_config=8),
+                      local_flow_rule(1, count=5),
+                      local_flow_rule(0, count=1, cluster_mode=abi.CLUSTER_MODE_INVALID)])
+    assert ch.load_flow_rules(rules) == 3
+    assert ch.rule_order(1) == [2, 1]
+    assert ch.entry(t0, res=0)[0] == abi.LOCAL_PASS          # not activated
+    assert ch.entry(t0, res=1)[0] == abi.LOCAL_PASS
+    assert ch.entry(t0, res=1)[0] == abi.LOCAL_BLOCK_FLOW    # the fallback's local check (count 1)
 
 
 def test_flow_rule_comparator_order():
