@@ -1165,15 +1165,31 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
             wait = pr;  // reported in wait_ms: the rule that threw ParamFlowException
         }
     }
-    for (uint32_t i = 0; status == SG_LOCAL_PASS && i < R.fr_n; ++i) {
-        const LFlowRule r = a.frules[R.fr_begin + i];
+    // the rules in check order; a resource whose one DefaultController rule the fast walkers read from R (it is
+    // walked here because of its param rules) gets that rule back as a plain DIRECT / "default" rule
+    const uint32_t n_rules = R.fr_n ? R.fr_n : (R.flow_grade >= 0 ? 1u : 0u);
+    LCtl stateless{0, 0, -1, 0};
+    for (uint32_t i = 0; status == SG_LOCAL_PASS && i < n_rules; ++i) {
+        LFlowRule r;
+        if (R.fr_n) {
+            r = a.frules[R.fr_begin + i];
+        } else {
+            r = LFlowRule{};
+            r.count = R.flow_count;
+            r.grade = R.flow_grade;
+            r.behavior = SG_CONTROL_DEFAULT;
+            r.limit_app = SG_LIMIT_APP_DEFAULT;
+            r.strategy = SG_STRATEGY_DIRECT;
+            r.ref = -1;
+            r.cluster_mode = SG_CLUSTER_MODE_OFF;
+        }
         if (r.cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) continue;  // cluster rule not activated: passes
         const int sel = cx_select(a, R, r, origin, ctx, [&]() {
             if (r.ref == (int32_t)nd.k) return true;  // this entry reached ClusterBuilderSlot
             return (uint32_t)r.ref < a.K && a.head[r.ref].created != 0;
         });
         if (sel < 0 || (sel == 1 && !have_on) || (sel == 2 && !have_cn)) continue;
-        LCtl& c = a.ctl[R.fr_begin + i];
+        LCtl& c = R.fr_n ? a.ctl[R.fr_begin + i] : stateless;
         int64_t w = 0;
         int v;
         if (sel == 0 || (sel == 3 && r.ref == (int32_t)nd.k)) {

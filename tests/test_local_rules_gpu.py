@@ -183,19 +183,37 @@ def test_hot_cx_resource():
 
 
 def test_reload_keeps_statistics_and_resets_controllers():
+    """A reload keeps every resource's statistics and its origin nodes (ClusterNode.originCountMap outlives it) and
+    starts fresh controllers. The new rule sets name origins only on resources that named them before: the device
+    keeps origin nodes from the first load that names an origin for the resource (the reference from the
+    resource's first entry with that origin)."""
     rng = np.random.default_rng(6)
     n_res, n_origins = 12, 3
-    ora, eng, fr = _setup(n_res, rng, n_origins)
+    sets0 = [_rule_set(rng, r, n_origins) for r in range(n_res)]
+    ora, eng, fr = _setup(n_res, rng, n_origins, rule_sets=sets0)
     t = _run(ora, eng, fr, n_res, n_origins, [(10_000, 2000)], 6)
-    sets = [_rule_set(rng, r, n_origins) for r in range(n_res)]
-    flat = np.array([x for rs in sets for x in rs], abi.LOCAL_FLOW_RULE_DTYPE)
+    sets = []
+    for rs in sets0:  # same shapes, new thresholds, some resources' rules dropped, shuffled
+        if rng.random() < 0.25:
+            sets.append([])
+            continue
+        new = []
+        for x in rs:
+            y = x.copy()
+            y["count"] = float(rng.integers(1, 60))
+            new.append(y)
+        sets.append(new)
+    flat = [x for rs in sets for x in rs]
+    rng.shuffle(flat)
+    flat = np.array(flat, abi.LOCAL_FLOW_RULE_DTYPE)
     assert eng.local_load_flow_rules(flat, n_origins) == ora.load_flow_rules(flat, n_origins)
     gen = LocalTraceGen(ora)
     ent = _entries(rng, 10_000, n_res, t, 2000, n_origins)
     ev, want = gen.run(ent, rng.integers(0, 40, 10_000).astype(np.int32), np.zeros(10_000, np.uint8), t + 2000)
     got = eng.local_decide_host(ev)
     assert np.array_equal(got, want)
-    _compare(eng, ora, flat, n_res, n_origins)
+    _compare(eng, ora, fr, n_res, n_origins)    # every origin node the first load created
+    _compare(eng, ora, flat, n_res, n_origins)  # the new rules' controllers
 
 
 def test_bad_origin_rejected():

@@ -244,7 +244,8 @@ def test_hot_resources_with_params():
             [local_flow_rule(3, 30.0, strategy=CHAIN, ref=1)], [local_flow_rule(4, 200.0)], []]
     params = np.array([prule(res=0, idx=0, count=20.0), prule(res=1, idx=1, count=3.0, grade=THREAD),
                        prule(res=2, idx=0, count=15.0, behavior=abi.BEHAVIOR_RATE_LIMITER, max_q=100),
-                       prule(res=3, idx=0, count=8.0), prule(res=5, idx=0, count=5.0)], abi.PSLOT_RULE_DTYPE)
+                       prule(res=3, idx=0, count=8.0), prule(res=4, idx=0, count=30.0),  # + the fast-path rule
+                       prule(res=5, idx=0, count=5.0)], abi.PSLOT_RULE_DTYPE)
     ora, ps, eng, fr, params = _setup(rng, n_res, 2, 2, rule_sets=sets, params=params)
     _run(ora, ps, eng, fr, params, n_res, 2, 2, [(60_000, 3000), (60_000, 3000)], 11, zipf=1.5)
 
