@@ -650,8 +650,17 @@ int sg_local_read_context_state(sg_handle* h, uint32_t res, int32_t context, int
  *                      than the node's lastFetchTime and older than now's second, non-empty; lastFetchTime advances.
  *                      Rows sorted by (timestamp, resource) into HOST memory; *n_rows = the number of rows (with
  *                      SG_E_CAPACITY and no side effect when cap is too small). The host formats them as metrics.log
- *                      lines (MetricNode.toFatString, MetricNode.java:213-229; sentinel_amd/metrics.py). The
- *                      ENTRY_NODE aggregate (__total_inbound_traffic__) is not kept on the device. */
+ *                      lines (MetricNode.toFatString, MetricNode.java:213-229; sentinel_amd/metrics.py). After
+ *                      the resources, Constants.ENTRY_NODE (__total_inbound_traffic__, MetricTimerListener.java:46):
+ *                      rows with resource = SG_ENTRY_NODE_RESOURCE, the sums of the inbound resources' buckets of each
+ *                      second (StatisticSlot adds every EntryType.IN entry / exit to it, StatisticSlot.java:71-75,
+ *                      :139-141) less their occupied passes (StatisticNode.addOccupiedPass raises only the selected
+ *                      node's PASS, StatisticNode.java:333-336), occupied_pass_qps 0, with the ENTRY_NODE's own
+ *                      lastFetchTime. Exact when rows are fetched at least once a minute (a resource's bucket of a
+ *                      second outlives it by the minute window).
+ *   sg_local_set_entry_types ← the EntryType of each resource's SphU.entry calls (1 = IN; default OUT, as
+ *                      SphU.entry(name)). */
+#define SG_ENTRY_NODE_RESOURCE 0xFFFFFFFFu
 typedef struct sg_metric_node {
     int64_t  timestamp;
     int64_t  pass_qps, block_qps, success_qps, exception_qps;
@@ -661,6 +670,7 @@ typedef struct sg_metric_node {
     int32_t  concurrency;         /* 0, as fromBucket leaves it */
 } sg_metric_node;
 int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows);
+int sg_local_set_entry_types(sg_handle* h, const uint8_t* inbound, uint32_t n);
 int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64_t* second, int64_t* borrow,
                                int64_t* minute, int64_t* head);
 int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);

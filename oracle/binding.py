@@ -88,6 +88,7 @@ def lib():
         "or_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
         "or_local_decide_ext": (C.c_int, [vp, vp, vp, u64, vp, vp, vp]),
         "or_local_attach_pslot": (None, [vp, vp]),
+        "or_local_set_entry_types": (C.c_int, [vp, vp, u32]),
         "or_local_context_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
         "or_lgen_run_ext": (u64, [vp, vp, vp, vp, vp, u64, i64, vp, vp, vp, u64, vp, vp]),
         "or_local_set_cold_factor": (None, [vp, C.c_int]),
@@ -687,6 +688,10 @@ class LocalChain:
         e = np.zeros(1, abi.LOCAL_EVENT_DTYPE)
         e[0] = (t, create_ts, res, count, abi.LOCAL_EXIT_ERROR if error else abi.LOCAL_EXIT, origin)
         self.decide(e)
+
+    def set_entry_types(self, inbound):
+        v = np.ascontiguousarray(inbound, dtype=np.uint8)
+        assert lib().or_local_set_entry_types(self.h, abi.ptr(v), len(v)) == 0
 
     def attach_params(self, pslot):
         """The ParamFlowSlot of the chain: a ParamSlot whose rules name this chain's resources."""

@@ -907,6 +907,9 @@ struct or_local {
     int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
     uint32_t n_rules;
     struct or_pslot* ps;     /* ParamFlowSlot's rules and metrics (or_local_attach_pslot), NULL = none */
+    uint8_t* inbound;        /* per resource: its entries are EntryType.IN (Constants.ENTRY_NODE counts them) */
+    or_node* entry;          /* Constants.ENTRY_NODE, the global inbound StatisticNode (created with the resources) */
+    int64_t entry_fetch;     /* its lastFetchTime */
 };
 
 or_local* or_local_new(int second_sample_count, int second_interval_ms, int occupy_timeout_ms) {
@@ -957,6 +960,10 @@ static void free_nodes(or_local* l) {
     free(l->nodes);
     free(l->rule_pos);
     free(l->last_fetch);
+    free(l->inbound);
+    l->inbound = NULL;
+    free_plain(l->entry);
+    l->entry = NULL;
     l->last_fetch = NULL;
     l->rule_pos = NULL;
     l->n_rules = 0;
@@ -1070,6 +1077,9 @@ int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
     l->n = n;
     l->n_origins = 0;
     l->n_contexts = 0;
+    l->inbound = (uint8_t*)calloc(n ? n : 1, 1);   /* SphU.entry's default EntryType.OUT */
+    l->entry = node_new_plain(l);
+    l->entry_fetch = -1;
     for (uint32_t i = 0; i < n; i++) {
         or_node* nd = &l->nodes[i];
         nd->rule = rules[i];
@@ -1454,6 +1464,7 @@ static void local_event(or_local* l, const sg_local_event* e, const sg_slot_ext*
     or_node* nd = &l->nodes[res];
     or_node* on = origin_node(l, nd, e->origin);   /* context.getCurEntry().getOriginNode() */
     or_node* dn = context_node(l, nd, context);    /* the DefaultNode (NodeSelectorSlot); mirrors into nd */
+    or_node* en = l->inbound[res] ? l->entry : NULL; /* EntryType.IN: Constants.ENTRY_NODE (StatisticSlot :71-75) */
     int64_t t = e->ts_ms;
     int count = e->count;
     if (e->kind == SG_LOCAL_ENTRY) {
@@ -1479,9 +1490,9 @@ static void local_event(or_local* l, const sg_local_event* e, const sg_slot_ext*
                     if (half[j] && nd->cb[j].state == OR_CB_HALF_OPEN) nd->cb[j].state = OR_CB_OPEN;
         }
         /* StatisticSlot.entry (:55-122): the DefaultNode (→ ClusterNode) and the origin node */
-        or_node* upd[3] = {nd, on, dn};
+        or_node* upd[4] = {nd, on, dn, en};
         if (status == SG_LOCAL_PASS) {
-            for (int u = 0; u < 3; u++) {
+            for (int u = 0; u < 4; u++) {
                 if (!upd[u]) continue;
                 upd[u]->threads++;
                 node_add(upd[u]->second, t, OR_M_PASS, count); /* addPassRequest: both windows */
@@ -1489,11 +1500,11 @@ static void local_event(or_local* l, const sg_local_event* e, const sg_slot_ext*
             }
             out->wait_ms = wait > INT32_MAX ? INT32_MAX : (int32_t)wait;   /* the rate limiters' sleep */
         } else if (status == SG_LOCAL_PASS_WAIT) {
-            for (int u = 0; u < 3; u++)
+            for (int u = 0; u < 4; u++)
                 if (upd[u]) upd[u]->threads++;
             out->wait_ms = (int32_t)wait;
         } else {
-            for (int u = 0; u < 3; u++) {
+            for (int u = 0; u < 4; u++) {
                 if (!upd[u]) continue;
                 node_add(upd[u]->second, t, OR_M_BLOCK, count); /* increaseBlockQps */
                 node_add(upd[u]->minute, t, OR_M_BLOCK, count);
@@ -1510,6 +1521,7 @@ static void local_event(or_local* l, const sg_local_event* e, const sg_slot_ext*
         record_complete(nd, t, count, rt, error);
         if (on) record_complete(on, t, count, rt, error);
         if (dn) record_complete(dn, t, count, rt, error);
+        if (en) record_complete(en, t, count, rt, error);
         /* ParamFlowStatisticExitCallback.onExit: decreaseThreadCount(args) (the entry passed) */
         if (l->ps && !args_null) pslot_exit(l->ps, res, t, a, na, values, -1);
         /* DegradeSlot.exit → onRequestComplete */
@@ -2323,47 +2335,56 @@ static int metric_row_less(const sg_metric_node* a, const sg_metric_node* b) {
 
 /* MetricTimerListener.run over every resource: rows sorted by (timestamp, resource); returns the number of rows
  * (all of them are written when cap allows; lastFetchTime advances only then). */
+/* StatisticNode.metrics() of one node at now (StatisticNode.java:116-147): the minute window's buckets newer than
+ * *last_fetch, older than now's second, non-empty; emit: write them (resource id `res`), advance *last_fetch and run
+ * currentWindow's side effect. Returns the rows. */
+static uint64_t node_rows(or_leap* m, int64_t now, int64_t* last_fetch, uint32_t res, sg_metric_node* out, int emit) {
+    const int64_t cur = now - now % 1000;
+    if (emit) or_leap_current_window(m, now);                   /* data.currentWindow() */
+    int64_t newest = *last_fetch;
+    uint64_t rows = 0;
+    for (int j = 0; j < m->S; j++) {                            /* data.list(): not deprecated at now */
+        if (!m->present[j] || is_deprecated(m, now, &m->b[j])) continue;
+        const or_bucket* b = &m->b[j];
+        if (!(b->start > *last_fetch && b->start < cur)) continue;   /* isNodeInTime */
+        const int64_t succ = b->c[OR_M_SUCCESS];
+        const int64_t rt = succ != 0 ? b->c[OR_M_RT] / succ : b->c[OR_M_RT];
+        if (!(b->c[OR_M_PASS] > 0 || b->c[OR_M_BLOCK] > 0 || succ > 0 || b->c[OR_M_EXCEPTION] > 0 || rt > 0 ||
+              b->c[OR_M_OCCUPIED_PASS] > 0))
+            continue;                                           /* isValidMetricNode */
+        if (emit) {
+            sg_metric_node* r = &out[rows];
+            r->timestamp = b->start;
+            r->pass_qps = b->c[OR_M_PASS];
+            r->block_qps = b->c[OR_M_BLOCK];
+            r->success_qps = succ;
+            r->exception_qps = b->c[OR_M_EXCEPTION];
+            r->rt = rt;
+            r->occupied_pass_qps = b->c[OR_M_OCCUPIED_PASS];
+            r->resource = res;
+            r->concurrency = 0;
+            if (b->start > newest) newest = b->start;
+        }
+        rows++;
+    }
+    if (emit) *last_fetch = newest;
+    return rows;
+}
+
+/* MetricTimerListener.run (MetricTimerListener.java:40-55): every resource's ClusterNode, then Constants.ENTRY_NODE
+ * (resource id SG_ENTRY_NODE_RESOURCE), rows sorted by (timestamp, resource) as its TreeMap of time → list */
 int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap) {
     if (!l->last_fetch) {
         l->last_fetch = (int64_t*)malloc((l->n ? l->n : 1) * sizeof(int64_t));
         for (uint32_t k = 0; k < l->n; k++) l->last_fetch[k] = -1;
     }
-    const int64_t cur = now - now % 1000;
     uint64_t rows = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        rows = 0;
-        for (uint32_t k = 0; k < l->n; k++) {
-            or_leap* m = l->nodes[k].minute;
-            if (pass == 1) or_leap_current_window(m, now);           /* data.currentWindow() */
-            int64_t newest = l->last_fetch[k];
-            for (int j = 0; j < m->S; j++) {                        /* data.list(): not deprecated at now */
-                if (!m->present[j] || is_deprecated(m, now, &m->b[j])) continue;
-                const or_bucket* b = &m->b[j];
-                if (!(b->start > l->last_fetch[k] && b->start < cur)) continue;   /* isNodeInTime */
-                const int64_t succ = b->c[OR_M_SUCCESS];
-                const int64_t rt = succ != 0 ? b->c[OR_M_RT] / succ : b->c[OR_M_RT];
-                if (!(b->c[OR_M_PASS] > 0 || b->c[OR_M_BLOCK] > 0 || succ > 0 || b->c[OR_M_EXCEPTION] > 0 || rt > 0 ||
-                      b->c[OR_M_OCCUPIED_PASS] > 0))
-                    continue;                                       /* isValidMetricNode */
-                if (pass == 1) {
-                    sg_metric_node* r = &out[rows];
-                    r->timestamp = b->start;
-                    r->pass_qps = b->c[OR_M_PASS];
-                    r->block_qps = b->c[OR_M_BLOCK];
-                    r->success_qps = succ;
-                    r->exception_qps = b->c[OR_M_EXCEPTION];
-                    r->rt = rt;
-                    r->occupied_pass_qps = b->c[OR_M_OCCUPIED_PASS];
-                    r->resource = k;
-                    r->concurrency = 0;
-                    if (b->start > newest) newest = b->start;
-                }
-                rows++;
-            }
-            if (pass == 1) l->last_fetch[k] = newest;
-        }
-        if (pass == 0 && rows > cap) return (int64_t)rows;
-    }
+    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, NULL, 0);
+    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, NULL, 0);
+    if (rows > cap) return (int64_t)rows;
+    rows = 0;
+    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, out + rows, 1);
+    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, out + rows, 1);
     for (uint64_t i = 1; i < rows; i++) {                           /* insertion sort by (timestamp, resource) */
         sg_metric_node x = out[i];
         uint64_t j = i;
@@ -2374,6 +2395,12 @@ int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t
         out[j] = x;
     }
     return (int64_t)rows;
+}
+
+int or_local_set_entry_types(or_local* l, const uint8_t* inbound, uint32_t n) {
+    if (n != l->n) return SG_E_INVAL;
+    for (uint32_t k = 0; k < n; k++) l->inbound[k] = inbound[k] ? 1 : 0;
+    return 0;
 }
 
 typedef struct { uint64_t v; int64_t c; } or_topent;

@@ -145,6 +145,7 @@ CLUSTER_CLIENT, CLUSTER_SERVER, CLUSTER_NOT_STARTED = 0, 1, -1
 SLOT_EXT_DTYPE = np.dtype([("context", "<u4"), ("arg_begin", "<u4"), ("arg_count", "<u4"), ("args_null", "<i4")],
                           align=True)
 LOCAL_BLOCK_PARAM = 4
+ENTRY_NODE_RESOURCE = 0xFFFFFFFF  # sg_local_metrics rows of Constants.ENTRY_NODE
 CONTROL_DEFAULT, CONTROL_WARM_UP, CONTROL_RATE_LIMITER, CONTROL_WARM_UP_RATE_LIMITER = 0, 1, 2, 3
 LIMIT_APP_DEFAULT, LIMIT_APP_OTHER = 0, -1
 STRATEGY_DIRECT, STRATEGY_RELATE, STRATEGY_CHAIN = 0, 1, 2

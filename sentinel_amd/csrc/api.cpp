@@ -169,6 +169,9 @@ struct sg_handle {
     uint64_t l_ps_applied = 0;        // ps_gen whose param flags d_lrules carries (0: none)
     bool l_has_cx_ps = false;         // some resource is cx because of param rules
     sg_slot_ext* d_lext_h = nullptr;  // host-path buffers of sg_slot_decide_batch_host
+    uint8_t* d_linbound = nullptr;    // [K] EntryType.IN resources (sg_local_set_entry_types), null = none
+    LBucket* d_lentry_acc = nullptr;  // [60] the ENTRY_NODE's buckets, summed per metric call
+    int64_t* d_lentry_fetch = nullptr;// the ENTRY_NODE's lastFetchTime
 
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
@@ -613,6 +616,9 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lout_h);
     dfree(h->d_lext_h);
     dfree(h->d_lgkey);
+    dfree(h->d_linbound);
+    dfree(h->d_lentry_acc);
+    dfree(h->d_lentry_fetch);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
     drain_async(h);
@@ -1081,6 +1087,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.skip_cap = (uint32_t)(2 * h->cfg.max_batch / kSkipMin + 1);
     a.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u
                   : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : h->short_max;
+    a.tiny = tiny_walker_enabled(a) ? 1 : 0;
     return a;
 }
 
@@ -1137,11 +1144,13 @@ int flow_back(sg_handle* h, const BatchArgs& a, hipStream_t stream, hipStream_t 
     if (h->dbg & 2) {
         HIP_TRY(h, launch_walk_long(a, stream));
         HIP_TRY(h, launch_walk_short(a, stream));
+        HIP_TRY(h, launch_walk_tiny(a, stream));
     } else {
         HIP_TRY(h, hipEventRecord(fork, stream));
         HIP_TRY(h, hipStreamWaitEvent(aux, fork, 0));
         HIP_TRY(h, launch_walk_long(a, aux));
         HIP_TRY(h, launch_walk_short(a, stream));
+        HIP_TRY(h, launch_walk_tiny(a, stream));
         HIP_TRY(h, hipEventRecord(join, aux));
         HIP_TRY(h, hipStreamWaitEvent(stream, join, 0));
     }
@@ -2266,7 +2275,15 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     h->l_cn_n.assign(n, 0);
     h->l_cn_base.assign(n, kNoNode);
     dfree(h->d_lgkey);
+    dfree(h->d_linbound);  // every resource's entries EntryType.OUT until sg_local_set_entry_types
     h->l_ps_applied = 0;
+    if (!h->d_lentry_fetch && (hipMalloc(&h->d_lentry_fetch, sizeof(int64_t)) != hipSuccess ||
+                               hipMalloc(&h->d_lentry_acc, sizeof(LBucket) * kMinuteS) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "ENTRY_NODE state");
+    {
+        const int64_t neg1 = -1;  // StatisticNode.lastFetchTime of Constants.ENTRY_NODE
+        HIP_TRY(h, hipMemcpy(h->d_lentry_fetch, &neg1, sizeof(neg1), hipMemcpyHostToDevice));
+    }
     if (!h->d_llast_ts && hipMalloc(&h->d_llast_ts, sizeof(int64_t)) != hipSuccess) return fail(h, SG_E_NOMEM, "ts");
     const int64_t neg = -1;
     HIP_TRY(h, hipMemcpy(h->d_llast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice));
@@ -2297,6 +2314,20 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     return SG_OK;
 }
 
+int sg_local_set_entry_types(sg_handle* h, const uint8_t* inbound, uint32_t n) {
+    if (!h || (!inbound && n)) return SG_E_INVAL;
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    if (n != h->ltab.size()) return fail(h, SG_E_INVAL, "one entry type per resource");
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    std::vector<uint8_t> v(n);
+    for (uint32_t k = 0; k < n; ++k) v[k] = inbound[k] ? 1 : 0;
+    dfree(h->d_linbound);
+    if (n && hipMalloc(&h->d_linbound, n) != hipSuccess) return fail(h, SG_E_NOMEM, "entry types");
+    if (n) HIP_TRY(h, hipMemcpy(h->d_linbound, v.data(), n, hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
 int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows) {
     if (!h || !n_rows || (!out && cap)) return SG_E_INVAL;
     *n_rows = 0;
@@ -2308,11 +2339,28 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
     L.K = (uint32_t)h->ltab.size();
     L.minute = h->d_lmin;
     L.last_fetch = h->d_llast_fetch;
+    L.inbound = h->d_linbound;
+    L.entry_acc = h->d_lentry_acc;
+    L.entry_fetch = h->d_lentry_fetch;
+    // MetricTimerListener.run: the resources' rows, then the ENTRY_NODE's (counted first, then emitted: the emit
+    // pass has the side effects)
+    auto pass = [&](sg_metric_node* dst, unsigned long long* d_cnt, int emit) -> hipError_t {
+        std::vector<LBucket> acc0(kMinuteS);
+        for (auto& b : acc0) {
+            b.start = INT64_MIN;
+            for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+            b.min_rt = kStatMaxRt;
+        }
+        hipError_t e = hipMemcpy(h->d_lentry_acc, acc0.data(), sizeof(LBucket) * kMinuteS, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(unsigned long long));
+        if (e == hipSuccess) e = launch_local_metrics(L, now_ms, dst, d_cnt, emit, 0);
+        if (e == hipSuccess && h->d_linbound) e = launch_local_entry_rows(L, now_ms, dst, d_cnt, emit, 0);
+        return e;
+    };
     unsigned long long* d_cnt = nullptr;
     HIP_TRY(h, hipMalloc(&d_cnt, sizeof(unsigned long long)));
     unsigned long long cnt = 0;
-    hipError_t e = hipMemset(d_cnt, 0, sizeof(cnt));
-    if (e == hipSuccess) e = launch_local_metrics(L, now_ms, nullptr, d_cnt, 0, 0);
+    hipError_t e = pass(nullptr, d_cnt, 0);
     if (e == hipSuccess) e = hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
         (void)hipFree(d_cnt);
@@ -2328,8 +2376,7 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
         (void)hipFree(d_cnt);
         return fail(h, SG_E_NOMEM, "metric rows");
     }
-    e = hipMemset(d_cnt, 0, sizeof(cnt));
-    if (e == hipSuccess) e = launch_local_metrics(L, now_ms, d_out, d_cnt, 1, 0);
+    e = pass(d_out, d_cnt, 1);
     if (e == hipSuccess && cnt) e = hipMemcpy(out, d_out, sizeof(sg_metric_node) * cnt, hipMemcpyDeviceToHost);
     (void)hipFree(d_cnt);
     if (d_out) (void)hipFree(d_out);

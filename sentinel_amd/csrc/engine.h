@@ -98,9 +98,11 @@ struct BatchArgs {
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
     uint32_t short_max;  // segments longer than this go to the wave walker
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
-                         // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr
+                         // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr,
+                         // 128 = length class 0 through k_walk_tiny
     int narrow;          // PASS / WAITING of every bucket provably < 2^30 (short walker's 12 B LDS snapshot)
     int generic_walker;  // SG_FLAG_RING_REREAD: short walker re-reads the ring (no register snapshot)
+    int tiny;            // 1: length class 0 (<= kClassMax[0] records) is walked by k_walk_tiny, not k_walk_short
     unsigned long long* dbg_ctr;  // [32]
     // ranges of records the wave walker skipped as certainly BLOCKED: {flow key, period q, begin, end}
     uint4* skips;
@@ -521,6 +523,9 @@ struct LArgs {
     uint32_t* skip_count;
     uint32_t skip_cap;
     int64_t* last_fetch;      // [K] StatisticNode.lastFetchTime (metric rows already reported)
+    const uint8_t* inbound;   // [K] 1: the resource's entries are EntryType.IN (Constants.ENTRY_NODE), or null
+    LBucket* entry_acc;       // [60] the ENTRY_NODE's minute buckets summed from the inbound resources' (metric rows)
+    int64_t* entry_fetch;     // the ENTRY_NODE's lastFetchTime
 };
 
 constexpr int kLFlagPrio = 1;    // some entry is prioritized (may occupy in a saturated window)
@@ -540,6 +545,9 @@ hipError_t launch_local_remap(const LArgs& L, const int64_t* src, const LHead* o
                               const LFuture* obor, const LBucket* omin, hipStream_t stream);
 // StatisticNode.metrics() of every resource at now: emit == 0 counts the rows (no side effect), emit == 1 writes
 // them (any order) and applies currentWindow / lastFetchTime.
+// Constants.ENTRY_NODE's metric rows from the summed buckets (k_local_metrics accumulated them into a.entry_acc).
+hipError_t launch_local_entry_rows(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
+                                   hipStream_t stream);
 hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
                                 hipStream_t stream);
 
@@ -553,6 +561,8 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
+bool tiny_walker_enabled(const BatchArgs& a);
+hipError_t launch_walk_tiny(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);

@@ -999,6 +999,11 @@ __device__ __forceinline__ bool narrow_span(const BatchArgs& a, int64_t T0) {
     return ok;
 }
 
+// k_walk_tiny takes length class 0 (same answer in every kernel of the batch: batch constants only)
+__device__ __forceinline__ bool tiny_active(const BatchArgs& a) {
+    return a.tiny && a.narrow && narrow_span(a, a.p0[0] * (int64_t)a.wl[0]);
+}
+
 __device__ __forceinline__ void store_bucket(Bucket* b, int64_t start, const int64_t* c) {
     ulonglong2* p = reinterpret_cast<ulonglong2*>(b);
     p[0] = make_ulonglong2((unsigned long long)start, (unsigned long long)c[0]);
@@ -1329,13 +1334,14 @@ template <int SM, bool L>
 __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* snap_all, uint32_t* recs_all) {
     static_assert(SM > 0, "LDS ring snapshot");
     const int lane = lane_id();
+    const bool tiny = tiny_active(a);
     SlotSnap* snap = snap_all + (threadIdx.x / 64) * (64 * SM);
     uint32_t* wrecs = recs_all + (threadIdx.x / 64) * (kRecW * 64);
     uint32_t cnt[kClasses], grp_end[kClasses];
     uint32_t total = 0;
 #pragma unroll
     for (int c = kClasses - 1; c >= 0; --c) {  // group order: longest class first
-        cnt[c] = a.short_count[c];
+        cnt[c] = (c == 0 && tiny) ? 0u : a.short_count[c];  // class 0: k_walk_tiny
         total += (cnt[c] + 63) / 64;
         grp_end[c] = total;
     }
@@ -1445,12 +1451,13 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
     }
     constexpr int kSnapPerWave = SM > 0 ? 64 * SM : 1;
     const int lane = lane_id();
+    const bool tiny = tiny_active(a);
     SlotSnap* snap = snap_all + (threadIdx.x / 64) * kSnapPerWave;
     uint32_t cnt[kClasses], grp_end[kClasses];
     uint32_t total = 0;
 #pragma unroll
     for (int c = kClasses - 1; c >= 0; --c) {  // group order: longest class first
-        cnt[c] = a.short_count[c];
+        cnt[c] = (c == 0 && tiny) ? 0u : a.short_count[c];  // class 0: k_walk_tiny
         total += (cnt[c] + 63) / 64;
         grp_end[c] = total;
     }
@@ -1551,6 +1558,128 @@ __global__ void __launch_bounds__(256, C ? 2 : kShortBlocksPerCu) k_walk_short(B
     stage_periods(a);
     if (g_blds) walk_short_body<SM, true, C>(a, snap_all, recs_all);
     else walk_short_body<SM, false, C>(a, snap_all, recs_all);
+}
+
+// Tiny-segment walker: one thread per flowId of length class 0 (<= kClassMax[0] records, most touched flowIds of a
+// Zipf batch), everything in registers — the ring's {start, PASS, WAITING} (S <= SM slots, the 32-bit encoding of
+// SlotSnap: exact under BatchArgs::narrow and narrow_span), the records, the open bucket — so the kernel needs no
+// LDS beyond the period tables and runs at more waves per SIMD: a group of 64 such segments in the lane-per-segment
+// walker paid two memory round trips and a wave-wide period phase for a handful of decisions. Same decisions as
+// walk_serial (ClusterFlowChecker.acquireClusterToken :67-111).
+template <int SM, bool L>
+__device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
+    constexpr int kR = (int)kClassMax[0];
+    const uint32_t cnt = a.short_count[0];
+    const uint64_t base = a.class_off[0];
+    const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += gridDim.x * blockDim.x) {
+        const uint64_t s = a.short_list[base + t];
+        const uint32_t k = a.short_key[base + t];
+        const uint32_t e = a.short_end[base + t];
+        const Rule R = a.rules[k];
+        const Occ occ = a.occ[k];
+        uint64_t r0 = a.rec_sorted[s], r1 = a.rec_sorted[min(s + 1, a.n - 1)];
+        uint64_t r2 = a.rec_sorted[min(s + 2, a.n - 1)], r3 = a.rec_sorted[min(s + 3, a.n - 1)];
+        static_assert(kR == 4, "four record registers");
+        Bucket* ring = a.ring + (size_t)k * a.stride;
+        int32_t st[SM], pa[SM], wa[SM];
+#pragma unroll
+        for (int x = 0; x < SM; ++x) {
+            const int xx = x < R.S ? x : 0;
+            const ulonglong2 sp = *reinterpret_cast<const ulonglong2*>(ring + xx);          // {start, PASS}
+            const ulonglong2 ow = *(reinterpret_cast<const ulonglong2*>(ring + xx) + 3);    // {OCC_BLOCK, WAITING}
+            st[x] = snap_rel((int64_t)sp.x, T0);
+            pa[x] = (int32_t)sp.y;
+            wa[x] = (int32_t)ow.y;
+        }
+        PeriodCursor<L> pc;
+        pc.init(a, R.wl_idx);
+        const int64_t P0 = g_p0[R.wl_idx];
+        const int S = R.S;
+        PeriodState ps;
+        ps.occ_pass = occ.pass;
+        ps.occ_req = occ.pass_req;
+#pragma unroll
+        for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
+        ps.wo_pass = ps.wo_wait = ps.head_other = 0;
+        int I = -1;
+        int64_t ws = 0;
+        const uint32_t m = e - (uint32_t)s;
+        for (uint32_t u = 0; u < m; ++u) {
+            const Decoded d = decode(a, r0);
+            r0 = r1;
+            r1 = r2;
+            r2 = r3;
+            const uint32_t q = pc.of(d.idx);
+            if (q != pc.q) {
+                if (I >= 0) {  // close the open bucket: memory and the register ring
+                    store_bucket(ring + I, ws, ps.cur);
+#pragma unroll
+                    for (int x = 0; x < SM; ++x) {
+                        st[x] = x == I ? (int32_t)(ws - T0) : st[x];
+                        pa[x] = x == I ? (int32_t)ps.cur[SG_EV_PASS] : pa[x];
+                        wa[x] = x == I ? (int32_t)ps.cur[SG_EV_WAITING] : wa[x];
+                    }
+                }
+                const uint32_t qprev = pc.q;
+                pc.seek(q);
+                const int64_t P = P0 + (int64_t)q;
+                I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(q - qprev)) % (uint32_t)S);
+                ws = P * R.wl;
+                const int64_t lo_rel = ws - (int64_t)S * R.wl - T0;  // valid iff start > ws - S * wl
+                const int h = I + 1 == S ? 0 : I + 1;
+                uint32_t wp = 0, ww = 0, ho = 0;
+                int32_t stI_rel = INT32_MIN;
+#pragma unroll
+                for (int x = 0; x < SM; ++x) {
+                    const bool v = (x < S) & (x != I) & ((int64_t)st[x] > lo_rel);
+                    const uint32_t mk = v ? 0xFFFFFFFFu : 0u;
+                    wp += (uint32_t)pa[x] & mk;
+                    ww += (uint32_t)wa[x] & mk;
+                    ho = (x == h) ? ((uint32_t)pa[x] & mk) : ho;
+                    stI_rel = x == I ? st[x] : stI_rel;
+                }
+                ps.wo_pass = (int64_t)wp;
+                ps.wo_wait = (int64_t)ww;
+                ps.head_other = (int64_t)ho;
+                const int64_t stI = stI_rel == INT32_MIN ? INT64_MIN : T0 + (int64_t)stI_rel;
+                int64_t cI[SG_NUM_EVENTS];
+                if (stI == ws) {  // the batch continues the stored period
+#pragma unroll
+                    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
+                }
+                open_bucket(ps, stI, cI, ws);
+            }
+            const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
+            const double next_remaining = R.thr - latest - (double)d.acq;
+            if (next_remaining >= 0) {
+                ps.cur[SG_EV_PASS] += d.acq;
+                ps.cur[SG_EV_PASS_REQUEST] += 1;
+                if (d.prio) ps.cur[SG_EV_OCCUPIED_PASS] += d.acq;
+                store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
+            } else {
+                int32_t wait;
+                const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, d.acq, d.prio, &wait);
+                if (stt != SG_STATUS_BLOCKED) store_result(a.out, d.idx, stt, 0, wait);
+            }
+        }
+        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        Occ o;
+        o.pass = ps.occ_pass;
+        o.pass_req = ps.occ_req;
+        a.occ[k] = o;
+    }
+}
+
+template <int SM>
+#ifndef SG_TINY_BLOCKS
+#define SG_TINY_BLOCKS 4
+#endif
+__global__ void __launch_bounds__(256, SG_TINY_BLOCKS) k_walk_tiny(BatchArgs a) {
+    if (*a.err || !tiny_active(a)) return;
+    stage_periods(a);
+    if (g_blds) walk_tiny_body<SM, true>(a);
+    else walk_tiny_body<SM, false>(a);
 }
 
 // One wave per skipped piece: Σ acquire and Σ prioritized acquire over its records, added with 64-bit
@@ -1719,6 +1848,30 @@ static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
     if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
     return hipGetLastError();
+}
+
+template <int SM>
+static hipError_t launch_tiny_sm(const BatchArgs& a, hipStream_t stream) {
+    static unsigned blocks[2] = {0, 0};  // all CUs / the pipeline's walker CUs
+    const int m = a.walk_cus > 0 ? 1 : 0;
+    if (blocks[m] == 0) blocks[m] = resident_blocks((const void*)k_walk_tiny<SM>, 256, a.walk_cus);
+    hipLaunchKernelGGL((k_walk_tiny<SM>), dim3(blocks[m]), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+// Whether k_walk_tiny takes length class 0 (the host sets BatchArgs::tiny from the same answer).
+bool tiny_walker_enabled(const BatchArgs& a) {
+    // opt-in (SG_DEBUG & 128): measured 11 % slower per C3 step than class 0 inside k_walk_short (r03 A/B:
+    // 0.999 vs 0.897 ms), the extra launch serialises behind the short walker on the same stream
+    return !a.generic_walker && a.stride <= 10 && a.short_max >= kClassMax[0] && (a.dbg & 128);
+}
+
+hipError_t launch_walk_tiny(const BatchArgs& a, hipStream_t stream) {
+    if (!a.tiny) return hipSuccess;
+    if (a.stride <= 2) return launch_tiny_sm<2>(a, stream);
+    if (a.stride <= 4) return launch_tiny_sm<4>(a, stream);
+    if (a.stride <= 8) return launch_tiny_sm<8>(a, stream);
+    return launch_tiny_sm<10>(a, stream);
 }
 
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream) {

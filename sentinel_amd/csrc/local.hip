@@ -1431,41 +1431,60 @@ __global__ void k_local_finish(LArgs a) {
 // ------------------------------------------------------------------------------- metric rows
 
 // StatisticNode.metrics() at now (StatisticNode.java:116-147, ArrayMetric.details / fromBucket :156-204), one
-// thread per resource over its 60 minute buckets.
+// thread per resource over its 60 minute buckets. An inbound resource's buckets newer than the ENTRY_NODE's
+// lastFetchTime are also summed into a.entry_acc: StatisticSlot adds every EntryType.IN entry and exit to
+// Constants.ENTRY_NODE as to the resource (StatisticSlot.java:71-75, :139-141), so the ENTRY_NODE's bucket of a
+// second is the sum of the inbound resources' buckets of that second (k_local_entry_rows emits its rows).
+__device__ __forceinline__ bool metric_row_valid(const LBucket& b) {  // MetricNode validity (isValidMetricNode)
+    const int64_t succ = b.c[kLSucc];
+    const int64_t rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
+    return b.c[kLPass] > 0 || b.c[kLBlock] > 0 || succ > 0 || b.c[kLExc] > 0 || rt > 0 || b.c[kLOccPass] > 0;
+}
+
 __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_metric_node* out,
                                                        unsigned long long* count, int emit) {
+    const int64_t cur = now - now % 1000;
+    const int I = (int)((now / kMinuteWl) % kMinuteS);
+    const int64_t efetch = a.entry_fetch ? *a.entry_fetch : INT64_MAX;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.K; k += (uint64_t)gridDim.x * blockDim.x) {
         LBucket* m = a.minute + k * kMinuteS;
-        const int64_t cur = now - now % 1000;
-        // data.currentWindow(now): an absent or stale bucket in now's slot becomes an empty one
-        const int I = (int)((now / kMinuteWl) % kMinuteS);
-        if (emit && (m[I].start == INT64_MIN || m[I].start < cur)) {
+        // data.currentWindow(now): an absent or stale bucket in now's slot becomes an empty one (emit: for real;
+        // counting: as if, so that both passes list the same buckets)
+        const bool reset_I = m[I].start == INT64_MIN || m[I].start < cur;
+        if (emit && reset_I) {
             LBucket b;
             b.start = cur;
             for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
             b.min_rt = kStatMaxRt;
             m[I] = b;
         }
+        const bool inb = a.inbound && a.inbound[k];
         const int64_t last = a.last_fetch[k];
         int64_t newest = last;
         uint32_t rows = 0;
         for (int j = 0; j < kMinuteS; ++j) {  // data.list(now): present and not deprecated
+            if (j == I && reset_I) continue;  // the fresh bucket at cur is never in time
             const LBucket b = m[j];
             if (b.start == INT64_MIN || now - b.start > (int64_t)kMinuteS * kMinuteWl) continue;
+            if (inb && b.start > efetch && b.start < cur) {  // the ENTRY_NODE's bucket of that second
+                LBucket& acc = a.entry_acc[j];
+                acc.start = b.start;  // every inbound bucket of slot j in the window has this start
+                for (int e = 0; e < kLEv; ++e)
+                    if (b.c[e]) atomicAdd((unsigned long long*)&acc.c[e], (unsigned long long)b.c[e]);
+            }
             if (!(b.start > last && b.start < cur)) continue;  // isNodeInTime
-            const int64_t pass = b.c[kLPass], block = b.c[kLBlock], succ = b.c[kLSucc], exc = b.c[kLExc];
-            const int64_t rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
-            if (!(pass > 0 || block > 0 || succ > 0 || exc > 0 || rt > 0 || b.c[kLOccPass] > 0)) continue;
+            if (!metric_row_valid(b)) continue;
             newest = b.start > newest ? b.start : newest;
             ++rows;
             if (!emit) continue;
+            const int64_t pass = b.c[kLPass], block = b.c[kLBlock], succ = b.c[kLSucc], exc = b.c[kLExc];
             sg_metric_node r;
             r.timestamp = b.start;
             r.pass_qps = pass;
             r.block_qps = block;
             r.success_qps = succ;
             r.exception_qps = exc;
-            r.rt = rt;
+            r.rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
             r.occupied_pass_qps = b.c[kLOccPass];
             r.resource = (uint32_t)k;
             r.concurrency = 0;
@@ -1474,6 +1493,46 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
         if (!emit && rows) atomicAdd(count, (unsigned long long)rows);
         if (emit) a.last_fetch[k] = newest;
     }
+}
+
+// Constants.ENTRY_NODE.metrics() rows from the summed buckets (one thread per minute slot; resource id
+// SG_ENTRY_NODE_RESOURCE); emit advances the ENTRY_NODE's lastFetchTime.
+__global__ void __launch_bounds__(64) k_local_entry_rows(LArgs a, int64_t now, sg_metric_node* out,
+                                                         unsigned long long* count, int emit) {
+    const int j = threadIdx.x;
+    const int64_t cur = now - now % 1000;
+    bool row = false;
+    LBucket b;
+    if (j < kMinuteS) {
+        b = a.entry_acc[j];
+        // StatisticNode.addOccupiedPass raises the minute PASS and OCCUPIED_PASS of the selected node only: the
+        // ENTRY_NODE sees StatisticSlot's addPassRequest of real passes, never a prioritized wait's occupied pass
+        b.c[kLPass] -= b.c[kLOccPass];
+        b.c[kLOccPass] = 0;
+        row = b.start != INT64_MIN && b.start > *a.entry_fetch && b.start < cur && metric_row_valid(b);
+    }
+    if (row) {
+        if (emit) {
+            const int64_t succ = b.c[kLSucc];
+            sg_metric_node r;
+            r.timestamp = b.start;
+            r.pass_qps = b.c[kLPass];
+            r.block_qps = b.c[kLBlock];
+            r.success_qps = succ;
+            r.exception_qps = b.c[kLExc];
+            r.rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
+            r.occupied_pass_qps = 0;
+            r.resource = SG_ENTRY_NODE_RESOURCE;
+            r.concurrency = 0;
+            out[atomicAdd(count, 1ull)] = r;
+        } else {
+            atomicAdd(count, 1ull);
+        }
+    }
+    // newest row start → lastFetchTime (wave max; one wave)
+    int64_t nb = row ? b.start : INT64_MIN;
+    for (int o = 32; o > 0; o >>= 1) nb = max(nb, (int64_t)__shfl_xor((long long)nb, o, 64));
+    if (emit && j == 0 && nb != INT64_MIN && nb > *a.entry_fetch) *a.entry_fetch = nb;
 }
 
 // ---------------------------------------------------------------------------------- launchers
@@ -1502,6 +1561,12 @@ hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out
                                 hipStream_t stream) {
     if (a.K == 0) return hipSuccess;
     hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_entry_rows(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
+                                   hipStream_t stream) {
+    hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit);
     return hipGetLastError();
 }
 

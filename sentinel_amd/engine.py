@@ -21,7 +21,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_cparam_load_rules", "sg_cparam_decide_batch", "sg_cparam_decide_batch_host", "sg_cparam_read_sum",
            "sg_local_load_rules", "sg_local_decide_batch", "sg_local_decide_batch_host", "sg_local_read_state",
            "sg_local_load_flow_rules", "sg_local_read_origin_state", "sg_local_read_controller",
-           "sg_local_read_context_state", "sg_local_set_cluster_state", "sg_slot_decide_batch",
+           "sg_local_read_context_state", "sg_local_set_cluster_state", "sg_slot_decide_batch", "sg_local_set_entry_types",
            "sg_slot_decide_batch_host",
            "sg_codec_decode_flow", "sg_codec_encode_flow",
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
@@ -92,6 +92,7 @@ def load_library():
         "sg_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
         "sg_local_read_context_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
         "sg_local_set_cluster_state": (C.c_int, [vp, C.c_int32]),
+        "sg_local_set_entry_types": (C.c_int, [vp, vp, u32]),
         "sg_slot_decide_batch": (C.c_int, [vp, vp, vp, u64, vp, u64, vp, u64, vp, vp]),
         "sg_slot_decide_batch_host": (C.c_int, [vp, vp, vp, u64, vp, u64, vp, u64, vp]),
         "sg_local_read_origin_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
@@ -460,6 +461,11 @@ class FlowEngine:
         rc = self._L.sg_local_load_flow_rules(self.h, abi.ptr(rules), len(rules), n_origins, n_contexts)
         self._check(min(rc, 0))
         return rc
+
+    def local_set_entry_types(self, inbound):
+        """EntryType of each resource's entries (1 = IN: counted by Constants.ENTRY_NODE); default OUT."""
+        v = np.ascontiguousarray(inbound, dtype=np.uint8)
+        self._check(self._L.sg_local_set_entry_types(self.h, abi.ptr(v), len(v)))
 
     def local_set_cluster_state(self, state):
         """ClusterStateManager state (CLUSTER_NOT_STARTED -1 is the one the device decides cluster rules in)."""

@@ -373,3 +373,18 @@ def test_hot_flow_saturated_periods_are_skipped_exactly(prio):
         skipped += eng.stats()["skipped_ranges"]
         _compare_state(eng, ora, rules)
     assert skipped > 0
+
+
+@pytest.mark.parametrize("n_keys,n,S", [(1000, 100_000, 10), (3000, 60_000, 2), (200_000, 400_000, 10)])
+def test_tiny_walker_opt_in_matches_oracle(monkeypatch, n_keys, n, S):
+    """SG_DEBUG=128 walks length class 0 with k_walk_tiny (off by default: slower in the r03 A/B)."""
+    monkeypatch.setenv("SG_DEBUG", "128")
+    rng = np.random.default_rng(n_keys + n)
+    rules = _rules(n_keys, rng, S=S)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_017
+    for _ in range(3):
+        req = _trace(rng, n, n_keys, t, int(rng.integers(1, 3000)), zipf=0.8, prio=0.05)
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, 2000))
+        _compare_results(ora.decide(req), eng.decide_host(req), req)
+    _compare_state(eng, ora, rules)

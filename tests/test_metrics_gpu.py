@@ -20,8 +20,11 @@ from test_local_gpu import _entries
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("S,interval", [(2, 1000), (4, 1000), (5, 500)])
-def test_local_metric_rows(S, interval):
+@pytest.mark.parametrize("S,interval,inbound", [(2, 1000, False), (4, 1000, True), (5, 500, True)])
+def test_local_metric_rows(S, interval, inbound):
+    """inbound: a third of the resources are EntryType.IN, so the rows end with Constants.ENTRY_NODE's
+    (__total_inbound_traffic__, MetricTimerListener.java:46): the device sums the inbound resources' buckets, the
+    oracle keeps the ENTRY_NODE as its own StatisticNode."""
     from sentinel_amd.engine import FlowEngine
     rng = np.random.default_rng(40 + S)
     n_res = 40
@@ -34,6 +37,11 @@ def test_local_metric_rows(S, interval):
     gen = LocalTraceGen(ora)
     eng = FlowEngine(device=0, max_batch=1 << 20)
     eng.local_load_rules(rules, S, interval, 500)
+    if inbound:
+        ib = (np.arange(n_res) % 3 == 0).astype(np.uint8)
+        ora.set_entry_types(ib)
+        eng.local_set_entry_types(ib)
+    entry_rows = 0
     t = 1_700_000_000_000 + int(rng.integers(0, 1000))
     for b, (n, span) in enumerate([(20_000, 2500), (20_000, 1800), (5_000, 65_000), (10_000, 900)]):
         ent = _entries(rng, n, n_res, t, span, prio=0.1)
@@ -45,8 +53,10 @@ def test_local_metric_rows(S, interval):
             w_rows = ora.metrics(now)
             g_rows = eng.local_metrics(now)
             assert np.array_equal(w_rows, g_rows), f"batch {b} now {now}: {len(w_rows)} vs {len(g_rows)} rows"
+            entry_rows += int((w_rows["resource"] == abi.ENTRY_NODE_RESOURCE).sum())
         for r in range(0, n_res, 7):
             assert np.array_equal(ora.dump(r)[2], eng.local_state(r)[2]), f"minute window of {r}"
+    assert (entry_rows > 0) == inbound
 
 
 def test_cparam_top_values():
