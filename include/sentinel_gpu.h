@@ -656,8 +656,9 @@ int sg_local_read_context_state(sg_handle* h, uint32_t res, int32_t context, int
  *                      second (StatisticSlot adds every EntryType.IN entry / exit to it, StatisticSlot.java:71-75,
  *                      :139-141) less their occupied passes (StatisticNode.addOccupiedPass raises only the selected
  *                      node's PASS, StatisticNode.java:333-336), occupied_pass_qps 0, with the ENTRY_NODE's own
- *                      lastFetchTime. Exact when rows are fetched at least once a minute (a resource's bucket of a
- *                      second outlives it by the minute window).
+ *                      lastFetchTime. Exact when rows are fetched at least once a minute and at a time not behind the
+ *                      latest decided event, as MetricTimerListener does (a resource's bucket of a second outlives
+ *                      the ENTRY_NODE's by up to the minute window).
  *   sg_local_set_entry_types ← the EntryType of each resource's SphU.entry calls (1 = IN; default OUT, as
  *                      SphU.entry(name)). */
 #define SG_ENTRY_NODE_RESOURCE 0xFFFFFFFFu

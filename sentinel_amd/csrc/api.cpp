@@ -259,6 +259,8 @@ struct sg_handle {
     hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
     uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
+    bool d2h_kernel = true;           // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=0: off)
+    int d2h_blocks = 64;              // its workgroups (env SG_D2H_BLOCKS)
     int front_eighths = 3;            // CU partition of the pipeline streams (see pipe_setup; 3/8 measured best)
     int walk_cus = 0;                 // CUs of the walkers' streams when partitioned (0 = all)
     struct DevTicket {                // sg_flow_enqueue batches in flight
@@ -473,6 +475,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         hipEventCreateWithFlags(&h->join, hipEventDisableTiming) != hipSuccess)
         return bail(SG_E_DEVICE);
     if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
+    if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
+    if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
         h->short_max_env = true;
@@ -1367,7 +1371,19 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
     int rc = enqueue_flow_pipelined(h, sl.d_req, n, sl.d_out, sl.h2d, sl.h_err, sl.comp);
     if (rc) return rc;
     HIP_TRY(h, hipStreamWaitEvent(h->s_out, sl.comp, 0));
-    HIP_TRY(h, hipMemcpyAsync(out, sl.d_out, sizeof(sg_result) * n, hipMemcpyDeviceToHost, h->s_out));
+    // results back: by a copy kernel when `out` is pinned host memory the device can address (env SG_D2H = 0: the
+    // copy engine), so that the link carries this batch's results while the copy engine brings the next requests
+    void* out_dev = nullptr;
+    if (h->d2h_kernel) {
+        hipPointerAttribute_t pa{};
+        if (hipPointerGetAttributes(&pa, out) == hipSuccess && pa.type == hipMemoryTypeHost && pa.devicePointer &&
+            ((uintptr_t)pa.devicePointer & 15) == 0)
+            out_dev = pa.devicePointer;
+        else
+            (void)hipGetLastError();  // pageable memory: not an error, the copy engine takes it
+    }
+    if (out_dev) HIP_TRY(h, launch_copy_out(sl.d_out, out_dev, sizeof(sg_result) * n, h->d2h_blocks, h->s_out));
+    else HIP_TRY(h, hipMemcpyAsync(out, sl.d_out, sizeof(sg_result) * n, hipMemcpyDeviceToHost, h->s_out));
     HIP_TRY(h, hipEventRecord(sl.d2h, h->s_out));
     // (a slot is reused only after its batch completed: above, or when its ticket was collected)
     sl.ticket = h->next_ticket++;

@@ -214,11 +214,14 @@ hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out,
 // request's duplicate values are adjacent. A lane walks a slot: single-value requests exactly as k_cp_walk; a
 // multi-value request (ClusterParamFlowChecker.java:58-80: every value checked against the pre-request state,
 // then all added iff all passed) writes its check for this value and adds its count iff its outcome is assumed to
-// be a pass. k_cp_combine then sets each multi-value request's outcome to the AND of its checks. The walk of a
-// slot is exact once the outcomes of the earlier multi-value requests touching it are, so re-walking from the
-// saved pre-batch rings until no outcome changes converges to the sequential answer; with the assumption
-// "passes" most batches need one or two rounds. k_cp_serial (one thread, arrival order) is the fallback when
-// the rounds run out.
+// be a pass and this check passed (a failing check on the exact state decides the request). k_cp_combine then
+// sets each multi-value request's outcome to the AND of its checks and marks for a re-walk only the slots whose
+// adds change (those whose check passed). The walk of a slot is exact once the outcomes of the earlier
+// multi-value requests touching it are, so re-walking from the saved pre-batch rings until no outcome changes
+// converges to the sequential answer (any consistent assignment is it: by induction over the requests in
+// arrival order, each one's checks see exact states); with the assumption "passes" most batches need one or two
+// rounds, and a saturated hot slot, whose checks fail, is not re-walked for the outcomes it already decided.
+// k_cp_serial (one thread, arrival order) is the fallback when the rounds run out.
 
 namespace sg {
 
@@ -384,7 +387,9 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
             b.chk[sg.rec_sorted[e] & b.pmask] = rem >= 0 ? 1 : 0;
             ++e;
         }
-        if (b.assume[i]) cur += (int64_t)q.acquire * (int64_t)(e - j);
+        // the request adds here iff its outcome is assumed a pass and this slot's check passed: a failing check on
+        // the exact pre-request state decides the request (all-or-nothing), whatever its other slots say
+        if (b.assume[i] && rem >= 0) cur += (int64_t)q.acquire * (int64_t)(e - j);
         j = e;
     }
     if (P != INT64_MIN) {
@@ -451,15 +456,17 @@ __device__ __forceinline__ int64_t cp_wave_sum(int64_t v) {
 }
 
 enum : int { kCpSkip = 0, kCpSingle = 1, kCpMulti = 2, kCpDup = 3 };
+constexpr int kCpU = 4;  // 64-record chunks whose loads are issued together (three dependent round trips per block)
 
 // One wave per slot of more than short_max records (a hot (rule, value)), 64 records per step with the ring in
 // registers (lane x < S holds bucket x). Within one window period the state is the running count `cur`; every
 // record's check is thr - (other + cur_before) / intervalSec - acquire >= 0, monotone in cur_before. A step
-// assumes every unresolved single-value request passes, takes the exclusive scan of the adds, and commits the
-// lanes up to the first single-value request whose check fails (that one is blocked); single-value requests
-// that fail even at the committed state are blocked at once (cur only grows). Multi-value records add their
-// count unconditionally when their outcome is assumed a pass, and record their check; a repeated value of the
-// same request (adjacent record, same owner) only adds. A saturated period resolves in two steps per 64
+// assumes every unresolved record adds what it would add on passing — a single-value request its count, a
+// multi-value request's first record here its count iff the request is assumed to pass — takes the exclusive scan
+// of the adds, and commits the lanes up to the first such record whose check fails (that one adds nothing);
+// records that fail even at the committed state are blocked at once (cur only grows). A repeated value of a
+// multi-value request (adjacent record, same owner) adds its count iff the request is assumed to pass. Records,
+// owners and requests of kCpU chunks are loaded together. A saturated period resolves in two steps per 64
 // records, an open one in one.
 __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
@@ -490,84 +497,110 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
             bcnt = bk.count;
         }
         int64_t P = INT64_MIN, other = 0, cur = 0;
-        for (uint64_t base = s; base < e; base += 64) {
-            const uint64_t j = base + (uint64_t)lane;
-            const bool act = j < e;
-            int typ = kCpSkip;
-            uint32_t i = 0;
-            uint64_t p = 0;
-            int64_t acq = 0, Pq = 0, uadd = 0;
-            if (act) {
-                p = sg.rec_sorted[j] & b.pmask;
-                i = b.owner[p];
-                if (!(b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST)) {
-                    const sg_cparam_req q = c.req[i];
-                    acq = q.acquire;
-                    Pq = q.ts_ms / wl;
-                    if (q.value_count == 1) {
+        uint32_t carry = kNoOwner;  // owner of the record before the current chunk
+        for (uint64_t blk = s; blk < e; blk += 64ull * kCpU) {
+            // loads of kCpU chunks at once; indices clamped to the segment (unconditional loads)
+            uint64_t rc[kCpU];
+            uint32_t ow[kCpU];
+            int64_t ts[kCpU];
+            int32_t aq[kCpU], st[kCpU];
+            uint32_t vc[kCpU];
+            uint8_t as[kCpU];
+#pragma unroll
+            for (int u = 0; u < kCpU; ++u) rc[u] = sg.rec_sorted[min(blk + (uint64_t)u * 64 + lane, e - 1)];
+#pragma unroll
+            for (int u = 0; u < kCpU; ++u) ow[u] = b.owner[rc[u] & b.pmask];
+#pragma unroll
+            for (int u = 0; u < kCpU; ++u) {
+                const sg_cparam_req q = c.req[ow[u]];
+                ts[u] = q.ts_ms;
+                aq[u] = q.acquire;
+                vc[u] = q.value_count;
+                st[u] = b.lim ? c.out[ow[u]].status : 0;
+                as[u] = b.assume[ow[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < kCpU; ++u) {
+                const uint64_t base = blk + (uint64_t)u * 64;
+                if (base >= e) break;
+                const uint64_t j = base + (uint64_t)lane;
+                const bool act = j < e;
+                const uint32_t i = ow[u];
+                const uint64_t p = rc[u] & b.pmask;
+                uint32_t prev = (uint32_t)__shfl_up((int)i, 1u, 64);
+                if (lane == 0) prev = carry;
+                carry = (uint32_t)__shfl((int)i, 63, 64);
+                int typ = kCpSkip;
+                int64_t acq = 0, Pq = 0, add = 0;
+                if (act && !(b.lim && st[u] == SG_STATUS_TOO_MANY_REQUEST)) {
+                    acq = aq[u];
+                    Pq = ts[u] / wl;
+                    if (vc[u] == 1) {
                         typ = kCpSingle;
+                        add = acq;
                     } else {
-                        const uint32_t prev = j > s ? b.owner[sg.rec_sorted[j - 1] & b.pmask] : kNoOwner;
                         typ = prev == i ? kCpDup : kCpMulti;
-                        if (b.assume[i]) uadd = acq;
+                        add = as[u] ? acq : 0;
                         if (typ == kCpDup) b.chk[p] = 1;  // the request's first record here carries the check
                     }
                 }
-            }
-            uint64_t pending = __ballot(typ != kCpSkip);
-            uint64_t failed = 0;
-            while (pending) {
-                const int f = __builtin_ctzll(pending);
-                const int64_t Pf = __shfl((long long)Pq, f, 64);
-                if (Pf != P) {  // currentWindow: close the open period, open Pf
-                    if (P != INT64_MIN && lane == (int)(P % S)) {
-                        bst = P * wl;
-                        bcnt = cur;
-                    }
-                    P = Pf;
-                    const int I = (int)(P % S);
-                    const int64_t ws = P * wl, lo = ws - (int64_t)(S - 1) * wl;
-                    int64_t o = 0, cc = 0;
-                    if (lane < S) {
-                        if (lane == I) cc = bst == ws ? bcnt : 0;
-                        else if (bst != INT64_MIN && bst >= lo) o = bcnt;
-                    }
-                    other = cp_wave_sum(o);
-                    cur = cp_wave_sum(cc);
-                }
-                uint64_t open = pending & __ballot(typ != kCpSkip && Pq == P);
-                pending &= ~open;
-                while (open) {
-                    const bool mine = (open >> lane) & 1ull;
-                    const bool dead = (failed >> lane) & 1ull;
-                    int64_t a = 0;
-                    if (mine) a = typ == kCpSingle ? (dead ? 0 : acq) : uadd;
-                    const int64_t excl = cp_excl_scan(a, lane);
-                    const double rem = thr - (double)(other + cur + excl) / r.isec - (double)acq;
-                    const bool ok = rem >= 0;
-                    const uint64_t bad = __ballot(mine && typ == kCpSingle && !dead && !ok);
-                    uint64_t done = open;
-                    int64_t adv;
-                    if (bad) {
-                        const int k = __builtin_ctzll(bad);
-                        done = open & ((2ull << k) - 1ull);
-                        adv = __shfl((long long)excl, k, 64);  // the blocked lane k adds nothing
-                    } else {
-                        adv = cp_wave_sum(a);
-                    }
-                    if ((done >> lane) & 1ull) {
-                        if (typ == kCpSingle) {
-                            if (ok && !dead) cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
-                            else cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
-                        } else if (typ == kCpMulti) {
-                            b.chk[p] = ok ? 1 : 0;
+                // lanes whose own check decides their add (a failing check adds nothing)
+                const bool cut_kind = typ == kCpSingle || (typ == kCpMulti && add != 0);
+                uint64_t pending = __ballot(typ != kCpSkip);
+                uint64_t failed = 0;
+                while (pending) {
+                    const int f = __builtin_ctzll(pending);
+                    const int64_t Pf = __shfl((long long)Pq, f, 64);
+                    if (Pf != P) {  // currentWindow: close the open period, open Pf
+                        if (P != INT64_MIN && lane == (int)(P % S)) {
+                            bst = P * wl;
+                            bcnt = cur;
                         }
+                        P = Pf;
+                        const int I = (int)(P % S);
+                        const int64_t ws = P * wl, lo = ws - (int64_t)(S - 1) * wl;
+                        int64_t o = 0, cc = 0;
+                        if (lane < S) {
+                            if (lane == I) cc = bst == ws ? bcnt : 0;
+                            else if (bst != INT64_MIN && bst >= lo) o = bcnt;
+                        }
+                        other = cp_wave_sum(o);
+                        cur = cp_wave_sum(cc);
                     }
-                    cur += adv;
-                    open &= ~done;
-                    if (bad && open) {  // blocked even at the committed state: blocked for good
-                        const double lb = thr - (double)(other + cur) / r.isec - (double)acq;
-                        failed |= __ballot(((open >> lane) & 1ull) && typ == kCpSingle && lb < 0);
+                    uint64_t open = pending & __ballot(typ != kCpSkip && Pq == P);
+                    pending &= ~open;
+                    while (open) {
+                        const bool mine = (open >> lane) & 1ull;
+                        const bool dead = (failed >> lane) & 1ull;
+                        const int64_t a = (mine && !dead) ? add : 0;
+                        const int64_t excl = cp_excl_scan(a, lane);
+                        const double rem = thr - (double)(other + cur + excl) / r.isec - (double)acq;
+                        const bool ok = rem >= 0 && !dead;
+                        // a dead lane adds nothing already: not a cut (else every pass would stop at one)
+                        const uint64_t bad = __ballot(mine && cut_kind && !dead && !(rem >= 0));
+                        uint64_t done = open;
+                        int64_t adv;
+                        if (bad) {
+                            const int k = __builtin_ctzll(bad);
+                            done = open & ((2ull << k) - 1ull);
+                            adv = __shfl((long long)excl, k, 64);  // the failing lane k adds nothing
+                        } else {
+                            adv = cp_wave_sum(a);
+                        }
+                        if ((done >> lane) & 1ull) {
+                            if (typ == kCpSingle) {
+                                if (ok) cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
+                                else cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+                            } else if (typ == kCpMulti) {
+                                b.chk[p] = ok ? 1 : 0;
+                            }
+                        }
+                        cur += adv;
+                        open &= ~done;
+                        if (bad && open) {  // failing even at the committed state: fails for good
+                            const double lb = thr - (double)(other + cur) / r.isec - (double)acq;
+                            failed |= __ballot(((open >> lane) & 1ull) && (cut_kind || typ == kCpMulti) && lb < 0);
+                        }
                     }
                 }
             }
@@ -594,10 +627,16 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
         bool pass = true;
         for (uint32_t j = 0; j < q.value_count && pass; ++j) pass = b.chk[(uint64_t)q.value_begin + j] != 0;
         cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? -1 : 0);  // remaining -1: multi-value
-        if ((b.assume[i] != 0) != pass) {  // its slots are re-walked in the next round
+        if ((b.assume[i] != 0) != pass) {
+            // re-walk the slots whose adds change: a slot adds the request's count iff it is assumed to pass and
+            // the slot's check passed (a repeated value's extra records carry check 1), so slots where the check
+            // failed add nothing either way
             b.assume[i] = pass ? 1 : 0;
             *b.changed = 1;
-            for (uint32_t j = 0; j < q.value_count; ++j) b.dirty[b.pslot[(uint64_t)q.value_begin + j]] = 1;
+            for (uint32_t j = 0; j < q.value_count; ++j) {
+                const uint64_t p = (uint64_t)q.value_begin + j;
+                if (b.chk[p]) b.dirty[b.pslot[p]] = 1;
+            }
         }
     }
 }

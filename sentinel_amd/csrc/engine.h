@@ -566,6 +566,8 @@ hipError_t launch_walk_tiny(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
+// bytes (a multiple of 4) from device memory to a device-accessible host buffer by the shader
+hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,
                              const Bucket* old_ring, const Occ* old_occ, int old_stride, hipStream_t stream);

@@ -1894,6 +1894,34 @@ hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// Result copy to host memory by the shader (sg_flow_submit with a device-accessible host buffer): 16-B stores in
+// order over the PCIe link, so the results of batch i travel while the copy engine brings batch i + 1's requests
+// in (the two directions of the link in use at once, whatever the SDMA engine assignment). `dst` is the buffer's
+// device alias; bytes % 16 == 0 or the tail is copied by 4-B words.
+__global__ void __launch_bounds__(256) k_copy_out(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16,
+                                                  const uint32_t* __restrict__ src_tail, uint32_t* __restrict__ dst_tail,
+                                                  uint32_t tail_words) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {  // four loads in flight per thread
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < tail_words) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
+}
+
+hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int blocks, hipStream_t stream) {
+    const uint64_t n16 = bytes / 16;
+    const uint32_t tail = (uint32_t)((bytes % 16) / 4);
+    hipLaunchKernelGGL(k_copy_out, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst_dev, n16,
+                       (const uint32_t*)src + n16 * 4, (uint32_t*)dst_dev + n16 * 4, tail);
+    return hipGetLastError();
+}
+
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, stream, a);
     return hipGetLastError();

@@ -54,6 +54,25 @@ def test_pipelined_batches_equal_oracle(pinned):
     assert np.array_equal(ring, ring_o) and np.array_equal(occ, occ_o)
 
 
+@pytest.mark.parametrize("offset,trim", [(1, 0), (4, 3), (0, 1)])
+def test_pinned_outputs_any_alignment_and_length(offset, trim):
+    """Results into views of pinned buffers: a 12-B offset (not 16-B aligned: the copy engine takes it), a 48-B
+    offset (the shader copy), and batch lengths whose result bytes are not a multiple of 16 (the copy kernel's
+    4-B tail)."""
+    wl, eng, ora = _setup(seed=35)
+    reqs = [wl.requests(b)[: 100_000 - trim - b] for b in range(4)]
+    bufs = [eng.host_array(len(r) + offset, abi.RES_DTYPE) for r in reqs]
+    outs = [bf[offset:offset + len(r)] for bf, r in zip(bufs, reqs)]
+    for bf in bufs:
+        bf["status"] = -7  # sentinel: every slot must be overwritten
+    tickets = [eng.submit(r, o) for r, o in zip(reqs, outs)]
+    for t in tickets:
+        eng.wait(t)
+    for b, (r, o, bf) in enumerate(zip(reqs, outs, bufs)):
+        assert np.array_equal(o, ora.decide(r)), f"batch {b}"
+        assert (bf["status"][:offset] == -7).all()  # nothing written before the view
+
+
 def test_rejected_batch_reports_on_its_ticket():
     from sentinel_amd.engine import EngineError
     wl, eng, ora = _setup()
