@@ -152,8 +152,8 @@ def cpu_baseline(n_flows, n_requests, seconds_budget=25.0, threads=None):
 
 def end_to_end(eng, wl, first_b, n_batches, n_req, n_out=4):
     """Decisions/s with the requests in HOST memory (what a JVM token server hands over through JNI): pinned
-    buffers → sg_flow_submit (H2D on the copy engine, decide, results back by the shader into the pinned output,
-    3 batches in flight) → sg_flow_wait, n_batches back to back in steady state. Every batch has its own pinned
+    buffers → sg_flow_submit (H2D and D2H on the copy engines, overlapping each other and the decisions, 3 batches
+    in flight) → sg_flow_wait, n_batches back to back in steady state. Every batch has its own pinned
     request buffer (time-ordered batches, generated before the clock starts); the outputs cycle through n_out
     buffers, as a caller reusing its result buffers would."""
     ins = [eng.host_array(n_req, abi.REQ_DTYPE) for _ in range(n_batches)]
@@ -177,7 +177,7 @@ def end_to_end(eng, wl, first_b, n_batches, n_req, n_out=4):
     return {"value": n_batches * n_req / el, "unit": "decisions/s", "batches": n_batches,
             "ms_per_batch": el * 1000.0 / n_batches, "h2d_bytes_per_batch": h2d, "d2h_bytes_per_batch": d2h,
             "h2d_GBps": h2d * n_batches / el / 1e9, "d2h_GBps": d2h * n_batches / el / 1e9, "ok_last_batch": ok,
-            "d2h_path": "copy engine" if os.environ.get("SG_D2H") == "0" else "shader copy (k_copy_out)",
+            "d2h_path": "shader copy (k_copy_out)" if os.environ.get("SG_D2H") == "1" else "copy engine",
             "path": "pinned host buffers -> sg_flow_submit (H2D / decide / D2H overlapped, 3 in flight) -> sg_flow_wait"}
 
 

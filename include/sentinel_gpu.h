@@ -417,18 +417,23 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n);
  * no collective on the decision path). GlobalRequestLimiter's per-namespace QPS limiter counts every request of
  * the namespace in node order (GlobalRequestLimiter.java:46-55, ClusterFlowChecker.allowProceed :45-51), which a
  * shard does not see on its own: with world > 1 and limiter-enabled namespaces every flow batch of the shard goes
- * through the exchange below (the pipelined / async flow entry points and cluster param batches refuse such a
- * handle with SG_E_UNSUPPORTED; sg_flow_decide_batch without an armed exchange does too). */
+ * through the exchange below — synchronous, pipelined (sg_flow_enqueue) and host-pipelined (sg_flow_submit) flow
+ * batches and cluster param batches (sg_cparam_decide_batch) alike; a batch without an armed exchange is refused
+ * with SG_E_UNSUPPORTED. */
 int sg_set_shard(sg_handle* h, int32_t rank, int32_t world);
 
 /* Sharded namespace limiter exchange (replaces GlobalRequestLimiter.tryPass's node-wide counting):
- *   1. sg_lim_arrivals: this shard's valid requests of limited namespaces per (limiter slot, millisecond),
- *      counts_out[slot * n_ms + (ts_ms - t_base)] (DEVICE, n_lim * n_ms uint32; slots = the limiter-enabled
- *      namespaces in sg_set_namespaces order). [t_base, t_base + n_ms) is node-wide and must hold every shard's
- *      limited requests of the node batch (SG_E_INVAL otherwise); n_ms <= 65536. Synchronous on `stream`.
+ *   1. sg_lim_arrivals (flow batches) / sg_lim_arrivals_param (cluster param batches, ClusterParamFlowChecker
+ *      .java:43-45 shares the limiter): this shard's valid requests of limited namespaces per (limiter slot,
+ *      millisecond), counts_out[slot * n_ms + (ts_ms - t_base)] (DEVICE, n_lim * n_ms uint32; slots = the
+ *      limiter-enabled namespaces in sg_set_namespaces order). [t_base, t_base + n_ms) is node-wide and must hold
+ *      every shard's limited requests of the node batch (SG_E_INVAL otherwise); n_ms <= 65536. `req` is device
+ *      memory (or pinned host memory the device can read). Synchronous on `stream`; batches in flight on the
+ *      pipeline go on.
  *   2. the node all-gathers the counts of its `world` shards (RCCL) into gathered[world][n_lim][n_ms] (DEVICE);
- *   3. sg_lim_exchange arms the handle's next sg_flow_decide_batch / _host with them (that call consumes it; the
- *      buffer must stay valid until it returns).
+ *   3. sg_lim_exchange arms the handle's next flow or param batch with them: sg_flow_decide_batch / _host,
+ *      sg_flow_enqueue, sg_flow_submit or sg_cparam_decide_batch / _host consumes it. The buffer must stay valid
+ *      until that call returns (the pipelined calls copy it before returning).
  * The node's arrival order is (ts_ms, shard rank, position in the shard's batch). Every shard walks the same
  * per-100 ms node arrivals, so each keeps an identical replica of the namespace windows, and admits its request
  * iff its node-wide rank in the period is below the period's quota: the results equal one handle deciding the
@@ -438,6 +443,8 @@ int sg_set_shard(sg_handle* h, int32_t rank, int32_t world);
  * requests as limiter arrivals; their flow decisions did not happen). */
 int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base, uint32_t n_ms, uint32_t* counts_out,
                     uint64_t counts_words, void* stream);
+int sg_lim_arrivals_param(sg_handle* h, const sg_cparam_req* req, uint64_t n, int64_t t_base, uint32_t n_ms,
+                          uint32_t* counts_out, uint64_t counts_words, void* stream);
 int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, uint64_t gathered_words, int64_t t_base, uint32_t n_ms);
 /* The handle's limiter-slot count n_lim (limiter-enabled namespaces of sg_set_namespaces): counts_words of
  * sg_lim_arrivals must equal n_lim * n_ms and gathered_words of sg_lim_exchange world * n_lim * n_ms (SG_E_INVAL). */

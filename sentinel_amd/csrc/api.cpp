@@ -126,6 +126,7 @@ struct sg_handle {
     int* d_cp_changed = nullptr;
     uint8_t* d_cp_rule_lim = nullptr; // [cparam rules] limiter slot of the rule's namespace (0xFF none)
     std::vector<uint8_t> cp_rule_lim_host;
+    bool cp_any_lim = false;          // some cluster param rule's namespace has a limiter
     uint32_t cp_rounds = 0;           // fixed-point rounds of the last batch (stats / tests)
     uint32_t cp_max_rounds = 64;      // env SG_CP_MAX_ROUNDS overrides (tests force the serial fallback)
     sg_cparam_req* d_cpreq_h = nullptr;
@@ -176,6 +177,10 @@ struct sg_handle {
     int kbits = 0, ibits = 0, abits = 0;
     int32_t shard_rank = 0, shard_world = 1;  // sg_set_shard: this handle's share of a node's flowIds
     // sg_lim_exchange: the node's gathered per-millisecond limiter arrivals for the next flow batch of a shard
+    uint32_t* d_xg_ws[2]{};           // the gathered arrivals a pipelined batch of workspace x reads (copied at enqueue)
+    uint64_t xg_ws_cap = 0;           // words per buffer
+    int* d_limx_err = nullptr;        // sg_lim_arrivals' own error word (the pipelined batches keep theirs)
+    int* h_limx_err = nullptr;        // pinned
     const uint32_t* lim_xg = nullptr;
     int64_t lim_xt = 0;
     uint32_t lim_xn = 0;
@@ -259,7 +264,8 @@ struct sg_handle {
     hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
     uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
-    bool d2h_kernel = true;           // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=0: off)
+    bool d2h_kernel = false;          // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=1; the
+                                      // copy engine measured faster: 2.64 vs 2.45 G decisions/s end to end)
     int d2h_blocks = 64;              // its workgroups (env SG_D2H_BLOCKS)
     int front_eighths = 3;            // CU partition of the pipeline streams (see pipe_setup; 3/8 measured best)
     int walk_cus = 0;                 // CUs of the walkers' streams when partitioned (0 = all)
@@ -536,6 +542,10 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_rule_lim);
     dfree(h->d_lim_slot);
     dfree(h->d_lim_tile);
+    dfree(h->d_xg_ws[0]);
+    dfree(h->d_xg_ws[1]);
+    dfree(h->d_limx_err);
+    if (h->h_limx_err) (void)hipHostFree(h->h_limx_err);
     dfree(h->d_lim_period);
     dfree(h->d_bnd);
     dfree(h->d_p0);
@@ -670,16 +680,47 @@ int sg_lim_arrivals(sg_handle* h, const sg_req* req, uint64_t n, int64_t t_base,
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
-    drain_async(h);
+    // reads only the request batch and the rule → limiter table: batches in flight on the pipeline go on
     int rc = ensure_layout(h);
     if (rc) return rc;
+    if (!h->d_limx_err && (hipMalloc(&h->d_limx_err, sizeof(int)) != hipSuccess ||
+                           hipHostMalloc(&h->h_limx_err, sizeof(int)) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "exchange error word");
     HIP_TRY(h, hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * (size_t)h->n_lim * n_ms, stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_limx_err, 0, sizeof(int), stream));
     if (h->n_lim > 0)
-        HIP_TRY(h, launch_lim_arrivals(req, n, h->K, h->d_rule_lim, t_base, n_ms, counts_out, h->d_err, stream));
-    HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, launch_lim_arrivals(req, n, h->K, h->d_rule_lim, t_base, n_ms, counts_out, h->d_limx_err, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_limx_err, h->d_limx_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipStreamSynchronize(stream));
-    return flow_status(h, *h->h_err);
+    return flow_status(h, *h->h_limx_err);
+}
+
+namespace {
+int cp_rule_limiters(sg_handle* h, hipStream_t stream);
+}
+
+int sg_lim_arrivals_param(sg_handle* h, const sg_cparam_req* req, uint64_t n, int64_t t_base, uint32_t n_ms,
+                          uint32_t* counts_out, uint64_t counts_words, void* stream_) {
+    if (!h || (!req && n) || !counts_out) return SG_E_INVAL;
+    if (t_base < 0 || n_ms == 0 || n_ms > kMaxPeriods) return fail(h, SG_E_INVAL, "exchange range: t_base >= 0, 1 <= n_ms <= 65536");
+    if (counts_words != (uint64_t)h->n_lim * n_ms)
+        return fail(h, SG_E_INVAL, "counts buffer must hold n_lim * n_ms words (sg_lim_slots)");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    int rc = cp_rule_limiters(h, stream);
+    if (rc) return rc;
+    if (!h->d_limx_err && (hipMalloc(&h->d_limx_err, sizeof(int)) != hipSuccess ||
+                           hipHostMalloc(&h->h_limx_err, sizeof(int)) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "exchange error word");
+    HIP_TRY(h, hipMemsetAsync(counts_out, 0, sizeof(uint32_t) * (size_t)h->n_lim * n_ms, stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_limx_err, 0, sizeof(int), stream));
+    if (h->n_lim > 0 && h->d_cp_rule_lim)
+        HIP_TRY(h, launch_lim_arrivals_param(req, n, (uint32_t)h->cprules.size(), h->d_cp_rule_lim, t_base, n_ms,
+                                             counts_out, h->d_limx_err, stream));
+    HIP_TRY(h, hipMemcpyAsync(h->h_limx_err, h->d_limx_err, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipStreamSynchronize(stream));
+    return flow_status(h, *h->h_limx_err);
 }
 
 int sg_lim_exchange(sg_handle* h, const uint32_t* gathered, uint64_t gathered_words, int64_t t_base, uint32_t n_ms) {
@@ -1120,6 +1161,8 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
         L.ring = h->d_lim_ring;
         if (h->lim_x_armed) {
             L.xg = h->lim_xg;
+            L.ts = &a.req[0].ts_ms;
+            L.ts_stride = sizeof(sg_req) / sizeof(int64_t);
             L.t_base = h->lim_xt;
             L.n_ms = h->lim_xn;
             L.world = h->shard_world;
@@ -1196,8 +1239,6 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
 // that marks the batch's completion through *done (the back half's end, recorded on s_back).
 int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hipEvent_t after, int* err_dst,
                            hipEvent_t done) {
-    if (h->shard_world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
     int rc = ensure_layout(h);
     if (rc) return rc;
     rc = pipe_setup(h);
@@ -1207,6 +1248,24 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
     const bool first = h->pipe_seq == 0;
     sg_handle::FlowWs w = h->pws;
     if (x == 0) main_ws(h, w);
+    // sharded namespace limiter: the armed exchange is copied into workspace x's own buffer now (the caller's
+    // buffer is free again when this returns); the batch two back, which read that buffer, has finished its
+    // front half by then
+    const bool xshard = h->shard_world > 1 && h->n_lim > 0;
+    if (xshard) {
+        const uint64_t words = (uint64_t)h->shard_world * h->n_lim * h->lim_xn;
+        if (words > h->xg_ws_cap) {
+            (void)hipDeviceSynchronize();
+            dfree(h->d_xg_ws[0]);
+            dfree(h->d_xg_ws[1]);
+            if (hipMalloc(&h->d_xg_ws[0], 4 * words) != hipSuccess || hipMalloc(&h->d_xg_ws[1], 4 * words) != hipSuccess)
+                return fail(h, SG_E_NOMEM, "exchange buffers");
+            h->xg_ws_cap = words;
+        } else if (h->pipe_seq >= 2) {
+            HIP_TRY(h, hipEventSynchronize(h->front_done[x]));
+        }
+        HIP_TRY(h, hipMemcpy(h->d_xg_ws[x], h->lim_xg, 4 * words, hipMemcpyDeviceToDevice));
+    }
     BatchArgs a = flow_args(h, w, req, n, out);
     if (after) HIP_TRY(h, hipStreamWaitEvent(h->s_front, after, 0));
     if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
@@ -1215,7 +1274,12 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
     } else {
         a.check_last = 0;  // checked by the back half, after the previous batch has advanced last_ts
     }
+    if (xshard) {
+        h->lim_xg = h->d_xg_ws[x];
+        h->lim_x_armed = true;  // read by flow_front
+    }
     rc = flow_front(h, a, w.hist, h->s_front, false);
+    h->lim_x_armed = false;
     if (rc) return rc;
     HIP_TRY(h, hipEventRecord(h->front_done[x], h->s_front));
     HIP_TRY(h, hipStreamWaitEvent(h->s_back, h->front_done[x], 0));
@@ -1334,14 +1398,28 @@ void sg_host_free(sg_handle* h, void* p) {
     (void)hipHostFree(p);
 }
 
+// A pipelined batch of a shard with a namespace limiter consumes the armed exchange (sg_lim_exchange before every
+// batch, as for sg_flow_decide_batch); an empty or refused batch walks it at once (the replica advances).
+static int xshard_gate(sg_handle* h, uint64_t n, const char* early) {
+    if (!(h->shard_world > 1 && h->n_lim > 0)) return early ? (n == 0 ? 1 : fail(h, SG_E_INVAL, early)) : SG_OK;
+    if (!h->lim_x_armed)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: sg_lim_exchange must precede every flow batch");
+    if (!early) return SG_OK;
+    h->lim_x_armed = false;
+    int rc = lim_plan_only(h, nullptr);
+    if (rc) return rc;
+    return n == 0 ? 1 : fail(h, n > h->cfg.max_batch ? SG_E_CAPACITY : SG_E_INVAL, early);
+}
+
 int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
     if (!h || !ticket) return SG_E_INVAL;
     *ticket = 0;
-    if (h->shard_world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
-    if (n == 0) return SG_OK;
-    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    {
+        const char* early = n == 0 ? "" : (!req || !out) ? "null buffer"
+                            : n > h->cfg.max_batch ? "batch larger than max_batch" : nullptr;
+        const int g = xshard_gate(h, n, early);
+        if (g) return g == 1 ? SG_OK : g;
+    }
     HIP_TRY(h, hipSetDevice(h->device));
     if (!h->s_comp) {  // first use: streams, per-slot device buffers, events, pinned error words
         HIP_TRY(h, hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking));
@@ -1371,8 +1449,8 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
     int rc = enqueue_flow_pipelined(h, sl.d_req, n, sl.d_out, sl.h2d, sl.h_err, sl.comp);
     if (rc) return rc;
     HIP_TRY(h, hipStreamWaitEvent(h->s_out, sl.comp, 0));
-    // results back: by a copy kernel when `out` is pinned host memory the device can address (env SG_D2H = 0: the
-    // copy engine), so that the link carries this batch's results while the copy engine brings the next requests
+    // results back on the copy engine (both directions of the link overlap: H2D of the next batch on s_in), or with
+    // SG_D2H=1 by a copy kernel when `out` is pinned host memory the device can address
     void* out_dev = nullptr;
     if (h->d2h_kernel) {
         hipPointerAttribute_t pa{};
@@ -1394,11 +1472,12 @@ int sg_flow_submit(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, 
 int sg_flow_enqueue(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
     if (!h || !ticket) return SG_E_INVAL;
     *ticket = 0;
-    if (h->shard_world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: decide with sg_lim_exchange + sg_flow_decide_batch");
-    if (n == 0) return SG_OK;
-    if (!req || !out) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    {
+        const char* early = n == 0 ? "" : (!req || !out) ? "null buffer"
+                            : n > h->cfg.max_batch ? "batch larger than max_batch" : nullptr;
+        const int g = xshard_gate(h, n, early);
+        if (g) return g == 1 ? SG_OK : g;
+    }
     HIP_TRY(h, hipSetDevice(h->device));
     sg_handle::DevTicket& d = h->dev[h->next_ticket % kDevSlots];
     if (!d.done) {
@@ -1456,8 +1535,8 @@ int sg_flow_wait(sg_handle* h, uint64_t ticket) {
 
 int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out) {
     if (!h) return SG_E_INVAL;
-    if (n == 0) return sg_flow_decide_batch(h, nullptr, 0, nullptr, nullptr);  // (advances a sharded limiter)
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    // empty or refused before the device: the device entry point answers (and walks an armed exchange)
+    if (n == 0 || n > h->cfg.max_batch || !req || !out) return sg_flow_decide_batch(h, n ? req : nullptr, n, out, nullptr);
     HIP_TRY(h, hipSetDevice(h->device));
     if (!h->d_req_h) {
         if (hipMalloc(&h->d_req_h, sizeof(sg_req) * h->cfg.max_batch) != hipSuccess ||
@@ -1942,18 +2021,77 @@ static CPArgs cp_args(sg_handle* h, const sg_cparam_req* req, uint64_t n, const 
     return c;
 }
 
+namespace {
+
+// allowProceed → GlobalRequestLimiter.tryPass for the namespaces with a limiter (state shared with flow tokens):
+// the limiter slot of every cluster param rule's namespace on the device (h->cp_any_lim: some rule has one)
+int cp_rule_limiters(sg_handle* h, hipStream_t stream) {
+    const uint32_t R = (uint32_t)h->cprules.size();
+    std::vector<uint8_t> rl(R ? R : 1, 0xFF);
+    bool any_lim = false;
+    for (uint32_t k = 0; k < R; ++k) {
+        const int ns = h->cprules[k].namespace_id;
+        if (ns >= 0 && (size_t)ns < h->ns_slot.size() && h->ns_slot[ns] >= 0) {
+            rl[k] = (uint8_t)h->ns_slot[ns];
+            any_lim = true;
+        }
+    }
+    h->cp_any_lim = any_lim;
+    if (any_lim && (rl != h->cp_rule_lim_host || !h->d_cp_rule_lim)) {
+        dfree(h->d_cp_rule_lim);
+        if (hipMalloc(&h->d_cp_rule_lim, rl.size()) != hipSuccess) return fail(h, SG_E_NOMEM, "cparam limiter table");
+        HIP_TRY(h, hipMemcpyAsync(h->d_cp_rule_lim, rl.data(), rl.size(), hipMemcpyHostToDevice, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        h->cp_rule_lim_host = rl;
+    }
+    return SG_OK;
+}
+
+int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values, uint64_t n_values,
+                 sg_result* out, hipStream_t stream);
+
+}  // namespace
+
+// With a sharded namespace limiter (sg_set_shard, world > 1) every batch consumes an armed sg_lim_exchange over the
+// node's param requests (sg_lim_arrivals_param); a batch rejected on the device, an empty one or one refused
+// before the device still walks the armed arrivals (the shard's replica of the namespace windows advances).
 int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
                            uint64_t n_values, sg_result* out, void* stream_) {
     if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
-    if (!req || !out || (!values && n_values)) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
-    if (!h->d_cplast_ts) return fail(h, SG_E_INVAL, "sg_cparam_load_rules first");
-    if (h->shard_world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "cluster param tokens on a shard with a namespace limiter (the exchange covers flow batches)");
+    const bool xshard = h->shard_world > 1 && h->n_lim > 0;
+    if (xshard && !h->lim_x_armed)
+        return fail(h, SG_E_UNSUPPORTED, "sharded namespace limiter: sg_lim_exchange must precede every param batch");
+    const bool armed = h->lim_x_armed;
+    h->lim_x_armed = false;  // consumed by this call, whatever its outcome
     hipStream_t stream = (hipStream_t)stream_;
+    const char* early = n == 0 ? "" : (!req || !out || (!values && n_values)) ? "null buffer"
+                        : n > h->cfg.max_batch ? "batch larger than max_batch"
+                        : !h->d_cplast_ts ? "sg_cparam_load_rules first" : nullptr;
+    if (early) {
+        if (armed) {
+            int rc = lim_plan_only(h, stream);
+            if (rc) return rc;
+        }
+        if (n == 0) return SG_OK;
+        return fail(h, n > h->cfg.max_batch ? SG_E_CAPACITY : SG_E_INVAL, early);
+    }
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
+    h->lim_x_armed = armed;  // read by cparam_batch's limiter step
+    const int rc = cparam_batch(h, req, n, values, n_values, out, stream);
+    const bool unused = h->lim_x_armed;  // still set: the batch stopped before its limiter step
+    h->lim_x_armed = false;
+    if (unused && armed) {
+        const int rc2 = lim_plan_only(h, stream);
+        if (rc2 && !rc) return rc2;
+    }
+    return rc;
+}
+
+namespace {
+
+int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values, uint64_t n_values,
+                 sg_result* out, hipStream_t stream) {
     CPArgs c = cp_args(h, req, n, values, n_values, out);
     const uint64_t nv = n_values ? n_values : 1;
     const int gbits = bits_for(h->cptotal + 1);
@@ -1993,24 +2131,10 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     if (!h->d_cp_assume && (hipMalloc(&h->d_cp_assume, h->cfg.max_batch) != hipSuccess ||
                             hipMalloc(&h->d_cp_changed, sizeof(int)) != hipSuccess))
         return fail(h, SG_E_NOMEM, "cparam batch scratch");
-    // allowProceed → GlobalRequestLimiter.tryPass for the namespaces with a limiter (state shared with flow tokens)
+    int rc = cp_rule_limiters(h, stream);
+    if (rc) return rc;
+    const bool any_lim = h->cp_any_lim;
     const uint32_t R = (uint32_t)h->cprules.size();
-    std::vector<uint8_t> rl(R ? R : 1, 0xFF);
-    bool any_lim = false;
-    for (uint32_t k = 0; k < R; ++k) {
-        const int ns = h->cprules[k].namespace_id;
-        if (ns >= 0 && (size_t)ns < h->ns_slot.size() && h->ns_slot[ns] >= 0) {
-            rl[k] = (uint8_t)h->ns_slot[ns];
-            any_lim = true;
-        }
-    }
-    if (any_lim && (rl != h->cp_rule_lim_host || !h->d_cp_rule_lim)) {
-        dfree(h->d_cp_rule_lim);
-        if (hipMalloc(&h->d_cp_rule_lim, rl.size()) != hipSuccess) return fail(h, SG_E_NOMEM, "cparam limiter table");
-        HIP_TRY(h, hipMemcpyAsync(h->d_cp_rule_lim, rl.data(), rl.size(), hipMemcpyHostToDevice, stream));
-        HIP_TRY(h, hipStreamSynchronize(stream));
-        h->cp_rule_lim_host = rl;
-    }
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     CPBatch b{};
     b.owner = h->d_cp_owner;
@@ -2066,6 +2190,16 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
         L.prefix = h->d_lim_period + (size_t)kMaxLim * kMaxPeriods;
         L.quota = h->d_lim_period + (size_t)2 * kMaxLim * kMaxPeriods;
         L.ring = h->d_lim_ring;
+        if (h->lim_x_armed) {  // sharded: the node's gathered param arrivals (sg_lim_exchange)
+            L.xg = h->lim_xg;
+            L.ts = &req[0].ts_ms;
+            L.ts_stride = sizeof(sg_cparam_req) / sizeof(int64_t);
+            L.t_base = h->lim_xt;
+            L.n_ms = h->lim_xn;
+            L.world = h->shard_world;
+            L.rank = h->shard_rank;
+            h->lim_x_armed = false;
+        }
         HIP_TRY(h, launch_limiter(a, L, stream));
     }
     // one lane per (rule, value) slot: k_seg's lists over the sorted value records
@@ -2142,6 +2276,8 @@ int sg_cparam_decide_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, c
     return SG_OK;
 }
 
+}  // namespace
+
 int sg_cparam_last_rounds(const sg_handle* h, uint32_t* rounds) {
     if (!h || !rounds) return SG_E_INVAL;
     *rounds = h->cp_rounds;
@@ -2151,8 +2287,9 @@ int sg_cparam_last_rounds(const sg_handle* h, uint32_t* rounds) {
 int sg_cparam_decide_batch_host(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
                                 uint64_t n_values, sg_result* out) {
     if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    // empty or refused before the device: the device entry point answers (and walks an armed exchange)
+    if (n == 0 || n > h->cfg.max_batch || !req || !out || (!values && n_values))
+        return sg_cparam_decide_batch(h, n ? req : nullptr, n, values, n_values, out, nullptr);
     HIP_TRY(h, hipSetDevice(h->device));
     if (!h->d_cpreq_h) {
         if (hipMalloc(&h->d_cpreq_h, sizeof(sg_cparam_req) * h->cfg.max_batch) != hipSuccess ||

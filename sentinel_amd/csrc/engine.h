@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/sentinel_gpu.h"
@@ -125,6 +126,9 @@ struct LimRing {                    // one UnaryLeapArray(10, 1000); start INT64
     int64_t count[kLimSamples];
 };
 
+static_assert(sizeof(sg_req) % sizeof(int64_t) == 0 && sizeof(sg_cparam_req) % sizeof(int64_t) == 0 &&
+                  offsetof(sg_req, ts_ms) == 0 && offsetof(sg_cparam_req, ts_ms) == 0,
+              "LimArgs::ts strides over the request records");
 struct LimArgs {
     int n_lim;
     int wl_idx;                     // index of the 100 ms window length in the period table
@@ -140,6 +144,8 @@ struct LimArgs {
     // sharded limiter: per-millisecond arrivals of every shard, gathered by the node; null = this
     // handle sees the namespace's whole arrival sequence
     const uint32_t* xg;             // [world][n_lim][n_ms]
+    const int64_t* ts;              // request i's ts_ms at ts[i * ts_stride] (sg_req: 2 words, sg_cparam_req: 3)
+    uint32_t ts_stride;
     int64_t t_base;                 // the exchange's first millisecond (node-wide)
     uint32_t n_ms;                  // milliseconds covered, <= kMaxPeriods
     int world, rank;
@@ -151,6 +157,8 @@ hipError_t launch_limiter_plan_only(const BatchArgs& a, const LimArgs& L, hipStr
 // This shard's arrivals per (limiter slot, millisecond) for the exchange: counts[slot * n_ms + (ts - t_base)].
 hipError_t launch_lim_arrivals(const sg_req* req, uint64_t n, uint32_t K, const uint8_t* rule_lim, int64_t t_base,
                                uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream);
+hipError_t launch_lim_arrivals_param(const sg_cparam_req* req, uint64_t n, uint32_t K, const uint8_t* rule_lim,
+                                     int64_t t_base, uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream);
 
 // ---- hot-parameter flow control (param.hip) ----
 constexpr int kErrNonPositive = 4;  // some acquireCount <= 0 in the batch (disables the skip shortcut)

@@ -155,19 +155,21 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         // DefaultTokenService.requestToken validation, srv/flow/DefaultTokenService.java:39-47, 87-89
         const uint32_t key = r.key & SG_KEY_INDEX;
         uint64_t rec;
+        int32_t st;
         if (key == SG_KEY_BAD || r.acquire <= 0) {
-            store_result(a.out, (uint32_t)i, SG_STATUS_BAD_REQUEST, 0, 0);
+            st = SG_STATUS_BAD_REQUEST;
             rec = sentinel;
         } else if (key >= a.K) {
-            store_result(a.out, (uint32_t)i, SG_STATUS_NO_RULE_EXISTS, 0, 0);
+            st = SG_STATUS_NO_RULE_EXISTS;
             rec = sentinel;
         } else {
             uint64_t q = (uint64_t)(uint32_t)r.acquire;
             if (q > a.aesc) q = a.aesc;
             const uint64_t ac = (q << 1) | (uint64_t)(r.key >> 31);
             rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
-            store_result(a.out, (uint32_t)i, SG_STATUS_BLOCKED, 0, 0);  // walkers write only non-BLOCKED
+            st = SG_STATUS_BLOCKED;  // walkers write only non-BLOCKED
         }
+        store_result(a.out, (uint32_t)i, st, 0, 0);
         a.rec[i] = rec;
         if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
     }

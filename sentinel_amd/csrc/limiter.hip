@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(kLimThreads) k_lim_count(BatchArgs a, LimArgs 
         }
         if (slot != 0xFF && L.xg) {
             atomicAdd(&tot[slot], 1u);
-            const int64_t m = a.req[i].ts_ms - L.t_base;
+            const int64_t m = L.ts[i * L.ts_stride] - L.t_base;
             if (m < 0 || m >= (int64_t)L.n_ms) atomicOr(a.err, kErrExchange);
         } else if (slot != 0xFF) {
             atomicAdd(&tot[slot], 1u);
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(kLimThreads) k_lim_apply(BatchArgs a, LimArgs 
             uint32_t q;
             int64_t rank;
             if (L.xg) {  // the node-wide rank within the period (k_lim_plan's xoff)
-                const uint32_t m = (uint32_t)(a.req[i].ts_ms - L.t_base);
+                const uint32_t m = (uint32_t)(L.ts[i * L.ts_stride] - L.t_base);
                 q = (m + (uint32_t)(L.t_base % kLimWindowMs)) / kLimWindowMs;
                 rank = (int64_t)C + (int64_t)((const int32_t*)L.arrivals)[(size_t)slot * kMaxPeriods + m];
             } else {
@@ -307,7 +307,23 @@ hipError_t launch_limiter_plan_only(const BatchArgs& a, const LimArgs& L, hipStr
 
 constexpr uint32_t kLimxWin = 256;  // milliseconds a tile aggregates in LDS (a time-ordered tile spans few)
 
-__global__ void __launch_bounds__(kLimThreads) k_limx_arrivals(const sg_req* req, uint64_t n, uint32_t K,
+// The limiter's tryPass candidates of a flow batch (DefaultTokenService.requestToken validation, as k_prep) and of a
+// cluster param batch (requestParamToken validation, as k_cp_prep2): key = rule index, or none.
+struct LimxFlowReq {
+    __device__ static uint32_t key(const sg_req& q, uint32_t K) {
+        const uint32_t k = q.key & SG_KEY_INDEX;
+        return (k == SG_KEY_BAD || q.acquire <= 0 || k >= K) ? 0xFFFFFFFFu : k;
+    }
+};
+struct LimxParamReq {
+    __device__ static uint32_t key(const sg_cparam_req& q, uint32_t K) {
+        const uint32_t k = q.key & SG_KEY_INDEX;
+        return (k == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0 || k >= K) ? 0xFFFFFFFFu : k;
+    }
+};
+
+template <class Req, class V>
+__global__ void __launch_bounds__(kLimThreads) k_limx_arrivals(const Req* req, uint64_t n, uint32_t K,
                                                               const uint8_t* rule_lim, int64_t t_base, uint32_t n_ms,
                                                               uint32_t* counts, int* err) {
     __shared__ uint32_t hist[kMaxLim][kLimxWin];
@@ -321,9 +337,9 @@ __global__ void __launch_bounds__(kLimThreads) k_limx_arrivals(const sg_req* req
     for (int r = 0; r < kLimRounds; ++r) {
         const uint64_t i = base + (uint64_t)r * kLimThreads + tid;
         if (i >= n) break;
-        const sg_req q = req[i];
-        const uint32_t key = q.key & SG_KEY_INDEX;  // DefaultTokenService.requestToken validation, as k_prep
-        if (key == SG_KEY_BAD || q.acquire <= 0 || key >= K) continue;
+        const Req q = req[i];
+        const uint32_t key = V::key(q, K);
+        if (key == 0xFFFFFFFFu) continue;
         const uint8_t slot = rule_lim[key];
         if (slot == 0xFF) continue;
         const int64_t m = q.ts_ms - t_base;
@@ -347,8 +363,17 @@ hipError_t launch_lim_arrivals(const sg_req* req, uint64_t n, uint32_t K, const 
                                uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t ntiles = (uint32_t)((n + kLimTile - 1) / kLimTile);
-    hipLaunchKernelGGL(k_limx_arrivals, dim3(ntiles), dim3(kLimThreads), 0, stream, req, n, K, rule_lim, t_base, n_ms,
-                       counts, err);
+    hipLaunchKernelGGL((k_limx_arrivals<sg_req, LimxFlowReq>), dim3(ntiles), dim3(kLimThreads), 0, stream, req, n, K,
+                       rule_lim, t_base, n_ms, counts, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_lim_arrivals_param(const sg_cparam_req* req, uint64_t n, uint32_t K, const uint8_t* rule_lim,
+                                     int64_t t_base, uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t ntiles = (uint32_t)((n + kLimTile - 1) / kLimTile);
+    hipLaunchKernelGGL((k_limx_arrivals<sg_cparam_req, LimxParamReq>), dim3(ntiles), dim3(kLimThreads), 0, stream, req,
+                       n, K, rule_lim, t_base, n_ms, counts, err);
     return hipGetLastError();
 }
 

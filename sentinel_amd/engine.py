@@ -12,7 +12,7 @@ from . import abi
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libsentinel_gpu.so")  # override: A/B tuning runs
 
-EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_lim_arrivals",
+EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_set_shard", "sg_lim_arrivals", "sg_lim_arrivals_param",
            "sg_lim_exchange", "sg_lim_slots", "sg_load_flow_rules",
            "sg_flow_decide_batch", "sg_flow_decide_batch_host", "sg_flow_submit", "sg_flow_enqueue", "sg_flow_poll", "sg_flow_wait",
            "sg_host_alloc", "sg_host_free", "sg_enable_stats", "sg_get_stats",
@@ -56,6 +56,7 @@ def load_library():
         "sg_set_namespaces": (C.c_int, [vp, vp, u32]),
         "sg_set_shard": (C.c_int, [vp, C.c_int32, C.c_int32]),
         "sg_lim_arrivals": (C.c_int, [vp, vp, u64, i64, u32, vp, u64, vp]),
+        "sg_lim_arrivals_param": (C.c_int, [vp, vp, u64, i64, u32, vp, u64, vp]),
         "sg_lim_exchange": (C.c_int, [vp, vp, u64, i64, u32]),
         "sg_lim_slots": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
         "sg_load_flow_rules": (C.c_int, [vp, vp, u32]),
@@ -184,6 +185,14 @@ class FlowEngine:
         if counts_words is None:
             counts_words = self.lim_slots() * n_ms
         self._check(self._L.sg_lim_arrivals(self.h, req_ptr, n, t_base, n_ms, counts_ptr, counts_words, stream_ptr))
+
+    def lim_arrivals_param(self, req_ptr: int, n: int, t_base: int, n_ms: int, counts_ptr: int, stream_ptr: int = 0,
+                           counts_words: int = None):
+        """sg_lim_arrivals over a device batch of sg_cparam_req (cluster param tokens share the namespace limiter)."""
+        if counts_words is None:
+            counts_words = self.lim_slots() * n_ms
+        self._check(self._L.sg_lim_arrivals_param(self.h, req_ptr, n, t_base, n_ms, counts_ptr, counts_words,
+                                                  stream_ptr))
 
     def lim_exchange(self, gathered_ptr: int, t_base: int, n_ms: int, gathered_words: int = None):
         """Arm the next flow batch with the node's gathered arrivals (device [world][n_lim][n_ms]; gathered_words

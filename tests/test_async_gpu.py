@@ -54,11 +54,13 @@ def test_pipelined_batches_equal_oracle(pinned):
     assert np.array_equal(ring, ring_o) and np.array_equal(occ, occ_o)
 
 
+@pytest.mark.parametrize("d2h", ["0", "1"])
 @pytest.mark.parametrize("offset,trim", [(1, 0), (4, 3), (0, 1)])
-def test_pinned_outputs_any_alignment_and_length(offset, trim):
-    """Results into views of pinned buffers: a 12-B offset (not 16-B aligned: the copy engine takes it), a 48-B
-    offset (the shader copy), and batch lengths whose result bytes are not a multiple of 16 (the copy kernel's
-    4-B tail)."""
+def test_pinned_outputs_any_alignment_and_length(monkeypatch, d2h, offset, trim):
+    """Results into views of pinned buffers, by the copy engine (SG_D2H=0, the default) or the shader copy
+    (SG_D2H=1): a 12-B offset (not 16-B aligned: the copy engine takes it either way), a 48-B offset, and batch
+    lengths whose result bytes are not a multiple of 16 (the copy kernel's 4-B tail)."""
+    monkeypatch.setenv("SG_D2H", d2h)
     wl, eng, ora = _setup(seed=35)
     reqs = [wl.requests(b)[: 100_000 - trim - b] for b in range(4)]
     bufs = [eng.host_array(len(r) + offset, abi.RES_DTYPE) for r in reqs]

@@ -263,3 +263,185 @@ def test_rejected_shard_batch_keeps_replicas_equal():
                 compared += n
             off += n
     assert compared > 0
+
+
+def _shard_engines(world, rules, ns, max_batch=1 << 16):
+    from sentinel_amd.engine import FlowEngine
+    shards = [shard_flows(N_FLOWS, r, world) for r in range(world)]
+    local = []
+    for s in shards:
+        m = np.full(N_FLOWS, abi.KEY_NO_RULE, np.int64)
+        m[s] = np.arange(len(s))
+        local.append(m)
+    engs = []
+    for r in range(world):
+        e = FlowEngine(device=0, max_batch=max_batch)
+        e.set_shard(r, world)
+        e.set_namespaces(ns)
+        e.load_rules(rules[shards[r]])
+        engs.append(e)
+    return shards, local, engs
+
+
+@pytest.mark.parametrize("path", ["enqueue", "submit"])
+def test_sharded_limiter_pipelined_equals_node_replay(path):
+    """The exchange on the pipelined entry points: per node batch every shard counts, the node gathers, and every
+    shard arms its next sg_flow_enqueue (device batches) / sg_flow_submit (pinned host batches) and goes on without
+    waiting — batches of one shard overlap (front half beside the previous walkers), each armed with its own
+    exchange. Every result equals one oracle replay of the merged batches in node order."""
+    from oracle.binding import ClusterTokenService
+    world = 2
+    rng = np.random.default_rng(91 if path == "enqueue" else 92)
+    rules = _rules(rng)
+    ns = _ns(60.0)
+    shards, local, engs = _shard_engines(world, rules, ns)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(rules)
+    dev = torch.device("cuda:0")
+    n_lim = int(ns["limiter_enabled"].sum())
+    pending = []  # (tickets per shard, outputs per shard, wanted results per shard)
+    keep = []
+    batches = _batches(rng, 1_700_000_000_101) + _batches(rng, 1_700_000_020_000)
+    for req in batches:
+        parts = _split(req, world, local)
+        ts = [p[1]["ts_ms"] for p in parts]
+        t_base = min(int(t[0]) for t in ts if len(t))
+        n_ms = max(int(t[-1]) for t in ts if len(t)) - t_base + 1
+        reqs_d = [torch.from_numpy(p[1].view(np.uint8).copy()).to(dev) for p in parts]
+        counts = []
+        for r in range(world):
+            c = torch.zeros(n_lim * n_ms, dtype=torch.int32, device=dev)
+            engs[r].lim_arrivals(reqs_d[r].data_ptr() if len(parts[r][1]) else 0, len(parts[r][1]), t_base, n_ms,
+                                 c.data_ptr())
+            counts.append(c)
+        gathered = torch.cat(counts)
+        torch.cuda.synchronize()
+        tickets, outs = [], []
+        for r in range(world):
+            n = len(parts[r][1])
+            engs[r].lim_exchange(gathered.data_ptr(), t_base, n_ms)
+            if path == "enqueue":
+                out = torch.zeros(max(1, n) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+                tickets.append(engs[r].enqueue_device(reqs_d[r].data_ptr() if n else 0, n, out.data_ptr()))
+            else:
+                hin = engs[r].host_array(max(1, n), abi.REQ_DTYPE)
+                out = engs[r].host_array(max(1, n), abi.RES_DTYPE)
+                hin[:n] = parts[r][1]
+                tickets.append(engs[r].submit(hin[:n], out[:n]))
+                keep.append((engs[r], hin))
+            outs.append(out)
+        del gathered  # the pipelined calls copied it
+        cat_idx = np.concatenate([p[0] for p in parts])
+        perm = node_order(ts)
+        want_node = ora.decide(req[cat_idx[perm]])
+        want = np.empty_like(want_node)
+        want[perm] = want_node
+        wants, off = [], 0
+        for r in range(world):
+            n = len(parts[r][1])
+            wants.append(want[off:off + n])
+            off += n
+        pending.append((tickets, outs, wants))
+    saw_tmr = False
+    for b, (tickets, outs, wants) in enumerate(pending):
+        for r in range(world):
+            if tickets[r]:
+                engs[r].wait(tickets[r])
+            n = len(wants[r])
+            got = outs[r].cpu().numpy().view(abi.RES_DTYPE)[:n] if path == "enqueue" else outs[r][:n]
+            bad = np.nonzero(got != wants[r])[0]
+            assert len(bad) == 0, f"batch {b} shard {r}: {len(bad)} of {n} differ"
+            saw_tmr |= bool((wants[r]["status"] == abi.TOO_MANY_REQUEST).any())
+    assert saw_tmr
+    for e, a in keep:
+        e.free_host(a)
+
+
+def test_sharded_limiter_cluster_param_equals_node_replay():
+    """Cluster param tokens share the namespace limiter (ClusterParamFlowChecker.java:43-45): param rules sharded
+    over the shards by rule, sg_lim_arrivals_param counts each shard's param requests, the node gathers them and
+    every shard's sg_cparam_decide_batch consumes the exchange. Results equal the oracle's decide_param over the
+    merged batch in node order, batch after batch, including a shard without requests."""
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.engine import FlowEngine
+    world = 3
+    rng = np.random.default_rng(93)
+    R = 24
+    prules = np.zeros(R, abi.CPARAM_RULE_DTYPE)
+    prules["flow_id"] = np.arange(R) * 5 + 3
+    prules["count"] = rng.integers(5, 60, R)
+    prules["threshold_type"] = abi.THRESHOLD_GLOBAL
+    prules["sample_count"], prules["window_interval_ms"] = 10, 1000
+    prules["namespace_id"] = rng.integers(0, 3, R)
+    ns = _ns(150.0)
+    owner = np.arange(R) % world                 # rule r lives on shard r % world
+    local = np.zeros(R, np.int64)
+    engs = []
+    for s in range(world):
+        mine = np.nonzero(owner == s)[0]
+        local[mine] = np.arange(len(mine))
+        e = FlowEngine(device=0, max_batch=1 << 16)
+        e.set_shard(s, world)
+        e.set_namespaces(ns)
+        e.cparam_load_rules(prules[mine], None, 12)
+        engs.append(e)
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_param_rules(prules)
+    dev = torch.device("cuda:0")
+    n_lim = int(ns["limiter_enabled"].sum())
+    t = 1_700_000_000_000
+    saw_tmr = False
+    for b in range(4):
+        n = int(rng.integers(8_000, 20_000))
+        req = np.zeros(n, abi.CPARAM_REQ_DTYPE)
+        req["ts_ms"] = t + np.sort(rng.integers(0, int(rng.integers(100, 1500)), n))
+        req["key"] = rng.integers(0, R, n) if b != 2 else rng.choice([0, 3], n)  # batch 2: shards 1, 2 get nothing
+        req["acquire"] = rng.integers(1, 3, n)
+        cnt = np.where(rng.random(n) < 0.2, rng.integers(2, 4, n), 1).astype(np.uint32)
+        req["value_count"] = cnt
+        req["value_begin"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint32)
+        values = (rng.zipf(1.3, int(cnt.sum())) % 500).astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        req["acquire"][rng.random(n) < 0.01] = 0  # BAD_REQUEST: not a tryPass
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, 700))
+        parts = []
+        for s in range(world):
+            idx = np.nonzero(owner[req["key"]] == s)[0]
+            sub = req[idx].copy()
+            sub["key"] = local[req["key"][idx]].astype(np.uint32)
+            vb = np.concatenate([[0], np.cumsum(sub["value_count"])[:-1]]).astype(np.uint32)
+            vals = np.concatenate([values[q["value_begin"]:q["value_begin"] + q["value_count"]] for q in req[idx]]) \
+                if len(idx) else np.zeros(0, np.uint64)
+            sub["value_begin"] = vb
+            parts.append((idx, sub, vals.astype(np.uint64)))
+        ts = [p[1]["ts_ms"] for p in parts]
+        t_base = min(int(x[0]) for x in ts if len(x))
+        n_ms = max(int(x[-1]) for x in ts if len(x)) - t_base + 1
+        reqs_d = [torch.from_numpy(p[1].view(np.uint8).copy()).to(dev) for p in parts]
+        counts = []
+        for s in range(world):
+            c = torch.zeros(n_lim * n_ms, dtype=torch.int32, device=dev)
+            engs[s].lim_arrivals_param(reqs_d[s].data_ptr() if len(parts[s][1]) else 0, len(parts[s][1]), t_base, n_ms,
+                                       c.data_ptr())
+            counts.append(c)
+        gathered = torch.cat(counts)
+        torch.cuda.synchronize()
+        got = []
+        for s in range(world):
+            engs[s].lim_exchange(gathered.data_ptr(), t_base, n_ms)
+            got.append(engs[s].cparam_decide_host(parts[s][1], parts[s][2]))
+        cat_idx = np.concatenate([p[0] for p in parts])
+        perm = node_order(ts)
+        node = req[cat_idx[perm]]
+        want_node = ora.decide_param(node, values)   # value_begin still indexes the node's value array
+        want = np.empty_like(want_node)
+        want[perm] = want_node
+        off = 0
+        for s in range(world):
+            k = len(parts[s][1])
+            bad = np.nonzero(got[s] != want[off:off + k])[0]
+            assert len(bad) == 0, f"batch {b} shard {s}: {len(bad)} of {k} differ"
+            off += k
+        saw_tmr |= bool((want["status"] == abi.TOO_MANY_REQUEST).any())
+    assert saw_tmr
