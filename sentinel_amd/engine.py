@@ -166,9 +166,9 @@ class FlowEngine:
         self._check(self._L.sg_set_namespaces(self.h, abi.ptr(ns), len(ns)))
 
     def set_shard(self, rank: int, world: int):
-        """This handle decides shard `rank` of `world`. With world > 1 and a namespace QPS limiter every
-        decide_device / decide_host must follow lim_arrivals + lim_exchange (cluster.LimiterExchange); the
-        pipelined submit / enqueue entry points and cluster param batches refuse such a handle."""
+        """This handle decides shard `rank` of `world`. With world > 1 and a namespace QPS limiter every flow
+        batch (decide_device / decide_host / enqueue_device / submit) must follow lim_arrivals + lim_exchange, and
+        every cluster param batch lim_arrivals_param + lim_exchange (cluster.LimiterExchange)."""
         self._check(self._L.sg_set_shard(self.h, rank, world))
         self._world = world
 
