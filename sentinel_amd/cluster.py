@@ -128,16 +128,17 @@ class LimiterExchange:
             return None
         return lo, hi - lo + 1
 
-    def arm(self, req_ptr: int, n: int, t_first, t_last, stream_ptr: int = 0):
-        """Count, exchange and arm for this rank's batch (device records at req_ptr). Every rank calls this for
-        every node batch, with n = 0 when it has no requests; the caller then decides its batch (n may be 0)."""
+    def arm(self, req_ptr: int, n: int, t_first, t_last, stream_ptr: int = 0, param: bool = False):
+        """Count, exchange and arm for this rank's batch (device records at req_ptr: sg_req, or sg_cparam_req with
+        param=True). Every rank calls this for every node batch, with n = 0 when it has no requests; the caller
+        then decides its batch (n may be 0) on any flow entry point, or sg_cparam_decide_batch for param=True."""
         rng = self.time_range(t_first, t_last)
         if rng is None:
             rng = (0, 1)  # no requests anywhere: nothing to count, the windows see no tryPass
         t_base, n_ms = rng
         mine = torch.zeros(max(1, self.n_lim * n_ms), dtype=torch.int32, device=self.device)
-        self.eng.lim_arrivals(req_ptr if n else 0, n, t_base, n_ms, mine.data_ptr(), stream_ptr,
-                              counts_words=self.n_lim * n_ms)
+        count = self.eng.lim_arrivals_param if param else self.eng.lim_arrivals
+        count(req_ptr if n else 0, n, t_base, n_ms, mine.data_ptr(), stream_ptr, counts_words=self.n_lim * n_ms)
         if self.world > 1:
             parts = [torch.zeros_like(mine, device=self.coll) for _ in range(self.world)]
             dist.all_gather(parts, mine.to(self.coll), group=self.group)
