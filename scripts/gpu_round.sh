@@ -28,6 +28,7 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
   # HBM traffic: one counter per pass (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2)
   step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
   step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
-  step pmc_summary 60 python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_summary.json
+  step pmc_size 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum -d gpurun_out/pmc_size -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
+  step pmc_summary 60 python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_summary.json gpurun_out/pmc_size
 fi
 echo done
