@@ -262,6 +262,8 @@ struct sg_handle {
     FlowWs pws{};
     uint32_t pws_segcap = 0;
     hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
+    hipStream_t s_xcopy = nullptr;    // the sharded limiter exchange's copy into a pipeline workspace
+    hipEvent_t xcopy_done = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
     uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
     bool d2h_kernel = false;          // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=1; the
@@ -518,8 +520,9 @@ void sg_destroy(sg_handle* h) {
         dfree(w.skips);
         dfree(w.skip_count);
         dfree(w.seg_end);
-        for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2})
+        for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2, &h->s_xcopy})
             if (*st) (void)hipStreamDestroy(*st);
+        if (h->xcopy_done) (void)hipEventDestroy(h->xcopy_done);
         for (int x = 0; x < 2; ++x) {
             if (h->front_done[x]) (void)hipEventDestroy(h->front_done[x]);
             if (h->back_done[x]) (void)hipEventDestroy(h->back_done[x]);
@@ -1264,7 +1267,15 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
         } else if (h->pipe_seq >= 2) {
             HIP_TRY(h, hipEventSynchronize(h->front_done[x]));
         }
-        HIP_TRY(h, hipMemcpy(h->d_xg_ws[x], h->lim_xg, 4 * words, hipMemcpyDeviceToDevice));
+        // complete before returning (the caller may free or refill its buffer then): a device-to-device hipMemcpy
+        // may return before the copy has run, and the front half on s_front could read a half-copied exchange
+        if (!h->s_xcopy) {
+            HIP_TRY(h, hipStreamCreateWithFlags(&h->s_xcopy, hipStreamNonBlocking));
+            HIP_TRY(h, hipEventCreateWithFlags(&h->xcopy_done, hipEventDisableTiming));
+        }
+        HIP_TRY(h, hipMemcpyAsync(h->d_xg_ws[x], h->lim_xg, 4 * words, hipMemcpyDeviceToDevice, h->s_xcopy));
+        HIP_TRY(h, hipEventRecord(h->xcopy_done, h->s_xcopy));
+        HIP_TRY(h, hipEventSynchronize(h->xcopy_done));
     }
     BatchArgs a = flow_args(h, w, req, n, out);
     if (after) HIP_TRY(h, hipStreamWaitEvent(h->s_front, after, 0));

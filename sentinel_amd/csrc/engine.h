@@ -37,12 +37,19 @@ struct alignas(16) Occ {
     int64_t pass_req;
 };
 
+#ifndef SG_SORT_ROUNDS
+#define SG_SORT_ROUNDS 16
+#endif
+constexpr int kSortRounds = SG_SORT_ROUNDS;  // records per thread of a sort tile (256 threads): 4096-record tiles
 constexpr int kMaxWl = 8;                 // distinct window lengths per handle
 constexpr uint32_t kMaxPeriods = 1u << 16; // window periods a single batch may span per window length
 constexpr int kShortMax = 256;            // default: segments longer than this are walked by a whole wave
 constexpr int kLdsBnd = 4096;             // period-table entries the walk kernel stages in LDS
 constexpr int kLdsBndFlow = 1024;         // the same for the cluster flow walkers (LDS budget of the short walker)
-constexpr int kRecW = 32;                 // records per lane the short walker stages in LDS at a time
+#ifndef SG_RECW
+#define SG_RECW 32
+#endif
+constexpr int kRecW = SG_RECW;            // records per lane the short walker stages in LDS at a time
 // Short segments are grouped by length class (length <= 4, 16, 64, 256, 1024, more) so that the 64 lanes
 // of a short-walker wave walk segments of similar length.
 constexpr int kClasses = 6;

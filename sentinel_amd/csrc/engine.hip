@@ -104,7 +104,7 @@ __device__ __forceinline__ Decoded decode_c(const BatchArgs& a, uint32_t c) {
 
 // One block per 4096-request tile (the radix sort's tile). With a.hist0 set the block also counts the
 // first sort pass's digits of its records (the sort then skips that histogram read).
-constexpr int kPrepItems = 16;
+constexpr int kPrepItems = kSortRounds;  // k_prep's tile is the sort's (its first-pass histogram rows)
 constexpr uint32_t kPrepTile = 256 * kPrepItems;
 
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
@@ -1151,10 +1151,12 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
 
     if (act) {
         if (I >= 0) store_bucket(ring + I, ws, ps.cur);
-        Occ o;
-        o.pass = ps.occ_pass;
-        o.pass_req = ps.occ_req;
-        a.occ[k] = o;
+        if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
+            Occ o;
+            o.pass = ps.occ_pass;
+            o.pass_req = ps.occ_req;
+            a.occ[k] = o;
+        }
     }
 }
 
@@ -1306,10 +1308,12 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
     }
     if (act) {
         if (I >= 0) store_bucket(ring + I, ws, ps.cur);
-        Occ o;
-        o.pass = ps.occ_pass;
-        o.pass_req = ps.occ_req;
-        a.occ[k] = o;
+        if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
+            Occ o;
+            o.pass = ps.occ_pass;
+            o.pass_req = ps.occ_req;
+            a.occ[k] = o;
+        }
     }
 }
 
@@ -1552,7 +1556,10 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
 }
 
 template <int SM, bool C>
-__global__ void __launch_bounds__(256, C ? 2 : kShortBlocksPerCu) k_walk_short(BatchArgs a) {
+#ifndef SG_SHORT_C_BLOCKS
+#define SG_SHORT_C_BLOCKS 2
+#endif
+__global__ void __launch_bounds__(256, C ? SG_SHORT_C_BLOCKS : kShortBlocksPerCu) k_walk_short(BatchArgs a) {
     static_assert(SM <= kGatherMaxS, "LDS budget of the ring snapshot");
     __shared__ SlotSnap snap_all[4 * (SM > 0 ? 64 * SM : 1)];
     __shared__ uint32_t recs_all[SM > 0 && C ? 4 * kRecW * 64 : 1];
@@ -1666,10 +1673,12 @@ __device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
             }
         }
         if (I >= 0) store_bucket(ring + I, ws, ps.cur);
-        Occ o;
-        o.pass = ps.occ_pass;
-        o.pass_req = ps.occ_req;
-        a.occ[k] = o;
+        if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
+            Occ o;
+            o.pass = ps.occ_pass;
+            o.pass_req = ps.occ_req;
+            a.occ[k] = o;
+        }
     }
 }
 
@@ -1794,6 +1803,7 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
     if (g > cap) g = cap;
     return (unsigned)g;
 }
+
 
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_prep, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
