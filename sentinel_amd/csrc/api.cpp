@@ -122,6 +122,9 @@ struct sg_handle {
     uint32_t* d_cp_hist = nullptr;
     uint64_t cp_val_cap = 0;
     CPBucket* d_cp_save = nullptr;
+    uint2* d_cp_skips = nullptr;      // saturated ranges of the hot-slot walker (k_cp_skipfill), [cp_skip_cap]
+    uint32_t* d_cp_skip_count = nullptr;
+    uint64_t cp_skip_cap = 0;
     uint64_t cp_save_cap = 0;
     int* d_cp_changed = nullptr;
     uint8_t* d_cp_rule_lim = nullptr; // [cparam rules] limiter slot of the rule's namespace (0xFF none)
@@ -607,6 +610,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_rec2);
     dfree(h->d_cp_hist);
     dfree(h->d_cp_save);
+    dfree(h->d_cp_skips);
+    dfree(h->d_cp_skip_count);
     dfree(h->d_cp_changed);
     dfree(h->d_cp_rule_lim);
     dfree(h->d_cnow);
@@ -1049,11 +1054,13 @@ int pipe_setup(sg_handle* h) {
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device);
         int k8 = h->front_eighths;
         if (const char* e = std::getenv("SG_FRONT_EIGHTHS")) k8 = std::atoi(e);
+        // env SG_CU_BLOCKED=1 (tuning): the front half gets CUs i with i / (cus / 8) < k (contiguous eighths)
+        const bool blocked = std::getenv("SG_CU_BLOCKED") && std::atoi(std::getenv("SG_CU_BLOCKED")) == 1;
         if (k8 > 0 && k8 < 8 && cus >= 8) {
             std::vector<uint32_t> fm((cus + 31) / 32, 0u), bm((cus + 31) / 32, 0u);
             int nb = 0;
             for (int i = 0; i < cus; ++i) {
-                if (i % 8 < k8) fm[i / 32] |= 1u << (i % 32);
+                if ((blocked ? i / (cus / 8) : i % 8) < k8) fm[i / 32] |= 1u << (i % 32);
                 else {
                     bm[i / 32] |= 1u << (i % 32);
                     ++nb;
@@ -2248,17 +2255,33 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         }
         b.save = h->d_cp_save;  // the first walk saves the touched rings, re-walks restore the dirty ones
     }
+    // saturated ranges of hot slots (pieces of <= 4096 records, each >= 256: at most 2 nv / 256 + 1)
+    {
+        const uint64_t cap = 2 * nv / 256 + 1;
+        if (cap > h->cp_skip_cap) {
+            dfree(h->d_cp_skips);
+            if (hipMalloc(&h->d_cp_skips, sizeof(uint2) * cap) != hipSuccess ||
+                (!h->d_cp_skip_count && hipMalloc(&h->d_cp_skip_count, sizeof(uint32_t)) != hipSuccess))
+                return fail(h, SG_E_NOMEM, "cparam skip list");
+            h->cp_skip_cap = cap;
+        }
+        b.skips = h->d_cp_skips;
+        b.skip_count = h->d_cp_skip_count;
+        b.skip_cap = (uint32_t)cap;
+    }
     // rounds: walk every slot under the assumed multi-value outcomes, then recompute the outcomes
     const uint32_t kMaxRounds = h->cp_max_rounds;
     uint32_t round = 0;
     bool converged = false;
     if (!err && !has_multi) {  // single-value requests only: the slots are independent, one walk is exact
+        HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), stream));
         HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
         converged = true;
     }
     while (!err && !converged && round < kMaxRounds) {
         b.round = (int)round;
         HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
+        HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), stream));
         HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
         HIP_TRY(h, launch_cp_combine(c, b, stream));
         int changed = 0;

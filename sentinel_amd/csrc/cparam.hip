@@ -456,18 +456,28 @@ __device__ __forceinline__ int64_t cp_wave_sum(int64_t v) {
 }
 
 enum : int { kCpSkip = 0, kCpSingle = 1, kCpMulti = 2, kCpDup = 3 };
+__device__ __forceinline__ uint64_t cp_below(int f) { return f >= 64 ? ~0ull : ((1ull << f) - 1ull); }
 constexpr int kCpU = 4;  // 64-record chunks whose loads are issued together (three dependent round trips per block)
+constexpr uint64_t kCpSkipMin = 256;     // shortest saturated tail worth handing to k_cp_skipfill (records)
+constexpr uint64_t kCpSkipPiece = 4096;  // skipped ranges go to k_cp_skipfill in pieces of this size
 
 // One wave per slot of more than short_max records (a hot (rule, value)), 64 records per step with the ring in
 // registers (lane x < S holds bucket x). Within one window period the state is the running count `cur`; every
 // record's check is thr - (other + cur_before) / intervalSec - acquire >= 0, monotone in cur_before. A step
 // assumes every unresolved record adds what it would add on passing — a single-value request its count, a
-// multi-value request's first record here its count iff the request is assumed to pass — takes the exclusive scan
-// of the adds, and commits the lanes up to the first such record whose check fails (that one adds nothing);
-// records that fail even at the committed state are blocked at once (cur only grows). A repeated value of a
-// multi-value request (adjacent record, same owner) adds its count iff the request is assumed to pass. Records,
-// owners and requests of kCpU chunks are loaded together. A saturated period resolves in two steps per 64
-// records, an open one in one.
+// multi-value request's first record here its count for each of its records in the chunk iff the request is
+// assumed to pass — takes the exclusive scan of the adds, and commits the lanes up to the first such record whose
+// check fails (that one adds nothing); records that fail even at the committed state are blocked at once (cur only
+// grows). A repeated value of a multi-value request (adjacent record, same owner) carries check 1 and adds only
+// through its first record (as cp_walk_serial: the request's count per record iff it is assumed to pass and this
+// slot's check passed), or, when the chunk starts inside the request's run, iff that first record passed.
+// Records, owners and requests of kCpU chunks are loaded together.
+//
+// Saturated periods: once not even acquireCount = 1 fits the window (every valid request has acquireCount >= 1,
+// and cur only grows within the period), every later record of the period fails its check and adds nothing — a
+// single-value request is BLOCKED, a multi-value request's first record checks 0. The wave finds where the period
+// ends (64-way search on the requests' timestamps), hands the range to k_cp_skipfill and goes on there: a hot
+// slot costs a few steps per window period instead of one or two per 64 records.
 __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
     const int lane = (int)__lane_id();
@@ -498,7 +508,9 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
         }
         int64_t P = INT64_MIN, other = 0, cur = 0;
         uint32_t carry = kNoOwner;  // owner of the record before the current chunk
-        for (uint64_t blk = s; blk < e; blk += 64ull * kCpU) {
+        bool carry_ok = false;      // that owner is a multi-value request whose first record here passed its check
+        uint64_t blk = s;
+        while (blk < e) {
             // loads of kCpU chunks at once; indices clamped to the segment (unconditional loads)
             uint64_t rc[kCpU];
             uint32_t ow[kCpU];
@@ -519,6 +531,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 st[u] = b.lim ? c.out[ow[u]].status : 0;
                 as[u] = b.assume[ow[u]];
             }
+            uint64_t next = blk + 64ull * kCpU;
 #pragma unroll
             for (int u = 0; u < kCpU; ++u) {
                 const uint64_t base = blk + (uint64_t)u * 64;
@@ -531,23 +544,31 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 if (lane == 0) prev = carry;
                 carry = (uint32_t)__shfl((int)i, 63, 64);
                 int typ = kCpSkip;
-                int64_t acq = 0, Pq = 0, add = 0;
+                int64_t acq = 0, Pq = 0;
                 if (act && !(b.lim && st[u] == SG_STATUS_TOO_MANY_REQUEST)) {
                     acq = aq[u];
                     Pq = ts[u] / wl;
-                    if (vc[u] == 1) {
-                        typ = kCpSingle;
-                        add = acq;
-                    } else {
-                        typ = prev == i ? kCpDup : kCpMulti;
-                        add = as[u] ? acq : 0;
-                        if (typ == kCpDup) b.chk[p] = 1;  // the request's first record here carries the check
-                    }
+                    typ = vc[u] == 1 ? kCpSingle : prev == i ? kCpDup : kCpMulti;
+                }
+                // a request's records in this slot are adjacent: a repeated value's first record is the nearest
+                // non-repeated lane below it, or (none in the chunk) the carried owner's
+                const uint64_t nondup = __ballot(typ != kCpDup);
+                int64_t add = 0;
+                if (typ == kCpSingle) {
+                    add = acq;
+                } else if (typ == kCpMulti) {
+                    const uint64_t after = nondup & ~cp_below(lane + 1);
+                    const int nxt = after ? __builtin_ctzll(after) : 64;
+                    add = as[u] ? acq * (int64_t)(nxt - lane) : 0;  // this record and its repeats in the chunk
+                } else if (typ == kCpDup) {
+                    add = ((nondup & cp_below(lane)) == 0 && carry_ok && as[u]) ? acq : 0;
+                    b.chk[p] = 1;  // the request's first record here carries the check
                 }
                 // lanes whose own check decides their add (a failing check adds nothing)
                 const bool cut_kind = typ == kCpSingle || (typ == kCpMulti && add != 0);
                 uint64_t pending = __ballot(typ != kCpSkip);
                 uint64_t failed = 0;
+                bool okv = false;  // this lane's check passed (multi-value first records: carry_ok of the next chunk)
                 while (pending) {
                     const int f = __builtin_ctzll(pending);
                     const int64_t Pf = __shfl((long long)Pq, f, 64);
@@ -588,6 +609,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                             adv = cp_wave_sum(a);
                         }
                         if ((done >> lane) & 1ull) {
+                            okv = ok;
                             if (typ == kCpSingle) {
                                 if (ok) cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
                                 else cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
@@ -603,7 +625,42 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                         }
                     }
                 }
+                // the next chunk's carried request: lane 63's, whose first record is the highest non-repeated lane
+                {
+                    const int t63 = __shfl(typ, 63, 64);
+                    if (t63 == kCpMulti || t63 == kCpDup) {
+                        if (nondup) carry_ok = __shfl((int)okv, 63 - __builtin_clzll(nondup), 64) != 0;
+                    } else {
+                        carry_ok = false;
+                    }
+                }
+                // saturated period: hand the rest of it to k_cp_skipfill (not while a passed multi-value request's
+                // repeated values may still follow: they add)
+                const uint64_t pos = base + 64;
+                if (pos < e && P != INT64_MIN && !carry_ok && b.skips &&
+                    thr - (double)(other + cur) / r.isec - 1.0 < 0) {
+                    const int64_t Pc = P;
+                    const uint64_t pe = cp_wave_search(pos, e, [&](uint64_t q) {
+                        return c.req[b.owner[sg.rec_sorted[q] & b.pmask]].ts_ms / wl > Pc;
+                    }, lane);
+                    if (pe - pos >= kCpSkipMin) {
+                        const uint32_t np = (uint32_t)((pe - pos + kCpSkipPiece - 1) / kCpSkipPiece);
+                        uint32_t slot = 0;
+                        if (lane == 0) slot = atomicAdd(b.skip_count, np);
+                        slot = (uint32_t)__shfl((int)slot, 0, 64);
+                        if (slot + np <= b.skip_cap) {
+                            for (uint32_t pi = (uint32_t)lane; pi < np; pi += 64) {
+                                const uint64_t b0 = pos + (uint64_t)pi * kCpSkipPiece;
+                                b.skips[slot + pi] = make_uint2((uint32_t)b0, (uint32_t)min(pe, b0 + kCpSkipPiece));
+                            }
+                            carry = b.owner[sg.rec_sorted[pe - 1] & b.pmask];
+                            next = pe;
+                            break;
+                        }
+                    }
+                }
             }
+            blk = next;
         }
         if (P != INT64_MIN && lane == (int)(P % S)) {
             bst = P * wl;
@@ -614,6 +671,31 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
             bk.start = bst;
             bk.count = bcnt;
             ring[lane] = bk;
+        }
+    }
+}
+
+// The saturated ranges of k_cp_walk2_long (one wave per piece): every record fails its check and adds nothing — a
+// single-value request is BLOCKED, a multi-value request's first record in the slot checks 0, a repeated value
+// carries check 1.
+__global__ void __launch_bounds__(256) k_cp_skipfill(CPArgs c, CPBatch b, BatchArgs sg) {
+    if (*c.err) return;
+    const uint32_t cnt = min(*b.skip_count, b.skip_cap);
+    const int lane = (int)__lane_id();
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t w = wave; w < cnt; w += nwaves) {
+        const uint2 pc = b.skips[w];
+        for (uint64_t j = (uint64_t)pc.x + lane; j < pc.y; j += 64) {
+            const uint64_t p = sg.rec_sorted[j] & b.pmask;
+            const uint32_t i = b.owner[p];
+            if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
+            if (c.req[i].value_count == 1) {
+                cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+            } else {
+                const uint32_t prev = b.owner[sg.rec_sorted[j - 1] & b.pmask];  // j > the segment start
+                b.chk[p] = prev == i ? 1 : 0;
+            }
         }
     }
 }
@@ -731,6 +813,7 @@ hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& s
     const uint64_t waves = sg.n / ((uint64_t)sg.short_max + 1) + 1;  // bound on the long list's length
     hipLaunchKernelGGL(k_cp_walk2_long, dim3(cgrid2(waves * 64, 2048)), dim3(256), 0, stream, c, b, sg);
     hipLaunchKernelGGL(k_cp_walk2, dim3(cgrid2(sg.n, 4096)), dim3(256), 0, stream, c, b, sg);
+    if (b.skips) hipLaunchKernelGGL(k_cp_skipfill, dim3(1024), dim3(256), 0, stream, c, b, sg);
     return hipGetLastError();
 }
 

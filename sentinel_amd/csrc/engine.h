@@ -338,6 +338,9 @@ struct CPBatch {
     uint8_t* dirty;           // [total slots] slot must be re-walked (an assumed outcome in it changed)
     int round;                // 0: first walk (saves the rings); > 0: re-walk the dirty slots from the saves
     int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
+    uint2* skips;             // saturated ranges [x, y) of sorted records handed to k_cp_skipfill (null: no skipping)
+    uint32_t* skip_count;     // zeroed by the host before every walk
+    uint32_t skip_cap;
 };
 hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream);
 hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream);

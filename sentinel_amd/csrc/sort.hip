@@ -75,101 +75,105 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in,
 }
 
 // The per-tile histograms are stored tile-major (hist[t][d]: each tile writes and reads one contiguous row); the
-// scatter needs each (tile, digit) run's global start, the exclusive scan in (digit, tile) order. Three passes:
-// per-chunk column sums, one block scanning the chunks per digit and the digit totals, then each chunk rewrites
-// its rows in place as offsets. These kernels are latency-bound (a few MB): every load of a thread is issued
-// before any is used (indices clamped, values masked, no branch between the loads), so each pass costs one or
-// two memory round trips instead of one per tile / chunk — in the pipelined flow path they run beside the
-// walkers, whose traffic stretches each round trip to several µs (a per-tile loop took 120 µs there).
-constexpr uint32_t kChunkTiles = 32;
+// scatter needs each (tile, digit) run's global start, the exclusive scan in (digit, tile) order. In the pipelined
+// flow path these kernels run beside the previous batch's walkers, whose random traffic stretches every dependent
+// memory round trip to ~20-30 µs (measured: a 4-way longer chunk-scan chain took 4x as long there), so each kernel
+// issues all of a thread's loads at once and costs one load round trip:
+//   k_colsum    one thread per (chunk of kChunkTiles tiles, digit): the chunk's column sums;
+//   k_chunkscan 64 digits x 16 chunk groups per block: column-relative exclusive scan of the chunk sums in place,
+//               and each digit's total (tot[d]);
+//   k_rescan    one thread per (chunk, digit): each tile's run start (column-relative) written over its row;
+//   k_radix_scatter adds each digit's base, an exclusive scan of the totals it does in LDS.
+#ifndef SG_CHUNK_TILES
+#define SG_CHUNK_TILES 32
+#endif
+constexpr uint32_t kChunkTiles = SG_CHUNK_TILES;
+constexpr int kScanGroups = 16;  // chunk groups per digit in k_chunkscan
+constexpr int kScanLoads = 8;    // chunk sums per thread loaded at once (nchunks <= 128: 16M-record batches)
 
 template <int D>
-__global__ void __launch_bounds__(kSortThreads) k_colsum(const uint32_t* hist, uint32_t ntiles, uint32_t* csum) {
+__global__ void __launch_bounds__(1 << D) k_colsum(const uint32_t* hist, uint32_t ntiles, uint32_t* csum) {
     constexpr int kBins = 1 << D;
-    constexpr int kPer = kBins / kSortThreads;
     const uint32_t t0 = blockIdx.x * kChunkTiles, nt = min(kChunkTiles, ntiles - t0);
-    uint32_t v[kChunkTiles][kPer];
+    const int d = threadIdx.x;
+    uint32_t v[kChunkTiles];
 #pragma unroll
-    for (uint32_t u = 0; u < kChunkTiles; ++u)
+    for (uint32_t u = 0; u < kChunkTiles; ++u) v[u] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + d];
+    uint32_t acc = 0;
 #pragma unroll
-        for (int i = 0; i < kPer; ++i)
-            v[u][i] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + threadIdx.x + i * kSortThreads];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kChunkTiles; ++u) acc += u < nt ? v[u][i] : 0u;
-        csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads] = acc;
-    }
+    for (uint32_t u = 0; u < kChunkTiles; ++u) acc += u < nt ? v[u] : 0u;
+    csum[(size_t)blockIdx.x * kBins + d] = acc;
 }
 
-// One block of kBins threads (thread = digit): exclusive scan of the chunk sums per digit, plus the base of the
-// digit (exclusive scan of the digit totals), written back into csum as each chunk's starting offsets.
 template <int D>
-__global__ void __launch_bounds__(1024) k_chunkscan(uint32_t* csum, uint32_t nchunks) {
+__global__ void __launch_bounds__(1024) k_chunkscan(uint32_t* csum, uint32_t nchunks, uint32_t* tot) {
     constexpr int kBins = 1 << D;
-    __shared__ uint32_t wsum[kBins / 64];
-    const int d = threadIdx.x, lane = d & 63, wave = d >> 6;
-    constexpr uint32_t kB = 64;  // chunks loaded before any is stored (one round trip per kB chunks)
+    __shared__ uint32_t gs[kScanGroups][64];
+    const int dl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int d = blockIdx.x * 64 + dl;
+    const uint32_t G = (nchunks + kScanGroups - 1) / kScanGroups;  // chunks per group
+    const uint32_t c0 = grp * G, c1 = min(c0 + G, nchunks);
     const uint32_t last = nchunks - 1;
-    uint32_t run = 0;
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
-        uint32_t v[kB];
+    uint32_t v[kScanLoads];
+    uint32_t sum = 0;
+    for (uint32_t b0 = c0; b0 < c1; b0 += kScanLoads) {
 #pragma unroll
-        for (uint32_t u = 0; u < kB; ++u) v[u] = csum[(size_t)min(c0 + u, last) * kBins + d];
+        for (int u = 0; u < kScanLoads; ++u) v[u] = csum[(size_t)min(b0 + u, last) * kBins + d];
 #pragma unroll
-        for (uint32_t u = 0; u < kB; ++u) {
-            if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = run;
-            run += c0 + u < nchunks ? v[u] : 0u;
+        for (int u = 0; u < kScanLoads; ++u) sum += b0 + u < c1 ? v[u] : 0u;
+    }
+    gs[grp][dl] = sum;
+    __syncthreads();
+    if (grp == 0) {  // exclusive scan over the groups of digit d, and its total
+        uint32_t run = 0;
+#pragma unroll
+        for (int g = 0; g < kScanGroups; ++g) {
+            const uint32_t x = gs[g][dl];
+            gs[g][dl] = run;
+            run += x;
+        }
+        tot[d] = run;
+    }
+    __syncthreads();
+    uint32_t run = gs[grp][dl];
+    for (uint32_t b0 = c0; b0 < c1; b0 += kScanLoads) {
+        if (b0 != c0) {  // more than kScanLoads chunks per group (batches > 16M records): reload
+#pragma unroll
+            for (int u = 0; u < kScanLoads; ++u) v[u] = csum[(size_t)min(b0 + u, last) * kBins + d];
+        } else if (G > (uint32_t)kScanLoads) {
+#pragma unroll
+            for (int u = 0; u < kScanLoads; ++u) v[u] = csum[(size_t)min(b0 + u, last) * kBins + d];
+        }
+#pragma unroll
+        for (int u = 0; u < kScanLoads; ++u) {
+            if (b0 + u < c1) {
+                csum[(size_t)(b0 + u) * kBins + d] = run;
+                run += v[u];
+            }
         }
     }
-    uint32_t x = run;  // inclusive scan of the digit totals over the block
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t base = x - run;
-    for (int w = 0; w < wave; ++w) base += wsum[w];
-    for (uint32_t c0 = 0; c0 < nchunks; c0 += kB) {
-        uint32_t v[kB];
-#pragma unroll
-        for (uint32_t u = 0; u < kB; ++u) v[u] = csum[(size_t)min(c0 + u, last) * kBins + d];
-#pragma unroll
-        for (uint32_t u = 0; u < kB; ++u)
-            if (c0 + u < nchunks) csum[(size_t)(c0 + u) * kBins + d] = v[u] + base;
-    }
 }
 
 template <int D>
-__global__ void __launch_bounds__(kSortThreads) k_rescan(uint32_t* hist, const uint32_t* csum, uint32_t ntiles) {
+__global__ void __launch_bounds__(1 << D) k_rescan(uint32_t* hist, const uint32_t* csum, uint32_t ntiles) {
     constexpr int kBins = 1 << D;
-    constexpr int kPer = kBins / kSortThreads;
     const uint32_t t0 = blockIdx.x * kChunkTiles, nt = min(kChunkTiles, ntiles - t0);
-    uint32_t run[kPer];
+    const int d = threadIdx.x;
+    uint32_t run = csum[(size_t)blockIdx.x * kBins + d];
+    uint32_t v[kChunkTiles];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) run[i] = csum[(size_t)blockIdx.x * kBins + threadIdx.x + i * kSortThreads];
-    uint32_t v[kChunkTiles][kPer];
-#pragma unroll
-    for (uint32_t u = 0; u < kChunkTiles; ++u)
-#pragma unroll
-        for (int i = 0; i < kPer; ++i)
-            v[u][i] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + threadIdx.x + i * kSortThreads];
+    for (uint32_t u = 0; u < kChunkTiles; ++u) v[u] = hist[(size_t)(t0 + min(u, nt - 1)) * kBins + d];
 #pragma unroll
     for (uint32_t u = 0; u < kChunkTiles; ++u) {
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            if (u < nt) hist[(size_t)(t0 + u) * kBins + threadIdx.x + i * kSortThreads] = run[i];
-            run[i] += v[u][i];  // (past nt: unused)
-        }
+        if (u < nt) hist[(size_t)(t0 + u) * kBins + d] = run;
+        run += v[u];  // (past nt: unused)
     }
 }
 
 template <int D>
 __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* in, uint64_t* out, uint64_t n, int shift,
-                                                                const uint32_t* hist, uint32_t ntiles) {
+                                                                const uint32_t* hist, uint32_t ntiles,
+                                                                const uint32_t* tot) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;  // digits per thread
     using Cnt = typename std::conditional<(D > 8), uint16_t, uint32_t>::type;  // wave counts <= 1024
@@ -178,16 +182,31 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     __shared__ uint32_t dstart[kBins];       // tile-local start of each digit's run
     __shared__ uint32_t gbase[kBins];        // global start of each digit's run of this tile
     __shared__ uint32_t wtot[kSortWaves];
+    __shared__ uint32_t btot[kSortWaves];
     const uint32_t tile = xcd_tile(blockIdx.x, ntiles);
     if (tile >= ntiles) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t tv[kPer];  // totals of digits tid*kPer .. (k_chunkscan)
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) tv[i] = tot[tid * kPer + i];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
         const int d = tid + i * kSortThreads;
-        gbase[d] = hist[(size_t)tile * kBins + d];  // the tile's row of run offsets (k_rescan)
+        gbase[d] = hist[(size_t)tile * kBins + d];  // the tile's row of column-relative run offsets (k_rescan)
 #pragma unroll
         for (int w = 0; w < kSortWaves; ++w) wcnt[w][d] = 0;
     }
+    // digit bases: exclusive scan of the totals (digits tid*kPer .. contiguous per thread), added after the barrier
+    uint32_t bsum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) bsum += tv[i];
+    uint32_t bx = bsum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)bx, (unsigned)o, 64);
+        if (lane >= o) bx += y;
+    }
+    if (lane == 63) btot[wave] = bx;
     const uint64_t base = (uint64_t)tile * kTile;
     const uint64_t wbase = base + (uint64_t)wave * kWaveRecs;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -199,6 +218,15 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
         rec[r] = idx < n ? in[idx] : 0ull;
     }
     __syncthreads();
+    {
+        uint32_t b = bx - bsum;
+        for (int w = 0; w < wave; ++w) b += btot[w];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            gbase[tid * kPer + i] += b;
+            b += tv[i];
+        }
+    }
     // 1. rank within the wave (wave-private counters: LDS ops of one wave execute in order)
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
@@ -264,7 +292,7 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
 size_t radix_hist_words(uint64_t n) {
     const uint64_t ntiles = (n + kTile - 1) / kTile;
     const uint64_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
-    return (size_t)((ntiles + nchunks) * (1ull << kMaxDigit) + 64);
+    return (size_t)((ntiles + nchunks + 1) * (1ull << kMaxDigit) + 64);  // rows, chunk sums, digit totals
 }
 
 // Digit width of a sort over `bits` key bits: 8-bit digits, except 2 passes of 10 bits for 17..20 bits (one pass
@@ -278,13 +306,15 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     uint32_t* hist = hist_ws;                                   // [ntiles][bins], then run offsets in place
     uint32_t* csum = hist_ws + (size_t)ntiles * (1u << D);       // [nchunks][bins]
+    uint32_t* tot = csum + (size_t)nchunks * (1u << D);          // [bins]
     if (!hist_ready)
         hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
-    hipLaunchKernelGGL(k_colsum<D>, dim3(nchunks), dim3(kSortThreads), 0, stream, hist, ntiles, csum);
-    hipLaunchKernelGGL(k_chunkscan<D>, dim3(1), dim3(1u << D), 0, stream, csum, nchunks);
-    hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(kSortThreads), 0, stream, hist, csum, ntiles);
+    hipLaunchKernelGGL(k_colsum<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, ntiles, csum);
+    hipLaunchKernelGGL(k_chunkscan<D>, dim3((1u << D) / 64), dim3(1024), 0, stream, csum, nchunks, tot);
+    hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, csum, ntiles);
     const uint32_t grid = 8 * ((ntiles + 7) / 8);  // xcd_tile: blocks past ntiles return at once
-    hipLaunchKernelGGL(k_radix_scatter<D>, dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, ntiles);
+    hipLaunchKernelGGL(k_radix_scatter<D>, dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, ntiles,
+                       tot);
 }
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),
