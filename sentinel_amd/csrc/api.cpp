@@ -113,8 +113,11 @@ struct sg_handle {
     uint32_t* d_cp_long = nullptr;    // segment lists over the value records (capacity cp_val_cap)
     uint32_t* d_cp_short = nullptr;
     uint64_t cp_class_off[kClasses]{};
-    uint8_t* d_cp_dirty = nullptr;    // [cptotal] re-walk flags, kept all-zero between batches
-    uint64_t cp_dirty_cap = 0;
+    uint32_t* d_cp_slot_item = nullptr;  // [cptotal] work item of each touched slot (k_cp_items)
+    uint64_t cp_slot_item_cap = 0;
+    uint32_t* d_cp_items = nullptr;   // [4 * cp_val_cap] per work item: re-walk flag, segment start; re-walk lists x2
+    uint32_t* d_cp_counts = nullptr;  // [6]: re-walk list counts (2 buffers x {long, short}), multi-value count
+    uint32_t* d_cp_mlist = nullptr;   // [max_batch] multi-value requests
     uint8_t* d_cp_chk = nullptr;
     uint8_t* d_cp_assume = nullptr;
     uint64_t* d_cp_rec = nullptr;
@@ -603,7 +606,10 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_pslot);
     dfree(h->d_cp_long);
     dfree(h->d_cp_short);
-    dfree(h->d_cp_dirty);
+    dfree(h->d_cp_slot_item);
+    dfree(h->d_cp_items);
+    dfree(h->d_cp_counts);
+    dfree(h->d_cp_mlist);
     dfree(h->d_cp_chk);
     dfree(h->d_cp_assume);
     dfree(h->d_cp_rec);
@@ -2125,7 +2131,9 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         dfree(h->d_cp_rec);
         dfree(h->d_cp_rec2);
         dfree(h->d_cp_hist);
-        if (hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
+        dfree(h->d_cp_items);
+        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 6 * nv) != hipSuccess ||
+            hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_pslot, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_hist, sizeof(uint32_t) * radix_hist_words(nv)) != hipSuccess)
@@ -2140,12 +2148,15 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
             return fail(h, SG_E_NOMEM, "cparam segment lists");
         h->cp_val_cap = nv;
     }
-    if (h->cptotal > h->cp_dirty_cap) {
-        dfree(h->d_cp_dirty);
-        if (hipMalloc(&h->d_cp_dirty, h->cptotal) != hipSuccess) return fail(h, SG_E_NOMEM, "cparam re-walk flags");
-        HIP_TRY(h, hipMemsetAsync(h->d_cp_dirty, 0, h->cptotal, stream));
-        h->cp_dirty_cap = h->cptotal;
+    if (h->cptotal > h->cp_slot_item_cap) {
+        dfree(h->d_cp_slot_item);
+        if (hipMalloc(&h->d_cp_slot_item, sizeof(uint32_t) * h->cptotal) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "cparam slot items");
+        h->cp_slot_item_cap = h->cptotal;
     }
+    if (!h->d_cp_counts && (hipMalloc(&h->d_cp_counts, 8 * sizeof(uint32_t)) != hipSuccess ||
+                            hipMalloc(&h->d_cp_mlist, sizeof(uint32_t) * h->cfg.max_batch) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "cparam batch scratch");
     if (!h->d_cp_assume && (hipMalloc(&h->d_cp_assume, h->cfg.max_batch) != hipSuccess ||
                             hipMalloc(&h->d_cp_changed, sizeof(int)) != hipSuccess))
         return fail(h, SG_E_NOMEM, "cparam batch scratch");
@@ -2163,10 +2174,16 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     b.pmask = (1ull << pbits) - 1;
     b.changed = h->d_cp_changed;
     b.pslot = h->d_cp_pslot;
-    b.dirty = h->d_cp_dirty;
+    b.dflag = h->d_cp_items;                      // [nv] (items <= value positions)
+    b.item_start = h->d_cp_items + nv;           // [nv]
+    b.slot_item = h->d_cp_slot_item;
+    b.dcap = (uint32_t)nv;                       // re-walk lists: 2 buffers x {long, short} x nv
+    b.mlist = h->d_cp_mlist;
+    b.mcount = h->d_cp_counts + 4;
     b.lim = any_lim ? 1 : 0;
     HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
-    HIP_TRY(h, launch_cp_prep2(c, b, stream));  // sets *changed iff a request has several values
+    HIP_TRY(h, hipMemsetAsync(b.mcount, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_cp_prep2(c, b, stream));  // sets *changed iff a request has several values, lists them
     if (n_values == 0) {  // every request is BAD_REQUEST, NO_RULE_EXISTS or out of bounds (none reaches the limiter)
         HIP_TRY(h, launch_cp_finish_batch(c, stream));
         int err = 0;
@@ -2247,6 +2264,10 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     uint64_t touched = 0;
     for (uint32_t x : counts) touched += x;
     if (!err && has_multi && touched > 0) {
+        // work items: re-walk flags clear, segment starts and each touched slot's item
+        HIP_TRY(h, hipMemsetAsync(b.dflag, 0, sizeof(uint32_t) * touched, stream));
+        HIP_TRY(h, launch_cp_items(b, sgm, touched, stream));
+        HIP_TRY(h, launch_cp_mlist(c, b, stream));
         if (touched * h->cpstride > h->cp_save_cap) {
             dfree(h->d_cp_save);
             if (hipMalloc(&h->d_cp_save, sizeof(CPBucket) * touched * h->cpstride) != hipSuccess)
@@ -2275,15 +2296,21 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     bool converged = false;
     if (!err && !has_multi) {  // single-value requests only: the slots are independent, one walk is exact
         HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), stream));
-        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
+        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream, h->aux, h->fork, h->join));
         converged = true;
     }
     while (!err && !converged && round < kMaxRounds) {
         b.round = (int)round;
+        // this round walks the lists the previous combine filled (buffer round & 1), and combine fills the other
+        b.din = h->d_cp_items + (size_t)(2 + 2 * (round & 1)) * nv;
+        b.din_count = h->d_cp_counts + 2 * (round & 1);
+        b.dout = h->d_cp_items + (size_t)(2 + 2 * ((round + 1) & 1)) * nv;
+        b.dout_count = h->d_cp_counts + 2 * ((round + 1) & 1);
         HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
         HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), stream));
-        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream));
-        HIP_TRY(h, launch_cp_combine(c, b, stream));
+        HIP_TRY(h, hipMemsetAsync(b.dout_count, 0, 2 * sizeof(uint32_t), stream));
+        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream, h->aux, h->fork, h->join));
+        HIP_TRY(h, launch_cp_combine(c, b, sgm, touched, stream));
         int changed = 0;
         HIP_TRY(h, hipMemcpyAsync(&changed, h->d_cp_changed, sizeof(int), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));

@@ -314,6 +314,53 @@ __global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
     }
 }
 
+// Block-aggregated list appends: each thread holds kAggItems candidates; a block scan of the (two 16-bit packed)
+// per-thread counts and one atomic per block and list (one per wave on a single counter serialised at ~10 ns each:
+// 2.8 ms for a 16M-request batch).
+constexpr int kAggItems = 16;
+
+__device__ __forceinline__ uint32_t cp_block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t off = x - v, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wave) off += wsum[w];
+        tot += wsum[w];
+    }
+    *total = tot;
+    return off;
+}
+
+// The valid multi-value requests: k_cp_combine's work list (any order).
+__global__ void __launch_bounds__(256) k_cp_mlist(CPArgs c, CPBatch b) {
+    __shared__ uint32_t wsum[4], gbase;
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * kAggItems);
+    bool m[kAggItems];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kAggItems; ++u) {
+        const uint64_t i = base + (uint64_t)u * 256 + threadIdx.x;
+        const sg_cparam_req q = c.req[min(i, c.n - 1)];
+        m[u] = i < c.n && q.value_count > 1 && cp_valid(c, q) && (uint64_t)q.value_begin + q.value_count <= c.n_values;
+        cnt += m[u] ? 1u : 0u;
+    }
+    uint32_t tot;
+    uint32_t off = cp_block_excl_scan(cnt, wsum, &tot);
+    if (threadIdx.x == 0) gbase = tot ? atomicAdd(b.mcount, tot) : 0u;
+    __syncthreads();
+    off += gbase;
+#pragma unroll
+    for (int u = 0; u < kAggItems; ++u)
+        if (m[u]) b.mlist[off++] = (uint32_t)(base + (uint64_t)u * 256 + threadIdx.x);
+}
+
 // Within a slot, value positions (the sort order) must follow the request order: the walk replays them in that
 // order. Checked on the sorted records, before anything is charged.
 __global__ void __launch_bounds__(256) k_cp_order(CPArgs c, CPBatch b, const uint64_t* sorted, uint64_t n) {
@@ -325,15 +372,16 @@ __global__ void __launch_bounds__(256) k_cp_order(CPArgs c, CPBatch b, const uin
     }
 }
 
-// Slot prologue of a walk: round 0 saves the pre-batch ring (when re-walks may follow); later rounds skip clean
-// slots and restore the dirty ones. `x0`/`dx` spread the bucket copies over the caller's lanes.
+// Slot prologue of a walk: round 0 saves the pre-batch ring (when re-walks may follow); later rounds walk only the
+// work items k_cp_combine listed (their flag set) and restore their rings first. `x0`/`dx` spread the bucket copies
+// over the caller's lanes.
 __device__ __forceinline__ bool cp_prologue(const CPArgs& c, const CPBatch& b, uint64_t g, uint64_t t, int x0, int dx) {
     CPBucket* ring = c.ring + g * (uint64_t)c.stride;
     CPBucket* sv = b.save + t * (uint64_t)c.stride;
     if (b.round > 0) {
-        if (!b.dirty[g]) return false;
+        if (!b.dflag[t]) return false;
         for (int x = x0; x < c.stride; x += dx) ring[x] = sv[x];
-        if (x0 == 0) b.dirty[g] = 0;
+        if (x0 == 0) b.dflag[t] = 0;
     } else if (b.save) {
         for (int x = x0; x < c.stride; x += dx) sv[x] = ring[x];
     }
@@ -401,10 +449,21 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
 }
 
 // One lane per slot of at most short_max records. Work item t: the slot's index in the save area (the long
-// list comes first, then the short lists in class order).
+// list comes first, then the short lists in class order); rounds > 0 walk the re-walk list of short items.
 __global__ void __launch_bounds__(256) k_cp_walk2(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
     const uint32_t nlong = *sg.long_count;
+    if (b.round > 0) {
+        const uint32_t cnt = b.din_count[1];
+        for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < cnt; x += gridDim.x * blockDim.x) {
+            const uint32_t t = b.din[b.dcap + x];
+            const uint64_t j = b.item_start[t];
+            const uint64_t g = sg.rec_sorted[j] >> b.pbits;
+            if (!cp_prologue(c, b, g, t, 0, 1)) continue;
+            cp_walk_serial(c, b, sg, g, j);
+        }
+        return;
+    }
     uint32_t total = 0;
     for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
     for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
@@ -415,6 +474,27 @@ __global__ void __launch_bounds__(256) k_cp_walk2(CPArgs c, CPBatch b, BatchArgs
         const uint64_t g = sg.rec_sorted[j] >> b.pbits;
         if (!cp_prologue(c, b, g, (uint64_t)nlong + u, 0, 1)) continue;
         cp_walk_serial(c, b, sg, g, j);
+    }
+}
+
+// Work items of the batch (long list, then the short lists in class order): each item's segment start, and each
+// touched slot's item (k_cp_combine lists the items of the slots a changed outcome dirties).
+__global__ void __launch_bounds__(256) k_cp_items(CPBatch b, BatchArgs sg) {
+    const uint32_t nlong = *sg.long_count;
+    uint32_t total = nlong;
+    for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        uint64_t j;
+        if (t < nlong) {
+            j = sg.long_list[t];
+        } else {
+            uint32_t r0 = t - nlong;
+            int k = 0;
+            while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
+            j = sg.short_list[sg.class_off[k] + r0];
+        }
+        b.item_start[t] = (uint32_t)j;
+        b.slot_item[sg.rec_sorted[j] >> b.pbits] = t;
     }
 }
 
@@ -483,9 +563,10 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
     const int lane = (int)__lane_id();
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    const uint32_t cnt = *sg.long_count;
-    for (uint32_t t = wave; t < cnt; t += nwaves) {
-        const uint64_t s = sg.long_list[t];
+    const uint32_t cnt = b.round > 0 ? b.din_count[0] : *sg.long_count;
+    for (uint32_t x = wave; x < cnt; x += nwaves) {
+        const uint32_t t = b.round > 0 ? b.din[x] : x;  // rounds > 0: the re-walk list of long items
+        const uint64_t s = b.round > 0 ? (uint64_t)b.item_start[t] : (uint64_t)sg.long_list[t];
         const uint64_t g = sg.rec_sorted[s] >> b.pbits;
         if (!cp_prologue(c, b, g, t, lane, 64)) continue;
         const CPRule r = c.rules[cp_rule_of_slot(c, g)];
@@ -702,9 +783,10 @@ __global__ void __launch_bounds__(256) k_cp_skipfill(CPArgs c, CPBatch b, BatchA
 
 __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
     if (*c.err) return;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t m = *b.mcount;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
+        const uint64_t i = b.mlist[x];  // a valid multi-value request (k_cp_prep2)
         const sg_cparam_req q = c.req[i];
-        if (q.value_count < 2 || !cp_valid(c, q)) continue;
         if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
         bool pass = true;
         for (uint32_t j = 0; j < q.value_count && pass; ++j) pass = b.chk[(uint64_t)q.value_begin + j] != 0;
@@ -717,9 +799,39 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
             *b.changed = 1;
             for (uint32_t j = 0; j < q.value_count; ++j) {
                 const uint64_t p = (uint64_t)q.value_begin + j;
-                if (b.chk[p]) b.dirty[b.pslot[p]] = 1;
+                if (b.chk[p]) b.dflag[b.slot_item[b.pslot[p]]] = 1u;  // listed by k_cp_relist
             }
         }
+    }
+}
+
+// The next round's re-walk lists from the flags k_cp_combine set (long items, short items; block-aggregated).
+__global__ void __launch_bounds__(256) k_cp_relist(CPBatch b, BatchArgs sg, uint32_t items) {
+    __shared__ uint32_t wsum[4], gbase[2];
+    const uint32_t nlong = *sg.long_count;
+    const uint32_t base = blockIdx.x * (256 * kAggItems);
+    bool f[kAggItems];
+    uint32_t cnt = 0;  // long count | short count << 16
+#pragma unroll
+    for (int u = 0; u < kAggItems; ++u) {
+        const uint32_t t = base + (uint32_t)u * 256 + threadIdx.x;
+        f[u] = t < items && b.dflag[min(t, items - 1)] != 0u;
+        cnt += f[u] ? (t < nlong ? 1u : 0x10000u) : 0u;
+    }
+    uint32_t tot;
+    const uint32_t off = cp_block_excl_scan(cnt, wsum, &tot);
+    if (threadIdx.x < 2) {
+        const uint32_t c2 = threadIdx.x == 0 ? (tot & 0xFFFFu) : (tot >> 16);
+        gbase[threadIdx.x] = c2 ? atomicAdd(&b.dout_count[threadIdx.x], c2) : 0u;
+    }
+    __syncthreads();
+    uint32_t o0 = gbase[0] + (off & 0xFFFFu), o1 = gbase[1] + (off >> 16);
+#pragma unroll
+    for (int u = 0; u < kAggItems; ++u) {
+        if (!f[u]) continue;
+        const uint32_t t = base + (uint32_t)u * 256 + threadIdx.x;
+        if (t < nlong) b.dout[o0++] = t;
+        else b.dout[(size_t)b.dcap + o1++] = t;
     }
 }
 
@@ -745,7 +857,7 @@ __global__ void __launch_bounds__(256) k_cp_saverings(CPArgs c, CPBatch b, Batch
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
         if (restore) {
             ring[x] = b.save[(uint64_t)t * c.stride + x];
-            if (x == 0) b.dirty[g] = 0;
+            if (x == 0) b.dflag[t] = 0;
         } else {
             b.save[(uint64_t)t * c.stride + x] = ring[x];
         }
@@ -809,16 +921,42 @@ hipError_t launch_cp_order(const CPArgs& c, const CPBatch& b, const uint64_t* so
     return hipGetLastError();
 }
 
-hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream) {
+// The long (hot-slot) walker on `aux` beside the lane walker, then the saturated ranges.
+hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream, hipStream_t aux,
+                           hipEvent_t fork, hipEvent_t join) {
     const uint64_t waves = sg.n / ((uint64_t)sg.short_max + 1) + 1;  // bound on the long list's length
-    hipLaunchKernelGGL(k_cp_walk2_long, dim3(cgrid2(waves * 64, 2048)), dim3(256), 0, stream, c, b, sg);
+#ifdef SG_CP_ONE_STREAM
+    aux = stream;
+#endif
+    hipError_t e = hipEventRecord(fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_cp_walk2_long, dim3(cgrid2(waves * 64, 2048)), dim3(256), 0, aux, c, b, sg);
     hipLaunchKernelGGL(k_cp_walk2, dim3(cgrid2(sg.n, 4096)), dim3(256), 0, stream, c, b, sg);
+    e = hipEventRecord(join, aux);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
+    if (e != hipSuccess) return e;
     if (b.skips) hipLaunchKernelGGL(k_cp_skipfill, dim3(1024), dim3(256), 0, stream, c, b, sg);
     return hipGetLastError();
 }
 
-hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
-    hipLaunchKernelGGL(k_cp_combine, dim3(cgrid2(c.n, 8192)), dim3(256), 0, stream, c, b);
+hipError_t launch_cp_items(const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_items, dim3(cgrid2(items, 8192)), dim3(256), 0, stream, b, sg);
+    return hipGetLastError();
+}
+
+hipError_t launch_cp_mlist(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
+    if (c.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cp_mlist, dim3((unsigned)((c.n + 256 * kAggItems - 1) / (256 * kAggItems))), dim3(256), 0, stream,
+                       c, b);
+    return hipGetLastError();
+}
+
+// k_cp_combine over the multi-value requests, then the re-walk lists of the next round (`items` work items)
+hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream) {
+    hipLaunchKernelGGL(k_cp_combine, dim3(cgrid2(c.n / 8 + 1, 4096)), dim3(256), 0, stream, c, b);
+    if (items) hipLaunchKernelGGL(k_cp_relist, dim3((unsigned)((items + 256 * kAggItems - 1) / (256 * kAggItems))),
+                                  dim3(256), 0, stream, b, sg, (uint32_t)items);
     return hipGetLastError();
 }
 

@@ -335,16 +335,28 @@ struct CPBatch {
     int* changed;
     CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots (null: no re-walks)
     uint32_t* pslot;          // [n_values] slot of value position p
-    uint8_t* dirty;           // [total slots] slot must be re-walked (an assumed outcome in it changed)
-    int round;                // 0: first walk (saves the rings); > 0: re-walk the dirty slots from the saves
+    uint32_t* dflag;          // [work items] the item is listed for the next re-walk (an assumed outcome changed)
+    uint32_t* item_start;     // [work items] segment start of item t (long items first, then short: k_cp_items)
+    uint32_t* slot_item;      // [total slots] work item of each slot this batch touches
+    uint32_t* din;            // re-walk lists walked this round: [2][dcap] long / short items
+    uint32_t* din_count;      // [2]
+    uint32_t* dout;           // re-walk lists k_cp_combine fills for the next round
+    uint32_t* dout_count;     // [2], zeroed by the host before each combine
+    uint32_t dcap;
+    uint32_t* mlist;          // valid multi-value requests (k_cp_prep2 appends, any order)
+    uint32_t* mcount;
+    int round;                // 0: first walk (saves the rings); > 0: re-walk the listed items from the saves
     int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
     uint2* skips;             // saturated ranges [x, y) of sorted records handed to k_cp_skipfill (null: no skipping)
     uint32_t* skip_count;     // zeroed by the host before every walk
     uint32_t skip_cap;
 };
 hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream);
-hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream);
-hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+hipError_t launch_cp_walk2(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, hipStream_t stream, hipStream_t aux,
+                           hipEvent_t fork, hipEvent_t join);
+hipError_t launch_cp_items(const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream);
+hipError_t launch_cp_mlist(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream);
 hipError_t launch_cp_saverings(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, int restore, hipStream_t stream);
 hipError_t launch_cp_serial(const CPArgs& c, const CPBatch& b, hipStream_t stream);
 hipError_t launch_cp_finish_batch(const CPArgs& c, hipStream_t stream);
