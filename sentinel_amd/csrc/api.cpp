@@ -113,6 +113,10 @@ struct sg_handle {
     uint32_t* d_cp_long = nullptr;    // segment lists over the value records (capacity cp_val_cap)
     uint32_t* d_cp_short = nullptr;
     uint64_t cp_class_off[kClasses]{};
+    std::vector<int32_t> cp_wls;      // distinct window lengths of the cluster param rules (CPRule::wl_idx)
+    uint32_t* d_cp_bnd = nullptr;     // [kMaxWl][kMaxPeriods] the batch's period tables (request index -> period)
+    int64_t* d_cp_p0 = nullptr;
+    uint32_t* d_cp_np = nullptr;
     uint32_t* d_cp_slot_item = nullptr;  // [cptotal] work item of each touched slot (k_cp_items)
     uint64_t cp_slot_item_cap = 0;
     uint32_t* d_cp_items = nullptr;   // [4 * cp_val_cap] per work item: re-walk flag, segment start; re-walk lists x2
@@ -607,6 +611,9 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_long);
     dfree(h->d_cp_short);
     dfree(h->d_cp_slot_item);
+    dfree(h->d_cp_bnd);
+    dfree(h->d_cp_p0);
+    dfree(h->d_cp_np);
     dfree(h->d_cp_items);
     dfree(h->d_cp_counts);
     dfree(h->d_cp_mlist);
@@ -1939,6 +1946,7 @@ int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, 
     std::unordered_map<int64_t, uint32_t> seen, old_index;
     for (uint32_t k = 0; k < h->cprules.size(); ++k) old_index.emplace(h->cprules[k].flow_id, k);
     std::vector<CPRule> tab(n);
+    std::vector<int32_t> wls;  // distinct window lengths (the batch's period tables)
     std::vector<sg_param_hot_item> hs(hot, hot + n_hot);
     int stride = 1;
     uint64_t base = 0;
@@ -1969,6 +1977,16 @@ int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, 
         R.hot_count = r.hot_count;
         R.table_base = base;
         R.table_mask = (1ull << lg) - 1;
+        {
+            auto wit = std::find(wls.begin(), wls.end(), R.wl);
+            if (wit == wls.end()) {
+                if ((int)wls.size() == kMaxWl) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct param window lengths");
+                wls.push_back(R.wl);
+                wit = wls.end() - 1;
+            }
+            R.wl_idx = (int32_t)(wit - wls.begin());
+            R.pad = 0;
+        }
         base += per;
         stride = std::max(stride, S);
         std::sort(hs.begin() + r.hot_begin, hs.begin() + r.hot_begin + r.hot_count,
@@ -2013,6 +2031,7 @@ int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, 
     h->d_cpring = d_ring;
     h->cprules.assign(rules, rules + n);
     h->cptab = tab;
+    h->cp_wls = wls;
     h->cptotal = base;
     h->cpstride = stride;
     if (!h->d_cplast_ts) {
@@ -2040,6 +2059,7 @@ static CPArgs cp_args(sg_handle* h, const sg_cparam_req* req, uint64_t n, const 
     c.ring = h->d_cpring;
     c.stride = h->cpstride;
     c.total_slots = h->cptotal;
+    c.per = h->cptab.empty() ? 1 : h->cptab[0].table_mask + 2;
     c.err = h->d_err;
     c.last_ts = h->d_cplast_ts;
     return c;
@@ -2119,8 +2139,11 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     CPArgs c = cp_args(h, req, n, values, n_values, out);
     const uint64_t nv = n_values ? n_values : 1;
     const int gbits = bits_for(h->cptotal + 1);
-    const int pbits = bits_for(nv);
-    if (pbits + gbits > 64 || gbits > 32) return fail(h, SG_E_UNSUPPORTED, "param tables x values too large for 64-bit records");
+    // value records {slot : gbits | multi : 1 | acquire code : 7 | request index or value position : idbits}
+    const int pbits = 64 - gbits;
+    const int idbits = pbits - 8;
+    if (gbits > 32 || idbits < std::max(bits_for(nv), bits_for(n)))
+        return fail(h, SG_E_UNSUPPORTED, "param tables x values too large for 64-bit records");
     // scratch sized for the batch's value positions
     if (nv > h->cp_val_cap) {
         dfree(h->d_cp_owner);
@@ -2132,7 +2155,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         dfree(h->d_cp_rec2);
         dfree(h->d_cp_hist);
         dfree(h->d_cp_items);
-        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 6 * nv) != hipSuccess ||
+        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 7 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_pslot, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
@@ -2172,11 +2195,23 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     b.rec = h->d_cp_rec;
     b.pbits = pbits;
     b.pmask = (1ull << pbits) - 1;
+    b.idbits = idbits;
+    b.idmask = (1ull << idbits) - 1;
+    b.n_wl = (int)h->cp_wls.size();
+    for (int w = 0; w < b.n_wl; ++w) b.wl[w] = h->cp_wls[w];
+    if (!h->d_cp_bnd && (hipMalloc(&h->d_cp_bnd, sizeof(uint32_t) * kMaxWl * kMaxPeriods) != hipSuccess ||
+                         hipMalloc(&h->d_cp_p0, sizeof(int64_t) * kMaxWl) != hipSuccess ||
+                         hipMalloc(&h->d_cp_np, sizeof(uint32_t) * kMaxWl) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "cparam period tables");
+    b.bnd = h->d_cp_bnd;
+    b.p0 = h->d_cp_p0;
+    b.np = h->d_cp_np;
     b.changed = h->d_cp_changed;
     b.pslot = h->d_cp_pslot;
     b.dflag = h->d_cp_items;                      // [nv] (items <= value positions)
     b.item_start = h->d_cp_items + nv;           // [nv]
     b.slot_item = h->d_cp_slot_item;
+    b.item_end = h->d_cp_items + 6 * nv;         // [nv]
     b.dcap = (uint32_t)nv;                       // re-walk lists: 2 buffers x {long, short} x nv
     b.mlist = h->d_cp_mlist;
     b.mcount = h->d_cp_counts + 4;
@@ -2196,7 +2231,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         return SG_OK;
     }
     uint64_t* sorted = nullptr;
-    HIP_TRY(h, radix_sort_records(h->d_cp_rec, h->d_cp_rec2, nv, pbits, h->d_cp_hist, &sorted, stream, pbits + gbits));
+    HIP_TRY(h, radix_sort_records(h->d_cp_rec, h->d_cp_rec2, nv, pbits, h->d_cp_hist, &sorted, stream, 64));
     HIP_TRY(h, launch_cp_order(c, b, sorted, nv, stream));
     if (any_lim) {  // after validation: a rejected batch leaves the limiter untouched
         BatchArgs a{};
@@ -2263,10 +2298,11 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     HIP_TRY(h, hipStreamSynchronize(stream));
     uint64_t touched = 0;
     for (uint32_t x : counts) touched += x;
+    // work items: segment bounds and each touched slot's item (the walkers need the bounds in every round)
+    if (!err && touched > 0) HIP_TRY(h, launch_cp_items(b, sgm, touched, stream));
     if (!err && has_multi && touched > 0) {
-        // work items: re-walk flags clear, segment starts and each touched slot's item
+        // re-walk flags clear, the multi-value requests' list
         HIP_TRY(h, hipMemsetAsync(b.dflag, 0, sizeof(uint32_t) * touched, stream));
-        HIP_TRY(h, launch_cp_items(b, sgm, touched, stream));
         HIP_TRY(h, launch_cp_mlist(c, b, stream));
         if (touched * h->cpstride > h->cp_save_cap) {
             dfree(h->d_cp_save);

@@ -81,13 +81,7 @@ __device__ __forceinline__ uint64_t cp_slot(const CPArgs& c, const CPRule& r, ui
 }
 
 __device__ __forceinline__ uint32_t cp_rule_of_slot(const CPArgs& c, uint64_t g) {
-    uint32_t lo = 0, hi = c.n_rules;  // rules by table_base
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (c.rules[mid].table_base <= g) lo = mid;
-        else hi = mid;
-    }
-    return lo;
+    return (uint32_t)(g / c.per);  // every rule's sub-table has the same size
 }
 
 // Σ of the value's counts over the window at period P (slot I = P % S is current or stale; the others
@@ -234,7 +228,81 @@ __device__ __forceinline__ bool cp_valid(const CPArgs& c, const sg_cparam_req& q
     return !(key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) && key < c.n_rules;
 }
 
+constexpr uint32_t kCpAesc = 127;  // acquire code: read req[i].acquire
+
+// A value record, decoded (CPBatch::rec): the request, the value position (multi-value requests), the count.
+struct CPRec {
+    uint32_t i;
+    uint64_t p;
+    bool multi;
+    int64_t acq;
+};
+
+__device__ __forceinline__ CPRec cp_dec(const CPArgs& c, const CPBatch& b, uint64_t rec) {
+    CPRec d;
+    const uint64_t pl = rec & b.pmask;
+    d.multi = ((pl >> (b.pbits - 1)) & 1ull) != 0;
+    const uint32_t ac = (uint32_t)(pl >> b.idbits) & 127u;
+    d.p = pl & b.idmask;
+    d.i = d.multi ? b.owner[d.p] : (uint32_t)d.p;
+    d.acq = ac == kCpAesc ? (int64_t)c.req[d.i].acquire : (int64_t)ac;
+    return d;
+}
+
 }  // namespace
+
+// The batch's period tables (first request index of every window period, per distinct window length of the rules)
+// staged in LDS when they fit, else read from b.bnd: a value record's window period is a function of its request
+// index (requests are time-ordered), so the walkers never read a request's timestamp.
+constexpr int kCpLdsBnd = 2048;
+__shared__ uint32_t cp_sbnd[kCpLdsBnd];
+__shared__ uint32_t cp_boff[kMaxWl];
+__shared__ int cp_blds;
+__shared__ int64_t cp_p0[kMaxWl];
+__shared__ uint32_t cp_np[kMaxWl];
+
+__device__ __forceinline__ void cp_stage_periods(const CPBatch& b) {
+    uint32_t tot = 0;
+    for (int w = 0; w < b.n_wl; ++w) tot += b.np[w];
+    const bool lds = tot <= (uint32_t)kCpLdsBnd;
+    uint32_t off = 0;
+    for (int w = 0; w < b.n_wl; ++w) {
+        const uint32_t npw = b.np[w];
+        if (lds) {
+            const uint32_t* g = b.bnd + (size_t)w * kMaxPeriods;
+            for (uint32_t x = threadIdx.x; x < npw; x += blockDim.x) cp_sbnd[off + x] = g[x];
+        }
+        if (threadIdx.x == 0) cp_boff[w] = off;
+        off += npw;
+    }
+    if (threadIdx.x == 0) cp_blds = lds ? 1 : 0;
+    if (threadIdx.x < (unsigned)b.n_wl) {
+        cp_p0[threadIdx.x] = b.p0[threadIdx.x];
+        cp_np[threadIdx.x] = b.np[threadIdx.x];
+    }
+    __syncthreads();
+}
+
+// window period (absolute) of request i for window length w: the largest q with table[q] <= i (entry 0 unused)
+__device__ __forceinline__ int64_t cp_period(const CPBatch& b, int w, uint32_t i) {
+    uint32_t lo = 0, hi = cp_np[w];
+    if (cp_blds) {
+        const uint32_t* t = cp_sbnd + cp_boff[w];
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (t[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+    } else {
+        const uint32_t* t = b.bnd + (size_t)w * kMaxPeriods;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (t[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+    }
+    return cp_p0[w] + (int64_t)lo;
+}
 
 // The 100 ms limiter periods of the batch (row 0 of the period table) and {cparam rule | request} records of the
 // valid requests; runs after k_cp_prep2, and the limiter then overwrites the refused requests' results with
@@ -277,9 +345,40 @@ __global__ void __launch_bounds__(256) k_cp_recinit(CPBatch b, uint64_t n_values
 }
 
 __global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
+    const int64_t t0 = c.req[0].ts_ms;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
         const sg_cparam_req q = c.req[i];
-        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *c.last_ts : q.ts_ms < c.req[i - 1].ts_ms)) atomicOr(c.err, kErrTime);
+        const int64_t t = q.ts_ms;
+        // timestamps, and the window-period tables (as k_prep: a new period can only start at a new timestamp)
+        if (i == 0) {
+            if (t < 0 || t < *c.last_ts) atomicOr(c.err, kErrTime);
+            for (int w = 0; w < b.n_wl; ++w) b.p0[w] = t / b.wl[w];
+        } else {
+            const int64_t tp = c.req[i - 1].ts_ms;
+            if (t < tp || t < 0) {
+                atomicOr(c.err, kErrTime);
+            } else if (t != tp) {
+                for (int w = 0; w < b.n_wl; ++w) {
+                    const int64_t wl = b.wl[w];
+                    const int64_t P0 = t0 / wl;
+                    for (int64_t pp = tp / wl + 1; pp <= t / wl; ++pp) {
+                        const int64_t qq = pp - P0;
+                        if (qq <= 0) continue;
+                        if (qq >= (int64_t)kMaxPeriods) {
+                            atomicOr(c.err, kErrPeriods);
+                            break;
+                        }
+                        b.bnd[(size_t)w * kMaxPeriods + qq] = (uint32_t)i;
+                    }
+                }
+            }
+        }
+        if (i == c.n - 1) {
+            for (int w = 0; w < b.n_wl; ++w) {
+                const int64_t qq = t / b.wl[w] - t0 / b.wl[w] + 1;
+                b.np[w] = qq > (int64_t)kMaxPeriods ? kMaxPeriods : qq < 1 ? 1u : (uint32_t)qq;
+            }
+        }
         const uint32_t key = q.key & SG_KEY_INDEX;
         b.assume[i] = 1;
         if (key == SG_KEY_BAD || q.acquire <= 0 || q.value_count == 0) {
@@ -307,7 +406,10 @@ __global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
             if (g == ~0ull) {
                 atomicOr(c.err, kErrTableFull);
             } else {
-                b.rec[p] = (g << b.pbits) | p;
+                const uint64_t ac = q.acquire >= (int32_t)kCpAesc ? kCpAesc : (uint64_t)q.acquire;
+                const uint64_t pl = q.value_count > 1 ? ((1ull << (b.pbits - 1)) | (ac << b.idbits) | p)
+                                                      : ((ac << b.idbits) | i);
+                b.rec[p] = (g << b.pbits) | pl;
                 b.pslot[p] = (uint32_t)g;
             }
         }
@@ -366,9 +468,9 @@ __global__ void __launch_bounds__(256) k_cp_mlist(CPArgs c, CPBatch b) {
 __global__ void __launch_bounds__(256) k_cp_order(CPArgs c, CPBatch b, const uint64_t* sorted, uint64_t n) {
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r0 = sorted[j - 1], r1 = sorted[j];
-        if ((r0 >> b.pbits) != (r1 >> b.pbits)) continue;
-        const uint32_t a0 = b.owner[r0 & b.pmask], a1 = b.owner[r1 & b.pmask];
-        if (a0 != kNoOwner && a1 != kNoOwner && a1 < a0) atomicOr(c.err, kErrBounds);
+        if ((r0 >> b.pbits) != (r1 >> b.pbits) || (r1 >> b.pbits) >= c.total_slots) continue;
+        const uint32_t a0 = cp_dec(c, b, r0).i, a1 = cp_dec(c, b, r1).i;
+        if (a1 < a0) atomicOr(c.err, kErrBounds);
     }
 }
 
@@ -390,7 +492,7 @@ __device__ __forceinline__ bool cp_prologue(const CPArgs& c, const CPBatch& b, u
 
 // Sequential replay of the records [j, ...) of slot g (one lane). Single-value requests: window check and add.
 // A multi-value request's records in this slot (repeated values) check the state before the request, and add
-// its count each iff its outcome is assumed to be a pass.
+// its count each iff its outcome is assumed to be a pass and the check passed. Needs cp_stage_periods.
 __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j) {
     const CPRule r = c.rules[cp_rule_of_slot(c, g)];
     const double thr = cp_threshold(c, r, c.keys[g]);
@@ -398,18 +500,24 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
     const int S = r.S;
     const int64_t wl = r.wl;
     int64_t P = INT64_MIN, other = 0, cur = 0;
-    while (j < sg.n) {
-        const uint64_t rec = sg.rec_sorted[j];
-        if ((rec >> b.pbits) != g) break;
-        const uint64_t p = rec & b.pmask;
-        const uint32_t i = b.owner[p];
-        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) {  // allowProceed refused it
-            ++j;
+    uint32_t qn = 0xFFFFFFFFu;  // first request index of the period after P (monotone cursor)
+    uint32_t mi = kNoOwner;     // the multi-value request of the previous record, and its check here
+    bool mok = false;
+    uint64_t rec = sg.rec_sorted[j];
+    while ((rec >> b.pbits) == g) {
+        const uint64_t nrec = j + 1 < sg.n ? sg.rec_sorted[j + 1] : ~0ull;  // issued before this record is decided
+        const CPRec d = cp_dec(c, b, rec);
+        const uint32_t i = d.i;
+        rec = nrec;
+        ++j;
+        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;  // allowProceed refused it
+        if (d.multi && i == mi) {  // a repeated value: the check of the request's first record here, and its add
+            b.chk[d.p] = mok ? 1 : 0;
+            if (b.assume[i] && mok) cur += d.acq;
             continue;
         }
-        const sg_cparam_req q = c.req[i];
-        const int64_t Pq = q.ts_ms / wl;
-        if (Pq != P) {  // currentWindow(t): close the open period, open this one
+        if (P == INT64_MIN || i >= qn) {  // currentWindow(t): close the open period, open this one
+            const int64_t Pq = cp_period(b, r.wl_idx, i);
             if (P != INT64_MIN) {
                 CPBucket bk;
                 bk.start = P * wl;
@@ -418,27 +526,28 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
             }
             P = Pq;
             other = cp_window(ring, S, wl, P, &cur);
+            const uint32_t q1 = (uint32_t)(P - cp_p0[r.wl_idx]) + 1;
+            qn = q1 < cp_np[r.wl_idx] ? (cp_blds ? cp_sbnd[cp_boff[r.wl_idx] + q1]
+                                                  : b.bnd[(size_t)r.wl_idx * kMaxPeriods + q1])
+                                      : 0xFFFFFFFFu;
         }
-        const double rem = thr - (double)(other + cur) / r.isec - (double)q.acquire;
-        if (q.value_count == 1) {
+        const double rem = thr - (double)(other + cur) / r.isec - (double)d.acq;
+        if (!d.multi) {
+            mi = kNoOwner;
             if (rem >= 0) {
-                cur += q.acquire;
+                cur += d.acq;
                 cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
             } else {
                 cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
             }
-            ++j;
             continue;
         }
-        uint64_t e = j;
-        while (e < sg.n && (sg.rec_sorted[e] >> b.pbits) == g && b.owner[sg.rec_sorted[e] & b.pmask] == i) {
-            b.chk[sg.rec_sorted[e] & b.pmask] = rem >= 0 ? 1 : 0;
-            ++e;
-        }
-        // the request adds here iff its outcome is assumed a pass and this slot's check passed: a failing check on
-        // the exact pre-request state decides the request (all-or-nothing), whatever its other slots say
-        if (b.assume[i] && rem >= 0) cur += (int64_t)q.acquire * (int64_t)(e - j);
-        j = e;
+        // a multi-value request's first record here: its check on the pre-request state; it adds (and so do its
+        // repeated values after it) iff the request is assumed to pass and the check passed
+        mi = i;
+        mok = rem >= 0;
+        b.chk[d.p] = mok ? 1 : 0;
+        if (b.assume[i] && mok) cur += d.acq;
     }
     if (P != INT64_MIN) {
         CPBucket bk;
@@ -452,6 +561,7 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
 // list comes first, then the short lists in class order); rounds > 0 walk the re-walk list of short items.
 __global__ void __launch_bounds__(256) k_cp_walk2(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
+    cp_stage_periods(b);
     const uint32_t nlong = *sg.long_count;
     if (b.round > 0) {
         const uint32_t cnt = b.din_count[1];
@@ -493,8 +603,22 @@ __global__ void __launch_bounds__(256) k_cp_items(CPBatch b, BatchArgs sg) {
             while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
             j = sg.short_list[sg.class_off[k] + r0];
         }
+        const uint64_t g = sg.rec_sorted[j] >> b.pbits;
         b.item_start[t] = (uint32_t)j;
-        b.slot_item[sg.rec_sorted[j] >> b.pbits] = t;
+        b.slot_item[g] = t;
+        // the segment's end: exponential then binary search (once per batch; every round's walkers reuse it)
+        uint64_t lo = j, step = 1, hi = j + 1;
+        while (hi < sg.n && (sg.rec_sorted[hi] >> b.pbits) == g) {
+            lo = hi;
+            step *= 2;
+            hi = min(j + step, sg.n);
+        }
+        while (hi - lo > 1) {  // rec[lo] is g, rec[hi] (or the end) is not
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((sg.rec_sorted[mid] >> b.pbits) == g) lo = mid;
+            else hi = mid;
+        }
+        b.item_end[t] = (uint32_t)hi;
     }
 }
 
@@ -560,6 +684,7 @@ constexpr uint64_t kCpSkipPiece = 4096;  // skipped ranges go to k_cp_skipfill i
 // slot costs a few steps per window period instead of one or two per 64 records.
 __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, BatchArgs sg) {
     if (*c.err) return;
+    cp_stage_periods(b);
     const int lane = (int)__lane_id();
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
@@ -574,9 +699,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
             if (lane == 0) cp_walk_serial(c, b, sg, g, s);
             continue;
         }
-        const uint64_t e = cp_wave_search(s + sg.short_max, sg.n, [&](uint64_t q) {
-            return (sg.rec_sorted[q] >> b.pbits) != g;
-        }, lane);
+        const uint64_t e = b.item_end[t];
         const double thr = cp_threshold(c, r, c.keys[g]);
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
         const int S = r.S;
@@ -591,26 +714,37 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
         uint32_t carry = kNoOwner;  // owner of the record before the current chunk
         bool carry_ok = false;      // that owner is a multi-value request whose first record here passed its check
         uint64_t blk = s;
+        uint64_t pf = s;  // position of the records in rcn (the next block, loaded a block ahead)
+        uint64_t rcn[kCpU];
+#pragma unroll
+        for (int u = 0; u < kCpU; ++u) rcn[u] = sg.rec_sorted[min(s + (uint64_t)u * 64 + lane, e - 1)];
         while (blk < e) {
             // loads of kCpU chunks at once; indices clamped to the segment (unconditional loads)
             uint64_t rc[kCpU];
             uint32_t ow[kCpU];
-            int64_t ts[kCpU];
-            int32_t aq[kCpU], st[kCpU];
-            uint32_t vc[kCpU];
+            int64_t aq[kCpU];
+            int32_t st[kCpU];
             uint8_t as[kCpU];
+            const bool have = pf == blk;  // wave-uniform: the block was prefetched (no saturated skip since)
 #pragma unroll
-            for (int u = 0; u < kCpU; ++u) rc[u] = sg.rec_sorted[min(blk + (uint64_t)u * 64 + lane, e - 1)];
+            for (int u = 0; u < kCpU; ++u) rc[u] = have ? rcn[u] : sg.rec_sorted[min(blk + (uint64_t)u * 64 + lane, e - 1)];
+            pf = blk + 64ull * kCpU;
 #pragma unroll
-            for (int u = 0; u < kCpU; ++u) ow[u] = b.owner[rc[u] & b.pmask];
+            for (int u = 0; u < kCpU; ++u) rcn[u] = sg.rec_sorted[min(pf + (uint64_t)u * 64 + lane, e - 1)];
+#pragma unroll
+            for (int u = 0; u < kCpU; ++u) {  // the request: in the record (single value), owner[] (multi-value)
+                const uint64_t pl = rc[u] & b.pmask;
+                const uint64_t id = pl & b.idmask;
+                ow[u] = ((pl >> (b.pbits - 1)) & 1ull) ? b.owner[id] : (uint32_t)id;
+            }
 #pragma unroll
             for (int u = 0; u < kCpU; ++u) {
-                const sg_cparam_req q = c.req[ow[u]];
-                ts[u] = q.ts_ms;
-                aq[u] = q.acquire;
-                vc[u] = q.value_count;
+                const uint64_t pl = rc[u] & b.pmask;
+                const uint32_t ac = (uint32_t)(pl >> b.idbits) & 127u;
+                const bool mu = ((pl >> (b.pbits - 1)) & 1ull) != 0;
+                aq[u] = ac == kCpAesc ? (int64_t)c.req[ow[u]].acquire : (int64_t)ac;
                 st[u] = b.lim ? c.out[ow[u]].status : 0;
-                as[u] = b.assume[ow[u]];
+                as[u] = mu ? b.assume[ow[u]] : (uint8_t)1;
             }
             uint64_t next = blk + 64ull * kCpU;
 #pragma unroll
@@ -620,7 +754,8 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 const uint64_t j = base + (uint64_t)lane;
                 const bool act = j < e;
                 const uint32_t i = ow[u];
-                const uint64_t p = rc[u] & b.pmask;
+                const uint64_t p = rc[u] & b.idmask;  // the value position (multi-value records)
+                const bool mu = ((rc[u] >> (b.pbits - 1)) & 1ull) != 0;
                 uint32_t prev = (uint32_t)__shfl_up((int)i, 1u, 64);
                 if (lane == 0) prev = carry;
                 carry = (uint32_t)__shfl((int)i, 63, 64);
@@ -628,8 +763,8 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 int64_t acq = 0, Pq = 0;
                 if (act && !(b.lim && st[u] == SG_STATUS_TOO_MANY_REQUEST)) {
                     acq = aq[u];
-                    Pq = ts[u] / wl;
-                    typ = vc[u] == 1 ? kCpSingle : prev == i ? kCpDup : kCpMulti;
+                    Pq = cp_period(b, r.wl_idx, i);
+                    typ = !mu ? kCpSingle : prev == i ? kCpDup : kCpMulti;
                 }
                 // a request's records in this slot are adjacent: a repeated value's first record is the nearest
                 // non-repeated lane below it, or (none in the chunk) the carried owner's
@@ -722,7 +857,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                     thr - (double)(other + cur) / r.isec - 1.0 < 0) {
                     const int64_t Pc = P;
                     const uint64_t pe = cp_wave_search(pos, e, [&](uint64_t q) {
-                        return c.req[b.owner[sg.rec_sorted[q] & b.pmask]].ts_ms / wl > Pc;
+                        return cp_period(b, r.wl_idx, cp_dec(c, b, sg.rec_sorted[q]).i) > Pc;
                     }, lane);
                     if (pe - pos >= kCpSkipMin) {
                         const uint32_t np = (uint32_t)((pe - pos + kCpSkipPiece - 1) / kCpSkipPiece);
@@ -734,7 +869,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                                 const uint64_t b0 = pos + (uint64_t)pi * kCpSkipPiece;
                                 b.skips[slot + pi] = make_uint2((uint32_t)b0, (uint32_t)min(pe, b0 + kCpSkipPiece));
                             }
-                            carry = b.owner[sg.rec_sorted[pe - 1] & b.pmask];
+                            carry = cp_dec(c, b, sg.rec_sorted[pe - 1]).i;
                             next = pe;
                             break;
                         }
@@ -768,14 +903,13 @@ __global__ void __launch_bounds__(256) k_cp_skipfill(CPArgs c, CPBatch b, BatchA
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint2 pc = b.skips[w];
         for (uint64_t j = (uint64_t)pc.x + lane; j < pc.y; j += 64) {
-            const uint64_t p = sg.rec_sorted[j] & b.pmask;
-            const uint32_t i = b.owner[p];
-            if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
-            if (c.req[i].value_count == 1) {
-                cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+            const CPRec d = cp_dec(c, b, sg.rec_sorted[j]);
+            if (b.lim && c.out[d.i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
+            if (!d.multi) {
+                cp_store(c.out, d.i, SG_STATUS_BLOCKED, 0);
             } else {
-                const uint32_t prev = b.owner[sg.rec_sorted[j - 1] & b.pmask];  // j > the segment start
-                b.chk[p] = prev == i ? 1 : 0;
+                const uint32_t prev = cp_dec(c, b, sg.rec_sorted[j - 1]).i;  // j > the segment start
+                b.chk[d.p] = prev == d.i ? 1 : 0;
             }
         }
     }

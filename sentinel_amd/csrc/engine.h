@@ -296,6 +296,8 @@ struct CPRule {
     uint32_t hot_begin, hot_count;
     uint64_t table_base;      // first slot of this rule's (value → ring) sub-table
     uint64_t table_mask;      // 2^capacity_log2 - 1; slot table_base + mask + 1 holds the value ~0
+    int32_t wl_idx;           // index of wl in the handle's distinct window lengths (the batch's period tables)
+    int32_t pad;
 };
 
 struct CPBucket {             // one bucket of a (flowId, value) ring: window start, the value's count
@@ -319,6 +321,7 @@ struct CPArgs {
     CPBucket* ring;           // [total_slots][stride]
     int stride;
     uint64_t total_slots;
+    uint64_t per;             // slots per rule (every sub-table has 2^capacity_log2 + 1): rule of slot g = g / per
     int* err;
     int64_t* last_ts;
 };
@@ -329,14 +332,26 @@ struct CPBatch {
     uint32_t* owner;          // [n_values] request that owns value position p (~0 = none)
     uint8_t* chk;             // [n_values] the value's check at its request (multi-value requests)
     uint8_t* assume;          // [n] multi-value request: assumed outcome of this iteration
-    uint64_t* rec;            // [n_values] {slot : high bits | value position : pbits}
+    // value records, sorted by slot: {slot : 64 - pbits | payload : pbits}, payload = {multi : 1 | acquire code : 7 |
+    // id : idbits}; id = the request index of a single-value request, the value position of a multi-value one (its
+    // request: owner[id]); acquire code 127 = read req[i].acquire. The walkers read nothing else per single-value record
+    // but the period of its request (the batch's period tables: request index -> window period, per window length).
+    uint64_t* rec;
     int pbits;
     uint64_t pmask;
+    int idbits;
+    uint64_t idmask;
+    int n_wl;
+    int32_t wl[kMaxWl];
+    uint32_t* bnd;            // [kMaxWl][kMaxPeriods] first request index of each window period
+    int64_t* p0;              // [kMaxWl] first window period of the batch
+    uint32_t* np;             // [kMaxWl] window periods the batch spans
     int* changed;
     CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots (null: no re-walks)
     uint32_t* pslot;          // [n_values] slot of value position p
     uint32_t* dflag;          // [work items] the item is listed for the next re-walk (an assumed outcome changed)
     uint32_t* item_start;     // [work items] segment start of item t (long items first, then short: k_cp_items)
+    uint32_t* item_end;       // [work items] its end
     uint32_t* slot_item;      // [total slots] work item of each slot this batch touches
     uint32_t* din;            // re-walk lists walked this round: [2][dcap] long / short items
     uint32_t* din_count;      // [2]
