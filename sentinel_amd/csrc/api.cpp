@@ -113,6 +113,8 @@ struct sg_handle {
     uint32_t* d_cp_long = nullptr;    // segment lists over the value records (capacity cp_val_cap)
     uint32_t* d_cp_short = nullptr;
     uint64_t cp_class_off[kClasses]{};
+    uint32_t* d_p_msb = nullptr;      // hot-parameter batch: first request index of each millisecond
+    int64_t* d_p_mt = nullptr;        // its first timestamp, then the millisecond count (uint32)
     std::vector<int32_t> cp_wls;      // distinct window lengths of the cluster param rules (CPRule::wl_idx)
     uint32_t* d_cp_bnd = nullptr;     // [kMaxWl][kMaxPeriods] the batch's period tables (request index -> period)
     int64_t* d_cp_p0 = nullptr;
@@ -611,6 +613,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_long);
     dfree(h->d_cp_short);
     dfree(h->d_cp_slot_item);
+    dfree(h->d_p_msb);
+    dfree(h->d_p_mt);
     dfree(h->d_cp_bnd);
     dfree(h->d_cp_p0);
     dfree(h->d_cp_np);
@@ -1737,6 +1741,7 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
     if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);  // the main workspace's segment lists may belong to an enqueued flow batch
     PArgs p{};
     p.req = req;
     p.out = pass;
@@ -1758,11 +1763,25 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
     if (const char* e = std::getenv("SG_PARAM_SHORT_MAX")) psplit = (uint32_t)std::strtoul(e, nullptr, 10);
     p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : psplit;
     const int gbits = bits_for(h->ptotal + 1);
-    if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
+    p.gshift = p.ibits + 8;  // {slot | acquire code : 8 | request index}
+    if (p.gshift + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "param tables x max_batch too large for 64-bit records");
+    if (!h->d_p_msb && (hipMalloc(&h->d_p_msb, sizeof(uint32_t) * kMaxPeriods) != hipSuccess ||
+                        hipMalloc(&h->d_p_mt, 2 * sizeof(int64_t)) != hipSuccess))  // {t0, {np, zero word}}
+        return fail(h, SG_E_NOMEM, "param millisecond table");
+    p.msb = h->d_p_msb;
+    p.mt0 = h->d_p_mt;
+    p.mnp = reinterpret_cast<uint32_t*>(h->d_p_mt + 1);
+    BatchArgs sg{};  // k_seg's lists in the main workspace; its error word: a zero word (the param flags are no errors)
+    sg.err = reinterpret_cast<int*>(h->d_p_mt) + 3;
+    sg.short_list = h->d_short_list;
+    sg.short_count = h->d_long_count + 1;
+    for (int c = 0; c < kClasses; ++c) sg.class_off[c] = h->class_off[c];
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(sg.err, 0, sizeof(int), stream));
     uint64_t* sorted = nullptr;
-    HIP_TRY(h, launch_param_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream));
+    HIP_TRY(h, launch_param_batch(p, sg, h->d_rec, h->d_rec_sorted, h->d_hist, p.gshift, p.gshift + gbits, &sorted, stream,
+                                  h->aux, h->fork, h->join));
     h->last_sorted = sorted;
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipStreamSynchronize(stream));

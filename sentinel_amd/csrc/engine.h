@@ -195,10 +195,15 @@ struct PArgs {
     const sg_param_req* req;
     int32_t* out;
     uint64_t n;
-    uint64_t* rec;          // {global slot : high bits | request index : ibits}
+    uint64_t* rec;          // {global slot : high bits | request index : ibits} (ParamFlowSlot chain), or for the
+                            // hot-parameter batch {slot : 64 - gshift | acquire code : 8 | request index : ibits}
     uint64_t* rec_sorted;
     int ibits;
     uint64_t imask;
+    int gshift;             // the hot-parameter batch's slot shift (ibits + 8); acquire code 255 = read req[i].acquire
+    uint32_t* msb;          // [kMaxPeriods] first request index of each millisecond of the batch (entry 0 unused)
+    int64_t* mt0;           // the batch's first timestamp
+    uint32_t* mnp;          // milliseconds the batch spans (> kMaxPeriods: the walkers read the timestamps)
     const PRule* rules;
     uint32_t n_rules;
     const sg_param_hot_item* hot;  // per rule, sorted by value
@@ -249,8 +254,11 @@ hipError_t launch_pslot_thread_read(const PSArgs& s, uint32_t res, int32_t idx, 
                                     hipStream_t stream);
 
 hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
-hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
-                              uint64_t** sorted_out, hipStream_t stream);
+// The long-segment walker runs on `aux` beside the short one (fork / join events).
+// sg: the length-class lists (short_list / short_count / class_off) and a zero error word for k_seg.
+hipError_t launch_param_batch(const PArgs& p, const BatchArgs& sg, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist,
+                              int lo_bit, int hi_bit, uint64_t** sorted_out, hipStream_t stream, hipStream_t aux,
+                              hipEvent_t fork, hipEvent_t join);
 
 // ---- pace controller: RateLimiterController per FlowRule (pace.hip) ----
 struct PaceRule {

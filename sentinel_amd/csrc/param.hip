@@ -16,10 +16,26 @@
 
 namespace sg {
 
+constexpr uint32_t kPAesc = 255;    // acquire code: read req[i].acquire
+constexpr uint32_t kPLdsMs = 4096;  // millisecond table entries staged in LDS (a batch spanning <= 4 s)
+
 __global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
+    const int64_t t0 = p.req[0].ts_ms;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
         const sg_param_req q = p.req[i];
-        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *p.last_ts : q.ts_ms < p.req[i - 1].ts_ms)) atomicOr(p.err, kErrTime);
+        const int64_t tp = i == 0 ? *p.last_ts : p.req[i - 1].ts_ms;
+        if (q.ts_ms < 0 || q.ts_ms < tp) atomicOr(p.err, kErrTime);
+        // the millisecond table: request index -> timestamp for the walkers (a new millisecond starts at i)
+        if (i == 0) {
+            *p.mt0 = q.ts_ms;
+        } else if (q.ts_ms > tp) {
+            for (int64_t ms = (tp < t0 ? t0 : tp) + 1; ms <= q.ts_ms; ++ms) {
+                const int64_t qq = ms - t0;
+                if (qq >= (int64_t)kMaxPeriods) break;
+                p.msb[qq] = (uint32_t)i;
+            }
+        }
+        if (i == p.n - 1) *p.mnp = (uint32_t)min(q.ts_ms - t0 + 1, (int64_t)kMaxPeriods + 1);
         if (q.acquire <= 0) atomicOr(p.err, kErrNonPositive);
         uint64_t rec = sentinel;
         int32_t pass = 0;
@@ -31,8 +47,9 @@ __global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
             const bool early_block = tc == 0 || (r.behavior != 2 && (int64_t)q.acquire > tc + r.burst);
             if (!early_block) {
                 const uint64_t g = param_slot(p, r, q.value);
+                const uint64_t ac = (q.acquire <= 0 || (uint64_t)q.acquire >= kPAesc) ? kPAesc : (uint64_t)q.acquire;
                 if (g == ~0ull) atomicOr(p.err, kErrTableFull);
-                else rec = (g << p.ibits) | i;
+                else rec = (g << p.gshift) | (ac << p.ibits) | i;
             }
         }
         p.out[i] = pass;
@@ -50,42 +67,85 @@ __device__ __forceinline__ uint32_t rule_of_slot(const PArgs& p, uint64_t g) {
     return lo;
 }
 
-__device__ void pwalk_serial(const PArgs& p, uint64_t g, uint64_t s, uint64_t e) {
+// The millisecond table in LDS (the hot-parameter walkers): request index -> exact timestamp (requests are
+// time-ordered), so a walker reads nothing per request but its sorted record.
+__shared__ uint32_t p_sms[kPLdsMs];
+__shared__ uint32_t p_nms;   // table entries, 0: read the timestamps
+__shared__ int64_t p_t0;
+
+__device__ __forceinline__ void p_stage_ms(const PArgs& p) {
+    const uint32_t np = *p.mnp;
+    const bool lds = np <= kPLdsMs;
+    for (uint32_t x = threadIdx.x; lds && x < np; x += blockDim.x) p_sms[x] = p.msb[x];
+    if (threadIdx.x == 0) {
+        p_nms = lds ? np : 0u;
+        p_t0 = *p.mt0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int64_t p_ts(const PArgs& p, uint32_t idx) {
+    const uint32_t np = p_nms;
+    if (np == 0) return p.req[idx].ts_ms;
+    uint32_t lo = 0, hi = np;  // the largest q with table[q] <= idx (entry 0 unused)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (p_sms[mid] <= idx) lo = mid;
+        else hi = mid;
+    }
+    return p_t0 + (int64_t)lo;
+}
+
+struct PDec {
+    uint32_t idx;
+    int64_t acq;
+};
+
+__device__ __forceinline__ PDec p_dec(const PArgs& p, uint64_t rec) {
+    PDec d;
+    d.idx = (uint32_t)(rec & p.imask);
+    const uint32_t ac = (uint32_t)(rec >> p.ibits) & 255u;
+    d.acq = ac == kPAesc ? (int64_t)p.req[d.idx].acquire : (int64_t)ac;
+    return d;
+}
+
+// Sequential replay of slot g's records from position s on (one lane), until the slot changes.
+__device__ void pwalk_serial(const PArgs& p, uint64_t g, uint64_t s) {
     const uint32_t ri = rule_of_slot(p, g);
     const PRule r = p.rules[ri];
     PSlot& slot = p.table[g];
     const uint64_t value = slot.value;  // the side slot's word stays ~0, which is its value
     const int64_t tc = param_token_count(p, r, value);
     PState st{slot.time, slot.tokens, slot.flags};
-    for (uint64_t j = s; j < e; ++j) {
-        const uint32_t idx = (uint32_t)(p.rec_sorted[j] & p.imask);
-        const int64_t t = p.req[idx].ts_ms;
-        const int64_t acq = p.req[idx].acquire;
+    uint64_t rec = p.rec_sorted[s];
+    for (uint64_t j = s; (rec >> p.gshift) == g;) {
+        const uint64_t nrec = ++j < p.n ? p.rec_sorted[j] : ~0ull;  // issued before this request is decided
+        const PDec d = p_dec(p, rec);
+        rec = nrec;
+        const int64_t t = p_ts(p, d.idx);
         bool ok;
-        if (r.behavior == 2) ok = param_throttle_step(st, throttle_cost(r, tc, acq), r.max_queueing_ms, t);
-        else ok = param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, acq);
-        if (ok) p.out[idx] = 1;
+        if (r.behavior == 2) ok = param_throttle_step(st, throttle_cost(r, tc, d.acq), r.max_queueing_ms, t);
+        else ok = param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, d.acq);
+        if (ok) p.out[d.idx] = 1;
     }
     slot.time = st.time;
     slot.tokens = st.tokens;
     slot.flags = st.flags;
 }
 
-__global__ void __launch_bounds__(256) k_pwalk_short(PArgs p) {
+// One lane per segment of at most short_max records, from k_seg's length-class lists (longest class first, so the
+// lanes of a wave walk segments of similar length).
+__global__ void __launch_bounds__(256) k_pwalk_short(PArgs p, BatchArgs sg) {
     if (*p.err & ~kErrNonPositive) return;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < p.n; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t rec = p.rec_sorted[j];
-        const uint64_t g = rec >> p.ibits;
-        if (g >= p.total_slots) continue;  // rejected before the maps
-        if (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g) continue;
-        uint64_t e = j + 1;
-        while (e < p.n && e - j <= (uint64_t)p.short_max && (p.rec_sorted[e] >> p.ibits) == g) ++e;
-        if (e - j > (uint64_t)p.short_max) {
-            const uint32_t pos = atomicAdd(p.long_count, 1u);
-            p.long_list[pos] = (uint32_t)j;
-            continue;
-        }
-        pwalk_serial(p, g, j, e);
+    p_stage_ms(p);
+    uint32_t total = 0;
+    for (int k = 0; k < kClasses; ++k) total += sg.short_count[k];
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+        uint32_t r0 = u;
+        int k = kClasses - 1;
+        while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k--];
+        const uint64_t j = sg.short_list[sg.class_off[k] + r0];
+        pwalk_serial(p, p.rec_sorted[j] >> p.gshift, j);
     }
 }
 
@@ -141,11 +201,10 @@ __device__ void pwalk_wave_default(const PArgs& p, const PRule& r, int64_t tc, P
     while (pos < e) {
         // sequential head: first sight / refill zone
         {
-            const uint32_t idx = (uint32_t)(p.rec_sorted[pos] & p.imask);
-            const int64_t t = p.req[idx].ts_ms;
+            const PDec d = p_dec(p, p.rec_sorted[pos]);
+            const int64_t t = p_ts(p, d.idx);
             if (!(st.flags & 1u) || t - st.time > dur_ms) {
-                const int64_t acq = p.req[idx].acquire;
-                if (param_default_step(st, tc, maxc, dur_ms, t, acq) && lane == 0) p.out[idx] = 1;
+                if (param_default_step(st, tc, maxc, dur_ms, t, d.acq) && lane == 0) p.out[d.idx] = 1;
                 ++pos;
                 continue;
             }
@@ -153,7 +212,7 @@ __device__ void pwalk_wave_default(const PArgs& p, const PRule& r, int64_t tc, P
         // no-refill zone: requests with t <= time + duration
         const int64_t zone_end_t = st.time + dur_ms;
         const uint64_t z = pwave_search(pos, e, [&](uint64_t q) {
-            return p.req[(uint32_t)(p.rec_sorted[q] & p.imask)].ts_ms > zone_end_t;
+            return p_ts(p, (uint32_t)(p.rec_sorted[q] & p.imask)) > zone_end_t;
         }, lane);
         while (pos < z) {
             if (all_positive && st.tokens < 1) {  // nothing fits until the refill: all blocked
@@ -162,12 +221,10 @@ __device__ void pwalk_wave_default(const PArgs& p, const PRule& r, int64_t tc, P
             }
             const uint64_t j = pos + (uint64_t)lane;
             const bool act = j < z;
-            uint32_t idx = 0;
-            int64_t acq = 0;
-            if (act) {
-                idx = (uint32_t)(p.rec_sorted[j] & p.imask);
-                acq = p.req[idx].acquire;
-            }
+            PDec d{0, 0};
+            if (act) d = p_dec(p, p.rec_sorted[j]);
+            const uint32_t idx = d.idx;
+            const int64_t acq = d.acq;
             uint64_t pending = __ballot(act);
             while (pending) {
                 const bool pl = (pending >> lane) & 1ull;
@@ -203,9 +260,10 @@ __device__ void pwalk_wave_throttle(const PArgs& p, const PRule& r, int64_t tc, 
         uint32_t idx = 0;
         int64_t t = 0, cost = 0;
         if (act) {
-            idx = (uint32_t)(p.rec_sorted[j] & p.imask);
-            t = p.req[idx].ts_ms;
-            cost = throttle_cost(r, tc, p.req[idx].acquire);
+            const PDec d = p_dec(p, p.rec_sorted[j]);
+            idx = d.idx;
+            t = p_ts(p, idx);
+            cost = throttle_cost(r, tc, d.acq);
         }
         uint64_t pending = __ballot(act);
         while (pending) {
@@ -235,15 +293,16 @@ __device__ void pwalk_wave_throttle(const PArgs& p, const PRule& r, int64_t tc, 
 
 __global__ void __launch_bounds__(256) k_pwalk_long(PArgs p) {
     if (*p.err & ~kErrNonPositive) return;
+    p_stage_ms(p);
     const uint32_t cnt = *p.long_count;
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const int lane = (int)__lane_id();
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint64_t s = p.long_list[w];
-        const uint64_t g = p.rec_sorted[s] >> p.ibits;
+        const uint64_t g = p.rec_sorted[s] >> p.gshift;
         const uint64_t e = pwave_search(s + p.short_max, p.n, [&](uint64_t q) {
-            return (p.rec_sorted[q] >> p.ibits) != g;
+            return (p.rec_sorted[q] >> p.gshift) != g;
         }, lane);
         const uint32_t ri = rule_of_slot(p, g);
         const PRule r = p.rules[ri];
@@ -290,9 +349,10 @@ hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist, int lo_bit, int hi_bit,
-                              uint64_t** sorted_out, hipStream_t stream) {
-    const uint64_t sentinel = p.total_slots << p.ibits;
+hipError_t launch_param_batch(const PArgs& p, const BatchArgs& sg, uint64_t* a_buf, uint64_t* b_buf, uint32_t* hist,
+                              int lo_bit, int hi_bit, uint64_t** sorted_out, hipStream_t stream, hipStream_t aux,
+                              hipEvent_t fork, hipEvent_t join) {
+    const uint64_t sentinel = p.total_slots << p.gshift;
     hipLaunchKernelGGL(k_pprep, dim3(pgrid(p.n, 8192)), dim3(256), 0, stream, p, sentinel);
     uint64_t* sorted = nullptr;
     hipError_t e = radix_sort_records(a_buf, b_buf, p.n, lo_bit, hist, &sorted, stream, hi_bit);
@@ -300,9 +360,27 @@ hipError_t launch_param_batch(const PArgs& p, uint64_t* a_buf, uint64_t* b_buf, 
     PArgs q = p;
     q.rec_sorted = sorted;
     *sorted_out = sorted;
-    hipLaunchKernelGGL(k_pwalk_short, dim3(pgrid(p.n, 16384)), dim3(256), 0, stream, q);
+    // segments of the sorted records in length-class lists (k_seg; its error word is a zero word: kErrNonPositive
+    // is not an error), then the wave walker on aux beside the lane walker
+    BatchArgs sgb = sg;
+    sgb.n = p.n;
+    sgb.rec_sorted = sorted;
+    sgb.kshift = p.gshift;
+    sgb.K = (uint32_t)p.total_slots;
+    sgb.long_list = p.long_list;
+    sgb.long_count = p.long_count;
+    sgb.short_max = p.short_max;
+    e = launch_seg(sgb, stream);
+    if (e != hipSuccess) return e;
     const uint64_t max_long = p.n / ((uint64_t)p.short_max + 1) + 1;
-    hipLaunchKernelGGL(k_pwalk_long, dim3(pgrid(max_long * 64, 2048)), dim3(256), 0, stream, q);
+    e = hipEventRecord(fork, stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_pwalk_long, dim3(pgrid(max_long * 64, 2048)), dim3(256), 0, aux, q);
+    hipLaunchKernelGGL(k_pwalk_short, dim3(pgrid(p.n / 4, 8192)), dim3(256), 0, stream, q, sgb);
+    e = hipEventRecord(join, aux);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_pfinish, dim3(1), dim3(1), 0, stream, q);
     return hipGetLastError();
 }

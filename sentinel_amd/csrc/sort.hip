@@ -295,9 +295,9 @@ size_t radix_hist_words(uint64_t n) {
     return (size_t)((ntiles + nchunks + 1) * (1ull << kMaxDigit) + 64);  // rows, chunk sums, digit totals
 }
 
-// Digit width of a sort over `bits` key bits: 8-bit digits, except 2 passes of 10 bits for 17..20 bits (one pass
-// of memory traffic fewer than three 8-bit passes).
-int radix_digit_bits(int bits) { return (bits > 16 && bits <= 20) ? 10 : 8; }
+// Digit width of a sort over `bits` key bits: 8-bit digits, except 10-bit ones where they save a pass: 2 passes for
+// 17..20 bits (the C3 flowIds), 3 for 25..30 (hot-parameter value slots) instead of 3 / 4 8-bit passes.
+int radix_digit_bits(int bits) { return ((bits > 16 && bits <= 20) || (bits > 24 && bits <= 30)) ? 10 : 8; }
 
 template <int D>
 static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
