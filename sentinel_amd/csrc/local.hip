@@ -740,9 +740,32 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
     uint64_t xi = may_skip ? lwave_search(0, ne, [&](uint64_t i) { return (uint64_t)a.exit_pos[i] >= s; }, lane) : ne;
     uint32_t pe_qs = 0xFFFFFFFFu, pe_qm = 0xFFFFFFFFu;
     uint64_t pe = 0;
+    // the next chunk's records and event timestamps are loaded while this chunk is decided (records at the chunk's
+    // start, events once its records have arrived): two dependent loads per chunk off the critical path. Loads are
+    // unconditional with clamped indices; lanes past the segment ignore what they read.
+    const uint64_t n1 = a.n - 1;
+    auto ev_ts = [&](uint64_t rec, int64_t& tt, int64_t& cc) {  // exits always (rt, statistic window); entries
+        const LEvent x = ldecode(a, rec);                         // only when breakers may need them
+        const sg_local_event* le = a.ev + min((uint64_t)x.idx, n1);
+        const bool need = x.kind != SG_LOCAL_ENTRY || nb > 0;
+        tt = need ? le->ts_ms : 0;
+        cc = need ? le->create_ts : 0;
+    };
+    uint64_t pf = s;  // position of the prefetched chunk
+    uint64_t rec_n = a.rec_sorted[min(s + lane, n1)];
+    int64_t t_n, c_n;
+    ev_ts(rec_n, t_n, c_n);
     for (uint64_t base = s; base < e_end;) {
         const uint64_t j = base + lane;
         const bool act = j < e_end;
+        if (pf != base) {  // wave-uniform: a skip moved past the prefetched chunk
+            rec_n = a.rec_sorted[min(j, n1)];
+            ev_ts(rec_n, t_n, c_n);
+        }
+        const uint64_t rec_c = rec_n;
+        const int64_t t_c = t_n, c_c = c_n;
+        pf = base + 64;
+        rec_n = a.rec_sorted[min(pf + lane, n1)];
         LEvent ev;
         ev.idx = 0;
         ev.count = 0;
@@ -752,15 +775,11 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
         uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
         int64_t sw0 = 0, sw1 = 0;  // breaker statistic windows of this event (exits)
         if (act) {
-            ev = ldecode(a, a.rec_sorted[j]);
+            ev = ldecode(a, rec_c);
             qs = nd.cs.of(ev.idx);
             qm = nd.cm.of(ev.idx);
-            // timestamps: exits always (rt, statistic window); entries only when breakers may need them
-            if (ev.kind != SG_LOCAL_ENTRY || nb > 0) {
-                const sg_local_event le = a.ev[ev.idx];
-                t = le.ts_ms;
-                create = le.create_ts;
-            }
+            t = t_c;
+            create = c_c;
             if (ev.kind != SG_LOCAL_ENTRY) {
                 if (nb > 0) sw0 = t - t % nd.R.b[0].stat_ms;
                 if (nb > 1) sw1 = t - t % nd.R.b[1].stat_ms;
@@ -928,6 +947,7 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
             }
             pos = rend;
         }
+        ev_ts(rec_n, t_n, c_n);  // the next chunk's events (its records have arrived meanwhile)
         // dead-period skip: the open second window admits nothing any more → jump to the first of (end of
         // this second-window period, end of this minute period, next exit of the resource); k_lskip_apply
         // adds the skipped entries' BLOCK counts to both windows
