@@ -493,8 +493,8 @@ __device__ __forceinline__ bool cp_prologue(const CPArgs& c, const CPBatch& b, u
 // Sequential replay of the records [j, ...) of slot g (one lane). Single-value requests: window check and add.
 // A multi-value request's records in this slot (repeated values) check the state before the request, and add
 // its count each iff its outcome is assumed to be a pass and the check passed. Needs cp_stage_periods.
-__device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j) {
-    const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+__device__ void cp_walk_serial_mem(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j,
+                                   const CPRule& r) {
     const double thr = cp_threshold(c, r, c.keys[g]);
     CPBucket* ring = c.ring + g * (uint64_t)c.stride;
     const int S = r.S;
@@ -555,6 +555,105 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
         bk.count = cur;
         ring[(int)(P % S)] = bk;
     }
+}
+
+// cp_walk_serial with the slot's ring in registers (sampleCount <= SM): the ring is read once, with all loads issued
+// together, and the changed buckets are written back at the end — the memory version reads S buckets at every
+// window-period change, a dependent round trip per period of a slot's records.
+template <int SM>
+__device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j,
+                                   const CPRule& r) {
+    const double thr = cp_threshold(c, r, c.keys[g]);
+    CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+    const int S = r.S;
+    const int64_t wl = r.wl;
+    int64_t bs[SM], bc[SM];
+#pragma unroll
+    for (int x = 0; x < SM; ++x) {
+        const CPBucket bk = ring[x < S ? x : 0];
+        bs[x] = x < S ? bk.start : INT64_MIN;
+        bc[x] = bk.count;
+    }
+    uint32_t dirty = 0;
+    int64_t P = INT64_MIN, other = 0, cur = 0;
+    uint32_t qn = 0xFFFFFFFFu;  // first request index of the period after P (monotone cursor)
+    uint32_t mi = kNoOwner;     // the multi-value request of the previous record, and its check here
+    bool mok = false;
+    auto close = [&]() {  // the open period's bucket into the register ring
+        if (P == INT64_MIN) return;
+        const int xo = (int)(P % S);
+#pragma unroll
+        for (int x = 0; x < SM; ++x) {
+            if (x == xo) {
+                bs[x] = P * wl;
+                bc[x] = cur;
+            }
+        }
+        dirty |= 1u << xo;
+    };
+    uint64_t rec = sg.rec_sorted[j];
+    while ((rec >> b.pbits) == g) {
+        const uint64_t nrec = j + 1 < sg.n ? sg.rec_sorted[j + 1] : ~0ull;  // issued before this record is decided
+        const CPRec d = cp_dec(c, b, rec);
+        const uint32_t i = d.i;
+        rec = nrec;
+        ++j;
+        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;  // allowProceed refused it
+        if (d.multi && i == mi) {  // a repeated value: the check of the request's first record here, and its add
+            b.chk[d.p] = mok ? 1 : 0;
+            if (b.assume[i] && mok) cur += d.acq;
+            continue;
+        }
+        if (P == INT64_MIN || i >= qn) {  // currentWindow(t): close the open period, open this one
+            close();
+            P = cp_period(b, r.wl_idx, i);
+            const int I = (int)(P % S);
+            const int64_t ws = P * wl, lo = ws - (int64_t)(S - 1) * wl;
+            other = 0;
+            cur = 0;
+#pragma unroll
+            for (int x = 0; x < SM; ++x) {
+                const bool v = x < S && x != I && bs[x] != INT64_MIN && bs[x] >= lo;
+                other += v ? bc[x] : 0;
+                if (x == I) cur = bs[x] == ws ? bc[x] : 0;
+            }
+            const uint32_t q1 = (uint32_t)(P - cp_p0[r.wl_idx]) + 1;
+            qn = q1 < cp_np[r.wl_idx] ? (cp_blds ? cp_sbnd[cp_boff[r.wl_idx] + q1]
+                                                  : b.bnd[(size_t)r.wl_idx * kMaxPeriods + q1])
+                                      : 0xFFFFFFFFu;
+        }
+        const double rem = thr - (double)(other + cur) / r.isec - (double)d.acq;
+        if (!d.multi) {
+            mi = kNoOwner;
+            if (rem >= 0) {
+                cur += d.acq;
+                cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
+            } else {
+                cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+            }
+            continue;
+        }
+        mi = i;
+        mok = rem >= 0;
+        b.chk[d.p] = mok ? 1 : 0;
+        if (b.assume[i] && mok) cur += d.acq;
+    }
+    close();
+#pragma unroll
+    for (int x = 0; x < SM; ++x) {
+        if ((dirty >> x) & 1u) {
+            CPBucket bk;
+            bk.start = bs[x];
+            bk.count = bc[x];
+            ring[x] = bk;
+        }
+    }
+}
+
+__device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j) {
+    const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+    if (r.S <= 10) cp_walk_serial_reg<10>(c, b, sg, g, j, r);
+    else cp_walk_serial_mem(c, b, sg, g, j, r);
 }
 
 // One lane per slot of at most short_max records. Work item t: the slot's index in the save area (the long
