@@ -760,7 +760,10 @@ __device__ __forceinline__ int64_t cp_wave_sum(int64_t v) {
 
 enum : int { kCpSkip = 0, kCpSingle = 1, kCpMulti = 2, kCpDup = 3 };
 __device__ __forceinline__ uint64_t cp_below(int f) { return f >= 64 ? ~0ull : ((1ull << f) - 1ull); }
-constexpr int kCpU = 4;  // 64-record chunks whose loads are issued together (three dependent round trips per block)
+#ifndef SG_CPU
+#define SG_CPU 2
+#endif
+constexpr int kCpU = SG_CPU;  // 64-record chunks whose loads are issued together (three dependent round trips per block)
 constexpr uint64_t kCpSkipMin = 256;     // shortest saturated tail worth handing to k_cp_skipfill (records)
 constexpr uint64_t kCpSkipPiece = 4096;  // skipped ranges go to k_cp_skipfill in pieces of this size
 
