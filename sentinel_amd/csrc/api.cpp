@@ -2174,7 +2174,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         dfree(h->d_cp_rec2);
         dfree(h->d_cp_hist);
         dfree(h->d_cp_items);
-        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 7 * nv) != hipSuccess ||
+        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 8 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_pslot, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
@@ -2231,6 +2231,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     b.item_start = h->d_cp_items + nv;           // [nv]
     b.slot_item = h->d_cp_slot_item;
     b.item_end = h->d_cp_items + 6 * nv;         // [nv]
+    b.item_slot = h->d_cp_items + 7 * nv;        // [nv]
     b.dcap = (uint32_t)nv;                       // re-walk lists: 2 buffers x {long, short} x nv
     b.mlist = h->d_cp_mlist;
     b.mcount = h->d_cp_counts + 4;

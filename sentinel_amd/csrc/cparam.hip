@@ -704,6 +704,7 @@ __global__ void __launch_bounds__(256) k_cp_items(CPBatch b, BatchArgs sg) {
         }
         const uint64_t g = sg.rec_sorted[j] >> b.pbits;
         b.item_start[t] = (uint32_t)j;
+        b.item_slot[t] = (uint32_t)g;
         b.slot_item[g] = t;
         // the segment's end: exponential then binary search (once per batch; every round's walkers reuse it)
         uint64_t lo = j, step = 1, hi = j + 1;
@@ -791,17 +792,28 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const uint32_t cnt = b.round > 0 ? b.din_count[0] : *sg.long_count;
+    // the item headers (work item, segment bounds, slot) are loaded one item ahead: a slot's header is otherwise a
+    // chain of three dependent round trips before its first record
+    if (cnt == 0 || wave >= cnt) return;  // (after the block-wide staging)
+    const uint32_t last = cnt - 1;
+    uint32_t tq = b.round > 0 ? b.din[min(wave, last)] : min(wave, last);  // rounds > 0: the re-walk list
+    uint64_t sq = b.item_start[tq], eq = b.item_end[tq], gq = b.item_slot[tq];
     for (uint32_t x = wave; x < cnt; x += nwaves) {
-        const uint32_t t = b.round > 0 ? b.din[x] : x;  // rounds > 0: the re-walk list of long items
-        const uint64_t s = b.round > 0 ? (uint64_t)b.item_start[t] : (uint64_t)sg.long_list[t];
-        const uint64_t g = sg.rec_sorted[s] >> b.pbits;
+        const uint32_t t = tq;
+        const uint64_t s = sq, e = eq, g = gq;
+        {
+            const uint32_t xn = min(x + nwaves, last);
+            tq = b.round > 0 ? b.din[xn] : xn;
+            sq = b.item_start[tq];
+            eq = b.item_end[tq];
+            gq = b.item_slot[tq];
+        }
         if (!cp_prologue(c, b, g, t, lane, 64)) continue;
         const CPRule r = c.rules[cp_rule_of_slot(c, g)];
         if (r.S > 64) {  // the ring does not fit the wave's registers
             if (lane == 0) cp_walk_serial(c, b, sg, g, s);
             continue;
         }
-        const uint64_t e = b.item_end[t];
         const double thr = cp_threshold(c, r, c.keys[g]);
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
         const int S = r.S;

@@ -360,6 +360,7 @@ struct CPBatch {
     uint32_t* dflag;          // [work items] the item is listed for the next re-walk (an assumed outcome changed)
     uint32_t* item_start;     // [work items] segment start of item t (long items first, then short: k_cp_items)
     uint32_t* item_end;       // [work items] its end
+    uint32_t* item_slot;      // [work items] its slot
     uint32_t* slot_item;      // [total slots] work item of each slot this batch touches
     uint32_t* din;            // re-walk lists walked this round: [2][dcap] long / short items
     uint32_t* din_count;      // [2]
