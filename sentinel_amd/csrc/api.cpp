@@ -2247,7 +2247,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         h->cp_rounds = 0;
         if (err & kErrTime) return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
         if (err & kErrBounds) return fail(h, SG_E_INVAL, "a request's values lie outside the value array");
-        if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 limiter periods");
+        if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window or limiter periods");
         return SG_OK;
     }
     uint64_t* sorted = nullptr;
@@ -2389,7 +2389,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     if (err & kErrBounds)
         return fail(h, SG_E_INVAL, "a request's values lie outside the value array, overlap another's or go backwards");
     if (err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param rule's value table is full");
-    if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 limiter periods");
+    if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window or limiter periods");
     return SG_OK;
 }
 
