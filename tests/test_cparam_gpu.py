@@ -241,3 +241,36 @@ def test_value_range_contract():
             eng.cparam_decide_host(bad, bv if mutate == "backwards" else nvals)
     _check(eng, ora, nxt, nvals)   # the rejected batches left nothing behind
     _compare_sums(eng, ora, nxt, nvals, int(nxt["ts_ms"][-1]))
+
+
+@pytest.mark.parametrize("flags", WALKERS)
+def test_mixed_window_lengths(flags):
+    """Rules of one handle with different window shapes: each distinct windowIntervalMs / sampleCount gets its own
+    period table (request index -> window period) in the batch; single- and multi-value requests over all of them."""
+    rng = np.random.default_rng(61)
+    shapes = [(10, 1000), (2, 1000), (1, 500), (5, 25), (4, 2000), (3, 300), (10, 1000), (2, 1000)]
+    rules = _rules(len(shapes) * 3, rng)
+    for i in range(len(rules)):
+        rules["sample_count"][i], rules["window_interval_ms"][i] = shapes[i % len(shapes)]
+    eng, ora = _pair(rules, flags=flags)
+    t = 1_700_000_000_123
+    for _ in range(3):
+        req, vals = _trace(rng, 30_000, len(rules), 40, t, 2500, multi=0.15, bad=0.01)
+        _check(eng, ora, req, vals)
+        t = int(req["ts_ms"][-1]) + 3
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_more_than_eight_window_lengths_refused():
+    """Nine distinct window lengths do not fit the batch's period tables: SG_E_UNSUPPORTED at load."""
+    from sentinel_amd.engine import EngineError, FlowEngine
+    rng = np.random.default_rng(62)
+    rules = _rules(9, rng, S=1)
+    rules["window_interval_ms"] = np.arange(9) * 100 + 100
+    eng = FlowEngine(device=0, max_batch=1 << 16)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    eng.set_namespaces(ns)
+    with pytest.raises(EngineError):
+        eng.cparam_load_rules(rules, None, 10)
+    eng.cparam_load_rules(rules[:8], None, 10)  # eight are fine

@@ -133,3 +133,20 @@ def test_param_unknown_rule_passes_and_time_errors():
     with pytest.raises(EngineError) as ei:
         eng.param_decide_host(bad)
     assert ei.value.code == abi.SG_E_TIME
+
+
+@pytest.mark.parametrize("flags", WALKERS)
+@pytest.mark.parametrize("span", [3_000, 20_000, 100_000])
+def test_batch_spans_and_large_acquire(span, flags):
+    """The walkers recover each request's timestamp from the batch's millisecond table (request index -> ts, staged in
+    LDS up to 4096 ms; longer batches read the timestamps) and its acquireCount from the record's 8-bit code (255 and
+    above read the request): spans across both table regimes and past the 65,536-entry table, counts up to 300."""
+    rng = np.random.default_rng(span)
+    rules = _rules([{"count": 50, "duration": 1, "burst": 20}, {"count": 400, "duration": 2},
+                    {"count": 8, "behavior": abi.BEHAVIOR_RATE_LIMITER, "max_queue": 500}])
+    eng, ora = _pair(rules, flags=flags)
+    t = 1_700_000_000_000
+    for _ in range(2):
+        req = _trace(rng, 40_000, len(rules), 300, t, span, acq_hi=300)
+        _check(eng, ora, req)
+        t = int(req["ts_ms"][-1]) + 1
