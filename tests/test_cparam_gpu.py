@@ -274,3 +274,32 @@ def test_more_than_eight_window_lengths_refused():
     with pytest.raises(EngineError):
         eng.cparam_load_rules(rules, None, 10)
     eng.cparam_load_rules(rules[:8], None, 10)  # eight are fine
+
+
+@pytest.mark.parametrize("flags", WALKERS)
+def test_long_spans_and_large_acquire(flags):
+    """Value records carry a 7-bit acquire code (127 and above read the request) and the walkers take window periods
+    from the batch's period tables — staged in LDS up to 2048 periods, read from memory beyond (4000 here)."""
+    rng = np.random.default_rng(63)
+    rules = _rules(12, rng)
+    rules["count"] = rng.integers(100, 2000, len(rules))
+    eng, ora = _pair(rules, flags=flags)
+    t = 1_700_000_000_000
+    for _ in range(2):
+        req, vals = _trace(rng, 20_000, len(rules), 30, t, 400_000, multi=0.1, acq_hi=300)
+        _check(eng, ora, req, vals)
+        t = int(req["ts_ms"][-1]) + 1
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def test_batch_past_the_period_table_refused():
+    """A batch spanning more than 65,536 window periods of some rule is refused before anything is charged."""
+    from sentinel_amd.engine import EngineError
+    rng = np.random.default_rng(64)
+    rules = _rules(4, rng, S=10, interval=10)  # 1 ms periods
+    eng, ora = _pair(rules)
+    req, vals = _trace(rng, 5_000, len(rules), 20, 1_700_000_000_000, 70_000)
+    with pytest.raises(EngineError):
+        eng.cparam_decide_host(req, vals)
+    req, vals = _trace(rng, 5_000, len(rules), 20, 1_700_000_100_000, 30_000)
+    _check(eng, ora, req, vals)
