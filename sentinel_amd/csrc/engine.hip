@@ -804,19 +804,33 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
 // it), k_seg_classify walks the flowId range in order, turns each marked key into a list entry {start, end, key}
 // of its length class (or the long list) and clears the mark for the next batch. Both run whatever the batch's
 // error flags (the marks must be consumed); the walkers check them.
+constexpr int kMarkItems = 16;  // 64-record rows per wave of k_seg_mark, all loaded at once
+
 __global__ void __launch_bounds__(256) k_seg_mark(BatchArgs a) {
     const uint64_t n = a.n;
-    const int lane = lane_id();
-    for (uint64_t j0 = (uint64_t)blockIdx.x * 256 + (threadIdx.x & ~63u); j0 < n; j0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t j = j0 + lane;
-        const uint32_t key = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
-        uint32_t kp = (uint32_t)__shfl_up((int)key, 1u, 64);
-        if (lane == 0) kp = j0 > 0 ? (uint32_t)(a.rec_sorted[j0 - 1] >> a.kshift) : 0xFFFFFFFFu;
-        if (j < n && key != kp) {
-            if (key < a.K) a.seg_start[key] = (uint32_t)j;
+    const int lane = lane_id(), wave = threadIdx.x >> 6;
+    // row u of wave w covers records t0 + (w*kMarkItems + u)*64 + lane: one load round trip per thread (this runs at
+    // the end of the front half, on the pipeline's critical path)
+    const uint64_t t0 = (uint64_t)blockIdx.x * (256 * kMarkItems);
+    const uint64_t jw = t0 + ((uint64_t)(wave * kMarkItems) << 6);  // the wave's first record
+    uint32_t key[kMarkItems];
+#pragma unroll
+    for (int u = 0; u < kMarkItems; ++u) {
+        const uint64_t j = jw + ((uint64_t)u << 6) + lane;
+        key[u] = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
+    }
+    const uint32_t before = (jw > 0 && jw < n) ? (uint32_t)(a.rec_sorted[jw - 1] >> a.kshift) : 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < kMarkItems; ++u) {
+        const uint64_t j = jw + ((uint64_t)u << 6) + lane;
+        const uint32_t row_prev = u == 0 ? before : (uint32_t)__shfl((int)key[u - 1], 63, 64);  // all lanes active
+        uint32_t kp = (uint32_t)__shfl_up((int)key[u], 1u, 64);
+        if (lane == 0) kp = row_prev;
+        if (j < n && key[u] != kp) {
+            if (key[u] < a.K) a.seg_start[key[u]] = (uint32_t)j;
             if (kp < a.K) a.seg_end[kp] = (uint32_t)j;
         }
-        if (j == n - 1 && key < a.K) a.seg_end[key] = (uint32_t)n;
+        if (j == n - 1 && key[u] < a.K) a.seg_end[key[u]] = (uint32_t)n;
     }
 }
 
@@ -1816,7 +1830,8 @@ hipError_t launch_seg(const BatchArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_seg_mark, dim3(grid_for(a.n, 256 * 16, 8192)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_seg_mark, dim3((unsigned)((a.n + 256 * kMarkItems - 1) / (256 * kMarkItems))), dim3(256), 0,
+                       stream, a);
     if (a.K) hipLaunchKernelGGL(k_seg_classify, dim3(grid_for(a.K, 256 * kClsItems, 4096)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
