@@ -2200,7 +2200,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
                             hipMalloc(&h->d_cp_mlist, sizeof(uint32_t) * h->cfg.max_batch) != hipSuccess))
         return fail(h, SG_E_NOMEM, "cparam batch scratch");
     if (!h->d_cp_assume && (hipMalloc(&h->d_cp_assume, h->cfg.max_batch) != hipSuccess ||
-                            hipMalloc(&h->d_cp_changed, sizeof(int)) != hipSuccess))
+                            hipMalloc(&h->d_cp_changed, sizeof(int) * (2 + (size_t)h->cp_max_rounds)) != hipSuccess))
         return fail(h, SG_E_NOMEM, "cparam batch scratch");
     int rc = cp_rule_limiters(h, stream);
     if (rc) return rc;
@@ -2355,26 +2355,40 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream, h->aux, h->fork, h->join));
         converged = true;
     }
-    while (!err && !converged && round < kMaxRounds) {
-        b.round = (int)round;
-        // this round walks the lists the previous combine filled (buffer round & 1), and combine fills the other
-        b.din = h->d_cp_items + (size_t)(2 + 2 * (round & 1)) * nv;
-        b.din_count = h->d_cp_counts + 2 * (round & 1);
-        b.dout = h->d_cp_items + (size_t)(2 + 2 * ((round + 1) & 1)) * nv;
-        b.dout_count = h->d_cp_counts + 2 * ((round + 1) & 1);
-        HIP_TRY(h, hipMemsetAsync(h->d_cp_changed, 0, sizeof(int), stream));
+    // Rounds are enqueued kChain at a time and the host reads their flags once per chain (a host round trip costs
+    // ~90 us between rounds): round r's combine sets flag r (d_cp_changed[1 + r]) iff an outcome changed, and a round
+    // after one that changed nothing returns at once (its lists are empty, combine and relist check the flags).
+    // Each round's counters are zeroed on the device: dout_count by combine, skip_count by relist.
+    constexpr uint32_t kChain = 3;
+    if (!err && !converged) {
+        HIP_TRY(h, hipMemsetAsync(h->d_cp_changed + 1, 0, sizeof(int) * (1 + (size_t)kMaxRounds), stream));
         HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), stream));
-        HIP_TRY(h, hipMemsetAsync(b.dout_count, 0, 2 * sizeof(uint32_t), stream));
-        HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream, h->aux, h->fork, h->join));
-        HIP_TRY(h, launch_cp_combine(c, b, sgm, touched, stream));
-        int changed = 0;
-        HIP_TRY(h, hipMemcpyAsync(&changed, h->d_cp_changed, sizeof(int), hipMemcpyDeviceToHost, stream));
+    }
+    while (!err && !converged && round < kMaxRounds) {
+        const uint32_t r0 = round, r1 = std::min(round + kChain, kMaxRounds);
+        for (uint32_t r = r0; r < r1; ++r) {
+            b.round = (int)r;
+            // this round walks the lists the previous combine filled (buffer r & 1), and combine fills the other
+            b.din = h->d_cp_items + (size_t)(2 + 2 * (r & 1)) * nv;
+            b.din_count = h->d_cp_counts + 2 * (r & 1);
+            b.dout = h->d_cp_items + (size_t)(2 + 2 * ((r + 1) & 1)) * nv;
+            b.dout_count = h->d_cp_counts + 2 * ((r + 1) & 1);
+            b.changed = h->d_cp_changed + 1 + r;
+            b.changed_prev = r > 0 ? h->d_cp_changed + r : nullptr;
+            HIP_TRY(h, launch_cp_walk2(c, b, sgm, stream, h->aux, h->fork, h->join));
+            HIP_TRY(h, launch_cp_combine(c, b, sgm, touched, stream));
+        }
+        int changed[kChain] = {0, 0, 0};
+        HIP_TRY(h, hipMemcpyAsync(changed, h->d_cp_changed + 1 + r0, sizeof(int) * (r1 - r0), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipStreamSynchronize(stream));
-        ++round;
-        if (!changed) {
-            converged = true;
-            break;
+        round = r1;
+        for (uint32_t r = r0; r < r1; ++r) {
+            if (!changed[r - r0]) {
+                converged = true;
+                round = r + 1;
+                break;
+            }
         }
     }
     if (!err && !converged) {  // rare: the batch on one thread, from the saved rings

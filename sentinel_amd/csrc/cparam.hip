@@ -394,7 +394,10 @@ __global__ void __launch_bounds__(256) k_cp_prep2(CPArgs c, CPBatch b) {
             atomicOr(c.err, kErrBounds);
             continue;
         }
-        if (q.value_count > 1) *b.changed = 1;  // vector store; the host reads it as "has multi-value requests"
+        if (q.value_count > 1) {
+            *b.changed = 1;    // vector store; the host reads it as "has multi-value requests"
+            b.assume[i] = 3;   // assumed to pass, listed by k_cp_mlist
+        }
         const CPRule r = c.rules[key];
         for (uint32_t j = 0; j < q.value_count; ++j) {
             const uint64_t p = (uint64_t)q.value_begin + j;
@@ -440,27 +443,31 @@ __device__ __forceinline__ uint32_t cp_block_excl_scan(uint32_t v, uint32_t* wsu
     return off;
 }
 
-// The valid multi-value requests: k_cp_combine's work list (any order).
+// The valid multi-value requests (k_cp_prep2 flagged them in assume[], bit 1): k_cp_combine's work list (any order).
+// A thread reads the flag bytes of kAggItems consecutive requests at once.
 __global__ void __launch_bounds__(256) k_cp_mlist(CPArgs c, CPBatch b) {
     __shared__ uint32_t wsum[4], gbase;
-    const uint64_t base = (uint64_t)blockIdx.x * (256 * kAggItems);
-    bool m[kAggItems];
-    uint32_t cnt = 0;
+    const uint64_t i0 = (uint64_t)blockIdx.x * (256 * kAggItems) + (uint64_t)threadIdx.x * kAggItems;
+    static_assert(kAggItems == 16, "one 16-byte load of flags per thread");
+    uint32_t m = 0;
+    if (i0 + kAggItems <= c.n) {
+        const uint4 v = *(const uint4*)(b.assume + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int u = 0; u < kAggItems; ++u) {
-        const uint64_t i = base + (uint64_t)u * 256 + threadIdx.x;
-        const sg_cparam_req q = c.req[min(i, c.n - 1)];
-        m[u] = i < c.n && q.value_count > 1 && cp_valid(c, q) && (uint64_t)q.value_begin + q.value_count <= c.n_values;
-        cnt += m[u] ? 1u : 0u;
+        for (int u = 0; u < kAggItems; ++u) m |= ((w[u >> 2] >> (8 * (u & 3) + 1)) & 1u) << u;
+    } else {
+        for (int u = 0; u < kAggItems && i0 + u < c.n; ++u) m |= ((b.assume[i0 + u] >> 1) & 1u) << u;
     }
     uint32_t tot;
-    uint32_t off = cp_block_excl_scan(cnt, wsum, &tot);
+    uint32_t off = cp_block_excl_scan((uint32_t)__builtin_popcount(m), wsum, &tot);
     if (threadIdx.x == 0) gbase = tot ? atomicAdd(b.mcount, tot) : 0u;
     __syncthreads();
     off += gbase;
-#pragma unroll
-    for (int u = 0; u < kAggItems; ++u)
-        if (m[u]) b.mlist[off++] = (uint32_t)(base + (uint64_t)u * 256 + threadIdx.x);
+    while (m) {
+        const int u = __builtin_ctz(m);
+        m &= m - 1;
+        b.mlist[off++] = (uint32_t)(i0 + (uint64_t)u);
+    }
 }
 
 // Within a slot, value positions (the sort order) must follow the request order: the walk replays them in that
@@ -537,7 +544,7 @@ __device__ void cp_walk_serial_mem(const CPArgs& c, const CPBatch& b, const Batc
             if (rem >= 0) {
                 cur += d.acq;
                 cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
-            } else {
+            } else if (b.round > 0) {  // round 0: BLOCKED is k_cp_prep2's default already
                 cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
             }
             continue;
@@ -628,7 +635,7 @@ __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const Batc
             if (rem >= 0) {
                 cur += d.acq;
                 cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
-            } else {
+            } else if (b.round > 0) {  // round 0: BLOCKED is k_cp_prep2's default already
                 cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
             }
             continue;
@@ -942,7 +949,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                             okv = ok;
                             if (typ == kCpSingle) {
                                 if (ok) cp_store(c.out, i, SG_STATUS_OK, cp_d2i(rem));
-                                else cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
+                                else if (b.round > 0) cp_store(c.out, i, SG_STATUS_BLOCKED, 0);
                             } else if (typ == kCpMulti) {
                                 b.chk[p] = ok ? 1 : 0;
                             }
@@ -1007,9 +1014,10 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
 
 // The saturated ranges of k_cp_walk2_long (one wave per piece): every record fails its check and adds nothing — a
 // single-value request is BLOCKED, a multi-value request's first record in the slot checks 0, a repeated value
-// carries check 1.
+// carries check 1. In round 0 the BLOCKED results and the 0 checks are the defaults already (k_cp_prep2,
+// k_cp_recinit): only the repeated values are written.
 __global__ void __launch_bounds__(256) k_cp_skipfill(CPArgs c, CPBatch b, BatchArgs sg) {
-    if (*c.err) return;
+    if (*c.err || (b.changed_prev && *b.changed_prev == 0)) return;
     const uint32_t cnt = min(*b.skip_count, b.skip_cap);
     const int lane = (int)__lane_id();
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
@@ -1017,20 +1025,24 @@ __global__ void __launch_bounds__(256) k_cp_skipfill(CPArgs c, CPBatch b, BatchA
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint2 pc = b.skips[w];
         for (uint64_t j = (uint64_t)pc.x + lane; j < pc.y; j += 64) {
-            const CPRec d = cp_dec(c, b, sg.rec_sorted[j]);
+            const uint64_t rec = sg.rec_sorted[j];
+            const bool multi = ((rec >> (b.pbits - 1)) & 1ull) != 0;
+            if (b.round == 0 && !multi) continue;
+            const CPRec d = cp_dec(c, b, rec);
             if (b.lim && c.out[d.i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
             if (!d.multi) {
                 cp_store(c.out, d.i, SG_STATUS_BLOCKED, 0);
             } else {
                 const uint32_t prev = cp_dec(c, b, sg.rec_sorted[j - 1]).i;  // j > the segment start
-                b.chk[d.p] = prev == d.i ? 1 : 0;
+                if (b.round > 0 || prev == d.i) b.chk[d.p] = prev == d.i ? 1 : 0;
             }
         }
     }
 }
 
 __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
-    if (*c.err) return;
+    if (blockIdx.x == 0 && threadIdx.x < 2) b.dout_count[threadIdx.x] = 0;  // k_cp_relist fills them next
+    if (*c.err || (b.changed_prev && *b.changed_prev == 0)) return;
     const uint32_t m = *b.mcount;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
         const uint64_t i = b.mlist[x];  // a valid multi-value request (k_cp_prep2)
@@ -1056,6 +1068,8 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
 // The next round's re-walk lists from the flags k_cp_combine set (long items, short items; block-aggregated).
 __global__ void __launch_bounds__(256) k_cp_relist(CPBatch b, BatchArgs sg, uint32_t items) {
     __shared__ uint32_t wsum[4], gbase[2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *b.skip_count = 0;  // the next round's k_cp_walk2_long appends
+    if (*b.changed == 0) return;  // no outcome changed: no item is flagged
     const uint32_t nlong = *sg.long_count;
     const uint32_t base = blockIdx.x * (256 * kAggItems);
     bool f[kAggItems];

@@ -339,7 +339,8 @@ struct CPArgs {
 struct CPBatch {
     uint32_t* owner;          // [n_values] request that owns value position p (~0 = none)
     uint8_t* chk;             // [n_values] the value's check at its request (multi-value requests)
-    uint8_t* assume;          // [n] multi-value request: assumed outcome of this iteration
+    uint8_t* assume;          // [n] multi-value request: assumed outcome of this iteration (k_cp_prep2 writes 3 for
+                              // a valid multi-value request: bit 1 lists it for k_cp_mlist; k_cp_combine writes 0 / 1)
     // value records, sorted by slot: {slot : 64 - pbits | payload : pbits}, payload = {multi : 1 | acquire code : 7 |
     // id : idbits}; id = the request index of a single-value request, the value position of a multi-value one (its
     // request: owner[id]); acquire code 127 = read req[i].acquire. The walkers read nothing else per single-value record
@@ -354,7 +355,8 @@ struct CPBatch {
     uint32_t* bnd;            // [kMaxWl][kMaxPeriods] first request index of each window period
     int64_t* p0;              // [kMaxWl] first window period of the batch
     uint32_t* np;             // [kMaxWl] window periods the batch spans
-    int* changed;
+    int* changed;             // k_cp_prep2: the batch has multi-value requests; rounds: this round's combine changed an outcome
+    const int* changed_prev;  // rounds > 0: the previous round's flag (0: converged, the round's kernels return at once)
     CPBucket* save;           // [touched slots][stride] pre-batch rings of the touched slots (null: no re-walks)
     uint32_t* pslot;          // [n_values] slot of value position p
     uint32_t* dflag;          // [work items] the item is listed for the next re-walk (an assumed outcome changed)
@@ -365,14 +367,14 @@ struct CPBatch {
     uint32_t* din;            // re-walk lists walked this round: [2][dcap] long / short items
     uint32_t* din_count;      // [2]
     uint32_t* dout;           // re-walk lists k_cp_combine fills for the next round
-    uint32_t* dout_count;     // [2], zeroed by the host before each combine
+    uint32_t* dout_count;     // [2], zeroed by k_cp_combine before k_cp_relist fills it
     uint32_t dcap;
     uint32_t* mlist;          // valid multi-value requests (k_cp_prep2 appends, any order)
     uint32_t* mcount;
     int round;                // 0: first walk (saves the rings); > 0: re-walk the listed items from the saves
     int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
     uint2* skips;             // saturated ranges [x, y) of sorted records handed to k_cp_skipfill (null: no skipping)
-    uint32_t* skip_count;     // zeroed by the host before every walk
+    uint32_t* skip_count;     // zeroed by the host before round 0, by k_cp_relist before the next round
     uint32_t skip_cap;
 };
 hipError_t launch_cp_prep2(const CPArgs& c, const CPBatch& b, hipStream_t stream);
