@@ -835,7 +835,8 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
         uint32_t carry = kNoOwner;  // owner of the record before the current chunk
         bool carry_ok = false;      // that owner is a multi-value request whose first record here passed its check
         uint64_t blk = s;
-        uint64_t pf = s;  // position of the records in rcn (the next block, loaded a block ahead)
+        uint64_t pf = s;        // position of the records in rcn (the next block, loaded a block ahead)
+        uint64_t nosearch = s;  // a search found the saturated period ending before kCpSkipMin records: walk to there
         uint64_t rcn[kCpU];
 #pragma unroll
         for (int u = 0; u < kCpU; ++u) rcn[u] = sg.rec_sorted[min(s + (uint64_t)u * 64 + lane, e - 1)];
@@ -974,7 +975,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 // saturated period: hand the rest of it to k_cp_skipfill (not while a passed multi-value request's
                 // repeated values may still follow: they add)
                 const uint64_t pos = base + 64;
-                if (pos < e && P != INT64_MIN && !carry_ok && b.skips &&
+                if (pos < e && pos >= nosearch && P != INT64_MIN && !carry_ok && b.skips &&
                     thr - (double)(other + cur) / r.isec - 1.0 < 0) {
                     const int64_t Pc = P;
                     const uint64_t pe = cp_wave_search(pos, e, [&](uint64_t q) {
@@ -995,6 +996,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                             break;
                         }
                     }
+                    nosearch = pe;  // too short to hand over (or no room): the chunks walk it, with no search per chunk
                 }
             }
             blk = next;
@@ -1047,11 +1049,18 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
         const uint64_t i = b.mlist[x];  // a valid multi-value request (k_cp_prep2)
         const sg_cparam_req q = c.req[i];
+        const bool was = b.assume[i] != 0;
         if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
-        bool pass = true;
-        for (uint32_t j = 0; j < q.value_count && pass; ++j) pass = b.chk[(uint64_t)q.value_begin + j] != 0;
-        cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? -1 : 0);  // remaining -1: multi-value
-        if ((b.assume[i] != 0) != pass) {
+        // the checks of the first four values loaded together (value_count >= 2)
+        const uint64_t vb = q.value_begin;
+        const uint32_t vc = q.value_count;
+        const uint8_t c0 = b.chk[vb], c1 = b.chk[vb + 1], c2 = vc > 2 ? b.chk[vb + 2] : (uint8_t)1,
+                      c3 = vc > 3 ? b.chk[vb + 3] : (uint8_t)1;
+        bool pass = c0 && c1 && c2 && c3;
+        for (uint32_t j = 4; j < vc && pass; ++j) pass = b.chk[vb + j] != 0;
+        // the result stands from the previous round unless the outcome changed (remaining -1: multi-value)
+        if (b.round == 0 || was != pass) cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? -1 : 0);
+        if (was != pass) {
             // re-walk the slots whose adds change: a slot adds the request's count iff it is assumed to pass and
             // the slot's check passed (a repeated value's extra records carry check 1), so slots where the check
             // failed add nothing either way
