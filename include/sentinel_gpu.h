@@ -601,20 +601,24 @@ int sg_local_read_state(sg_handle* h, uint32_t res, int64_t* second, int64_t* bo
  *                              carry are 0 .. n_contexts - 1 (sg_slot_ext.context; 0 when no ext). Origin and context
  *                              ids are the caller's dense ids of the Context origin / name strings and must keep
  *                              their meaning across loads (neither count may shrink).
- *                              Nodes besides the ClusterNodes: a resource whose rules name an origin (a limitApp
- *                              other than "default") keeps an origin StatisticNode per origin id
- *                              (ClusterNode.getOrCreateOriginNode), and one with a CHAIN rule a DefaultNode per
- *                              context id (NodeSelectorSlot's per-context node). They are created empty at the
- *                              first load that needs them and then kept across every later load (ClusterNode
- *                              .originCountMap and the DefaultNodes outlive rule reloads); the reference creates
- *                              them at the resource's first entry with that origin / in that context, so traffic
- *                              before that load is the one difference. A RELATE rule joins its
+ *                              Nodes besides the ClusterNodes, created at the first event that needs them whatever
+ *                              the rules say, as the reference does, and kept for the life of the resources (rule
+ *                              reloads keep them): every event from an origin (id > 0) updates the resource's origin
+ *                              StatisticNode (ClusterBuilderSlot.java:99-102 → ClusterNode.getOrCreateOriginNode), and,
+ *                              with context tracking on (n_contexts >= 1), every event updates the resource's DefaultNode
+ *                              of its context (NodeSelectorSlot.java:156-170). Nodes live in a device pool that grows
+ *                              with the (resource, origin / context) pairs seen. Context tracking (needed by CHAIN rules,
+ *                              whose context ids must be < n_contexts) starts before the first batch: raising n_contexts
+ *                              from 0 after a batch is SG_E_UNSUPPORTED (the DefaultNodes would miss earlier entries).
+ *                              With it, every resource is walked by the full-chain walker. A RELATE rule joins its
  *                              resource and ref_resource into one key group walked in event order (the read of
  *                              another resource's ClusterNode, FlowRuleChecker.selectReferenceNode :96-112); a
  *                              resource never entered has no ClusterNode yet (ClusterBuilderSlot), and the rule
  *                              then passes.
- *   sg_local_read_origin_state  ← that origin node: same layout as sg_local_read_state (head[0] = curThreadNum).
- *   sg_local_read_context_state ← the DefaultNode of (resource, context): same layout.
+ *   sg_local_read_origin_state  ← that origin node: same layout as sg_local_read_state (head[0] = curThreadNum);
+ *                              returns 1 when the node exists, 0 when no event created it yet (the dumps of an empty
+ *                              node).
+ *   sg_local_read_context_state ← the DefaultNode of (resource, context): same layout and return values.
  *   sg_local_read_controller   ← the controller of input rule i: {storedTokens, lastFilledTime, latestPassedTime};
  *                              SG_E_INVAL for an ignored rule. */
 int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,

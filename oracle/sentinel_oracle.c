@@ -904,6 +904,7 @@ struct or_local {
     uint32_t n;
     int64_t* last_fetch;     /* StatisticNode.lastFetchTime per resource (metrics()) */
     int32_t n_origins, n_contexts;
+    uint64_t batches;        /* batches decided since or_local_load_rules */
     int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
     uint32_t n_rules;
     struct or_pslot* ps;     /* ParamFlowSlot's rules and metrics (or_local_attach_pslot), NULL = none */
@@ -1026,6 +1027,9 @@ static int flow_rule_same(const sg_local_flow_rule* a, const sg_local_flow_rule*
 int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
                              int32_t n_contexts) {
     if (n_origins < l->n_origins || n_contexts < l->n_contexts) return SG_E_INVAL;   /* ids keep their meaning */
+    /* the DefaultNodes are kept from the first batch on (NodeSelectorSlot creates one at a context's first entry):
+     * context tracking cannot start later */
+    if (n_contexts > 0 && l->n_contexts == 0 && l->batches > 0) return SG_E_UNSUPPORTED;
     for (uint32_t k = 0; k < l->n; k++) {   /* the origin / context nodes stay (they outlive rule reloads) */
         free(l->nodes[k].ctl);
         l->nodes[k].ctl = NULL;
@@ -1077,6 +1081,7 @@ int or_local_load_rules(or_local* l, const sg_local_rule* rules, uint32_t n) {
     l->n = n;
     l->n_origins = 0;
     l->n_contexts = 0;
+    l->batches = 0;
     l->inbound = (uint8_t*)calloc(n ? n : 1, 1);   /* SphU.entry's default EntryType.OUT */
     l->entry = node_new_plain(l);
     l->entry_fetch = -1;
@@ -1536,6 +1541,7 @@ int or_local_decide_ext(or_local* l, const sg_local_event* ev, const sg_slot_ext
         if (ext && (int64_t)ext[i].context >= (int64_t)(l->n_contexts > 0 ? l->n_contexts : 1)) return SG_E_INVAL;
     }
     for (uint64_t i = 0; i < n; i++) local_event(l, &ev[i], ext ? &ext[i] : NULL, args, values, &out[i]);
+    if (n) l->batches++;
     return 0;
 }
 

@@ -149,7 +149,7 @@ struct sg_handle {
     // local slot chain
     sg_local_config lcfg{2, 1000, 500, 0};
     std::vector<LRule> ltab;          // [K] the resources (sg_local_load_rules), origin nodes not included
-    uint32_t l_nodes = 0;             // resources + origin nodes
+    uint32_t l_nodes = 0;             // node arrays: the resources, then the pool (l_pool_cap nodes)
     int32_t l_n_origins = 0;
     bool l_has_cx = false;
     std::vector<int64_t> l_rule_slot; // loaded flow rule i → its LCtl index, -2 stateless fast-path rule, -1 ignored
@@ -172,9 +172,17 @@ struct sg_handle {
     uint32_t* d_lskip_count = nullptr;
     uint32_t lskip_cap = 0;
     sg_local_result* d_lout_h = nullptr;
-    // nodes besides the ClusterNodes (kept across flow-rule reloads): per resource, origin nodes (ids 1 .. on_n at
-    // on_base) and context DefaultNodes (ids 0 .. cn_n - 1 at cn_base)
-    std::vector<uint32_t> l_on_n, l_on_base, l_cn_n, l_cn_base;
+    // node pool (origin nodes, context DefaultNodes; created by the batches, kept across flow-rule reloads)
+    uint32_t l_pool_cap = 0, l_pool_used = 0;
+    uint64_t* d_lnkeys = nullptr;     // map (resource, kind, id) → node, l_nmap_cap slots
+    uint32_t* d_lnvals = nullptr;
+    uint64_t l_nmap_cap = 0;
+    uint32_t* d_lnode_new = nullptr;  // pool nodes a batch created
+    uint32_t* h_lnode_new = nullptr;  // pinned
+    uint2* d_lev_node = nullptr;      // [max_batch] map slots of each event's nodes
+    uint32_t* d_ldyn = nullptr;       // [K] batch epoch of each resource's last origin event
+    uint32_t l_epoch = 0;
+    uint64_t l_batches = 0;           // local batches decided since sg_local_load_rules
     int32_t l_n_contexts = 0;
     int32_t l_cluster_state = SG_CLUSTER_NOT_STARTED;
     bool l_cluster_rules = false;     // some loaded flow rule is in cluster mode
@@ -561,6 +569,12 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_xg_ws[1]);
     dfree(h->d_limx_err);
     if (h->h_limx_err) (void)hipHostFree(h->h_limx_err);
+    dfree(h->d_lnkeys);
+    dfree(h->d_lnvals);
+    dfree(h->d_lnode_new);
+    dfree(h->d_lev_node);
+    dfree(h->d_ldyn);
+    if (h->h_lnode_new) (void)hipHostFree(h->h_lnode_new);
     dfree(h->d_lim_period);
     dfree(h->d_bnd);
     dfree(h->d_p0);
@@ -2514,7 +2528,6 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
         L.flow_count = r.flow_count;
         L.flow_grade = r.flow_grade;
         L.nb = r.n_breakers;
-        L.onode = kNoNode;
         for (int j = 0; j < 2; ++j) {
             LBreakerRule& b = L.b[j];
             b = LBreakerRule{};
@@ -2554,10 +2567,13 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     h->l_has_cx = false;
     h->l_cluster_rules = false;
     h->l_rule_slot.clear();
-    h->l_on_n.assign(n, 0);
-    h->l_on_base.assign(n, kNoNode);
-    h->l_cn_n.assign(n, 0);
-    h->l_cn_base.assign(n, kNoNode);
+    dfree(h->d_lnkeys);
+    dfree(h->d_lnvals);
+    dfree(h->d_ldyn);
+    h->l_nmap_cap = 0;
+    h->l_pool_cap = h->l_pool_used = 0;
+    h->l_epoch = 0;
+    h->l_batches = 0;
     dfree(h->d_lgkey);
     dfree(h->d_linbound);  // every resource's entries EntryType.OUT until sg_local_set_entry_types
     h->l_ps_applied = 0;
@@ -2693,6 +2709,118 @@ int local_apply_params(sg_handle* h) {
     return SG_OK;
 }
 
+// Node pool: a map with room for every key a batch of n events may add at load <= 1/2 (host rehash when it
+// grows), the per-event slot buffer and the per-resource epochs.
+int lnode_prepare(sg_handle* h, uint64_t n) {
+    const uint32_t K = (uint32_t)h->ltab.size();
+    if (!h->d_lev_node) {
+        if (hipMalloc(&h->d_lev_node, sizeof(uint2) * h->cfg.max_batch) != hipSuccess ||
+            hipMalloc(&h->d_lnode_new, sizeof(uint32_t)) != hipSuccess ||
+            hipHostMalloc(&h->h_lnode_new, sizeof(uint32_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "node pool workspace");
+    }
+    if (!h->d_ldyn) {
+        if (hipMalloc(&h->d_ldyn, sizeof(uint32_t) * (K ? K : 1)) != hipSuccess) return fail(h, SG_E_NOMEM, "node pool");
+        HIP_TRY(h, hipMemset(h->d_ldyn, 0, sizeof(uint32_t) * (K ? K : 1)));
+        h->l_epoch = 0;
+    }
+    const uint64_t keys_per_event = (h->l_n_origins > 0 ? 1 : 0) + (h->l_n_contexts > 0 ? 1 : 0);
+    const uint64_t need = 2 * ((uint64_t)h->l_pool_used + n * keys_per_event);
+    if (h->d_lnkeys && need <= h->l_nmap_cap) return SG_OK;
+    uint64_t cap = h->l_nmap_cap ? h->l_nmap_cap : (1ull << 12);
+    while (cap < need) cap <<= 1;
+    std::vector<uint64_t> ok, nk(cap, 0);
+    std::vector<uint32_t> ov, nv(cap, kNoNode);
+    if (h->d_lnkeys) {  // rehash the existing keys
+        ok.resize(h->l_nmap_cap);
+        ov.resize(h->l_nmap_cap);
+        HIP_TRY(h, hipDeviceSynchronize());
+        HIP_TRY(h, hipMemcpy(ok.data(), h->d_lnkeys, sizeof(uint64_t) * ok.size(), hipMemcpyDeviceToHost));
+        HIP_TRY(h, hipMemcpy(ov.data(), h->d_lnvals, sizeof(uint32_t) * ov.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < ok.size(); ++i) {
+            if (!ok[i]) continue;
+            uint64_t j = lnode_hash(ok[i]) & (cap - 1);
+            while (nk[j]) j = (j + 1) & (cap - 1);
+            nk[j] = ok[i];
+            nv[j] = ov[i];
+        }
+    }
+    uint64_t* dk = nullptr;
+    uint32_t* dv = nullptr;
+    if (hipMalloc(&dk, sizeof(uint64_t) * cap) != hipSuccess || hipMalloc(&dv, sizeof(uint32_t) * cap) != hipSuccess) {
+        dfree(dk);
+        dfree(dv);
+        return fail(h, SG_E_NOMEM, "node pool map");
+    }
+    hipError_t e = hipMemcpy(dk, nk.data(), sizeof(uint64_t) * cap, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dv, nv.data(), sizeof(uint32_t) * cap, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        dfree(dk);
+        dfree(dv);
+        return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+    }
+    dfree(h->d_lnkeys);
+    dfree(h->d_lnvals);
+    h->d_lnkeys = dk;
+    h->d_lnvals = dv;
+    h->l_nmap_cap = cap;
+    return SG_OK;
+}
+
+// Pool capacity >= used nodes: new node arrays (the resources, the old pool, empty nodes), geometric growth.
+int lnode_grow(sg_handle* h, uint64_t used) {
+    if (used <= h->l_pool_cap) return SG_OK;
+    const uint64_t K = h->ltab.size();
+    uint64_t cap = std::max<uint64_t>({used, 2ull * h->l_pool_cap, 1024ull});
+    if (K + cap >= SG_KEY_BAD) cap = SG_KEY_BAD - 1 - K;
+    if (K + used >= SG_KEY_BAD || cap < used) return fail(h, SG_E_CAPACITY, "too many origin / context nodes");
+    const uint64_t N = K + cap, old = h->l_nodes;
+    const int S = h->lcfg.sample_count;
+    LHead* hd = nullptr;
+    LBucket *sec = nullptr, *mnt = nullptr;
+    LFuture* bor = nullptr;
+    if (hipMalloc(&hd, sizeof(LHead) * N) != hipSuccess || hipMalloc(&sec, sizeof(LBucket) * N * S) != hipSuccess ||
+        hipMalloc(&bor, sizeof(LFuture) * N * S) != hipSuccess || hipMalloc(&mnt, sizeof(LBucket) * N * kMinuteS) != hipSuccess) {
+        dfree(hd);
+        dfree(sec);
+        dfree(bor);
+        dfree(mnt);
+        return fail(h, SG_E_NOMEM, "node pool");
+    }
+    hipError_t e = hipMemcpy(hd, h->d_lhead, sizeof(LHead) * old, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sec, h->d_lsec, sizeof(LBucket) * old * S, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess) e = hipMemcpy(bor, h->d_lbor, sizeof(LFuture) * old * S, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess) e = hipMemcpy(mnt, h->d_lmin, sizeof(LBucket) * old * kMinuteS, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess) {
+        LArgs L{};
+        L.S = S;
+        L.head = hd;
+        L.sec = sec;
+        L.bor = bor;
+        L.minute = mnt;
+        e = launch_local_init_range(L, old, N, 0);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        dfree(hd);
+        dfree(sec);
+        dfree(bor);
+        dfree(mnt);
+        return fail(h, SG_E_DEVICE, std::string("node pool growth: ") + hipGetErrorString(e));
+    }
+    dfree(h->d_lhead);
+    dfree(h->d_lsec);
+    dfree(h->d_lbor);
+    dfree(h->d_lmin);
+    h->d_lhead = hd;
+    h->d_lsec = sec;
+    h->d_lbor = bor;
+    h->d_lmin = mnt;
+    h->l_nodes = (uint32_t)N;
+    h->l_pool_cap = (uint32_t)cap;
+    return SG_OK;
+}
+
 // StatisticSlot around ParamFlowSlot → FlowSlot → DegradeSlot for a time-ordered batch (ext nullable).
 int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n, const sg_pslot_arg* args,
                  uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_local_result* out, void* stream_) {
@@ -2769,6 +2897,24 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
             hipMalloc(&h->d_lskip_count, sizeof(uint32_t)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "local batch workspace");
     }
+    const bool track = h->l_n_origins > 0 || h->l_n_contexts > 0;
+    if (track) {
+        const int rc = lnode_prepare(h, n);
+        if (rc) return rc;
+        L.nkeys = h->d_lnkeys;
+        L.nvals = h->d_lnvals;
+        L.nmask = h->l_nmap_cap - 1;
+        L.node_base = K + h->l_pool_used;
+        L.node_new = h->d_lnode_new;
+        L.ev_node = h->d_lev_node;
+        L.dyn = h->d_ldyn;
+        if (++h->l_epoch == 0) {  // the epochs wrapped: no resource may match a stale one
+            HIP_TRY(h, hipMemset(h->d_ldyn, 0, sizeof(uint32_t) * (K ? K : 1)));
+            h->l_epoch = 1;
+        }
+        L.epoch = h->l_epoch;
+        L.track_ctx = h->l_n_contexts > 0 ? 1 : 0;
+    }
     L.flags = h->d_lflags;
     L.exit_pos = h->d_lexit_pos;
     L.exit_cnt = h->d_lexit_cnt;
@@ -2799,6 +2945,21 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     HIP_TRY(h, hipMemsetAsync(h->d_lflags, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_lskip_count, 0, sizeof(uint32_t), stream));
     HIP_TRY(h, launch_local_prep(L, stream));
+    if (track) {  // the batch's new pool nodes (only for a batch that passed validation), then room for them
+        HIP_TRY(h, hipMemsetAsync(h->d_lnode_new, 0, sizeof(uint32_t), stream));
+        HIP_TRY(h, launch_lnode_assign(L, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_lnode_new, h->d_lnode_new, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        const uint64_t used = (uint64_t)h->l_pool_used + *h->h_lnode_new;
+        const int rc = lnode_grow(h, used);
+        if (rc) return rc;
+        h->l_pool_used = (uint32_t)used;
+        L.N = h->l_nodes;
+        L.head = h->d_lhead;
+        L.sec = h->d_lsec;
+        L.bor = h->d_lbor;
+        L.minute = h->d_lmin;
+    }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     uint64_t* sorted = nullptr;
     HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, L.kshift, h->d_hist, &sorted, stream));
@@ -2807,7 +2968,7 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     sgm.rec_sorted = sorted;
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
     HIP_TRY(h, launch_seg(sgm, stream));
-    HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx || h->l_has_cx_ps, h->aux, stream, h->fork, h->join));
+    HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx || h->l_has_cx_ps || track, h->aux, stream, h->fork, h->join));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
@@ -2835,6 +2996,7 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
                                    "(the arg / value arrays) are out of range");
     if (*h->h_err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param value or thread-count table is full");
     if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    ++h->l_batches;
     return SG_OK;
 }
 
@@ -2945,6 +3107,34 @@ int local_read_node(sg_handle* h, uint32_t node, int64_t* second, int64_t* borro
     return SG_OK;
 }
 
+// A pool node's windows (sg_local_read_state layout): 1 when the node exists, 0 when no event created it yet (the
+// dumps of an empty node: null slots, zero counters and threads).
+int local_read_pool_node(sg_handle* h, uint64_t key, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    uint32_t node = kNoNode;
+    if (h->d_lnkeys) {
+        HIP_TRY(h, hipDeviceSynchronize());
+        HIP_TRY(h, launch_lnode_find(h->d_lnkeys, h->d_lnvals, h->l_nmap_cap - 1, key, h->d_lnode_new, 0));
+        HIP_TRY(h, hipMemcpy(&node, h->d_lnode_new, sizeof(node), hipMemcpyDeviceToHost));
+    }
+    if (node != kNoNode) {
+        const int rc = local_read_node(h, node, second, borrow, minute, head);
+        return rc ? rc : 1;
+    }
+    const int S = h->lcfg.sample_count;
+    for (int j = 0; j < S; ++j) {
+        for (int e = 0; e < 8; ++e) second[8 * j + e] = e == 0 ? INT64_MIN : 0;
+        borrow[2 * j] = INT64_MIN;
+        borrow[2 * j + 1] = 0;
+    }
+    for (int j = 0; j < kMinuteS; ++j)
+        for (int e = 0; e < 8; ++e) minute[8 * j + e] = e == 0 ? INT64_MIN : 0;
+    std::fill(head, head + 14, 0);
+    head[3] = head[9] = INT64_MIN;  // the breakers' stat buckets of a fresh node: never created
+    return 0;
+}
+
 // FlowRuleUtil.isValidRule (:167-251) for local rules: count >= 0, grade / strategy / behaviour >= 0; QPS rules:
 // checkClusterField (an invalid ClusterFlowConfig), checkStrategyField (RELATE / CHAIN need a refResource) and
 // checkControlBehaviorField (warm-up period > 0, queueing time > 0); THREAD rules: checkClusterConcurrentField
@@ -3014,20 +3204,14 @@ int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64
                                int64_t* minute, int64_t* head) {
     if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
     if (origin <= 0 || origin > h->l_n_origins) return fail(h, SG_E_INVAL, "origin id outside 1..n_origins");
-    const uint32_t on = h->ltab[res].onode;
-    if (on == kNoNode || (uint32_t)origin > h->ltab[res].on_n)
-        return fail(h, SG_E_INVAL, "the resource keeps no origin nodes (no rule of it named an origin)");
-    return local_read_node(h, on + (uint32_t)origin - 1, second, borrow, minute, head);
+    return local_read_pool_node(h, lnode_key(res, 0, (uint32_t)origin), second, borrow, minute, head);
 }
 
 int sg_local_read_context_state(sg_handle* h, uint32_t res, int32_t context, int64_t* second, int64_t* borrow,
                                 int64_t* minute, int64_t* head) {
     if (!h || res >= h->ltab.size() || !second || !borrow || !minute || !head) return SG_E_INVAL;
     if (context < 0 || context >= h->l_n_contexts) return fail(h, SG_E_INVAL, "context id outside 0..n_contexts-1");
-    const uint32_t cn = h->ltab[res].cnode;
-    if (cn == kNoNode || (uint32_t)context >= h->ltab[res].cn_n)
-        return fail(h, SG_E_INVAL, "the resource keeps no context DefaultNodes (no CHAIN rule)");
-    return local_read_node(h, cn + (uint32_t)context, second, borrow, minute, head);
+    return local_read_pool_node(h, lnode_key(res, kLNodeCtx, (uint32_t)context), second, borrow, minute, head);
 }
 
 int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3) {
@@ -3066,6 +3250,10 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     if (n_origins < 0 || n_contexts < 0) return fail(h, SG_E_INVAL, "n_origins / n_contexts < 0");
     if (n_origins < h->l_n_origins || n_contexts < h->l_n_contexts)
         return fail(h, SG_E_INVAL, "origin / context ids keep their meaning across loads: the counts cannot shrink");
+    if (n_contexts > 0 && h->l_n_contexts == 0 && h->l_batches > 0)
+        return fail(h, SG_E_UNSUPPORTED, "context tracking (n_contexts >= 1) starts before the first batch: a DefaultNode "
+                                         "holds every entry of its context since the resource's first one");
+    const bool track_ctx = n_contexts > 0;
     const uint32_t K = (uint32_t)h->ltab.size();
     const int cold = h->lcfg.cold_factor > 1 ? h->lcfg.cold_factor : 3;
     // FlowRuleUtil.buildFlowRuleMap (:83-130): drop invalid rules and duplicates (its HashSet), group by resource
@@ -3113,7 +3301,6 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
 
     std::vector<LRule> tab = h->ltab;
     std::vector<LFlowRule> fr;
-    std::vector<uint32_t> on_n(K), cn_n(K);
     bool has_cx = false;
     for (uint32_t k = 0; k < K; ++k) {
         std::vector<uint32_t>& v = by_res[k];
@@ -3122,24 +3309,15 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
             return (rules[x].cluster_mode != SG_CLUSTER_MODE_OFF ? 2 : 0) + (rules[x].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
         };
         std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) { return key(x) < key(y); });
-        bool origin_rules = false, chain_rules = false;
-        for (uint32_t i : v) {
-            origin_rules = origin_rules || rules[i].limit_app != SG_LIMIT_APP_DEFAULT;
-            chain_rules = chain_rules || rules[i].strategy == SG_STRATEGY_CHAIN;
-        }
-        // nodes, once kept, stay (and follow the grown id ranges)
-        on_n[k] = (h->l_on_n[k] > 0 || origin_rules) ? (uint32_t)n_origins : 0u;
-        cn_n[k] = (h->l_cn_n[k] > 0 || chain_rules) ? (uint32_t)n_contexts : 0u;
         LRule& L = tab[k];
         L.fr_begin = L.fr_n = 0;
-        L.onode = L.cnode = kNoNode;
-        L.on_n = L.cn_n = 0;
         L.cx = 0;
         L.ps = 0;
         L.grp = gsize[gkey[k]] > 1 ? 1 : 0;
         L.flow_grade = -1;
         L.flow_count = 0;
-        const bool fast = v.size() == 1 && !L.grp && on_n[k] == 0 && cn_n[k] == 0 &&
+        // (with context tracking every event also updates its context's DefaultNode: the cx walker)
+        const bool fast = v.size() == 1 && !L.grp && !track_ctx &&
                           rules[v[0]].limit_app == SG_LIMIT_APP_DEFAULT && rules[v[0]].strategy == SG_STRATEGY_DIRECT &&
                           rules[v[0]].cluster_mode == SG_CLUSTER_MODE_OFF &&
                           make_flow_rule(rules[v[0]], cold).behavior == SG_CONTROL_DEFAULT;
@@ -3149,7 +3327,7 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
             slot[v[0]] = -2;
             continue;
         }
-        if (v.empty() && !L.grp && on_n[k] == 0 && cn_n[k] == 0) continue;
+        if (v.empty() && !L.grp && !track_ctx) continue;
         L.cx = 1;
         has_cx = true;
         L.fr_begin = (uint32_t)fr.size();
@@ -3159,67 +3337,17 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
             fr.push_back(make_flow_rule(rules[i], cold));
         }
     }
-    // node layout: the K resources, then the origin blocks, then the context blocks; src = the old node of each
-    std::vector<int64_t> src;
-    src.reserve(K);
-    for (uint32_t k = 0; k < K; ++k) src.push_back(k);
-    std::vector<uint32_t> on_base(K, kNoNode), cn_base(K, kNoNode);
-    for (uint32_t k = 0; k < K; ++k) {
-        if (!on_n[k]) continue;
-        on_base[k] = (uint32_t)src.size();
-        for (uint32_t o = 1; o <= on_n[k]; ++o)
-            src.push_back(o <= h->l_on_n[k] ? (int64_t)h->l_on_base[k] + o - 1 : -1);
-    }
-    for (uint32_t k = 0; k < K; ++k) {
-        if (!cn_n[k]) continue;
-        cn_base[k] = (uint32_t)src.size();
-        for (uint32_t c = 0; c < cn_n[k]; ++c) src.push_back(c < h->l_cn_n[k] ? (int64_t)h->l_cn_base[k] + c : -1);
-    }
-    const uint64_t N = src.size();
-    if (N >= SG_KEY_BAD) return fail(h, SG_E_UNSUPPORTED, "too many origin / context nodes");
-    for (uint32_t k = 0; k < K; ++k) {
-        tab[k].onode = on_base[k];
-        tab[k].on_n = on_n[k];
-        tab[k].cnode = cn_base[k];
-        tab[k].cn_n = cn_n[k];
-    }
-    tab.resize(N);
-    for (uint64_t i = K; i < N; ++i) {  // origin / context nodes: no rules, no breakers
-        tab[i] = LRule{};
-        tab[i].flow_grade = -1;
-        tab[i].onode = tab[i].cnode = kNoNode;
-        for (int j = 0; j < 2; ++j) tab[i].b[j].stat_ms = 1;
-    }
+    // the nodes (ClusterNodes and the pool) are untouched: statistics outlive the reload
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipDeviceSynchronize());
-    const int S = h->lcfg.sample_count;
-    LRule* d_rules = nullptr;
-    LHead* d_head = nullptr;
-    LBucket *d_sec = nullptr, *d_min = nullptr;
-    LFuture* d_bor = nullptr;
     LFlowRule* d_fr = nullptr;
     LCtl* d_ctl = nullptr;
-    int64_t* d_src = nullptr;
     uint32_t* d_gkey = nullptr;
     auto release = [&]() {
-        dfree(d_rules);
-        dfree(d_head);
-        dfree(d_sec);
-        dfree(d_bor);
-        dfree(d_min);
         dfree(d_fr);
         dfree(d_ctl);
-        dfree(d_src);
         dfree(d_gkey);
     };
-    if (N && (hipMalloc(&d_rules, sizeof(LRule) * N) != hipSuccess || hipMalloc(&d_head, sizeof(LHead) * N) != hipSuccess ||
-              hipMalloc(&d_sec, sizeof(LBucket) * N * S) != hipSuccess ||
-              hipMalloc(&d_bor, sizeof(LFuture) * N * S) != hipSuccess ||
-              hipMalloc(&d_min, sizeof(LBucket) * N * kMinuteS) != hipSuccess ||
-              hipMalloc(&d_src, sizeof(int64_t) * N) != hipSuccess)) {
-        release();
-        return fail(h, SG_E_NOMEM, "local node allocation");
-    }
     if (!fr.empty() && (hipMalloc(&d_fr, sizeof(LFlowRule) * fr.size()) != hipSuccess ||
                         hipMalloc(&d_ctl, sizeof(LCtl) * fr.size()) != hipSuccess)) {
         release();
@@ -3230,19 +3358,7 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
         return fail(h, SG_E_NOMEM, "key groups");
     }
     hipError_t e = hipSuccess;
-    if (N) {
-        LArgs L{};
-        L.K = K;
-        L.N = (uint32_t)N;
-        L.S = S;
-        L.head = d_head;
-        L.sec = d_sec;
-        L.bor = d_bor;
-        L.minute = d_min;
-        e = hipMemcpy(d_src, src.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = launch_local_remap(L, d_src, h->d_lhead, h->d_lsec, h->d_lbor, h->d_lmin, 0);
-        if (e == hipSuccess) e = hipMemcpy(d_rules, tab.data(), sizeof(LRule) * N, hipMemcpyHostToDevice);
-    }
+    if (K) e = hipMemcpy(h->d_lrules, tab.data(), sizeof(LRule) * K, hipMemcpyHostToDevice);
     if (e == hipSuccess && groups) e = hipMemcpy(d_gkey, gkey.data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice);
     if (e == hipSuccess && !fr.empty()) {
         e = hipMemcpy(d_fr, fr.data(), sizeof(LFlowRule) * fr.size(), hipMemcpyHostToDevice);
@@ -3250,39 +3366,22 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
         if (e == hipSuccess) e = hipMemcpy(d_ctl, c.data(), sizeof(LCtl) * c.size(), hipMemcpyHostToDevice);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
-    dfree(d_src);
     if (e != hipSuccess) {
         release();
         return fail(h, SG_E_DEVICE, std::string("local flow rule upload: ") + hipGetErrorString(e));
     }
-    dfree(h->d_lrules);
-    dfree(h->d_lhead);
-    dfree(h->d_lsec);
-    dfree(h->d_lbor);
-    dfree(h->d_lmin);
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
     dfree(h->d_lgkey);
-    h->d_lrules = d_rules;
-    h->d_lhead = d_head;
-    h->d_lsec = d_sec;
-    h->d_lbor = d_bor;
-    h->d_lmin = d_min;
     h->d_lfrules = d_fr;
     h->d_lctl = d_ctl;
     h->d_lgkey = d_gkey;
-    tab.resize(K);
     h->ltab = tab;
-    h->l_nodes = (uint32_t)N;
     h->l_n_origins = n_origins;
     h->l_n_contexts = n_contexts;
     h->l_has_cx = has_cx;
     h->l_cluster_rules = cluster_rules;
     h->l_rule_slot = slot;
-    h->l_on_n = on_n;
-    h->l_on_base = on_base;
-    h->l_cn_n = cn_n;
-    h->l_cn_base = cn_base;
     h->l_ps_applied = 0;  // param flags are re-applied to the new rule image by the next batch
     int kept = 0;
     for (int64_t x : slot) kept += x != -1;

@@ -506,16 +506,31 @@ struct alignas(16) LRule {
     int32_t nb;               // breakers 0..2
     LBreakerRule b[2];
     uint32_t fr_begin, fr_n;  // cx: the resource's flow rules frules[fr_begin .. + fr_n) in check order
-    uint32_t onode;           // node index of origin 1 (origin o: onode + o - 1, o <= on_n); kNoNode without origin nodes
     int32_t cx;               // 1: walked by k_lwalk_cx (several rules, limitApps, shaping controllers, param rules,
-                              // origin / context nodes, RELATE groups)
-    uint32_t on_n;            // origin nodes of the resource (origin ids 1 .. on_n)
-    uint32_t cnode;           // node index of the DefaultNode of context 0 (context c: cnode + c, c < cn_n)
-    uint32_t cn_n;
+                              // context DefaultNodes, RELATE groups); a batch's events from an origin make their
+                              // resource cx for that batch (LArgs::dyn)
     int32_t ps;               // 1: the resource has ParamFlowSlot rules (sg_pslot_load_rules)
     int32_t grp;              // 1: in a RELATE key group (walked event by event from memory, k_lwalk_cx)
+    int32_t pad_;
 };
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
+
+// The node pool of the local chain: nodes besides the resources' ClusterNodes — ClusterNode.getOrCreateOriginNode
+// (ClusterBuilderSlot.java:99-102: every entry with an origin) and NodeSelectorSlot's DefaultNode per context
+// (NodeSelectorSlot.java:156-170: every entry in a context) — created at the first event that needs them, as the
+// reference does, and kept for the life of the resources (they outlive flow-rule reloads). An open-addressing map
+// {(resource, kind, id) → node index} in HBM; pool nodes follow the K resources in the node arrays.
+constexpr uint64_t kLNodeCtx = 1ull << 31;  // key bit: a context DefaultNode (else an origin node)
+__host__ __device__ __forceinline__ uint64_t lnode_key(uint32_t res, uint64_t kind, uint32_t id) {
+    return ((uint64_t)(res + 1u) << 32) | kind | (uint64_t)id;  // never 0 (the empty slot)
+}
+__host__ __device__ __forceinline__ uint64_t lnode_hash(uint64_t x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
 
 // A flow rule of the local chain with its controller's constants (FlowRuleUtil.generateRater, WarmUpController
 // .construct :83-106).
@@ -545,8 +560,8 @@ struct LArgs {
     int kshift, abits;
     uint64_t imask, amask, aesc;
     uint32_t K;               // resources (record keys)
-    uint32_t N;               // nodes: the K resources, then the origin nodes
-    const LRule* rules;       // [N] (origin nodes: no rules, no breakers)
+    uint32_t N;               // nodes: the K resources, then the pool (origin / context nodes)
+    const LRule* rules;       // [K]
     const LFlowRule* frules;  // flow rules of the cx resources
     LCtl* ctl;                // [frules] controller state
     int32_t n_origins;
@@ -578,6 +593,16 @@ struct LArgs {
     struct LSkip* skips;      // dead-period ranges handed to k_lskip_apply
     uint32_t* skip_count;
     uint32_t skip_cap;
+    // node pool (null nkeys: no origins / contexts tracked)
+    uint64_t* nkeys;          // [nmask + 1] lnode_key, 0 = empty
+    uint32_t* nvals;          // node index of each key
+    uint64_t nmask;
+    uint32_t node_base;       // index of the batch's first new pool node (K + pool nodes before the batch)
+    uint32_t* node_new;       // pool nodes the batch created (k_lnode_assign)
+    uint2* ev_node;           // [n] map slots of each event's {origin node, context DefaultNode}, kNoNode = none
+    uint32_t* dyn;            // [K] epoch of the last batch with an origin event of the resource (walked as cx)
+    uint32_t epoch;
+    int32_t track_ctx;        // 1: every event updates its context's DefaultNode (n_contexts >= 1)
     int64_t* last_fetch;      // [K] StatisticNode.lastFetchTime (metric rows already reported)
     const uint8_t* inbound;   // [K] 1: the resource's entries are EntryType.IN (Constants.ENTRY_NODE), or null
     LBucket* entry_acc;       // [60] the ENTRY_NODE's minute buckets summed from the inbound resources' (metric rows)
@@ -596,9 +621,13 @@ hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
 hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
-// New node arrays of a flow-rule reload: node i copies old node src[i] (>= 0) or starts empty (L: the new arrays, N nodes)
-hipError_t launch_local_remap(const LArgs& L, const int64_t* src, const LHead* ohead, const LBucket* osec,
-                              const LFuture* obor, const LBucket* omin, hipStream_t stream);
+// Empty nodes [lo, hi) of the node arrays L.head / sec / bor / minute.
+hipError_t launch_local_init_range(const LArgs& L, uint64_t lo, uint64_t hi, hipStream_t stream);
+// Node pool: every event's origin node / context DefaultNode found or created in the map (after k_local_prep,
+// nothing when the batch failed validation); node index of a key (kNoNode if absent) into *out (device).
+hipError_t launch_lnode_assign(const LArgs& L, hipStream_t stream);
+hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_t mask, uint64_t key, uint32_t* out,
+                             hipStream_t stream);
 // StatisticNode.metrics() of every resource at now: emit == 0 counts the rows (no side effect), emit == 1 writes
 // them (any order) and applies currentWindow / lastFetchTime.
 // Constants.ENTRY_NODE's metric rows from the summed buckets (k_local_metrics accumulated them into a.entry_acc).

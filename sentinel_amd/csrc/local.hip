@@ -180,16 +180,17 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_local_init(LArgs a) {
-    const uint64_t total = (uint64_t)a.N * kMinuteS;  // resources and origin nodes
+// Empty nodes [lo, hi) (one thread per minute slot of a node).
+__global__ void __launch_bounds__(256) k_local_init(LArgs a, uint64_t lo, uint64_t hi) {
+    const uint64_t total = (hi - lo) * kMinuteS;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         LBucket b;
         b.start = INT64_MIN;
         for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
         b.min_rt = kStatMaxRt;
-        a.minute[i] = b;
-        const uint64_t k = i / kMinuteS;
+        const uint64_t k = lo + i / kMinuteS;
         const int q = (int)(i % kMinuteS);
+        a.minute[k * kMinuteS + q] = b;
         if (q < a.S) {
             a.sec[k * a.S + q] = b;
             LFuture f;
@@ -214,42 +215,63 @@ __global__ void __launch_bounds__(256) k_local_init(LArgs a) {
     }
 }
 
-// Node i of the new arrays: a copy of old node src[i], or empty (src[i] < 0) — a flow-rule reload keeps every
-// resource's and every kept origin / context node's statistics (ClusterNode.originCountMap outlives the reload).
-__global__ void __launch_bounds__(256) k_local_remap(LArgs a, const int64_t* src, const LHead* ohead,
-                                                     const LBucket* osec, const LFuture* obor, const LBucket* omin) {
-    const uint64_t total = (uint64_t)a.N * kMinuteS;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = i / kMinuteS;
-        const int q = (int)(i % kMinuteS);
-        const int64_t from = src[k];
-        LBucket b;
-        b.start = INT64_MIN;
-        for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
-        b.min_rt = kStatMaxRt;
-        a.minute[i] = from >= 0 ? omin[(uint64_t)from * kMinuteS + q] : b;
-        if (q < a.S) {
-            LFuture f;
-            f.start = INT64_MIN;
-            f.pass = 0;
-            a.sec[k * a.S + q] = from >= 0 ? osec[(uint64_t)from * a.S + q] : b;
-            a.bor[k * a.S + q] = from >= 0 ? obor[(uint64_t)from * a.S + q] : f;
-        }
-        if (q == 0) {
-            LHead h;
-            h.threads = 0;
-            h.created = 0;
-            for (int j = 0; j < 2; ++j) {
-                h.cb[j].next_retry = 0;
-                h.cb[j].stat_start = INT64_MIN;
-                h.cb[j].bad = h.cb[j].total = 0;
-                h.cb[j].state = kCbClosed;
-                h.cb[j].pad = 0;
+// ------------------------------------------------------------------------------------ node pool
+
+namespace {
+
+// Find or insert key; returns its map slot. A new key takes the next pool node (a.node_base + creation order).
+// Lanes never wait on one another: the node index is written by the inserting lane and read only by later kernels.
+__device__ uint32_t lnode_slot(const LArgs& a, uint64_t key) {
+    uint64_t s = lnode_hash(key) & a.nmask;
+    for (;;) {
+        const uint64_t cur = a.nkeys[s];
+        if (cur == key) return (uint32_t)s;
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&a.nkeys[s], 0ull, (unsigned long long)key);
+            if (prev == 0) {
+                a.nvals[s] = a.node_base + atomicAdd(a.node_new, 1u);
+                return (uint32_t)s;
             }
-            h.pad2[0] = h.pad2[1] = 0;
-            a.head[k] = from >= 0 ? ohead[from] : h;
+            if (prev == key) return (uint32_t)s;
         }
+        s = (s + 1) & a.nmask;
     }
+}
+
+}  // namespace
+
+// ClusterBuilderSlot's origin node (an event with an origin) and NodeSelectorSlot's DefaultNode of the event's
+// context (context tracking on) of every event, created on first sight; the map slots go to ev_node, and a resource
+// with an origin event is walked by k_lwalk_cx in this batch. Runs only for a batch that passed validation (a
+// rejected batch creates nothing). The host sized the map for every event's keys at load <= 1/2.
+__global__ void __launch_bounds__(256) k_lnode_assign(LArgs a) {
+    if (*a.err) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_local_event e = a.ev[i];
+        const uint32_t res = e.resource & SG_KEY_INDEX;
+        uint2 v = make_uint2(kNoNode, kNoNode);
+        if (res < a.K) {
+            if (e.origin > 0) {
+                v.x = lnode_slot(a, lnode_key(res, 0, (uint32_t)e.origin));
+                if (a.dyn[res] != a.epoch) a.dyn[res] = a.epoch;
+            }
+            if (a.track_ctx) v.y = lnode_slot(a, lnode_key(res, kLNodeCtx, a.ext ? a.ext[i].context : 0u));
+        }
+        a.ev_node[i] = v;
+    }
+}
+
+__global__ void k_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_t mask, uint64_t key, uint32_t* out) {
+    uint64_t s = lnode_hash(key) & mask;
+    uint32_t r = kNoNode;
+    for (uint64_t probes = 0; probes <= mask; ++probes, s = (s + 1) & mask) {
+        if (keys[s] == key) {
+            r = vals[s];
+            break;
+        }
+        if (keys[s] == 0) break;
+    }
+    *out = r;
 }
 
 // ----------------------------------------------------------------------------- per-resource state
@@ -275,7 +297,14 @@ struct LNode {
     int64_t created;   // LHead.created (set by the walkers for a resource with events: ClusterBuilderSlot)
     LBreaker cb[2];
 
-    __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), R(a_.rules[k_]), k(k_) {
+    __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), k(k_) {
+        if (k_ < a.K) {
+            R = a.rules[k_];
+        } else {  // a pool node (origin / context): no rules, no breakers
+            R = LRule{};
+            R.flow_grade = -1;
+            R.b[0].stat_ms = R.b[1].stat_ms = 1;
+        }
         sec = a.sec + (size_t)k * a.S;
         bor = a.bor + (size_t)k * a.S;
         mnt = a.minute + (size_t)k * kMinuteS;
@@ -646,7 +675,7 @@ __global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
         if (i >= cnt[c]) continue;
         const uint64_t j = sg.short_list[sg.class_off[c] + i];
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
-        if (a.rules[k].cx) continue;  // k_lwalk_cx
+        if (a.rules[k].cx || (a.dyn && a.dyn[k] == a.epoch)) continue;  // k_lwalk_cx
         LNode nd(a, bndp, k);
         nd.created = 1;  // the resource has events, so an entry reached ClusterBuilderSlot
         // software pipeline: records kRecAhead ahead, exit timestamps kEvAhead ahead (a lane walks up to
@@ -1010,7 +1039,7 @@ __global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
     for (uint32_t item = wave; item < n_long; item += nwaves) {
         const uint64_t s = sg.long_list[item];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-        if (a.rules[k].cx) continue;  // k_lwalk_cx
+        if (a.rules[k].cx || (a.dyn && a.dyn[k] == a.epoch)) continue;  // k_lwalk_cx
         const uint64_t e = lwave_search(s + 1, a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
@@ -1153,12 +1182,11 @@ __device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, co
 }
 
 // The nodes StatisticSlot updates for one event besides the ClusterNode: the origin node (ClusterBuilderSlot, origin
-// o of the event) and the DefaultNode of the event's context (NodeSelectorSlot), when the resource keeps them.
-__device__ __forceinline__ uint32_t origin_node_of(const LRule& R, int origin) {
-    return (R.onode != kNoNode && origin > 0 && (uint32_t)origin <= R.on_n) ? R.onode + (uint32_t)origin - 1 : kNoNode;
-}
-__device__ __forceinline__ uint32_t context_node_of(const LRule& R, int ctx) {
-    return (R.cnode != kNoNode && ctx >= 0 && (uint32_t)ctx < R.cn_n) ? R.cnode + (uint32_t)ctx : kNoNode;
+// o of the event) and the DefaultNode of the event's context (NodeSelectorSlot, context tracking on), from the pool.
+__device__ __forceinline__ uint2 event_nodes(const LArgs& a, uint32_t idx) {
+    if (!a.nkeys) return make_uint2(kNoNode, kNoNode);
+    const uint2 s = a.ev_node[idx];
+    return make_uint2(s.x != kNoNode ? a.nvals[s.x] : kNoNode, s.y != kNoNode ? a.nvals[s.y] : kNoNode);
 }
 
 // One entry of a cx resource, the slot chain in SPI order inside StatisticSlot.entry (StatisticSlot.java:55-122):
@@ -1169,7 +1197,8 @@ __device__ __forceinline__ uint32_t context_node_of(const LRule& R, int ctx) {
 __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t, int origin,
                          int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
     const LRule& R = nd.R;
-    const uint32_t on_idx = origin_node_of(R, origin), cn_idx = context_node_of(R, ctx);
+    const uint2 nodes = event_nodes(a, e.idx);
+    const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
     LNode on(a, bndp, have_on ? on_idx : nd.k);
     if (have_on) on.at(qs, qm);
@@ -1279,7 +1308,8 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
 __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t,
                         int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
     nd.exit(e, t, create);
-    const uint32_t on_idx = origin_node_of(nd.R, origin), cn_idx = context_node_of(nd.R, ctx);
+    const uint2 nodes = event_nodes(a, e.idx);
+    const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
         LNode on(a, bndp, on_idx);
         on.at(qs, qm);
@@ -1319,7 +1349,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
             j = sg.short_list[sg.class_off[c] + r];
         }
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
-        if (!a.rules[k].cx) continue;
+        if (!a.rules[k].cx && !(a.dyn && a.dyn[k] == a.epoch)) continue;
         if (a.rules[k].grp) {
             for (uint64_t p = j; p < a.n; ++p) {
                 const uint64_t rec = a.rec_sorted[p];
@@ -1590,17 +1620,22 @@ hipError_t launch_local_entry_rows(const LArgs& a, int64_t now, sg_metric_node* 
     return hipGetLastError();
 }
 
-hipError_t launch_local_init(const LArgs& a, hipStream_t stream) {
-    if (a.K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_local_init, dim3(lgrid((uint64_t)a.K * kMinuteS, 256, 8192)), dim3(256), 0, stream, a);
+hipError_t launch_local_init(const LArgs& a, hipStream_t stream) { return launch_local_init_range(a, 0, a.K, stream); }
+
+hipError_t launch_local_init_range(const LArgs& a, uint64_t lo, uint64_t hi, hipStream_t stream) {
+    if (hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_local_init, dim3(lgrid((hi - lo) * kMinuteS, 256, 8192)), dim3(256), 0, stream, a, lo, hi);
     return hipGetLastError();
 }
 
-hipError_t launch_local_remap(const LArgs& a, const int64_t* src, const LHead* ohead, const LBucket* osec,
-                              const LFuture* obor, const LBucket* omin, hipStream_t stream) {
-    if (a.N == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_local_remap, dim3(lgrid((uint64_t)a.N * kMinuteS, 256, 8192)), dim3(256), 0, stream, a, src,
-                       ohead, osec, obor, omin);
+hipError_t launch_lnode_assign(const LArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_lnode_assign, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_t mask, uint64_t key, uint32_t* out,
+                             hipStream_t stream) {
+    hipLaunchKernelGGL(k_lnode_find, dim3(1), dim3(1), 0, stream, keys, vals, mask, key, out);
     return hipGetLastError();
 }
 

@@ -507,26 +507,25 @@ class FlowEngine:
                                                  C.c_void_p(args_ptr or None), n_args, C.c_void_p(values_ptr or None),
                                                  n_values, C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
 
-    def local_context_state(self, res, context):
-        """The DefaultNode of (res, context): (second, borrow, minute, head) as local_state."""
-        S = self.local_S
-        sec = np.zeros((S, 8), np.int64)
-        bor = np.zeros((S, 2), np.int64)
-        mnt = np.zeros((60, 8), np.int64)
-        head = np.zeros(14, np.int64)
-        self._check(self._L.sg_local_read_context_state(self.h, res, context, abi.ptr(sec), abi.ptr(bor),
-                                                        abi.ptr(mnt), abi.ptr(head)))
-        return sec, bor, mnt, head
+    def local_context_state(self, res, context, with_exists=False):
+        """The DefaultNode of (res, context): (second, borrow, minute, head) as local_state (+ whether an event created
+        it yet, with_exists)."""
+        return self._pool_node_state(self._L.sg_local_read_context_state, res, context, with_exists)
 
-    def local_origin_state(self, res, origin):
+    def local_origin_state(self, res, origin, with_exists=False):
+        """The origin node of (res, origin): (second, borrow, minute, head) as local_state (+ exists)."""
+        return self._pool_node_state(self._L.sg_local_read_origin_state, res, origin, with_exists)
+
+    def _pool_node_state(self, fn, res, ident, with_exists):
         S = self.local_S
         sec = np.zeros((S, 8), np.int64)
         bor = np.zeros((S, 2), np.int64)
         mnt = np.zeros((60, 8), np.int64)
         head = np.zeros(14, np.int64)
-        self._check(self._L.sg_local_read_origin_state(self.h, res, origin, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt),
-                                                       abi.ptr(head)))
-        return sec, bor, mnt, head
+        rc = fn(self.h, res, ident, abi.ptr(sec), abi.ptr(bor), abi.ptr(mnt), abi.ptr(head))
+        if rc < 0:
+            self._check(rc)
+        return (sec, bor, mnt, head, rc == 1) if with_exists else (sec, bor, mnt, head)
 
     def local_controller(self, rule):
         """{storedTokens, lastFilledTime, latestPassedTime} of input flow rule `rule`."""

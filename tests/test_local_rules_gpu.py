@@ -103,15 +103,10 @@ def _compare(eng, ora, frules, n_res, n_origins):
             st, nr = ora.breaker(r, i)
             if st >= 0:
                 assert tuple(head[1 + 6 * i: 6 + 6 * i]) == (st, nr) + ora.breaker_stat(r, i), f"breaker {i} of {r}"
-        has_origin_rules = any(f["resource"] == r and f["limit_app"] != abi.LIMIT_APP_DEFAULT for f in frules)
-        order = ora.rule_order(r)
-        if not has_origin_rules or not order or n_origins == 0:
-            continue
-        if len(order) == 1 and frules[order[0]]["limit_app"] == abi.LIMIT_APP_DEFAULT:
-            continue
-        for o in range(1, n_origins + 1):
-            so, bo, mo, th, _ = ora.origin_dump(r, o)
-            sg, bg, mg, hg = eng.local_origin_state(r, o)
+        for o in range(1, n_origins + 1):  # every origin node, whatever the rules (created at the first origin event)
+            so, bo, mo, th, ex = ora.origin_dump(r, o)
+            sg, bg, mg, hg, gx = eng.local_origin_state(r, o, with_exists=True)
+            assert ex == gx, f"origin {o} node of {r}: exists {ex} vs {gx}"
             assert np.array_equal(so, sg), f"origin {o} second window of {r}:\n{so}\nvs\n{sg}"
             assert np.array_equal(bo, bg), f"origin {o} borrow array of {r}"
             assert np.array_equal(mo, mg), f"origin {o} minute window of {r}"

@@ -312,3 +312,33 @@ def test_chain_two_rules_first_failure_wins(t0):
     assert ch.controller(1)[2] == t0                                  # the limiter did not run
     assert ch.entry(t0 + 5)[0] == abi.LOCAL_PASS                      # no origin: only the limiter
     assert ch.controller(1)[2] == t0 + 5
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_nodes_created_on_first_entry_whatever_the_rules(t0):
+    """ClusterBuilderSlot.entry (ClusterBuilderSlot.java:99-102) gets or creates the origin node of every entry with
+    an origin, and NodeSelectorSlot.entry (NodeSelectorSlot.java:156-170) the DefaultNode of every entry's context,
+    whether or not a rule reads them; StatisticSlot (StatisticSlot.java:62-69) counts the entry on both. A rule set
+    naming no origin and no context still grows them; context tracking cannot start after a batch."""
+    ch = LocalChain(2, 1000, 500)
+    ch.load_rules(np.array([local_rule(), local_rule()]))
+    assert ch.load_flow_rules(np.array([local_flow_rule(0, 100.0)]), n_origins=2, n_contexts=2) == 1
+    ev = np.zeros(3, abi.LOCAL_EVENT_DTYPE)
+    ev["ts_ms"], ev["resource"], ev["count"], ev["origin"] = t0, [0, 0, 1], [1, 2, 1], [1, 1, 0]
+    ext = np.zeros(3, abi.SLOT_EXT_DTYPE)
+    ext["context"], ext["args_null"] = [1, 1, 0], 1
+    out = ch.decide_ext(ev, ext, np.zeros(1, abi.PSLOT_ARG_DTYPE), np.zeros(1, np.uint64))
+    assert out["status"].tolist() == [abi.LOCAL_PASS] * 3
+    sec, _, mnt, th, exists = ch.origin_dump(0, 1)
+    assert exists and th == 2 and sec[:, 1].sum() == 3 and mnt[:, 1].sum() == 3
+    assert not ch.origin_dump(0, 2)[4] and not ch.origin_dump(1, 1)[4]      # resource 1's entry had no origin
+    sec, _, _, th, exists = ch.context_dump(0, 1)
+    assert exists and th == 2 and sec[:, 1].sum() == 3
+    assert not ch.context_dump(0, 0)[4] and ch.context_dump(1, 0)[4]
+    ch2 = LocalChain(2, 1000, 500)
+    ch2.load_rules(np.array([local_rule()]))
+    ch2.load_flow_rules(np.array([local_flow_rule(0, 100.0)]))
+    ch2.decide(np.array([(t0, 0, 0, 1, abi.LOCAL_ENTRY, 0)], abi.LOCAL_EVENT_DTYPE))
+    with pytest.raises(ValueError, match=str(abi.SG_E_UNSUPPORTED)):
+        ch2.load_flow_rules(np.array([local_flow_rule(0, 100.0)]), n_contexts=1)
+    assert ch2.load_flow_rules(np.array([local_flow_rule(0, 100.0, limit_app=1)]), n_origins=1) == 1

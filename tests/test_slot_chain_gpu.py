@@ -145,7 +145,7 @@ def _entries(rng, n, n_res, t_start, span, n_origins, zipf=1.0, prio=0.05, multi
     cnt[m] = rng.integers(2, 4, int(m.sum()))
     e["count"] = cnt
     e["resource"] |= np.where(rng.random(n) < prio, np.uint32(abi.KEY_PRIO), np.uint32(0))
-    og = rng.integers(1, n_origins + 1, n).astype(np.int32)
+    og = rng.integers(1, n_origins + 1, n).astype(np.int32) if n_origins else np.zeros(n, np.int32)
     og[rng.random(n) < 0.3] = 0
     e["origin"] = og
     return e
@@ -163,21 +163,20 @@ def _compare(eng, ora, ps, frules, params, n_res, n_origins, n_ctx, pool):
             st, nr = ora.breaker(r, i)
             if st >= 0:
                 assert tuple(head[1 + 6 * i: 6 + 6 * i]) == (st, nr) + ora.breaker_stat(r, i), f"breaker {i} of {r}"
-        mine = frules[frules["resource"] == r]
-        if n_origins and (mine["limit_app"] != abi.LIMIT_APP_DEFAULT).any():
-            for o in range(1, n_origins + 1):
-                so, bo, mo, th, _ = ora.origin_dump(r, o)
-                sg, bg, mg, hg = eng.local_origin_state(r, o)
-                assert np.array_equal(so, sg) and np.array_equal(bo, bg) and np.array_equal(mo, mg), \
-                    f"origin {o} node of {r}"
-                assert hg[0] == th, f"origin {o} threads of {r}"
-        if n_ctx and (mine["strategy"] == CHAIN).any():
-            for c in range(n_ctx):
-                so, bo, mo, th, _ = ora.context_dump(r, c)
-                sg, bg, mg, hg = eng.local_context_state(r, c)
-                assert np.array_equal(so, sg) and np.array_equal(bo, bg) and np.array_equal(mo, mg), \
-                    f"context {c} node of {r}"
-                assert hg[0] == th, f"context {c} threads of {r}"
+        for o in range(1, n_origins + 1):  # every origin node and DefaultNode, whatever the rules
+            so, bo, mo, th, ex = ora.origin_dump(r, o)
+            sg, bg, mg, hg, gx = eng.local_origin_state(r, o, with_exists=True)
+            assert ex == gx, f"origin {o} node of {r}: exists {ex} vs {gx}"
+            assert np.array_equal(so, sg) and np.array_equal(bo, bg) and np.array_equal(mo, mg), \
+                f"origin {o} node of {r}"
+            assert hg[0] == th, f"origin {o} threads of {r}"
+        for c in range(n_ctx):
+            so, bo, mo, th, ex = ora.context_dump(r, c)
+            sg, bg, mg, hg, gx = eng.local_context_state(r, c, with_exists=True)
+            assert ex == gx, f"context {c} node of {r}: exists {ex} vs {gx}"
+            assert np.array_equal(so, sg) and np.array_equal(bo, bg) and np.array_equal(mo, mg), \
+                f"context {c} node of {r}"
+            assert hg[0] == th, f"context {c} threads of {r}"
     for i in range(len(frules)):
         want = ora.controller(i)
         if want is not None:
@@ -268,9 +267,7 @@ def test_relate_to_a_resource_never_entered():
 
 def test_reload_keeps_origin_and_context_nodes():
     """A flow-rule reload keeps the origin nodes and context DefaultNodes (ClusterNode.originCountMap and
-    NodeSelectorSlot's nodes outlive it) and the param state; the new rules read them at once. The reload's rule
-    sets name origins / contexts only on resources that already named them (the device keeps nodes from the first
-    load that needs them; the reference from the first entry)."""
+    NodeSelectorSlot's nodes outlive it) and the param state; the new rules read them at once."""
     rng = np.random.default_rng(13)
     n_res, n_origins, n_ctx = 20, 3, 3
     sets = [_flow_rules(rng, r, n_res, n_origins, n_ctx) for r in range(n_res)]
@@ -293,8 +290,69 @@ def test_reload_keeps_origin_and_context_nodes():
     fr2 = np.array(flat, abi.LOCAL_FLOW_RULE_DTYPE)
     assert eng.local_load_flow_rules(fr2, n_origins, n_ctx) == ora.load_flow_rules(fr2, n_origins, n_ctx)
     _run(ora, ps, eng, fr2, params, n_res, n_origins, n_ctx, [(10_000, 2000), (10_000, 2000)], 14, pool=pool, gen=gen,
-         t=t, compare=False)
-    _compare(eng, ora, ps, fr, params, n_res, n_origins, n_ctx, pool)   # every node the first load created
+         t=t)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_reload_adds_origin_and_chain_rules_to_plain_resources(seed):
+    """Resources that had only the fast path's one rule (or none) get limitApp-origin, THREAD-grade origin, "other"
+    and CHAIN rules mid-stream, with entries in flight across the reload. The origin nodes and the DefaultNodes have
+    counted every event since the resources' first entries (ClusterBuilderSlot.java:99-102, NodeSelectorSlot
+    .java:156-170), so the new rules read the windows and curThreadNum the reference's nodes hold — including
+    threads of entries admitted before the reload that exit after it."""
+    rng = np.random.default_rng(seed)
+    n_res, n_origins, n_ctx = 24, 3, 3
+    plain = [[local_flow_rule(r, float(rng.integers(20, 80)))] if r % 3 else [] for r in range(n_res)]
+    ora, ps, eng, fr, params = _setup(rng, n_res, n_origins, n_ctx, rule_sets=plain,
+                                      params=np.zeros(0, abi.PSLOT_RULE_DTYPE), breakers=False)
+    # long response times keep entries in flight across the reload
+    t, pool, gen = _run(ora, ps, eng, fr, params, n_res, n_origins, n_ctx, [(12_000, 2000), (12_000, 2000)], seed,
+                        rt_hi=900)
+    o = lambda: int(rng.integers(1, n_origins + 1))  # noqa: E731
+    sets2 = []
+    for r in range(n_res):
+        u = r % 6
+        if u == 0:
+            sets2.append([local_flow_rule(r, float(rng.integers(1, 4)), grade=abi.FLOW_GRADE_THREAD, limit_app=o()),
+                          local_flow_rule(r, 60.0)])
+        elif u == 1:
+            sets2.append([local_flow_rule(r, float(rng.integers(2, 10)), limit_app=o())])
+        elif u == 2:
+            sets2.append([local_flow_rule(r, float(rng.integers(2, 6)), grade=abi.FLOW_GRADE_THREAD, limit_app=OTHER)])
+        elif u == 3:
+            sets2.append([local_flow_rule(r, float(rng.integers(2, 10)), strategy=CHAIN, ref=int(rng.integers(0, n_ctx)))])
+        elif u == 4:
+            sets2.append([local_flow_rule(r, float(rng.integers(1, 4)), grade=abi.FLOW_GRADE_THREAD, strategy=CHAIN,
+                                          ref=int(rng.integers(0, n_ctx))), local_flow_rule(r, 5.0, limit_app=o())])
+        else:
+            sets2.append(plain[r])
+    flat = [x for rs in sets2 for x in rs]
+    rng.shuffle(flat)
+    fr2 = np.array(flat, abi.LOCAL_FLOW_RULE_DTYPE)
+    assert eng.local_load_flow_rules(fr2, n_origins, n_ctx) == ora.load_flow_rules(fr2, n_origins, n_ctx)
+    _run(ora, ps, eng, fr2, params, n_res, n_origins, n_ctx, [(12_000, 2000), (12_000, 2000)], seed + 50, pool=pool,
+         gen=gen, t=t, rt_hi=900)
+
+
+def test_origins_declared_later_and_context_tracking_contract():
+    """Origin ids can be declared at a later load (no earlier event could carry them, so the origin nodes are exact
+    from their first event); context tracking cannot start after a batch (the DefaultNodes would miss the entries
+    before it): SG_E_UNSUPPORTED on the device and in the oracle."""
+    from sentinel_amd.engine import EngineError
+    rng = np.random.default_rng(23)
+    n_res = 10
+    plain = [[local_flow_rule(r, 30.0)] for r in range(n_res)]
+    ora, ps, eng, fr, params = _setup(rng, n_res, 0, 0, rule_sets=plain, params=np.zeros(0, abi.PSLOT_RULE_DTYPE))
+    t, pool, gen = _run(ora, ps, eng, fr, params, n_res, 0, 0, [(5_000, 1500)], 23, rt_hi=600)
+    with pytest.raises(EngineError) as ei:
+        eng.local_load_flow_rules(fr, 0, 2)
+    assert ei.value.code == abi.SG_E_UNSUPPORTED
+    with pytest.raises(ValueError, match=str(abi.SG_E_UNSUPPORTED)):
+        ora.load_flow_rules(fr, 0, 2)
+    fr2 = np.array([local_flow_rule(r, 3.0, grade=abi.FLOW_GRADE_THREAD, limit_app=1 + r % 2) for r in range(n_res)] +
+                   [local_flow_rule(r, 40.0) for r in range(n_res)], abi.LOCAL_FLOW_RULE_DTYPE)
+    assert eng.local_load_flow_rules(fr2, 2, 0) == ora.load_flow_rules(fr2, 2, 0)
+    _run(ora, ps, eng, fr2, params, n_res, 2, 0, [(5_000, 1500), (5_000, 1500)], 24, pool=pool, gen=gen, t=t, rt_hi=600)
 
 
 def test_cluster_state_contract():
