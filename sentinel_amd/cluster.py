@@ -109,7 +109,7 @@ class LimiterExchange:
 
     def __init__(self, engine, device, coll_device=None, group=None):
         self.eng = engine
-        self.n_lim = engine.lim_slots()  # the layout [world][n_lim][n_ms] is the engine's, not the caller's
+        self.n_lim = engine.lim_slots()  # the layout [world][n_lim][n_ms] is the engine's (re-read by every arm())
         self.device = torch.device(device)
         self.coll = torch.device(coll_device) if coll_device is not None else self.device
         self.group = group
@@ -132,6 +132,7 @@ class LimiterExchange:
         """Count, exchange and arm for this rank's batch (device records at req_ptr: sg_req, or sg_cparam_req with
         param=True). Every rank calls this for every node batch, with n = 0 when it has no requests; the caller
         then decides its batch (n may be 0) on any flow entry point, or sg_cparam_decide_batch for param=True."""
+        self.n_lim = self.eng.lim_slots()  # set_namespaces may have changed the limiter slots since the last batch
         rng = self.time_range(t_first, t_last)
         if rng is None:
             rng = (0, 1)  # no requests anywhere: nothing to count, the windows see no tryPass

@@ -124,6 +124,8 @@ class MetricWriter:
         self.base_dir = base_dir
         os.makedirs(base_dir, exist_ok=True)
         self.app, self.pid, self.tz = app_name, pid, tz
+        # MetricWriter.timeSecondBase: "1970-01-01 00:00:00" parsed in the writer's zone = -(the zone's offset then)
+        self._epoch_off = int(datetime.datetime(1970, 1, 1, tzinfo=tz).utcoffset().total_seconds())
         self.single_file_size, self.total_file_count = single_file_size, total_file_count
         self.last_second = start_ms // 1000
         self.base_file_name = None
@@ -163,9 +165,9 @@ class MetricWriter:
         return os.path.getsize(self.cur_file) < self.single_file_size
 
     def _is_new_day(self, last_second, second):
-        # timeSecondBase = "1970-01-01 00:00:00" parsed in the writer's zone, i.e. -utcoffset
-        off = int(datetime.datetime.fromtimestamp(second, self.tz).utcoffset().total_seconds())
-        return (second + off) // 86400 > (last_second + off) // 86400
+        # MetricWriter.isNewDay: (second - timeSecondBase) / 86400 with one timeSecondBase, "1970-01-01 00:00:00"
+        # parsed in the writer's zone once (the zone's offset at the epoch, not at either second)
+        return (second + self._epoch_off) // 86400 > (last_second + self._epoch_off) // 86400
 
     def _write_lines(self, nodes):
         buf = "".join(fat_line(r, self._name(r), self._cls(r), tz=self.tz) for r in nodes).encode("utf-8")

@@ -172,6 +172,30 @@ def test_serial_fallback(monkeypatch):
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
 
 
+@pytest.mark.parametrize("max_rounds", [1, 2, 4, 5])
+def test_round_budget_inside_a_chain(monkeypatch, max_rounds):
+    """Round budgets that end inside a chain of three enqueued rounds (r1 = min(round + 3, max)) and the serial
+    fallback after rounds > 0 (the saved rings restored by k_cp_saverings before k_cp_serial): a multi-value-heavy
+    trace over a few hot values needs more rounds than the budget, so the batch ends serially — same answers and
+    window sums; a batch that converges within the budget reports its rounds."""
+    monkeypatch.setenv("SG_CP_MAX_ROUNDS", str(max_rounds))
+    rng = np.random.default_rng(40 + max_rounds)
+    rules = _rules(5, rng)
+    rules["count"] = rng.integers(3, 12, 5)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_250
+    serial = 0
+    for _ in range(3):
+        req, vals = _trace(rng, 30_000, 5, 12, t, 2500, multi=0.8, zipf=1.3, bad=0.005)
+        _check(eng, ora, req, vals)
+        r = eng.cparam_last_rounds()
+        assert 1 <= r <= max_rounds + 1
+        serial += r == max_rounds + 1
+        t = int(req["ts_ms"][-1]) + 3
+    assert serial > 0, "the trace should outlast the round budget"
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
 def test_limiter_shared_with_flow_tokens():
     """allowProceed → GlobalRequestLimiter.tryPass (ClusterParamFlowChecker.java:45): the namespace's limiter
     admits param and flow requests from one 10 x 100 ms window, so time-ordered flow and param batches interleave."""

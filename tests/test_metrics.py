@@ -152,3 +152,18 @@ def test_timer_listener_groups_by_second_entry_node_last(tmp_path):
     idx = M.read_index(M.form_index_file_name(f))
     assert [s for s, _ in idx] == [t0 // 1000, t0 // 1000 + 1]
     assert idx[0][1] == 0 and idx[1][1] == sum(len(fat_line(_rows(t0, [0])[0], n)) for n in ("a", "b", M.ENTRY_NODE_NAME))
+
+
+def test_new_day_uses_the_epoch_offset_of_the_zone(tmp_path):
+    """MetricWriter.isNewDay divides (second - timeSecondBase) by 86400 with timeSecondBase = "1970-01-01 00:00:00"
+    parsed once in the writer's zone: in America/New_York (EST at the epoch) the day rolls at 05:00 UTC all year,
+    i.e. at 01:00 local time under daylight saving time."""
+    import datetime
+    import zoneinfo
+    tz = zoneinfo.ZoneInfo("America/New_York")
+    w = MetricWriter(str(tmp_path), "app", 1 << 20, tz=tz)
+    utc = datetime.timezone.utc
+    s = lambda h, m: int(datetime.datetime(2024, 7, 1, h, m, tzinfo=utc).timestamp())  # noqa: E731
+    assert not w._is_new_day(s(4, 10), s(4, 50))   # 00:10 → 00:50 EDT: the EST day has not rolled yet
+    assert w._is_new_day(s(4, 50), s(5, 10))       # 00:50 → 01:10 EDT: 00:00 EST passed
+    w.close()
