@@ -365,9 +365,14 @@ typedef struct sg_local_config {
 #define SG_STRATEGY_RELATE     1            /* STRATEGY_RELATE: the ClusterNode of resource ref_resource     */
 #define SG_STRATEGY_CHAIN      2            /* STRATEGY_CHAIN: the resource's DefaultNode of context ref_resource,
                                                only for entries in that context                             */
-/* FlowRule.clusterMode with its ClusterFlowConfig (FlowRuleChecker.passClusterCheck :147-164). The device decides
- * cluster-mode rules as a node whose ClusterStateManager is neither client nor server (the default,
- * CLUSTER_NOT_STARTED): pickClusterService() is null, so fallbackToLocalOrPass (:166-175) applies. */
+/* FlowRule.clusterMode with its ClusterFlowConfig (FlowRuleChecker.passClusterCheck :147-164). On a node that is
+ * neither token client nor server (CLUSTER_NOT_STARTED, the default) pickClusterService() is null, so
+ * fallbackToLocalOrPass (:166-175) applies. On a node whose embedded token server runs on this handle
+ * (sg_local_set_cluster_state(SERVER), DefaultEmbeddedTokenServer.requestToken → DefaultTokenService, :46-51) a
+ * cluster-mode rule requests a token for its flowId from the handle's own cluster flow state (sg_load_flow_rules,
+ * the namespace limiter included) in the batch's event order, and applyTokenResult (:186-209) maps the answer: OK
+ * passes, SHOULD_WAIT passes after wait_ms (added to the entry's wait), BLOCKED throws FlowException, and
+ * NO_RULE_EXISTS / BAD_REQUEST / FAIL / TOO_MANY_REQUEST go to fallbackToLocalOrPass. */
 #define SG_CLUSTER_MODE_OFF         0       /* a local rule                                                 */
 #define SG_CLUSTER_MODE_FALLBACK    1       /* clusterMode, fallbackToLocalWhenFail: checked as a local rule  */
 #define SG_CLUSTER_MODE_NO_FALLBACK 2       /* clusterMode without fallback: the rule is not activated (pass) */
@@ -386,12 +391,19 @@ typedef struct sg_local_flow_rule {
     int32_t  cluster_mode;        /* SG_CLUSTER_MODE_*                                            */
     int32_t  cluster_config;      /* the caller's id of the ClusterFlowConfig value (FlowRule.equals
                                      compares it; 0 = none)                                       */
+    uint32_t cluster_key;         /* cluster mode on an embedded server: ClusterFlowConfig.flowId as a rule
+                                     index of this handle's sg_load_flow_rules (SG_KEY_NO_RULE: the server
+                                     has no rule for it, as sg_req.key)                           */
 } sg_local_flow_rule;
 
 /* ClusterStateManager state of the node (ClusterStateManager.java: CLUSTER_CLIENT 0, CLUSTER_SERVER 1,
- * CLUSTER_NOT_STARTED -1). Only NOT_STARTED is decided on the device; with CLIENT / SERVER, cluster-mode rules go
- * through a token service the batch cannot call in order, so loading them (or setting such a state while they
- * are loaded) is SG_E_UNSUPPORTED. */
+ * CLUSTER_NOT_STARTED -1). NOT_STARTED and SERVER (the embedded token server on this handle, see above) are
+ * decided on the device. In SERVER state the resources whose cluster-mode rules share a flowId, or name flowIds of
+ * one limiter-enabled namespace, walk together in event order (one key group), and a local batch with such rules
+ * must not precede the handle's flow batches in time (SG_E_TIME), nor they it. CLIENT sends tokens over the
+ * network, which a batch cannot call in order: loading cluster-mode rules in CLIENT state (or entering it while they
+ * are loaded) is SG_E_UNSUPPORTED, as is SERVER on a sharded handle (sg_set_shard) whose cluster
+ * rules name a limiter-enabled namespace. */
 #define SG_CLUSTER_CLIENT        0
 #define SG_CLUSTER_SERVER        1
 #define SG_CLUSTER_NOT_STARTED (-1)

@@ -88,6 +88,7 @@ def lib():
         "or_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
         "or_local_decide_ext": (C.c_int, [vp, vp, vp, u64, vp, vp, vp]),
         "or_local_attach_pslot": (None, [vp, vp]),
+        "or_local_attach_cluster": (C.c_int, [vp, vp, C.c_int]),
         "or_local_set_entry_types": (C.c_int, [vp, vp, u32]),
         "or_local_context_dump": (C.c_int, [vp, u32, C.c_int, vp, vp, vp, vp]),
         "or_lgen_run_ext": (u64, [vp, vp, vp, vp, vp, u64, i64, vp, vp, vp, u64, vp, vp]),
@@ -581,14 +582,15 @@ def degrade_rule(grade, count, time_window_sec, min_request_amount=5, stat_inter
 
 def local_flow_rule(resource=0, count=0.0, grade=abi.FLOW_GRADE_QPS, behavior=abi.CONTROL_DEFAULT,
                     limit_app=abi.LIMIT_APP_DEFAULT, warm_up_sec=10, max_queueing_ms=500, strategy=abi.STRATEGY_DIRECT,
-                    ref=-1, cluster_mode=abi.CLUSTER_MODE_OFF, cluster_config=0):
+                    ref=-1, cluster_mode=abi.CLUSTER_MODE_OFF, cluster_config=0, cluster_key=abi.KEY_NO_RULE):
     """sg_local_flow_rule: FlowRule defaults (FlowRule.java: warmUpPeriodSec 10, maxQueueingTimeMs 500; refResource
-    null = -1; clusterMode false)."""
+    null = -1; clusterMode false). cluster_key: the flowId's rule index on an embedded token server."""
     r = np.zeros((), abi.LOCAL_FLOW_RULE_DTYPE)
     r["resource"], r["grade"], r["count"], r["control_behavior"] = resource, grade, count, behavior
     r["limit_app"], r["strategy"], r["warm_up_period_sec"], r["max_queueing_ms"] = (limit_app, strategy, warm_up_sec,
                                                                                    max_queueing_ms)
     r["ref_resource"], r["cluster_mode"], r["cluster_config"] = ref, cluster_mode, cluster_config
+    r["cluster_key"] = cluster_key
     return r
 
 
@@ -661,6 +663,14 @@ class LocalChain:
     def load_rules(self, rules):
         rules = np.ascontiguousarray(rules, dtype=abi.LOCAL_RULE_DTYPE).reshape(-1)
         assert lib().or_local_load_rules(self.h, abi.ptr(rules), len(rules)) == 0
+
+    def attach_cluster(self, cts, state):
+        """ClusterStateManager state of the node; with CLUSTER_SERVER the cluster-mode rules request tokens from
+        `cts` (a ClusterTokenService: the embedded token server's DefaultTokenService)."""
+        self._cts = cts
+        rc = lib().or_local_attach_cluster(self.h, cts.h if cts is not None else None, state)
+        if rc < 0:
+            raise ValueError(f"or_local_attach_cluster: {rc}")
 
     def load_flow_rules(self, rules, n_origins=0, n_contexts=0):
         """FlowRuleManager.loadRules: returns the number of rules kept."""

@@ -905,6 +905,8 @@ struct or_local {
     int64_t* last_fetch;     /* StatisticNode.lastFetchTime per resource (metrics()) */
     int32_t n_origins, n_contexts;
     uint64_t batches;        /* batches decided since or_local_load_rules */
+    or_cts* cts;             /* the embedded token server's DefaultTokenService (cluster_state SERVER) */
+    int cluster_state;       /* ClusterStateManager: SG_CLUSTER_NOT_STARTED (default), SERVER */
     int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
     uint32_t n_rules;
     struct or_pslot* ps;     /* ParamFlowSlot's rules and metrics (or_local_attach_pslot), NULL = none */
@@ -919,6 +921,7 @@ or_local* or_local_new(int second_sample_count, int second_interval_ms, int occu
     l->interval = second_interval_ms;      /* IntervalProperty.INTERVAL, default 1000        */
     l->occupy_timeout = occupy_timeout_ms; /* OccupyTimeoutProperty.occupyTimeout, 500      */
     l->cold_factor = 3;                    /* ColdFactorProperty.coldFactor (SentinelConfig default 3) */
+    l->cluster_state = SG_CLUSTER_NOT_STARTED;
     return l;
 }
 
@@ -1330,12 +1333,49 @@ static int default_can_pass(or_local* l, or_node* sn, const or_ctl* c, int64_t t
     return 0;
 }
 
+int or_local_attach_cluster(or_local* l, or_cts* cts, int state) {
+    if (state == SG_CLUSTER_CLIENT) return SG_E_UNSUPPORTED;
+    if (state == SG_CLUSTER_SERVER && !cts) return SG_E_INVAL;
+    l->cts = state == SG_CLUSTER_SERVER ? cts : NULL;
+    l->cluster_state = state;
+    return 0;
+}
+
+/* FlowRuleChecker.passClusterCheck (:147-164) with applyTokenResult (:186-209) on a node whose embedded token server
+ * answers (pickClusterService → EmbeddedClusterTokenServerProvider.getServer, :177-184; DefaultEmbeddedTokenServer
+ * .requestToken → DefaultTokenService.requestToken, DefaultEmbeddedTokenServer.java:46-51): 1 pass (*wait += the
+ * SHOULD_WAIT sleep), 0 BLOCKED, -1 fallbackToLocalOrPass. */
+static int cluster_token(or_local* l, const or_ctl* c, int64_t t, int count, int prio, int64_t* wait) {
+    sg_req q;
+    memset(&q, 0, sizeof(q));
+    q.ts_ms = t;
+    q.key = (c->rule.cluster_key & SG_KEY_INDEX) | (prio ? SG_KEY_PRIO : 0u);
+    q.acquire = count;
+    sg_result r;
+    or_cts_decide(l->cts, &q, 1, &r);
+    switch (r.status) {
+    case SG_STATUS_OK: return 1;
+    case SG_STATUS_SHOULD_WAIT: *wait += r.wait_ms; return 1;   /* Thread.sleep(waitInMs), then pass */
+    case SG_STATUS_NO_RULE_EXISTS:
+    case SG_STATUS_BAD_REQUEST:
+    case SG_STATUS_FAIL:
+    case SG_STATUS_TOO_MANY_REQUEST: return -1;
+    default: return 0;                                          /* BLOCKED */
+    }
+}
+
 /* FlowSlot.checkFlow → FlowRuleChecker.checkFlow (:44-57): the rules in order, the first failure throws. A cluster-mode
- * rule on a node that is neither token client nor server: passClusterCheck → fallbackToLocalOrPass (:147-175). */
+ * rule: passClusterCheck (:147-164) — the embedded server's token (SERVER state) or, with no token service
+ * (NOT_STARTED) and for the answers applyTokenResult sends there, fallbackToLocalOrPass (:166-175). */
 static int check_flow(or_local* l, or_node* nd, int64_t t, int count, int prio, int origin, int context, int64_t* wait) {
     *wait = 0;
     for (uint32_t i = 0; i < nd->n_ctl; i++) {
         or_ctl* c = &nd->ctl[i];
+        if (c->rule.cluster_mode != SG_CLUSTER_MODE_OFF && l->cluster_state == SG_CLUSTER_SERVER) {
+            const int v = cluster_token(l, c, t, count, prio, wait);
+            if (v == 0) return SG_LOCAL_BLOCK_FLOW;
+            if (v == 1) continue;
+        }
         if (c->rule.cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) continue;   /* the rule is not activated */
         const int32_t ref = c->rule.ref_resource;
         or_node* rn = (ref >= 0 && (uint32_t)ref < l->n) ? &l->nodes[ref] : NULL;

@@ -173,6 +173,9 @@ int       or_local_decide_ext(or_local* l, const sg_local_event* ev, const sg_sl
                               const sg_pslot_arg* args, const uint64_t* values, sg_local_result* out);
 struct or_pslot;
 void      or_local_attach_pslot(or_local* l, struct or_pslot* ps);
+/* ClusterStateManager state (SG_CLUSTER_*); SERVER: cluster-mode rules request tokens from `cts` (the embedded
+ * token server's DefaultTokenService). CLIENT is not modelled (SG_E_UNSUPPORTED). */
+int       or_local_attach_cluster(or_local* l, or_cts* cts, int state);
 int       or_local_context_dump(const or_local* l, uint32_t res, int context, int64_t* second, int64_t* borrow,
                                 int64_t* minute, int64_t* threads);
 void      or_local_set_cold_factor(or_local* l, int cold_factor);

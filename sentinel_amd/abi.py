@@ -137,7 +137,8 @@ LOCAL_PASS, LOCAL_BLOCK_FLOW, LOCAL_BLOCK_DEGRADE, LOCAL_PASS_WAIT = 0, 1, 2, 3
 LOCAL_FLOW_RULE_DTYPE = np.dtype([("resource", "<u4"), ("grade", "<i4"), ("count", "<f8"),
                                   ("control_behavior", "<i4"), ("limit_app", "<i4"), ("strategy", "<i4"),
                                   ("warm_up_period_sec", "<i4"), ("max_queueing_ms", "<i4"),
-                                  ("ref_resource", "<i4"), ("cluster_mode", "<i4"), ("cluster_config", "<i4")],
+                                  ("ref_resource", "<i4"), ("cluster_mode", "<i4"), ("cluster_config", "<i4"),
+                                  ("cluster_key", "<u4")],
                                  align=True)
 CLUSTER_MODE_OFF, CLUSTER_MODE_FALLBACK, CLUSTER_MODE_NO_FALLBACK, CLUSTER_MODE_INVALID = 0, 1, 2, -1
 CLUSTER_CLIENT, CLUSTER_SERVER, CLUSTER_NOT_STARTED = 0, 1, -1
@@ -162,7 +163,7 @@ assert NS_DTYPE.itemsize == C.sizeof(sg_namespace) == 16
 assert CPARAM_RULE_DTYPE.itemsize == 40 and CPARAM_REQ_DTYPE.itemsize == 24
 assert DEGRADE_RULE_DTYPE.itemsize == 32 and LOCAL_RULE_DTYPE.itemsize == 80
 assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
-assert LOCAL_FLOW_RULE_DTYPE.itemsize == 48 and SLOT_EXT_DTYPE.itemsize == 16
+assert LOCAL_FLOW_RULE_DTYPE.itemsize == 56 and SLOT_EXT_DTYPE.itemsize == 16
 assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
 assert METRIC_NODE_DTYPE.itemsize == 64
 assert PSLOT_RULE_DTYPE.itemsize == PARAM_RULE_DTYPE.itemsize + 16 and PSLOT_EVENT_DTYPE.itemsize == 32

@@ -186,6 +186,10 @@ struct sg_handle {
     int32_t l_n_contexts = 0;
     int32_t l_cluster_state = SG_CLUSTER_NOT_STARTED;
     bool l_cluster_rules = false;     // some loaded flow rule is in cluster mode
+    std::vector<uint8_t> l_base_cx;   // per resource: walked by the cx walker whatever the key groups
+    std::vector<std::pair<uint32_t, uint32_t>> l_relate;        // RELATE (resource, referenced resource)
+    std::vector<std::pair<uint32_t, uint32_t>> l_cluster_refs;  // cluster-mode rules: (resource, cluster_key)
+    bool l_groups_stale = false;      // cluster rules / namespaces / cluster state changed: regroup before a batch
     uint32_t* d_lgkey = nullptr;      // [K] RELATE key groups (record key of each resource), null without groups
     uint64_t l_ps_applied = 0;        // ps_gen whose param flags d_lrules carries (0: none)
     bool l_has_cx_ps = false;         // some resource is cx because of param rules
@@ -304,6 +308,7 @@ PSArgs pslot_args(sg_handle* h);          // below: the ParamFlowSlot state's de
 int ensure_layout(sg_handle* h);          // below: record layout of the loaded rules
 int flow_status(sg_handle* h, int err);   // below: batch error flags -> SG_E_*
 int drain_async(sg_handle* h);  // below: completes the handle's in-flight host-pipeline batches
+int local_apply_groups(sg_handle* h);  // below: key groups of the local chain
 }
 
 extern "C" {
@@ -405,6 +410,7 @@ int rebuild_wl_table(sg_handle* h) {
 }
 
 int upload_rule_table(sg_handle* h) {
+    h->l_groups_stale = true;  // an embedded token server's key groups follow the cluster rules / namespaces
     int rc = rebuild_wl_table(h);
     if (rc) return rc;
     // Bucket counts stay below thr * (2 + isec) * (2 + maxOccupyRatio): a pass needs PASS sum <= thr * isec,
@@ -2566,6 +2572,10 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
     h->l_n_contexts = 0;
     h->l_has_cx = false;
     h->l_cluster_rules = false;
+    h->l_base_cx.clear();
+    h->l_relate.clear();
+    h->l_cluster_refs.clear();
+    h->l_groups_stale = false;
     h->l_rule_slot.clear();
     dfree(h->d_lnkeys);
     dfree(h->d_lnvals);
@@ -2832,8 +2842,16 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
+    if (h->l_groups_stale && h->l_cluster_rules) {
+        const int grc = local_apply_groups(h);
+        if (grc) return grc;
+    }
     int prc = local_apply_params(h);
     if (prc) return prc;
+    const bool emb = h->l_cluster_state == SG_CLUSTER_SERVER && h->l_cluster_rules;
+    if (emb && h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "an embedded token server on a sharded handle with namespace limiters: the "
+                                         "limiter exchange covers flow and param batches only");
     const uint32_t K = (uint32_t)h->ltab.size();
     int kbits = bits_for((uint64_t)K);
     if (kbits < 1) kbits = 1;
@@ -2914,6 +2932,19 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         }
         L.epoch = h->l_epoch;
         L.track_ctx = h->l_n_contexts > 0 ? 1 : 0;
+    }
+    if (emb) {  // the embedded token server: this handle's cluster flow state
+        L.emb = 1;
+        L.c3_rules = h->d_rules;
+        L.c3_ring = h->d_ring;
+        L.c3_occ = h->d_occ;
+        L.c3_stride = h->stride;
+        L.c3_K = h->K;
+        L.max_occ_ratio = h->cfg.max_occupy_ratio;
+        L.c3_rule_lim = h->d_rule_lim;
+        L.lim_ring = h->d_lim_ring;
+        for (int j = 0; j < kMaxLim; ++j) L.lim_qps[j] = h->lim_qps[j];
+        L.c3_last_ts = h->d_last_ts;
     }
     L.flags = h->d_lflags;
     L.exit_pos = h->d_lexit_pos;
@@ -3184,6 +3215,7 @@ LFlowRule make_flow_rule(const sg_local_flow_rule& r, int cold) {
     f.strategy = r.strategy;
     f.ref = r.ref_resource < 0 ? -1 : r.ref_resource;
     f.cluster_mode = r.cluster_mode;
+    f.cluster_key = r.cluster_key;
     if (f.behavior == SG_CONTROL_WARM_UP || f.behavior == SG_CONTROL_WARM_UP_RATE_LIMITER) {
         f.warning_token = d2i_host(r.warm_up_period_sec * r.count) / (cold - 1);
         const int32_t two_w = (int32_t)(2u * (uint32_t)r.warm_up_period_sec);  // 2 * warmUpPeriodInSec: int
@@ -3236,12 +3268,76 @@ int sg_local_set_cluster_state(sg_handle* h, int32_t state) {
     if (!h) return SG_E_INVAL;
     if (state != SG_CLUSTER_CLIENT && state != SG_CLUSTER_SERVER && state != SG_CLUSTER_NOT_STARTED)
         return fail(h, SG_E_INVAL, "cluster state: CLIENT 0, SERVER 1 or NOT_STARTED -1");
-    if (state != SG_CLUSTER_NOT_STARTED && h->l_cluster_rules)
-        return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules need the token client / server: decided in order only "
-                                         "on a node that is neither (INTEGRATION.md §8)");
+    if (state == SG_CLUSTER_CLIENT && h->l_cluster_rules)
+        return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules on a token client: the tokens come over the network, "
+                                         "not in event order (INTEGRATION.md §8)");
+    if (state != h->l_cluster_state) h->l_groups_stale = true;  // embedded-server key groups follow the state
     h->l_cluster_state = state;
     return SG_OK;
 }
+
+namespace {
+
+// Key groups of the local chain (union-find, smallest resource first): a RELATE rule reads another resource's
+// ClusterNode (FlowRuleChecker.selectReferenceNode :96-112); on an embedded token server the resources whose
+// cluster-mode rules share a flowId share its ClusterMetric, and those naming flowIds of one limiter-enabled
+// namespace share its GlobalRequestLimiter — each group walks in event order on one lane. Sets LRule.grp / cx and
+// uploads the rule image and the record keys.
+int local_apply_groups(sg_handle* h) {
+    const uint32_t K = (uint32_t)h->ltab.size();
+    std::vector<uint32_t> parent(K);
+    for (uint32_t k = 0; k < K; ++k) parent[k] = k;
+    auto find = [&](uint32_t x) {
+        while (parent[x] != x) x = parent[x] = parent[parent[x]];
+        return x;
+    };
+    auto unite = [&](uint32_t a, uint32_t b) {
+        const uint32_t x = find(a), y = find(b);
+        if (x != y) parent[std::max(x, y)] = std::min(x, y);
+    };
+    for (const auto& pr : h->l_relate) unite(pr.first, pr.second);
+    if (h->l_cluster_state == SG_CLUSTER_SERVER) {
+        std::unordered_map<uint32_t, uint32_t> by_key;
+        int by_slot[kMaxLim];
+        for (int j = 0; j < kMaxLim; ++j) by_slot[j] = -1;
+        for (const auto& cr : h->l_cluster_refs) {
+            const uint32_t key = cr.second & SG_KEY_INDEX;
+            if (key >= h->K) continue;  // NO_RULE_EXISTS / BAD_REQUEST: no shared state
+            auto it = by_key.emplace(key, cr.first).first;
+            unite(cr.first, it->second);
+            const int ns = h->rules[key].namespace_id;
+            const int sl = (ns >= 0 && (size_t)ns < h->ns_slot.size()) ? h->ns_slot[ns] : -1;
+            if (sl >= 0) {
+                if (by_slot[sl] < 0) by_slot[sl] = (int)cr.first;
+                unite(cr.first, (uint32_t)by_slot[sl]);
+            }
+        }
+    }
+    std::vector<uint32_t> gkey(K), gsize(K, 0);
+    for (uint32_t k = 0; k < K; ++k) ++gsize[gkey[k] = find(k)];
+    bool groups = false, has_cx = false;
+    for (uint32_t k = 0; k < K; ++k) {
+        LRule& L = h->ltab[k];
+        L.grp = gsize[gkey[k]] > 1 ? 1 : 0;
+        L.cx = (h->l_base_cx.size() == K && h->l_base_cx[k]) || L.grp ? 1 : 0;
+        groups = groups || L.grp;
+        has_cx = has_cx || L.cx;
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipDeviceSynchronize());
+    dfree(h->d_lgkey);
+    if (groups) {
+        if (hipMalloc(&h->d_lgkey, sizeof(uint32_t) * K) != hipSuccess) return fail(h, SG_E_NOMEM, "key groups");
+        HIP_TRY(h, hipMemcpy(h->d_lgkey, gkey.data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice));
+    }
+    if (K) HIP_TRY(h, hipMemcpy(h->d_lrules, h->ltab.data(), sizeof(LRule) * K, hipMemcpyHostToDevice));
+    h->l_has_cx = has_cx;
+    h->l_ps_applied = 0;  // param flags are re-applied to the new rule image by the next batch
+    h->l_groups_stale = false;
+    return SG_OK;
+}
+
+}  // namespace
 
 int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint32_t n, int32_t n_origins,
                              int32_t n_contexts) {
@@ -3270,38 +3366,17 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
         if (r.cluster_mode != SG_CLUSTER_MODE_OFF && r.cluster_mode != SG_CLUSTER_MODE_FALLBACK &&
             r.cluster_mode != SG_CLUSTER_MODE_NO_FALLBACK)
             return fail(h, SG_E_INVAL, "cluster_mode");
-        if (r.cluster_mode != SG_CLUSTER_MODE_OFF && h->l_cluster_state != SG_CLUSTER_NOT_STARTED)
-            return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules on a token client / server (INTEGRATION.md §8)");
+        if (r.cluster_mode != SG_CLUSTER_MODE_OFF && h->l_cluster_state == SG_CLUSTER_CLIENT)
+            return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules on a token client (INTEGRATION.md §8)");
         bool dup = false;
         for (uint32_t j : by_res[r.resource]) dup = dup || local_flow_rule_same(rules[j], r);
         if (!dup) by_res[r.resource].push_back(i);
         cluster_rules = cluster_rules || r.cluster_mode != SG_CLUSTER_MODE_OFF;
     }
-    // RELATE key groups: a rule reading another resource's ClusterNode joins the two (union-find, smallest index first)
-    std::vector<uint32_t> parent(K);
-    for (uint32_t k = 0; k < K; ++k) parent[k] = k;
-    auto find = [&](uint32_t x) {
-        while (parent[x] != x) x = parent[x] = parent[parent[x]];
-        return x;
-    };
-    bool groups = false;
-    for (uint32_t k = 0; k < K; ++k)
-        for (uint32_t i : by_res[k]) {
-            const sg_local_flow_rule& r = rules[i];
-            if (r.strategy != SG_STRATEGY_RELATE || r.ref_resource < 0 || (uint32_t)r.ref_resource >= K ||
-                (uint32_t)r.ref_resource == k)
-                continue;
-            const uint32_t x = find(k), y = find((uint32_t)r.ref_resource);
-            if (x != y) parent[std::max(x, y)] = std::min(x, y);
-            groups = true;
-        }
-    std::vector<uint32_t> gkey(K);
-    std::vector<uint32_t> gsize(K, 0);
-    for (uint32_t k = 0; k < K; ++k) ++gsize[gkey[k] = find(k)];
-
+    std::vector<std::pair<uint32_t, uint32_t>> relate, cluster_refs;
+    std::vector<uint8_t> base_cx(K, 0);
     std::vector<LRule> tab = h->ltab;
     std::vector<LFlowRule> fr;
-    bool has_cx = false;
     for (uint32_t k = 0; k < K; ++k) {
         std::vector<uint32_t>& v = by_res[k];
         // Collections.sort(FlowRuleComparator) (:30-55): stable; cluster-mode rules last, then limitApp "default" last
@@ -3309,17 +3384,24 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
             return (rules[x].cluster_mode != SG_CLUSTER_MODE_OFF ? 2 : 0) + (rules[x].limit_app == SG_LIMIT_APP_DEFAULT ? 1 : 0);
         };
         std::stable_sort(v.begin(), v.end(), [&](uint32_t x, uint32_t y) { return key(x) < key(y); });
+        for (uint32_t i : v) {
+            const sg_local_flow_rule& r = rules[i];
+            if (r.strategy == SG_STRATEGY_RELATE && r.ref_resource >= 0 && (uint32_t)r.ref_resource < K &&
+                (uint32_t)r.ref_resource != k)
+                relate.emplace_back(k, (uint32_t)r.ref_resource);
+            if (r.cluster_mode != SG_CLUSTER_MODE_OFF) cluster_refs.emplace_back(k, r.cluster_key);
+        }
         LRule& L = tab[k];
         L.fr_begin = L.fr_n = 0;
         L.cx = 0;
         L.ps = 0;
-        L.grp = gsize[gkey[k]] > 1 ? 1 : 0;
+        L.grp = 0;
         L.flow_grade = -1;
         L.flow_count = 0;
-        // (with context tracking every event also updates its context's DefaultNode: the cx walker)
-        const bool fast = v.size() == 1 && !L.grp && !track_ctx &&
-                          rules[v[0]].limit_app == SG_LIMIT_APP_DEFAULT && rules[v[0]].strategy == SG_STRATEGY_DIRECT &&
-                          rules[v[0]].cluster_mode == SG_CLUSTER_MODE_OFF &&
+        // (with context tracking every event also updates its context's DefaultNode: the cx walker; a fast resource
+        // that lands in a key group is walked there too, its one rule read from flow_grade / flow_count)
+        const bool fast = v.size() == 1 && !track_ctx && rules[v[0]].limit_app == SG_LIMIT_APP_DEFAULT &&
+                          rules[v[0]].strategy == SG_STRATEGY_DIRECT && rules[v[0]].cluster_mode == SG_CLUSTER_MODE_OFF &&
                           make_flow_rule(rules[v[0]], cold).behavior == SG_CONTROL_DEFAULT;
         if (fast) {  // the fast walkers' one DefaultController rule on the ClusterNode
             L.flow_grade = rules[v[0]].grade;
@@ -3327,9 +3409,8 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
             slot[v[0]] = -2;
             continue;
         }
-        if (v.empty() && !L.grp && !track_ctx) continue;
-        L.cx = 1;
-        has_cx = true;
+        if (v.empty() && !track_ctx) continue;
+        base_cx[k] = 1;
         L.fr_begin = (uint32_t)fr.size();
         L.fr_n = (uint32_t)v.size();
         for (uint32_t i : v) {
@@ -3342,25 +3423,17 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     HIP_TRY(h, hipDeviceSynchronize());
     LFlowRule* d_fr = nullptr;
     LCtl* d_ctl = nullptr;
-    uint32_t* d_gkey = nullptr;
     auto release = [&]() {
         dfree(d_fr);
         dfree(d_ctl);
-        dfree(d_gkey);
     };
     if (!fr.empty() && (hipMalloc(&d_fr, sizeof(LFlowRule) * fr.size()) != hipSuccess ||
                         hipMalloc(&d_ctl, sizeof(LCtl) * fr.size()) != hipSuccess)) {
         release();
         return fail(h, SG_E_NOMEM, "local flow rule allocation");
     }
-    if (groups && hipMalloc(&d_gkey, sizeof(uint32_t) * K) != hipSuccess) {
-        release();
-        return fail(h, SG_E_NOMEM, "key groups");
-    }
     hipError_t e = hipSuccess;
-    if (K) e = hipMemcpy(h->d_lrules, tab.data(), sizeof(LRule) * K, hipMemcpyHostToDevice);
-    if (e == hipSuccess && groups) e = hipMemcpy(d_gkey, gkey.data(), sizeof(uint32_t) * K, hipMemcpyHostToDevice);
-    if (e == hipSuccess && !fr.empty()) {
+    if (!fr.empty()) {
         e = hipMemcpy(d_fr, fr.data(), sizeof(LFlowRule) * fr.size(), hipMemcpyHostToDevice);
         std::vector<LCtl> c(fr.size(), LCtl{0, 0, -1, 0});  // storedTokens 0, lastFilledTime 0, latestPassedTime -1
         if (e == hipSuccess) e = hipMemcpy(d_ctl, c.data(), sizeof(LCtl) * c.size(), hipMemcpyHostToDevice);
@@ -3372,17 +3445,18 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     }
     dfree(h->d_lfrules);
     dfree(h->d_lctl);
-    dfree(h->d_lgkey);
     h->d_lfrules = d_fr;
     h->d_lctl = d_ctl;
-    h->d_lgkey = d_gkey;
     h->ltab = tab;
+    h->l_base_cx = base_cx;
+    h->l_relate = relate;
+    h->l_cluster_refs = cluster_refs;
     h->l_n_origins = n_origins;
     h->l_n_contexts = n_contexts;
-    h->l_has_cx = has_cx;
     h->l_cluster_rules = cluster_rules;
     h->l_rule_slot = slot;
-    h->l_ps_applied = 0;  // param flags are re-applied to the new rule image by the next batch
+    const int rc = local_apply_groups(h);
+    if (rc) return rc;
     int kept = 0;
     for (int64_t x : slot) kept += x != -1;
     return kept;

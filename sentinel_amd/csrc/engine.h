@@ -544,7 +544,9 @@ struct alignas(16) LFlowRule {
     int32_t warning_token, max_token, cold;
     int32_t strategy;         // SG_STRATEGY_*
     int32_t ref;              // RELATE: resource index; CHAIN: context id; < 0: refResource blank
-    int32_t cluster_mode;     // SG_CLUSTER_MODE_* (cluster-mode rules are checked last, NOT_STARTED semantics)
+    int32_t cluster_mode;     // SG_CLUSTER_MODE_* (cluster-mode rules are checked last)
+    uint32_t cluster_key;     // embedded token server: the flowId's rule index in the cluster flow state
+    int32_t pad_[3];
 };
 
 struct alignas(32) LCtl {     // the controller's state: storedTokens, lastFilledTime, latestPassedTime
@@ -603,6 +605,18 @@ struct LArgs {
     uint32_t* dyn;            // [K] epoch of the last batch with an origin event of the resource (walked as cx)
     uint32_t epoch;
     int32_t track_ctx;        // 1: every event updates its context's DefaultNode (n_contexts >= 1)
+    // the embedded token server (ClusterStateManager SERVER, emb = 1): the handle's cluster flow state
+    int32_t emb;
+    const Rule* c3_rules;
+    Bucket* c3_ring;
+    Occ* c3_occ;
+    int c3_stride;
+    uint32_t c3_K;
+    double max_occ_ratio;
+    const uint8_t* c3_rule_lim;   // limiter slot of each cluster rule's namespace (0xFF none)
+    LimRing* lim_ring;
+    double lim_qps[kMaxLim];
+    int64_t* c3_last_ts;          // the cluster flow batches' last timestamp (time order across both paths)
     int64_t* last_fetch;      // [K] StatisticNode.lastFetchTime (metric rows already reported)
     const uint8_t* inbound;   // [K] 1: the resource's entries are EntryType.IN (Constants.ENTRY_NODE), or null
     LBucket* entry_acc;       // [60] the ENTRY_NODE's minute buckets summed from the inbound resources' (metric rows)

@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         const sg_local_event e = a.ev[i];
         const int64_t t = e.ts_ms;
         if (i == 0) {
-            if (t < 0 || t < *a.last_ts) atomicOr(a.err, kErrTime);
+            if (t < 0 || t < *a.last_ts || (a.c3_last_ts && t < *a.c3_last_ts)) atomicOr(a.err, kErrTime);
             for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
         } else {
             const int64_t tp = a.ev[i - 1].ts_ms;
@@ -1117,6 +1117,114 @@ __device__ bool pace_step(const LFlowRule& r, LCtl& c, int64_t now, int64_t cost
     return true;
 }
 
+// ---- the embedded token server (ClusterStateManager SERVER) ----
+
+// RequestLimiter.tryPass (RequestLimiter.java:72-87) over the namespace's UnaryLeapArray(10, 1000) at time t.
+__device__ bool emb_lim_try_pass(LimRing* r, int64_t t, double qps) {
+    const int64_t P = t / kLimWindowMs;
+    const int I = (int)(P % kLimSamples);
+    const int64_t ws = P * kLimWindowMs;
+    if (r->start[I] != ws) {  // currentWindow: create or reset (time-ordered: never an older window)
+        r->start[I] = ws;
+        r->count[I] = 0;
+    }
+    const int64_t lo = ws - (int64_t)(kLimSamples - 1) * kLimWindowMs;
+    int64_t sum = 0;
+    for (int j = 0; j < kLimSamples; ++j)
+        if (r->start[j] != INT64_MIN && r->start[j] >= lo) sum += r->count[j];
+    if (!((double)sum + 1 <= qps)) return false;  // getQps() + 1 <= qpsAllowed (intervalInSecond 1.0)
+    r->count[I] += 1;
+    return true;
+}
+
+__device__ __forceinline__ double c3_qps(int64_t sum, double isec) { return isec == 1.0 ? (double)sum : (double)sum / isec; }
+
+// DefaultTokenService.requestToken (DefaultTokenService.java:39-50) → ClusterFlowChecker.acquireClusterToken
+// (ClusterFlowChecker.java:55-112) for one request at time t, on the flowId's ClusterMetric ring in HBM
+// (ClusterMetric / ClusterMetricLeapArray: currentWindow with the occupy transfer on reset, :49-71; tryOccupyNext,
+// ClusterMetric.java:79-98). The same arithmetic as the cluster walkers (engine.hip), one request at a time.
+__device__ int32_t embedded_token(const LArgs& a, uint32_t key, int64_t t, int32_t acq, bool prio, int32_t* wait) {
+    *wait = 0;
+    key &= SG_KEY_INDEX;
+    if (key == SG_KEY_BAD || acq <= 0) return SG_STATUS_BAD_REQUEST;
+    if (key >= a.c3_K) return SG_STATUS_NO_RULE_EXISTS;
+    const uint8_t ls = a.c3_rule_lim ? a.c3_rule_lim[key] : (uint8_t)0xFF;
+    if (ls != 0xFF && !emb_lim_try_pass(a.lim_ring + ls, t, a.lim_qps[ls])) return SG_STATUS_TOO_MANY_REQUEST;
+    const Rule R = a.c3_rules[key];
+    Bucket* ring = a.c3_ring + (size_t)key * a.c3_stride;
+    const Occ o = a.c3_occ[key];
+    int64_t occ_pass = o.pass, occ_req = o.pass_req;
+    // currentWindow(t) on slot I, then values(t) of the other slots
+    const int64_t P = t / R.wl;
+    const int S = R.S;
+    const int I = (int)(P % S);
+    const int64_t ws = P * R.wl;
+    const int64_t lo = ws - (int64_t)(S - 1) * R.wl;
+    const int h = (int)((P + 1) % S);
+    int64_t wo_pass = 0, wo_wait = 0, head_other = 0;
+    for (int q = 0; q < S; ++q) {
+        const int64_t st = ring[q].start;
+        const bool v = q != I && st != INT64_MIN && st >= lo;
+        wo_pass += v ? ring[q].c[SG_EV_PASS] : 0;
+        wo_wait += v ? ring[q].c[SG_EV_WAITING] : 0;
+        if (q == h && v) head_other = ring[q].c[SG_EV_PASS];
+    }
+    int64_t cur[SG_NUM_EVENTS];
+    const int64_t stI = ring[I].start;
+    if (stI == ws) {
+        for (int e = 0; e < SG_NUM_EVENTS; ++e) cur[e] = ring[I].c[e];
+    } else {
+        for (int e = 0; e < SG_NUM_EVENTS; ++e) cur[e] = 0;
+        if (stI != INT64_MIN && occ_req > 0) {  // resetWindowTo transfers the occupied quota (not a creation)
+            cur[SG_EV_OCCUPIED_PASS] += occ_pass;
+            cur[SG_EV_PASS] += occ_pass;
+            cur[SG_EV_PASS_REQUEST] += occ_req;
+            occ_pass = occ_req = 0;
+        }
+    }
+    int32_t st = SG_STATUS_BLOCKED;
+    const double latest = c3_qps(wo_pass + cur[SG_EV_PASS], R.isec);
+    const double next_remaining = R.thr - latest - (double)acq;
+    if (next_remaining >= 0) {
+        cur[SG_EV_PASS] += acq;
+        cur[SG_EV_PASS_REQUEST] += 1;
+        if (prio) cur[SG_EV_OCCUPIED_PASS] += acq;
+        st = SG_STATUS_OK;
+    } else {
+        bool waited = false;
+        if (prio) {
+            const double occupy_avg = c3_qps(wo_wait + cur[SG_EV_WAITING], R.isec);
+            if (occupy_avg <= a.max_occ_ratio * R.thr) {
+                const int64_t head = (S == 1) ? cur[SG_EV_PASS] : head_other;
+                if (latest + (double)(acq + occ_pass) - (double)head <= R.thr) {
+                    occ_pass += acq;  // addOccupyPass
+                    occ_req += 1;
+                    cur[SG_EV_WAITING] += acq;
+                    if (R.wait_ms > 0) {
+                        *wait = R.wait_ms;
+                        st = SG_STATUS_SHOULD_WAIT;
+                        waited = true;
+                    }
+                }
+            }
+        }
+        if (!waited) {
+            cur[SG_EV_BLOCK] += acq;
+            cur[SG_EV_BLOCK_REQUEST] += 1;
+            if (prio) cur[SG_EV_OCCUPIED_BLOCK] += acq;
+        }
+    }
+    ring[I].start = ws;
+    for (int e = 0; e < SG_NUM_EVENTS; ++e) ring[I].c[e] = cur[e];
+    if (occ_pass != o.pass || occ_req != o.pass_req) {
+        Occ no;
+        no.pass = occ_pass;
+        no.pass_req = occ_req;
+        a.c3_occ[key] = no;
+    }
+    return st;
+}
+
 // FlowRuleChecker.selectNodeByRequesterAndStrategy (:115-145) with selectReferenceNode (:96-112): 0 the ClusterNode,
 // 1 the origin node, 2 the resource's DefaultNode of the current context (CHAIN), 3 the ClusterNode of r.ref
 // (RELATE; ref_exists() says whether ClusterBuilderSlot created it), -1 none (the rule passes)
@@ -1231,6 +1339,21 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
             r.strategy = SG_STRATEGY_DIRECT;
             r.ref = -1;
             r.cluster_mode = SG_CLUSTER_MODE_OFF;
+        }
+        if (r.cluster_mode != SG_CLUSTER_MODE_OFF && a.emb) {
+            // passClusterCheck on the embedded server (FlowRuleChecker.java:147-164), applyTokenResult (:186-209)
+            int32_t tw = 0;
+            const int32_t ts = embedded_token(a, r.cluster_key, t, e.count, e.prio, &tw);
+            if (ts == SG_STATUS_OK) continue;
+            if (ts == SG_STATUS_SHOULD_WAIT) {  // Thread.sleep(waitInMs), then the rule passes
+                wait += tw;
+                continue;
+            }
+            if (ts == SG_STATUS_BLOCKED) {
+                status = SG_LOCAL_BLOCK_FLOW;
+                break;
+            }
+            // NO_RULE_EXISTS / BAD_REQUEST / FAIL / TOO_MANY_REQUEST: fallbackToLocalOrPass
         }
         if (r.cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) continue;  // cluster rule not activated: passes
         const int sel = cx_select(a, R, r, origin, ctx, [&]() {
@@ -1475,7 +1598,10 @@ __global__ void __launch_bounds__(256) k_lskip_apply(LArgs a) {
 }
 
 __global__ void k_local_finish(LArgs a) {
-    if (*a.err == 0 && a.n > 0) *a.last_ts = a.ev[a.n - 1].ts_ms;
+    if (*a.err == 0 && a.n > 0) {
+        *a.last_ts = a.ev[a.n - 1].ts_ms;
+        if (a.c3_last_ts) *a.c3_last_ts = a.ev[a.n - 1].ts_ms;  // the embedded server's token requests came up to here
+    }
 }
 
 // ------------------------------------------------------------------------------- metric rows

@@ -342,3 +342,80 @@ def test_nodes_created_on_first_entry_whatever_the_rules(t0):
     with pytest.raises(ValueError, match=str(abi.SG_E_UNSUPPORTED)):
         ch2.load_flow_rules(np.array([local_flow_rule(0, 100.0)]), n_contexts=1)
     assert ch2.load_flow_rules(np.array([local_flow_rule(0, 100.0, limit_app=1)]), n_origins=1) == 1
+
+
+def _server(count, ns_qps=None, S=2, prio_ratio=1.0):
+    from oracle.binding import ClusterTokenService
+    cts = ClusterTokenService(1.0, prio_ratio)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    if ns_qps is not None:
+        ns["limiter_enabled"], ns["max_allowed_qps"] = 1, ns_qps
+    cts.set_namespaces(ns)
+    r = np.zeros(1, abi.RULE_DTYPE)
+    r["flow_id"], r["count"], r["threshold_type"] = 77, count, abi.THRESHOLD_GLOBAL
+    r["sample_count"], r["window_interval_ms"], r["namespace_id"] = S, 1000, 0
+    cts.load_rules(r)
+    return cts
+
+
+def _entries(t0, offsets, prio=()):
+    ev = np.zeros(len(offsets), abi.LOCAL_EVENT_DTYPE)
+    ev["ts_ms"], ev["count"], ev["kind"] = [t0 + o for o in offsets], 1, abi.LOCAL_ENTRY
+    for i in prio:
+        ev["resource"][i] |= abi.KEY_PRIO
+    return ev
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_embedded_server_token_results(t0):
+    """FlowRuleChecker.passClusterCheck on an embedded token server (FlowRuleChecker.java:147-209, pickClusterService →
+    EmbeddedClusterTokenServerProvider, DefaultEmbeddedTokenServer.requestToken → DefaultTokenService.requestToken): a
+    cluster rule with a global threshold of 2 per second admits the first two entries of a second (OK), blocks the
+    third (BLOCKED → FlowException, the local count of 100 is never consulted), and the server's ClusterMetric holds
+    the passes and the block; a prioritized entry that can occupy the next bucket passes after SHOULD_WAIT's 500 ms
+    (1000 / sampleCount, ClusterMetric.java:86)."""
+    t0 = t0 - t0 % 1000 + 100
+    cts = _server(2.0)
+    ch = LocalChain(2, 1000, 500)
+    ch.load_rules(np.array([local_rule()]))
+    rule = local_flow_rule(0, 100.0, cluster_mode=abi.CLUSTER_MODE_FALLBACK, cluster_config=1, cluster_key=0)
+    assert ch.load_flow_rules(np.array([rule])) == 1
+    ch.attach_cluster(cts, abi.CLUSTER_SERVER)
+    out = ch.decide(_entries(t0, [0, 1, 2]))
+    assert out["status"].tolist() == [abi.LOCAL_PASS, abi.LOCAL_PASS, abi.LOCAL_BLOCK_FLOW]
+    starts, c, occ = cts.read_state(0)
+    assert c[:, abi.EV_PASS].sum() == 2 and c[:, abi.EV_BLOCK].sum() == 1
+    # t0 + 600: the bucket of t0 + 100 is the window's head (PASS 2); occupying the next bucket fits
+    out = ch.decide(_entries(t0, [600], prio=[0]))
+    assert (out["status"][0], out["wait_ms"][0]) == (abi.LOCAL_PASS, 500)
+    assert cts.read_state(0)[2].tolist() == [1, 1]          # occupied PASS, PASS_REQUEST
+
+
+@pytest.mark.parametrize("t0", T0S)
+def test_embedded_server_fallbacks(t0):
+    """applyTokenResult (:186-209): NO_RULE_EXISTS (the flowId has no cluster rule on the server), BAD_REQUEST
+    (acquireCount 0) and TOO_MANY_REQUEST (the namespace's GlobalRequestLimiter) fall back to the local check when
+    fallbackToLocalWhenFail, else the rule passes; NOT_STARTED (no token service) always falls back."""
+    t0 = t0 - t0 % 1000 + 100
+    ch = LocalChain(2, 1000, 500)
+    ch.load_rules(np.array([local_rule(), local_rule(), local_rule()]))
+    rules = [local_flow_rule(0, 1.0, cluster_mode=abi.CLUSTER_MODE_FALLBACK, cluster_config=1),          # no rule
+             local_flow_rule(1, 1.0, cluster_mode=abi.CLUSTER_MODE_NO_FALLBACK, cluster_config=2),       # no rule
+             local_flow_rule(2, 1.0, cluster_mode=abi.CLUSTER_MODE_FALLBACK, cluster_config=3, cluster_key=0)]
+    assert ch.load_flow_rules(np.array(rules)) == 3
+    cts = _server(10.0, ns_qps=1.0)           # the namespace admits one token request per second
+    ch.attach_cluster(cts, abi.CLUSTER_SERVER)
+    ev = _entries(t0, [0, 1, 2, 3, 4, 5, 6])
+    ev["resource"] = [0, 0, 1, 1, 2, 2, 2]
+    out = ch.decide(ev)
+    # resource 0: local count 1 → pass, block; resource 1: not activated; resource 2: the token passes, then
+    # TOO_MANY_REQUEST twice → the local check (count 1, one pass in the window) blocks
+    assert out["status"].tolist() == [abi.LOCAL_PASS, abi.LOCAL_BLOCK_FLOW, abi.LOCAL_PASS, abi.LOCAL_PASS,
+                                      abi.LOCAL_PASS, abi.LOCAL_BLOCK_FLOW, abi.LOCAL_BLOCK_FLOW]
+    ch.attach_cluster(None, abi.CLUSTER_NOT_STARTED)
+    ev2 = _entries(t0 + 2000, [0, 1])
+    ev2["resource"] = 2
+    assert ch.decide(ev2)["status"].tolist() == [abi.LOCAL_PASS, abi.LOCAL_BLOCK_FLOW]
+    with pytest.raises(ValueError):
+        ch.attach_cluster(cts, abi.CLUSTER_CLIENT)

@@ -356,15 +356,17 @@ def test_origins_declared_later_and_context_tracking_contract():
 
 
 def test_cluster_state_contract():
-    """Cluster-mode rules are decided only on a node that is neither token client nor server."""
+    """Cluster-mode rules are decided on a node that is neither token client nor server, or on an embedded token
+    server (tests/test_embedded_server_gpu.py); a token client's tokens come over the network: unsupported."""
     from sentinel_amd.engine import EngineError
     eng = _engine()
     eng.local_load_rules(np.array([local_rule()]), 2, 1000, 500)
     cr = np.array([local_flow_rule(0, 5.0, cluster_mode=abi.CLUSTER_MODE_FALLBACK, cluster_config=1)])
     assert eng.local_load_flow_rules(cr) == 1
     with pytest.raises(EngineError) as ei:
-        eng.local_set_cluster_state(abi.CLUSTER_SERVER)
+        eng.local_set_cluster_state(abi.CLUSTER_CLIENT)
     assert ei.value.code == abi.SG_E_UNSUPPORTED
+    eng.local_set_cluster_state(abi.CLUSTER_SERVER)
     eng.local_load_flow_rules(np.array([local_flow_rule(0, 5.0)]))
     eng.local_set_cluster_state(abi.CLUSTER_CLIENT)
     with pytest.raises(EngineError) as ei:
