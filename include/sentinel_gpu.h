@@ -699,6 +699,34 @@ int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64
                                int64_t* minute, int64_t* head);
 int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);
 
+/* ---- the node handle: one token server over G shard handles (SURVEY §8(b) "multi-GPU fan-out is internal to the
+ * handle", §8(e) flowIds hashed over the GPUs) ----
+ * The reference serves every flowId from one TokenService (DefaultTokenService.requestToken, DefaultTokenService
+ * .java:39-50) for all Netty workers (NettyTransportServer.java:53-54). A node handle owns G shard handles (shard g on
+ * devices[g]; one device may hold several shards) and a front handle on devices[0]. A node batch in caller order is
+ * validated and passed through the namespace limiters by the front (GlobalRequestLimiter over the whole batch in
+ * caller order: the node's arrival order), split by owner — splitmix64(flowId) mod G — with a stable device multisplit,
+ * decided by every shard concurrently on its own stream (slices copied peer to peer for shards on other devices),
+ * and gathered back into caller order: the results equal one handle deciding the batch.
+ *   sg_node_create          ← G shards (1..64) on devices[0..G-1], each with cfg (max_batch per shard and node)
+ *   sg_node_set_namespaces  ← sg_set_namespaces (the front keeps the limiters)
+ *   sg_node_load_flow_rules ← sg_load_flow_rules for the node's rule set (keys = rule indices of this array);
+ *                             a surviving flowId keeps its owner, hence its ClusterMetric
+ *   sg_node_flow_decide_batch(_host) ← sg_flow_decide_batch over the node (device buffers on devices[0] / host)
+ *   sg_node_flow_read_state, sg_node_snapshot_metrics ← per node rule, as the single-handle calls
+ *   sg_node_shard_of        owner shard and local rule index of node rule `key` */
+typedef struct sg_node sg_node;
+int         sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shards, sg_node** out);
+void        sg_node_destroy(sg_node* nd);
+const char* sg_node_last_error(const sg_node* nd);
+int         sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n);
+int         sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n);
+int         sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out, void* stream);
+int         sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out);
+int         sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
+int         sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap);
+int         sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key);
+
 /* ---------- token-server wire codec ----------
  * The default token server frames every message with a 2-byte big-endian length
  * (LengthFieldBasedFrameDecoder(1024, 0, 2, 0, 2) / LengthFieldPrepender(2),

@@ -301,6 +301,7 @@ struct sg_handle {
         hipEvent_t done = nullptr;
     };
     DevTicket dev[kDevSlots];
+    bool front_only = false;          // a node handle's front (validation + namespace limiter): no flow state
 };
 
 namespace {
@@ -888,7 +889,9 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     Occ* d_occ = nullptr;
     uint32_t* d_seg_end = nullptr;
     int32_t* d_src = nullptr;
-    if (n) {
+    if (n && h->front_only) {  // a node's front: rule thresholds and limiter slots only
+        if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess) return fail(h, SG_E_NOMEM, "rule table");
+    } else if (n) {
         if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * 2 * n) != hipSuccess ||
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
@@ -1186,12 +1189,8 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
 // Front half of a batch on `stream`: validation and packed records (k_prep), the namespace limiter pre-pass,
 // the stable sort by flowId and the segment lists. Touches only the workspace, the caller's output (default
 // results) and the limiter state.
-int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, bool stats) {
-    if (stats) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
-    HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(a.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
-    HIP_TRY(h, hipMemsetAsync(a.skip_count, 0, sizeof(uint32_t), stream));
-    HIP_TRY(h, launch_prep(a, stream));
+// The namespace limiter pre-pass over a batch's records (after k_prep): TOO_MANY_REQUEST results, sentinel records.
+int flow_limiter(sg_handle* h, BatchArgs& a, hipStream_t stream) {
     if (h->n_lim > 0) {
         LimArgs L{};
         L.n_lim = h->n_lim;
@@ -1217,6 +1216,17 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
         }
         HIP_TRY(h, launch_limiter(a, L, stream));
     }
+    return SG_OK;
+}
+
+int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, bool stats) {
+    if (stats) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
+    HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(a.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(a.skip_count, 0, sizeof(uint32_t), stream));
+    HIP_TRY(h, launch_prep(a, stream));
+    const int lrc = flow_limiter(h, a, stream);
+    if (lrc) return lrc;
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
@@ -3865,6 +3875,347 @@ int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {
     if (bytes > cap) return SG_E_INVAL;
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------------ node handle
+//
+// One token server over G shard handles (include/sentinel_gpu.h, sg_node_*): the reference's single TokenService
+// (DefaultTokenService.java:39-50) serving every flowId, with the flowIds hashed over the shards (SURVEY §8(b)
+// "multi-GPU fan-out is internal to the handle", §8(e)). A batch in caller order goes to the front handle (on the
+// first shard's device: validation and the namespace limiter over the whole batch in caller order — the node's
+// exact arrival order), then is split by owner (node.hip), decided by every shard concurrently on its own stream
+// (peer copies for shards on other devices), and gathered back into caller order.
+
+struct sg_node {
+    std::string err;
+    sg_config cfg{};
+    std::vector<int32_t> devices;       // device of each shard
+    sg_handle* front = nullptr;         // devices[0]: validation + namespace limiter over the node batch
+    std::vector<sg_handle*> shards;
+    std::vector<hipStream_t> streams;   // one per shard, on its device
+    std::vector<hipEvent_t> done;       // per shard: its slice decided (and copied back)
+    std::vector<int*> h_err;            // pinned, per shard
+    hipStream_t s0 = nullptr;           // devices[0]
+    hipEvent_t routed = nullptr;
+    std::vector<sg_flow_rule> rules;
+    std::vector<uint8_t> shard_of;
+    std::vector<uint32_t> local_of;
+    uint8_t* d_shard_of = nullptr;
+    uint32_t* d_local_of = nullptr;
+    uint32_t* d_tile_cnt = nullptr;
+    uint32_t* d_base = nullptr;         // [kMaxShards + 1] bases, then [kMaxShards] totals
+    uint32_t* h_base = nullptr;         // pinned copy
+    int* h_front_err = nullptr;         // pinned
+    sg_req* d_sub_req = nullptr;
+    uint32_t* d_sub_pos = nullptr;
+    sg_result* d_sub_out = nullptr;
+    std::vector<sg_req*> r_req;         // per shard on another device: its slice there
+    std::vector<sg_result*> r_out;
+    sg_req* d_req_h = nullptr;          // host path
+    sg_result* d_out_h = nullptr;
+};
+
+namespace {
+
+int nfail(sg_node* nd, int code, const std::string& msg) {
+    if (nd) nd->err = msg;
+    return code;
+}
+
+#define NHIP(nd, expr)                                                                          \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return nfail((nd), SG_E_DEVICE, std::string(#expr ": ") + hipGetErrorString(_e));   \
+    } while (0)
+
+// splitmix64(flowId) mod G: the owner shard (sentinel_amd/cluster.py shard_of)
+uint32_t node_owner(int64_t flow_id, uint32_t G) {
+    uint64_t z = (uint64_t)flow_id + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (uint32_t)(z % G);
+}
+
+// A shard's error, in the node's words.
+int node_child(sg_node* nd, sg_handle* h, int rc) {
+    if (rc < 0) nd->err = h->err;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sg_node_destroy(sg_node* nd) {
+    if (!nd) return;
+    for (size_t g = 0; g < nd->shards.size(); ++g) {
+        (void)hipSetDevice(nd->devices[g]);
+        if (g < nd->streams.size() && nd->streams[g]) (void)hipStreamDestroy(nd->streams[g]);
+        if (g < nd->done.size() && nd->done[g]) (void)hipEventDestroy(nd->done[g]);
+        if (g < nd->h_err.size() && nd->h_err[g]) (void)hipHostFree(nd->h_err[g]);
+        if (g < nd->r_req.size()) dfree(nd->r_req[g]);
+        if (g < nd->r_out.size()) dfree(nd->r_out[g]);
+        sg_destroy(nd->shards[g]);
+    }
+    if (!nd->devices.empty()) (void)hipSetDevice(nd->devices[0]);
+    if (nd->s0) (void)hipStreamDestroy(nd->s0);
+    if (nd->routed) (void)hipEventDestroy(nd->routed);
+    dfree(nd->d_shard_of);
+    dfree(nd->d_local_of);
+    dfree(nd->d_tile_cnt);
+    dfree(nd->d_base);
+    dfree(nd->d_sub_req);
+    dfree(nd->d_sub_pos);
+    dfree(nd->d_sub_out);
+    dfree(nd->d_req_h);
+    dfree(nd->d_out_h);
+    if (nd->h_base) (void)hipHostFree(nd->h_base);
+    if (nd->h_front_err) (void)hipHostFree(nd->h_front_err);
+    sg_destroy(nd->front);
+    delete nd;
+}
+
+const char* sg_node_last_error(const sg_node* nd) { return nd ? nd->err.c_str() : "null node"; }
+
+int sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shards, sg_node** out) {
+    if (!cfg || !devices || !out || n_shards == 0 || n_shards > (uint32_t)kMaxShards) return SG_E_INVAL;
+    *out = nullptr;
+    sg_node* nd = new sg_node();
+    nd->cfg = *cfg;
+    nd->devices.assign(devices, devices + n_shards);
+    auto bail = [&](int rc) {
+        sg_node_destroy(nd);
+        return rc;
+    };
+    sg_config c = *cfg;
+    c.device = devices[0];
+    int rc = sg_create(&c, &nd->front);
+    if (rc) return bail(rc);
+    nd->front->front_only = true;
+    for (uint32_t g = 0; g < n_shards; ++g) {
+        c.device = devices[g];
+        sg_handle* h = nullptr;
+        rc = sg_create(&c, &h);
+        if (rc) return bail(rc);
+        nd->shards.push_back(h);
+        if (hipSetDevice(devices[g]) != hipSuccess) return bail(SG_E_DEVICE);
+        hipStream_t st = nullptr;
+        hipEvent_t ev = nullptr;
+        int* he = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(&he, sizeof(int)) != hipSuccess)
+            return bail(SG_E_DEVICE);
+        nd->streams.push_back(st);
+        nd->done.push_back(ev);
+        nd->h_err.push_back(he);
+        sg_req* rq = nullptr;
+        sg_result* ro = nullptr;
+        if (devices[g] != devices[0] &&
+            (hipMalloc(&rq, sizeof(sg_req) * cfg->max_batch) != hipSuccess ||
+             hipMalloc(&ro, sizeof(sg_result) * cfg->max_batch) != hipSuccess))
+            return bail(SG_E_NOMEM);
+        nd->r_req.push_back(rq);
+        nd->r_out.push_back(ro);
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess) return bail(SG_E_DEVICE);
+    const uint64_t n = cfg->max_batch;
+    if (hipStreamCreateWithFlags(&nd->s0, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&nd->routed, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&nd->d_tile_cnt, sizeof(uint32_t) * kMaxShards * (route_tiles(n) + 1)) != hipSuccess ||
+        hipMalloc(&nd->d_base, sizeof(uint32_t) * (2 * kMaxShards + 1)) != hipSuccess ||
+        hipMalloc(&nd->d_sub_req, sizeof(sg_req) * n) != hipSuccess ||
+        hipMalloc(&nd->d_sub_pos, sizeof(uint32_t) * n) != hipSuccess ||
+        hipMalloc(&nd->d_sub_out, sizeof(sg_result) * n) != hipSuccess ||
+        hipHostMalloc(&nd->h_base, sizeof(uint32_t) * (2 * kMaxShards + 1)) != hipSuccess ||
+        hipHostMalloc(&nd->h_front_err, sizeof(int)) != hipSuccess)
+        return bail(SG_E_NOMEM);
+    *out = nd;
+    return SG_OK;
+}
+
+int sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n) {
+    if (!nd || (!ns && n)) return SG_E_INVAL;
+    // the front runs every namespace limiter over the node batch; the shards see only admitted requests
+    int rc = sg_set_namespaces(nd->front, ns, n);
+    if (rc) return node_child(nd, nd->front, rc);
+    std::vector<sg_namespace> off(ns, ns + n);
+    for (auto& x : off) x.limiter_enabled = 0;
+    for (sg_handle* h : nd->shards) {
+        rc = sg_set_namespaces(h, off.data(), n);
+        if (rc) return node_child(nd, h, rc);
+    }
+    return SG_OK;
+}
+
+int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) {
+    if (!nd || (!rules && n)) return SG_E_INVAL;
+    int rc = sg_load_flow_rules(nd->front, rules, n);  // validates the node's rule set
+    if (rc) return node_child(nd, nd->front, rc);
+    const uint32_t G = (uint32_t)nd->shards.size();
+    std::vector<std::vector<sg_flow_rule>> part(G);
+    std::vector<uint8_t> so(n);
+    std::vector<uint32_t> lo(n);
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t g = node_owner(rules[k].flow_id, G);
+        so[k] = (uint8_t)g;
+        lo[k] = (uint32_t)part[g].size();
+        part[g].push_back(rules[k]);
+    }
+    for (uint32_t g = 0; g < G; ++g) {  // a surviving flowId keeps its owner, hence its ClusterMetric
+        rc = sg_load_flow_rules(nd->shards[g], part[g].data(), (uint32_t)part[g].size());
+        if (rc) return node_child(nd, nd->shards[g], rc);
+    }
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    dfree(nd->d_shard_of);
+    dfree(nd->d_local_of);
+    if (n) {
+        if (hipMalloc(&nd->d_shard_of, n) != hipSuccess || hipMalloc(&nd->d_local_of, sizeof(uint32_t) * n) != hipSuccess)
+            return nfail(nd, SG_E_NOMEM, "routing tables");
+        NHIP(nd, hipMemcpy(nd->d_shard_of, so.data(), n, hipMemcpyHostToDevice));
+        NHIP(nd, hipMemcpy(nd->d_local_of, lo.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+    }
+    nd->rules.assign(rules, rules + n);
+    nd->shard_of = so;
+    nd->local_of = lo;
+    return SG_OK;
+}
+
+int sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key) {
+    if (!nd || !shard || !local_key || key >= nd->shard_of.size()) return SG_E_INVAL;
+    *shard = nd->shard_of[key];
+    *local_key = nd->local_of[key];
+    return SG_OK;
+}
+
+int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out, void* stream_) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    sg_handle* f = nd->front;
+    const uint32_t G = (uint32_t)nd->shards.size();
+    hipStream_t user = (hipStream_t)stream_;
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    for (sg_handle* h : nd->shards) drain_async(h);
+    int rc = ensure_layout(f);
+    if (rc) return node_child(nd, f, rc);
+    // 1. the front: validation + namespace limiter in caller order, the batch's time check, its last timestamp
+    NHIP(nd, hipStreamSynchronize(user));  // the caller's batch is in place
+    sg_handle::FlowWs w;
+    main_ws(f, w);
+    BatchArgs a = flow_args(f, w, req, n, out);
+    a.hist0 = nullptr;
+    NHIP(nd, hipMemsetAsync(a.err, 0, sizeof(int), nd->s0));
+    NHIP(nd, launch_prep(a, nd->s0));
+    rc = flow_limiter(f, a, nd->s0);
+    if (rc) return node_child(nd, f, rc);
+    NHIP(nd, launch_finish(a, nd->s0));
+    // 2. routing by owner
+    RouteArgs r{};
+    r.req = req;
+    r.rec = a.rec;
+    r.n = n;
+    r.kshift = a.kshift;
+    r.abits = a.abits;
+    r.imask = a.imask;
+    r.K = f->K;
+    r.shard_of = nd->d_shard_of;
+    r.local_of = nd->d_local_of;
+    r.G = (int)G;
+    r.tile_cnt = nd->d_tile_cnt;
+    r.shard_base = nd->d_base;
+    r.shard_tot = nd->d_base + kMaxShards + 1;
+    r.sub_req = nd->d_sub_req;
+    r.sub_pos = nd->d_sub_pos;
+    NHIP(nd, launch_route(r, nd->s0));
+    NHIP(nd, hipMemcpyAsync(nd->h_base, nd->d_base, sizeof(uint32_t) * (2 * kMaxShards + 1), hipMemcpyDeviceToHost,
+                            nd->s0));
+    NHIP(nd, hipMemcpyAsync(nd->h_front_err, a.err, sizeof(int), hipMemcpyDeviceToHost, nd->s0));
+    NHIP(nd, hipEventRecord(nd->routed, nd->s0));
+    NHIP(nd, hipStreamSynchronize(nd->s0));
+    if (*nd->h_front_err) return node_child(nd, f, flow_status(f, *nd->h_front_err));
+    // 3. every shard decides its slice on its own stream
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t base = nd->h_base[g], cnt = nd->h_base[kMaxShards + 1 + g];
+        *nd->h_err[g] = 0;
+        if (cnt == 0) continue;
+        sg_handle* h = nd->shards[g];
+        const int dev = nd->devices[g];
+        NHIP(nd, hipSetDevice(dev));
+        NHIP(nd, hipStreamWaitEvent(nd->streams[g], nd->routed, 0));
+        const sg_req* sreq = nd->d_sub_req + base;
+        sg_result* sout = nd->d_sub_out + base;
+        if (dev != nd->devices[0]) {
+            NHIP(nd, hipMemcpyPeerAsync(nd->r_req[g], dev, sreq, nd->devices[0], sizeof(sg_req) * cnt, nd->streams[g]));
+            sreq = nd->r_req[g];
+            sout = nd->r_out[g];
+        }
+        rc = enqueue_flow(h, sreq, cnt, sout, nd->streams[g], nd->h_err[g], false);
+        if (rc) return node_child(nd, h, rc);
+        if (dev != nd->devices[0])
+            NHIP(nd, hipMemcpyPeerAsync(nd->d_sub_out + base, nd->devices[0], sout, dev, sizeof(sg_result) * cnt,
+                                        nd->streams[g]));
+        NHIP(nd, hipEventRecord(nd->done[g], nd->streams[g]));
+    }
+    // 4. back into caller order
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    for (uint32_t g = 0; g < G; ++g)
+        if (nd->h_base[kMaxShards + 1 + g]) NHIP(nd, hipStreamWaitEvent(nd->s0, nd->done[g], 0));
+    NHIP(nd, launch_route_gather(nd->d_sub_out, nd->d_sub_pos, nd->h_base[G], out, nd->s0));
+    NHIP(nd, hipEventRecord(nd->routed, nd->s0));
+    NHIP(nd, hipStreamWaitEvent(user, nd->routed, 0));
+    NHIP(nd, hipStreamSynchronize(nd->s0));
+    for (uint32_t g = 0; g < G; ++g) {
+        const int e = *nd->h_err[g];
+        if (e) return node_child(nd, nd->shards[g], flow_status(nd->shards[g], e));
+    }
+    return SG_OK;
+}
+
+int sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    if (!nd->d_req_h && (hipMalloc(&nd->d_req_h, sizeof(sg_req) * nd->cfg.max_batch) != hipSuccess ||
+                         hipMalloc(&nd->d_out_h, sizeof(sg_result) * nd->cfg.max_batch) != hipSuccess))
+        return nfail(nd, SG_E_NOMEM, "host-path buffers");
+    NHIP(nd, hipMemcpy(nd->d_req_h, req, sizeof(sg_req) * n, hipMemcpyHostToDevice));
+    const int rc = sg_node_flow_decide_batch(nd, nd->d_req_h, n, nd->d_out_h, nullptr);
+    if (rc) return rc;
+    NHIP(nd, hipMemcpy(out, nd->d_out_h, sizeof(sg_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
+    if (!nd || key >= nd->shard_of.size()) return SG_E_INVAL;
+    sg_handle* h = nd->shards[nd->shard_of[key]];
+    return node_child(nd, h, sg_flow_read_state(h, nd->local_of[key], starts, counters, occupy));
+}
+
+int sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap) {
+    if (!nd || (!out && cap)) return SG_E_INVAL;
+    const uint64_t K = nd->shard_of.size();
+    if (cap < 2 * K) return nfail(nd, SG_E_CAPACITY, "snapshot buffer smaller than 2 * rules");
+    std::vector<std::vector<double>> part(nd->shards.size());
+    for (size_t g = 0; g < nd->shards.size(); ++g) {
+        sg_handle* h = nd->shards[g];
+        part[g].assign(2 * (size_t)h->K + 2, 0.0);
+        const int rc = sg_snapshot_metrics(h, now_ms, part[g].data(), part[g].size());
+        if (rc) return node_child(nd, h, rc);
+    }
+    for (uint64_t k = 0; k < K; ++k) {
+        const std::vector<double>& p = part[nd->shard_of[k]];
+        out[2 * k] = p[2 * (size_t)nd->local_of[k]];
+        out[2 * k + 1] = p[2 * (size_t)nd->local_of[k] + 1];
+    }
     return SG_OK;
 }
 

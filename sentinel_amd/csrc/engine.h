@@ -652,6 +652,30 @@ hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out
 
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
+
+// ---- node handle routing (node.hip) ----
+constexpr int kMaxShards = 64;
+constexpr uint32_t kRouteNone = 127;  // shard id of a request that is not routed (answered by the front)
+struct RouteArgs {
+    const sg_req* req;         // the node batch (caller order)
+    const uint64_t* rec;       // the front's packed records (request order; rejected ones carry the sentinel key)
+    uint64_t n;
+    int kshift, abits;
+    uint64_t imask;
+    uint32_t K;                // node rules
+    const uint8_t* shard_of;   // [K] owner shard of each node rule
+    const uint32_t* local_of;  // [K] its rule index on that shard
+    int G;
+    uint32_t* tile_cnt;        // [tiles][kMaxShards]
+    uint32_t* shard_base;      // [G + 1] first sub-batch position of each shard
+    uint32_t* shard_tot;       // [G] requests routed to each shard
+    sg_req* sub_req;           // [n] the shard slices, one after the other
+    uint32_t* sub_pos;         // [n] node position of each sub-request
+};
+hipError_t launch_route(const RouteArgs& r, hipStream_t stream);
+hipError_t launch_route_gather(const sg_result* sub_out, const uint32_t* sub_pos, uint64_t total, sg_result* out,
+                               hipStream_t stream);
+uint64_t route_tiles(uint64_t n);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 int radix_digit_bits(int bits);  // digit width radix_sort_records uses for `bits` key bits (8 or 10)

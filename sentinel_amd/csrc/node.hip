@@ -1,0 +1,167 @@
+// node.hip — the node handle's request routing (include/sentinel_gpu.h, sg_node_*): one token server's batch split
+// over G shard handles by flowId owner, and the shards' results put back in the caller's order.
+//
+// The reference serves every flowId from one TokenService (DefaultTokenService.requestToken, DefaultTokenService.java
+// :39-50, called by all Netty workers, NettyTransportServer.java:53-54). Here the flowIds are hashed over G shards
+// (splitmix64(flowId) mod G); the node's front handle has already validated the batch and run the
+// namespace limiter over it in caller order (k_prep + the limiter pre-pass), so each request of its packed records
+// that survived carries its node rule index. Routing is a stable multisplit of those records by shard:
+//   k_route_count    per 4096-record tile: requests per shard (LDS counters)
+//   k_route_scan     one block: per shard, the exclusive scan of the tile counts; shard slices laid out one after
+//                    the other (shard g at base[g]) in one sub-batch buffer, the per-shard totals for the host
+//   k_route_scatter  per tile: each wave ranks its 64-record rounds by shard (match ballots, as the radix scatter)
+//                    and writes the sub-request {ts, local rule index | prio, acquire} and the node position of
+//                    every routed request — time order within a shard is kept (stable), so each slice is a valid
+//                    batch for its shard
+//   k_route_gather   out[pos[j]] = sub_out[j]: the shards' results in caller order
+// HBM-bound byte work: 16 B read + 16 B + 4 B written per request (scatter), 12 B + 4 B read and 12 B written
+// (gather); no MFMA.
+#include "engine.h"
+
+namespace sg {
+
+namespace {
+
+constexpr int kRouteThreads = 256;
+constexpr int kRouteRounds = 16;
+constexpr uint32_t kRouteTile = kRouteThreads * kRouteRounds;
+constexpr int kRouteWaveRecs = kRouteTile / (kRouteThreads / 64);
+
+__device__ __forceinline__ int route_lane() { return (int)__lane_id(); }
+
+// Lanes of the wave whose 6-bit shard equals this lane's (shard 64: not routed).
+__device__ __forceinline__ uint64_t match_shard(uint32_t s) {
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t m = __ballot((s >> b) & 1u);
+        peers &= ((s >> b) & 1u) ? m : ~m;
+    }
+    return peers;
+}
+
+__device__ __forceinline__ uint32_t shard_of_rec(const RouteArgs& r, uint64_t rec) {
+    const uint32_t k = (uint32_t)(rec >> r.kshift);
+    return k < r.K ? (uint32_t)r.shard_of[k] : (uint32_t)kRouteNone;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kRouteThreads) k_route_count(RouteArgs r) {
+    __shared__ uint32_t cnt[kMaxShards];
+    const int tid = threadIdx.x;
+    if (tid < kMaxShards) cnt[tid] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+#pragma unroll 4
+    for (int it = 0; it < kRouteRounds; ++it) {
+        const uint64_t i = base + (uint64_t)it * kRouteThreads + tid;
+        if (i >= r.n) break;
+        const uint32_t s = shard_of_rec(r, r.rec[i]);
+        if (s < (uint32_t)r.G) atomicAdd(&cnt[s], 1u);
+    }
+    __syncthreads();
+    if (tid < r.G) r.tile_cnt[(size_t)blockIdx.x * kMaxShards + tid] = cnt[tid];
+}
+
+// One block of kMaxShards waves' worth of threads: thread g scans shard g's column serially over the tiles (tiles
+// = n / 4096, a few thousand at most: a few µs), then the shard bases.
+__global__ void __launch_bounds__(kMaxShards) k_route_scan(RouteArgs r, uint32_t ntiles) {
+    __shared__ uint32_t tot[kMaxShards];
+    const int g = threadIdx.x;
+    uint32_t run = 0;
+    if (g < r.G) {
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            const uint32_t c = r.tile_cnt[(size_t)t * kMaxShards + g];
+            r.tile_cnt[(size_t)t * kMaxShards + g] = run;
+            run += c;
+        }
+    }
+    tot[g] = g < r.G ? run : 0u;
+    __syncthreads();
+    if (g == 0) {
+        uint32_t b = 0;
+        for (int x = 0; x < r.G; ++x) {
+            r.shard_base[x] = b;
+            r.shard_tot[x] = tot[x];
+            b += tot[x];
+        }
+        r.shard_base[r.G] = b;
+    }
+}
+
+__global__ void __launch_bounds__(kRouteThreads) k_route_scatter(RouteArgs r) {
+    __shared__ uint32_t wrun[kRouteThreads / 64][kMaxShards];  // each wave's running count per shard in its range
+    __shared__ uint32_t wtot[kRouteThreads / 64][kMaxShards];  // each wave's total per shard (its range's prefix)
+    const int tid = threadIdx.x, lane = route_lane(), wave = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
+    const uint64_t w0 = base + (uint64_t)wave * kRouteWaveRecs;  // the wave's contiguous records
+    for (int x = lane; x < kMaxShards; x += 64) {
+        wrun[wave][x] = 0;
+        wtot[wave][x] = 0;
+    }
+    // 1. per wave: records per shard over its range (the tile's stable order is wave 0's records, then wave 1's …)
+    for (int it = 0; it < kRouteWaveRecs / 64; ++it) {
+        const uint64_t i = w0 + (uint64_t)it * 64 + lane;
+        const uint32_t s = i < r.n ? shard_of_rec(r, r.rec[i]) : (uint32_t)kRouteNone;
+        const uint64_t peers = match_shard(s);
+        if (s < (uint32_t)r.G && (peers & ((1ull << lane) - 1ull)) == 0) wtot[wave][s] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // 2. place: position = shard base + the tile's offset + earlier waves of the tile + earlier rounds + rank in round
+    for (int it = 0; it < kRouteWaveRecs / 64; ++it) {
+        const uint64_t i = w0 + (uint64_t)it * 64 + lane;
+        uint64_t rec = 0;
+        uint32_t s = (uint32_t)kRouteNone;
+        if (i < r.n) {
+            rec = r.rec[i];
+            s = shard_of_rec(r, rec);
+        }
+        const uint64_t peers = match_shard(s);
+        const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (s < (uint32_t)r.G) {
+            uint32_t before = 0;
+            for (int w = 0; w < wave; ++w) before += wtot[w][s];
+            const uint32_t pos = r.shard_base[s] + r.tile_cnt[(size_t)blockIdx.x * kMaxShards + s] + before +
+                                 wrun[wave][s] + rank;
+            const uint32_t k = (uint32_t)(rec >> r.kshift);
+            const uint32_t idx = (uint32_t)((rec >> r.abits) & r.imask);
+            const sg_req q = r.req[idx];
+            sg_req o;
+            o.ts_ms = q.ts_ms;
+            o.key = r.local_of[k] | (q.key & SG_KEY_PRIO);
+            o.acquire = q.acquire;
+            r.sub_req[pos] = o;
+            r.sub_pos[pos] = idx;
+        }
+        if (s < (uint32_t)r.G && rank == 0) wrun[wave][s] += (uint32_t)__popcll(peers);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_route_gather(const sg_result* sub_out, const uint32_t* sub_pos, uint64_t total,
+                                                      sg_result* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < total; j += (uint64_t)gridDim.x * blockDim.x)
+        out[sub_pos[j]] = sub_out[j];
+}
+
+hipError_t launch_route(const RouteArgs& r, hipStream_t stream) {
+    const uint32_t tiles = (uint32_t)((r.n + kRouteTile - 1) / kRouteTile);
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kMaxShards), 0, stream, r, tiles);
+    hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_gather(const sg_result* sub_out, const uint32_t* sub_pos, uint64_t total, sg_result* out,
+                               hipStream_t stream) {
+    if (total == 0) return hipSuccess;
+    uint64_t g = (total + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_route_gather, dim3((unsigned)g), dim3(256), 0, stream, sub_out, sub_pos, total, out);
+    return hipGetLastError();
+}
+
+uint64_t route_tiles(uint64_t n) { return (n + kRouteTile - 1) / kRouteTile; }
+
+}  // namespace sg

@@ -28,7 +28,10 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values", "sg_cparam_last_rounds",
            "sg_pslot_load_rules", "sg_pslot_decide_batch", "sg_pslot_decide_batch_host", "sg_pslot_thread_count",
            "sg_pslot_param_idx",
-           "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state"]
+           "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state",
+           "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
+           "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
+           "sg_node_snapshot_metrics", "sg_node_shard_of"]
 
 _lib = None
 
@@ -117,6 +120,16 @@ def load_library():
         "sg_pace_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_pace_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_pace_read_state": (C.c_int, [vp, u32, vp]),
+        "sg_node_create": (C.c_int, [C.POINTER(abi.sg_config), vp, u32, C.POINTER(vp)]),
+        "sg_node_destroy": (None, [vp]),
+        "sg_node_last_error": (C.c_char_p, [vp]),
+        "sg_node_set_namespaces": (C.c_int, [vp, vp, u32]),
+        "sg_node_load_flow_rules": (C.c_int, [vp, vp, u32]),
+        "sg_node_flow_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_node_flow_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_node_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
+        "sg_node_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
+        "sg_node_shard_of": (C.c_int, [vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -124,6 +137,67 @@ def load_library():
         f.argtypes = args
     _lib = L
     return L
+
+
+class NodeEngine:
+    """One sg_node: a token server's cluster flow rules over G shard handles (devices[g] per shard; one device may
+    hold several), with routing by flowId owner inside the library."""
+
+    def __init__(self, devices, max_batch=1 << 20, exceed_count=1.0, max_occupy_ratio=1.0, flags=0):
+        L = load_library()
+        cfg = abi.sg_config(device=int(devices[0]), flags=flags, exceed_count=exceed_count,
+                            max_occupy_ratio=max_occupy_ratio, max_batch=max_batch)
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = C.c_void_p()
+        rc = L.sg_node_create(C.byref(cfg), abi.ptr(devs), len(devs), C.byref(h))
+        if rc != 0:
+            raise EngineError(rc, "sg_node_create failed")
+        self._L, self.h, self.G = L, h, len(devs)
+        self._S = {}
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self._L.sg_node_destroy(self.h)
+            self.h = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise EngineError(rc, self._L.sg_node_last_error(self.h).decode())
+
+    def set_namespaces(self, ns: np.ndarray):
+        ns = np.ascontiguousarray(ns, dtype=abi.NS_DTYPE)
+        self._check(self._L.sg_node_set_namespaces(self.h, abi.ptr(ns), len(ns)))
+
+    def load_rules(self, rules: np.ndarray):
+        rules = np.ascontiguousarray(rules, dtype=abi.RULE_DTYPE)
+        self._check(self._L.sg_node_load_flow_rules(self.h, abi.ptr(rules), len(rules)))
+        self._S = {int(k): int(s) for k, s in enumerate(rules["sample_count"])} if len(rules) else {}
+
+    def decide_host(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.REQ_DTYPE)
+        out = np.zeros(len(req), dtype=abi.RES_DTYPE)
+        self._check(self._L.sg_node_flow_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        self._check(self._L.sg_node_flow_decide_batch(self.h, req_ptr, n, out_ptr, stream_ptr))
+
+    def shard_of(self, key):
+        s, lk = C.c_uint32(), C.c_uint32()
+        self._check(self._L.sg_node_shard_of(self.h, key, C.byref(s), C.byref(lk)))
+        return s.value, lk.value
+
+    def read_state(self, key, sample_count):
+        starts = np.zeros(sample_count, np.int64)
+        counters = np.zeros(sample_count * abi.NUM_EVENTS, np.int64)
+        occ = np.zeros(2, np.int64)
+        self._check(self._L.sg_node_flow_read_state(self.h, key, abi.ptr(starts), abi.ptr(counters), abi.ptr(occ)))
+        return starts, counters.reshape(sample_count, abi.NUM_EVENTS), occ
+
+    def snapshot(self, now_ms, n_rules):
+        out = np.zeros(2 * max(n_rules, 1), np.float64)
+        self._check(self._L.sg_node_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
+        return out[:2 * n_rules].reshape(n_rules, 2)
 
 
 class FlowEngine:

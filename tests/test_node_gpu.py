@@ -1,0 +1,152 @@
+"""Parity of the node handle (sg_node_*: one token server over G shard handles with routing inside the library) with
+one sequential DefaultTokenService over the whole node's rules (oracle.binding.ClusterTokenService).
+
+The node hashes flowIds over its shards (splitmix64(flowId) mod G), runs validation and the namespace limiters over
+each node batch in caller order on its front handle, splits the admitted requests by owner (a stable device
+multisplit, node.hip), lets every shard decide its slice on its own stream, and gathers the results back. Here the
+G shards share device 0 (the one-GPU box); the same code peer-copies slices for shards on other devices. Compared
+bit-exactly: every result (BAD_REQUEST / NO_RULE_EXISTS / TOO_MANY_REQUEST / OK / BLOCKED / SHOULD_WAIT, remaining,
+wait), every flowId's ClusterMetric ring and occupy counters, across rule reloads; the node's metric snapshot equals
+a single handle's that decided the same batches.
+"""
+import numpy as np
+import pytest
+
+from oracle.binding import ClusterTokenService
+from sentinel_amd import abi
+from sentinel_amd.workload import zipf_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def _rules(rng, K, fid0=1000):
+    r = np.zeros(K, abi.RULE_DTYPE)
+    r["flow_id"] = fid0 + rng.permutation(10 * K)[:K]
+    r["count"] = rng.integers(1, 40, K)
+    r["threshold_type"] = np.where(rng.random(K) < 0.8, abi.THRESHOLD_GLOBAL, 0)
+    r["sample_count"] = rng.choice([2, 5, 10], K)
+    r["window_interval_ms"] = 1000
+    r["namespace_id"] = rng.integers(0, 3, K)
+    return r
+
+
+def _ns(lim_qps):
+    ns = np.zeros(3, abi.NS_DTYPE)
+    ns["connected_count"] = [2, 1, 4]
+    if lim_qps:
+        ns["limiter_enabled"][[0, 2]] = 1
+        ns["max_allowed_qps"][[0, 2]] = [lim_qps, lim_qps / 2]
+    return ns
+
+
+def _batch(rng, n, K, t, span):
+    req = np.zeros(n, abi.REQ_DTYPE)
+    req["ts_ms"] = t + np.sort(rng.integers(0, span, n))
+    req["key"] = zipf_keys(rng, K, n, 1.0, perm_seed=int(rng.integers(1 << 30))).astype(np.uint32)
+    u = rng.random(n)
+    req["key"][u < 0.01] = abi.KEY_NO_RULE
+    req["key"][(u >= 0.01) & (u < 0.015)] = abi.KEY_BAD
+    req["key"] |= np.where(rng.random(n) < 0.05, np.uint32(abi.KEY_PRIO), np.uint32(0))
+    acq = np.ones(n, np.int32)
+    m = rng.random(n) < 0.1
+    acq[m] = rng.integers(2, 5, int(m.sum()))
+    acq[rng.random(n) < 0.005] = 0
+    req["acquire"] = acq
+    return req
+
+
+def _compare_state(node, cts, rules):
+    for k in range(len(rules)):
+        S = int(rules["sample_count"][k])
+        s_g, c_g, o_g = node.read_state(k, S)
+        s_o, c_o, o_o = cts.read_state(k)
+        assert np.array_equal(s_g, s_o) and np.array_equal(c_g, c_o) and np.array_equal(o_g, o_o), f"flowId key {k}"
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+@pytest.mark.parametrize("lim_qps", [0.0, 3000.0])
+def test_node_equals_one_token_service(G, lim_qps):
+    from sentinel_amd.engine import FlowEngine, NodeEngine
+    rng = np.random.default_rng(10 * G + int(lim_qps > 0))
+    K = 300
+    rules = _rules(rng, K)
+    ns = _ns(lim_qps)
+    node = NodeEngine([0] * G, max_batch=1 << 17)
+    node.set_namespaces(ns)
+    node.load_rules(rules)
+    single = FlowEngine(device=0, max_batch=1 << 17)
+    single.set_namespaces(ns)
+    single.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(ns)
+    cts.load_rules(rules)
+    owners = {node.shard_of(k)[0] for k in range(K)}
+    assert owners == set(range(G))
+    t = 1_700_000_000_000 + int(rng.integers(0, 1000))
+    for b in range(3):
+        req = _batch(rng, 40_000, K, t, 1800)
+        want = cts.decide(req)
+        got = node.decide_host(req)
+        if not np.array_equal(got, want):
+            bad = np.nonzero(got != want)[0]
+            raise AssertionError(f"batch {b}: {len(bad)} results differ; first at {bad[0]}: req={req[bad[0]]} "
+                                 f"oracle={want[bad[0]]} node={got[bad[0]]}")
+        assert np.array_equal(single.decide_host(req), want)
+        t = int(req["ts_ms"][-1]) + 1
+    _compare_state(node, cts, rules)
+    now = t + 5
+    assert np.array_equal(node.snapshot(now, K), single.snapshot(now, K).reshape(K, 2))
+
+
+def test_node_rule_reload_keeps_surviving_metrics():
+    """ClusterFlowRuleManager reload (ClusterFlowRuleManager.java:361, putMetricIfAbsent): a surviving flowId keeps its
+    owner shard and its ClusterMetric; new flowIds start empty; removed ones disappear."""
+    from sentinel_amd.engine import NodeEngine
+    rng = np.random.default_rng(5)
+    K = 200
+    rules = _rules(rng, K)
+    ns = _ns(0.0)
+    node = NodeEngine([0, 0, 0], max_batch=1 << 16)
+    node.set_namespaces(ns)
+    node.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(ns)
+    cts.load_rules(rules)
+    t = 1_700_000_000_000
+    req = _batch(rng, 20_000, K, t, 900)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    keep = rng.permutation(K)[:120]
+    fresh = _rules(rng, 60, fid0=900_000)
+    rules2 = np.concatenate([rules[keep], fresh])
+    rng.shuffle(rules2)
+    rules2["count"] = rng.integers(1, 40, len(rules2))
+    node.load_rules(rules2)
+    cts.load_rules(rules2)
+    t = int(req["ts_ms"][-1]) + 1
+    for _ in range(2):
+        req = _batch(rng, 20_000, len(rules2), t, 900)
+        assert np.array_equal(node.decide_host(req), cts.decide(req))
+        t = int(req["ts_ms"][-1]) + 1
+    _compare_state(node, cts, rules2)
+
+
+def test_node_rejects_a_batch_as_a_whole():
+    """A batch out of time order is refused before any shard sees it (SG_E_TIME): no state changes."""
+    from sentinel_amd.engine import EngineError, NodeEngine
+    rng = np.random.default_rng(6)
+    rules = _rules(rng, 50)
+    node = NodeEngine([0, 0], max_batch=1 << 14)
+    node.set_namespaces(_ns(500.0))
+    node.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(_ns(500.0))
+    cts.load_rules(rules)
+    req = _batch(rng, 5000, 50, 10_000, 500)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    late = _batch(rng, 100, 50, 9_000, 10)
+    with pytest.raises(EngineError) as ei:
+        node.decide_host(late)
+    assert ei.value.code == abi.SG_E_TIME
+    req = _batch(rng, 5000, 50, 10_600, 500)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    _compare_state(node, cts, rules)
