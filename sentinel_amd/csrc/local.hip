@@ -402,6 +402,14 @@ struct LNode {
         if (qs != cs.q) sec_open(qs);
         if (qm != cm.q) min_open(qm);
     }
+    // one window only: each read or add of the reference calls currentWindow on the window it touches, and a node
+    // the event leaves alone keeps its stale buckets (the full-chain walker opens exactly what the reference touches)
+    __device__ __forceinline__ void at_s(uint32_t qs) {
+        if (qs != cs.q) sec_open(qs);
+    }
+    __device__ __forceinline__ void at_m(uint32_t qm) {
+        if (qm != cm.q) min_open(qm);
+    }
 
     __device__ __forceinline__ double pass_qps() const { return qps_of(s_wo + sc[kLPass], a.isec); }
 
@@ -1249,12 +1257,16 @@ __device__ int cx_select(const LArgs& a, const LRule& R, const LFlowRule& r, int
     return -1;
 }
 
-// One rule's canPass on the selected node: 0 block, 1 pass (*wait: the controller's sleep), 2 PriorityWaitException
+// One rule's canPass on the selected node: 0 block, 1 pass (*wait: the controller's sleep), 2 PriorityWaitException.
+// The node's windows are opened as the controller reads them: passQps the second window, previousPassQps the minute
+// window, the occupy path both (tryOccupyNext, addWaitingRequest, addOccupiedPass); a THREAD rule reads neither.
 __device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, const LEvent& e, int64_t t,
-                       int64_t* wait) {
+                       uint32_t qs, uint32_t qm, int64_t* wait) {
     *wait = 0;
     switch (r.behavior) {
     case SG_CONTROL_WARM_UP: {  // WarmUpController.canPass (:113-138)
+        n.at_s(qs);
+        n.at_m(qm);
         const int64_t pass_qps = java_d2l(n.pass_qps());
         warm_sync(r, c, t, java_d2l((double)n.prev_pass(t)));
         const int64_t sum = (int64_t)((uint64_t)pass_qps + (uint64_t)(int64_t)e.count);
@@ -1266,14 +1278,17 @@ __device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, co
         if (r.count <= 0) return 0;
         return pace_step(r, c, t, java_round(1.0 * (double)e.count / r.count * 1000), wait) ? 1 : 0;
     case SG_CONTROL_WARM_UP_RATE_LIMITER: {  // WarmUpRateLimiterController.canPass (:43-87)
+        n.at_m(qm);
         warm_sync(r, c, t, java_d2l((double)n.prev_pass(t)));
         const double q = c.stored >= r.warning_token ? warm_qps(r, c.stored - r.warning_token) : r.count;
         return pace_step(r, c, t, java_round(1.0 * (double)e.count / q * 1000), wait) ? 1 : 0;
     }
     default: {  // DefaultController.canPass (:49-76)
+        if (r.grade != 0) n.at_s(qs);
         const int32_t cur = r.grade == 0 ? (int32_t)n.threads : java_d2i(n.pass_qps());
         if (!((double)(int32_t)((uint32_t)cur + (uint32_t)e.count) > r.count)) return 1;
         if (e.prio && r.grade == 1) {
+            n.at_m(qm);
             const int64_t w = n.try_occupy_next(t, e.count, r.count);
             if (w < a.occupy_timeout) {
                 const int s = n.bor_window(t + w);  // addWaitingRequest
@@ -1308,10 +1323,8 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
     const uint2 nodes = event_nodes(a, e.idx);
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
-    LNode on(a, bndp, have_on ? on_idx : nd.k);
-    if (have_on) on.at(qs, qm);
+    LNode on(a, bndp, have_on ? on_idx : nd.k);  // windows opened as touched (cx_rule, the StatisticSlot adds)
     LNode cn(a, bndp, have_cn ? cn_idx : nd.k);
-    if (have_cn) cn.at(qs, qm);
     const bool params = R.ps && a.has_ps && x && !x->args_null;
     int32_t status = SG_LOCAL_PASS;
     int64_t wait = 0;
@@ -1365,15 +1378,14 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
         int64_t w = 0;
         int v;
         if (sel == 0 || (sel == 3 && r.ref == (int32_t)nd.k)) {
-            v = cx_rule(a, nd, r, c, e, t, &w);
+            v = cx_rule(a, nd, r, c, e, t, qs, qm, &w);
         } else if (sel == 1) {
-            v = cx_rule(a, on, r, c, e, t, &w);
+            v = cx_rule(a, on, r, c, e, t, qs, qm, &w);
         } else if (sel == 2) {
-            v = cx_rule(a, cn, r, c, e, t, &w);
+            v = cx_rule(a, cn, r, c, e, t, qs, qm, &w);
         } else {  // RELATE: another resource of this key group, kept in memory between its events
             LNode rn(a, bndp, (uint32_t)r.ref);
-            rn.at(qs, qm);
-            v = cx_rule(a, rn, r, c, e, t, &w);
+            v = cx_rule(a, rn, r, c, e, t, qs, qm, &w);
             rn.finish();
         }
         if (v == 0) {
@@ -1388,32 +1400,38 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
         wait += w;  // each rate limiter sleeps in turn
     }
     if (status == SG_LOCAL_PASS && nd.degrade_blocks([&]() { return t; })) status = SG_LOCAL_BLOCK_DEGRADE;
-    if (status == SG_LOCAL_PASS) {
+    if (status == SG_LOCAL_PASS) {  // addPassRequest: both windows of each node
+        nd.at(qs, qm);
         nd.threads += 1;
         nd.sc[kLPass] += e.count;
         nd.mc[kLPass] += e.count;
         if (have_on) {
+            on.at(qs, qm);
             on.threads += 1;
             on.sc[kLPass] += e.count;
             on.mc[kLPass] += e.count;
         }
         if (have_cn) {
+            cn.at(qs, qm);
             cn.threads += 1;
             cn.sc[kLPass] += e.count;
             cn.mc[kLPass] += e.count;
         }
-    } else if (status == SG_LOCAL_PASS_WAIT) {
+    } else if (status == SG_LOCAL_PASS_WAIT) {  // PriorityWaitException: thread counts only
         nd.threads += 1;
         if (have_on) on.threads += 1;
         if (have_cn) cn.threads += 1;
-    } else {
+    } else {  // increaseBlockQps: both windows
+        nd.at(qs, qm);
         nd.sc[kLBlock] += e.count;
         nd.mc[kLBlock] += e.count;
         if (have_on) {
+            on.at(qs, qm);
             on.sc[kLBlock] += e.count;
             on.mc[kLBlock] += e.count;
         }
         if (have_cn) {
+            cn.at(qs, qm);
             cn.sc[kLBlock] += e.count;
             cn.mc[kLBlock] += e.count;
         }
@@ -1484,7 +1502,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
                 LNode nd(a, bndp, le.resource & SG_KEY_INDEX);
                 nd.created = 1;
                 const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
-                nd.at(qs, qm);
+                if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);  // an entry opens what it touches (cx_entry)
                 if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
                 else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
                 nd.finish();
@@ -1501,7 +1519,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
             const sg_slot_ext* x = a.ext ? a.ext + e.idx : nullptr;
             const int ctx = x ? (int)x->context : 0;
             const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
-            nd.at(qs, qm);
+            if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);
             if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
             else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
         }
