@@ -726,6 +726,11 @@ int         sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint6
 int         sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
 int         sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap);
 int         sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key);
+/* The node's front handle (devices[0]; owned by the node, not to be destroyed): it holds the namespace limiters, so
+ * the node's cluster param tokens (sg_cparam_*: ClusterParamFlowChecker.java:43-45 shares the limiter) and
+ * concurrent tokens (sg_conc_*) are decided on it, beside the sharded flow tokens. Its own sg_flow_* entry points
+ * must not be called. */
+sg_handle*  sg_node_front(sg_node* nd);
 
 /* ---------- token-server wire codec ----------
  * The default token server frames every message with a 2-byte big-endian length

@@ -53,6 +53,7 @@ struct sg_handle {
     uint32_t* d_short_key = nullptr;  // flowId of each d_short_list entry (cluster flow path)
     uint32_t* d_short_end = nullptr;  // segment end of each d_short_list entry (cluster flow path)
     uint32_t* d_long_key = nullptr;   // flowId of each d_long_list entry (cluster flow path)
+    uint32_t* d_long_end = nullptr;   // segment end of each d_long_list entry (cluster flow path)
     uint32_t* d_long_pend = nullptr;
     FidSlot* d_fid = nullptr;         // flowId → rule index (wire codec), 2^k slots
     uint64_t fid_mask = 0;  // [kLongTab][kLongPeriods] period ends of the long segments
@@ -273,6 +274,7 @@ struct sg_handle {
         int* err = nullptr;
         uint32_t* long_list = nullptr;
         uint32_t* long_key = nullptr;
+        uint32_t* long_end = nullptr;
         uint32_t* long_pend = nullptr;
         uint32_t* short_list = nullptr;
         uint32_t* short_key = nullptr;
@@ -302,6 +304,7 @@ struct sg_handle {
     };
     DevTicket dev[kDevSlots];
     bool front_only = false;          // a node handle's front (validation + namespace limiter): no flow state
+    bool seg_mark_pass = false;       // env SG_SEG_MARK=1: k_seg_mark over the sorted records (A/B of the fused marks)
 };
 
 namespace {
@@ -480,6 +483,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&h->d_long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+        hipMalloc(&h->d_long_end, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&h->d_long_pend, sizeof(uint32_t) * (size_t)kLongTab * kLongPeriods) != hipSuccess)
         return bail(SG_E_NOMEM);
     {  // short-segment class slices: class c holds segments longer than kClassMax[c-1], so at most n/(that+1)
@@ -511,6 +515,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         return bail(SG_E_DEVICE);
     if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
     if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
+    if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -539,6 +544,7 @@ void sg_destroy(sg_handle* h) {
         dfree(w.err);
         dfree(w.long_list);
         dfree(w.long_key);
+        dfree(w.long_end);
         dfree(w.long_pend);
         dfree(w.short_list);
         dfree(w.short_key);
@@ -594,6 +600,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_short_key);
     dfree(h->d_short_end);
     dfree(h->d_long_key);
+    dfree(h->d_long_end);
     dfree(h->d_long_pend);
     dfree(h->d_fid);
     dfree(h->d_dbg);
@@ -902,6 +909,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
             dfree(d_src);
             return fail(h, SG_E_NOMEM, "rule state allocation failed");
         }
+        HIP_TRY(h, hipMemset(d_seg_end, 0, sizeof(uint32_t) * n));           // no segment ends marked
         HIP_TRY(h, hipMemset(d_seg_end + n, 0xFF, sizeof(uint32_t) * n));  // no segment starts marked
         HIP_TRY(h, hipMemcpy(d_src, src.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, launch_init_state(d_ring, d_occ, n, stride, d_src, h->d_ring, h->d_occ, h->stride, 0));
@@ -1055,6 +1063,7 @@ void main_ws(sg_handle* h, sg_handle::FlowWs& w) {
     w.err = h->d_err;
     w.long_list = h->d_long_list;
     w.long_key = h->d_long_key;
+    w.long_end = h->d_long_end;
     w.long_pend = h->d_long_pend;
     w.short_list = h->d_short_list;
     w.short_key = h->d_short_key;
@@ -1080,6 +1089,7 @@ int pipe_setup(sg_handle* h) {
             hipMalloc(&w.np, sizeof(uint32_t) * kMaxWl) != hipSuccess || hipMalloc(&w.err, sizeof(int)) != hipSuccess ||
             hipMalloc(&w.long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
             hipMalloc(&w.long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
+            hipMalloc(&w.long_end, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
             hipMalloc(&w.long_pend, sizeof(uint32_t) * (size_t)kLongTab * kLongPeriods) != hipSuccess ||
             hipMalloc(&w.short_list, sizeof(uint32_t) * short_words) != hipSuccess ||
             hipMalloc(&w.short_key, sizeof(uint32_t) * short_words) != hipSuccess ||
@@ -1127,6 +1137,7 @@ int pipe_setup(sg_handle* h) {
         if (hipMalloc(&w.seg_end, sizeof(uint32_t) * 2 * (h->K + 1)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "pipeline workspace");
         h->pws_segcap = h->K + 1;
+        HIP_TRY(h, hipMemset(w.seg_end, 0, sizeof(uint32_t) * h->pws_segcap));
         HIP_TRY(h, hipMemset(w.seg_end + h->pws_segcap, 0xFF, sizeof(uint32_t) * h->pws_segcap));
     }
     w.seg_start = w.seg_end + h->pws_segcap;
@@ -1170,6 +1181,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.short_list = w.short_list;
     a.short_key = w.short_key;
     a.long_key = w.long_key;
+    a.long_end = w.long_end;
     a.long_pend = w.long_pend;
     a.short_count = w.counts + 1;
     for (int c = 0; c < kClasses; ++c) a.class_off[c] = h->class_off[c];
@@ -1230,7 +1242,11 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
-        HIP_TRY(h, radix_sort_records(a.rec, a.rec_sorted, a.n, a.kshift, hist, &sorted, stream, 64, a.hist0 != nullptr));
+        // the last pass also marks each flowId's segment (env SG_SEG_MARK=1: the separate k_seg_mark pass instead)
+        const SegMark mk{a.seg_start, a.seg_end, a.K, a.kshift};
+        a.seg_marked = (a.seg_start && a.seg_end && a.long_end && !h->seg_mark_pass) ? 1 : 0;
+        HIP_TRY(h, radix_sort_records(a.rec, a.rec_sorted, a.n, a.kshift, hist, &sorted, stream, 64, a.hist0 != nullptr,
+                                      a.seg_marked ? &mk : nullptr));
         a.rec_sorted = sorted;
         if (a.rec == h->d_rec) h->last_sorted = sorted;
     }
@@ -4085,6 +4101,8 @@ int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) 
     nd->local_of = lo;
     return SG_OK;
 }
+
+sg_handle* sg_node_front(sg_node* nd) { return nd ? nd->front : nullptr; }
 
 int sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key) {
     if (!nd || !shard || !local_key || key >= nd->shard_of.size()) return SG_E_INVAL;

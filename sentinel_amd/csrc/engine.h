@@ -101,6 +101,8 @@ struct BatchArgs {
     uint32_t* seg_end;     // [K] end of each present key's segment in rec_sorted (nullptr: not written)
     uint32_t* seg_start;   // [K] start of each present key's segment (k_seg_mark), 0xFFFFFFFF between batches
     uint32_t* short_end;   // end of each short_list entry's segment (k_seg_classify)
+    uint32_t* long_end;    // end of each long_list entry's segment (k_seg_classify; nullptr: seg_end[long_key])
+    int seg_marked;        // the sort's last pass marked seg_start / seg_end (launch_seg_flow skips k_seg_mark)
     uint32_t* long_pend;   // [kLongTab][kLongPeriods]: position in rec_sorted where period q + 1 of long segment
                            // i begins (k_long_bounds; nullptr: the wave walker searches for it)
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
@@ -679,8 +681,16 @@ uint64_t route_tiles(uint64_t n);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 int radix_digit_bits(int bits);  // digit width radix_sort_records uses for `bits` key bits (8 or 10)
+// Segment marks of a flowId-keyed sort's last pass (seg_start atomicMin / seg_end atomicMax per key, see sort.hip)
+struct SegMark {
+    uint32_t* seg_start;
+    uint32_t* seg_end;
+    uint32_t K;
+    int kshift;
+};
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false);
+                              uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false,
+                              const SegMark* mark = nullptr);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with

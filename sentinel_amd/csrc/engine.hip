@@ -854,8 +854,9 @@ __global__ void __launch_bounds__(256) k_seg_classify(BatchArgs a) {
             const uint64_t k = k0 + (uint64_t)u * 256 + tid;
             slot[u] = 0xFFFFFFFFu;
             if (st[u] == 0xFFFFFFFFu) continue;
-            a.seg_start[k] = 0xFFFFFFFFu;
-            en[u] = a.seg_end[k];
+            a.seg_start[k] = 0xFFFFFFFFu;  // both marks cleared for the next batch (the sort's last pass
+            en[u] = a.seg_end[k];          // takes atomicMin / atomicMax of them)
+            a.seg_end[k] = 0;
             const uint32_t len = en[u] - st[u];
             uint32_t l = 0;
 #pragma unroll
@@ -878,6 +879,7 @@ __global__ void __launch_bounds__(256) k_seg_classify(BatchArgs a) {
             if (l == (uint32_t)kClasses) {
                 a.long_list[pos] = st[u];
                 a.long_key[pos] = k;
+                a.long_end[pos] = en[u];
             } else {
                 const uint64_t q = a.class_off[l] + pos;
                 a.short_list[q] = st[u];
@@ -926,9 +928,9 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
         const uint64_t s = a.long_list[item];
         uint32_t k;
         uint64_t e;
-        if (a.long_key && a.seg_end) {  // segment key and end from k_seg
+        if (a.long_key && a.seg_end) {  // segment key and end from k_seg / k_seg_classify
             k = a.long_key[item];
-            e = a.seg_end[k];
+            e = a.long_end ? a.long_end[item] : a.seg_end[k];
         } else {  // segment end: the first record with another flowId
             k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
             e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
@@ -964,7 +966,7 @@ __global__ void __launch_bounds__(256) k_long_bounds(BatchArgs a) {
         const uint32_t npw = a.np[w];
         if (npw > (uint32_t)kLongPeriods || q + 1 >= npw) continue;
         const uint32_t nb = a.bnd[(size_t)w * kMaxPeriods + q + 1];
-        uint64_t lo = a.long_list[item], hi = a.seg_end[k];
+        uint64_t lo = a.long_list[item], hi = a.long_end ? a.long_end[item] : a.seg_end[k];
         while (lo < hi) {  // first record of the segment in period q + 1 or later
             const uint64_t mid = (lo + hi) >> 1;
             if ((uint32_t)((a.rec_sorted[mid] >> a.abits) & a.imask) >= nb) hi = mid;
@@ -1503,7 +1505,7 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
             const uint64_t s = a.short_list[li];
             const uint32_t k = a.short_key[li];
             // 2. everything that depends on (s, k) only
-            const uint64_t e = a.seg_end[k];
+            const uint64_t e = a.short_end ? a.short_end[li] : a.seg_end[k];
             const Rule R = a.rules[k];
             const Occ occ = a.occ[k];
             uint64_t buf[kBlk];
@@ -1830,7 +1832,8 @@ hipError_t launch_seg(const BatchArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_seg_mark, dim3((unsigned)((a.n + 256 * kMarkItems - 1) / (256 * kMarkItems))), dim3(256), 0,
+    if (!a.seg_marked)
+        hipLaunchKernelGGL(k_seg_mark, dim3((unsigned)((a.n + 256 * kMarkItems - 1) / (256 * kMarkItems))), dim3(256), 0,
                        stream, a);
     if (a.K) hipLaunchKernelGGL(k_seg_classify, dim3(grid_for(a.K, 256 * kClsItems, 4096)), dim3(256), 0, stream, a);
     return hipGetLastError();

@@ -170,10 +170,16 @@ __global__ void __launch_bounds__(1 << D) k_rescan(uint32_t* hist, const uint32_
     }
 }
 
-template <int D>
+// MARK (the last pass of a sort whose key is a flowId index, SegMark): besides the records, each key's segment in
+// the sorted output — within a digit's run of the tile the records are sorted by the whole key, so the first and
+// last record of every key in the run are found by comparing LDS neighbours; the segment's start is the smallest of
+// its runs' firsts (atomicMin on seg_start, 0xFFFFFFFF between batches) and its end the largest of their lasts + 1
+// (atomicMax on seg_end, 0 between batches; k_seg_classify consumes and clears both). This replaces a separate pass
+// over the sorted records (k_seg_mark).
+template <int D, bool MARK>
 __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* in, uint64_t* out, uint64_t n, int shift,
                                                                 const uint32_t* hist, uint32_t ntiles,
-                                                                const uint32_t* tot) {
+                                                                const uint32_t* tot, SegMark mk) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;  // digits per thread
     using Cnt = typename std::conditional<(D > 8), uint16_t, uint32_t>::type;  // wave counts <= 1024
@@ -285,7 +291,17 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     for (uint32_t p = tid; p < cnt; p += kSortThreads) {
         const uint64_t v = stage[p];
         const uint32_t d = (uint32_t)(v >> shift) & (kBins - 1);
-        out[(uint64_t)gbase[d] + (p - dstart[d])] = v;
+        const uint32_t gp = gbase[d] + (p - dstart[d]);
+        out[gp] = v;
+        if constexpr (MARK) {
+            const uint32_t k = (uint32_t)(v >> mk.kshift);
+            if (k < mk.K) {
+                const uint32_t r0 = dstart[d];
+                const uint32_t r1 = d + 1 < (uint32_t)kBins ? dstart[d + 1] : cnt;  // the digit's run in the tile
+                if (p == r0 || (uint32_t)(stage[p - 1] >> mk.kshift) != k) atomicMin(mk.seg_start + k, gp);
+                if (p + 1 == r1 || (uint32_t)(stage[p + 1] >> mk.kshift) != k) atomicMax(mk.seg_end + k, gp + 1);
+            }
+        }
     }
 }
 
@@ -301,7 +317,7 @@ int radix_digit_bits(int bits) { return ((bits > 16 && bits <= 20) || (bits > 24
 
 template <int D>
 static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
-                       bool hist_ready) {
+                       bool hist_ready, const SegMark* mark) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     uint32_t* hist = hist_ws;                                   // [ntiles][bins], then run offsets in place
@@ -313,22 +329,28 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
     hipLaunchKernelGGL(k_chunkscan<D>, dim3((1u << D) / 64), dim3(1024), 0, stream, csum, nchunks, tot);
     hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, csum, ntiles);
     const uint32_t grid = 8 * ((ntiles + 7) / 8);  // xcd_tile: blocks past ntiles return at once
-    hipLaunchKernelGGL(k_radix_scatter<D>, dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift, hist, ntiles,
-                       tot);
+    if (mark)
+        hipLaunchKernelGGL((k_radix_scatter<D, true>), dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift,
+                           hist, ntiles, tot, *mark);
+    else
+        hipLaunchKernelGGL((k_radix_scatter<D, false>), dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift,
+                           hist, ntiles, tot, SegMark{});
 }
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),
 // ping-ponging between a and b. Returns the buffer that holds the result through *result.
 // first_hist_ready: the first pass's per-tile histogram (radix_digit_bits wide) is already in hist_ws (k_prep).
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
-                              uint64_t** result, hipStream_t stream, int hi_bit, bool first_hist_ready) {
+                              uint64_t** result, hipStream_t stream, int hi_bit, bool first_hist_ready,
+                              const SegMark* mark) {
     uint64_t* src = a;
     uint64_t* dst = b;
     const int D = radix_digit_bits(hi_bit - lo_bit);
     for (int shift = lo_bit; shift < hi_bit && n > 0; shift += D) {
         const bool ready = shift == lo_bit && first_hist_ready;
-        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready);
-        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready);
+        const SegMark* mk = shift + D >= hi_bit ? mark : nullptr;  // the last pass marks the segments
+        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready, mk);
+        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready, mk);
         uint64_t* t = src;
         src = dst;
         dst = t;

@@ -112,8 +112,15 @@ GpuTokenService::GpuTokenService(Options opt) : opt_(std::move(opt)) {
     cfg.exceed_count = opt_.exceedCount;
     cfg.max_occupy_ratio = opt_.maxOccupyRatio;
     cfg.max_batch = opt_.maxBatch;
-    int rc = sg_create(&cfg, &h_);
-    if (rc != SG_OK) throw std::runtime_error("sg_create failed: " + std::to_string(rc));
+    if (!opt_.shardDevices.empty()) {  // node mode: flow tokens over the shards, the rest on the front handle
+        std::vector<int32_t> devs(opt_.shardDevices.begin(), opt_.shardDevices.end());
+        int rc = sg_node_create(&cfg, devs.data(), (uint32_t)devs.size(), &node_);
+        if (rc != SG_OK) throw std::runtime_error("sg_node_create failed: " + std::to_string(rc));
+        h_ = sg_node_front(node_);
+    } else {
+        int rc = sg_create(&cfg, &h_);
+        if (rc != SG_OK) throw std::runtime_error("sg_create failed: " + std::to_string(rc));
+    }
     const int depth = std::max(1, std::min(3, opt_.pipelineDepth));
     for (int i = 0; i < depth; ++i) {
         sg_req* rq = static_cast<sg_req*>(sg_host_alloc(h_, sizeof(sg_req) * opt_.maxBatch));
@@ -125,7 +132,8 @@ GpuTokenService::GpuTokenService(Options opt) : opt_(std::move(opt)) {
                 sg_host_free(h_, b.first);
                 sg_host_free(h_, b.second);
             }
-            sg_destroy(h_);
+            if (node_) sg_node_destroy(node_);
+            else sg_destroy(h_);
             throw std::runtime_error("sg_host_alloc failed");
         }
         bufs_.emplace_back(rq, rs);
@@ -159,7 +167,8 @@ GpuTokenService::~GpuTokenService() {
         sg_host_free(h_, b.first);
         sg_host_free(h_, b.second);
     }
-    sg_destroy(h_);
+    if (node_) sg_node_destroy(node_);  // owns the front handle
+    else sg_destroy(h_);
 }
 
 void GpuTokenService::waitIdle() {
@@ -229,6 +238,11 @@ int GpuTokenService::nsIndex(const std::string& ns) {
 void GpuTokenService::pushNamespacesLocked() {
     waitIdle();
     std::lock_guard<std::mutex> e(engMu_);
+    if (node_) {
+        int rc = sg_node_set_namespaces(node_, nsCfg_.data(), (uint32_t)nsCfg_.size());
+        if (rc != SG_OK) err_ = sg_node_last_error(node_);
+        return;
+    }
     int rc = sg_set_namespaces(h_, nsCfg_.data(), (uint32_t)nsCfg_.size());
     if (rc != SG_OK) err_ = sg_last_error(h_);
 }
@@ -255,9 +269,10 @@ void GpuTokenService::pushRulesLocked() {
     }
     pushNamespacesLocked();
     std::lock_guard<std::mutex> e(engMu_);
-    int rc = sg_load_flow_rules(h_, tab.data(), (uint32_t)tab.size());
+    int rc = node_ ? sg_node_load_flow_rules(node_, tab.data(), (uint32_t)tab.size())
+                   : sg_load_flow_rules(h_, tab.data(), (uint32_t)tab.size());
     if (rc != SG_OK) {
-        err_ = sg_last_error(h_);
+        err_ = node_ ? sg_node_last_error(node_) : sg_last_error(h_);
         keyOfFlow_.clear();
     }
 }
@@ -337,9 +352,10 @@ std::vector<TokenResult> GpuTokenService::decideLocked(std::vector<sg_req>& reqs
     std::vector<sg_result> out(reqs.size());
     for (size_t off = 0; off < reqs.size(); off += opt_.maxBatch) {
         const size_t n = std::min<size_t>(opt_.maxBatch, reqs.size() - off);
-        int rc = sg_flow_decide_batch_host(h_, reqs.data() + off, n, out.data() + off);
+        int rc = node_ ? sg_node_flow_decide_batch_host(node_, reqs.data() + off, n, out.data() + off)
+                       : sg_flow_decide_batch_host(h_, reqs.data() + off, n, out.data() + off);
         if (rc != SG_OK) {  // TokenResult(FAIL) → the client falls back to local checking
-            err_ = sg_last_error(h_);
+            err_ = node_ ? sg_node_last_error(node_) : sg_last_error(h_);
             continue;
         }
         for (size_t i = off; i < off + n; ++i)
@@ -403,8 +419,13 @@ void GpuTokenService::flushLocked(std::unique_lock<std::mutex>& lk) {
         }
         {
             std::lock_guard<std::mutex> e(engMu_);
-            f.rc = sg_flow_submit(h_, bufs_[b].first, n, bufs_[b].second, &f.ticket);
-            if (f.rc != SG_OK) err_ = sg_last_error(h_);
+            if (node_) {  // the node routes and decides synchronously (ticket 0: done)
+                f.rc = sg_node_flow_decide_batch_host(node_, bufs_[b].first, n, bufs_[b].second);
+                if (f.rc != SG_OK) err_ = sg_node_last_error(node_);
+            } else {
+                f.rc = sg_flow_submit(h_, bufs_[b].first, n, bufs_[b].second, &f.ticket);
+                if (f.rc != SG_OK) err_ = sg_last_error(h_);
+            }
         }
         {
             std::lock_guard<std::mutex> q(qmu_);

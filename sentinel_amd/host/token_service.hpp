@@ -194,6 +194,9 @@ public:
         std::chrono::microseconds flushDelay{200};  // ... or when the oldest has waited this long
         std::function<int64_t()> clock;             // TimeUtil.currentTimeMillis (default: system clock)
         int pipelineDepth = 3;                      // micro-batches in flight on the GPU (1..3)
+        // non-empty: one token server over these shard devices (sg_node_*: flowIds hashed over the shards, routing
+        // inside the library; a device may repeat); param and concurrent tokens on the node's front handle
+        std::vector<int> shardDevices;
         int paramCapacityLog2 = 16;                 // exact (value → window) table per cluster param rule
         // observer of every decided micro-batch (requests as submitted, results, status) — tests and tracing
         std::function<void(const std::vector<sg_req>&, const std::vector<sg_result>&, int)> onBatch;
@@ -272,7 +275,8 @@ private:
     std::vector<TokenResult> decideLocked(std::vector<sg_req>& reqs);
 
     Options opt_;
-    sg_handle* h_ = nullptr;
+    sg_handle* h_ = nullptr;               // the engine, or the node's front handle (node mode)
+    sg_node* node_ = nullptr;              // node mode: the sharded flow tokens
     std::string err_;
 
     mutable std::mutex mu_;                // rules, namespaces, pending queue, engine calls
