@@ -106,4 +106,22 @@ int sg_conc_decide_batch_host(sg_handle*, const sg_conc_req* req, uint64_t n, sg
     }
     return SG_OK;
 }
+
+// node handle: a front handle (param / concurrent tokens) over the same recording flow path
+struct sg_node { sg_handle* front; };
+int sg_node_create(const sg_config* cfg, const int32_t*, uint32_t, sg_node** out) {
+    *out = new sg_node{nullptr};
+    return sg_create(cfg, &(*out)->front);
+}
+void sg_node_destroy(sg_node* nd) {
+    sg_destroy(nd->front);
+    delete nd;
+}
+const char* sg_node_last_error(const sg_node*) { return "fake node"; }
+sg_handle* sg_node_front(sg_node* nd) { return nd->front; }
+int sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n) { return sg_set_namespaces(nd->front, ns, n); }
+int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* r, uint32_t n) { return sg_load_flow_rules(nd->front, r, n); }
+int sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out) {
+    return sg_flow_decide_batch_host(nd->front, req, n, out);
+}
 }

@@ -31,6 +31,7 @@ using namespace sentinel::cluster;
 int main(int argc, char** argv) {
     const int threads = argc > 1 ? std::atoi(argv[1]) : 16;
     const int per_thread = argc > 2 ? std::atoi(argv[2]) : 20000;
+    const int shards = argc > 3 ? std::atoi(argv[3]) : 0;  // > 0: node mode over that many shards of device 0
     const int n_rules = 300;
 
     std::atomic<int64_t> calls{0};
@@ -43,6 +44,7 @@ int main(int argc, char** argv) {
     opt.flushSize = 2048;
     opt.flushDelay = std::chrono::microseconds(150);
     opt.maxBatch = 1 << 16;
+    for (int g = 0; g < shards; ++g) opt.shardDevices.push_back(0);
     // TimeUtil: advances 1 ms every 40 calls (read under the batcher's lock, so non-decreasing in arrival order)
     opt.clock = [&] { return (int64_t)1'700'000'000'000 + calls.fetch_add(1) / 40; };
     opt.onBatch = [&](const std::vector<sg_req>& rq, const std::vector<sg_result>& rs, int rc) {

@@ -14,10 +14,13 @@ EXE = os.path.join(ROOT, "build", "tests", "tsg_gpu")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("threads,per_thread", [(16, 20000), (4, 5000)])
-def test_mirror_many_threads_against_device(threads, per_thread):
+@pytest.mark.parametrize("threads,per_thread,shards", [(16, 20000, 0), (4, 5000, 0), (16, 10000, 3), (4, 5000, 1)])
+def test_mirror_many_threads_against_device(threads, per_thread, shards):
+    """shards > 0: the mirror in node mode (GpuTokenService::Options::shardDevices, sg_node_*: the flowIds hashed over
+    that many shard handles of device 0, routing inside the library; param and concurrent tokens on the node's front
+    handle) — the same replay must hold."""
     assert os.path.exists(EXE), f"{EXE} is missing: run __graft_entry__.build() (make -C tests/cpp)"
-    out = subprocess.run([EXE, str(threads), str(per_thread)], capture_output=True, text=True, timeout=240)
+    out = subprocess.run([EXE, str(threads), str(per_thread), str(shards)], capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-4000:]
     assert out.stdout.startswith("OK"), out.stdout
     n, batches = map(int, out.stdout.split()[1:3])
