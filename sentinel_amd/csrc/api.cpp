@@ -2437,9 +2437,36 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
             }
         }
     }
-    if (!err && !converged) {  // rare: the batch on one thread, from the saved rings
-        if (round > 0) HIP_TRY(h, launch_cp_saverings(c, b, sgm, 1, stream));
-        HIP_TRY(h, launch_cp_serial(c, b, stream));
+    if (!err && !converged) {  // rare: replay the groups of linked slots, each in arrival order, from the saved rings
+        CPGroups g{};
+        g.items = (uint32_t)touched;
+        g.label = h->d_cp_items;           // the re-walk flags and lists are done with
+        g.flag = h->d_cp_items + 2 * nv;
+        g.heads = h->d_cp_items + 3 * nv;
+        g.changed = h->d_cp_changed;
+        g.ent = h->d_cp_rec;               // the sorted value records are done with too
+        g.ent_count = h->d_cp_counts + 5;
+        g.head_count = h->d_cp_counts + 6;
+        g.ibits = bits_for(n);
+        g.all = round == 0 ? 1 : 0;
+        uint32_t mreq = 0;
+        HIP_TRY(h, hipMemcpyAsync(&mreq, b.mcount, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, launch_cpfb(c, b, g, 0, 0, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        for (int moved = 1; moved;) {  // labels strictly decrease: terminates
+            HIP_TRY(h, hipMemsetAsync(g.changed, 0, sizeof(int), stream));
+            HIP_TRY(h, launch_cpfb(c, b, g, 1, mreq, stream));
+            HIP_TRY(h, hipMemcpyAsync(&moved, g.changed, sizeof(int), hipMemcpyDeviceToHost, stream));
+            HIP_TRY(h, hipStreamSynchronize(stream));
+        }
+        HIP_TRY(h, hipMemsetAsync(g.ent_count, 0, 2 * sizeof(uint32_t), stream));
+        HIP_TRY(h, launch_cpfb(c, b, g, 2, mreq, stream));
+        uint32_t m = 0;
+        HIP_TRY(h, hipMemcpyAsync(&m, g.ent_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipStreamSynchronize(stream));
+        HIP_TRY(h, radix_sort_records(h->d_cp_rec, h->d_cp_rec2, m, 0, h->d_cp_hist, &g.ent_sorted, stream,
+                                      g.ibits + bits_for(touched)));
+        HIP_TRY(h, launch_cpfb(c, b, g, 3, m, stream));
     }
     h->cp_rounds = converged ? (round ? round : 1) : kMaxRounds + 1;
     HIP_TRY(h, launch_cp_finish_batch(c, stream));

@@ -215,7 +215,7 @@ hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out,
 // converges to the sequential answer (any consistent assignment is it: by induction over the requests in
 // arrival order, each one's checks see exact states); with the assumption "passes" most batches need one or two
 // rounds, and a saturated hot slot, whose checks fail, is not re-walked for the outcomes it already decided.
-// k_cp_serial (one thread, arrival order) is the fallback when the rounds run out.
+// When the rounds run out, the slots linked by multi-value requests are replayed per connected group (k_cpfb_*).
 
 namespace sg {
 
@@ -978,7 +978,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 if (pos < e && pos >= nosearch && P != INT64_MIN && !carry_ok && b.skips &&
                     thr - (double)(other + cur) / r.isec - 1.0 < 0) {
                     const int64_t Pc = P;
-                    const uint64_t pe = cp_wave_search(pos, e, [&](uint64_t q) {
+                    const uint64_t pe = gallop_search(pos, e, [&](uint64_t q) {
                         return cp_period(b, r.wl_idx, cp_dec(c, b, sg.rec_sorted[q]).i) > Pc;
                     }, lane);
                     if (pe - pos >= kCpSkipMin) {
@@ -1135,38 +1135,130 @@ __global__ void __launch_bounds__(256) k_cp_saverings(CPArgs c, CPBatch b, Batch
     }
 }
 
-// Fallback: the whole batch on one thread in arrival order (the rings are the pre-batch ones).
-__global__ void k_cp_serial(CPArgs c, CPBatch b) {
-    if (*c.err) return;
-    for (uint64_t i = 0; i < c.n; ++i) {
-        const sg_cparam_req q = c.req[i];
-        if (!cp_valid(c, q)) continue;
-        if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;
-        const CPRule r = c.rules[q.key & SG_KEY_INDEX];
-        const int64_t P = q.ts_ms / r.wl;
-        bool pass = true;
-        double rem = -1;
-        for (uint32_t v = 0; v < q.value_count && pass; ++v) {
-            const uint64_t value = c.values[q.value_begin + v];
-            const uint64_t g = cp_slot(c, r, value);
-            int64_t cur = 0;
-            const int64_t other = cp_window(c.ring + g * (uint64_t)c.stride, r.S, r.wl, P, &cur);
-            rem = cp_threshold(c, r, value) - (double)(other + cur) / r.isec - (double)q.acquire;
-            pass = rem >= 0;
-        }
-        if (pass) {
-            for (uint32_t v = 0; v < q.value_count; ++v) {
-                const uint64_t g = cp_slot(c, r, c.values[q.value_begin + v]);
-                CPBucket& bk = c.ring[g * (uint64_t)c.stride + (int)(P % r.S)];
-                if (bk.start != P * r.wl) {
-                    bk.start = P * r.wl;
-                    bk.count = 0;
-                }
-                bk.count += q.acquire;
+// ------------------------------------------------- fallback: groups of linked slots replayed in arrival order
+//
+// When the rounds run out (a chain of multi-value requests deeper than the round budget), the work items (touched
+// slots) linked by multi-value requests are grouped into connected components — min-label hooking with pointer
+// jumping, one launch pair per iteration until no label moves (labels only decrease, so a read that misses another
+// block's update in the same launch only delays convergence, and the iteration that changes nothing reads settled
+// labels) — the linked groups' rings are restored from the round-0 saves, and every group's requests are replayed on
+// one lane in arrival order: each value checked against the state before the request, all added iff all pass
+// (ClusterParamFlowChecker.java:58-80, as sequential calls). Groups run in parallel. Slots no multi-value request
+// touches were walked exactly in round 0 and keep that walk.
+
+__global__ void __launch_bounds__(256) k_cpfb_init(CPGroups g) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < g.items; t += gridDim.x * blockDim.x) {
+        g.label[t] = t;
+        g.flag[t] = 0;
+    }
+}
+
+// Every multi-value request pulls its items' labels (and the items those labels name) down to their minimum.
+__global__ void __launch_bounds__(256) k_cpfb_hook(CPArgs c, CPBatch b, CPGroups g) {
+    const uint32_t m = *b.mcount;
+    bool moved = false;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[b.mlist[x]];
+        uint32_t lo = 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < q.value_count; ++j) lo = min(lo, g.label[b.slot_item[b.pslot[q.value_begin + j]]]);
+        for (uint32_t j = 0; j < q.value_count; ++j) {
+            const uint32_t t = b.slot_item[b.pslot[q.value_begin + j]];
+            const uint32_t old = atomicMin(&g.label[t], lo);
+            if (old > lo) {
+                atomicMin(&g.label[old], lo);
+                moved = true;
             }
         }
-        if (q.value_count > 1) rem = -1;
-        cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? cp_d2i(rem) : 0);
+    }
+    if (__ballot(moved) && __lane_id() == 0) *g.changed = 1;
+}
+
+__global__ void __launch_bounds__(256) k_cpfb_jump(CPGroups g) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < g.items; t += gridDim.x * blockDim.x) {
+        uint32_t l = g.label[t];
+        for (uint32_t ll = g.label[l]; ll < l; ll = g.label[l]) l = ll;
+        atomicMin(&g.label[t], l);
+    }
+}
+
+// The groups with a multi-value request, their rings restored, and one entry {group | request} per request in them.
+__global__ void __launch_bounds__(256) k_cpfb_flag(CPArgs c, CPBatch b, CPGroups g) {
+    const uint32_t m = *b.mcount;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[b.mlist[x]];
+        g.flag[g.label[b.slot_item[b.pslot[q.value_begin]]]] = 1;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cpfb_restore(CPArgs c, CPBatch b, CPGroups g) {
+    const uint64_t work = (uint64_t)g.items * c.stride;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < work; w += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = (uint32_t)(w / c.stride);
+        if (!g.flag[g.label[t]]) continue;
+        const int x = (int)(w % c.stride);
+        c.ring[(uint64_t)b.item_slot[t] * c.stride + x] = b.save[(uint64_t)t * c.stride + x];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cpfb_entries(CPArgs c, CPBatch b, CPGroups g) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const sg_cparam_req q = c.req[i];
+        bool in = cp_valid(c, q) && !(b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST);
+        uint32_t lab = 0;
+        if (in) {
+            lab = g.label[b.slot_item[b.pslot[q.value_begin]]];
+            in = g.all || g.flag[lab] != 0;
+        }
+        const uint64_t mask = __ballot(in);
+        if (!mask) continue;
+        const int lane = (int)__lane_id();
+        uint32_t base = 0;
+        if (lane == __builtin_ctzll(mask)) base = atomicAdd(g.ent_count, (uint32_t)__popcll(mask));
+        base = (uint32_t)__shfl((int)base, __builtin_ctzll(mask), 64);
+        if (in) g.ent[base + __popcll(mask & ((1ull << lane) - 1ull))] = ((uint64_t)lab << g.ibits) | i;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cpfb_heads(CPGroups g, uint32_t m) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        const uint64_t k = g.ent_sorted[j] >> g.ibits;
+        if (j == 0 || (g.ent_sorted[j - 1] >> g.ibits) != k) g.heads[atomicAdd(g.head_count, 1u)] = j;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cpfb_replay(CPArgs c, CPBatch b, CPGroups g, uint32_t m) {
+    const uint32_t nh = *g.head_count;
+    const uint64_t imask = (1ull << g.ibits) - 1ull;
+    for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
+        uint32_t j = g.heads[h];
+        const uint64_t key = g.ent_sorted[j] >> g.ibits;
+        for (; j < m && (g.ent_sorted[j] >> g.ibits) == key; ++j) {
+            const uint64_t i = g.ent_sorted[j] & imask;
+            const sg_cparam_req q = c.req[i];
+            const CPRule r = c.rules[q.key & SG_KEY_INDEX];
+            const int64_t P = q.ts_ms / r.wl;
+            bool pass = true;
+            double rem = -1;
+            for (uint32_t v = 0; v < q.value_count && pass; ++v) {
+                const uint64_t gs = b.pslot[q.value_begin + v];
+                int64_t cur = 0;
+                const int64_t other = cp_window(c.ring + gs * (uint64_t)c.stride, r.S, r.wl, P, &cur);
+                rem = cp_threshold(c, r, c.values[q.value_begin + v]) - (double)(other + cur) / r.isec - (double)q.acquire;
+                pass = rem >= 0;
+            }
+            if (pass) {
+                for (uint32_t v = 0; v < q.value_count; ++v) {
+                    CPBucket& bk = c.ring[(uint64_t)b.pslot[q.value_begin + v] * c.stride + (int)(P % r.S)];
+                    if (bk.start != P * r.wl) {
+                        bk.start = P * r.wl;
+                        bk.count = 0;
+                    }
+                    bk.count += q.acquire;
+                }
+            }
+            if (q.value_count > 1) rem = -1;
+            cp_store(c.out, i, pass ? SG_STATUS_OK : SG_STATUS_BLOCKED, pass ? cp_d2i(rem) : 0);
+        }
     }
 }
 
@@ -1246,8 +1338,27 @@ hipError_t launch_cp_finish_batch(const CPArgs& c, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_cp_serial(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
-    hipLaunchKernelGGL(k_cp_serial, dim3(1), dim3(1), 0, stream, c, b);
+hipError_t launch_cpfb(const CPArgs& c, const CPBatch& b, const CPGroups& g, int step, uint32_t m, hipStream_t stream) {
+    switch (step) {
+        case 0:
+            hipLaunchKernelGGL(k_cpfb_init, dim3(cgrid2(g.items, 4096)), dim3(256), 0, stream, g);
+            break;
+        case 1:
+            hipLaunchKernelGGL(k_cpfb_hook, dim3(cgrid2(m, 4096)), dim3(256), 0, stream, c, b, g);
+            hipLaunchKernelGGL(k_cpfb_jump, dim3(cgrid2(g.items, 4096)), dim3(256), 0, stream, g);
+            break;
+        case 2:
+            hipLaunchKernelGGL(k_cpfb_flag, dim3(cgrid2(m, 4096)), dim3(256), 0, stream, c, b, g);
+            if (!g.all)
+                hipLaunchKernelGGL(k_cpfb_restore, dim3(cgrid2((uint64_t)g.items * c.stride, 8192)), dim3(256), 0,
+                                   stream, c, b, g);
+            hipLaunchKernelGGL(k_cpfb_entries, dim3(cgrid2(c.n, 8192)), dim3(256), 0, stream, c, b, g);
+            break;
+        default:
+            if (m == 0) break;
+            hipLaunchKernelGGL(k_cpfb_heads, dim3(cgrid2(m, 4096)), dim3(256), 0, stream, g, m);
+            hipLaunchKernelGGL(k_cpfb_replay, dim3(cgrid2(m, 4096)), dim3(256), 0, stream, c, b, g, m);
+    }
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "../../include/sentinel_gpu.h"
+#include "search_dev.h"
 
 namespace sg {
 
@@ -386,7 +387,24 @@ hipError_t launch_cp_items(const CPBatch& b, const BatchArgs& sg, uint64_t items
 hipError_t launch_cp_mlist(const CPArgs& c, const CPBatch& b, hipStream_t stream);
 hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream);
 hipError_t launch_cp_saverings(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, int restore, hipStream_t stream);
-hipError_t launch_cp_serial(const CPArgs& c, const CPBatch& b, hipStream_t stream);
+// Fallback when the fixed point's rounds run out: the work items linked by multi-value requests grouped into
+// connected components, each group's requests replayed in arrival order on one lane (cparam.hip, k_cpfb_*).
+struct CPGroups {
+    uint32_t items;        // work items (touched slots)
+    uint32_t* label;       // [items] group label (the smallest item of the group once settled)
+    uint32_t* flag;        // [items] label l names a group with a multi-value request
+    int* changed;          // a hooking launch moved a label
+    uint64_t* ent;         // [valid requests] {label : 64 - ibits | request index : ibits} of the linked groups
+    uint64_t* ent_sorted;  // the entries sorted (radix_sort_records)
+    uint32_t* ent_count;
+    uint32_t* heads;       // first entry of every group
+    uint32_t* head_count;
+    int ibits;
+    int all;               // no round ran (a zero round budget): every group is replayed, over the untouched rings
+};
+// step 0: labels; 1: one hook + jump iteration over the m multi-value requests; 2: flags, restore, entries;
+// 3: replay of the m sorted entries
+hipError_t launch_cpfb(const CPArgs& c, const CPBatch& b, const CPGroups& g, int step, uint32_t m, hipStream_t stream);
 hipError_t launch_cp_finish_batch(const CPArgs& c, hipStream_t stream);
 hipError_t launch_cp_order(const CPArgs& c, const CPBatch& b, const uint64_t* sorted, uint64_t n, hipStream_t stream);
 // The namespace limiter for a cparam batch: 100 ms period table (row 0 of a.bnd) and per-request records with the

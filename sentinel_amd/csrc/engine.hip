@@ -666,7 +666,7 @@ __device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e
                     pe = w.pc.q + 1 >= w.pc.np ? e : (uint64_t)(uint32_t)bcast32((int)pend_l, (int)w.pc.q);
                     pe = pe < after ? after : pe;
                 } else {
-                    pe = wave_search(after, e, [&](uint64_t p) {
+                    pe = gallop_search(after, e, [&](uint64_t p) {
                         return (uint32_t)((rec[p] >> a.abits) & a.imask) >= nb;
                     }, lane);
                 }
@@ -933,7 +933,7 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
             e = a.long_end ? a.long_end[item] : a.seg_end[k];
         } else {  // segment end: the first record with another flowId
             k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
-            e = wave_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
+            e = gallop_search(s + (a.short_max ? a.short_max : 1), a.n, [&](uint64_t p) {
                 return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
             }, lane);
         }

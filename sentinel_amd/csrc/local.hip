@@ -994,7 +994,7 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                 pe_qs = nd.cs.q;
                 pe_qm = nd.cm.q;
                 const uint32_t nbs = nd.cs.next_b, nbm = nd.cm.next_b;
-                pe = lwave_search(base, e_end, [&](uint64_t p) {
+                pe = gallop_search(base, e_end, [&](uint64_t p) {
                     const uint32_t idx = (uint32_t)((a.rec_sorted[p] >> a.abits) & a.imask);
                     return idx >= nbs || idx >= nbm;
                 }, lane);
@@ -1048,7 +1048,7 @@ __global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
         const uint64_t s = sg.long_list[item];
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
         if (a.rules[k].cx || (a.dyn && a.dyn[k] == a.epoch)) continue;  // k_lwalk_cx
-        const uint64_t e = lwave_search(s + 1, a.n, [&](uint64_t p) {
+        const uint64_t e = gallop_search(s + (sg.short_max ? sg.short_max : 1), a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
         lwalk_wave(a, bndp, k, s, e);

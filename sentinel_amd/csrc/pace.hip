@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
         const uint64_t s = p.long_list[w];
         const uint64_t g = p.rec_sorted[s] >> p.ibits;
         // segment end: first record of another rule (records are sorted by rule)
-        const uint64_t e = pace_wave_search(s + p.short_max, p.n, [&](uint64_t q) {
+        const uint64_t e = gallop_search(s + (p.short_max ? p.short_max : 1), p.n, [&](uint64_t q) {
             return (p.rec_sorted[q] >> p.ibits) != g;
         }, lane);
         const PaceRule r = p.rules[g];
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
             if (!__builtin_add_overflow(latest, cost_max, &top) && !__builtin_add_overflow(latest, cost1, &horizon)) {
                 horizon -= slack;
                 if (ts_at(base) < horizon) {
-                    base = pace_wave_search(base, e, [&](uint64_t q) { return ts_at(q) >= horizon; }, lane);
+                    base = gallop_search(base, e, [&](uint64_t q) { return ts_at(q) >= horizon; }, lane);
                     continue;
                 }
             }

@@ -211,7 +211,7 @@ __device__ void pwalk_wave_default(const PArgs& p, const PRule& r, int64_t tc, P
         }
         // no-refill zone: requests with t <= time + duration
         const int64_t zone_end_t = st.time + dur_ms;
-        const uint64_t z = pwave_search(pos, e, [&](uint64_t q) {
+        const uint64_t z = gallop_search(pos, e, [&](uint64_t q) {
             return p_ts(p, (uint32_t)(p.rec_sorted[q] & p.imask)) > zone_end_t;
         }, lane);
         while (pos < z) {
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(256) k_pwalk_long(PArgs p) {
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint64_t s = p.long_list[w];
         const uint64_t g = p.rec_sorted[s] >> p.gshift;
-        const uint64_t e = pwave_search(s + p.short_max, p.n, [&](uint64_t q) {
+        const uint64_t e = gallop_search(s + (p.short_max ? p.short_max : 1), p.n, [&](uint64_t q) {
             return (p.rec_sorted[q] >> p.gshift) != g;
         }, lane);
         const uint32_t ri = rule_of_slot(p, g);

@@ -161,23 +161,24 @@ def test_multi_value_heavy_fixed_point(seed, multi, flags):
 
 
 def test_serial_fallback(monkeypatch):
-    """With no fixed-point rounds allowed the batch is decided on one thread — same answers."""
+    """With no fixed-point rounds allowed every group of linked slots is replayed from the untouched rings — same
+    answers."""
     monkeypatch.setenv("SG_CP_MAX_ROUNDS", "0")
     rng = np.random.default_rng(13)
     rules = _rules(4, rng)
     eng, ora = _pair(rules)
     req, vals = _trace(rng, 4_000, 4, 10, 1_700_000_000_000, 1500, multi=0.4, zipf=1.2, bad=0.01)
     _check(eng, ora, req, vals)
-    assert eng.cparam_last_rounds() == 1  # max_rounds (0) + 1: serial
+    assert eng.cparam_last_rounds() == 1  # max_rounds (0) + 1: the group replay
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
 
 
 @pytest.mark.parametrize("max_rounds", [1, 2, 4, 5])
 def test_round_budget_inside_a_chain(monkeypatch, max_rounds):
     """Round budgets that end inside a chain of three enqueued rounds (r1 = min(round + 3, max)) and the serial
-    fallback after rounds > 0 (the saved rings restored by k_cp_saverings before k_cp_serial): a multi-value-heavy
-    trace over a few hot values needs more rounds than the budget, so the batch ends serially — same answers and
-    window sums; a batch that converges within the budget reports its rounds."""
+    fallback after rounds > 0 (the linked groups' saved rings restored, k_cpfb_restore): a multi-value-heavy trace
+    over a few hot values needs more rounds than the budget, so the groups are replayed — same answers and window
+    sums; a batch that converges within the budget reports its rounds."""
     monkeypatch.setenv("SG_CP_MAX_ROUNDS", str(max_rounds))
     rng = np.random.default_rng(40 + max_rounds)
     rules = _rules(5, rng)
@@ -193,6 +194,53 @@ def test_round_budget_inside_a_chain(monkeypatch, max_rounds):
         serial += r == max_rounds + 1
         t = int(req["ts_ms"][-1]) + 3
     assert serial > 0, "the trace should outlast the round budget"
+    _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
+
+
+def _merge(parts):
+    """Requests of several traces in one time order (stable), their value lists carried along."""
+    req = np.concatenate([r for r, _ in parts])
+    vals = [v[int(q["value_begin"]): int(q["value_begin"]) + int(q["value_count"])] for r, v in parts for q in r]
+    order = np.argsort(req["ts_ms"], kind="stable")
+    req = req[order]
+    vals = [vals[i] for i in order]
+    req["value_begin"] = np.concatenate([[0], np.cumsum(req["value_count"])[:-1]]).astype(np.uint32)
+    return req, np.concatenate(vals).astype(np.uint64)
+
+
+def _chain(L, key, t0, step_ms, v0=1 << 40):
+    """L two-value requests of rule `key`, request k over (c_k, c_k+1): under a threshold of one per window every
+    outcome depends on the previous one (they alternate), and the fixed point settles one link per round."""
+    req = np.zeros(L, abi.CPARAM_REQ_DTYPE)
+    req["ts_ms"] = t0 + step_ms * np.arange(L)
+    req["key"] = key
+    req["acquire"] = 1
+    req["value_count"] = 2
+    req["value_begin"] = 2 * np.arange(L)
+    c = np.uint64(v0) + np.arange(L + 1, dtype=np.uint64)
+    vals = np.stack([c[:-1], c[1:]], axis=1).reshape(-1)
+    return req, vals
+
+
+@pytest.mark.parametrize("L", [100, 300])
+def test_deep_chain_replays_the_linked_group(L):
+    """A multi-value dependency chain deeper than the 64-round budget among ordinary traffic: the slots the chain
+    links are replayed as one group in arrival order (k_cpfb_*), every other slot keeps its walk — same results and
+    window sums as the sequential oracle, the alternating chain outcomes included."""
+    rng = np.random.default_rng(70 + L)
+    rules = _rules(5, rng)
+    rules["count"][0] = 1
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_000
+    for b in range(2):
+        noise = _trace(rng, 40_000, 4, 400, t, 900, multi=0.1, zipf=1.1)
+        noise[0]["key"] += 1  # rules 1..4; rule 0 (threshold 1) carries the chain alone
+        req, vals = _merge([noise, _chain(L, 0, t + 50, 1, v0=(1 << 40) + 10_000 * b)])
+        want = _check(eng, ora, req, vals)
+        assert eng.cparam_last_rounds() == 65  # the budget ran out: the group fallback decided the batch
+        st = want["status"][req["key"] == 0]
+        assert (st[0::2] == abi.OK).all() and (st[1::2] == abi.BLOCKED).all()
+        t = int(req["ts_ms"][-1]) + 1
     _compare_sums(eng, ora, req, vals, int(req["ts_ms"][-1]))
 
 
