@@ -350,6 +350,8 @@ def cparam(args, dev):
     rules["count"] = rng.integers(1, 41, R)
     rules["threshold_type"] = abi.THRESHOLD_GLOBAL
     rules["sample_count"], rules["window_interval_ms"] = 10, 1000
+    if args.chain:
+        rules["count"][0] = 1
     rcdf, rperm = zipf_cdf(R, 1.0, 7)
     vcdf, vperm = zipf_cdf(V, 1.1, 8)
     rcdf_t, rperm_t = torch.from_numpy(rcdf).to(dev), torch.from_numpy(rperm.astype(np.int64)).to(dev)
@@ -362,12 +364,20 @@ def cparam(args, dev):
         key = gpu_keys(rcdf_t, rperm_t, n, gen)
         cnt = torch.where(torch.rand(n, generator=gen, device=dev) < 0.1,
                           torch.randint(2, 4, (n,), generator=gen, device=dev), torch.ones(n, dtype=torch.int64, device=dev))
+        if args.chain:  # chain link k at request k * n / L: rule 0 (threshold 1), values (c_k, c_k+1)
+            ci = torch.arange(args.chain, device=dev) * (n // args.chain)
+            key[ci] = 0
+            cnt[ci] = 2
         begin = torch.cumsum(cnt, 0) - cnt
         w[:, 1] = key | (1 << 32)                     # key, acquireCount 1
         w[:, 2] = begin | (cnt << 32)                 # value_begin, value_count
         nv = int(cnt.sum())
         owner = torch.repeat_interleave(key, cnt)
         vals = gpu_keys(vcdf_t, vperm_t, nv, gen) * 0x9E3779B1 + owner * 0x85EBCA77 + 11
+        if args.chain:
+            c = (0x5C4A << 48) + b * (args.chain + 1) + torch.arange(args.chain + 1, device=dev)
+            vals[begin[ci]] = c[:-1]
+            vals[begin[ci] + 1] = c[1:]
         return w.view(torch.uint8).reshape(-1), vals, nv
 
     batches = [batch(b) for b in range(args.warmup + args.steps)]
@@ -412,7 +422,8 @@ def cparam(args, dev):
                 "sample": f"first {m} requests of batch 0 through oracle ClusterTokenService.decide_param (1 thread), "
                           f"{dt:.1f} s"}
     return {"metric": "cluster hot-parameter token decisions/sec (ClusterParamFlowChecker), 1000 param rules",
-            "workload": "cparam: 1000 ClusterParamFlowRules x 50k values Zipf(1.1), 16M requests/batch, 10% multi-value",
+            "workload": "cparam: 1000 ClusterParamFlowRules x 50k values Zipf(1.1), 16M requests/batch, 10% multi-value"
+                        + (f", a {args.chain}-deep two-value dependency chain per batch (rule 0, threshold 1)" if args.chain else ""),
             "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
             "extra": {"fixed_point_rounds": rounds[args.warmup:], "values_per_step": nv_l},
             "data": "synthetic (GPU-generated, seeded): rules Zipf(1.0), values Zipf(1.1) per rule, 10% 2-3 values"}
@@ -427,6 +438,9 @@ def main():
     ap.add_argument("--resources", type=int, default=1_000_000)
     ap.add_argument("--cpu-events", type=int, default=4_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chain", type=int, default=0,
+                    help="cparam: embed a chain of this many two-value requests per batch, each sharing a value with "
+                         "the next under a threshold of one (adversarial: one link per fixed-point round)")
     ap.add_argument("--pmc-summary", default=None,
                     help="scripts/pmc_summary.py output of this workload's FETCH_SIZE / WRITE_SIZE passes (roofline traffic)")
     args = ap.parse_args()
