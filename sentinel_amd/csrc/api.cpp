@@ -132,6 +132,8 @@ struct sg_handle {
     uint32_t* d_cp_hist = nullptr;
     uint64_t cp_val_cap = 0;
     CPBucket* d_cp_save = nullptr;
+    CPBucket* d_cp_ckpt = nullptr;    // hot-slot ring checkpoints, one per window period of the batch
+    uint64_t cp_ckpt_cap = 0;
     uint2* d_cp_skips = nullptr;      // saturated ranges of the hot-slot walker (k_cp_skipfill), [cp_skip_cap]
     uint32_t* d_cp_skip_count = nullptr;
     uint64_t cp_skip_cap = 0;
@@ -655,6 +657,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_rec2);
     dfree(h->d_cp_hist);
     dfree(h->d_cp_save);
+    dfree(h->d_cp_ckpt);
     dfree(h->d_cp_skips);
     dfree(h->d_cp_skip_count);
     dfree(h->d_cp_changed);
@@ -2220,7 +2223,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
         dfree(h->d_cp_rec2);
         dfree(h->d_cp_hist);
         dfree(h->d_cp_items);
-        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 8 * nv) != hipSuccess ||
+        if (hipMalloc(&h->d_cp_items, sizeof(uint32_t) * 9 * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_owner, sizeof(uint32_t) * nv) != hipSuccess ||
             hipMalloc(&h->d_cp_pslot, sizeof(uint32_t) * nv) != hipSuccess || hipMalloc(&h->d_cp_chk, nv) != hipSuccess ||
             hipMalloc(&h->d_cp_rec, 8 * nv) != hipSuccess || hipMalloc(&h->d_cp_rec2, 8 * nv) != hipSuccess ||
@@ -2278,6 +2281,7 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     b.slot_item = h->d_cp_slot_item;
     b.item_end = h->d_cp_items + 6 * nv;         // [nv]
     b.item_slot = h->d_cp_items + 7 * nv;        // [nv]
+    b.dq = h->d_cp_items + 8 * nv;               // [nv]
     b.dcap = (uint32_t)nv;                       // re-walk lists: 2 buffers x {long, short} x nv
     b.mlist = h->d_cp_mlist;
     b.mcount = h->d_cp_counts + 4;
@@ -2356,9 +2360,10 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, launch_seg(sgm, stream));
     // are there multi-value requests? (then the first walk saves the touched rings for the re-walks)
-    uint32_t counts[1 + kClasses];
+    uint32_t counts[1 + kClasses], np[kMaxWl] = {};
     int err = 0, has_multi = 0;
     HIP_TRY(h, hipMemcpyAsync(counts, h->d_long_count, sizeof(counts), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(h, hipMemcpyAsync(np, b.np, sizeof(uint32_t) * b.n_wl, hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipMemcpyAsync(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipMemcpyAsync(&has_multi, h->d_cp_changed, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(h, hipStreamSynchronize(stream));
@@ -2377,6 +2382,25 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
             h->cp_save_cap = touched * h->cpstride;
         }
         b.save = h->d_cp_save;  // the first walk saves the touched rings, re-walks restore the dirty ones
+        // hot slots' ring at the opening of every window period, so a re-walk resumes at the first period a changed
+        // outcome touches (batches of <= kCkMaxPeriods periods, within a memory cap)
+        constexpr uint32_t kCkMaxPeriods = 64;
+        constexpr uint64_t kCkMaxBytes = 1ull << 30;
+        uint32_t ck_np = 0;
+        for (int w = 0; w < b.n_wl; ++w) ck_np = std::max(ck_np, np[w]);
+        const uint64_t ck = (uint64_t)counts[0] * ck_np * h->cpstride;
+        if (counts[0] > 0 && ck_np <= kCkMaxPeriods && ck * sizeof(CPBucket) <= kCkMaxBytes &&
+            !std::getenv("SG_CP_NO_CKPT")) {
+            if (ck > h->cp_ckpt_cap) {
+                dfree(h->d_cp_ckpt);
+                if (hipMalloc(&h->d_cp_ckpt, sizeof(CPBucket) * ck) != hipSuccess)
+                    return fail(h, SG_E_NOMEM, "cparam ring checkpoints");
+                h->cp_ckpt_cap = ck;
+            }
+            b.ckpt = h->d_cp_ckpt;
+            b.ck_np = ck_np;
+            HIP_TRY(h, hipMemsetAsync(b.dq, 0xFF, sizeof(uint32_t) * touched, stream));
+        }
     }
     // saturated ranges of hot slots (pieces of <= 4096 records, each >= 256: at most 2 nv / 256 + 1)
     {

@@ -815,31 +815,60 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
             eq = b.item_end[tq];
             gq = b.item_slot[tq];
         }
-        if (!cp_prologue(c, b, g, t, lane, 64)) continue;
         const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+        // rounds > 0 with checkpoints: resume at the first record of the earliest window period a changed outcome
+        // touches, from the ring as that period opened in the latest walk (the records before it saw unchanged
+        // inputs); else restore the pre-batch ring and walk the whole segment
+        uint64_t s0 = s;
+        int64_t ckq = -1;  // checkpoint to start from (batch-relative period), -1: the ring in memory
+        if (b.round > 0 && b.ckpt && r.S <= 64) {
+            if (!b.dflag[t]) continue;
+            const uint32_t q0 = b.dq[t];
+            if (q0 != 0 && q0 < b.ck_np) {
+                const int64_t P0 = cp_p0[r.wl_idx];
+                s0 = gallop_search(s, e, [&](uint64_t q) {
+                    return cp_period(b, r.wl_idx, cp_dec(c, b, sg.rec_sorted[q]).i) - P0 >= (int64_t)q0;
+                }, lane);
+                if (s0 < e) ckq = cp_period(b, r.wl_idx, cp_dec(c, b, sg.rec_sorted[s0]).i) - P0;
+                else s0 = s;
+            }
+            if (ckq < 0) {
+                const CPBucket* sv = b.save + t * (uint64_t)c.stride;
+                CPBucket* rg = c.ring + g * (uint64_t)c.stride;
+                for (int x = lane; x < c.stride; x += 64) rg[x] = sv[x];
+            }
+            if (lane == 0) {
+                b.dflag[t] = 0;
+                b.dq[t] = 0xFFFFFFFFu;
+            }
+        } else if (!cp_prologue(c, b, g, t, lane, 64)) {
+            continue;
+        }
         if (r.S > 64) {  // the ring does not fit the wave's registers
             if (lane == 0) cp_walk_serial(c, b, sg, g, s);
             continue;
         }
         const double thr = cp_threshold(c, r, c.keys[g]);
         CPBucket* ring = c.ring + g * (uint64_t)c.stride;
+        CPBucket* ck = b.ckpt ? b.ckpt + (uint64_t)t * b.ck_np * c.stride : nullptr;
+        const int64_t P0 = cp_p0[r.wl_idx];
         const int S = r.S;
         const int64_t wl = r.wl;
         int64_t bst = INT64_MIN, bcnt = 0;
         if (lane < S) {
-            const CPBucket bk = ring[lane];
+            const CPBucket bk = ckq >= 0 ? ck[(uint64_t)ckq * c.stride + lane] : ring[lane];
             bst = bk.start;
             bcnt = bk.count;
         }
         int64_t P = INT64_MIN, other = 0, cur = 0;
         uint32_t carry = kNoOwner;  // owner of the record before the current chunk
         bool carry_ok = false;      // that owner is a multi-value request whose first record here passed its check
-        uint64_t blk = s;
-        uint64_t pf = s;        // position of the records in rcn (the next block, loaded a block ahead)
-        uint64_t nosearch = s;  // a search found the saturated period ending before kCpSkipMin records: walk to there
+        uint64_t blk = s0;
+        uint64_t pf = s0;        // position of the records in rcn (the next block, loaded a block ahead)
+        uint64_t nosearch = s0;  // a search found the saturated period ending before kCpSkipMin records: walk to there
         uint64_t rcn[kCpU];
 #pragma unroll
-        for (int u = 0; u < kCpU; ++u) rcn[u] = sg.rec_sorted[min(s + (uint64_t)u * 64 + lane, e - 1)];
+        for (int u = 0; u < kCpU; ++u) rcn[u] = sg.rec_sorted[min(s0 + (uint64_t)u * 64 + lane, e - 1)];
         while (blk < e) {
             // loads of kCpU chunks at once; indices clamped to the segment (unconditional loads)
             uint64_t rc[kCpU];
@@ -914,6 +943,12 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                         if (P != INT64_MIN && lane == (int)(P % S)) {
                             bst = P * wl;
                             bcnt = cur;
+                        }
+                        if (ck && lane < S && Pf - P0 < (int64_t)b.ck_np) {  // the ring as Pf opens
+                            CPBucket o;
+                            o.start = bst;
+                            o.count = bcnt;
+                            ck[(uint64_t)(Pf - P0) * c.stride + lane] = o;
                         }
                         P = Pf;
                         const int I = (int)(P % S);
@@ -1066,9 +1101,15 @@ __global__ void __launch_bounds__(256) k_cp_combine(CPArgs c, CPBatch b) {
             // failed add nothing either way
             b.assume[i] = pass ? 1 : 0;
             *b.changed = 1;
+            // the slots' re-walks may resume at this request's window period (hot slots' ring checkpoints)
+            const CPRule r = c.rules[q.key & SG_KEY_INDEX];
+            const uint32_t qrel = (uint32_t)(q.ts_ms / r.wl - b.p0[r.wl_idx]);
             for (uint32_t j = 0; j < q.value_count; ++j) {
                 const uint64_t p = (uint64_t)q.value_begin + j;
-                if (b.chk[p]) b.dflag[b.slot_item[b.pslot[p]]] = 1u;  // listed by k_cp_relist
+                if (!b.chk[p]) continue;
+                const uint32_t t = b.slot_item[b.pslot[p]];
+                b.dflag[t] = 1u;  // listed by k_cp_relist
+                if (b.ckpt) atomicMin(&b.dq[t], qrel);
             }
         }
     }

@@ -376,6 +376,10 @@ struct CPBatch {
     uint32_t* mcount;
     int round;                // 0: first walk (saves the rings); > 0: re-walk the listed items from the saves
     int lim;                  // the namespace limiter already ran (TOO_MANY_REQUEST results stand)
+    uint32_t* dq;             // [work items] earliest window period (batch-relative) a changed outcome touches (~0: none)
+    CPBucket* ckpt;           // [long items][ck_np][stride] hot-slot ring at the opening of each window period (null:
+                              // re-walks start at the slot's first record)
+    uint32_t ck_np;
     uint2* skips;             // saturated ranges [x, y) of sorted records handed to k_cp_skipfill (null: no skipping)
     uint32_t* skip_count;     // zeroed by the host before round 0, by k_cp_relist before the next round
     uint32_t skip_cap;
