@@ -538,7 +538,7 @@ __device__ void cp_walk_serial_mem(const CPArgs& c, const CPBatch& b, const Batc
                                                   : b.bnd[(size_t)r.wl_idx * kMaxPeriods + q1])
                                       : 0xFFFFFFFFu;
         }
-        const double rem = thr - (double)(other + cur) / r.isec - (double)d.acq;
+        const double rem = thr - avg_div((double)(other + cur), r.isec) - (double)d.acq;
         if (!d.multi) {
             mi = kNoOwner;
             if (rem >= 0) {
@@ -629,7 +629,7 @@ __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const Batc
                                                   : b.bnd[(size_t)r.wl_idx * kMaxPeriods + q1])
                                       : 0xFFFFFFFFu;
         }
-        const double rem = thr - (double)(other + cur) / r.isec - (double)d.acq;
+        const double rem = thr - avg_div((double)(other + cur), r.isec) - (double)d.acq;
         if (!d.multi) {
             mi = kNoOwner;
             if (rem >= 0) {
@@ -968,7 +968,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                         const bool dead = (failed >> lane) & 1ull;
                         const int64_t a = (mine && !dead) ? add : 0;
                         const int64_t excl = cp_excl_scan(a, lane);
-                        const double rem = thr - (double)(other + cur + excl) / r.isec - (double)acq;
+                        const double rem = thr - avg_div((double)(other + cur + excl), r.isec) - (double)acq;
                         const bool ok = rem >= 0 && !dead;
                         // a dead lane adds nothing already: not a cut (else every pass would stop at one)
                         const uint64_t bad = __ballot(mine && cut_kind && !dead && !(rem >= 0));
@@ -993,7 +993,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                         cur += adv;
                         open &= ~done;
                         if (bad && open) {  // failing even at the committed state: fails for good
-                            const double lb = thr - (double)(other + cur) / r.isec - (double)acq;
+                            const double lb = thr - avg_div((double)(other + cur), r.isec) - (double)acq;
                             failed |= __ballot(((open >> lane) & 1ull) && (cut_kind || typ == kCpMulti) && lb < 0);
                         }
                     }
@@ -1011,7 +1011,7 @@ __global__ void __launch_bounds__(256) k_cp_walk2_long(CPArgs c, CPBatch b, Batc
                 // repeated values may still follow: they add)
                 const uint64_t pos = base + 64;
                 if (pos < e && pos >= nosearch && P != INT64_MIN && !carry_ok && b.skips &&
-                    thr - (double)(other + cur) / r.isec - 1.0 < 0) {
+                    thr - avg_div((double)(other + cur), r.isec) - 1.0 < 0) {
                     const int64_t Pc = P;
                     const uint64_t pe = gallop_search(pos, e, [&](uint64_t q) {
                         return cp_period(b, r.wl_idx, cp_dec(c, b, sg.rec_sorted[q]).i) > Pc;
@@ -1284,7 +1284,7 @@ __global__ void __launch_bounds__(256) k_cpfb_replay(CPArgs c, CPBatch b, CPGrou
                 const uint64_t gs = b.pslot[q.value_begin + v];
                 int64_t cur = 0;
                 const int64_t other = cp_window(c.ring + gs * (uint64_t)c.stride, r.S, r.wl, P, &cur);
-                rem = cp_threshold(c, r, c.values[q.value_begin + v]) - (double)(other + cur) / r.isec - (double)q.acquire;
+                rem = cp_threshold(c, r, c.values[q.value_begin + v]) - avg_div((double)(other + cur), r.isec) - (double)q.acquire;
                 pass = rem >= 0;
             }
             if (pass) {

@@ -39,11 +39,8 @@ __device__ __forceinline__ int32_t java_d2i(double x) {
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
-// LeapArray sum / intervalInSecond (ClusterMetric.getAvg, ClusterMetric.java:70-72). x / 1.0 == x exactly,
-// so the common 1000 ms interval skips the fp64 division.
-__device__ __forceinline__ double qps_of(int64_t sum, double isec) {
-    return isec == 1.0 ? (double)sum : (double)sum / isec;
-}
+// LeapArray sum / intervalInSecond (ClusterMetric.getAvg, ClusterMetric.java:70-72)
+__device__ __forceinline__ double qps_of(int64_t sum, double isec) { return avg_div((double)sum, isec); }
 
 __device__ __forceinline__ int64_t wave_sum(int64_t v) {
 #pragma unroll
@@ -247,6 +244,18 @@ __shared__ uint32_t g_boff[kMaxWl];  // offset of window length w's table in g_s
 __shared__ int g_blds;               // 1: tables in g_sbnd, 0: read from a.bnd
 __shared__ int64_t g_p0[kMaxWl];     // a.p0 / a.np staged by stage_periods: per-lane reads of these tiny tables
 __shared__ uint32_t g_np[kMaxWl];    // (indexed by the rule's window length) were each a memory round trip
+constexpr int kModS = 64;
+__shared__ uint8_t g_p0mod[kMaxWl][kModS + 1];  // g_p0[w] mod s (s = 1..kModS), staged by stage_periods
+constexpr int kCoarseN = 4096;
+__shared__ uint16_t g_coarse[kCoarseN];  // period of the first request of each 2^g_cshift-request chunk (one window
+__shared__ int g_cshift;                 // length, tables in LDS); g_cshift -1: not staged
+
+// Ring slot of the batch's window period q (period P0 + q of window length w) for sampleCount S: (P0 + q) % S in
+// 32 bits from the staged residue (a 64-bit modulo of the absolute period is ~120 instructions).
+__device__ __forceinline__ int period_slot(int w, uint32_t q, int S) {
+    if (S <= kModS) return (int)(((uint32_t)g_p0mod[w][S] + q) % (uint32_t)S);
+    return (int)((g_p0[w] + (int64_t)q) % S);
+}
 
 // Period tracking shared by the walkers: requests of one flowId arrive in index order, so the
 // window period only moves forward; the cached boundary of the next period answers most lookups.
@@ -278,6 +287,14 @@ struct PeriodCursor {
     // period of a request index >= every index seen so far: the largest p with table[p] <= idx
     __device__ __forceinline__ uint32_t of(uint32_t idx) const {
         if (q != 0xFFFFFFFFu && idx < next_b) return q;
+        if constexpr (L) {
+            const int sh = g_cshift;
+            if (sh >= 0) {  // from the chunk's period: a chunk spans a boundary or two at most in practice
+                uint32_t p = g_coarse[idx >> sh];
+                while (p + 1 < np && at(p + 1) <= idx) ++p;
+                return p;
+            }
+        }
         uint32_t lo = 0, hi = np;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -452,7 +469,7 @@ struct WaveWalker {
         pc.seek(q);
         const int64_t P = P0 + (int64_t)q;
         const int S = R.S;
-        I = (int)(P % S);
+        I = period_slot(R.wl_idx, q, S);
         ws = P * R.wl;
         int64_t cI[SG_NUM_EVENTS];
 #pragma unroll
@@ -462,7 +479,7 @@ struct WaveWalker {
         const bool valid = lane < S && lane != I && st != INT64_MIN && st >= lo;
         ps.wo_pass = wave_sum(valid ? c[SG_EV_PASS] : 0);
         ps.wo_wait = wave_sum(valid ? c[SG_EV_WAITING] : 0);
-        const int h = (int)((P + 1) % S);
+        const int h = I + 1 == S ? 0 : I + 1;
         ps.head_other = (h != I) ? bcast64(valid ? c[SG_EV_PASS] : 0, h) : 0;
     }
 
@@ -911,7 +928,30 @@ __device__ __forceinline__ void stage_periods(const BatchArgs& a) {
         g_p0[threadIdx.x] = a.p0[threadIdx.x];
         g_np[threadIdx.x] = a.np[threadIdx.x];
     }
+    for (uint32_t x = threadIdx.x; x < (uint32_t)a.n_wl * (kModS + 1); x += blockDim.x) {
+        const uint32_t w = x / (kModS + 1), m = x % (kModS + 1);
+        g_p0mod[w][m] = m ? (uint8_t)(a.p0[w] % (int64_t)m) : (uint8_t)0;  // p0 >= 0: timestamps are
+    }
+    // one window length with its table in LDS: the period of the first request of every 2^shift-request chunk
+    int shift = 0;
+    while (((uint64_t)kCoarseN << shift) < a.n) ++shift;
+    const bool coarse = lds && a.n_wl == 1 && shift < 32;
+    if (threadIdx.x == 0) g_cshift = coarse ? shift : -1;
     __syncthreads();
+    if (coarse) {
+        const uint32_t npw = a.np[0], nch = (uint32_t)((a.n + (1ull << shift) - 1) >> shift);
+        for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+            const uint32_t idx = c << shift;
+            uint32_t lo = 0, hi = npw;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (g_sbnd[mid] <= idx) lo = mid;
+                else hi = mid;
+            }
+            g_coarse[c] = (uint16_t)lo;
+        }
+        __syncthreads();
+    }
 }
 
 // Long-segment walker: one wave per segment of more than short_max records (grid-stride over the list,
@@ -998,6 +1038,12 @@ struct SlotSnap {
     int32_t st, pass, wait;
 };
 constexpr int32_t kSnapOld = -(1 << 30);
+
+// A relative bound clamped to 32 bits: compares with snapshot starts as the 64-bit one (an empty slot, INT32_MIN,
+// holds no counts either way).
+__device__ __forceinline__ int32_t rel32(int64_t x) {
+    return x > (int64_t)INT32_MAX ? INT32_MAX : x < (int64_t)INT32_MIN ? INT32_MIN : (int32_t)x;
+}
 
 __device__ __forceinline__ int32_t snap_rel(int64_t start, int64_t T0) {
     if (start == INT64_MIN) return INT32_MIN;
@@ -1110,10 +1156,11 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
             const uint32_t qprev = pc.q;
             pc.seek(qn);
             const int64_t P = P0 + (int64_t)qn;
-            I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
+            I = I < 0 ? period_slot(R.wl_idx, qn, S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
             ws = P * wl;
             // LeapArray.isWindowDeprecated: valid iff start > ws - S*wl (compared relative to T0)
             const int64_t lo_rel = ws - (int64_t)S * wl - T0;
+            const int32_t lo32 = rel32(lo_rel);  // snapshot starts are 32-bit (snap_rel)
             const int h = I + 1 == S ? 0 : I + 1;
             // all slots read at once, then summed branch-free; sums of valid buckets are window sums, < 2^30
             // under BatchArgs::narrow, so 32-bit accumulation is exact
@@ -1127,7 +1174,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
             uint32_t wp = 0, ww = 0, ho = 0;
 #pragma unroll
             for (int x = 0; x < SM; ++x) {
-                const bool v = (x < S) & (x != I) & ((int64_t)sx[x] > lo_rel);
+                const bool v = (x < S) & (x != I) & (sx[x] > lo32);
                 const uint32_t m = v ? 0xFFFFFFFFu : 0u;
                 wp += (uint32_t)px[x] & m;
                 ww += (uint32_t)wx[x] & m;
@@ -1272,9 +1319,10 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
             const uint32_t qprev = pc.q;
             pc.seek(qn);
             const int64_t P = P0 + (int64_t)qn;
-            I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
+            I = I < 0 ? period_slot(R.wl_idx, qn, S) : (int)((uint32_t)(I + (int)(qn - qprev)) % (uint32_t)S);
             ws = P * wl;
             const int64_t lo_rel = ws - (int64_t)S * wl - T0;
+            const int32_t lo32 = rel32(lo_rel);  // snapshot starts are 32-bit (snap_rel)
             const int h = I + 1 == S ? 0 : I + 1;
             int32_t sx[SM], px[SM], wx[SM];
 #pragma unroll
@@ -1286,7 +1334,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
             uint32_t wp = 0, ww = 0, ho = 0;
 #pragma unroll
             for (int x = 0; x < SM; ++x) {
-                const bool v = (x < S) & (x != I) & ((int64_t)sx[x] > lo_rel);
+                const bool v = (x < S) & (x != I) & (sx[x] > lo32);
                 const uint32_t m = v ? 0xFFFFFFFFu : 0u;
                 wp += (uint32_t)px[x] & m;
                 ww += (uint32_t)wx[x] & m;
@@ -1649,15 +1697,16 @@ __device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
                 const uint32_t qprev = pc.q;
                 pc.seek(q);
                 const int64_t P = P0 + (int64_t)q;
-                I = I < 0 ? (int)(P % S) : (int)((uint32_t)(I + (int)(q - qprev)) % (uint32_t)S);
+                I = I < 0 ? period_slot(R.wl_idx, q, S) : (int)((uint32_t)(I + (int)(q - qprev)) % (uint32_t)S);
                 ws = P * R.wl;
                 const int64_t lo_rel = ws - (int64_t)S * R.wl - T0;  // valid iff start > ws - S * wl
+                const int32_t lo32 = rel32(lo_rel);  // snapshot starts are 32-bit (snap_rel)
                 const int h = I + 1 == S ? 0 : I + 1;
                 uint32_t wp = 0, ww = 0, ho = 0;
                 int32_t stI_rel = INT32_MIN;
 #pragma unroll
                 for (int x = 0; x < SM; ++x) {
-                    const bool v = (x < S) & (x != I) & ((int64_t)st[x] > lo_rel);
+                    const bool v = (x < S) & (x != I) & (st[x] > lo32);
                     const uint32_t mk = v ? 0xFFFFFFFFu : 0u;
                     wp += (uint32_t)pa[x] & mk;
                     ww += (uint32_t)wa[x] & mk;

@@ -29,9 +29,7 @@ __device__ __forceinline__ int32_t java_d2i(double x) {  // JLS §5.1.3
     return (int32_t)x;
 }
 
-__device__ __forceinline__ double qps_of(int64_t sum, double isec) {
-    return isec == 1.0 ? (double)sum : (double)sum / isec;
-}
+__device__ __forceinline__ double qps_of(int64_t sum, double isec) { return avg_div((double)sum, isec); }
 
 __device__ __forceinline__ int64_t wave_sum(int64_t v) {
 #pragma unroll
@@ -1145,7 +1143,7 @@ __device__ bool emb_lim_try_pass(LimRing* r, int64_t t, double qps) {
     return true;
 }
 
-__device__ __forceinline__ double c3_qps(int64_t sum, double isec) { return isec == 1.0 ? (double)sum : (double)sum / isec; }
+__device__ __forceinline__ double c3_qps(int64_t sum, double isec) { return avg_div((double)sum, isec); }
 
 // DefaultTokenService.requestToken (DefaultTokenService.java:39-50) → ClusterFlowChecker.acquireClusterToken
 // (ClusterFlowChecker.java:55-112) for one request at time t, on the flowId's ClusterMetric ring in HBM

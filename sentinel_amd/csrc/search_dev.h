@@ -1,4 +1,5 @@
-// search_dev.h — wave-wide searches over the sorted records, shared by the walkers.
+// search_dev.h — device helpers shared by the walkers: wave-wide searches over the sorted records, the window
+// average's division.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,6 +44,18 @@ __device__ __forceinline__ uint64_t gallop_search(uint64_t lo, uint64_t hi, Pred
     const uint64_t b0 = lo + (1ull << (f - 1));            // probe f - 1 (at b0 - 1) was false
     const uint64_t b1 = lo + ((1ull << f) - 1ull);          // probe f: true, or past hi
     return search64(b0, b1 < hi ? b1 : hi, pred, lane);
+}
+
+// sum / intervalInSecond (LeapArray averages: ClusterMetric.getAvg, StatisticNode.passQps, …) as Java computes it.
+// For a power-of-two interval (1 s, 2 s, 0.5 s, …) the quotient is the product with the exact reciprocal, built from
+// the exponent bits; the fp64 division sequence (~13 instructions a record on the walkers' hot path) runs only
+// for other intervals. (A test for isec == 1.0 alone is folded away by the compiler: x / 1.0 == x.)
+__device__ __forceinline__ double avg_div(double x, double isec) {
+    const uint64_t b = (uint64_t)__double_as_longlong(isec);
+    const uint64_t e = (b >> 52) & 0x7FF;
+    if ((b & 0x800FFFFFFFFFFFFFull) == 0 && e - 1 < 0x7FD)
+        return x * __longlong_as_double((long long)((0x7FEull - e) << 52));
+    return x / isec;
 }
 
 }  // namespace sg
