@@ -31,4 +31,10 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
   step pmc_size 120 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum -d gpurun_out/pmc_size -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
   step pmc_summary 60 python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_summary.json gpurun_out/pmc_size
 fi
+if [ "$MODE" = sq ]; then
+  # two passes of 8 SQ counters (one block's limit per pass)
+  step sq1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/sq1 -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
+  step sq2 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_FLAT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT -d gpurun_out/sq2 -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-batches 0
+  step sq_summary 60 python scripts/sq_summary.py gpurun_out/sq_summary.json 0 gpurun_out/sq1 gpurun_out/sq2
+fi
 echo done

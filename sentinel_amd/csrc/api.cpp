@@ -2464,9 +2464,9 @@ int cparam_batch(sg_handle* h, const sg_cparam_req* req, uint64_t n, const uint6
     if (!err && !converged) {  // rare: replay the groups of linked slots, each in arrival order, from the saved rings
         CPGroups g{};
         g.items = (uint32_t)touched;
-        g.label = h->d_cp_items;           // the re-walk flags and lists are done with
-        g.flag = h->d_cp_items + 2 * nv;
-        g.heads = h->d_cp_items + 3 * nv;
+        g.label = h->d_cp_items + 2 * nv;  // the re-walk lists are done with (the flags [0, nv) mark moving groups)
+        g.flag = h->d_cp_items + 3 * nv;
+        g.heads = h->d_cp_items + 4 * nv;
         g.changed = h->d_cp_changed;
         g.ent = h->d_cp_rec;               // the sorted value records are done with too
         g.ent_count = h->d_cp_counts + 5;

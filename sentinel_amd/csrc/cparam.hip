@@ -1182,10 +1182,10 @@ __global__ void __launch_bounds__(256) k_cp_saverings(CPArgs c, CPBatch b, Batch
 // slots) linked by multi-value requests are grouped into connected components — min-label hooking with pointer
 // jumping, one launch pair per iteration until no label moves (labels only decrease, so a read that misses another
 // block's update in the same launch only delays convergence, and the iteration that changes nothing reads settled
-// labels) — the linked groups' rings are restored from the round-0 saves, and every group's requests are replayed on
-// one lane in arrival order: each value checked against the state before the request, all added iff all pass
-// (ClusterParamFlowChecker.java:58-80, as sequential calls). Groups run in parallel. Slots no multi-value request
-// touches were walked exactly in round 0 and keep that walk.
+// labels) — the groups the last round still changed get their rings restored from the round-0 saves, and each of
+// their requests is replayed on one lane per group in arrival order: each value checked against the state before the
+// request, all added iff all pass (ClusterParamFlowChecker.java:58-80, as sequential calls). Groups run in parallel;
+// settled groups (and slots no multi-value request touches) keep their walks.
 
 __global__ void __launch_bounds__(256) k_cpfb_init(CPGroups g) {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < g.items; t += gridDim.x * blockDim.x) {
@@ -1222,13 +1222,13 @@ __global__ void __launch_bounds__(256) k_cpfb_jump(CPGroups g) {
     }
 }
 
-// The groups with a multi-value request, their rings restored, and one entry {group | request} per request in them.
-__global__ void __launch_bounds__(256) k_cpfb_flag(CPArgs c, CPBatch b, CPGroups g) {
-    const uint32_t m = *b.mcount;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
-        const sg_cparam_req q = c.req[b.mlist[x]];
-        g.flag[g.label[b.slot_item[b.pslot[q.value_begin]]]] = 1;
-    }
+// The groups still moving — an item listed for a re-walk by the last round (an outcome of the group changed and
+// changes an add) — their rings restored, and one entry {group | request} per request in them. A group whose
+// outcomes the last round left unchanged holds a consistent assignment, which is the sequential answer (every
+// request's checks then see exact states, by induction in arrival order), and keeps its walk.
+__global__ void __launch_bounds__(256) k_cpfb_flag(CPBatch b, CPGroups g) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < g.items; t += gridDim.x * blockDim.x)
+        if (b.dflag[t]) g.flag[g.label[t]] = 1;
 }
 
 __global__ void __launch_bounds__(256) k_cpfb_restore(CPArgs c, CPBatch b, CPGroups g) {
@@ -1389,7 +1389,7 @@ hipError_t launch_cpfb(const CPArgs& c, const CPBatch& b, const CPGroups& g, int
             hipLaunchKernelGGL(k_cpfb_jump, dim3(cgrid2(g.items, 4096)), dim3(256), 0, stream, g);
             break;
         case 2:
-            hipLaunchKernelGGL(k_cpfb_flag, dim3(cgrid2(m, 4096)), dim3(256), 0, stream, c, b, g);
+            if (!g.all) hipLaunchKernelGGL(k_cpfb_flag, dim3(cgrid2(g.items, 4096)), dim3(256), 0, stream, b, g);
             if (!g.all)
                 hipLaunchKernelGGL(k_cpfb_restore, dim3(cgrid2((uint64_t)g.items * c.stride, 8192)), dim3(256), 0,
                                    stream, c, b, g);

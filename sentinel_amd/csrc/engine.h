@@ -396,7 +396,7 @@ hipError_t launch_cp_saverings(const CPArgs& c, const CPBatch& b, const BatchArg
 struct CPGroups {
     uint32_t items;        // work items (touched slots)
     uint32_t* label;       // [items] group label (the smallest item of the group once settled)
-    uint32_t* flag;        // [items] label l names a group with a multi-value request
+    uint32_t* flag;        // [items] label l names a group the last round still changed
     int* changed;          // a hooking launch moved a label
     uint64_t* ent;         // [valid requests] {label : 64 - ibits | request index : ibits} of the linked groups
     uint64_t* ent_sorted;  // the entries sorted (radix_sort_records)
