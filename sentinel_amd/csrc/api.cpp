@@ -1239,6 +1239,11 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(a.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, hipMemsetAsync(a.skip_count, 0, sizeof(uint32_t), stream));
+    a.csum0 = nullptr;
+    if (a.hist0 && radix_csum_atomic()) {
+        a.csum0 = radix_csum(a.hist0, a.n, a.hist0_bits);
+        HIP_TRY(h, hipMemsetAsync(a.csum0, 0, radix_csum_bytes(a.n, a.hist0_bits), stream));
+    }
     HIP_TRY(h, launch_prep(a, stream));
     const int lrc = flow_limiter(h, a, stream);
     if (lrc) return lrc;
@@ -1249,7 +1254,7 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
         const SegMark mk{a.seg_start, a.seg_end, a.K, a.kshift};
         a.seg_marked = (a.seg_start && a.seg_end && a.long_end && !h->seg_mark_pass) ? 1 : 0;
         HIP_TRY(h, radix_sort_records(a.rec, a.rec_sorted, a.n, a.kshift, hist, &sorted, stream, 64, a.hist0 != nullptr,
-                                      a.seg_marked ? &mk : nullptr));
+                                      a.seg_marked ? &mk : nullptr, a.csum0 != nullptr));
         a.rec_sorted = sorted;
         if (a.rec == h->d_rec) h->last_sorted = sorted;
     }

@@ -68,6 +68,7 @@ struct BatchArgs {
     uint64_t n;
     uint64_t* rec;       // packed records, request order
     uint32_t* hist0;     // k_prep: per-tile histogram of the first sort digit (radix_hist layout), or nullptr
+    uint32_t* csum0;     // k_prep also adds each tile's counts to its chunk's column sums (radix_csum), or nullptr
     int hist0_bits;      // width of that digit (radix_digit_bits of the key width)
     uint64_t* rec_sorted;
     // record layout: [key : kbits][0 …][idx : ibits][acode : abits], acode = acquire << 1 | prio, abits <= 8;
@@ -703,6 +704,15 @@ uint64_t route_tiles(uint64_t n);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 int radix_digit_bits(int bits);  // digit width radix_sort_records uses for `bits` key bits (8 or 10)
+#ifndef SG_CHUNK_TILES
+#define SG_CHUNK_TILES 32
+#endif
+constexpr uint32_t kChunkTiles = SG_CHUNK_TILES;  // sort tiles per column-sum chunk (sort.hip)
+// Column sums by atomics in the histogram kernels (k_prep, k_radix_hist) instead of a k_colsum pass over the rows:
+// one dependent launch fewer per sort pass (env SG_CSUM_ATOMIC=0: the k_colsum pass).
+bool radix_csum_atomic();
+uint32_t* radix_csum(uint32_t* hist_ws, uint64_t n, int D);   // the chunk column sums' place in hist_ws
+size_t radix_csum_bytes(uint64_t n, int D);
 // Segment marks of a flowId-keyed sort's last pass (seg_start atomicMin / seg_end atomicMax per key, see sort.hip)
 struct SegMark {
     uint32_t* seg_start;
@@ -712,7 +722,7 @@ struct SegMark {
 };
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false,
-                              const SegMark* mark = nullptr);
+                              const SegMark* mark = nullptr, bool first_csum_ready = false);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with

@@ -173,6 +173,11 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
     if (a.hist0) {
         __syncthreads();
         for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)blockIdx.x * (dmask + 1) + d] = dcnt[d];
+        if (a.csum0) {  // the chunk's column sums (zeroed before the launch): no k_colsum pass for the first digit
+            uint32_t* cs = a.csum0 + (size_t)(blockIdx.x / kChunkTiles) * (dmask + 1);
+            for (uint32_t d = threadIdx.x; d <= dmask; d += 256)
+                if (dcnt[d]) atomicAdd(cs + d, dcnt[d]);
+        }
     }
 }
 

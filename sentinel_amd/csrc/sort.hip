@@ -18,6 +18,7 @@
 // Stability: waves in index order within a tile, rounds then lanes within a wave.
 #include "engine.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace sg {
@@ -51,7 +52,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t ntiles) {
 
 template <int D>
 __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in, uint64_t n, int shift, uint32_t* hist,
-                                                             uint32_t ntiles) {
+                                                             uint32_t ntiles, uint32_t* csum) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;
     __shared__ uint32_t cnt[kBins];
@@ -72,6 +73,14 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in,
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kPer; ++i) hist[(size_t)blockIdx.x * kBins + tid + i * kSortThreads] = cnt[tid + i * kSortThreads];
+    if (csum) {  // the chunk's column sums (zeroed before the launch)
+        uint32_t* cs = csum + (size_t)(blockIdx.x / kChunkTiles) * kBins;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const uint32_t v = cnt[tid + i * kSortThreads];
+            if (v) atomicAdd(cs + tid + i * kSortThreads, v);
+        }
+    }
 }
 
 // The per-tile histograms are stored tile-major (hist[t][d]: each tile writes and reads one contiguous row); the
@@ -84,10 +93,6 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_hist(const uint64_t* in,
 //               and each digit's total (tot[d]);
 //   k_rescan    one thread per (chunk, digit): each tile's run start (column-relative) written over its row;
 //   k_radix_scatter adds each digit's base, an exclusive scan of the totals it does in LDS.
-#ifndef SG_CHUNK_TILES
-#define SG_CHUNK_TILES 32
-#endif
-constexpr uint32_t kChunkTiles = SG_CHUNK_TILES;
 constexpr int kScanGroups = 16;  // chunk groups per digit in k_chunkscan
 constexpr int kScanLoads = 8;    // chunk sums per thread loaded at once (nchunks <= 128: 16M-record batches)
 
@@ -305,6 +310,23 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     }
 }
 
+bool radix_csum_atomic() {
+    static const bool on = [] {
+        const char* e = std::getenv("SG_CSUM_ATOMIC");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
+uint32_t* radix_csum(uint32_t* hist_ws, uint64_t n, int D) {
+    return hist_ws + (size_t)((n + kTile - 1) / kTile) * (1u << D);
+}
+
+size_t radix_csum_bytes(uint64_t n, int D) {
+    const uint64_t ntiles = (n + kTile - 1) / kTile;
+    return sizeof(uint32_t) * (size_t)((ntiles + kChunkTiles - 1) / kChunkTiles) * (1u << D);
+}
+
 size_t radix_hist_words(uint64_t n) {
     const uint64_t ntiles = (n + kTile - 1) / kTile;
     const uint64_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
@@ -317,15 +339,20 @@ int radix_digit_bits(int bits) { return ((bits > 16 && bits <= 20) || (bits > 24
 
 template <int D>
 static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
-                       bool hist_ready, const SegMark* mark) {
+                       bool hist_ready, const SegMark* mark, bool csum_ready) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     uint32_t* hist = hist_ws;                                   // [ntiles][bins], then run offsets in place
     uint32_t* csum = hist_ws + (size_t)ntiles * (1u << D);       // [nchunks][bins]
     uint32_t* tot = csum + (size_t)nchunks * (1u << D);          // [bins]
-    if (!hist_ready)
-        hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles);
-    hipLaunchKernelGGL(k_colsum<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, ntiles, csum);
+    if (!hist_ready) {
+        const bool atom = radix_csum_atomic();
+        if (atom) hipMemsetAsync(csum, 0, radix_csum_bytes(n, D), stream);
+        hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles,
+                           atom ? csum : nullptr);
+        csum_ready = atom;
+    }
+    if (!csum_ready) hipLaunchKernelGGL(k_colsum<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, ntiles, csum);
     hipLaunchKernelGGL(k_chunkscan<D>, dim3((1u << D) / 64), dim3(1024), 0, stream, csum, nchunks, tot);
     hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, csum, ntiles);
     const uint32_t grid = 8 * ((ntiles + 7) / 8);  // xcd_tile: blocks past ntiles return at once
@@ -342,15 +369,16 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
 // first_hist_ready: the first pass's per-tile histogram (radix_digit_bits wide) is already in hist_ws (k_prep).
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit, bool first_hist_ready,
-                              const SegMark* mark) {
+                              const SegMark* mark, bool first_csum_ready) {
     uint64_t* src = a;
     uint64_t* dst = b;
     const int D = radix_digit_bits(hi_bit - lo_bit);
     for (int shift = lo_bit; shift < hi_bit && n > 0; shift += D) {
         const bool ready = shift == lo_bit && first_hist_ready;
         const SegMark* mk = shift + D >= hi_bit ? mark : nullptr;  // the last pass marks the segments
-        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready, mk);
-        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready, mk);
+        const bool cready = ready && first_csum_ready;
+        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready, mk, cready);
+        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready, mk, cready);
         uint64_t* t = src;
         src = dst;
         dst = t;
