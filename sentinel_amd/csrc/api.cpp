@@ -290,6 +290,8 @@ struct sg_handle {
     FlowWs pws{};
     uint32_t pws_segcap = 0;
     hipStream_t s_front = nullptr, s_back = nullptr, s_aux2 = nullptr;
+    hipStream_t s_aux3 = nullptr;     // the length-class-0 walker beside the other two (SG_DEBUG & 128, tuning)
+    hipEvent_t tjoin = nullptr;
     hipStream_t s_xcopy = nullptr;    // the sharded limiter exchange's copy into a pipeline workspace
     hipEvent_t xcopy_done = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
@@ -555,13 +557,14 @@ void sg_destroy(sg_handle* h) {
         dfree(w.skips);
         dfree(w.skip_count);
         dfree(w.seg_end);
-        for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2, &h->s_xcopy})
+        for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2, &h->s_aux3, &h->s_xcopy})
             if (*st) (void)hipStreamDestroy(*st);
         if (h->xcopy_done) (void)hipEventDestroy(h->xcopy_done);
         for (int x = 0; x < 2; ++x) {
             if (h->front_done[x]) (void)hipEventDestroy(h->front_done[x]);
             if (h->back_done[x]) (void)hipEventDestroy(h->back_done[x]);
         }
+        if (h->tjoin) (void)hipEventDestroy(h->tjoin);
         if (h->pfork) (void)hipEventDestroy(h->pfork);
         if (h->pjoin) (void)hipEventDestroy(h->pjoin);
         for (auto& d : h->dev) {
@@ -1122,12 +1125,15 @@ int pipe_setup(sg_handle* h) {
             HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_front, (uint32_t)fm.size(), fm.data()));
             HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_back, (uint32_t)bm.size(), bm.data()));
             HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_aux2, (uint32_t)bm.size(), bm.data()));
+            HIP_TRY(h, hipExtStreamCreateWithCUMask(&h->s_aux3, (uint32_t)bm.size(), bm.data()));
             h->walk_cus = nb;
         } else {
             HIP_TRY(h, hipStreamCreateWithFlags(&h->s_front, hipStreamNonBlocking));
             HIP_TRY(h, hipStreamCreateWithFlags(&h->s_back, hipStreamNonBlocking));
             HIP_TRY(h, hipStreamCreateWithFlags(&h->s_aux2, hipStreamNonBlocking));
+            HIP_TRY(h, hipStreamCreateWithFlags(&h->s_aux3, hipStreamNonBlocking));
         }
+        HIP_TRY(h, hipEventCreateWithFlags(&h->tjoin, hipEventDisableTiming));
         for (int x = 0; x < 2; ++x) {
             HIP_TRY(h, hipEventCreateWithFlags(&h->front_done[x], hipEventDisableTiming));
             HIP_TRY(h, hipEventCreateWithFlags(&h->back_done[x], hipEventDisableTiming));
@@ -1277,10 +1283,19 @@ int flow_back(sg_handle* h, const BatchArgs& a, hipStream_t stream, hipStream_t 
         HIP_TRY(h, hipEventRecord(fork, stream));
         HIP_TRY(h, hipStreamWaitEvent(aux, fork, 0));
         HIP_TRY(h, launch_walk_long(a, aux));
+        // the length-class-0 walker on a third stream beside the other two (pipelined flow path), else after the
+        // short walker
+        const bool third = a.tiny && aux == h->s_aux2 && h->s_aux3;
+        if (third) {
+            HIP_TRY(h, hipStreamWaitEvent(h->s_aux3, fork, 0));
+            HIP_TRY(h, launch_walk_tiny(a, h->s_aux3));
+            HIP_TRY(h, hipEventRecord(h->tjoin, h->s_aux3));
+        }
         HIP_TRY(h, launch_walk_short(a, stream));
-        HIP_TRY(h, launch_walk_tiny(a, stream));
+        if (!third) HIP_TRY(h, launch_walk_tiny(a, stream));
         HIP_TRY(h, hipEventRecord(join, aux));
         HIP_TRY(h, hipStreamWaitEvent(stream, join, 0));
+        if (third) HIP_TRY(h, hipStreamWaitEvent(stream, h->tjoin, 0));
     }
     HIP_TRY(h, launch_skip_apply(a, stream));
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
