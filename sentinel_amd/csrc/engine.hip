@@ -645,8 +645,16 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
     return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
+#ifndef SG_WAVE_INLINE
+#define SG_WAVE_INLINE 0
+#endif
+#if SG_WAVE_INLINE
+#define SG_WAVE_ATTR __device__ __forceinline__
+#else
+#define SG_WAVE_ATTR __device__ __noinline__  // (tuning: SG_WAVE_INLINE=1 inlines it into k_walk_long)
+#endif
 template <bool L>
-__device__ void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e, uint32_t item) {
+SG_WAVE_ATTR void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e, uint32_t item) {
     WaveWalker<L> w(a, k);
     const int lane = w.lane;
     // period ends of this segment from k_long_bounds: lane q holds the first position of period q + 1

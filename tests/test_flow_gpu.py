@@ -117,6 +117,8 @@ def test_cluster_flow_checker_occupy_pass_gpu(t0, flags):
     (40, 30_000, 1.1, 0.2, 3, 1500),
     (40, 30_000, 1.1, 0.2, 5, 25),
     (40, 30_000, 1.1, 0.2, 60, 60000),
+    (40, 30_000, 1.1, 0.2, 4, 2000),   # power-of-two intervals other than 1 s: the average's exact-reciprocal path
+    (40, 30_000, 1.1, 0.2, 2, 500),
 ])
 @pytest.mark.parametrize("flags", WALKERS)
 def test_random_traces_match_oracle(n_keys, n, zipf, prio, S, interval, flags):
