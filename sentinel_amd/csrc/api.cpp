@@ -308,7 +308,9 @@ struct sg_handle {
     };
     DevTicket dev[kDevSlots];
     bool front_only = false;          // a node handle's front (validation + namespace limiter): no flow state
-    bool seg_mark_pass = false;       // env SG_SEG_MARK=1: k_seg_mark over the sorted records (A/B of the fused marks)
+    // k_seg_mark over the sorted records (default), or the marks fused into the last scatter pass (env SG_SEG_MARK=0:
+    // its ~20M atomicMin/Max per 16M-record batch cost more than the separate read — 0.97 vs 0.91 ms/step, same box)
+    bool seg_mark_pass = true;
 };
 
 namespace {
@@ -1256,7 +1258,7 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
-        // the last pass also marks each flowId's segment (env SG_SEG_MARK=1: the separate k_seg_mark pass instead)
+        // segment marks: k_seg_mark after the sort, or (SG_SEG_MARK=0) fused into the last scatter pass
         const SegMark mk{a.seg_start, a.seg_end, a.K, a.kshift};
         a.seg_marked = (a.seg_start && a.seg_end && a.long_end && !h->seg_mark_pass) ? 1 : 0;
         HIP_TRY(h, radix_sort_records(a.rec, a.rec_sorted, a.n, a.kshift, hist, &sorted, stream, 64, a.hist0 != nullptr,

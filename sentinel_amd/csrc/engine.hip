@@ -251,13 +251,13 @@ __shared__ int64_t g_p0[kMaxWl];     // a.p0 / a.np staged by stage_periods: per
 __shared__ uint32_t g_np[kMaxWl];    // (indexed by the rule's window length) were each a memory round trip
 constexpr int kModS = 64;
 __shared__ uint8_t g_p0mod[kMaxWl][kModS + 1];  // g_p0[w] mod s (s = 1..kModS), staged by stage_periods
-constexpr int kCoarseN = 4096;
-__shared__ uint16_t g_coarse[kCoarseN];  // period of the first request of each 2^g_cshift-request chunk (one window
-__shared__ int g_cshift;                 // length, tables in LDS); g_cshift -1: not staged
 
 // Ring slot of the batch's window period q (period P0 + q of window length w) for sampleCount S: (P0 + q) % S in
 // 32 bits from the staged residue (a 64-bit modulo of the absolute period is ~120 instructions).
 __device__ __forceinline__ int period_slot(int w, uint32_t q, int S) {
+#ifdef SG_NO_PSLOT
+    return (int)((g_p0[w] + (int64_t)q) % S);
+#endif
     if (S <= kModS) return (int)(((uint32_t)g_p0mod[w][S] + q) % (uint32_t)S);
     return (int)((g_p0[w] + (int64_t)q) % S);
 }
@@ -292,14 +292,6 @@ struct PeriodCursor {
     // period of a request index >= every index seen so far: the largest p with table[p] <= idx
     __device__ __forceinline__ uint32_t of(uint32_t idx) const {
         if (q != 0xFFFFFFFFu && idx < next_b) return q;
-        if constexpr (L) {
-            const int sh = g_cshift;
-            if (sh >= 0) {  // from the chunk's period: a chunk spans a boundary or two at most in practice
-                uint32_t p = g_coarse[idx >> sh];
-                while (p + 1 < np && at(p + 1) <= idx) ++p;
-                return p;
-            }
-        }
         uint32_t lo = 0, hi = np;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -945,26 +937,7 @@ __device__ __forceinline__ void stage_periods(const BatchArgs& a) {
         const uint32_t w = x / (kModS + 1), m = x % (kModS + 1);
         g_p0mod[w][m] = m ? (uint8_t)(a.p0[w] % (int64_t)m) : (uint8_t)0;  // p0 >= 0: timestamps are
     }
-    // one window length with its table in LDS: the period of the first request of every 2^shift-request chunk
-    int shift = 0;
-    while (((uint64_t)kCoarseN << shift) < a.n) ++shift;
-    const bool coarse = lds && a.n_wl == 1 && shift < 32;
-    if (threadIdx.x == 0) g_cshift = coarse ? shift : -1;
     __syncthreads();
-    if (coarse) {
-        const uint32_t npw = a.np[0], nch = (uint32_t)((a.n + (1ull << shift) - 1) >> shift);
-        for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
-            const uint32_t idx = c << shift;
-            uint32_t lo = 0, hi = npw;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (g_sbnd[mid] <= idx) lo = mid;
-                else hi = mid;
-            }
-            g_coarse[c] = (uint16_t)lo;
-        }
-        __syncthreads();
-    }
 }
 
 // Long-segment walker: one wave per segment of more than short_max records (grid-stride over the list,

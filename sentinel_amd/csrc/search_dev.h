@@ -51,6 +51,9 @@ __device__ __forceinline__ uint64_t gallop_search(uint64_t lo, uint64_t hi, Pred
 // the exponent bits; the fp64 division sequence (~13 instructions a record on the walkers' hot path) runs only
 // for other intervals. (A test for isec == 1.0 alone is folded away by the compiler: x / 1.0 == x.)
 __device__ __forceinline__ double avg_div(double x, double isec) {
+#ifdef SG_NO_AVGDIV
+    return x / isec;
+#endif
     const uint64_t b = (uint64_t)__double_as_longlong(isec);
     const uint64_t e = (b >> 52) & 0x7FF;
     if ((b & 0x800FFFFFFFFFFFFFull) == 0 && e - 1 < 0x7FD)

@@ -310,12 +310,9 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     }
 }
 
-bool radix_csum_atomic() {
-    static const bool on = [] {
-        const char* e = std::getenv("SG_CSUM_ATOMIC");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    return on;
+bool radix_csum_atomic() {  // read per sort (a getenv per batch): tests switch it per engine
+    const char* e = std::getenv("SG_CSUM_ATOMIC");
+    return e ? std::atoi(e) != 0 : true;
 }
 
 uint32_t* radix_csum(uint32_t* hist_ws, uint64_t n, int D) {

@@ -134,6 +134,23 @@ def test_random_traces_match_oracle(n_keys, n, zipf, prio, S, interval, flags):
     _compare_state(eng, ora, rules)
 
 
+@pytest.mark.parametrize("seg_mark,csum", [("0", "1"), ("1", "0"), ("0", "0")])
+def test_sort_variants(monkeypatch, seg_mark, csum):
+    """The non-default sort paths stay exact: segment marks fused into the last scatter pass (SG_SEG_MARK=0) and the
+    k_colsum pass instead of the histogram kernels' atomic column sums (SG_CSUM_ATOMIC=0)."""
+    monkeypatch.setenv("SG_SEG_MARK", seg_mark)
+    monkeypatch.setenv("SG_CSUM_ATOMIC", csum)
+    rng = np.random.default_rng(int(seg_mark) * 2 + int(csum) + 90)
+    rules = _rules(3000, rng, S=10, interval=1000)
+    eng, ora = _pair(rules)
+    t = 1_700_000_000_003
+    for batch in range(3):
+        req = _trace(rng, 200_000, 3000, t, 1500, zipf=1.0, prio=0.02)
+        t = int(req["ts_ms"][-1]) + 7
+        _compare_results(ora.decide(req), eng.decide_host(req), req)
+    _compare_state(eng, ora, rules)
+
+
 @pytest.mark.parametrize("flags", WALKERS)
 def test_fractional_thresholds_and_exceed(flags):
     """Non-integer count and exceedCount: the double comparisons of ClusterFlowChecker.java:67-71."""
