@@ -779,26 +779,38 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
     // start, events once its records have arrived): two dependent loads per chunk off the critical path. Loads are
     // unconditional with clamped indices; lanes past the segment ignore what they read.
     const uint64_t n1 = a.n - 1;
-    auto ev_ts = [&](uint64_t rec, int64_t& tt, int64_t& cc) {  // exits always (rt, statistic window); entries
-        const LEvent x = ldecode(a, rec);                         // only when breakers may need them
+    // an entry's time matters only while a breaker is not CLOSED (the retry check) and in the serial step (which
+    // reads it itself when not loaded): entries' times are prefetched only while some breaker is open or half-open,
+    // and loaded on demand when one opens inside a chunk (a random 32-B event read per entry otherwise)
+    auto breakers_closed = [&]() {
+        bool c = true;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) c = c && (x >= nb || nd.cb[x].state == kCbClosed);
+        return c;
+    };
+    auto ev_ts = [&](uint64_t rec, int64_t& tt, int64_t& cc, bool ents) {  // exits always (rt, statistic window)
+        const LEvent x = ldecode(a, rec);
         const sg_local_event* le = a.ev + min((uint64_t)x.idx, n1);
-        const bool need = x.kind != SG_LOCAL_ENTRY || nb > 0;
-        tt = need ? le->ts_ms : 0;
+        const bool need = x.kind != SG_LOCAL_ENTRY || ents;
+        tt = need ? le->ts_ms : INT64_MIN;
         cc = need ? le->create_ts : 0;
     };
     uint64_t pf = s;  // position of the prefetched chunk
     uint64_t rec_n = a.rec_sorted[min(s + lane, n1)];
     int64_t t_n, c_n;
-    ev_ts(rec_n, t_n, c_n);
+    bool ents_n = nb > 0 && !breakers_closed();  // the prefetched chunk's entries carry their times
+    ev_ts(rec_n, t_n, c_n, ents_n);
     for (uint64_t base = s; base < e_end;) {
         const uint64_t j = base + lane;
         const bool act = j < e_end;
         if (pf != base) {  // wave-uniform: a skip moved past the prefetched chunk
             rec_n = a.rec_sorted[min(j, n1)];
-            ev_ts(rec_n, t_n, c_n);
+            ents_n = nb > 0 && !breakers_closed();
+            ev_ts(rec_n, t_n, c_n, ents_n);
         }
         const uint64_t rec_c = rec_n;
         const int64_t t_c = t_n, c_c = c_n;
+        bool t_ok = ents_n || nb == 0;  // wave-uniform: the chunk's entries have their times
         pf = base + 64;
         rec_n = a.rec_sorted[min(pf + lane, n1)];
         LEvent ev;
@@ -879,6 +891,10 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
                 int E = special ? __builtin_ctzll(special) : rend;
                 todo &= below(E);
                 if (!all_closed) {
+                    if (!t_ok) {  // a breaker opened inside this chunk: the entries' times, on demand
+                        if (act && ev.kind == SG_LOCAL_ENTRY) t = a.ev[ev.idx].ts_ms;
+                        t_ok = true;
+                    }
                     // fixed window: an entry passes the flow check iff it fits on its own
                     const int32_t cur = java_d2i(nd.pass_qps());
                     const bool fits = !flow_rule || !((double)(int32_t)((uint32_t)cur + (uint32_t)ev.count) > thr);
@@ -982,7 +998,8 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
             }
             pos = rend;
         }
-        ev_ts(rec_n, t_n, c_n);  // the next chunk's events (its records have arrived meanwhile)
+        ents_n = nb > 0 && !breakers_closed();
+        ev_ts(rec_n, t_n, c_n, ents_n);  // the next chunk's events (its records have arrived meanwhile)
         // dead-period skip: the open second window admits nothing any more → jump to the first of (end of
         // this second-window period, end of this minute period, next exit of the resource); k_lskip_apply
         // adds the skipped entries' BLOCK counts to both windows
