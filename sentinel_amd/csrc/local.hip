@@ -655,7 +655,10 @@ __device__ __forceinline__ void stage_lperiods(const LArgs& a, uint32_t* sbnd, c
 }
 
 // One lane per resource segment: the serial step for every event.
-__global__ void __launch_bounds__(256) k_lwalk_short(LArgs a, BatchArgs sg) {
+#ifndef SG_LWALK_BLOCKS
+#define SG_LWALK_BLOCKS 1
+#endif
+__global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_short(LArgs a, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
     if (*a.err) return;
@@ -1050,7 +1053,7 @@ __device__ void lwalk_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t
     nd.finish();
 }
 
-__global__ void __launch_bounds__(256) k_lwalk_long(LArgs a, BatchArgs sg) {
+__global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_long(LArgs a, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
     if (*a.err) return;
