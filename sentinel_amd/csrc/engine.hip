@@ -399,7 +399,10 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
 
 // --------------------------------------------------------------------------- wave walker (long)
 
-constexpr int kWaveUnroll = 8;  // 64-record chunks kept in flight per wave (register double buffer)
+#ifndef SG_WAVE_UNROLL
+#define SG_WAVE_UNROLL 4  // 255 VGPRs with no spill once inlined (8: 21 spills; 0.89 vs 0.92 ms/step)
+#endif
+constexpr int kWaveUnroll = SG_WAVE_UNROLL;  // 64-record chunks kept in flight per wave (register double buffer)
 
 template <bool L>
 struct WaveWalker {
