@@ -3074,6 +3074,14 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_lflags, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_lskip_count, 0, sizeof(uint32_t), stream));
+    // the first sort pass's histogram (and column sums) counted by k_local_prep
+    L.hist0 = h->d_hist;
+    L.hist0_bits = radix_digit_bits(64 - L.kshift);
+    L.csum0 = nullptr;
+    if (radix_csum_atomic()) {
+        L.csum0 = radix_csum(h->d_hist, n, L.hist0_bits);
+        HIP_TRY(h, hipMemsetAsync(L.csum0, 0, radix_csum_bytes(n, L.hist0_bits), stream));
+    }
     HIP_TRY(h, launch_local_prep(L, stream));
     if (track) {  // the batch's new pool nodes (only for a batch that passed validation), then room for them
         HIP_TRY(h, hipMemsetAsync(h->d_lnode_new, 0, sizeof(uint32_t), stream));
@@ -3092,7 +3100,8 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     uint64_t* sorted = nullptr;
-    HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, L.kshift, h->d_hist, &sorted, stream));
+    HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, L.kshift, h->d_hist, &sorted, stream, 64, true, nullptr,
+                                  L.csum0 != nullptr));
     h->last_sorted = sorted;
     L.rec_sorted = sorted;
     sgm.rec_sorted = sorted;

@@ -584,6 +584,9 @@ struct LArgs {
     uint64_t n;
     uint64_t* rec;            // [res : kbits][idx : ibits][count << 3 | kind << 1 | prio : abits]
     uint64_t* rec_sorted;
+    uint32_t* hist0;          // k_local_prep: per-tile histogram of the first sort digit (radix_hist layout), or null
+    uint32_t* csum0;          // and its chunk column sums (radix_csum), or null
+    int hist0_bits;
     int kshift, abits;
     uint64_t imask, amask, aesc;
     uint32_t K;               // resources (record keys)

@@ -108,11 +108,23 @@ __device__ __forceinline__ void lstore(const LArgs& a, uint32_t idx, int32_t st,
 
 // ------------------------------------------------------------------------------------------ prep
 
+// One block per 4096-event tile (the radix sort's): with a.hist0 the block also counts its records' first sort
+// digit, so the sort skips that histogram pass (as k_prep does for the cluster flow batch).
+constexpr int kLPrepItems = 16;
 __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
+    __shared__ uint32_t dcnt[1024];
     const uint64_t n = a.n;
     const int64_t t0 = a.ev[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t dmask = (1u << a.hist0_bits) - 1u;
+    if (a.hist0)
+        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) dcnt[d] = 0;
+    __syncthreads();
+    const uint64_t tile = (uint64_t)blockIdx.x * (256 * kLPrepItems);
+#pragma unroll 4
+    for (int it = 0; it < kLPrepItems; ++it) {
+        const uint64_t i = tile + (uint64_t)it * 256 + threadIdx.x;
+        if (i >= n) break;
         const sg_local_event e = a.ev[i];
         const int64_t t = e.ts_ms;
         if (i == 0) {
@@ -175,6 +187,16 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         // write every other outcome), plain 0 for exits and events of unknown resources
         lstore(a, (uint32_t)i, (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS, 0);
         a.rec[i] = rec;
+        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
+    }
+    if (a.hist0) {
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)blockIdx.x * (dmask + 1) + d] = dcnt[d];
+        if (a.csum0) {
+            uint32_t* cs = a.csum0 + (size_t)(blockIdx.x / kChunkTiles) * (dmask + 1);
+            for (uint32_t d = threadIdx.x; d <= dmask; d += 256)
+                if (dcnt[d]) atomicAdd(cs + d, dcnt[d]);
+        }
     }
 }
 
@@ -1765,7 +1787,8 @@ static unsigned lresident(const void* kernel) {
 }
 
 hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_local_prep, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_local_prep, dim3((unsigned)((a.n + 256 * kLPrepItems - 1) / (256 * kLPrepItems))), dim3(256), 0,
+                       stream, a);
     return hipGetLastError();
 }
 
