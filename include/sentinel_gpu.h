@@ -766,6 +766,39 @@ int sg_codec_decode_flow(sg_handle* h, const uint8_t* payload, const uint32_t* o
 int sg_codec_encode_flow(sg_handle* h, const int32_t* xid, const uint8_t* kind, const sg_result* res, uint64_t n,
                          uint8_t* frames_out, void* stream);
 
+/* ---------- Envoy rate-limit service ----------
+ * SentinelEnvoyRlsServiceImpl.shouldRateLimit (sentinel-cluster/sentinel-cluster-server-envoy-rls/.../service/v3/
+ * SentinelEnvoyRlsServiceImpl.java:34-85) for a time-ordered batch of n RateLimitRequests on a handle whose flow
+ * rules were loaded as the RLS checker reads them (SimpleClusterFlowChecker.acquireClusterToken, flow/
+ * SimpleClusterFlowChecker.java:33-65: GLOBAL threshold count · exceedCount, no namespace limiter, no prioritized
+ * occupy). Request j is served at ts_ms with acquireCount = hits_addend (0 → 1) over its descriptors
+ * desc_rule[desc_begin, desc_begin + desc_count): a descriptor's rule index (the caller resolves
+ * EnvoySentinelRuleConverter.generateFlowId over domain + entries on its side), or -1 when it has no rule. Every
+ * descriptor is one token request, all of a batch in one device batch, in order.
+ *   overall[j]  SG_RLS_OK / SG_RLS_OVER_LIMIT (any descriptor not OK), or SG_RLS_ERROR when hits_addend < 0
+ *               (responseObserver.onError, :36-40; its descriptors are not requested and get code 0)
+ *   status[d]   code (SG_RLS_OK when the result is OK or the rule is missing, :55-58, else SG_RLS_OVER_LIMIT),
+ *               and for a descriptor with a rule: limit_remaining = the TokenResult's remaining and
+ *               requests_per_unit = (int) rule.getCount() (:67-73), has_rule = 1. */
+#define SG_RLS_OK          1   /* envoy.service.ratelimit.v3.RateLimitResponse.Code.OK         */
+#define SG_RLS_OVER_LIMIT  2   /* ... Code.OVER_LIMIT                                          */
+#define SG_RLS_ERROR      (-1) /* hits_addend < 0: the call fails                               */
+typedef struct {
+    int64_t  ts_ms;        /* TimeUtil.currentTimeMillis() when the call is served */
+    int32_t  hits_addend;  /* RateLimitRequest.hits_addend                         */
+    uint32_t desc_begin;
+    uint32_t desc_count;
+    uint32_t pad;
+} sg_rls_request;          /* 24 bytes */
+typedef struct {
+    int32_t code;
+    int32_t limit_remaining;
+    int32_t requests_per_unit;
+    int32_t has_rule;
+} sg_rls_status;           /* 16 bytes */
+int sg_rls_should_rate_limit(sg_handle* h, const sg_rls_request* req, uint32_t n, const int32_t* desc_rule,
+                             uint64_t n_desc, int32_t* overall, sg_rls_status* status);
+
 /* Testing aid: copy an internal buffer of the last batch to host memory.
  * what: 0 = records (request order, u64), 1 = records sorted by flowId, 2 = window-period table
  * (u32 [8][65536]), 3 = first period per window length (i64[8]), 4 = periods per window length (u32[8]). */

@@ -76,6 +76,12 @@ class sg_batch_stats(C.Structure):
 
 # numpy views of the request / result records (same layout as the C structs)
 REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("key", "<u4"), ("acquire", "<i4")], align=True)
+# sg_rls_request / sg_rls_status (Envoy RLS entry point)
+RLS_REQ_DTYPE = np.dtype([("ts_ms", "<i8"), ("hits_addend", "<i4"), ("desc_begin", "<u4"), ("desc_count", "<u4"),
+                          ("pad", "<u4")], align=True)
+RLS_STATUS_DTYPE = np.dtype([("code", "<i4"), ("limit_remaining", "<i4"), ("requests_per_unit", "<i4"),
+                             ("has_rule", "<i4")], align=True)
+RLS_OK, RLS_OVER_LIMIT, RLS_ERROR = 1, 2, -1
 RES_DTYPE = np.dtype([("status", "<i4"), ("remaining", "<i4"), ("wait_ms", "<i4")], align=True)
 RULE_DTYPE = np.dtype([("flow_id", "<i8"), ("count", "<f8"), ("threshold_type", "<i4"), ("sample_count", "<i4"),
                        ("window_interval_ms", "<i4"), ("namespace_id", "<i4")], align=True)

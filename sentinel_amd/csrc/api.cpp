@@ -1656,6 +1656,67 @@ int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_re
     return SG_OK;
 }
 
+// Envoy RLS (SentinelEnvoyRlsServiceImpl.shouldRateLimit, service/v3/SentinelEnvoyRlsServiceImpl.java:34-85): every
+// descriptor of the batch one token request of one device batch (chunked by max_batch), then the per-request codes.
+int sg_rls_should_rate_limit(sg_handle* h, const sg_rls_request* req, uint32_t n, const int32_t* desc_rule,
+                             uint64_t n_desc, int32_t* overall, sg_rls_status* status) {
+    if (!h) return SG_E_INVAL;
+    if (n && (!req || !overall)) return fail(h, SG_E_INVAL, "null buffer");
+    if (n_desc && (!desc_rule || !status)) return fail(h, SG_E_INVAL, "null buffer");
+    for (uint32_t j = 0; j < n; ++j)
+        if ((uint64_t)req[j].desc_begin + req[j].desc_count > n_desc)
+            return fail(h, SG_E_INVAL, "a request's descriptors lie outside desc_rule");
+    std::vector<sg_req> batch;
+    std::vector<uint64_t> owner;  // descriptor of each token request
+    batch.reserve(n_desc);
+    owner.reserve(n_desc);
+    for (uint64_t d = 0; d < n_desc; ++d) status[d] = sg_rls_status{0, 0, 0, 0};
+    for (uint32_t j = 0; j < n; ++j) {
+        const sg_rls_request& q = req[j];
+        if (q.hits_addend < 0) {  // "acquireCount should be positive": onError, no token requests (:36-40)
+            overall[j] = SG_RLS_ERROR;
+            continue;
+        }
+        overall[j] = SG_RLS_OK;
+        const int32_t acquire = q.hits_addend == 0 ? 1 : q.hits_addend;  // :41-44
+        for (uint32_t x = 0; x < q.desc_count; ++x) {
+            const uint64_t d = (uint64_t)q.desc_begin + x;
+            const int32_t r = desc_rule[d];
+            sg_req t{};
+            t.ts_ms = q.ts_ms;
+            t.key = (r < 0 || (uint32_t)r >= h->K) ? SG_KEY_NO_RULE : (uint32_t)r;  // checkToken: no rule
+            t.acquire = acquire;
+            batch.push_back(t);
+            owner.push_back(d);
+        }
+    }
+    std::vector<sg_result> res(batch.size());
+    for (uint64_t b = 0; b < batch.size(); b += h->cfg.max_batch) {
+        const uint64_t m = std::min<uint64_t>(h->cfg.max_batch, batch.size() - b);
+        const int rc = sg_flow_decide_batch_host(h, batch.data() + b, m, res.data() + b);
+        if (rc) return rc;
+    }
+    for (uint64_t x = 0; x < batch.size(); ++x) {
+        const uint64_t d = owner[x];
+        int32_t st = res[x].status;
+        if (st == SG_STATUS_NO_RULE_EXISTS) st = SG_STATUS_OK;  // a descriptor without a rule passes (:55-58)
+        sg_rls_status& o = status[d];
+        o.code = st == SG_STATUS_OK ? SG_RLS_OK : SG_RLS_OVER_LIMIT;
+        if (batch[x].key != SG_KEY_NO_RULE) {
+            const double c = h->rules[batch[x].key].count;  // (int) rule.getCount(), JLS narrowing
+            o.requests_per_unit = c >= 2147483647.0 ? INT32_MAX : (int32_t)c;
+            o.limit_remaining = res[x].remaining;
+            o.has_rule = 1;
+        }
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        if (overall[j] == SG_RLS_ERROR) continue;
+        for (uint32_t x = 0; x < req[j].desc_count; ++x)
+            if (status[(uint64_t)req[j].desc_begin + x].code != SG_RLS_OK) overall[j] = SG_RLS_OVER_LIMIT;
+    }
+    return SG_OK;
+}
+
 int sg_flow_read_state(sg_handle* h, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
     if (!h || key >= h->K || !starts || !counters || !occupy) return SG_E_INVAL;
     HIP_TRY(h, hipSetDevice(h->device));

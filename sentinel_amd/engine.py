@@ -27,7 +27,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
            "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values", "sg_cparam_last_rounds",
            "sg_pslot_load_rules", "sg_pslot_decide_batch", "sg_pslot_decide_batch_host", "sg_pslot_thread_count",
-           "sg_pslot_param_idx",
+           "sg_pslot_param_idx", "sg_rls_should_rate_limit",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state",
            "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
            "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
@@ -120,6 +120,7 @@ def load_library():
         "sg_pace_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_pace_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
         "sg_pace_read_state": (C.c_int, [vp, u32, vp]),
+        "sg_rls_should_rate_limit": (C.c_int, [vp, vp, u32, vp, u64, vp, vp]),
         "sg_node_create": (C.c_int, [C.POINTER(abi.sg_config), vp, u32, C.POINTER(vp)]),
         "sg_node_destroy": (None, [vp]),
         "sg_node_last_error": (C.c_char_p, [vp]),
@@ -304,6 +305,16 @@ class FlowEngine:
         out = np.zeros(len(req), abi.RES_DTYPE)
         self._check(self._L.sg_flow_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
         return out
+
+    def rls_should_rate_limit(self, req: np.ndarray, desc_rule: np.ndarray):
+        """sg_rls_should_rate_limit: (overall codes per request, sg_rls_status per descriptor)."""
+        req = np.ascontiguousarray(req, dtype=abi.RLS_REQ_DTYPE)
+        desc_rule = np.ascontiguousarray(desc_rule, dtype=np.int32)
+        overall = np.zeros(len(req), np.int32)
+        status = np.zeros(len(desc_rule), abi.RLS_STATUS_DTYPE)
+        self._check(self._L.sg_rls_should_rate_limit(self.h, abi.ptr(req), len(req), abi.ptr(desc_rule), len(desc_rule),
+                                                     abi.ptr(overall), abi.ptr(status)))
+        return overall, status
 
     # ---- asynchronous host pipeline (pinned buffers, tickets)
     def host_array(self, n, dtype):

@@ -9,6 +9,10 @@ the GLOBAL threshold, count * exceedCount, as SimpleClusterFlowChecker computes 
 and maps the TokenResults back to Envoy codes. The descriptor → rule lookup
 (EnvoySentinelRuleConverter.generateFlowId over domain + descriptor entries) is string work the caller does;
 here a descriptor arrives as its rule index, or -1 when no rule exists.
+
+`should_rate_limit` builds the descriptor batch in Python over any decide() (the device engine or the oracle);
+`should_rate_limit_abi` calls the library's own entry point, sg_rls_should_rate_limit (the same mapping in C++ for
+C++ / JNI callers), and returns the same responses.
 """
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -83,4 +87,30 @@ def should_rate_limit(requests: List[RateLimitRequest], rule_counts: np.ndarray,
         out[j].statuses.append(st)
         if code != CODE_OK:
             out[j].overall_code = CODE_OVER_LIMIT
+    return out
+
+
+def should_rate_limit_abi(eng, requests: List[RateLimitRequest]) -> List[RateLimitResponse]:
+    """The same responses through sg_rls_should_rate_limit (one call for the whole batch)."""
+    req = np.zeros(len(requests), abi.RLS_REQ_DTYPE)
+    desc, begin = [], 0
+    for j, q in enumerate(requests):
+        req[j] = (q.ts_ms, q.hits_addend, begin, len(q.descriptors), 0)
+        desc.extend(q.descriptors)
+        begin += len(q.descriptors)
+    overall, status = eng.rls_should_rate_limit(req, np.array(desc, np.int32))
+    out = []
+    for j, q in enumerate(requests):
+        if overall[j] == abi.RLS_ERROR:
+            out.append(RateLimitResponse(error=f"acquireCount should be positive, but actual: {q.hits_addend}"))
+            continue
+        r = RateLimitResponse(overall_code=int(overall[j]))
+        b = int(req[j]["desc_begin"])
+        for st in status[b:b + len(q.descriptors)]:
+            if st["has_rule"]:
+                r.statuses.append(DescriptorStatus(int(st["code"]), int(st["limit_remaining"]),
+                                                   int(st["requests_per_unit"])))
+            else:
+                r.statuses.append(DescriptorStatus(int(st["code"])))
+        out.append(r)
     return out

@@ -53,6 +53,8 @@ int main(void) {{
          sizeof(sg_req), sizeof(sg_result), sizeof(sg_batch_stats));
   printf("%zu %zu %zu %zu\\n", offsetof(sg_req, key), offsetof(sg_req, acquire), offsetof(sg_flow_rule, count),
          offsetof(sg_flow_rule, namespace_id));
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(sg_rls_request), offsetof(sg_rls_request, hits_addend),
+         offsetof(sg_rls_request, desc_begin), offsetof(sg_rls_request, desc_count), sizeof(sg_rls_status));
   return 0;
 }}''')
     exe = tmp_path / "layout"
@@ -64,6 +66,10 @@ int main(void) {{
     offs = [int(x) for x in lines[1].split()]
     assert offs == [abi.sg_req.key.offset, abi.sg_req.acquire.offset, abi.sg_flow_rule.count.offset,
                     abi.sg_flow_rule.namespace_id.offset]
+    rls = [int(x) for x in lines[2].split()]
+    assert rls == [abi.RLS_REQ_DTYPE.itemsize, abi.RLS_REQ_DTYPE.fields["hits_addend"][1],
+                   abi.RLS_REQ_DTYPE.fields["desc_begin"][1], abi.RLS_REQ_DTYPE.fields["desc_count"][1],
+                   abi.RLS_STATUS_DTYPE.itemsize]
 
 
 def test_create_fails_cleanly_without_device():

@@ -5,15 +5,16 @@ import pytest
 
 from oracle.binding import ClusterTokenService
 from sentinel_amd import abi
-from sentinel_amd.rls import RateLimitRequest, rls_rules, should_rate_limit
+from sentinel_amd.rls import RateLimitRequest, rls_rules, should_rate_limit, should_rate_limit_abi
 
 pytestmark = pytest.mark.gpu
 
 T = 1_700_000_000_000
 
 
-@pytest.mark.parametrize("seed,exceed", [(1, 1.0), (2, 1.5)])
-def test_rls_device_matches_oracle(seed, exceed):
+@pytest.mark.parametrize("seed,exceed,via_abi", [(1, 1.0, False), (2, 1.5, False), (3, 1.0, True), (4, 1.5, True)])
+def test_rls_device_matches_oracle(seed, exceed, via_abi):
+    """via_abi: the library's sg_rls_should_rate_limit instead of the Python shim over sg_flow_decide_batch."""
     from sentinel_amd.engine import FlowEngine
     rng = np.random.default_rng(seed)
     K = 300
@@ -43,7 +44,7 @@ def test_rls_device_matches_oracle(seed, exceed):
             d = [int(x) if rng.random() < 0.95 else -1 for x in rng.choice(K, nd, p=p)]
             hits = int(rng.choice([0, 1, 1, 1, 2, 5, -1], p=[0.1, 0.5, 0.2, 0.1, 0.05, 0.04, 0.01]))
             reqs.append(RateLimitRequest(t, hits, d))
-        got = should_rate_limit(reqs, rules["count"], eng.decide_host)
+        got = should_rate_limit_abi(eng, reqs) if via_abi else should_rate_limit(reqs, rules["count"], eng.decide_host)
         want = should_rate_limit(reqs, rules["count"], ora.decide_rls)
         assert got == want, f"batch {batch}: responses differ"
     for k in range(K):
