@@ -429,9 +429,51 @@ def cparam(args, dev):
             "data": "synthetic (GPU-generated, seeded): rules Zipf(1.0), values Zipf(1.1) per rule, 10% 2-3 values"}
 
 
+def node(args, dev):
+    """The node handle (sg_node_*) on one GPU: the C3 workload (1M flowIds, 16M requests per 1000 ms batch) decided
+    by G same-device shard handles with the routing inside the library — validation and the namespace limiters on the
+    front handle, the stable multisplit by splitmix64(flowId) mod G, every shard on its own stream, the gather back
+    into caller order — against one handle's synchronous sg_flow_decide_batch on the same batches."""
+    import bench
+    from sentinel_amd.engine import NodeEngine
+    G = args.shards
+    wl = bench.ShardWorkload(1_000_000, args.events, 0, 1, dev)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    nd = NodeEngine([0] * G, max_batch=args.events)
+    nd.set_namespaces(ns)
+    nd.load_rules(wl.rules)
+    one = FlowEngine(device=0, max_batch=args.events)
+    one.set_namespaces(ns)
+    one.load_rules(wl.rules)
+    batches = [wl.batch(b) for b in range(args.warmup + args.steps)]
+    out = torch.empty(args.events * 12, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    el = timed(lambda b: nd.decide_device(batches[b].data_ptr(), args.events, out.data_ptr(), stream),
+               args.warmup, args.steps)
+    # the single handle on the same batches, one second later each (time order), synchronous entry point
+    later = [b.clone() for b in batches]
+    for x in later:
+        x.view(torch.int64).view(-1, 2)[:, 0] += 1000 * (args.warmup + args.steps)
+    el1 = timed(lambda b: one.decide_device(later[b].data_ptr(), args.events, out.data_ptr(), stream),
+                args.warmup, args.steps)
+    n = args.events
+    keys = batches[-1].view(torch.int64).view(-1, 2)[:, 1] & 0x7FFFFFFF
+    touched = int(torch.unique(keys).numel())
+    b_alg = n * (bench.REQ_B + bench.RES_B) + touched * (bench.STATE_B + bench.RULE_B)  # bench.py's C3 bytes
+    return {"metric": f"flow decisions/sec through the node handle, {G} shards on one GPU (routing inside)",
+            "workload": f"C3 workload (1M flowIds, 16M requests/batch, Zipf 1.0) on sg_node with {G} same-device "
+                        "shards",
+            "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": None,
+            "extra": {"shards": G, "single_handle_ms_per_step": el1 / args.steps * 1e3,
+                      "single_handle_decisions_per_s": n * args.steps / el1},
+            "data": "synthetic (GPU-generated, seeded): bench.py's C3 batches"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam", "node"], default="c2")
+    ap.add_argument("--shards", type=int, default=2, help="node: shard handles on the one GPU")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=16_000_000)
@@ -446,7 +488,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace, "cparam": cparam}[args.workload](args, dev)
+    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace, "cparam": cparam, "node": node}[args.workload](args, dev)
     ms = r["el"] * 1000.0 / args.steps
     gbs = r["b_alg"] / (ms / 1000.0) / 1e9
     res = {"metric": r["metric"], "value": r["value"], "unit": r.get("unit", "decisions/s"), "n_gpus": 1,

@@ -7,8 +7,8 @@
 // namespace limiter over it in caller order (k_prep + the limiter pre-pass), so each request of its packed records
 // that survived carries its node rule index. Routing is a stable multisplit of those records by shard:
 //   k_route_count    per 4096-record tile: requests per shard (LDS counters)
-//   k_route_scan     one block: per shard, the exclusive scan of the tile counts; shard slices laid out one after
-//                    the other (shard g at base[g]) in one sub-batch buffer, the per-shard totals for the host
+//   k_route_scan     one block per shard: the exclusive scan of its tile counts, its total; k_route_bases lays the
+//                    shard slices out one after the other (shard g at base[g]) in one sub-batch buffer
 //   k_route_scatter  per tile: each wave ranks its 64-record rounds by shard (match ballots, as the radix scatter)
 //                    and writes the sub-request {ts, local rule index | prio, acquire} and the node position of
 //                    every routed request — time order within a shard is kept (stable), so each slice is a valid
@@ -64,30 +64,50 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_count(RouteArgs r) {
     if (tid < r.G) r.tile_cnt[(size_t)blockIdx.x * kMaxShards + tid] = cnt[tid];
 }
 
-// One block of kMaxShards waves' worth of threads: thread g scans shard g's column serially over the tiles (tiles
-// = n / 4096, a few thousand at most: a few µs), then the shard bases.
-__global__ void __launch_bounds__(kMaxShards) k_route_scan(RouteArgs r, uint32_t ntiles) {
-    __shared__ uint32_t tot[kMaxShards];
-    const int g = threadIdx.x;
-    uint32_t run = 0;
-    if (g < r.G) {
-        for (uint32_t t = 0; t < ntiles; ++t) {
-            const uint32_t c = r.tile_cnt[(size_t)t * kMaxShards + g];
-            r.tile_cnt[(size_t)t * kMaxShards + g] = run;
-            run += c;
-        }
+// One block per shard: the exclusive scan of the shard's column of tile counts (1024 threads, a few tiles each,
+// then a block scan), the shard's total for the host. (A serial column walk was one dependent load per tile:
+// 1.4 ms for a 16M-request batch.)
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) k_route_scan(RouteArgs r, uint32_t ntiles) {
+    __shared__ uint32_t wsum[kScanThreads / 64];
+    const int g = blockIdx.x, tid = threadIdx.x, lane = route_lane(), wave = tid >> 6;
+    const uint32_t per = (ntiles + kScanThreads - 1) / kScanThreads;
+    const uint32_t t0 = (uint32_t)tid * per, t1 = min(t0 + per, ntiles);
+    uint32_t mine = 0;
+    for (uint32_t t = t0; t < t1; ++t) mine += r.tile_cnt[(size_t)t * kMaxShards + g];
+    uint32_t x = mine;  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
     }
-    tot[g] = g < r.G ? run : 0u;
+    if (lane == 63) wsum[wave] = x;
     __syncthreads();
-    if (g == 0) {
-        uint32_t b = 0;
-        for (int x = 0; x < r.G; ++x) {
-            r.shard_base[x] = b;
-            r.shard_tot[x] = tot[x];
-            b += tot[x];
-        }
-        r.shard_base[r.G] = b;
+    uint32_t run = x - mine, total = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        if (w < wave) run += wsum[w];
+        total += wsum[w];
     }
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t c = r.tile_cnt[(size_t)t * kMaxShards + g];
+        r.tile_cnt[(size_t)t * kMaxShards + g] = run;
+        run += c;
+    }
+    if (tid == 0) r.shard_tot[g] = total;
+}
+
+// The shard slices one after the other: base[g] = Σ totals before g (G <= 64: one wave).
+__global__ void __launch_bounds__(64) k_route_bases(RouteArgs r) {
+    const int lane = route_lane();
+    const uint32_t v = lane < r.G ? r.shard_tot[lane] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane < r.G) r.shard_base[lane] = x - v;
+    if (lane == 63) r.shard_base[r.G] = x;
 }
 
 __global__ void __launch_bounds__(kRouteThreads) k_route_scatter(RouteArgs r) {
@@ -148,7 +168,8 @@ hipError_t launch_route(const RouteArgs& r, hipStream_t stream) {
     const uint32_t tiles = (uint32_t)((r.n + kRouteTile - 1) / kRouteTile);
     if (tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
-    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(kMaxShards), 0, stream, r, tiles);
+    hipLaunchKernelGGL(k_route_scan, dim3((unsigned)r.G), dim3(kScanThreads), 0, stream, r, tiles);
+    hipLaunchKernelGGL(k_route_bases, dim3(1), dim3(64), 0, stream, r);
     hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
     return hipGetLastError();
 }
