@@ -34,6 +34,7 @@ struct sg_handle {
 
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
+    BucketHot* d_hot = nullptr;       // start / PASS / WAITING of every bucket (the short walkers' gather)
     Occ* d_occ = nullptr;
     uint32_t* d_seg_end = nullptr;   // [2K] end, then start (k_seg_mark) of each flowId's segment in the sorted records
 
@@ -576,6 +577,7 @@ void sg_destroy(sg_handle* h) {
     }
     dfree(h->d_rules);
     dfree(h->d_ring);
+    dfree(h->d_hot);
     dfree(h->d_occ);
     dfree(h->d_seg_end);
     dfree(h->d_rec);
@@ -901,6 +903,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
 
     Rule* d_rules = nullptr;
     Bucket* d_ring = nullptr;
+    BucketHot* d_hot = nullptr;
     Occ* d_occ = nullptr;
     uint32_t* d_seg_end = nullptr;
     int32_t* d_src = nullptr;
@@ -909,9 +912,11 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     } else if (n) {
         if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess || hipMalloc(&d_seg_end, sizeof(uint32_t) * 2 * n) != hipSuccess ||
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
+            hipMalloc(&d_hot, sizeof(BucketHot) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
             dfree(d_rules);
             dfree(d_ring);
+            dfree(d_hot);
             dfree(d_occ);
             dfree(d_seg_end);
             dfree(d_src);
@@ -921,6 +926,7 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         HIP_TRY(h, hipMemset(d_seg_end + n, 0xFF, sizeof(uint32_t) * n));  // no segment starts marked
         HIP_TRY(h, hipMemcpy(d_src, src.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, launch_init_state(d_ring, d_occ, n, stride, d_src, h->d_ring, h->d_occ, h->stride, 0));
+        HIP_TRY(h, launch_hot_sync(d_ring, d_hot, (uint64_t)n * stride, 0));
         HIP_TRY(h, hipDeviceSynchronize());
         dfree(d_src);
     }
@@ -943,10 +949,12 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     h->conc_dirty = true;
     dfree(h->d_rules);
     dfree(h->d_ring);
+    dfree(h->d_hot);
     dfree(h->d_occ);
     dfree(h->d_seg_end);
     h->d_rules = d_rules;
     h->d_ring = d_ring;
+    h->d_hot = d_hot;
     h->d_occ = d_occ;
     h->d_seg_end = d_seg_end;
     h->rules.assign(rules, rules + n);
@@ -1172,6 +1180,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.K = h->K;
     a.rules = h->d_rules;
     a.ring = h->d_ring;
+    a.hot = h->d_hot;
     a.occ = h->d_occ;
     a.seg_end = w.seg_end;
     a.seg_start = w.seg_start;
@@ -1760,6 +1769,8 @@ int sg_flow_import_state(sg_handle* h, const int64_t* ring, uint64_t ring_words,
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
     HIP_TRY(h, hipMemcpy(h->d_ring, ring, rw * 8, hipMemcpyHostToDevice));
+    HIP_TRY(h, launch_hot_sync(h->d_ring, h->d_hot, (uint64_t)h->K * h->stride, 0));
+    HIP_TRY(h, hipDeviceSynchronize());
     HIP_TRY(h, hipMemcpy(h->d_occ, occ, ow * 8, hipMemcpyHostToDevice));
     return SG_OK;
 }
@@ -3097,6 +3108,7 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         L.emb = 1;
         L.c3_rules = h->d_rules;
         L.c3_ring = h->d_ring;
+        L.c3_hot = h->d_hot;
         L.c3_occ = h->d_occ;
         L.c3_stride = h->stride;
         L.c3_K = h->K;

@@ -32,6 +32,25 @@ struct alignas(64) Bucket {
 };
 static_assert(sizeof(Bucket) == 64, "Bucket layout");
 
+// The fields of a bucket the window sums read — its start, PASS and WAITING — kept beside the ring, 16 B per bucket
+// (PASS / WAITING in int32: read only under BatchArgs::narrow, where every count is proven below 2^30). The short
+// walkers gather a flowId's ten buckets from here in 160 contiguous bytes instead of five 128-B lines of the ring;
+// every writer of a bucket's start, PASS or WAITING writes both (store_bucket), bulk changes resync it (k_hot_sync).
+struct alignas(16) BucketHot {
+    int64_t start;
+    int32_t pass;
+    int32_t wait;
+};
+static_assert(sizeof(BucketHot) == 16, "BucketHot layout");
+
+__device__ __forceinline__ void store_hot(BucketHot* h, int64_t start, int64_t pass, int64_t wait) {
+    BucketHot x;
+    x.start = start;
+    x.pass = (int32_t)pass;
+    x.wait = (int32_t)wait;
+    *h = x;
+}
+
 // ClusterMetricLeapArray.occupyCounter[PASS], [PASS_REQUEST]; hasOccupied == (pass_req > 0).
 struct alignas(16) Occ {
     int64_t pass;
@@ -82,6 +101,7 @@ struct BatchArgs {
     uint32_t K;          // number of rules
     const Rule* rules;
     Bucket* ring;        // [K][stride]
+    BucketHot* hot;      // [K][stride] start / PASS / WAITING of every bucket (the short walkers' gather)
     Occ* occ;            // [K]
     int stride;          // buckets per flowId (max sampleCount)
     double max_occ_ratio;
@@ -637,6 +657,7 @@ struct LArgs {
     int32_t emb;
     const Rule* c3_rules;
     Bucket* c3_ring;
+    BucketHot* c3_hot;
     Occ* c3_occ;
     int c3_stride;
     uint32_t c3_K;
@@ -737,6 +758,7 @@ hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
 // bytes (a multiple of 4) from device memory to a device-accessible host buffer by the shader
 hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_hot_sync(const Bucket* ring, BucketHot* hot, uint64_t buckets, hipStream_t stream);
 hipError_t launch_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride, const int32_t* src_map,
                              const Bucket* old_ring, const Occ* old_occ, int old_stride, hipStream_t stream);
 hipError_t launch_snapshot(const Rule* rules, const Bucket* ring, const Occ* occ, uint32_t K, int stride,

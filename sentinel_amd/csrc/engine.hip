@@ -344,6 +344,7 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
     uint32_t opened = 0;
     const Rule R = a.rules[k];
     Bucket* ring = a.ring + (size_t)k * a.stride;
+    BucketHot* hot = a.hot + (size_t)k * a.stride;
     PeriodCursor<L> pc;
     pc.init(a, R.wl_idx);
     const int64_t P0 = g_p0[R.wl_idx];
@@ -366,6 +367,7 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
                 ring[I].start = ws;
 #pragma unroll
                 for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[I].c[ev] = ps.cur[ev];
+                store_hot(hot + I, ws, ps.cur[SG_EV_PASS], ps.cur[SG_EV_WAITING]);
             }
             pc.seek(q);
             open_period_serial(ps, ring, R, P0 + (int64_t)q, &I, &ws);
@@ -389,6 +391,7 @@ __device__ uint32_t walk_serial(const BatchArgs& a, uint32_t k, uint64_t s, uint
         ring[I].start = ws;
 #pragma unroll
         for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[I].c[ev] = ps.cur[ev];
+        store_hot(hot + I, ws, ps.cur[SG_EV_PASS], ps.cur[SG_EV_WAITING]);
     }
     Occ o;
     o.pass = ps.occ_pass;
@@ -410,6 +413,7 @@ struct WaveWalker {
     const Rule R;
     const int lane;
     Bucket* ring;
+    BucketHot* hot;
     PeriodCursor<L> pc;
     int64_t P0;
     // lane q < S holds slot q of the ring
@@ -427,6 +431,7 @@ struct WaveWalker {
     __device__ WaveWalker(const BatchArgs& a_, uint32_t k)
         : a(a_), R(a_.rules[k]), lane(lane_id()) {
         ring = a.ring + (size_t)k * a.stride;
+        hot = a.hot + (size_t)k * a.stride;
         pc.init(a, R.wl_idx);
         P0 = g_p0[R.wl_idx];
         st = INT64_MIN;
@@ -607,6 +612,7 @@ struct WaveWalker {
             ring[lane].start = st;
 #pragma unroll
             for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ring[lane].c[ev] = c[ev];
+            store_hot(hot + lane, st, c[SG_EV_PASS], c[SG_EV_WAITING]);
         }
         if (lane == 0) {
             Occ o;
@@ -1062,12 +1068,13 @@ __device__ __forceinline__ bool tiny_active(const BatchArgs& a) {
     return a.tiny && a.narrow && narrow_span(a, a.p0[0] * (int64_t)a.wl[0]);
 }
 
-__device__ __forceinline__ void store_bucket(Bucket* b, int64_t start, const int64_t* c) {
+__device__ __forceinline__ void store_bucket(Bucket* b, BucketHot* h, int64_t start, const int64_t* c) {
     ulonglong2* p = reinterpret_cast<ulonglong2*>(b);
     p[0] = make_ulonglong2((unsigned long long)start, (unsigned long long)c[0]);
     p[1] = make_ulonglong2((unsigned long long)c[1], (unsigned long long)c[2]);
     p[2] = make_ulonglong2((unsigned long long)c[3], (unsigned long long)c[4]);
     p[3] = make_ulonglong2((unsigned long long)c[5], (unsigned long long)c[6]);
+    store_hot(h, start, c[SG_EV_PASS], c[SG_EV_WAITING]);
 }
 
 constexpr int kBlk = 4;  // records per block of the short walker's double-buffered record stream
@@ -1085,6 +1092,7 @@ template <int SM, bool L>
 __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, uint64_t e,
                                          const Rule& R, const Occ& occ, SlotSnap* snap, uint64_t* buf, int64_t T0) {
     Bucket* ring = a.ring + (size_t)k * a.stride;
+    BucketHot* hot = a.hot + (size_t)k * a.stride;
     const int S = R.S;
     const int64_t wl = R.wl;
     PeriodCursor<L> pc;
@@ -1142,7 +1150,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                if (!(a.dbg & 512)) store_bucket(ring + I, ws, ps.cur);
+                if (!(a.dbg & 512)) store_bucket(ring + I, hot + I, ws, ps.cur);
                 snap[I].st = (int32_t)(ws - T0);
                 snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
                 snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
@@ -1207,7 +1215,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
     }
 
     if (act) {
-        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        if (I >= 0) store_bucket(ring + I, hot + I, ws, ps.cur);
         if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
             Occ o;
             o.pass = ps.occ_pass;
@@ -1252,6 +1260,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
                                          const Rule& R, const Occ& occ, SlotSnap* snap, uint32_t* wrecs, int lane,
                                          int64_t T0, int rows) {
     Bucket* ring = a.ring + (size_t)k * a.stride;
+    BucketHot* hot = a.hot + (size_t)k * a.stride;
     const int S = R.S;
     const int64_t wl = R.wl;
     PeriodCursor<L> pc;
@@ -1305,7 +1314,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
         // 1. open the period of every lane whose next record starts one (the first record included)
         if (live && !park && qn != pc.q) {
             if (I >= 0) {  // close the open bucket: memory and the snapshot
-                store_bucket(ring + I, ws, ps.cur);
+                store_bucket(ring + I, hot + I, ws, ps.cur);
                 snap[I].st = (int32_t)(ws - T0);
                 snap[I].pass = (int32_t)ps.cur[SG_EV_PASS];
                 snap[I].wait = (int32_t)ps.cur[SG_EV_WAITING];
@@ -1365,7 +1374,7 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
         }
     }
     if (act) {
-        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        if (I >= 0) store_bucket(ring + I, hot + I, ws, ps.cur);
         if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
             Occ o;
             o.pass = ps.occ_pass;
@@ -1452,11 +1461,12 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
         // the next group's descriptors (unconditional: a conditional load would be copied, and wait, at the merge)
         desc(min(g + nwaves, total - 1), c_n, act_n, s_n, k_n, e_n);
         {
-            // ring gather: piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS},
-            // 1: WAITING); slots past the handle's stride read slot 0 again (ignored: q >= S)
-            // every piece is loaded before any is used (the scheduling barrier keeps the compiler from
-            // interleaving the loads with their LDS writes, which serialised the gather into round trips)
-            constexpr int kT = 2 * SM;
+            // ring gather from the hot mirror: piece t*64 + lane = bucket q of the ring of lane j = piece / SM,
+            // {start, PASS | WAITING << 32} (16 B: a flowId's ten buckets are 160 contiguous bytes); slots past the
+            // handle's stride read slot 0 again (ignored: q >= S). Every piece is loaded before any is used (the
+            // scheduling barrier keeps the compiler from interleaving the loads with their LDS writes, which
+            // serialised the gather into round trips)
+            constexpr int kT = SM;
             int gl = lane;
             asm volatile("" : "+v"(gl));
             ulonglong2 v[kT];
@@ -1464,10 +1474,10 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
             for (int t = 0; t < kT; ++t) {
                 const int pc = t * 64 + gl;
                 const int j = pc / kT;
-                const int q = (pc % kT) >> 1;
+                const int q = pc % kT;
                 const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
                 const int qq = q < a.stride ? q : 0;
-                v[t] = *(reinterpret_cast<const ulonglong2*>(a.ring + (size_t)kj * a.stride + qq) + ((pc & 1) ? 3 : 0));
+                v[t] = *reinterpret_cast<const ulonglong2*>(a.hot + (size_t)kj * a.stride + qq);
             }
             __builtin_amdgcn_sched_barrier(0);
             // every dword of every piece stays live until here: the allocator would otherwise reuse the unused
@@ -1477,13 +1487,10 @@ __device__ __forceinline__ void walk_short_lds(const BatchArgs& a, SlotSnap* sna
 #pragma unroll
             for (int t = 0; t < kT; ++t) {
                 const int pc = t * 64 + gl;
-                SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
-                if (pc & 1) {
-                    d.wait = (int32_t)v[t].y;
-                } else {
-                    d.st = snap_rel((int64_t)v[t].x, T0);
-                    d.pass = (int32_t)v[t].y;
-                }
+                SlotSnap& d = snap[pc];  // (pc / SM) * SM + pc % SM
+                d.st = snap_rel((int64_t)v[t].x, T0);
+                d.pass = (int32_t)(uint32_t)v[t].y;
+                d.wait = (int32_t)(uint32_t)(v[t].y >> 32);
             }
         }
         wait_vm0();  // the staged records have landed
@@ -1554,36 +1561,30 @@ __device__ __forceinline__ void walk_short_body(const BatchArgs& a, SlotSnap* sn
 #pragma unroll
             for (int u = 0; u < kBlk; ++u) buf[u] = a.rec_sorted[min(s + u, a.n - 1)];
             {
-                // piece t*64 + lane: ring of lane j = piece / (2*SM), slot q, half (0: {start, PASS}, 1: WAITING);
-                // slots past the handle's stride read slot 0 again (ignored: q >= S)
-                constexpr int kT = 2 * SM;  // pieces per lane, loaded in two batches of SM
+                // piece t*64 + lane: bucket q = piece % SM of the ring of lane j = piece / SM, from the hot mirror
+                // ({start, PASS | WAITING << 32}); slots past the handle's stride read slot 0 again (ignored: q >= S)
+                constexpr int kT = SM;  // pieces per lane
                 // the piece addresses depend on the lane only: an opaque copy of it keeps the compiler from
                 // hoisting ~3 * kT of them out of the group loop (they held 60+ VGPRs for the whole walk)
                 int gl = lane;
                 asm volatile("" : "+v"(gl));
-#pragma unroll
-                for (int t0 = 0; t0 < kT; t0 += SM) {
+                {
                     ulonglong2 v[SM];
 #pragma unroll
                     for (int t = 0; t < SM; ++t) {
-                        const int pc = (t0 + t) * 64 + gl;
+                        const int pc = t * 64 + gl;
                         const int j = pc / kT;
-                        const int q = (pc % kT) >> 1;
+                        const int q = pc % kT;
                         const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
                         const int qq = q < a.stride ? q : 0;
-                        v[t] = *(reinterpret_cast<const ulonglong2*>(a.ring + (size_t)kj * a.stride + qq) +
-                                 ((pc & 1) ? 3 : 0));
+                        v[t] = *reinterpret_cast<const ulonglong2*>(a.hot + (size_t)kj * a.stride + qq);
                     }
 #pragma unroll
                     for (int t = 0; t < SM; ++t) {
-                        const int pc = (t0 + t) * 64 + gl;
-                        SlotSnap& d = snap[(pc / kT) * SM + ((pc % kT) >> 1)];
-                        if (pc & 1) {
-                            d.wait = (int32_t)v[t].y;
-                        } else {
-                            d.st = snap_rel((int64_t)v[t].x, T0);
-                            d.pass = (int32_t)v[t].y;
-                        }
+                        SlotSnap& d = snap[t * 64 + gl];
+                        d.st = snap_rel((int64_t)v[t].x, T0);
+                        d.pass = (int32_t)(uint32_t)v[t].y;
+                        d.wait = (int32_t)(uint32_t)(v[t].y >> 32);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1649,15 +1650,15 @@ __device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
         uint64_t r2 = a.rec_sorted[min(s + 2, a.n - 1)], r3 = a.rec_sorted[min(s + 3, a.n - 1)];
         static_assert(kR == 4, "four record registers");
         Bucket* ring = a.ring + (size_t)k * a.stride;
+        BucketHot* hot = a.hot + (size_t)k * a.stride;
         int32_t st[SM], pa[SM], wa[SM];
 #pragma unroll
         for (int x = 0; x < SM; ++x) {
             const int xx = x < R.S ? x : 0;
-            const ulonglong2 sp = *reinterpret_cast<const ulonglong2*>(ring + xx);          // {start, PASS}
-            const ulonglong2 ow = *(reinterpret_cast<const ulonglong2*>(ring + xx) + 3);    // {OCC_BLOCK, WAITING}
-            st[x] = snap_rel((int64_t)sp.x, T0);
-            pa[x] = (int32_t)sp.y;
-            wa[x] = (int32_t)ow.y;
+            const ulonglong2 hv = *reinterpret_cast<const ulonglong2*>(hot + xx);  // {start, PASS | WAITING << 32}
+            st[x] = snap_rel((int64_t)hv.x, T0);
+            pa[x] = (int32_t)(uint32_t)hv.y;
+            wa[x] = (int32_t)(uint32_t)(hv.y >> 32);
         }
         PeriodCursor<L> pc;
         pc.init(a, R.wl_idx);
@@ -1680,7 +1681,7 @@ __device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
             const uint32_t q = pc.of(d.idx);
             if (q != pc.q) {
                 if (I >= 0) {  // close the open bucket: memory and the register ring
-                    store_bucket(ring + I, ws, ps.cur);
+                    store_bucket(ring + I, hot + I, ws, ps.cur);
 #pragma unroll
                     for (int x = 0; x < SM; ++x) {
                         st[x] = x == I ? (int32_t)(ws - T0) : st[x];
@@ -1731,7 +1732,7 @@ __device__ __forceinline__ void walk_tiny_body(const BatchArgs& a) {
                 if (stt != SG_STATUS_BLOCKED) store_result(a.out, d.idx, stt, 0, wait);
             }
         }
-        if (I >= 0) store_bucket(ring + I, ws, ps.cur);
+        if (I >= 0) store_bucket(ring + I, hot + I, ws, ps.cur);
         if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
             Occ o;
             o.pass = ps.occ_pass;
@@ -1794,6 +1795,12 @@ __global__ void k_finish(BatchArgs a) {
 }
 
 // ---------------------------------------------------------------------------- state management
+
+// The hot mirror of every bucket, rebuilt from the ring (after rule loads and state imports).
+__global__ void __launch_bounds__(256) k_hot_sync(const Bucket* ring, BucketHot* hot, uint64_t buckets) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < buckets; i += (uint64_t)gridDim.x * blockDim.x)
+        store_hot(hot + i, ring[i].start, ring[i].c[SG_EV_PASS], ring[i].c[SG_EV_WAITING]);
+}
 
 __global__ void __launch_bounds__(256) k_init_state(Bucket* ring, Occ* occ, uint32_t K, int stride,
                                                     const int32_t* src_map, const Bucket* old_ring,
@@ -1997,6 +2004,12 @@ hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int b
 
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(1), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_sync(const Bucket* ring, BucketHot* hot, uint64_t buckets, hipStream_t stream) {
+    if (buckets == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hot_sync, dim3(grid_for(buckets, 256, 8192)), dim3(256), 0, stream, ring, hot, buckets);
     return hipGetLastError();
 }
 

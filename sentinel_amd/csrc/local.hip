@@ -1264,6 +1264,7 @@ __device__ int32_t embedded_token(const LArgs& a, uint32_t key, int64_t t, int32
     }
     ring[I].start = ws;
     for (int e = 0; e < SG_NUM_EVENTS; ++e) ring[I].c[e] = cur[e];
+    store_hot(a.c3_hot + (size_t)key * a.c3_stride + I, ws, cur[SG_EV_PASS], cur[SG_EV_WAITING]);
     if (occ_pass != o.pass || occ_req != o.pass_req) {
         Occ no;
         no.pass = occ_pass;
