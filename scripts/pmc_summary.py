@@ -20,7 +20,7 @@ from collections import defaultdict
 
 # every decision-pipeline kernel (k_*) except one-off state setup / readout; steps = launches of the batch's finish kernel
 NOT_PIPELINE = ("k_init_state", "k_local_init", "k_ptable_clear", "k_psclear", "k_psread", "k_snapshot", "k_cp_clear",
-                "k_local_metrics")
+                "k_local_metrics", "k_hot_sync")
 FINISH = ("k_finish", "k_local_finish", "k_pfinish", "k_psfinish", "k_pace_finish", "k_cp_finish_batch")
 
 
