@@ -64,6 +64,29 @@ def timed(step, warmup, steps):
     return time.perf_counter() - t0
 
 
+def local_timed(eng, batches, sizes, args, dev, stream):
+    """C2 / C5 steps through sg_local_enqueue (the pipelined local path: a batch's front half — validation, sort by
+    resource, segment and exit lists — beside the previous batch's walkers): at most two batches in flight (the two
+    workspaces), each ticket collected two batches later, two out buffers alternating. --local-sync: the synchronous
+    sg_local_decide_batch, one batch at a time."""
+    outs = [torch.empty(max(sizes) * 8, dtype=torch.uint8, device=dev) for _ in range(2)]
+    if args.local_sync:
+        return timed(lambda b: eng.local_decide_device(batches[b].data_ptr(), sizes[b], outs[0].data_ptr(), stream),
+                     args.warmup, args.steps)
+    tickets = []
+
+    def step(b):
+        if len(tickets) >= 2:
+            eng.local_wait(tickets.pop(0))
+        tickets.append(eng.local_enqueue(batches[b].data_ptr(), sizes[b], outs[b % 2].data_ptr()))
+
+    torch.cuda.synchronize()  # the batches were generated on torch's stream
+    el = timed(step, args.warmup, args.steps)
+    for t in tickets:
+        eng.local_wait(t)
+    return el
+
+
 def c2(args, dev):
     K, n = 10_000, args.events
     rng = np.random.default_rng(2)
@@ -85,9 +108,8 @@ def c2(args, dev):
     eng = FlowEngine(device=0, max_batch=n)
     eng.local_load_rules(rules, 2, 1000, 500)
     batches = [batch(b) for b in range(args.warmup + args.steps)]
-    out = torch.empty(n * 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    el = timed(lambda b: eng.local_decide_device(batches[b].data_ptr(), n, out.data_ptr(), stream), args.warmup, args.steps)
+    el = local_timed(eng, batches, [n] * len(batches), args, dev, stream)
     touched = int(torch.unique(batches[-1].view(torch.int64).reshape(-1, 4)[:, 2] & 0xFFFFFFFF).numel())
     # per event: 32 B sg_local_event in + 8 B result out; per touched resource: second window 2x64 B read +
     # write, one minute bucket read + write, curThreadNum/breaker head 2x16 B, rule 16 B
@@ -184,11 +206,9 @@ def c5(args, dev):
     eng = FlowEngine(device=0, max_batch=max(len(e) for e in host))
     eng.local_load_rules(rules, 2, 1000, 500)
     batches = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e in host]
-    out = torch.empty(max(len(e) for e in host) * 8, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     sizes = [len(e) for e in host]
-    el = timed(lambda b: eng.local_decide_device(batches[b].data_ptr(), sizes[b], out.data_ptr(), stream),
-               args.warmup, args.steps)
+    el = local_timed(eng, batches, sizes, args, dev, stream)
     decided = sum(sizes[args.warmup:])
     touched = int(np.unique(host[-1]["resource"] & 0x7FFFFFFF).size)
     # per event 32 B in + 8 B out; per touched resource: second window 2x128 B, two minute buckets 2x2x64 B,
@@ -480,6 +500,8 @@ def main():
     ap.add_argument("--resources", type=int, default=1_000_000)
     ap.add_argument("--cpu-events", type=int, default=4_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--local-sync", action="store_true",
+                    help="c2 / c5: time the synchronous sg_local_decide_batch instead of the sg_local_enqueue pipeline")
     ap.add_argument("--chain", type=int, default=0,
                     help="cparam: embed a chain of this many two-value requests per batch, each sharing a value with "
                          "the next under a threshold of one (adversarial: one link per fixed-point round)")

@@ -596,6 +596,19 @@ int sg_cparam_top_values(sg_handle* h, int64_t now_ms, uint32_t number, uint64_t
 int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local_rule* rules, uint32_t n);
 int sg_local_decide_batch(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, void* stream);
 int sg_local_decide_batch_host(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out);
+/* sg_local_decide_batch on the device pipeline (DEVICE buffers, like sg_flow_enqueue): enqueues the batch and
+ * returns at once with a ticket for sg_local_poll / sg_local_wait (same meaning as sg_flow_poll / _wait; tickets
+ * are shared with the flow pipeline). The front half of batch i+1 (validation, sort by resource, segment and exit
+ * lists) runs beside the walkers of batch i; the walkers run in enqueue order, so batches must be time-ordered as
+ * for sg_local_decide_batch, and a batch older than the one before is rejected as a whole (checked before its
+ * walkers). ev/out must stay allocated and untouched until the ticket completes (each batch in flight needs its
+ * own out buffer); up to 4 batches in flight. A batch the pipeline does not take — origin or context nodes tracked,
+ * the embedded token server, or rules loaded since the last batch — first completes the batches in flight and is
+ * decided synchronously (its status still comes with its ticket). Every other call on the handle first completes
+ * the batches in flight. */
+int sg_local_enqueue(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, uint64_t* ticket);
+int sg_local_poll(sg_handle* h, uint64_t ticket);
+int sg_local_wait(sg_handle* h, uint64_t ticket);
 /* Resource state: second window [S][8] {start, PASS, BLOCK, EXCEPTION, SUCCESS, RT, OCCUPIED_PASS, minRt},
  * borrow array [S][2] {start, PASS}, minute window [60][8] (start INT64_MIN = never created; counters of
  * such slots read 0), head[14] = {curThreadNum, then per breaker: state, nextRetry, stat start, slow/error

@@ -169,11 +169,14 @@ struct sg_handle {
     int l_n_wl = 0, l_wsec = 0, l_wmin = 0;
     int32_t l_wl[kMaxWl]{};
     sg_local_event* d_lev_h = nullptr;
-    int* d_lflags = nullptr;
-    uint32_t* d_lexit_pos = nullptr;
-    uint32_t* d_lexit_cnt = nullptr;
-    LSkip* d_lskips = nullptr;
-    uint32_t* d_lskip_count = nullptr;
+    struct LocalWs {                  // the local path's own batch buffers of a pipeline workspace (0: every local
+        int* flags = nullptr;         // batch; 1: every other sg_local_enqueue batch), sized for max_batch
+        uint32_t* exit_pos = nullptr;
+        uint32_t* exit_cnt = nullptr;
+        LSkip* skips = nullptr;
+        uint32_t* skip_count = nullptr;
+    };
+    LocalWs lws[2];
     uint32_t lskip_cap = 0;
     sg_local_result* d_lout_h = nullptr;
     // node pool (origin nodes, context DefaultNodes; created by the batches, kept across flow-rule reloads)
@@ -306,6 +309,7 @@ struct sg_handle {
         uint64_t ticket = 0;
         int* h_err = nullptr;         // pinned
         hipEvent_t done = nullptr;
+        bool local = false;           // an sg_local_enqueue batch (its error flags map through local_status)
     };
     DevTicket dev[kDevSlots];
     bool front_only = false;          // a node handle's front (validation + namespace limiter): no flow state
@@ -685,11 +689,13 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lmin);
     dfree(h->d_llast_ts);
     dfree(h->d_lev_h);
-    dfree(h->d_lflags);
-    dfree(h->d_lexit_pos);
-    dfree(h->d_lexit_cnt);
-    dfree(h->d_lskips);
-    dfree(h->d_lskip_count);
+    for (auto& w : h->lws) {
+        dfree(w.flags);
+        dfree(w.exit_pos);
+        dfree(w.exit_cnt);
+        dfree(w.skips);
+        dfree(w.skip_count);
+    }
     dfree(h->d_lout_h);
     dfree(h->d_lext_h);
     dfree(h->d_lgkey);
@@ -1068,6 +1074,23 @@ int flow_status(sg_handle* h, int err) {
     return SG_OK;
 }
 
+// A local batch's error flags → return code (rejected as a whole; no state changed).
+int local_status(sg_handle* h, int err) {
+    if (err & kErrTime)
+        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
+    if (err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
+    if (err & kErrBounds)
+        return fail(h, SG_E_INVAL, "an event's origin id (0..n_origins), context id (0..n_contexts-1) or arguments "
+                                   "(the arg / value arrays) are out of range");
+    if (err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param value or thread-count table is full");
+    if (err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    return SG_OK;
+}
+
+int ticket_status(sg_handle* h, const sg_handle::DevTicket& d) {
+    return d.local ? local_status(h, *d.h_err) : flow_status(h, *d.h_err);
+}
+
 // Workspace 0: the handle's own batch buffers.
 void main_ws(sg_handle* h, sg_handle::FlowWs& w) {
     w.rec = h->d_rec;
@@ -1419,7 +1442,7 @@ int drain_async(sg_handle* h) {
     for (auto& d : h->dev) {
         if (!d.ticket) continue;
         hipError_t e = hipEventSynchronize(d.done);
-        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : ticket_status(h, d);
         d.ticket = 0;
     }
     if (h->s_back) (void)hipStreamSynchronize(h->s_back);  // workspace 0 is the synchronous path's too
@@ -1601,11 +1624,12 @@ int sg_flow_enqueue(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out,
     }
     if (d.ticket) {  // every slot in flight: complete the oldest (its status waits in `finished`)
         hipError_t e = hipEventSynchronize(d.done);
-        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : ticket_status(h, d);
         d.ticket = 0;
     }
     int rc = enqueue_flow_pipelined(h, req, n, out, nullptr, d.h_err, d.done);
     if (rc) return rc;
+    d.local = false;
     d.ticket = h->next_ticket++;
     *ticket = d.ticket;
     return SG_OK;
@@ -1635,7 +1659,7 @@ static int collect(sg_handle* h, uint64_t ticket, bool block) {
         if (e == hipErrorNotReady) return 0;
         d.ticket = 0;
         if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
-        const int st = flow_status(h, *d.h_err);
+        const int st = ticket_status(h, d);
         return st == SG_OK ? 1 : st;
     }
     return fail(h, SG_E_INVAL, "unknown or already collected ticket");
@@ -1814,12 +1838,13 @@ int sg_snapshot_metrics_enqueue(sg_handle* h, int64_t now_ms, double* out_dev, u
     }
     if (d.ticket) {
         hipError_t e = hipEventSynchronize(d.done);
-        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : flow_status(h, *d.h_err);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : ticket_status(h, d);
         d.ticket = 0;
     }
     *d.h_err = 0;
     HIP_TRY(h, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, out_dev, h->s_back));
     HIP_TRY(h, hipEventRecord(d.done, h->s_back));
+    d.local = false;
     d.ticket = h->next_ticket++;
     *ticket = d.ticket;
     return SG_OK;
@@ -2694,6 +2719,7 @@ int sg_local_load_rules(sg_handle* h, const sg_local_config* cfg, const sg_local
         return fail(h, SG_E_INVAL, "invalid statistic window (SAMPLE_COUNT / INTERVAL)");
     if (cfg->sample_count > kMinuteS) return fail(h, SG_E_UNSUPPORTED, "SAMPLE_COUNT > 60");
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     std::vector<LRule> tab(n);
     for (uint32_t i = 0; i < n; ++i) {
         const sg_local_rule& r = rules[i];
@@ -3002,27 +3028,48 @@ int lnode_grow(sg_handle* h, uint64_t used) {
     return SG_OK;
 }
 
-// StatisticSlot around ParamFlowSlot → FlowSlot → DegradeSlot for a time-ordered batch (ext nullable).
-int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n, const sg_pslot_arg* args,
-                 uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_local_result* out, void* stream_) {
-    if (!h) return SG_E_INVAL;
-    if (n == 0) return SG_OK;
-    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
-    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
-    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
-    hipStream_t stream = (hipStream_t)stream_;
-    HIP_TRY(h, hipSetDevice(h->device));
-    drain_async(h);
-    if (h->l_groups_stale && h->l_cluster_rules) {
-        const int grc = local_apply_groups(h);
-        if (grc) return grc;
+// The local path's batch buffers of one pipeline workspace: 0 the handle's own (every synchronous batch), 1 the
+// flow pipeline's second workspace plus lws[1] (every other sg_local_enqueue batch).
+struct LocalBufs {
+    uint64_t* rec;
+    uint64_t* rec_sorted;
+    uint32_t* hist;
+    uint32_t* bnd;
+    int64_t* p0;
+    uint32_t* np;
+    int* err;
+    uint32_t* long_list;
+    uint32_t* counts;  // [1 + kClasses]: long count, short counts per class
+    uint32_t* short_list;
+    sg_handle::LocalWs* lw;
+};
+
+int local_bufs(sg_handle* h, int x, LocalBufs& b) {
+    if (x == 0) {
+        b = LocalBufs{h->d_rec, h->d_rec_sorted, h->d_hist, h->d_bnd, h->d_p0, h->d_np, h->d_err, h->d_long_list,
+                      h->d_long_count, h->d_short_list, &h->lws[0]};
+    } else {
+        const auto& w = h->pws;
+        b = LocalBufs{w.rec, w.rec_sorted, w.hist, w.bnd, w.p0, w.np, w.err, w.long_list, w.counts, w.short_list, &h->lws[1]};
     }
-    int prc = local_apply_params(h);
-    if (prc) return prc;
-    const bool emb = h->l_cluster_state == SG_CLUSTER_SERVER && h->l_cluster_rules;
-    if (emb && h->shard_world > 1 && h->n_lim > 0)
-        return fail(h, SG_E_UNSUPPORTED, "an embedded token server on a sharded handle with namespace limiters: the "
-                                         "limiter exchange covers flow and param batches only");
+    sg_handle::LocalWs& lw = h->lws[x];
+    if (!lw.flags) {  // the local path's own buffers of the workspace (sized for max_batch)
+        const uint64_t mb = h->cfg.max_batch;
+        h->lskip_cap = (uint32_t)(2 * mb / kSkipMin + 1);
+        if (hipMalloc(&lw.flags, sizeof(int)) != hipSuccess ||
+            hipMalloc(&lw.exit_pos, sizeof(uint32_t) * (mb + 1)) != hipSuccess ||
+            hipMalloc(&lw.exit_cnt, sizeof(uint32_t) * (mb / kLTile + 2)) != hipSuccess ||
+            hipMalloc(&lw.skips, sizeof(LSkip) * h->lskip_cap) != hipSuccess ||
+            hipMalloc(&lw.skip_count, sizeof(uint32_t)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "local batch workspace");
+    }
+    return SG_OK;
+}
+
+// The kernels' arguments of a local batch on workspace buffers b (node tracking set up by the caller).
+int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
+               const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_local_result* out,
+               bool emb, LArgs& L, BatchArgs& sgm) {
     const uint32_t K = (uint32_t)h->ltab.size();
     int kbits = bits_for((uint64_t)K);
     if (kbits < 1) kbits = 1;
@@ -3030,12 +3077,12 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     const int abits = 64 - kbits - ibits;
     if (abits < 4) return fail(h, SG_E_UNSUPPORTED, "resources x max_batch too large for 64-bit records");
 
-    LArgs L{};
+    L = LArgs{};
     L.ev = ev;
     L.out = out;
     L.n = n;
-    L.rec = h->d_rec;
-    L.rec_sorted = h->d_rec_sorted;
+    L.rec = b.rec;
+    L.rec_sorted = b.rec_sorted;
     L.kshift = 64 - kbits;
     L.abits = abits;
     L.imask = (ibits >= 64) ? ~0ull : ((1ull << ibits) - 1);
@@ -3060,10 +3107,10 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     L.wmin = h->l_wmin;
     L.n_wl = h->l_n_wl;
     std::memcpy(L.wl, h->l_wl, sizeof(L.wl));
-    L.bnd = h->d_bnd;
-    L.p0 = h->d_p0;
-    L.np = h->d_np;
-    L.err = h->d_err;
+    L.bnd = b.bnd;
+    L.p0 = b.p0;
+    L.np = b.np;
+    L.err = b.err;
     L.last_ts = h->d_llast_ts;
     L.ext = ext;
     L.n_contexts = h->l_n_contexts;
@@ -3076,16 +3123,105 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         L.ps.values = values;
         L.ps.n_values = values ? n_values : 0;
     }
-    if (!h->d_lflags) {  // batch workspace of the local path (sized for max_batch)
-        const uint64_t mb = h->cfg.max_batch;
-        h->lskip_cap = (uint32_t)(2 * mb / kSkipMin + 1);
-        if (hipMalloc(&h->d_lflags, sizeof(int)) != hipSuccess ||
-            hipMalloc(&h->d_lexit_pos, sizeof(uint32_t) * (mb + 1)) != hipSuccess ||
-            hipMalloc(&h->d_lexit_cnt, sizeof(uint32_t) * (mb / kLTile + 2)) != hipSuccess ||
-            hipMalloc(&h->d_lskips, sizeof(LSkip) * h->lskip_cap) != hipSuccess ||
-            hipMalloc(&h->d_lskip_count, sizeof(uint32_t)) != hipSuccess)
-            return fail(h, SG_E_NOMEM, "local batch workspace");
+    if (emb) {  // the embedded token server: this handle's cluster flow state
+        L.emb = 1;
+        L.c3_rules = h->d_rules;
+        L.c3_ring = h->d_ring;
+        L.c3_hot = h->d_hot;
+        L.c3_occ = h->d_occ;
+        L.c3_stride = h->stride;
+        L.c3_K = h->K;
+        L.max_occ_ratio = h->cfg.max_occupy_ratio;
+        L.c3_rule_lim = h->d_rule_lim;
+        L.lim_ring = h->d_lim_ring;
+        for (int j = 0; j < kMaxLim; ++j) L.lim_qps[j] = h->lim_qps[j];
+        L.c3_last_ts = h->d_last_ts;
     }
+    L.flags = b.lw->flags;
+    L.exit_pos = b.lw->exit_pos;
+    L.exit_cnt = b.lw->exit_cnt;
+    L.skips = b.lw->skips;
+    L.skip_count = b.lw->skip_count;
+    L.skip_cap = h->lskip_cap;
+    L.hist0 = b.hist;
+    L.hist0_bits = radix_digit_bits(64 - L.kshift);
+
+    sgm = BatchArgs{};  // segment lists (k_seg)
+    sgm.n = n;
+    sgm.rec_sorted = b.rec_sorted;
+    sgm.kshift = L.kshift;
+    sgm.K = K;
+    sgm.err = b.err;
+    sgm.long_list = b.long_list;
+    sgm.long_count = b.counts;
+    sgm.short_list = b.short_list;
+    sgm.short_count = b.counts + 1;
+    for (int c = 0; c < kClasses; ++c) sgm.class_off[c] = h->class_off[c];
+    // Lane / wave walker split: with many events per resource (n >= 256 K) the lanes' longest class (65..256 events)
+    // sets the lane walker's end and the wave walker takes those segments sooner (C2, 10k resources: 0.88 → 0.82
+    // ms/step); with few (C5, 1M resources) 256 stays best (1.97 against 2.28 ms at 64). SG_SHORT_MAX overrides.
+    const uint32_t lsplit = (!h->short_max_env && (uint64_t)n >= 256ull * K) ? 64u : h->short_max;
+    sgm.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : lsplit;
+
+    return SG_OK;
+}
+
+// Front half of a local batch on `stream`: validation, default results and packed records (k_local_prep, with the
+// first sort digit's histogram), the stable sort by resource, the segment lists and the exit positions. Reads no
+// state a walker writes (with L.defer_last the first timestamp's check waits for the back half).
+int local_front(sg_handle* h, LArgs& L, BatchArgs& sgm, hipStream_t stream) {
+    HIP_TRY(h, hipMemsetAsync(L.err, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(sgm.long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
+    HIP_TRY(h, hipMemsetAsync(L.flags, 0, sizeof(int), stream));
+    HIP_TRY(h, hipMemsetAsync(L.skip_count, 0, sizeof(uint32_t), stream));
+    L.csum0 = nullptr;
+    if (radix_csum_atomic()) {
+        L.csum0 = radix_csum(L.hist0, L.n, L.hist0_bits);
+        HIP_TRY(h, hipMemsetAsync(L.csum0, 0, radix_csum_bytes(L.n, L.hist0_bits), stream));
+    }
+    HIP_TRY(h, launch_local_prep(L, stream));
+    return SG_OK;
+}
+
+int local_sort(sg_handle* h, LArgs& L, BatchArgs& sgm, uint64_t* spare, hipStream_t stream) {
+    uint64_t* sorted = nullptr;
+    HIP_TRY(h, radix_sort_records(L.rec, spare, L.n, L.kshift, L.hist0, &sorted, stream, 64, true, nullptr,
+                                  L.csum0 != nullptr));
+    L.rec_sorted = sorted;
+    sgm.rec_sorted = sorted;
+    HIP_TRY(h, launch_seg(sgm, stream));
+    return SG_OK;
+}
+
+// StatisticSlot around ParamFlowSlot → FlowSlot → DegradeSlot for a time-ordered batch (ext nullable).
+int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n, const sg_pslot_arg* args,
+                 uint64_t n_args, const uint64_t* values, uint64_t n_values, sg_local_result* out, void* stream_) {
+    if (!h) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
+    if (h->l_groups_stale && h->l_cluster_rules) {
+        const int grc = local_apply_groups(h);
+        if (grc) return grc;
+    }
+    int prc = local_apply_params(h);
+    if (prc) return prc;
+    const bool emb = h->l_cluster_state == SG_CLUSTER_SERVER && h->l_cluster_rules;
+    if (emb && h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "an embedded token server on a sharded handle with namespace limiters: the "
+                                         "limiter exchange covers flow and param batches only");
+    LocalBufs b;
+    int rc = local_bufs(h, 0, b);
+    if (rc) return rc;
+    LArgs L;
+    BatchArgs sgm;
+    rc = local_args(h, b, ev, ext, n, args, n_args, values, n_values, out, emb, L, sgm);
+    if (rc) return rc;
+    const uint32_t K = L.K;
     const bool track = h->l_n_origins > 0 || h->l_n_contexts > 0;
     if (track) {
         const int rc = lnode_prepare(h, n);
@@ -3104,58 +3240,10 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         L.epoch = h->l_epoch;
         L.track_ctx = h->l_n_contexts > 0 ? 1 : 0;
     }
-    if (emb) {  // the embedded token server: this handle's cluster flow state
-        L.emb = 1;
-        L.c3_rules = h->d_rules;
-        L.c3_ring = h->d_ring;
-        L.c3_hot = h->d_hot;
-        L.c3_occ = h->d_occ;
-        L.c3_stride = h->stride;
-        L.c3_K = h->K;
-        L.max_occ_ratio = h->cfg.max_occupy_ratio;
-        L.c3_rule_lim = h->d_rule_lim;
-        L.lim_ring = h->d_lim_ring;
-        for (int j = 0; j < kMaxLim; ++j) L.lim_qps[j] = h->lim_qps[j];
-        L.c3_last_ts = h->d_last_ts;
-    }
-    L.flags = h->d_lflags;
-    L.exit_pos = h->d_lexit_pos;
-    L.exit_cnt = h->d_lexit_cnt;
-    L.skips = h->d_lskips;
-    L.skip_count = h->d_lskip_count;
-    L.skip_cap = h->lskip_cap;
-
-    BatchArgs sgm{};  // segment lists (k_seg)
-    sgm.n = n;
-    sgm.rec_sorted = h->d_rec_sorted;
-    sgm.kshift = L.kshift;
-    sgm.K = K;
-    sgm.err = h->d_err;
-    sgm.long_list = h->d_long_list;
-    sgm.long_count = h->d_long_count;
-    sgm.short_list = h->d_short_list;
-    sgm.short_count = h->d_long_count + 1;
-    for (int c = 0; c < kClasses; ++c) sgm.class_off[c] = h->class_off[c];
-    // Lane / wave walker split: with many events per resource (n >= 256 K) the lanes' longest class (65..256 events)
-    // sets the lane walker's end and the wave walker takes those segments sooner (C2, 10k resources: 0.88 → 0.82
-    // ms/step); with few (C5, 1M resources) 256 stays best (1.97 against 2.28 ms at 64). SG_SHORT_MAX overrides.
-    const uint32_t lsplit = (!h->short_max_env && (uint64_t)n >= 256ull * K) ? 64u : h->short_max;
-    sgm.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : lsplit;
 
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_lflags, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_lskip_count, 0, sizeof(uint32_t), stream));
-    // the first sort pass's histogram (and column sums) counted by k_local_prep
-    L.hist0 = h->d_hist;
-    L.hist0_bits = radix_digit_bits(64 - L.kshift);
-    L.csum0 = nullptr;
-    if (radix_csum_atomic()) {
-        L.csum0 = radix_csum(h->d_hist, n, L.hist0_bits);
-        HIP_TRY(h, hipMemsetAsync(L.csum0, 0, radix_csum_bytes(n, L.hist0_bits), stream));
-    }
-    HIP_TRY(h, launch_local_prep(L, stream));
+    rc = local_front(h, L, sgm, stream);
+    if (rc) return rc;
     if (track) {  // the batch's new pool nodes (only for a batch that passed validation), then room for them
         HIP_TRY(h, hipMemsetAsync(h->d_lnode_new, 0, sizeof(uint32_t), stream));
         HIP_TRY(h, launch_lnode_assign(L, stream));
@@ -3172,20 +3260,16 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         L.minute = h->d_lmin;
     }
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
-    uint64_t* sorted = nullptr;
-    HIP_TRY(h, radix_sort_records(h->d_rec, h->d_rec_sorted, n, L.kshift, h->d_hist, &sorted, stream, 64, true, nullptr,
-                                  L.csum0 != nullptr));
-    h->last_sorted = sorted;
-    L.rec_sorted = sorted;
-    sgm.rec_sorted = sorted;
+    rc = local_sort(h, L, sgm, b.rec_sorted, stream);
+    if (rc) return rc;
+    h->last_sorted = L.rec_sorted;
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
-    HIP_TRY(h, launch_seg(sgm, stream));
     HIP_TRY(h, launch_local_walk(L, sgm, h->l_has_cx || h->l_has_cx_ps || track, h->aux, stream, h->fork, h->join));
     if (h->stats_on) HIP_TRY(h, hipEventRecord(h->ev[3], stream));
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));
     if (h->stats_on) {
         HIP_TRY(h, hipMemcpyAsync(h->h_long, h->d_long_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, h->d_lskip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_long + 1, L.skip_count, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipEventRecord(h->ev[4], stream));
     }
     HIP_TRY(h, hipStreamSynchronize(stream));
@@ -3200,14 +3284,51 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         h->stats.long_segments = h->h_long[0];
         h->stats.skipped_ranges = h->h_long[1];
     }
-    if (*h->h_err & kErrTime)
-        return fail(h, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than earlier batches");
-    if (*h->h_err & kErrPeriods) return fail(h, SG_E_UNSUPPORTED, "batch spans more than 65536 window periods");
-    if (*h->h_err & kErrBounds)
-        return fail(h, SG_E_INVAL, "an event's origin id (0..n_origins), context id (0..n_contexts-1) or arguments "
-                                   "(the arg / value arrays) are out of range");
-    if (*h->h_err & kErrTableFull) return fail(h, SG_E_CAPACITY, "a param value or thread-count table is full");
-    if (*h->h_err & kErrInternal) return fail(h, SG_E_DEVICE, "internal walker error");
+    rc = local_status(h, *h->h_err);
+    if (rc) return rc;
+    ++h->l_batches;
+    return SG_OK;
+}
+
+// Whether a local batch may go on the pipeline: no node tracking (the pool grows with a host round trip inside the
+// batch), no embedded token server (it shares the cluster flow state and its last timestamp), no rule tables
+// waiting to be uploaded, no per-batch phase timing. Other batches drain the pipeline and run synchronously.
+bool local_pipelinable(sg_handle* h) {
+    const uint64_t want = h->ps_loaded ? h->ps_gen : 0;
+    return h->l_n_origins == 0 && h->l_n_contexts == 0 && h->l_cluster_state != SG_CLUSTER_SERVER &&
+           !(h->l_groups_stale && h->l_cluster_rules) && h->l_ps_applied == want && !h->stats_on;
+}
+
+// One local batch on the pipeline, as enqueue_flow_pipelined: its front half (validation, sort, segments, exit
+// positions) on s_front waits for the back half of the batch two back (same workspace) and runs beside the previous
+// batch's walkers; its back half on s_back follows its front half and the previous batch's back half (the batches
+// share the window state), and checks the first timestamp against last_ts once that batch has advanced it.
+int enqueue_local_pipelined(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, int* err_dst,
+                            hipEvent_t done) {
+    int rc = pipe_setup(h);
+    if (rc) return rc;
+    const int x = (int)(h->pipe_seq & 1);
+    LocalBufs b;
+    rc = local_bufs(h, x, b);
+    if (rc) return rc;
+    LArgs L;
+    BatchArgs sgm;
+    rc = local_args(h, b, ev, nullptr, n, nullptr, 0, nullptr, 0, out, false, L, sgm);
+    if (rc) return rc;
+    L.defer_last = 1;
+    if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
+    rc = local_front(h, L, sgm, h->s_front);
+    if (rc) return rc;
+    rc = local_sort(h, L, sgm, b.rec_sorted, h->s_front);
+    if (rc) return rc;
+    HIP_TRY(h, launch_local_exits(L, h->s_front));
+    HIP_TRY(h, hipEventRecord(h->front_done[x], h->s_front));
+    HIP_TRY(h, hipStreamWaitEvent(h->s_back, h->front_done[x], 0));
+    HIP_TRY(h, launch_local_back(L, sgm, h->l_has_cx || h->l_has_cx_ps, h->s_aux2, h->s_back, h->pfork, h->pjoin));
+    HIP_TRY(h, hipMemcpyAsync(err_dst, L.err, sizeof(int), hipMemcpyDeviceToHost, h->s_back));
+    HIP_TRY(h, hipEventRecord(h->back_done[x], h->s_back));
+    if (done) HIP_TRY(h, hipEventRecord(done, h->s_back));
+    h->pipe_seq++;
     ++h->l_batches;
     return SG_OK;
 }
@@ -3223,6 +3344,43 @@ int sg_slot_decide_batch(sg_handle* h, const sg_local_event* ev, const sg_slot_e
                          sg_local_result* out, void* stream) {
     return local_decide(h, ev, ext, n, args, n_args, values, n_values, out, stream);
 }
+
+int sg_local_enqueue(sg_handle* h, const sg_local_event* ev, uint64_t n, sg_local_result* out, uint64_t* ticket) {
+    if (!h || !ticket) return SG_E_INVAL;
+    *ticket = 0;
+    if (n == 0) return SG_OK;
+    if (!ev || !out) return fail(h, SG_E_INVAL, "null buffer");
+    if (n > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "batch larger than max_batch");
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!local_pipelinable(h)) {  // the synchronous path (after the pipeline drained); its status waits for the ticket
+        const int rc = local_decide(h, ev, nullptr, n, nullptr, 0, nullptr, 0, out, nullptr);
+        if (rc == SG_E_DEVICE) return rc;
+        *ticket = h->next_ticket++;
+        h->finished[*ticket] = rc;
+        return SG_OK;
+    }
+    sg_handle::DevTicket& d = h->dev[h->next_ticket % kDevSlots];
+    if (!d.done) {
+        if (hipHostMalloc(&d.h_err, sizeof(int)) != hipSuccess) return fail(h, SG_E_NOMEM, "pinned error word");
+        HIP_TRY(h, hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    }
+    if (d.ticket) {  // every slot in flight: complete the oldest (its status waits in `finished`)
+        hipError_t e = hipEventSynchronize(d.done);
+        h->finished[d.ticket] = e != hipSuccess ? fail(h, SG_E_DEVICE, hipGetErrorString(e)) : ticket_status(h, d);
+        d.ticket = 0;
+    }
+    const int rc = enqueue_local_pipelined(h, ev, n, out, d.h_err, d.done);
+    if (rc) return rc;
+    d.local = true;
+    d.ticket = h->next_ticket++;
+    *ticket = d.ticket;
+    return SG_OK;
+}
+
+int sg_local_poll(sg_handle* h, uint64_t ticket) { return sg_flow_poll(h, ticket); }
+
+int sg_local_wait(sg_handle* h, uint64_t ticket) { return sg_flow_wait(h, ticket); }
 
 int sg_slot_decide_batch_host(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext, uint64_t n,
                               const sg_pslot_arg* args, uint64_t n_args, const uint64_t* values, uint64_t n_values,
@@ -3285,6 +3443,7 @@ namespace {
 // One node's windows (resource or origin node) in the sg_local_read_state layout.
 int local_read_node(sg_handle* h, uint32_t node, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     const int S = h->lcfg.sample_count;
     std::vector<LBucket> sb(S), mb(kMinuteS);
     std::vector<LFuture> fb(S);
@@ -3437,6 +3596,7 @@ int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3) {
         return SG_OK;
     }
     HIP_TRY(h, hipSetDevice(h->device));
+    drain_async(h);
     LCtl c;
     HIP_TRY(h, hipMemcpy(&c, h->d_lctl + slot, sizeof(LCtl), hipMemcpyDeviceToHost));
     state3[0] = c.stored;
@@ -3530,6 +3690,7 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     if (n_contexts > 0 && h->l_n_contexts == 0 && h->l_batches > 0)
         return fail(h, SG_E_UNSUPPORTED, "context tracking (n_contexts >= 1) starts before the first batch: a DefaultNode "
                                          "holds every entry of its context since the resource's first one");
+    drain_async(h);  // batches on the pipeline decide under the rules they were enqueued with
     const bool track_ctx = n_contexts > 0;
     const uint32_t K = (uint32_t)h->ltab.size();
     const int cold = h->lcfg.cold_factor > 1 ? h->lcfg.cold_factor : 3;

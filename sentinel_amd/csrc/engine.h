@@ -632,6 +632,8 @@ struct LArgs {
     uint32_t* np;
     int* err;
     int64_t* last_ts;
+    int32_t defer_last;       // 1 (pipelined batches): k_local_check_last, in the back half, compares the first
+                              // timestamp with last_ts once the previous batch has advanced it; 0: k_local_prep does
     const sg_slot_ext* ext;   // per event: context and arguments (nullable: context 0, null args)
     int32_t n_contexts;       // context ids 0 .. n_contexts - 1
     const uint32_t* gkey;     // [K] record key of each resource (its RELATE group's first resource), or null
@@ -682,6 +684,12 @@ struct LSkip {                   // entries [b0, b1) of resource k, all FLOW-blo
 
 hipError_t launch_local_prep(const LArgs& L, hipStream_t stream);
 hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
+                             hipEvent_t fork, hipEvent_t join);
+// launch_local_walk in two halves for the pipelined local path: the exit-position list (reads only the batch's
+// sorted records: front half), then the cross-batch time check when deferred, the walkers, the skipped BLOCK counts
+// and last_ts (back half, in batch order).
+hipError_t launch_local_exits(const LArgs& L, hipStream_t stream);
+hipError_t launch_local_back(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);
 // Empty nodes [lo, hi) of the node arrays L.head / sec / bor / minute.

@@ -128,7 +128,8 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         const sg_local_event e = a.ev[i];
         const int64_t t = e.ts_ms;
         if (i == 0) {
-            if (t < 0 || t < *a.last_ts || (a.c3_last_ts && t < *a.c3_last_ts)) atomicOr(a.err, kErrTime);
+            if (t < 0 || (!a.defer_last && t < *a.last_ts) || (a.c3_last_ts && t < *a.c3_last_ts))
+                atomicOr(a.err, kErrTime);
             for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
         } else {
             const int64_t tp = a.ev[i - 1].ts_ms;
@@ -1656,6 +1657,11 @@ __global__ void __launch_bounds__(256) k_lskip_apply(LArgs a) {
     }
 }
 
+// The pipelined batch's first timestamp against the previous batch's last (k_local_prep ran before that batch ended).
+__global__ void k_local_check_last(LArgs a) {
+    if (a.n > 0 && a.ev[0].ts_ms < *a.last_ts) atomicOr(a.err, kErrTime);
+}
+
 __global__ void k_local_finish(LArgs a) {
     if (*a.err == 0 && a.n > 0) {
         *a.last_ts = a.ev[a.n - 1].ts_ms;
@@ -1825,15 +1831,20 @@ hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_
     return hipGetLastError();
 }
 
-hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, bool has_cx, hipStream_t aux, hipStream_t stream,
-                             hipEvent_t fork, hipEvent_t join) {
-    static unsigned bl = 0, bs = 0;
-    if (bl == 0) bl = lresident((const void*)k_lwalk_long);
-    if (bs == 0) bs = lresident((const void*)k_lwalk_short);
+hipError_t launch_local_exits(const LArgs& a, hipStream_t stream) {
     const uint32_t tiles = (uint32_t)((a.n + kLTile - 1) / kLTile);
     hipLaunchKernelGGL(k_lexit_count, dim3(tiles), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(k_lexit_scan, dim3(1), dim3(1024), 0, stream, a, tiles);
     hipLaunchKernelGGL(k_lexit_write, dim3(tiles), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, hipStream_t aux, hipStream_t stream,
+                             hipEvent_t fork, hipEvent_t join) {
+    static unsigned bl = 0, bs = 0;
+    if (bl == 0) bl = lresident((const void*)k_lwalk_long);
+    if (bs == 0) bs = lresident((const void*)k_lwalk_short);
+    if (a.defer_last) hipLaunchKernelGGL(k_local_check_last, dim3(1), dim3(1), 0, stream, a);
     hipError_t e = hipEventRecord(fork, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e != hipSuccess) return e;
@@ -1846,6 +1857,13 @@ hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     hipLaunchKernelGGL(k_lskip_apply, dim3(1024), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(k_local_finish, dim3(1), dim3(1), 0, stream, a);
     return hipGetLastError();
+}
+
+hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, bool has_cx, hipStream_t aux, hipStream_t stream,
+                             hipEvent_t fork, hipEvent_t join) {
+    const hipError_t e = launch_local_exits(a, stream);
+    if (e != hipSuccess) return e;
+    return launch_local_back(a, sg, has_cx, aux, stream, fork, join);
 }
 
 }  // namespace sg

@@ -335,7 +335,7 @@ size_t radix_hist_words(uint64_t n) {
 int radix_digit_bits(int bits) { return ((bits > 16 && bits <= 20) || (bits > 24 && bits <= 30)) ? 10 : 8; }
 
 template <int D>
-static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
+static hipError_t radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
                        bool hist_ready, const SegMark* mark, bool csum_ready) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
@@ -344,7 +344,10 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
     uint32_t* tot = csum + (size_t)nchunks * (1u << D);          // [bins]
     if (!hist_ready) {
         const bool atom = radix_csum_atomic();
-        if (atom) hipMemsetAsync(csum, 0, radix_csum_bytes(n, D), stream);
+        if (atom) {
+            const hipError_t e = hipMemsetAsync(csum, 0, radix_csum_bytes(n, D), stream);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles,
                            atom ? csum : nullptr);
         csum_ready = atom;
@@ -359,6 +362,7 @@ static void radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint
     else
         hipLaunchKernelGGL((k_radix_scatter<D, false>), dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift,
                            hist, ntiles, tot, SegMark{});
+    return hipGetLastError();
 }
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),
@@ -374,8 +378,9 @@ hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, 
         const bool ready = shift == lo_bit && first_hist_ready;
         const SegMark* mk = shift + D >= hi_bit ? mark : nullptr;  // the last pass marks the segments
         const bool cready = ready && first_csum_ready;
-        if (D == 10) radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready, mk, cready);
-        else radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready, mk, cready);
+        const hipError_t e = D == 10 ? radix_pass<10>(src, dst, n, shift, hist_ws, stream, ready, mk, cready)
+                                     : radix_pass<8>(src, dst, n, shift, hist_ws, stream, ready, mk, cready);
+        if (e != hipSuccess) return e;
         uint64_t* t = src;
         src = dst;
         dst = t;

@@ -27,7 +27,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_conc_set_rule_timeouts", "sg_conc_decide_batch", "sg_conc_decide_batch_host", "sg_conc_expire",
            "sg_conc_read_state", "sg_local_metrics", "sg_cparam_top_values", "sg_cparam_last_rounds",
            "sg_pslot_load_rules", "sg_pslot_decide_batch", "sg_pslot_decide_batch_host", "sg_pslot_thread_count",
-           "sg_pslot_param_idx", "sg_rls_should_rate_limit",
+           "sg_pslot_param_idx", "sg_rls_should_rate_limit", "sg_local_enqueue", "sg_local_poll", "sg_local_wait",
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state",
            "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
            "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
@@ -92,6 +92,9 @@ def load_library():
         "sg_cparam_read_sum": (C.c_int, [vp, u32, u64, i64, vp]),
         "sg_local_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
         "sg_local_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_local_enqueue": (C.c_int, [vp, vp, u64, vp, C.POINTER(u64)]),
+        "sg_local_poll": (C.c_int, [vp, u64]),
+        "sg_local_wait": (C.c_int, [vp, u64]),
         "sg_local_read_state": (C.c_int, [vp, u32, vp, vp, vp, vp]),
         "sg_local_load_flow_rules": (C.c_int, [vp, vp, u32, C.c_int32, C.c_int32]),
         "sg_local_read_context_state": (C.c_int, [vp, u32, C.c_int32, vp, vp, vp, vp]),
@@ -530,6 +533,22 @@ class FlowEngine:
     def local_decide_device(self, ev_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
         self._check(self._L.sg_local_decide_batch(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr),
                                                   C.c_void_p(stream_ptr)))
+
+    def local_enqueue(self, ev_ptr: int, n: int, out_ptr: int) -> int:
+        """sg_local_enqueue: a device-resident local batch on the pipelined path (its front half beside the previous
+        batch's walkers); returns the ticket for local_wait. The buffers must stay untouched until it completes."""
+        t = C.c_uint64()
+        self._check(self._L.sg_local_enqueue(self.h, C.c_void_p(ev_ptr), n, C.c_void_p(out_ptr), C.byref(t)))
+        return t.value
+
+    def local_wait(self, ticket):
+        self._check(self._L.sg_local_wait(self.h, ticket))
+
+    def local_poll(self, ticket) -> bool:
+        r = self._L.sg_local_poll(self.h, ticket)
+        if r < 0:
+            self._check(r)
+        return r == 1
 
     def local_state(self, res):
         """(second [S][8], borrow [S][2], minute [60][8], head[14]) — see sg_local_read_state."""
