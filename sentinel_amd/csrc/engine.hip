@@ -166,8 +166,11 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
             st = SG_STATUS_BLOCKED;  // walkers write only non-BLOCKED
         }
-        store_result(a.out, (uint32_t)i, st, 0, 0);
-        a.rec[i] = rec;
+        int32_t* o = &a.out[i].status;  // the default result {st, 0, 0}
+        st_stream(o, st);
+        st_stream(o + 1, 0);
+        st_stream(o + 2, 0);
+        st_stream(a.rec + i, rec);
         if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
     }
     if (a.hist0) {

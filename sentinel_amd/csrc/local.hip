@@ -186,8 +186,9 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         }
         // default result: FlowException for entries (the common outcome of a saturated resource; the walkers
         // write every other outcome), plain 0 for exits and events of unknown resources
-        lstore(a, (uint32_t)i, (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS, 0);
-        a.rec[i] = rec;
+        const uint32_t dst = (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS;
+        st_stream(reinterpret_cast<uint64_t*>(a.out + i), (uint64_t)dst);  // {status, wait_ms 0}
+        st_stream(a.rec + i, rec);
         if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
     }
     if (a.hist0) {

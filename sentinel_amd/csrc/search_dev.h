@@ -61,4 +61,19 @@ __device__ __forceinline__ double avg_div(double x, double isec) {
     return x / isec;
 }
 
+// Streaming stores for the prep kernels' outputs (default results, packed records: written once, read by a later
+// kernel): non-temporal, so a batch's front half does not fill L2 with lines the walkers beside it would have used.
+// SG_NT_PREP=0 builds plain stores.
+#ifndef SG_NT_PREP
+#define SG_NT_PREP 1
+#endif
+template <class T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+#if SG_NT_PREP
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 }  // namespace sg
