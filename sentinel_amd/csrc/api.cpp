@@ -303,7 +303,7 @@ struct sg_handle {
     bool d2h_kernel = false;          // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=1; the
                                       // copy engine measured faster: 2.64 vs 2.45 G decisions/s end to end)
     int d2h_blocks = 64;              // its workgroups (env SG_D2H_BLOCKS)
-    int front_eighths = 4;            // CU partition of the pipeline streams (pipe_setup; round 4: 4/8 beat 3/8 by ~1.5%)
+    int front_eighths = 3;            // CU partition of the pipeline streams (pipe_setup; round 4, final kernels: 3/8 beats 4/8 by 1.1 %)
     int walk_cus = 0;                 // CUs of the walkers' streams when partitioned (0 = all)
     struct DevTicket {                // sg_flow_enqueue batches in flight
         uint64_t ticket = 0;
