@@ -1898,12 +1898,17 @@ static unsigned resident_blocks(const void* kernel, int block, int cus_used) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0);
-    if (cus_used > 0 && cus_used < cus) cus = cus_used;
+    const bool all = !(cus_used > 0 && cus_used < cus);
+    if (!all) cus = cus_used;
     unsigned b = (unsigned)((cus > 0 ? cus : 256) * (per_cu > 0 ? per_cu : 1));
+    // on the whole chip (synchronous batches) twice that: the waves stride over the segments statically, and blocks
+    // that start as others finish even out the lanes' uneven work (r04: one batch 0.965 -> 0.91 ms); on the pipeline's
+    // walker CUs, beside the next batch's front half, exactly what fits (oversubscribed there: +1-2 %)
+    if (all) b *= 2;
     // env SG_WALK_PCT (tuning): persistent walker grids at this percentage of what is resident at once
     if (const char* e = std::getenv("SG_WALK_PCT")) {
         const long pct = std::strtol(e, nullptr, 10);
-        if (pct > 0 && pct < 100) b = std::max(1u, (unsigned)(b * pct / 100));
+        if (pct > 0 && pct <= 400) b = std::max(1u, (unsigned)(b * pct / 100));
     }
     return b;
 }
