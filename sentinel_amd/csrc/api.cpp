@@ -3183,12 +3183,18 @@ int local_front(sg_handle* h, LArgs& L, BatchArgs& sgm, hipStream_t stream) {
     return SG_OK;
 }
 
-int local_sort(sg_handle* h, LArgs& L, BatchArgs& sgm, uint64_t* spare, hipStream_t stream) {
+// count_exits: k_seg also counts the exit records per exit tile (k_lexit_count's pass, pipelined path)
+int local_sort(sg_handle* h, LArgs& L, BatchArgs& sgm, uint64_t* spare, hipStream_t stream, bool count_exits = false) {
     uint64_t* sorted = nullptr;
     HIP_TRY(h, radix_sort_records(L.rec, spare, L.n, L.kshift, L.hist0, &sorted, stream, 64, true, nullptr,
                                   L.csum0 != nullptr));
     L.rec_sorted = sorted;
     sgm.rec_sorted = sorted;
+    if (count_exits) {
+        HIP_TRY(h, hipMemsetAsync(L.exit_cnt, 0, sizeof(uint32_t) * (L.n / kLTile + 2), stream));
+        sgm.exit_cnt = L.exit_cnt;
+        sgm.exit_amask = L.amask;
+    }
     HIP_TRY(h, launch_seg(sgm, stream));
     return SG_OK;
 }
@@ -3319,9 +3325,9 @@ int enqueue_local_pipelined(sg_handle* h, const sg_local_event* ev, uint64_t n, 
     if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
     rc = local_front(h, L, sgm, h->s_front);
     if (rc) return rc;
-    rc = local_sort(h, L, sgm, b.rec_sorted, h->s_front);
+    rc = local_sort(h, L, sgm, b.rec_sorted, h->s_front, true);
     if (rc) return rc;
-    HIP_TRY(h, launch_local_exits(L, h->s_front));
+    HIP_TRY(h, launch_local_exits(L, h->s_front, true));
     HIP_TRY(h, hipEventRecord(h->front_done[x], h->s_front));
     HIP_TRY(h, hipStreamWaitEvent(h->s_back, h->front_done[x], 0));
     HIP_TRY(h, launch_local_back(L, sgm, h->l_has_cx || h->l_has_cx_ps, h->s_aux2, h->s_back, h->pfork, h->pjoin));

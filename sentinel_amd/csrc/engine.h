@@ -129,6 +129,8 @@ struct BatchArgs {
                            // i begins (k_long_bounds; nullptr: the wave walker searches for it)
     uint64_t class_off[kClasses]; // first entry of each class slice in short_list
     uint32_t short_max;  // segments longer than this go to the wave walker
+    uint32_t* exit_cnt;  // local chain: k_seg also counts the exit records per kLTile-record tile into exit_cnt[1 + t]
+    uint64_t exit_amask; // (zeroed before; an exit is a record of a resource whose kind bits (amask >> 1 & 3) are set)
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
                          // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr,
                          // 128 = length class 0 through k_walk_tiny
@@ -688,7 +690,7 @@ hipError_t launch_local_walk(const LArgs& L, const BatchArgs& seg, bool has_cx, 
 // launch_local_walk in two halves for the pipelined local path: the exit-position list (reads only the batch's
 // sorted records: front half), then the cross-batch time check when deferred, the walkers, the skipped BLOCK counts
 // and last_ts (back half, in batch order).
-hipError_t launch_local_exits(const LArgs& L, hipStream_t stream);
+hipError_t launch_local_exits(const LArgs& L, hipStream_t stream, bool counted);  // counted: by k_seg
 hipError_t launch_local_back(const LArgs& L, const BatchArgs& seg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join);
 hipError_t launch_local_init(const LArgs& L, hipStream_t stream);

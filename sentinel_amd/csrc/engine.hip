@@ -771,7 +771,13 @@ __global__ void __launch_bounds__(kSegThreads) k_seg(BatchArgs a) {
 #pragma unroll
         for (int u = 0; u < kSegItems; ++u) {
             const uint64_t j = t0 + ((uint64_t)(wave * kSegItems + u) << 6) + lane;
-            key[u] = j < n ? (uint32_t)(a.rec_sorted[j] >> a.kshift) : 0xFFFFFFFFu;
+            const uint64_t r = j < n ? a.rec_sorted[j] : ~0ull;
+            key[u] = j < n ? (uint32_t)(r >> a.kshift) : 0xFFFFFFFFu;
+            if (a.exit_cnt) {  // the local chain's exit records of this 64-record row (one exit tile holds the row)
+                const uint64_t xm = __ballot(key[u] < a.K && ((r & a.exit_amask) >> 1 & 3ull) != 0);
+                const uint64_t j0 = t0 + ((uint64_t)(wave * kSegItems + u) << 6);
+                if (xm && lane == 0) atomicAdd(a.exit_cnt + 1 + j0 / kLTile, (uint32_t)__popcll(xm));
+            }
         }
         const uint64_t jw = t0 + ((uint64_t)(wave * kSegItems) << 6);  // the wave's first record
         const uint32_t before = (jw > 0 && jw < n) ? (uint32_t)(a.rec_sorted[jw - 1] >> a.kshift) : 0xFFFFFFFFu;

@@ -1832,9 +1832,9 @@ hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_
     return hipGetLastError();
 }
 
-hipError_t launch_local_exits(const LArgs& a, hipStream_t stream) {
+hipError_t launch_local_exits(const LArgs& a, hipStream_t stream, bool counted) {
     const uint32_t tiles = (uint32_t)((a.n + kLTile - 1) / kLTile);
-    hipLaunchKernelGGL(k_lexit_count, dim3(tiles), dim3(256), 0, stream, a);
+    if (!counted) hipLaunchKernelGGL(k_lexit_count, dim3(tiles), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(k_lexit_scan, dim3(1), dim3(1024), 0, stream, a, tiles);
     hipLaunchKernelGGL(k_lexit_write, dim3(tiles), dim3(256), 0, stream, a);
     return hipGetLastError();
@@ -1862,7 +1862,7 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
 
 hipError_t launch_local_walk(const LArgs& a, const BatchArgs& sg, bool has_cx, hipStream_t aux, hipStream_t stream,
                              hipEvent_t fork, hipEvent_t join) {
-    const hipError_t e = launch_local_exits(a, stream);
+    const hipError_t e = launch_local_exits(a, stream, false);
     if (e != hipSuccess) return e;
     return launch_local_back(a, sg, has_cx, aux, stream, fork, join);
 }
