@@ -174,11 +174,26 @@ typedef struct sg_param_req {
 #define SG_ARG_NULL        0
 #define SG_ARG_VALUE       1
 #define SG_ARG_COLLECTION  2
+/* ParamFlowRule.clusterMode with its ParamFlowClusterConfig (cluster_mode: SG_CLUSTER_MODE_* as for flow rules,
+ * below). passCheck sends a clusterMode QPS rule to passClusterCheck (ParamFlowChecker.java:71-73, :278-303): on a
+ * node that is neither token client nor server (sg_local_set_cluster_state, NOT_STARTED the default) pickClusterService
+ * is null and fallbackToLocalOrPass (:305-313) applies — SG_CLUSTER_MODE_FALLBACK checks the rule locally,
+ * SG_CLUSTER_MODE_NO_FALLBACK passes it. On a node whose embedded token server runs on this handle (SERVER) the rule
+ * requests a param token for all of the argument's values (toCollection) from the handle's cluster param state
+ * (sg_cparam_load_rules, the namespace limiter included: DefaultTokenService.requestParamToken →
+ * ClusterParamFlowChecker.acquireClusterToken) in event order: OK passes, BLOCKED throws ParamFlowException,
+ * NO_RULE_EXISTS / BAD_REQUEST / TOO_MANY_REQUEST go to fallbackToLocalOrPass. THREAD-grade cluster rules are checked
+ * locally (passCheck's condition). SG_CLUSTER_MODE_INVALID (ParamFlowRuleUtil.checkCluster :54-66 failed: no config,
+ * an invalid window or flowId <= 0) drops the rule at load, as ParamFlowRuleManager does. A token client (CLIENT)
+ * with cluster-mode QPS rules loaded is SG_E_UNSUPPORTED. */
 typedef struct sg_pslot_rule {
     sg_param_rule rule;          /* token bucket / throttle parameters, hot items                          */
     uint32_t      resource;      /* resource index                                                         */
     int32_t       param_idx;     /* ParamFlowRule.paramIdx                                                 */
     int32_t       grade;         /* 0 FLOW_GRADE_THREAD, 1 FLOW_GRADE_QPS                                 */
+    int32_t       cluster_mode;  /* SG_CLUSTER_MODE_* (0: a local rule)                                     */
+    uint32_t      cluster_key;   /* SERVER: ParamFlowClusterConfig.flowId as a rule index of this handle's
+                                    sg_cparam_load_rules (SG_KEY_NO_RULE: the server has no rule for it)     */
     int32_t       reserved;
 } sg_pslot_rule;
 typedef struct sg_pslot_arg {    /* one argument: null, a value, or a collection / array of values        */
@@ -403,7 +418,11 @@ typedef struct sg_local_flow_rule {
  * must not precede the handle's flow batches in time (SG_E_TIME), nor they it. CLIENT sends tokens over the
  * network, which a batch cannot call in order: loading cluster-mode rules in CLIENT state (or entering it while they
  * are loaded) is SG_E_UNSUPPORTED, as is SERVER on a sharded handle (sg_set_shard) whose cluster
- * rules name a limiter-enabled namespace. */
+ * rules name a limiter-enabled namespace. The state is the handle's (one ClusterStateManager per node): it also decides
+ * the cluster-mode ParamFlowRules of sg_pslot_load_rules, in sg_pslot_decide_batch and in the slot chain
+ * (sg_slot_decide_batch). In SERVER state the resources whose cluster-mode param rules share a flowId (a cluster param
+ * rule of sg_cparam_load_rules) or a limiter-enabled namespace walk as one key group, and the batch's events may not
+ * precede the handle's cluster param batches in time (SG_E_TIME), nor they it. */
 #define SG_CLUSTER_CLIENT        0
 #define SG_CLUSTER_SERVER        1
 #define SG_CLUSTER_NOT_STARTED (-1)

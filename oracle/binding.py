@@ -105,6 +105,7 @@ def lib():
         "or_pslot_thread_count": (i64, [vp, u32, C.c_int32, u64]),
         "or_pslot_param_idx": (C.c_int32, [vp, u32]),
         "or_pslot_token_state": (C.c_int, [vp, u32, u64, vp, vp]),
+        "or_pslot_attach_cluster": (C.c_int, [vp, vp, C.c_int]),
         "or_conc_new": (vp, []), "or_conc_free": (None, [vp]),
         "or_conc_set_namespaces": (C.c_int, [vp, vp, u32]), "or_conc_load_rules": (C.c_int, [vp, vp, u32]),
         "or_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
@@ -408,6 +409,14 @@ class ParamFlowSlot:
         lib().or_pslot_decide(self.h, abi.ptr(ev), len(ev), abi.ptr(args) if len(args) else None,
                               abi.ptr(values) if len(values) else None, abi.ptr(out))
         return out
+
+    def attach_cluster(self, cts, state):
+        """ClusterStateManager state for the cluster-mode param rules; SERVER: param tokens from `cts` (a
+        ClusterTokenService with param rules), kept referenced here."""
+        self._cts = cts
+        rc = lib().or_pslot_attach_cluster(self.h, cts.h if cts is not None else None, state)
+        if rc:
+            raise ValueError(f"or_pslot_attach_cluster: {rc}")
 
     def thread_count(self, res, idx, value):
         return int(lib().or_pslot_thread_count(self.h, res, idx, int(value)))

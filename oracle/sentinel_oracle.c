@@ -1338,6 +1338,7 @@ int or_local_attach_cluster(or_local* l, or_cts* cts, int state) {
     if (state == SG_CLUSTER_SERVER && !cts) return SG_E_INVAL;
     l->cts = state == SG_CLUSTER_SERVER ? cts : NULL;
     l->cluster_state = state;
+    if (l->ps) or_pslot_attach_cluster(l->ps, l->cts, state);  /* one ClusterStateManager per node */
     return 0;
 }
 
@@ -1589,7 +1590,10 @@ int or_local_decide(or_local* l, const sg_local_event* ev, uint64_t n, sg_local_
     return or_local_decide_ext(l, ev, NULL, n, NULL, NULL, out);
 }
 
-void or_local_attach_pslot(or_local* l, struct or_pslot* ps) { l->ps = ps; }
+void or_local_attach_pslot(or_local* l, struct or_pslot* ps) {
+    l->ps = ps;
+    if (ps) or_pslot_attach_cluster(ps, l->cts, l->cluster_state);
+}
 
 int64_t or_local_second_sum(or_local* l, uint32_t res, int64_t t, int ev) {
     return res < l->n ? or_leap_get_sum(l->nodes[res].second, t, ev) : 0;
@@ -2006,47 +2010,38 @@ static double cparam_threshold(const or_cts* s, const or_cpr* r, uint64_t value)
 }
 
 /* DefaultTokenService.requestParamToken (DefaultTokenService.java:53-64) → ClusterParamFlowChecker.
- * acquireClusterToken (ClusterParamFlowChecker.java:42-87): all values are checked (first failure blocks,
- * nothing added), then the count is added to every value. */
+ * acquireClusterToken (ClusterParamFlowChecker.java:42-87) for one request of m values at time t: all values are
+ * checked (first failure blocks, nothing added), then the count is added to every value. *remaining: the last
+ * value's nextRemaining (-1 for several values, "remaining is unsupported for multi-values"). */
+static int32_t cts_param_token(or_cts* s, uint32_t key, int64_t t, int32_t acquire, const uint64_t* vals, uint32_t m,
+                               double* remaining) {
+    *remaining = -1;
+    key &= SG_KEY_INDEX;
+    if (key == SG_KEY_BAD || acquire <= 0 || m == 0) return SG_STATUS_BAD_REQUEST;  /* notValidRequest, params empty */
+    if (key >= s->n_prules) return SG_STATUS_NO_RULE_EXISTS;
+    or_cpr* r = &s->prules[key];
+    int ns = r->rule.namespace_id;  /* allowProceed → GlobalRequestLimiter.tryPass(namespace) */
+    if (ns < 0 || (uint32_t)ns >= s->n_ns) return SG_STATUS_TOO_MANY_REQUEST;
+    if (s->limiters[ns] && !or_limiter_try_pass(s->limiters[ns], t)) return SG_STATUS_TOO_MANY_REQUEST;
+    double rem = -1;
+    for (uint32_t v = 0; v < m; v++) {
+        double latest = (double)cpm_get_sum(r->metric, t, vals[v]) / r->metric->isec;  /* getAvg */
+        double next_remaining = cparam_threshold(s, r, vals[v]) - latest - acquire;
+        rem = next_remaining;
+        if (next_remaining < 0) return SG_STATUS_BLOCKED;
+    }
+    for (uint32_t v = 0; v < m; v++) cpm_add(r->metric, t, vals[v], acquire);
+    *remaining = m > 1 ? -1 : rem;
+    return SG_STATUS_OK;
+}
+
 int or_cts_decide_param(or_cts* s, const sg_cparam_req* req, uint64_t n, const uint64_t* values, sg_result* out) {
     for (uint64_t i = 0; i < n; i++) {
         const sg_cparam_req* q = &req[i];
-        uint32_t key = q->key & SG_KEY_INDEX;
-        if (key == SG_KEY_BAD || q->acquire <= 0 || q->value_count == 0) {
-            out[i] = mk(SG_STATUS_BAD_REQUEST, 0, 0);
-            continue;
-        }
-        if (key >= s->n_prules) {
-            out[i] = mk(SG_STATUS_NO_RULE_EXISTS, 0, 0);
-            continue;
-        }
-        or_cpr* r = &s->prules[key];
-        int64_t t = q->ts_ms;
-        int ns = r->rule.namespace_id;  /* allowProceed → GlobalRequestLimiter.tryPass(namespace) */
-        if (ns < 0 || (uint32_t)ns >= s->n_ns) {
-            out[i] = mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0);
-            continue;
-        }
-        if (s->limiters[ns] && !or_limiter_try_pass(s->limiters[ns], t)) {
-            out[i] = mk(SG_STATUS_TOO_MANY_REQUEST, 0, 0);
-            continue;
-        }
-        double remaining = -1;
-        int passed = 1;
-        for (uint32_t v = 0; v < q->value_count; v++) {
-            uint64_t value = values[q->value_begin + v];
-            double latest = (double)cpm_get_sum(r->metric, t, value) / r->metric->isec;  /* getAvg */
-            double next_remaining = cparam_threshold(s, r, value) - latest - q->acquire;
-            remaining = next_remaining;
-            if (next_remaining < 0) {
-                passed = 0;
-                break;
-            }
-        }
-        if (passed)
-            for (uint32_t v = 0; v < q->value_count; v++) cpm_add(r->metric, t, values[q->value_begin + v], q->acquire);
-        if (q->value_count > 1) remaining = -1;  /* remaining is unsupported for multi-values */
-        out[i] = passed ? mk(SG_STATUS_OK, or_d2i(remaining), 0) : mk(SG_STATUS_BLOCKED, 0, 0);
+        double remaining;
+        const int32_t st = cts_param_token(s, q->key, q->ts_ms, q->acquire, values + q->value_begin, q->value_count,
+                                           &remaining);
+        out[i] = st == SG_STATUS_OK ? mk(SG_STATUS_OK, or_d2i(remaining), 0) : mk(st, 0, 0);
     }
     return 0;
 }
@@ -2521,6 +2516,8 @@ struct or_pslot {
     or_tc* tc;
     uint64_t tc_cap, tc_size;
     int64_t now;                  /* the event's TimeUtil time */
+    or_cts* cts;                  /* the embedded token server's DefaultTokenService (cluster_state SERVER) */
+    int cluster_state;            /* ClusterStateManager: SG_CLUSTER_NOT_STARTED (default), SERVER */
 };
 
 or_pslot* or_pslot_new(void) {
@@ -2528,7 +2525,15 @@ or_pslot* or_pslot_new(void) {
     s->pf = or_pf_new();
     s->tc_cap = 1024;
     s->tc = (or_tc*)calloc(s->tc_cap, sizeof(or_tc));
+    s->cluster_state = SG_CLUSTER_NOT_STARTED;
     return s;
+}
+
+int or_pslot_attach_cluster(or_pslot* s, or_cts* cts, int state) {
+    if (state == SG_CLUSTER_SERVER && !cts) return -1;
+    s->cts = cts;
+    s->cluster_state = state;
+    return 0;
 }
 
 void or_pslot_free(or_pslot* s) {
@@ -2629,7 +2634,8 @@ static void pslot_threads(or_pslot* s, uint32_t res, const sg_pslot_arg* args, u
     for (uint32_t idx = 0; idx < na; idx++) {
         int has_map = 0;
         for (uint32_t r = 0; r < s->n && !has_map; r++)
-            has_map = s->rules[r].resource == res && s->inited[r] && s->cur_idx[r] == (int32_t)idx;
+            has_map = s->rules[r].resource == res && s->rules[r].cluster_mode != SG_CLUSTER_MODE_INVALID &&
+                      s->inited[r] && s->cur_idx[r] == (int32_t)idx;
         if (!has_map) continue;
         const sg_pslot_arg* a = &args[idx];
         if (a->kind == SG_ARG_NULL) continue;
@@ -2650,6 +2656,31 @@ static void pslot_threads(or_pslot* s, uint32_t res, const sg_pslot_arg* args, u
     }
 }
 
+/* ParamFlowChecker.passLocalCheck (:78-103): every value of the argument in order, the first failing one blocks */
+static int pslot_local(or_pslot* s, uint32_t r, uint32_t res, int count, const sg_pslot_arg* x, const uint64_t* values) {
+    const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
+    for (uint32_t j = 0; j < m; j++)
+        if (!pslot_single(s, r, res, count, values[x->value_begin + j])) return 0;
+    return 1;
+}
+
+/* ParamFlowChecker.passClusterCheck (:278-303): the embedded server's param token for all of the argument's values
+ * (toCollection) on SERVER — OK passes, BLOCKED blocks, any other status falls back — else (no token service)
+ * fallbackToLocalOrPass (:305-313): the local check with fallbackToLocalWhenFail, a pass without it. */
+static int pslot_cluster(or_pslot* s, uint32_t r, uint32_t res, int count, const sg_pslot_arg* x,
+                         const uint64_t* values) {
+    const sg_pslot_rule* rule = &s->rules[r];
+    if (s->cluster_state == SG_CLUSTER_SERVER && s->cts) {
+        const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
+        double rem;
+        const int32_t st = cts_param_token(s->cts, rule->cluster_key, s->now, count, values + x->value_begin, m, &rem);
+        if (st == SG_STATUS_OK) return 1;
+        if (st == SG_STATUS_BLOCKED) return 0;
+    }
+    if (rule->cluster_mode == SG_CLUSTER_MODE_NO_FALLBACK) return 1;  /* the rule won't be activated: pass */
+    return pslot_local(s, r, res, count, x, values);
+}
+
 /* ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93) for one entry with non-null args: the index of the rule that
  * throws ParamFlowException, or -1 */
 static int pslot_entry(or_pslot* s, uint32_t res, int64_t t, int count, const sg_pslot_arg* a, uint32_t na,
@@ -2658,6 +2689,7 @@ static int pslot_entry(or_pslot* s, uint32_t res, int64_t t, int count, const sg
     if (res >= s->n_res) return -1;
     for (uint32_t r = 0; r < s->n; r++) {
         if (s->rules[r].resource != res) continue;
+        if (s->rules[r].cluster_mode == SG_CLUSTER_MODE_INVALID) continue;  /* isValidRule → checkCluster: never loaded */
         /* applyRealParamIdx(rule, args.length) */
         if (s->cur_idx[r] < 0) s->cur_idx[r] = (-s->cur_idx[r] <= (int32_t)na) ? (int32_t)na + s->cur_idx[r] : -s->cur_idx[r];
         s->inited[r] = 1;                      /* ParameterMetricStorage.initParamMetricsFor */
@@ -2665,9 +2697,11 @@ static int pslot_entry(or_pslot* s, uint32_t res, int64_t t, int count, const sg
         if ((int32_t)na <= idx) continue;      /* args.length <= paramIdx */
         const sg_pslot_arg* x = &a[idx];
         if (x->kind == SG_ARG_NULL) continue;
-        const uint32_t m = x->kind == SG_ARG_COLLECTION ? x->value_count : 1;
-        for (uint32_t j = 0; j < m; j++)
-            if (!pslot_single(s, r, res, count, values[x->value_begin + j])) return (int32_t)r;
+        /* passCheck (:71-75): clusterMode with grade QPS → passClusterCheck, else passLocalCheck */
+        const int ok = (s->rules[r].cluster_mode != SG_CLUSTER_MODE_OFF && s->rules[r].grade == 1)
+                           ? pslot_cluster(s, r, res, count, x, values)
+                           : pslot_local(s, r, res, count, x, values);
+        if (!ok) return (int32_t)r;
     }
     return -1;
 }

@@ -137,6 +137,9 @@ int       or_pslot_decide(or_pslot* s, const sg_pslot_event* ev, uint64_t n, con
 int64_t   or_pslot_thread_count(const or_pslot* s, uint32_t res, int32_t idx, uint64_t v);
 int32_t   or_pslot_param_idx(const or_pslot* s, uint32_t rule);
 int       or_pslot_token_state(const or_pslot* s, uint32_t rule, uint64_t value, int64_t* last_time, int64_t* tokens);
+/* ClusterStateManager state for the cluster-mode param rules (SG_CLUSTER_*); SERVER: they request param tokens from
+ * `cts` (the embedded token server's DefaultTokenService, its or_cts_load_param_rules). */
+int       or_pslot_attach_cluster(or_pslot* s, or_cts* cts, int state);
 
 /* ---------- pace controller: RateLimiterController (core/.../flow/controller/RateLimiterController.java) ---------- */
 typedef struct or_pace or_pace;

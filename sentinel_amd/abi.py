@@ -106,6 +106,7 @@ BEHAVIOR_RATE_LIMITER = 2
 
 # ParamFlowSlot chain (sg_pslot_*)
 PSLOT_RULE_DTYPE = np.dtype([("rule", PARAM_RULE_DTYPE), ("resource", "<u4"), ("param_idx", "<i4"), ("grade", "<i4"),
+                             ("cluster_mode", "<i4"), ("cluster_key", "<u4"),
                              ("reserved", "<i4")], align=True)
 PSLOT_ARG_DTYPE = np.dtype([("value_begin", "<u4"), ("value_count", "<u4"), ("kind", "<i4"), ("reserved", "<i4")],
                            align=True)
@@ -172,7 +173,7 @@ assert LOCAL_EVENT_DTYPE.itemsize == 32 and LOCAL_RES_DTYPE.itemsize == 8
 assert LOCAL_FLOW_RULE_DTYPE.itemsize == 56 and SLOT_EXT_DTYPE.itemsize == 16
 assert CONC_REQ_DTYPE.itemsize == 32 and CONC_RES_DTYPE.itemsize == 16
 assert METRIC_NODE_DTYPE.itemsize == 64
-assert PSLOT_RULE_DTYPE.itemsize == PARAM_RULE_DTYPE.itemsize + 16 and PSLOT_EVENT_DTYPE.itemsize == 32
+assert PSLOT_RULE_DTYPE.itemsize == PARAM_RULE_DTYPE.itemsize + 24 and PSLOT_EVENT_DTYPE.itemsize == 32
 
 
 def ptr(a: np.ndarray) -> C.c_void_p:

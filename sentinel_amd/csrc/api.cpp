@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -229,6 +230,12 @@ struct sg_handle {
     int64_t* d_ps_last_ts = nullptr;
     std::vector<uint32_t> ps_res_rules;  // param rules per resource
     uint64_t ps_gen = 0;              // sg_pslot_load_rules calls so far
+    int32_t* d_ps_cmode = nullptr;    // per rule: SG_CLUSTER_MODE_*
+    uint32_t* d_ps_ckey = nullptr;    // per rule: its flowId's cluster param rule index (embedded server)
+    bool ps_cluster = false;          // some loaded param rule is a cluster-mode QPS rule
+    std::vector<std::pair<uint32_t, uint32_t>> ps_cluster_refs;  // (resource, cluster_key) of those rules
+    uint32_t* d_ps_gkey = nullptr;    // [n_res] key groups of sg_pslot_decide_batch on an embedded server, or null
+    bool ps_groups_stale = true;      // param rules / cluster param rules / namespaces / state changed
     // concurrent cluster tokens (sg_conc_*)
     int32_t* d_cnow = nullptr;        // nowCalls per rule
     double* d_cthr = nullptr;
@@ -320,6 +327,7 @@ struct sg_handle {
 
 namespace {
 PSArgs pslot_args(sg_handle* h);          // below: the ParamFlowSlot state's device arguments
+int pslot_embed(sg_handle* h, PSArgs& s, hipStream_t stream);  // below: its embedded token server (SERVER)
 int ensure_layout(sg_handle* h);          // below: record layout of the loaded rules
 int flow_status(sg_handle* h, int err);   // below: batch error flags -> SG_E_*
 int drain_async(sg_handle* h);  // below: completes the handle's in-flight host-pipeline batches
@@ -426,6 +434,7 @@ int rebuild_wl_table(sg_handle* h) {
 
 int upload_rule_table(sg_handle* h) {
     h->l_groups_stale = true;  // an embedded token server's key groups follow the cluster rules / namespaces
+    h->ps_groups_stale = true;
     int rc = rebuild_wl_table(h);
     if (rc) return rc;
     // Bucket counts stay below thr * (2 + isec) * (2 + maxOccupyRatio): a pass needs PASS sum <= thr * isec,
@@ -649,6 +658,9 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_ps_init);
     dfree(h->d_ps_tc);
     dfree(h->d_ps_last_ts);
+    dfree(h->d_ps_cmode);
+    dfree(h->d_ps_ckey);
+    dfree(h->d_ps_gkey);
     dfree(h->d_cp_owner);
     dfree(h->d_cp_pslot);
     dfree(h->d_cp_long);
@@ -2218,6 +2230,8 @@ int sg_cparam_load_rules(sg_handle* h, const sg_cparam_rule* rules, uint32_t n, 
     h->d_cpring = d_ring;
     h->cprules.assign(rules, rules + n);
     h->cptab = tab;
+    h->l_groups_stale = true;  // cluster-mode param rules group by these rules' flowIds and namespaces
+    h->ps_groups_stale = true;
     h->cp_wls = wls;
     h->cptotal = base;
     h->cpstride = stride;
@@ -3122,6 +3136,8 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
         L.ps.n_args = args ? n_args : 0;
         L.ps.values = values;
         L.ps.n_values = values ? n_values : 0;
+        const int prc = pslot_embed(h, L.ps, 0);  // cluster-mode param rules on the embedded token server
+        if (prc) return prc;
     }
     if (emb) {  // the embedded token server: this handle's cluster flow state
         L.emb = 1;
@@ -3210,7 +3226,7 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
-    if (h->l_groups_stale && h->l_cluster_rules) {
+    if (h->l_groups_stale && (h->l_cluster_rules || h->ps_cluster)) {
         const int grc = local_apply_groups(h);
         if (grc) return grc;
     }
@@ -3302,7 +3318,7 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
 bool local_pipelinable(sg_handle* h) {
     const uint64_t want = h->ps_loaded ? h->ps_gen : 0;
     return h->l_n_origins == 0 && h->l_n_contexts == 0 && h->l_cluster_state != SG_CLUSTER_SERVER &&
-           !(h->l_groups_stale && h->l_cluster_rules) && h->l_ps_applied == want && !h->stats_on;
+           !(h->l_groups_stale && (h->l_cluster_rules || h->ps_cluster)) && h->l_ps_applied == want && !h->stats_on;
 }
 
 // One local batch on the pipeline, as enqueue_flow_pipelined: its front half (validation, sort, segments, exit
@@ -3615,15 +3631,35 @@ int sg_local_set_cluster_state(sg_handle* h, int32_t state) {
     if (!h) return SG_E_INVAL;
     if (state != SG_CLUSTER_CLIENT && state != SG_CLUSTER_SERVER && state != SG_CLUSTER_NOT_STARTED)
         return fail(h, SG_E_INVAL, "cluster state: CLIENT 0, SERVER 1 or NOT_STARTED -1");
-    if (state == SG_CLUSTER_CLIENT && h->l_cluster_rules)
-        return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow rules on a token client: the tokens come over the network, "
-                                         "not in event order (INTEGRATION.md §8)");
-    if (state != h->l_cluster_state) h->l_groups_stale = true;  // embedded-server key groups follow the state
+    if (state == SG_CLUSTER_CLIENT && (h->l_cluster_rules || h->ps_cluster))
+        return fail(h, SG_E_UNSUPPORTED, "cluster-mode flow / param rules on a token client: the tokens come over the "
+                                         "network, not in event order (INTEGRATION.md §8)");
+    if (state != h->l_cluster_state) h->l_groups_stale = h->ps_groups_stale = true;  // key groups follow the state
     h->l_cluster_state = state;
     return SG_OK;
 }
 
 namespace {
+
+// The embedded token server's sharing among the cluster-mode param rules (ParamFlowChecker.passClusterCheck →
+// requestParamToken): rules naming one cluster param rule share its ClusterParamMetric, rules whose cluster param rule
+// lies in a limiter-enabled namespace share its GlobalRequestLimiter (by_slot: a resource per limiter slot, shared with
+// the flow rules' groups). unite(a, b) joins two resources.
+void ps_cluster_unions(sg_handle* h, const std::function<void(uint32_t, uint32_t)>& unite, int* by_slot) {
+    std::unordered_map<uint32_t, uint32_t> by_key;
+    for (const auto& cr : h->ps_cluster_refs) {
+        const uint32_t key = cr.second & SG_KEY_INDEX;
+        if (key >= h->cprules.size()) continue;  // NO_RULE_EXISTS / BAD_REQUEST: no shared state
+        auto it = by_key.emplace(key, cr.first).first;
+        unite(cr.first, it->second);
+        const int ns = h->cprules[key].namespace_id;
+        const int sl = (ns >= 0 && (size_t)ns < h->ns_slot.size()) ? h->ns_slot[ns] : -1;
+        if (sl >= 0) {
+            if (by_slot[sl] < 0) by_slot[sl] = (int)cr.first;
+            unite(cr.first, (uint32_t)by_slot[sl]);
+        }
+    }
+}
 
 // Key groups of the local chain (union-find, smallest resource first): a RELATE rule reads another resource's
 // ClusterNode (FlowRuleChecker.selectReferenceNode :96-112); on an embedded token server the resources whose
@@ -3639,6 +3675,7 @@ int local_apply_groups(sg_handle* h) {
         return x;
     };
     auto unite = [&](uint32_t a, uint32_t b) {
+        if (a >= K || b >= K) return;  // param rules of resources the chain does not have
         const uint32_t x = find(a), y = find(b);
         if (x != y) parent[std::max(x, y)] = std::min(x, y);
     };
@@ -3647,6 +3684,7 @@ int local_apply_groups(sg_handle* h) {
         std::unordered_map<uint32_t, uint32_t> by_key;
         int by_slot[kMaxLim];
         for (int j = 0; j < kMaxLim; ++j) by_slot[j] = -1;
+        if (h->ps_loaded && h->ps_cluster) ps_cluster_unions(h, unite, by_slot);
         for (const auto& cr : h->l_cluster_refs) {
             const uint32_t key = cr.second & SG_KEY_INDEX;
             if (key >= h->K) continue;  // NO_RULE_EXISTS / BAD_REQUEST: no shared state
@@ -4031,6 +4069,8 @@ namespace {
 
 PSArgs pslot_args(sg_handle* h) {
     PSArgs s{};
+    s.cmode = h->d_ps_cmode;
+    s.ckey = h->d_ps_ckey;
     s.p.rules = h->d_prules;
     s.p.n_rules = (uint32_t)h->ptab.size();
     s.p.hot = h->d_phot;
@@ -4050,6 +4090,57 @@ PSArgs pslot_args(sg_handle* h) {
     return s;
 }
 
+// The embedded token server of the cluster-mode param rules (ClusterStateManager SERVER with cluster rules loaded):
+// this handle's cluster param state (sg_cparam_load_rules), its namespace limiters and the param batches' last
+// timestamp. Without cluster param rules every token would be NO_RULE_EXISTS, which falls back as NOT_STARTED does.
+int pslot_embed(sg_handle* h, PSArgs& s, hipStream_t stream) {
+    s.emb = 0;
+    if (!(h->l_cluster_state == SG_CLUSTER_SERVER && h->ps_cluster && h->d_cplast_ts)) return SG_OK;
+    if (h->shard_world > 1 && h->n_lim > 0)
+        return fail(h, SG_E_UNSUPPORTED, "an embedded token server on a sharded handle with namespace limiters: the "
+                                         "limiter exchange covers flow and param batches only");
+    const int rc = cp_rule_limiters(h, stream);
+    if (rc) return rc;
+    s.emb = 1;
+    s.cp = cp_args(h, nullptr, 0, nullptr, 0, nullptr);
+    s.cp_rule_lim = h->cp_any_lim ? h->d_cp_rule_lim : nullptr;
+    s.lim_ring = h->d_lim_ring;
+    for (int j = 0; j < kMaxLim; ++j) s.lim_qps[j] = h->lim_qps[j];
+    s.cp_last_ts = h->d_cplast_ts;
+    return SG_OK;
+}
+
+// Key groups of sg_pslot_decide_batch on an embedded token server (ps_cluster_unions): the record key of each resource.
+int pslot_apply_groups(sg_handle* h) {
+    if (!h->ps_groups_stale) return SG_OK;
+    const uint32_t R = h->ps_nres;
+    std::vector<uint32_t> parent(R);
+    for (uint32_t k = 0; k < R; ++k) parent[k] = k;
+    auto find = [&](uint32_t x) {
+        while (parent[x] != x) x = parent[x] = parent[parent[x]];
+        return x;
+    };
+    auto unite = [&](uint32_t a, uint32_t b) {
+        const uint32_t x = find(a), y = find(b);
+        if (x != y) parent[std::max(x, y)] = std::min(x, y);
+    };
+    int by_slot[kMaxLim];
+    for (int j = 0; j < kMaxLim; ++j) by_slot[j] = -1;
+    if (h->l_cluster_state == SG_CLUSTER_SERVER && h->ps_cluster) ps_cluster_unions(h, unite, by_slot);
+    std::vector<uint32_t> gkey(R);
+    bool groups = false;
+    for (uint32_t k = 0; k < R; ++k) groups = (gkey[k] = find(k)) != k || groups;
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipDeviceSynchronize());
+    dfree(h->d_ps_gkey);
+    if (groups) {
+        if (hipMalloc(&h->d_ps_gkey, sizeof(uint32_t) * R) != hipSuccess) return fail(h, SG_E_NOMEM, "key groups");
+        HIP_TRY(h, hipMemcpy(h->d_ps_gkey, gkey.data(), sizeof(uint32_t) * R, hipMemcpyHostToDevice));
+    }
+    h->ps_groups_stale = false;
+    return SG_OK;
+}
+
 }  // namespace
 
 int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, const sg_param_hot_item* hot,
@@ -4058,15 +4149,30 @@ int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, co
     drain_async(h);
     std::vector<sg_param_rule> pr(n);
     std::vector<std::vector<uint32_t>> per(n_resources);
-    std::vector<int32_t> grade(n), idx(n), zero(n, 0);
+    std::vector<int32_t> grade(n), idx(n), zero(n, 0), cmode(n);
+    std::vector<uint32_t> ckey(n);
+    std::vector<std::pair<uint32_t, uint32_t>> cluster_refs;
     for (uint32_t i = 0; i < n; ++i) {
         if (rules[i].resource >= n_resources) return fail(h, SG_E_INVAL, "rule resource >= n_resources");
         if (rules[i].grade != 0 && rules[i].grade != 1) return fail(h, SG_E_INVAL, "grade must be THREAD or QPS");
+        const int32_t cm = rules[i].cluster_mode;
+        if (cm != SG_CLUSTER_MODE_OFF && cm != SG_CLUSTER_MODE_FALLBACK && cm != SG_CLUSTER_MODE_NO_FALLBACK &&
+            cm != SG_CLUSTER_MODE_INVALID)
+            return fail(h, SG_E_INVAL, "cluster_mode must be SG_CLUSTER_MODE_*");
         pr[i] = rules[i].rule;
-        per[rules[i].resource].push_back(i);  // ParamFlowRuleManager.getRulesOfResource: load order
+        // ParamFlowRuleManager keeps the valid rules only (ParamFlowRuleUtil.isValidRule → checkCluster :54-66), per
+        // resource in load order (getRulesOfResource)
+        if (cm != SG_CLUSTER_MODE_INVALID) per[rules[i].resource].push_back(i);
         grade[i] = rules[i].grade;
         idx[i] = rules[i].param_idx;
+        cmode[i] = cm;
+        ckey[i] = rules[i].cluster_key;
+        if ((cm == SG_CLUSTER_MODE_FALLBACK || cm == SG_CLUSTER_MODE_NO_FALLBACK) && rules[i].grade == 1)
+            cluster_refs.emplace_back(rules[i].resource, rules[i].cluster_key);  // passCheck → passClusterCheck
     }
+    if (!cluster_refs.empty() && h->l_cluster_state == SG_CLUSTER_CLIENT)
+        return fail(h, SG_E_UNSUPPORTED, "cluster-mode param rules on a token client: the tokens come over the network, "
+                                         "not in event order (INTEGRATION.md §8)");
     int rc = sg_param_load_rules(h, pr.data(), n, hot, n_hot);
     if (rc) return rc;
     std::vector<uint32_t> begin(n_resources + 1, 0), list;
@@ -4081,15 +4187,20 @@ int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, co
     dfree(h->d_ps_grade);
     dfree(h->d_ps_idx);
     dfree(h->d_ps_init);
+    dfree(h->d_ps_cmode);
+    dfree(h->d_ps_ckey);
     const size_t n1 = n ? n : 1;
     if (hipMalloc(&h->d_ps_begin, sizeof(uint32_t) * (n_resources + 1)) != hipSuccess ||
         hipMalloc(&h->d_ps_rules, sizeof(uint32_t) * n1) != hipSuccess ||
         hipMalloc(&h->d_ps_grade, sizeof(int32_t) * n1) != hipSuccess ||
-        hipMalloc(&h->d_ps_idx, sizeof(int32_t) * n1) != hipSuccess || hipMalloc(&h->d_ps_init, sizeof(int32_t) * n1) != hipSuccess)
+        hipMalloc(&h->d_ps_idx, sizeof(int32_t) * n1) != hipSuccess || hipMalloc(&h->d_ps_init, sizeof(int32_t) * n1) != hipSuccess ||
+        hipMalloc(&h->d_ps_cmode, sizeof(int32_t) * n1) != hipSuccess || hipMalloc(&h->d_ps_ckey, sizeof(uint32_t) * n1) != hipSuccess)
         return fail(h, SG_E_NOMEM, "param slot rules");
     HIP_TRY(h, hipMemcpy(h->d_ps_begin, begin.data(), sizeof(uint32_t) * (n_resources + 1), hipMemcpyHostToDevice));
+    if (!list.empty()) HIP_TRY(h, hipMemcpy(h->d_ps_rules, list.data(), sizeof(uint32_t) * list.size(), hipMemcpyHostToDevice));
     if (n) {
-        HIP_TRY(h, hipMemcpy(h->d_ps_rules, list.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_ps_cmode, cmode.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
+        HIP_TRY(h, hipMemcpy(h->d_ps_ckey, ckey.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, hipMemcpy(h->d_ps_grade, grade.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, hipMemcpy(h->d_ps_idx, idx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
         HIP_TRY(h, hipMemcpy(h->d_ps_init, zero.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice));
@@ -4106,6 +4217,10 @@ int sg_pslot_load_rules(sg_handle* h, const sg_pslot_rule* rules, uint32_t n, co
     HIP_TRY(h, hipDeviceSynchronize());
     h->ps_nres = n_resources;
     h->ps_loaded = true;
+    h->ps_cluster = !cluster_refs.empty();
+    h->ps_cluster_refs = cluster_refs;
+    h->ps_groups_stale = true;
+    h->l_groups_stale = true;  // the slot chain's key groups include the cluster-mode param rules
     h->ps_res_rules.assign(n_resources, 0);
     for (uint32_t r = 0; r < n_resources; ++r) h->ps_res_rules[r] = (uint32_t)per[r].size();
     ++h->ps_gen;
@@ -4125,7 +4240,12 @@ int sg_pslot_decide_batch(sg_handle* h, const sg_pslot_event* ev, uint64_t n, co
     if (kbits < 1) kbits = 1;
     if (kbits + bits_for(h->cfg.max_batch) > 64) return fail(h, SG_E_UNSUPPORTED, "resources x max_batch too large");
     hipStream_t stream = (hipStream_t)stream_;
+    int rc = pslot_apply_groups(h);
+    if (rc) return rc;
     PSArgs s = pslot_args(h);
+    rc = pslot_embed(h, s, stream);
+    if (rc) return rc;
+    s.gkey = s.emb ? h->d_ps_gkey : nullptr;
     s.ev = ev;
     s.args = args;
     s.n_args = n_args;

@@ -242,42 +242,13 @@ struct PArgs {
     uint32_t short_max;
 };
 
-// ParamFlowSlot chain (param.hip): every param rule of a resource on one lane per resource
+// ParameterMetric's thread counts of the ParamFlowSlot chain (PSArgs below)
 struct alignas(32) PSThread {  // ParameterMetric.threadCountMap entry: (resource, paramIdx) owner word + value
     unsigned long long owner;  // 0 = empty, else (resource + 1) << 32 | (paramIdx + 1)
     uint64_t value;
     int64_t count;
     int64_t pad;
 };
-
-struct PSArgs {
-    PArgs p;                  // rules (token / throttle parameters), hot items, token table
-    const sg_pslot_event* ev;
-    const sg_pslot_arg* args;
-    uint64_t n_args;
-    const uint64_t* values;
-    uint64_t n_values;
-    sg_pslot_result* out;
-    uint64_t n;
-    uint32_t n_res;
-    const uint32_t* res_begin;  // [n_res + 1] the resource's rules: res_rules[res_begin[r] .. res_begin[r + 1])
-    const uint32_t* res_rules;  // rule indices in load order
-    const int32_t* grade;       // per rule
-    int32_t* cur_idx;           // per rule: paramIdx (applyRealParamIdx rewrites a negative one once)
-    int32_t* inited;            // per rule: initParamMetricsFor ran (its paramIdx has a thread map)
-    PSThread* tc;
-    uint64_t tc_mask;
-    uint64_t* rec;              // [resource : high bits][event index]
-    int kshift;
-    uint64_t imask;
-    int* err;
-    int64_t* last_ts;
-};
-
-hipError_t launch_pslot_batch(PSArgs& s, uint64_t* b_buf, uint32_t* hist, hipStream_t stream);
-hipError_t launch_pslot_clear(PSThread* tc, uint64_t n, hipStream_t stream);
-hipError_t launch_pslot_thread_read(const PSArgs& s, uint32_t res, int32_t idx, uint64_t value, int64_t* out,
-                                    hipStream_t stream);
 
 hipError_t launch_param_clear(PSlot* table, uint64_t n, hipStream_t stream);
 // The long-segment walker runs on `aux` beside the short one (fork / join events).
@@ -449,6 +420,46 @@ struct CPTop {                // a (rule, value) window sum for ClusterParamMetr
 };
 hipError_t launch_cp_top(const CPArgs& c, int64_t now, uint64_t per, CPTop* out, unsigned long long* count,
                          hipStream_t stream);
+
+// ParamFlowSlot chain (param.hip): every param rule of a resource on one lane per resource (or key group)
+struct PSArgs {
+    PArgs p;                  // rules (token / throttle parameters), hot items, token table
+    const sg_pslot_event* ev;
+    const sg_pslot_arg* args;
+    uint64_t n_args;
+    const uint64_t* values;
+    uint64_t n_values;
+    sg_pslot_result* out;
+    uint64_t n;
+    uint32_t n_res;
+    const uint32_t* res_begin;  // [n_res + 1] the resource's rules: res_rules[res_begin[r] .. res_begin[r + 1])
+    const uint32_t* res_rules;  // rule indices in load order
+    const int32_t* grade;       // per rule
+    int32_t* cur_idx;           // per rule: paramIdx (applyRealParamIdx rewrites a negative one once)
+    int32_t* inited;            // per rule: initParamMetricsFor ran (its paramIdx has a thread map)
+    PSThread* tc;
+    uint64_t tc_mask;
+    uint64_t* rec;              // [resource : high bits][event index]
+    int kshift;
+    uint64_t imask;
+    int* err;
+    int64_t* last_ts;
+    // cluster-mode rules (ParamFlowChecker.passCheck :71-73 → passClusterCheck :278-303)
+    const int32_t* cmode;        // per rule: SG_CLUSTER_MODE_* (null: every rule is local)
+    const uint32_t* ckey;        // per rule: its flowId's rule index in the embedded server's cluster param state
+    int32_t emb;                 // 1: ClusterStateManager SERVER, the cluster rules request param tokens from `cp`
+    CPArgs cp;                   // the embedded token server's ClusterParamMetrics (rules, hot items, keys, rings)
+    const uint8_t* cp_rule_lim;  // limiter slot of each cluster param rule's namespace (0xFF none), or null
+    LimRing* lim_ring;
+    double lim_qps[kMaxLim];
+    int64_t* cp_last_ts;         // emb: the cluster param batches' last timestamp (time order across both paths)
+    const uint32_t* gkey;        // [n_res] record key of each resource (its embedded-server key group), or null
+};
+
+hipError_t launch_pslot_batch(PSArgs& s, uint64_t* b_buf, uint32_t* hist, hipStream_t stream);
+hipError_t launch_pslot_clear(PSThread* tc, uint64_t n, hipStream_t stream);
+hipError_t launch_pslot_thread_read(const PSArgs& s, uint32_t res, int32_t idx, uint64_t value, int64_t* out,
+                                    hipStream_t stream);
 
 struct FidSlot {      // flowId → rule index, open addressing with linear probing (fid 0 = empty)
     int64_t fid;

@@ -128,7 +128,8 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         const sg_local_event e = a.ev[i];
         const int64_t t = e.ts_ms;
         if (i == 0) {
-            if (t < 0 || (!a.defer_last && t < *a.last_ts) || (a.c3_last_ts && t < *a.c3_last_ts))
+            if (t < 0 || (!a.defer_last && t < *a.last_ts) || (a.c3_last_ts && t < *a.c3_last_ts) ||
+                (a.has_ps && a.ps.emb && t < *a.ps.cp_last_ts))  // the embedded server's flow / param tokens
                 atomicOr(a.err, kErrTime);
             for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
         } else {
@@ -1169,24 +1170,6 @@ __device__ bool pace_step(const LFlowRule& r, LCtl& c, int64_t now, int64_t cost
 
 // ---- the embedded token server (ClusterStateManager SERVER) ----
 
-// RequestLimiter.tryPass (RequestLimiter.java:72-87) over the namespace's UnaryLeapArray(10, 1000) at time t.
-__device__ bool emb_lim_try_pass(LimRing* r, int64_t t, double qps) {
-    const int64_t P = t / kLimWindowMs;
-    const int I = (int)(P % kLimSamples);
-    const int64_t ws = P * kLimWindowMs;
-    if (r->start[I] != ws) {  // currentWindow: create or reset (time-ordered: never an older window)
-        r->start[I] = ws;
-        r->count[I] = 0;
-    }
-    const int64_t lo = ws - (int64_t)(kLimSamples - 1) * kLimWindowMs;
-    int64_t sum = 0;
-    for (int j = 0; j < kLimSamples; ++j)
-        if (r->start[j] != INT64_MIN && r->start[j] >= lo) sum += r->count[j];
-    if (!((double)sum + 1 <= qps)) return false;  // getQps() + 1 <= qpsAllowed (intervalInSecond 1.0)
-    r->count[I] += 1;
-    return true;
-}
-
 __device__ __forceinline__ double c3_qps(int64_t sum, double isec) { return avg_div((double)sum, isec); }
 
 // DefaultTokenService.requestToken (DefaultTokenService.java:39-50) → ClusterFlowChecker.acquireClusterToken
@@ -1667,6 +1650,7 @@ __global__ void k_local_finish(LArgs a) {
     if (*a.err == 0 && a.n > 0) {
         *a.last_ts = a.ev[a.n - 1].ts_ms;
         if (a.c3_last_ts) *a.c3_last_ts = a.ev[a.n - 1].ts_ms;  // the embedded server's token requests came up to here
+        if (a.has_ps && a.ps.emb) *a.ps.cp_last_ts = a.ev[a.n - 1].ts_ms;
     }
 }
 

@@ -403,6 +403,7 @@ __global__ void __launch_bounds__(256) k_psprep(PSArgs s) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < s.n; i += (uint64_t)gridDim.x * blockDim.x) {
         const sg_pslot_event e = s.ev[i];
         if (e.ts_ms < 0 || (i == 0 ? e.ts_ms < *s.last_ts : e.ts_ms < s.ev[i - 1].ts_ms)) atomicOr(s.err, kErrTime);
+        if (i == 0 && s.emb && e.ts_ms < *s.cp_last_ts) atomicOr(s.err, kErrTime);  // the embedded server's param tokens
         sg_pslot_result r;
         r.pass = 1;
         r.rule = -1;
@@ -416,23 +417,25 @@ __global__ void __launch_bounds__(256) k_psprep(PSArgs s) {
                 ok = (uint64_t)a.value_begin + m <= s.n_values;
             }
             if (!ok) atomicOr(s.err, kErrBounds);
-            else rec = ((uint64_t)e.resource << s.kshift) | i;
+            else rec = ((uint64_t)(s.gkey ? s.gkey[e.resource] : e.resource) << s.kshift) | i;
         }
         s.rec[i] = rec;
     }
 }
 
-// One lane per resource segment of the sorted records.
+// One lane per resource segment of the sorted records (per key group on an embedded token server: the resources whose
+// cluster-mode rules share a cluster param rule or a limiter, walked together in event order).
 __global__ void __launch_bounds__(256) k_pswalk(PSArgs s, const uint64_t* sorted) {
     if (*s.err) return;
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < s.n; p += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t res = (uint32_t)(sorted[p] >> s.kshift);
-        if (res >= s.n_res || (p > 0 && (uint32_t)(sorted[p - 1] >> s.kshift) == res)) continue;
+        const uint32_t key = (uint32_t)(sorted[p] >> s.kshift);
+        if (key >= s.n_res || (p > 0 && (uint32_t)(sorted[p - 1] >> s.kshift) == key)) continue;
         for (uint64_t q = p; q < s.n; ++q) {
             const uint64_t rec = sorted[q];
-            if ((uint32_t)(rec >> s.kshift) != res) break;
+            if ((uint32_t)(rec >> s.kshift) != key) break;
             const uint64_t i = rec & s.imask;
             const sg_pslot_event e = s.ev[i];
+            const uint32_t res = e.resource;
             if (e.kind != SG_LOCAL_ENTRY) {  // ParamFlowStatisticExitCallback (passed entries only)
                 ps_threads(s, res, e.arg_begin, e.arg_count, -1);
                 continue;
@@ -451,7 +454,10 @@ __global__ void __launch_bounds__(256) k_pswalk(PSArgs s, const uint64_t* sorted
 }
 
 __global__ void k_psfinish(PSArgs s) {
-    if (*s.err == 0 && s.n > 0) *s.last_ts = s.ev[s.n - 1].ts_ms;
+    if (*s.err == 0 && s.n > 0) {
+        *s.last_ts = s.ev[s.n - 1].ts_ms;
+        if (s.emb) *s.cp_last_ts = s.ev[s.n - 1].ts_ms;  // the embedded server's param tokens came up to here
+    }
 }
 
 __global__ void __launch_bounds__(256) k_psclear(PSThread* tc, uint64_t n) {

@@ -4,6 +4,7 @@
 // exact per-rule value tables, ParameterMetric's thread counts (ParameterMetric.java:125-239) and ParamFlowSlot.checkFlow
 // (ParamFlowSlot.java:66-93).
 #pragma once
+#include "cparam_dev.h"
 #include "engine.h"
 
 namespace sg {
@@ -218,6 +219,72 @@ __device__ inline void ps_threads(const PSArgs& s, uint32_t res, uint32_t arg_be
     }
 }
 
+// RequestLimiter.tryPass (RequestLimiter.java:72-87) over the namespace's UnaryLeapArray(10, 1000) at time t.
+__device__ inline bool emb_lim_try_pass(LimRing* r, int64_t t, double qps) {
+    const int64_t P = t / kLimWindowMs;
+    const int I = (int)(P % kLimSamples);
+    const int64_t ws = P * kLimWindowMs;
+    if (r->start[I] != ws) {  // currentWindow: create or reset (time-ordered: never an older window)
+        r->start[I] = ws;
+        r->count[I] = 0;
+    }
+    const int64_t lo = ws - (int64_t)(kLimSamples - 1) * kLimWindowMs;
+    int64_t sum = 0;
+    for (int j = 0; j < kLimSamples; ++j)
+        if (r->start[j] != INT64_MIN && r->start[j] >= lo) sum += r->count[j];
+    if (!((double)sum + 1 <= qps)) return false;  // getQps() + 1 <= qpsAllowed (intervalInSecond 1.0)
+    r->count[I] += 1;
+    return true;
+}
+
+// DefaultTokenService.requestParamToken (DefaultTokenService.java:53-64) → ClusterParamFlowChecker.acquireClusterToken
+// (ClusterParamFlowChecker.java:42-87) on the embedded token server, for one request of the m values vals at time t: the
+// namespace limiter (allowProceed), every value checked on its window (the first failure blocks and adds nothing), then
+// the count added to every value (addValue: currentWindow resets a stale bucket). One lane walks all requests that
+// share the rule's metric or limiter (key groups), in event order.
+__device__ inline int32_t ps_emb_param_token(const PSArgs& s, uint32_t key, int64_t t, int32_t acq, const uint64_t* vals,
+                                             uint32_t m) {
+    const CPArgs& c = s.cp;
+    key &= SG_KEY_INDEX;
+    if (key == SG_KEY_BAD || acq <= 0 || m == 0) return SG_STATUS_BAD_REQUEST;  // notValidRequest, params.isEmpty()
+    if (key >= c.n_rules) return SG_STATUS_NO_RULE_EXISTS;                      // getParamRuleById == null
+    const uint8_t ls = s.cp_rule_lim ? s.cp_rule_lim[key] : (uint8_t)0xFF;
+    if (ls != 0xFF && !emb_lim_try_pass(s.lim_ring + ls, t, s.lim_qps[ls])) return SG_STATUS_TOO_MANY_REQUEST;
+    const CPRule r = c.rules[key];
+    const int64_t P = t / r.wl;
+    for (uint32_t j = 0; j < m; ++j) {  // getAvg(value): the value's window sum at t / intervalInSecond
+        const uint64_t g = cp_find(c, r, vals[j]);
+        int64_t cur = 0;
+        const int64_t other = g != ~0ull ? cp_window(c.ring + g * (uint64_t)c.stride, r.S, r.wl, P, &cur) : 0;
+        const double rem = cp_threshold(c, r, vals[j]) - avg_div((double)(other + cur), r.isec) - (double)acq;
+        if (rem < 0) return SG_STATUS_BLOCKED;
+    }
+    const int I = (int)(P % r.S);
+    const int64_t ws = P * r.wl;
+    for (uint32_t j = 0; j < m; ++j) {  // addValue(value, count) on currentWindow
+        const uint64_t g = cp_slot(c, r, vals[j]);
+        if (g == ~0ull) {
+            atomicOr(s.err, kErrTableFull);
+            return SG_STATUS_FAIL;
+        }
+        CPBucket& b = c.ring[g * (uint64_t)c.stride + I];
+        if (b.start != ws) {
+            b.start = ws;
+            b.count = 0;
+        }
+        b.count += acq;
+    }
+    return SG_STATUS_OK;
+}
+
+// ParamFlowChecker.passLocalCheck (:78-103) of rule ri on argument a: every value in order, the first failing one blocks
+__device__ inline bool ps_local(const PSArgs& s, uint32_t ri, uint32_t res, int64_t t, int64_t acq, const sg_pslot_arg& a) {
+    const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
+    for (uint32_t j = 0; j < m; ++j)
+        if (!ps_single(s, ri, res, t, acq, s.values[a.value_begin + j])) return false;
+    return true;
+}
+
 // ParamFlowSlot.checkFlow (ParamFlowSlot.java:66-93) for one entry of resource res with non-null args: every rule
 // of the resource in load order — applyRealParamIdx, initParamMetricsFor, passCheck on args[paramIdx] (a collection /
 // array element by element, the state changes before a failing element kept). Returns the index of the rule that
@@ -236,9 +303,18 @@ __device__ inline int32_t ps_check_entry(const PSArgs& s, uint32_t res, int64_t 
         if ((int32_t)arg_count <= idx) continue;
         const sg_pslot_arg a = s.args[arg_begin + (uint32_t)idx];
         if (a.kind == SG_ARG_NULL) continue;
-        const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
-        for (uint32_t j = 0; j < m; ++j)
-            if (!ps_single(s, ri, res, t, (int64_t)count, s.values[a.value_begin + j])) return (int32_t)ri;
+        const int32_t cm = s.cmode ? s.cmode[ri] : SG_CLUSTER_MODE_OFF;
+        if (cm != SG_CLUSTER_MODE_OFF && s.grade[ri] == 1) {  // passClusterCheck (:278-303)
+            if (s.emb) {
+                const uint32_t m = a.kind == SG_ARG_COLLECTION ? a.value_count : 1u;
+                const int32_t st = ps_emb_param_token(s, s.ckey[ri], t, count, s.values + a.value_begin, m);
+                if (st == SG_STATUS_OK) continue;
+                if (st == SG_STATUS_BLOCKED) return (int32_t)ri;
+            }
+            // no token service, or NO_RULE_EXISTS / BAD_REQUEST / TOO_MANY_REQUEST: fallbackToLocalOrPass (:305-313)
+            if (cm == SG_CLUSTER_MODE_NO_FALLBACK) continue;
+        }
+        if (!ps_local(s, ri, res, t, (int64_t)count, a)) return (int32_t)ri;
     }
     return -1;
 }

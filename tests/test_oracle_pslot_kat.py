@@ -132,3 +132,103 @@ def test_several_rules_first_failure_wins():
     out = run(ps, Calls().call(T0, 1, 50).call(T0, 1, 50).call(T0, 1, 51).call(T0, 2, 51))
     assert list(out["pass"]) == [1, 0, 0, 1] and list(out["rule"]) == [-1, 1, 0, -1]
     assert ps.token_state(1, 51)[0] == 3   # only the 4th call reached rule 1 with value 51
+
+
+# ---- cluster-mode ParamFlowRules (ParamFlowChecker.passCheck :71-73 → passClusterCheck :278-303,
+# fallbackToLocalOrPass :305-313). No reference test drives this composition: the expected values below are traced
+# by hand through the Java text (parity unpinned beyond the pinned pieces: the local checks and ClusterParamMetric).
+
+from oracle.binding import ClusterTokenService  # noqa: E402
+
+
+def cluster_rule(mode, key=0, **kw):
+    r = rule(**kw)
+    r["cluster_mode"], r["cluster_key"] = mode, key
+    return r
+
+
+def server(count=2.0, limiter_qps=None, flow_id=100):
+    """An embedded token server with one cluster param rule (GLOBAL, 10 x 100 ms) in namespace 0."""
+    cts = ClusterTokenService()
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    if limiter_qps is not None:
+        ns["limiter_enabled"], ns["max_allowed_qps"] = 1, limiter_qps
+    cts.set_namespaces(ns)
+    pr = np.zeros(1, abi.CPARAM_RULE_DTYPE)
+    pr["flow_id"], pr["count"], pr["threshold_type"] = flow_id, count, abi.THRESHOLD_GLOBAL
+    pr["sample_count"], pr["window_interval_ms"], pr["namespace_id"] = 10, 1000, 0
+    cts.load_param_rules(pr)
+    return cts
+
+
+def test_cluster_rule_not_started_falls_back_to_local():
+    """No token service (NOT_STARTED): fallbackToLocalWhenFail checks the rule locally (count 2: the third call at
+    the same millisecond finds the bucket empty)."""
+    ps = ParamFlowSlot(np.array([cluster_rule(abi.CLUSTER_MODE_FALLBACK, count=2)]))
+    out = run(ps, Calls().call(T0, 5).call(T0, 5).call(T0, 5))
+    assert list(out["pass"]) == [1, 1, 0] and list(out["rule"]) == [-1, -1, 0]
+
+
+def test_cluster_rule_without_fallback_is_not_activated():
+    """fallbackToLocalWhenFail false: "The rule won't be activated, just pass" — even at count 0."""
+    ps = ParamFlowSlot(np.array([cluster_rule(abi.CLUSTER_MODE_NO_FALLBACK, count=0)]))
+    out = run(ps, Calls().call(T0, 5).call(T0, 5).call(T0, [5, 6]))
+    assert list(out["pass"]) == [1, 1, 1]
+    assert ps.token_state(0, 5)[0] == 0   # the local counters were never touched
+
+
+def test_cluster_rule_on_embedded_server():
+    """SERVER: requestParamToken(flowId, count, toCollection(value)) on the embedded server. ClusterParamFlowChecker:
+    threshold 2 - avg - 1 >= 0 passes and adds to every value; BLOCKED throws ParamFlowException (the local count 100
+    is not consulted); a multi-value request is all-or-nothing."""
+    cts = server(count=2)
+    ps = ParamFlowSlot(np.array([cluster_rule(abi.CLUSTER_MODE_FALLBACK, key=0, count=100)]))
+    ps.attach_cluster(cts, abi.CLUSTER_SERVER)
+    c = Calls().call(T0, 5).call(T0, 5).call(T0, 5)          # sums 0, 1 pass; 2: 2 - 2 - 1 < 0 blocks
+    c.call(T0 + 1000, 5)                                      # the T0 bucket left the window (start < ws - 900)
+    c.call(T0 + 1000, [5, 6])                                 # 5: 2 - 1 - 1 = 0, 6: 1 → both added
+    c.call(T0 + 1000, [6, 5])                                 # 6: 0 ok, 5: 2 - 2 - 1 < 0 → blocked, nothing added
+    c.call(T0 + 1000, [6])                                    # 6: sum 1 (the blocked call added nothing) → 0 ok
+    out = run(ps, c)
+    assert list(out["pass"]) == [1, 1, 0, 1, 1, 0, 1]
+    assert list(out["rule"]) == [-1, -1, 0, -1, -1, 0, -1]
+    assert cts.param_sum(0, 5, T0 + 1000) == 2 and cts.param_sum(0, 6, T0 + 1000) == 2
+    assert ps.token_state(0, 5)[0] == 0                        # no local fallback ran
+
+
+def test_cluster_rule_server_without_rule_falls_back():
+    """SERVER, but the server has no rule for the flowId (NO_RULE_EXISTS) → fallbackToLocalOrPass."""
+    cts = server()
+    ps = ParamFlowSlot(np.array([cluster_rule(abi.CLUSTER_MODE_FALLBACK, key=abi.KEY_NO_RULE, count=1),
+                                 cluster_rule(abi.CLUSTER_MODE_NO_FALLBACK, key=abi.KEY_NO_RULE, idx=1, count=0)]))
+    ps.attach_cluster(cts, abi.CLUSTER_SERVER)
+    out = run(ps, Calls().call(T0, 5, 9).call(T0, 5, 9))
+    assert list(out["pass"]) == [1, 0] and list(out["rule"]) == [-1, 0]   # rule 1 passes without fallback
+
+
+def test_cluster_rule_limited_namespace_falls_back():
+    """allowProceed: the namespace limiter (1 QPS) answers TOO_MANY_REQUEST to the second request of the second →
+    fallbackToLocalOrPass; the local count 0 then blocks (tokenCount == 0)."""
+    cts = server(count=10, limiter_qps=1.0)
+    ps = ParamFlowSlot(np.array([cluster_rule(abi.CLUSTER_MODE_FALLBACK, key=0, count=0)]))
+    ps.attach_cluster(cts, abi.CLUSTER_SERVER)
+    out = run(ps, Calls().call(T0, 5).call(T0 + 10, 5).call(T0 + 1500, 5))
+    assert list(out["pass"]) == [1, 0, 1]
+
+
+def test_cluster_thread_rule_and_empty_collection_and_invalid_rule():
+    """passCheck sends only QPS cluster rules to the token server: a THREAD-grade cluster rule is checked locally.
+    An empty collection passes (requestParamToken's BAD_REQUEST falls back to a local check of no values). A rule
+    with an invalid cluster config is never loaded."""
+    cts = server(count=0)
+    rules = np.array([cluster_rule(abi.CLUSTER_MODE_NO_FALLBACK, key=0, grade=THREAD, count=1),
+                      cluster_rule(abi.CLUSTER_MODE_FALLBACK, key=0, idx=1, count=0),
+                      cluster_rule(abi.CLUSTER_MODE_INVALID, key=0, idx=2, count=0)])
+    ps = ParamFlowSlot(rules)
+    ps.attach_cluster(cts, abi.CLUSTER_SERVER)
+    out = run(ps, Calls().call(T0, 5, [], 7).call(T0, 5, [], 7))
+    # call 1: THREAD 0 + 1 <= 1 passes (the entry's thread count is raised on pass); rule 1: empty collection → pass
+    # call 2: THREAD 1 + 1 > 1 blocks
+    assert list(out["pass"]) == [1, 0] and list(out["rule"]) == [-1, 0]
+    assert ps.param_idx(2) == 2   # the invalid rule was never reached (applyRealParamIdx does not run on it)
