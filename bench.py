@@ -204,6 +204,9 @@ def main():
     ap.add_argument("--requests", type=int, default=16_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-batches", type=int, default=16, help="host-buffer batches for the end-to-end figure (0: skip)")
+    ap.add_argument("--limiter-qps", type=float, default=0.0,
+                    help="namespace GlobalRequestLimiter maxAllowedQps (SURVEY §8d C3's second run: 1e12 exercises the "
+                         "pre-pass without rejecting); 0: limiter off, the headline configuration")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -235,7 +238,8 @@ def main():
     eng = FlowEngine(device=local_rank, max_batch=args.requests)
     ns = np.zeros(1, abi.NS_DTYPE)
     ns["connected_count"] = 1
-    ns["max_allowed_qps"] = 30000
+    ns["max_allowed_qps"] = args.limiter_qps if args.limiter_qps > 0 else 30000
+    ns["limiter_enabled"] = 1 if args.limiter_qps > 0 else 0
     eng.set_namespaces(ns)
     eng.load_rules(wl.rules)
 
@@ -320,7 +324,8 @@ def main():
         "config": {"workload": "C3 cluster token server: ClusterFlowChecker, FLOW_THRESHOLD_GLOBAL, S=10/1000 ms",
                    "flow_ids": args.flows, "flow_ids_per_gpu": wl.K, "requests_per_step_per_gpu": args.requests,
                    "simulated_ms_per_step": wl.span_ms, "parallelism": f"hash-sharded flowIds x{world}" + (" (one-device rehearsal)" if one_dev else ""),
-                   "rollup": "RCCL all_reduce + all_gather per step" if world > 1 else "none (1 GPU)"},
+                   "rollup": "RCCL all_reduce + all_gather per step" if world > 1 else "none (1 GPU)",
+                   "namespace_limiter": (f"on, maxAllowedQps {args.limiter_qps:g}" if args.limiter_qps > 0 else "off")},
         "roofline": {"bound": "hbm", "kernel": "whole batch pipeline (prep + sort + walk), step time with batches "
                                                "pipelined (sort of batch i+1 beside the walkers of batch i)",
                      "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_gbs / HBM_PEAK_GBS,

@@ -811,7 +811,10 @@ int sg_codec_encode_flow(sg_handle* h, const int32_t* xid, const uint8_t* kind, 
  *               (responseObserver.onError, :36-40; its descriptors are not requested and get code 0)
  *   status[d]   code (SG_RLS_OK when the result is OK or the rule is missing, :55-58, else SG_RLS_OVER_LIMIT),
  *               and for a descriptor with a rule: limit_remaining = the TokenResult's remaining and
- *               requests_per_unit = (int) rule.getCount() (:67-73), has_rule = 1. */
+ *               requests_per_unit = (int) rule.getCount() (:67-73), has_rule = 1.
+ * A descriptor whose rule is not GLOBAL or lies in a namespace with a limiter (the cluster path would apply them,
+ * SimpleClusterFlowChecker does not) is SG_E_UNSUPPORTED, more descriptors than max_batch SG_E_CAPACITY: both
+ * before any state change. */
 #define SG_RLS_OK          1   /* envoy.service.ratelimit.v3.RateLimitResponse.Code.OK         */
 #define SG_RLS_OVER_LIMIT  2   /* ... Code.OVER_LIMIT                                          */
 #define SG_RLS_ERROR      (-1) /* hits_addend < 0: the call fails                               */

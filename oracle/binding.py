@@ -120,6 +120,7 @@ def lib():
         "or_lgen_new": (vp, [vp]), "or_lgen_free": (None, [vp]), "or_lgen_pending": (u64, [vp]),
         "or_lgen_run": (u64, [vp, vp, vp, vp, u64, i64, vp, vp, u64]),
         "or_rls_decide": (C.c_int, [vp, vp, u64, vp]),
+        "or_rls_should_rate_limit": (C.c_int, [vp, vp, u32, vp, u64, vp, vp]),
         "or_codec_decode_flow": (None, [vp, vp, vp, u64, vp, u32, vp, vp, vp]),
         "or_codec_encode_flow": (None, [vp, vp, vp, u64, vp]),
     }
@@ -288,6 +289,19 @@ class ClusterTokenService:
         out = np.zeros(max(len(req), 1), dtype=abi.RES_DTYPE)
         lib().or_rls_decide(self.h, abi.ptr(req), len(req), abi.ptr(out))
         return out[:len(req)]
+
+    def should_rate_limit(self, req: np.ndarray, desc_rule: np.ndarray):
+        """SentinelEnvoyRlsServiceImpl.shouldRateLimit over sg_rls_request records (the oracle's own restatement of
+        the descriptor mapping): (overall codes per request, sg_rls_status per descriptor)."""
+        req = np.ascontiguousarray(req, dtype=abi.RLS_REQ_DTYPE)
+        desc_rule = np.ascontiguousarray(desc_rule, dtype=np.int32)
+        overall = np.zeros(max(len(req), 1), np.int32)
+        status = np.zeros(max(len(desc_rule), 1), abi.RLS_STATUS_DTYPE)
+        rc = lib().or_rls_should_rate_limit(self.h, abi.ptr(req), len(req), abi.ptr(desc_rule), len(desc_rule),
+                                            abi.ptr(overall), abi.ptr(status))
+        if rc:
+            raise ValueError(f"or_rls_should_rate_limit: {rc}")
+        return overall[:len(req)], status[:len(desc_rule)]
 
     # ---- requestParamToken → ClusterParamFlowChecker
     def load_param_rules(self, rules: np.ndarray, hot: np.ndarray = None):

@@ -2191,6 +2191,50 @@ int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out) {
     return 0;
 }
 
+/* SentinelEnvoyRlsServiceImpl.shouldRateLimit (sentinel-cluster/sentinel-cluster-server-envoy-rls/src/main/java/com/
+ * alibaba/csp/sentinel/cluster/server/envoy/rls/service/v3/SentinelEnvoyRlsServiceImpl.java:34-85), one request after
+ * the other: hits_addend < 0 fails the call (onError :36-40), 0 means 1 (:41-44); every descriptor is checkToken →
+ * SimpleClusterFlowChecker.acquireClusterToken (or_rls_decide above) on its rule (desc_rule: the rule index
+ * EnvoySentinelRuleConverter.generateFlowId resolves to, < 0 or unknown: no rule); NO_RULE_EXISTS passes (:55-58); the
+ * call is OVER_LIMIT when any descriptor is not OK (:60-62); a descriptor with a rule reports (int) rule.getCount() and
+ * the TokenResult's remaining (:66-73). */
+int or_rls_should_rate_limit(or_cts* s, const sg_rls_request* req, uint32_t n, const int32_t* desc_rule,
+                             uint64_t n_desc, int32_t* overall, sg_rls_status* status) {
+    for (uint64_t d = 0; d < n_desc; d++) memset(&status[d], 0, sizeof(sg_rls_status));
+    for (uint32_t j = 0; j < n; j++) {
+        const sg_rls_request* q = &req[j];
+        if ((uint64_t)q->desc_begin + q->desc_count > n_desc) return SG_E_INVAL;
+        if (q->hits_addend < 0) {
+            overall[j] = SG_RLS_ERROR;
+            continue;
+        }
+        const int acquire = q->hits_addend == 0 ? 1 : q->hits_addend;
+        int blocked = 0;
+        for (uint32_t i = 0; i < q->desc_count; i++) {
+            const int32_t rule = desc_rule[q->desc_begin + i];
+            const int has_rule = rule >= 0 && (uint32_t)rule < s->n_rules;
+            sg_req one;
+            one.ts_ms = q->ts_ms;
+            one.key = has_rule ? (uint32_t)rule : SG_KEY_NO_RULE;
+            one.acquire = acquire;
+            sg_result r;
+            or_rls_decide(s, &one, 1, &r);
+            int st = r.status;
+            if (st == SG_STATUS_NO_RULE_EXISTS) st = SG_STATUS_OK;
+            if (st != SG_STATUS_OK) blocked = 1;
+            sg_rls_status* o = &status[q->desc_begin + i];
+            o->code = st == SG_STATUS_OK ? SG_RLS_OK : SG_RLS_OVER_LIMIT;
+            if (has_rule) {
+                o->has_rule = 1;
+                o->requests_per_unit = or_d2i(s->rules[rule].count);
+                o->limit_remaining = r.remaining;
+            }
+        }
+        overall[j] = blocked ? SG_RLS_OVER_LIMIT : SG_RLS_OK;
+    }
+    return 0;
+}
+
 /* ===================================================================================== */
 /* Concurrent cluster tokens: ConcurrentClusterFlowChecker (srv/flow/ConcurrentClusterFlowChecker.java:34-101), */
 /* CurrentConcurrencyManager (nowCalls per flowId), TokenCacheNodeManager (the token map) and              */

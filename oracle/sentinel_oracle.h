@@ -236,6 +236,9 @@ uint64_t or_conc_live(const or_conc* c);
 
 /* ---------- Envoy RLS (SimpleClusterFlowChecker over the same ClusterMetric) ---------- */
 int or_rls_decide(or_cts* s, const sg_req* req, uint64_t n, sg_result* out);
+/* SentinelEnvoyRlsServiceImpl.shouldRateLimit over a batch of RateLimitRequests (sg_rls_should_rate_limit's contract). */
+int or_rls_should_rate_limit(or_cts* s, const sg_rls_request* req, uint32_t n, const int32_t* desc_rule,
+                             uint64_t n_desc, int32_t* overall, sg_rls_status* status);
 
 /* ---------- token-server wire codec (srv/server/codec and the cluster-common codec package) ---------- */
 /* Decodes n frame payloads (frame i = payload[offsets[i] .. offsets[i+1])) as the default token server

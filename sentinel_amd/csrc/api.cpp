@@ -1702,7 +1702,7 @@ int sg_flow_decide_batch_host(sg_handle* h, const sg_req* req, uint64_t n, sg_re
 }
 
 // Envoy RLS (SentinelEnvoyRlsServiceImpl.shouldRateLimit, service/v3/SentinelEnvoyRlsServiceImpl.java:34-85): every
-// descriptor of the batch one token request of one device batch (chunked by max_batch), then the per-request codes.
+// descriptor of the batch one token request of one device batch (at most max_batch of them), then the per-request codes.
 int sg_rls_should_rate_limit(sg_handle* h, const sg_rls_request* req, uint32_t n, const int32_t* desc_rule,
                              uint64_t n_desc, int32_t* overall, sg_rls_status* status) {
     if (!h) return SG_E_INVAL;
@@ -1711,6 +1711,25 @@ int sg_rls_should_rate_limit(sg_handle* h, const sg_rls_request* req, uint32_t n
     for (uint32_t j = 0; j < n; ++j)
         if ((uint64_t)req[j].desc_begin + req[j].desc_count > n_desc)
             return fail(h, SG_E_INVAL, "a request's descriptors lie outside desc_rule");
+    // SimpleClusterFlowChecker (flow/SimpleClusterFlowChecker.java:33-65) reads count * exceedCount and has neither a
+    // namespace limiter nor AVG_LOCAL thresholds: refuse rules the cluster path would treat differently, and a batch
+    // that would need several device batches (no partial commit), before any state changes
+    uint64_t n_tok = 0;
+    for (uint32_t j = 0; j < n; ++j) {
+        if (req[j].hits_addend < 0) continue;
+        n_tok += req[j].desc_count;
+        for (uint32_t x = 0; x < req[j].desc_count; ++x) {
+            const int32_t r = desc_rule[(uint64_t)req[j].desc_begin + x];
+            if (r < 0 || (uint32_t)r >= h->K) continue;
+            const sg_flow_rule& fr = h->rules[r];
+            const int ns = fr.namespace_id;
+            if (fr.threshold_type != SG_THRESHOLD_GLOBAL ||
+                (ns >= 0 && (size_t)ns < h->ns_slot.size() && h->ns_slot[ns] >= 0))
+                return fail(h, SG_E_UNSUPPORTED, "RLS rules are loaded GLOBAL in namespaces without a limiter "
+                                                 "(SimpleClusterFlowChecker reads count * exceedCount only)");
+        }
+    }
+    if (n_tok > h->cfg.max_batch) return fail(h, SG_E_CAPACITY, "more descriptors than max_batch");
     std::vector<sg_req> batch;
     std::vector<uint64_t> owner;  // descriptor of each token request
     batch.reserve(n_desc);
@@ -1736,9 +1755,8 @@ int sg_rls_should_rate_limit(sg_handle* h, const sg_rls_request* req, uint32_t n
         }
     }
     std::vector<sg_result> res(batch.size());
-    for (uint64_t b = 0; b < batch.size(); b += h->cfg.max_batch) {
-        const uint64_t m = std::min<uint64_t>(h->cfg.max_batch, batch.size() - b);
-        const int rc = sg_flow_decide_batch_host(h, batch.data() + b, m, res.data() + b);
+    if (!batch.empty()) {
+        const int rc = sg_flow_decide_batch_host(h, batch.data(), batch.size(), res.data());
         if (rc) return rc;
     }
     for (uint64_t x = 0; x < batch.size(); ++x) {
