@@ -692,6 +692,9 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
 #ifndef SG_WAVE_INLINE
 #define SG_WAVE_INLINE 1
 #endif
+#ifndef SG_LONG_PCACHE
+#define SG_LONG_PCACHE 1  // the long walker is walk_wave_tab (0: walk_wave, round 4)
+#endif
 #if SG_WAVE_INLINE
 #define SG_WAVE_ATTR __device__ __forceinline__
 #else
@@ -779,6 +782,137 @@ SG_WAVE_ATTR void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
         pos = npos;
     }
     w.finish(k);
+}
+
+// s_waitcnt vmcnt(0) as a builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), not inline asm: the compiler's
+// wait-count pass sees it and knows the LDS-DMA writes have landed (see glds_rows).
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// The first 64 records of every window period of the long segment being walked, per wave of k_walk_long: filled by
+// LDS-DMA in one round trip at the segment's start (low / high words of the records in separate rows).
+__shared__ uint32_t g_lcache[4][kLongPeriods][2][64];
+
+__device__ __forceinline__ void glds_word(const uint32_t* src, uint32_t* lds_row) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)lds_row, 4, 0, 0);
+}
+
+// walk_wave over a segment whose period starts k_long_bounds tabulated: every period's first chunk is fetched at once,
+// so a period that cannot admit anything more after its first chunk (a hot flowId's saturated periods) hands its rest
+// to k_skip_apply and the walk goes on to the next period without a memory round trip. Periods that stay open are
+// walked chunk by chunk as walk_wave does (SG_LONG_PCACHE=0: walk_wave for every segment).
+template <bool L>
+__device__ __forceinline__ void walk_wave_tab(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e, uint32_t item) {
+    WaveWalker<L> w(a, k);
+    const int lane = w.lane;
+    const uint32_t npw = w.pc.np;
+    // tabulated period starts (k_long_bounds): lane q holds the first position of period q + 1
+    const bool tab = a.long_pend != nullptr && item < kLongTab && npw <= (uint32_t)kLongPeriods;
+    const uint32_t pend_l = (tab && lane < kLongPeriods) ? a.long_pend[(size_t)item * kLongPeriods + lane] : 0u;
+    auto pbeg = [&](uint32_t q) -> uint64_t {  // tab: first position of period q in the segment
+        if (q == 0) return s;
+        if (q >= npw) return e;
+        const uint64_t x = (uint64_t)(uint32_t)bcast32((int)pend_l, (int)q - 1);
+        return x < s ? s : x > e ? e : x;
+    };
+    uint32_t (*cache)[2][64] = g_lcache[(threadIdx.x / 64) & 3];
+    const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(a.rec_sorted);
+    const uint64_t n1 = a.n - 1;
+    if (tab) {
+        for (uint32_t q = 0; q < npw; ++q) {
+            const uint64_t j = min(pbeg(q) + (uint64_t)lane, n1);
+            glds_word(rec32 + 2 * j, cache[q][0]);
+            glds_word(rec32 + 2 * j + 1, cache[q][1]);
+        }
+        wait_vm0();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // tab: the skipped rest of period q (lane q), [skb, ske), handed to k_skip_apply at the end (one atomic)
+    uint32_t skb = 0, ske = 0;
+    uint32_t qi = 0;
+    for (uint64_t pos = s; pos < e;) {
+        // the period of `pos` and where it ends in the segment; its first chunk
+        uint64_t end, cur;
+        if (tab) {
+            while (pbeg(qi + 1) <= pos) ++qi;  // periods without records have pbeg(q) == pbeg(q + 1)
+            end = pbeg(qi + 1);
+            cur = ((uint64_t)cache[qi][1][lane] << 32) | cache[qi][0][lane];
+        } else {
+            cur = a.rec_sorted[min(pos + (uint64_t)lane, n1)];
+            const uint32_t i0 = (uint32_t)bcast32((int)(uint32_t)((cur >> a.abits) & a.imask), 0);
+            const uint32_t q = w.pc.of(i0);
+            const uint32_t nb = q + 1 < npw ? w.pc.at(q + 1) : 0xFFFFFFFFu;
+            end = nb == 0xFFFFFFFFu ? e : gallop_search(pos + 1, e, [&](uint64_t p) {
+                return (uint32_t)((a.rec_sorted[p] >> a.abits) & a.imask) >= nb;
+            }, lane);
+        }
+        for (;;) {  // the chunks of this period in order (one chunk() site: registers)
+            w.chunk(cur, pos + lane < end);
+            pos += 64;
+            if (pos >= end) break;
+            if (w.dead && end - pos >= kSkipMin) {  // the rest of the period is BLOCKED
+                if (tab) {
+                    if (lane == (int)qi) {
+                        skb = (uint32_t)pos;
+                        ske = (uint32_t)end;
+                    }
+                    break;
+                }
+                const uint32_t np = (uint32_t)((end - pos + kSkipPiece - 1) / kSkipPiece);
+                uint32_t slot = 0;
+                if (lane == 0) slot = atomicAdd(a.skip_count, np);
+                slot = (uint32_t)bcast32((int)slot, 0);
+                if (slot + np <= a.skip_cap) {
+                    for (uint32_t pi = lane; pi < np; pi += 64) {
+                        const uint64_t b0 = pos + (uint64_t)pi * kSkipPiece;
+                        a.skips[slot + pi] = make_uint4(k, w.pc.q, (uint32_t)b0, (uint32_t)min(end, b0 + kSkipPiece));
+                    }
+                    break;
+                }
+            }
+            cur = a.rec_sorted[min(pos + (uint64_t)lane, n1)];
+        }
+        pos = end;
+    }
+    w.finish(k);
+    const uint32_t np = ske > skb ? (ske - skb + kSkipPiece - 1) / kSkipPiece : 0u;
+    const uint32_t tot = (uint32_t)wave_sum((int64_t)np);
+    if (tot == 0) return;
+    const uint32_t off = (uint32_t)wave_excl_scan((int64_t)np, lane);
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(a.skip_count, tot);
+    slot = (uint32_t)bcast32((int)slot, 0);
+    if (slot + tot <= a.skip_cap) {
+        for (uint32_t pi = 0; pi < np; ++pi) {
+            const uint32_t b0 = skb + pi * kSkipPiece;
+            a.skips[slot + off + pi] = make_uint4(k, (uint32_t)lane, b0, min(ske, b0 + kSkipPiece));
+        }
+        return;
+    }
+    // no room in the skip list: add the skipped ranges' BLOCK counts here (k_skip_apply's work, one wave)
+    for (uint32_t q = 0; q < npw; ++q) {
+        const uint32_t b0 = (uint32_t)bcast32((int)skb, (int)q), b1 = (uint32_t)bcast32((int)ske, (int)q);
+        if (b1 <= b0) continue;
+        int64_t sa = 0, spa = 0;
+        for (uint64_t j = (uint64_t)b0 + lane; j < b1; j += 64) {
+            const Decoded d = decode(a, a.rec_sorted[j]);
+            sa += d.acq;
+            spa += d.prio ? d.acq : 0;
+        }
+        sa = wave_sum(sa);
+        spa = wave_sum(spa);
+        if (lane == 0) {
+            const int64_t P = g_p0[w.R.wl_idx] + (int64_t)q;
+            Bucket& bk = a.ring[(size_t)k * a.stride + (int)(P % w.R.S)];
+            if (bk.start == P * w.R.wl) {
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK], (unsigned long long)sa);
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK_REQUEST], (unsigned long long)(b1 - b0));
+                atomicAdd((unsigned long long*)&bk.c[SG_EV_OCCUPIED_BLOCK], (unsigned long long)spa);
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------- segments and the walk kernel
@@ -1022,7 +1156,11 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
             }, lane);
         }
         const uint64_t t0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
+#if SG_LONG_PCACHE
+        walk_wave_tab<L>(a, k, s, e, item);
+#else
         walk_wave<L>(a, k, s, e, item);
+#endif
         if (a.dbg & 64) {
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
             const uint64_t len = e - s;
@@ -1280,7 +1418,6 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
 // wait-count pass sees it and knows the LDS-DMA writes have landed. After an inline-asm wait it still counted them
 // as pending and put a vmcnt(0) before every later LDS read of the loop — each one also waiting for the stores
 // issued since (a store round trip per period open).
-__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 template <int R>
 __device__ __forceinline__ void glds_rows(const uint32_t* src, uint32_t* wrecs) {
