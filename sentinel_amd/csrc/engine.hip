@@ -97,25 +97,6 @@ __device__ __forceinline__ Decoded decode_c(const BatchArgs& a, uint32_t c) {
     return d;
 }
 
-// decode_c without the escape load: acquire code 127 is left in d.acq for esc_fixup. A conditional load whose value
-// meets the other path at a select puts an s_waitcnt vmcnt(0) on the path every lane takes — on gfx9 vmcnt counts the
-// wave's stores too, so every record step would wait for all its result and bucket stores to land.
-__device__ __forceinline__ Decoded decode_c_raw(uint32_t c) {
-    Decoded d;
-    d.idx = c >> 8;
-    d.prio = (c & 1u) != 0;
-    d.acq = (int64_t)((c >> 1) & 127u);
-    return d;
-}
-
-// The escaped acquire counts of the lanes in `live` (a wave-uniform branch: skipped, with its wait, when no lane has one).
-__device__ __forceinline__ void esc_fixup(const BatchArgs& a, bool live, Decoded& d) {
-    const bool esc = live && d.acq == 127;
-    if (__ballot(esc)) {
-        if (esc) d.acq = (int64_t)a.req[d.idx].acquire;
-    }
-}
-
 // ------------------------------------------------------------------------------------------- prep
 
 // One block per 4096-request tile (the radix sort's tile). With a.hist0 set the block also counts the
@@ -259,25 +240,6 @@ __device__ __forceinline__ void open_bucket(PeriodState& ps, int64_t start, cons
         ps.cur[SG_EV_PASS_REQUEST] += ps.occ_req;
         ps.occ_pass = 0;
         ps.occ_req = 0;
-    }
-}
-
-#ifndef SG_GUARD_LOADS
-#define SG_GUARD_LOADS 0
-#endif
-// open_bucket with slot I's counts read from the ring only when the batch continues the stored period, in a
-// wave-uniform branch (the load's wait is skipped with it when no lane of the wave continues one).
-__device__ __forceinline__ void open_period_cur(const Bucket* ring, int I, PeriodState& ps, int64_t start, int64_t ws) {
-    int64_t zero[SG_NUM_EVENTS];
-#pragma unroll
-    for (int e = 0; e < SG_NUM_EVENTS; ++e) zero[e] = 0;
-    open_bucket(ps, start == ws ? INT64_MIN : start, zero, ws);  // reset / created (continued: zeros, no transfer)
-    const bool cont = start == ws;
-    if (__ballot(cont)) {
-        if (cont) {
-#pragma unroll
-            for (int e = 0; e < SG_NUM_EVENTS; ++e) ps.cur[e] = ring[I].c[e];
-        }
     }
 }
 
@@ -692,9 +654,6 @@ __device__ __forceinline__ uint64_t wave_search(uint64_t lo, uint64_t hi, Pred p
 #ifndef SG_WAVE_INLINE
 #define SG_WAVE_INLINE 1
 #endif
-#ifndef SG_LONG_PCACHE
-#define SG_LONG_PCACHE 1  // the long walker is walk_wave_tab (0: walk_wave, round 4)
-#endif
 #if SG_WAVE_INLINE
 #define SG_WAVE_ATTR __device__ __forceinline__
 #else
@@ -782,137 +741,6 @@ SG_WAVE_ATTR void walk_wave(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t
         pos = npos;
     }
     w.finish(k);
-}
-
-// s_waitcnt vmcnt(0) as a builtin (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15), not inline asm: the compiler's
-// wait-count pass sees it and knows the LDS-DMA writes have landed (see glds_rows).
-__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-
-// The first 64 records of every window period of the long segment being walked, per wave of k_walk_long: filled by
-// LDS-DMA in one round trip at the segment's start (low / high words of the records in separate rows).
-__shared__ uint32_t g_lcache[4][kLongPeriods][2][64];
-
-__device__ __forceinline__ void glds_word(const uint32_t* src, uint32_t* lds_row) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)lds_row, 4, 0, 0);
-}
-
-// walk_wave over a segment whose period starts k_long_bounds tabulated: every period's first chunk is fetched at once,
-// so a period that cannot admit anything more after its first chunk (a hot flowId's saturated periods) hands its rest
-// to k_skip_apply and the walk goes on to the next period without a memory round trip. Periods that stay open are
-// walked chunk by chunk as walk_wave does (SG_LONG_PCACHE=0: walk_wave for every segment).
-template <bool L>
-__device__ __forceinline__ void walk_wave_tab(const BatchArgs& a, uint32_t k, uint64_t s, uint64_t e, uint32_t item) {
-    WaveWalker<L> w(a, k);
-    const int lane = w.lane;
-    const uint32_t npw = w.pc.np;
-    // tabulated period starts (k_long_bounds): lane q holds the first position of period q + 1
-    const bool tab = a.long_pend != nullptr && item < kLongTab && npw <= (uint32_t)kLongPeriods;
-    const uint32_t pend_l = (tab && lane < kLongPeriods) ? a.long_pend[(size_t)item * kLongPeriods + lane] : 0u;
-    auto pbeg = [&](uint32_t q) -> uint64_t {  // tab: first position of period q in the segment
-        if (q == 0) return s;
-        if (q >= npw) return e;
-        const uint64_t x = (uint64_t)(uint32_t)bcast32((int)pend_l, (int)q - 1);
-        return x < s ? s : x > e ? e : x;
-    };
-    uint32_t (*cache)[2][64] = g_lcache[(threadIdx.x / 64) & 3];
-    const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(a.rec_sorted);
-    const uint64_t n1 = a.n - 1;
-    if (tab) {
-        for (uint32_t q = 0; q < npw; ++q) {
-            const uint64_t j = min(pbeg(q) + (uint64_t)lane, n1);
-            glds_word(rec32 + 2 * j, cache[q][0]);
-            glds_word(rec32 + 2 * j + 1, cache[q][1]);
-        }
-        wait_vm0();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // tab: the skipped rest of period q (lane q), [skb, ske), handed to k_skip_apply at the end (one atomic)
-    uint32_t skb = 0, ske = 0;
-    uint32_t qi = 0;
-    for (uint64_t pos = s; pos < e;) {
-        // the period of `pos` and where it ends in the segment; its first chunk
-        uint64_t end, cur;
-        if (tab) {
-            while (pbeg(qi + 1) <= pos) ++qi;  // periods without records have pbeg(q) == pbeg(q + 1)
-            end = pbeg(qi + 1);
-            cur = ((uint64_t)cache[qi][1][lane] << 32) | cache[qi][0][lane];
-        } else {
-            cur = a.rec_sorted[min(pos + (uint64_t)lane, n1)];
-            const uint32_t i0 = (uint32_t)bcast32((int)(uint32_t)((cur >> a.abits) & a.imask), 0);
-            const uint32_t q = w.pc.of(i0);
-            const uint32_t nb = q + 1 < npw ? w.pc.at(q + 1) : 0xFFFFFFFFu;
-            end = nb == 0xFFFFFFFFu ? e : gallop_search(pos + 1, e, [&](uint64_t p) {
-                return (uint32_t)((a.rec_sorted[p] >> a.abits) & a.imask) >= nb;
-            }, lane);
-        }
-        for (;;) {  // the chunks of this period in order (one chunk() site: registers)
-            w.chunk(cur, pos + lane < end);
-            pos += 64;
-            if (pos >= end) break;
-            if (w.dead && end - pos >= kSkipMin) {  // the rest of the period is BLOCKED
-                if (tab) {
-                    if (lane == (int)qi) {
-                        skb = (uint32_t)pos;
-                        ske = (uint32_t)end;
-                    }
-                    break;
-                }
-                const uint32_t np = (uint32_t)((end - pos + kSkipPiece - 1) / kSkipPiece);
-                uint32_t slot = 0;
-                if (lane == 0) slot = atomicAdd(a.skip_count, np);
-                slot = (uint32_t)bcast32((int)slot, 0);
-                if (slot + np <= a.skip_cap) {
-                    for (uint32_t pi = lane; pi < np; pi += 64) {
-                        const uint64_t b0 = pos + (uint64_t)pi * kSkipPiece;
-                        a.skips[slot + pi] = make_uint4(k, w.pc.q, (uint32_t)b0, (uint32_t)min(end, b0 + kSkipPiece));
-                    }
-                    break;
-                }
-            }
-            cur = a.rec_sorted[min(pos + (uint64_t)lane, n1)];
-        }
-        pos = end;
-    }
-    w.finish(k);
-    const uint32_t np = ske > skb ? (ske - skb + kSkipPiece - 1) / kSkipPiece : 0u;
-    const uint32_t tot = (uint32_t)wave_sum((int64_t)np);
-    if (tot == 0) return;
-    const uint32_t off = (uint32_t)wave_excl_scan((int64_t)np, lane);
-    uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(a.skip_count, tot);
-    slot = (uint32_t)bcast32((int)slot, 0);
-    if (slot + tot <= a.skip_cap) {
-        for (uint32_t pi = 0; pi < np; ++pi) {
-            const uint32_t b0 = skb + pi * kSkipPiece;
-            a.skips[slot + off + pi] = make_uint4(k, (uint32_t)lane, b0, min(ske, b0 + kSkipPiece));
-        }
-        return;
-    }
-    // no room in the skip list: add the skipped ranges' BLOCK counts here (k_skip_apply's work, one wave)
-    for (uint32_t q = 0; q < npw; ++q) {
-        const uint32_t b0 = (uint32_t)bcast32((int)skb, (int)q), b1 = (uint32_t)bcast32((int)ske, (int)q);
-        if (b1 <= b0) continue;
-        int64_t sa = 0, spa = 0;
-        for (uint64_t j = (uint64_t)b0 + lane; j < b1; j += 64) {
-            const Decoded d = decode(a, a.rec_sorted[j]);
-            sa += d.acq;
-            spa += d.prio ? d.acq : 0;
-        }
-        sa = wave_sum(sa);
-        spa = wave_sum(spa);
-        if (lane == 0) {
-            const int64_t P = g_p0[w.R.wl_idx] + (int64_t)q;
-            Bucket& bk = a.ring[(size_t)k * a.stride + (int)(P % w.R.S)];
-            if (bk.start == P * w.R.wl) {
-                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK], (unsigned long long)sa);
-                atomicAdd((unsigned long long*)&bk.c[SG_EV_BLOCK_REQUEST], (unsigned long long)(b1 - b0));
-                atomicAdd((unsigned long long*)&bk.c[SG_EV_OCCUPIED_BLOCK], (unsigned long long)spa);
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------------------- segments and the walk kernel
@@ -1156,11 +984,7 @@ __device__ __forceinline__ void walk_long_body(const BatchArgs& a) {
             }, lane);
         }
         const uint64_t t0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-#if SG_LONG_PCACHE
-        walk_wave_tab<L>(a, k, s, e, item);
-#else
         walk_wave<L>(a, k, s, e, item);
-#endif
         if (a.dbg & 64) {
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
             const uint64_t len = e - s;
@@ -1418,6 +1242,7 @@ __device__ __forceinline__ void walk_reg(const BatchArgs& a, bool act, uint32_t 
 // wait-count pass sees it and knows the LDS-DMA writes have landed. After an inline-asm wait it still counted them
 // as pending and put a vmcnt(0) before every later LDS read of the loop — each one also waiting for the stores
 // issued since (a store round trip per period open).
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 template <int R>
 __device__ __forceinline__ void glds_rows(const uint32_t* src, uint32_t* wrecs) {
@@ -1474,17 +1299,10 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
             park = true;
             return;
         }
-#if SG_GUARD_LOADS
-        dn = decode_c_raw(wrecs[(uint32_t)(p - wb) * 64 + lane]);
-#else
         dn = decode_c(a, wrecs[(uint32_t)(p - wb) * 64 + lane]);
-#endif
         qn = pc.of(dn.idx);
     };
     if (live) peek();
-#if SG_GUARD_LOADS
-    esc_fixup(a, live && !park, dn);
-#endif
     for (;;) {
         if (!__ballot(live && !park)) {
             if (!__ballot(live)) break;
@@ -1500,9 +1318,6 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
                 park = false;
                 peek();
             }
-#if SG_GUARD_LOADS
-            esc_fixup(a, live && !park, dn);
-#endif
             continue;
         }
         // 1. open the period of every lane whose next record starts one (the first record included)
@@ -1542,16 +1357,12 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
             ps.head_other = (int64_t)ho;
             const int32_t stI_rel = snap[I].st;
             const int64_t stI = stI_rel == INT32_MIN ? INT64_MIN : T0 + (int64_t)stI_rel;
-#if SG_GUARD_LOADS
-            open_period_cur(ring, I, ps, stI, ws);
-#else
             int64_t cI[SG_NUM_EVENTS];
             if (stI == ws) {
 #pragma unroll
                 for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) cI[ev] = ring[I].c[ev];
             }
             open_bucket(ps, stI, cI, ws);
-#endif
         }
         // 2. decide records while they stay in the open period (ClusterFlowChecker.acquireClusterToken :67-111)
         while (live && !park && qn == pc.q) {
@@ -1569,9 +1380,6 @@ __device__ __forceinline__ void walk_lds(const BatchArgs& a, bool act, uint32_t 
             }
             ++p;
             peek();
-#if SG_GUARD_LOADS
-            esc_fixup(a, live && !park, dn);
-#endif
         }
     }
     if (act) {
@@ -1827,211 +1635,6 @@ __global__ void __launch_bounds__(256, C ? SG_SHORT_C_BLOCKS : kShortBlocksPerCu
     stage_periods(a);
     if (g_blds) walk_short_body<SM, true, C>(a, snap_all, recs_all);
     else walk_short_body<SM, false, C>(a, snap_all, recs_all);
-}
-
-// Lean short walker (SG_DEBUG & 1024, A/B): one lane per segment as k_walk_short, with everything the walk reads in
-// registers — the ring snapshot {start, PASS, WAITING} of S <= SM slots (the SlotSnap encoding, exact under
-// BatchArgs::narrow and narrow_span) and the records in chunks of kRsChunk compact records, the next chunk loaded
-// while the lanes step through the current one. Every lane takes its next record in the same step (a period opens
-// inside the step, for the lanes that need one), so the walk has no phases, no LDS staging round trips and no
-// parking: the instruction count per record step is the decision plus, when it starts a period, the ring sums.
-// Same decisions as walk_serial (ClusterFlowChecker.acquireClusterToken :67-111).
-constexpr int kRsChunk = 8;
-
-template <int SM, bool L>
-__device__ __forceinline__ void walk_rs_seg(const BatchArgs& a, bool act, uint32_t k, uint64_t s, uint64_t e,
-                                            const Rule& R, const Occ& occ, int32_t (&st)[SM], int32_t (&pa)[SM],
-                                            int32_t (&wa)[SM], uint32_t (&buf)[kRsChunk], int64_t T0) {
-    Bucket* ring = a.ring + (size_t)k * a.stride;
-    BucketHot* hot = a.hot + (size_t)k * a.stride;
-    const int S = R.S;
-    const int64_t wl = R.wl;
-    PeriodCursor<L> pc;
-    pc.init(a, act ? R.wl_idx : 0);
-    const int64_t P0 = g_p0[act ? R.wl_idx : 0];
-    PeriodState ps;
-    ps.occ_pass = occ.pass;
-    ps.occ_req = occ.pass_req;
-#pragma unroll
-    for (int ev = 0; ev < SG_NUM_EVENTS; ++ev) ps.cur[ev] = 0;
-    ps.wo_pass = ps.wo_wait = ps.head_other = 0;
-    int I = -1;      // slot of the open period
-    int64_t ws = 0;  // its window start
-    const uint64_t n1 = a.n - 1;
-    const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(a.rec_sorted);  // low word: the compact record
-    for (uint64_t p = s; __ballot(act && p < e); p += kRsChunk) {
-        uint32_t nb[kRsChunk];
-#pragma unroll
-        for (int u = 0; u < kRsChunk; ++u) nb[u] = rec32[2 * min(p + kRsChunk + u, n1)];  // the next chunk, in flight
-#pragma unroll 1
-        for (int u = 0; u < kRsChunk; ++u) {  // a loop (not unrolled: registers), buf[0] is the step's record
-            const bool live = act && p + u < e;
-            if (!__ballot(live)) break;
-            Decoded d = decode_c_raw(buf[0]);
-            esc_fixup(a, live, d);
-            if (live) {
-                const uint32_t q = pc.of(d.idx);
-                if (q != pc.q) {  // close the open bucket (memory and registers), open period q
-                    if (I >= 0) {
-                        store_bucket(ring + I, hot + I, ws, ps.cur);
-                        const int32_t sr = (int32_t)(ws - T0), pr = (int32_t)ps.cur[SG_EV_PASS],
-                                      wr = (int32_t)ps.cur[SG_EV_WAITING];
-#pragma unroll
-                        for (int x = 0; x < SM; ++x) {
-                            st[x] = x == I ? sr : st[x];
-                            pa[x] = x == I ? pr : pa[x];
-                            wa[x] = x == I ? wr : wa[x];
-                        }
-                    }
-                    const uint32_t qprev = pc.q;
-                    pc.seek(q);
-                    const int64_t P = P0 + (int64_t)q;
-                    I = I < 0 ? period_slot(R.wl_idx, q, S) : (int)((uint32_t)(I + (int)(q - qprev)) % (uint32_t)S);
-                    ws = P * wl;
-                    const int32_t lo32 = rel32(ws - (int64_t)S * wl - T0);  // valid iff start > ws - S * wl
-                    const int h = I + 1 == S ? 0 : I + 1;
-                    uint32_t wp = 0, ww = 0, ho = 0;
-                    int32_t stI_rel = INT32_MIN;
-#pragma unroll
-                    for (int x = 0; x < SM; ++x) {
-                        const bool v = (x < S) & (x != I) & (st[x] > lo32);
-                        const uint32_t m = v ? 0xFFFFFFFFu : 0u;
-                        wp += (uint32_t)pa[x] & m;
-                        ww += (uint32_t)wa[x] & m;
-                        ho = (x == h) ? ((uint32_t)pa[x] & m) : ho;
-                        stI_rel = x == I ? st[x] : stI_rel;
-                    }
-                    ps.wo_pass = (int64_t)wp;
-                    ps.wo_wait = (int64_t)ww;
-                    ps.head_other = (int64_t)ho;
-                    const int64_t stI = stI_rel == INT32_MIN ? INT64_MIN : T0 + (int64_t)stI_rel;
-                    open_period_cur(ring, I, ps, stI, ws);  // the batch may continue the stored period
-                }
-                const double latest = qps_of(ps.wo_pass + ps.cur[SG_EV_PASS], R.isec);
-                const double next_remaining = R.thr - latest - (double)d.acq;
-                if (next_remaining >= 0) {
-                    ps.cur[SG_EV_PASS] += d.acq;
-                    ps.cur[SG_EV_PASS_REQUEST] += 1;
-                    if (d.prio) ps.cur[SG_EV_OCCUPIED_PASS] += d.acq;
-                    store_result(a.out, d.idx, SG_STATUS_OK, java_d2i(next_remaining), 0);
-                } else {
-                    int32_t wait;
-                    const int32_t stt = decide_fail(R, a.max_occ_ratio, ps, d.acq, d.prio, &wait);
-                    if (stt != SG_STATUS_BLOCKED) store_result(a.out, d.idx, stt, 0, wait);
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < kRsChunk - 1; ++v) buf[v] = buf[v + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kRsChunk; ++u) buf[u] = nb[u];
-    }
-    if (act) {
-        if (I >= 0) store_bucket(ring + I, hot + I, ws, ps.cur);
-        if (ps.occ_pass != occ.pass || ps.occ_req != occ.pass_req) {  // rarely changes: no partial-line store
-            Occ o;
-            o.pass = ps.occ_pass;
-            o.pass_req = ps.occ_req;
-            a.occ[k] = o;
-        }
-    }
-}
-
-template <int SM, bool L>
-__device__ __forceinline__ void walk_rs_body(const BatchArgs& a) {
-    const int lane = lane_id();
-    const bool tiny = tiny_active(a);
-    uint32_t cnt[kClasses], grp_end[kClasses];
-    uint32_t total = 0;
-#pragma unroll
-    for (int c = kClasses - 1; c >= 0; --c) {  // group order: longest class first
-        cnt[c] = (c == 0 && tiny) ? 0u : a.short_count[c];
-        total += (cnt[c] + 63) / 64;
-        grp_end[c] = total;
-    }
-    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    if (wave >= total) return;
-    const int64_t T0 = a.p0[0] * (int64_t)a.wl[0];
-    if (!(a.narrow && narrow_span(a, T0))) {  // the 32-bit snapshot is not exact: every lane re-reads its ring
-        for (uint32_t g = wave; g < total; g += nwaves) {
-            int c = kClasses - 1;
-            uint32_t g0 = 0;
-            while (g >= grp_end[c]) {
-                g0 = grp_end[c];
-                --c;
-            }
-            const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
-            if (i >= cnt[c]) continue;
-            const uint64_t li = a.class_off[c] + i;
-            walk_serial<L>(a, a.short_key[li], a.short_list[li], a.short_end[li]);
-        }
-        return;
-    }
-    auto desc = [&](uint32_t g, bool& act, uint32_t& s, uint32_t& k, uint32_t& e) {
-        int c = kClasses - 1;
-        uint32_t g0 = 0;
-        while (g >= grp_end[c]) {
-            g0 = grp_end[c];
-            --c;
-        }
-        const uint32_t i = (g - g0) * 64 + (uint32_t)lane;
-        act = i < cnt[c];
-        const uint64_t li = a.class_off[c] + (act ? i : 0u);
-        s = a.short_list[li];
-        k = a.short_key[li];
-        e = a.short_end[li];
-    };
-    bool act_n;
-    uint32_t s_n, k_n, e_n;
-    desc(wave, act_n, s_n, k_n, e_n);
-    const uint64_t n1 = a.n - 1;
-    const uint32_t* rec32 = reinterpret_cast<const uint32_t*>(a.rec_sorted);
-    for (uint32_t g = wave; g < total; g += nwaves) {
-        const uint64_t tw0 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-        const bool act = act_n;
-        const uint64_t s = s_n;
-        const uint32_t k = k_n;
-        const uint64_t e = e_n;
-        const Rule R = a.rules[k];
-        const Occ occ = a.occ[k];
-        int32_t st[SM], pa[SM], wa[SM];
-        const BucketHot* hk = a.hot + (size_t)k * a.stride;
-#pragma unroll
-        for (int x = 0; x < SM; ++x) {
-            const int xx = x < a.stride ? x : 0;  // slots past the handle's stride: never read (x >= S)
-            const ulonglong2 hv = *reinterpret_cast<const ulonglong2*>(hk + xx);  // {start, PASS | WAITING << 32}
-            st[x] = snap_rel((int64_t)hv.x, T0);
-            pa[x] = (int32_t)(uint32_t)hv.y;
-            wa[x] = (int32_t)(uint32_t)(hv.y >> 32);
-        }
-        uint32_t buf[kRsChunk];
-#pragma unroll
-        for (int u = 0; u < kRsChunk; ++u) buf[u] = rec32[2 * min(s + u, n1)];
-        desc(min(g + nwaves, total - 1), act_n, s_n, k_n, e_n);  // the next group's descriptors
-        const uint64_t tw1 = (a.dbg & 64) ? __builtin_amdgcn_s_memrealtime() : 0;
-        walk_rs_seg<SM, L>(a, act, k, s, e, R, occ, st, pa, wa, buf, T0);
-        if (a.dbg & 64) {  // groups, gather and walk time (100 MHz ticks), all classes in counter slot 0
-            const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
-            if (lane == 0) {
-                atomicAdd(&a.dbg_ctr[0], (unsigned long long)(tw2 - tw0));
-                atomicAdd(&a.dbg_ctr[1], 1ull);
-                atomicAdd(&a.dbg_ctr[7], (unsigned long long)(tw1 - tw0));
-                atomicAdd(&a.dbg_ctr[7], (unsigned long long)(tw2 - tw1) << 32);
-            }
-        }
-    }
-}
-
-#ifndef SG_RS_BLOCKS
-#define SG_RS_BLOCKS 4
-#endif
-template <int SM>
-__global__ void __launch_bounds__(256, SG_RS_BLOCKS) k_walk_rs(BatchArgs a) {
-    if (*a.err) return;
-    stage_periods(a);
-    if (g_blds) walk_rs_body<SM, true>(a);
-    else walk_rs_body<SM, false>(a);
 }
 
 // Tiny-segment walker: one thread per flowId of length class 0 (<= kClassMax[0] records, most touched flowIds of a
@@ -2334,14 +1937,6 @@ static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
     static unsigned blocks[2][2] = {{0, 0}, {0, 0}};  // [compact][all CUs / the pipeline's walker CUs]
     const bool c = SM > 0 && short_compact(a);
     const int m = a.walk_cus > 0 ? 1 : 0;
-    if constexpr (SM > 0) {
-        if (c && (a.dbg & 1024) && a.short_key && a.short_end) {  // the lean register walker (A/B)
-            static unsigned rs_blocks[2] = {0, 0};
-            if (rs_blocks[m] == 0) rs_blocks[m] = resident_blocks((const void*)k_walk_rs<SM>, 256, a.walk_cus);
-            hipLaunchKernelGGL((k_walk_rs<SM>), dim3(rs_blocks[m]), dim3(256), 0, stream, a);
-            return hipGetLastError();
-        }
-    }
     const void* kern = c ? (const void*)k_walk_short<SM, true> : (const void*)k_walk_short<SM, false>;
     if (blocks[c][m] == 0) blocks[c][m] = resident_blocks(kern, 256, a.walk_cus);
     if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
