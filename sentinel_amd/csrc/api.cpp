@@ -867,13 +867,16 @@ int sg_set_namespaces(sg_handle* h, const sg_namespace* ns, uint32_t n) {
     return upload_rule_table(h);
 }
 
-int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
-    if (h) drain_async(h);
-    if (!h || (!rules && n)) return SG_E_INVAL;
+namespace {
+
+// Every check sg_load_flow_rules makes before it changes anything (FlowRuleUtil.isValidRule / checkClusterField,
+// FlowRuleUtil.java:167-229, and the device path's limits: sampleCount <= 64 for a surviving metric's window shape
+// too, <= 8 distinct window lengths with the limiter's 100 ms): after SG_OK only allocation or device errors remain.
+int flow_rules_validate(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     if (n >= SG_KEY_BAD) return fail(h, SG_E_INVAL, "too many rules");
-    (void)hipSetDevice(h->device);
-    // validate (FlowRuleUtil.isValidRule / checkClusterField, FlowRuleUtil.java:167-229)
-    std::unordered_map<int64_t, uint32_t> seen;
+    std::unordered_map<int64_t, uint32_t> seen, old_index;
+    for (uint32_t k = 0; k < h->K; ++k) old_index.emplace(h->rules[k].flow_id, k);
+    std::vector<int32_t> wls;
     for (uint32_t i = 0; i < n; ++i) {
         const sg_flow_rule& r = rules[i];
         if (r.flow_id <= 0) return fail(h, SG_E_INVAL, "flowId must be > 0");
@@ -883,16 +886,60 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         if (r.namespace_id < 0 || (size_t)r.namespace_id >= h->ns.size())
             return fail(h, SG_E_INVAL, "unknown namespace");
         if (!seen.emplace(r.flow_id, i).second) return fail(h, SG_E_INVAL, "duplicate flowId");
+        int S = r.sample_count, wl = r.window_interval_ms / r.sample_count;
+        auto it = old_index.find(r.flow_id);
+        if (it != old_index.end()) {
+            S = h->rule_tab[it->second].S;
+            wl = h->rule_tab[it->second].wl;
+        }
+        if (S > SG_MAX_SAMPLE_COUNT) return fail(h, SG_E_UNSUPPORTED, "sampleCount > 64 is not supported by the device path");
+        if (std::find(wls.begin(), wls.end(), wl) == wls.end()) wls.push_back(wl);
     }
+    if (h->n_lim > 0 && std::find(wls.begin(), wls.end(), (int32_t)kLimWindowMs) == wls.end()) wls.push_back(kLimWindowMs);
+    if (wls.size() > (size_t)kMaxWl) return fail(h, SG_E_UNSUPPORTED, "more than 8 distinct window lengths");
+    return SG_OK;
+}
+
+}  // namespace
+
+namespace {
+
+// The new rule set's device state, built beside the live one (which it only reads: surviving flowIds' rings and
+// occupy counters are copied over), so that a failure leaves the handle as it was; flow_rules_commit swaps it in,
+// flow_rules_abort frees it. The node handle prepares every shard before it commits any.
+struct FlowLoad {
+    std::vector<Rule> tab;
+    std::vector<int32_t> src;
+    int stride = 1;
+    int n_wl = 0;
+    int32_t wl[kMaxWl]{};
+    Rule* d_rules = nullptr;
+    Bucket* d_ring = nullptr;
+    BucketHot* d_hot = nullptr;
+    Occ* d_occ = nullptr;
+    uint32_t* d_seg_end = nullptr;
+};
+
+void flow_rules_abort(FlowLoad& L) {
+    dfree(L.d_rules);
+    dfree(L.d_ring);
+    dfree(L.d_hot);
+    dfree(L.d_occ);
+    dfree(L.d_seg_end);
+}
+
+int flow_rules_prepare_impl(sg_handle* h, const sg_flow_rule* rules, uint32_t n, FlowLoad& L) {
     // old flowId → old index, to keep the metric of surviving flows (ClusterFlowRuleManager.java:361)
     std::unordered_map<int64_t, uint32_t> old_index;
     for (uint32_t k = 0; k < h->K; ++k) old_index.emplace(h->rules[k].flow_id, k);
 
-    std::vector<Rule> tab(n);
-    std::vector<int32_t> src(n, -1);
-    int stride = 1;
-    int n_wl = 0;
-    int32_t wl[kMaxWl]{};
+    L.tab.assign(n, Rule{});
+    L.src.assign(n, -1);
+    std::vector<Rule>& tab = L.tab;
+    std::vector<int32_t>& src = L.src;
+    int& stride = L.stride;
+    int& n_wl = L.n_wl;
+    int32_t* wl = L.wl;
     for (uint32_t i = 0; i < n; ++i) {
         int S = rules[i].sample_count, interval = rules[i].window_interval_ms;
         auto it = old_index.find(rules[i].flow_id);
@@ -919,11 +966,11 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         tab[i] = R;
     }
 
-    Rule* d_rules = nullptr;
-    Bucket* d_ring = nullptr;
-    BucketHot* d_hot = nullptr;
-    Occ* d_occ = nullptr;
-    uint32_t* d_seg_end = nullptr;
+    Rule*& d_rules = L.d_rules;
+    Bucket*& d_ring = L.d_ring;
+    BucketHot*& d_hot = L.d_hot;
+    Occ*& d_occ = L.d_occ;
+    uint32_t*& d_seg_end = L.d_seg_end;
     int32_t* d_src = nullptr;
     if (n && h->front_only) {  // a node's front: rule thresholds and limiter slots only
         if (hipMalloc(&d_rules, sizeof(Rule) * n) != hipSuccess) return fail(h, SG_E_NOMEM, "rule table");
@@ -932,11 +979,6 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
             hipMalloc(&d_ring, sizeof(Bucket) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_hot, sizeof(BucketHot) * (size_t)n * stride) != hipSuccess ||
             hipMalloc(&d_occ, sizeof(Occ) * n) != hipSuccess || hipMalloc(&d_src, sizeof(int32_t) * n) != hipSuccess) {
-            dfree(d_rules);
-            dfree(d_ring);
-            dfree(d_hot);
-            dfree(d_occ);
-            dfree(d_seg_end);
             dfree(d_src);
             return fail(h, SG_E_NOMEM, "rule state allocation failed");
         }
@@ -948,6 +990,17 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
         HIP_TRY(h, hipDeviceSynchronize());
         dfree(d_src);
     }
+    return SG_OK;
+}
+
+int flow_rules_prepare(sg_handle* h, const sg_flow_rule* rules, uint32_t n, FlowLoad& L) {
+    const int rc = flow_rules_prepare_impl(h, rules, n, L);
+    if (rc) flow_rules_abort(L);
+    return rc;
+}
+
+int flow_rules_commit(sg_handle* h, const sg_flow_rule* rules, uint32_t n, FlowLoad& L) {
+    std::vector<int32_t>& src = L.src;
     if (h->d_cnow) {  // CurrentConcurrencyManager: surviving flowIds keep nowCalls, new ones start at 0
         // the counters in the current rule order: a reload not yet uploaded (cnow_pending) already holds them
         // remapped to h->K / h->rules; d_cnow is still in the order of the rules before that reload
@@ -970,22 +1023,41 @@ int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
     dfree(h->d_hot);
     dfree(h->d_occ);
     dfree(h->d_seg_end);
-    h->d_rules = d_rules;
-    h->d_ring = d_ring;
-    h->d_hot = d_hot;
-    h->d_occ = d_occ;
-    h->d_seg_end = d_seg_end;
+    h->d_rules = L.d_rules;
+    h->d_ring = L.d_ring;
+    h->d_hot = L.d_hot;
+    h->d_occ = L.d_occ;
+    h->d_seg_end = L.d_seg_end;
+    L.d_rules = nullptr;
+    L.d_ring = nullptr;
+    L.d_hot = nullptr;
+    L.d_occ = nullptr;
+    L.d_seg_end = nullptr;
     h->rules.assign(rules, rules + n);
-    h->rule_tab = tab;
+    h->rule_tab = L.tab;
     h->K = n;
-    h->stride = stride;
-    h->n_wl = n_wl;
-    std::memcpy(h->wl, wl, sizeof(wl));
+    h->stride = L.stride;
+    h->n_wl = L.n_wl;
+    std::memcpy(h->wl, L.wl, sizeof(L.wl));
     int rc = layout_records(h);
     if (rc) return rc;
     rc = upload_fid_table(h);
     if (rc) return rc;
     return upload_rule_table(h);
+}
+
+}  // namespace
+
+int sg_load_flow_rules(sg_handle* h, const sg_flow_rule* rules, uint32_t n) {
+    if (h) drain_async(h);
+    if (!h || (!rules && n)) return SG_E_INVAL;
+    (void)hipSetDevice(h->device);
+    const int vrc = flow_rules_validate(h, rules, n);
+    if (vrc) return vrc;
+    FlowLoad L;
+    const int rc = flow_rules_prepare(h, rules, n, L);
+    if (rc) return rc;
+    return flow_rules_commit(h, rules, n, L);
 }
 
 // flowId → rule index for the wire codec: open addressing, linear probing, load factor <= 1/2 (the same
@@ -4392,6 +4464,11 @@ struct sg_node {
     std::vector<sg_result*> r_out;
     sg_req* d_req_h = nullptr;          // host path
     sg_result* d_out_h = nullptr;
+    // every shard on the front's device with the front's request-index / acquire layout: the records path (the
+    // shards start at the sort, on the front's period tables, and write the caller's results in place)
+    bool rec_path = false;
+    uint64_t* d_sub_rec = nullptr;      // [max_batch] the shards' record slices
+    std::vector<sg_namespace> ns;       // the node's namespaces (rollback of a failed sg_node_set_namespaces)
 };
 
 namespace {
@@ -4423,6 +4500,50 @@ int node_child(sg_node* nd, sg_handle* h, int rc) {
     return rc;
 }
 
+// The shards' rules indexed into the front's window-length table (a superset: the front holds every node rule, and the
+// limiter's 100 ms), so that a shard walks the node batch's period tables as the front's k_prep built them; and
+// whether the records path applies (every shard on the front's device, the same record layout below the key).
+int node_sync_layout(sg_node* nd) {
+    sg_handle* f = nd->front;
+    int rc = ensure_layout(f);
+    if (rc) return node_child(nd, f, rc);
+    bool same = true;
+    for (size_t g = 0; g < nd->shards.size(); ++g) {
+        sg_handle* h = nd->shards[g];
+        rc = ensure_layout(h);
+        if (rc) return node_child(nd, h, rc);
+        same = same && nd->devices[g] == nd->devices[0] && h->ibits == f->ibits && h->abits == f->abits;
+        if (!h->K) continue;
+        for (uint32_t k = 0; k < h->K; ++k) {
+            Rule& R = h->rule_tab[k];
+            int w = 0;
+            while (w < f->n_wl && f->wl[w] != R.wl) ++w;
+            if (w == f->n_wl) return nfail(nd, SG_E_DEVICE, "a shard window length missing at the front");
+            R.wl_idx = w;
+        }
+        h->n_wl = f->n_wl;
+        std::memcpy(h->wl, f->wl, sizeof(h->wl));
+        NHIP(nd, hipSetDevice(h->device));
+        NHIP(nd, hipMemcpy(h->d_rules, h->rule_tab.data(), sizeof(Rule) * h->K, hipMemcpyHostToDevice));
+    }
+    nd->rec_path = same && std::getenv("SG_NODE_LEGACY") == nullptr;
+    if (nd->rec_path && !nd->d_sub_rec) {
+        NHIP(nd, hipSetDevice(nd->devices[0]));
+        if (hipMalloc(&nd->d_sub_rec, sizeof(uint64_t) * (nd->cfg.max_batch + kRecW)) != hipSuccess)
+            return nfail(nd, SG_E_NOMEM, "shard record slices");
+    }
+    return SG_OK;
+}
+
+// Waits for the shard streams [0, g) (an early return must not leave slices in flight).
+void node_sync_shards(sg_node* nd, uint32_t g) {
+    for (uint32_t x = 0; x < g && x < nd->streams.size(); ++x) {
+        (void)hipSetDevice(nd->devices[x]);
+        (void)hipStreamSynchronize(nd->streams[x]);
+    }
+    (void)hipSetDevice(nd->devices[0]);
+}
+
 }  // namespace
 
 extern "C" {
@@ -4450,6 +4571,7 @@ void sg_node_destroy(sg_node* nd) {
     dfree(nd->d_sub_out);
     dfree(nd->d_req_h);
     dfree(nd->d_out_h);
+    dfree(nd->d_sub_rec);
     if (nd->h_base) (void)hipHostFree(nd->h_base);
     if (nd->h_front_err) (void)hipHostFree(nd->h_front_err);
     sg_destroy(nd->front);
@@ -4499,6 +4621,25 @@ int sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shar
         nd->r_req.push_back(rq);
         nd->r_out.push_back(ro);
     }
+    // shards on other devices: peer access both ways (their slices and results cross xGMI as peer copies)
+    for (uint32_t g = 1; g < n_shards; ++g) {
+        const int d0 = devices[0], dg = devices[g];
+        if (dg == d0) continue;
+        int can0 = 0, can1 = 0;
+        (void)hipDeviceCanAccessPeer(&can0, d0, dg);
+        (void)hipDeviceCanAccessPeer(&can1, dg, d0);
+        if (can0) {
+            (void)hipSetDevice(d0);
+            const hipError_t e = hipDeviceEnablePeerAccess(dg, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return bail(SG_E_DEVICE);
+        }
+        if (can1) {
+            (void)hipSetDevice(dg);
+            const hipError_t e = hipDeviceEnablePeerAccess(d0, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return bail(SG_E_DEVICE);
+        }
+        (void)hipGetLastError();  // an already-enabled peer leaves its error behind
+    }
     if (hipSetDevice(devices[0]) != hipSuccess) return bail(SG_E_DEVICE);
     const uint64_t n = cfg->max_batch;
     if (hipStreamCreateWithFlags(&nd->s0, hipStreamNonBlocking) != hipSuccess ||
@@ -4517,22 +4658,43 @@ int sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shar
 
 int sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n) {
     if (!nd || (!ns && n)) return SG_E_INVAL;
-    // the front runs every namespace limiter over the node batch; the shards see only admitted requests
+    // the front runs every namespace limiter over the node batch (and validates the set); the shards see only admitted
+    // requests. A shard that fails (allocation, device) puts the front and the shards before it back on the node's
+    // previous namespaces.
+    const std::vector<sg_namespace> old = nd->ns;
+    auto limiters_off = [](std::vector<sg_namespace> v) {
+        for (auto& x : v) x.limiter_enabled = 0;
+        return v;
+    };
     int rc = sg_set_namespaces(nd->front, ns, n);
     if (rc) return node_child(nd, nd->front, rc);
-    std::vector<sg_namespace> off(ns, ns + n);
-    for (auto& x : off) x.limiter_enabled = 0;
-    for (sg_handle* h : nd->shards) {
-        rc = sg_set_namespaces(h, off.data(), n);
-        if (rc) return node_child(nd, h, rc);
+    const std::vector<sg_namespace> off = limiters_off(std::vector<sg_namespace>(ns, ns + n));
+    for (size_t g = 0; g < nd->shards.size(); ++g) {
+        rc = sg_set_namespaces(nd->shards[g], off.data(), n);
+        if (rc) {
+            rc = node_child(nd, nd->shards[g], rc);
+            const std::vector<sg_namespace> old_off = limiters_off(old);
+            (void)sg_set_namespaces(nd->front, old.data(), (uint32_t)old.size());
+            for (size_t x = 0; x < g; ++x) (void)sg_set_namespaces(nd->shards[x], old_off.data(), (uint32_t)old_off.size());
+            (void)node_sync_layout(nd);
+            return rc;
+        }
     }
-    return SG_OK;
+    nd->ns.assign(ns, ns + n);
+    return node_sync_layout(nd);
 }
 
 int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) {
     if (!nd || (!rules && n)) return SG_E_INVAL;
-    int rc = sg_load_flow_rules(nd->front, rules, n);  // validates the node's rule set
-    if (rc) return node_child(nd, nd->front, rc);
+    // All or nothing: the node's rule set is validated on the front, every shard's part and the front's whole set are
+    // prepared beside the live state (surviving flowIds' metrics copied: a surviving flowId keeps its owner, hence its
+    // ClusterMetric) together with the routing tables, and only when all of that succeeded is anything committed. A
+    // failure (validation, allocation, device) leaves the node deciding with its previous rules.
+    sg_handle* f = nd->front;
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    drain_async(f);
+    int rc = flow_rules_validate(f, rules, n);
+    if (rc) return node_child(nd, f, rc);
     const uint32_t G = (uint32_t)nd->shards.size();
     std::vector<std::vector<sg_flow_rule>> part(G);
     std::vector<uint8_t> so(n);
@@ -4543,23 +4705,63 @@ int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) 
         lo[k] = (uint32_t)part[g].size();
         part[g].push_back(rules[k]);
     }
-    for (uint32_t g = 0; g < G; ++g) {  // a surviving flowId keeps its owner, hence its ClusterMetric
-        rc = sg_load_flow_rules(nd->shards[g], part[g].data(), (uint32_t)part[g].size());
+    std::vector<FlowLoad> prep(G + 1);
+    uint8_t* d_so = nullptr;
+    uint32_t* d_lo = nullptr;
+    auto abort_all = [&](uint32_t upto) {  // the prepared shards [0, upto), the front's (index G) and the tables
+        for (uint32_t x = 0; x < upto; ++x) {
+            (void)hipSetDevice(nd->devices[x]);
+            flow_rules_abort(prep[x]);
+        }
+        (void)hipSetDevice(nd->devices[0]);
+        flow_rules_abort(prep[G]);
+        dfree(d_so);
+        dfree(d_lo);
+    };
+    // env SG_TEST_NODE_FAIL_SHARD = g (tests): preparing shard g fails as an allocation would
+    const char* inj = std::getenv("SG_TEST_NODE_FAIL_SHARD");
+    const int fail_g = inj ? std::atoi(inj) : -1;
+    for (uint32_t g = 0; g < G; ++g) {
+        sg_handle* h = nd->shards[g];
+        NHIP(nd, hipSetDevice(h->device));
+        drain_async(h);
+        rc = (int)g == fail_g ? fail(h, SG_E_NOMEM, "injected shard load failure (SG_TEST_NODE_FAIL_SHARD)")
+                              : flow_rules_validate(h, part[g].data(), (uint32_t)part[g].size());
+        if (!rc) rc = flow_rules_prepare(h, part[g].data(), (uint32_t)part[g].size(), prep[g]);
+        if (rc) {
+            rc = node_child(nd, h, rc);
+            abort_all(g);
+            return rc;
+        }
+    }
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    rc = flow_rules_prepare(f, rules, n, prep[G]);
+    if (!rc && n && (hipMalloc(&d_so, n) != hipSuccess || hipMalloc(&d_lo, sizeof(uint32_t) * n) != hipSuccess ||
+                     hipMemcpy(d_so, so.data(), n, hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMemcpy(d_lo, lo.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice) != hipSuccess))
+        rc = fail(f, SG_E_NOMEM, "routing tables");
+    if (rc) {
+        rc = node_child(nd, f, rc);
+        abort_all(G);
+        return rc;
+    }
+    // commit (host tables and pointer swaps; only the small per-rule uploads can still fail)
+    for (uint32_t g = 0; g < G; ++g) {
+        NHIP(nd, hipSetDevice(nd->devices[g]));
+        rc = flow_rules_commit(nd->shards[g], part[g].data(), (uint32_t)part[g].size(), prep[g]);
         if (rc) return node_child(nd, nd->shards[g], rc);
     }
     NHIP(nd, hipSetDevice(nd->devices[0]));
+    rc = flow_rules_commit(f, rules, n, prep[G]);
+    if (rc) return node_child(nd, f, rc);
     dfree(nd->d_shard_of);
     dfree(nd->d_local_of);
-    if (n) {
-        if (hipMalloc(&nd->d_shard_of, n) != hipSuccess || hipMalloc(&nd->d_local_of, sizeof(uint32_t) * n) != hipSuccess)
-            return nfail(nd, SG_E_NOMEM, "routing tables");
-        NHIP(nd, hipMemcpy(nd->d_shard_of, so.data(), n, hipMemcpyHostToDevice));
-        NHIP(nd, hipMemcpy(nd->d_local_of, lo.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
-    }
+    nd->d_shard_of = d_so;
+    nd->d_local_of = d_lo;
     nd->rules.assign(rules, rules + n);
     nd->shard_of = so;
     nd->local_of = lo;
-    return SG_OK;
+    return node_sync_layout(nd);
 }
 
 sg_handle* sg_node_front(sg_node* nd) { return nd ? nd->front : nullptr; }
@@ -4583,18 +4785,26 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
     for (sg_handle* h : nd->shards) drain_async(h);
     int rc = ensure_layout(f);
     if (rc) return node_child(nd, f, rc);
-    // 1. the front: validation + namespace limiter in caller order, the batch's time check, its last timestamp
+    // 1. the front: validation + namespace limiter in caller order, the batch's time check, its last timestamp, the
+    // default results in the caller's buffer, the batch's period tables
     NHIP(nd, hipStreamSynchronize(user));  // the caller's batch is in place
     sg_handle::FlowWs w;
     main_ws(f, w);
     BatchArgs a = flow_args(f, w, req, n, out);
-    a.hist0 = nullptr;
+    // one shard holding every rule in the front's order (G = 1): the front's records are its records as they are
+    const bool direct = nd->rec_path && G == 1 && nd->shards[0]->K == f->K && nd->shards[0]->kbits == f->kbits;
+    if (!direct) a.hist0 = nullptr;
+    a.csum0 = nullptr;
     NHIP(nd, hipMemsetAsync(a.err, 0, sizeof(int), nd->s0));
+    if (a.hist0 && radix_csum_atomic()) {
+        a.csum0 = radix_csum(a.hist0, a.n, a.hist0_bits);
+        NHIP(nd, hipMemsetAsync(a.csum0, 0, radix_csum_bytes(a.n, a.hist0_bits), nd->s0));
+    }
     NHIP(nd, launch_prep(a, nd->s0));
     rc = flow_limiter(f, a, nd->s0);
     if (rc) return node_child(nd, f, rc);
     NHIP(nd, launch_finish(a, nd->s0));
-    // 2. routing by owner
+    // 2. routing by owner (not for one shard on the records path)
     RouteArgs r{};
     r.req = req;
     r.rec = a.rec;
@@ -4611,13 +4821,24 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
     r.shard_tot = nd->d_base + kMaxShards + 1;
     r.sub_req = nd->d_sub_req;
     r.sub_pos = nd->d_sub_pos;
-    NHIP(nd, launch_route(r, nd->s0));
-    NHIP(nd, hipMemcpyAsync(nd->h_base, nd->d_base, sizeof(uint32_t) * (2 * kMaxShards + 1), hipMemcpyDeviceToHost,
-                            nd->s0));
+    if (nd->rec_path) {
+        r.sub_rec = nd->d_sub_rec;
+        r.low_mask = (1ull << a.kshift) - 1;
+        for (uint32_t g = 0; g < G; ++g) r.skshift[g] = 64 - nd->shards[g]->kbits;
+    }
+    if (!direct) {
+        NHIP(nd, launch_route(r, nd->s0));
+        NHIP(nd, hipMemcpyAsync(nd->h_base, nd->d_base, sizeof(uint32_t) * (2 * kMaxShards + 1), hipMemcpyDeviceToHost,
+                                nd->s0));
+    }
     NHIP(nd, hipMemcpyAsync(nd->h_front_err, a.err, sizeof(int), hipMemcpyDeviceToHost, nd->s0));
     NHIP(nd, hipEventRecord(nd->routed, nd->s0));
     NHIP(nd, hipStreamSynchronize(nd->s0));
     if (*nd->h_front_err) return node_child(nd, f, flow_status(f, *nd->h_front_err));
+    if (direct) {
+        nd->h_base[0] = 0;
+        nd->h_base[kMaxShards + 1] = (uint32_t)n;  // the sentinel records of rejected requests sort to the end
+    }
     // 3. every shard decides its slice on its own stream
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t base = nd->h_base[g], cnt = nd->h_base[kMaxShards + 1 + g];
@@ -4627,25 +4848,73 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
         const int dev = nd->devices[g];
         NHIP(nd, hipSetDevice(dev));
         NHIP(nd, hipStreamWaitEvent(nd->streams[g], nd->routed, 0));
-        const sg_req* sreq = nd->d_sub_req + base;
-        sg_result* sout = nd->d_sub_out + base;
-        if (dev != nd->devices[0]) {
-            NHIP(nd, hipMemcpyPeerAsync(nd->r_req[g], dev, sreq, nd->devices[0], sizeof(sg_req) * cnt, nd->streams[g]));
-            sreq = nd->r_req[g];
-            sout = nd->r_out[g];
+        if (nd->rec_path) {
+            // the slice's records (node request indices) through the shard's sort and walkers; the period tables,
+            // window lengths, requests and results are the node batch's
+            sg_handle::FlowWs sw;
+            main_ws(h, sw);
+            BatchArgs b = flow_args(h, sw, req, cnt, out);
+            b.rec = direct ? a.rec : nd->d_sub_rec + base;
+            b.rec_sorted = direct ? h->d_rec_sorted : sw.rec;  // the sort's other buffer
+            b.hist0 = direct ? a.hist0 : nullptr;
+            b.hist0_bits = a.hist0_bits;
+            b.csum0 = direct ? a.csum0 : nullptr;
+            b.n_wl = a.n_wl;
+            std::memcpy(b.wl, a.wl, sizeof(b.wl));
+            b.bnd = a.bnd;
+            b.p0 = a.p0;
+            b.np = a.np;
+            hipStream_t st = nd->streams[g];
+            rc = [&]() -> int {
+                HIP_TRY(h, hipMemsetAsync(b.err, 0, sizeof(int), st));
+                HIP_TRY(h, hipMemsetAsync(b.long_count, 0, (1 + kClasses) * sizeof(uint32_t), st));
+                HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), st));
+                uint64_t* sorted = nullptr;
+                const SegMark mk{b.seg_start, b.seg_end, b.K, b.kshift};
+                b.seg_marked = (b.seg_start && b.seg_end && b.long_end && !h->seg_mark_pass) ? 1 : 0;
+                // direct: the first pass's histogram rows are the front's (k_prep counted them in its workspace)
+                HIP_TRY(h, radix_sort_records(b.rec, b.rec_sorted, cnt, b.kshift, direct ? w.hist : sw.hist, &sorted, st,
+                                              64, b.hist0 != nullptr, b.seg_marked ? &mk : nullptr, b.csum0 != nullptr));
+                b.rec_sorted = sorted;
+                HIP_TRY(h, launch_seg_flow(b, st));
+                HIP_TRY(h, hipEventRecord(h->fork, st));
+                HIP_TRY(h, hipStreamWaitEvent(h->aux, h->fork, 0));
+                HIP_TRY(h, launch_walk_long(b, h->aux));
+                HIP_TRY(h, launch_walk_short(b, st));
+                HIP_TRY(h, hipEventRecord(h->join, h->aux));
+                HIP_TRY(h, hipStreamWaitEvent(st, h->join, 0));
+                HIP_TRY(h, launch_skip_apply(b, st));
+                HIP_TRY(h, hipMemcpyAsync(nd->h_err[g], b.err, sizeof(int), hipMemcpyDeviceToHost, st));
+                return SG_OK;
+            }();
+            if (rc) {
+                node_sync_shards(nd, g + 1);
+                return node_child(nd, h, rc);
+            }
+        } else {
+            const sg_req* sreq = nd->d_sub_req + base;
+            sg_result* sout = nd->d_sub_out + base;
+            if (dev != nd->devices[0]) {
+                NHIP(nd, hipMemcpyPeerAsync(nd->r_req[g], dev, sreq, nd->devices[0], sizeof(sg_req) * cnt, nd->streams[g]));
+                sreq = nd->r_req[g];
+                sout = nd->r_out[g];
+            }
+            rc = enqueue_flow(h, sreq, cnt, sout, nd->streams[g], nd->h_err[g], false);
+            if (rc) {
+                node_sync_shards(nd, g + 1);
+                return node_child(nd, h, rc);
+            }
+            if (dev != nd->devices[0])
+                NHIP(nd, hipMemcpyPeerAsync(nd->d_sub_out + base, nd->devices[0], sout, dev, sizeof(sg_result) * cnt,
+                                            nd->streams[g]));
         }
-        rc = enqueue_flow(h, sreq, cnt, sout, nd->streams[g], nd->h_err[g], false);
-        if (rc) return node_child(nd, h, rc);
-        if (dev != nd->devices[0])
-            NHIP(nd, hipMemcpyPeerAsync(nd->d_sub_out + base, nd->devices[0], sout, dev, sizeof(sg_result) * cnt,
-                                        nd->streams[g]));
         NHIP(nd, hipEventRecord(nd->done[g], nd->streams[g]));
     }
-    // 4. back into caller order
+    // 4. back into caller order (the sub_req path; the records path wrote the results in place)
     NHIP(nd, hipSetDevice(nd->devices[0]));
     for (uint32_t g = 0; g < G; ++g)
         if (nd->h_base[kMaxShards + 1 + g]) NHIP(nd, hipStreamWaitEvent(nd->s0, nd->done[g], 0));
-    NHIP(nd, launch_route_gather(nd->d_sub_out, nd->d_sub_pos, nd->h_base[G], out, nd->s0));
+    if (!nd->rec_path) NHIP(nd, launch_route_gather(nd->d_sub_out, nd->d_sub_pos, nd->h_base[G], out, nd->s0));
     NHIP(nd, hipEventRecord(nd->routed, nd->s0));
     NHIP(nd, hipStreamWaitEvent(user, nd->routed, 0));
     NHIP(nd, hipStreamSynchronize(nd->s0));

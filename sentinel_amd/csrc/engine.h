@@ -133,7 +133,8 @@ struct BatchArgs {
     uint64_t exit_amask; // (zeroed before; an exit is a record of a resource whose kind bits (amask >> 1 & 3) are set)
     int dbg;             // debugging switches (env SG_DEBUG): 1 = period table from HBM, 2 = one stream
                          // (serialised walkers, for per-kernel profiles), 64 = short-walker counters into dbg_ctr,
-                         // 128 = length class 0 through k_walk_tiny
+                         // 128 = length class 0 through k_walk_tiny; timing experiments only (wrong results):
+                         // 4096 = no k_walk_long, 8192 = no k_walk_short, 16384 = k_prep writes no default results
     int narrow;          // PASS / WAITING of every bucket provably < 2^30 (short walker's 12 B LDS snapshot)
     int generic_walker;  // SG_FLAG_RING_REREAD: short walker re-reads the ring (no register snapshot)
     int tiny;            // 1: length class 0 (<= kClassMax[0] records) is walked by k_walk_tiny, not k_walk_short
@@ -741,6 +742,13 @@ struct RouteArgs {
     uint32_t* shard_tot;       // [G] requests routed to each shard
     sg_req* sub_req;           // [n] the shard slices, one after the other
     uint32_t* sub_pos;         // [n] node position of each sub-request
+    // shards on the front's device (sub_rec != null): the slices are the shards' packed records instead — the
+    // front's record with its key field replaced by the shard-local rule index (shifted by the shard's kshift); the
+    // request index stays the node's, so the shards' walkers read the node batch's period tables and write the
+    // caller's results in place (no sub_req / sub_pos, no gather)
+    uint64_t* sub_rec;
+    uint64_t low_mask;         // the record bits below the front's key field (request index, acquire code)
+    int skshift[kMaxShards];   // each shard's key shift
 };
 hipError_t launch_route(const RouteArgs& r, hipStream_t stream);
 hipError_t launch_route_gather(const sg_result* sub_out, const uint32_t* sub_pos, uint64_t total, sg_result* out,

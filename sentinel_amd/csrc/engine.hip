@@ -166,10 +166,12 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
             st = SG_STATUS_BLOCKED;  // walkers write only non-BLOCKED
         }
-        int32_t* o = &a.out[i].status;  // the default result {st, 0, 0}
-        st_stream(o, st);
-        st_stream(o + 1, 0);
-        st_stream(o + 2, 0);
+        if (!(a.dbg & 16384)) {
+            int32_t* o = &a.out[i].status;  // the default result {st, 0, 0}
+            st_stream(o, st);
+            st_stream(o + 1, 0);
+            st_stream(o + 2, 0);
+        }
         st_stream(a.rec + i, rec);
         if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
     }
@@ -1026,7 +1028,7 @@ __global__ void __launch_bounds__(256) k_long_bounds(BatchArgs a) {
 #define SG_WLONG_BLOCKS 2
 #endif
 __global__ void __launch_bounds__(256, SG_WLONG_BLOCKS) k_walk_long(BatchArgs a) {
-    if (*a.err) return;
+    if (*a.err || (a.dbg & 4096)) return;
     stage_periods(a);
     if (g_blds) walk_long_body<true>(a);
     else walk_long_body<false>(a);
@@ -1631,7 +1633,7 @@ __global__ void __launch_bounds__(256, C ? SG_SHORT_C_BLOCKS : kShortBlocksPerCu
     static_assert(SM <= kGatherMaxS, "LDS budget of the ring snapshot");
     __shared__ SlotSnap snap_all[4 * (SM > 0 ? 64 * SM : 1)];
     __shared__ uint32_t recs_all[SM > 0 && C ? 4 * kRecW * 64 : 1];
-    if (*a.err) return;
+    if (*a.err || (a.dbg & 8192)) return;
     stage_periods(a);
     if (g_blds) walk_short_body<SM, true, C>(a, snap_all, recs_all);
     else walk_short_body<SM, false, C>(a, snap_all, recs_all);

@@ -14,6 +14,8 @@
 //                    every routed request — time order within a shard is kept (stable), so each slice is a valid
 //                    batch for its shard
 //   k_route_gather   out[pos[j]] = sub_out[j]: the shards' results in caller order
+// Shards on the front's device take packed records instead (RouteArgs::sub_rec): 8 B read and 8 B written per routed
+// request, and the shards write the caller's results in place (no gather).
 // HBM-bound byte work: 16 B read + 16 B + 4 B written per request (scatter), 12 B + 4 B read and 12 B written
 // (gather); no MFMA.
 #include "engine.h"
@@ -145,14 +147,18 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_scatter(RouteArgs r) {
             const uint32_t pos = r.shard_base[s] + r.tile_cnt[(size_t)blockIdx.x * kMaxShards + s] + before +
                                  wrun[wave][s] + rank;
             const uint32_t k = (uint32_t)(rec >> r.kshift);
-            const uint32_t idx = (uint32_t)((rec >> r.abits) & r.imask);
-            const sg_req q = r.req[idx];
-            sg_req o;
-            o.ts_ms = q.ts_ms;
-            o.key = r.local_of[k] | (q.key & SG_KEY_PRIO);
-            o.acquire = q.acquire;
-            r.sub_req[pos] = o;
-            r.sub_pos[pos] = idx;
+            if (r.sub_rec) {
+                r.sub_rec[pos] = ((uint64_t)r.local_of[k] << r.skshift[s]) | (rec & r.low_mask);
+            } else {
+                const uint32_t idx = (uint32_t)((rec >> r.abits) & r.imask);
+                const sg_req q = r.req[idx];
+                sg_req o;
+                o.ts_ms = q.ts_ms;
+                o.key = r.local_of[k] | (q.key & SG_KEY_PRIO);
+                o.acquire = q.acquire;
+                r.sub_req[pos] = o;
+                r.sub_pos[pos] = idx;
+            }
         }
         if (s < (uint32_t)r.G && rank == 0) wrun[wave][s] += (uint32_t)__popcll(peers);
     }

@@ -150,3 +150,50 @@ def test_node_rejects_a_batch_as_a_whole():
     req = _batch(rng, 5000, 50, 10_600, 500)
     assert np.array_equal(node.decide_host(req), cts.decide(req))
     _compare_state(node, cts, rules)
+
+
+@pytest.mark.parametrize("G", [1, 3])
+def test_node_sub_request_path(monkeypatch, G):
+    """The sub-request path (shards re-validate their slices and the results are gathered back; the path of shards on
+    other devices), forced on one device with SG_NODE_LEGACY: the same answers as the records path."""
+    monkeypatch.setenv("SG_NODE_LEGACY", "1")
+    test_node_equals_one_token_service(G, 3000.0)
+
+
+@pytest.mark.parametrize("fail_shard", [0, 2])
+def test_node_rule_load_is_all_or_nothing(monkeypatch, fail_shard):
+    """sg_node_load_flow_rules validates the node's set before it changes anything (a duplicate flowId: SG_E_INVAL) and
+    puts the shards already loaded back when a later one fails (an injected allocation failure): either way the node
+    keeps deciding with its previous rules, equal to a token service that never saw the failed loads."""
+    from sentinel_amd.engine import EngineError, NodeEngine
+    rng = np.random.default_rng(7 + fail_shard)
+    K = 150
+    rules = _rules(rng, K)
+    ns = _ns(2000.0)
+    node = NodeEngine([0, 0, 0], max_batch=1 << 16)
+    node.set_namespaces(ns)
+    node.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(ns)
+    cts.load_rules(rules)
+    t = 1_700_000_000_000
+    req = _batch(rng, 20_000, K, t, 900)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    dup = rules.copy()
+    dup["flow_id"][5] = dup["flow_id"][6]
+    with pytest.raises(EngineError) as ei:
+        node.load_rules(dup)
+    assert ei.value.code == abi.SG_E_INVAL
+    other = _rules(rng, K + 40, fid0=2_000_000)
+    monkeypatch.setenv("SG_TEST_NODE_FAIL_SHARD", str(fail_shard))
+    with pytest.raises(EngineError) as ei:
+        node.load_rules(other)
+    assert ei.value.code == abi.SG_E_NOMEM
+    monkeypatch.delenv("SG_TEST_NODE_FAIL_SHARD")
+    t = int(req["ts_ms"][-1]) + 1
+    for _ in range(2):
+        req = _batch(rng, 20_000, K, t, 900)
+        got, want = node.decide_host(req), cts.decide(req)
+        assert np.array_equal(got, want), f"{int((got != want).sum())} results differ after the failed loads"
+        t = int(req["ts_ms"][-1]) + 1
+    _compare_state(node, cts, rules)
