@@ -1172,7 +1172,12 @@ int local_status(sg_handle* h, int err) {
 }
 
 int ticket_status(sg_handle* h, const sg_handle::DevTicket& d) {
-    return d.local ? local_status(h, *d.h_err) : flow_status(h, *d.h_err);
+    if (!d.local) return flow_status(h, *d.h_err);
+    const int rc = local_status(h, *d.h_err);
+    // a refused pipelined batch (e.g. its first timestamp behind the previous batch's, found by the back half)
+    // decided nothing: it does not count as a batch seen (enqueue_local_pipelined counted it)
+    if (rc != SG_OK && h->l_batches > 0) --h->l_batches;
+    return rc;
 }
 
 // Workspace 0: the handle's own batch buffers.
@@ -3362,9 +3367,13 @@ int local_decide(sg_handle* h, const sg_local_event* ev, const sg_slot_ext* ext,
         HIP_TRY(h, hipMemcpyAsync(h->h_lnode_new, h->d_lnode_new, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(h, hipStreamSynchronize(stream));
         const uint64_t used = (uint64_t)h->l_pool_used + *h->h_lnode_new;
+        // The map now holds the batch's new nodes (indices below K + used), so the allocator moves past them even
+        // when the pool cannot grow now: this batch is then refused, and the next one grows the pool before any
+        // walker reads a node. Nodes a refused batch created stay, with zero counts (NodeSelectorSlot and
+        // ClusterBuilderSlot create them at entry, before any rule is checked).
         const int rc = lnode_grow(h, used);
-        if (rc) return rc;
         h->l_pool_used = (uint32_t)used;
+        if (rc) return rc;
         L.N = h->l_nodes;
         L.head = h->d_lhead;
         L.sec = h->d_lsec;
@@ -3821,10 +3830,10 @@ int sg_local_load_flow_rules(sg_handle* h, const sg_local_flow_rule* rules, uint
     if (n_origins < 0 || n_contexts < 0) return fail(h, SG_E_INVAL, "n_origins / n_contexts < 0");
     if (n_origins < h->l_n_origins || n_contexts < h->l_n_contexts)
         return fail(h, SG_E_INVAL, "origin / context ids keep their meaning across loads: the counts cannot shrink");
+    drain_async(h);  // batches on the pipeline decide under the rules they were enqueued with (and settle l_batches)
     if (n_contexts > 0 && h->l_n_contexts == 0 && h->l_batches > 0)
         return fail(h, SG_E_UNSUPPORTED, "context tracking (n_contexts >= 1) starts before the first batch: a DefaultNode "
                                          "holds every entry of its context since the resource's first one");
-    drain_async(h);  // batches on the pipeline decide under the rules they were enqueued with
     const bool track_ctx = n_contexts > 0;
     const uint32_t K = (uint32_t)h->ltab.size();
     const int cold = h->lcfg.cold_factor > 1 ? h->lcfg.cold_factor : 3;
