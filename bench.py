@@ -181,6 +181,70 @@ def end_to_end(eng, wl, first_b, n_batches, n_req, n_out=4):
             "path": "pinned host buffers -> sg_flow_submit (H2D / decide / D2H overlapped, 3 in flight) -> sg_flow_wait"}
 
 
+def node_main(args):
+    """--node: the node handle (sg_node_*) as a token server over N devices in ONE process — the front on device 0
+    validates and runs the namespace limiters over each node batch in caller order, routes the requests by owner
+    (splitmix64(flowId) mod N) and every shard decides its slice on its device (the records path and the node
+    pipeline, sg_node_flow_enqueue, when all shards share device 0; peer copies of the slices over xGMI otherwise).
+    Weak scaling: N x --requests per node batch over N x --flows flowIds. Not the driver's launch (that one is
+    torch.distributed.run with one rank per GPU and no routing); this line prices the routing."""
+    from sentinel_amd.engine import NodeEngine
+    N = args.gpus
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n_req = args.requests * N
+    wl = ShardWorkload(args.flows * N, n_req, 0, 1, dev)
+    nd = NodeEngine(list(range(N)), max_batch=n_req)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = args.limiter_qps if args.limiter_qps > 0 else 30000
+    ns["limiter_enabled"] = 1 if args.limiter_qps > 0 else 0
+    nd.set_namespaces(ns)
+    nd.load_rules(wl.rules)
+    total_steps = args.warmup + args.steps
+    batches = [wl.batch(b) for b in range(total_steps)]
+    outs = [torch.empty(n_req * RES_B, dtype=torch.uint8, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+
+    def run_steps(b0, b1):
+        tickets = []
+        for b in range(b0, b1):
+            if len(tickets) >= 2:
+                nd.wait(tickets.pop(0))
+            tickets.append(nd.enqueue_device(batches[b].data_ptr(), n_req, outs[b % 2].data_ptr()))
+        for t in tickets:
+            nd.wait(t)
+
+    run_steps(0, args.warmup)
+    for d in range(N):
+        torch.cuda.synchronize(d)
+    t0 = time.perf_counter()
+    run_steps(args.warmup, total_steps)
+    for d in range(N):
+        torch.cuda.synchronize(d)
+    elapsed = time.perf_counter() - t0
+    last = batches[-1].view(torch.int64).reshape(-1, 2)[:, 1] & 0x7FFFFFFF
+    touched = int(torch.unique(last).numel())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    b_alg = n_req * (REQ_B + RES_B) + touched * (STATE_B + RULE_B)
+    step_gbs = b_alg / (ms_per_step / 1000.0) / 1e9
+    peak = HBM_PEAK_GBS * N
+    print(json.dumps({
+        "metric": "flow decisions/sec (node) at 1M flowIds, 1/2/4/8 GPU; HBM GB/s vs peak",
+        "value": n_req / (elapsed / args.steps), "unit": "decisions/s", "n_gpus": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (GPU-generated, seeded): Zipf(1.0) flowIds, counts U{1..32}, 10% acquire U{2..4}, 1% prioritized",
+        "config": {"workload": "C3 cluster token server through the node handle (sg_node, routing inside)",
+                   "flow_ids": args.flows * N, "requests_per_step": n_req, "simulated_ms_per_step": wl.span_ms,
+                   "parallelism": f"sg_node over {N} device(s), one process",
+                   "namespace_limiter": (f"on, maxAllowedQps {args.limiter_qps:g}" if args.limiter_qps > 0 else "off")},
+        "roofline": {"bound": "hbm", "kernel": "whole node batch (front prep + routing + shard sort + walk), step time",
+                     "achieved": step_gbs, "peak": peak, "unit": "GB/s", "frac": step_gbs / peak, "traffic": None,
+                     "algorithmic_bytes_per_step": b_alg, "touched_flow_ids": touched},
+    }), flush=True)
+
+
 def launch_ranks(n):
     """Run this script as n ranks of one node (the driver's own launch line), as a child process."""
     import socket
@@ -207,7 +271,12 @@ def main():
     ap.add_argument("--limiter-qps", type=float, default=0.0,
                     help="namespace GlobalRequestLimiter maxAllowedQps (SURVEY §8d C3's second run: 1e12 exercises the "
                          "pre-pass without rejecting); 0: limiter off, the headline configuration")
+    ap.add_argument("--node", action="store_true",
+                    help="one process, one sg_node over --gpus N devices: node-order batches of N x --requests over "
+                         "N x --flows flowIds, routing inside the library and inside the timed region")
     args = ap.parse_args()
+    if args.node:
+        return node_main(args)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `bench.py --gpus N` outside a launcher: start N ranks (one process per GPU) through torch.distributed.run

@@ -13,6 +13,9 @@ bench.py (which measures the headline C3 workload).
                  the CPU oracle's client model (oracle.binding.LocalTraceGen) before the timed region.
   --workload cparam  cluster hot-parameter tokens: 1000 ClusterParamFlowRules, 50k values each Zipf(1.1), 16M
                  requests per batch, 10 % with 2-3 values (the fixed-point path).
+  --workload slot  the whole slot chain at C5 size with 10 % of the resources carrying an origin-limitApp rule, a
+                 WarmUp rule or a ParamFlowRule (the cx walker's share); every batch checked against the oracle.
+  --workload node  the C3 workload through the node handle (G same-device shards, --shards), pipelined.
   --workload pace  1M resources, each a FlowRule with CONTROL_BEHAVIOR_RATE_LIMITER (RateLimiterController,
                  count U{1..64}, maxQueueingTimeMs 500), 16M canPass calls per 1000 ms batch, Zipf(1.0),
                  acquire 1 (10 % U{2..4}).
@@ -223,6 +226,130 @@ def c5(args, dev):
             "value": decided / el, "el": el, "n": decided // args.steps, "b_alg": b_alg, "touched": touched,
             "cpu": base, "data": "synthetic (seeded): Zipf(1.0) resources, rt lognormal(2.5, 0.8) ms, 5% errors; "
                                  "exits generated by the oracle client model"}
+
+
+def slot(args, dev):
+    """The whole slot chain at C5 size (sg_slot_decide_batch: ParamFlowSlot -> FlowSlot -> DegradeSlot inside
+    StatisticSlot), with 10 % of the 1M resources off the fast walkers' single-DefaultController shape: a third carry an
+    origin-limitApp rule beside their default rule (their callers pass an origin: 70 % of their entries, U{1..4}), a
+    third a WarmUp rule (warmUpPeriodSec 10, coldFactor 3), a third a ParamFlowRule on argument 0 (QPS, count U{5..20},
+    1 s; the argument one of 1000 values, Zipf 1.1). Every resource keeps C5's RT and exception-ratio breakers. Those
+    resources go through the cx walker (k_lwalk_cx); with Zipf(1.0) popularity some of the hottest are among them.
+    Entries + the exits of passed entries (the oracle's client model, as C5); the batches are synchronous (origin
+    nodes are created with a host round trip). Every timed batch's results are checked against the oracle."""
+    from oracle.binding import LocalChain, LocalTraceGen, ParamFlowSlot, degrade_rule
+    K, n = args.resources, args.events
+    rng = np.random.default_rng(7)
+    base = np.zeros(K, abi.LOCAL_RULE_DTYPE)
+    base["flow_grade"] = abi.FLOW_GRADE_NONE
+    base["n_breakers"] = 2
+    b = np.zeros(2, abi.DEGRADE_RULE_DTYPE)
+    b[0] = degrade_rule(abi.DEGRADE_RT, 100, 10, 5, 1000, 0.5)
+    b[1] = degrade_rule(abi.DEGRADE_EXCEPTION_RATIO, 0.5, 10, 5, 1000)
+    base["breakers"] = b
+    kind = np.zeros(K, np.int64)  # 0 plain, 1 origin-limitApp, 2 WarmUp, 3 param rule
+    cx = rng.random(K) < 0.10
+    kind[cx] = rng.integers(1, 4, int(cx.sum()))
+    n_org = int((kind == 1).sum())
+    fr = np.zeros(K + n_org, abi.LOCAL_FLOW_RULE_DTYPE)
+    fr["resource"][:K] = np.arange(K)
+    fr["grade"] = abi.FLOW_GRADE_QPS
+    fr["count"][:K] = rng.integers(1, 65, K)
+    fr["control_behavior"][:K] = np.where(kind == 2, abi.CONTROL_WARM_UP, abi.CONTROL_DEFAULT)
+    fr["limit_app"] = abi.LIMIT_APP_DEFAULT
+    fr["strategy"] = abi.STRATEGY_DIRECT
+    fr["warm_up_period_sec"] = 10
+    fr["max_queueing_ms"] = 500
+    fr["ref_resource"] = -1
+    fr["cluster_key"] = abi.KEY_NO_RULE
+    org_res = np.nonzero(kind == 1)[0]
+    fr["resource"][K:] = org_res
+    fr["count"][K:] = rng.integers(1, 17, n_org)
+    fr["limit_app"][K:] = rng.integers(1, 5, n_org)
+    par_res = np.nonzero(kind == 3)[0]
+    params = np.zeros(len(par_res), abi.PSLOT_RULE_DTYPE)
+    params["resource"] = par_res
+    params["param_idx"] = 0
+    params["grade"] = abi.FLOW_GRADE_QPS
+    params["rule"]["count"] = rng.integers(5, 21, len(par_res))
+    params["rule"]["duration_sec"] = 1
+    n_vals = 1000
+    pargs = np.zeros(n_vals, abi.PSLOT_ARG_DTYPE)
+    pargs["value_begin"] = np.arange(n_vals)
+    pargs["value_count"] = 1
+    pargs["kind"] = abi.ARG_VALUE
+    values = np.arange(1, n_vals + 1, dtype=np.uint64)
+    vcdf, _ = zipf_cdf(n_vals, 1.1, 8)
+    cdf, perm = zipf_cdf(K, 1.0, 7)
+    ora = LocalChain(2, 1000, 500)
+    ora.load_rules(base)
+    kept = ora.load_flow_rules(fr, 4, 0)
+    ps = ParamFlowSlot(params, n_resources=K)
+    ora.attach_params(ps)
+    gen = LocalTraceGen(ora)
+    host, wants = [], []
+    gen_s = 0.0
+    for bt in range(args.warmup + args.steps):
+        ent = np.zeros(n, abi.LOCAL_EVENT_DTYPE)
+        ent["ts_ms"] = T0 + 1000 * bt + np.sort(rng.integers(0, 1000, n))
+        res = perm[np.minimum(np.searchsorted(cdf, rng.random(n), side="right"), K - 1)]
+        ent["resource"] = res
+        ent["count"] = 1
+        og = rng.integers(1, 5, n).astype(np.int32)
+        og[(kind[res] != 1) | (rng.random(n) < 0.3)] = 0
+        ent["origin"] = og
+        ext = np.zeros(n, abi.SLOT_EXT_DTYPE)
+        ext["args_null"] = (kind[res] != 3).astype(np.int32)
+        ext["arg_begin"] = np.minimum(np.searchsorted(vcdf, rng.random(n), side="right"), n_vals - 1)
+        ext["arg_count"] = 1
+        rt = np.minimum(np.round(np.exp(rng.normal(2.5, 0.8, n))), 10_000).astype(np.int32)
+        err = (rng.random(n) < 0.05).astype(np.uint8)
+        t = time.perf_counter()
+        ev, xo, want = gen.run_ext(ent, ext, rt, err, T0 + 1000 * (bt + 1), pargs, values)
+        gen_s += time.perf_counter() - t
+        host.append((ev, xo))
+        wants.append(want)
+        print(f"# slot trace batch {bt}: {len(ev)} events, {gen_s:.1f} s so far", file=sys.stderr, flush=True)
+    print(f"# slot trace: {sum(len(e) for e, _ in host)} events generated by the oracle client model in {gen_s:.1f} s",
+          file=sys.stderr)
+    eng = FlowEngine(device=0, max_batch=max(len(e) for e, _ in host))
+    eng.local_load_rules(base, 2, 1000, 500)
+    assert eng.local_load_flow_rules(fr, 4, 0) == kept
+    eng.pslot_load_rules(params, n_resources=K)
+    d_args = torch.from_numpy(pargs.view(np.uint8).copy()).to(dev)
+    d_vals = torch.from_numpy(values.view(np.uint8).copy()).to(dev)
+    evs = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e, _ in host]
+    exs = [torch.from_numpy(x.view(np.uint8).copy()).to(dev) for _, x in host]
+    sizes = [len(e) for e, _ in host]
+    outs = [torch.empty(sz * 8, dtype=torch.uint8, device=dev) for sz in sizes]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    el = timed(lambda i: eng.slot_decide_device(evs[i].data_ptr(), exs[i].data_ptr(), sizes[i], d_args.data_ptr(),
+                                                n_vals, d_vals.data_ptr(), n_vals, outs[i].data_ptr(), stream),
+               args.warmup, args.steps)
+    for i in range(len(sizes)):  # full-size parity of every batch
+        got = outs[i].cpu().numpy().view(abi.LOCAL_RES_DTYPE)
+        if not np.array_equal(got, wants[i]):
+            bad = np.nonzero(got != wants[i])[0]
+            raise AssertionError(f"slot batch {i}: {len(bad)} results differ from the oracle (first at {bad[0]})")
+    decided = sum(sizes[args.warmup:])
+    last = host[-1][0]
+    touched = int(np.unique(last["resource"] & 0x7FFFFFFF).size)
+    hot = perm[:1000]
+    b_alg = sizes[-1] * (32 + 16 + 8) + touched * (2 * 128 + 2 * 2 * 64 + 2 * 128 + 80)  # C5's bytes + the ext
+    base_cpu = {"value": sum(sizes) / gen_s, "unit": "decisions/s", "cores": 1, "kind": "port",
+                "sample": f"the oracle replaying all {sum(sizes)} events while generating them (client model, 1 thread), "
+                          f"{gen_s:.1f} s"}
+    return {"metric": "slot-chain decisions/sec (entries + exits), 1M resources, 10 % origin / WarmUp / param rules",
+            "workload": "slot: C5 (1M resources, QPS FlowRule + RT + exception-ratio breakers, 16M entries/batch + exits) "
+                        "with 10 % of resources carrying an origin-limitApp rule, a WarmUp rule or a ParamFlowRule",
+            "value": decided / el, "el": el, "n": decided // args.steps, "b_alg": b_alg, "touched": touched,
+            "cpu": base_cpu,
+            "extra": {"cx_resources": int(cx.sum()), "cx_among_hottest_1000": int(cx[hot].sum()),
+                      "cx_share_of_entries": float(np.isin(last["resource"] & 0x7FFFFFFF,
+                                                            np.nonzero(cx)[0])[last["kind"] == 0].mean()),
+                      "parity": "every batch equal to the oracle"},
+            "data": "synthetic (seeded): Zipf(1.0) resources, rt lognormal(2.5, 0.8) ms, 5% errors; exits generated by "
+                    "the oracle client model"}
 
 
 def codec(args, dev):
@@ -452,8 +579,10 @@ def cparam(args, dev):
 def node(args, dev):
     """The node handle (sg_node_*) on one GPU: the C3 workload (1M flowIds, 16M requests per 1000 ms batch) decided
     by G same-device shard handles with the routing inside the library — validation and the namespace limiters on the
-    front handle, the stable multisplit by splitmix64(flowId) mod G, every shard on its own stream, the gather back
-    into caller order — against one handle's synchronous sg_flow_decide_batch on the same batches."""
+    front handle, the stable multisplit by splitmix64(flowId) mod G, every shard's sort and walkers — through the node
+    pipeline (sg_node_flow_enqueue: the front's part of batch i+1 and the shards' sorts beside the shards' walkers of
+    batch i, at most two batches in flight), against one handle's pipeline (sg_flow_enqueue) on the same batches;
+    --local-sync: both synchronous (sg_node_flow_decide_batch / sg_flow_decide_batch)."""
     import bench
     from sentinel_amd.engine import NodeEngine
     G = args.shards
@@ -467,32 +596,49 @@ def node(args, dev):
     one.set_namespaces(ns)
     one.load_rules(wl.rules)
     batches = [wl.batch(b) for b in range(args.warmup + args.steps)]
-    out = torch.empty(args.events * 12, dtype=torch.uint8, device=dev)
+    outs = [torch.empty(args.events * 12, dtype=torch.uint8, device=dev) for _ in range(2)]
     stream = torch.cuda.current_stream(dev).cuda_stream
-    el = timed(lambda b: nd.decide_device(batches[b].data_ptr(), args.events, out.data_ptr(), stream),
-               args.warmup, args.steps)
-    # the single handle on the same batches, one second later each (time order), synchronous entry point
+
+    def run(eng, bs, sync):
+        if sync:
+            return timed(lambda b: eng.decide_device(bs[b].data_ptr(), args.events, outs[0].data_ptr(), stream),
+                         args.warmup, args.steps)
+        tickets = []
+
+        def step(b):
+            if len(tickets) >= 2:
+                eng.wait(tickets.pop(0))
+            tickets.append(eng.enqueue_device(bs[b].data_ptr(), args.events, outs[b % 2].data_ptr()))
+        torch.cuda.synchronize()
+        el = timed(step, args.warmup, args.steps)
+        for t in tickets:
+            eng.wait(t)
+        return el
+
+    el = run(nd, batches, args.local_sync)
+    # the single handle on the same batches, later in time (each batch shifted past the node's last)
     later = [b.clone() for b in batches]
     for x in later:
         x.view(torch.int64).view(-1, 2)[:, 0] += 1000 * (args.warmup + args.steps)
-    el1 = timed(lambda b: one.decide_device(later[b].data_ptr(), args.events, out.data_ptr(), stream),
-                args.warmup, args.steps)
+    el1 = run(one, later, args.local_sync)
     n = args.events
     keys = batches[-1].view(torch.int64).view(-1, 2)[:, 1] & 0x7FFFFFFF
     touched = int(torch.unique(keys).numel())
     b_alg = n * (bench.REQ_B + bench.RES_B) + touched * (bench.STATE_B + bench.RULE_B)  # bench.py's C3 bytes
+    mode = "synchronous" if args.local_sync else "pipelined"
     return {"metric": f"flow decisions/sec through the node handle, {G} shards on one GPU (routing inside)",
             "workload": f"C3 workload (1M flowIds, 16M requests/batch, Zipf 1.0) on sg_node with {G} same-device "
-                        "shards",
+                        f"shards, {mode} node batches",
             "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": None,
-            "extra": {"shards": G, "single_handle_ms_per_step": el1 / args.steps * 1e3,
-                      "single_handle_decisions_per_s": n * args.steps / el1},
+            "extra": {"shards": G, "mode": mode, "single_handle_ms_per_step": el1 / args.steps * 1e3,
+                      "single_handle_decisions_per_s": n * args.steps / el1,
+                      "node_over_single": el / el1},
             "data": "synthetic (GPU-generated, seeded): bench.py's C3 batches"}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam", "node"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam", "node", "slot"], default="c2")
     ap.add_argument("--shards", type=int, default=2, help="node: shard handles on the one GPU")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -510,7 +656,8 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace, "cparam": cparam, "node": node}[args.workload](args, dev)
+    r = {"c2": c2, "c4": c4, "c5": c5, "codec": codec, "pace": pace, "cparam": cparam, "node": node,
+         "slot": slot}[args.workload](args, dev)
     ms = r["el"] * 1000.0 / args.steps
     gbs = r["b_alg"] / (ms / 1000.0) / 1e9
     res = {"metric": r["metric"], "value": r["value"], "unit": r.get("unit", "decisions/s"), "n_gpus": 1,

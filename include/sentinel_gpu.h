@@ -745,6 +745,7 @@ int sg_local_read_controller(sg_handle* h, uint32_t rule, int64_t* state3);
  *   sg_node_load_flow_rules ← sg_load_flow_rules for the node's rule set (keys = rule indices of this array);
  *                             a surviving flowId keeps its owner, hence its ClusterMetric
  *   sg_node_flow_decide_batch(_host) ← sg_flow_decide_batch over the node (device buffers on devices[0] / host)
+ *   sg_node_flow_enqueue / _poll / _wait ← sg_flow_enqueue / _poll / _wait over the node (pipelined)
  *   sg_node_flow_read_state, sg_node_snapshot_metrics ← per node rule, as the single-handle calls
  *   sg_node_shard_of        owner shard and local rule index of node rule `key` */
 typedef struct sg_node sg_node;
@@ -755,6 +756,16 @@ int         sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t
 int         sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n);
 int         sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out, void* stream);
 int         sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out);
+/* sg_flow_enqueue / _poll / _wait over the node (DEVICE buffers on devices[0], same ticket meaning): with every shard
+ * on devices[0] the node batches are pipelined — the front's validation, limiter and routing of batch i+1 and the
+ * shards' sorts run beside the shards' walkers of batch i, two node workspaces alternating; the host waits only for
+ * the front of the batch it enqueues (the slice sizes). Batches must be time-ordered; a batch the front refuses
+ * (validation, time order) reaches no shard and its ticket carries the error. With shards on other devices a node
+ * batch is decided synchronously and its status kept for the ticket. Every other sg_node_* call first completes
+ * the batches in flight. */
+int         sg_node_flow_enqueue(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket);
+int         sg_node_flow_poll(sg_node* nd, uint64_t ticket);
+int         sg_node_flow_wait(sg_node* nd, uint64_t ticket);
 int         sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy);
 int         sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap);
 int         sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key);

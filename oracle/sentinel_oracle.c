@@ -907,7 +907,7 @@ struct or_local {
     uint64_t batches;        /* batches decided since or_local_load_rules */
     or_cts* cts;             /* the embedded token server's DefaultTokenService (cluster_state SERVER) */
     int cluster_state;       /* ClusterStateManager: SG_CLUSTER_NOT_STARTED (default), SERVER */
-    int32_t* rule_pos;       /* loaded flow rule i → (resource << 16 | position), -1 = ignored */
+    int64_t* rule_pos;       /* loaded flow rule i → (resource << 32 | position), -1 = ignored */
     uint32_t n_rules;
     struct or_pslot* ps;     /* ParamFlowSlot's rules and metrics (or_local_attach_pslot), NULL = none */
     uint8_t* inbound;        /* per resource: its entries are EntryType.IN (Constants.ENTRY_NODE counts them) */
@@ -1041,21 +1041,34 @@ int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint3
     l->n_origins = n_origins;
     l->n_contexts = n_contexts;
     free(l->rule_pos);
-    l->rule_pos = (int32_t*)malloc((n ? n : 1) * sizeof(int32_t));
+    l->rule_pos = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
     l->n_rules = n;
     uint32_t* cnt = (uint32_t*)calloc(l->n ? l->n : 1, sizeof(uint32_t));
+    /* the kept rules of each resource as a chain (a duplicate has the same resource): last kept index per resource,
+     * previous kept index of the same resource per rule */
+    int64_t* last = (int64_t*)malloc((l->n ? l->n : 1) * sizeof(int64_t));
+    int64_t* prev = (int64_t*)malloc((n ? n : 1) * sizeof(int64_t));
+    for (uint32_t k = 0; k < l->n; k++) last[k] = -1;
     for (uint32_t i = 0; i < n; i++) {
         l->rule_pos[i] = -1;
         const sg_local_flow_rule* r = &rules[i];
         if (r->resource >= l->n || !flow_rule_valid(r)) continue;   /* ignored, as RecordLog.warn + continue */
-        if (r->limit_app > n_origins) { free(cnt); return SG_E_INVAL; }
-        if (r->strategy == SG_STRATEGY_CHAIN && r->ref_resource >= n_contexts) { free(cnt); return SG_E_INVAL; }
+        if (r->limit_app > n_origins || (r->strategy == SG_STRATEGY_CHAIN && r->ref_resource >= n_contexts)) {
+            free(cnt);
+            free(last);
+            free(prev);
+            return SG_E_INVAL;
+        }
         int dup = 0;
-        for (uint32_t j = 0; j < i && !dup; j++) dup = l->rule_pos[j] >= 0 && flow_rule_same(&rules[j], r);
+        for (int64_t j = last[r->resource]; j >= 0 && !dup; j = prev[j]) dup = flow_rule_same(&rules[j], r);
         if (dup) continue;
         l->rule_pos[i] = 0;
+        prev[i] = last[r->resource];
+        last[r->resource] = i;
         cnt[r->resource]++;
     }
+    free(last);
+    free(prev);
     for (uint32_t k = 0; k < l->n; k++)
         if (cnt[k]) l->nodes[k].ctl = (or_ctl*)calloc(cnt[k], sizeof(or_ctl));
     /* Collections.sort(rules, FlowRuleComparator): stable; local rules before cluster-mode ones, then non-"default"
@@ -1068,7 +1081,7 @@ int or_local_load_flow_rules(or_local* l, const sg_local_flow_rule* rules, uint3
             if (key != pass) continue;
             or_node* nd = &l->nodes[rules[i].resource];
             ctl_init(&nd->ctl[nd->n_ctl], &rules[i], l->cold_factor, (int32_t)i);
-            l->rule_pos[i] = (int32_t)((rules[i].resource << 16) | nd->n_ctl);
+            l->rule_pos[i] = (int64_t)(((uint64_t)rules[i].resource << 32) | (uint32_t)nd->n_ctl);
             nd->n_ctl++;
         }
     }
@@ -1686,8 +1699,8 @@ int or_local_rule_order(const or_local* l, uint32_t res, int32_t* out, uint32_t 
 /* {storedTokens, lastFilledTime, latestPassedTime} of loaded flow rule i; SG_E_INVAL when it was ignored. */
 int or_local_controller(const or_local* l, uint32_t i, int64_t* out3) {
     if (i >= l->n_rules || l->rule_pos[i] < 0) return SG_E_INVAL;
-    const or_node* nd = &l->nodes[(uint32_t)l->rule_pos[i] >> 16];
-    or_ctl_state(&nd->ctl[l->rule_pos[i] & 0xFFFF], out3);
+    const or_node* nd = &l->nodes[(uint64_t)l->rule_pos[i] >> 32];
+    or_ctl_state(&nd->ctl[l->rule_pos[i] & 0xFFFFFFFF], out3);
     return 0;
 }
 
@@ -2562,6 +2575,8 @@ struct or_pslot {
     int64_t now;                  /* the event's TimeUtil time */
     or_cts* cts;                  /* the embedded token server's DefaultTokenService (cluster_state SERVER) */
     int cluster_state;            /* ClusterStateManager: SG_CLUSTER_NOT_STARTED (default), SERVER */
+    uint32_t* res_off;            /* [n_res + 1]: rules of resource r = res_rules[res_off[r] .. res_off[r + 1]) */
+    uint32_t* res_rules;          /* rule indices grouped by resource, ascending (getRulesOfResource: load order) */
 };
 
 or_pslot* or_pslot_new(void) {
@@ -2587,6 +2602,8 @@ void or_pslot_free(or_pslot* s) {
     free(s->cur_idx);
     free(s->inited);
     free(s->tc);
+    free(s->res_off);
+    free(s->res_rules);
     free(s);
 }
 
@@ -2606,6 +2623,20 @@ int or_pslot_load_rules(or_pslot* s, const sg_pslot_rule* rules, uint32_t n, con
     for (uint32_t i = 0; i < n; i++) s->cur_idx[i] = rules[i].param_idx;
     s->n = n;
     s->n_res = n_res;
+    free(s->res_off);
+    free(s->res_rules);
+    s->res_off = (uint32_t*)calloc((size_t)n_res + 1, sizeof(uint32_t));
+    s->res_rules = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    for (uint32_t i = 0; i < n; i++)
+        if (rules[i].resource < n_res) s->res_off[rules[i].resource + 1]++;
+    for (uint32_t r = 0; r < n_res; r++) s->res_off[r + 1] += s->res_off[r];
+    {
+        uint32_t* fill = (uint32_t*)malloc(((size_t)n_res + 1) * sizeof(uint32_t));
+        memcpy(fill, s->res_off, ((size_t)n_res + 1) * sizeof(uint32_t));
+        for (uint32_t i = 0; i < n; i++)
+            if (rules[i].resource < n_res) s->res_rules[fill[rules[i].resource]++] = i;
+        free(fill);
+    }
     memset(s->tc, 0, s->tc_cap * sizeof(or_tc));
     s->tc_size = 0;
     return 0;
@@ -2677,9 +2708,10 @@ static int pslot_single(or_pslot* s, uint32_t ri, uint32_t res, int count, uint6
 static void pslot_threads(or_pslot* s, uint32_t res, const sg_pslot_arg* args, uint32_t na, const uint64_t* values, int d) {
     for (uint32_t idx = 0; idx < na; idx++) {
         int has_map = 0;
-        for (uint32_t r = 0; r < s->n && !has_map; r++)
-            has_map = s->rules[r].resource == res && s->rules[r].cluster_mode != SG_CLUSTER_MODE_INVALID &&
-                      s->inited[r] && s->cur_idx[r] == (int32_t)idx;
+        for (uint32_t q = s->res_off[res]; q < s->res_off[res + 1] && !has_map; q++) {
+            const uint32_t r = s->res_rules[q];
+            has_map = s->rules[r].cluster_mode != SG_CLUSTER_MODE_INVALID && s->inited[r] && s->cur_idx[r] == (int32_t)idx;
+        }
         if (!has_map) continue;
         const sg_pslot_arg* a = &args[idx];
         if (a->kind == SG_ARG_NULL) continue;
@@ -2731,8 +2763,8 @@ static int pslot_entry(or_pslot* s, uint32_t res, int64_t t, int count, const sg
                        const uint64_t* values) {
     s->now = t;
     if (res >= s->n_res) return -1;
-    for (uint32_t r = 0; r < s->n; r++) {
-        if (s->rules[r].resource != res) continue;
+    for (uint32_t q = s->res_off[res]; q < s->res_off[res + 1]; q++) {
+        const uint32_t r = s->res_rules[q];
         if (s->rules[r].cluster_mode == SG_CLUSTER_MODE_INVALID) continue;  /* isValidRule → checkCluster: never loaded */
         /* applyRealParamIdx(rule, args.length) */
         if (s->cur_idx[r] < 0) s->cur_idx[r] = (-s->cur_idx[r] <= (int32_t)na) ? (int32_t)na + s->cur_idx[r] : -s->cur_idx[r];

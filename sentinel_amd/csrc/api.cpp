@@ -49,6 +49,7 @@ struct sg_handle {
     uint32_t* d_np = nullptr;
     int* d_err = nullptr;
     int64_t* d_last_ts = nullptr;
+    int64_t* d_front_ts = nullptr;    // pipelined limiter batches: last timestamp of the latest accepted front half
     uint32_t* d_long_list = nullptr;
     uint32_t* d_long_count = nullptr;  // [4]: long count, short count, work cursors (long, short)
     uint32_t* d_short_list = nullptr;
@@ -525,6 +526,8 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipHostMalloc(&h->h_long, 2 * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     int64_t neg = -1;
     if (hipMemcpy(h->d_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
+    if (hipMalloc(&h->d_front_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMemcpy(h->d_front_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     if (hipMalloc(&h->d_plast_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMemcpy(h->d_plast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     for (auto& e : h->ev)
@@ -616,6 +619,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_np);
     dfree(h->d_err);
     dfree(h->d_last_ts);
+    dfree(h->d_front_ts);
     dfree(h->d_long_list);
     dfree(h->d_long_count);
     dfree(h->d_short_list);
@@ -1376,6 +1380,7 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     HIP_TRY(h, launch_prep(a, stream));
     const int lrc = flow_limiter(h, a, stream);
     if (lrc) return lrc;
+    if (a.front_ts) HIP_TRY(h, launch_front_ts(a, stream));
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
     {
         uint64_t* sorted = nullptr;
@@ -1497,7 +1502,16 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
     if (after) HIP_TRY(h, hipStreamWaitEvent(h->s_front, after, 0));
     if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
     if (h->n_lim > 0) {
-        if (!first) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[xp], 0));
+        // the limiter pre-pass must see only accepted batches: k_prep checks the time order against the previous
+        // front half's last timestamp (front_ts, advanced once a batch passed validation) as well as last_ts, so
+        // this front half need not wait for the previous batch's walkers (env SG_LIM_PIPE=0: it waits, as before)
+        const char* lp = std::getenv("SG_LIM_PIPE");
+        const bool wait_back = lp && std::atoi(lp) == 0;
+        if (wait_back) {
+            if (!first) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[xp], 0));
+        } else {
+            a.front_ts = h->d_front_ts;
+        }
     } else {
         a.check_last = 0;  // checked by the back half, after the previous batch has advanced last_ts
     }
@@ -4478,6 +4492,21 @@ struct sg_node {
     bool rec_path = false;
     uint64_t* d_sub_rec = nullptr;      // [max_batch] the shards' record slices
     std::vector<sg_namespace> ns;       // the node's namespaces (rollback of a failed sg_node_set_namespaces)
+    // pipelined node batches (sg_node_flow_enqueue, records path): two workspaces alternating, as the single
+    // handle's pipeline — the front's k_prep / limiter / routing of batch i+1 and the shards' sorts beside the
+    // shards' walkers of batch i
+    struct PipeSlot {
+        uint64_t ticket = 0;
+        hipEvent_t done = nullptr;   // every shard's back half of the slot's batch (recorded on s0)
+        int* h_err = nullptr;        // pinned [kMaxShards]: each shard's error word
+        uint32_t* h_base = nullptr;  // pinned [2 * kMaxShards + 1]: slice bases and counts
+        uint32_t G_used = 0;         // shards the batch went to
+    };
+    PipeSlot pipe[2];
+    hipEvent_t fdone[2] = {nullptr, nullptr};  // the front's part of the slot's batch
+    uint64_t* d_sub_rec2 = nullptr;            // workspace 1's record slices
+    uint64_t pseq = 0, next_ticket = 1;
+    std::unordered_map<uint64_t, int> finished;  // tickets completed while making room, not yet collected
 };
 
 namespace {
@@ -4553,12 +4582,67 @@ void node_sync_shards(sg_node* nd, uint32_t g) {
     (void)hipSetDevice(nd->devices[0]);
 }
 
+// One shard's slice of a node batch on the records path: the sort of its records (node request indices), its
+// segments, both walkers and the skipped BLOCK counts, its error word into err_dst. `front` carries the sort and
+// segments, `back` the walkers (the same stream for a synchronous node batch); front_done (may be null) joins them.
+int node_shard_rec(sg_handle* h, BatchArgs b, uint64_t cnt, uint32_t* hist, hipStream_t front, hipStream_t back,
+                   hipStream_t aux, hipEvent_t fork, hipEvent_t join, hipEvent_t front_done, int* err_dst) {
+    HIP_TRY(h, hipMemsetAsync(b.err, 0, sizeof(int), front));
+    HIP_TRY(h, hipMemsetAsync(b.long_count, 0, (1 + kClasses) * sizeof(uint32_t), front));
+    HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), front));
+    uint64_t* sorted = nullptr;
+    const SegMark mk{b.seg_start, b.seg_end, b.K, b.kshift};
+    b.seg_marked = (b.seg_start && b.seg_end && b.long_end && !h->seg_mark_pass) ? 1 : 0;
+    HIP_TRY(h, radix_sort_records(b.rec, b.rec_sorted, cnt, b.kshift, hist, &sorted, front, 64, b.hist0 != nullptr,
+                                  b.seg_marked ? &mk : nullptr, b.csum0 != nullptr));
+    b.rec_sorted = sorted;
+    HIP_TRY(h, launch_seg_flow(b, front));
+    if (front_done) {
+        HIP_TRY(h, hipEventRecord(front_done, front));
+        HIP_TRY(h, hipStreamWaitEvent(back, front_done, 0));
+    }
+    HIP_TRY(h, hipEventRecord(fork, back));
+    HIP_TRY(h, hipStreamWaitEvent(aux, fork, 0));
+    HIP_TRY(h, launch_walk_long(b, aux));
+    HIP_TRY(h, launch_walk_short(b, back));
+    HIP_TRY(h, launch_walk_tiny(b, back));
+    HIP_TRY(h, hipEventRecord(join, aux));
+    HIP_TRY(h, hipStreamWaitEvent(back, join, 0));
+    HIP_TRY(h, launch_skip_apply(b, back));
+    HIP_TRY(h, hipMemcpyAsync(err_dst, b.err, sizeof(int), hipMemcpyDeviceToHost, back));
+    return SG_OK;
+}
+
+// A completed pipelined node batch's status: the first shard error (the front's was answered at enqueue).
+int node_slot_status(sg_node* nd, const sg_node::PipeSlot& sl) {
+    for (uint32_t g = 0; g < sl.G_used; ++g)
+        if (sl.h_err[g]) return node_child(nd, nd->shards[g], flow_status(nd->shards[g], sl.h_err[g]));
+    return SG_OK;
+}
+
+// Completes the node's pipelined batches (their statuses wait for sg_node_flow_poll / _wait): every other node call
+// starts from a drained node, and the synchronous path uses workspace 0.
+int node_drain(sg_node* nd) {
+    for (auto& sl : nd->pipe) {
+        if (!sl.ticket) continue;
+        (void)hipSetDevice(nd->devices[0]);
+        const hipError_t e = hipEventSynchronize(sl.done);
+        nd->finished[sl.ticket] = e != hipSuccess ? nfail(nd, SG_E_DEVICE, hipGetErrorString(e)) : node_slot_status(nd, sl);
+        sl.ticket = 0;
+    }
+    for (sg_handle* h : nd->shards) drain_async(h);
+    if (nd->front) drain_async(nd->front);
+    if (!nd->devices.empty()) (void)hipSetDevice(nd->devices[0]);
+    return SG_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 void sg_node_destroy(sg_node* nd) {
     if (!nd) return;
+    node_drain(nd);
     for (size_t g = 0; g < nd->shards.size(); ++g) {
         (void)hipSetDevice(nd->devices[g]);
         if (g < nd->streams.size() && nd->streams[g]) (void)hipStreamDestroy(nd->streams[g]);
@@ -4581,6 +4665,14 @@ void sg_node_destroy(sg_node* nd) {
     dfree(nd->d_req_h);
     dfree(nd->d_out_h);
     dfree(nd->d_sub_rec);
+    dfree(nd->d_sub_rec2);
+    for (auto& sl : nd->pipe) {
+        if (sl.done) (void)hipEventDestroy(sl.done);
+        if (sl.h_err) (void)hipHostFree(sl.h_err);
+        if (sl.h_base) (void)hipHostFree(sl.h_base);
+    }
+    for (hipEvent_t e : nd->fdone)
+        if (e) (void)hipEventDestroy(e);
     if (nd->h_base) (void)hipHostFree(nd->h_base);
     if (nd->h_front_err) (void)hipHostFree(nd->h_front_err);
     sg_destroy(nd->front);
@@ -4667,6 +4759,7 @@ int sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shar
 
 int sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n) {
     if (!nd || (!ns && n)) return SG_E_INVAL;
+    node_drain(nd);
     // the front runs every namespace limiter over the node batch (and validates the set); the shards see only admitted
     // requests. A shard that fails (allocation, device) puts the front and the shards before it back on the node's
     // previous namespaces.
@@ -4695,6 +4788,7 @@ int sg_node_set_namespaces(sg_node* nd, const sg_namespace* ns, uint32_t n) {
 
 int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) {
     if (!nd || (!rules && n)) return SG_E_INVAL;
+    node_drain(nd);
     // All or nothing: the node's rule set is validated on the front, every shard's part and the front's whole set are
     // prepared beside the live state (surviving flowIds' metrics copied: a surviving flowId keeps its owner, hence its
     // ClusterMetric) together with the routing tables, and only when all of that succeeded is anything committed. A
@@ -4791,7 +4885,7 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
     const uint32_t G = (uint32_t)nd->shards.size();
     hipStream_t user = (hipStream_t)stream_;
     NHIP(nd, hipSetDevice(nd->devices[0]));
-    for (sg_handle* h : nd->shards) drain_async(h);
+    node_drain(nd);
     int rc = ensure_layout(f);
     if (rc) return node_child(nd, f, rc);
     // 1. the front: validation + namespace limiter in caller order, the batch's time check, its last timestamp, the
@@ -4874,28 +4968,8 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
             b.p0 = a.p0;
             b.np = a.np;
             hipStream_t st = nd->streams[g];
-            rc = [&]() -> int {
-                HIP_TRY(h, hipMemsetAsync(b.err, 0, sizeof(int), st));
-                HIP_TRY(h, hipMemsetAsync(b.long_count, 0, (1 + kClasses) * sizeof(uint32_t), st));
-                HIP_TRY(h, hipMemsetAsync(b.skip_count, 0, sizeof(uint32_t), st));
-                uint64_t* sorted = nullptr;
-                const SegMark mk{b.seg_start, b.seg_end, b.K, b.kshift};
-                b.seg_marked = (b.seg_start && b.seg_end && b.long_end && !h->seg_mark_pass) ? 1 : 0;
-                // direct: the first pass's histogram rows are the front's (k_prep counted them in its workspace)
-                HIP_TRY(h, radix_sort_records(b.rec, b.rec_sorted, cnt, b.kshift, direct ? w.hist : sw.hist, &sorted, st,
-                                              64, b.hist0 != nullptr, b.seg_marked ? &mk : nullptr, b.csum0 != nullptr));
-                b.rec_sorted = sorted;
-                HIP_TRY(h, launch_seg_flow(b, st));
-                HIP_TRY(h, hipEventRecord(h->fork, st));
-                HIP_TRY(h, hipStreamWaitEvent(h->aux, h->fork, 0));
-                HIP_TRY(h, launch_walk_long(b, h->aux));
-                HIP_TRY(h, launch_walk_short(b, st));
-                HIP_TRY(h, hipEventRecord(h->join, h->aux));
-                HIP_TRY(h, hipStreamWaitEvent(st, h->join, 0));
-                HIP_TRY(h, launch_skip_apply(b, st));
-                HIP_TRY(h, hipMemcpyAsync(nd->h_err[g], b.err, sizeof(int), hipMemcpyDeviceToHost, st));
-                return SG_OK;
-            }();
+            rc = node_shard_rec(h, b, cnt, direct ? w.hist : sw.hist, st, st, h->aux, h->fork, h->join, nullptr,
+                                nd->h_err[g]);
             if (rc) {
                 node_sync_shards(nd, g + 1);
                 return node_child(nd, h, rc);
@@ -4950,14 +5024,188 @@ int sg_node_flow_decide_batch_host(sg_node* nd, const sg_req* req, uint64_t n, s
     return SG_OK;
 }
 
+int sg_node_flow_enqueue(sg_node* nd, const sg_req* req, uint64_t n, sg_result* out, uint64_t* ticket) {
+    if (!nd || !ticket) return SG_E_INVAL;
+    *ticket = 0;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    sg_handle* f = nd->front;
+    const uint32_t G = (uint32_t)nd->shards.size();
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    int rc = ensure_layout(f);
+    if (rc) return node_child(nd, f, rc);
+    if (!nd->rec_path) {  // shards on other devices: the synchronous node batch, its status kept for the ticket
+        rc = sg_node_flow_decide_batch(nd, req, n, out, nullptr);
+        if (rc == SG_E_DEVICE) return rc;
+        *ticket = nd->next_ticket++;
+        nd->finished[*ticket] = rc;
+        return SG_OK;
+    }
+    rc = pipe_setup(f);
+    if (rc) return node_child(nd, f, rc);
+    for (sg_handle* h : nd->shards) {
+        rc = pipe_setup(h);
+        if (rc) return node_child(nd, h, rc);
+    }
+    const int x = (int)(nd->pseq & 1);
+    sg_node::PipeSlot& sl = nd->pipe[x];
+    if (!sl.done) {
+        if (hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&nd->fdone[x], hipEventDisableTiming) != hipSuccess ||
+            hipHostMalloc(&sl.h_err, sizeof(int) * kMaxShards) != hipSuccess ||
+            hipHostMalloc(&sl.h_base, sizeof(uint32_t) * (2 * kMaxShards + 1)) != hipSuccess)
+            return nfail(nd, SG_E_NOMEM, "node pipeline slot");
+    }
+    if (x == 1 && !nd->d_sub_rec2 && hipMalloc(&nd->d_sub_rec2, sizeof(uint64_t) * (nd->cfg.max_batch + kRecW)) != hipSuccess)
+        return nfail(nd, SG_E_NOMEM, "shard record slices");
+    if (sl.ticket) {  // the batch two back used this workspace: complete it (its status waits in `finished`)
+        const hipError_t e = hipEventSynchronize(sl.done);
+        nd->finished[sl.ticket] = e != hipSuccess ? nfail(nd, SG_E_DEVICE, hipGetErrorString(e)) : node_slot_status(nd, sl);
+        sl.ticket = 0;
+    }
+    // 1. the front on its pipeline stream: validation, the namespace limiter in caller order, the time check against
+    // the previous node batch (the front's own last timestamp, in stream order), the period tables, the routing
+    sg_handle::FlowWs w = f->pws;
+    if (x == 0) main_ws(f, w);
+    BatchArgs a = flow_args(f, w, req, n, out);
+    const bool direct = G == 1 && nd->shards[0]->K == f->K && nd->shards[0]->kbits == f->kbits;
+    if (!direct) a.hist0 = nullptr;
+    a.csum0 = nullptr;
+    hipStream_t fs = f->s_front;
+    if (nd->pseq >= 2) NHIP(nd, hipStreamWaitEvent(fs, sl.done, 0));
+    NHIP(nd, hipMemsetAsync(a.err, 0, sizeof(int), fs));
+    if (a.hist0 && radix_csum_atomic()) {
+        a.csum0 = radix_csum(a.hist0, a.n, a.hist0_bits);
+        NHIP(nd, hipMemsetAsync(a.csum0, 0, radix_csum_bytes(a.n, a.hist0_bits), fs));
+    }
+    NHIP(nd, launch_prep(a, fs));
+    rc = flow_limiter(f, a, fs);
+    if (rc) return node_child(nd, f, rc);
+    NHIP(nd, launch_finish(a, fs));
+    uint64_t* sub_rec = x == 0 ? nd->d_sub_rec : nd->d_sub_rec2;
+    if (!direct) {
+        RouteArgs r{};
+        r.req = req;
+        r.rec = a.rec;
+        r.n = n;
+        r.kshift = a.kshift;
+        r.abits = a.abits;
+        r.imask = a.imask;
+        r.K = f->K;
+        r.shard_of = nd->d_shard_of;
+        r.local_of = nd->d_local_of;
+        r.G = (int)G;
+        r.tile_cnt = nd->d_tile_cnt;
+        r.shard_base = nd->d_base;
+        r.shard_tot = nd->d_base + kMaxShards + 1;
+        r.sub_req = nd->d_sub_req;
+        r.sub_pos = nd->d_sub_pos;
+        r.sub_rec = sub_rec;
+        r.low_mask = (1ull << a.kshift) - 1;
+        for (uint32_t g = 0; g < G; ++g) r.skshift[g] = 64 - nd->shards[g]->kbits;
+        NHIP(nd, launch_route(r, fs));
+        NHIP(nd, hipMemcpyAsync(sl.h_base, nd->d_base, sizeof(uint32_t) * (2 * kMaxShards + 1), hipMemcpyDeviceToHost, fs));
+    }
+    NHIP(nd, hipMemcpyAsync(nd->h_front_err, a.err, sizeof(int), hipMemcpyDeviceToHost, fs));
+    NHIP(nd, hipEventRecord(nd->fdone[x], fs));
+    // the slice sizes are launch parameters of the shards' sorts: wait for the front (the shards' walkers of the
+    // previous batch keep the device busy meanwhile)
+    NHIP(nd, hipEventSynchronize(nd->fdone[x]));
+    const uint64_t t = nd->next_ticket++;
+    *ticket = t;
+    if (*nd->h_front_err) {  // refused as a whole (nothing reached the shards)
+        nd->finished[t] = node_child(nd, f, flow_status(f, *nd->h_front_err));
+        NHIP(nd, hipEventRecord(sl.done, fs));
+        sl.G_used = 0;
+        nd->pseq++;
+        return SG_OK;
+    }
+    if (direct) {
+        sl.h_base[0] = 0;
+        sl.h_base[kMaxShards + 1] = (uint32_t)n;
+    }
+    // 2. every shard: its sort on its front stream (beside its walkers of the previous batch), then its walkers
+    for (uint32_t g = 0; g < G; ++g) {
+        sl.h_err[g] = 0;
+        const uint32_t base = sl.h_base[g], cnt = sl.h_base[kMaxShards + 1 + g];
+        if (cnt == 0) continue;
+        sg_handle* h = nd->shards[g];
+        sg_handle::FlowWs sw = h->pws;
+        if (x == 0) main_ws(h, sw);
+        BatchArgs b = flow_args(h, sw, req, cnt, out);
+        b.rec = direct ? a.rec : sub_rec + base;
+        b.rec_sorted = direct ? sw.rec_sorted : sw.rec;
+        b.hist0 = direct ? a.hist0 : nullptr;
+        b.hist0_bits = a.hist0_bits;
+        b.csum0 = direct ? a.csum0 : nullptr;
+        b.n_wl = a.n_wl;
+        std::memcpy(b.wl, a.wl, sizeof(b.wl));
+        b.bnd = a.bnd;
+        b.p0 = a.p0;
+        b.np = a.np;
+        b.walk_cus = h->walk_cus;
+        NHIP(nd, hipStreamWaitEvent(h->s_front, nd->fdone[x], 0));
+        rc = node_shard_rec(h, b, cnt, direct ? w.hist : sw.hist, h->s_front, h->s_back, h->s_aux2, h->pfork, h->pjoin,
+                            h->front_done[x], &sl.h_err[g]);
+        if (rc) {
+            for (uint32_t q = 0; q <= g; ++q) {
+                (void)hipStreamSynchronize(nd->shards[q]->s_front);
+                (void)hipStreamSynchronize(nd->shards[q]->s_back);
+            }
+            nd->finished.erase(t);
+            *ticket = 0;
+            return node_child(nd, h, rc);
+        }
+        NHIP(nd, hipEventRecord(h->back_done[x], h->s_back));
+        NHIP(nd, hipStreamWaitEvent(nd->s0, h->back_done[x], 0));
+    }
+    NHIP(nd, hipEventRecord(sl.done, nd->s0));
+    sl.G_used = G;
+    sl.ticket = t;
+    nd->pseq++;
+    return SG_OK;
+}
+
+static int node_collect(sg_node* nd, uint64_t ticket, bool block) {
+    if (!nd) return SG_E_INVAL;
+    if (ticket == 0) return 1;
+    auto it = nd->finished.find(ticket);
+    if (it != nd->finished.end()) {
+        const int st = it->second;
+        nd->finished.erase(it);
+        return st == SG_OK ? 1 : st;
+    }
+    for (auto& sl : nd->pipe) {
+        if (sl.ticket != ticket) continue;
+        (void)hipSetDevice(nd->devices[0]);
+        const hipError_t e = block ? hipEventSynchronize(sl.done) : hipEventQuery(sl.done);
+        if (e == hipErrorNotReady) return 0;
+        sl.ticket = 0;
+        if (e != hipSuccess) return nfail(nd, SG_E_DEVICE, hipGetErrorString(e));
+        const int st = node_slot_status(nd, sl);
+        return st == SG_OK ? 1 : st;
+    }
+    return nfail(nd, SG_E_INVAL, "unknown or already collected ticket");
+}
+
+int sg_node_flow_poll(sg_node* nd, uint64_t ticket) { return node_collect(nd, ticket, false); }
+
+int sg_node_flow_wait(sg_node* nd, uint64_t ticket) {
+    const int r = node_collect(nd, ticket, true);
+    return r == 1 ? SG_OK : r;
+}
+
 int sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, int64_t* counters, int64_t* occupy) {
     if (!nd || key >= nd->shard_of.size()) return SG_E_INVAL;
+    node_drain(nd);
     sg_handle* h = nd->shards[nd->shard_of[key]];
     return node_child(nd, h, sg_flow_read_state(h, nd->local_of[key], starts, counters, occupy));
 }
 
 int sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap) {
     if (!nd || (!out && cap)) return SG_E_INVAL;
+    node_drain(nd);
     const uint64_t K = nd->shard_of.size();
     if (cap < 2 * K) return nfail(nd, SG_E_CAPACITY, "snapshot buffer smaller than 2 * rules");
     std::vector<std::vector<double>> part(nd->shards.size());

@@ -113,6 +113,8 @@ struct BatchArgs {
     int* err;
     int64_t* last_ts;    // max timestamp of all earlier batches (-1 before the first)
     int check_last;      // k_prep checks the first timestamp against last_ts (0: k_check_last does, pipelined)
+    int64_t* front_ts;   // pipelined batches with namespace limiters: the last timestamp of the latest front half that
+                         // passed validation (k_prep also checks against it; k_front_ts advances it); else nullptr
     int walk_cus;        // CUs the walkers' stream may use (CU-masked pipeline streams), 0 = all
     uint32_t* long_list; // segment starts handed to the wave walker
     uint32_t* long_count;
@@ -784,6 +786,7 @@ hipError_t launch_walk_tiny(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_walk_short(const BatchArgs& a, hipStream_t stream);  // the short walker
 hipError_t launch_check_last(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_finish(const BatchArgs& a, hipStream_t stream);
+hipError_t launch_front_ts(const BatchArgs& a, hipStream_t stream);
 // bytes (a multiple of 4) from device memory to a device-accessible host buffer by the shader
 hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int blocks, hipStream_t stream);
 hipError_t launch_skip_apply(const BatchArgs& a, hipStream_t stream);

@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         const sg_req r = a.req[i];
         const int64_t t = r.ts_ms;
         if (i == 0) {
-            if (t < 0 || (a.check_last && t < *a.last_ts)) atomicOr(a.err, kErrTime);
+            if (t < 0 || (a.check_last && (t < *a.last_ts || (a.front_ts && t < *a.front_ts)))) atomicOr(a.err, kErrTime);
             for (int w = 0; w < a.n_wl; ++w) a.p0[w] = t / a.wl[w];
         } else {
             const int64_t tp = a.req[i - 1].ts_ms;
@@ -1805,6 +1805,13 @@ __global__ void k_finish(BatchArgs a) {
     if (*a.err == 0 && a.n > 0) *a.last_ts = a.req[a.n - 1].ts_ms;
 }
 
+// The front half's own time order (pipelined batches with namespace limiters): once a batch has passed validation
+// and the limiter pre-pass, the next front half may start, checked against this batch's last timestamp, without
+// waiting for this batch's walkers to advance last_ts.
+__global__ void k_front_ts(BatchArgs a) {
+    if (*a.err == 0 && a.n > 0) *a.front_ts = a.req[a.n - 1].ts_ms;
+}
+
 // ---------------------------------------------------------------------------- state management
 
 // The hot mirror of every bucket, rebuilt from the ring (after rule loads and state imports).
@@ -2015,6 +2022,11 @@ hipError_t launch_copy_out(const void* src, void* dst_dev, uint64_t bytes, int b
     const uint32_t tail = (uint32_t)((bytes % 16) / 4);
     hipLaunchKernelGGL(k_copy_out, dim3(blocks), dim3(256), 0, stream, (const uint4*)src, (uint4*)dst_dev, n16,
                        (const uint32_t*)src + n16 * 4, (uint32_t*)dst_dev + n16 * 4, tail);
+    return hipGetLastError();
+}
+
+hipError_t launch_front_ts(const BatchArgs& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_front_ts, dim3(1), dim3(1), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -31,7 +31,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_pace_load_rules", "sg_pace_decide_batch", "sg_pace_decide_batch_host", "sg_pace_read_state",
            "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
            "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
-           "sg_node_snapshot_metrics", "sg_node_shard_of"]
+           "sg_node_snapshot_metrics", "sg_node_shard_of", "sg_node_flow_enqueue", "sg_node_flow_poll",
+           "sg_node_flow_wait"]
 
 _lib = None
 
@@ -134,6 +135,9 @@ def load_library():
         "sg_node_flow_read_state": (C.c_int, [vp, u32, vp, vp, vp]),
         "sg_node_snapshot_metrics": (C.c_int, [vp, i64, vp, u64]),
         "sg_node_shard_of": (C.c_int, [vp, u32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "sg_node_flow_enqueue": (C.c_int, [vp, vp, u64, vp, C.POINTER(C.c_uint64)]),
+        "sg_node_flow_poll": (C.c_int, [vp, u64]),
+        "sg_node_flow_wait": (C.c_int, [vp, u64]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("SG_LIB_PATH") and not hasattr(L, name):
@@ -187,6 +191,21 @@ class NodeEngine:
 
     def decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
         self._check(self._L.sg_node_flow_decide_batch(self.h, req_ptr, n, out_ptr, stream_ptr))
+
+    def enqueue_device(self, req_ptr: int, n: int, out_ptr: int) -> int:
+        """sg_node_flow_enqueue: a device-resident node batch on the node pipeline; returns the ticket."""
+        t = C.c_uint64()
+        self._check(self._L.sg_node_flow_enqueue(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr), C.byref(t)))
+        return t.value
+
+    def poll(self, ticket) -> bool:
+        r = self._L.sg_node_flow_poll(self.h, ticket)
+        if r < 0:
+            self._check(r)
+        return r == 1
+
+    def wait(self, ticket):
+        self._check(self._L.sg_node_flow_wait(self.h, ticket))
 
     def shard_of(self, key):
         s, lk = C.c_uint32(), C.c_uint32()

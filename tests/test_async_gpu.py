@@ -159,8 +159,9 @@ def test_device_enqueue_cross_batch_time_check():
 
 
 def test_device_enqueue_with_limiter_and_sync_calls_between():
-    """Pipelined batches with a namespace limiter (front halves wait for the previous batch: the limiter pre-pass
-    sees accepted batches only) mixed with synchronous calls, which drain the pipeline first."""
+    """Pipelined batches with a namespace limiter (each front half checks the time order against the previous front
+    half's, so the limiter pre-pass sees accepted batches only, without waiting for the previous walkers) mixed with
+    synchronous calls, which drain the pipeline first."""
     import torch
     from oracle.binding import ClusterTokenService
     from sentinel_amd.engine import FlowEngine
@@ -196,3 +197,47 @@ def test_device_enqueue_with_limiter_and_sync_calls_between():
     for b, r in enumerate(reqs):
         want = ora.decide(r)
         assert np.array_equal(outs[b], want), f"batch {b}: {(outs[b] != want).sum()} differ"
+
+
+@pytest.mark.parametrize("lim_pipe", ["1", "0"])
+def test_device_enqueue_with_limiter_rejects_a_late_batch(monkeypatch, lim_pipe):
+    """Four limiter batches in flight, the second older than the first: it is refused on its own ticket, its
+    requests never reach the namespace limiter (the following batches' TOO_MANY_REQUEST answers equal the oracle's,
+    which never saw it), and the flowIds' rings equal the oracle's. SG_LIM_PIPE=0: the front halves wait for the
+    previous back half (the round-4 order), same answers."""
+    import torch
+    from oracle.binding import ClusterTokenService
+    from sentinel_amd.engine import EngineError, FlowEngine
+    from sentinel_amd.workload import ClusterWorkload
+    monkeypatch.setenv("SG_LIM_PIPE", lim_pipe)
+    wl = ClusterWorkload(n_flows=1500, n_requests=50_000, seed=41, prio_frac=0.05)
+    ns = np.zeros(1, abi.NS_DTYPE)
+    ns["connected_count"] = 1
+    ns["max_allowed_qps"] = 30_000
+    ns["limiter_enabled"] = 1
+    eng = FlowEngine(device=0, max_batch=50_000)
+    eng.set_namespaces(ns)
+    eng.load_rules(wl.rules())
+    ora = ClusterTokenService()
+    ora.set_namespaces(ns)
+    ora.load_rules(wl.rules())
+    r0, r1, r2 = wl.requests(0), wl.requests(1), wl.requests(2)
+    late = r0.copy()
+    bufs = [(_dev(r), torch.empty(len(r) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0"))
+            for r in (r0, late, r1, r2)]
+    torch.cuda.synchronize()
+    t = [eng.enqueue_device(i.data_ptr(), len(i) // abi.REQ_DTYPE.itemsize, o.data_ptr()) for i, o in bufs]
+    eng.wait(t[0])
+    with pytest.raises(EngineError) as ei:
+        eng.wait(t[1])
+    assert ei.value.code == abi.SG_E_TIME
+    eng.wait(t[2])
+    eng.wait(t[3])
+    for (i, o), r in zip([bufs[0], bufs[2], bufs[3]], [r0, r1, r2]):
+        want = ora.decide(r)
+        got = o.cpu().numpy().view(abi.RES_DTYPE)
+        assert (want["status"] == abi.TOO_MANY_REQUEST).any()
+        assert np.array_equal(got, want), f"{(got != want).sum()} results differ"
+    ring, occ = eng.export_state(len(wl.rules()))
+    ring_o, occ_o = ora.export_state(len(wl.rules()), ring.shape[1])
+    assert np.array_equal(ring, ring_o) and np.array_equal(occ, occ_o)

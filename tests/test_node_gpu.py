@@ -197,3 +197,109 @@ def test_node_rule_load_is_all_or_nothing(monkeypatch, fail_shard):
         assert np.array_equal(got, want), f"{int((got != want).sum())} results differ after the failed loads"
         t = int(req["ts_ms"][-1]) + 1
     _compare_state(node, cts, rules)
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+@pytest.mark.parametrize("lim_qps", [0.0, 3000.0])
+def test_node_pipelined_batches_equal_one_token_service(G, lim_qps):
+    """sg_node_flow_enqueue / _poll / _wait: five node batches in flight back to back (two node workspaces
+    alternating, the front's routing of batch i+1 beside the shards' walkers of batch i), one of them out of time
+    order and refused by the front as a whole, equal to the sequential token service batch by batch; then a
+    synchronous node batch after the pipeline, and the rings."""
+    import torch
+    from sentinel_amd.engine import NodeEngine
+    rng = np.random.default_rng(70 + 10 * G + int(lim_qps > 0))
+    K = 300
+    rules = _rules(rng, K)
+    ns = _ns(lim_qps)
+    node = NodeEngine([0] * G, max_batch=1 << 16)
+    node.set_namespaces(ns)
+    node.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(ns)
+    cts.load_rules(rules)
+    t = 1_700_000_000_000 + int(rng.integers(0, 1000))
+    reqs, wants = [], []
+    for b in range(5):
+        n = int(rng.integers(20_000, 40_000))
+        if b == 2:  # starts behind the previous batch: refused, no state change
+            req = _batch(rng, n, K, t - 50, 600)
+            wants.append(None)
+        else:
+            req = _batch(rng, n, K, t, 900)
+            wants.append(cts.decide(req))
+            t = int(req["ts_ms"][-1]) + 1
+        reqs.append(req)
+    dev_req = [torch.from_numpy(r.view(np.uint8).copy()).cuda() for r in reqs]
+    dev_out = [torch.zeros(len(r) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for r in reqs]
+    torch.cuda.synchronize()
+    tickets = [node.enqueue_device(q.data_ptr(), len(r), o.data_ptr()) for q, r, o in zip(dev_req, reqs, dev_out)]
+    assert all(tk > 0 for tk in tickets) and len(set(tickets)) == 5
+    for b, (tk, o) in enumerate(zip(tickets, dev_out)):
+        if wants[b] is None:
+            with pytest.raises(Exception):
+                node.wait(tk)
+            continue
+        node.wait(tk)
+        got = o.cpu().numpy().view(abi.RES_DTYPE)
+        if not np.array_equal(got, wants[b]):
+            bad = np.nonzero(got != wants[b])[0]
+            raise AssertionError(f"batch {b}: {len(bad)} results differ; first at {bad[0]}: "
+                                 f"oracle={wants[b][bad[0]]} node={got[bad[0]]}")
+    with pytest.raises(Exception):  # collected already
+        node.wait(tickets[0])
+    req = _batch(rng, 20_000, K, t, 900)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    _compare_state(node, cts, rules)
+
+
+def test_node_pipelined_poll_and_interleaved_calls():
+    """poll answers 0 / 1 without consuming a running ticket twice; a rule reload or a state read between enqueues
+    first completes the batches in flight (their tickets stay collectable)."""
+    import torch
+    from sentinel_amd.engine import NodeEngine
+    rng = np.random.default_rng(91)
+    K = 120
+    rules = _rules(rng, K)
+    ns = _ns(0.0)
+    node = NodeEngine([0, 0], max_batch=1 << 16)
+    node.set_namespaces(ns)
+    node.load_rules(rules)
+    cts = ClusterTokenService()
+    cts.set_namespaces(ns)
+    cts.load_rules(rules)
+    t = 1_700_000_000_000
+    outs, tks, wants = [], [], []
+    for b in range(3):
+        req = _batch(rng, 30_000, K, t, 700)
+        wants.append(cts.decide(req))
+        t = int(req["ts_ms"][-1]) + 1
+        q = torch.from_numpy(req.view(np.uint8).copy()).cuda()
+        o = torch.zeros(len(req) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        tks.append(node.enqueue_device(q.data_ptr(), len(req), o.data_ptr()))
+        outs.append((q, o))
+        if b == 1:
+            _compare_state(node, cts, rules)  # drains the node first
+    while not node.poll(tks[2]):
+        pass
+    for b in range(3):
+        if b != 2:
+            node.wait(tks[b])
+        assert np.array_equal(outs[b][1].cpu().numpy().view(abi.RES_DTYPE), wants[b])
+    rules2 = rules.copy()
+    rules2["count"] = rng.integers(1, 40, K)
+    req = _batch(rng, 30_000, K, t, 700)
+    q = torch.from_numpy(req.view(np.uint8).copy()).cuda()
+    o = torch.zeros(len(req) * abi.RES_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    want = cts.decide(req)
+    tk = node.enqueue_device(q.data_ptr(), len(req), o.data_ptr())
+    node.load_rules(rules2)  # completes the batch in flight under the old rules
+    cts.load_rules(rules2)
+    node.wait(tk)
+    assert np.array_equal(o.cpu().numpy().view(abi.RES_DTYPE), want)
+    t = int(req["ts_ms"][-1]) + 1
+    req = _batch(rng, 30_000, K, t, 700)
+    assert np.array_equal(node.decide_host(req), cts.decide(req))
+    _compare_state(node, cts, rules2)
