@@ -501,7 +501,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMalloc(&h->d_p0, sizeof(int64_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_np, sizeof(uint32_t) * kMaxWl) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_err, sizeof(int)) != hipSuccess) return bail(SG_E_NOMEM);
-    if (hipMalloc(&h->d_last_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_last_ts, 2 * sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);  // + front_ts
     if (hipMalloc(&h->d_long_list, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&h->d_long_key, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
         hipMalloc(&h->d_long_end, sizeof(uint32_t) * (n + 1)) != hipSuccess ||
@@ -526,7 +526,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipHostMalloc(&h->h_long, 2 * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     int64_t neg = -1;
     if (hipMemcpy(h->d_last_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
-    if (hipMalloc(&h->d_front_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
+    h->d_front_ts = h->d_last_ts + 1;
     if (hipMemcpy(h->d_front_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     if (hipMalloc(&h->d_plast_ts, sizeof(int64_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMemcpy(h->d_plast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
@@ -619,7 +619,6 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_np);
     dfree(h->d_err);
     dfree(h->d_last_ts);
-    dfree(h->d_front_ts);
     dfree(h->d_long_list);
     dfree(h->d_long_count);
     dfree(h->d_short_list);
@@ -1506,8 +1505,7 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
         // front half's last timestamp (front_ts, advanced once a batch passed validation) as well as last_ts, so
         // this front half need not wait for the previous batch's walkers (env SG_LIM_PIPE=0: it waits, as before)
         const char* lp = std::getenv("SG_LIM_PIPE");
-        const bool wait_back = lp && std::atoi(lp) == 0;
-        if (wait_back) {
+        if (lp && std::atoi(lp) == 0) {
             if (!first) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[xp], 0));
         } else {
             a.front_ts = h->d_front_ts;

@@ -235,6 +235,9 @@ __global__ void __launch_bounds__(kLimThreads) k_lim_apply(BatchArgs a, LimArgs 
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
     if (*a.err) return;
     if (tid < kMaxLim) run[tid] = L.tile_off[(size_t)blockIdx.x * kMaxLim + tid];
+    // every (wave, slot) count starts at 0: a round sets only the slots present in a wave, and the first round would
+    // otherwise read what an earlier kernel left in this CU's LDS for the others
+    if (tid < (kLimThreads / 64) * kMaxLim) wcnt[tid / kMaxLim][tid % kMaxLim] = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
     for (int r = 0; r < kLimRounds; ++r) {

@@ -351,7 +351,8 @@ def test_sharded_limiter_pipelined_equals_node_replay(path):
             n = len(wants[r])
             got = outs[r].cpu().numpy().view(abi.RES_DTYPE)[:n] if path == "enqueue" else outs[r][:n]
             bad = np.nonzero(got != wants[r])[0]
-            assert len(bad) == 0, f"batch {b} shard {r}: {len(bad)} of {n} differ"
+            assert len(bad) == 0, (f"batch {b} shard {r}: {len(bad)} of {n} differ; first (got, want): "
+                                   f"{[(tuple(got[i]), tuple(wants[r][i])) for i in bad[:6]]}")
             saw_tmr |= bool((wants[r]["status"] == abi.TOO_MANY_REQUEST).any())
     assert saw_tmr
     for e, a in keep:
