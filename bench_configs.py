@@ -273,6 +273,7 @@ def slot(args, dev):
     params["grade"] = abi.FLOW_GRADE_QPS
     params["rule"]["count"] = rng.integers(5, 21, len(par_res))
     params["rule"]["duration_sec"] = 1
+    params["rule"]["capacity_log2"] = 11  # exact value table of 2048 slots per rule (1000 values)
     n_vals = 1000
     pargs = np.zeros(n_vals, abi.PSLOT_ARG_DTYPE)
     pargs["value_begin"] = np.arange(n_vals)

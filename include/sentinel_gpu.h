@@ -726,6 +726,19 @@ typedef struct sg_metric_node {
     int32_t  concurrency;         /* 0, as fromBucket leaves it */
 } sg_metric_node;
 int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows);
+/* sg_local_metrics with `rt` as the bucket's raw sum in every row (not divided by success): one GPU's share of a node's
+ * rows, which the node's rollup merges (sentinel_amd/cluster.py LocalMetricRollup: the ENTRY_NODE rows of the same
+ * second are summed over the GPUs, then rt = Σrt / Σsuccess), with the same side effects as sg_local_metrics. */
+int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows);
+/* The local chain sharded over a node's GPUs (one process per GPU): every GPU loads the same rules and
+ * decides the entries and exits of the resources it owns — owner[r] = splitmix64(g(r)) mod world, g(r) the smallest
+ * resource of r's key group (RELATE references; on an embedded token server also the resources sharing a flowId or
+ * a limited namespace), so every state a decision reads (ClusterNode, origin and context nodes, breakers, flow
+ * controllers, param tables) lives on one GPU. The caller routes each event to owner[event.resource] in arrival order;
+ * the per-GPU metric rows merge by sg_local_metrics_raw. SG_E_UNSUPPORTED: an embedded token server with namespace
+ * limiters (its GlobalRequestLimiter sees the whole node). Replaces nothing in the reference (one JVM, one chain):
+ * the node-level deployment of StatisticSlot / FlowSlot / DegradeSlot. */
+int sg_local_owners(sg_handle* h, uint32_t world, uint32_t* owner, uint32_t n);
 int sg_local_set_entry_types(sg_handle* h, const uint8_t* inbound, uint32_t n);
 int sg_local_read_origin_state(sg_handle* h, uint32_t res, int32_t origin, int64_t* second, int64_t* borrow,
                                int64_t* minute, int64_t* head);

@@ -97,6 +97,7 @@ def lib():
         "or_local_controller": (C.c_int, [vp, u32, vp]),
         "or_local_rule_order": (C.c_int, [vp, u32, vp, u32]),
         "or_local_metrics": (i64, [vp, i64, vp, u64]),
+        "or_local_metrics_raw": (i64, [vp, i64, vp, u64, C.c_int]),
         "or_cts_param_top": (C.c_int, [vp, u32, i64, C.c_int, vp, vp]),
         "or_cpm_top": (C.c_int, [vp, i64, C.c_int, vp, vp]),
         "or_pslot_new": (vp, []), "or_pslot_free": (None, [vp]),
@@ -768,11 +769,12 @@ class LocalChain:
         assert rc >= 0
         return sec, bor, mnt, th.value, rc == 1
 
-    def metrics(self, now):
-        """StatisticNode.metrics() rows of every resource at now (MetricTimerListener.run), time-sorted."""
-        n = int(lib().or_local_metrics(self.h, now, None, 0))
+    def metrics(self, now, raw=False):
+        """StatisticNode.metrics() rows of every resource at now (MetricTimerListener.run), time-sorted (raw: rt as
+        the bucket's sum, as sg_local_metrics_raw)."""
+        n = int(lib().or_local_metrics_raw(self.h, now, None, 0, int(raw)))
         out = np.zeros(max(1, n), abi.METRIC_NODE_DTYPE)
-        m = int(lib().or_local_metrics(self.h, now, abi.ptr(out), len(out)))
+        m = int(lib().or_local_metrics_raw(self.h, now, abi.ptr(out), len(out), int(raw)))
         assert m == n
         return out[:n]
 

@@ -2436,7 +2436,8 @@ static int metric_row_less(const sg_metric_node* a, const sg_metric_node* b) {
 /* StatisticNode.metrics() of one node at now (StatisticNode.java:116-147): the minute window's buckets newer than
  * *last_fetch, older than now's second, non-empty; emit: write them (resource id `res`), advance *last_fetch and run
  * currentWindow's side effect. Returns the rows. */
-static uint64_t node_rows(or_leap* m, int64_t now, int64_t* last_fetch, uint32_t res, sg_metric_node* out, int emit) {
+static uint64_t node_rows(or_leap* m, int64_t now, int64_t* last_fetch, uint32_t res, sg_metric_node* out, int emit,
+                          int raw) {
     const int64_t cur = now - now % 1000;
     if (emit) or_leap_current_window(m, now);                   /* data.currentWindow() */
     int64_t newest = *last_fetch;
@@ -2457,7 +2458,7 @@ static uint64_t node_rows(or_leap* m, int64_t now, int64_t* last_fetch, uint32_t
             r->block_qps = b->c[OR_M_BLOCK];
             r->success_qps = succ;
             r->exception_qps = b->c[OR_M_EXCEPTION];
-            r->rt = rt;
+            r->rt = raw ? b->c[OR_M_RT] : rt;   /* raw: the sum, for a node rollup (sg_local_metrics_raw) */
             r->occupied_pass_qps = b->c[OR_M_OCCUPIED_PASS];
             r->resource = res;
             r->concurrency = 0;
@@ -2471,18 +2472,18 @@ static uint64_t node_rows(or_leap* m, int64_t now, int64_t* last_fetch, uint32_t
 
 /* MetricTimerListener.run (MetricTimerListener.java:40-55): every resource's ClusterNode, then Constants.ENTRY_NODE
  * (resource id SG_ENTRY_NODE_RESOURCE), rows sorted by (timestamp, resource) as its TreeMap of time → list */
-int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap) {
+int64_t or_local_metrics_raw(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap, int raw) {
     if (!l->last_fetch) {
         l->last_fetch = (int64_t*)malloc((l->n ? l->n : 1) * sizeof(int64_t));
         for (uint32_t k = 0; k < l->n; k++) l->last_fetch[k] = -1;
     }
     uint64_t rows = 0;
-    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, NULL, 0);
-    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, NULL, 0);
+    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, NULL, 0, raw);
+    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, NULL, 0, raw);
     if (rows > cap) return (int64_t)rows;
     rows = 0;
-    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, out + rows, 1);
-    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, out + rows, 1);
+    for (uint32_t k = 0; k < l->n; k++) rows += node_rows(l->nodes[k].minute, now, &l->last_fetch[k], k, out + rows, 1, raw);
+    if (l->entry) rows += node_rows(l->entry->minute, now, &l->entry_fetch, SG_ENTRY_NODE_RESOURCE, out + rows, 1, raw);
     for (uint64_t i = 1; i < rows; i++) {                           /* insertion sort by (timestamp, resource) */
         sg_metric_node x = out[i];
         uint64_t j = i;
@@ -2493,6 +2494,10 @@ int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t
         out[j] = x;
     }
     return (int64_t)rows;
+}
+
+int64_t or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap) {
+    return or_local_metrics_raw(l, now, out, cap, 0);
 }
 
 int or_local_set_entry_types(or_local* l, const uint8_t* inbound, uint32_t n) {

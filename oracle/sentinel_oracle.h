@@ -216,6 +216,7 @@ uint64_t  or_lgen_run_ext(or_lgen* g, const sg_local_event* entries, const sg_sl
 /* StatisticNode.metrics() of every resource at now (MetricTimerListener.run), sorted by (timestamp, resource);
  * returns the number of rows (written only when <= cap). */
 int64_t  or_local_metrics(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap);
+int64_t  or_local_metrics_raw(or_local* l, int64_t now, sg_metric_node* out, uint64_t cap, int raw);
 /* EntryType of every resource's entries (1 = IN: Constants.ENTRY_NODE counts them); default OUT. */
 int      or_local_set_entry_types(or_local* l, const uint8_t* inbound, uint32_t n);
 /* ClusterParamMetric.getTopValues(number) of cluster param rule key at now; returns the entries written. */

@@ -151,3 +151,101 @@ class LimiterExchange:
             torch.cuda.current_stream(self.device).synchronize()
         self.eng.lim_exchange(gathered.data_ptr(), t_base, n_ms, gathered_words=self.world * self.n_lim * n_ms)
         return t_base, n_ms
+
+
+# ---------------------------------------------------------------------------------------- the sharded local chain
+
+ENTRY_NODE_RESOURCE = 0xFFFFFFFF
+
+
+def local_group_keys(n_res: int, relate_pairs) -> np.ndarray:
+    """The smallest resource of each resource's key group (union-find over RELATE references (resource, ref)): the
+    resources whose decisions read each other's ClusterNode. The library's sg_local_owners computes the same groups
+    from the loaded rules (plus, on an embedded token server, flowId / limited-namespace sharing)."""
+    parent = np.arange(n_res, dtype=np.int64)
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    for a, b in relate_pairs:
+        if 0 <= a < n_res and 0 <= b < n_res:
+            x, y = find(int(a)), find(int(b))
+            if x != y:
+                parent[max(x, y)] = min(x, y)
+    return np.array([find(k) for k in range(n_res)], dtype=np.int64)
+
+
+def local_owners(n_res: int, relate_pairs, world: int) -> np.ndarray:
+    """GPU that owns each resource of the local chain: splitmix64(group key) mod world (sg_local_owners)."""
+    return owner_of(local_group_keys(n_res, relate_pairs).astype(np.uint64), world)
+
+
+def split_local_events(events: np.ndarray, owners: np.ndarray, world: int):
+    """Per rank, the positions of its events in arrival order: an entry and its exit go to the owner of their
+    resource (the key bits only; the prioritized bit is not part of the resource)."""
+    res = (events["resource"] & np.uint32(0x7FFFFFFF)).astype(np.int64)
+    own = np.asarray(owners)[res]
+    return [np.nonzero(own == r)[0] for r in range(world)]
+
+
+def merge_metric_rows(parts) -> np.ndarray:
+    """The node's MetricTimerListener rows from every GPU's sg_local_metrics_raw rows: a resource's rows come from
+    its owner alone (rt = Σrt / success when success != 0, ArrayMetric.fromBucket); Constants.ENTRY_NODE's rows of
+    one second are the sums over the GPUs (each summed its inbound resources), then the same rt and the
+    isValidMetricNode filter on the sums. Sorted by (timestamp, resource) as the listener's TreeMap."""
+    from sentinel_amd import abi
+    rows = np.concatenate([np.asarray(p, abi.METRIC_NODE_DTYPE) for p in parts]) if parts else \
+        np.zeros(0, abi.METRIC_NODE_DTYPE)
+    res_rows = rows[rows["resource"] != ENTRY_NODE_RESOURCE].copy()
+    succ = res_rows["success_qps"]
+    res_rows["rt"] = np.where(succ != 0, res_rows["rt"] // np.where(succ != 0, succ, 1), res_rows["rt"])
+    ent = rows[rows["resource"] == ENTRY_NODE_RESOURCE]
+    merged = []
+    for ts in np.unique(ent["timestamp"]):
+        g = ent[ent["timestamp"] == ts]
+        r = np.zeros((), abi.METRIC_NODE_DTYPE)
+        r["timestamp"] = ts
+        for f in ("pass_qps", "block_qps", "success_qps", "exception_qps", "rt"):
+            r[f] = g[f].sum()
+        s = int(r["success_qps"])
+        if s != 0:
+            r["rt"] = int(r["rt"]) // s
+        r["resource"] = ENTRY_NODE_RESOURCE
+        if r["pass_qps"] > 0 or r["block_qps"] > 0 or s > 0 or r["exception_qps"] > 0 or r["rt"] > 0:
+            merged.append(r)
+    out = np.concatenate([res_rows, np.array(merged, abi.METRIC_NODE_DTYPE)]) if merged else res_rows
+    order = np.lexsort((out["resource"], out["timestamp"]))
+    return out[order]
+
+
+class LocalMetricRollup:
+    """SURVEY §8(e) for the sharded local chain: every GPU's sg_local_metrics_raw rows gathered to every rank
+    (all_gather of the row counts, then of the rows padded to the largest, 64 B each as 8 int64 words) and merged
+    by merge_metric_rows — the node's metrics.log lines, ENTRY_NODE included. RCCL on the rank's GPU for "nccl",
+    CPU tensors for gloo."""
+
+    def __init__(self, coll_device, group=None):
+        self.coll = torch.device(coll_device)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def run(self, rows: np.ndarray) -> np.ndarray:
+        from sentinel_amd import abi
+        rows = np.ascontiguousarray(rows, abi.METRIC_NODE_DTYPE)
+        if self.world == 1:
+            return merge_metric_rows([rows])
+        n = torch.tensor([len(rows)], dtype=torch.int64, device=self.coll)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(s.item()) for s in sizes]
+        m = max(1, max(sizes))
+        words = np.zeros((m, 8), np.int64)
+        words[:len(rows)] = rows.view(np.int64).reshape(-1, 8)
+        mine = torch.from_numpy(words).to(self.coll)
+        parts = [torch.zeros_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        got = [p.cpu().numpy()[:k].copy().view(abi.METRIC_NODE_DTYPE).reshape(-1) for p, k in zip(parts, sizes)]
+        return merge_metric_rows(got)

@@ -2956,7 +2956,40 @@ int sg_local_set_entry_types(sg_handle* h, const uint8_t* inbound, uint32_t n) {
     return SG_OK;
 }
 
+namespace {
+int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw);
+void local_group_keys(sg_handle* h, std::vector<uint32_t>& gkey);
+}
+
 int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows) {
+    return local_metrics(h, now_ms, out, cap, n_rows, 0);
+}
+
+int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows) {
+    return local_metrics(h, now_ms, out, cap, n_rows, 1);
+}
+
+int sg_local_owners(sg_handle* h, uint32_t world, uint32_t* owner, uint32_t n) {
+    if (!h || world == 0 || (!owner && n)) return SG_E_INVAL;
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    const uint32_t K = (uint32_t)h->ltab.size();
+    if (n != K) return fail(h, SG_E_INVAL, "owner buffer must hold one entry per resource");
+    if (world > 1 && h->l_cluster_state == SG_CLUSTER_SERVER && h->n_lim > 0 && (h->l_cluster_rules || h->ps_cluster))
+        return fail(h, SG_E_UNSUPPORTED, "an embedded token server with namespace limiters serves the node from one GPU");
+    std::vector<uint32_t> gkey;
+    local_group_keys(h, gkey);
+    for (uint32_t k = 0; k < K; ++k) {  // splitmix64(group key) mod world (sentinel_amd/cluster.py local_owners)
+        uint64_t z = (uint64_t)gkey[k] + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        owner[k] = (uint32_t)(z % world);
+    }
+    return SG_OK;
+}
+
+namespace {
+int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw) {
     if (!h || !n_rows || (!out && cap)) return SG_E_INVAL;
     *n_rows = 0;
     if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
@@ -2981,8 +3014,8 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
         }
         hipError_t e = hipMemcpy(h->d_lentry_acc, acc0.data(), sizeof(LBucket) * kMinuteS, hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(unsigned long long));
-        if (e == hipSuccess) e = launch_local_metrics(L, now_ms, dst, d_cnt, emit, 0);
-        if (e == hipSuccess && h->d_linbound) e = launch_local_entry_rows(L, now_ms, dst, d_cnt, emit, 0);
+        if (e == hipSuccess) e = launch_local_metrics(L, now_ms, dst, d_cnt, emit, raw, 0);
+        if (e == hipSuccess && h->d_linbound) e = launch_local_entry_rows(L, now_ms, dst, d_cnt, emit, raw, 0);
         return e;
     };
     unsigned long long* d_cnt = nullptr;
@@ -3014,6 +3047,7 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
     });
     return SG_OK;
 }
+}  // namespace
 
 namespace {
 
@@ -3777,7 +3811,10 @@ void ps_cluster_unions(sg_handle* h, const std::function<void(uint32_t, uint32_t
 // cluster-mode rules share a flowId share its ClusterMetric, and those naming flowIds of one limiter-enabled
 // namespace share its GlobalRequestLimiter — each group walks in event order on one lane. Sets LRule.grp / cx and
 // uploads the rule image and the record keys.
-int local_apply_groups(sg_handle* h) {
+// The key groups of the local chain (resources whose decisions read each other's state): RELATE references and, on
+// an embedded token server, resources sharing a flowId's ClusterMetric or a limited namespace. gkey[k] = the smallest
+// resource of k's group.
+void local_group_keys(sg_handle* h, std::vector<uint32_t>& gkey) {
     const uint32_t K = (uint32_t)h->ltab.size();
     std::vector<uint32_t> parent(K);
     for (uint32_t k = 0; k < K; ++k) parent[k] = k;
@@ -3809,8 +3846,15 @@ int local_apply_groups(sg_handle* h) {
             }
         }
     }
-    std::vector<uint32_t> gkey(K), gsize(K, 0);
-    for (uint32_t k = 0; k < K; ++k) ++gsize[gkey[k] = find(k)];
+    gkey.resize(K);
+    for (uint32_t k = 0; k < K; ++k) gkey[k] = find(k);
+}
+
+int local_apply_groups(sg_handle* h) {
+    const uint32_t K = (uint32_t)h->ltab.size();
+    std::vector<uint32_t> gkey, gsize(K, 0);
+    local_group_keys(h, gkey);
+    for (uint32_t k = 0; k < K; ++k) ++gsize[gkey[k]];
     bool groups = false, has_cx = false;
     for (uint32_t k = 0; k < K; ++k) {
         LRule& L = h->ltab[k];

@@ -1668,7 +1668,7 @@ __device__ __forceinline__ bool metric_row_valid(const LBucket& b) {  // MetricN
 }
 
 __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_metric_node* out,
-                                                       unsigned long long* count, int emit) {
+                                                       unsigned long long* count, int emit, int raw) {
     const int64_t cur = now - now % 1000;
     const int I = (int)((now / kMinuteWl) % kMinuteS);
     const int64_t efetch = a.entry_fetch ? *a.entry_fetch : INT64_MAX;
@@ -1710,7 +1710,7 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
             r.block_qps = block;
             r.success_qps = succ;
             r.exception_qps = exc;
-            r.rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
+            r.rt = (succ != 0 && !raw) ? b.c[kLRt] / succ : b.c[kLRt];
             r.occupied_pass_qps = b.c[kLOccPass];
             r.resource = (uint32_t)k;
             r.concurrency = 0;
@@ -1724,7 +1724,7 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
 // Constants.ENTRY_NODE.metrics() rows from the summed buckets (one thread per minute slot; resource id
 // SG_ENTRY_NODE_RESOURCE); emit advances the ENTRY_NODE's lastFetchTime.
 __global__ void __launch_bounds__(64) k_local_entry_rows(LArgs a, int64_t now, sg_metric_node* out,
-                                                         unsigned long long* count, int emit) {
+                                                         unsigned long long* count, int emit, int raw) {
     const int j = threadIdx.x;
     const int64_t cur = now - now % 1000;
     bool row = false;
@@ -1746,7 +1746,7 @@ __global__ void __launch_bounds__(64) k_local_entry_rows(LArgs a, int64_t now, s
             r.block_qps = b.c[kLBlock];
             r.success_qps = succ;
             r.exception_qps = b.c[kLExc];
-            r.rt = succ != 0 ? b.c[kLRt] / succ : b.c[kLRt];
+            r.rt = (succ != 0 && !raw) ? b.c[kLRt] / succ : b.c[kLRt];
             r.occupied_pass_qps = 0;
             r.resource = SG_ENTRY_NODE_RESOURCE;
             r.concurrency = 0;
@@ -1785,15 +1785,15 @@ hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                hipStream_t stream) {
+                                int raw, hipStream_t stream) {
     if (a.K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit);
+    hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit, raw);
     return hipGetLastError();
 }
 
 hipError_t launch_local_entry_rows(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                   hipStream_t stream) {
-    hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit);
+                                   int raw, hipStream_t stream) {
+    hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit, raw);
     return hipGetLastError();
 }
 

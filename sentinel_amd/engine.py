@@ -32,7 +32,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
            "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
            "sg_node_snapshot_metrics", "sg_node_shard_of", "sg_node_flow_enqueue", "sg_node_flow_poll",
-           "sg_node_flow_wait"]
+           "sg_node_flow_wait", "sg_local_metrics_raw", "sg_local_owners"]
 
 _lib = None
 
@@ -138,6 +138,8 @@ def load_library():
         "sg_node_flow_enqueue": (C.c_int, [vp, vp, u64, vp, C.POINTER(C.c_uint64)]),
         "sg_node_flow_poll": (C.c_int, [vp, u64]),
         "sg_node_flow_wait": (C.c_int, [vp, u64]),
+        "sg_local_metrics_raw": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
+        "sg_local_owners": (C.c_int, [vp, u32, vp, u32]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("SG_LIB_PATH") and not hasattr(L, name):
@@ -542,6 +544,7 @@ class FlowEngine:
                                   occupy_timeout_ms=occupy_timeout_ms, cold_factor=cold_factor)
         self._check(self._L.sg_local_load_rules(self.h, C.byref(cfg), abi.ptr(rules), len(rules)))
         self.local_S = sample_count
+        self.local_K = len(rules)
 
     def local_decide_host(self, ev: np.ndarray) -> np.ndarray:
         ev = np.ascontiguousarray(ev, dtype=abi.LOCAL_EVENT_DTYPE).reshape(-1)
@@ -588,6 +591,22 @@ class FlowEngine:
         out = np.zeros(max(1, n.value), abi.METRIC_NODE_DTYPE)
         self._check(self._L.sg_local_metrics(self.h, now_ms, abi.ptr(out), len(out), C.byref(n)))
         return out[:n.value]
+
+    def local_metrics_raw(self, now_ms) -> np.ndarray:
+        """sg_local_metrics_raw: this GPU's share of the node's rows, rt as the raw sum (LocalMetricRollup merges)."""
+        n = C.c_uint64()
+        rc = self._L.sg_local_metrics_raw(self.h, now_ms, None, 0, C.byref(n))
+        if rc not in (0, abi.SG_E_CAPACITY):
+            self._check(rc)
+        out = np.zeros(max(1, n.value), abi.METRIC_NODE_DTYPE)
+        self._check(self._L.sg_local_metrics_raw(self.h, now_ms, abi.ptr(out), len(out), C.byref(n)))
+        return out[:n.value]
+
+    def local_owners(self, world) -> np.ndarray:
+        """sg_local_owners: the GPU of `world` that owns each resource (key groups co-located)."""
+        out = np.zeros(max(1, self.local_K), np.uint32)
+        self._check(self._L.sg_local_owners(self.h, world, abi.ptr(out), self.local_K))
+        return out[:self.local_K]
 
     def local_load_flow_rules(self, rules: np.ndarray, n_origins=0, n_contexts=0) -> int:
         """FlowRuleManager.loadRules for the local chain; returns the number of rules kept."""
