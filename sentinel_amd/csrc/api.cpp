@@ -270,6 +270,7 @@ struct sg_handle {
     uint32_t short_max = kShortMax;   // default walker split (env SG_SHORT_MAX overrides, for tuning)
     bool short_max_env = false;
     int dbg = 0;                      // env SG_DEBUG: see BatchArgs::dbg
+    int l_cxw = 1;                    // env SG_CXW=0: long cx segments on the lane walker too (LArgs::cxw)
     bool wide_seen = false;           // some loaded rule allowed bucket counts >= 2^30 (sticky: the ring keeps them)
     hipEvent_t ev[5]{};
     sg_batch_stats stats{};
@@ -537,6 +538,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         hipEventCreateWithFlags(&h->join, hipEventDisableTiming) != hipSuccess)
         return bail(SG_E_DEVICE);
     if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
+    if (const char* d = std::getenv("SG_CXW")) h->l_cxw = std::atoi(d) != 0 ? 1 : 0;
     if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
@@ -3235,6 +3237,7 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
     L = LArgs{};
     L.ev = ev;
     L.out = out;
+    L.cxw = h->l_cxw;
     L.n = n;
     L.rec = b.rec;
     L.rec_sorted = b.rec_sorted;

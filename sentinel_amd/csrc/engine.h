@@ -671,6 +671,7 @@ struct LArgs {
     uint32_t* dyn;            // [K] epoch of the last batch with an origin event of the resource (walked as cx)
     uint32_t epoch;
     int32_t track_ctx;        // 1: every event updates its context's DefaultNode (n_contexts >= 1)
+    int32_t cxw;              // 1: long cx segments (not RELATE groups) go to the wave walker k_lwalk_cxw
     // the embedded token server (ClusterStateManager SERVER, emb = 1): the handle's cluster flow state
     int32_t emb;
     const Rule* c3_rules;

@@ -1344,9 +1344,8 @@ __device__ __forceinline__ uint2 event_nodes(const LArgs& a, uint32_t idx) {
 // passClusterCheck → fallbackToLocalOrPass :147-175) → DegradeSlot, then the StatisticSlot updates of the
 // ClusterNode, the origin node and the context's DefaultNode, and ParamFlowStatisticEntryCallback.onPass.
 __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t, int origin,
-                         int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
+                         int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes) {
     const LRule& R = nd.R;
-    const uint2 nodes = event_nodes(a, e.idx);
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
     LNode on(a, bndp, have_on ? on_idx : nd.k);  // windows opened as touched (cx_rule, the StatisticSlot adds)
@@ -1473,9 +1472,8 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
 // One exit of a cx resource: StatisticSlot.exit (:124-165) on the ClusterNode (+ DegradeSlot.exit), the origin node
 // and the context's DefaultNode; ParamFlowStatisticExitCallback.onExit (decreaseThreadCount of the exit's args).
 __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t,
-                        int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm) {
+                        int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes) {
     nd.exit(e, t, create);
-    const uint2 nodes = event_nodes(a, e.idx);
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
         LNode on(a, bndp, on_idx);
@@ -1509,6 +1507,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
         uint64_t j;
         if (r < *sg.long_count) {
             j = sg.long_list[r];
+            if (a.cxw && !a.rules[(uint32_t)(a.rec_sorted[j] >> a.kshift)].grp) continue;  // k_lwalk_cxw
         } else {
             r -= *sg.long_count;
             int c = 0;
@@ -1529,8 +1528,9 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
                 nd.created = 1;
                 const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
                 if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);  // an entry opens what it touches (cx_entry)
-                if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
-                else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
+                const uint2 nodes = event_nodes(a, e.idx);
+                if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
+                else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
                 nd.finish();
             }
             continue;
@@ -1546,10 +1546,329 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
             const int ctx = x ? (int)x->context : 0;
             const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
             if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);
-            if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm);
-            else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm);
+            const uint2 nodes = event_nodes(a, e.idx);
+            if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
+            else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
         }
         nd.finish();
+    }
+}
+
+// ------------------------------------------------------------------------------ the cx wave walker
+//
+// One wave per long segment of a cx resource (not a RELATE group): the lanes load 64 events at a time (record,
+// event, arguments, origin / context nodes) and every lane runs the same serial step for each event in turn
+// (cx_entry / cx_exit with the values broadcast from that event's lane), so the resource's ClusterNode stays in
+// registers and an event costs no dependent loads of its own. Once a window period goes "dead" — a QPS rule that
+// every entry reaches is saturated (DefaultController: (int)(passQps + 1) > count; a lone WarmUp rule: passQps + 1 >
+// its synced warning-zone QPS), and every rule before it is side-effect free — every further entry of the period is
+// FLOW-blocked: its only effects are BLOCK counts (ClusterNode, origin node) and its ParamFlowSlot check, which the
+// wave decides 64 entries at a time (the rule's token chains of equal values in lane order, ParamFlowChecker
+// .passDefaultLocalCheck / passThrottleLocalCheck :127-254); exits stay serial. Prioritized entries, entries with
+// acquireCount <= 0, context tracking, shaping controllers other than a lone WarmUp, several ParamFlowRules or
+// collection arguments keep the serial step.
+
+// Whether resource k's periods can go dead; *prule = its one QPS ParamFlowRule (-1: none).
+__device__ bool cxw_dead_able(const LArgs& a, const LRule& R, uint32_t k, int32_t* prule) {
+    *prule = -1;
+    if (a.track_ctx) return false;
+    if (R.fr_n == 0) {
+        if (R.flow_grade != 1) return false;
+    } else {
+        bool any = false;
+        for (uint32_t i = 0; i < R.fr_n; ++i) {
+            const LFlowRule r = a.frules[R.fr_begin + i];
+            if (r.strategy != SG_STRATEGY_DIRECT || r.cluster_mode != SG_CLUSTER_MODE_OFF) return false;
+            if (r.behavior == SG_CONTROL_WARM_UP) {
+                if (R.fr_n != 1 || r.limit_app != SG_LIMIT_APP_DEFAULT) return false;
+            } else if (r.behavior != SG_CONTROL_DEFAULT) {
+                return false;
+            }
+            any = any || (r.grade == 1 && r.limit_app == SG_LIMIT_APP_DEFAULT);
+        }
+        if (!any) return false;
+    }
+    if (R.ps && a.has_ps) {
+        const uint32_t rb = a.ps.res_begin[k], re = a.ps.res_begin[k + 1];
+        if (re - rb > 1) return false;
+        if (re == rb + 1) {
+            const uint32_t ri = a.ps.res_rules[rb];
+            const int32_t cm = a.ps.cmode ? a.ps.cmode[ri] : SG_CLUSTER_MODE_OFF;
+            if (a.ps.grade[ri] != 1 || cm != SG_CLUSTER_MODE_OFF || a.ps.cur_idx[ri] < 0) return false;
+            *prule = (int32_t)ri;
+        }
+    }
+    return true;
+}
+
+// Is the open second-window period saturated for a rule every entry reaches? (nd's windows are at the period.)
+__device__ bool cxw_saturated(const LArgs& a, const LNode& nd) {
+    const LRule& R = nd.R;
+    const double qps = nd.pass_qps();
+    if (R.fr_n == 0) return (double)(int32_t)((uint32_t)java_d2i(qps) + 1u) > R.flow_count;
+    for (uint32_t i = 0; i < R.fr_n; ++i) {
+        const LFlowRule r = a.frules[R.fr_begin + i];
+        if (r.grade != 1 || r.limit_app != SG_LIMIT_APP_DEFAULT) continue;
+        if (r.behavior == SG_CONTROL_WARM_UP) {
+            const LCtl c = a.ctl[R.fr_begin + i];
+            if (c.last_filled < nd.m_ws) return false;  // no entry reached it in this second yet: syncToken pending
+            const double lim = c.stored >= r.warning_token ? warm_qps(r, c.stored - r.warning_token) : r.count;
+            if ((double)(int64_t)((uint64_t)java_d2l(qps) + 1ull) > lim) return true;
+        } else if ((double)(int32_t)((uint32_t)java_d2i(qps) + 1u) > r.count) {
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e_end) {
+    const int lane = lane_id();
+    LNode nd(a, bndp, k);
+    nd.created = 1;
+    int32_t prule = -1;
+    const bool dead_ok = !(*a.flags & (kLFlagPrio | kLFlagNonPos)) && cxw_dead_able(a, nd.R, k, &prule);
+    bool dead = false;
+    uint32_t dead_qs = 0xFFFFFFFFu, dead_qm = 0xFFFFFFFFu;
+    // BLOCK counts of the dead period's entries per origin node, one table slot per lane {node, sum}, added to the
+    // nodes when the period ends (before any later period can reuse their bucket slots)
+    uint32_t ob_node = kNoNode;
+    int64_t ob_sum = 0;
+    auto flush_origins = [&]() {
+        uint64_t used = __ballot(ob_node != kNoNode);
+        while (used) {
+            const int j = __builtin_ctzll(used);
+            used &= used - 1;
+            LNode on(a, bndp, (uint32_t)bcast32((int)ob_node, j));
+            on.at(dead_qs, dead_qm);
+            const int64_t sum = bcast64(ob_sum, j);
+            on.sc[kLBlock] += sum;
+            on.mc[kLBlock] += sum;
+            on.finish();
+        }
+        ob_node = kNoNode;
+        ob_sum = 0;
+    };
+    for (uint64_t base = s; base < e_end; base += 64) {
+        const uint64_t j = base + (uint64_t)lane;
+        const bool act = j < e_end;
+        LEvent ev;
+        ev.idx = 0;
+        ev.count = 0;
+        ev.kind = -1;
+        ev.prio = false;
+        int64_t t = 0, cr = 0;
+        int32_t org = 0;
+        sg_slot_ext xx;
+        xx.context = 0;
+        xx.arg_begin = xx.arg_count = 0;
+        xx.args_null = 1;
+        uint2 nodes = make_uint2(kNoNode, kNoNode);
+        uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
+        if (act) {
+            ev = ldecode(a, a.rec_sorted[j]);
+            const sg_local_event le = a.ev[ev.idx];
+            t = le.ts_ms;
+            cr = le.create_ts;
+            org = le.origin;
+            if (a.ext) xx = a.ext[ev.idx];
+            nodes = event_nodes(a, ev.idx);
+            qs = nd.cs.of(ev.idx);
+            qm = nd.cm.of(ev.idx);
+        }
+        // the serial step of lane q, every lane with lane q's values
+        auto step = [&](int q, uint32_t qs0, uint32_t qm0) {
+            LEvent es;
+            es.idx = (uint32_t)bcast32((int)ev.idx, q);
+            es.count = bcast32(ev.count, q);
+            es.kind = bcast32(ev.kind, q);
+            es.prio = bcast32((int)ev.prio, q) != 0;
+            const int64_t te = bcast64(t, q), ce = bcast64(cr, q);
+            const int og = bcast32(org, q);
+            sg_slot_ext xe;
+            xe.context = (uint32_t)bcast32((int)xx.context, q);
+            xe.arg_begin = (uint32_t)bcast32((int)xx.arg_begin, q);
+            xe.arg_count = (uint32_t)bcast32((int)xx.arg_count, q);
+            xe.args_null = bcast32(xx.args_null, q);
+            const uint2 nn = make_uint2((uint32_t)bcast32((int)nodes.x, q), (uint32_t)bcast32((int)nodes.y, q));
+            const sg_slot_ext* xp = a.ext ? &xe : nullptr;
+            if (es.kind == SG_LOCAL_ENTRY) {
+                cx_entry(a, bndp, nd, es, te, og, (int)xe.context, xp, qs0, qm0, nn);
+                return true;
+            }
+            nd.at(qs0, qm0);
+            cx_exit(a, bndp, nd, es, te, ce, og, (int)xe.context, xp, qs0, qm0, nn);
+            return false;
+        };
+        const int nact = (int)__popcll(__ballot(act));
+        int p = 0;
+        while (p < nact) {
+            // run: lanes [p, rend) in the window periods of lane p
+            const uint32_t qs0 = (uint32_t)bcast32((int)qs, p), qm0 = (uint32_t)bcast32((int)qm, p);
+            const uint64_t diff = __ballot(act && lane > p && (qs != qs0 || qm != qm0));
+            const int rend = diff ? __builtin_ctzll(diff) : nact;
+            if (dead && (qs0 != dead_qs || qm0 != dead_qm)) {  // the dead period ended
+                flush_origins();
+                dead = false;
+            }
+            while (p < rend && !dead) {
+                const bool entry = step(p, qs0, qm0);
+                ++p;
+                if (entry && dead_ok && nd.cs.q == qs0 && nd.cm.q == qm0 && cxw_saturated(a, nd)) {
+                    dead = true;
+                    dead_qs = qs0;
+                    dead_qm = qm0;
+                }
+            }
+            if (p >= rend) continue;
+            // ---- lanes [p, rend) of a dead period: entries FLOW-blocked unless their ParamFlowSlot check fails
+            const bool in = act && lane >= p && lane < rend;
+            const bool ent = in && ev.kind == SG_LOCAL_ENTRY;
+            bool pfail = false;
+            if (prule >= 0) {
+                const uint32_t ri = (uint32_t)prule;
+                const int32_t pidx = a.ps.cur_idx[ri];
+                const bool args = ent && a.ext && !xx.args_null;
+                bool has = args && (int32_t)xx.arg_count > pidx;
+                sg_pslot_arg ag;
+                ag.kind = SG_ARG_NULL;
+                ag.value_begin = ag.value_count = 0;
+                if (has) {
+                    ag = a.ps.args[xx.arg_begin + (uint32_t)pidx];
+                    has = ag.kind != SG_ARG_NULL;
+                }
+                if (__ballot(has && ag.kind == SG_ARG_COLLECTION)) {  // element by element: the serial step
+                    while (p < rend) step(p++, qs0, qm0);
+                    continue;
+                }
+                if (__ballot(args)) a.ps.inited[ri] = 1;  // initParamMetricsFor (ParamFlowSlot.checkFlow :84)
+                const PRule pr = a.ps.p.rules[ri];
+                int64_t tc = 0;
+                uint64_t g = ~0ull;
+                bool early = false;
+                if (has) {
+                    const uint64_t v = a.ps.values[ag.value_begin];
+                    tc = param_token_count(a.ps.p, pr, v);
+                    if (tc == 0 || (pr.behavior != 2 && (int64_t)ev.count > tc + pr.burst)) {
+                        early = true;
+                    } else {
+                        g = param_slot(a.ps.p, pr, v);
+                        if (g == ~0ull) {
+                            atomicOr(a.ps.err, kErrTableFull);
+                            early = true;
+                        }
+                    }
+                }
+                // token chains: the lanes of one (rule, value) slot in lane (event) order
+                const bool chain = has && !early;
+                int rank = 0, prev = lane;
+                uint64_t gm = 0;
+                uint64_t todo = __ballot(chain);
+                while (todo) {
+                    const int l0 = __builtin_ctzll(todo);
+                    const uint64_t g0 = (uint64_t)bcast64((int64_t)g, l0);
+                    const uint64_t m = __ballot(chain && g == g0);
+                    todo &= ~m;
+                    if (chain && g == g0) {
+                        gm = m;
+                        const uint64_t lo = m & below(lane);
+                        rank = (int)__popcll(lo);
+                        prev = lo ? 63 - __builtin_clzll(lo) : lane;
+                    }
+                }
+                int maxrank = chain ? rank : 0;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) maxrank = max(maxrank, __shfl_xor(maxrank, o, 64));
+                PState st{0, 0, 0u};
+                if (chain && rank == 0) {
+                    const PSlot& sl = a.ps.p.table[g];
+                    st.time = sl.time;
+                    st.tokens = sl.tokens;
+                    st.flags = sl.flags;
+                }
+                bool ok = true;
+                for (int r = 0; r <= maxrank; ++r) {
+                    const int64_t ptm = __shfl((long long)st.time, prev, 64);
+                    const int64_t ptk = __shfl((long long)st.tokens, prev, 64);
+                    const uint32_t pfl = (uint32_t)__shfl((int)st.flags, prev, 64);
+                    if (chain && rank == r) {
+                        if (r > 0) {
+                            st.time = ptm;
+                            st.tokens = ptk;
+                            st.flags = pfl;
+                        }
+                        ok = pr.behavior == 2
+                                 ? param_throttle_step(st, throttle_cost(pr, tc, ev.count), pr.max_queueing_ms, t)
+                                 : param_default_step(st, tc, tc + pr.burst, pr.duration_sec * 1000, t, ev.count);
+                    }
+                }
+                if (chain && (gm & ~below(lane + 1)) == 0) {  // the slot's last request writes it back
+                    PSlot& sl = a.ps.p.table[g];
+                    sl.time = st.time;
+                    sl.tokens = st.tokens;
+                    sl.flags = st.flags;
+                }
+                pfail = has && (early || !ok);
+            }
+            if (pfail) lstore(a, ev.idx, SG_LOCAL_BLOCK_PARAM, prule);  // ParamFlowException (FLOW: the default)
+            // increaseBlockQps: the ClusterNode and the origin nodes (table), both windows
+            const int64_t blk = wave_sum(ent ? (int64_t)ev.count : 0);
+            nd.at(qs0, qm0);
+            nd.sc[kLBlock] += blk;
+            nd.mc[kLBlock] += blk;
+            uint64_t todo_o = __ballot(ent && nodes.x != kNoNode);
+            while (todo_o) {
+                const int l0 = __builtin_ctzll(todo_o);
+                const uint32_t node0 = (uint32_t)bcast32((int)nodes.x, l0);
+                const bool mine = ent && nodes.x == node0;
+                todo_o &= ~__ballot(mine);
+                const int64_t sum = wave_sum(mine ? (int64_t)ev.count : 0);
+                const uint64_t hit = __ballot(ob_node == node0);
+                if (hit) {
+                    if (lane == __builtin_ctzll(hit)) ob_sum += sum;
+                } else {
+                    uint64_t fr = __ballot(ob_node == kNoNode);
+                    if (!fr) {
+                        flush_origins();
+                        fr = ~0ull;
+                    }
+                    if (lane == __builtin_ctzll(fr)) {
+                        ob_node = node0;
+                        ob_sum = sum;
+                    }
+                }
+            }
+            // exits, in order (they change no pass count: the period stays dead)
+            uint64_t ex = __ballot(in && ev.kind != SG_LOCAL_ENTRY);
+            while (ex) {
+                const int q = __builtin_ctzll(ex);
+                ex &= ex - 1;
+                step(q, qs0, qm0);
+            }
+            p = rend;
+        }
+    }
+    if (dead) flush_origins();
+    nd.finish();
+}
+
+__global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, BatchArgs sg) {
+    __shared__ uint32_t sbnd[kLdsBnd];
+    __shared__ const uint32_t* bndp[kMaxWl];
+    if (*a.err) return;
+    stage_lperiods(a, sbnd, bndp);
+    const int lane = lane_id();
+    const uint32_t n_long = *sg.long_count;
+    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
+    for (uint32_t item = wave; item < n_long; item += nwaves) {
+        const uint64_t s = sg.long_list[item];
+        const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
+        const LRule& R = a.rules[k];
+        if (!(R.cx || (a.dyn && a.dyn[k] == a.epoch)) || R.grp) continue;  // k_lwalk_long / k_lwalk_cx
+        const uint64_t e = gallop_search(s + (sg.short_max ? sg.short_max : 1), a.n, [&](uint64_t p) {
+            return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
+        }, lane);
+        cx_wave(a, bndp, k, s, e);
     }
 }
 
@@ -1835,6 +2154,11 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
     hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
+    if (has_cx && a.cxw) {
+        static unsigned bw = 0;
+        if (bw == 0) bw = lresident((const void*)k_lwalk_cxw);
+        hipLaunchKernelGGL(k_lwalk_cxw, dim3(bw), dim3(256), 0, stream, a, sg);
+    }
     if (has_cx) hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, stream, a, sg);
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);

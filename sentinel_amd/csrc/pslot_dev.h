@@ -150,8 +150,11 @@ __device__ inline int64_t ps_tc(const PSArgs& s, uint32_t res, int32_t idx, uint
         if (o == own && e.value == v) return (int64_t)h;
         if (o == 0) {
             if (!create) return -1;
-            // claim the slot; only this resource's lane ever reads entries with this owner word
-            if (atomicCAS(&e.owner, 0ull, own) == 0ull) {
+            // claim the slot; only this resource's walker ever reads entries with this owner word — one lane, or
+            // one wave whose lanes run the same step (k_lwalk_cxw): a lane of the same wave that lost the claim to
+            // another with the same owner claims it with the same value
+            const unsigned long long prev = atomicCAS(&e.owner, 0ull, own);
+            if (prev == 0ull || prev == own) {
                 e.value = v;
                 e.count = 0;
                 return (int64_t)h;
