@@ -1666,14 +1666,19 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
         uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
         if (act) {
             ev = ldecode(a, a.rec_sorted[j]);
-            const sg_local_event le = a.ev[ev.idx];
-            t = le.ts_ms;
-            cr = le.create_ts;
-            org = le.origin;
-            if (a.ext) xx = a.ext[ev.idx];
-            nodes = event_nodes(a, ev.idx);
             qs = nd.cs.of(ev.idx);
             qm = nd.cm.of(ev.idx);
+            // an entry of the current dead period of a resource without ParamFlowSlot rules needs only its count and
+            // origin node: no event / argument read
+            const bool light = dead && prule < 0 && ev.kind == SG_LOCAL_ENTRY && qs == dead_qs && qm == dead_qm;
+            if (!light) {
+                const sg_local_event le = a.ev[ev.idx];
+                t = le.ts_ms;
+                cr = le.create_ts;
+                org = le.origin;
+                if (a.ext) xx = a.ext[ev.idx];
+            }
+            nodes = event_nodes(a, ev.idx);
         }
         // the serial step of lane q, every lane with lane q's values
         auto step = [&](int q, uint32_t qs0, uint32_t qm0) {
@@ -2152,14 +2157,16 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     hipError_t e = hipEventRecord(fork, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
-    hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
+    // the hot cx segments' waves first (the batch's longest serial chains), the lane walker of the other cx
+    // segments beside them after the plain wave walker
     if (has_cx && a.cxw) {
         static unsigned bw = 0;
         if (bw == 0) bw = lresident((const void*)k_lwalk_cxw);
         hipLaunchKernelGGL(k_lwalk_cxw, dim3(bw), dim3(256), 0, stream, a, sg);
     }
-    if (has_cx) hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, stream, a, sg);
+    hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
+    if (has_cx) hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, aux, a, sg);
+    hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
     if (e != hipSuccess) return e;
