@@ -672,6 +672,8 @@ struct LArgs {
     uint32_t epoch;
     int32_t track_ctx;        // 1: every event updates its context's DefaultNode (n_contexts >= 1)
     int32_t cxw;              // 1: long cx segments (not RELATE groups) go to the wave walker k_lwalk_cxw
+    uint64_t* pslot;          // [n] or null: k_local_prep's ParamFlowSlot lookup of each entry of a resource with one
+                              // QPS param rule (kPsNoCheck / kPsEarlyFail / kPsUnknown, else the (rule, value) slot)
     // the embedded token server (ClusterStateManager SERVER, emb = 1): the handle's cluster flow state
     int32_t emb;
     const Rule* c3_rules;
@@ -691,6 +693,10 @@ struct LArgs {
     int64_t* entry_fetch;     // the ENTRY_NODE's lastFetchTime
 };
 
+constexpr uint64_t kPsUnknown = ~0ull;     // LArgs::pslot codes: not looked up (the walker's own step decides)
+constexpr uint64_t kPsNoCheck = ~0ull - 1;  // args null: ParamFlowSlot passes without a look
+constexpr uint64_t kPsEarlyFail = ~0ull - 2;  // blocked before the maps (tokenCount 0, acquire > tokens + burst)
+constexpr uint64_t kPsNoCheckInit = ~0ull - 3;  // arguments, but none at paramIdx (too short or null): no check
 constexpr int kLFlagPrio = 1;    // some entry is prioritized (may occupy in a saturated window)
 constexpr int kLFlagNonPos = 2;  // some entry has acquireCount <= 0 (may fit in a saturated window)
 constexpr uint32_t kLTile = 4096;  // records per tile of the exit-position compaction

@@ -185,6 +185,45 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
             if (kind == 0 && (e.resource >> 31)) atomicOr(a.flags, kLFlagPrio);
             if (kind == 0 && e.count <= 0) atomicOr(a.flags, kLFlagNonPos);
         }
+        // ParamFlowSlot lookup of an entry of a resource with one QPS param rule (resolved paramIdx, local): the
+        // walkers' dead periods read the (rule, value) slot instead of the arguments (ParamFlowChecker.passSingleValue
+        // Check's early exits and the CacheMap putIfAbsent happen at the check: every such entry reaches it first)
+        if (a.pslot) {
+            uint64_t code = kPsUnknown;
+            if (res < a.K && e.kind == SG_LOCAL_ENTRY && a.rules[res].ps && a.has_ps) {
+                const uint32_t rb = a.ps.res_begin[res];
+                if (a.ps.res_begin[res + 1] == rb + 1) {
+                    const uint32_t ri = a.ps.res_rules[rb];
+                    const int32_t idx = a.ps.cur_idx[ri];
+                    const int32_t cm = a.ps.cmode ? a.ps.cmode[ri] : SG_CLUSTER_MODE_OFF;
+                    if (a.ps.grade[ri] == 1 && cm == SG_CLUSTER_MODE_OFF && idx >= 0) {
+                        const sg_slot_ext x = a.ext ? a.ext[i] : sg_slot_ext{0, 0, 0, 1};
+                        code = x.args_null ? kPsNoCheck : kPsNoCheckInit;
+                        // out-of-range argument records (kErrBounds above: the batch is refused) are not read
+                        const bool in_range = (uint64_t)x.arg_begin + x.arg_count <= a.ps.n_args;
+                        if (!x.args_null && (int32_t)x.arg_count > idx && in_range) {
+                            const sg_pslot_arg g = a.ps.args[x.arg_begin + (uint32_t)idx];
+                            if (g.kind != SG_ARG_NULL && (uint64_t)g.value_begin + 1 > a.ps.n_values) {
+                                code = kPsUnknown;
+                            } else if (g.kind == SG_ARG_COLLECTION) {
+                                code = kPsUnknown;
+                            } else if (g.kind == SG_ARG_VALUE) {
+                                const PRule pr = a.ps.p.rules[ri];
+                                const uint64_t v = a.ps.values[g.value_begin];
+                                const int64_t tc = param_token_count(a.ps.p, pr, v);
+                                if (tc == 0 || (pr.behavior != 2 && (int64_t)e.count > tc + pr.burst)) {
+                                    code = kPsEarlyFail;
+                                } else {
+                                    code = param_slot(a.ps.p, pr, v);
+                                    if (code == ~0ull) atomicOr(a.err, kErrTableFull);
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            a.pslot[i] = code;
+        }
         // default result: FlowException for entries (the common outcome of a saturated resource; the walkers
         // write every other outcome), plain 0 for exits and events of unknown resources
         const uint32_t dst = (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS;
@@ -281,6 +320,16 @@ __global__ void __launch_bounds__(256) k_lnode_assign(LArgs a) {
             if (a.track_ctx) v.y = lnode_slot(a, lnode_key(res, kLNodeCtx, a.ext ? a.ext[i].context : 0u));
         }
         a.ev_node[i] = v;
+    }
+}
+
+// Every event's map slots → node indices (after k_lnode_assign: the inserting lanes have written them), so the walkers
+// read an event's nodes with one load.
+__global__ void __launch_bounds__(256) k_lnode_resolve(LArgs a) {
+    if (*a.err) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint2 s = a.ev_node[i];
+        a.ev_node[i] = make_uint2(s.x != kNoNode ? a.nvals[s.x] : kNoNode, s.y != kNoNode ? a.nvals[s.y] : kNoNode);
     }
 }
 
@@ -1334,8 +1383,7 @@ __device__ int cx_rule(const LArgs& a, LNode& n, const LFlowRule& r, LCtl& c, co
 // o of the event) and the DefaultNode of the event's context (NodeSelectorSlot, context tracking on), from the pool.
 __device__ __forceinline__ uint2 event_nodes(const LArgs& a, uint32_t idx) {
     if (!a.nkeys) return make_uint2(kNoNode, kNoNode);
-    const uint2 s = a.ev_node[idx];
-    return make_uint2(s.x != kNoNode ? a.nvals[s.x] : kNoNode, s.y != kNoNode ? a.nvals[s.y] : kNoNode);
+    return a.ev_node[idx];  // node indices (k_lnode_resolve)
 }
 
 // One entry of a cx resource, the slot chain in SPI order inside StatisticSlot.entry (StatisticSlot.java:55-122):
@@ -1664,19 +1712,25 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
         xx.args_null = 1;
         uint2 nodes = make_uint2(kNoNode, kNoNode);
         uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
+        uint64_t psl = kPsUnknown;
         if (act) {
             ev = ldecode(a, a.rec_sorted[j]);
             qs = nd.cs.of(ev.idx);
             qm = nd.cm.of(ev.idx);
-            // an entry of the current dead period of a resource without ParamFlowSlot rules needs only its count and
-            // origin node: no event / argument read
-            const bool light = dead && prule < 0 && ev.kind == SG_LOCAL_ENTRY && qs == dead_qs && qm == dead_qm;
-            if (!light) {
+            // an entry of the current dead period needs only its count, origin node and (param rule) its time and
+            // k_local_prep's (rule, value) slot: no event record beyond the time, no argument read
+            const bool light = dead && ev.kind == SG_LOCAL_ENTRY && qs == dead_qs && qm == dead_qm &&
+                               (prule < 0 || a.pslot);
+            if (light && prule >= 0) {
+                t = a.ev[ev.idx].ts_ms;
+                psl = a.pslot[ev.idx];
+            } else if (!light) {
                 const sg_local_event le = a.ev[ev.idx];
                 t = le.ts_ms;
                 cr = le.create_ts;
                 org = le.origin;
                 if (a.ext) xx = a.ext[ev.idx];
+                if (a.pslot && prule >= 0 && ev.kind == SG_LOCAL_ENTRY) psl = a.pslot[ev.idx];
             }
             nodes = event_nodes(a, ev.idx);
         }
@@ -1731,35 +1785,51 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
             bool pfail = false;
             if (prule >= 0) {
                 const uint32_t ri = (uint32_t)prule;
-                const int32_t pidx = a.ps.cur_idx[ri];
-                const bool args = ent && a.ext && !xx.args_null;
-                bool has = args && (int32_t)xx.arg_count > pidx;
-                sg_pslot_arg ag;
-                ag.kind = SG_ARG_NULL;
-                ag.value_begin = ag.value_count = 0;
-                if (has) {
-                    ag = a.ps.args[xx.arg_begin + (uint32_t)pidx];
-                    has = ag.kind != SG_ARG_NULL;
-                }
-                if (__ballot(has && ag.kind == SG_ARG_COLLECTION)) {  // element by element: the serial step
-                    while (p < rend) step(p++, qs0, qm0);
-                    continue;
-                }
-                if (__ballot(args)) a.ps.inited[ri] = 1;  // initParamMetricsFor (ParamFlowSlot.checkFlow :84)
                 const PRule pr = a.ps.p.rules[ri];
                 int64_t tc = 0;
                 uint64_t g = ~0ull;
-                bool early = false;
-                if (has) {
-                    const uint64_t v = a.ps.values[ag.value_begin];
-                    tc = param_token_count(a.ps.p, pr, v);
-                    if (tc == 0 || (pr.behavior != 2 && (int64_t)ev.count > tc + pr.burst)) {
-                        early = true;
-                    } else {
-                        g = param_slot(a.ps.p, pr, v);
-                        if (g == ~0ull) {
-                            atomicOr(a.ps.err, kErrTableFull);
+                bool has = false, early = false;
+                if (a.pslot) {  // k_local_prep looked the entries up
+                    if (__ballot(ent && psl == kPsUnknown)) {  // a collection argument: element by element, serially
+                        while (p < rend) step(p++, qs0, qm0);
+                        continue;
+                    }
+                    // initParamMetricsFor ran for every entry with arguments; here: every entry of such a resource
+                    // with a resolved paramIdx has them when its lookup says so (no check: args null or too short)
+                    if (__ballot(ent && psl != kPsNoCheck)) a.ps.inited[ri] = 1;
+                    has = ent && psl != kPsNoCheck && psl != kPsNoCheckInit;
+                    early = has && psl == kPsEarlyFail;
+                    if (has && !early) {
+                        g = psl;
+                        tc = param_token_count(a.ps.p, pr, a.ps.p.table[g].value);
+                    }
+                } else {
+                    const int32_t pidx = a.ps.cur_idx[ri];
+                    const bool args = ent && a.ext && !xx.args_null;
+                    has = args && (int32_t)xx.arg_count > pidx;
+                    sg_pslot_arg ag;
+                    ag.kind = SG_ARG_NULL;
+                    ag.value_begin = ag.value_count = 0;
+                    if (has) {
+                        ag = a.ps.args[xx.arg_begin + (uint32_t)pidx];
+                        has = ag.kind != SG_ARG_NULL;
+                    }
+                    if (__ballot(has && ag.kind == SG_ARG_COLLECTION)) {  // element by element: the serial step
+                        while (p < rend) step(p++, qs0, qm0);
+                        continue;
+                    }
+                    if (__ballot(args)) a.ps.inited[ri] = 1;  // initParamMetricsFor (ParamFlowSlot.checkFlow :84)
+                    if (has) {
+                        const uint64_t v = a.ps.values[ag.value_begin];
+                        tc = param_token_count(a.ps.p, pr, v);
+                        if (tc == 0 || (pr.behavior != 2 && (int64_t)ev.count > tc + pr.burst)) {
                             early = true;
+                        } else {
+                            g = param_slot(a.ps.p, pr, v);
+                            if (g == ~0ull) {
+                                atomicOr(a.ps.err, kErrTableFull);
+                                early = true;
+                            }
                         }
                     }
                 }
@@ -2131,6 +2201,7 @@ hipError_t launch_local_init_range(const LArgs& a, uint64_t lo, uint64_t hi, hip
 
 hipError_t launch_lnode_assign(const LArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(k_lnode_assign, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_lnode_resolve, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
