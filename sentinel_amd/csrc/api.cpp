@@ -3314,6 +3314,8 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
     L.hist0_bits = radix_digit_bits(64 - L.kshift);
 
     sgm = BatchArgs{};  // segment lists (k_seg)
+    sgm.dbg = h->dbg;
+    sgm.dbg_ctr = h->d_dbg;
     sgm.n = n;
     sgm.rec_sorted = b.rec_sorted;
     sgm.kshift = L.kshift;

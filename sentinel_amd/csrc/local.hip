@@ -1616,6 +1616,21 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
 // acquireCount <= 0, context tracking, shaping controllers other than a lone WarmUp, several ParamFlowRules or
 // collection arguments keep the serial step.
 
+// The wave walker's serial step as a called function: its registers (the entry's origin / context nodes, the
+// controllers) stay out of the walker's loop, whose dead-period chunks then run without spilling.
+__device__ __noinline__ bool cxw_step(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& es,
+                                      int64_t te, int64_t ce, int og, const sg_slot_ext* xp, uint32_t qs0, uint32_t qm0,
+                                      uint2 nn) {
+    const int ctx = xp ? (int)xp->context : 0;
+    if (es.kind == SG_LOCAL_ENTRY) {
+        cx_entry(a, bndp, nd, es, te, og, ctx, xp, qs0, qm0, nn);
+        return true;
+    }
+    nd.at(qs0, qm0);
+    cx_exit(a, bndp, nd, es, te, ce, og, ctx, xp, qs0, qm0, nn);
+    return false;
+}
+
 // Whether resource k's periods can go dead; *prule = its one QPS ParamFlowRule (-1: none).
 __device__ bool cxw_dead_able(const LArgs& a, const LRule& R, uint32_t k, int32_t* prule) {
     *prule = -1;
@@ -1669,18 +1684,59 @@ __device__ bool cxw_saturated(const LArgs& a, const LNode& nd) {
     return false;
 }
 
-__device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k, uint64_t s, uint64_t e_end) {
+__device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* const* bndp, uint32_t k, uint64_t s,
+                        uint64_t e_end) {
     const int lane = lane_id();
+    // SG_DEBUG & 64: counters into sg.dbg_ctr[20..]: segments, wave ticks (sum, max), dead / general chunks, serial
+    // entry / exit steps, ticks in dead chunks, in serial steps (s_memrealtime, 100 MHz)
+    const bool dg = (sg.dbg & 64) && sg.dbg_ctr;
+    const uint64_t tw0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t c_dead = 0, c_gen = 0, c_sent = 0, c_sexit = 0, t_dead = 0, t_ser = 0;
     LNode nd(a, bndp, k);
     nd.created = 1;
     int32_t prule = -1;
     const bool dead_ok = !(*a.flags & (kLFlagPrio | kLFlagNonPos)) && cxw_dead_able(a, nd.R, k, &prule);
     bool dead = false;
     uint32_t dead_qs = 0xFFFFFFFFu, dead_qm = 0xFFFFFFFFu;
-    // BLOCK counts of the dead period's entries per origin node, one table slot per lane {node, sum}, added to the
-    // nodes when the period ends (before any later period can reuse their bucket slots)
+    uint32_t dead_end = 0;  // first event index past the dead period (its records are sorted by index)
+    int64_t dblk = 0;       // this lane's BLOCK counts of the dead period's entries (the ClusterNode's, at its end)
+    // ... per origin node: this lane's {node, sum} of its own entries (4 slots, no cross-lane work per chunk), merged
+    // into the wave's table — one slot per lane {node, sum} — when a lane runs out of slots or the period ends; the
+    // nodes get the sums when the period ends (before any later period can reuse their bucket slots)
+    uint32_t ln[4] = {kNoNode, kNoNode, kNoNode, kNoNode};
+    int64_t ls[4] = {0, 0, 0, 0};
     uint32_t ob_node = kNoNode;
     int64_t ob_sum = 0;
+    auto table_add = [&](uint32_t node0, int64_t sum) {  // wave-uniform
+        const uint64_t hit = __ballot(ob_node == node0);
+        if (hit) {
+            if (lane == __builtin_ctzll(hit)) ob_sum += sum;
+            return false;
+        }
+        const uint64_t fr = __ballot(ob_node == kNoNode);
+        if (!fr) return true;  // full: the caller flushes and retries
+        if (lane == __builtin_ctzll(fr)) {
+            ob_node = node0;
+            ob_sum = sum;
+        }
+        return false;
+    };
+    auto lane_add = [&](uint32_t node, int64_t c) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (ln[q] == node) {
+                ls[q] += c;
+                return true;
+            }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (ln[q] == kNoNode) {
+                ln[q] = node;
+                ls[q] = c;
+                return true;
+            }
+        return false;
+    };
     auto flush_origins = [&]() {
         uint64_t used = __ballot(ob_node != kNoNode);
         while (used) {
@@ -1696,9 +1752,87 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
         ob_node = kNoNode;
         ob_sum = 0;
     };
+    auto merge_lanes = [&]() {  // wave-uniform: every lane's {node, sum} slots into the wave's table
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint64_t todo = __ballot(ln[q] != kNoNode);
+            while (todo) {
+                const uint32_t node0 = (uint32_t)bcast32((int)ln[q], __builtin_ctzll(todo));
+                const bool mine = ln[q] == node0;
+                todo &= ~__ballot(mine);
+                const int64_t sum = wave_sum(mine ? ls[q] : 0);
+                if (table_add(node0, sum)) {
+                    flush_origins();
+                    table_add(node0, sum);
+                }
+            }
+            ln[q] = kNoNode;
+            ls[q] = 0;
+        }
+    };
+    auto end_dead = [&]() {
+        nd.at(dead_qs, dead_qm);
+        const int64_t b = wave_sum(dblk);
+        nd.sc[kLBlock] += b;
+        nd.mc[kLBlock] += b;
+        dblk = 0;
+        merge_lanes();
+        flush_origins();
+        dead = false;
+    };
+    uint64_t rec_n = s + (uint64_t)lane < e_end ? a.rec_sorted[s + lane] : 0;
     for (uint64_t base = s; base < e_end; base += 64) {
+        // ---- dead period, no ParamFlowSlot rule: four chunks per step while they hold only the period's entries
+        // (count and origin node are all an entry needs; every load of the step issued together)
+        if (dead && prule < 0) {
+            const uint64_t b0 = base;
+            for (;;) {
+                uint64_t r[4];
+                r[0] = base + (uint64_t)lane < e_end ? a.rec_sorted[base + lane] : 0;
+#pragma unroll
+                for (int u = 1; u < 4; ++u) {
+                    const uint64_t jj = base + (uint64_t)(u * 64 + lane);
+                    r[u] = jj < e_end ? a.rec_sorted[jj] : 0;
+                }
+                bool ok = true;
+                LEvent eu[4];
+                uint2 nu[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint64_t jj = base + (uint64_t)(u * 64 + lane);
+                    eu[u].kind = -1;
+                    eu[u].count = 0;
+                    eu[u].idx = 0;
+                    if (jj < e_end) {
+                        eu[u] = ldecode(a, r[u]);
+                        ok = ok && eu[u].kind == SG_LOCAL_ENTRY && eu[u].idx < dead_end;
+                    }
+                }
+                if (__ballot(!ok) || base + 256 > e_end) break;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) nu[u] = event_nodes(a, eu[u].idx);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    dblk += eu[u].count;
+                    const bool on = nu[u].x != kNoNode;
+                    const bool ovf = on && !lane_add(nu[u].x, eu[u].count);
+                    if (__ballot(ovf)) {
+                        merge_lanes();
+                        if (ovf) lane_add(nu[u].x, eu[u].count);
+                    }
+                }
+                base += 256;
+                if (dg) c_dead += 4;
+            }
+            if (base != b0) {
+                if (base >= e_end) break;
+                rec_n = a.rec_sorted[min(base + (uint64_t)lane, a.n - 1)];
+            }
+        }
         const uint64_t j = base + (uint64_t)lane;
         const bool act = j < e_end;
+        const uint64_t rec_c = rec_n;
+        rec_n = j + 64 < e_end ? a.rec_sorted[j + 64] : 0;  // the next chunk's records, in flight meanwhile
         LEvent ev;
         ev.idx = 0;
         ev.count = 0;
@@ -1713,29 +1847,18 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
         uint2 nodes = make_uint2(kNoNode, kNoNode);
         uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
         uint64_t psl = kPsUnknown;
-        if (act) {
-            ev = ldecode(a, a.rec_sorted[j]);
-            qs = nd.cs.of(ev.idx);
-            qm = nd.cm.of(ev.idx);
-            // an entry of the current dead period needs only its count, origin node and (param rule) its time and
-            // k_local_prep's (rule, value) slot: no event record beyond the time, no argument read
-            const bool light = dead && ev.kind == SG_LOCAL_ENTRY && qs == dead_qs && qm == dead_qm &&
-                               (prule < 0 || a.pslot);
-            if (light && prule >= 0) {
-                t = a.ev[ev.idx].ts_ms;
-                psl = a.pslot[ev.idx];
-            } else if (!light) {
-                const sg_local_event le = a.ev[ev.idx];
-                t = le.ts_ms;
-                cr = le.create_ts;
-                org = le.origin;
-                if (a.ext) xx = a.ext[ev.idx];
-                if (a.pslot && prule >= 0 && ev.kind == SG_LOCAL_ENTRY) psl = a.pslot[ev.idx];
-            }
-            nodes = event_nodes(a, ev.idx);
-        }
+        if (act) ev = ldecode(a, rec_c);
+        auto load_full = [&]() {  // the event record, its arguments and (param rule) lookup
+            const sg_local_event le = a.ev[ev.idx];
+            t = le.ts_ms;
+            cr = le.create_ts;
+            org = le.origin;
+            if (a.ext) xx = a.ext[ev.idx];
+            if (a.pslot && prule >= 0 && ev.kind == SG_LOCAL_ENTRY) psl = a.pslot[ev.idx];
+        };
         // the serial step of lane q, every lane with lane q's values
         auto step = [&](int q, uint32_t qs0, uint32_t qm0) {
+            const uint64_t ts0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
             LEvent es;
             es.idx = (uint32_t)bcast32((int)ev.idx, q);
             es.count = bcast32(ev.count, q);
@@ -1750,37 +1873,17 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
             xe.args_null = bcast32(xx.args_null, q);
             const uint2 nn = make_uint2((uint32_t)bcast32((int)nodes.x, q), (uint32_t)bcast32((int)nodes.y, q));
             const sg_slot_ext* xp = a.ext ? &xe : nullptr;
-            if (es.kind == SG_LOCAL_ENTRY) {
-                cx_entry(a, bndp, nd, es, te, og, (int)xe.context, xp, qs0, qm0, nn);
-                return true;
+            const bool entry = cxw_step(a, bndp, nd, es, te, ce, og, xp, qs0, qm0, nn);
+            if (dg) {
+                if (entry) ++c_sent;
+                else ++c_sexit;
+                t_ser += __builtin_amdgcn_s_memrealtime() - ts0;
             }
-            nd.at(qs0, qm0);
-            cx_exit(a, bndp, nd, es, te, ce, og, (int)xe.context, xp, qs0, qm0, nn);
-            return false;
+            return entry;
         };
-        const int nact = (int)__popcll(__ballot(act));
-        int p = 0;
-        while (p < nact) {
-            // run: lanes [p, rend) in the window periods of lane p
-            const uint32_t qs0 = (uint32_t)bcast32((int)qs, p), qm0 = (uint32_t)bcast32((int)qm, p);
-            const uint64_t diff = __ballot(act && lane > p && (qs != qs0 || qm != qm0));
-            const int rend = diff ? __builtin_ctzll(diff) : nact;
-            if (dead && (qs0 != dead_qs || qm0 != dead_qm)) {  // the dead period ended
-                flush_origins();
-                dead = false;
-            }
-            while (p < rend && !dead) {
-                const bool entry = step(p, qs0, qm0);
-                ++p;
-                if (entry && dead_ok && nd.cs.q == qs0 && nd.cm.q == qm0 && cxw_saturated(a, nd)) {
-                    dead = true;
-                    dead_qs = qs0;
-                    dead_qm = qm0;
-                }
-            }
-            if (p >= rend) continue;
-            // ---- lanes [p, rend) of a dead period: entries FLOW-blocked unless their ParamFlowSlot check fails
-            const bool in = act && lane >= p && lane < rend;
+        // Lanes `in` of the dead period: entries FLOW-blocked unless their ParamFlowSlot check fails, exits serial.
+        // Returns false (nothing done) when an entry needs the serial step (a collection argument).
+        auto dead_lanes = [&](bool in) {
             const bool ent = in && ev.kind == SG_LOCAL_ENTRY;
             bool pfail = false;
             if (prule >= 0) {
@@ -1790,18 +1893,13 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
                 uint64_t g = ~0ull;
                 bool has = false, early = false;
                 if (a.pslot) {  // k_local_prep looked the entries up
-                    if (__ballot(ent && psl == kPsUnknown)) {  // a collection argument: element by element, serially
-                        while (p < rend) step(p++, qs0, qm0);
-                        continue;
-                    }
-                    // initParamMetricsFor ran for every entry with arguments; here: every entry of such a resource
-                    // with a resolved paramIdx has them when its lookup says so (no check: args null or too short)
-                    if (__ballot(ent && psl != kPsNoCheck)) a.ps.inited[ri] = 1;
+                    if (__ballot(ent && psl == kPsUnknown)) return false;
+                    if (__ballot(ent && psl != kPsNoCheck)) a.ps.inited[ri] = 1;  // initParamMetricsFor
                     has = ent && psl != kPsNoCheck && psl != kPsNoCheckInit;
                     early = has && psl == kPsEarlyFail;
                     if (has && !early) {
                         g = psl;
-                        tc = param_token_count(a.ps.p, pr, a.ps.p.table[g].value);
+                        tc = pr.hot_count ? param_token_count(a.ps.p, pr, a.ps.p.table[g].value) : pr.token_count;
                     }
                 } else {
                     const int32_t pidx = a.ps.cur_idx[ri];
@@ -1814,10 +1912,7 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
                         ag = a.ps.args[xx.arg_begin + (uint32_t)pidx];
                         has = ag.kind != SG_ARG_NULL;
                     }
-                    if (__ballot(has && ag.kind == SG_ARG_COLLECTION)) {  // element by element: the serial step
-                        while (p < rend) step(p++, qs0, qm0);
-                        continue;
-                    }
+                    if (__ballot(has && ag.kind == SG_ARG_COLLECTION)) return false;
                     if (__ballot(args)) a.ps.inited[ri] = 1;  // initParamMetricsFor (ParamFlowSlot.checkFlow :84)
                     if (has) {
                         const uint64_t v = a.ps.values[ag.value_begin];
@@ -1885,45 +1980,103 @@ __device__ void cx_wave(const LArgs& a, const uint32_t* const* bndp, uint32_t k,
                 pfail = has && (early || !ok);
             }
             if (pfail) lstore(a, ev.idx, SG_LOCAL_BLOCK_PARAM, prule);  // ParamFlowException (FLOW: the default)
-            // increaseBlockQps: the ClusterNode and the origin nodes (table), both windows
-            const int64_t blk = wave_sum(ent ? (int64_t)ev.count : 0);
-            nd.at(qs0, qm0);
-            nd.sc[kLBlock] += blk;
-            nd.mc[kLBlock] += blk;
-            uint64_t todo_o = __ballot(ent && nodes.x != kNoNode);
-            while (todo_o) {
-                const int l0 = __builtin_ctzll(todo_o);
-                const uint32_t node0 = (uint32_t)bcast32((int)nodes.x, l0);
-                const bool mine = ent && nodes.x == node0;
-                todo_o &= ~__ballot(mine);
-                const int64_t sum = wave_sum(mine ? (int64_t)ev.count : 0);
-                const uint64_t hit = __ballot(ob_node == node0);
-                if (hit) {
-                    if (lane == __builtin_ctzll(hit)) ob_sum += sum;
-                } else {
-                    uint64_t fr = __ballot(ob_node == kNoNode);
-                    if (!fr) {
-                        flush_origins();
-                        fr = ~0ull;
-                    }
-                    if (lane == __builtin_ctzll(fr)) {
-                        ob_node = node0;
-                        ob_sum = sum;
-                    }
-                }
+            // increaseBlockQps of the ClusterNode and the origin nodes, both windows (added when the period ends)
+            if (ent) dblk += ev.count;
+            const bool on = ent && nodes.x != kNoNode;
+            const bool ovf = on && !lane_add(nodes.x, ev.count);
+            if (__ballot(ovf)) {
+                merge_lanes();
+                if (ovf) lane_add(nodes.x, ev.count);
             }
             // exits, in order (they change no pass count: the period stays dead)
             uint64_t ex = __ballot(in && ev.kind != SG_LOCAL_ENTRY);
             while (ex) {
                 const int q = __builtin_ctzll(ex);
                 ex &= ex - 1;
-                step(q, qs0, qm0);
+                step(q, dead_qs, dead_qm);
+            }
+            return true;
+        };
+        // ---- a chunk wholly inside the dead period: its entries need only count, node, time and param lookup
+        if (dead && (prule < 0 || a.pslot != nullptr)) {
+            const bool in = act && ev.idx < dead_end;
+            if (__ballot(act && !in) == 0) {
+                const uint64_t td0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+                if (act) {
+                    if (ev.kind != SG_LOCAL_ENTRY) {
+                        load_full();
+                    } else if (prule >= 0) {
+                        t = a.ev[ev.idx].ts_ms;
+                        psl = a.pslot[ev.idx];
+                    }
+                    nodes = event_nodes(a, ev.idx);
+                }
+                if (dead_lanes(in)) {
+                    if (dg) {
+                        ++c_dead;
+                        t_dead += __builtin_amdgcn_s_memrealtime() - td0;
+                    }
+                    continue;
+                }
+                // a collection argument: the general path below (its serial steps)
+                if (act && ev.kind == SG_LOCAL_ENTRY) load_full();
+            }
+        }
+        // ---- the general path: runs of equal window periods, serial until dead
+        if (dg) ++c_gen;
+        if (act) {
+            if (ev.kind != SG_LOCAL_ENTRY || !(dead && ev.idx < dead_end) || psl == kPsUnknown) load_full();
+            nodes = event_nodes(a, ev.idx);
+            qs = nd.cs.of(ev.idx);
+            qm = nd.cm.of(ev.idx);
+        }
+        const int nact = (int)__popcll(__ballot(act));
+        int p = 0;
+        while (p < nact) {
+            // run: lanes [p, rend) in the window periods of lane p
+            const uint32_t qs0 = (uint32_t)bcast32((int)qs, p), qm0 = (uint32_t)bcast32((int)qm, p);
+            const uint64_t diff = __ballot(act && lane > p && (qs != qs0 || qm != qm0));
+            const int rend = diff ? __builtin_ctzll(diff) : nact;
+            if (dead && (qs0 != dead_qs || qm0 != dead_qm)) end_dead();  // the dead period ended
+            while (p < rend && !dead) {
+                const bool entry = step(p, qs0, qm0);
+                ++p;
+                if (entry && dead_ok && nd.cs.q == qs0 && nd.cm.q == qm0 && cxw_saturated(a, nd)) {
+                    dead = true;
+                    dead_qs = qs0;
+                    dead_qm = qm0;
+                    dead_end = min(nd.cs.next_b, nd.cm.next_b);
+                }
+            }
+            if (p >= rend) continue;
+            const bool in = act && lane >= p && lane < rend;
+            if (!dead_lanes(in)) {
+                while (p < rend) step(p++, qs0, qm0);
+                continue;
             }
             p = rend;
         }
     }
-    if (dead) flush_origins();
+    if (dead) end_dead();
     nd.finish();
+    if (dg && lane == 0) {
+        const uint64_t tw = __builtin_amdgcn_s_memrealtime() - tw0;
+        atomicAdd(&sg.dbg_ctr[20], 1ull);
+        atomicAdd(&sg.dbg_ctr[21], (unsigned long long)tw);
+        atomicMax(&sg.dbg_ctr[22], (unsigned long long)tw);
+        atomicAdd(&sg.dbg_ctr[23], (unsigned long long)c_dead);
+        atomicAdd(&sg.dbg_ctr[24], (unsigned long long)c_gen);
+        atomicAdd(&sg.dbg_ctr[25], (unsigned long long)c_sent);
+        atomicAdd(&sg.dbg_ctr[26], (unsigned long long)c_sexit);
+        atomicAdd(&sg.dbg_ctr[27], (unsigned long long)t_dead);
+        atomicAdd(&sg.dbg_ctr[28], (unsigned long long)t_ser);
+        if (tw > 500000ull) {  // segments over 5 ms: their serial steps, serial ticks, dead chunks
+            atomicAdd(&sg.dbg_ctr[29], (unsigned long long)(c_sent + c_sexit));
+            atomicAdd(&sg.dbg_ctr[30], (unsigned long long)t_ser);
+            atomicAdd(&sg.dbg_ctr[31], (unsigned long long)c_dead);
+            atomicAdd(&sg.dbg_ctr[19], 1ull);
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, BatchArgs sg) {
@@ -1943,7 +2096,7 @@ __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, Bat
         const uint64_t e = gallop_search(s + (sg.short_max ? sg.short_max : 1), a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
-        cx_wave(a, bndp, k, s, e);
+        cx_wave(a, sg, bndp, k, s, e);
     }
 }
 
