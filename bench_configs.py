@@ -328,14 +328,20 @@ def slot(args, dev):
                                                 n_vals, d_vals.data_ptr(), n_vals, outs[i].data_ptr(), stream),
                args.warmup, args.steps)
     if int(os.environ.get("SG_DEBUG", "0")) & 64:  # the cx wave walker's counters (local.hip cx_wave), per batch
-        d = eng.debug_copy(5, np.uint64, 32).astype(np.int64)
+        d = eng.debug_copy(5, np.uint64, 128).astype(np.int64)
         nb = len(sizes)
         print("# cxw per batch: segments %.0f, wave-ms sum %.2f max %.2f, dead chunks %.0f, general chunks %.0f, "
               "serial entries %.0f exits %.0f, dead-chunk ms %.2f, serial ms %.2f" % (
                   d[20] / nb, d[21] / nb / 1e5, d[22] / 1e5, d[23] / nb, d[24] / nb, d[25] / nb, d[26] / nb,
                   d[27] / nb / 1e5, d[28] / nb / 1e5), file=sys.stderr, flush=True)
+        print("# cxw dead-chunk head ms per batch: %.2f" % (d[17] / nb / 1e5), file=sys.stderr, flush=True)
         print("# cxw segments over 5 ms per batch: %.1f; their serial steps %.0f (%.2f ms), dead chunks %.0f" % (
             d[19] / nb, d[29] / nb, d[30] / nb / 1e5, d[31] / nb), file=sys.stderr, flush=True)
+        for sl in range(min(12, int(d[18]))):
+            o = d[32 + 8 * sl: 40 + 8 * sl]
+            print("#   segment: resource %d records %d wave-ms %.2f dead-ms %.2f dead chunks %d serial %d (%.2f ms) "
+                  "param rule %d" % (o[0], o[1], o[2] / 1e5, o[3] / 1e5, o[4], o[5], o[6] / 1e5, o[7]),
+                  file=sys.stderr, flush=True)
     for i in range(len(sizes)):  # full-size parity of every batch
         got = outs[i].cpu().numpy().view(abi.LOCAL_RES_DTYPE)
         if not np.array_equal(got, wants[i]):

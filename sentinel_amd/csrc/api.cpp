@@ -61,7 +61,7 @@ struct sg_handle {
     FidSlot* d_fid = nullptr;         // flowId → rule index (wire codec), 2^k slots
     uint64_t fid_mask = 0;  // [kLongTab][kLongPeriods] period ends of the long segments
     uint64_t class_off[kClasses]{};
-    unsigned long long* d_dbg = nullptr;   // [32] debug counters (SG_DEBUG & 64)
+    unsigned long long* d_dbg = nullptr;   // [128] debug counters (SG_DEBUG & 64)
     uint4* d_skips = nullptr;
     uint32_t* d_skip_count = nullptr;
     int* h_err = nullptr;       // pinned
@@ -520,7 +520,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
             hipMalloc(&h->d_short_end, sizeof(uint32_t) * off) != hipSuccess)
             return bail(SG_E_NOMEM);
     }
-    if (hipMalloc(&h->d_dbg, 32 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 32 * 8) != hipSuccess) return bail(SG_E_NOMEM);
+    if (hipMalloc(&h->d_dbg, 128 * 8) != hipSuccess || hipMemset(h->d_dbg, 0, 128 * 8) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_long_count, (1 + kClasses) * sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_skips, sizeof(uint4) * (2 * n / kSkipMin + 1)) != hipSuccess) return bail(SG_E_NOMEM);
     if (hipMalloc(&h->d_skip_count, sizeof(uint32_t)) != hipSuccess) return bail(SG_E_NOMEM);
@@ -4494,7 +4494,7 @@ int sg_debug_copy(sg_handle* h, int what, void* dst, uint64_t bytes) {
     case 2: src = h->d_bnd; cap = sizeof(uint32_t) * kMaxWl * kMaxPeriods; break;
     case 3: src = h->d_p0; cap = sizeof(int64_t) * kMaxWl; break;
     case 4: src = h->d_np; cap = sizeof(uint32_t) * kMaxWl; break;
-    case 5: src = h->d_dbg; cap = 32 * 8; break;
+    case 5: src = h->d_dbg; cap = 128 * 8; break;
     default: return SG_E_INVAL;
     }
     if (bytes > cap) return SG_E_INVAL;

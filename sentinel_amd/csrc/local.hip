@@ -1696,6 +1696,10 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
     nd.created = 1;
     int32_t prule = -1;
     const bool dead_ok = !(*a.flags & (kLFlagPrio | kLFlagNonPos)) && cxw_dead_able(a, nd.R, k, &prule);
+    prule = __builtin_amdgcn_readfirstlane(prule);
+    PRule pr{};  // the ParamFlowRule the dead periods check
+    if (prule >= 0) pr = a.ps.p.rules[prule];
+    bool inited = false;  // this walker set the rule's initParamMetricsFor flag
     bool dead = false;
     uint32_t dead_qs = 0xFFFFFFFFu, dead_qm = 0xFFFFFFFFu;
     uint32_t dead_end = 0;  // first event index past the dead period (its records are sorted by index)
@@ -1780,8 +1784,35 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         flush_origins();
         dead = false;
     };
-    uint64_t rec_n = s + (uint64_t)lane < e_end ? a.rec_sorted[s + lane] : 0;
-    for (uint64_t base = s; base < e_end; base += 64) {
+    // Records are read two chunks ahead and the next chunk's per-event words (time and ParamFlowSlot lookup of an
+    // entry, origin / context nodes) one chunk ahead, so a dead chunk waits on one load latency (its slot states).
+    // The chunk step runs twice per loop turn with the two register sets swapped: the prefetched values then need
+    // no copy at the turn's end (a copy would wait for their loads).
+    struct Pf {
+        int64_t t;
+        uint64_t psl;
+        uint2 nodes;
+    };
+    auto gather = [&](uint64_t j, uint64_t rec) {
+        Pf f;
+        f.t = 0;
+        f.psl = kPsUnknown;
+        f.nodes = make_uint2(kNoNode, kNoNode);
+        if (j < e_end) {
+            const LEvent e = ldecode(a, rec);
+            f.nodes = event_nodes(a, e.idx);
+            if (prule >= 0 && a.pslot && e.kind == SG_LOCAL_ENTRY) {
+                f.t = a.ev[e.idx].ts_ms;
+                f.psl = a.pslot[e.idx];
+            }
+        }
+        return f;
+    };
+    // one chunk at base: rec_c its records (then the records two chunks ahead), rec_n the next chunk's, fc its
+    // prefetched words, fn the next chunk's (issued here); false: the segment is done
+    uint64_t t_head = 0;  // SG_DEBUG & 64: ticks from a dead chunk's start to its dead-period work
+    auto chunk = [&](uint64_t& base, uint64_t& rec_c, uint64_t& rec_n, Pf& fc, Pf& fn) -> bool {
+        const uint64_t th0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
         // ---- dead period, no ParamFlowSlot rule: four chunks per step while they hold only the period's entries
         // (count and origin node are all an entry needs; every load of the step issued together)
         if (dead && prule < 0) {
@@ -1825,14 +1856,15 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 if (dg) c_dead += 4;
             }
             if (base != b0) {
-                if (base >= e_end) break;
-                rec_n = a.rec_sorted[min(base + (uint64_t)lane, a.n - 1)];
+                if (base >= e_end) return false;
+                rec_c = a.rec_sorted[min(base + (uint64_t)lane, a.n - 1)];
+                rec_n = base + 64 + (uint64_t)lane < e_end ? a.rec_sorted[base + 64 + lane] : 0;
+                fc = gather(base + (uint64_t)lane, rec_c);
             }
         }
         const uint64_t j = base + (uint64_t)lane;
         const bool act = j < e_end;
-        const uint64_t rec_c = rec_n;
-        rec_n = j + 64 < e_end ? a.rec_sorted[j + 64] : 0;  // the next chunk's records, in flight meanwhile
+        fn = gather(j + 64, rec_n);
         LEvent ev;
         ev.idx = 0;
         ev.count = 0;
@@ -1848,6 +1880,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         uint32_t qs = 0xFFFFFFFFu, qm = 0xFFFFFFFFu;
         uint64_t psl = kPsUnknown;
         if (act) ev = ldecode(a, rec_c);
+        rec_c = j + 128 < e_end ? a.rec_sorted[j + 128] : 0;  // in flight meanwhile
         auto load_full = [&]() {  // the event record, its arguments and (param rule) lookup
             const sg_local_event le = a.ev[ev.idx];
             t = le.ts_ms;
@@ -1888,13 +1921,15 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
             bool pfail = false;
             if (prule >= 0) {
                 const uint32_t ri = (uint32_t)prule;
-                const PRule pr = a.ps.p.rules[ri];
                 int64_t tc = 0;
                 uint64_t g = ~0ull;
                 bool has = false, early = false;
                 if (a.pslot) {  // k_local_prep looked the entries up
                     if (__ballot(ent && psl == kPsUnknown)) return false;
-                    if (__ballot(ent && psl != kPsNoCheck)) a.ps.inited[ri] = 1;  // initParamMetricsFor
+                    if (!inited && __ballot(ent && psl != kPsNoCheck)) {  // initParamMetricsFor
+                        a.ps.inited[ri] = 1;
+                        inited = true;
+                    }
                     has = ent && psl != kPsNoCheck && psl != kPsNoCheckInit;
                     early = has && psl == kPsEarlyFail;
                     if (has && !early) {
@@ -1928,8 +1963,21 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                         }
                     }
                 }
+                // every request reads its slot; one the state already refuses — a token bucket within its
+                // duration with no token left — leaves the slot as it is, and so does every earlier request of the
+                // slot in the chunk (times non-decreasing, acquireCount >= 1): only the requests after them chain
+                const bool chain0 = has && !early;
+                PState st{0, 0, 0u};
+                if (chain0) {
+                    const PSlot& sl = a.ps.p.table[g];
+                    st.time = sl.time;
+                    st.tokens = sl.tokens;
+                    st.flags = sl.flags;
+                }
+                const bool stuck = chain0 && pr.behavior != 2 && (st.flags & 3u) == 3u &&
+                                   t - st.time <= pr.duration_sec * 1000 && st.tokens <= 0;
                 // token chains: the lanes of one (rule, value) slot in lane (event) order
-                const bool chain = has && !early;
+                const bool chain = chain0 && !stuck;
                 int rank = 0, prev = lane;
                 uint64_t gm = 0;
                 uint64_t todo = __ballot(chain);
@@ -1948,14 +1996,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 int maxrank = chain ? rank : 0;
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) maxrank = max(maxrank, __shfl_xor(maxrank, o, 64));
-                PState st{0, 0, 0u};
-                if (chain && rank == 0) {
-                    const PSlot& sl = a.ps.p.table[g];
-                    st.time = sl.time;
-                    st.tokens = sl.tokens;
-                    st.flags = sl.flags;
-                }
-                bool ok = true;
+                bool ok = !stuck;
                 for (int r = 0; r <= maxrank; ++r) {
                     const int64_t ptm = __shfl((long long)st.time, prev, 64);
                     const int64_t ptk = __shfl((long long)st.tokens, prev, 64);
@@ -2002,21 +2043,23 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
             const bool in = act && ev.idx < dead_end;
             if (__ballot(act && !in) == 0) {
                 const uint64_t td0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+                if (dg) t_head += td0 - th0;
                 if (act) {
                     if (ev.kind != SG_LOCAL_ENTRY) {
                         load_full();
-                    } else if (prule >= 0) {
-                        t = a.ev[ev.idx].ts_ms;
-                        psl = a.pslot[ev.idx];
+                    } else {
+                        t = fc.t;
+                        psl = fc.psl;
                     }
-                    nodes = event_nodes(a, ev.idx);
+                    nodes = fc.nodes;
                 }
                 if (dead_lanes(in)) {
                     if (dg) {
                         ++c_dead;
                         t_dead += __builtin_amdgcn_s_memrealtime() - td0;
                     }
-                    continue;
+                    base += 64;
+                    return base < e_end;
                 }
                 // a collection argument: the general path below (its serial steps)
                 if (act && ev.kind == SG_LOCAL_ENTRY) load_full();
@@ -2026,7 +2069,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         if (dg) ++c_gen;
         if (act) {
             if (ev.kind != SG_LOCAL_ENTRY || !(dead && ev.idx < dead_end) || psl == kPsUnknown) load_full();
-            nodes = event_nodes(a, ev.idx);
+            nodes = fc.nodes;
             qs = nd.cs.of(ev.idx);
             qm = nd.cm.of(ev.idx);
         }
@@ -2056,6 +2099,13 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
             }
             p = rend;
         }
+        base += 64;
+        return base < e_end;
+    };
+    uint64_t ra = s + (uint64_t)lane < e_end ? a.rec_sorted[s + lane] : 0;
+    uint64_t rb = s + 64 + (uint64_t)lane < e_end ? a.rec_sorted[s + 64 + lane] : 0;
+    Pf fa = gather(s + (uint64_t)lane, ra), fb;
+    for (uint64_t base = s; chunk(base, ra, rb, fa, fb) && chunk(base, rb, ra, fb, fa);) {
     }
     if (dead) end_dead();
     nd.finish();
@@ -2070,11 +2120,25 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         atomicAdd(&sg.dbg_ctr[26], (unsigned long long)c_sexit);
         atomicAdd(&sg.dbg_ctr[27], (unsigned long long)t_dead);
         atomicAdd(&sg.dbg_ctr[28], (unsigned long long)t_ser);
+        atomicAdd(&sg.dbg_ctr[17], (unsigned long long)t_head);
         if (tw > 500000ull) {  // segments over 5 ms: their serial steps, serial ticks, dead chunks
             atomicAdd(&sg.dbg_ctr[29], (unsigned long long)(c_sent + c_sexit));
             atomicAdd(&sg.dbg_ctr[30], (unsigned long long)t_ser);
             atomicAdd(&sg.dbg_ctr[31], (unsigned long long)c_dead);
             atomicAdd(&sg.dbg_ctr[19], 1ull);
+            const unsigned long long sl = atomicAdd(&sg.dbg_ctr[18], 1ull);
+            if (sl < 12) {  // [32 + 8 * sl]: resource, records, wave ticks, dead ticks, dead chunks, serial steps /
+                            // ticks, param rule
+                unsigned long long* o = sg.dbg_ctr + 32 + 8 * sl;
+                o[0] = k;
+                o[1] = e_end - s;
+                o[2] = tw;
+                o[3] = t_dead;
+                o[4] = c_dead;
+                o[5] = c_sent + c_sexit;
+                o[6] = t_ser;
+                o[7] = (unsigned long long)(int64_t)prule;
+            }
         }
     }
 }
