@@ -178,6 +178,7 @@ struct sg_handle {
         LSkip* skips = nullptr;
         uint32_t* skip_count = nullptr;
         uint64_t* pslot = nullptr;    // [max_batch] LArgs::pslot (param rules loaded and the cx wave walker on)
+        CxSide* cxside = nullptr;     // [max_batch] LArgs::cxside (with pslot)
     };
     LocalWs lws[2];
     uint32_t lskip_cap = 0;
@@ -709,6 +710,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lev_h);
     for (auto& w : h->lws) {
         dfree(w.pslot);
+        dfree(w.cxside);
         dfree(w.flags);
         dfree(w.exit_pos);
         dfree(w.exit_cnt);
@@ -3285,9 +3287,11 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
         const int prc = pslot_embed(h, L.ps, 0);  // cluster-mode param rules on the embedded token server
         if (prc) return prc;
         if (h->l_cxw) {
-            if (!b.lw->pslot && hipMalloc(&b.lw->pslot, sizeof(uint64_t) * h->cfg.max_batch) != hipSuccess)
+            if (!b.lw->pslot && (hipMalloc(&b.lw->pslot, sizeof(uint64_t) * h->cfg.max_batch) != hipSuccess ||
+                                 hipMalloc(&b.lw->cxside, sizeof(CxSide) * h->cfg.max_batch) != hipSuccess))
                 return fail(h, SG_E_NOMEM, "param lookups of the local batch");
             L.pslot = b.lw->pslot;
+            L.cxside = b.lw->cxside;
         }
     }
     if (emb) {  // the embedded token server: this handle's cluster flow state

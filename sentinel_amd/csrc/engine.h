@@ -212,6 +212,15 @@ struct PRule {
     uint64_t table_mask;    // 2^capacity_log2 - 1; slot table_base + mask + 1 holds the value ~0
 };
 
+// The words a dead period of the cx wave walker reads per entry of a resource with a param rule, in sorted-record order
+// (k_lcx_side): the event time, its ParamFlowSlot lookup (LArgs::pslot in 32 bits: 0xFFFFFFFC.. = the kPs* codes,
+// else the slot) and its origin node.
+struct alignas(16) CxSide {
+    int64_t t;
+    uint32_t psl;
+    uint32_t node;
+};
+
 struct alignas(32) PSlot {  // one (rule, value): timeCounters / tokenCounters entries
     uint64_t value;         // ~0 = empty (except in the side slot)
     uint32_t flags;         // bit0 time counter present, bit1 token counter present
@@ -674,6 +683,7 @@ struct LArgs {
     int32_t cxw;              // 1: long cx segments (not RELATE groups) go to the wave walker k_lwalk_cxw
     uint64_t* pslot;          // [n] or null: k_local_prep's ParamFlowSlot lookup of each entry of a resource with one
                               // QPS param rule (kPsNoCheck / kPsEarlyFail / kPsUnknown, else the (rule, value) slot)
+    CxSide* cxside;           // [n] or null (with pslot): k_lcx_side's words of the sorted records of param cx resources
     // the embedded token server (ClusterStateManager SERVER, emb = 1): the handle's cluster flow state
     int32_t emb;
     const Rule* c3_rules;

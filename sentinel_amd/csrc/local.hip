@@ -56,6 +56,29 @@ __device__ __forceinline__ int64_t bcast64(int64_t v, int src) { return __shfl((
 __device__ __forceinline__ int bcast32(int v, int src) { return __shfl(v, src, 64); }
 __device__ __forceinline__ uint64_t below(int f) { return f >= 64 ? ~0ull : ((1ull << f) - 1ull); }
 
+// Loads / stores through a pointer known to address global memory: global_load / global_store, counted by vmcnt
+// alone — a flat access (what a generic pointer reached through a non-kernel function's arguments gets) also counts
+// in lgkmcnt, so every LDS / cross-lane wait after it would wait for it too.
+template <typename T>
+__device__ __forceinline__ T gload(const T* p) {
+    static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 32, "gload: 4-byte words, at most 32 bytes");
+    typedef unsigned int W __attribute__((ext_vector_type(sizeof(T) / 4)));
+    typedef const __attribute__((address_space(1))) W GW;
+    const W w = *(GW*)p;
+    T v;
+    __builtin_memcpy(&v, &w, sizeof(T));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ void gstore(T* p, const T& v) {
+    static_assert(sizeof(T) % 4 == 0 && sizeof(T) <= 32, "gstore: 4-byte words, at most 32 bytes");
+    typedef unsigned int W __attribute__((ext_vector_type(sizeof(T) / 4)));
+    typedef __attribute__((address_space(1))) W GW;
+    W w;
+    __builtin_memcpy(&w, &v, sizeof(T));
+    *(GW*)p = w;
+}
+
 __device__ __forceinline__ uint32_t period_of(const uint32_t* bnd, uint32_t np, uint32_t idx) {
     uint32_t lo = 0, hi = np;
     while (hi - lo > 1) {
@@ -101,7 +124,7 @@ __device__ __forceinline__ void lstore(const LArgs& a, uint32_t idx, int32_t st,
     sg_local_result r;
     r.status = st;
     r.wait_ms = wait;
-    a.out[idx] = r;
+    gstore(a.out + idx, r);
 }
 
 }  // namespace
@@ -1862,6 +1885,159 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 fc = gather(base + (uint64_t)lane, rec_c);
             }
         }
+        // ---- dead period, one QPS ParamFlowRule: chunks of entries decided from their side words (k_lcx_side), the
+        // next chunk's slot states read while this one is decided — a slot this chunk writes is then taken from its
+        // writer lane — until a chunk holds an exit, an entry past the period or one the lookup left to the serial step
+        if (dead && prule >= 0 && a.cxside) {
+            const uint64_t b0 = base;
+            const uint64_t td0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+            const uint32_t ri = (uint32_t)prule;
+            const int64_t dur = pr.duration_sec * 1000;
+            const uint64_t* const recs = a.rec_sorted;
+            const CxSide* const side = a.cxside;
+            PSlot* const tab = a.ps.p.table;
+            auto ld_rec = [&](uint64_t c) {
+                const uint64_t jj = c + (uint64_t)lane;
+                return jj < e_end ? gload(recs + jj) : 0ull;
+            };
+            auto ld_side = [&](uint64_t c) {
+                const uint64_t jj = c + (uint64_t)lane;
+                CxSide z;
+                z.t = 0;
+                z.psl = 0xFFFFFFFCu;  // no check
+                z.node = kNoNode;
+                if (jj < e_end) z = gload(side + jj);
+                return z;
+            };
+            struct Sv {  // a slot's value and state
+                uint64_t value;
+                PState st;
+            };
+            auto ld_state = [&](const CxSide& z) {
+                Sv v{0ull, {0, 0, 0u}};
+                if (z.psl < 0xFFFFFFFCu) {
+                    const PSlot sl = gload(tab + z.psl);
+                    v.value = sl.value;
+                    v.st.time = sl.time;
+                    v.st.tokens = sl.tokens;
+                    v.st.flags = sl.flags;
+                }
+                return v;
+            };
+            uint64_t r_c = ld_rec(base), r_n = ld_rec(base + 64);
+            CxSide s_c = ld_side(base), s_n = ld_side(base + 64);
+            Sv v_c = ld_state(s_c);
+            uint32_t w_g = 0xFFFFFFFFu;  // the slot this lane (its last request) wrote in the previous chunk
+            PState w_st{0, 0, 0u};
+            for (;;) {
+                const bool act = base + (uint64_t)lane < e_end;
+                LEvent e;
+                e.kind = SG_LOCAL_ENTRY;
+                e.count = 0;
+                e.idx = 0;
+                if (act) e = ldecode(a, r_c);
+                const bool okl = !act || (e.kind == SG_LOCAL_ENTRY && e.idx < dead_end && s_c.psl != 0xFFFFFFFFu);
+                if (__ballot(!okl)) break;
+                // two chunks ahead: records and side words; the next chunk: its slot states
+                const uint64_t r_n2 = ld_rec(base + 128);
+                const CxSide s_n2 = ld_side(base + 128);
+                const Sv v_n = ld_state(s_n);
+                // this chunk's states were read before the previous chunk's writes landed
+                uint64_t wm = __ballot(w_g != 0xFFFFFFFFu);
+                while (wm) {
+                    const int q = __builtin_ctzll(wm);
+                    wm &= wm - 1;
+                    const uint32_t g0 = (uint32_t)bcast32((int)w_g, q);
+                    const int64_t tm = bcast64(w_st.time, q), tk = bcast64(w_st.tokens, q);
+                    const uint32_t fl = (uint32_t)bcast32((int)w_st.flags, q);
+                    if (s_c.psl == g0) {
+                        v_c.st.time = tm;
+                        v_c.st.tokens = tk;
+                        v_c.st.flags = fl;
+                    }
+                }
+                const uint32_t psl = s_c.psl;
+                if (!inited && __ballot(act && psl != 0xFFFFFFFEu)) {  // initParamMetricsFor
+                    a.ps.inited[ri] = 1;
+                    inited = true;
+                }
+                const bool has = act && psl != 0xFFFFFFFEu && psl != 0xFFFFFFFCu;
+                const bool early = has && psl == 0xFFFFFFFDu;
+                const bool chain0 = has && !early;
+                const int64_t tc = !chain0 ? 0 : pr.hot_count ? param_token_count(a.ps.p, pr, v_c.value) : pr.token_count;
+                PState st = v_c.st;
+                const bool stuck = chain0 && pr.behavior != 2 && (st.flags & 3u) == 3u && s_c.t - st.time <= dur &&
+                                   st.tokens <= 0;
+                const bool chain = chain0 && !stuck;
+                int rank = 0, prev = lane;
+                uint64_t gm = 0;
+                uint64_t todo = __ballot(chain);
+                while (todo) {
+                    const int l0 = __builtin_ctzll(todo);
+                    const uint32_t g0 = (uint32_t)bcast32((int)psl, l0);
+                    const uint64_t m = __ballot(chain && psl == g0);
+                    todo &= ~m;
+                    if (chain && psl == g0) {
+                        gm = m;
+                        const uint64_t lo = m & below(lane);
+                        rank = (int)__popcll(lo);
+                        prev = lo ? 63 - __builtin_clzll(lo) : lane;
+                    }
+                }
+                int maxrank = chain ? rank : 0;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) maxrank = max(maxrank, __shfl_xor(maxrank, o, 64));
+                bool ok = !stuck;
+                for (int r = 0; r <= maxrank; ++r) {
+                    const int64_t ptm = __shfl((long long)st.time, prev, 64);
+                    const int64_t ptk = __shfl((long long)st.tokens, prev, 64);
+                    const uint32_t pfl = (uint32_t)__shfl((int)st.flags, prev, 64);
+                    if (chain && rank == r) {
+                        if (r > 0) {
+                            st.time = ptm;
+                            st.tokens = ptk;
+                            st.flags = pfl;
+                        }
+                        ok = pr.behavior == 2
+                                 ? param_throttle_step(st, throttle_cost(pr, tc, e.count), pr.max_queueing_ms, s_c.t)
+                                 : param_default_step(st, tc, tc + pr.burst, dur, s_c.t, e.count);
+                    }
+                }
+                w_g = 0xFFFFFFFFu;
+                if (chain && (gm & ~below(lane + 1)) == 0) {  // the slot's last request writes it back
+                    PSlot* const sl = tab + psl;
+                    gstore(&sl->time, st.time);
+                    gstore(&sl->tokens, st.tokens);
+                    gstore(&sl->flags, st.flags);
+                    w_g = psl;
+                    w_st = st;
+                }
+                if (has && (early || !ok)) lstore(a, e.idx, SG_LOCAL_BLOCK_PARAM, prule);
+                // BLOCK counts of the ClusterNode and the origin nodes (added when the period ends)
+                if (act) dblk += e.count;
+                const bool on = act && s_c.node != kNoNode;
+                const bool ovf = on && !lane_add(s_c.node, e.count);
+                if (__ballot(ovf)) {
+                    merge_lanes();
+                    if (ovf) lane_add(s_c.node, e.count);
+                }
+                if (dg) ++c_dead;
+                base += 64;
+                if (base >= e_end) break;
+                r_c = r_n;
+                r_n = r_n2;
+                s_c = s_n;
+                s_n = s_n2;
+                v_c = v_n;
+            }
+            if (dg) t_dead += __builtin_amdgcn_s_memrealtime() - td0;
+            if (base != b0) {
+                if (base >= e_end) return false;
+                rec_c = a.rec_sorted[base + (uint64_t)lane < e_end ? base + lane : base];
+                rec_n = base + 64 + (uint64_t)lane < e_end ? a.rec_sorted[base + 64 + lane] : 0;
+                fc = gather(base + (uint64_t)lane, rec_c);
+            }
+        }
         const uint64_t j = base + (uint64_t)lane;
         const bool act = j < e_end;
         fn = gather(j + 64, rec_n);
@@ -2140,6 +2316,23 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 o[7] = (unsigned long long)(int64_t)prule;
             }
         }
+    }
+}
+
+// The cx wave walker's dead-period words of every sorted record of a resource with ParamFlowSlot rules (CxSide), so
+// that a dead chunk reads them contiguously rather than through three gathers per entry.
+__global__ void __launch_bounds__(256) k_lcx_side(LArgs a) {
+    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = a.rec_sorted[p];
+        const uint32_t k = (uint32_t)(r >> a.kshift);
+        if (k >= a.K || !a.rules[k].ps) continue;
+        const LEvent e = ldecode(a, r);
+        CxSide z;
+        z.t = a.ev[e.idx].ts_ms;
+        const uint64_t ps = e.kind == SG_LOCAL_ENTRY ? a.pslot[e.idx] : kPsUnknown;
+        z.psl = (ps >= kPsNoCheckInit || ps < 0xFFFFFFFCull) ? (uint32_t)ps : 0xFFFFFFFFu;  // a slot that looks like a code
+        z.node = event_nodes(a, e.idx).x;
+        a.cxside[p] = z;
     }
 }
 
@@ -2448,6 +2641,7 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     // the hot cx segments' waves first (the batch's longest serial chains), the lane walker of the other cx
     // segments beside them after the plain wave walker
     if (has_cx && a.cxw) {
+        if (a.cxside) hipLaunchKernelGGL(k_lcx_side, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
         static unsigned bw = 0;
         if (bw == 0) bw = lresident((const void*)k_lwalk_cxw);
         hipLaunchKernelGGL(k_lwalk_cxw, dim3(bw), dim3(256), 0, stream, a, sg);
