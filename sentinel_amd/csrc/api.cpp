@@ -273,6 +273,7 @@ struct sg_handle {
     bool short_max_env = false;
     int dbg = 0;                      // env SG_DEBUG: see BatchArgs::dbg
     int l_cxw = 1;                    // env SG_CXW=0: long cx segments on the lane walker too (LArgs::cxw)
+    uint32_t l_cxw_min = 0xFFFFFFFFu;          // env SG_CXW_MIN: shortest cx segment class the wave walker takes (LArgs::cxw_cls)
     bool wide_seen = false;           // some loaded rule allowed bucket counts >= 2^30 (sticky: the ring keeps them)
     hipEvent_t ev[5]{};
     sg_batch_stats stats{};
@@ -541,6 +542,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
         return bail(SG_E_DEVICE);
     if (const char* d = std::getenv("SG_DEBUG")) h->dbg = std::atoi(d);
     if (const char* d = std::getenv("SG_CXW")) h->l_cxw = std::atoi(d) != 0 ? 1 : 0;
+    if (const char* d = std::getenv("SG_CXW_MIN")) h->l_cxw_min = (uint32_t)std::strtoul(d, nullptr, 10);
     if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
@@ -3242,6 +3244,10 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
     L.ev = ev;
     L.out = out;
     L.cxw = h->l_cxw;
+    // the short classes whose segments all have >= l_cxw_min records: one lane walking a few hundred records event by
+    // event outlasts a wave that decides their dead periods 64 at a time
+    L.cxw_cls = kClasses;
+    for (int c = kClasses - 1; c >= 0 && (c == 0 ? 1u : kClassMax[c - 1] + 1u) >= h->l_cxw_min; --c) L.cxw_cls = c;
     L.n = n;
     L.rec = b.rec;
     L.rec_sorted = b.rec_sorted;

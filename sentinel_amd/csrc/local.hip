@@ -1581,9 +1581,10 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
             if (a.cxw && !a.rules[(uint32_t)(a.rec_sorted[j] >> a.kshift)].grp) continue;  // k_lwalk_cxw
         } else {
             r -= *sg.long_count;
-            int c = 0;
-            while (r >= sg.short_count[c]) r -= sg.short_count[c++];
+            int c = kClasses - 1;  // longest class first: the lanes with the longest chains start first
+            while (r >= sg.short_count[c]) r -= sg.short_count[c--];
             j = sg.short_list[sg.class_off[c] + r];
+            if (a.cxw && c >= a.cxw_cls && !a.rules[(uint32_t)(a.rec_sorted[j] >> a.kshift)].grp) continue;
         }
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
         if (!a.rules[k].cx && !(a.dyn && a.dyn[k] == a.epoch)) continue;
@@ -2343,14 +2344,26 @@ __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, Bat
     stage_lperiods(a, sbnd, bndp);
     const int lane = lane_id();
     const uint32_t n_long = *sg.long_count;
+    uint32_t total = n_long;  // the long list, then the short classes >= cxw_cls (longest first)
+    for (int c = a.cxw_cls; c < kClasses; ++c) total += sg.short_count[c];
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t item = wave; item < n_long; item += nwaves) {
-        const uint64_t s = sg.long_list[item];
+    for (uint32_t item = wave; item < total; item += nwaves) {
+        uint64_t s, lo;
+        if (item < n_long) {
+            s = sg.long_list[item];
+            lo = sg.short_max ? sg.short_max : 1;
+        } else {
+            uint32_t r = item - n_long;
+            int c = kClasses - 1;
+            while (r >= sg.short_count[c]) r -= sg.short_count[c--];
+            s = sg.short_list[sg.class_off[c] + r];
+            lo = c == 0 ? 1 : kClassMax[c - 1];
+        }
         const uint32_t k = (uint32_t)(a.rec_sorted[s] >> a.kshift);
         const LRule& R = a.rules[k];
-        if (!(R.cx || (a.dyn && a.dyn[k] == a.epoch)) || R.grp) continue;  // k_lwalk_long / k_lwalk_cx
-        const uint64_t e = gallop_search(s + (sg.short_max ? sg.short_max : 1), a.n, [&](uint64_t p) {
+        if (!(R.cx || (a.dyn && a.dyn[k] == a.epoch)) || R.grp) continue;  // k_lwalk_long / k_lwalk_short / k_lwalk_cx
+        const uint64_t e = gallop_search(s + lo, a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
         cx_wave(a, sg, bndp, k, s, e);
