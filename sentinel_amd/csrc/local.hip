@@ -1566,6 +1566,9 @@ __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, 
 // One lane per segment of a cx resource (or a RELATE key group), from every length class of k_seg's lists. A lone
 // resource keeps its ClusterNode in registers for the whole segment; a group's events belong to several resources
 // (one reads another's ClusterNode), so each event opens its resource's node from memory and writes it back.
+__device__ bool cxw_dead_able(const LArgs& a, const LRule& R, uint32_t k, int32_t* prule);
+__device__ bool cxw_saturated(const LArgs& a, const LNode& nd);
+
 __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
@@ -1609,18 +1612,119 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
         }
         LNode nd(a, bndp, k);
         nd.created = 1;
+        // Dead periods as in the wave walker (cx_wave), one lane at a time: once a QPS rule every entry reaches is
+        // saturated, the period's further entries need only their ParamFlowSlot check and BLOCK counts (ClusterNode
+        // and origin node, added when the period ends), not the whole chain.
+        int32_t prule = -1;
+        const bool dead_ok =
+            a.cxw && !(*a.flags & (kLFlagPrio | kLFlagNonPos)) && cxw_dead_able(a, nd.R, k, &prule);
+        PRule pr{};
+        if (prule >= 0) pr = a.ps.p.rules[prule];
+        bool dead = false, inited = false;
+        uint32_t dqs = 0, dqm = 0, dend = 0;
+        int64_t dblk = 0;
+        uint32_t onode[2] = {kNoNode, kNoNode};
+        int64_t osum[2] = {0, 0};
+        auto flush_origins = [&]() {
+            for (int q = 0; q < 2; ++q) {
+                if (onode[q] == kNoNode) continue;
+                LNode on(a, bndp, onode[q]);
+                on.at(dqs, dqm);
+                on.sc[kLBlock] += osum[q];
+                on.mc[kLBlock] += osum[q];
+                on.finish();
+                onode[q] = kNoNode;
+                osum[q] = 0;
+            }
+        };
         for (uint64_t p = j; p < a.n; ++p) {
             const uint64_t rec = a.rec_sorted[p];
             if ((uint32_t)(rec >> a.kshift) != k) break;
             const LEvent e = ldecode(a, rec);
+            if (dead && e.idx >= dend) {  // the dead period ended
+                nd.at(dqs, dqm);
+                nd.sc[kLBlock] += dblk;
+                nd.mc[kLBlock] += dblk;
+                dblk = 0;
+                flush_origins();
+                dead = false;
+            }
+            if (dead && e.kind == SG_LOCAL_ENTRY) {
+                uint64_t psl = kPsNoCheck;
+                int64_t t = 0;
+                uint32_t node;
+                if (prule >= 0 && a.cxside) {
+                    const CxSide z = a.cxside[p];
+                    t = z.t;
+                    psl = z.psl >= 0xFFFFFFFCu ? ~0ull - (uint64_t)(0xFFFFFFFFu - z.psl) : (uint64_t)z.psl;
+                    node = z.node;
+                } else {
+                    node = event_nodes(a, e.idx).x;
+                    if (prule >= 0) {
+                        psl = a.pslot ? a.pslot[e.idx] : kPsUnknown;
+                        t = a.ev[e.idx].ts_ms;
+                    }
+                }
+                if (psl != kPsUnknown) {
+                    bool pfail = false;
+                    if (prule >= 0 && psl != kPsNoCheck) {
+                        if (!inited) {  // initParamMetricsFor
+                            a.ps.inited[prule] = 1;
+                            inited = true;
+                        }
+                        if (psl == kPsEarlyFail) {
+                            pfail = true;
+                        } else if (psl != kPsNoCheckInit) {
+                            PSlot& sl = a.ps.p.table[psl];
+                            const int64_t tc = pr.hot_count ? param_token_count(a.ps.p, pr, sl.value) : pr.token_count;
+                            PState st{sl.time, sl.tokens, sl.flags};
+                            const bool ok =
+                                pr.behavior == 2
+                                    ? param_throttle_step(st, throttle_cost(pr, tc, e.count), pr.max_queueing_ms, t)
+                                    : param_default_step(st, tc, tc + pr.burst, pr.duration_sec * 1000, t, e.count);
+                            sl.time = st.time;
+                            sl.tokens = st.tokens;
+                            sl.flags = st.flags;
+                            pfail = !ok;
+                        }
+                    }
+                    if (pfail) lstore(a, e.idx, SG_LOCAL_BLOCK_PARAM, prule);  // (FLOW: the default result)
+                    dblk += e.count;
+                    if (node != kNoNode) {
+                        int q = onode[0] == node ? 0 : onode[1] == node ? 1 : onode[0] == kNoNode ? 0 : onode[1] == kNoNode ? 1 : -1;
+                        if (q < 0) {
+                            flush_origins();
+                            q = 0;
+                        }
+                        onode[q] = node;
+                        osum[q] += e.count;
+                    }
+                    continue;
+                }
+            }
             const sg_local_event le = a.ev[e.idx];
             const sg_slot_ext* x = a.ext ? a.ext + e.idx : nullptr;
             const int ctx = x ? (int)x->context : 0;
             const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
             if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);
             const uint2 nodes = event_nodes(a, e.idx);
-            if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
-            else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
+            if (e.kind == SG_LOCAL_ENTRY) {
+                cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
+                if (dead_ok && !dead && nd.cs.q == qs && nd.cm.q == qm && cxw_saturated(a, nd)) {
+                    dead = true;
+                    dqs = qs;
+                    dqm = qm;
+                    dend = min(nd.cs.next_b, nd.cm.next_b);
+                }
+            } else {
+                cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
+            }
+        }
+        if (dead) {
+            nd.at(dqs, dqm);
+            nd.sc[kLBlock] += dblk;
+            nd.mc[kLBlock] += dblk;
+            flush_origins();
         }
         nd.finish();
     }
