@@ -392,6 +392,23 @@ struct LNode {
     int64_t created;   // LHead.created (set by the walkers for a resource with events: ClusterBuilderSlot)
     LBreaker cb[2];
 
+    // a node the event does not touch (no origin / context node): nothing loaded, never opened or finished
+    struct None {};
+    __device__ LNode(const LArgs& a_, None) : a(a_), k(0) {
+        R = LRule{};
+        sec = nullptr;
+        bor = nullptr;
+        mnt = nullptr;
+        cs = cm = Cursor{nullptr, 0, 0xFFFFFFFFu, 0};
+        P0s = P0m = 0;
+        sI = mI = -1;
+        s_ws = m_ws = s_wo = 0;
+        s_min = m_min = kStatMaxRt;
+        for (int e = 0; e < kLEv; ++e) sc[e] = mc[e] = 0;
+        threads = created = 0;
+        cb[0] = cb[1] = LBreaker{};
+    }
+
     __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), k(k_) {
         if (k_ < a.K) {
             R = a.rules[k_];
@@ -1419,13 +1436,35 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
     const LRule& R = nd.R;
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
-    LNode on(a, bndp, have_on ? on_idx : nd.k);  // windows opened as touched (cx_rule, the StatisticSlot adds)
-    LNode cn(a, bndp, have_cn ? cn_idx : nd.k);
+    // windows opened as touched (cx_rule, the StatisticSlot adds); an absent node loads nothing
+    LNode on = have_on ? LNode(a, bndp, on_idx) : LNode(a, LNode::None{});
+    LNode cn = have_cn ? LNode(a, bndp, cn_idx) : LNode(a, LNode::None{});
     const bool params = R.ps && a.has_ps && x && !x->args_null;
     int32_t status = SG_LOCAL_PASS;
     int64_t wait = 0;
     if (params) {  // ParamFlowSlot (@Spi order -3000): before FlowSlot
-        const int32_t pr = ps_check_entry(a.ps, nd.k, t, e.count, x->arg_begin, x->arg_count);
+        // the resource's one QPS rule, its (rule, value) slot looked up by k_local_prep (LArgs::pslot), else every rule
+        const uint64_t psl = a.pslot ? a.pslot[e.idx] : kPsUnknown;
+        int32_t pr = -1;
+        if (psl != kPsUnknown) {
+            const uint32_t ri = a.ps.res_rules[a.ps.res_begin[nd.k]];
+            a.ps.inited[ri] = 1;  // initParamMetricsFor (the arguments are not null here)
+            bool ok = psl != kPsEarlyFail;
+            if (ok && psl != kPsNoCheckInit && psl != kPsNoCheck) {
+                const PRule r = a.ps.p.rules[ri];
+                PSlot& sl = a.ps.p.table[psl];
+                const int64_t tc = r.hot_count ? param_token_count(a.ps.p, r, sl.value) : r.token_count;
+                PState st{sl.time, sl.tokens, sl.flags};
+                ok = r.behavior == 2 ? param_throttle_step(st, throttle_cost(r, tc, e.count), r.max_queueing_ms, t)
+                                     : param_default_step(st, tc, tc + r.burst, r.duration_sec * 1000, t, e.count);
+                sl.time = st.time;
+                sl.tokens = st.tokens;
+                sl.flags = st.flags;
+            }
+            if (!ok) pr = (int32_t)ri;
+        } else {
+            pr = ps_check_entry(a.ps, nd.k, t, e.count, x->arg_begin, x->arg_count);
+        }
         if (pr >= 0) {
             status = SG_LOCAL_BLOCK_PARAM;
             wait = pr;  // reported in wait_ms: the rule that threw ParamFlowException
