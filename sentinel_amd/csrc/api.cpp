@@ -179,6 +179,8 @@ struct sg_handle {
         uint32_t* skip_count = nullptr;
         uint64_t* pslot = nullptr;    // [max_batch] LArgs::pslot (param rules loaded and the cx wave walker on)
         CxSide* cxside = nullptr;     // [max_batch] LArgs::cxside (with pslot)
+        uint32_t* cxw_next = nullptr; // LArgs::cxw_next
+        uint32_t* cx_list = nullptr;  // [max_batch + 1] LArgs::cx_list, then cx_count (cx resources loaded)
     };
     LocalWs lws[2];
     uint32_t lskip_cap = 0;
@@ -714,6 +716,8 @@ void sg_destroy(sg_handle* h) {
         dfree(w.pslot);
         dfree(w.cxside);
         dfree(w.flags);
+        dfree(w.cxw_next);
+        dfree(w.cx_list);
         dfree(w.exit_pos);
         dfree(w.exit_cnt);
         dfree(w.skips);
@@ -3223,7 +3227,8 @@ int local_bufs(sg_handle* h, int x, LocalBufs& b) {
             hipMalloc(&lw.exit_pos, sizeof(uint32_t) * (mb + 1)) != hipSuccess ||
             hipMalloc(&lw.exit_cnt, sizeof(uint32_t) * (mb / kLTile + 2)) != hipSuccess ||
             hipMalloc(&lw.skips, sizeof(LSkip) * h->lskip_cap) != hipSuccess ||
-            hipMalloc(&lw.skip_count, sizeof(uint32_t)) != hipSuccess)
+            hipMalloc(&lw.skip_count, sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&lw.cxw_next, sizeof(uint32_t)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "local batch workspace");
     }
     return SG_OK;
@@ -3315,6 +3320,13 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
         L.c3_last_ts = h->d_last_ts;
     }
     L.flags = b.lw->flags;
+    L.cxw_next = b.lw->cxw_next;
+    if (h->l_has_cx || h->l_has_cx_ps || h->l_n_contexts > 0) {
+        if (!b.lw->cx_list && hipMalloc(&b.lw->cx_list, sizeof(uint32_t) * (h->cfg.max_batch + 1)) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "cx segment list of the local batch");
+        L.cx_list = b.lw->cx_list;
+        L.cx_count = b.lw->cx_list + h->cfg.max_batch;
+    }
     L.exit_pos = b.lw->exit_pos;
     L.exit_cnt = b.lw->exit_cnt;
     L.skips = b.lw->skips;

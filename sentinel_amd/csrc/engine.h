@@ -682,6 +682,9 @@ struct LArgs {
     int32_t track_ctx;        // 1: every event updates its context's DefaultNode (n_contexts >= 1)
     int32_t cxw;              // 1: long cx segments (not RELATE groups) go to the wave walker k_lwalk_cxw
     int32_t cxw_cls;          // ... and so do those of the short length classes >= cxw_cls (kClasses: none)
+    uint32_t* cxw_next;       // the wave walker's next work item (zeroed before it starts; waves take items in turn)
+    uint32_t* cx_list;        // [n] or null: the lane cx walker's segment heads (k_lcx_list), cx_count of them
+    uint32_t* cx_count;
     uint64_t* pslot;          // [n] or null: k_local_prep's ParamFlowSlot lookup of each entry of a resource with one
                               // QPS param rule (kPsNoCheck / kPsEarlyFail / kPsUnknown, else the (rule, value) slot)
     CxSide* cxside;           // [n] or null (with pslot): k_lcx_side's words of the sorted records of param cx resources

@@ -1608,28 +1608,68 @@ __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, 
 __device__ bool cxw_dead_able(const LArgs& a, const LRule& R, uint32_t k, int32_t* prule);
 __device__ bool cxw_saturated(const LArgs& a, const LNode& nd);
 
+// Work items of the lane cx walker: k_seg's long list, then its length classes longest first (the lanes with the
+// longest chains start first).
+__device__ __forceinline__ uint32_t cx_items(const BatchArgs& sg) {
+    uint32_t total = *sg.long_count;
+    for (int c = 0; c < kClasses; ++c) total += sg.short_count[c];
+    return total;
+}
+
+// Item i: the head of a segment the lane cx walker takes (a cx or origin-event resource the wave walker leaves; a
+// RELATE group), else ~0.
+__device__ __forceinline__ uint64_t cx_item(const LArgs& a, const BatchArgs& sg, uint32_t i) {
+    uint32_t r = i;
+    uint64_t j;
+    bool wave = false;  // the wave walker's (k_lwalk_cxw), unless a RELATE group
+    if (r < *sg.long_count) {
+        j = sg.long_list[r];
+        wave = a.cxw != 0;
+    } else {
+        r -= *sg.long_count;
+        int c = kClasses - 1;
+        while (r >= sg.short_count[c]) r -= sg.short_count[c--];
+        j = sg.short_list[sg.class_off[c] + r];
+        wave = a.cxw != 0 && c >= a.cxw_cls;
+    }
+    const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
+    const LRule& R = a.rules[k];
+    const bool dyn = a.dyn && a.dyn[k] == a.epoch;
+    const bool take = (R.cx || dyn) && !(wave && !R.grp);
+    return take ? j : ~0ull;
+}
+
+// The lane cx walker's segments, compacted in item order (wave-aggregated appends): a cx resource is ~10 % of the
+// batch's segments, so walking k_seg's lists directly left ~9 of every 10 lanes of its waves idle.
+__global__ void __launch_bounds__(256) k_lcx_list(LArgs a, BatchArgs sg) {
+    if (*a.err) return;
+    const uint32_t total = cx_items(sg);
+    const int lane = lane_id();
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < total; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + (uint32_t)lane;
+        const uint64_t j = i < total ? cx_item(a, sg, i) : ~0ull;
+        const bool take = j != ~0ull;
+        const uint64_t m = __ballot(take);
+        if (!m) continue;
+        uint32_t at = 0;
+        if (lane == 0) at = atomicAdd(a.cx_count, (uint32_t)__popcll(m));
+        at = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
+        if (take) a.cx_list[at + (uint32_t)__popcll(m & below(lane))] = (uint32_t)j;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
     if (*a.err) return;
     stage_lperiods(a, sbnd, bndp);
-    uint32_t total = *sg.long_count;
-    for (int c = 0; c < kClasses; ++c) total += sg.short_count[c];
+    // the segments k_lcx_list compacted (64 of them per wave), else every segment of k_seg's lists
+    const bool listed = a.cx_list != nullptr;
+    const uint32_t total = listed ? *a.cx_count : cx_items(sg);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-        uint32_t r = i;
-        uint64_t j;
-        if (r < *sg.long_count) {
-            j = sg.long_list[r];
-            if (a.cxw && !a.rules[(uint32_t)(a.rec_sorted[j] >> a.kshift)].grp) continue;  // k_lwalk_cxw
-        } else {
-            r -= *sg.long_count;
-            int c = kClasses - 1;  // longest class first: the lanes with the longest chains start first
-            while (r >= sg.short_count[c]) r -= sg.short_count[c--];
-            j = sg.short_list[sg.class_off[c] + r];
-            if (a.cxw && c >= a.cxw_cls && !a.rules[(uint32_t)(a.rec_sorted[j] >> a.kshift)].grp) continue;
-        }
+        const uint64_t j = listed ? (uint64_t)a.cx_list[i] : cx_item(a, sg, i);
+        if (j == ~0ull) continue;
         const uint32_t k = (uint32_t)(a.rec_sorted[j] >> a.kshift);
-        if (!a.rules[k].cx && !(a.dyn && a.dyn[k] == a.epoch)) continue;
         if (a.rules[k].grp) {
             for (uint64_t p = j; p < a.n; ++p) {
                 const uint64_t rec = a.rec_sorted[p];
@@ -2489,9 +2529,12 @@ __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, Bat
     const uint32_t n_long = *sg.long_count;
     uint32_t total = n_long;  // the long list, then the short classes >= cxw_cls (longest first)
     for (int c = a.cxw_cls; c < kClasses; ++c) total += sg.short_count[c];
-    const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
-    for (uint32_t item = wave; item < total; item += nwaves) {
+    // a wave takes the next item when it is free: the waves that start on the longest segments take no more
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(a.cxw_next, 1u);
+        item = (uint32_t)__builtin_amdgcn_readfirstlane((int)item);
+        if (item >= total) break;
         uint64_t s, lo;
         if (item < n_long) {
             s = sg.long_list[item];
@@ -2800,10 +2843,19 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
         if (a.cxside) hipLaunchKernelGGL(k_lcx_side, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
         static unsigned bw = 0;
         if (bw == 0) bw = lresident((const void*)k_lwalk_cxw);
+        e = hipMemsetAsync(a.cxw_next, 0, sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_lwalk_cxw, dim3(bw), dim3(256), 0, stream, a, sg);
     }
     hipLaunchKernelGGL(k_lwalk_long, dim3(bl), dim3(256), 0, aux, a, sg);
-    if (has_cx) hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, aux, a, sg);
+    if (has_cx) {
+        if (a.cx_list) {
+            e = hipMemsetAsync(a.cx_count, 0, sizeof(uint32_t), aux);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_lcx_list, dim3(lgrid(a.n, 256, 4096)), dim3(256), 0, aux, a, sg);
+        }
+        hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, aux, a, sg);
+    }
     hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
     e = hipEventRecord(join, aux);
     if (e == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
