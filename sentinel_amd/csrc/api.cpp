@@ -3298,11 +3298,9 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
         const int prc = pslot_embed(h, L.ps, 0);  // cluster-mode param rules on the embedded token server
         if (prc) return prc;
         if (h->l_cxw) {
-            if (!b.lw->pslot && (hipMalloc(&b.lw->pslot, sizeof(uint64_t) * h->cfg.max_batch) != hipSuccess ||
-                                 hipMalloc(&b.lw->cxside, sizeof(CxSide) * h->cfg.max_batch) != hipSuccess))
+            if (!b.lw->pslot && hipMalloc(&b.lw->pslot, sizeof(uint64_t) * h->cfg.max_batch) != hipSuccess)
                 return fail(h, SG_E_NOMEM, "param lookups of the local batch");
             L.pslot = b.lw->pslot;
-            L.cxside = b.lw->cxside;
         }
     }
     if (emb) {  // the embedded token server: this handle's cluster flow state
@@ -3321,6 +3319,11 @@ int local_args(sg_handle* h, const LocalBufs& b, const sg_local_event* ev, const
     }
     L.flags = b.lw->flags;
     L.cxw_next = b.lw->cxw_next;
+    if (h->l_cxw && (h->l_has_cx || h->l_has_cx_ps)) {  // the cx wave walker's sorted-order side words
+        if (!b.lw->cxside && hipMalloc(&b.lw->cxside, sizeof(CxSide) * h->cfg.max_batch) != hipSuccess)
+            return fail(h, SG_E_NOMEM, "side words of the local batch");
+        L.cxside = b.lw->cxside;
+    }
     if (h->l_has_cx || h->l_has_cx_ps || h->l_n_contexts > 0) {
         if (!b.lw->cx_list && hipMalloc(&b.lw->cx_list, sizeof(uint32_t) * (h->cfg.max_batch + 1)) != hipSuccess)
             return fail(h, SG_E_NOMEM, "cx segment list of the local batch");

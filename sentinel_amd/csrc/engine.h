@@ -687,7 +687,7 @@ struct LArgs {
     uint32_t* cx_count;
     uint64_t* pslot;          // [n] or null: k_local_prep's ParamFlowSlot lookup of each entry of a resource with one
                               // QPS param rule (kPsNoCheck / kPsEarlyFail / kPsUnknown, else the (rule, value) slot)
-    CxSide* cxside;           // [n] or null (with pslot): k_lcx_side's words of the sorted records of param cx resources
+    CxSide* cxside;           // [n] or null: k_lcx_side's words of the sorted records of the cx resources
     // the embedded token server (ClusterStateManager SERVER, emb = 1): the handle's cluster flow state
     int32_t emb;
     const Rule* c3_rules;

@@ -1732,11 +1732,13 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
                 uint64_t psl = kPsNoCheck;
                 int64_t t = 0;
                 uint32_t node;
-                if (prule >= 0 && a.cxside) {
+                if (a.cxside) {
                     const CxSide z = a.cxside[p];
-                    t = z.t;
-                    psl = z.psl >= 0xFFFFFFFCu ? ~0ull - (uint64_t)(0xFFFFFFFFu - z.psl) : (uint64_t)z.psl;
                     node = z.node;
+                    if (prule >= 0) {
+                        t = z.t;
+                        psl = z.psl >= 0xFFFFFFFCu ? ~0ull - (uint64_t)(0xFFFFFFFFu - z.psl) : (uint64_t)z.psl;
+                    }
                 } else {
                     node = event_nodes(a, e.idx).x;
                     if (prule >= 0) {
@@ -2026,11 +2028,17 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
             const uint64_t b0 = base;
             for (;;) {
                 uint64_t r[4];
+                uint32_t sn[4];  // the entries' origin nodes from the side words (read beside the records)
                 r[0] = base + (uint64_t)lane < e_end ? a.rec_sorted[base + lane] : 0;
 #pragma unroll
                 for (int u = 1; u < 4; ++u) {
                     const uint64_t jj = base + (uint64_t)(u * 64 + lane);
                     r[u] = jj < e_end ? a.rec_sorted[jj] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint64_t jj = base + (uint64_t)(u * 64 + lane);
+                    sn[u] = (a.cxside && jj < e_end) ? a.cxside[jj].node : kNoNode;
                 }
                 bool ok = true;
                 LEvent eu[4];
@@ -2048,7 +2056,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 }
                 if (__ballot(!ok) || base + 256 > e_end) break;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) nu[u] = event_nodes(a, eu[u].idx);
+                for (int u = 0; u < 4; ++u) nu[u] = a.cxside ? make_uint2(sn[u], kNoNode) : event_nodes(a, eu[u].idx);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     dblk += eu[u].count;
@@ -2503,17 +2511,17 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
     }
 }
 
-// The cx wave walker's dead-period words of every sorted record of a resource with ParamFlowSlot rules (CxSide), so
-// that a dead chunk reads them contiguously rather than through three gathers per entry.
+// The cx walkers' dead-period words of every sorted record of a cx resource (CxSide), so that a dead chunk reads them
+// contiguously rather than through a gather per word and entry.
 __global__ void __launch_bounds__(256) k_lcx_side(LArgs a) {
     for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.n; p += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = a.rec_sorted[p];
         const uint32_t k = (uint32_t)(r >> a.kshift);
-        if (k >= a.K || !a.rules[k].ps) continue;
+        if (k >= a.K || !(a.rules[k].cx || (a.dyn && a.dyn[k] == a.epoch))) continue;
         const LEvent e = ldecode(a, r);
         CxSide z;
         z.t = a.ev[e.idx].ts_ms;
-        const uint64_t ps = e.kind == SG_LOCAL_ENTRY ? a.pslot[e.idx] : kPsUnknown;
+        const uint64_t ps = (a.pslot && e.kind == SG_LOCAL_ENTRY) ? a.pslot[e.idx] : kPsUnknown;
         z.psl = (ps >= kPsNoCheckInit || ps < 0xFFFFFFFCull) ? (uint32_t)ps : 0xFFFFFFFFu;  // a slot that looks like a code
         z.node = event_nodes(a, e.idx).x;
         a.cxside[p] = z;
