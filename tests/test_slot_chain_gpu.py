@@ -249,6 +249,39 @@ def test_hot_resources_with_params():
     _run(ora, ps, eng, fr, params, n_res, 2, 2, [(60_000, 3000), (60_000, 3000)], 11, zipf=1.5)
 
 
+@pytest.mark.parametrize("env", [{}, {"SG_CXW_MIN": "17"}, {"SG_CXW": "0"}], ids=["default", "cxw17", "lanes"])
+@pytest.mark.parametrize("flags", [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY])
+def test_dead_periods(flags, env, monkeypatch):
+    """Hot cx resources whose window periods saturate, with no prioritized entry and no context tracking: the cx
+    walkers' dead periods (the wave walker's chunks, the lane walker's per-entry path) decide the rest of each period —
+    origin-limitApp, "other", lone WarmUp and one-QPS-param-rule resources (token buckets and a throttle over Zipf
+    values, null and collection arguments among them), with the wave walker on the short classes too (SG_CXW_MIN=17)
+    or off (SG_CXW=0)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("SG_DEBUG", "64")  # the wave walker's counters (local.hip cx_wave; results unchanged)
+    rng = np.random.default_rng(21)
+    n_res, n_origins = 12, 3
+    sets = [[local_flow_rule(0, 30.0), local_flow_rule(0, 6.0, limit_app=1)],
+            [local_flow_rule(1, 25.0, behavior=WU, warm_up_sec=3)],
+            [local_flow_rule(2, 40.0)],
+            [local_flow_rule(3, 20.0), local_flow_rule(3, 4.0, limit_app=OTHER)],
+            [local_flow_rule(4, 15.0)],
+            [local_flow_rule(5, 12.0, behavior=WU, warm_up_sec=2)],
+            [local_flow_rule(6, 50.0)],
+            [local_flow_rule(7, 8.0), local_flow_rule(7, 2.0, limit_app=2)],
+            [local_flow_rule(8, 5.0)], [local_flow_rule(9, 60.0)], [], [local_flow_rule(11, 3.0)]]
+    params = np.array([prule(res=2, idx=0, count=8.0), prule(res=4, idx=0, count=3.0, dur=2),
+                       prule(res=6, idx=0, count=20.0, behavior=abi.BEHAVIOR_RATE_LIMITER, max_q=50),
+                       prule(res=9, idx=1, count=5.0), prule(res=10, idx=0, count=4.0)], abi.PSLOT_RULE_DTYPE)
+    ora, ps, eng, fr, params = _setup(rng, n_res, n_origins, 0, flags=flags, rule_sets=sets, params=params)
+    _run(ora, ps, eng, fr, params, n_res, n_origins, 0, [(60_000, 3000), (60_000, 2500), (30_000, 4000)], 21,
+         zipf=1.2, prio=0.0)
+    if flags != abi.FLAG_SERIAL_ONLY and env.get("SG_CXW") != "0":  # the wave walker decided dead chunks
+        d = eng.debug_copy(5, np.uint64, 32)
+        assert d[20] > 0 and d[23] > 0, f"wave walker segments {d[20]}, dead chunks {d[23]}"
+
+
 def test_relate_to_a_resource_never_entered():
     """RELATE to a resource with no entry yet: no ClusterNode, the rule passes (even at count 0); once that
     resource is entered, its ClusterNode is read."""
