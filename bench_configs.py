@@ -335,6 +335,8 @@ def slot(args, dev):
                   d[20] / nb, d[21] / nb / 1e5, d[22] / 1e5, d[23] / nb, d[24] / nb, d[25] / nb, d[26] / nb,
                   d[27] / nb / 1e5, d[28] / nb / 1e5), file=sys.stderr, flush=True)
         print("# cxw dead-chunk head ms per batch: %.2f" % (d[17] / nb / 1e5), file=sys.stderr, flush=True)
+        print("# cxw param dead loop phases ms per batch: prefetch+fixup %.2f, chains %.2f, stores %.2f" % (
+            d[12] / nb / 1e5, d[13] / nb / 1e5, d[14] / nb / 1e5), file=sys.stderr, flush=True)
         print("# cxw segments over 5 ms per batch: %.1f; their serial steps %.0f (%.2f ms), dead chunks %.0f" % (
             d[19] / nb, d[29] / nb, d[30] / nb / 1e5, d[31] / nb), file=sys.stderr, flush=True)
         for sl in range(min(12, int(d[18]))):

@@ -52,8 +52,13 @@ __device__ __forceinline__ int64_t wave_incl_scan(int64_t v, int lane) {
     return v;
 }
 
-__device__ __forceinline__ int64_t bcast64(int64_t v, int src) { return __shfl((long long)v, src, 64); }
-__device__ __forceinline__ int bcast32(int v, int src) { return __shfl(v, src, 64); }
+// v of lane src (wave-uniform src): v_readlane, not an LDS permute round trip
+__device__ __forceinline__ int bcast32(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ int64_t bcast64(int64_t v, int src) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ uint64_t below(int f) { return f >= 64 ? ~0ull : ((1ull << f) - 1ull); }
 
 // Loads / stores through a pointer known to address global memory: global_load / global_store, counted by vmcnt
@@ -1897,10 +1902,13 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                         uint64_t e_end) {
     const int lane = lane_id();
     // SG_DEBUG & 64: counters into sg.dbg_ctr[20..]: segments, wave ticks (sum, max), dead / general chunks, serial
-    // entry / exit steps, ticks in dead chunks, in serial steps (s_memrealtime, 100 MHz)
+    // entry / exit steps, ticks in dead chunks, in serial steps (s_memrealtime, 100 MHz); [12..14] the param dead
+    // loop's phases (decode + prefetch + fix-up, token chains, stores); [17] dead-chunk heads; [18..19], [29..] and
+    // [32..127] the segments over 5 ms
     const bool dg = (sg.dbg & 64) && sg.dbg_ctr;
     const uint64_t tw0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t c_dead = 0, c_gen = 0, c_sent = 0, c_sexit = 0, t_dead = 0, t_ser = 0;
+    uint64_t ph[3] = {0, 0, 0};
     LNode nd(a, bndp, k);
     nd.created = 1;
     int32_t prule = -1;
@@ -2128,6 +2136,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 e.count = 0;
                 e.idx = 0;
                 if (act) e = ldecode(a, r_c);
+                const uint64_t tp0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;  // SG_DEBUG & 64: phase ticks
                 const bool okl = !act || (e.kind == SG_LOCAL_ENTRY && e.idx < dead_end && s_c.psl != 0xFFFFFFFFu);
                 if (__ballot(!okl)) break;
                 // two chunks ahead: records and side words; the next chunk: its slot states
@@ -2148,6 +2157,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                         v_c.st.flags = fl;
                     }
                 }
+                const uint64_t tp1 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
                 const uint32_t psl = s_c.psl;
                 if (!inited && __ballot(act && psl != 0xFFFFFFFEu)) {  // initParamMetricsFor
                     a.ps.inited[ri] = 1;
@@ -2164,11 +2174,13 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 int rank = 0, prev = lane;
                 uint64_t gm = 0;
                 uint64_t todo = __ballot(chain);
+                int maxrank = 0;  // the longest chain's last rank
                 while (todo) {
                     const int l0 = __builtin_ctzll(todo);
                     const uint32_t g0 = (uint32_t)bcast32((int)psl, l0);
                     const uint64_t m = __ballot(chain && psl == g0);
                     todo &= ~m;
+                    maxrank = max(maxrank, (int)__popcll(m) - 1);
                     if (chain && psl == g0) {
                         gm = m;
                         const uint64_t lo = m & below(lane);
@@ -2176,9 +2188,6 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                         prev = lo ? 63 - __builtin_clzll(lo) : lane;
                     }
                 }
-                int maxrank = chain ? rank : 0;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) maxrank = max(maxrank, __shfl_xor(maxrank, o, 64));
                 bool ok = !stuck;
                 for (int r = 0; r <= maxrank; ++r) {
                     const int64_t ptm = __shfl((long long)st.time, prev, 64);
@@ -2195,6 +2204,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                                  : param_default_step(st, tc, tc + pr.burst, dur, s_c.t, e.count);
                     }
                 }
+                const uint64_t tp2 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
                 w_g = 0xFFFFFFFFu;
                 if (chain && (gm & ~below(lane + 1)) == 0) {  // the slot's last request writes it back
                     PSlot* const sl = tab + psl;
@@ -2213,7 +2223,13 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                     merge_lanes();
                     if (ovf) lane_add(s_c.node, e.count);
                 }
-                if (dg) ++c_dead;
+                if (dg) {
+                    ++c_dead;
+                    const uint64_t tp3 = __builtin_amdgcn_s_memrealtime();
+                    ph[0] += tp1 - tp0;
+                    ph[1] += tp2 - tp1;
+                    ph[2] += tp3 - tp2;
+                }
                 base += 64;
                 if (base >= e_end) break;
                 r_c = r_n;
@@ -2349,11 +2365,13 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                 int rank = 0, prev = lane;
                 uint64_t gm = 0;
                 uint64_t todo = __ballot(chain);
+                int maxrank = 0;  // the longest chain's last rank
                 while (todo) {
                     const int l0 = __builtin_ctzll(todo);
                     const uint64_t g0 = (uint64_t)bcast64((int64_t)g, l0);
                     const uint64_t m = __ballot(chain && g == g0);
                     todo &= ~m;
+                    maxrank = max(maxrank, (int)__popcll(m) - 1);
                     if (chain && g == g0) {
                         gm = m;
                         const uint64_t lo = m & below(lane);
@@ -2361,9 +2379,6 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
                         prev = lo ? 63 - __builtin_clzll(lo) : lane;
                     }
                 }
-                int maxrank = chain ? rank : 0;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) maxrank = max(maxrank, __shfl_xor(maxrank, o, 64));
                 bool ok = !stuck;
                 for (int r = 0; r <= maxrank; ++r) {
                     const int64_t ptm = __shfl((long long)st.time, prev, 64);
@@ -2489,6 +2504,9 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         atomicAdd(&sg.dbg_ctr[27], (unsigned long long)t_dead);
         atomicAdd(&sg.dbg_ctr[28], (unsigned long long)t_ser);
         atomicAdd(&sg.dbg_ctr[17], (unsigned long long)t_head);
+        atomicAdd(&sg.dbg_ctr[12], (unsigned long long)ph[0]);
+        atomicAdd(&sg.dbg_ctr[13], (unsigned long long)ph[1]);
+        atomicAdd(&sg.dbg_ctr[14], (unsigned long long)ph[2]);
         if (tw > 500000ull) {  // segments over 5 ms: their serial steps, serial ticks, dead chunks
             atomicAdd(&sg.dbg_ctr[29], (unsigned long long)(c_sent + c_sexit));
             atomicAdd(&sg.dbg_ctr[30], (unsigned long long)t_ser);
