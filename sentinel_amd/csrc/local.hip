@@ -414,6 +414,31 @@ struct LNode {
         cb[0] = cb[1] = LBreaker{};
     }
 
+    // a pool node (origin / context) of the same batch as `like`: its window cursors and period bases are like's
+    // (the batch's), only its head is read
+    __device__ LNode(const LArgs& a_, const LNode& like, uint32_t k_) : a(a_), k(k_) {
+        R = LRule{};
+        R.flow_grade = -1;
+        R.b[0].stat_ms = R.b[1].stat_ms = 1;
+        sec = a.sec + (size_t)k * a.S;
+        bor = a.bor + (size_t)k * a.S;
+        mnt = a.minute + (size_t)k * kMinuteS;
+        cs = Cursor{like.cs.bnd, like.cs.np, 0xFFFFFFFFu, 0};
+        cm = Cursor{like.cm.bnd, like.cm.np, 0xFFFFFFFFu, 0};
+        P0s = like.P0s;
+        P0m = like.P0m;
+        sI = mI = -1;
+        s_ws = m_ws = 0;
+        s_wo = 0;
+        s_min = m_min = kStatMaxRt;
+        for (int e = 0; e < kLEv; ++e) sc[e] = mc[e] = 0;
+        const LHead h = a.head[k];
+        threads = h.threads;
+        created = h.created;
+        cb[0] = h.cb[0];
+        cb[1] = h.cb[1];
+    }
+
     __device__ LNode(const LArgs& a_, const uint32_t* const* bndp, uint32_t k_) : a(a_), k(k_) {
         if (k_ < a.K) {
             R = a.rules[k_];
@@ -1442,8 +1467,8 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
     // windows opened as touched (cx_rule, the StatisticSlot adds); an absent node loads nothing
-    LNode on = have_on ? LNode(a, bndp, on_idx) : LNode(a, LNode::None{});
-    LNode cn = have_cn ? LNode(a, bndp, cn_idx) : LNode(a, LNode::None{});
+    LNode on = have_on ? LNode(a, nd, on_idx) : LNode(a, LNode::None{});
+    LNode cn = have_cn ? LNode(a, nd, cn_idx) : LNode(a, LNode::None{});
     const bool params = R.ps && a.has_ps && x && !x->args_null;
     int32_t status = SG_LOCAL_PASS;
     int64_t wait = 0;
@@ -1591,13 +1616,13 @@ __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, 
     nd.exit(e, t, create);
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
-        LNode on(a, bndp, on_idx);
+        LNode on(a, nd, on_idx);
         on.at(qs, qm);
         on.exit(e, t, create);
         on.finish();
     }
     if (cn_idx != kNoNode) {
-        LNode cn(a, bndp, cn_idx);
+        LNode cn(a, nd, cn_idx);
         cn.at(qs, qm);
         cn.exit(e, t, create);
         cn.finish();
@@ -1712,7 +1737,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
         auto flush_origins = [&]() {
             for (int q = 0; q < 2; ++q) {
                 if (onode[q] == kNoNode) continue;
-                LNode on(a, bndp, onode[q]);
+                LNode on(a, nd, onode[q]);
                 on.at(dqs, dqm);
                 on.sc[kLBlock] += osum[q];
                 on.mc[kLBlock] += osum[q];
@@ -1963,7 +1988,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         while (used) {
             const int j = __builtin_ctzll(used);
             used &= used - 1;
-            LNode on(a, bndp, (uint32_t)bcast32((int)ob_node, j));
+            LNode on(a, nd, (uint32_t)bcast32((int)ob_node, j));
             on.at(dead_qs, dead_qm);
             const int64_t sum = bcast64(ob_sum, j);
             on.sc[kLBlock] += sum;
