@@ -1647,7 +1647,9 @@ __device__ __forceinline__ uint32_t cx_items(const BatchArgs& sg) {
 }
 
 // Item i: the head of a segment the lane cx walker takes (a cx or origin-event resource the wave walker leaves; a
-// RELATE group), else ~0.
+// RELATE group), else ~0. (Returned, not written through an out-parameter: that form, inlined into k_lcx_list under
+// -O3, stored 0 for the origin-event segments — test_local_rules_gpu.py::test_mixed_rule_sets with one lane per
+// segment caught it.)
 __device__ __forceinline__ uint64_t cx_item(const LArgs& a, const BatchArgs& sg, uint32_t i) {
     uint32_t r = i;
     uint64_t j;
