@@ -330,6 +330,8 @@ struct sg_handle {
     // k_seg_mark over the sorted records (default), or the marks fused into the last scatter pass (env SG_SEG_MARK=0:
     // its ~20M atomicMin/Max per 16M-record batch cost more than the separate read — 0.97 vs 0.91 ms/step, same box)
     bool seg_mark_pass = true;
+    bool lim_pipe = true;             // limiter batches: the front half does not wait for the previous back half
+                                      // (env SG_LIM_PIPE=0: it waits); read once in sg_create
 };
 
 namespace {
@@ -547,6 +549,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (const char* d = std::getenv("SG_CXW_MIN")) h->l_cxw_min = (uint32_t)std::strtoul(d, nullptr, 10);
     if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
+    if (const char* d = std::getenv("SG_LIM_PIPE")) h->lim_pipe = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -1515,9 +1518,10 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
     if (h->n_lim > 0) {
         // the limiter pre-pass must see only accepted batches: k_prep checks the time order against the previous
         // front half's last timestamp (front_ts, advanced once a batch passed validation) as well as last_ts, so
-        // this front half need not wait for the previous batch's walkers (env SG_LIM_PIPE=0: it waits, as before)
-        const char* lp = std::getenv("SG_LIM_PIPE");
-        if (lp && std::atoi(lp) == 0) {
+        // this front half need not wait for the previous batch's walkers (env SG_LIM_PIPE=0: it waits, as before).
+        // A batch the back half later refuses has still advanced front_ts: the next batch is checked against its
+        // timestamps too (a batch must be time-ordered after every batch submitted before it, accepted or not).
+        if (!h->lim_pipe) {
             if (!first) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[xp], 0));
         } else {
             a.front_ts = h->d_front_ts;
@@ -3646,6 +3650,7 @@ namespace {
 
 // One node's windows (resource or origin node) in the sg_local_read_state layout.
 int local_read_node(sg_handle* h, uint32_t node, int64_t* second, int64_t* borrow, int64_t* minute, int64_t* head) {
+    if ((uint64_t)node >= h->l_nodes) return fail(h, SG_E_INVAL, "node index past the node arrays");
     HIP_TRY(h, hipSetDevice(h->device));
     drain_async(h);
     const int S = h->lcfg.sample_count;
@@ -3693,7 +3698,10 @@ int local_read_pool_node(sg_handle* h, uint64_t key, int64_t* second, int64_t* b
         HIP_TRY(h, launch_lnode_find(h->d_lnkeys, h->d_lnvals, h->l_nmap_cap - 1, key, h->d_lnode_new, 0));
         HIP_TRY(h, hipMemcpy(&node, h->d_lnode_new, sizeof(node), hipMemcpyDeviceToHost));
     }
-    if (node != kNoNode) {
+    // A node a refused batch created past the pool's capacity (lnode_grow failed, l_pool_used moved past it) has
+    // no storage yet: it exists with zero counts, which is what the empty dumps below say.
+    const bool stored = node != kNoNode && (uint64_t)node < h->l_nodes;
+    if (stored) {
         const int rc = local_read_node(h, node, second, borrow, minute, head);
         return rc ? rc : 1;
     }
@@ -3707,7 +3715,7 @@ int local_read_pool_node(sg_handle* h, uint64_t key, int64_t* second, int64_t* b
         for (int e = 0; e < 8; ++e) minute[8 * j + e] = e == 0 ? INT64_MIN : 0;
     std::fill(head, head + 14, 0);
     head[3] = head[9] = INT64_MIN;  // the breakers' stat buckets of a fresh node: never created
-    return 0;
+    return node != kNoNode ? 1 : 0;
 }
 
 // FlowRuleUtil.isValidRule (:167-251) for local rules: count >= 0, grade / strategy / behaviour >= 0; QPS rules:

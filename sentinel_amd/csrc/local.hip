@@ -2887,13 +2887,16 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     if (bl == 0) bl = lresident((const void*)k_lwalk_long);
     if (bs == 0) bs = lresident((const void*)k_lwalk_short);
     if (a.defer_last) hipLaunchKernelGGL(k_local_check_last, dim3(1), dim3(1), 0, stream, a);
+    // the side words are read by both cx walkers (the lane walker on `aux` in its dead periods): they are
+    // written before the fork, so `aux` is ordered after them
+    if (has_cx && a.cxw && a.cxside)
+        hipLaunchKernelGGL(k_lcx_side, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
     hipError_t e = hipEventRecord(fork, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e != hipSuccess) return e;
     // the hot cx segments' waves first (the batch's longest serial chains), the lane walker of the other cx
     // segments beside them after the plain wave walker
     if (has_cx && a.cxw) {
-        if (a.cxside) hipLaunchKernelGGL(k_lcx_side, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
         static unsigned bw = 0;
         if (bw == 0) bw = lresident((const void*)k_lwalk_cxw);
         e = hipMemsetAsync(a.cxw_next, 0, sizeof(uint32_t), stream);
