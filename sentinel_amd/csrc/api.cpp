@@ -38,6 +38,12 @@ struct sg_handle {
     BucketHot* d_hot = nullptr;       // start / PASS / WAITING of every bucket (the short walkers' gather)
     Occ* d_occ = nullptr;
     uint32_t* d_seg_end = nullptr;   // [2K] end, then start (k_seg_mark) of each flowId's segment in the sorted records
+    // binned front half (engine.hip k_bin_sort): the hot flowIds of the previous batch and workspace 0's bin buffer
+    uint32_t* d_hot_key = nullptr;    // [kBinHot] flowId per hot slot, then the table [kHotTab] {flowId, slot}
+    uint64_t hot_gen = ~0ull;         // rules_gen the hot set was reset for
+    uint64_t rules_gen = 0;           // flow rule loads so far (a reload renumbers flowIds: the hot set restarts)
+    uint64_t* d_bin_buf = nullptr;
+    int bin_mode = 1;                 // env SG_BIN: 0 off, 1 on for >= 2^14 flowIds, 2 on whenever the records allow
 
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
@@ -304,6 +310,7 @@ struct sg_handle {
         uint32_t* seg_end = nullptr;  // [K]
         uint32_t* seg_start = nullptr;  // [K], all 0xFFFFFFFF between batches
         uint32_t* short_end = nullptr;
+        uint64_t* bin_buf = nullptr;    // binned front half: the regular bins after the scatter (max_batch records)
     };
     FlowWs pws{};
     uint32_t pws_segcap = 0;
@@ -550,6 +557,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (const char* d = std::getenv("SG_D2H")) h->d2h_kernel = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_LIM_PIPE")) h->lim_pipe = std::atoi(d) != 0;
+    if (const char* d = std::getenv("SG_BIN")) h->bin_mode = std::atoi(d);
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -587,6 +595,7 @@ void sg_destroy(sg_handle* h) {
         dfree(w.skips);
         dfree(w.skip_count);
         dfree(w.seg_end);
+        dfree(w.bin_buf);
         for (auto* st : {&h->s_front, &h->s_back, &h->s_aux2, &h->s_aux3, &h->s_xcopy})
             if (*st) (void)hipStreamDestroy(*st);
         if (h->xcopy_done) (void)hipEventDestroy(h->xcopy_done);
@@ -607,6 +616,8 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_hot);
     dfree(h->d_occ);
     dfree(h->d_seg_end);
+    dfree(h->d_hot_key);
+    dfree(h->d_bin_buf);
     dfree(h->d_rec);
     dfree(h->d_rec_sorted);
     dfree(h->d_hist);
@@ -1054,6 +1065,7 @@ int flow_rules_commit(sg_handle* h, const sg_flow_rule* rules, uint32_t n, FlowL
     h->rules.assign(rules, rules + n);
     h->rule_tab = L.tab;
     h->K = n;
+    ++h->rules_gen;
     h->stride = L.stride;
     h->n_wl = L.n_wl;
     std::memcpy(h->wl, L.wl, sizeof(L.wl));
@@ -1219,6 +1231,7 @@ void main_ws(sg_handle* h, sg_handle::FlowWs& w) {
     w.seg_end = h->d_seg_end;
     w.seg_start = h->d_seg_end ? h->d_seg_end + h->K : nullptr;
     w.short_end = h->d_short_end;
+    w.bin_buf = h->d_bin_buf;
 }
 
 // Workspace 1 and the pipeline's streams / events, allocated on first pipelined batch (seg_end grows with K).
@@ -1303,6 +1316,7 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     a.hist0 = h->n_lim > 0 ? nullptr : w.hist;  // the limiter pre-pass rewrites records after k_prep
     a.hist0_bits = radix_digit_bits(h->kbits);
     a.kshift = 64 - h->kbits;
+    a.hist0_shift = a.kshift;
     a.abits = h->abits;
     a.imask = (h->ibits >= 64) ? ~0ull : ((1ull << h->ibits) - 1);
     a.amask = (1ull << h->abits) - 1;
@@ -1381,6 +1395,43 @@ int flow_limiter(sg_handle* h, BatchArgs& a, hipStream_t stream) {
     return SG_OK;
 }
 
+// The binned front half (engine.hip k_bin_sort) for a flow batch of workspace w when the handle's records allow it:
+// >= 2^14 flowIds (SG_BIN=2: any), at most 2^20 (a regular bin holds <= 2048 flowIds), kBinDigit free middle bits,
+// no namespace limiter (its pre-pass rewrites records after k_prep). Sets a's bin fields; false: the two-pass sort.
+bool bin_setup(sg_handle* h, sg_handle::FlowWs& w, BatchArgs& a, hipStream_t stream) {
+    if (h->bin_mode == 0 || h->n_lim > 0 || !a.hist0 || a.n == 0 || h->K == 0) return false;
+    if (h->bin_mode == 1 && h->K < (1u << 14)) return false;
+    if (64 - h->kbits - h->ibits - h->abits < kBinDigit) return false;
+    const int kb = h->K > 1 ? bits_for((uint64_t)h->K - 1) : 1;
+    const int bsh = std::max(0, kb - 9);
+    if (bsh > kBinMaxBsh || (((h->K - 1) >> bsh) + 1) > kBinRegular) return false;
+    if (!h->d_hot_key) {
+        if (hipMalloc(&h->d_hot_key, sizeof(uint32_t) * (kBinHot + 1) + sizeof(uint2) * kHotTab) != hipSuccess)
+            return false;
+        h->hot_gen = ~0ull;
+    }
+    uint2* tab = reinterpret_cast<uint2*>(h->d_hot_key + kBinHot + 1);
+    if (!w.bin_buf) {
+        if (hipMalloc(&w.bin_buf, (h->cfg.max_batch + kRecW) * 8) != hipSuccess) return false;
+        if (w.rec == h->d_rec) h->d_bin_buf = w.bin_buf;
+        else h->pws.bin_buf = w.bin_buf;
+    }
+    if (h->hot_gen != h->rules_gen) {  // flowIds renumbered: no hot flowIds yet (stream-ordered before k_prep)
+        if (launch_hot_reset(tab, stream) != hipSuccess) return false;
+        h->hot_gen = h->rules_gen;
+    }
+    a.bin_on = 1;
+    a.bin_dshift = h->abits + h->ibits;
+    a.bin_bsh = bsh;
+    a.bin_R = ((h->K - 1) >> bsh) + 1;
+    a.hot_tab = tab;
+    a.hot_key = h->d_hot_key;
+    a.bin_buf = w.bin_buf;
+    a.hist0_bits = kBinDigit;
+    a.hist0_shift = a.bin_dshift;
+    return true;
+}
+
 int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, bool stats) {
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[0], stream));
     HIP_TRY(h, hipMemsetAsync(a.err, 0, sizeof(int), stream));
@@ -1396,6 +1447,12 @@ int flow_front(sg_handle* h, BatchArgs& a, uint32_t* hist, hipStream_t stream, b
     if (lrc) return lrc;
     if (a.front_ts) HIP_TRY(h, launch_front_ts(a, stream));
     if (stats) HIP_TRY(h, hipEventRecord(h->ev[1], stream));
+    if (a.bin_on) {  // one scatter pass by bin digit, the regular bins sorted and every segment listed in LDS
+        HIP_TRY(h, launch_bin_front(a, hist, true, a.csum0 != nullptr, stream));
+        if (a.rec == h->d_rec) h->last_sorted = a.rec_sorted;
+        if (stats) HIP_TRY(h, hipEventRecord(h->ev[2], stream));
+        return SG_OK;
+    }
     {
         uint64_t* sorted = nullptr;
         // segment marks: k_seg_mark after the sort, or (SG_SEG_MARK=0) fused into the last scatter pass
@@ -1465,6 +1522,7 @@ int enqueue_flow(sg_handle* h, const sg_req* req, uint64_t n, sg_result* out, hi
     sg_handle::FlowWs w;
     main_ws(h, w);
     BatchArgs a = flow_args(h, w, req, n, out);
+    bin_setup(h, w, a, stream);
     rc = flow_front(h, a, w.hist, stream, stats);
     if (rc) return rc;
     return flow_back(h, a, stream, h->aux, h->fork, h->join, err_dst, stats);
@@ -1513,6 +1571,7 @@ int enqueue_flow_pipelined(sg_handle* h, const sg_req* req, uint64_t n, sg_resul
         HIP_TRY(h, hipEventSynchronize(h->xcopy_done));
     }
     BatchArgs a = flow_args(h, w, req, n, out);
+    bin_setup(h, w, a, h->s_front);
     if (after) HIP_TRY(h, hipStreamWaitEvent(h->s_front, after, 0));
     if (h->pipe_seq >= 2) HIP_TRY(h, hipStreamWaitEvent(h->s_front, h->back_done[x], 0));
     if (h->n_lim > 0) {

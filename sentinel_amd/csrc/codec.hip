@@ -128,6 +128,7 @@ static unsigned codec_grid(uint64_t n) {
 
 hipError_t launch_codec_decode(const CodecArgs& c, hipStream_t stream) {
     if (((uintptr_t)c.payload & 3u) != 0) return hipErrorInvalidValue;  // staged loads are 4-byte words
+    lds_poison(stream);
     hipLaunchKernelGGL(k_codec_decode, dim3(codec_grid(c.n)), dim3(kDecFrames), 0, stream, c);
     return hipGetLastError();
 }

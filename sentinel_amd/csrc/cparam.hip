@@ -1294,6 +1294,7 @@ hipError_t launch_cp_items(const CPBatch& b, const BatchArgs& sg, uint64_t items
 
 hipError_t launch_cp_mlist(const CPArgs& c, const CPBatch& b, hipStream_t stream) {
     if (c.n == 0) return hipSuccess;
+    lds_poison(stream);
     hipLaunchKernelGGL(k_cp_mlist, dim3((unsigned)((c.n + 256 * kAggItems - 1) / (256 * kAggItems))), dim3(256), 0, stream,
                        c, b);
     return hipGetLastError();
@@ -1302,6 +1303,7 @@ hipError_t launch_cp_mlist(const CPArgs& c, const CPBatch& b, hipStream_t stream
 // k_cp_combine over the multi-value requests, then the re-walk lists of the next round (`items` work items)
 hipError_t launch_cp_combine(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t items, hipStream_t stream) {
     hipLaunchKernelGGL(k_cp_combine, dim3(cgrid2(c.n / 8 + 1, 4096)), dim3(256), 0, stream, c, b);
+    lds_poison(stream);
     if (items) hipLaunchKernelGGL(k_cp_relist, dim3((unsigned)((items + 256 * kAggItems - 1) / (256 * kAggItems))),
                                   dim3(256), 0, stream, b, sg, (uint32_t)items);
     return hipGetLastError();

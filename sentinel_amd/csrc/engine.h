@@ -145,7 +145,30 @@ struct BatchArgs {
     uint4* skips;
     uint32_t* skip_count;
     uint32_t skip_cap;
+    // Binned front half (bin_on = 1, see k_bin_sort): k_prep writes a 10-bit bin digit into the record's free
+    // middle bits [bin_dshift, bin_dshift + 10) — the flowId's hot slot (R + slot) for the hot flowIds of the previous
+    // batch, else its key range (key >> bin_bsh), kBinDrop for rejected requests — and counts it for the one global
+    // scatter pass; hot bins hold one flowId each, already in order, the regular bins are sorted in LDS by k_bin_sort.
+    int hist0_shift;       // k_prep's histogram digit: (rec >> hist0_shift) & mask (kshift, or bin_dshift)
+    int bin_on;
+    int bin_dshift;
+    int bin_bsh;
+    uint32_t bin_R;        // regular bins [0, R) (R = ((K - 1) >> bin_bsh) + 1 <= kBinRegular)
+    uint2* hot_tab;        // [kHotTab] {flowId, hot slot} open-addressing table (k_prep stages it in LDS)
+    uint32_t* hot_key;     // [kBinHot] flowId of each hot slot
+    uint64_t* bin_buf;     // the regular bins after the scatter (k_bin_sort's input, rec_sorted's index space)
+    const uint32_t* bin_tot;  // [1 << kBinDigit] digit totals (k_chunkscan)
 };
+
+constexpr int kBinDigit = 10;                        // bin digit width: one radix_pass<10>
+constexpr uint32_t kBinRegular = 512;                // regular bins (key ranges)
+constexpr uint32_t kBinHot = (1u << kBinDigit) - kBinRegular - 1;  // hot slots: one flowId each
+constexpr uint32_t kBinDrop = (1u << kBinDigit) - 1; // rejected requests
+constexpr int kBinMaxBsh = 11;                       // keys per regular bin <= 2048 (k_bin_sort's LDS counters)
+constexpr int kHotTabBits = 10;                      // the hot set's table: <= kBinHot keys in 1024 slots
+constexpr uint32_t kHotTab = 1u << kHotTabBits;
+constexpr uint32_t kHotEmpty = 0xFFFFFFFFu;
+__host__ __device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 2654435761u) >> (32 - kHotTabBits); }
 
 constexpr int kLongPeriods = 16;       // period-end table of the wave walker: batches of <= 16 window periods
 constexpr uint32_t kLongTab = 65536;  // long segments with a table (later ones search)
@@ -745,6 +768,10 @@ hipError_t launch_local_entry_rows(const LArgs& L, int64_t now, sg_metric_node* 
 hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
                                 int raw, hipStream_t stream);
 
+// Test aid (env SG_LDS_POISON=1): before every kernel that keeps counters or tables in LDS, a kernel fills the LDS of
+// every CU with 0xA5 bytes on the same stream, so a counter a kernel forgets to initialise reads garbage at once.
+void lds_poison(hipStream_t stream);
+
 // Launchers (engine.hip). All are asynchronous on `stream`.
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream);
 
@@ -800,8 +827,16 @@ struct SegMark {
 hipError_t radix_sort_records(uint64_t* a, uint64_t* b, uint64_t n, int lo_bit, uint32_t* hist_ws,
                               uint64_t** result, hipStream_t stream, int hi_bit = 64, bool first_hist_ready = false,
                               const SegMark* mark = nullptr, bool first_csum_ready = false);
+const uint32_t* radix_tot(const uint32_t* hist_ws, uint64_t n, int D);
+hipError_t radix_bin_pass(uint64_t* src, uint64_t* out, uint64_t* reg, uint32_t R, uint64_t n, int shift,
+                          uint32_t* hist_ws, bool hist_ready, bool csum_ready, hipStream_t stream);
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream);
 hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream);  // k_seg_mark + k_seg_classify
+// Binned front half after k_prep: the scatter by bin digit (regular bins to a.bin_buf, hot bins and rejected requests
+// to a.rec_sorted), k_bin_sort (regular bins sorted in LDS into a.rec_sorted, every segment listed), k_hot_update (the
+// next batch's hot flowIds: this batch's longest segments).
+hipError_t launch_bin_front(const BatchArgs& a, uint32_t* hist_ws, bool hist_ready, bool csum_ready, hipStream_t stream);
+hipError_t launch_hot_reset(uint2* hot_tab, hipStream_t stream);
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream);   // on an aux stream, concurrent with
 bool tiny_walker_enabled(const BatchArgs& a);
 hipError_t launch_walk_tiny(const BatchArgs& a, hipStream_t stream);

@@ -104,8 +104,19 @@ __device__ __forceinline__ Decoded decode_c(const BatchArgs& a, uint32_t c) {
 constexpr int kPrepItems = kSortRounds;  // k_prep's tile is the sort's (its first-pass histogram rows)
 constexpr uint32_t kPrepTile = 256 * kPrepItems;
 
+// BIN (the binned front half): each record also gets its bin digit (a.bin_on, see k_bin_sort) — after the main loop,
+// so that the hot-flowId table's loads (issued first, staged in LDS after the loop) ride with the requests' loads
+// instead of adding a round trip before them.
+template <bool BIN>
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
     __shared__ uint32_t dcnt[1024];
+    __shared__ uint2 htab[BIN ? kHotTab : 1];  // the hot flowIds: a short LDS probe per request
+    constexpr int kTabPer = BIN ? (int)kHotTab / 256 : 1;
+    uint2 tv[kTabPer];
+    if constexpr (BIN) {
+#pragma unroll
+        for (int u = 0; u < kTabPer; ++u) tv[u] = a.hot_tab[u * 256 + threadIdx.x];
+    }
     const uint64_t n = a.n;
     const int64_t t0 = a.req[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
@@ -114,7 +125,9 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         for (uint32_t d = threadIdx.x; d <= dmask; d += 256) dcnt[d] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kPrepTile;
-#pragma unroll 4
+    uint64_t rv[BIN ? kPrepItems : 1];
+    constexpr int kUnroll = BIN ? kPrepItems : 4;  // BIN: rv[] stays in registers
+#pragma unroll kUnroll
     for (int it = 0; it < kPrepItems; ++it) {
         const uint64_t i = base + (uint64_t)it * 256 + threadIdx.x;
         if (i >= n) break;
@@ -172,8 +185,41 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             st_stream(o + 1, 0);
             st_stream(o + 2, 0);
         }
-        st_stream(a.rec + i, rec);
-        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
+        if constexpr (BIN) {
+            rv[it] = rec;
+        } else {
+            st_stream(a.rec + i, rec);
+            if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.hist0_shift) & dmask], 1u);
+        }
+    }
+    if constexpr (BIN) {
+#pragma unroll
+        for (int u = 0; u < kTabPer; ++u) htab[u * 256 + threadIdx.x] = tv[u];
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPrepItems; ++it) {
+            const uint64_t i = base + (uint64_t)it * 256 + threadIdx.x;
+            if (i >= n) break;
+            uint64_t rec = rv[it];
+            const uint32_t key = (uint32_t)(rec >> a.kshift);
+            uint32_t d = kBinDrop;  // a rejected request: its own bin
+            if (key < a.K) {        // the flowId's hot slot, else its key range
+                d = key >> a.bin_bsh;
+                uint32_t x = hot_hash(key);
+                for (uint32_t probe = 0; probe < kHotTab; ++probe) {  // linear probing, load <= 1/2
+                    const uint2 e = htab[x];
+                    if (e.x == key) {
+                        d = a.bin_R + e.y;
+                        break;
+                    }
+                    if (e.x == kHotEmpty) break;
+                    x = (x + 1) & (kHotTab - 1);
+                }
+            }
+            rec |= (uint64_t)d << a.bin_dshift;
+            st_stream(a.rec + i, rec);
+            atomicAdd(&dcnt[d], 1u);
+        }
     }
     if (a.hist0) {
         __syncthreads();
@@ -933,6 +979,296 @@ __global__ void __launch_bounds__(256) k_seg_classify(BatchArgs a) {
         }
         __syncthreads();  // cnt / base are reused by the next range
     }
+}
+
+constexpr uint32_t kPoisonBytes = 65536;
+
+// ------------------------------------------------------------------------------ binned front half
+//
+// One global pass instead of two: k_prep writes each valid record's bin digit into its free middle bits — the hot slot
+// of a flowId among the previous batch's longest segments (a bin of its own: after the stable scatter its records
+// are already its segment, in arrival order), else the flowId's key range key >> bin_bsh (a regular bin of at most
+// 2^kBinMaxBsh flowIds) — and the one radix pass by that digit leaves the regular bins in a.bin_buf. k_bin_sort then
+// sorts each regular bin by flowId with a counting sort in LDS (no second global pass, no segment-marking read) and
+// lists every segment by length class as k_seg_classify would; k_hot_update picks the next batch's hot flowIds. The
+// sorted array is rec_sorted: regular bins in flowId order, then one segment per hot flowId; the walkers need only
+// each flowId's records contiguous and in arrival order, which both kinds of bin give. The hot set is a speed hint:
+// a flowId outside it (or a stale one) is sorted by its regular bin, whatever its length.
+
+// Block-aggregated list appends (k_seg_classify's scheme): class of a segment of `len` records.
+__device__ __forceinline__ uint32_t seg_class(const BatchArgs& a, uint32_t len) {
+    uint32_t l = 0;
+#pragma unroll
+    for (int c = 0; c < kClasses - 1; ++c) l += len > kClassMax[c] ? 1u : 0u;
+    return len > a.short_max ? (uint32_t)kClasses : l;
+}
+
+__device__ __forceinline__ void seg_emit(const BatchArgs& a, uint32_t l, uint32_t pos, uint32_t st, uint32_t en,
+                                         uint32_t k) {
+    if (l == (uint32_t)kClasses) {
+        a.long_list[pos] = st;
+        a.long_key[pos] = k;
+        a.long_end[pos] = en;
+    } else {
+        const uint64_t q = a.class_off[l] + pos;
+        a.short_list[q] = st;
+        a.short_key[q] = k;
+        a.short_end[q] = en;
+    }
+}
+
+constexpr uint32_t kBinKeys = 1u << kBinMaxBsh;
+constexpr int kBinThreads = 512;
+constexpr int kBinWaves = kBinThreads / 64;
+constexpr int kBinPer = kBinKeys / kBinThreads;  // keys per thread in the scan (contiguous)
+constexpr int kBinRows = 24;                     // 64-record rows a lane holds at once (a wave's whole quarter, usually)
+
+// Exclusive scan of the 1024 digit totals into dbase (every block: 4 KB, L2-resident).
+__device__ __forceinline__ void bin_digit_bases(const BatchArgs& a, uint32_t* dbase, uint32_t* wsum) {
+    constexpr int kD = 1 << kBinDigit, kPerT = kD / kBinThreads;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    uint32_t v[kPerT], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+        v[i] = a.bin_tot[tid * kPerT + i];
+        sum += v[i];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+#pragma unroll
+    for (int i = 0; i < kPerT; ++i) {
+        dbase[tid * kPerT + i] = run;
+        run += v[i];
+    }
+    __syncthreads();
+}
+
+// Lanes of this wave whose `bits`-bit local key equals this lane's (wave-uniform bits <= kBinMaxBsh).
+__device__ __forceinline__ uint64_t match_key(uint32_t d, int bits) {
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < kBinMaxBsh; ++b) {
+        if (b < bits) {
+            const uint64_t m = __ballot((d >> b) & 1u);
+            peers &= ((d >> b) & 1u) ? m : ~m;
+        }
+    }
+    return peers;
+}
+
+// Blocks [0, R): regular bin b — a stable counting sort by flowId: wave w takes the w-th eighth of the bin in order and
+// keeps its own counters, so its records of a flowId follow the earlier waves' ones. A wave's eighth (<= kBinRows rows,
+// the usual case) is loaded once, all rows at once, and kept in registers for both the count and the placement; longer
+// ones (a flowId that outgrew the hot set) go by groups of kBinRows rows, read twice. Block R: the hot bins' segments.
+__global__ void __launch_bounds__(kBinThreads) k_bin_sort(BatchArgs a) {
+    constexpr int kL = kClasses + 1;
+    __shared__ uint32_t cnt[kBinWaves][kBinKeys];
+    __shared__ uint32_t dbase[1 << kBinDigit];
+    __shared__ uint32_t wsum[kBinWaves];
+    __shared__ uint32_t lcnt[kL], lbase[kL];
+    if (*a.err) return;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    if (tid < kL) lcnt[tid] = 0;
+    bin_digit_bases(a, dbase, wsum);
+    const uint32_t b = blockIdx.x;
+    if (b >= a.bin_R) {  // the hot bins: one flowId each, in order already
+        constexpr int kHR = (kBinHot + kBinThreads - 1) / kBinThreads;
+        uint32_t slot[kHR];
+#pragma unroll
+        for (int r = 0; r < kHR; ++r) {
+            const uint32_t hs = (uint32_t)r * kBinThreads + tid;
+            slot[r] = 0xFFFFFFFFu;
+            if (hs >= kBinHot) continue;
+            const uint32_t len = a.bin_tot[a.bin_R + hs];
+            if (len == 0) continue;
+            const uint32_t l = seg_class(a, len);
+            slot[r] = (l << 24) | atomicAdd(&lcnt[l], 1u);
+        }
+        __syncthreads();
+        if (tid < kL) {
+            const uint32_t t = lcnt[tid];
+            uint32_t* ctr = tid == kClasses ? a.long_count : a.short_count + tid;
+            lbase[tid] = t ? atomicAdd(ctr, t) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < kHR; ++r) {
+            if (slot[r] == 0xFFFFFFFFu) continue;
+            const uint32_t hs = (uint32_t)r * kBinThreads + tid;
+            const uint32_t st = dbase[a.bin_R + hs], l = slot[r] >> 24;
+            seg_emit(a, l, lbase[l] + (slot[r] & 0xFFFFFFu), st, st + a.bin_tot[a.bin_R + hs], a.hot_key[hs]);
+        }
+        return;
+    }
+    const uint32_t s0 = dbase[b], len = a.bin_tot[b];
+    if (len == 0) return;
+    const int bsh = a.bin_bsh;
+    const uint32_t kb0 = b << bsh;
+    const uint32_t nk = min(1u << bsh, a.K - kb0);
+    const uint32_t C = (len + kBinWaves - 1) / kBinWaves;
+    const uint32_t c0 = s0 + min((uint32_t)wave * C, len), c1 = s0 + min((uint32_t)(wave + 1) * C, len);
+    const bool one = C <= 64u * kBinRows;  // every wave's eighth fits its registers
+    const uint32_t last = s0 + len - 1;    // loads are clamped into the bin (unconditional: no phi waits)
+    const uint64_t* src = a.bin_buf;
+    uint64_t v[kBinRows];
+    // 0. the first (usually only) group of rows: issued before the counters are cleared
+#pragma unroll
+    for (int u = 0; u < kBinRows; ++u) v[u] = src[min(c0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
+    for (uint32_t j = tid; j < (uint32_t)kBinWaves * kBinKeys; j += kBinThreads) (&cnt[0][0])[j] = 0;
+    __syncthreads();
+    // 1. counts per (wave, flowId)
+    for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
+        if (r0 != c0) {
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
+        }
+#pragma unroll
+        for (int u = 0; u < kBinRows; ++u) {
+            const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
+            if (j < c1) atomicAdd(&cnt[wave][(uint32_t)(v[u] >> a.kshift) - kb0], 1u);
+        }
+    }
+    __syncthreads();
+    // 2. segment starts (exclusive scan over flowIds, tid's kBinPer contiguous flowIds), per-wave bases, list entries
+    uint32_t tk[kBinPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        const uint32_t j = (uint32_t)tid * kBinPer + i;
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kBinWaves; ++w) t += cnt[w][j];
+        tk[i] = t;
+        sum += t;
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    uint32_t slot[kBinPer], sst[kBinPer];
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        const uint32_t j = (uint32_t)tid * kBinPer + i;
+        sst[i] = run;
+        uint32_t pre = run;
+#pragma unroll
+        for (int w = 0; w < kBinWaves; ++w) {
+            const uint32_t c = cnt[w][j];
+            cnt[w][j] = pre;
+            pre += c;
+        }
+        slot[i] = 0xFFFFFFFFu;
+        if (tk[i] && j < nk) {
+            const uint32_t l = seg_class(a, tk[i]);
+            slot[i] = (l << 24) | atomicAdd(&lcnt[l], 1u);
+        }
+        run += tk[i];
+    }
+    __syncthreads();
+    if (tid < kL) {
+        const uint32_t t = lcnt[tid];
+        uint32_t* ctr = tid == kClasses ? a.long_count : a.short_count + tid;
+        lbase[tid] = t ? atomicAdd(ctr, t) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        if (slot[i] == 0xFFFFFFFFu) continue;
+        const uint32_t l = slot[i] >> 24;
+        seg_emit(a, l, lbase[l] + (slot[i] & 0xFFFFFFu), s0 + sst[i], s0 + sst[i] + tk[i],
+                 kb0 + (uint32_t)tid * kBinPer + i);
+    }
+    // 3. stable placement: each wave goes over its eighth again in order, 64 records a round; the rank among equal
+    // flowIds of a round comes from ballots, the wave's own running counter (LDS ops of one wave execute in order) does
+    // the rest
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t* dst = a.rec_sorted + s0;
+    for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
+        if (!one) {
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
+        }
+#pragma unroll
+        for (int u = 0; u < kBinRows; ++u) {
+            const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
+            const bool valid = j < c1;
+            const uint32_t d = valid ? (uint32_t)(v[u] >> a.kshift) - kb0 : 0u;
+            const uint64_t peers = match_key(d, bsh) & __ballot(valid);
+            const uint32_t c = cnt[wave][d];
+            if (valid) {
+                dst[c + (uint32_t)__popcll(peers & lt)] = v[u];
+                if (lane == __builtin_ctzll(peers)) cnt[wave][d] = c + (uint32_t)__popcll(peers);
+            }
+        }
+    }
+}
+
+// The next batch's hot flowIds: the segments of more than short_max records, the longest first (a histogram of
+// floor(log2 len) picks the length class that fills kBinHot slots), as an open-addressing table {flowId, slot} built in
+// LDS and written whole. One block; runs after k_bin_sort on the front stream, so the next k_prep reads the new table.
+__global__ void __launch_bounds__(1024) k_hot_update(BatchArgs a) {
+    __shared__ uint32_t hcnt[32];
+    __shared__ uint32_t thr, nslot;
+    __shared__ uint32_t tkey[kHotTab], tslot[kHotTab];
+    const uint32_t tid = threadIdx.x;
+    if (tid < 32) hcnt[tid] = 0;
+    if (tid == 0) nslot = 0;
+    for (uint32_t x = tid; x < kHotTab; x += 1024) tkey[x] = kHotEmpty;
+    __syncthreads();
+    const uint32_t nl = *a.err ? 0u : *a.long_count;  // a refused batch listed nothing: no hot flowIds next
+    for (uint32_t i = tid; i < nl; i += 1024) {
+        const uint32_t len = a.long_end[i] - a.long_list[i];
+        atomicAdd(&hcnt[31 - __clz(len)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // the lowest length class whose longer segments still fit the slots
+        uint32_t cum = 0, t = 0;
+        for (int c = 31; c >= 0; --c) {
+            cum += hcnt[c];
+            if (cum >= kBinHot) {
+                t = (uint32_t)c;
+                break;
+            }
+        }
+        thr = t;
+    }
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {  // the classes above thr first (they fit), then thr's own in any order
+        for (uint32_t i = tid; i < nl; i += 1024) {
+            const uint32_t len = a.long_end[i] - a.long_list[i];
+            const uint32_t c = 31 - __clz(len);
+            if (pass == 0 ? c <= thr : c != thr) continue;
+            const uint32_t s = atomicAdd(&nslot, 1u);
+            if (s >= kBinHot) continue;
+            const uint32_t k = a.long_key[i];
+            a.hot_key[s] = k;
+            for (uint32_t x = hot_hash(k);; x = (x + 1) & (kHotTab - 1)) {  // kBinHot < kHotTab: a free slot exists
+                if (atomicCAS(&tkey[x], kHotEmpty, k) == kHotEmpty) {
+                    tslot[x] = s;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t x = tid; x < kHotTab; x += 1024) a.hot_tab[x] = make_uint2(tkey[x], tslot[x]);
+}
+
+__global__ void __launch_bounds__(256) k_hot_reset(uint2* hot_tab) {
+    for (uint32_t x = threadIdx.x; x < kHotTab; x += 256) hot_tab[x] = make_uint2(kHotEmpty, 0u);
 }
 
 // Stage the batch's period tables in g_sbnd when they fit (else the cursors read a.bnd).
@@ -1890,12 +2226,55 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 
 
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
+    lds_poison(stream);
+    if (a.bin_on) hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_seg(const BatchArgs& a, hipStream_t stream) {
+    lds_poison(stream);
     hipLaunchKernelGGL(k_seg, dim3(grid_for(a.n, kSegTile, 8192)), dim3(kSegThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_lds_poison() {
+    extern __shared__ uint32_t lds_all[];
+    volatile uint32_t* p = lds_all;  // stores no later read needs: volatile keeps them
+    for (uint32_t i = threadIdx.x; i < kPoisonBytes / 4; i += 256) p[i] = 0xA5A5A5A5u;
+}
+
+void lds_poison(hipStream_t stream) {
+    static int mode = -1;
+    static unsigned blocks = 0;
+    if (mode < 0) {
+        const char* e = std::getenv("SG_LDS_POISON");
+        mode = e ? std::atoi(e) : 0;
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        blocks = 2u * (unsigned)(cus > 0 ? cus : 256);  // two 64 KB blocks per CU: 128 of its 160 KB
+        if (mode) (void)hipFuncSetAttribute((const void*)k_lds_poison, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)kPoisonBytes);
+    }
+    if (mode) hipLaunchKernelGGL(k_lds_poison, dim3(blocks), dim3(256), kPoisonBytes, stream);
+}
+
+hipError_t launch_bin_front(const BatchArgs& a, uint32_t* hist_ws, bool hist_ready, bool csum_ready, hipStream_t stream) {
+    hipError_t e = radix_bin_pass(a.rec, a.rec_sorted, a.bin_buf, a.bin_R, a.n, a.bin_dshift, hist_ws, hist_ready,
+                                  csum_ready, stream);
+    if (e != hipSuccess) return e;
+    BatchArgs b = a;
+    b.bin_tot = radix_tot(hist_ws, a.n, kBinDigit);
+    lds_poison(stream);
+    hipLaunchKernelGGL(k_bin_sort, dim3(a.bin_R + 1), dim3(kBinThreads), 0, stream, b);
+    lds_poison(stream);
+    hipLaunchKernelGGL(k_hot_update, dim3(1), dim3(1024), 0, stream, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_hot_reset(uint2* hot_tab, hipStream_t stream) {
+    hipLaunchKernelGGL(k_hot_reset, dim3(1), dim3(256), 0, stream, hot_tab);
     return hipGetLastError();
 }
 
@@ -1903,6 +2282,7 @@ hipError_t launch_seg_flow(const BatchArgs& a, hipStream_t stream) {
     if (!a.seg_marked)
         hipLaunchKernelGGL(k_seg_mark, dim3((unsigned)((a.n + 256 * kMarkItems - 1) / (256 * kMarkItems))), dim3(256), 0,
                        stream, a);
+    lds_poison(stream);
     if (a.K) hipLaunchKernelGGL(k_seg_classify, dim3(grid_for(a.K, 256 * kClsItems, 4096)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

@@ -299,6 +299,7 @@ hipError_t launch_limiter(const BatchArgs& a, const LimArgs& L, hipStream_t stre
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lim_count, dim3(ntiles), dim3(kLimThreads), 0, stream, a, L);
     hipLaunchKernelGGL(k_lim_plan, dim3(1), dim3(kLimThreads), 0, stream, a, L, ntiles);
+    lds_poison(stream);
     hipLaunchKernelGGL(k_lim_apply, dim3(ntiles), dim3(kLimThreads), 0, stream, a, L);
     return hipGetLastError();
 }
@@ -366,6 +367,7 @@ hipError_t launch_lim_arrivals(const sg_req* req, uint64_t n, uint32_t K, const 
                                uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t ntiles = (uint32_t)((n + kLimTile - 1) / kLimTile);
+    lds_poison(stream);
     hipLaunchKernelGGL((k_limx_arrivals<sg_req, LimxFlowReq>), dim3(ntiles), dim3(kLimThreads), 0, stream, req, n, K,
                        rule_lim, t_base, n_ms, counts, err);
     return hipGetLastError();
@@ -375,6 +377,7 @@ hipError_t launch_lim_arrivals_param(const sg_cparam_req* req, uint64_t n, uint3
                                      int64_t t_base, uint32_t n_ms, uint32_t* counts, int* err, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t ntiles = (uint32_t)((n + kLimTile - 1) / kLimTile);
+    lds_poison(stream);
     hipLaunchKernelGGL((k_limx_arrivals<sg_cparam_req, LimxParamReq>), dim3(ntiles), dim3(kLimThreads), 0, stream, req,
                        n, K, rule_lim, t_base, n_ms, counts, err);
     return hipGetLastError();

@@ -2835,6 +2835,7 @@ static unsigned lresident(const void* kernel) {
 }
 
 hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
+    lds_poison(stream);
     hipLaunchKernelGGL(k_local_prep, dim3((unsigned)((a.n + 256 * kLPrepItems - 1) / (256 * kLPrepItems))), dim3(256), 0,
                        stream, a);
     return hipGetLastError();
@@ -2875,8 +2876,11 @@ hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_
 
 hipError_t launch_local_exits(const LArgs& a, hipStream_t stream, bool counted) {
     const uint32_t tiles = (uint32_t)((a.n + kLTile - 1) / kLTile);
+    lds_poison(stream);
     if (!counted) hipLaunchKernelGGL(k_lexit_count, dim3(tiles), dim3(256), 0, stream, a);
+    lds_poison(stream);
     hipLaunchKernelGGL(k_lexit_scan, dim3(1), dim3(1024), 0, stream, a, tiles);
+    lds_poison(stream);
     hipLaunchKernelGGL(k_lexit_write, dim3(tiles), dim3(256), 0, stream, a);
     return hipGetLastError();
 }

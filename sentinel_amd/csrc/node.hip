@@ -173,9 +173,11 @@ __global__ void __launch_bounds__(256) k_route_gather(const sg_result* sub_out, 
 hipError_t launch_route(const RouteArgs& r, hipStream_t stream) {
     const uint32_t tiles = (uint32_t)((r.n + kRouteTile - 1) / kRouteTile);
     if (tiles == 0) return hipSuccess;
+    lds_poison(stream);
     hipLaunchKernelGGL(k_route_count, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
     hipLaunchKernelGGL(k_route_scan, dim3((unsigned)r.G), dim3(kScanThreads), 0, stream, r, tiles);
     hipLaunchKernelGGL(k_route_bases, dim3(1), dim3(64), 0, stream, r);
+    lds_poison(stream);
     hipLaunchKernelGGL(k_route_scatter, dim3(tiles), dim3(kRouteThreads), 0, stream, r);
     return hipGetLastError();
 }

@@ -274,6 +274,7 @@ hipError_t launch_pace_batch(const PaceArgs& p, uint64_t* a_buf, uint64_t* b_buf
     q.rec_sorted = sorted;
     *sorted_out = sorted;
     const uint64_t chunk = ((p.n + 2047) / 2048 + 255) / 256 * 256;  // <= 2048 blocks, whole rounds of 256
+    lds_poison(stream);
     hipLaunchKernelGGL(k_pace_seg, dim3((unsigned)((p.n + chunk - 1) / chunk)), dim3(256), 0, stream, q, chunk);
     if ((e = hipEventRecord(fork, stream)) != hipSuccess || (e = hipStreamWaitEvent(aux, fork, 0)) != hipSuccess) return e;
     const uint64_t max_long = p.n / ((uint64_t)p.short_max + 1) + 1;

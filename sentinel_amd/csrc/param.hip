@@ -353,6 +353,7 @@ hipError_t launch_param_batch(const PArgs& p, const BatchArgs& sg, uint64_t* a_b
                               int lo_bit, int hi_bit, uint64_t** sorted_out, hipStream_t stream, hipStream_t aux,
                               hipEvent_t fork, hipEvent_t join) {
     const uint64_t sentinel = p.total_slots << p.gshift;
+    lds_poison(stream);
     hipLaunchKernelGGL(k_pprep, dim3(pgrid(p.n, 8192)), dim3(256), 0, stream, p, sentinel);
     uint64_t* sorted = nullptr;
     hipError_t e = radix_sort_records(a_buf, b_buf, p.n, lo_bit, hist, &sorted, stream, hi_bit);

@@ -181,10 +181,18 @@ __global__ void __launch_bounds__(1 << D) k_rescan(uint32_t* hist, const uint32_
 // its runs' firsts (atomicMin on seg_start, 0xFFFFFFFF between batches) and its end the largest of their lasts + 1
 // (atomicMax on seg_end, 0 between batches; k_seg_classify consumes and clears both). This replaces a separate pass
 // over the sorted records (k_seg_mark).
+// BIN (the binned front half's one pass, engine.h kBinDigit): the digit is the bin digit k_prep wrote into the
+// record's middle bits; it is cleared on the way out, and the records of regular bins (digit < R) go to `reg` (k_bin_sort
+// sorts them from there into `out`), the hot bins' and rejected requests' records to `out`, at the same positions.
+struct BinSplit {
+    uint64_t* reg;
+    uint32_t R;
+};
+
 template <int D, bool MARK>
 __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* in, uint64_t* out, uint64_t n, int shift,
                                                                 const uint32_t* hist, uint32_t ntiles,
-                                                                const uint32_t* tot, SegMark mk) {
+                                                                const uint32_t* tot, SegMark mk, BinSplit bs) {
     constexpr int kBins = 1 << D;
     constexpr int kPer = kBins / kSortThreads;  // digits per thread
     using Cnt = typename std::conditional<(D > 8), uint16_t, uint32_t>::type;  // wave counts <= 1024
@@ -293,11 +301,12 @@ __global__ void __launch_bounds__(kSortThreads) k_radix_scatter(const uint64_t* 
     __syncthreads();
     // 4. write out in digit order
     const uint32_t cnt = (uint32_t)min((uint64_t)kTile, n - base);
+    const uint64_t keep = bs.reg ? ~((uint64_t)(kBins - 1) << shift) : ~0ull;
     for (uint32_t p = tid; p < cnt; p += kSortThreads) {
         const uint64_t v = stage[p];
         const uint32_t d = (uint32_t)(v >> shift) & (kBins - 1);
         const uint32_t gp = gbase[d] + (p - dstart[d]);
-        out[gp] = v;
+        (bs.reg && d < bs.R ? bs.reg : out)[gp] = v & keep;
         if constexpr (MARK) {
             const uint32_t k = (uint32_t)(v >> mk.kshift);
             if (k < mk.K) {
@@ -336,7 +345,7 @@ int radix_digit_bits(int bits) { return ((bits > 16 && bits <= 20) || (bits > 24
 
 template <int D>
 static hipError_t radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift, uint32_t* hist_ws, hipStream_t stream,
-                       bool hist_ready, const SegMark* mark, bool csum_ready) {
+                       bool hist_ready, const SegMark* mark, bool csum_ready, BinSplit bs = BinSplit{}) {
     const uint32_t ntiles = (uint32_t)((n + kTile - 1) / kTile);
     const uint32_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
     uint32_t* hist = hist_ws;                                   // [ntiles][bins], then run offsets in place
@@ -348,6 +357,7 @@ static hipError_t radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift
             const hipError_t e = hipMemsetAsync(csum, 0, radix_csum_bytes(n, D), stream);
             if (e != hipSuccess) return e;
         }
+        lds_poison(stream);
         hipLaunchKernelGGL(k_radix_hist<D>, dim3(ntiles), dim3(kSortThreads), 0, stream, src, n, shift, hist, ntiles,
                            atom ? csum : nullptr);
         csum_ready = atom;
@@ -356,13 +366,29 @@ static hipError_t radix_pass(uint64_t* src, uint64_t* dst, uint64_t n, int shift
     hipLaunchKernelGGL(k_chunkscan<D>, dim3((1u << D) / 64), dim3(1024), 0, stream, csum, nchunks, tot);
     hipLaunchKernelGGL(k_rescan<D>, dim3(nchunks), dim3(1u << D), 0, stream, hist, csum, ntiles);
     const uint32_t grid = 8 * ((ntiles + 7) / 8);  // xcd_tile: blocks past ntiles return at once
+    lds_poison(stream);
     if (mark)
         hipLaunchKernelGGL((k_radix_scatter<D, true>), dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift,
-                           hist, ntiles, tot, *mark);
+                           hist, ntiles, tot, *mark, BinSplit{});
     else
         hipLaunchKernelGGL((k_radix_scatter<D, false>), dim3(grid), dim3(kSortThreads), 0, stream, src, dst, n, shift,
-                           hist, ntiles, tot, SegMark{});
+                           hist, ntiles, tot, SegMark{}, bs);
     return hipGetLastError();
+}
+
+// The digit totals radix_pass<D> leaves in hist_ws (k_chunkscan), [1 << D].
+const uint32_t* radix_tot(const uint32_t* hist_ws, uint64_t n, int D) {
+    const uint64_t ntiles = (n + kTile - 1) / kTile;
+    const uint64_t nchunks = (ntiles + kChunkTiles - 1) / kChunkTiles;
+    return hist_ws + (size_t)(ntiles + nchunks) * (1ull << D);
+}
+
+// The binned front half's scatter pass (engine.h kBinDigit): records by bin digit at bit `shift`, regular bins
+// (digit < R) into `reg`, the rest into `out`.
+hipError_t radix_bin_pass(uint64_t* src, uint64_t* out, uint64_t* reg, uint32_t R, uint64_t n, int shift,
+                          uint32_t* hist_ws, bool hist_ready, bool csum_ready, hipStream_t stream) {
+    static_assert(kBinDigit == 10, "radix_pass<10>");
+    return radix_pass<10>(src, out, n, shift, hist_ws, stream, hist_ready, nullptr, csum_ready, BinSplit{reg, R});
 }
 
 // Sorts n records on bits [lo_bit, hi_bit) (bits above hi_bit must be zero or already grouped),

@@ -323,7 +323,16 @@ def test_radix_sort_is_stable_partition_by_flow(n_keys, n):
     rec, kshift = _host_records(req, n_keys, max_batch)
     want = rec[np.argsort(rec >> np.uint64(kshift), kind="stable")]
     got = eng.debug_copy(1, np.uint64, n)
-    assert np.array_equal(got, want)
+    assert_stable_partition(got, want, kshift)
+
+
+def assert_stable_partition(got, want, kshift):
+    """`got` holds every flowId's records contiguous and in arrival order (the two-pass sort: in flowId order; the binned
+    front half: regular bins in flowId order, then one segment per hot flowId)."""
+    keys = got >> np.uint64(kshift)
+    runs = 1 + int(np.count_nonzero(keys[1:] != keys[:-1])) if len(keys) else 0
+    assert runs == len(np.unique(keys)), "a flowId's records are split"
+    assert np.array_equal(got[np.argsort(keys, kind="stable")], want)
 
 
 def _ns_multi(specs):
