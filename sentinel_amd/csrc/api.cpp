@@ -44,6 +44,7 @@ struct sg_handle {
     uint64_t rules_gen = 0;           // flow rule loads so far (a reload renumbers flowIds: the hot set restarts)
     uint64_t* d_bin_buf = nullptr;
     int bin_mode = 1;                 // env SG_BIN: 0 off, 1 on for >= 2^14 flowIds, 2 on whenever the records allow
+    int prep_tiles = 4;               // env SG_PREP_TILES: sort tiles per k_prep block on the binned path
 
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
@@ -324,7 +325,8 @@ struct sg_handle {
     bool d2h_kernel = false;          // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=1; the
                                       // copy engine measured faster: 2.64 vs 2.45 G decisions/s end to end)
     int d2h_blocks = 64;              // its workgroups (env SG_D2H_BLOCKS)
-    int front_eighths = 3;            // CU partition of the pipeline streams (pipe_setup; round 4, final kernels: 3/8 beats 4/8 by 1.1 %)
+    int front_eighths = 4;            // CU partition of the pipeline streams (pipe_setup; round 6: the binned front half
+                                      // (k_bin_sort) takes 4/8, -2.5 % against 3/8; the two-pass sort measures the same at 3 or 4)
     int walk_cus = 0;                 // CUs of the walkers' streams when partitioned (0 = all)
     struct DevTicket {                // sg_flow_enqueue batches in flight
         uint64_t ticket = 0;
@@ -558,6 +560,7 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (const char* d = std::getenv("SG_SEG_MARK")) h->seg_mark_pass = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_LIM_PIPE")) h->lim_pipe = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_BIN")) h->bin_mode = std::atoi(d);
+    if (const char* d = std::getenv("SG_PREP_TILES")) h->prep_tiles = std::max(1, std::min(64, std::atoi(d)));
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -1421,6 +1424,7 @@ bool bin_setup(sg_handle* h, sg_handle::FlowWs& w, BatchArgs& a, hipStream_t str
         h->hot_gen = h->rules_gen;
     }
     a.bin_on = 1;
+    a.prep_tiles = h->prep_tiles;
     a.bin_dshift = h->abits + h->ibits;
     a.bin_bsh = bsh;
     a.bin_R = ((h->K - 1) >> bsh) + 1;

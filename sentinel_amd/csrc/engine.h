@@ -151,6 +151,7 @@ struct BatchArgs {
     // scatter pass; hot bins hold one flowId each, already in order, the regular bins are sorted in LDS by k_bin_sort.
     int hist0_shift;       // k_prep's histogram digit: (rec >> hist0_shift) & mask (kshift, or bin_dshift)
     int bin_on;
+    int prep_tiles;        // tiles (of the sort's 4096 records) per k_prep block on the binned path (env SG_PREP_TILES)
     int bin_dshift;
     int bin_bsh;
     uint32_t bin_R;        // regular bins [0, R) (R = ((K - 1) >> bin_bsh) + 1 <= kBinRegular)
@@ -165,10 +166,15 @@ constexpr uint32_t kBinRegular = 512;                // regular bins (key ranges
 constexpr uint32_t kBinHot = (1u << kBinDigit) - kBinRegular - 1;  // hot slots: one flowId each
 constexpr uint32_t kBinDrop = (1u << kBinDigit) - 1; // rejected requests
 constexpr int kBinMaxBsh = 11;                       // keys per regular bin <= 2048 (k_bin_sort's LDS counters)
-constexpr int kHotTabBits = 10;                      // the hot set's table: <= kBinHot keys in 1024 slots
-constexpr uint32_t kHotTab = 1u << kHotTabBits;
+// The hot set's table: 512 buckets of 4 {flowId, slot} entries (16 KB), a flowId only in its home bucket (k_hot_update
+// leaves a flowId whose bucket is full out of the hot set), so k_prep's lookup is two independent 16-B LDS reads.
+constexpr int kHotBucketBits = 9;
+constexpr uint32_t kHotWays = 4;
+constexpr uint32_t kHotTab = kHotWays << kHotBucketBits;
 constexpr uint32_t kHotEmpty = 0xFFFFFFFFu;
-__host__ __device__ __forceinline__ uint32_t hot_hash(uint32_t key) { return (key * 2654435761u) >> (32 - kHotTabBits); }
+__host__ __device__ __forceinline__ uint32_t hot_hash(uint32_t key) {
+    return (key * 2654435761u) >> (32 - kHotBucketBits);
+}
 
 constexpr int kLongPeriods = 16;       // period-end table of the wave walker: batches of <= 16 window periods
 constexpr uint32_t kLongTab = 65536;  // long segments with a table (later ones search)

@@ -104,30 +104,29 @@ __device__ __forceinline__ Decoded decode_c(const BatchArgs& a, uint32_t c) {
 constexpr int kPrepItems = kSortRounds;  // k_prep's tile is the sort's (its first-pass histogram rows)
 constexpr uint32_t kPrepTile = 256 * kPrepItems;
 
-// BIN (the binned front half): each record also gets its bin digit (a.bin_on, see k_bin_sort) — after the main loop,
-// so that the hot-flowId table's loads (issued first, staged in LDS after the loop) ride with the requests' loads
-// instead of adding a round trip before them.
+// BIN (the binned front half): each record also gets its bin digit (a.bin_on, see k_bin_sort): the flowId's hot slot
+// from the hot-flowId table, staged in LDS once per block (a block takes kPrepBinTiles tiles), else its key range.
 template <bool BIN>
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
     __shared__ uint32_t dcnt[1024];
-    __shared__ uint2 htab[BIN ? kHotTab : 1];  // the hot flowIds: a short LDS probe per request
-    constexpr int kTabPer = BIN ? (int)kHotTab / 256 : 1;
-    uint2 tv[kTabPer];
-    if constexpr (BIN) {
-#pragma unroll
-        for (int u = 0; u < kTabPer; ++u) tv[u] = a.hot_tab[u * 256 + threadIdx.x];
-    }
+    __shared__ alignas(16) uint2 htab[BIN ? kHotTab : 1];  // the hot flowIds: two 16-B LDS reads per request
+    if constexpr (BIN)
+        for (uint32_t x = threadIdx.x; x < kHotTab; x += 256) htab[x] = a.hot_tab[x];
     const uint64_t n = a.n;
     const int64_t t0 = a.req[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
     const uint32_t dmask = (1u << a.hist0_bits) - 1u;
+    const uint32_t kTiles = BIN ? (uint32_t)a.prep_tiles : 1u;
+#pragma unroll 1
+    for (uint32_t tt = 0; tt < kTiles; ++tt) {
+    const uint32_t tile = blockIdx.x * kTiles + tt;
+    if ((uint64_t)tile * kPrepTile >= n) break;
+    if (tt) __syncthreads();  // the previous tile's histogram row is written
     if (a.hist0)
         for (uint32_t d = threadIdx.x; d <= dmask; d += 256) dcnt[d] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kPrepTile;
-    uint64_t rv[BIN ? kPrepItems : 1];
-    constexpr int kUnroll = BIN ? kPrepItems : 4;  // BIN: rv[] stays in registers
-#pragma unroll kUnroll
+    const uint64_t base = (uint64_t)tile * kPrepTile;
+#pragma unroll 4
     for (int it = 0; it < kPrepItems; ++it) {
         const uint64_t i = base + (uint64_t)it * 256 + threadIdx.x;
         if (i >= n) break;
@@ -166,6 +165,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         const uint32_t key = r.key & SG_KEY_INDEX;
         uint64_t rec;
         int32_t st;
+        uint32_t d = kBinDrop;  // BIN: a rejected request's bin
         if (key == SG_KEY_BAD || r.acquire <= 0) {
             st = SG_STATUS_BAD_REQUEST;
             rec = sentinel;
@@ -178,58 +178,38 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             const uint64_t ac = (q << 1) | (uint64_t)(r.key >> 31);
             rec = ((uint64_t)key << a.kshift) | ((uint64_t)i << a.abits) | ac;
             st = SG_STATUS_BLOCKED;  // walkers write only non-BLOCKED
+            if constexpr (BIN) {  // the flowId's hot slot, else its key range
+                d = key >> a.bin_bsh;
+                if (!(a.dbg & 131072)) {  // (timing experiment: no hot lookup, every flowId regular)
+                    const uint4* hb = reinterpret_cast<const uint4*>(htab + hot_hash(key) * kHotWays);
+                    const uint4 e0 = hb[0], e1 = hb[1];
+                    d = e0.x == key ? a.bin_R + e0.y : d;
+                    d = e0.z == key ? a.bin_R + e0.w : d;
+                    d = e1.x == key ? a.bin_R + e1.y : d;
+                    d = e1.z == key ? a.bin_R + e1.w : d;
+                }
+            }
         }
+        if constexpr (BIN) rec |= (uint64_t)d << a.bin_dshift;
         if (!(a.dbg & 16384)) {
             int32_t* o = &a.out[i].status;  // the default result {st, 0, 0}
             st_stream(o, st);
             st_stream(o + 1, 0);
             st_stream(o + 2, 0);
         }
-        if constexpr (BIN) {
-            rv[it] = rec;
-        } else {
-            st_stream(a.rec + i, rec);
-            if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.hist0_shift) & dmask], 1u);
-        }
-    }
-    if constexpr (BIN) {
-#pragma unroll
-        for (int u = 0; u < kTabPer; ++u) htab[u * 256 + threadIdx.x] = tv[u];
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < kPrepItems; ++it) {
-            const uint64_t i = base + (uint64_t)it * 256 + threadIdx.x;
-            if (i >= n) break;
-            uint64_t rec = rv[it];
-            const uint32_t key = (uint32_t)(rec >> a.kshift);
-            uint32_t d = kBinDrop;  // a rejected request: its own bin
-            if (key < a.K) {        // the flowId's hot slot, else its key range
-                d = key >> a.bin_bsh;
-                uint32_t x = hot_hash(key);
-                for (uint32_t probe = 0; probe < kHotTab; ++probe) {  // linear probing, load <= 1/2
-                    const uint2 e = htab[x];
-                    if (e.x == key) {
-                        d = a.bin_R + e.y;
-                        break;
-                    }
-                    if (e.x == kHotEmpty) break;
-                    x = (x + 1) & (kHotTab - 1);
-                }
-            }
-            rec |= (uint64_t)d << a.bin_dshift;
-            st_stream(a.rec + i, rec);
-            atomicAdd(&dcnt[d], 1u);
-        }
+        st_stream(a.rec + i, rec);
+        if (a.hist0) atomicAdd(&dcnt[BIN ? d : (uint32_t)(rec >> a.hist0_shift) & dmask], 1u);
     }
     if (a.hist0) {
         __syncthreads();
-        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)blockIdx.x * (dmask + 1) + d] = dcnt[d];
+        for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)tile * (dmask + 1) + d] = dcnt[d];
         if (a.csum0) {  // the chunk's column sums (zeroed before the launch): no k_colsum pass for the first digit
-            uint32_t* cs = a.csum0 + (size_t)(blockIdx.x / kChunkTiles) * (dmask + 1);
+            uint32_t* cs = a.csum0 + (size_t)(tile / kChunkTiles) * (dmask + 1);
             for (uint32_t d = threadIdx.x; d <= dmask; d += 256)
                 if (dcnt[d]) atomicAdd(cs + d, dcnt[d]);
         }
     }
+    }  // tiles
 }
 
 // ------------------------------------------------------------------------------------ the decision
@@ -1021,7 +1001,11 @@ constexpr uint32_t kBinKeys = 1u << kBinMaxBsh;
 constexpr int kBinThreads = 512;
 constexpr int kBinWaves = kBinThreads / 64;
 constexpr int kBinPer = kBinKeys / kBinThreads;  // keys per thread in the scan (contiguous)
-constexpr int kBinRows = 24;                     // 64-record rows a lane holds at once (a wave's whole quarter, usually)
+constexpr int kBinRows = 48;                     // 64-record rows a lane holds in registers
+constexpr uint32_t kBinRegCap = kBinWaves * 64 * kBinRows;  // bins up to this size take the LDS path (24576)
+constexpr uint32_t kBinStage = 14336;            // records of one output window staged in LDS (112 KB)
+constexpr uint32_t kBinLdsWords = (kBinWaves * kBinKeys * 2 + kBinStage * 8) / 8;  // u16 counters + stage, in u64
+static_assert(kBinWaves * kBinKeys * 4 <= kBinLdsWords * 8, "the big path's u32 counters fit the same LDS");
 
 // Exclusive scan of the 1024 digit totals into dbase (every block: 4 KB, L2-resident).
 __device__ __forceinline__ void bin_digit_bases(const BatchArgs& a, uint32_t* dbase, uint32_t* wsum) {
@@ -1051,26 +1035,107 @@ __device__ __forceinline__ void bin_digit_bases(const BatchArgs& a, uint32_t* db
     __syncthreads();
 }
 
-// Lanes of this wave whose `bits`-bit local key equals this lane's (wave-uniform bits <= kBinMaxBsh).
-__device__ __forceinline__ uint64_t match_key(uint32_t d, int bits) {
+// Lanes of this wave whose local key (< 2^kBinMaxBsh) equals this lane's: kBinMaxBsh ballots, branch-free (the
+// bits above the bin's bsh are 0 in every lane and change nothing).
+__device__ __forceinline__ uint64_t match_key(uint32_t d) {
     uint64_t peers = ~0ull;
 #pragma unroll
     for (int b = 0; b < kBinMaxBsh; ++b) {
-        if (b < bits) {
-            const uint64_t m = __ballot((d >> b) & 1u);
-            peers &= ((d >> b) & 1u) ? m : ~m;
-        }
+        const uint64_t m = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? m : ~m;
     }
     return peers;
 }
 
+// Counters of the LDS path: u16 per (wave, flowId). Counted by 32-bit LDS atomics on the word holding two of them
+// (1 << 16 for an odd index; a bin of <= kBinRegCap records keeps every count below 2^16, so no carry crosses), read
+// and written as u16 only after a barrier: every access of the scan and of the placement has the same type, so the
+// compiler keeps a wave's read of a counter after its earlier write (type-based alias analysis would let a u32 read
+// pass a u16 store, and the placement's ranks depend on that order).
+struct Cnt16 {
+    uint32_t* w;
+    __device__ __forceinline__ uint32_t get(uint32_t i) const { return reinterpret_cast<const uint16_t*>(w)[i]; }
+    __device__ __forceinline__ void inc(uint32_t i) const { atomicAdd(&w[i >> 1], 1u << ((i & 1) * 16)); }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t v) const {
+        reinterpret_cast<uint16_t*>(w)[i] = (uint16_t)v;
+    }
+};
+
+// The per-flowId exclusive scan of a regular bin (thread tid's kBinPer contiguous flowIds), each flowId's per-wave
+// bases written over its counters, and each segment's list slot within the block (wave ballots per class, lcnt).
+template <class CNT>
+__device__ __forceinline__ void bin_scan_lists(const BatchArgs& a, CNT cnt, uint32_t nk, uint32_t* wsum, uint32_t* lcnt,
+                                               uint32_t* tk, uint32_t* sst, uint32_t* slot) {
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        const uint32_t j = (uint32_t)tid * kBinPer + i;
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kBinWaves; ++w) t += cnt.get((uint32_t)w * kBinKeys + j);
+        tk[i] = t;
+        sum += t;
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();  // (wsum: the digit bases' scan is done with it)
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int w = 0; w < wave; ++w) run += wsum[w];
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        const uint32_t j = (uint32_t)tid * kBinPer + i;
+        sst[i] = run;
+        uint32_t pre = run;
+#pragma unroll
+        for (int w = 0; w < kBinWaves; ++w) {
+            const uint32_t c = cnt.get((uint32_t)w * kBinKeys + j);
+            cnt.set((uint32_t)w * kBinKeys + j, pre);
+            pre += c;
+        }
+        run += tk[i];
+        const uint32_t l = (tk[i] && j < nk) ? seg_class(a, tk[i]) : 0xFFu;
+        slot[i] = 0xFFFFFFFFu;
+#pragma unroll
+        for (int c = 0; c <= kClasses; ++c) {  // wave-aggregated slots per class
+            const uint64_t m = __ballot(l == (uint32_t)c);
+            if (!m) continue;
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(&lcnt[c], (uint32_t)__popcll(m));
+            b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+            if (l == (uint32_t)c) slot[i] = ((uint32_t)c << 24) | (b + (uint32_t)__popcll(m & lt));
+        }
+    }
+}
+
+__device__ __forceinline__ void bin_emit(const BatchArgs& a, const uint32_t* lbase, uint32_t s0, uint32_t kb0,
+                                         const uint32_t* tk, const uint32_t* sst, const uint32_t* slot) {
+#pragma unroll
+    for (int i = 0; i < kBinPer; ++i) {
+        if (slot[i] == 0xFFFFFFFFu) continue;
+        const uint32_t l = slot[i] >> 24;
+        seg_emit(a, l, lbase[l] + (slot[i] & 0xFFFFFFu), s0 + sst[i], s0 + sst[i] + tk[i],
+                 kb0 + (uint32_t)threadIdx.x * kBinPer + i);
+    }
+}
+
 // Blocks [0, R): regular bin b — a stable counting sort by flowId: wave w takes the w-th eighth of the bin in order and
-// keeps its own counters, so its records of a flowId follow the earlier waves' ones. A wave's eighth (<= kBinRows rows,
-// the usual case) is loaded once, all rows at once, and kept in registers for both the count and the placement; longer
-// ones (a flowId that outgrew the hot set) go by groups of kBinRows rows, read twice. Block R: the hot bins' segments.
-__global__ void __launch_bounds__(kBinThreads) k_bin_sort(BatchArgs a) {
+// keeps its own counters, so its records of a flowId follow the earlier waves' ones. A bin of <= kBinRegCap records
+// (the usual case) is read once into registers, all rows at once; every record's position is found there (ballot
+// ranks, the wave's running counters), and the sorted bin leaves through LDS in windows of kBinStage records, one
+// coalesced stream. A larger bin (a flowId that outgrew the hot set) counts in u32, reads its rows twice in groups and
+// stores each record straight to its position. The list slots' global atomics (one per class per block) are issued
+// before the placement and waited for after it. Block R: the hot bins' segments (one flowId each, in order already).
+__global__ void __launch_bounds__(kBinThreads, 1) k_bin_sort(BatchArgs a) {
     constexpr int kL = kClasses + 1;
-    __shared__ uint32_t cnt[kBinWaves][kBinKeys];
+    __shared__ uint64_t lds[kBinLdsWords];
     __shared__ uint32_t dbase[1 << kBinDigit];
     __shared__ uint32_t wsum[kBinWaves];
     __shared__ uint32_t lcnt[kL], lbase[kL];
@@ -1079,7 +1144,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_sort(BatchArgs a) {
     if (tid < kL) lcnt[tid] = 0;
     bin_digit_bases(a, dbase, wsum);
     const uint32_t b = blockIdx.x;
-    if (b >= a.bin_R) {  // the hot bins: one flowId each, in order already
+    if (b >= a.bin_R) {  // the hot bins
         constexpr int kHR = (kBinHot + kBinThreads - 1) / kBinThreads;
         uint32_t slot[kHR];
 #pragma unroll
@@ -1110,108 +1175,138 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_sort(BatchArgs a) {
     }
     const uint32_t s0 = dbase[b], len = a.bin_tot[b];
     if (len == 0) return;
+    const bool diag = (a.dbg & 65536) != 0;  // per-phase wall clock of the regular bins (dbg_ctr[40..47])
+    uint64_t tk0 = diag ? __builtin_amdgcn_s_memrealtime() : 0, tk1 = 0, tk2 = 0, tk3 = 0, tp4 = 0, tp5 = 0, tp6 = 0;
     const int bsh = a.bin_bsh;
     const uint32_t kb0 = b << bsh;
     const uint32_t nk = min(1u << bsh, a.K - kb0);
     const uint32_t C = (len + kBinWaves - 1) / kBinWaves;
     const uint32_t c0 = s0 + min((uint32_t)wave * C, len), c1 = s0 + min((uint32_t)(wave + 1) * C, len);
-    const bool one = C <= 64u * kBinRows;  // every wave's eighth fits its registers
-    const uint32_t last = s0 + len - 1;    // loads are clamped into the bin (unconditional: no phi waits)
+    const bool small = len <= kBinRegCap;
+    const uint32_t last = s0 + len - 1;  // loads are clamped into the bin (unconditional: no phi waits)
     const uint64_t* src = a.bin_buf;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t* lw = reinterpret_cast<uint32_t*>(lds);
     uint64_t v[kBinRows];
-    // 0. the first (usually only) group of rows: issued before the counters are cleared
 #pragma unroll
     for (int u = 0; u < kBinRows; ++u) v[u] = src[min(c0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
-    for (uint32_t j = tid; j < (uint32_t)kBinWaves * kBinKeys; j += kBinThreads) (&cnt[0][0])[j] = 0;
+    const uint32_t zw = small ? kBinWaves * kBinKeys / 2 : kBinWaves * kBinKeys;  // counter words
+    for (uint32_t j = tid; j < zw; j += kBinThreads) lw[j] = 0;
     __syncthreads();
-    // 1. counts per (wave, flowId)
-    for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
-        if (r0 != c0) {
-#pragma unroll
-            for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
-        }
+    if (diag) tk1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t tk[kBinPer], sst[kBinPer], slot[kBinPer], gb = 0;
+    if (small) {
+        const Cnt16 cnt{lw};
+        // 1. counts per (wave, flowId)
 #pragma unroll
         for (int u = 0; u < kBinRows; ++u) {
-            const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
-            if (j < c1) atomicAdd(&cnt[wave][(uint32_t)(v[u] >> a.kshift) - kb0], 1u);
+            const uint32_t j = c0 + (uint32_t)u * 64 + (uint32_t)lane;
+            if (j < c1) cnt.inc((uint32_t)wave * kBinKeys + (uint32_t)(v[u] >> a.kshift) - kb0);
         }
-    }
-    __syncthreads();
-    // 2. segment starts (exclusive scan over flowIds, tid's kBinPer contiguous flowIds), per-wave bases, list entries
-    uint32_t tk[kBinPer], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kBinPer; ++i) {
-        const uint32_t j = (uint32_t)tid * kBinPer + i;
-        uint32_t t = 0;
-#pragma unroll
-        for (int w = 0; w < kBinWaves; ++w) t += cnt[w][j];
-        tk[i] = t;
-        sum += t;
-    }
-    uint32_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t run = x - sum;
-    for (int w = 0; w < wave; ++w) run += wsum[w];
-    uint32_t slot[kBinPer], sst[kBinPer];
-#pragma unroll
-    for (int i = 0; i < kBinPer; ++i) {
-        const uint32_t j = (uint32_t)tid * kBinPer + i;
-        sst[i] = run;
-        uint32_t pre = run;
-#pragma unroll
-        for (int w = 0; w < kBinWaves; ++w) {
-            const uint32_t c = cnt[w][j];
-            cnt[w][j] = pre;
-            pre += c;
-        }
-        slot[i] = 0xFFFFFFFFu;
-        if (tk[i] && j < nk) {
-            const uint32_t l = seg_class(a, tk[i]);
-            slot[i] = (l << 24) | atomicAdd(&lcnt[l], 1u);
-        }
-        run += tk[i];
-    }
-    __syncthreads();
-    if (tid < kL) {
-        const uint32_t t = lcnt[tid];
-        uint32_t* ctr = tid == kClasses ? a.long_count : a.short_count + tid;
-        lbase[tid] = t ? atomicAdd(ctr, t) : 0u;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kBinPer; ++i) {
-        if (slot[i] == 0xFFFFFFFFu) continue;
-        const uint32_t l = slot[i] >> 24;
-        seg_emit(a, l, lbase[l] + (slot[i] & 0xFFFFFFu), s0 + sst[i], s0 + sst[i] + tk[i],
-                 kb0 + (uint32_t)tid * kBinPer + i);
-    }
-    // 3. stable placement: each wave goes over its eighth again in order, 64 records a round; the rank among equal
-    // flowIds of a round comes from ballots, the wave's own running counter (LDS ops of one wave execute in order) does
-    // the rest
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t* dst = a.rec_sorted + s0;
-    for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
-        if (!one) {
-#pragma unroll
-            for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
-        }
+        __syncthreads();
+        if (diag) tk2 = __builtin_amdgcn_s_memrealtime();
+        // 2. segment starts and list slots; the list atomics issued now, waited for after the placement
+        bin_scan_lists(a, cnt, nk, wsum, lcnt, tk, sst, slot);
+        __syncthreads();
+        if (tid < kL && lcnt[tid]) gb = atomicAdd(tid == kClasses ? a.long_count : a.short_count + tid, lcnt[tid]);
+        if (diag) tk3 = __builtin_amdgcn_s_memrealtime();
+        // 3. positions (ballot ranks, the wave's running counters: LDS ops of one wave execute in order)
+        uint32_t pos[kBinRows / 2];  // two u16 positions per register (< kBinRegCap; 0xFFFF: no record)
 #pragma unroll
         for (int u = 0; u < kBinRows; ++u) {
-            const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
+            const uint32_t j = c0 + (uint32_t)u * 64 + (uint32_t)lane;
             const bool valid = j < c1;
             const uint32_t d = valid ? (uint32_t)(v[u] >> a.kshift) - kb0 : 0u;
-            const uint64_t peers = match_key(d, bsh) & __ballot(valid);
-            const uint32_t c = cnt[wave][d];
-            if (valid) {
-                dst[c + (uint32_t)__popcll(peers & lt)] = v[u];
-                if (lane == __builtin_ctzll(peers)) cnt[wave][d] = c + (uint32_t)__popcll(peers);
+            const uint64_t peers = match_key(d) & __ballot(valid);
+            const uint32_t ci = (uint32_t)wave * kBinKeys + d;
+            const uint32_t c = cnt.get(ci);
+            const uint32_t p16 = valid ? c + (uint32_t)__popcll(peers & lt) : 0xFFFFu;
+            pos[u / 2] = (u & 1) ? (pos[u / 2] | (p16 << 16)) : p16;
+            // every lane writes its key's new count: peers write the same value, and an invalid lane (d = 0) writes
+            // the count of the valid key-0 lanes or, without any, the count it read
+            cnt.set(ci, c + (uint32_t)__popcll(peers));
+            __builtin_amdgcn_sched_barrier(0);  // row by row: hoisting every row's ballots spilled them
+        }
+        if (diag) tp4 = __builtin_amdgcn_s_memrealtime();
+        // 4. the sorted bin through LDS, kBinStage records at a time (the stage lies past the counters)
+        uint64_t* stage = lds + (kBinWaves * kBinKeys * 2) / 8;
+        uint64_t* dst = a.rec_sorted + s0;
+        for (uint32_t w0 = 0; w0 < len; w0 += kBinStage) {
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) {
+                const uint32_t p = (pos[u / 2] >> ((u & 1) * 16)) & 0xFFFFu;
+                if (p != 0xFFFFu && p - w0 < kBinStage) stage[p - w0] = v[u];
             }
+            __syncthreads();
+            const uint32_t m = min(kBinStage, len - w0);
+            for (uint32_t p = tid; p < m; p += kBinThreads) dst[w0 + p] = stage[p];
+            __syncthreads();
+        }
+    } else {
+        uint32_t(*cnt)[kBinKeys] = reinterpret_cast<uint32_t(*)[kBinKeys]>(lw);
+        struct Cnt32 {
+            uint32_t* w;
+            __device__ __forceinline__ uint32_t get(uint32_t i) const { return w[i]; }
+            __device__ __forceinline__ void set(uint32_t i, uint32_t x) const { w[i] = x; }
+        } c32{lw};
+        for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
+            if (r0 != c0) {
+#pragma unroll
+                for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
+            }
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) {
+                const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
+                if (j < c1) atomicAdd(&cnt[wave][(uint32_t)(v[u] >> a.kshift) - kb0], 1u);
+            }
+        }
+        __syncthreads();
+        if (diag) tk2 = __builtin_amdgcn_s_memrealtime();
+        bin_scan_lists(a, c32, nk, wsum, lcnt, tk, sst, slot);
+        __syncthreads();
+        if (tid < kL && lcnt[tid]) gb = atomicAdd(tid == kClasses ? a.long_count : a.short_count + tid, lcnt[tid]);
+        if (diag) tk3 = __builtin_amdgcn_s_memrealtime();
+        uint64_t* dst = a.rec_sorted + s0;
+        for (uint32_t r0 = c0; r0 < c1; r0 += 64u * kBinRows) {
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) v[u] = src[min(r0 + (uint32_t)u * 64 + (uint32_t)lane, last)];
+#pragma unroll
+            for (int u = 0; u < kBinRows; ++u) {
+                const uint32_t j = r0 + (uint32_t)u * 64 + (uint32_t)lane;
+                const bool valid = j < c1;
+                const uint32_t d = valid ? (uint32_t)(v[u] >> a.kshift) - kb0 : 0u;
+                const uint64_t peers = match_key(d) & __ballot(valid);
+                const uint32_t c = cnt[wave][d];
+                if (valid) {
+                    dst[c + (uint32_t)__popcll(peers & lt)] = v[u];
+                    if (lane == __builtin_ctzll(peers)) cnt[wave][d] = c + (uint32_t)__popcll(peers);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    if (diag) tp5 = __builtin_amdgcn_s_memrealtime();
+    if (tid < kL) lbase[tid] = gb;
+    __syncthreads();
+    if (diag) tp6 = __builtin_amdgcn_s_memrealtime();
+    bin_emit(a, lbase, s0, kb0, tk, sst, slot);
+    if (diag) {
+        __syncthreads();
+        if (tid == 0) {
+            const uint64_t tk4 = __builtin_amdgcn_s_memrealtime();
+            if (small) {
+                atomicAdd(&a.dbg_ctr[48], (unsigned long long)(tp4 - tk3));
+                atomicAdd(&a.dbg_ctr[49], (unsigned long long)(tp5 - tp4));
+                atomicAdd(&a.dbg_ctr[50], (unsigned long long)(tp6 - tp5));
+                atomicAdd(&a.dbg_ctr[51], (unsigned long long)(tk4 - tp6));
+            }
+            atomicAdd(&a.dbg_ctr[40], (unsigned long long)(tk1 - tk0));
+            atomicAdd(&a.dbg_ctr[41], (unsigned long long)(tk2 - tk1));
+            atomicAdd(&a.dbg_ctr[42], (unsigned long long)(tk3 - tk2));
+            atomicAdd(&a.dbg_ctr[43], (unsigned long long)(tk4 - tk3));
+            atomicAdd(&a.dbg_ctr[44], 1ull);
+            atomicAdd(&a.dbg_ctr[45], small ? 0ull : 1ull);
+            atomicAdd(&a.dbg_ctr[47], (unsigned long long)len);
         }
     }
 }
@@ -1222,11 +1317,15 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_sort(BatchArgs a) {
 __global__ void __launch_bounds__(1024) k_hot_update(BatchArgs a) {
     __shared__ uint32_t hcnt[32];
     __shared__ uint32_t thr, nslot;
-    __shared__ uint32_t tkey[kHotTab], tslot[kHotTab];
+    __shared__ uint32_t tkey[kHotTab], tslot[kHotTab], bfill[kHotTab / kHotWays];
     const uint32_t tid = threadIdx.x;
     if (tid < 32) hcnt[tid] = 0;
     if (tid == 0) nslot = 0;
-    for (uint32_t x = tid; x < kHotTab; x += 1024) tkey[x] = kHotEmpty;
+    for (uint32_t x = tid; x < kHotTab; x += 1024) {
+        tkey[x] = kHotEmpty;
+        tslot[x] = 0;
+    }
+    for (uint32_t x = tid; x < kHotTab / kHotWays; x += 1024) bfill[x] = 0;
     __syncthreads();
     const uint32_t nl = *a.err ? 0u : *a.long_count;  // a refused batch listed nothing: no hot flowIds next
     for (uint32_t i = tid; i < nl; i += 1024) {
@@ -1251,16 +1350,19 @@ __global__ void __launch_bounds__(1024) k_hot_update(BatchArgs a) {
             const uint32_t len = a.long_end[i] - a.long_list[i];
             const uint32_t c = 31 - __clz(len);
             if (pass == 0 ? c <= thr : c != thr) continue;
-            const uint32_t s = atomicAdd(&nslot, 1u);
-            if (s >= kBinHot) continue;
+            if (nslot >= kBinHot) continue;  // (a stale read only costs a wasted attempt)
             const uint32_t k = a.long_key[i];
-            a.hot_key[s] = k;
-            for (uint32_t x = hot_hash(k);; x = (x + 1) & (kHotTab - 1)) {  // kBinHot < kHotTab: a free slot exists
-                if (atomicCAS(&tkey[x], kHotEmpty, k) == kHotEmpty) {
-                    tslot[x] = s;
-                    break;
-                }
+            const uint32_t bk = hot_hash(k);
+            const uint32_t w = atomicAdd(&bfill[bk], 1u);
+            if (w >= kHotWays) continue;  // home bucket full: the flowId stays in its regular bin
+            const uint32_t s = atomicAdd(&nslot, 1u);
+            if (s >= kBinHot) {
+                tkey[bk * kHotWays + w] = kHotEmpty;  // (this way stays empty)
+                continue;
             }
+            a.hot_key[s] = k;
+            tkey[bk * kHotWays + w] = k;
+            tslot[bk * kHotWays + w] = s;
         }
         __syncthreads();
     }
@@ -2227,7 +2329,11 @@ static unsigned grid_for(uint64_t n, unsigned block, unsigned cap) {
 
 hipError_t launch_prep(const BatchArgs& a, hipStream_t stream) {
     lds_poison(stream);
-    if (a.bin_on) hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
+    if (a.bin_on) {
+        const uint64_t tiles = (a.n + kPrepTile - 1) / kPrepTile;
+        hipLaunchKernelGGL(k_prep<true>, dim3((unsigned)((tiles + a.prep_tiles - 1) / a.prep_tiles)), dim3(256), 0,
+                           stream, a);
+    }
     else hipLaunchKernelGGL(k_prep<false>, dim3((unsigned)((a.n + kPrepTile - 1) / kPrepTile)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
