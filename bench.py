@@ -77,7 +77,7 @@ class ShardWorkload:
         return words.view(torch.uint8).reshape(-1)
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_c3_pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_c3_pmc_summary.json")
 
 
 def pmc_traffic():
