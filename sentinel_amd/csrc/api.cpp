@@ -4723,6 +4723,21 @@ int node_sync_layout(sg_node* nd) {
     return SG_OK;
 }
 
+// The walker CUs of shard g: its device's share when several shards of the node live on one device (each shard's
+// persistent walker grids were sized for the whole CU set, and G of them contended for it: round 5's G = 4 step took
+// 5x one handle's). `cus` is the CU set the walkers' streams may use (0: the whole device).
+int node_walk_cus(const sg_node* nd, uint32_t g, int cus) {
+    int same = 0;
+    for (int32_t d : nd->devices) same += d == nd->devices[g] ? 1 : 0;
+    if (same <= 1) return cus;
+    if (cus <= 0) {
+        int all = 0;
+        (void)hipDeviceGetAttribute(&all, hipDeviceAttributeMultiprocessorCount, nd->devices[g]);
+        cus = all > 0 ? all : 256;
+    }
+    return std::max(1, cus / same);
+}
+
 // Waits for the shard streams [0, g) (an early return must not leave slices in flight).
 void node_sync_shards(sg_node* nd, uint32_t g) {
     for (uint32_t x = 0; x < g && x < nd->streams.size(); ++x) {
@@ -5117,6 +5132,7 @@ int sg_node_flow_decide_batch(sg_node* nd, const sg_req* req, uint64_t n, sg_res
             b.bnd = a.bnd;
             b.p0 = a.p0;
             b.np = a.np;
+            b.walk_cus = node_walk_cus(nd, g, 0);
             hipStream_t st = nd->streams[g];
             rc = node_shard_rec(h, b, cnt, direct ? w.hist : sw.hist, st, st, h->aux, h->fork, h->join, nullptr,
                                 nd->h_err[g]);
@@ -5294,7 +5310,7 @@ int sg_node_flow_enqueue(sg_node* nd, const sg_req* req, uint64_t n, sg_result* 
         b.bnd = a.bnd;
         b.p0 = a.p0;
         b.np = a.np;
-        b.walk_cus = h->walk_cus;
+        b.walk_cus = node_walk_cus(nd, g, h->walk_cus);
         NHIP(nd, hipStreamWaitEvent(h->s_front, nd->fdone[x], 0));
         rc = node_shard_rec(h, b, cnt, direct ? w.hist : sw.hist, h->s_front, h->s_back, h->s_aux2, h->pfork, h->pjoin,
                             h->front_done[x], &sl.h_err[g]);

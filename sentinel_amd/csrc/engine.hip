@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 namespace sg {
 
@@ -2414,13 +2415,29 @@ static unsigned resident_blocks(const void* kernel, int block, int cus_used) {
     return b;
 }
 
+// A persistent walker's grid for `walk_cus` CUs (0: the whole chip; the pipeline's walker CUs; a same-device node
+// shard's share of either), cached per (kernel, CU count).
+static unsigned walker_grid(const void* kern, int walk_cus) {
+    struct Entry {
+        const void* k;
+        int cus;
+        unsigned blocks;
+    };
+    static std::mutex mu;
+    static Entry cache[64];
+    static int used = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    for (int i = 0; i < used; ++i)
+        if (cache[i].k == kern && cache[i].cus == walk_cus) return cache[i].blocks;
+    const unsigned b = resident_blocks(kern, 256, walk_cus);
+    if (used < 64) cache[used++] = Entry{kern, walk_cus, b};
+    return b;
+}
+
 // Persistent walkers: at most as many blocks as fit on the chip at once (each wave loops over its queue).
 hipError_t launch_walk_long(const BatchArgs& a, hipStream_t stream) {
     if (a.long_pend && a.long_key && a.seg_end) hipLaunchKernelGGL(k_long_bounds, dim3(1024), dim3(256), 0, stream, a);
-    static unsigned blocks[2] = {0, 0};  // all CUs / the pipeline's walker CUs
-    const int m = a.walk_cus > 0 ? 1 : 0;
-    if (blocks[m] == 0) blocks[m] = resident_blocks((const void*)k_walk_long, 256, a.walk_cus);
-    hipLaunchKernelGGL(k_walk_long, dim3(blocks[m]), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_walk_long, dim3(walker_grid((const void*)k_walk_long, a.walk_cus)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -2429,22 +2446,18 @@ static bool short_compact(const BatchArgs& a) { return a.abits == 8 && a.imask <
 
 template <int SM>
 static hipError_t launch_short_sm(const BatchArgs& a, hipStream_t stream) {
-    static unsigned blocks[2][2] = {{0, 0}, {0, 0}};  // [compact][all CUs / the pipeline's walker CUs]
     const bool c = SM > 0 && short_compact(a);
-    const int m = a.walk_cus > 0 ? 1 : 0;
     const void* kern = c ? (const void*)k_walk_short<SM, true> : (const void*)k_walk_short<SM, false>;
-    if (blocks[c][m] == 0) blocks[c][m] = resident_blocks(kern, 256, a.walk_cus);
-    if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks[c][m]), dim3(256), 0, stream, a);
+    const unsigned blocks = walker_grid(kern, a.walk_cus);
+    if (c) hipLaunchKernelGGL((k_walk_short<SM, true>), dim3(blocks), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_walk_short<SM, false>), dim3(blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 template <int SM>
 static hipError_t launch_tiny_sm(const BatchArgs& a, hipStream_t stream) {
-    static unsigned blocks[2] = {0, 0};  // all CUs / the pipeline's walker CUs
-    const int m = a.walk_cus > 0 ? 1 : 0;
-    if (blocks[m] == 0) blocks[m] = resident_blocks((const void*)k_walk_tiny<SM>, 256, a.walk_cus);
-    hipLaunchKernelGGL((k_walk_tiny<SM>), dim3(blocks[m]), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((k_walk_tiny<SM>), dim3(walker_grid((const void*)k_walk_tiny<SM>, a.walk_cus)), dim3(256), 0,
+                       stream, a);
     return hipGetLastError();
 }
 

@@ -55,13 +55,19 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_count(RouteArgs r) {
     if (tid < kMaxShards) cnt[tid] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kRouteTile;
-#pragma unroll 4
+    // every record's load, then every owner lookup, issued before any is used (two round trips per thread)
+    uint64_t rec[kRouteRounds];
+    uint32_t sh[kRouteRounds];
+#pragma unroll
     for (int it = 0; it < kRouteRounds; ++it) {
         const uint64_t i = base + (uint64_t)it * kRouteThreads + tid;
-        if (i >= r.n) break;
-        const uint32_t s = shard_of_rec(r, r.rec[i]);
-        if (s < (uint32_t)r.G) atomicAdd(&cnt[s], 1u);
+        rec[it] = i < r.n ? r.rec[i] : ~0ull;
     }
+#pragma unroll
+    for (int it = 0; it < kRouteRounds; ++it) sh[it] = shard_of_rec(r, rec[it]);
+#pragma unroll
+    for (int it = 0; it < kRouteRounds; ++it)
+        if (sh[it] < (uint32_t)r.G) atomicAdd(&cnt[sh[it]], 1u);
     __syncthreads();
     if (tid < r.G) r.tile_cnt[(size_t)blockIdx.x * kMaxShards + tid] = cnt[tid];
 }
@@ -122,23 +128,36 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_scatter(RouteArgs r) {
         wrun[wave][x] = 0;
         wtot[wave][x] = 0;
     }
-    // 1. per wave: records per shard over its range (the tile's stable order is wave 0's records, then wave 1's …)
-    for (int it = 0; it < kRouteWaveRecs / 64; ++it) {
+    // every record, then every owner and local index, loaded before any is used (kept for both passes: a dependent
+    // load chain per round was the kernel's time beside the walkers)
+    constexpr int kR = kRouteWaveRecs / 64;
+    uint64_t recs[kR];
+    uint32_t sh[kR], loc[kR];
+#pragma unroll
+    for (int it = 0; it < kR; ++it) {
         const uint64_t i = w0 + (uint64_t)it * 64 + lane;
-        const uint32_t s = i < r.n ? shard_of_rec(r, r.rec[i]) : (uint32_t)kRouteNone;
+        recs[it] = i < r.n ? r.rec[i] : ~0ull;
+    }
+#pragma unroll
+    for (int it = 0; it < kR; ++it) {
+        sh[it] = shard_of_rec(r, recs[it]);
+        const uint32_t k = (uint32_t)(recs[it] >> r.kshift);
+        loc[it] = sh[it] < (uint32_t)r.G ? r.local_of[k] : 0u;
+    }
+    // 1. per wave: records per shard over its range (the tile's stable order is wave 0's records, then wave 1's …)
+#pragma unroll
+    for (int it = 0; it < kR; ++it) {
+        const uint32_t s = sh[it];
         const uint64_t peers = match_shard(s);
         if (s < (uint32_t)r.G && (peers & ((1ull << lane) - 1ull)) == 0) wtot[wave][s] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_sched_barrier(0);  // round by round (hoisted ballots spilled)
     }
     __syncthreads();
     // 2. place: position = shard base + the tile's offset + earlier waves of the tile + earlier rounds + rank in round
-    for (int it = 0; it < kRouteWaveRecs / 64; ++it) {
-        const uint64_t i = w0 + (uint64_t)it * 64 + lane;
-        uint64_t rec = 0;
-        uint32_t s = (uint32_t)kRouteNone;
-        if (i < r.n) {
-            rec = r.rec[i];
-            s = shard_of_rec(r, rec);
-        }
+#pragma unroll
+    for (int it = 0; it < kR; ++it) {
+        const uint64_t rec = recs[it];
+        const uint32_t s = sh[it];
         const uint64_t peers = match_shard(s);
         const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
         if (s < (uint32_t)r.G) {
@@ -146,21 +165,21 @@ __global__ void __launch_bounds__(kRouteThreads) k_route_scatter(RouteArgs r) {
             for (int w = 0; w < wave; ++w) before += wtot[w][s];
             const uint32_t pos = r.shard_base[s] + r.tile_cnt[(size_t)blockIdx.x * kMaxShards + s] + before +
                                  wrun[wave][s] + rank;
-            const uint32_t k = (uint32_t)(rec >> r.kshift);
             if (r.sub_rec) {
-                r.sub_rec[pos] = ((uint64_t)r.local_of[k] << r.skshift[s]) | (rec & r.low_mask);
+                r.sub_rec[pos] = ((uint64_t)loc[it] << r.skshift[s]) | (rec & r.low_mask);
             } else {
                 const uint32_t idx = (uint32_t)((rec >> r.abits) & r.imask);
                 const sg_req q = r.req[idx];
                 sg_req o;
                 o.ts_ms = q.ts_ms;
-                o.key = r.local_of[k] | (q.key & SG_KEY_PRIO);
+                o.key = loc[it] | (q.key & SG_KEY_PRIO);
                 o.acquire = q.acquire;
                 r.sub_req[pos] = o;
                 r.sub_pos[pos] = idx;
             }
         }
         if (s < (uint32_t)r.G && rank == 0) wrun[wave][s] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
