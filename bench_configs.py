@@ -547,7 +547,12 @@ def cparam(args, dev):
 
     batches = [batch(b) for b in range(args.warmup + args.steps)]
     max_nv = max(x[2] for x in batches)
-    eng = FlowEngine(device=0, max_batch=max(n, max_nv))
+    G = args.shards  # --shards G: the node handle's sharded param path (sg_node_cparam_*), G shards on this GPU
+    if G:
+        from sentinel_amd.engine import NodeEngine
+        eng = NodeEngine([0] * G, max_batch=max(n, max_nv))
+    else:
+        eng = FlowEngine(device=0, max_batch=max(n, max_nv))
     ns = np.zeros(1, abi.NS_DTYPE)
     ns["connected_count"] = 1
     eng.set_namespaces(ns)
@@ -559,7 +564,8 @@ def cparam(args, dev):
     def step(b):
         req, vals, nv = batches[b]
         eng.cparam_decide_device(req.data_ptr(), n, vals.data_ptr(), nv, out.data_ptr(), stream)
-        rounds.append(eng.cparam_last_rounds())
+        if not G:
+            rounds.append(eng.cparam_last_rounds())
 
     el = timed(step, args.warmup, args.steps)
     req_l, vals_l, nv_l = batches[-1]
@@ -586,11 +592,13 @@ def cparam(args, dev):
         base = {"value": m / dt, "unit": "decisions/s", "cores": 1, "kind": "port",
                 "sample": f"first {m} requests of batch 0 through oracle ClusterTokenService.decide_param (1 thread), "
                           f"{dt:.1f} s"}
-    return {"metric": "cluster hot-parameter token decisions/sec (ClusterParamFlowChecker), 1000 param rules",
+    return {"metric": "cluster hot-parameter token decisions/sec (ClusterParamFlowChecker), 1000 param rules"
+                      + (f", node handle with {G} shards on one GPU (routing inside)" if G else ""),
             "workload": "cparam: 1000 ClusterParamFlowRules x 50k values Zipf(1.1), 16M requests/batch, 10% multi-value"
-                        + (f", a {args.chain}-deep two-value dependency chain per batch (rule 0, threshold 1)" if args.chain else ""),
+                        + (f", a {args.chain}-deep two-value dependency chain per batch (rule 0, threshold 1)" if args.chain else "")
+                        + (f", sg_node_cparam_decide_batch over {G} same-device shards" if G else ""),
             "value": n * args.steps / el, "el": el, "n": n, "b_alg": b_alg, "touched": touched, "cpu": base,
-            "extra": {"fixed_point_rounds": rounds[args.warmup:], "values_per_step": nv_l},
+            "extra": {"fixed_point_rounds": rounds[args.warmup:], "values_per_step": nv_l, "shards": G},
             "data": "synthetic (GPU-generated, seeded): rules Zipf(1.0), values Zipf(1.1) per rule, 10% 2-3 values"}
 
 
@@ -603,7 +611,7 @@ def node(args, dev):
     --local-sync: both synchronous (sg_node_flow_decide_batch / sg_flow_decide_batch)."""
     import bench
     from sentinel_amd.engine import NodeEngine
-    G = args.shards
+    G = args.shards or 2
     wl = bench.ShardWorkload(1_000_000, args.events, 0, 1, dev)
     ns = np.zeros(1, abi.NS_DTYPE)
     ns["connected_count"] = 1
@@ -657,7 +665,9 @@ def node(args, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["c2", "c4", "c5", "codec", "pace", "cparam", "node", "slot"], default="c2")
-    ap.add_argument("--shards", type=int, default=2, help="node: shard handles on the one GPU")
+    ap.add_argument("--shards", type=int, default=0,
+                    help="node: shard handles on the one GPU (default 2); cparam: decide through the node handle "
+                         "with this many shards (default: one handle)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--events", type=int, default=16_000_000)

@@ -787,6 +787,34 @@ int         sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, u
  * concurrent tokens (sg_conc_*) are decided on it, beside the sharded flow tokens. Its own sg_flow_* entry points
  * must not be called. */
 sg_handle*  sg_node_front(sg_node* nd);
+/* Cluster param and concurrent tokens sharded over the node (DefaultTokenService.requestParamToken /
+ * requestConcurrentToken / releaseConcurrentToken, DefaultTokenService.java:53-85): a param rule (with its hot items)
+ * lives on the shard owning its flowId; a concurrent acquire goes to the owner of its flow rule's flowId, a release
+ * to the shard its token id names (node token id = (shard token id - 1) * G + shard + 1). A node batch in caller order
+ * is checked for time order and value bounds on devices[0] (refused whole, nothing decided), split stably by owner
+ * with one 8-bit radix pass, decided shard by shard in the node's order and gathered back: the statuses, counters and
+ * metrics equal one handle deciding the batch; token ids are the node's own (unique, as the reference's are only
+ * unique). Param batches whose rules name a namespace with the GlobalRequestLimiter enabled are refused
+ * (SG_E_UNSUPPORTED): allowProceed (ClusterParamFlowChecker.java:43-45) takes the limiter in caller order, which the
+ * front handle serves (sg_node_front). Device buffers are on devices[0]; the _host forms take host buffers.
+ *   sg_node_cparam_load_rules      ← sg_cparam_load_rules for the node's param rule set (rule = index of this array)
+ *   sg_node_cparam_read_sum / _top_values ← per node param rule, as the single-handle calls
+ *   sg_node_conc_*                 ← sg_conc_* with node flow rule indices (timeouts per node rule) */
+int sg_node_cparam_load_rules(sg_node* nd, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                              uint32_t n_hot, int32_t capacity_log2);
+int sg_node_cparam_decide_batch(sg_node* nd, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                uint64_t n_values, sg_result* out, void* stream);
+int sg_node_cparam_decide_batch_host(sg_node* nd, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                     uint64_t n_values, sg_result* out);
+int sg_node_cparam_read_sum(sg_node* nd, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum);
+int sg_node_cparam_top_values(sg_node* nd, int64_t now_ms, uint32_t number, uint64_t* values, double* qps,
+                              uint32_t* counts);
+int sg_node_conc_set_rule_timeouts(sg_node* nd, const int64_t* client_offline_ms, const int64_t* resource_timeout_ms,
+                                   uint32_t n);
+int sg_node_conc_decide_batch(sg_node* nd, const sg_conc_req* req, uint64_t n, sg_conc_result* out, void* stream);
+int sg_node_conc_decide_batch_host(sg_node* nd, const sg_conc_req* req, uint64_t n, sg_conc_result* out);
+int sg_node_conc_expire(sg_node* nd, int64_t now_ms, const uint8_t* client_online, uint32_t n_clients, uint64_t* removed);
+int sg_node_conc_read_state(sg_node* nd, uint32_t key, int32_t* now_calls, uint64_t* live_tokens);
 
 /* ---------- token-server wire codec ----------
  * The default token server frames every message with a 2-byte big-endian length

@@ -4657,6 +4657,39 @@ struct sg_node {
     uint64_t* d_sub_rec2 = nullptr;            // workspace 1's record slices
     uint64_t pseq = 0, next_ticket = 1;
     std::unordered_map<uint64_t, int> finished;  // tickets completed while making room, not yet collected
+    // cluster param and concurrent tokens over the node (sg_node_cparam_*, sg_node_conc_*): a param rule lives on the
+    // shard owning its flowId; a concurrent token on the shard owning its flow rule's flowId
+    std::vector<sg_cparam_rule> cp_rules;
+    std::vector<uint8_t> cp_shard_of;
+    std::vector<uint32_t> cp_local_of;
+    uint8_t* d_cp_shard_of = nullptr;
+    uint32_t* d_cp_local_of = nullptr;
+    uint64_t* d_nrec = nullptr;        // [max_batch] owner records, then the sort's other buffer
+    uint64_t* d_nrec2 = nullptr;
+    uint32_t* d_nhist = nullptr;
+    uint32_t* d_nvals = nullptr;       // [max_batch]
+    uint32_t* d_ncnt = nullptr;        // [3 * kMaxShards]: requests, values, value bases per shard
+    uint32_t* d_ntsum = nullptr;       // [tiles]
+    int* d_nerr = nullptr;
+    void* d_sub_nreq = nullptr;        // [max_batch] slices (sg_cparam_req / sg_conc_req: 24 B / 32 B each)
+    void* d_sub_nout = nullptr;        // [max_batch] slice results (sg_result / sg_conc_result)
+    uint64_t* d_sub_vals = nullptr;    // the param slices' values
+    uint64_t sub_vals_cap = 0;
+    std::vector<void*> r_nreq, r_nout; // shards on other devices: their slices there
+    std::vector<uint64_t*> r_vals;
+    std::vector<uint64_t> r_vals_cap;
+    int64_t cp_last_ts = -1, cc_last_ts = -1;  // the node's previous param / concurrent batch (time order)
+    // host-path staging
+    void* d_nreq_h = nullptr;
+    void* d_nout_h = nullptr;
+    uint64_t* d_nvals_h = nullptr;
+    uint64_t nvals_h_cap = 0;
+    // node snapshot on the device: each shard's part gathered into the front's buffer in node rule order
+    std::vector<uint32_t*> d_node_key;  // per shard (on the front's device): node rule of each local rule
+    double* d_snap = nullptr;
+    uint64_t snap_cap = 0;
+    bool node_key_stale = true;         // the flow rules changed since d_node_key was built
+    std::vector<double*> r_snap;        // per shard on another device: its part there
 };
 
 namespace {
@@ -4831,6 +4864,31 @@ void sg_node_destroy(sg_node* nd) {
     dfree(nd->d_out_h);
     dfree(nd->d_sub_rec);
     dfree(nd->d_sub_rec2);
+    dfree(nd->d_cp_shard_of);
+    dfree(nd->d_cp_local_of);
+    dfree(nd->d_nrec);
+    dfree(nd->d_nrec2);
+    dfree(nd->d_nhist);
+    dfree(nd->d_nvals);
+    dfree(nd->d_ncnt);
+    dfree(nd->d_ntsum);
+    dfree(nd->d_nerr);
+    dfree(nd->d_sub_nreq);
+    dfree(nd->d_sub_nout);
+    dfree(nd->d_sub_vals);
+    dfree(nd->d_nreq_h);
+    dfree(nd->d_nout_h);
+    dfree(nd->d_nvals_h);
+    dfree(nd->d_snap);
+    for (uint32_t* p : nd->d_node_key) dfree(p);
+    for (size_t g = 0; g < nd->r_nreq.size(); ++g) {
+        (void)hipSetDevice(nd->devices[g]);
+        dfree(nd->r_nreq[g]);
+        dfree(nd->r_nout[g]);
+        dfree(nd->r_vals[g]);
+        if (g < nd->r_snap.size()) dfree(nd->r_snap[g]);
+    }
+    (void)hipSetDevice(nd->devices.empty() ? 0 : nd->devices[0]);
     for (auto& sl : nd->pipe) {
         if (sl.done) (void)hipEventDestroy(sl.done);
         if (sl.h_err) (void)hipHostFree(sl.h_err);
@@ -4907,6 +4965,11 @@ int sg_node_create(const sg_config* cfg, const int32_t* devices, uint32_t n_shar
         (void)hipGetLastError();  // an already-enabled peer leaves its error behind
     }
     if (hipSetDevice(devices[0]) != hipSuccess) return bail(SG_E_DEVICE);
+    nd->r_nreq.assign(n_shards, nullptr);
+    nd->r_nout.assign(n_shards, nullptr);
+    nd->r_vals.assign(n_shards, nullptr);
+    nd->r_vals_cap.assign(n_shards, 0);
+    nd->r_snap.assign(n_shards, nullptr);
     const uint64_t n = cfg->max_batch;
     if (hipStreamCreateWithFlags(&nd->s0, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&nd->routed, hipEventDisableTiming) != hipSuccess ||
@@ -5029,6 +5092,7 @@ int sg_node_load_flow_rules(sg_node* nd, const sg_flow_rule* rules, uint32_t n) 
     nd->rules.assign(rules, rules + n);
     nd->shard_of = so;
     nd->local_of = lo;
+    nd->node_key_stale = true;
     return node_sync_layout(nd);
 }
 
@@ -5374,18 +5438,456 @@ int sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t 
     node_drain(nd);
     const uint64_t K = nd->shard_of.size();
     if (cap < 2 * K) return nfail(nd, SG_E_CAPACITY, "snapshot buffer smaller than 2 * rules");
-    std::vector<std::vector<double>> part(nd->shards.size());
-    for (size_t g = 0; g < nd->shards.size(); ++g) {
+    if (K == 0) return SG_OK;
+    // ClusterMetricNodeGenerator.generateCurrentNodeMap (ClusterMetricNodeGenerator.java:39-61) over the node: every
+    // shard's {passQps, blockQps} computed on its device, moved to the front's device (peer copies), scattered into
+    // node rule order there, one copy to the host
+    const uint32_t G = (uint32_t)nd->shards.size();
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    if (nd->node_key_stale || nd->d_node_key.size() != G) {
+        for (uint32_t* p : nd->d_node_key) dfree(p);
+        nd->d_node_key.assign(G, nullptr);
+        std::vector<std::vector<uint32_t>> keys(G);
+        for (uint64_t k = 0; k < K; ++k) {
+            auto& v = keys[nd->shard_of[k]];
+            if (v.size() <= nd->local_of[k]) v.resize(nd->local_of[k] + 1);
+            v[nd->local_of[k]] = (uint32_t)k;
+        }
+        for (uint32_t g = 0; g < G; ++g) {
+            if (keys[g].empty()) continue;
+            if (hipMalloc(&nd->d_node_key[g], sizeof(uint32_t) * keys[g].size()) != hipSuccess)
+                return nfail(nd, SG_E_NOMEM, "node snapshot keys");
+            NHIP(nd, hipMemcpy(nd->d_node_key[g], keys[g].data(), sizeof(uint32_t) * keys[g].size(), hipMemcpyHostToDevice));
+        }
+        nd->node_key_stale = false;
+    }
+    uint64_t part_max = 0;
+    for (sg_handle* h : nd->shards) part_max = std::max<uint64_t>(part_max, h->K);
+    const uint64_t need = 2 * K + 2 * part_max;  // the node's rows, then one shard part staged on the front
+    if (need > nd->snap_cap) {
+        dfree(nd->d_snap);
+        if (hipMalloc(&nd->d_snap, sizeof(double) * need) != hipSuccess) return nfail(nd, SG_E_NOMEM, "node snapshot");
+        nd->snap_cap = need;
+    }
+    double* stage = nd->d_snap + 2 * K;
+    for (uint32_t g = 0; g < G; ++g) {
         sg_handle* h = nd->shards[g];
-        part[g].assign(2 * (size_t)h->K + 2, 0.0);
-        const int rc = sg_snapshot_metrics(h, now_ms, part[g].data(), part[g].size());
+        if (h->K == 0) continue;
+        const int dev = nd->devices[g];
+        double* part = stage;
+        if (dev != nd->devices[0]) {  // computed on its device, then copied over xGMI
+            NHIP(nd, hipSetDevice(dev));
+            if (!nd->r_snap[g] && hipMalloc(&nd->r_snap[g], sizeof(double) * 2 * part_max) != hipSuccess)
+                return nfail(nd, SG_E_NOMEM, "node snapshot part");
+            part = nd->r_snap[g];
+        }
+        NHIP(nd, launch_snapshot(h->d_rules, h->d_ring, h->d_occ, h->K, h->stride, now_ms, part, nd->streams[g]));
+        NHIP(nd, hipStreamSynchronize(nd->streams[g]));
+        NHIP(nd, hipSetDevice(nd->devices[0]));
+        if (dev != nd->devices[0])
+            NHIP(nd, hipMemcpyPeerAsync(stage, nd->devices[0], part, dev, sizeof(double) * 2 * h->K, nd->s0));
+        NHIP(nd, launch_nsnap_scatter(stage, nd->d_node_key[g], h->K, nd->d_snap, nd->s0));
+        NHIP(nd, hipStreamSynchronize(nd->s0));  // the stage is reused by the next shard
+    }
+    NHIP(nd, hipMemcpy(out, nd->d_snap, sizeof(double) * 2 * K, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+// ---- cluster param and concurrent tokens over the node ----
+
+int sg_node_cparam_load_rules(sg_node* nd, const sg_cparam_rule* rules, uint32_t n, const sg_param_hot_item* hot,
+                              uint32_t n_hot, int32_t capacity_log2) {
+    if (!nd || (!rules && n) || (!hot && n_hot)) return SG_E_INVAL;
+    node_drain(nd);
+    // ClusterParamFlowRuleManager over the node: a rule (and its hot items) lives on the shard owning its flowId. The
+    // shards' loads are validated by each shard; a failing one leaves the earlier shards on the new rules (node-wide
+    // all-or-nothing is the flow rules' contract, not this one's: reload after a failure)
+    const uint32_t G = (uint32_t)nd->shards.size();
+    for (uint32_t i = 0; i < n; ++i)
+        if ((uint64_t)rules[i].hot_begin + rules[i].hot_count > n_hot) return nfail(nd, SG_E_INVAL, "hot item range out of bounds");
+    std::vector<std::vector<sg_cparam_rule>> part(G);
+    std::vector<std::vector<sg_param_hot_item>> hp(G);
+    std::vector<uint8_t> so(n);
+    std::vector<uint32_t> lo(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t g = node_owner(rules[i].flow_id, G);
+        so[i] = (uint8_t)g;
+        lo[i] = (uint32_t)part[g].size();
+        sg_cparam_rule r = rules[i];
+        r.hot_begin = (uint32_t)hp[g].size();
+        hp[g].insert(hp[g].end(), hot + rules[i].hot_begin, hot + rules[i].hot_begin + rules[i].hot_count);
+        part[g].push_back(r);
+    }
+    for (uint32_t g = 0; g < G; ++g) {
+        sg_handle* h = nd->shards[g];
+        NHIP(nd, hipSetDevice(h->device));
+        const int rc = sg_cparam_load_rules(h, part[g].data(), (uint32_t)part[g].size(), hp[g].data(),
+                                            (uint32_t)hp[g].size(), capacity_log2);
         if (rc) return node_child(nd, h, rc);
     }
-    for (uint64_t k = 0; k < K; ++k) {
-        const std::vector<double>& p = part[nd->shard_of[k]];
-        out[2 * k] = p[2 * (size_t)nd->local_of[k]];
-        out[2 * k + 1] = p[2 * (size_t)nd->local_of[k] + 1];
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    dfree(nd->d_cp_shard_of);
+    dfree(nd->d_cp_local_of);
+    if (n && (hipMalloc(&nd->d_cp_shard_of, n) != hipSuccess || hipMalloc(&nd->d_cp_local_of, sizeof(uint32_t) * n) != hipSuccess))
+        return nfail(nd, SG_E_NOMEM, "param routing tables");
+    if (n) {
+        NHIP(nd, hipMemcpy(nd->d_cp_shard_of, so.data(), n, hipMemcpyHostToDevice));
+        NHIP(nd, hipMemcpy(nd->d_cp_local_of, lo.data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice));
     }
+    nd->cp_rules.assign(rules, rules + n);
+    nd->cp_shard_of = so;
+    nd->cp_local_of = lo;
+    return SG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Scratch of the node's param / concurrent routing, sized for max_batch requests (values: n_values).
+int node_nreq_scratch(sg_node* nd, uint64_t n_values) {
+    const uint64_t n = nd->cfg.max_batch;
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    if (!nd->d_nrec) {
+        if (hipMalloc(&nd->d_nrec, 8 * n) != hipSuccess || hipMalloc(&nd->d_nrec2, 8 * n) != hipSuccess ||
+            hipMalloc(&nd->d_nhist, sizeof(uint32_t) * radix_hist_words(n)) != hipSuccess ||
+            hipMalloc(&nd->d_nvals, sizeof(uint32_t) * n) != hipSuccess ||
+            hipMalloc(&nd->d_ncnt, sizeof(uint32_t) * 3 * kMaxShards) != hipSuccess ||
+            hipMalloc(&nd->d_ntsum, sizeof(uint32_t) * (nreq_tiles(n) + 1)) != hipSuccess ||
+            hipMalloc(&nd->d_nerr, sizeof(int)) != hipSuccess ||
+            hipMalloc(&nd->d_sub_nreq, std::max(sizeof(sg_cparam_req), sizeof(sg_conc_req)) * n) != hipSuccess ||
+            hipMalloc(&nd->d_sub_nout, std::max(sizeof(sg_result), sizeof(sg_conc_result)) * n) != hipSuccess)
+            return nfail(nd, SG_E_NOMEM, "node token routing scratch");
+    }
+    if (n_values > nd->sub_vals_cap) {
+        dfree(nd->d_sub_vals);
+        if (hipMalloc(&nd->d_sub_vals, 8 * n_values) != hipSuccess) return nfail(nd, SG_E_NOMEM, "node param values");
+        nd->sub_vals_cap = n_values;
+    }
+    return SG_OK;
+}
+
+// The node batch's slices (stable by owner): per-shard request bases / counts and value bases / counts on the host.
+int node_nreq_route(sg_node* nd, NodeReqArgs q, std::vector<uint64_t>& base, std::vector<uint64_t>& cnt,
+                    std::vector<uint64_t>& vbase, std::vector<uint64_t>& vcnt) {
+    const uint32_t G = (uint32_t)nd->shards.size();
+    hipStream_t st = nd->s0;
+    q.G = (int)G;
+    q.rec = nd->d_nrec;
+    q.nvals = nd->d_nvals;
+    q.cnt = nd->d_ncnt;
+    q.vcnt = nd->d_ncnt + kMaxShards;
+    q.tsum = nd->d_ntsum;
+    q.vbase = nd->d_ncnt + 2 * kMaxShards;
+    q.sub_vals = nd->d_sub_vals;
+    q.sub_pos = nd->d_sub_pos;
+    q.err = nd->d_nerr;
+    NHIP(nd, hipMemsetAsync(nd->d_ncnt, 0, sizeof(uint32_t) * 2 * kMaxShards, st));
+    NHIP(nd, hipMemsetAsync(nd->d_nerr, 0, sizeof(int), st));
+    NHIP(nd, launch_nreq_keys(q, st));
+    uint32_t h_cnt[2 * kMaxShards];
+    int err = 0;
+    NHIP(nd, hipMemcpyAsync(h_cnt, nd->d_ncnt, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+    NHIP(nd, hipMemcpyAsync(&err, nd->d_nerr, sizeof(int), hipMemcpyDeviceToHost, st));
+    NHIP(nd, hipStreamSynchronize(st));
+    if (err & kErrTime)
+        return nfail(nd, SG_E_TIME, "timestamps must be >= 0, non-decreasing, and not older than the node's earlier batches");
+    if (err & kErrBounds) return nfail(nd, SG_E_INVAL, "a request's values lie outside the value array");
+    base.assign(G, 0);
+    cnt.assign(G, 0);
+    vbase.assign(G, 0);
+    vcnt.assign(G, 0);
+    uint32_t vb[kMaxShards] = {};
+    uint64_t b = 0, v = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        base[g] = b;
+        cnt[g] = h_cnt[g];
+        vbase[g] = v;
+        vcnt[g] = h_cnt[kMaxShards + g];
+        vb[g] = (uint32_t)v;
+        b += cnt[g];
+        v += vcnt[g];
+    }
+    NHIP(nd, hipMemcpyAsync(nd->d_ncnt + 2 * kMaxShards, vb, sizeof(vb), hipMemcpyHostToDevice, st));
+    uint64_t* sorted = nullptr;
+    NHIP(nd, radix_sort_records(nd->d_nrec, nd->d_nrec2, q.n, 56, nd->d_nhist, &sorted, st, 64));
+    NHIP(nd, launch_nreq_gather(q, sorted, st));
+    NHIP(nd, hipStreamSynchronize(st));
+    return SG_OK;
+}
+
+// Shard g's slice on its device: `bytes` per request / result, the values (param) — peer copies for shards off the
+// front's device (buffers there grown as needed). *req / *vals / *out point at what the shard decides on.
+int node_slice_to(sg_node* nd, uint32_t g, uint64_t cnt, size_t req_b, size_t out_b, const void* sreq,
+                  const uint64_t* svals, uint64_t nv, const void** req, const uint64_t** vals, void** out) {
+    const int dev = nd->devices[g];
+    *req = sreq;
+    *vals = svals;
+    *out = nullptr;
+    if (dev == nd->devices[0]) return SG_OK;
+    NHIP(nd, hipSetDevice(dev));
+    const uint64_t n = nd->cfg.max_batch;
+    if (!nd->r_nreq[g] && (hipMalloc(&nd->r_nreq[g], std::max(sizeof(sg_cparam_req), sizeof(sg_conc_req)) * n) != hipSuccess ||
+                           hipMalloc(&nd->r_nout[g], std::max(sizeof(sg_result), sizeof(sg_conc_result)) * n) != hipSuccess))
+        return nfail(nd, SG_E_NOMEM, "shard slice buffers");
+    if (nv > nd->r_vals_cap[g]) {
+        dfree(nd->r_vals[g]);
+        if (hipMalloc(&nd->r_vals[g], 8 * nv) != hipSuccess) return nfail(nd, SG_E_NOMEM, "shard values");
+        nd->r_vals_cap[g] = nv;
+    }
+    NHIP(nd, hipMemcpyPeer(nd->r_nreq[g], dev, sreq, nd->devices[0], req_b * cnt));
+    if (nv) NHIP(nd, hipMemcpyPeer(nd->r_vals[g], dev, svals, nd->devices[0], 8 * nv));
+    *req = nd->r_nreq[g];
+    *vals = nd->r_vals[g];
+    *out = nd->r_nout[g];
+    (void)out_b;
+    return SG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sg_node_cparam_decide_batch(sg_node* nd, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                uint64_t n_values, sg_result* out, void* stream) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out || (!values && n_values)) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    if (n_values >= (1ull << 32)) return nfail(nd, SG_E_CAPACITY, "more than 2^32 values");
+    node_drain(nd);
+    // allowProceed (ClusterParamFlowChecker.java:43-45) needs the namespace's limiter in the node's caller order: the
+    // node's param path serves namespaces without one
+    for (const auto& r : nd->cp_rules)
+        if (r.namespace_id >= 0 && (size_t)r.namespace_id < nd->ns.size() && nd->ns[r.namespace_id].limiter_enabled)
+            return nfail(nd, SG_E_UNSUPPORTED, "node param tokens with a namespace limiter (use one handle, or the "
+                                               "sharded limiter exchange)");
+    int rc = node_nreq_scratch(nd, n_values ? n_values : 1);
+    if (rc) return rc;
+    const uint32_t G = (uint32_t)nd->shards.size();
+    NodeReqArgs q{};
+    q.n = n;
+    q.cp = req;
+    q.values = values;
+    q.n_values = n_values;
+    q.K = (uint32_t)nd->cp_rules.size();
+    q.shard_of = nd->d_cp_shard_of;
+    q.local_of = nd->d_cp_local_of;
+    q.sub_cp = static_cast<sg_cparam_req*>(nd->d_sub_nreq);
+    q.last_ts = nd->cp_last_ts;
+    (void)stream;  // synchronous: the shards' fixed points wait on the host between rounds
+    std::vector<uint64_t> base, cnt, vbase, vcnt;
+    rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
+    if (rc) return rc;
+    sg_result* sub_out = static_cast<sg_result*>(nd->d_sub_nout);
+    for (uint32_t g = 0; g < G; ++g) {
+        if (!cnt[g]) continue;
+        const void* sr = nullptr;
+        const uint64_t* sv = nullptr;
+        void* so = nullptr;
+        rc = node_slice_to(nd, g, cnt[g], sizeof(sg_cparam_req), sizeof(sg_result), q.sub_cp + base[g],
+                           nd->d_sub_vals + vbase[g], vcnt[g], &sr, &sv, &so);
+        if (rc) return rc;
+        sg_handle* h = nd->shards[g];
+        NHIP(nd, hipSetDevice(h->device));
+        sg_result* o = so ? static_cast<sg_result*>(so) : sub_out + base[g];
+        rc = sg_cparam_decide_batch(h, static_cast<const sg_cparam_req*>(sr), cnt[g], vcnt[g] ? sv : nullptr, vcnt[g], o,
+                                    nd->streams[g]);
+        if (rc) return node_child(nd, h, rc);
+        NHIP(nd, hipStreamSynchronize(nd->streams[g]));
+        if (so) NHIP(nd, hipMemcpyPeer(sub_out + base[g], nd->devices[0], so, h->device, sizeof(sg_result) * cnt[g]));
+    }
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    NHIP(nd, launch_route_gather(sub_out, nd->d_sub_pos, n, out, nd->s0));
+    int64_t last = 0;
+    NHIP(nd, hipMemcpyAsync(&last, &req[n - 1].ts_ms, sizeof(int64_t), hipMemcpyDeviceToHost, nd->s0));
+    NHIP(nd, hipStreamSynchronize(nd->s0));
+    nd->cp_last_ts = last;
+    return SG_OK;
+}
+
+int sg_node_cparam_decide_batch_host(sg_node* nd, const sg_cparam_req* req, uint64_t n, const uint64_t* values,
+                                     uint64_t n_values, sg_result* out) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out || (!values && n_values)) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    node_drain(nd);
+    if (!nd->d_nreq_h && (hipMalloc(&nd->d_nreq_h, sizeof(sg_conc_req) * nd->cfg.max_batch) != hipSuccess ||
+                          hipMalloc(&nd->d_nout_h, sizeof(sg_conc_result) * nd->cfg.max_batch) != hipSuccess))
+        return nfail(nd, SG_E_NOMEM, "node host-path buffers");
+    if (n_values > nd->nvals_h_cap) {
+        dfree(nd->d_nvals_h);
+        if (hipMalloc(&nd->d_nvals_h, 8 * n_values) != hipSuccess) return nfail(nd, SG_E_NOMEM, "node host-path values");
+        nd->nvals_h_cap = n_values;
+    }
+    NHIP(nd, hipMemcpy(nd->d_nreq_h, req, sizeof(sg_cparam_req) * n, hipMemcpyHostToDevice));
+    if (n_values) NHIP(nd, hipMemcpy(nd->d_nvals_h, values, 8 * n_values, hipMemcpyHostToDevice));
+    const int rc = sg_node_cparam_decide_batch(nd, static_cast<const sg_cparam_req*>(nd->d_nreq_h), n,
+                                               n_values ? nd->d_nvals_h : nullptr, n_values,
+                                               static_cast<sg_result*>(nd->d_nout_h), nullptr);
+    if (rc) return rc;
+    NHIP(nd, hipMemcpy(out, nd->d_nout_h, sizeof(sg_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_node_cparam_read_sum(sg_node* nd, uint32_t rule, uint64_t value, int64_t now_ms, int64_t* sum) {
+    if (!nd || !sum || rule >= nd->cp_rules.size()) return SG_E_INVAL;
+    node_drain(nd);
+    sg_handle* h = nd->shards[nd->cp_shard_of[rule]];
+    return node_child(nd, h, sg_cparam_read_sum(h, nd->cp_local_of[rule], value, now_ms, sum));
+}
+
+// ClusterParamMetric.getTopValues per node rule (ClusterMetricNodeGenerator.paramToMetricNode :88-104): each rule's
+// values come from its owner (its metric lives there), laid out in node rule order as sg_cparam_top_values does.
+int sg_node_cparam_top_values(sg_node* nd, int64_t now_ms, uint32_t number, uint64_t* values, double* qps,
+                              uint32_t* counts) {
+    const uint64_t R = nd ? nd->cp_rules.size() : 0;
+    if (!nd || (R && (!values || !qps || !counts))) return SG_E_INVAL;
+    node_drain(nd);
+    const uint32_t G = (uint32_t)nd->shards.size();
+    for (uint32_t g = 0; g < G; ++g) {
+        sg_handle* h = nd->shards[g];
+        const uint64_t r = h->cprules.size();
+        if (!r) continue;
+        std::vector<uint64_t> v(r * number);
+        std::vector<double> q(r * number);
+        std::vector<uint32_t> c(r);
+        const int rc = sg_cparam_top_values(h, now_ms, number, v.data(), q.data(), c.data());
+        if (rc) return node_child(nd, h, rc);
+        for (uint64_t k = 0; k < R; ++k) {
+            if (nd->cp_shard_of[k] != g) continue;
+            const uint32_t l = nd->cp_local_of[k];
+            counts[k] = c[l];
+            for (uint32_t j = 0; j < number; ++j) {
+                values[k * number + j] = v[(uint64_t)l * number + j];
+                qps[k * number + j] = q[(uint64_t)l * number + j];
+            }
+        }
+    }
+    return SG_OK;
+}
+
+int sg_node_conc_decide_batch(sg_node* nd, const sg_conc_req* req, uint64_t n, sg_conc_result* out, void* stream) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    node_drain(nd);
+    int rc = node_nreq_scratch(nd, 1);
+    if (rc) return rc;
+    const uint32_t G = (uint32_t)nd->shards.size();
+    NodeReqArgs q{};
+    q.n = n;
+    q.cc = req;
+    q.K = (uint32_t)nd->shard_of.size();
+    q.shard_of = nd->d_shard_of;
+    q.local_of = nd->d_local_of;
+    q.sub_cc = static_cast<sg_conc_req*>(nd->d_sub_nreq);
+    q.last_ts = nd->cc_last_ts;
+    (void)stream;
+    std::vector<uint64_t> base, cnt, vbase, vcnt;
+    rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
+    if (rc) return rc;
+    sg_conc_result* sub_out = static_cast<sg_conc_result*>(nd->d_sub_nout);
+    for (uint32_t g = 0; g < G; ++g) {
+        if (!cnt[g]) continue;
+        const void* sr = nullptr;
+        const uint64_t* sv = nullptr;
+        void* so = nullptr;
+        rc = node_slice_to(nd, g, cnt[g], sizeof(sg_conc_req), sizeof(sg_conc_result), q.sub_cc + base[g], nullptr, 0,
+                           &sr, &sv, &so);
+        if (rc) return rc;
+        sg_handle* h = nd->shards[g];
+        NHIP(nd, hipSetDevice(h->device));
+        sg_conc_result* o = so ? static_cast<sg_conc_result*>(so) : sub_out + base[g];
+        rc = sg_conc_decide_batch(h, static_cast<const sg_conc_req*>(sr), cnt[g], o, nd->streams[g]);
+        if (rc) return node_child(nd, h, rc);
+        NHIP(nd, hipStreamSynchronize(nd->streams[g]));
+        if (so) NHIP(nd, hipMemcpyPeer(sub_out + base[g], nd->devices[0], so, h->device, sizeof(sg_conc_result) * cnt[g]));
+    }
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    for (uint32_t g = 0; g < G; ++g)
+        NHIP(nd, launch_nconc_scatter(sub_out, nd->d_sub_pos, q.sub_cc, base[g], cnt[g], g, G, out, nd->s0));
+    int64_t last = 0;
+    NHIP(nd, hipMemcpyAsync(&last, &req[n - 1].ts_ms, sizeof(int64_t), hipMemcpyDeviceToHost, nd->s0));
+    NHIP(nd, hipStreamSynchronize(nd->s0));
+    nd->cc_last_ts = last;
+    return SG_OK;
+}
+
+int sg_node_conc_decide_batch_host(sg_node* nd, const sg_conc_req* req, uint64_t n, sg_conc_result* out) {
+    if (!nd) return SG_E_INVAL;
+    if (n == 0) return SG_OK;
+    if (!req || !out) return nfail(nd, SG_E_INVAL, "null buffer");
+    if (n > nd->cfg.max_batch) return nfail(nd, SG_E_CAPACITY, "batch larger than max_batch");
+    NHIP(nd, hipSetDevice(nd->devices[0]));
+    node_drain(nd);
+    if (!nd->d_nreq_h && (hipMalloc(&nd->d_nreq_h, sizeof(sg_conc_req) * nd->cfg.max_batch) != hipSuccess ||
+                          hipMalloc(&nd->d_nout_h, sizeof(sg_conc_result) * nd->cfg.max_batch) != hipSuccess))
+        return nfail(nd, SG_E_NOMEM, "node host-path buffers");
+    NHIP(nd, hipMemcpy(nd->d_nreq_h, req, sizeof(sg_conc_req) * n, hipMemcpyHostToDevice));
+    const int rc = sg_node_conc_decide_batch(nd, static_cast<const sg_conc_req*>(nd->d_nreq_h), n,
+                                             static_cast<sg_conc_result*>(nd->d_nout_h), nullptr);
+    if (rc) return rc;
+    NHIP(nd, hipMemcpy(out, nd->d_nout_h, sizeof(sg_conc_result) * n, hipMemcpyDeviceToHost));
+    return SG_OK;
+}
+
+int sg_node_conc_set_rule_timeouts(sg_node* nd, const int64_t* client_offline_ms, const int64_t* resource_timeout_ms,
+                                   uint32_t n) {
+    if (!nd || (n && (!client_offline_ms || !resource_timeout_ms))) return SG_E_INVAL;
+    if (n != nd->shard_of.size()) return nfail(nd, SG_E_INVAL, "one timeout pair per loaded rule");
+    node_drain(nd);
+    const uint32_t G = (uint32_t)nd->shards.size();
+    std::vector<std::vector<int64_t>> off(G), res(G);
+    for (uint32_t g = 0; g < G; ++g) {
+        off[g].resize(nd->shards[g]->K);
+        res[g].resize(nd->shards[g]->K);
+    }
+    for (uint32_t k = 0; k < n; ++k) {
+        off[nd->shard_of[k]][nd->local_of[k]] = client_offline_ms[k];
+        res[nd->shard_of[k]][nd->local_of[k]] = resource_timeout_ms[k];
+    }
+    for (uint32_t g = 0; g < G; ++g) {
+        sg_handle* h = nd->shards[g];
+        const int rc = sg_conc_set_rule_timeouts(h, off[g].data(), res[g].data(), (uint32_t)off[g].size());
+        if (rc) return node_child(nd, h, rc);
+    }
+    return SG_OK;
+}
+
+int sg_node_conc_expire(sg_node* nd, int64_t now_ms, const uint8_t* client_online, uint32_t n_clients, uint64_t* removed) {
+    if (!nd || !removed) return SG_E_INVAL;
+    node_drain(nd);
+    uint64_t total = 0;
+    for (sg_handle* h : nd->shards) {
+        uint64_t r = 0;
+        const int rc = sg_conc_expire(h, now_ms, client_online, n_clients, &r);
+        if (rc) return node_child(nd, h, rc);
+        total += r;
+    }
+    *removed = total;
+    return SG_OK;
+}
+
+int sg_node_conc_read_state(sg_node* nd, uint32_t key, int32_t* now_calls, uint64_t* live_tokens) {
+    if (!nd || !now_calls || !live_tokens || key >= nd->shard_of.size()) return SG_E_INVAL;
+    node_drain(nd);
+    uint64_t live = 0;
+    for (uint32_t g = 0; g < (uint32_t)nd->shards.size(); ++g) {
+        int32_t nc = 0;
+        uint64_t l = 0;
+        sg_handle* h = nd->shards[g];
+        const bool owner = g == nd->shard_of[key];
+        if (!owner && h->K == 0) continue;
+        const int rc = sg_conc_read_state(h, owner ? nd->local_of[key] : 0u, &nc, &l);
+        if (rc) return node_child(nd, h, rc);
+        if (owner) *now_calls = nc;
+        live += l;
+    }
+    *live_tokens = live;
     return SG_OK;
 }
 

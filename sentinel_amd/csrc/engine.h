@@ -811,6 +811,38 @@ hipError_t launch_route(const RouteArgs& r, hipStream_t stream);
 hipError_t launch_route_gather(const sg_result* sub_out, const uint32_t* sub_pos, uint64_t total, sg_result* out,
                                hipStream_t stream);
 uint64_t route_tiles(uint64_t n);
+// Node routing of cluster param / concurrent token batches (node.hip k_nreq_*): owner records, the slices.
+struct NodeReqArgs {
+    uint64_t n;
+    const sg_cparam_req* cp;   // a param batch (node order), or null
+    const sg_conc_req* cc;     // a concurrent-token batch, or null
+    const uint64_t* values;    // param: the batch's values
+    uint64_t n_values;
+    uint32_t K;                // node rules of the kind (param rules / flow rules)
+    const uint8_t* shard_of;   // [K] owner shard
+    const uint32_t* local_of;  // [K] the rule's index on its owner
+    int G;
+    uint64_t* rec;             // [n] {owner : 8 | request index : 56}
+    uint32_t* nvals;           // [n] value count per request (param; 0 out of bounds)
+    uint32_t* cnt;             // [kMaxShards] requests per shard (zeroed before)
+    uint32_t* vcnt;            // [kMaxShards] values per shard (zeroed before)
+    uint32_t* tsum;            // [tiles] value-count tile sums, then their exclusive scan
+    const uint32_t* vbase;     // [kMaxShards] first value of each shard's slice (node value array)
+    sg_cparam_req* sub_cp;     // [n] param slices, one after the other
+    sg_conc_req* sub_cc;       // [n] concurrent slices
+    uint64_t* sub_vals;        // [n_values] the slices' values
+    uint32_t* sub_pos;         // [n] node position of each slice entry
+    int* err;
+    int64_t last_ts;           // the node's previous batch of this kind: its last timestamp (-1: none)
+};
+hipError_t launch_nreq_keys(const NodeReqArgs& q, hipStream_t stream);
+hipError_t launch_nreq_gather(const NodeReqArgs& q, const uint64_t* sorted, hipStream_t stream);
+uint64_t nreq_tiles(uint64_t n);
+hipError_t launch_nsnap_scatter(const double* part, const uint32_t* node_key, uint64_t cnt, double* out,
+                                hipStream_t stream);
+hipError_t launch_nconc_scatter(const sg_conc_result* sub_out, const uint32_t* sub_pos, const sg_conc_req* sub_req,
+                                uint64_t base, uint64_t cnt, uint32_t g, uint32_t G, sg_conc_result* out,
+                                hipStream_t stream);
 // sort.hip: stable LSD radix sort of records on bits [lo_bit, hi_bit); result buffer is a or b.
 size_t radix_hist_words(uint64_t n);
 int radix_digit_bits(int bits);  // digit width radix_sort_records uses for `bits` key bits (8 or 10)

@@ -212,4 +212,204 @@ hipError_t launch_route_gather(const sg_result* sub_out, const uint32_t* sub_pos
 
 uint64_t route_tiles(uint64_t n) { return (n + kRouteTile - 1) / kRouteTile; }
 
+// ---- cluster param and concurrent token batches over the node (sg_node_cparam_*, sg_node_conc_*) ----
+//
+// DefaultTokenService.requestParamToken / requestConcurrentToken / releaseConcurrentToken (DefaultTokenService.java
+// :53-85) for the whole node: a request goes to the shard that owns its flowId (a param rule's flowId; a flow rule's
+// for concurrent tokens; a release to the shard whose token it names: node token id = (shard token id - 1) * G +
+// shard + 1), and every shard decides its slice in the node's order. Requests nothing owns (invalid keys, null
+// tokens) go to shard 0, whose validation answers them. Routing is a stable partition by owner: a record {owner : 8 |
+// request index} per request, one 8-bit radix pass, then the slices gathered (keys and token ids made shard-local;
+// a param request's values copied after the slice's earlier ones, its value_begin rebased).
+
+__global__ void __launch_bounds__(256) k_nreq_keys(NodeReqArgs q) {
+    __shared__ uint32_t cnt[kMaxShards], vcnt[kMaxShards];
+    const int tid = threadIdx.x;
+    if (tid < kMaxShards) cnt[tid] = vcnt[tid] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + tid; i < q.n; i += (uint64_t)gridDim.x * 256) {
+        uint32_t g = 0, nv = 0;
+        {  // the node's time order (a batch older than the node's previous one, or unsorted, is refused whole)
+            const int64_t t = q.cp ? q.cp[i].ts_ms : q.cc[i].ts_ms;
+            const int64_t tp = i == 0 ? q.last_ts : (q.cp ? q.cp[i - 1].ts_ms : q.cc[i - 1].ts_ms);
+            if (t < 0 || t < tp) atomicOr(q.err, kErrTime);
+        }
+        if (q.cp) {
+            const sg_cparam_req r = q.cp[i];
+            if (r.key < q.K) g = q.shard_of[r.key];
+            nv = r.value_count;
+            if (nv && ((uint64_t)r.value_begin + nv > q.n_values)) {  // the whole batch is refused (SG_E_INVAL)
+                atomicOr(q.err, kErrBounds);
+                nv = 0;
+            }
+        } else {
+            const sg_conc_req r = q.cc[i];
+            if (r.kind == SG_CONC_RELEASE) g = r.token_id ? (uint32_t)((r.token_id - 1) % (uint64_t)q.G) : 0u;
+            else if ((r.key & SG_KEY_INDEX) < q.K) g = q.shard_of[r.key & SG_KEY_INDEX];
+        }
+        q.rec[i] = ((uint64_t)g << 56) | i;
+        q.nvals[i] = nv;
+        atomicAdd(&cnt[g], 1u);
+        if (nv) atomicAdd(&vcnt[g], nv);
+    }
+    __syncthreads();
+    if (tid < q.G) {
+        if (cnt[tid]) atomicAdd(&q.cnt[tid], cnt[tid]);
+        if (vcnt[tid]) atomicAdd(&q.vcnt[tid], vcnt[tid]);
+    }
+}
+
+// Exclusive scan of the sorted requests' value counts (param batches): per 4096-request tile sums, one block over the
+// tile sums, then each tile's requests (nvals in node order, read through the sorted records).
+constexpr uint32_t kNvTile = 4096;
+__global__ void __launch_bounds__(256) k_nreq_vsum(NodeReqArgs q, const uint64_t* sorted) {
+    __shared__ uint32_t ws[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kNvTile;
+    uint32_t s = 0;
+    for (uint64_t j = t0 + threadIdx.x; j < min(q.n, t0 + kNvTile); j += 256)
+        s += q.nvals[sorted[j] & 0xFFFFFFFFFFFFFFull];
+    for (int o = 32; o > 0; o >>= 1) s += (uint32_t)__shfl_xor((int)s, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) q.tsum[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void __launch_bounds__(1024) k_nreq_vscan(NodeReqArgs q, uint32_t tiles) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < tiles; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < tiles ? q.tsum[i] : 0u;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t x = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] += x;
+            __syncthreads();
+        }
+        const uint32_t c = carry;
+        if (i < tiles) q.tsum[i] = c + part[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = c + part[1023];
+        __syncthreads();
+    }
+}
+
+// The slices: sub_req[j] = the request of sorted record j with its key (and token id) made shard-local, its value
+// range copied and rebased (param), sub_pos[j] its node position. One block per 4096 sorted records; the value
+// offsets inside the tile by a block scan.
+__global__ void __launch_bounds__(256) k_nreq_gather(NodeReqArgs q, const uint64_t* sorted) {
+    __shared__ uint32_t ws[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kNvTile;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t run = q.cp ? q.tsum[blockIdx.x] : 0u;
+    for (uint64_t b0 = t0; b0 < min(q.n, t0 + kNvTile); b0 += 256) {
+        const uint64_t j = b0 + threadIdx.x;
+        const bool act = j < q.n;
+        const uint64_t rec = act ? sorted[j] : 0ull;
+        const uint32_t g = (uint32_t)(rec >> 56);
+        const uint64_t i = rec & 0xFFFFFFFFFFFFFFull;
+        uint32_t nv = (act && q.cp) ? q.nvals[i] : 0u;
+        // block-exclusive scan of nv
+        uint32_t x = nv;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wave] = x;
+        __syncthreads();
+        uint32_t off = run + x - nv;
+        uint32_t tot = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wave) off += ws[w];
+            tot += ws[w];
+        }
+        __syncthreads();
+        run += tot;
+        if (!act) continue;
+        q.sub_pos[j] = (uint32_t)i;
+        if (q.cp) {
+            sg_cparam_req r = q.cp[i];
+            if (r.key < q.K) r.key = q.local_of[r.key];
+            for (uint32_t v = 0; v < nv; ++v) q.sub_vals[off + v] = q.values[r.value_begin + v];
+            r.value_begin = nv ? off - q.vbase[g] : 0u;
+            q.sub_cp[j] = r;
+        } else {
+            sg_conc_req r = q.cc[i];
+            if (r.kind == SG_CONC_RELEASE) {
+                if (r.token_id) r.token_id = (r.token_id - 1) / (uint64_t)q.G + 1;
+            } else if ((r.key & SG_KEY_INDEX) < q.K) {
+                r.key = q.local_of[r.key & SG_KEY_INDEX] | (r.key & ~SG_KEY_INDEX);
+            }
+            q.sub_cc[j] = r;
+        }
+    }
+}
+
+// Concurrent results back in node order, shard g's slice [base, base + cnt): an acquire's token id in node terms.
+__global__ void __launch_bounds__(256) k_nconc_scatter(const sg_conc_result* sub_out, const uint32_t* sub_pos,
+                                                       const sg_conc_req* sub_req, uint64_t base, uint64_t cnt,
+                                                       uint32_t g, uint32_t G, sg_conc_result* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < cnt; j += (uint64_t)gridDim.x * 256) {
+        sg_conc_result r = sub_out[base + j];
+        if (sub_req[base + j].kind != SG_CONC_RELEASE && r.token_id) r.token_id = (r.token_id - 1) * G + g + 1;
+        out[sub_pos[base + j]] = r;
+    }
+}
+
+// The node snapshot from shard g's part (its local rule order): out[2 node_key[j] + c] = part[2 j + c].
+__global__ void __launch_bounds__(256) k_nsnap_scatter(const double* part, const uint32_t* node_key, uint64_t cnt,
+                                                       double* out) {
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < cnt; j += (uint64_t)gridDim.x * 256) {
+        const uint32_t k = node_key[j];
+        out[2 * (uint64_t)k] = part[2 * j];
+        out[2 * (uint64_t)k + 1] = part[2 * j + 1];
+    }
+}
+
+hipError_t launch_nsnap_scatter(const double* part, const uint32_t* node_key, uint64_t cnt, double* out,
+                                hipStream_t stream) {
+    if (cnt == 0) return hipSuccess;
+    uint64_t b = (cnt + 255) / 256;
+    if (b > 8192) b = 8192;
+    hipLaunchKernelGGL(k_nsnap_scatter, dim3((unsigned)b), dim3(256), 0, stream, part, node_key, cnt, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_nreq_keys(const NodeReqArgs& q, hipStream_t stream) {
+    if (q.n == 0) return hipSuccess;
+    uint64_t g = (q.n + 255) / 256;
+    if (g > 4096) g = 4096;
+    lds_poison(stream);
+    hipLaunchKernelGGL(k_nreq_keys, dim3((unsigned)g), dim3(256), 0, stream, q);
+    return hipGetLastError();
+}
+
+hipError_t launch_nreq_gather(const NodeReqArgs& q, const uint64_t* sorted, hipStream_t stream) {
+    if (q.n == 0) return hipSuccess;
+    const uint32_t tiles = (uint32_t)((q.n + kNvTile - 1) / kNvTile);
+    if (q.cp) {
+        hipLaunchKernelGGL(k_nreq_vsum, dim3(tiles), dim3(256), 0, stream, q, sorted);
+        hipLaunchKernelGGL(k_nreq_vscan, dim3(1), dim3(1024), 0, stream, q, tiles);
+    }
+    hipLaunchKernelGGL(k_nreq_gather, dim3(tiles), dim3(256), 0, stream, q, sorted);
+    return hipGetLastError();
+}
+
+uint64_t nreq_tiles(uint64_t n) { return (n + kNvTile - 1) / kNvTile; }
+
+hipError_t launch_nconc_scatter(const sg_conc_result* sub_out, const uint32_t* sub_pos, const sg_conc_req* sub_req,
+                                uint64_t base, uint64_t cnt, uint32_t g, uint32_t G, sg_conc_result* out,
+                                hipStream_t stream) {
+    if (cnt == 0) return hipSuccess;
+    uint64_t b = (cnt + 255) / 256;
+    if (b > 8192) b = 8192;
+    hipLaunchKernelGGL(k_nconc_scatter, dim3((unsigned)b), dim3(256), 0, stream, sub_out, sub_pos, sub_req, base, cnt, g,
+                       G, out);
+    return hipGetLastError();
+}
+
 }  // namespace sg

@@ -32,7 +32,10 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_node_create", "sg_node_destroy", "sg_node_last_error", "sg_node_set_namespaces", "sg_node_load_flow_rules",
            "sg_node_flow_decide_batch", "sg_node_flow_decide_batch_host", "sg_node_flow_read_state",
            "sg_node_snapshot_metrics", "sg_node_shard_of", "sg_node_flow_enqueue", "sg_node_flow_poll",
-           "sg_node_flow_wait", "sg_local_metrics_raw", "sg_local_owners"]
+           "sg_node_flow_wait", "sg_local_metrics_raw", "sg_local_owners", "sg_node_cparam_load_rules",
+           "sg_node_cparam_decide_batch", "sg_node_cparam_decide_batch_host", "sg_node_cparam_read_sum",
+           "sg_node_cparam_top_values", "sg_node_conc_set_rule_timeouts", "sg_node_conc_decide_batch",
+           "sg_node_conc_decide_batch_host", "sg_node_conc_expire", "sg_node_conc_read_state"]
 
 _lib = None
 
@@ -140,6 +143,16 @@ def load_library():
         "sg_node_flow_wait": (C.c_int, [vp, u64]),
         "sg_local_metrics_raw": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
         "sg_local_owners": (C.c_int, [vp, u32, vp, u32]),
+        "sg_node_cparam_load_rules": (C.c_int, [vp, vp, u32, vp, u32, C.c_int32]),
+        "sg_node_cparam_decide_batch": (C.c_int, [vp, vp, u64, vp, u64, vp, vp]),
+        "sg_node_cparam_decide_batch_host": (C.c_int, [vp, vp, u64, vp, u64, vp]),
+        "sg_node_cparam_read_sum": (C.c_int, [vp, u32, u64, i64, vp]),
+        "sg_node_cparam_top_values": (C.c_int, [vp, i64, u32, vp, vp, vp]),
+        "sg_node_conc_set_rule_timeouts": (C.c_int, [vp, vp, vp, u32]),
+        "sg_node_conc_decide_batch": (C.c_int, [vp, vp, u64, vp, vp]),
+        "sg_node_conc_decide_batch_host": (C.c_int, [vp, vp, u64, vp]),
+        "sg_node_conc_expire": (C.c_int, [vp, i64, vp, u32, C.POINTER(u64)]),
+        "sg_node_conc_read_state": (C.c_int, [vp, u32, C.POINTER(C.c_int32), C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("SG_LIB_PATH") and not hasattr(L, name):
@@ -225,6 +238,67 @@ class NodeEngine:
         out = np.zeros(2 * max(n_rules, 1), np.float64)
         self._check(self._L.sg_node_snapshot_metrics(self.h, now_ms, abi.ptr(out), len(out)))
         return out[:2 * n_rules].reshape(n_rules, 2)
+
+    # ---- cluster param and concurrent tokens sharded over the node (FlowEngine's cparam_* / conc_* shapes)
+    def cparam_load_rules(self, rules: np.ndarray, hot: np.ndarray = None, capacity_log2=0):
+        rules = np.ascontiguousarray(rules, dtype=abi.CPARAM_RULE_DTYPE)
+        hot = np.ascontiguousarray(np.zeros(0, abi.PARAM_HOT_DTYPE) if hot is None else hot, dtype=abi.PARAM_HOT_DTYPE)
+        self._check(self._L.sg_node_cparam_load_rules(self.h, abi.ptr(rules), len(rules), abi.ptr(hot), len(hot),
+                                                      capacity_log2))
+
+    def cparam_decide_host(self, req: np.ndarray, values: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.CPARAM_REQ_DTYPE)
+        values = np.ascontiguousarray(values, dtype=np.uint64)
+        out = np.zeros(len(req), abi.RES_DTYPE)
+        self._check(self._L.sg_node_cparam_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(values),
+                                                              len(values), abi.ptr(out)))
+        return out
+
+    def cparam_decide_device(self, req_ptr: int, n: int, values_ptr: int, n_values: int, out_ptr: int,
+                             stream_ptr: int = 0):
+        self._check(self._L.sg_node_cparam_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(values_ptr),
+                                                        n_values, C.c_void_p(out_ptr), C.c_void_p(stream_ptr)))
+
+    def cparam_top_values(self, now_ms, n_rules, number=5):
+        vals = np.zeros(max(1, n_rules * number), np.uint64)
+        qps = np.zeros(max(1, n_rules * number), np.float64)
+        cnt = np.zeros(max(1, n_rules), np.uint32)
+        self._check(self._L.sg_node_cparam_top_values(self.h, now_ms, number, abi.ptr(vals), abi.ptr(qps),
+                                                      abi.ptr(cnt)))
+        return [[(int(vals[r * number + i]), float(qps[r * number + i])) for i in range(int(cnt[r]))]
+                for r in range(n_rules)]
+
+    def cparam_sum(self, rule, value, now):
+        v = C.c_int64()
+        self._check(self._L.sg_node_cparam_read_sum(self.h, rule, int(value), now, C.byref(v)))
+        return v.value
+
+    def conc_set_rule_timeouts(self, client_offline_ms, resource_timeout_ms):
+        a = np.ascontiguousarray(client_offline_ms, dtype=np.int64)
+        b = np.ascontiguousarray(resource_timeout_ms, dtype=np.int64)
+        self._check(self._L.sg_node_conc_set_rule_timeouts(self.h, abi.ptr(a), abi.ptr(b), len(a)))
+
+    def conc_decide_host(self, req: np.ndarray) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=abi.CONC_REQ_DTYPE)
+        out = np.zeros(len(req), abi.CONC_RES_DTYPE)
+        self._check(self._L.sg_node_conc_decide_batch_host(self.h, abi.ptr(req), len(req), abi.ptr(out)))
+        return out
+
+    def conc_decide_device(self, req_ptr: int, n: int, out_ptr: int, stream_ptr: int = 0):
+        self._check(self._L.sg_node_conc_decide_batch(self.h, C.c_void_p(req_ptr), n, C.c_void_p(out_ptr),
+                                                      C.c_void_p(stream_ptr)))
+
+    def conc_expire(self, now_ms, online) -> int:
+        online = np.ascontiguousarray(online, dtype=np.uint8)
+        rm = C.c_uint64()
+        self._check(self._L.sg_node_conc_expire(self.h, now_ms, abi.ptr(online) if len(online) else None,
+                                                len(online), C.byref(rm)))
+        return rm.value
+
+    def conc_state(self, key):
+        now, live = C.c_int32(), C.c_uint64()
+        self._check(self._L.sg_node_conc_read_state(self.h, key, C.byref(now), C.byref(live)))
+        return now.value, live.value
 
 
 class FlowEngine:
