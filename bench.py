@@ -245,6 +245,197 @@ def node_main(args):
     }), flush=True)
 
 
+C5_PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06_c5_node_pmc_summary.json")
+
+
+def c5_rules(K):
+    """BASELINE configs[4]: every resource a QPS FlowRule (count U{1..64}) + an RT breaker (100 ms, slow ratio 0.5)
+    + an exception-ratio breaker (0.5), statIntervalMs 1000, minRequestAmount 5, timeWindow 10 s (bench_configs c5)."""
+    from oracle.binding import degrade_rule
+    rng = np.random.default_rng(5)
+    rules = np.zeros(K, abi.LOCAL_RULE_DTYPE)
+    rules["flow_count"] = rng.integers(1, 65, K).astype(np.float64)
+    rules["flow_grade"] = abi.FLOW_GRADE_QPS
+    rules["n_breakers"] = 2
+    b = np.zeros(2, abi.DEGRADE_RULE_DTYPE)
+    b[0] = degrade_rule(abi.DEGRADE_RT, 100, 10, 5, 1000, 0.5)
+    b[1] = degrade_rule(abi.DEGRADE_EXCEPTION_RATIO, 0.5, 10, 5, 1000)
+    rules["breakers"] = b
+    return rules
+
+
+def c5_trace(rules, own, n, n_batches, rank, check, t0=1_700_000_000_000):
+    """This rank's share of the node's C5 trace: the entries of the resources it owns (Zipf(1.0) popularity over the
+    node's resources, restricted to `own` — the node trace split by owner, since resources share no state) and the
+    exits of the passed ones, produced by the oracle's client model over the owned resources (oracle.binding
+    LocalTraceGen: the exits depend on the decisions). Returns per batch (events with node resource ids, the
+    oracle's decisions, the oracle's raw metric rows at the batch's end with node ids — check only) and the oracle's
+    replay seconds (the cpu_baseline)."""
+    from oracle.binding import LocalChain, LocalTraceGen
+    K = len(rules)
+    perm = np.random.default_rng(5).permutation(K)             # popularity rank -> resource
+    rank_of = np.empty(K, np.int64)
+    rank_of[perm] = np.arange(K)
+    w = 1.0 / (rank_of[own].astype(np.float64) + 1.0)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    ora = LocalChain(2, 1000, 500)
+    ora.load_rules(rules[own])
+    ora.set_entry_types(np.ones(len(own), np.uint8))
+    gen = LocalTraceGen(ora)
+    rng = np.random.default_rng(5 + 1000 * rank)
+    out, gen_s = [], 0.0
+    for bt in range(n_batches):
+        ent = np.zeros(n, abi.LOCAL_EVENT_DTYPE)
+        ent["ts_ms"] = t0 + 1000 * bt + np.sort(rng.integers(0, 1000, n))
+        ent["resource"] = np.minimum(np.searchsorted(cdf, rng.random(n), side="right"), len(own) - 1)
+        ent["count"] = 1
+        rt = np.minimum(np.round(np.exp(rng.normal(2.5, 0.8, n))), 10_000).astype(np.int32)
+        err = (rng.random(n) < 0.05).astype(np.uint8)
+        t = time.perf_counter()
+        ev, res = gen.run(ent, rt, err, t0 + 1000 * (bt + 1))
+        gen_s += time.perf_counter() - t
+        rows = ora.metrics(t0 + 1000 * (bt + 1), raw=True) if check else None
+        ev["resource"] = own[ev["resource"]].astype(np.uint32)
+        if rows is not None:
+            m = rows["resource"] != abi.ENTRY_NODE_RESOURCE
+            rows["resource"][m] = own[rows["resource"][m]].astype(np.uint32)
+        out.append((ev, res, rows))
+    return out, gen_s
+
+
+def c5_main(args, rank, world, dev, coll, one_dev):
+    """--workload c5: BASELINE configs[4] (1M resources, QPS FlowRule + RT + exception-ratio breakers, minute window)
+    over the node's GPUs, one rank per GPU. Every rank loads the node's rules (all resources EntryType.IN) and decides
+    the entries and exits of the resources sg_local_owners gives it (weak scaling: --requests entries per rank per
+    1000 ms step plus the exits of the passed ones); after each batch the node's MetricTimerListener rows of that
+    second are rolled up on the devices (sg_local_metrics_raw_device, then DeviceLocalMetricRollup: RCCL all_gather
+    of the rows, ENTRY_NODE sums and the (timestamp, resource) order on the GPU). The event stream depends on the
+    decisions, so each rank's share is produced by the oracle's client model before the timed region. With --check
+    (on by default in the SG_BENCH_ONE_DEVICE rehearsal) every decision and every merged row is compared with the
+    oracle's node replay after the timed region."""
+    from sentinel_amd.cluster import DeviceLocalMetricRollup, merge_metric_rows
+    check = args.check or one_dev
+    K, n = args.resources, args.requests
+    rules = c5_rules(K)
+    eng = FlowEngine(device=dev.index, max_batch=1)
+    eng.local_load_rules(rules, 2, 1000, 500)
+    eng.local_set_entry_types(np.ones(K, np.uint8))
+    owners = eng.local_owners(world)                         # sg_local_owners: the routing of the node's events
+    own = np.nonzero(owners == rank)[0]
+    total_steps = args.warmup + args.steps
+    t_gen = time.time()
+    trace, gen_s = c5_trace(rules, own, n, total_steps, rank, check)
+    print(f"# c5 rank {rank}: {len(own)} resources, {sum(len(e) for e, _, _ in trace)} events from the oracle client "
+          f"model in {time.time() - t_gen:.1f} s", file=sys.stderr, flush=True)
+    sizes = [len(e) for e, _, _ in trace]
+    eng.close()
+    eng = FlowEngine(device=dev.index, max_batch=max(sizes))
+    eng.local_load_rules(rules, 2, 1000, 500)
+    eng.local_set_entry_types(np.ones(K, np.uint8))
+    batches = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e, _, _ in trace]
+    outs = [torch.empty(sz * abi.LOCAL_RES_DTYPE.itemsize, dtype=torch.uint8, device=dev) for sz in sizes]
+    rows_buf = torch.empty((2 * len(own) + 256, 8), dtype=torch.int64, device=dev)
+    rollup = DeviceLocalMetricRollup(coll)
+    merged = [None] * total_steps
+    t0 = 1_700_000_000_000
+    torch.cuda.synchronize()
+
+    def step(b):
+        tk = eng.local_enqueue(batches[b].data_ptr(), sizes[b], outs[b].data_ptr())
+        k = eng.local_metrics_raw_device(t0 + 1000 * (b + 1), rows_buf)   # completes batch b first
+        merged[b] = rollup.run(rows_buf[:k])
+        eng.local_wait(tk)
+
+    for b in range(args.warmup):
+        step(b)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for b in range(args.warmup, total_steps):
+        step(b)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    stats = torch.tensor([elapsed, float(sum(sizes[args.warmup:]))], dtype=torch.float64, device=coll)
+    if world > 1:
+        t_max = stats[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, decided = float(t_max.item()), float(tot.item())
+    else:
+        elapsed, decided = elapsed, float(stats[1].item())
+
+    parity = None
+    if check:  # every decision of this rank, then the merged rows of every second against the node replay
+        bad = 0
+        for b in range(total_steps):
+            got = outs[b].cpu().numpy().view(abi.LOCAL_RES_DTYPE)
+            bad += int((got != trace[b][1]).sum())
+        rows_ok = True
+        for b in range(total_steps):
+            parts = [trace[b][2]]
+            if world > 1:
+                allp = [None] * world
+                dist.all_gather_object(allp, trace[b][2])
+                parts = allp
+            want = merge_metric_rows(parts)
+            got = merged[b].cpu().numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+            rows_ok &= bool(np.array_equal(got, want))
+        flags = torch.tensor([bad, 0 if rows_ok else 1], dtype=torch.int64, device=coll)
+        if world > 1:
+            dist.all_reduce(flags)
+        parity = {"decisions_differing": int(flags[0].item()), "metric_steps_differing": int(flags[1].item()),
+                  "checked": f"all {total_steps} batches on every rank against the oracle's node replay; merged "
+                             f"metric rows (ENTRY_NODE included) of every second against merge_metric_rows"}
+
+    touched = int(np.unique(trace[-1][0]["resource"] & 0x7FFFFFFF).size)
+    ms_per_step = elapsed * 1000.0 / args.steps
+    # per event 32 B in + 8 B out; per touched resource: second window 2x128 B, two minute buckets 2x2x64 B, head
+    # (threads + two breakers) 2x128 B, rule 80 B (bench_configs c5); per rank and step
+    b_alg = sizes[-1] * (32 + 8) + touched * (2 * 128 + 2 * 2 * 64 + 2 * 128 + 80)
+    step_gbs = b_alg / (ms_per_step / 1000.0) / 1e9
+    traffic = None
+    if os.path.exists(C5_PMC_SUMMARY):
+        traffic = json.load(open(C5_PMC_SUMMARY)).get("pipeline_bytes_per_step")
+    result = {
+        "metric": "local flow + circuit-breaker decisions/sec (entries + exits), 1M resources, 1/2/4/8 GPU",
+        "value": decided / elapsed, "unit": "decisions/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded): Zipf(1.0) resources, rt lognormal(2.5, 0.8) ms, 5% errors; exits generated by "
+                "the oracle client model",
+        "config": {"workload": "C5: 1M resources x (QPS FlowRule + RT breaker + exception-ratio breaker), minute "
+                               "window, --requests entries per GPU per 1000 ms step + exits of passed entries, "
+                               "resources sharded by sg_local_owners, per-step device metric rollup",
+                   "resources": K, "resources_per_gpu": len(own), "entries_per_step_per_gpu": n,
+                   "events_last_step_per_gpu": sizes[-1],
+                   "parallelism": f"resources sharded by sg_local_owners x{world}" + (" (one-device rehearsal)" if one_dev else ""),
+                   "rollup": ("DeviceLocalMetricRollup per step (RCCL all_gather of raw rows, merge on device)"
+                              if world > 1 and not one_dev else
+                              "DeviceLocalMetricRollup per step (gloo rehearsal)" if world > 1 else
+                              "DeviceLocalMetricRollup per step (merge on device, 1 GPU)")},
+        "roofline": {"bound": "hbm", "kernel": "whole step (local pipeline + metric rows + rollup), step time",
+                     "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_gbs / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": os.path.relpath(C5_PMC_SUMMARY, ROOT) if traffic else None,
+                     "algorithmic_bytes_per_step": b_alg, "touched_resources": touched},
+    }
+    if parity is not None:
+        result["parity"] = parity
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = {"value": sum(sizes) / gen_s, "unit": "decisions/s", "cores": 1, "kind": "port",
+                                  "sample": f"the oracle (oracle/liboracle.so LocalChain) replaying all {sum(sizes)} "
+                                            f"events of this rank while generating them (client model, 1 thread), "
+                                            f"{gen_s:.1f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def launch_ranks(n):
     """Run this script as n ranks of one node (the driver's own launch line), as a child process."""
     import socket
@@ -271,6 +462,13 @@ def main():
     ap.add_argument("--limiter-qps", type=float, default=0.0,
                     help="namespace GlobalRequestLimiter maxAllowedQps (SURVEY §8d C3's second run: 1e12 exercises the "
                          "pre-pass without rejecting); 0: limiter off, the headline configuration")
+    ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
+                    help="c3: the headline cluster token server (default); c5: BASELINE configs[4], the local chain "
+                         "with breakers over --resources resources, sharded by sg_local_owners, per-step metric rollup")
+    ap.add_argument("--resources", type=int, default=1_000_000, help="c5: the node's resources")
+    ap.add_argument("--check", action="store_true",
+                    help="c5: compare every decision and merged metric row with the oracle's node replay (untimed; "
+                         "on by default under SG_BENCH_ONE_DEVICE=1)")
     ap.add_argument("--node", action="store_true",
                     help="one process, one sg_node over --gpus N devices: node-order batches of N x --requests over "
                          "N x --flows flowIds, routing inside the library and inside the timed region")
@@ -302,6 +500,8 @@ def main():
     dev = torch.device("cuda", local_rank)
     coll = torch.device("cpu") if one_dev else dev  # where the collectives' tensors live
     torch.cuda.set_device(dev)
+    if args.workload == "c5":
+        return c5_main(args, rank, world, dev, coll, one_dev)
 
     wl = ShardWorkload(args.flows, args.requests, rank, world, dev)
     eng = FlowEngine(device=local_rank, max_batch=args.requests)

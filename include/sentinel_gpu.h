@@ -730,6 +730,10 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
  * rows, which the node's rollup merges (sentinel_amd/cluster.py LocalMetricRollup: the ENTRY_NODE rows of the same
  * second are summed over the GPUs, then rt = Σrt / Σsuccess), with the same side effects as sg_local_metrics. */
 int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows);
+/* sg_local_metrics_raw into DEVICE memory (d_out on the handle's device), rows unsorted, complete on return: the
+ * node's device rollup (cluster.DeviceLocalMetricRollup: RCCL all_gather of the rows, ENTRY_NODE sums and the
+ * (timestamp, resource) order on the GPU). Same side effects, same SG_E_CAPACITY contract. */
+int sg_local_metrics_raw_device(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* n_rows);
 /* The local chain sharded over a node's GPUs (one process per GPU): every GPU loads the same rules and
  * decides the entries and exits of the resources it owns — owner[r] = splitmix64(g(r)) mod world, g(r) the smallest
  * resource of r's key group (RELATE references; on an embedded token server also the resources sharing a flowId or

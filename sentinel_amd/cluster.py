@@ -249,3 +249,64 @@ class LocalMetricRollup:
         dist.all_gather(parts, mine, group=self.group)
         got = [p.cpu().numpy()[:k].copy().view(abi.METRIC_NODE_DTYPE).reshape(-1) for p, k in zip(parts, sizes)]
         return merge_metric_rows(got)
+
+
+class DeviceLocalMetricRollup:
+    """LocalMetricRollup with the rows kept in HBM: every GPU's sg_local_metrics_raw_device rows (int64 [n, 8], 64 B
+    each) all-gathered over RCCL (row counts first, then the rows padded to the largest) and merged on the device —
+    resource rows' rt = rt / success when success != 0, Constants.ENTRY_NODE rows of one second summed over the GPUs
+    then rt = Σrt / Σsuccess and isValidMetricNode on the sums, every row ordered by (timestamp, resource) — the same
+    table as merge_metric_rows, as a device tensor. Collective tensors live on coll_device (the rank's GPU for "nccl",
+    the CPU for gloo); the merged table is returned there."""
+
+    def __init__(self, coll_device, group=None):
+        self.coll = torch.device(coll_device)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+
+    def gather(self, rows: torch.Tensor) -> torch.Tensor:
+        rows = rows.to(self.coll)
+        if self.world == 1:
+            return rows
+        n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=self.coll)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(x.item()) for x in sizes]
+        m = max(1, max(sizes))
+        mine = torch.zeros((m, 8), dtype=torch.int64, device=self.coll)
+        mine[:rows.shape[0]] = rows
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        return torch.cat([p[:k] for p, k in zip(parts, sizes)])
+
+    @staticmethod
+    def merge(rows: torch.Tensor) -> torch.Tensor:
+        """merge_metric_rows on an int64 [n, 8] tensor (words: timestamp, pass, block, success, exception, rt,
+        occupied pass, resource | concurrency << 32)."""
+        res = rows[:, 7] & 0xFFFFFFFF
+        ent = res == ENTRY_NODE_RESOURCE
+        rr = rows[~ent].clone()
+        succ = rr[:, 3]
+        rr[:, 5] = torch.where(succ != 0, torch.div(rr[:, 5], torch.where(succ != 0, succ, 1), rounding_mode="floor"),
+                               rr[:, 5])
+        er = rows[ent]
+        if er.shape[0]:
+            ts, inv = torch.unique(er[:, 0], return_inverse=True)
+            sums = torch.zeros((ts.shape[0], 8), dtype=torch.int64, device=rows.device)
+            sums.index_add_(0, inv, er)
+            m = torch.zeros_like(sums)
+            m[:, 0] = ts
+            m[:, 1:6] = sums[:, 1:6]
+            s = m[:, 3]
+            m[:, 5] = torch.where(s != 0, torch.div(m[:, 5], torch.where(s != 0, s, 1), rounding_mode="floor"), m[:, 5])
+            m[:, 7] = ENTRY_NODE_RESOURCE
+            keep = (m[:, 1] > 0) | (m[:, 2] > 0) | (s > 0) | (m[:, 4] > 0) | (m[:, 5] > 0)
+            rr = torch.cat([rr, m[keep]])
+        # (timestamp, resource) order: stable sort by resource, then stable by timestamp
+        o = torch.sort(rr[:, 7] & 0xFFFFFFFF, stable=True).indices
+        rr = rr[o]
+        o = torch.sort(rr[:, 0], stable=True).indices
+        return rr[o]
+
+    def run(self, rows: torch.Tensor) -> torch.Tensor:
+        return self.merge(self.gather(rows))

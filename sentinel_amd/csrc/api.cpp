@@ -3036,7 +3036,8 @@ int sg_local_set_entry_types(sg_handle* h, const uint8_t* inbound, uint32_t n) {
 }
 
 namespace {
-int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw);
+int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw,
+                  bool device_out = false);
 void local_group_keys(sg_handle* h, std::vector<uint32_t>& gkey);
 }
 
@@ -3046,6 +3047,10 @@ int sg_local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t
 
 int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows) {
     return local_metrics(h, now_ms, out, cap, n_rows, 1);
+}
+
+int sg_local_metrics_raw_device(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* n_rows) {
+    return local_metrics(h, now_ms, d_out, cap, n_rows, 1, true);
 }
 
 int sg_local_owners(sg_handle* h, uint32_t world, uint32_t* owner, uint32_t n) {
@@ -3068,7 +3073,8 @@ int sg_local_owners(sg_handle* h, uint32_t world, uint32_t* owner, uint32_t n) {
 }
 
 namespace {
-int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw) {
+int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t cap, uint64_t* n_rows, int raw,
+                  bool device_out) {
     if (!h || !n_rows || (!out && cap)) return SG_E_INVAL;
     *n_rows = 0;
     if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
@@ -3110,6 +3116,13 @@ int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t ca
     if (cnt > cap) {
         (void)hipFree(d_cnt);
         return fail(h, SG_E_CAPACITY, "metric row buffer too small (*n_rows rows)");
+    }
+    if (device_out) {  // the rows straight into the caller's device buffer, unsorted (the node rollup sorts)
+        e = pass(out, d_cnt, 1);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        (void)hipFree(d_cnt);
+        if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
+        return SG_OK;
     }
     sg_metric_node* d_out = nullptr;
     if (cnt && hipMalloc(&d_out, sizeof(sg_metric_node) * cnt) != hipSuccess) {

@@ -2744,7 +2744,17 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
         const int64_t last = a.last_fetch[k];
         int64_t newest = last;
         uint32_t rows = 0;
-        for (int j = 0; j < kMinuteS; ++j) {  // data.list(now): present and not deprecated
+        // Only buckets that start after the earlier of the two fetch times (the resource's, and the ENTRY_NODE's for
+        // an inbound resource), before cur and inside the minute can yield a row or an ENTRY_NODE sum: their seconds
+        // s in [cur - 59 s, cur) past that fetch time, slot (s / 1000) mod 60 — one bucket per resource when the
+        // listener fetches every second, instead of all 60 (a bucket whose start is some other second fails the
+        // checks below, as in the full scan).
+        const int64_t lo_f = (inb && efetch < last) ? efetch : last;
+        int64_t s_lo = cur - (int64_t)(kMinuteS - 1) * kMinuteWl;
+        if (lo_f >= s_lo) s_lo = (lo_f >= 0 ? lo_f / kMinuteWl : -((-lo_f + kMinuteWl - 1) / kMinuteWl)) * kMinuteWl + kMinuteWl;
+        if (s_lo < 0) s_lo = 0;
+        for (int64_t s = s_lo; s < cur; s += kMinuteWl) {  // data.list(now): present and not deprecated
+            const int j = (int)((s / kMinuteWl) % kMinuteS);
             if (j == I && reset_I) continue;  // the fresh bucket at cur is never in time
             const LBucket b = m[j];
             if (b.start == INT64_MIN || now - b.start > (int64_t)kMinuteS * kMinuteWl) continue;

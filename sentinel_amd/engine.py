@@ -35,7 +35,8 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_node_flow_wait", "sg_local_metrics_raw", "sg_local_owners", "sg_node_cparam_load_rules",
            "sg_node_cparam_decide_batch", "sg_node_cparam_decide_batch_host", "sg_node_cparam_read_sum",
            "sg_node_cparam_top_values", "sg_node_conc_set_rule_timeouts", "sg_node_conc_decide_batch",
-           "sg_node_conc_decide_batch_host", "sg_node_conc_expire", "sg_node_conc_read_state"]
+           "sg_node_conc_decide_batch_host", "sg_node_conc_expire", "sg_node_conc_read_state",
+           "sg_local_metrics_raw_device"]
 
 _lib = None
 
@@ -142,6 +143,7 @@ def load_library():
         "sg_node_flow_poll": (C.c_int, [vp, u64]),
         "sg_node_flow_wait": (C.c_int, [vp, u64]),
         "sg_local_metrics_raw": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
+        "sg_local_metrics_raw_device": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
         "sg_local_owners": (C.c_int, [vp, u32, vp, u32]),
         "sg_node_cparam_load_rules": (C.c_int, [vp, vp, u32, vp, u32, C.c_int32]),
         "sg_node_cparam_decide_batch": (C.c_int, [vp, vp, u64, vp, u64, vp, vp]),
@@ -675,6 +677,14 @@ class FlowEngine:
         out = np.zeros(max(1, n.value), abi.METRIC_NODE_DTYPE)
         self._check(self._L.sg_local_metrics_raw(self.h, now_ms, abi.ptr(out), len(out), C.byref(n)))
         return out[:n.value]
+
+    def local_metrics_raw_device(self, now_ms, out) -> int:
+        """sg_local_metrics_raw_device: this GPU's raw rows into `out` (a device tensor of at least cap x 64 B, as
+        int64 [cap, 8]), unsorted; returns the row count."""
+        n = C.c_uint64()
+        cap = out.numel() * out.element_size() // abi.METRIC_NODE_DTYPE.itemsize
+        self._check(self._L.sg_local_metrics_raw_device(self.h, now_ms, C.c_void_p(out.data_ptr()), cap, C.byref(n)))
+        return n.value
 
     def local_owners(self, world) -> np.ndarray:
         """sg_local_owners: the GPU of `world` that owns each resource (key groups co-located)."""

@@ -9,12 +9,13 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from sentinel_amd import abi
-from sentinel_amd.cluster import (ENTRY_NODE_RESOURCE, LocalMetricRollup, local_group_keys, local_owners,
-                                  merge_metric_rows, split_local_events)
+from sentinel_amd.cluster import (ENTRY_NODE_RESOURCE, DeviceLocalMetricRollup, LocalMetricRollup, local_group_keys,
+                                  local_owners, merge_metric_rows, split_local_events)
 
 N_RES, N_ORIGINS = 48, 2
 T0 = 1_700_000_000_000
@@ -107,6 +108,32 @@ def test_merge_metric_rows_sums_entry_node():
     assert len(m) == 2
     assert tuple(m[0])[:6] == (1000, 3, 1, 2, 0, 25) and m[0]["resource"] == 5
     assert tuple(m[1])[:6] == (1000, 3, 0, 3, 1, 23) and m[1]["resource"] == ENTRY_NODE_RESOURCE
+    d = DeviceLocalMetricRollup.merge(torch.from_numpy(rows.view(np.int64).reshape(-1, 8).copy()))
+    assert np.array_equal(d.numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1), m)
+
+
+def test_device_merge_equals_host_merge():
+    """DeviceLocalMetricRollup.merge (torch, the device rollup's merge) equals merge_metric_rows on random rows of
+    three GPUs: resources disjoint per GPU, ENTRY_NODE rows of overlapping seconds (some empty), rows unsorted."""
+    rng = np.random.default_rng(9)
+    parts = []
+    for g in range(3):
+        n = 400
+        r = np.zeros(n + 6, abi.METRIC_NODE_DTYPE)
+        r["timestamp"] = T0 + 1000 * rng.integers(0, 5, n + 6)
+        for f in ("pass_qps", "block_qps", "success_qps", "exception_qps", "occupied_pass_qps"):
+            r[f] = rng.integers(0, 4, n + 6)
+        r["rt"] = rng.integers(0, 500, n + 6)
+        r["resource"][:n] = rng.permutation(1000)[:n] * 3 + g
+        r["resource"][n:] = ENTRY_NODE_RESOURCE
+        r["timestamp"][n:] = T0 + 1000 * (np.arange(6) // 2)   # two GPUs share each second
+        r[n + 5]["pass_qps"] = r[n + 5]["block_qps"] = r[n + 5]["success_qps"] = 0
+        r[n + 5]["exception_qps"] = r[n + 5]["rt"] = 0
+        parts.append(r[rng.permutation(n + 6)])
+    want = merge_metric_rows(parts)
+    t = torch.from_numpy(np.concatenate(parts).view(np.int64).reshape(-1, 8).copy())
+    got = DeviceLocalMetricRollup.merge(t).numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+    assert np.array_equal(got, want)
 
 
 def _worker(rank, world, port, q):
@@ -123,15 +150,20 @@ def _worker(rank, world, port, q):
         mine_chain.load_flow_rules(frules, N_ORIGINS, 0)
         mine_chain.set_entry_types(inbound)
         rollup = LocalMetricRollup("cpu")
+        drollup = DeviceLocalMetricRollup("cpu")
         bad = []
         for b, (ev, want, now, rows_want) in enumerate(trace):
             pos = split_local_events(ev, owners, world)[rank]
             got = mine_chain.decide(ev[pos])
             if not np.array_equal(got, want[pos]):
                 bad.append(f"batch {b}: {(got != want[pos]).sum()} results differ")
-            rows = rollup.run(mine_chain.metrics(now, raw=True))
+            raw = mine_chain.metrics(now, raw=True)
+            rows = rollup.run(raw)
             if not np.array_equal(rows, rows_want):
                 bad.append(f"batch {b}: metric rows differ ({len(rows)} vs {len(rows_want)})")
+            drows = drollup.run(torch.from_numpy(raw.view(np.int64).reshape(-1, 8).copy()))
+            if not np.array_equal(drows.numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1), rows_want):
+                bad.append(f"batch {b}: device-rollup rows differ")
             if b == 0 and not (rows_want["resource"] == ENTRY_NODE_RESOURCE).any():
                 bad.append("no ENTRY_NODE row in the reference")
         q.put((rank, bad))

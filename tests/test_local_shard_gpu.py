@@ -13,8 +13,13 @@ from tests.test_local_shard import N_ORIGINS, N_RES, node_setup, node_trace
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("device_rows", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_local_chain_handles_equal_node_replay(world):
+def test_sharded_local_chain_handles_equal_node_replay(world, device_rows):
+    """device_rows: sg_local_metrics_raw_device into HBM and the device rollup's merge (DeviceLocalMetricRollup)."""
+    import torch
+
+    from sentinel_amd.cluster import DeviceLocalMetricRollup
     from sentinel_amd.engine import FlowEngine
     base, frules, relate, inbound = node_setup()
     trace = node_trace(base, frules, inbound)
@@ -35,7 +40,13 @@ def test_sharded_local_chain_handles_equal_node_replay(world):
         for r in range(world):
             got = engs[r].local_decide_host(ev[parts[r]])
             assert np.array_equal(got, want[parts[r]]), f"batch {b} shard {r}: {(got != want[parts[r]]).sum()} differ"
-        rows = merge_metric_rows([e.local_metrics_raw(now) for e in engs])
+        if device_rows:
+            bufs = [torch.empty((4 * N_RES + 64, 8), dtype=torch.int64, device="cuda") for _ in engs]
+            got_rows = [buf[:e.local_metrics_raw_device(now, buf)] for e, buf in zip(engs, bufs)]
+            m = DeviceLocalMetricRollup.merge(torch.cat(got_rows))
+            rows = m.cpu().numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+        else:
+            rows = merge_metric_rows([e.local_metrics_raw(now) for e in engs])
         assert np.array_equal(rows, rows_want), f"batch {b}: metric rows differ"
         saw_entry |= bool((rows_want["resource"] == ENTRY_NODE_RESOURCE).any())
     assert saw_entry
