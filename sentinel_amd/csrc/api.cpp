@@ -11,6 +11,7 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -5629,14 +5630,10 @@ int node_nreq_route(sg_node* nd, NodeReqArgs q, std::vector<uint64_t>& base, std
     return SG_OK;
 }
 
-// Shard g's slice on its device: `bytes` per request / result, the values (param) — peer copies for shards off the
-// front's device (buffers there grown as needed). *req / *vals / *out point at what the shard decides on.
-int node_slice_to(sg_node* nd, uint32_t g, uint64_t cnt, size_t req_b, size_t out_b, const void* sreq,
-                  const uint64_t* svals, uint64_t nv, const void** req, const uint64_t** vals, void** out) {
+// Buffers for shard g's slice on its own device (shards off the front's device; grown as needed): requests,
+// results, values.
+int node_slice_alloc(sg_node* nd, uint32_t g, uint64_t nv) {
     const int dev = nd->devices[g];
-    *req = sreq;
-    *vals = svals;
-    *out = nullptr;
     if (dev == nd->devices[0]) return SG_OK;
     NHIP(nd, hipSetDevice(dev));
     const uint64_t n = nd->cfg.max_batch;
@@ -5648,12 +5645,80 @@ int node_slice_to(sg_node* nd, uint32_t g, uint64_t cnt, size_t req_b, size_t ou
         if (hipMalloc(&nd->r_vals[g], 8 * nv) != hipSuccess) return nfail(nd, SG_E_NOMEM, "shard values");
         nd->r_vals_cap[g] = nv;
     }
-    NHIP(nd, hipMemcpyPeer(nd->r_nreq[g], dev, sreq, nd->devices[0], req_b * cnt));
-    if (nv) NHIP(nd, hipMemcpyPeer(nd->r_vals[g], dev, svals, nd->devices[0], 8 * nv));
-    *req = nd->r_nreq[g];
-    *vals = nd->r_vals[g];
-    *out = nd->r_nout[g];
-    (void)out_b;
+    return SG_OK;
+}
+
+// Shard g's part of a node token batch, run by `decide(h, req, vals, out, stream)` on the shard's slice [base, base +
+// cnt) of the routed requests (req_b / out_b bytes each; nv values from svals): peer copies in and out for a shard
+// off the front's device. Every shard with work runs in its own host thread — a shard's call waits on the host
+// between its own kernels (the param fixed point's rounds, the concurrent batch's error check), so the shards overlap
+// whether they share a device or not. The first failure is reported after all have finished.
+template <class Decide>
+int node_run_shards(sg_node* nd, const std::vector<uint64_t>& base, const std::vector<uint64_t>& cnt,
+                    const std::vector<uint64_t>& vbase, const std::vector<uint64_t>& vcnt, size_t req_b, size_t out_b,
+                    const void* sub_req, void* sub_out, Decide decide) {
+    const uint32_t G = (uint32_t)nd->shards.size();
+    for (uint32_t g = 0; g < G; ++g)
+        if (cnt[g]) {
+            const int rc = node_slice_alloc(nd, g, vcnt[g]);
+            if (rc) return rc;
+        }
+    std::vector<int> rc(G, SG_OK);
+    std::vector<char> child(G, 0);
+    std::vector<std::string> msg(G);
+    auto run = [&](uint32_t g) {
+        sg_handle* h = nd->shards[g];
+        const int dev = h->device;
+        const bool remote = dev != nd->devices[0];
+        const char* sreq = static_cast<const char*>(sub_req) + req_b * base[g];
+        const uint64_t* svals = nd->d_sub_vals + vbase[g];
+        char* sout = static_cast<char*>(sub_out) + out_b * base[g];
+        hipError_t e = hipSetDevice(dev);
+        const void* req = sreq;
+        const uint64_t* vals = svals;
+        void* out = sout;
+        if (remote) {
+            if (e == hipSuccess) e = hipMemcpyPeer(nd->r_nreq[g], dev, sreq, nd->devices[0], req_b * cnt[g]);
+            if (e == hipSuccess && vcnt[g]) e = hipMemcpyPeer(nd->r_vals[g], dev, svals, nd->devices[0], 8 * vcnt[g]);
+            req = nd->r_nreq[g];
+            vals = nd->r_vals[g];
+            out = nd->r_nout[g];
+        }
+        if (e != hipSuccess) {
+            rc[g] = SG_E_DEVICE;
+            msg[g] = hipGetErrorString(e);
+            return;
+        }
+        const int r = decide(h, req, vcnt[g] ? vals : nullptr, vcnt[g], cnt[g], out, nd->streams[g]);
+        if (r) {
+            rc[g] = r;
+            child[g] = 1;
+            return;
+        }
+        e = hipStreamSynchronize(nd->streams[g]);
+        if (e == hipSuccess && remote) e = hipMemcpyPeer(sout, nd->devices[0], out, dev, out_b * cnt[g]);
+        if (e != hipSuccess) {
+            rc[g] = SG_E_DEVICE;
+            msg[g] = hipGetErrorString(e);
+        }
+    };
+    std::vector<uint32_t> work;
+    for (uint32_t g = 0; g < G; ++g)
+        if (cnt[g]) work.push_back(g);
+    if (work.size() == 1) {
+        run(work[0]);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(work.size());
+        for (uint32_t g : work) th.emplace_back(run, g);
+        for (auto& t : th) t.join();
+    }
+    (void)hipSetDevice(nd->devices[0]);
+    for (uint32_t g : work) {
+        if (!rc[g]) continue;
+        if (child[g]) return node_child(nd, nd->shards[g], rc[g]);
+        return nfail(nd, rc[g], msg[g].c_str());
+    }
     return SG_OK;
 }
 
@@ -5677,7 +5742,6 @@ int sg_node_cparam_decide_batch(sg_node* nd, const sg_cparam_req* req, uint64_t 
                                                "sharded limiter exchange)");
     int rc = node_nreq_scratch(nd, n_values ? n_values : 1);
     if (rc) return rc;
-    const uint32_t G = (uint32_t)nd->shards.size();
     NodeReqArgs q{};
     q.n = n;
     q.cp = req;
@@ -5693,23 +5757,12 @@ int sg_node_cparam_decide_batch(sg_node* nd, const sg_cparam_req* req, uint64_t 
     rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
     if (rc) return rc;
     sg_result* sub_out = static_cast<sg_result*>(nd->d_sub_nout);
-    for (uint32_t g = 0; g < G; ++g) {
-        if (!cnt[g]) continue;
-        const void* sr = nullptr;
-        const uint64_t* sv = nullptr;
-        void* so = nullptr;
-        rc = node_slice_to(nd, g, cnt[g], sizeof(sg_cparam_req), sizeof(sg_result), q.sub_cp + base[g],
-                           nd->d_sub_vals + vbase[g], vcnt[g], &sr, &sv, &so);
-        if (rc) return rc;
-        sg_handle* h = nd->shards[g];
-        NHIP(nd, hipSetDevice(h->device));
-        sg_result* o = so ? static_cast<sg_result*>(so) : sub_out + base[g];
-        rc = sg_cparam_decide_batch(h, static_cast<const sg_cparam_req*>(sr), cnt[g], vcnt[g] ? sv : nullptr, vcnt[g], o,
-                                    nd->streams[g]);
-        if (rc) return node_child(nd, h, rc);
-        NHIP(nd, hipStreamSynchronize(nd->streams[g]));
-        if (so) NHIP(nd, hipMemcpyPeer(sub_out + base[g], nd->devices[0], so, h->device, sizeof(sg_result) * cnt[g]));
-    }
+    rc = node_run_shards(nd, base, cnt, vbase, vcnt, sizeof(sg_cparam_req), sizeof(sg_result), q.sub_cp, sub_out,
+                         [](sg_handle* h, const void* r, const uint64_t* v, uint64_t nv, uint64_t c, void* o, hipStream_t st) {
+                             return sg_cparam_decide_batch(h, static_cast<const sg_cparam_req*>(r), c, v, nv,
+                                                           static_cast<sg_result*>(o), st);
+                         });
+    if (rc) return rc;
     NHIP(nd, hipSetDevice(nd->devices[0]));
     NHIP(nd, launch_route_gather(sub_out, nd->d_sub_pos, n, out, nd->s0));
     int64_t last = 0;
@@ -5804,22 +5857,12 @@ int sg_node_conc_decide_batch(sg_node* nd, const sg_conc_req* req, uint64_t n, s
     rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
     if (rc) return rc;
     sg_conc_result* sub_out = static_cast<sg_conc_result*>(nd->d_sub_nout);
-    for (uint32_t g = 0; g < G; ++g) {
-        if (!cnt[g]) continue;
-        const void* sr = nullptr;
-        const uint64_t* sv = nullptr;
-        void* so = nullptr;
-        rc = node_slice_to(nd, g, cnt[g], sizeof(sg_conc_req), sizeof(sg_conc_result), q.sub_cc + base[g], nullptr, 0,
-                           &sr, &sv, &so);
-        if (rc) return rc;
-        sg_handle* h = nd->shards[g];
-        NHIP(nd, hipSetDevice(h->device));
-        sg_conc_result* o = so ? static_cast<sg_conc_result*>(so) : sub_out + base[g];
-        rc = sg_conc_decide_batch(h, static_cast<const sg_conc_req*>(sr), cnt[g], o, nd->streams[g]);
-        if (rc) return node_child(nd, h, rc);
-        NHIP(nd, hipStreamSynchronize(nd->streams[g]));
-        if (so) NHIP(nd, hipMemcpyPeer(sub_out + base[g], nd->devices[0], so, h->device, sizeof(sg_conc_result) * cnt[g]));
-    }
+    rc = node_run_shards(nd, base, cnt, vbase, vcnt, sizeof(sg_conc_req), sizeof(sg_conc_result), q.sub_cc, sub_out,
+                         [](sg_handle* h, const void* r, const uint64_t*, uint64_t, uint64_t c, void* o, hipStream_t st) {
+                             return sg_conc_decide_batch(h, static_cast<const sg_conc_req*>(r), c,
+                                                         static_cast<sg_conc_result*>(o), st);
+                         });
+    if (rc) return rc;
     NHIP(nd, hipSetDevice(nd->devices[0]));
     for (uint32_t g = 0; g < G; ++g)
         NHIP(nd, launch_nconc_scatter(sub_out, nd->d_sub_pos, q.sub_cc, base[g], cnt[g], g, G, out, nd->s0));

@@ -2352,19 +2352,22 @@ __global__ void __launch_bounds__(256) k_lds_poison() {
 }
 
 void lds_poison(hipStream_t stream) {
-    static int mode = -1;
-    static unsigned blocks = 0;
-    if (mode < 0) {
+    struct Cfg {
+        int mode;
+        unsigned blocks;
+    };
+    static const Cfg cfg = [] {  // once, thread-safe (node shards decide from several host threads)
         const char* e = std::getenv("SG_LDS_POISON");
-        mode = e ? std::atoi(e) : 0;
+        Cfg c{e ? std::atoi(e) : 0, 0u};
         int dev = 0, cus = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        blocks = 2u * (unsigned)(cus > 0 ? cus : 256);  // two 64 KB blocks per CU: 128 of its 160 KB
-        if (mode) (void)hipFuncSetAttribute((const void*)k_lds_poison, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)kPoisonBytes);
-    }
-    if (mode) hipLaunchKernelGGL(k_lds_poison, dim3(blocks), dim3(256), kPoisonBytes, stream);
+        c.blocks = 2u * (unsigned)(cus > 0 ? cus : 256);  // two 64 KB blocks per CU: 128 of its 160 KB
+        if (c.mode) (void)hipFuncSetAttribute((const void*)k_lds_poison, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)kPoisonBytes);
+        return c;
+    }();
+    if (cfg.mode) hipLaunchKernelGGL(k_lds_poison, dim3(cfg.blocks), dim3(256), kPoisonBytes, stream);
 }
 
 hipError_t launch_bin_front(const BatchArgs& a, uint32_t* hist_ws, bool hist_ready, bool csum_ready, hipStream_t stream) {

@@ -2725,50 +2725,81 @@ __device__ __forceinline__ bool metric_row_valid(const LBucket& b) {  // MetricN
 
 __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_metric_node* out,
                                                        unsigned long long* count, int emit, int raw) {
+    // the ENTRY_NODE sums of this block's inbound resources, per minute slot, in LDS (one global atomic per slot and
+    // event per block instead of one per resource); rows placed with one counter atomic per wave
+    __shared__ unsigned long long eacc[kMinuteS][kLEv];
+    __shared__ int64_t estart[kMinuteS];
+    for (int i = threadIdx.x; i < kMinuteS * kLEv; i += blockDim.x) (&eacc[0][0])[i] = 0ull;
+    for (int i = threadIdx.x; i < kMinuteS; i += blockDim.x) estart[i] = INT64_MIN;
+    __syncthreads();
     const int64_t cur = now - now % 1000;
     const int I = (int)((now / kMinuteWl) % kMinuteS);
     const int64_t efetch = a.entry_fetch ? *a.entry_fetch : INT64_MAX;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.K; k += (uint64_t)gridDim.x * blockDim.x) {
-        LBucket* m = a.minute + k * kMinuteS;
-        // data.currentWindow(now): an absent or stale bucket in now's slot becomes an empty one (emit: for real;
-        // counting: as if, so that both passes list the same buckets)
-        const bool reset_I = m[I].start == INT64_MIN || m[I].start < cur;
-        if (emit && reset_I) {
-            LBucket b;
-            b.start = cur;
-            for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
-            b.min_rt = kStatMaxRt;
-            m[I] = b;
-        }
-        const bool inb = a.inbound && a.inbound[k];
-        const int64_t last = a.last_fetch[k];
-        int64_t newest = last;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x; k0 < a.K; k0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = k0 + threadIdx.x;
+        const bool act = k < a.K;
+        LBucket* m = a.minute + (act ? k : 0) * kMinuteS;
+        bool reset_I = false;
+        int64_t last = 0, s_lo = 0, newest = 0;
         uint32_t rows = 0;
-        // Only buckets that start after the earlier of the two fetch times (the resource's, and the ENTRY_NODE's for
-        // an inbound resource), before cur and inside the minute can yield a row or an ENTRY_NODE sum: their seconds
-        // s in [cur - 59 s, cur) past that fetch time, slot (s / 1000) mod 60 — one bucket per resource when the
-        // listener fetches every second, instead of all 60 (a bucket whose start is some other second fails the
-        // checks below, as in the full scan).
-        const int64_t lo_f = (inb && efetch < last) ? efetch : last;
-        int64_t s_lo = cur - (int64_t)(kMinuteS - 1) * kMinuteWl;
-        if (lo_f >= s_lo) s_lo = (lo_f >= 0 ? lo_f / kMinuteWl : -((-lo_f + kMinuteWl - 1) / kMinuteWl)) * kMinuteWl + kMinuteWl;
-        if (s_lo < 0) s_lo = 0;
-        for (int64_t s = s_lo; s < cur; s += kMinuteWl) {  // data.list(now): present and not deprecated
+        if (act) {
+            // data.currentWindow(now): an absent or stale bucket in now's slot becomes an empty one (emit: for real;
+            // counting: as if, so that both passes list the same buckets)
+            reset_I = m[I].start == INT64_MIN || m[I].start < cur;
+            if (emit && reset_I) {
+                LBucket b;
+                b.start = cur;
+                for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+                b.min_rt = kStatMaxRt;
+                m[I] = b;
+            }
+            const bool inb = a.inbound && a.inbound[k];
+            last = a.last_fetch[k];
+            newest = last;
+            // Only buckets that start after the earlier of the two fetch times (the resource's, and the ENTRY_NODE's
+            // for an inbound resource), before cur and inside the minute can yield a row or an ENTRY_NODE sum: their
+            // seconds s in [cur - 59 s, cur) past that fetch time, slot (s / 1000) mod 60 — one bucket per resource
+            // when the listener fetches every second, instead of all 60 (a bucket whose start is some other second
+            // fails the checks below, as in the full scan).
+            const int64_t lo_f = (inb && efetch < last) ? efetch : last;
+            s_lo = cur - (int64_t)(kMinuteS - 1) * kMinuteWl;
+            if (lo_f >= s_lo) s_lo = (lo_f >= 0 ? lo_f / kMinuteWl : -((-lo_f + kMinuteWl - 1) / kMinuteWl)) * kMinuteWl + kMinuteWl;
+            if (s_lo < 0) s_lo = 0;
+            for (int64_t s = s_lo; s < cur; s += kMinuteWl) {  // data.list(now): present and not deprecated
+                const int j = (int)((s / kMinuteWl) % kMinuteS);
+                if (j == I && reset_I) continue;  // the fresh bucket at cur is never in time
+                const LBucket b = m[j];
+                if (b.start == INT64_MIN || now - b.start > (int64_t)kMinuteS * kMinuteWl) continue;
+                if (inb && b.start > efetch && b.start < cur) {  // the ENTRY_NODE's bucket of that second
+                    estart[j] = b.start;  // every inbound bucket of slot j in the window has this start
+                    for (int e = 0; e < kLEv; ++e)
+                        if (b.c[e]) atomicAdd(&eacc[j][e], (unsigned long long)b.c[e]);
+                }
+                if (!(b.start > last && b.start < cur)) continue;  // isNodeInTime
+                if (!metric_row_valid(b)) continue;
+                newest = b.start > newest ? b.start : newest;
+                ++rows;
+            }
+        }
+        // the wave's rows: one counter atomic, each lane's rows after its lower lanes'
+        uint32_t incl = rows;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, (unsigned)o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t wtot = (uint32_t)__shfl((int)incl, 63, 64);
+        unsigned long long base = 0;
+        if (lane == 0 && wtot) base = atomicAdd(count, (unsigned long long)wtot);
+        base = (unsigned long long)__shfl((long long)base, 0, 64);
+        if (!emit || !act) continue;
+        unsigned long long pos = base + incl - rows;
+        for (int64_t s = s_lo; rows && s < cur; s += kMinuteWl) {  // the same buckets again, now written out
             const int j = (int)((s / kMinuteWl) % kMinuteS);
-            if (j == I && reset_I) continue;  // the fresh bucket at cur is never in time
+            if (j == I && reset_I) continue;
             const LBucket b = m[j];
             if (b.start == INT64_MIN || now - b.start > (int64_t)kMinuteS * kMinuteWl) continue;
-            if (inb && b.start > efetch && b.start < cur) {  // the ENTRY_NODE's bucket of that second
-                LBucket& acc = a.entry_acc[j];
-                acc.start = b.start;  // every inbound bucket of slot j in the window has this start
-                for (int e = 0; e < kLEv; ++e)
-                    if (b.c[e]) atomicAdd((unsigned long long*)&acc.c[e], (unsigned long long)b.c[e]);
-            }
-            if (!(b.start > last && b.start < cur)) continue;  // isNodeInTime
-            if (!metric_row_valid(b)) continue;
-            newest = b.start > newest ? b.start : newest;
-            ++rows;
-            if (!emit) continue;
+            if (!(b.start > last && b.start < cur) || !metric_row_valid(b)) continue;
             const int64_t pass = b.c[kLPass], block = b.c[kLBlock], succ = b.c[kLSucc], exc = b.c[kLExc];
             sg_metric_node r;
             r.timestamp = b.start;
@@ -2780,11 +2811,17 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
             r.occupied_pass_qps = b.c[kLOccPass];
             r.resource = (uint32_t)k;
             r.concurrency = 0;
-            out[atomicAdd(count, 1ull)] = r;
+            out[pos++] = r;
         }
-        if (!emit && rows) atomicAdd(count, (unsigned long long)rows);
-        if (emit) a.last_fetch[k] = newest;
+        a.last_fetch[k] = newest;
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kMinuteS * kLEv; i += blockDim.x) {
+        const unsigned long long v = (&eacc[0][0])[i];
+        if (v) atomicAdd((unsigned long long*)&a.entry_acc[i / kLEv].c[i % kLEv], v);
+    }
+    for (int i = threadIdx.x; i < kMinuteS; i += blockDim.x)
+        if (estart[i] != INT64_MIN) a.entry_acc[i].start = estart[i];
 }
 
 // Constants.ENTRY_NODE.metrics() rows from the summed buckets (one thread per minute slot; resource id
