@@ -10,3 +10,8 @@ timeout -k 10 400 python -u bench.py --workload c5 --steps 5 --warmup 2 > gpurun
 for G in 0 1 2 3; do
   timeout -k 10 240 python -u bench_configs.py --workload cparam --shards $G --no-cpu-baseline --steps 5 --warmup 2 >> gpurun_out/r6/cparam_node.jsonl 2>> gpurun_out/r6/cparam_node.err || exit 1
 done
+rm -f gpurun_out/r6/node_hwq.jsonl
+for G in 2 4; do
+  timeout -k 10 240 python -u bench_configs.py --workload node --shards $G --no-cpu-baseline --steps 10 --warmup 3 >> gpurun_out/r6/node_hwq.jsonl 2>> gpurun_out/r6/node_hwq.err || exit 1
+  GPU_MAX_HW_QUEUES=16 timeout -k 10 240 python -u bench_configs.py --workload node --shards $G --no-cpu-baseline --steps 10 --warmup 3 >> gpurun_out/r6/node_hwq.jsonl 2>> gpurun_out/r6/node_hwq.err || exit 1
+done
