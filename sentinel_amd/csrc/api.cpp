@@ -217,6 +217,7 @@ struct sg_handle {
     sg_slot_ext* d_lext_h = nullptr;  // host-path buffers of sg_slot_decide_batch_host
     uint8_t* d_linbound = nullptr;    // [K] EntryType.IN resources (sg_local_set_entry_types), null = none
     LBucket* d_lentry_acc = nullptr;  // [60] the ENTRY_NODE's buckets, summed per metric call
+    unsigned long long* d_lm_cnt = nullptr;  // the metric passes' row counter
     int64_t* d_lentry_fetch = nullptr;// the ENTRY_NODE's lastFetchTime
 
     int kbits = 0, ibits = 0, abits = 0;
@@ -746,6 +747,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_lgkey);
     dfree(h->d_linbound);
     dfree(h->d_lentry_acc);
+    dfree(h->d_lm_cnt);
     dfree(h->d_lentry_fetch);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
@@ -3092,47 +3094,32 @@ int local_metrics(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint64_t ca
     // MetricTimerListener.run: the resources' rows, then the ENTRY_NODE's (counted first, then emitted: the emit
     // pass has the side effects)
     auto pass = [&](sg_metric_node* dst, unsigned long long* d_cnt, int emit) -> hipError_t {
-        std::vector<LBucket> acc0(kMinuteS);
-        for (auto& b : acc0) {
-            b.start = INT64_MIN;
-            for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
-            b.min_rt = kStatMaxRt;
-        }
-        hipError_t e = hipMemcpy(h->d_lentry_acc, acc0.data(), sizeof(LBucket) * kMinuteS, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(unsigned long long));
+        hipError_t e = launch_entry_acc_reset(h->d_lentry_acc, 0);
+        if (e == hipSuccess) e = hipMemsetAsync(d_cnt, 0, sizeof(unsigned long long), 0);
         if (e == hipSuccess) e = launch_local_metrics(L, now_ms, dst, d_cnt, emit, raw, 0);
         if (e == hipSuccess && h->d_linbound) e = launch_local_entry_rows(L, now_ms, dst, d_cnt, emit, raw, 0);
         return e;
     };
-    unsigned long long* d_cnt = nullptr;
-    HIP_TRY(h, hipMalloc(&d_cnt, sizeof(unsigned long long)));
+    if (!h->d_lm_cnt && hipMalloc(&h->d_lm_cnt, sizeof(unsigned long long)) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "metric row counter");
+    unsigned long long* d_cnt = h->d_lm_cnt;
     unsigned long long cnt = 0;
     hipError_t e = pass(nullptr, d_cnt, 0);
     if (e == hipSuccess) e = hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) {
-        (void)hipFree(d_cnt);
-        return fail(h, SG_E_DEVICE, hipGetErrorString(e));
-    }
+    if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
     *n_rows = cnt;
-    if (cnt > cap) {
-        (void)hipFree(d_cnt);
-        return fail(h, SG_E_CAPACITY, "metric row buffer too small (*n_rows rows)");
-    }
+    if (cnt > cap) return fail(h, SG_E_CAPACITY, "metric row buffer too small (*n_rows rows)");
     if (device_out) {  // the rows straight into the caller's device buffer, unsorted (the node rollup sorts)
         e = pass(out, d_cnt, 1);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        (void)hipFree(d_cnt);
+        if (e == hipSuccess) e = hipStreamSynchronize(0);
         if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
         return SG_OK;
     }
     sg_metric_node* d_out = nullptr;
-    if (cnt && hipMalloc(&d_out, sizeof(sg_metric_node) * cnt) != hipSuccess) {
-        (void)hipFree(d_cnt);
-        return fail(h, SG_E_NOMEM, "metric rows");
-    }
+    if (cnt && hipMalloc(&d_out, sizeof(sg_metric_node) * cnt) != hipSuccess) return fail(h, SG_E_NOMEM, "metric rows");
     e = pass(d_out, d_cnt, 1);
     if (e == hipSuccess && cnt) e = hipMemcpy(out, d_out, sizeof(sg_metric_node) * cnt, hipMemcpyDeviceToHost);
-    (void)hipFree(d_cnt);
+    if (e == hipSuccess) e = hipStreamSynchronize(0);
     if (d_out) (void)hipFree(d_out);
     if (e != hipSuccess) return fail(h, SG_E_DEVICE, hipGetErrorString(e));
     std::sort(out, out + cnt, [](const sg_metric_node& a, const sg_metric_node& b) {  // the listener's TreeMap by time

@@ -2895,6 +2895,21 @@ hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out
     return hipGetLastError();
 }
 
+__global__ void k_entry_acc_reset(LBucket* acc) {  // the ENTRY_NODE's summed buckets, empty before a metric pass
+    const int j = threadIdx.x;
+    if (j >= kMinuteS) return;
+    LBucket b;
+    b.start = INT64_MIN;
+    for (int e = 0; e < kLEv; ++e) b.c[e] = 0;
+    b.min_rt = kStatMaxRt;
+    acc[j] = b;
+}
+
+hipError_t launch_entry_acc_reset(LBucket* acc, hipStream_t stream) {
+    hipLaunchKernelGGL(k_entry_acc_reset, dim3(1), dim3(64), 0, stream, acc);
+    return hipGetLastError();
+}
+
 hipError_t launch_local_entry_rows(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
                                    int raw, hipStream_t stream) {
     hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit, raw);
