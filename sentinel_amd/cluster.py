@@ -280,33 +280,62 @@ class DeviceLocalMetricRollup:
         return torch.cat([p[:k] for p, k in zip(parts, sizes)])
 
     @staticmethod
+    def _entry_rows(er: torch.Tensor) -> torch.Tensor:
+        """Constants.ENTRY_NODE rows of every GPU, one per second: sums, rt = Σrt / Σsuccess, isValidMetricNode."""
+        ts, inv = torch.unique(er[:, 0], return_inverse=True)
+        sums = torch.zeros((ts.shape[0], 8), dtype=torch.int64, device=er.device)
+        sums.index_add_(0, inv, er)
+        m = torch.zeros_like(sums)
+        m[:, 0] = ts
+        m[:, 1:6] = sums[:, 1:6]
+        s = m[:, 3]
+        m[:, 5] = torch.where(s != 0, torch.div(m[:, 5], torch.where(s != 0, s, 1), rounding_mode="floor"), m[:, 5])
+        m[:, 7] = ENTRY_NODE_RESOURCE
+        keep = (m[:, 1] > 0) | (m[:, 2] > 0) | (s > 0) | (m[:, 4] > 0) | (m[:, 5] > 0)
+        return m[keep]
+
+    @staticmethod
     def merge(rows: torch.Tensor) -> torch.Tensor:
         """merge_metric_rows on an int64 [n, 8] tensor (words: timestamp, pass, block, success, exception, rt,
-        occupied pass, resource | concurrency << 32)."""
+        occupied pass, resource | concurrency << 32). The resource rows are ordered by one sort of the key
+        (timestamp - the earliest) << 32 | resource and one gather of the rows; the few ENTRY_NODE rows (one per
+        second after the merge, the largest resource id) are spliced in after their second's resource rows."""
+        n = rows.shape[0]
+        if n == 0:
+            return rows.clone()
         res = rows[:, 7] & 0xFFFFFFFF
         ent = res == ENTRY_NODE_RESOURCE
-        rr = rows[~ent].clone()
-        succ = rr[:, 3]
-        rr[:, 5] = torch.where(succ != 0, torch.div(rr[:, 5], torch.where(succ != 0, succ, 1), rounding_mode="floor"),
-                               rr[:, 5])
-        er = rows[ent]
-        if er.shape[0]:
-            ts, inv = torch.unique(er[:, 0], return_inverse=True)
-            sums = torch.zeros((ts.shape[0], 8), dtype=torch.int64, device=rows.device)
-            sums.index_add_(0, inv, er)
-            m = torch.zeros_like(sums)
-            m[:, 0] = ts
-            m[:, 1:6] = sums[:, 1:6]
-            s = m[:, 3]
-            m[:, 5] = torch.where(s != 0, torch.div(m[:, 5], torch.where(s != 0, s, 1), rounding_mode="floor"), m[:, 5])
-            m[:, 7] = ENTRY_NODE_RESOURCE
-            keep = (m[:, 1] > 0) | (m[:, 2] > 0) | (s > 0) | (m[:, 4] > 0) | (m[:, 5] > 0)
-            rr = torch.cat([rr, m[keep]])
-        # (timestamp, resource) order: stable sort by resource, then stable by timestamp
-        o = torch.sort(rr[:, 7] & 0xFFFFFFFF, stable=True).indices
-        rr = rr[o]
-        o = torch.sort(rr[:, 0], stable=True).indices
-        return rr[o]
+        ts = rows[:, 0]
+        t_lo, t_hi = int(ts.min().item()), int(ts.max().item())
+        if t_hi - t_lo >= (1 << 31):  # rows spanning ~24 days: two stable sorts instead of the packed key
+            rr = torch.cat([rows[~ent], DeviceLocalMetricRollup._entry_rows(rows[ent])]) if bool(ent.any()) else rows[~ent]
+            succ = rr[:, 3]
+            is_res = (rr[:, 7] & 0xFFFFFFFF) != ENTRY_NODE_RESOURCE
+            rr[:, 5] = torch.where(is_res & (succ != 0),
+                                   torch.div(rr[:, 5], torch.where(succ != 0, succ, 1), rounding_mode="floor"), rr[:, 5])
+            rr = rr[torch.sort(rr[:, 7] & 0xFFFFFFFF, stable=True).indices]
+            return rr[torch.sort(rr[:, 0], stable=True).indices]
+        key = torch.where(ent, torch.full_like(ts, (1 << 63) - 1), ((ts - t_lo) << 32) | res)
+        skey, order = torch.sort(key)
+        n_e = int(ent.sum().item())
+        n_r = n - n_e
+        out = rows.index_select(0, order[:n_r])
+        succ = out[:, 3]
+        out[:, 5] = torch.where(succ != 0, torch.div(out[:, 5], torch.where(succ != 0, succ, 1), rounding_mode="floor"),
+                                out[:, 5])
+        if n_e == 0:
+            return out
+        m = DeviceLocalMetricRollup._entry_rows(rows[ent])
+        if m.shape[0] == 0:
+            return out
+        mkey = ((m[:, 0] - t_lo) << 32) | ENTRY_NODE_RESOURCE
+        pos = torch.searchsorted(skey[:n_r], mkey).tolist()  # m is sorted by second (torch.unique)
+        parts, prev = [], 0
+        for i, p in enumerate(pos):
+            parts += [out[prev:p], m[i:i + 1]]
+            prev = p
+        parts.append(out[prev:])
+        return torch.cat(parts)
 
     def run(self, rows: torch.Tensor) -> torch.Tensor:
         return self.merge(self.gather(rows))

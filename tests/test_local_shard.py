@@ -134,6 +134,11 @@ def test_device_merge_equals_host_merge():
     t = torch.from_numpy(np.concatenate(parts).view(np.int64).reshape(-1, 8).copy())
     got = DeviceLocalMetricRollup.merge(t).numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
     assert np.array_equal(got, want)
+    parts[1]["timestamp"] += 1000 * (1 << 32)  # rows spanning more than 2^31 ms: the two-sort path
+    want = merge_metric_rows(parts)
+    t = torch.from_numpy(np.concatenate(parts).view(np.int64).reshape(-1, 8).copy())
+    got = DeviceLocalMetricRollup.merge(t).numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+    assert np.array_equal(got, want)
 
 
 def _worker(rank, world, port, q):
