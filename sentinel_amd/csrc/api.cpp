@@ -46,7 +46,6 @@ struct sg_handle {
     uint64_t* d_bin_buf = nullptr;
     int bin_mode = 1;                 // env SG_BIN: 0 off, 1 on for >= 2^14 flowIds, 2 on whenever the records allow
     int prep_tiles = 4;               // env SG_PREP_TILES: sort tiles per k_prep block on the binned path
-    int prep_outv = 1;                // env SG_PREP_OUTV: k_prep's default results as whole 16-B stores per tile
 
     // batch workspace (sized for cfg.max_batch)
     uint64_t* d_rec = nullptr;
@@ -564,7 +563,6 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (const char* d = std::getenv("SG_LIM_PIPE")) h->lim_pipe = std::atoi(d) != 0;
     if (const char* d = std::getenv("SG_BIN")) h->bin_mode = std::atoi(d);
     if (const char* d = std::getenv("SG_PREP_TILES")) h->prep_tiles = std::max(1, std::min(64, std::atoi(d)));
-    if (const char* d = std::getenv("SG_PREP_OUTV")) h->prep_outv = std::atoi(d);
     if (const char* d = std::getenv("SG_D2H_BLOCKS")) h->d2h_blocks = std::max(1, std::atoi(d));
     if (const char* sm = std::getenv("SG_SHORT_MAX")) {
         h->short_max = (uint32_t)std::strtoul(sm, nullptr, 10);
@@ -1318,7 +1316,6 @@ BatchArgs flow_args(sg_handle* h, const sg_handle::FlowWs& w, const sg_req* req,
     BatchArgs a{};
     a.req = req;
     a.out = out;
-    a.outv = h->prep_outv && ((uintptr_t)out & 15) == 0;
     a.n = n;
     a.rec = w.rec;
     a.rec_sorted = w.rec_sorted;

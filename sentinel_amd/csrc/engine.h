@@ -152,7 +152,6 @@ struct BatchArgs {
     int hist0_shift;       // k_prep's histogram digit: (rec >> hist0_shift) & mask (kshift, or bin_dshift)
     int bin_on;
     int prep_tiles;        // tiles (of the sort's 4096 records) per k_prep block on the binned path (env SG_PREP_TILES)
-    int outv;              // k_prep writes a tile's default results as 16-B stores (a.out 16-B aligned; env SG_PREP_OUTV)
     int bin_dshift;
     int bin_bsh;
     uint32_t bin_R;        // regular bins [0, R) (R = ((K - 1) >> bin_bsh) + 1 <= kBinRegular)

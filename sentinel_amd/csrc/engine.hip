@@ -111,7 +111,6 @@ template <bool BIN>
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
     __shared__ uint32_t dcnt[1024];
     __shared__ alignas(16) uint2 htab[BIN ? kHotTab : 1];  // the hot flowIds: two 16-B LDS reads per request
-    __shared__ int8_t sst[kPrepTile];  // a.outv: the tile's default statuses, written out as whole 16-B stores
     if constexpr (BIN)
         for (uint32_t x = threadIdx.x; x < kHotTab; x += 256) htab[x] = a.hot_tab[x];
     const uint64_t n = a.n;
@@ -193,9 +192,7 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             }
         }
         if constexpr (BIN) rec |= (uint64_t)d << a.bin_dshift;
-        if (a.outv) {
-            sst[it * 256 + threadIdx.x] = (int8_t)st;
-        } else if (!(a.dbg & 16384)) {
+        if (!(a.dbg & 16384)) {
             int32_t* o = &a.out[i].status;  // the default result {st, 0, 0}
             st_stream(o, st);
             st_stream(o + 1, 0);
@@ -203,24 +200,6 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
         }
         st_stream(a.rec + i, rec);
         if (a.hist0) atomicAdd(&dcnt[BIN ? d : (uint32_t)(rec >> a.hist0_shift) & dmask], 1u);
-    }
-    if (a.outv) {  // the tile's default results {st, 0, 0}: 12 B each, 16-B aligned as a whole (a.out is, base % 4 == 0)
-        __syncthreads();
-        const uint32_t nreq = (uint32_t)min((uint64_t)kPrepTile, n - base);
-        const uint32_t words = 3 * nreq;
-        int32_t* o = &a.out[base].status;
-        typedef int32_t v4i __attribute__((ext_vector_type(4)));
-        for (uint32_t v = threadIdx.x; v < words / 4; v += 256) {
-            v4i x;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t wd = 4 * v + j, r = wd / 3;
-                x[j] = wd - 3 * r == 0 ? (int32_t)sst[r] : 0;
-            }
-            st_stream(reinterpret_cast<v4i*>(o) + v, x);
-        }
-        for (uint32_t wd = (words & ~3u) + threadIdx.x; wd < words; wd += 256)
-            st_stream(o + wd, wd % 3 == 0 ? (int32_t)sst[wd / 3] : 0);
     }
     if (a.hist0) {
         __syncthreads();
