@@ -12,3 +12,5 @@ timeout -k 10 300 python -u bench_configs.py --workload pace --steps 5 --warmup 
 SG_LDS_POISON=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r6f/poison -o run --output-format csv -- \
   python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_flow_gpu.py tests/test_node_gpu.py > gpurun_out/r6f/poison.txt 2>&1 || exit 1
 python scripts/kstats.py $(ls gpurun_out/r6f/poison/*kernel_stats.csv | head -1) > gpurun_out/r6f/poison_kstats.txt
+grep -i "poison" $(ls gpurun_out/r6f/poison/*kernel_stats.csv | head -1) > gpurun_out/r6f/poison_stats_row.txt
+rm -f gpurun_out/r6f/poison/*kernel_trace.csv  # (hundreds of MB: gpurun copies back at most 64 MiB)
