@@ -309,8 +309,9 @@ def c5_main(args, rank, world, dev, coll, one_dev):
     over the node's GPUs, one rank per GPU. Every rank loads the node's rules (all resources EntryType.IN) and decides
     the entries and exits of the resources sg_local_owners gives it (weak scaling: --requests entries per rank per
     1000 ms step plus the exits of the passed ones); after each batch the node's MetricTimerListener rows of that
-    second are rolled up on the devices (sg_local_metrics_raw_device, then DeviceLocalMetricRollup: RCCL all_gather
-    of the rows, ENTRY_NODE sums and the (timestamp, resource) order on the GPU). The event stream depends on the
+    second are rolled up on the devices (sg_local_metrics_raw_enqueue behind the batch's walkers, then
+    DeviceLocalMetricRollup while the next batch runs: RCCL all_gather of the rows, ENTRY_NODE sums and the
+    (timestamp, resource) order on the GPU). The event stream depends on the
     decisions, so each rank's share is produced by the oracle's client model before the timed region. With --check
     (on by default in the SG_BENCH_ONE_DEVICE rehearsal) every decision and every merged row is compared with the
     oracle's node replay after the timed region."""
@@ -335,26 +336,43 @@ def c5_main(args, rank, world, dev, coll, one_dev):
     eng.local_set_entry_types(np.ones(K, np.uint8))
     batches = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e, _, _ in trace]
     outs = [torch.empty(sz * abi.LOCAL_RES_DTYPE.itemsize, dtype=torch.uint8, device=dev) for sz in sizes]
-    rows_buf = torch.empty((2 * len(own) + 256, 8), dtype=torch.int64, device=dev)
+    rows_buf = [torch.empty((2 * len(own) + 256, 8), dtype=torch.int64, device=dev) for _ in range(2)]
+    rows_cnt = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(2)]
     rollup = DeviceLocalMetricRollup(coll)
     merged = [None] * total_steps
     t0 = 1_700_000_000_000
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    tickets = []
     torch.cuda.synchronize()
 
+    def roll(b):  # second b's rows: on torch's stream, which waits for their metric pass only
+        merged[b] = rollup.run(rows_buf[b % 2][:int(rows_cnt[b % 2].item())])
+
     def step(b):
-        tk = eng.local_enqueue(batches[b].data_ptr(), sizes[b], outs[b].data_ptr())
-        k = eng.local_metrics_raw_device(t0 + 1000 * (b + 1), rows_buf)   # completes batch b first
-        merged[b] = rollup.run(rows_buf[:k])
-        eng.local_wait(tk)
+        """Batch b on the local pipeline; the rollup of second b - 1 while it runs; then second b's metric pass,
+        enqueued behind batch b's walkers (sg_local_metrics_raw_enqueue: no pipeline drain)."""
+        if len(tickets) >= 2:
+            eng.local_wait(tickets.pop(0))
+        tickets.append(eng.local_enqueue(batches[b].data_ptr(), sizes[b], outs[b].data_ptr()))
+        if b > 0:
+            roll(b - 1)
+        eng.local_metrics_raw_enqueue(t0 + 1000 * (b + 1), rows_buf[b % 2], rows_cnt[b % 2], stream)
+
+    def drain(b_last):
+        roll(b_last)
+        while tickets:
+            eng.local_wait(tickets.pop(0))
 
     for b in range(args.warmup):
         step(b)
+    drain(args.warmup - 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for b in range(args.warmup, total_steps):
         step(b)
+    drain(total_steps - 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -734,6 +734,12 @@ int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint
  * node's device rollup (cluster.DeviceLocalMetricRollup: RCCL all_gather of the rows, ENTRY_NODE sums and the
  * (timestamp, resource) order on the GPU). Same side effects, same SG_E_CAPACITY contract. */
 int sg_local_metrics_raw_device(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* n_rows);
+/* sg_local_metrics_raw_device enqueued, no host wait: the rows of now_ms after every local batch enqueued so far
+ * (sg_local_enqueue) and after the caller's earlier work on `stream`, before every batch enqueued later; `stream` is
+ * made to wait for them. *d_count (DEVICE memory) receives the row count; when it exceeds cap, no row is written and
+ * nothing changes (the listener's state included). Rows unsorted, as sg_local_metrics_raw_device. */
+int sg_local_metrics_raw_enqueue(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* d_count,
+                                 void* stream);
 /* The local chain sharded over a node's GPUs (one process per GPU): every GPU loads the same rules and
  * decides the entries and exits of the resources it owns — owner[r] = splitmix64(g(r)) mod world, g(r) the smallest
  * resource of r's key group (RELATE references; on an embedded token server also the resources sharing a flowId or

@@ -323,6 +323,8 @@ struct sg_handle {
     hipStream_t s_xcopy = nullptr;    // the sharded limiter exchange's copy into a pipeline workspace
     hipEvent_t xcopy_done = nullptr;
     hipEvent_t front_done[2]{}, back_done[2]{}, pfork = nullptr, pjoin = nullptr;
+    hipEvent_t lm_in = nullptr, lm_done = nullptr;  // sg_local_metrics_raw_enqueue: the caller's stream <-> s_back
+    int* d_lm_gate = nullptr;                        // its capacity gate (count <= cap)
     uint64_t pipe_seq = 0;            // batches put on the pipeline so far (workspace = seq % 2)
     bool d2h_kernel = false;          // sg_flow_submit: results to pinned host buffers by k_copy_out (env SG_D2H=1; the
                                       // copy engine measured faster: 2.64 vs 2.45 G decisions/s end to end)
@@ -609,6 +611,8 @@ void sg_destroy(sg_handle* h) {
             if (h->back_done[x]) (void)hipEventDestroy(h->back_done[x]);
         }
         if (h->tjoin) (void)hipEventDestroy(h->tjoin);
+        if (h->lm_in) (void)hipEventDestroy(h->lm_in);
+        if (h->lm_done) (void)hipEventDestroy(h->lm_done);
         if (h->pfork) (void)hipEventDestroy(h->pfork);
         if (h->pjoin) (void)hipEventDestroy(h->pjoin);
         for (auto& d : h->dev) {
@@ -748,6 +752,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_linbound);
     dfree(h->d_lentry_acc);
     dfree(h->d_lm_cnt);
+    dfree(h->d_lm_gate);
     dfree(h->d_lentry_fetch);
     dfree(h->d_req_h);
     dfree(h->d_out_h);
@@ -3054,6 +3059,52 @@ int sg_local_metrics_raw(sg_handle* h, int64_t now_ms, sg_metric_node* out, uint
 
 int sg_local_metrics_raw_device(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* n_rows) {
     return local_metrics(h, now_ms, d_out, cap, n_rows, 1, true);
+}
+
+int sg_local_metrics_raw_enqueue(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* d_count,
+                                 void* stream_) {
+    if (!h || !d_count || (!d_out && cap)) return SG_E_INVAL;
+    if (!h->d_llast_ts) return fail(h, SG_E_INVAL, "sg_local_load_rules first");
+    HIP_TRY(h, hipSetDevice(h->device));
+    hipStream_t stream = (hipStream_t)stream_;
+    if (h->ltab.empty()) {
+        HIP_TRY(h, hipMemsetAsync(d_count, 0, sizeof(uint64_t), stream));
+        return SG_OK;
+    }
+    int rc = pipe_setup(h);
+    if (rc) return rc;
+    if (!h->lm_done) {
+        HIP_TRY(h, hipEventCreateWithFlags(&h->lm_in, hipEventDisableTiming));
+        HIP_TRY(h, hipEventCreateWithFlags(&h->lm_done, hipEventDisableTiming));
+    }
+    if ((!h->d_lm_cnt && hipMalloc(&h->d_lm_cnt, sizeof(unsigned long long)) != hipSuccess) ||
+        (!h->d_lm_gate && hipMalloc(&h->d_lm_gate, sizeof(int)) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "metric row counter");
+    LArgs L{};
+    L.K = (uint32_t)h->ltab.size();
+    L.minute = h->d_lmin;
+    L.last_fetch = h->d_llast_fetch;
+    L.inbound = h->d_linbound;
+    L.entry_acc = h->d_lentry_acc;
+    L.entry_fetch = h->d_lentry_fetch;
+    // after the batches already enqueued (their back halves on s_back) and the caller's earlier work on `stream`
+    // (e.g. the rollup still reading a previous call's rows); before every batch enqueued later
+    hipStream_t s = h->s_back;
+    HIP_TRY(h, hipEventRecord(h->lm_in, stream));
+    HIP_TRY(h, hipStreamWaitEvent(s, h->lm_in, 0));
+    for (int emit = 0; emit < 2; ++emit) {
+        HIP_TRY(h, launch_entry_acc_reset(h->d_lentry_acc, s));
+        HIP_TRY(h, hipMemsetAsync(h->d_lm_cnt, 0, sizeof(unsigned long long), s));
+        HIP_TRY(h, launch_local_metrics(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s,
+                                        emit ? h->d_lm_gate : nullptr));
+        if (h->d_linbound)
+            HIP_TRY(h, launch_local_entry_rows(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s,
+                                               emit ? h->d_lm_gate : nullptr));
+        if (!emit) HIP_TRY(h, launch_metrics_gate(h->d_lm_cnt, cap, (unsigned long long*)d_count, h->d_lm_gate, s));
+    }
+    HIP_TRY(h, hipEventRecord(h->lm_done, s));
+    HIP_TRY(h, hipStreamWaitEvent(stream, h->lm_done, 0));
+    return SG_OK;
 }
 
 int sg_local_owners(sg_handle* h, uint32_t world, uint32_t* owner, uint32_t n) {

@@ -770,10 +770,12 @@ hipError_t launch_lnode_find(const uint64_t* keys, const uint32_t* vals, uint64_
 // Constants.ENTRY_NODE's metric rows from the summed buckets (k_local_metrics accumulated them into a.entry_acc).
 // raw: rt is the bucket's raw sum in every row (sg_local_metrics_raw, for a node rollup) instead of rt / success.
 hipError_t launch_entry_acc_reset(LBucket* acc, hipStream_t stream);
+hipError_t launch_metrics_gate(const unsigned long long* cnt, uint64_t cap, unsigned long long* count_out, int* gate,
+                               hipStream_t stream);
 hipError_t launch_local_entry_rows(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                   int raw, hipStream_t stream);
+                                   int raw, hipStream_t stream, const int* gate = nullptr);
 hipError_t launch_local_metrics(const LArgs& L, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                int raw, hipStream_t stream);
+                                int raw, hipStream_t stream, const int* gate = nullptr);
 
 // Test aid (env SG_LDS_POISON=1): before every kernel that keeps counters or tables in LDS, a kernel fills the LDS of
 // every CU with 0xA5 bytes on the same stream, so a counter a kernel forgets to initialise reads garbage at once.

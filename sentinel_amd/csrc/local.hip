@@ -2724,7 +2724,8 @@ __device__ __forceinline__ bool metric_row_valid(const LBucket& b) {  // MetricN
 }
 
 __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_metric_node* out,
-                                                       unsigned long long* count, int emit, int raw) {
+                                                       unsigned long long* count, int emit, int raw, const int* gate) {
+    if (gate && !*gate) return;  // sg_local_metrics_raw_enqueue: more rows than the caller's capacity, no side effect
     // the ENTRY_NODE sums of this block's inbound resources, per minute slot, in LDS (one global atomic per slot and
     // event per block instead of one per resource); rows placed with one counter atomic per wave
     __shared__ unsigned long long eacc[kMinuteS][kLEv];
@@ -2827,7 +2828,8 @@ __global__ void __launch_bounds__(256) k_local_metrics(LArgs a, int64_t now, sg_
 // Constants.ENTRY_NODE.metrics() rows from the summed buckets (one thread per minute slot; resource id
 // SG_ENTRY_NODE_RESOURCE); emit advances the ENTRY_NODE's lastFetchTime.
 __global__ void __launch_bounds__(64) k_local_entry_rows(LArgs a, int64_t now, sg_metric_node* out,
-                                                         unsigned long long* count, int emit, int raw) {
+                                                         unsigned long long* count, int emit, int raw, const int* gate) {
+    if (gate && !*gate) return;
     const int j = threadIdx.x;
     const int64_t cur = now - now % 1000;
     bool row = false;
@@ -2889,9 +2891,24 @@ hipError_t launch_local_prep(const LArgs& a, hipStream_t stream) {
 }
 
 hipError_t launch_local_metrics(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                int raw, hipStream_t stream) {
+                                int raw, hipStream_t stream, const int* gate) {
     if (a.K == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit, raw);
+    lds_poison(stream);
+    hipLaunchKernelGGL(k_local_metrics, dim3(lgrid(a.K, 256, 4096)), dim3(256), 0, stream, a, now, out, count, emit, raw,
+                       gate);
+    return hipGetLastError();
+}
+
+// The count pass's rows against the caller's capacity: the count for the caller, and whether the emit pass runs.
+__global__ void k_metrics_gate(const unsigned long long* cnt, uint64_t cap, unsigned long long* count_out, int* gate) {
+    const unsigned long long c = *cnt;
+    *count_out = c;
+    *gate = c <= cap ? 1 : 0;
+}
+
+hipError_t launch_metrics_gate(const unsigned long long* cnt, uint64_t cap, unsigned long long* count_out, int* gate,
+                               hipStream_t stream) {
+    hipLaunchKernelGGL(k_metrics_gate, dim3(1), dim3(1), 0, stream, cnt, cap, count_out, gate);
     return hipGetLastError();
 }
 
@@ -2911,8 +2928,8 @@ hipError_t launch_entry_acc_reset(LBucket* acc, hipStream_t stream) {
 }
 
 hipError_t launch_local_entry_rows(const LArgs& a, int64_t now, sg_metric_node* out, unsigned long long* count, int emit,
-                                   int raw, hipStream_t stream) {
-    hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit, raw);
+                                   int raw, hipStream_t stream, const int* gate) {
+    hipLaunchKernelGGL(k_local_entry_rows, dim3(1), dim3(64), 0, stream, a, now, out, count, emit, raw, gate);
     return hipGetLastError();
 }
 

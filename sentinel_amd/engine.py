@@ -36,7 +36,7 @@ EXPORTS = ["sg_create", "sg_destroy", "sg_last_error", "sg_set_namespaces", "sg_
            "sg_node_cparam_decide_batch", "sg_node_cparam_decide_batch_host", "sg_node_cparam_read_sum",
            "sg_node_cparam_top_values", "sg_node_conc_set_rule_timeouts", "sg_node_conc_decide_batch",
            "sg_node_conc_decide_batch_host", "sg_node_conc_expire", "sg_node_conc_read_state",
-           "sg_local_metrics_raw_device"]
+           "sg_local_metrics_raw_device", "sg_local_metrics_raw_enqueue"]
 
 _lib = None
 
@@ -144,6 +144,7 @@ def load_library():
         "sg_node_flow_wait": (C.c_int, [vp, u64]),
         "sg_local_metrics_raw": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
         "sg_local_metrics_raw_device": (C.c_int, [vp, i64, vp, u64, C.POINTER(C.c_uint64)]),
+        "sg_local_metrics_raw_enqueue": (C.c_int, [vp, i64, vp, u64, vp, vp]),
         "sg_local_owners": (C.c_int, [vp, u32, vp, u32]),
         "sg_node_cparam_load_rules": (C.c_int, [vp, vp, u32, vp, u32, C.c_int32]),
         "sg_node_cparam_decide_batch": (C.c_int, [vp, vp, u64, vp, u64, vp, vp]),
@@ -685,6 +686,13 @@ class FlowEngine:
         cap = out.numel() * out.element_size() // abi.METRIC_NODE_DTYPE.itemsize
         self._check(self._L.sg_local_metrics_raw_device(self.h, now_ms, C.c_void_p(out.data_ptr()), cap, C.byref(n)))
         return n.value
+
+    def local_metrics_raw_enqueue(self, now_ms, out, count, stream_ptr: int = 0):
+        """sg_local_metrics_raw_enqueue: the rows into `out` (device int64 [cap, 8]) and their number into `count`
+        (a device int64 tensor of one element), after the batches enqueued so far; `stream_ptr` waits for them."""
+        cap = out.numel() * out.element_size() // abi.METRIC_NODE_DTYPE.itemsize
+        self._check(self._L.sg_local_metrics_raw_enqueue(self.h, now_ms, C.c_void_p(out.data_ptr()), cap,
+                                                         C.c_void_p(count.data_ptr()), C.c_void_p(stream_ptr)))
 
     def local_owners(self, world) -> np.ndarray:
         """sg_local_owners: the GPU of `world` that owns each resource (key groups co-located)."""

@@ -13,10 +13,11 @@ from tests.test_local_shard import N_ORIGINS, N_RES, node_setup, node_trace
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("device_rows", [False, True])
+@pytest.mark.parametrize("device_rows", ["host", "device", "enqueue"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_local_chain_handles_equal_node_replay(world, device_rows):
-    """device_rows: sg_local_metrics_raw_device into HBM and the device rollup's merge (DeviceLocalMetricRollup)."""
+    """device_rows: sg_local_metrics_raw_device into HBM (or sg_local_metrics_raw_enqueue, ordered on a stream, first
+    with a buffer too small: no rows, no side effect) and the device rollup's merge (DeviceLocalMetricRollup)."""
     import torch
 
     from sentinel_amd.cluster import DeviceLocalMetricRollup
@@ -40,7 +41,21 @@ def test_sharded_local_chain_handles_equal_node_replay(world, device_rows):
         for r in range(world):
             got = engs[r].local_decide_host(ev[parts[r]])
             assert np.array_equal(got, want[parts[r]]), f"batch {b} shard {r}: {(got != want[parts[r]]).sum()} differ"
-        if device_rows:
+        if device_rows == "enqueue":
+            st = torch.cuda.current_stream().cuda_stream
+            bufs = [torch.empty((4 * N_RES + 64, 8), dtype=torch.int64, device="cuda") for _ in engs]
+            cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in engs]
+            tiny = torch.empty((1, 8), dtype=torch.int64, device="cuda")
+            for e, c in zip(engs, cnts):
+                e.local_metrics_raw_enqueue(now, tiny, c, st)   # too small: only the count
+            need = [int(c.item()) for c in cnts]
+            for e, buf, c in zip(engs, bufs, cnts):
+                e.local_metrics_raw_enqueue(now, buf, c, st)
+            assert [int(c.item()) for c in cnts] == need
+            got_rows = [buf[:int(c.item())] for buf, c in zip(bufs, cnts)]
+            m = DeviceLocalMetricRollup.merge(torch.cat(got_rows))
+            rows = m.cpu().numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+        elif device_rows == "device":
             bufs = [torch.empty((4 * N_RES + 64, 8), dtype=torch.int64, device="cuda") for _ in engs]
             got_rows = [buf[:e.local_metrics_raw_device(now, buf)] for e, buf in zip(engs, bufs)]
             m = DeviceLocalMetricRollup.merge(torch.cat(got_rows))
