@@ -336,17 +336,22 @@ def c5_main(args, rank, world, dev, coll, one_dev):
     eng.local_set_entry_types(np.ones(K, np.uint8))
     batches = [torch.from_numpy(e.view(np.uint8).copy()).to(dev) for e, _, _ in trace]
     outs = [torch.empty(sz * abi.LOCAL_RES_DTYPE.itemsize, dtype=torch.uint8, device=dev) for sz in sizes]
-    rows_buf = [torch.empty((2 * len(own) + 256, 8), dtype=torch.int64, device=dev) for _ in range(2)]
+    # room for every row the listener could return (59 per resource + 60): the metric pass skips its counting pass
+    rows_buf = [torch.empty((59 * K + 60, 8), dtype=torch.int64, device=dev) for _ in range(2)]
     rows_cnt = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(2)]
     rollup = DeviceLocalMetricRollup(coll)
     merged = [None] * total_steps
     t0 = 1_700_000_000_000
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # the rollup on a stream of its own: torch's default stream is the null stream, which would also wait for the
+    # pipeline's walkers (blocking streams)
+    side = torch.cuda.Stream(dev)
+    stream = side.cuda_stream
     tickets = []
     torch.cuda.synchronize()
 
-    def roll(b):  # second b's rows: on torch's stream, which waits for their metric pass only
-        merged[b] = rollup.run(rows_buf[b % 2][:int(rows_cnt[b % 2].item())])
+    def roll(b):  # second b's rows, on the side stream, which waits for their metric pass only
+        with torch.cuda.stream(side):
+            merged[b] = rollup.run(rows_buf[b % 2][:int(rows_cnt[b % 2].item())])
 
     def step(b):
         """Batch b on the local pipeline; the rollup of second b - 1 while it runs; then second b's metric pass,

@@ -737,7 +737,8 @@ int sg_local_metrics_raw_device(sg_handle* h, int64_t now_ms, sg_metric_node* d_
 /* sg_local_metrics_raw_device enqueued, no host wait: the rows of now_ms after every local batch enqueued so far
  * (sg_local_enqueue) and after the caller's earlier work on `stream`, before every batch enqueued later; `stream` is
  * made to wait for them. *d_count (DEVICE memory) receives the row count; when it exceeds cap, no row is written and
- * nothing changes (the listener's state included). Rows unsorted, as sg_local_metrics_raw_device. */
+ * nothing changes (the listener's state included). A cap of at least 59 rows per resource + 60 skips the counting
+ * pass. Rows unsorted, as sg_local_metrics_raw_device. */
 int sg_local_metrics_raw_enqueue(sg_handle* h, int64_t now_ms, sg_metric_node* d_out, uint64_t cap, uint64_t* d_count,
                                  void* stream);
 /* The local chain sharded over a node's GPUs (one process per GPU): every GPU loads the same rules and

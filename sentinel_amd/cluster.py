@@ -306,9 +306,9 @@ class DeviceLocalMetricRollup:
         res = rows[:, 7] & 0xFFFFFFFF
         ent = res == ENTRY_NODE_RESOURCE
         ts = rows[:, 0]
-        t_lo, t_hi = int(ts.min().item()), int(ts.max().item())
+        t_lo, t_hi, n_e = torch.stack([ts.min(), ts.max(), ent.sum()]).tolist()  # one host round trip
         if t_hi - t_lo >= (1 << 31):  # rows spanning ~24 days: two stable sorts instead of the packed key
-            rr = torch.cat([rows[~ent], DeviceLocalMetricRollup._entry_rows(rows[ent])]) if bool(ent.any()) else rows[~ent]
+            rr = torch.cat([rows[~ent], DeviceLocalMetricRollup._entry_rows(rows[ent])]) if n_e else rows[~ent]
             succ = rr[:, 3]
             is_res = (rr[:, 7] & 0xFFFFFFFF) != ENTRY_NODE_RESOURCE
             rr[:, 5] = torch.where(is_res & (succ != 0),
@@ -317,7 +317,6 @@ class DeviceLocalMetricRollup:
             return rr[torch.sort(rr[:, 0], stable=True).indices]
         key = torch.where(ent, torch.full_like(ts, (1 << 63) - 1), ((ts - t_lo) << 32) | res)
         skey, order = torch.sort(key)
-        n_e = int(ent.sum().item())
         n_r = n - n_e
         out = rows.index_select(0, order[:n_r])
         succ = out[:, 3]

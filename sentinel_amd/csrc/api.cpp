@@ -3092,16 +3092,19 @@ int sg_local_metrics_raw_enqueue(sg_handle* h, int64_t now_ms, sg_metric_node* d
     hipStream_t s = h->s_back;
     HIP_TRY(h, hipEventRecord(h->lm_in, stream));
     HIP_TRY(h, hipStreamWaitEvent(s, h->lm_in, 0));
-    for (int emit = 0; emit < 2; ++emit) {
+    // a capacity that covers every possible row (59 per resource, 60 of the ENTRY_NODE) needs no count pass: the
+    // emit pass alone, its counter copied out
+    const bool worst = cap >= (uint64_t)L.K * (kMinuteS - 1) + kMinuteS;
+    for (int emit = worst ? 1 : 0; emit < 2; ++emit) {
         HIP_TRY(h, launch_entry_acc_reset(h->d_lentry_acc, s));
         HIP_TRY(h, hipMemsetAsync(h->d_lm_cnt, 0, sizeof(unsigned long long), s));
-        HIP_TRY(h, launch_local_metrics(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s,
-                                        emit ? h->d_lm_gate : nullptr));
+        const int* gate = emit && !worst ? h->d_lm_gate : nullptr;
+        HIP_TRY(h, launch_local_metrics(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s, gate));
         if (h->d_linbound)
-            HIP_TRY(h, launch_local_entry_rows(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s,
-                                               emit ? h->d_lm_gate : nullptr));
+            HIP_TRY(h, launch_local_entry_rows(L, now_ms, emit ? d_out : nullptr, h->d_lm_cnt, emit, 1, s, gate));
         if (!emit) HIP_TRY(h, launch_metrics_gate(h->d_lm_cnt, cap, (unsigned long long*)d_count, h->d_lm_gate, s));
     }
+    if (worst) HIP_TRY(h, hipMemcpyAsync(d_count, h->d_lm_cnt, sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
     HIP_TRY(h, hipEventRecord(h->lm_done, s));
     HIP_TRY(h, hipStreamWaitEvent(stream, h->lm_done, 0));
     return SG_OK;

@@ -13,11 +13,12 @@ from tests.test_local_shard import N_ORIGINS, N_RES, node_setup, node_trace
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("device_rows", ["host", "device", "enqueue"])
+@pytest.mark.parametrize("device_rows", ["host", "device", "enqueue", "enqueue_worst"])
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_local_chain_handles_equal_node_replay(world, device_rows):
     """device_rows: sg_local_metrics_raw_device into HBM (or sg_local_metrics_raw_enqueue, ordered on a stream, first
-    with a buffer too small: no rows, no side effect) and the device rollup's merge (DeviceLocalMetricRollup)."""
+    with a buffer too small: no rows, no side effect; enqueue_worst: a buffer for every possible row, no counting pass)
+    and the device rollup's merge (DeviceLocalMetricRollup)."""
     import torch
 
     from sentinel_amd.cluster import DeviceLocalMetricRollup
@@ -41,7 +42,16 @@ def test_sharded_local_chain_handles_equal_node_replay(world, device_rows):
         for r in range(world):
             got = engs[r].local_decide_host(ev[parts[r]])
             assert np.array_equal(got, want[parts[r]]), f"batch {b} shard {r}: {(got != want[parts[r]]).sum()} differ"
-        if device_rows == "enqueue":
+        if device_rows == "enqueue_worst":
+            st = torch.cuda.current_stream().cuda_stream
+            bufs = [torch.empty((59 * N_RES + 60, 8), dtype=torch.int64, device="cuda") for _ in engs]
+            cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in engs]
+            for e, buf, c in zip(engs, bufs, cnts):
+                e.local_metrics_raw_enqueue(now, buf, c, st)
+            got_rows = [buf[:int(c.item())] for buf, c in zip(bufs, cnts)]
+            m = DeviceLocalMetricRollup.merge(torch.cat(got_rows))
+            rows = m.cpu().numpy().copy().view(abi.METRIC_NODE_DTYPE).reshape(-1)
+        elif device_rows == "enqueue":
             st = torch.cuda.current_stream().cuda_stream
             bufs = [torch.empty((4 * N_RES + 64, 8), dtype=torch.int64, device="cuda") for _ in engs]
             cnts = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in engs]
