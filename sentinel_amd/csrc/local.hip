@@ -1690,9 +1690,25 @@ __global__ void __launch_bounds__(256) k_lcx_list(LArgs a, BatchArgs sg) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a, BatchArgs sg) {
+// The cx walkers' serial step (cx_entry / cx_exit / cxw_step, out of line) takes the batch arguments by reference:
+// taken from the kernel parameter, that reference made the compiler copy all 1,248 B of LArgs to every lane's
+// scratch at kernel entry and read the fields from there. A copy in LDS, staged once per block straight from the
+// kernarg segment (LArgs is the first parameter), serves those reads instead.
+__device__ __forceinline__ void stage_largs(LArgs* dst) {
+    const uint32_t* src = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(LArgs) / 4); i += blockDim.x) d[i] = src[i];
+    __syncthreads();
+}
+static_assert(sizeof(LArgs) % 4 == 0, "LArgs staged by dwords");
+
+__global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
+    __shared__ LArgs a_lds;
+    (void)a_arg;
+    stage_largs(&a_lds);
+    const LArgs& a = a_lds;
     if (*a.err) return;
     stage_lperiods(a, sbnd, bndp);
     // the segments k_lcx_list compacted (64 of them per wave), else every segment of k_seg's lists
@@ -2573,9 +2589,13 @@ __global__ void __launch_bounds__(256) k_lcx_side(LArgs a) {
     }
 }
 
-__global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a, BatchArgs sg) {
+__global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a_arg, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
+    __shared__ LArgs a_lds;  // as k_lwalk_cx
+    (void)a_arg;
+    stage_largs(&a_lds);
+    const LArgs& a = a_lds;
     if (*a.err) return;
     stage_lperiods(a, sbnd, bndp);
     const int lane = lane_id();
