@@ -1461,14 +1461,43 @@ __device__ __forceinline__ uint2 event_nodes(const LArgs& a, uint32_t idx) {
 // FlowRuleChecker.checkFlow :44-57; cluster-mode rules as on a node that is neither token client nor server,
 // passClusterCheck → fallbackToLocalOrPass :147-175) → DegradeSlot, then the StatisticSlot updates of the
 // ClusterNode, the origin node and the context's DefaultNode, and ParamFlowStatisticEntryCallback.onPass.
+// The lane cx walker's per-lane resource node lives in dynamic LDS (kCxNdBytes per lane): the out-of-line serial
+// step takes it by reference, which kept it in scratch.
+constexpr uint32_t kCxNdBytes = (uint32_t)((sizeof(LNode) + 15) / 16 * 16);
+constexpr uint32_t kCxLdsBytes = 256 * kCxNdBytes;
+
+// The origin / context / RELATE nodes of one event: on the stack (the lane walker: one per lane), or — W, the wave
+// walker, whose serial step every lane runs on wave-uniform values — in the wave's three LDS slots `slots`
+// (kCxNdBytes each), one copy instead of 64 private ones in scratch.
+template <bool W>
+struct CxNodes;
+template <>
+struct CxNodes<false> {
+    LNode on, cn;
+    __device__ CxNodes(const LArgs& a, const LNode& nd, uint32_t on_idx, uint32_t cn_idx, unsigned char*)
+        : on(on_idx != kNoNode ? LNode(a, nd, on_idx) : LNode(a, LNode::None{})),
+          cn(cn_idx != kNoNode ? LNode(a, nd, cn_idx) : LNode(a, LNode::None{})) {}
+};
+template <>
+struct CxNodes<true> {
+    LNode& on;
+    LNode& cn;
+    __device__ CxNodes(const LArgs& a, const LNode& nd, uint32_t on_idx, uint32_t cn_idx, unsigned char* slots)
+        : on(on_idx != kNoNode ? *::new (slots) LNode(a, nd, on_idx) : *::new (slots) LNode(a, LNode::None{})),
+          cn(cn_idx != kNoNode ? *::new (slots + kCxNdBytes) LNode(a, nd, cn_idx)
+                               : *::new (slots + kCxNdBytes) LNode(a, LNode::None{})) {}
+};
+
+template <bool W>
 __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t, int origin,
-                         int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes) {
+                         int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes, unsigned char* slots) {
     const LRule& R = nd.R;
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
     const bool have_on = on_idx != kNoNode, have_cn = cn_idx != kNoNode;
     // windows opened as touched (cx_rule, the StatisticSlot adds); an absent node loads nothing
-    LNode on = have_on ? LNode(a, nd, on_idx) : LNode(a, LNode::None{});
-    LNode cn = have_cn ? LNode(a, nd, cn_idx) : LNode(a, LNode::None{});
+    CxNodes<W> nn(a, nd, on_idx, cn_idx, slots);
+    LNode& on = nn.on;
+    LNode& cn = nn.cn;
     const bool params = R.ps && a.has_ps && x && !x->args_null;
     int32_t status = SG_LOCAL_PASS;
     int64_t wait = 0;
@@ -1548,6 +1577,10 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
             v = cx_rule(a, on, r, c, e, t, qs, qm, &w);
         } else if (sel == 2) {
             v = cx_rule(a, cn, r, c, e, t, qs, qm, &w);
+        } else if constexpr (W) {  // (a RELATE group is walked by the lane walker; kept for completeness)
+            LNode& rn = *::new (slots + 2 * kCxNdBytes) LNode(a, bndp, (uint32_t)r.ref);
+            v = cx_rule(a, rn, r, c, e, t, qs, qm, &w);
+            rn.finish();
         } else {  // RELATE: another resource of this key group, kept in memory between its events
             LNode rn(a, bndp, (uint32_t)r.ref);
             v = cx_rule(a, rn, r, c, e, t, qs, qm, &w);
@@ -1611,22 +1644,27 @@ __device__ void cx_entry(const LArgs& a, const uint32_t* const* bndp, LNode& nd,
 
 // One exit of a cx resource: StatisticSlot.exit (:124-165) on the ClusterNode (+ DegradeSlot.exit), the origin node
 // and the context's DefaultNode; ParamFlowStatisticExitCallback.onExit (decreaseThreadCount of the exit's args).
+template <bool W>
 __device__ void cx_exit(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& e, int64_t t,
-                        int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes) {
+                        int64_t create, int origin, int ctx, const sg_slot_ext* x, uint32_t qs, uint32_t qm, uint2 nodes,
+                        unsigned char* slots) {
     nd.exit(e, t, create);
     const uint32_t on_idx = nodes.x, cn_idx = nodes.y;
-    if (on_idx != kNoNode) {  // recordCompleteFor(originNode)
-        LNode on(a, nd, on_idx);
-        on.at(qs, qm);
-        on.exit(e, t, create);
-        on.finish();
-    }
-    if (cn_idx != kNoNode) {
-        LNode cn(a, nd, cn_idx);
-        cn.at(qs, qm);
-        cn.exit(e, t, create);
-        cn.finish();
-    }
+    auto node_exit = [&](uint32_t idx, unsigned char* slot) {
+        if constexpr (W) {
+            LNode& m = *::new (slot) LNode(a, nd, idx);
+            m.at(qs, qm);
+            m.exit(e, t, create);
+            m.finish();
+        } else {
+            LNode m(a, nd, idx);
+            m.at(qs, qm);
+            m.exit(e, t, create);
+            m.finish();
+        }
+    };
+    if (on_idx != kNoNode) node_exit(on_idx, slots);  // recordCompleteFor(originNode)
+    if (cn_idx != kNoNode) node_exit(cn_idx, slots ? slots + kCxNdBytes : nullptr);
     if (nd.R.ps && a.has_ps && x && !x->args_null) ps_threads(a.ps, nd.k, x->arg_begin, x->arg_count, -1);
 }
 
@@ -1702,10 +1740,13 @@ __device__ __forceinline__ void stage_largs(LArgs* dst) {
 }
 static_assert(sizeof(LArgs) % 4 == 0, "LArgs staged by dwords");
 
+
 __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
     __shared__ LArgs a_lds;
+    extern __shared__ __attribute__((aligned(16))) unsigned char cx_nd_lds[];
+    void* const nd_mem = cx_nd_lds + (size_t)threadIdx.x * kCxNdBytes;
     (void)a_arg;
     stage_largs(&a_lds);
     const LArgs& a = a_lds;
@@ -1726,18 +1767,18 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
                 const sg_local_event le = a.ev[e.idx];
                 const sg_slot_ext* x = a.ext ? a.ext + e.idx : nullptr;
                 const int ctx = x ? (int)x->context : 0;
-                LNode nd(a, bndp, le.resource & SG_KEY_INDEX);
+                LNode& nd = *::new (nd_mem) LNode(a, bndp, le.resource & SG_KEY_INDEX);
                 nd.created = 1;
                 const uint32_t qs = nd.cs.of(e.idx), qm = nd.cm.of(e.idx);
                 if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);  // an entry opens what it touches (cx_entry)
                 const uint2 nodes = event_nodes(a, e.idx);
-                if (e.kind == SG_LOCAL_ENTRY) cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
-                else cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
+                if (e.kind == SG_LOCAL_ENTRY) cx_entry<false>(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes, nullptr);
+                else cx_exit<false>(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes, nullptr);
                 nd.finish();
             }
             continue;
         }
-        LNode nd(a, bndp, k);
+        LNode& nd = *::new (nd_mem) LNode(a, bndp, k);
         nd.created = 1;
         // Dead periods as in the wave walker (cx_wave), one lane at a time: once a QPS rule every entry reaches is
         // saturated, the period's further entries need only their ParamFlowSlot check and BLOCK counts (ClusterNode
@@ -1838,7 +1879,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
             if (e.kind != SG_LOCAL_ENTRY) nd.at(qs, qm);
             const uint2 nodes = event_nodes(a, e.idx);
             if (e.kind == SG_LOCAL_ENTRY) {
-                cx_entry(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes);
+                cx_entry<false>(a, bndp, nd, e, le.ts_ms, le.origin, ctx, x, qs, qm, nodes, nullptr);
                 if (dead_ok && !dead && nd.cs.q == qs && nd.cm.q == qm && cxw_saturated(a, nd)) {
                     dead = true;
                     dqs = qs;
@@ -1846,7 +1887,7 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
                     dend = min(nd.cs.next_b, nd.cm.next_b);
                 }
             } else {
-                cx_exit(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes);
+                cx_exit<false>(a, bndp, nd, e, le.ts_ms, le.create_ts, le.origin, ctx, x, qs, qm, nodes, nullptr);
             }
         }
         if (dead) {
@@ -1877,14 +1918,14 @@ __global__ void __launch_bounds__(256) k_lwalk_cx(LArgs a_arg, BatchArgs sg) {
 // controllers) stay out of the walker's loop, whose dead-period chunks then run without spilling.
 __device__ __noinline__ bool cxw_step(const LArgs& a, const uint32_t* const* bndp, LNode& nd, const LEvent& es,
                                       int64_t te, int64_t ce, int og, const sg_slot_ext* xp, uint32_t qs0, uint32_t qm0,
-                                      uint2 nn) {
+                                      uint2 nn, unsigned char* slots) {
     const int ctx = xp ? (int)xp->context : 0;
     if (es.kind == SG_LOCAL_ENTRY) {
-        cx_entry(a, bndp, nd, es, te, og, ctx, xp, qs0, qm0, nn);
+        cx_entry<true>(a, bndp, nd, es, te, og, ctx, xp, qs0, qm0, nn, slots);
         return true;
     }
     nd.at(qs0, qm0);
-    cx_exit(a, bndp, nd, es, te, ce, og, ctx, xp, qs0, qm0, nn);
+    cx_exit<true>(a, bndp, nd, es, te, ce, og, ctx, xp, qs0, qm0, nn, slots);
     return false;
 }
 
@@ -1942,7 +1983,7 @@ __device__ bool cxw_saturated(const LArgs& a, const LNode& nd) {
 }
 
 __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* const* bndp, uint32_t k, uint64_t s,
-                        uint64_t e_end) {
+                        uint64_t e_end, void* nd_mem, unsigned char* slots) {
     const int lane = lane_id();
     // SG_DEBUG & 64: counters into sg.dbg_ctr[20..]: segments, wave ticks (sum, max), dead / general chunks, serial
     // entry / exit steps, ticks in dead chunks, in serial steps (s_memrealtime, 100 MHz); [12..14] the param dead
@@ -1952,7 +1993,9 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
     const uint64_t tw0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
     uint64_t c_dead = 0, c_gen = 0, c_sent = 0, c_sexit = 0, t_dead = 0, t_ser = 0;
     uint64_t ph[3] = {0, 0, 0};
-    LNode nd(a, bndp, k);
+    // the resource's node in the wave's LDS slot: its fields are wave-uniform, and the out-of-line serial step takes it
+    // by reference — on the stack every lane kept its own copy in scratch, 64 private copies of one value
+    LNode& nd = *::new (nd_mem) LNode(a, bndp, k);
     nd.created = 1;
     int32_t prule = -1;
     const bool dead_ok = !(*a.flags & (kLFlagPrio | kLFlagNonPos)) && cxw_dead_able(a, nd.R, k, &prule);
@@ -2006,7 +2049,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
         while (used) {
             const int j = __builtin_ctzll(used);
             used &= used - 1;
-            LNode on(a, nd, (uint32_t)bcast32((int)ob_node, j));
+            LNode& on = *::new (slots) LNode(a, nd, (uint32_t)bcast32((int)ob_node, j));  // the wave's LDS slot
             on.at(dead_qs, dead_qm);
             const int64_t sum = bcast64(ob_sum, j);
             on.sc[kLBlock] += sum;
@@ -2333,7 +2376,7 @@ __device__ void cx_wave(const LArgs& a, const BatchArgs& sg, const uint32_t* con
             xe.args_null = bcast32(xx.args_null, q);
             const uint2 nn = make_uint2((uint32_t)bcast32((int)nodes.x, q), (uint32_t)bcast32((int)nodes.y, q));
             const sg_slot_ext* xp = a.ext ? &xe : nullptr;
-            const bool entry = cxw_step(a, bndp, nd, es, te, ce, og, xp, qs0, qm0, nn);
+            const bool entry = cxw_step(a, bndp, nd, es, te, ce, og, xp, qs0, qm0, nn, slots);
             if (dg) {
                 if (entry) ++c_sent;
                 else ++c_sexit;
@@ -2593,6 +2636,8 @@ __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a_arg,
     __shared__ uint32_t sbnd[kLdsBnd];
     __shared__ const uint32_t* bndp[kMaxWl];
     __shared__ LArgs a_lds;  // as k_lwalk_cx
+    __shared__ alignas(16) unsigned char cxw_nd[4][kCxNdBytes];         // each wave's resource node (cx_wave)
+    __shared__ alignas(16) unsigned char cxw_slots[4][3 * kCxNdBytes];  // and its event's origin / context nodes
     (void)a_arg;
     stage_largs(&a_lds);
     const LArgs& a = a_lds;
@@ -2625,7 +2670,7 @@ __global__ void __launch_bounds__(256, SG_LWALK_BLOCKS) k_lwalk_cxw(LArgs a_arg,
         const uint64_t e = gallop_search(s + lo, a.n, [&](uint64_t p) {
             return (uint32_t)(a.rec_sorted[p] >> a.kshift) != k;
         }, lane);
-        cx_wave(a, sg, bndp, k, s, e);
+        cx_wave(a, sg, bndp, k, s, e, cxw_nd[threadIdx.x >> 6], cxw_slots[threadIdx.x >> 6]);
     }
 }
 
@@ -3013,7 +3058,10 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k_lcx_list, dim3(lgrid(a.n, 256, 4096)), dim3(256), 0, aux, a, sg);
         }
-        hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), 0, aux, a, sg);
+        static const bool lds_ok = hipFuncSetAttribute((const void*)k_lwalk_cx, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)kCxLdsBytes) == hipSuccess;
+        if (!lds_ok) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_lwalk_cx, dim3(bs), dim3(256), kCxLdsBytes, aux, a, sg);
     }
     hipLaunchKernelGGL(k_lwalk_short, dim3(bs), dim3(256), 0, stream, a, sg);
     e = hipEventRecord(join, aux);
