@@ -3263,11 +3263,13 @@ int lnode_prepare(sg_handle* h, uint64_t n) {
     return SG_OK;
 }
 
-// Pool capacity >= used nodes: new node arrays (the resources, the old pool, empty nodes), geometric growth.
+// Pool capacity >= used nodes: new node arrays (the resources, the old pool, empty nodes), geometric growth. Every
+// growth copies the resources' nodes too (~4.2 KB each: 4 GB at 1M resources), so the pool starts at K / 16 nodes
+// (~260 MB at 1M resources) and grows fourfold with room for twice the nodes in use.
 int lnode_grow(sg_handle* h, uint64_t used) {
     if (used <= h->l_pool_cap) return SG_OK;
     const uint64_t K = h->ltab.size();
-    uint64_t cap = std::max<uint64_t>({used, 2ull * h->l_pool_cap, 1024ull});
+    uint64_t cap = std::max<uint64_t>({2ull * used, 4ull * h->l_pool_cap, 1024ull, K / 16});
     if (K + cap >= SG_KEY_BAD) cap = SG_KEY_BAD - 1 - K;
     if (K + used >= SG_KEY_BAD || cap < used) return fail(h, SG_E_CAPACITY, "too many origin / context nodes");
     const uint64_t N = K + cap, old = h->l_nodes;
