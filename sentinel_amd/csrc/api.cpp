@@ -3268,6 +3268,8 @@ int lnode_prepare(sg_handle* h, uint64_t n) {
 // (~260 MB at 1M resources) and grows fourfold with room for twice the nodes in use.
 int lnode_grow(sg_handle* h, uint64_t used) {
     if (used <= h->l_pool_cap) return SG_OK;
+    if (const char* f = std::getenv("SG_TEST_POOL_FAIL"))  // test aid: a failed growth (tests/test_local_rules_gpu.py)
+        if (std::atoi(f)) return fail(h, SG_E_NOMEM, "node pool (SG_TEST_POOL_FAIL)");
     const uint64_t K = h->ltab.size();
     uint64_t cap = std::max<uint64_t>({2ull * used, 4ull * h->l_pool_cap, 1024ull, K / 16});
     if (K + cap >= SG_KEY_BAD) cap = SG_KEY_BAD - 1 - K;

@@ -3037,8 +3037,13 @@ hipError_t launch_local_back(const LArgs& a, const BatchArgs& sg, bool has_cx, h
     if (a.defer_last) hipLaunchKernelGGL(k_local_check_last, dim3(1), dim3(1), 0, stream, a);
     // the side words are read by both cx walkers (the lane walker on `aux` in its dead periods): they are
     // written before the fork, so `aux` is ordered after them
-    if (has_cx && a.cxw && a.cxside)
+    if (has_cx && a.cxw && a.cxside) {
+        // test aid (env SG_TEST_CXSIDE_POISON=1): the side words start as garbage, so a walker that read them before
+        // k_lcx_side wrote them would fail every time (the lane walker's fork comes after k_lcx_side)
+        if (const char* p = std::getenv("SG_TEST_CXSIDE_POISON"))
+            if (std::atoi(p)) (void)hipMemsetAsync(a.cxside, 0xFF, sizeof(CxSide) * a.n, stream);
         hipLaunchKernelGGL(k_lcx_side, dim3(lgrid(a.n, 256, 8192)), dim3(256), 0, stream, a);
+    }
     hipError_t e = hipEventRecord(fork, stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(aux, fork, 0);
     if (e != hipSuccess) return e;

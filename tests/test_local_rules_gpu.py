@@ -222,3 +222,29 @@ def test_bad_origin_rejected():
     with pytest.raises(EngineError) as ei:
         eng.local_decide_host(ev)
     assert ei.value.code == abi.SG_E_INVAL
+
+
+def test_pool_growth_failure_leaves_nodes_readable(monkeypatch):
+    """A node-pool growth that fails (injected: SG_TEST_POOL_FAIL) refuses the batch; the origin nodes its map
+    entries already name have no storage yet and read as empty nodes (no read past the node arrays); once the pool
+    can grow, the same batch decides as the oracle does and every node equals the oracle's."""
+    from sentinel_amd.engine import EngineError
+    rng = np.random.default_rng(8)
+    n_res, n_origins = 10, 3
+    sets = [[local_flow_rule(r, 20.0), local_flow_rule(r, 4.0, limit_app=1)] for r in range(n_res)]
+    ora, eng, fr = _setup(n_res, rng, n_origins, rule_sets=sets)
+    gen = LocalTraceGen(ora)
+    t = 1_700_000_000_000
+    ent = _entries(rng, 5_000, n_res, t, 2000, n_origins)
+    ev, want = gen.run(ent, rng.integers(0, 40, 5_000).astype(np.int32), np.zeros(5_000, np.uint8), t + 2000)
+    monkeypatch.setenv("SG_TEST_POOL_FAIL", "1")
+    with pytest.raises(EngineError):
+        eng.local_decide_host(ev)
+    for r in range(n_res):
+        for o in range(1, n_origins + 1):
+            s, b, m, h, _ = eng.local_origin_state(r, o, with_exists=True)
+            assert not s[:, 1:].any() and not m[:, 1:].any() and not b[:, 1:].any() and h[0] == 0
+    monkeypatch.delenv("SG_TEST_POOL_FAIL")
+    got = eng.local_decide_host(ev)
+    assert np.array_equal(got, want)
+    _compare(eng, ora, fr, n_res, n_origins)

@@ -249,14 +249,16 @@ def test_hot_resources_with_params():
     _run(ora, ps, eng, fr, params, n_res, 2, 2, [(60_000, 3000), (60_000, 3000)], 11, zipf=1.5)
 
 
-@pytest.mark.parametrize("env", [{}, {"SG_CXW_MIN": "17"}, {"SG_CXW": "0"}], ids=["default", "cxw17", "lanes"])
+@pytest.mark.parametrize("env", [{}, {"SG_CXW_MIN": "17"}, {"SG_CXW": "0"}, {"SG_TEST_CXSIDE_POISON": "1"}],
+                         ids=["default", "cxw17", "lanes", "cxside_poison"])
 @pytest.mark.parametrize("flags", [0, abi.FLAG_SERIAL_ONLY, abi.FLAG_WAVE_ONLY])
 def test_dead_periods(flags, env, monkeypatch):
     """Hot cx resources whose window periods saturate, with no prioritized entry and no context tracking: the cx
     walkers' dead periods (the wave walker's chunks, the lane walker's per-entry path) decide the rest of each period —
     origin-limitApp, "other", lone WarmUp and one-QPS-param-rule resources (token buckets and a throttle over Zipf
     values, null and collection arguments among them), with the wave walker on the short classes too (SG_CXW_MIN=17)
-    or off (SG_CXW=0)."""
+    or off (SG_CXW=0); with the side words poisoned before k_lcx_side writes them (SG_TEST_CXSIDE_POISON: a walker
+    ordered before that kernel would read garbage slot indices)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("SG_DEBUG", "64")  # the wave walker's counters (local.hip cx_wave; results unchanged)
