@@ -236,8 +236,12 @@ __global__ void __launch_bounds__(256) k_nreq_keys(NodeReqArgs q) {
         }
         if (q.cp) {
             const sg_cparam_req r = q.cp[i];
-            if (r.key < q.K) g = q.shard_of[r.key];
-            nv = r.value_count;
+            const uint32_t key = r.key & SG_KEY_INDEX;
+            if (key < q.K) g = q.shard_of[key];
+            // only a valid request's values are read (DefaultTokenService answers the others without them); an
+            // invalid one reaches its shard with no values, and the shard answers it as one handle would
+            const bool valid = key < q.K && r.acquire > 0 && r.value_count > 0;
+            nv = valid ? r.value_count : 0u;
             if (nv && ((uint64_t)r.value_begin + nv > q.n_values)) {  // the whole batch is refused (SG_E_INVAL)
                 atomicOr(q.err, kErrBounds);
                 nv = 0;
@@ -333,7 +337,7 @@ __global__ void __launch_bounds__(256) k_nreq_gather(NodeReqArgs q, const uint64
         q.sub_pos[j] = (uint32_t)i;
         if (q.cp) {
             sg_cparam_req r = q.cp[i];
-            if (r.key < q.K) r.key = q.local_of[r.key];
+            if ((r.key & SG_KEY_INDEX) < q.K) r.key = q.local_of[r.key & SG_KEY_INDEX] | (r.key & ~SG_KEY_INDEX);
             for (uint32_t v = 0; v < nv; ++v) q.sub_vals[off + v] = q.values[r.value_begin + v];
             r.value_begin = nv ? off - q.vbase[g] : 0u;
             q.sub_cp[j] = r;
@@ -379,12 +383,94 @@ hipError_t launch_nsnap_scatter(const double* part, const uint32_t* node_key, ui
     return hipGetLastError();
 }
 
+// The contract on a param batch's value ranges (sg_cparam_decide_batch): the valid requests' ranges follow request
+// order and do not overlap — each begins at or after the largest end of the earlier valid requests. One handle
+// checks it slot by slot on its sorted records (k_cp_order); the node copies each request's values into its slice,
+// so it checks the node batch as a whole: per 4096-request tile the largest end, one block's exclusive prefix max
+// over the tiles, then each tile against that carry (16 consecutive requests per thread, a block-wide prefix max).
+__device__ __forceinline__ bool nreq_valid(const NodeReqArgs& q, const sg_cparam_req& r) {
+    return (r.key & SG_KEY_INDEX) < q.K && r.acquire > 0 && r.value_count > 0;
+}
+
+__global__ void __launch_bounds__(256) k_nreq_vmax(NodeReqArgs q) {
+    __shared__ uint32_t wm[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kNvTile;
+    uint32_t m = 0;
+    for (uint64_t i = t0 + threadIdx.x; i < min(q.n, t0 + kNvTile); i += 256) {
+        const sg_cparam_req r = q.cp[i];
+        if (nreq_valid(q, r)) m = max(m, r.value_begin + r.value_count);
+    }
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) q.tsum[blockIdx.x] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
+}
+
+__global__ void __launch_bounds__(1024) k_nreq_vmax_scan(NodeReqArgs q, uint32_t tiles) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < tiles; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < tiles ? q.tsum[i] : 0u;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const uint32_t x = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
+            __syncthreads();
+            part[threadIdx.x] = max(part[threadIdx.x], x);
+            __syncthreads();
+        }
+        const uint32_t c = carry;
+        const uint32_t excl = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+        if (i < tiles) q.tsum[i] = max(c, excl);
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = max(c, part[1023]);
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_nreq_vorder(NodeReqArgs q) {
+    __shared__ uint32_t tm[256];
+    constexpr int kPer = (int)(kNvTile / 256);
+    const uint64_t i0 = (uint64_t)blockIdx.x * kNvTile + (uint64_t)threadIdx.x * kPer;
+    uint32_t m = 0;
+    for (int u = 0; u < kPer && i0 + u < q.n; ++u) {
+        const sg_cparam_req r = q.cp[i0 + u];
+        if (nreq_valid(q, r)) m = max(m, r.value_begin + r.value_count);
+    }
+    tm[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive prefix max of the threads' maxima
+        const uint32_t x = threadIdx.x >= (unsigned)o ? tm[threadIdx.x - o] : 0u;
+        __syncthreads();
+        tm[threadIdx.x] = max(tm[threadIdx.x], x);
+        __syncthreads();
+    }
+    uint32_t carry = max(q.tsum[blockIdx.x], threadIdx.x ? tm[threadIdx.x - 1] : 0u);
+    bool bad = false;
+    for (int u = 0; u < kPer && i0 + u < q.n; ++u) {
+        const sg_cparam_req r = q.cp[i0 + u];
+        if (!nreq_valid(q, r)) continue;
+        bad |= r.value_begin < carry;
+        carry = max(carry, r.value_begin + r.value_count);
+    }
+    if (bad) atomicOr(q.err, kErrBounds);
+}
+
 hipError_t launch_nreq_keys(const NodeReqArgs& q, hipStream_t stream) {
     if (q.n == 0) return hipSuccess;
     uint64_t g = (q.n + 255) / 256;
     if (g > 4096) g = 4096;
     lds_poison(stream);
     hipLaunchKernelGGL(k_nreq_keys, dim3((unsigned)g), dim3(256), 0, stream, q);
+    if (q.cp) {  // the value ranges' order (the tile maxima use tsum before the gather's value scan does)
+        const uint32_t tiles = (uint32_t)((q.n + kNvTile - 1) / kNvTile);
+        hipLaunchKernelGGL(k_nreq_vmax, dim3(tiles), dim3(256), 0, stream, q);
+        hipLaunchKernelGGL(k_nreq_vmax_scan, dim3(1), dim3(1024), 0, stream, q, tiles);
+        hipLaunchKernelGGL(k_nreq_vorder, dim3(tiles), dim3(256), 0, stream, q);
+    }
     return hipGetLastError();
 }
 

@@ -109,7 +109,8 @@ def test_node_param_tokens_equal_one_token_service(G):
 
 def test_node_param_reload_and_refused_batches():
     """A reload re-partitions the rules (surviving flowIds keep their owner, hence their metric); a batch with a
-    value range past the value array or out of time order is refused whole, leaving every shard untouched."""
+    value range past the value array, valid requests' ranges that overlap or run against request order (the
+    sg_cparam_decide_batch contract), or out of time order is refused whole, leaving every shard untouched."""
     from sentinel_amd.engine import EngineError
     rng = np.random.default_rng(210)
     rules = _prules(rng, 24)
@@ -126,6 +127,17 @@ def test_node_param_reload_and_refused_batches():
     bad["value_begin"][-1] = len(nvals)
     with pytest.raises(EngineError):
         node.cparam_decide_host(bad, nvals)
+    valid = np.nonzero((nxt["key"] < len(new)) & (nxt["acquire"] > 0) & (nxt["value_count"] > 0))[0]
+    a, b = int(valid[100]), int(valid[101])
+    ovl = nxt.copy()  # two valid requests' ranges overlap
+    ovl["value_begin"][b] = ovl["value_begin"][a]
+    with pytest.raises(EngineError):
+        node.cparam_decide_host(ovl, nvals)
+    back = nxt.copy()  # two valid requests' ranges out of request order
+    back["value_begin"][[a, b]] = back["value_begin"][[b, a]]
+    back["value_count"][[a, b]] = 1
+    with pytest.raises(EngineError):
+        node.cparam_decide_host(back, nvals)
     old = nxt.copy()
     old["ts_ms"][0] = t - 5
     with pytest.raises(EngineError):
