@@ -802,7 +802,9 @@ sg_handle*  sg_node_front(sg_node* nd);
  * requestConcurrentToken / releaseConcurrentToken, DefaultTokenService.java:53-85): a param rule (with its hot items)
  * lives on the shard owning its flowId; a concurrent acquire goes to the owner of its flow rule's flowId, a release
  * to the shard its token id names (node token id = (shard token id - 1) * G + shard + 1). A node batch in caller order
- * is checked for time order and value bounds on devices[0] (refused whole, nothing decided), split stably by owner
+ * is checked for time order and the value-range contract of sg_cparam_decide_batch over the whole batch (the valid
+ * requests' ranges inside the value array, in request order, not overlapping) on devices[0] (refused whole, nothing
+ * decided), split stably by owner
  * with one 8-bit radix pass, decided shard by shard in the node's order and gathered back: the statuses, counters and
  * metrics equal one handle deciding the batch; token ids are the node's own (unique, as the reference's are only
  * unique). Param batches whose rules name a namespace with the GlobalRequestLimiter enabled are refused
