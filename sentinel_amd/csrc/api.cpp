@@ -5814,7 +5814,7 @@ int sg_node_cparam_decide_batch(sg_node* nd, const sg_cparam_req* req, uint64_t 
     q.local_of = nd->d_cp_local_of;
     q.sub_cp = static_cast<sg_cparam_req*>(nd->d_sub_nreq);
     q.last_ts = nd->cp_last_ts;
-    (void)stream;  // synchronous: the shards' fixed points wait on the host between rounds
+    NHIP(nd, hipStreamSynchronize((hipStream_t)stream));  // the caller's batch is in place (synchronous call)
     std::vector<uint64_t> base, cnt, vbase, vcnt;
     rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
     if (rc) return rc;
@@ -5914,7 +5914,7 @@ int sg_node_conc_decide_batch(sg_node* nd, const sg_conc_req* req, uint64_t n, s
     q.local_of = nd->d_local_of;
     q.sub_cc = static_cast<sg_conc_req*>(nd->d_sub_nreq);
     q.last_ts = nd->cc_last_ts;
-    (void)stream;
+    NHIP(nd, hipStreamSynchronize((hipStream_t)stream));  // the caller's batch is in place (synchronous call)
     std::vector<uint64_t> base, cnt, vbase, vcnt;
     rc = node_nreq_route(nd, q, base, cnt, vbase, vcnt);
     if (rc) return rc;
