@@ -176,7 +176,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_local_chain_equals_node_replay(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
