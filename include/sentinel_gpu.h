@@ -794,9 +794,10 @@ int         sg_node_flow_read_state(sg_node* nd, uint32_t key, int64_t* starts, 
 int         sg_node_snapshot_metrics(sg_node* nd, int64_t now_ms, double* out, uint64_t cap);
 int         sg_node_shard_of(const sg_node* nd, uint32_t key, uint32_t* shard, uint32_t* local_key);
 /* The node's front handle (devices[0]; owned by the node, not to be destroyed): it holds the namespace limiters, so
- * the node's cluster param tokens (sg_cparam_*: ClusterParamFlowChecker.java:43-45 shares the limiter) and
- * concurrent tokens (sg_conc_*) are decided on it, beside the sharded flow tokens. Its own sg_flow_* entry points
- * must not be called. */
+ * cluster param tokens whose rules sit under an enabled GlobalRequestLimiter (ClusterParamFlowChecker.java:43-45
+ * shares the limiter in caller order) are decided on it with sg_cparam_*; every other param and concurrent token
+ * goes through the sharded sg_node_cparam_* / sg_node_conc_* below. Its own sg_flow_* entry points must not be
+ * called. */
 sg_handle*  sg_node_front(sg_node* nd);
 /* Cluster param and concurrent tokens sharded over the node (DefaultTokenService.requestParamToken /
  * requestConcurrentToken / releaseConcurrentToken, DefaultTokenService.java:53-85): a param rule (with its hot items)
