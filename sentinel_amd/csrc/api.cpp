@@ -2286,11 +2286,19 @@ int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32
     if (const char* e = std::getenv("SG_PACE_SHORT_MAX")) psplit = (uint32_t)std::strtoul(e, nullptr, 10);
     p.short_max = (h->cfg.flags & SG_FLAG_WAVE_ONLY) ? 0u : (h->cfg.flags & SG_FLAG_SERIAL_ONLY) ? 0xFFFFFFFFu : psplit;
     const int gbits = bits_for((uint64_t)p.n_rules + 1);
-    if (p.ibits + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "pace rules x max_batch too large for 64-bit records");
+    p.gshift = p.ibits + 8;  // {rule | acquire code : 8 | request index}
+    if (p.gshift + gbits > 64) return fail(h, SG_E_UNSUPPORTED, "pace rules x max_batch too large for 64-bit records");
+    // the millisecond table (shared with the hot-parameter path: both are synchronous calls of this handle)
+    if (!h->d_p_msb && (hipMalloc(&h->d_p_msb, sizeof(uint32_t) * kMaxPeriods) != hipSuccess ||
+                        hipMalloc(&h->d_p_mt, 2 * sizeof(int64_t)) != hipSuccess))
+        return fail(h, SG_E_NOMEM, "pace millisecond table");
+    p.msb = h->d_p_msb;
+    p.mt0 = h->d_p_mt;
+    p.mnp = reinterpret_cast<uint32_t*>(h->d_p_mt + 1);
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, 2 * sizeof(uint32_t), stream));
     uint64_t* sorted = nullptr;
-    HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.ibits, p.ibits + gbits, &sorted, stream,
+    HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.gshift, p.gshift + gbits, &sorted, stream,
                                  h->aux, h->fork, h->join));
     h->last_sorted = sorted;
     HIP_TRY(h, hipMemcpyAsync(h->h_err, h->d_err, sizeof(int), hipMemcpyDeviceToHost, stream));

@@ -322,6 +322,10 @@ struct PaceArgs {
     uint32_t* long_count;   // [0] long segments, [1] short segments
     uint32_t* short_list;
     uint32_t short_max;
+    int gshift;             // records {rule : high bits | acquire code : 8 | request index : ibits}: rule at gshift
+    uint32_t* msb;          // the millisecond table: first request index of every millisecond of the batch
+    int64_t* mt0;           // [0] the batch's first timestamp, then {millisecond count, zero word}
+    uint32_t* mnp;
 };
 
 // The long-rule walker runs on `aux` beside the short one (fork / join events).

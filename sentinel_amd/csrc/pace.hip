@@ -11,8 +11,9 @@
 //   expected - now > maxQ → block, latest unchanged
 //   else                 → latest = expected, pass after sleeping expected - now ms
 // A batch:
-//   k_pace_prep     decides what never touches latestPassedTime (no rule, acquireCount <= 0 → pass;
-//                   count <= 0 → block), packs {rule | request index} for the rest, outputs "blocked"
+//   k_pace_prep     decides what never touches latestPassedTime (no rule, acquireCount <= 0 → pass), packs
+//                   {rule | acquire code | request index} for the rest, outputs "blocked", writes the batch's
+//                   millisecond table (the walkers' timestamps); a rule with count <= 0 blocks in its walker
 //   radix sort by rule (sort.hip): each rule's requests contiguous, in arrival order
 //   k_pace_seg      segment heads split by length into the lane walker's and the wave walker's lists
 //   k_pace_short    one lane per rule with <= short_max requests, serial recurrence in registers
@@ -88,31 +89,81 @@ __device__ __forceinline__ uint64_t pace_wave_search(uint64_t lo, uint64_t hi, P
 
 }  // namespace
 
+// Validation and the records. A request reads nothing but itself: its acquireCount rides in the record (8-bit code,
+// 255 = read the request) and its timestamp is recovered from the batch's millisecond table (first request index of
+// every millisecond), so neither the rule table nor the requests are gathered per request — count <= 0 (:53-55) is
+// answered by the walkers once per rule.
+constexpr uint32_t kPcAesc = 255;
+constexpr uint32_t kPcLdsMs = 4096;  // millisecond table entries staged in LDS (a batch spanning <= 4 s)
+
 __global__ void __launch_bounds__(256) k_pace_prep(PaceArgs p) {
-    const uint64_t none = (uint64_t)p.n_rules << p.ibits;
+    const uint64_t none = (uint64_t)p.n_rules << p.gshift;
+    const int64_t t0 = p.req[0].ts_ms;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (uint64_t)gridDim.x * blockDim.x) {
         const sg_pace_req q = p.req[i];
-        if (q.ts_ms < 0 || (i == 0 ? q.ts_ms < *p.last_ts : q.ts_ms < p.req[i - 1].ts_ms)) atomicOr(p.err, kErrTime);
+        const int64_t tp = i == 0 ? *p.last_ts : p.req[i - 1].ts_ms;
+        if (q.ts_ms < 0 || q.ts_ms < tp) atomicOr(p.err, kErrTime);
+        if (i == 0) {
+            *p.mt0 = q.ts_ms;
+        } else if (q.ts_ms > tp) {  // a new millisecond starts at i
+            for (int64_t ms = (tp < t0 ? t0 : tp) + 1; ms <= q.ts_ms; ++ms) {
+                const int64_t qq = ms - t0;
+                if (qq >= (int64_t)kMaxPeriods) break;
+                p.msb[qq] = (uint32_t)i;
+            }
+        }
+        if (i == p.n - 1) *p.mnp = (uint32_t)min(q.ts_ms - t0 + 1, (int64_t)kMaxPeriods + 1);
         uint64_t rec = none;
-        int32_t out = SG_PACE_BLOCKED;
+        int32_t out = SG_PACE_BLOCKED;  // a walked request passes by its walker; count <= 0 leaves it blocked
         if (q.rule >= p.n_rules || q.acquire <= 0) {
             out = 0;  // no rule for the resource / acquireCount <= 0 (:48-50)
-        } else if (!(p.rules[q.rule].count > 0.0)) {
-            out = SG_PACE_BLOCKED;  // count <= 0 (:53-55)
         } else {
-            rec = ((uint64_t)q.rule << p.ibits) | i;
+            const uint64_t ac = (uint64_t)q.acquire >= kPcAesc ? kPcAesc : (uint64_t)q.acquire;
+            rec = ((uint64_t)q.rule << p.gshift) | (ac << p.ibits) | i;
         }
         p.out[i] = out;
         p.rec[i] = rec;
     }
 }
 
+__shared__ uint32_t pc_sms[kPcLdsMs];
+__shared__ uint32_t pc_nms;  // table entries in LDS, 0: read the timestamps
+__shared__ int64_t pc_t0;
+
+__device__ __forceinline__ void pc_stage_ms(const PaceArgs& p) {
+    const uint32_t np = *p.mnp;
+    const bool lds = np <= kPcLdsMs;
+    for (uint32_t x = threadIdx.x; lds && x < np; x += blockDim.x) pc_sms[x] = p.msb[x];
+    if (threadIdx.x == 0) {
+        pc_nms = lds ? np : 0u;
+        pc_t0 = *p.mt0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int64_t pc_ts(const PaceArgs& p, uint32_t idx) {
+    const uint32_t np = pc_nms;
+    if (np == 0) return p.req[idx].ts_ms;
+    uint32_t lo = 0, hi = np;  // the largest q with table[q] <= idx (entry 0 unused)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pc_sms[mid] <= idx) lo = mid;
+        else hi = mid;
+    }
+    return pc_t0 + (int64_t)lo;
+}
+
+__device__ __forceinline__ int32_t pc_acq(const PaceArgs& p, uint64_t rec, uint32_t idx) {
+    const uint32_t ac = (uint32_t)(rec >> p.ibits) & 255u;
+    return ac == kPcAesc ? p.req[idx].acquire : (int32_t)ac;
+}
+
 // 0 = not a segment head, 1 = head of a rule walked by one lane, 2 = head of a rule walked by a wave
 __device__ __forceinline__ int pace_head_class(const PaceArgs& p, uint64_t j) {
-    const uint64_t g = p.rec_sorted[j] >> p.ibits;
-    if (g >= p.n_rules || (j > 0 && (p.rec_sorted[j - 1] >> p.ibits) == g)) return 0;
+    const uint64_t g = p.rec_sorted[j] >> p.gshift;
+    if (g >= p.n_rules || (j > 0 && (p.rec_sorted[j - 1] >> p.gshift) == g)) return 0;
     const uint64_t e = j + (uint64_t)p.short_max;  // segments are contiguous: one probe decides the length class
-    return e < p.n && (p.rec_sorted[e] >> p.ibits) == g ? 2 : 1;
+    return e < p.n && (p.rec_sorted[e] >> p.gshift) == g ? 2 : 1;
 }
 
 // Segment heads by length class: rules with more than short_max requests go to the wave walker's list,
@@ -170,18 +221,19 @@ __global__ void __launch_bounds__(256) k_pace_seg(PaceArgs p, uint64_t chunk) {
 
 __global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
     if (*p.err) return;
+    pc_stage_ms(p);
     const uint32_t cnt = p.long_count[1];
     for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < cnt; w += gridDim.x * blockDim.x) {
         const uint64_t j = p.short_list[w];
-        const uint64_t g = p.rec_sorted[j] >> p.ibits;
+        const uint64_t g = p.rec_sorted[j] >> p.gshift;
         const PaceRule r = p.rules[g];
+        if (!(r.count > 0.0)) continue;  // count <= 0 (:53-55): every request stays blocked
         int64_t latest = p.latest[g];
         for (uint64_t k = j; k < p.n; ++k) {
             const uint64_t rec = p.rec_sorted[k];
-            if ((rec >> p.ibits) != g) break;
+            if ((rec >> p.gshift) != g) break;
             const uint32_t idx = (uint32_t)(rec & p.imask);
-            const sg_pace_req q = p.req[idx];
-            const int32_t w8 = pace_step(latest, pace_cost(r.count, q.acquire), r.max_queueing_ms, q.ts_ms);
+            const int32_t w8 = pace_step(latest, pace_cost(r.count, pc_acq(p, rec, idx)), r.max_queueing_ms, pc_ts(p, idx));
             if (w8 != SG_PACE_BLOCKED) p.out[idx] = w8;
         }
         p.latest[g] = latest;
@@ -190,18 +242,20 @@ __global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
 
 __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
     if (*p.err) return;
+    pc_stage_ms(p);
     const uint32_t cnt = *p.long_count;
     const uint32_t wave = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint32_t nwaves = gridDim.x * (blockDim.x / 64);
     const int lane = (int)__lane_id();
     for (uint32_t w = wave; w < cnt; w += nwaves) {
         const uint64_t s = p.long_list[w];
-        const uint64_t g = p.rec_sorted[s] >> p.ibits;
+        const uint64_t g = p.rec_sorted[s] >> p.gshift;
+        const PaceRule r = p.rules[g];
+        if (!(r.count > 0.0)) continue;  // count <= 0 (:53-55): every request stays blocked
         // segment end: first record of another rule (records are sorted by rule)
         const uint64_t e = gallop_search(s + (p.short_max ? p.short_max : 1), p.n, [&](uint64_t q) {
-            return (p.rec_sorted[q] >> p.ibits) != g;
+            return (p.rec_sorted[q] >> p.gshift) != g;
         }, lane);
-        const PaceRule r = p.rules[g];
         int64_t latest = p.latest[g];
         // Every walked request has acquireCount >= 1 (k_pace_prep decides the rest), so its cost is at
         // least cost(1) and it can only pass at t >= latest + cost(1) - max(maxQ, 0): requests before that
@@ -212,7 +266,7 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
         const int64_t cost1 = pace_cost(r.count, 1);
         const int64_t cost_max = pace_cost(r.count, INT32_MAX);
         const int64_t slack = r.max_queueing_ms > 0 ? (int64_t)r.max_queueing_ms : 0;
-        auto ts_at = [&](uint64_t q) { return p.req[(uint32_t)(p.rec_sorted[q] & p.imask)].ts_ms; };
+        auto ts_at = [&](uint64_t q) { return pc_ts(p, (uint32_t)(p.rec_sorted[q] & p.imask)); };
         uint64_t base = s;
         while (base < e) {
             int64_t horizon, top;
@@ -228,10 +282,10 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
             uint32_t idx = 0;
             int64_t t = 0, cost = 0;
             if (act) {
-                idx = (uint32_t)(p.rec_sorted[j] & p.imask);
-                const sg_pace_req q = p.req[idx];
-                t = q.ts_ms;
-                cost = pace_cost(r.count, q.acquire);
+                const uint64_t rec = p.rec_sorted[j];
+                idx = (uint32_t)(rec & p.imask);
+                t = pc_ts(p, idx);
+                cost = pace_cost(r.count, pc_acq(p, rec, idx));
             }
             uint64_t pending = __ballot(act);
             while (pending) {
