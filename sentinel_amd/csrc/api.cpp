@@ -127,6 +127,7 @@ struct sg_handle {
     uint64_t cp_class_off[kClasses]{};
     uint32_t* d_p_msb = nullptr;      // hot-parameter batch: first request index of each millisecond
     int64_t* d_p_mt = nullptr;        // its first timestamp, then the millisecond count (uint32)
+    uint16_t* d_p_mbk = nullptr;      // pace: the millisecond of every kPcBuckets-th request
     std::vector<int32_t> cp_wls;      // distinct window lengths of the cluster param rules (CPRule::wl_idx)
     uint32_t* d_cp_bnd = nullptr;     // [kMaxWl][kMaxPeriods] the batch's period tables (request index -> period)
     int64_t* d_cp_p0 = nullptr;
@@ -702,6 +703,7 @@ void sg_destroy(sg_handle* h) {
     dfree(h->d_cp_slot_item);
     dfree(h->d_p_msb);
     dfree(h->d_p_mt);
+    dfree(h->d_p_mbk);
     dfree(h->d_cp_bnd);
     dfree(h->d_cp_p0);
     dfree(h->d_cp_np);
@@ -2295,6 +2297,11 @@ int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32
     p.msb = h->d_p_msb;
     p.mt0 = h->d_p_mt;
     p.mnp = reinterpret_cast<uint32_t*>(h->d_p_mt + 1);
+    if (!h->d_p_mbk && hipMalloc(&h->d_p_mbk, sizeof(uint16_t) * kPcBuckets) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "pace millisecond buckets");
+    p.mbk = h->d_p_mbk;
+    p.bshift = 0;
+    while ((((uint64_t)n - 1) >> p.bshift) >= kPcBuckets) ++p.bshift;
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
     HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, 2 * sizeof(uint32_t), stream));
     uint64_t* sorted = nullptr;

@@ -305,6 +305,8 @@ struct PaceRule {
     int32_t pad;
 };
 
+constexpr uint32_t kPcBuckets = 2048;  // pace: request buckets of the index → millisecond lookup
+
 struct PaceArgs {
     const sg_pace_req* req;
     int32_t* out;           // wait ms or SG_PACE_BLOCKED
@@ -326,6 +328,8 @@ struct PaceArgs {
     uint32_t* msb;          // the millisecond table: first request index of every millisecond of the batch
     int64_t* mt0;           // [0] the batch's first timestamp, then {millisecond count, zero word}
     uint32_t* mnp;
+    uint16_t* mbk;          // [n >> bshift buckets] millisecond (from the first) of request bucket << bshift
+    int bshift;
 };
 
 // The long-rule walker runs on `aux` beside the short one (fork / join events).

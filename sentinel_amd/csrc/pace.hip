@@ -87,6 +87,54 @@ __device__ __forceinline__ uint64_t pace_wave_search(uint64_t lo, uint64_t hi, P
     return m ? lo + (uint64_t)__builtin_ctzll(m) : hi;
 }
 
+// A window start for the wave walker: some q <= a with a - q < 64, a = the first q in [lo, hi) with pred(q)
+// (monotone), hi if none. The walker's step takes 64 requests from q, and those before a are blocked anyway, so the
+// search stops as soon as the bracket is 64 wide and its last round doubles as the step's load. One round of 64
+// probes g + (lane - 32) w (clamped to [lo, hi - 1]) around a guess g brackets a; a guess that misses falls back to
+// a gallop past the last probe or a 64-way search before the first.
+template <class Pred>
+__device__ __forceinline__ uint64_t pace_window(uint64_t lo, uint64_t hi, Pred pred, int lane) {
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t q = lo + (uint64_t)lane * step;
+        const uint64_t m = __ballot(q >= hi || pred(q));
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+            continue;
+        }
+        const int f = __builtin_ctzll(m);
+        if (f == 0) return lo;
+        const uint64_t nhi = lo + (uint64_t)f * step;
+        lo = lo + (uint64_t)(f - 1) * step + 1;
+        hi = nhi < hi ? nhi : hi;
+    }
+    return lo;
+}
+
+template <class Pred>
+__device__ __forceinline__ uint64_t pace_guess_window(uint64_t lo, uint64_t hi, uint64_t g, uint64_t w, Pred pred,
+                                                      int lane) {
+    if (lo >= hi) return hi;
+    const int64_t pq = (int64_t)g + ((int64_t)lane - 32) * (int64_t)w;
+    const uint64_t q = pq < (int64_t)lo ? lo : (pq >= (int64_t)hi ? hi - 1 : (uint64_t)pq);
+    const uint64_t m = __ballot(pred(q));
+    if (m == 0) {  // a > every probe: bracket it by doubling steps past the last one
+        const uint64_t l2 = (uint64_t)__shfl((long long)q, 63, 64) + 1;
+        if (l2 >= hi) return hi;
+        const uint64_t span = hi - l2;
+        const uint64_t off = lane < 63 ? (1ull << lane) - 1ull : ~0ull;
+        const uint64_t m2 = __ballot(off >= span || pred(l2 + off));
+        const int f2 = __builtin_ctzll(m2);
+        if (f2 == 0) return l2;
+        const uint64_t b1 = l2 + ((1ull << f2) - 1ull);
+        return pace_window(l2 + (1ull << (f2 - 1)), b1 < hi ? b1 + 1 : hi, pred, lane);
+    }
+    const int f = __builtin_ctzll(m);
+    const uint64_t qf = (uint64_t)__shfl((long long)q, f, 64);
+    const uint64_t qp = f == 0 ? lo : (uint64_t)__shfl((long long)q, f - 1, 64) + 1;
+    return pace_window(qp, qf + 1, pred, lane);
+}
+
 }  // namespace
 
 // Validation and the records. A request reads nothing but itself: its acquireCount rides in the record (8-bit code,
@@ -113,6 +161,7 @@ __global__ void __launch_bounds__(256) k_pace_prep(PaceArgs p) {
             }
         }
         if (i == p.n - 1) *p.mnp = (uint32_t)min(q.ts_ms - t0 + 1, (int64_t)kMaxPeriods + 1);
+        if ((i & ((1ull << p.bshift) - 1ull)) == 0) p.mbk[i >> p.bshift] = (uint16_t)min(max(q.ts_ms - t0, (int64_t)0), (int64_t)65535);
         uint64_t rec = none;
         int32_t out = SG_PACE_BLOCKED;  // a walked request passes by its walker; count <= 0 leaves it blocked
         if (q.rule >= p.n_rules || q.acquire <= 0) {
@@ -127,24 +176,33 @@ __global__ void __launch_bounds__(256) k_pace_prep(PaceArgs p) {
 }
 
 __shared__ uint32_t pc_sms[kPcLdsMs];
+__shared__ uint16_t pc_sbk[kPcBuckets];  // the millisecond of request b << bshift
 __shared__ uint32_t pc_nms;  // table entries in LDS, 0: read the timestamps
+__shared__ uint32_t pc_nbk;
 __shared__ int64_t pc_t0;
 
 __device__ __forceinline__ void pc_stage_ms(const PaceArgs& p) {
     const uint32_t np = *p.mnp;
     const bool lds = np <= kPcLdsMs;
+    const uint32_t nb = (uint32_t)((p.n - 1) >> p.bshift) + 1;
     for (uint32_t x = threadIdx.x; lds && x < np; x += blockDim.x) pc_sms[x] = p.msb[x];
+    for (uint32_t x = threadIdx.x; lds && x < nb; x += blockDim.x) pc_sbk[x] = p.mbk[x];
     if (threadIdx.x == 0) {
         pc_nms = lds ? np : 0u;
+        pc_nbk = nb;
         pc_t0 = *p.mt0;
     }
     __syncthreads();
 }
 
+// A request's timestamp: the largest millisecond q whose first request index table[q] <= idx. Its bucket's first
+// request and the next bucket's bound q to a few milliseconds (a bucket of a 16M batch holds 8192 requests), so the
+// binary search takes a step or two instead of twelve.
 __device__ __forceinline__ int64_t pc_ts(const PaceArgs& p, uint32_t idx) {
     const uint32_t np = pc_nms;
     if (np == 0) return p.req[idx].ts_ms;
-    uint32_t lo = 0, hi = np;  // the largest q with table[q] <= idx (entry 0 unused)
+    const uint32_t b = idx >> p.bshift;
+    uint32_t lo = pc_sbk[b], hi = b + 1 < pc_nbk ? (uint32_t)pc_sbk[b + 1] + 1u : np;  // table[lo] <= idx (entry 0 unused)
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (pc_sms[mid] <= idx) lo = mid;
@@ -167,55 +225,55 @@ __device__ __forceinline__ int pace_head_class(const PaceArgs& p, uint64_t j) {
 }
 
 // Segment heads by length class: rules with more than short_max requests go to the wave walker's list,
-// the rest to the lane walker's. Each block owns a contiguous chunk: it counts its heads, reserves its
-// slice of each list with one global atomic per list, then writes the heads in order.
+// the rest to the lane walker's. Each block owns a contiguous chunk: one pass classifies its records (the classes
+// kept in registers, 2 bits a round for the first 32 rounds) and counts each wave's heads, one global atomic per list
+// reserves the block's slice, and each wave then writes its heads into its own part of the slice — no block barrier
+// per round and no second read of the records.
 __global__ void __launch_bounds__(256) k_pace_seg(PaceArgs p, uint64_t chunk) {
     if (*p.err) return;
-    __shared__ uint32_t tot[2], wcnt[4][2], base[2];
+    __shared__ uint32_t wtot[4][2], base[2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < p.n ? lo + chunk : p.n;
-    if (tid < 2) tot[tid] = 0;
-    __syncthreads();
-    uint32_t cs = 0, cl = 0;
-    for (uint64_t j = lo + tid; j < hi; j += 256) {
+    uint64_t cls = 0;
+    int cs = 0, cl = 0, r = 0;
+    for (uint64_t j = lo + tid; j < hi; j += 256, ++r) {
         const int c = pace_head_class(p, j);
+        if (r < 32) cls |= (uint64_t)c << (2 * r);
         cs += c == 1;
         cl += c == 2;
     }
-    if (cs) atomicAdd(&tot[0], cs);
-    if (cl) atomicAdd(&tot[1], cl);
-    __syncthreads();
-    if (tid == 0) {
-        base[0] = tot[0] ? atomicAdd(&p.long_count[1], tot[0]) : 0;
-        base[1] = tot[1] ? atomicAdd(&p.long_count[0], tot[1]) : 0;
+    for (int o = 32; o > 0; o >>= 1) {
+        cs += __shfl_xor(cs, o, 64);
+        cl += __shfl_xor(cl, o, 64);
+    }
+    if (lane == 0) {
+        wtot[wv][0] = (uint32_t)cs;
+        wtot[wv][1] = (uint32_t)cl;
     }
     __syncthreads();
+    if (tid == 0) {
+        const uint32_t ts = wtot[0][0] + wtot[1][0] + wtot[2][0] + wtot[3][0];
+        const uint32_t tl = wtot[0][1] + wtot[1][1] + wtot[2][1] + wtot[3][1];
+        base[0] = ts ? atomicAdd(&p.long_count[1], ts) : 0;
+        base[1] = tl ? atomicAdd(&p.long_count[0], tl) : 0;
+    }
+    __syncthreads();
+    uint32_t os = base[0], ol = base[1];
+    for (int w = 0; w < wv; ++w) {
+        os += wtot[w][0];
+        ol += wtot[w][1];
+    }
     const uint64_t below = (1ull << lane) - 1ull;
-    for (uint64_t r = lo; r < hi; r += 256) {
-        const uint64_t j = r + tid;
-        const int c = j < hi ? pace_head_class(p, j) : 0;
+    r = 0;
+    for (uint64_t rr = lo; rr < hi; rr += 256, ++r) {
+        const uint64_t j = rr + tid;
+        const int c = j >= hi ? 0 : r < 32 ? (int)((cls >> (2 * r)) & 3ull) : pace_head_class(p, j);
         const uint64_t sm = __ballot(c == 1), lm = __ballot(c == 2);
-        if (lane == 0) {
-            wcnt[wv][0] = (uint32_t)__popcll(sm);
-            wcnt[wv][1] = (uint32_t)__popcll(lm);
-        }
-        __syncthreads();
-        uint32_t os = base[0], ol = base[1];
-        for (int w = 0; w < wv; ++w) {
-            os += wcnt[w][0];
-            ol += wcnt[w][1];
-        }
         if (c == 1) p.short_list[os + __popcll(sm & below)] = (uint32_t)j;
         if (c == 2) p.long_list[ol + __popcll(lm & below)] = (uint32_t)j;
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 0; w < 4; ++w) {
-                base[0] += wcnt[w][0];
-                base[1] += wcnt[w][1];
-            }
-        }
-        __syncthreads();
+        os += (uint32_t)__popcll(sm);
+        ol += (uint32_t)__popcll(lm);
     }
 }
 
@@ -267,15 +325,37 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
         const int64_t cost_max = pace_cost(r.count, INT32_MAX);
         const int64_t slack = r.max_queueing_ms > 0 ? (int64_t)r.max_queueing_ms : 0;
         auto ts_at = [&](uint64_t q) { return pc_ts(p, (uint32_t)(p.rec_sorted[q] & p.imask)); };
+        // With the millisecond table in LDS the horizon becomes a request index (the first request of its
+        // millisecond) and the search compares record indices, no timestamp lookups. Its first probes are
+        // guessed: the rule's requests are spread over the batch at density (e - s) / (index span), so the
+        // answer lies about (index distance) x density past the last admitted request, within a few sqrt of it.
+        const bool tab = pc_nms != 0;
+        uint64_t hq = s;
+        uint32_t hidx = (uint32_t)(p.rec_sorted[s] & p.imask);
+        const double dens = (double)(e - s) / ((double)(uint32_t)(p.rec_sorted[e - 1] & p.imask) - (double)hidx + 1.0);
+        bool seek = true;  // latestPassedTime moved since the last search
         uint64_t base = s;
         while (base < e) {
             int64_t horizon, top;
-            if (!__builtin_add_overflow(latest, cost_max, &top) && !__builtin_add_overflow(latest, cost1, &horizon)) {
+            if (seek && !__builtin_add_overflow(latest, cost_max, &top) && !__builtin_add_overflow(latest, cost1, &horizon)) {
                 horizon -= slack;
-                if (ts_at(base) < horizon) {
+                seek = false;
+                if (tab) {
+                    const int64_t x = horizon - pc_t0;
+                    if (x >= (int64_t)pc_nms) break;  // past the batch's last millisecond: the rest is blocked
+                    if (x >= 1) {
+                        const uint32_t ih = pc_sms[x];
+                        const double d = ((double)ih - (double)hidx) * dens;
+                        const uint64_t gq = hq + (d > 0.0 ? (uint64_t)d : 0ull);
+                        const uint64_t w = (uint64_t)(sqrt(d > 0.0 ? d : 0.0) * 0.125) + 1ull;
+                        base = pace_guess_window(base, e, gq < base ? base : gq, w, [&](uint64_t q) {
+                            return (uint32_t)(p.rec_sorted[q] & p.imask) >= ih;
+                        }, lane);
+                    }
+                } else if (ts_at(base) < horizon) {
                     base = gallop_search(base, e, [&](uint64_t q) { return ts_at(q) >= horizon; }, lane);
-                    continue;
                 }
+                continue;
             }
             const uint64_t j = base + (uint64_t)lane;
             const bool act = j < e;
@@ -288,6 +368,7 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
                 cost = pace_cost(r.count, pc_acq(p, rec, idx));
             }
             uint64_t pending = __ballot(act);
+            int lastf = -1;
             while (pending) {
                 const int64_t expected = wrap_add(latest, cost);
                 const bool ok = ((pending >> lane) & 1ull) && (expected <= t || expected - t <= (int64_t)r.max_queueing_ms);
@@ -299,6 +380,12 @@ __global__ void __launch_bounds__(256) k_pace_long(PaceArgs p) {
                 if (lane == f) p.out[idx] = ef <= tf ? 0 : (int32_t)(ef - tf);
                 latest = ef <= tf ? tf : ef;
                 pending &= ~((2ull << f) - 1ull);
+                lastf = f;
+            }
+            if (lastf >= 0) {
+                seek = true;
+                hq = base + (uint64_t)lastf;
+                hidx = (uint32_t)__shfl((int)idx, lastf, 64);
             }
             base += 64;
         }

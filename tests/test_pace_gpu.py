@@ -128,3 +128,32 @@ def test_pace_saturated_cost_wraps(flags):
         w = _check(eng, ora, req, 2)
         assert (w[req["acquire"] > 1] == 0).any() and (w[req["acquire"] == 1] == abi.PACE_BLOCKED).any()
         t = int(req["ts_ms"][-1])
+
+
+@pytest.mark.parametrize("span", [1000, 6000])
+def test_pace_bursty_rules_guess_misses(span):
+    """The wave walker guesses where its next admissible request lies from the rule's average density over the
+    batch; bursty rules (requests packed into a few short windows, idle elsewhere) make the guess land before and
+    after the answer. A batch spanning 6 s has no millisecond table in LDS and searches by timestamp instead."""
+    rng = np.random.default_rng(21 + span)
+    n, n_rules = 200_000, 8
+    rules = np.zeros(n_rules, abi.PACE_RULE_DTYPE)
+    rules["count"] = [50.0, 7.0, 300.0, 1.5, 64.0, 20.0, 1000.0, 3.0]
+    rules["max_queueing_ms"] = [500, 0, 100, 2000, 500, -5, 20, 500]
+    eng = _engine(abi.FLAG_WAVE_ONLY)
+    eng.pace_load_rules(rules)
+    ora = RateLimiterController(rules)
+    t = 1_700_000_000_000
+    for _ in range(3):
+        ts = np.sort(rng.integers(0, span, n))
+        rule = rng.integers(0, n_rules, n)
+        burst = (ts % 400) < 40                         # rule 0-3 live only in the first 40 ms of every 400
+        rule[burst] = rng.integers(0, 4, burst.sum())
+        rule[~burst] = rng.integers(4, n_rules, (~burst).sum())
+        req = np.zeros(n, abi.PACE_REQ_DTYPE)
+        req["ts_ms"] = t + ts
+        req["rule"] = rule
+        req["acquire"] = np.where(rng.random(n) < 0.1, rng.integers(2, 300, n), 1)
+        w = _check(eng, ora, req, n_rules)
+        assert (w == abi.PACE_BLOCKED).any() and (w > 0).any() and (w == 0).any()
+        t = int(req["ts_ms"][-1]) + int(rng.integers(0, 3000))
