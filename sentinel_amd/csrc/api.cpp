@@ -2147,6 +2147,11 @@ int sg_param_decide_batch(sg_handle* h, const sg_param_req* req, uint64_t n, int
     p.msb = h->d_p_msb;
     p.mt0 = h->d_p_mt;
     p.mnp = reinterpret_cast<uint32_t*>(h->d_p_mt + 1);
+    if (!h->d_p_mbk && hipMalloc(&h->d_p_mbk, sizeof(uint16_t) * kPcBuckets) != hipSuccess)
+        return fail(h, SG_E_NOMEM, "param millisecond buckets");
+    p.mbk = h->d_p_mbk;
+    p.bshift = 0;
+    while ((((uint64_t)n - 1) >> p.bshift) >= kPcBuckets) ++p.bshift;
     BatchArgs sg{};  // k_seg's lists in the main workspace; its error word: a zero word (the param flags are no errors)
     sg.err = reinterpret_cast<int*>(h->d_p_mt) + 3;
     sg.short_list = h->d_short_list;

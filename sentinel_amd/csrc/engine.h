@@ -258,6 +258,8 @@ struct alignas(32) PSlot {  // one (rule, value): timeCounters / tokenCounters e
     int64_t tokens;
 };
 
+constexpr uint32_t kPcBuckets = 2048;  // request buckets of the index → millisecond lookup (pace, hot params)
+
 struct PArgs {
     const sg_param_req* req;
     int32_t* out;
@@ -271,6 +273,8 @@ struct PArgs {
     uint32_t* msb;          // [kMaxPeriods] first request index of each millisecond of the batch (entry 0 unused)
     int64_t* mt0;           // the batch's first timestamp
     uint32_t* mnp;          // milliseconds the batch spans (> kMaxPeriods: the walkers read the timestamps)
+    uint16_t* mbk;          // [n >> bshift buckets] millisecond (from the first) of request bucket << bshift
+    int bshift;
     const PRule* rules;
     uint32_t n_rules;
     const sg_param_hot_item* hot;  // per rule, sorted by value
@@ -304,8 +308,6 @@ struct PaceRule {
     int32_t max_queueing_ms;
     int32_t pad;
 };
-
-constexpr uint32_t kPcBuckets = 2048;  // pace: request buckets of the index → millisecond lookup
 
 struct PaceArgs {
     const sg_pace_req* req;

@@ -36,6 +36,7 @@ __global__ void __launch_bounds__(256) k_pprep(PArgs p, uint64_t sentinel) {
             }
         }
         if (i == p.n - 1) *p.mnp = (uint32_t)min(q.ts_ms - t0 + 1, (int64_t)kMaxPeriods + 1);
+        if ((i & ((1ull << p.bshift) - 1ull)) == 0) p.mbk[i >> p.bshift] = (uint16_t)min(max(q.ts_ms - t0, (int64_t)0), (int64_t)65535);
         if (q.acquire <= 0) atomicOr(p.err, kErrNonPositive);
         uint64_t rec = sentinel;
         int32_t pass = 0;
@@ -70,24 +71,32 @@ __device__ __forceinline__ uint32_t rule_of_slot(const PArgs& p, uint64_t g) {
 // The millisecond table in LDS (the hot-parameter walkers): request index -> exact timestamp (requests are
 // time-ordered), so a walker reads nothing per request but its sorted record.
 __shared__ uint32_t p_sms[kPLdsMs];
+__shared__ uint16_t p_sbk[kPcBuckets];  // the millisecond of request b << bshift
 __shared__ uint32_t p_nms;   // table entries, 0: read the timestamps
+__shared__ uint32_t p_nbk;
 __shared__ int64_t p_t0;
 
 __device__ __forceinline__ void p_stage_ms(const PArgs& p) {
     const uint32_t np = *p.mnp;
     const bool lds = np <= kPLdsMs;
+    const uint32_t nb = (uint32_t)((p.n - 1) >> p.bshift) + 1;
     for (uint32_t x = threadIdx.x; lds && x < np; x += blockDim.x) p_sms[x] = p.msb[x];
+    for (uint32_t x = threadIdx.x; lds && x < nb; x += blockDim.x) p_sbk[x] = p.mbk[x];
     if (threadIdx.x == 0) {
         p_nms = lds ? np : 0u;
+        p_nbk = nb;
         p_t0 = *p.mt0;
     }
     __syncthreads();
 }
 
+// The request's bucket bounds its millisecond to [first request's, next bucket's first request's]: a step or two
+// of binary search instead of twelve (as pace.hip's pc_ts).
 __device__ __forceinline__ int64_t p_ts(const PArgs& p, uint32_t idx) {
     const uint32_t np = p_nms;
     if (np == 0) return p.req[idx].ts_ms;
-    uint32_t lo = 0, hi = np;  // the largest q with table[q] <= idx (entry 0 unused)
+    const uint32_t b = idx >> p.bshift;
+    uint32_t lo = p_sbk[b], hi = b + 1 < p_nbk ? (uint32_t)p_sbk[b + 1] + 1u : np;  // table[lo] <= idx (entry 0 unused)
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (p_sms[mid] <= idx) lo = mid;
