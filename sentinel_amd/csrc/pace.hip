@@ -287,11 +287,12 @@ __global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
         const PaceRule r = p.rules[g];
         if (!(r.count > 0.0)) continue;  // count <= 0 (:53-55): every request stays blocked
         int64_t latest = p.latest[g];
-        for (uint64_t k = j; k < p.n; ++k) {
-            const uint64_t rec = p.rec_sorted[k];
-            if ((rec >> p.gshift) != g) break;
-            const uint32_t idx = (uint32_t)(rec & p.imask);
-            const int32_t w8 = pace_step(latest, pace_cost(r.count, pc_acq(p, rec, idx)), r.max_queueing_ms, pc_ts(p, idx));
+        uint64_t rec = p.rec_sorted[j];
+        for (uint64_t k = j; (rec >> p.gshift) == g;) {  // the next record is loaded before this one is decided
+            const uint64_t cur = rec;
+            rec = ++k < p.n ? p.rec_sorted[k] : ~0ull;
+            const uint32_t idx = (uint32_t)(cur & p.imask);
+            const int32_t w8 = pace_step(latest, pace_cost(r.count, pc_acq(p, cur, idx)), r.max_queueing_ms, pc_ts(p, idx));
             if (w8 != SG_PACE_BLOCKED) p.out[idx] = w8;
         }
         p.latest[g] = latest;
