@@ -2308,7 +2308,8 @@ int sg_pace_decide_batch(sg_handle* h, const sg_pace_req* req, uint64_t n, int32
     p.bshift = 0;
     while ((((uint64_t)n - 1) >> p.bshift) >= kPcBuckets) ++p.bshift;
     HIP_TRY(h, hipMemsetAsync(h->d_err, 0, sizeof(int), stream));
-    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, 2 * sizeof(uint32_t), stream));
+    for (int c = 0; c < kClasses; ++c) p.class_off[c] = h->class_off[c];
+    HIP_TRY(h, hipMemsetAsync(h->d_long_count, 0, (1 + kClasses) * sizeof(uint32_t), stream));
     uint64_t* sorted = nullptr;
     HIP_TRY(h, launch_pace_batch(p, h->d_rec, h->d_rec_sorted, h->d_hist, p.gshift, p.gshift + gbits, &sorted, stream,
                                  h->aux, h->fork, h->join));

@@ -323,7 +323,7 @@ struct PaceArgs {
     int* err;
     int64_t* last_ts;
     uint32_t* long_list;
-    uint32_t* long_count;   // [0] long segments, [1] short segments
+    uint32_t* long_count;   // [0] long segments, [1 + c] short segments of length class c
     uint32_t* short_list;
     uint32_t short_max;
     int gshift;             // records {rule : high bits | acquire code : 8 | request index : ibits}: rule at gshift
@@ -332,6 +332,7 @@ struct PaceArgs {
     uint32_t* mnp;
     uint16_t* mbk;          // [n >> bshift buckets] millisecond (from the first) of request bucket << bshift
     int bshift;
+    uint64_t class_off[kClasses];  // the lane walker's length classes in short_list (counts at long_count[1 + c])
 };
 
 // The long-rule walker runs on `aux` beside the short one (fork / join events).

@@ -216,73 +216,99 @@ __device__ __forceinline__ int32_t pc_acq(const PaceArgs& p, uint64_t rec, uint3
     return ac == kPcAesc ? p.req[idx].acquire : (int32_t)ac;
 }
 
-// 0 = not a segment head, 1 = head of a rule walked by one lane, 2 = head of a rule walked by a wave
+// Segment head classes: 0 = not a head; 1 + c = a rule walked by one lane, in length class c (longer than
+// kClassMax[c - 1], at most kClassMax[c] requests, class kClasses - 1 unbounded); kPcLong = a rule with more than
+// short_max requests, walked by a wave. Segments are contiguous, so one probe per bound decides the length.
+constexpr int kPcLong = kClasses + 1;
+constexpr int kPcLists = kClasses + 1;  // list l < kClasses: lane-walker class l; kClasses: the wave walker's
+
 __device__ __forceinline__ int pace_head_class(const PaceArgs& p, uint64_t j) {
     const uint64_t g = p.rec_sorted[j] >> p.gshift;
     if (g >= p.n_rules || (j > 0 && (p.rec_sorted[j - 1] >> p.gshift) == g)) return 0;
-    const uint64_t e = j + (uint64_t)p.short_max;  // segments are contiguous: one probe decides the length class
-    return e < p.n && (p.rec_sorted[e] >> p.gshift) == g ? 2 : 1;
+    auto longer = [&](uint64_t m) {  // the segment holds more than m requests
+        const uint64_t e = j + m;
+        return e < p.n && (p.rec_sorted[e] >> p.gshift) == g;
+    };
+    if (longer((uint64_t)p.short_max)) return kPcLong;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kClasses - 1; ++k) c += (kClassMax[k] < p.short_max && longer(kClassMax[k])) ? 1 : 0;
+    return 1 + c;
 }
 
-// Segment heads by length class: rules with more than short_max requests go to the wave walker's list,
-// the rest to the lane walker's. Each block owns a contiguous chunk: one pass classifies its records (the classes
-// kept in registers, 2 bits a round for the first 32 rounds) and counts each wave's heads, one global atomic per list
-// reserves the block's slice, and each wave then writes its heads into its own part of the slice — no block barrier
-// per round and no second read of the records.
+// Segment heads by class: the wave walker's list and the lane walker's length classes (a lane walker wave then
+// holds rules of similar length: its time is its longest lane's). Each block owns a contiguous chunk: one pass
+// classifies its records (classes kept in registers, 3 bits a round for the first 42 rounds) and counts each wave's
+// heads per list, one global atomic per list reserves the block's slices, and each wave writes its heads into its
+// own part of them — no block barrier per round and no second read of the records.
 __global__ void __launch_bounds__(256) k_pace_seg(PaceArgs p, uint64_t chunk) {
     if (*p.err) return;
-    __shared__ uint32_t wtot[4][2], base[2];
+    __shared__ uint32_t wtot[4][kPcLists], base[kPcLists];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < p.n ? lo + chunk : p.n;
-    uint64_t cls = 0;
-    int cs = 0, cl = 0, r = 0;
+    uint64_t cls[2] = {0, 0};
+    int cnt[kPcLists];
+#pragma unroll
+    for (int l = 0; l < kPcLists; ++l) cnt[l] = 0;
+    int r = 0;
     for (uint64_t j = lo + tid; j < hi; j += 256, ++r) {
         const int c = pace_head_class(p, j);
-        if (r < 32) cls |= (uint64_t)c << (2 * r);
-        cs += c == 1;
-        cl += c == 2;
+        if (r < 42) cls[r / 21] |= (uint64_t)c << (3 * (r % 21));
+#pragma unroll
+        for (int l = 0; l < kPcLists; ++l) cnt[l] += c == (l < kClasses ? 1 + l : kPcLong);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        cs += __shfl_xor(cs, o, 64);
-        cl += __shfl_xor(cl, o, 64);
-    }
-    if (lane == 0) {
-        wtot[wv][0] = (uint32_t)cs;
-        wtot[wv][1] = (uint32_t)cl;
+#pragma unroll
+    for (int l = 0; l < kPcLists; ++l) {
+        for (int o = 32; o > 0; o >>= 1) cnt[l] += __shfl_xor(cnt[l], o, 64);
+        if (lane == 0) wtot[wv][l] = (uint32_t)cnt[l];
     }
     __syncthreads();
-    if (tid == 0) {
-        const uint32_t ts = wtot[0][0] + wtot[1][0] + wtot[2][0] + wtot[3][0];
-        const uint32_t tl = wtot[0][1] + wtot[1][1] + wtot[2][1] + wtot[3][1];
-        base[0] = ts ? atomicAdd(&p.long_count[1], ts) : 0;
-        base[1] = tl ? atomicAdd(&p.long_count[0], tl) : 0;
+    if (tid < kPcLists) {
+        const uint32_t t = wtot[0][tid] + wtot[1][tid] + wtot[2][tid] + wtot[3][tid];
+        base[tid] = t ? atomicAdd(&p.long_count[tid < kClasses ? 1 + tid : 0], t) : 0;
     }
     __syncthreads();
-    uint32_t os = base[0], ol = base[1];
-    for (int w = 0; w < wv; ++w) {
-        os += wtot[w][0];
-        ol += wtot[w][1];
+    uint32_t off[kPcLists];
+#pragma unroll
+    for (int l = 0; l < kPcLists; ++l) {
+        off[l] = base[l];
+        for (int w = 0; w < wv; ++w) off[l] += wtot[w][l];
     }
     const uint64_t below = (1ull << lane) - 1ull;
     r = 0;
     for (uint64_t rr = lo; rr < hi; rr += 256, ++r) {
         const uint64_t j = rr + tid;
-        const int c = j >= hi ? 0 : r < 32 ? (int)((cls >> (2 * r)) & 3ull) : pace_head_class(p, j);
-        const uint64_t sm = __ballot(c == 1), lm = __ballot(c == 2);
-        if (c == 1) p.short_list[os + __popcll(sm & below)] = (uint32_t)j;
-        if (c == 2) p.long_list[ol + __popcll(lm & below)] = (uint32_t)j;
-        os += (uint32_t)__popcll(sm);
-        ol += (uint32_t)__popcll(lm);
+        const int c = j >= hi ? 0 : r < 42 ? (int)((cls[r / 21] >> (3 * (r % 21))) & 7ull) : pace_head_class(p, j);
+#pragma unroll
+        for (int l = 0; l < kPcLists; ++l) {
+            const bool mine = c == (l < kClasses ? 1 + l : kPcLong);
+            const uint64_t m = __ballot(mine);
+            if (mine) {
+                const uint32_t pos = off[l] + (uint32_t)__popcll(m & below);
+                if (l < kClasses) p.short_list[p.class_off[l] + pos] = (uint32_t)j;
+                else p.long_list[pos] = (uint32_t)j;
+            }
+            off[l] += (uint32_t)__popcll(m);
+        }
     }
 }
 
+// One lane per rule of at most short_max requests, the longest length class first.
 __global__ void __launch_bounds__(256) k_pace_short(PaceArgs p) {
     if (*p.err) return;
     pc_stage_ms(p);
-    const uint32_t cnt = p.long_count[1];
-    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < cnt; w += gridDim.x * blockDim.x) {
-        const uint64_t j = p.short_list[w];
+    uint32_t cc[kClasses], total = 0;
+#pragma unroll
+    for (int c = 0; c < kClasses; ++c) {
+        cc[c] = p.long_count[1 + c];
+        total += cc[c];
+    }
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < total; w += gridDim.x * blockDim.x) {
+        uint32_t r0 = w;
+        int c = kClasses - 1;
+        while (c > 0 && r0 >= cc[c]) r0 -= cc[c--];
+        const uint64_t j = p.short_list[p.class_off[c] + r0];
         const uint64_t g = p.rec_sorted[j] >> p.gshift;
         const PaceRule r = p.rules[g];
         if (!(r.count > 0.0)) continue;  // count <= 0 (:53-55): every request stays blocked
