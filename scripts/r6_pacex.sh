@@ -1,5 +1,6 @@
 #!/bin/bash
 # Pace walker timing experiments (variants built with scripts/build_variant.sh; the skip ones give wrong results).
+# (The SG_PACE_SKIP_* / SG_PACE_LONG_GRID macros lived in a temporary build of pace.hip for these runs only.)
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 mkdir -p gpurun_out/r6
 export TMPDIR=/tmp
