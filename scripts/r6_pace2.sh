@@ -9,7 +9,7 @@ for r in 1 2; do
   timeout -k 10 200 python -u bench_configs.py --workload pace --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r6/pace2_new_$r.json 2>/dev/null || exit 1
   SG_LIB_PATH=build/ab/pacebase.so timeout -k 10 200 python -u bench_configs.py --workload pace --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r6/pace2_base_$r.json 2>/dev/null || exit 1
 done
-for sm in 64 256 512; do
+for sm in; do
   SG_PACE_SHORT_MAX=$sm timeout -k 10 200 python -u bench_configs.py --workload pace --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/r6/pace2_sm$sm.json 2>/dev/null || exit 1
 done
 grep -o '"ms_per_step": [0-9.]*' gpurun_out/r6/pace2_new_*.json gpurun_out/r6/pace2_base_*.json gpurun_out/r6/pace2_sm*.json

@@ -238,59 +238,40 @@ __device__ __forceinline__ int pace_head_class(const PaceArgs& p, uint64_t j) {
 
 // Segment heads by class: the wave walker's list and the lane walker's length classes (a lane walker wave then
 // holds rules of similar length: its time is its longest lane's). Each block owns a contiguous chunk: one pass
-// classifies its records (classes kept in registers, 3 bits a round for the first 42 rounds) and counts each wave's
-// heads per list, one global atomic per list reserves the block's slices, and each wave writes its heads into its
-// own part of them — no block barrier per round and no second read of the records.
+// classifies its records (classes kept in registers, 3 bits a round for the first 42 rounds) and counts its heads per
+// list with LDS atomics, one global atomic per list reserves the block's slices, and the second pass places each head
+// with an LDS atomic (the order within a list is free) — no second read of the records.
 __global__ void __launch_bounds__(256) k_pace_seg(PaceArgs p, uint64_t chunk) {
     if (*p.err) return;
-    __shared__ uint32_t wtot[4][kPcLists], base[kPcLists];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ uint32_t tot[kPcLists], base[kPcLists];
+    const int tid = threadIdx.x;
     const uint64_t lo = (uint64_t)blockIdx.x * chunk;
     const uint64_t hi = lo + chunk < p.n ? lo + chunk : p.n;
+    if (tid < kPcLists) tot[tid] = 0;
+    __syncthreads();
+    auto list_of = [](int c) { return c == kPcLong ? kClasses : c - 1; };
     uint64_t cls[2] = {0, 0};
-    int cnt[kPcLists];
-#pragma unroll
-    for (int l = 0; l < kPcLists; ++l) cnt[l] = 0;
     int r = 0;
     for (uint64_t j = lo + tid; j < hi; j += 256, ++r) {
         const int c = pace_head_class(p, j);
         if (r < 42) cls[r / 21] |= (uint64_t)c << (3 * (r % 21));
-#pragma unroll
-        for (int l = 0; l < kPcLists; ++l) cnt[l] += c == (l < kClasses ? 1 + l : kPcLong);
-    }
-#pragma unroll
-    for (int l = 0; l < kPcLists; ++l) {
-        for (int o = 32; o > 0; o >>= 1) cnt[l] += __shfl_xor(cnt[l], o, 64);
-        if (lane == 0) wtot[wv][l] = (uint32_t)cnt[l];
+        if (c) atomicAdd(&tot[list_of(c)], 1u);
     }
     __syncthreads();
     if (tid < kPcLists) {
-        const uint32_t t = wtot[0][tid] + wtot[1][tid] + wtot[2][tid] + wtot[3][tid];
+        const uint32_t t = tot[tid];
         base[tid] = t ? atomicAdd(&p.long_count[tid < kClasses ? 1 + tid : 0], t) : 0;
+        tot[tid] = 0;
     }
     __syncthreads();
-    uint32_t off[kPcLists];
-#pragma unroll
-    for (int l = 0; l < kPcLists; ++l) {
-        off[l] = base[l];
-        for (int w = 0; w < wv; ++w) off[l] += wtot[w][l];
-    }
-    const uint64_t below = (1ull << lane) - 1ull;
     r = 0;
-    for (uint64_t rr = lo; rr < hi; rr += 256, ++r) {
-        const uint64_t j = rr + tid;
-        const int c = j >= hi ? 0 : r < 42 ? (int)((cls[r / 21] >> (3 * (r % 21))) & 7ull) : pace_head_class(p, j);
-#pragma unroll
-        for (int l = 0; l < kPcLists; ++l) {
-            const bool mine = c == (l < kClasses ? 1 + l : kPcLong);
-            const uint64_t m = __ballot(mine);
-            if (mine) {
-                const uint32_t pos = off[l] + (uint32_t)__popcll(m & below);
-                if (l < kClasses) p.short_list[p.class_off[l] + pos] = (uint32_t)j;
-                else p.long_list[pos] = (uint32_t)j;
-            }
-            off[l] += (uint32_t)__popcll(m);
-        }
+    for (uint64_t j = lo + tid; j < hi; j += 256, ++r) {
+        const int c = r < 42 ? (int)((cls[r / 21] >> (3 * (r % 21))) & 7ull) : pace_head_class(p, j);
+        if (!c) continue;
+        const int l = list_of(c);
+        const uint32_t pos = base[l] + atomicAdd(&tot[l], 1u);
+        if (l < kClasses) p.short_list[p.class_off[l] + pos] = (uint32_t)j;
+        else p.long_list[pos] = (uint32_t)j;
     }
 }
 
