@@ -110,6 +110,7 @@ constexpr uint32_t kPrepTile = 256 * kPrepItems;
 template <bool BIN>
 __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
     __shared__ uint32_t dcnt[1024];
+    __shared__ uint16_t ldig[kPrepItems * 256];  // each request's first sort digit (the histogram after the loop)
     __shared__ alignas(16) uint2 htab[BIN ? kHotTab : 1];  // the hot flowIds: two 16-B LDS reads per request
     if constexpr (BIN)
         for (uint32_t x = threadIdx.x; x < kHotTab; x += 256) htab[x] = a.hot_tab[x];
@@ -199,9 +200,15 @@ __global__ void __launch_bounds__(256) k_prep(BatchArgs a) {
             st_stream(o + 2, 0);
         }
         st_stream(a.rec + i, rec);
-        if (a.hist0) atomicAdd(&dcnt[BIN ? d : (uint32_t)(rec >> a.hist0_shift) & dmask], 1u);
+        if (a.hist0) ldig[it * 256 + threadIdx.x] = (uint16_t)(BIN ? d : (uint32_t)(rec >> a.hist0_shift) & dmask);
     }
     if (a.hist0) {
+        // the histogram's LDS atomics after the tile's loads: inside the loop they kept the compiler from overlapping
+        // one item's request load with the previous item's work
+        for (int it = 0; it < kPrepItems; ++it) {
+            if (base + (uint64_t)it * 256 + threadIdx.x >= n) break;
+            atomicAdd(&dcnt[ldig[it * 256 + threadIdx.x]], 1u);
+        }
         __syncthreads();
         for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)tile * (dmask + 1) + d] = dcnt[d];
         if (a.csum0) {  // the chunk's column sums (zeroed before the launch): no k_colsum pass for the first digit

@@ -141,6 +141,7 @@ __device__ __forceinline__ void lstore(const LArgs& a, uint32_t idx, int32_t st,
 constexpr int kLPrepItems = 16;
 __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
     __shared__ uint32_t dcnt[1024];
+    __shared__ uint16_t ldig[kLPrepItems * 256];  // each item's first sort digit (the histogram after the loop)
     const uint64_t n = a.n;
     const int64_t t0 = a.ev[0].ts_ms;
     const uint64_t sentinel = (uint64_t)a.K << a.kshift;
@@ -257,9 +258,16 @@ __global__ void __launch_bounds__(256) k_local_prep(LArgs a) {
         const uint32_t dst = (res < a.K && e.kind == SG_LOCAL_ENTRY) ? SG_LOCAL_BLOCK_FLOW : SG_LOCAL_PASS;
         st_stream(reinterpret_cast<uint64_t*>(a.out + i), (uint64_t)dst);  // {status, wait_ms 0}
         st_stream(a.rec + i, rec);
-        if (a.hist0) atomicAdd(&dcnt[(uint32_t)(rec >> a.kshift) & dmask], 1u);
+        if (a.hist0) ldig[it * 256 + threadIdx.x] = (uint16_t)((uint32_t)(rec >> a.kshift) & dmask);
     }
     if (a.hist0) {
+        // the histogram's LDS atomics after the tile's loads: inside the loop they kept the compiler from
+        // overlapping one item's event load with the previous item's work (k_local_prep 285 → ~200 µs at C5 without them)
+        for (int it = 0; it < kLPrepItems; ++it) {
+            const uint64_t i = tile + (uint64_t)it * 256 + threadIdx.x;
+            if (i >= n) break;
+            atomicAdd(&dcnt[ldig[it * 256 + threadIdx.x]], 1u);
+        }
         __syncthreads();
         for (uint32_t d = threadIdx.x; d <= dmask; d += 256) a.hist0[(size_t)blockIdx.x * (dmask + 1) + d] = dcnt[d];
         if (a.csum0) {
