@@ -504,9 +504,13 @@ __device__ void cp_walk_serial_mem(const CPArgs& c, const CPBatch& b, const Batc
 // cp_walk_serial with the slot's ring in registers (sampleCount <= SM): the ring is read once, with all loads issued
 // together, and the changed buckets are written back at the end — the memory version reads S buckets at every
 // window-period change, a dependent round trip per period of a slot's records.
+//
+// save_t >= 0 (round 0 of the lane walker): the pre-batch ring goes to save slot save_t only if the slot holds a
+// multi-value record — only such slots are ever restored (re-walks and the fallback groups follow multi-value
+// requests) — copied at the end of the walk, before the changed buckets are written back.
 template <int SM>
 __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j,
-                                   const CPRule& r) {
+                                   const CPRule& r, int64_t save_t = -1) {
     const double thr = cp_threshold(c, r, c.keys[g]);
     CPBucket* ring = c.ring + g * (uint64_t)c.stride;
     const int S = r.S;
@@ -523,6 +527,7 @@ __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const Batc
     uint32_t qn = 0xFFFFFFFFu;  // first request index of the period after P (monotone cursor)
     uint32_t mi = kNoOwner;     // the multi-value request of the previous record, and its check here
     bool mok = false;
+    bool any_multi = false;
     auto close = [&]() {  // the open period's bucket into the register ring
         if (P == INT64_MIN) return;
         const int xo = (int)(P % S);
@@ -543,6 +548,7 @@ __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const Batc
         rec = nrec;
         ++j;
         if (b.lim && c.out[i].status == SG_STATUS_TOO_MANY_REQUEST) continue;  // allowProceed refused it
+        any_multi |= d.multi;
         if (d.multi && i == mi) {  // a repeated value: the check of the request's first record here, and its add
             b.chk[d.p] = mok ? 1 : 0;
             if (b.assume[i] && mok) cur += d.acq;
@@ -583,6 +589,10 @@ __device__ void cp_walk_serial_reg(const CPArgs& c, const CPBatch& b, const Batc
         if (b.assume[i] && mok) cur += d.acq;
     }
     close();
+    if (save_t >= 0 && any_multi) {  // the ring in memory is still the pre-batch one
+        CPBucket* sv = b.save + (uint64_t)save_t * (uint64_t)c.stride;
+        for (int x = 0; x < c.stride; ++x) sv[x] = ring[x];
+    }
 #pragma unroll
     for (int x = 0; x < SM; ++x) {
         if ((dirty >> x) & 1u) {
@@ -598,6 +608,19 @@ __device__ void cp_walk_serial(const CPArgs& c, const CPBatch& b, const BatchArg
     const CPRule r = c.rules[cp_rule_of_slot(c, g)];
     if (r.S <= 10) cp_walk_serial_reg<10>(c, b, sg, g, j, r);
     else cp_walk_serial_mem(c, b, sg, g, j, r);
+}
+
+// Round 0 of the lane walker: the register walker saves the ring itself when the slot needs it (see
+// cp_walk_serial_reg), the memory walker (sampleCount > 10) through cp_prologue first.
+__device__ void cp_walk_serial_r0(const CPArgs& c, const CPBatch& b, const BatchArgs& sg, uint64_t g, uint64_t j,
+                                  uint64_t t) {
+    const CPRule r = c.rules[cp_rule_of_slot(c, g)];
+    if (r.S <= 10) {
+        cp_walk_serial_reg<10>(c, b, sg, g, j, r, b.save ? (int64_t)t : -1);
+    } else {
+        cp_prologue(c, b, g, t, 0, 1);
+        cp_walk_serial_mem(c, b, sg, g, j, r);
+    }
 }
 
 // One lane per slot of at most short_max records. Work item t: the slot's index in the save area (the long
@@ -628,8 +651,7 @@ __global__ void __launch_bounds__(256, SG_CPS_BLOCKS) k_cp_walk2(CPArgs c, CPBat
         while (r0 >= sg.short_count[k]) r0 -= sg.short_count[k++];
         const uint64_t j = sg.short_list[sg.class_off[k] + r0];
         const uint64_t g = sg.rec_sorted[j] >> b.pbits;
-        if (!cp_prologue(c, b, g, (uint64_t)nlong + u, 0, 1)) continue;
-        cp_walk_serial(c, b, sg, g, j);
+        cp_walk_serial_r0(c, b, sg, g, j, (uint64_t)nlong + u);  // round 0: cp_prologue only saves
     }
 }
 
