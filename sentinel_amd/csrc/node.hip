@@ -227,34 +227,52 @@ __global__ void __launch_bounds__(256) k_nreq_keys(NodeReqArgs q) {
     const int tid = threadIdx.x;
     if (tid < kMaxShards) cnt[tid] = vcnt[tid] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + tid; i < q.n; i += (uint64_t)gridDim.x * 256) {
+    // the loop runs block-uniformly (the shard counts below are wave-wide)
+    for (uint64_t b0 = (uint64_t)blockIdx.x * 256; b0 < q.n; b0 += (uint64_t)gridDim.x * 256) {
+        const uint64_t i = b0 + tid;
+        const bool act = i < q.n;
         uint32_t g = 0, nv = 0;
-        {  // the node's time order (a batch older than the node's previous one, or unsorted, is refused whole)
-            const int64_t t = q.cp ? q.cp[i].ts_ms : q.cc[i].ts_ms;
-            const int64_t tp = i == 0 ? q.last_ts : (q.cp ? q.cp[i - 1].ts_ms : q.cc[i - 1].ts_ms);
-            if (t < 0 || t < tp) atomicOr(q.err, kErrTime);
-        }
-        if (q.cp) {
-            const sg_cparam_req r = q.cp[i];
-            const uint32_t key = r.key & SG_KEY_INDEX;
-            if (key < q.K) g = q.shard_of[key];
-            // only a valid request's values are read (DefaultTokenService answers the others without them); an
-            // invalid one reaches its shard with no values, and the shard answers it as one handle would
-            const bool valid = key < q.K && r.acquire > 0 && r.value_count > 0;
-            nv = valid ? r.value_count : 0u;
-            if (nv && ((uint64_t)r.value_begin + nv > q.n_values)) {  // the whole batch is refused (SG_E_INVAL)
-                atomicOr(q.err, kErrBounds);
-                nv = 0;
+        if (act) {
+            {  // the node's time order (a batch older than the node's previous one, or unsorted, is refused whole)
+                const int64_t t = q.cp ? q.cp[i].ts_ms : q.cc[i].ts_ms;
+                const int64_t tp = i == 0 ? q.last_ts : (q.cp ? q.cp[i - 1].ts_ms : q.cc[i - 1].ts_ms);
+                if (t < 0 || t < tp) atomicOr(q.err, kErrTime);
             }
-        } else {
-            const sg_conc_req r = q.cc[i];
-            if (r.kind == SG_CONC_RELEASE) g = r.token_id ? (uint32_t)((r.token_id - 1) % (uint64_t)q.G) : 0u;
-            else if ((r.key & SG_KEY_INDEX) < q.K) g = q.shard_of[r.key & SG_KEY_INDEX];
+            if (q.cp) {
+                const sg_cparam_req r = q.cp[i];
+                const uint32_t key = r.key & SG_KEY_INDEX;
+                if (key < q.K) g = q.shard_of[key];
+                // only a valid request's values are read (DefaultTokenService answers the others without them); an
+                // invalid one reaches its shard with no values, and the shard answers it as one handle would
+                const bool valid = key < q.K && r.acquire > 0 && r.value_count > 0;
+                nv = valid ? r.value_count : 0u;
+                if (nv && ((uint64_t)r.value_begin + nv > q.n_values)) {  // the whole batch is refused (SG_E_INVAL)
+                    atomicOr(q.err, kErrBounds);
+                    nv = 0;
+                }
+            } else {
+                const sg_conc_req r = q.cc[i];
+                if (r.kind == SG_CONC_RELEASE) g = r.token_id ? (uint32_t)((r.token_id - 1) % (uint64_t)q.G) : 0u;
+                else if ((r.key & SG_KEY_INDEX) < q.K) g = q.shard_of[r.key & SG_KEY_INDEX];
+            }
+            q.rec[i] = ((uint64_t)g << 56) | i;
+            q.nvals[i] = nv;
         }
-        q.rec[i] = ((uint64_t)g << 56) | i;
-        q.nvals[i] = nv;
-        atomicAdd(&cnt[g], 1u);
-        if (nv) atomicAdd(&vcnt[g], nv);
+        // per shard present in the wave: one LDS add of its request count and value count (the lanes of a wave hit
+        // G addresses at most; per-lane atomics serialised on them and held back the next request's loads)
+        bool todo = act;
+        while (__ballot(todo)) {
+            const uint32_t g0 = (uint32_t)__shfl((int)g, __builtin_ctzll(__ballot(todo)), 64);
+            const bool mine = todo && g == g0;
+            const uint64_t m = __ballot(mine);
+            uint32_t v = mine ? nv : 0u;
+            for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+            if (__lane_id() == (uint32_t)__builtin_ctzll(m)) {
+                atomicAdd(&cnt[g0], (uint32_t)__popcll(m));
+                if (v) atomicAdd(&vcnt[g0], v);
+            }
+            todo = todo && !mine;
+        }
     }
     __syncthreads();
     if (tid < q.G) {
