@@ -2212,6 +2212,7 @@ __global__ void __launch_bounds__(256, SG_TINY_BLOCKS) k_walk_tiny(BatchArgs a) 
 
 // One wave per skipped piece: Σ acquire and Σ prioritized acquire over its records, added with 64-bit
 // atomics (pieces of one range share a bucket).
+constexpr int kSkipU = 8;
 __global__ void __launch_bounds__(256) k_skip_apply(BatchArgs a) {
     if (*a.err) return;
     const uint32_t cnt = min(*a.skip_count, a.skip_cap);
@@ -2221,10 +2222,22 @@ __global__ void __launch_bounds__(256) k_skip_apply(BatchArgs a) {
     for (uint32_t i = wave; i < cnt; i += nwaves) {
         const uint4 sk = a.skips[i];
         int64_t sa = 0, spa = 0;
-        for (uint64_t j = (uint64_t)sk.z + lane; j < sk.w; j += 64) {
-            const Decoded d = decode(a, a.rec_sorted[j]);
-            sa += d.acq;
-            spa += d.prio ? d.acq : 0;
+        // kSkipU rows of 64 records loaded together (one row per round trip left the wave latency-bound: a 4096-record
+        // piece took 64 of them)
+        for (uint64_t j0 = (uint64_t)sk.z; j0 < sk.w; j0 += 64ull * kSkipU) {
+            uint64_t r[kSkipU];
+#pragma unroll
+            for (int u = 0; u < kSkipU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * 64 + lane;
+                r[u] = j < sk.w ? a.rec_sorted[j] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < kSkipU; ++u) {
+                if (j0 + (uint64_t)u * 64 + lane >= sk.w) continue;
+                const Decoded d = decode(a, r[u]);
+                sa += d.acq;
+                spa += d.prio ? d.acq : 0;
+            }
         }
         sa = wave_sum(sa);
         spa = wave_sum(spa);

@@ -2749,6 +2749,7 @@ __global__ void __launch_bounds__(256) k_lexit_write(LArgs a) {
 // BLOCK counts of the skipped entries (one wave per piece; their FlowException results are k_local_prep's
 // default), added to the second- and minute-window buckets of their periods unless a later period of the
 // batch reset that slot.
+constexpr int kLSkipU = 8;
 __global__ void __launch_bounds__(256) k_lskip_apply(LArgs a) {
     if (*a.err) return;
     const uint32_t cnt = min(*a.skip_count, a.skip_cap);
@@ -2758,7 +2759,18 @@ __global__ void __launch_bounds__(256) k_lskip_apply(LArgs a) {
     for (uint32_t i = wave; i < cnt; i += nwaves) {
         const LSkip sk = a.skips[i];
         int64_t sum = 0;
-        for (uint64_t j = (uint64_t)sk.b0 + lane; j < sk.b1; j += 64) sum += ldecode(a, a.rec_sorted[j]).count;
+        // kLSkipU rows of 64 records loaded together (one row per round trip left the wave latency-bound)
+        for (uint64_t j0 = (uint64_t)sk.b0; j0 < sk.b1; j0 += 64ull * kLSkipU) {
+            uint64_t r[kLSkipU];
+#pragma unroll
+            for (int u = 0; u < kLSkipU; ++u) {
+                const uint64_t j = j0 + (uint64_t)u * 64 + lane;
+                r[u] = j < sk.b1 ? a.rec_sorted[j] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < kLSkipU; ++u)
+                if (j0 + (uint64_t)u * 64 + lane < sk.b1) sum += ldecode(a, r[u]).count;
+        }
         sum = wave_sum(sum);
         if (lane == 0) {
             const int64_t Ps = a.p0[a.wsec] + (int64_t)sk.qs, Pm = a.p0[a.wmin] + (int64_t)sk.qm;
