@@ -554,7 +554,14 @@ int sg_create(const sg_config* cfg, sg_handle** out) {
     if (hipMemcpy(h->d_plast_ts, &neg, sizeof(neg), hipMemcpyHostToDevice) != hipSuccess) return bail(SG_E_DEVICE);
     for (auto& e : h->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(SG_E_DEVICE);
-    if (hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) != hipSuccess ||
+    // the auxiliary stream carries the wave walkers beside the lane walkers (pace, hot params, cluster params);
+    // env SG_AUX_PRIO=1 (tuning) creates it at the highest stream priority
+    int aux_prio = 0;
+    if (const char* e = std::getenv("SG_AUX_PRIO"); e && std::atoi(e) == 1) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) aux_prio = greatest;
+    }
+    if (hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, aux_prio) != hipSuccess ||
         hipEventCreateWithFlags(&h->fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->join, hipEventDisableTiming) != hipSuccess)
         return bail(SG_E_DEVICE);
